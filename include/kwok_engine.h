@@ -1,0 +1,274 @@
+/*
+ * kwok_engine.h - C-ABI of the MI355X-native kwok fake-kubelet tick engine.
+ *
+ * This is the drop-in boundary for the per-tick work of the reference's
+ * pkg/kwok/controllers package (hezhizhen/kwok).  The Go side keeps the
+ * reference's API (Config, NewController, NodeController, PodController,
+ * watch/list/patch plumbing via client-go) and, instead of rendering templates
+ * and evaluating strategic-merge predicates per object, pushes decoded watch
+ * events into this library in batches and applies the patches/deletes it
+ * returns.  No torch or C++ types appear here: plain integers, pointers and
+ * sizes only (cgo / ctypes / JNI friendly).  See INTEGRATION.md for the cgo
+ * binding and DESIGN.md for the tick contract.
+ *
+ * Entry point -> reference interface it replaces (paths relative to the
+ * reference repo root):
+ *   kwok_engine_create       controllers.NewController       pkg/kwok/controllers/controller.go:80-152
+ *                            (NewNodeController node_controller.go:79-117,
+ *                             NewPodController pod_controller.go:84-128,
+ *                             parseCIDR/newIPPool utils.go:28-35,68)
+ *   kwok_ingest_nodes        NodeController.WatchNodes/ListNodes event switch
+ *                                                            node_controller.go:256-270,286-295
+ *   kwok_ingest_pods         PodController.WatchPods/ListPods event switch
+ *                                                            pod_controller.go:301-343,361-367
+ *   kwok_register_pod_spec   (spec part of the pod JSON document renderToJSON
+ *                             feeds to pod.status.tpl)      renderer.go:65-75
+ *   kwok_tick                one heartbeat interval: KeepNodeHeartbeat +
+ *                            LockNodes/LockNode/configureNode + LockPodsOnNode +
+ *                            LockPods/LockPod/configurePod/computePatchData +
+ *                            DeletePods/DeletePod + ipPool Get/Put/Use
+ *                                                            node_controller.go:145-204,301-401
+ *                                                            pod_controller.go:155-250,371-439
+ *                                                            utils.go:83-117
+ *   kwok_read_outputs        the PatchStatus / Patch / Delete request bodies
+ *                                                            node_controller.go:152,345;
+ *                                                            pod_controller.go:162,172,221
+ *   kwok_node_has / _size    NodeController.Has / Size        node_controller.go:403-409
+ *   kwok_pool_put            ipPool.Put (replicating an ingest-time release
+ *                            to the other ranks' pool replicas) utils.go:100-108
+ */
+#ifndef KWOK_ENGINE_H
+#define KWOK_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KWOK_ABI_VERSION 1u
+#define KWOK_COMM_ID_BYTES 128u
+
+/* ---- status codes (int return values; per-record codes in out_status) ---- */
+enum {
+    KWOK_OK = 0,
+    KWOK_EINVAL = -1,     /* bad argument / config */
+    KWOK_ENOMEM = -2,     /* host or device allocation failed */
+    KWOK_EDOMAIN = -3,    /* input outside the supported domain (e.g. not a "safe string",
+                             IPv6, custom templates, EnableCNI) - rejected, never emulated */
+    KWOK_EFULL = -4,      /* bucket slot capacity exhausted */
+    KWOK_EDEVICE = -5,    /* HIP runtime error */
+    KWOK_ECOMM = -6,      /* RCCL / exchange error */
+    KWOK_ENOTFOUND = -7,  /* unknown handle */
+    KWOK_ENOTMINE = -8    /* object hashes to a bucket owned by another rank (not an error
+                             for a sharded caller: route it to the owning rank) */
+};
+
+enum { KWOK_OP_UPSERT = 1 /* watch.Added / watch.Modified / list item */, KWOK_OP_DELETE = 2 /* watch.Deleted */ };
+
+/* corev1 PodPhase / NodePhase as far as the templates and predicates care */
+enum {
+    KWOK_PHASE_NONE = 0, KWOK_PHASE_PENDING = 1, KWOK_PHASE_RUNNING = 2,
+    KWOK_PHASE_SUCCEEDED = 3, KWOK_PHASE_FAILED = 4, KWOK_PHASE_UNKNOWN = 5,
+    KWOK_PHASE_OTHER = 6 /* any other node phase, e.g. "Terminated" */
+};
+
+/* pod event flags */
+enum {
+    KWOK_POD_DISREGARD = 1u << 0,       /* disregardStatusWith{Annotation,Label}Selector matched
+                                           (pod_controller.go:257-267) */
+    KWOK_POD_DELETING = 1u << 1,        /* metadata.deletionTimestamp != nil (:306) */
+    KWOK_POD_STATUS_NONEMPTY = 1u << 2, /* json(pod.status) is a non-empty map: the
+                                           `{{ with .status }}` guard of pod.status.tpl:44 */
+    KWOK_POD_CONFORMS = 1u << 3,        /* status.conditions / containerStatuses /
+                                           initContainerStatuses / startTime already equal what
+                                           pod.status.tpl renders (strategic-merge no-op for
+                                           those fields, pod_controller.go:411-435) */
+    KWOK_POD_HAS_FINALIZERS = 1u << 4   /* len(metadata.finalizers) != 0 (:161) */
+};
+
+/* byte range inside the caller's string arena passed with each batch */
+typedef struct kwok_str {
+    uint32_t off;
+    uint32_t len;
+} kwok_str;
+
+/* status.nodeInfo fields in JSON key order (node.status.tpl:31-42) */
+enum {
+    KWOK_NI_ARCHITECTURE = 0, KWOK_NI_BOOT_ID, KWOK_NI_CONTAINER_RUNTIME_VERSION,
+    KWOK_NI_KERNEL_VERSION, KWOK_NI_KUBE_PROXY_VERSION, KWOK_NI_KUBELET_VERSION,
+    KWOK_NI_MACHINE_ID, KWOK_NI_OPERATING_SYSTEM, KWOK_NI_OS_IMAGE, KWOK_NI_SYSTEM_UUID,
+    KWOK_NI_COUNT
+};
+
+typedef struct kwok_node_event {
+    uint8_t op;        /* KWOK_OP_* */
+    uint8_t managed;   /* needHeartbeat(node) = nodeSelectorFunc(node)  (node_controller.go:206) */
+    uint8_t lockable;  /* needLockNode(node)                            (node_controller.go:210) */
+    uint8_t phase;     /* status.phase: NONE, RUNNING or OTHER */
+    kwok_str name;
+    kwok_str addresses;   /* compact JSON of status.addresses   (len 0 = absent/empty) */
+    kwok_str allocatable; /* compact JSON of status.allocatable (len 0 = absent/empty) */
+    kwok_str capacity;    /* compact JSON of status.capacity    (len 0 = absent/empty) */
+    kwok_str node_info[KWOK_NI_COUNT]; /* status.nodeInfo.* (len 0 = "") */
+} kwok_node_event;
+
+typedef struct kwok_pod_event {
+    uint8_t op;        /* KWOK_OP_* */
+    uint8_t phase;     /* status.phase */
+    uint8_t flags;     /* KWOK_POD_* */
+    uint8_t reserved0;
+    int32_t handle;    /* UPSERT of a new pod: -1; otherwise the handle returned at add */
+    int32_t spec_id;   /* from kwok_register_pod_spec */
+    int32_t node_handle; /* -1: resolve node_name */
+    int64_t creation_unix; /* metadata.creationTimestamp (seconds, UTC) */
+    kwok_str node_name;  /* spec.nodeName */
+    kwok_str host_ip;    /* status.hostIP (dotted IPv4 or empty) */
+    kwok_str pod_ip;     /* status.podIP  (dotted IPv4 or empty) */
+} kwok_pod_event;
+
+typedef struct kwok_container {
+    kwok_str name;
+    kwok_str image;
+} kwok_container;
+
+typedef struct kwok_pod_spec {
+    const kwok_container* containers;      uint32_t n_containers;      /* spec.containers */
+    const kwok_container* init_containers; uint32_t n_init_containers; /* spec.initContainers */
+    const kwok_str* readiness_gates;       uint32_t n_readiness_gates; /* spec.readinessGates[].conditionType */
+} kwok_pod_spec;
+
+/* Allgather over host memory: every rank contributes `bytes` from `send`;
+ * `recv` receives world_size * bytes, rank-major.  Return 0 on success. */
+typedef int (*kwok_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
+
+typedef struct kwok_config {
+    uint32_t abi_version;          /* KWOK_ABI_VERSION */
+    const char* cidr;              /* Config.CIDR,   e.g. "10.0.0.1/24" (controller.go:72) */
+    const char* node_ip;           /* Config.NodeIP, e.g. "196.168.0.1" (controller.go:73) */
+    int64_t start_time_unix;       /* the StartTime() template func (controller.go:39-41) */
+    int32_t enable_cni;            /* Config.EnableCNI: must be 0 */
+    int32_t custom_templates;      /* must be 0: only templates.Default* are supported */
+    uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
+    uint32_t node_slots_per_bucket;
+    uint32_t pod_slots_per_bucket;
+    uint32_t max_pod_specs;
+    int32_t rank;                  /* this engine owns buckets [rank*B/W, (rank+1)*B/W) */
+    int32_t world_size;
+    int32_t device;                /* HIP device ordinal (ignored by the CPU oracle) */
+    const uint8_t* comm_id;        /* KWOK_COMM_ID_BYTES from kwok_comm_id(): RCCL exchange */
+    kwok_allgather_fn allgather;   /* alternative host-memory exchange (used when comm_id == NULL) */
+    void* allgather_user;
+} kwok_config;
+
+/* fleet counters (kwok_tick_result.counters, summed over ranks) */
+enum {
+    KWOK_CNT_HEARTBEAT = 0,   /* heartbeat patches emitted this tick */
+    KWOK_CNT_NODE_INIT,       /* node lock (initialisation) patches emitted */
+    KWOK_CNT_POD_PATCH,       /* pod status patches emitted */
+    KWOK_CNT_DELETE,          /* pods deleted (DeletePod) */
+    KWOK_CNT_ALLOC,           /* ipPool.Get calls */
+    KWOK_CNT_RELEASE,         /* ipPool.Put calls from this tick's deletions */
+    KWOK_CNT_EVALUATED,       /* pods evaluated (LockPod) incl. no-ops */
+    KWOK_CNT_LOCK_CHECKED,    /* nodes lock-checked (LockNode) incl. no-ops */
+    KWOK_CNT_NODES_MANAGED,   /* NodeController.Size() after the tick */
+    KWOK_CNT_NODES_READY,     /* managed nodes whose status is initialised */
+    KWOK_CNT_PODS_TOTAL,
+    KWOK_CNT_PODS_PENDING,
+    KWOK_CNT_PODS_RUNNING,
+    KWOK_COUNTER_COUNT
+};
+
+typedef struct kwok_tick_result {
+    uint32_t n_heartbeat;       /* number of heartbeat patches (one per managed node) */
+    uint32_t heartbeat_len;     /* bytes of every heartbeat patch (identical bodies) */
+    uint64_t heartbeat_stride;  /* arena distance between consecutive heartbeat patches */
+    uint32_t n_node_init;
+    uint32_t n_pod_patch;
+    uint32_t n_delete;
+    uint32_t reserved0;
+    uint64_t arena_bytes;       /* bytes of the output arena in use */
+    uint64_t counters[KWOK_COUNTER_COUNT];       /* fleet-wide (all ranks) */
+    uint64_t local_counters[KWOK_COUNTER_COUNT]; /* this rank */
+} kwok_tick_result;
+
+/* Host buffers the caller provides to kwok_read_outputs (NULL = skip). */
+typedef struct kwok_outputs {
+    int32_t* heartbeat_nodes;       /* [n_heartbeat] node handles, canonical order */
+    uint64_t heartbeat_off;         /* out: arena offset of heartbeat patch 0 */
+    int32_t* node_init_nodes;       /* [n_node_init] */
+    uint64_t* node_init_off;        /* [n_node_init] arena offsets */
+    uint32_t* node_init_len;        /* [n_node_init] */
+    int32_t* pod_patch_pods;        /* [n_pod_patch] pod handles, canonical order */
+    uint64_t* pod_patch_off;
+    uint32_t* pod_patch_len;
+    int32_t* delete_pods;           /* [n_delete] pod handles to Patch(finalizers)+Delete */
+    uint8_t* delete_has_finalizers; /* [n_delete] 1 = send kwok_finalizer_patch() first */
+    uint8_t* arena;                 /* [arena_cap] copy of the output arena */
+    uint64_t arena_cap;
+} kwok_outputs;
+
+typedef struct kwok_engine kwok_engine;
+
+uint32_t kwok_abi_version(void);
+int kwok_comm_id(uint8_t out[KWOK_COMM_ID_BYTES]);
+
+int kwok_engine_create(const kwok_config* cfg, kwok_engine** out);
+void kwok_engine_destroy(kwok_engine* e);
+const char* kwok_last_error(const kwok_engine* e);
+
+/* Register a pod spec (containers, init containers, readiness gates); identical
+ * specs share one id.  Strings must be "safe"  or KWOK_EDOMAIN. */
+int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char* arena,
+                           size_t arena_len, int32_t* out_id);
+
+/* Ingest a batch of watch events in order.  out_handles[i] receives the node/pod
+ * handle (canonical slot id), out_status[i] a per-record code (KWOK_OK,
+ * KWOK_EDOMAIN, KWOK_EFULL, KWOK_ENOTFOUND, KWOK_ENOTMINE).  Returns the number of
+ * rejected records (>= 0) or a negative error for the whole batch. */
+int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena,
+                      size_t arena_len, int32_t* out_handles, int32_t* out_status);
+/* out_released (optional) receives, per DELETE record, the IPv4 address released
+ * into the pool (0 if none); sharded callers replicate these to the other ranks
+ * with kwok_pool_put before the next tick. */
+int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena,
+                     size_t arena_len, int32_t* out_handles, int32_t* out_status,
+                     uint32_t* out_released);
+int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n);
+
+/* Advance one heartbeat interval at fixed clock now_unix (the Now() template
+ * func).  Blocks until the tick's outputs are ready. */
+int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res);
+int kwok_read_outputs(kwok_engine* e, kwok_outputs* out);
+
+/* The constant merge patch sent before Delete when a pod has finalizers
+ * (removeFinalizers, pod_controller.go:45). */
+const char* kwok_finalizer_patch(size_t* len);
+
+int kwok_node_has(kwok_engine* e, const char* name, size_t len);
+uint64_t kwok_node_size(kwok_engine* e);
+
+/* State dump for tests / checkpoint: pods with handles in [first, first+count). */
+int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase,
+                   uint32_t* host_ip, uint32_t* pod_ip);
+
+/* Device-resident outputs for zero-copy consumers (valid until the next tick). */
+typedef struct kwok_device_view {
+    const void* arena;
+    const int32_t* heartbeat_nodes;
+    const int32_t* pod_patch_pods;
+    const uint64_t* pod_patch_off;
+    const uint32_t* pod_patch_len;
+    void* stream;                   /* hipStream_t the engine runs on */
+} kwok_device_view;
+int kwok_device_outputs(kwok_engine* e, kwok_device_view* view);
+
+/* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
+uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);
+int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world_size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KWOK_ENGINE_H */

@@ -1,0 +1,156 @@
+"""ctypes / numpy mirrors of include/kwok_engine.h (the C-ABI boundary).
+
+Everything here is layout only; the structs must stay byte-identical to the
+header (tests/test_abi.py checks sizes and offsets against the compiled
+library's expectations)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+ABI_VERSION = 1
+COMM_ID_BYTES = 128
+
+OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+ERRNAMES = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDOMAIN", -4: "EFULL", -5: "EDEVICE",
+            -6: "ECOMM", -7: "ENOTFOUND", -8: "ENOTMINE"}
+
+OP_UPSERT, OP_DELETE = 1, 2
+PHASE_NONE, PHASE_PENDING, PHASE_RUNNING, PHASE_SUCCEEDED, PHASE_FAILED, PHASE_UNKNOWN, PHASE_OTHER = range(7)
+POD_PHASES = {"": PHASE_NONE, "Pending": PHASE_PENDING, "Running": PHASE_RUNNING, "Succeeded": PHASE_SUCCEEDED,
+              "Failed": PHASE_FAILED, "Unknown": PHASE_UNKNOWN}
+PHASE_NAMES = {v: k for k, v in POD_PHASES.items()}
+
+POD_DISREGARD, POD_DELETING, POD_STATUS_NONEMPTY, POD_CONFORMS, POD_HAS_FINALIZERS = 1, 2, 4, 8, 16
+
+NODEINFO_KEYS = ["architecture", "bootID", "containerRuntimeVersion", "kernelVersion", "kubeProxyVersion",
+                 "kubeletVersion", "machineID", "operatingSystem", "osImage", "systemUUID"]
+NI_COUNT = len(NODEINFO_KEYS)
+
+COUNTERS = ["heartbeat", "node_init", "pod_patch", "delete", "alloc", "release", "evaluated", "lock_checked",
+            "nodes_managed", "nodes_ready", "pods_total", "pods_pending", "pods_running"]
+COUNTER_COUNT = len(COUNTERS)
+
+
+class KwokStr(C.Structure):
+    _fields_ = [("off", C.c_uint32), ("len", C.c_uint32)]
+
+
+class NodeEvent(C.Structure):
+    _fields_ = [("op", C.c_uint8), ("managed", C.c_uint8), ("lockable", C.c_uint8), ("phase", C.c_uint8),
+                ("name", KwokStr), ("addresses", KwokStr), ("allocatable", KwokStr), ("capacity", KwokStr),
+                ("node_info", KwokStr * NI_COUNT)]
+
+
+class PodEvent(C.Structure):
+    _fields_ = [("op", C.c_uint8), ("phase", C.c_uint8), ("flags", C.c_uint8), ("reserved0", C.c_uint8),
+                ("handle", C.c_int32), ("spec_id", C.c_int32), ("node_handle", C.c_int32),
+                ("creation_unix", C.c_int64), ("node_name", KwokStr), ("host_ip", KwokStr), ("pod_ip", KwokStr)]
+
+
+class Container(C.Structure):
+    _fields_ = [("name", KwokStr), ("image", KwokStr)]
+
+
+class PodSpec(C.Structure):
+    _fields_ = [("containers", C.POINTER(Container)), ("n_containers", C.c_uint32),
+                ("init_containers", C.POINTER(Container)), ("n_init_containers", C.c_uint32),
+                ("readiness_gates", C.POINTER(KwokStr)), ("n_readiness_gates", C.c_uint32)]
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class Config(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("cidr", C.c_char_p), ("node_ip", C.c_char_p),
+                ("start_time_unix", C.c_int64), ("enable_cni", C.c_int32), ("custom_templates", C.c_int32),
+                ("buckets", C.c_uint32), ("node_slots_per_bucket", C.c_uint32),
+                ("pod_slots_per_bucket", C.c_uint32), ("max_pod_specs", C.c_uint32),
+                ("rank", C.c_int32), ("world_size", C.c_int32), ("device", C.c_int32),
+                ("comm_id", C.c_void_p), ("allgather", ALLGATHER_FN), ("allgather_user", C.c_void_p)]
+
+
+class TickResult(C.Structure):
+    _fields_ = [("n_heartbeat", C.c_uint32), ("heartbeat_len", C.c_uint32), ("heartbeat_stride", C.c_uint64),
+                ("n_node_init", C.c_uint32), ("n_pod_patch", C.c_uint32), ("n_delete", C.c_uint32),
+                ("reserved0", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("counters", C.c_uint64 * COUNTER_COUNT), ("local_counters", C.c_uint64 * COUNTER_COUNT)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [("heartbeat_nodes", C.c_void_p), ("heartbeat_off", C.c_uint64),
+                ("node_init_nodes", C.c_void_p), ("node_init_off", C.c_void_p), ("node_init_len", C.c_void_p),
+                ("pod_patch_pods", C.c_void_p), ("pod_patch_off", C.c_void_p), ("pod_patch_len", C.c_void_p),
+                ("delete_pods", C.c_void_p), ("delete_has_finalizers", C.c_void_p),
+                ("arena", C.c_void_p), ("arena_cap", C.c_uint64)]
+
+
+class DeviceView(C.Structure):
+    _fields_ = [("arena", C.c_void_p), ("heartbeat_nodes", C.c_void_p), ("pod_patch_pods", C.c_void_p),
+                ("pod_patch_off", C.c_void_p), ("pod_patch_len", C.c_void_p), ("stream", C.c_void_p)]
+
+
+def _np_dtype(st):
+    """numpy structured dtype with the exact ctypes layout (for bulk batches)."""
+    names, formats, offsets = [], [], []
+    for name, ty in st._fields_:
+        names.append(name)
+        offsets.append(getattr(st, name).offset)
+        if ty is KwokStr:
+            formats.append(np.dtype([("off", "<u4"), ("len", "<u4")]))
+        elif isinstance(ty, type) and issubclass(ty, C.Array):
+            formats.append((np.dtype([("off", "<u4"), ("len", "<u4")]), (ty._length_,)))
+        else:
+            formats.append(np.dtype(ty))
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": C.sizeof(st)})
+
+
+NODE_EVENT_DTYPE = _np_dtype(NodeEvent)
+POD_EVENT_DTYPE = _np_dtype(PodEvent)
+
+
+def ip4(s: str) -> int:
+    if not s:
+        return 0
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def ip4s(v: int) -> str:
+    return "" if not v else "%d.%d.%d.%d" % (v >> 24, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+def fnv1a32(s: str) -> int:
+    h = 0x811C9DC5
+    for b in s.encode():
+        h ^= b
+        h = (h * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+class Arena:
+    """Growing byte arena + kwok_str refs for one ingest batch."""
+
+    def __init__(self):
+        self.buf = bytearray()
+        self._intern = {}
+
+    def ref(self, s) -> tuple[int, int]:
+        if s is None or s == "" or s == b"":
+            return (0, 0)
+        b = s.encode() if isinstance(s, str) else bytes(s)
+        r = self._intern.get(b)
+        if r is None:
+            r = (len(self.buf), len(b))
+            self.buf += b
+            self._intern[b] = r
+        return r
+
+    def kstr(self, s) -> KwokStr:
+        o, n = self.ref(s)
+        return KwokStr(o, n)
+
+    def cbuf(self):
+        b = bytes(self.buf) or b"\0"
+        return C.create_string_buffer(b, len(b)), len(self.buf)

@@ -1,0 +1,288 @@
+"""Python binding of the C-ABI engine (include/kwok_engine.h).
+
+`Engine` drives libkwok_engine.so (HIP kernels on gfx950).  The class is
+written against the ABI only, parameterised by the symbol prefix, so test
+infrastructure can point the same driver at the CPU oracle
+(oracle/oracle.py); the product never does.
+
+Mirrors the reference's controller-facing calls (hezhizhen/kwok,
+pkg/kwok/controllers): ingest_nodes ~ WatchNodes/ListNodes event handling
+(node_controller.go:256-295), ingest_pods ~ WatchPods/ListPods
+(pod_controller.go:301-367), tick ~ one heartbeat interval of KeepNodeHeartbeat
++ LockNodes + LockPods + DeletePods (node_controller.go:175-204,301-354;
+pod_controller.go:155-250), has/size ~ NodeController.Has/Size (:403-409).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libkwok_engine.so")
+
+
+class KwokError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("%s (%d)%s" % (abi.ERRNAMES.get(code, "?"), code, (": " + msg) if msg else ""))
+        self.code = code
+
+
+_LIB = None
+
+
+def load_engine_lib(path=None):
+    """Load the in-tree HIP engine library.  Fails loudly when it is missing:
+    there is no CPU fallback for the product path."""
+    global _LIB
+    if _LIB is None or path:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError("kwok_amd: %s is missing - run __graft_entry__.build() (make -C kwok_amd)" % p)
+        lib = C.CDLL(p)
+        declare(lib, "kwok_")
+        if path:
+            return lib
+        _LIB = lib
+    return _LIB
+
+
+def declare(lib, pre):
+    P, I32, U32, U64, SZ, VP = C.POINTER, C.c_int32, C.c_uint32, C.c_uint64, C.c_size_t, C.c_void_p
+    sig = {
+        "engine_create" if pre == "kwok_" else "create": (C.c_int, [P(abi.Config), P(VP)]),
+        "engine_destroy" if pre == "kwok_" else "destroy": (None, [VP]),
+        "last_error": (C.c_char_p, [VP]),
+        "register_pod_spec": (C.c_int, [VP, P(abi.PodSpec), C.c_char_p, SZ, P(I32)]),
+        "ingest_nodes": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP]),
+        "ingest_pods": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP, VP]),
+        "pool_put": (C.c_int, [VP, VP, SZ]),
+        "tick": (C.c_int, [VP, C.c_int64, P(abi.TickResult)]),
+        "read_outputs": (C.c_int, [VP, P(abi.Outputs)]),
+        "node_has": (C.c_int, [VP, C.c_char_p, SZ]),
+        "node_size": (U64, [VP]),
+        "dump_pods": (C.c_int, [VP, I32, U32, VP, VP, VP, VP]),
+    }
+    if pre == "kwok_":
+        sig.update({
+            "abi_version": (U32, []),
+            "comm_id": (C.c_int, [VP]),
+            "finalizer_patch": (C.c_char_p, [P(SZ)]),
+            "device_outputs": (C.c_int, [VP, P(abi.DeviceView)]),
+            "bucket_of": (U32, [C.c_char_p, SZ, U32]),
+            "rank_of_bucket": (I32, [U32, U32, I32]),
+        })
+    for name, (res, args) in sig.items():
+        f = getattr(lib, pre + name)
+        f.restype = res
+        f.argtypes = args
+
+
+@dataclass
+class TickOutput:
+    counters: dict
+    local_counters: dict
+    heartbeat_nodes: np.ndarray
+    heartbeat_len: int
+    heartbeat_stride: int
+    heartbeat_off: int
+    node_inits: list = field(default_factory=list)   # [(handle, bytes)]
+    pod_patches: list = field(default_factory=list)  # [(handle, bytes)]
+    deletes: list = field(default_factory=list)      # [(handle, has_finalizers)]
+    arena: bytes = b""
+
+    def heartbeat_body(self, i=0):
+        o = self.heartbeat_off + i * self.heartbeat_stride
+        return self.arena[o:o + self.heartbeat_len]
+
+
+def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200, buckets=4096,
+                node_slots_per_bucket=64, pod_slots_per_bucket=512, max_pod_specs=1024, rank=0, world_size=1,
+                device=0, comm_id=None, allgather=None):
+    cfg = abi.Config()
+    cfg.abi_version = abi.ABI_VERSION
+    cfg.cidr = cidr.encode()
+    cfg.node_ip = node_ip.encode()
+    cfg.start_time_unix = start_time
+    cfg.buckets = buckets
+    cfg.node_slots_per_bucket = node_slots_per_bucket
+    cfg.pod_slots_per_bucket = pod_slots_per_bucket
+    cfg.max_pod_specs = max_pod_specs
+    cfg.rank, cfg.world_size, cfg.device = rank, world_size, device
+    keep = []
+    if comm_id is not None:
+        b = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
+        keep.append(b)
+        cfg.comm_id = C.cast(b, C.c_void_p)
+    if allgather is not None:
+        cb = abi.ALLGATHER_FN(allgather)
+        keep.append(cb)
+        cfg.allgather = cb
+    cfg._keep = keep  # keep buffers / callbacks alive with the struct
+    return cfg
+
+
+class EngineBase:
+    """Driver over one ABI implementation (lib + symbol prefix)."""
+
+    PREFIX = "kwok_"
+
+    def __init__(self, lib, cfg: abi.Config):
+        self._lib = lib
+        self._cfg = cfg
+        self._fn = lambda n: getattr(lib, self.PREFIX + n)
+        h = C.c_void_p()
+        create = self._fn("engine_create" if self.PREFIX == "kwok_" else "create")
+        rc = create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise KwokError(rc, "create")
+        self._h = h
+        self.last = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._fn("engine_destroy" if self.PREFIX == "kwok_" else "destroy")(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc < 0:
+            err = self._fn("last_error")(self._h)
+            raise KwokError(rc, "%s: %s" % (what, (err or b"").decode()))
+        return rc
+
+    # -- specs ----------------------------------------------------------------
+    def register_pod_spec(self, containers=(), init_containers=(), readiness_gates=()):
+        ar = abi.Arena()
+        cs = (abi.Container * max(1, len(containers)))(
+            *[abi.Container(ar.kstr(n), ar.kstr(i)) for n, i in containers])
+        ics = (abi.Container * max(1, len(init_containers)))(
+            *[abi.Container(ar.kstr(n), ar.kstr(i)) for n, i in init_containers])
+        gs = (abi.KwokStr * max(1, len(readiness_gates)))(*[ar.kstr(g) for g in readiness_gates])
+        spec = abi.PodSpec(cs, len(containers), ics, len(init_containers), gs, len(readiness_gates))
+        buf, n = ar.cbuf()
+        out = C.c_int32()
+        self._check(self._fn("register_pod_spec")(self._h, C.byref(spec), buf, n, C.byref(out)), "register_pod_spec")
+        return out.value
+
+    # -- ingest ---------------------------------------------------------------
+    def ingest_nodes_raw(self, events: np.ndarray, arena: bytes):
+        n = len(events)
+        hs = np.empty(n, np.int32)
+        st = np.empty(n, np.int32)
+        ev = np.ascontiguousarray(events, dtype=abi.NODE_EVENT_DTYPE)
+        rc = self._fn("ingest_nodes")(self._h, ev.ctypes.data, n, arena or b"\0", len(arena),
+                                      hs.ctypes.data, st.ctypes.data)
+        self._check(rc, "ingest_nodes")
+        return hs, st
+
+    def ingest_pods_raw(self, events: np.ndarray, arena: bytes):
+        n = len(events)
+        hs = np.empty(n, np.int32)
+        st = np.empty(n, np.int32)
+        rel = np.empty(n, np.uint32)
+        ev = np.ascontiguousarray(events, dtype=abi.POD_EVENT_DTYPE)
+        rc = self._fn("ingest_pods")(self._h, ev.ctypes.data, n, arena or b"\0", len(arena),
+                                     hs.ctypes.data, st.ctypes.data, rel.ctypes.data)
+        self._check(rc, "ingest_pods")
+        return hs, st, rel
+
+    def pool_put(self, ips):
+        a = np.ascontiguousarray(ips, dtype=np.uint32)
+        self._check(self._fn("pool_put")(self._h, a.ctypes.data, len(a)), "pool_put")
+
+    # -- tick -------------------------------------------------------------------
+    def tick_raw(self, now_unix):
+        res = abi.TickResult()
+        self._check(self._fn("tick")(self._h, now_unix, C.byref(res)), "tick")
+        self.last = res
+        return res
+
+    def tick(self, now_unix, read=True):
+        res = self.tick_raw(now_unix)
+        if not read:
+            return res
+        return self.read_outputs(res)
+
+    def read_outputs(self, res=None):
+        res = res or self.last
+        hb = np.empty(res.n_heartbeat, np.int32)
+        ini = np.empty(res.n_node_init, np.int32)
+        ini_off = np.empty(res.n_node_init, np.uint64)
+        ini_len = np.empty(res.n_node_init, np.uint32)
+        pp = np.empty(res.n_pod_patch, np.int32)
+        pp_off = np.empty(res.n_pod_patch, np.uint64)
+        pp_len = np.empty(res.n_pod_patch, np.uint32)
+        dl = np.empty(res.n_delete, np.int32)
+        dlf = np.empty(res.n_delete, np.uint8)
+        arena = np.empty(max(1, res.arena_bytes), np.uint8)
+        out = abi.Outputs(hb.ctypes.data, 0, ini.ctypes.data, ini_off.ctypes.data, ini_len.ctypes.data,
+                          pp.ctypes.data, pp_off.ctypes.data, pp_len.ctypes.data, dl.ctypes.data, dlf.ctypes.data,
+                          arena.ctypes.data, arena.nbytes)
+        self._check(self._fn("read_outputs")(self._h, C.byref(out)), "read_outputs")
+        ab = arena.tobytes()
+        return TickOutput(
+            counters=dict(zip(abi.COUNTERS, list(res.counters))),
+            local_counters=dict(zip(abi.COUNTERS, list(res.local_counters))),
+            heartbeat_nodes=hb, heartbeat_len=res.heartbeat_len, heartbeat_stride=res.heartbeat_stride,
+            heartbeat_off=out.heartbeat_off,
+            node_inits=[(int(h), ab[o:o + n]) for h, o, n in zip(ini, ini_off, ini_len)],
+            pod_patches=[(int(h), ab[o:o + n]) for h, o, n in zip(pp, pp_off, pp_len)],
+            deletes=[(int(h), int(f)) for h, f in zip(dl, dlf)],
+            arena=ab)
+
+    # -- queries ----------------------------------------------------------------
+    def node_has(self, name: str) -> bool:
+        b = name.encode()
+        return bool(self._fn("node_has")(self._h, b, len(b)))
+
+    def node_size(self) -> int:
+        return int(self._fn("node_size")(self._h))
+
+    def dump_pods(self, first, count):
+        used = np.zeros(count, np.uint8)
+        phase = np.zeros(count, np.uint8)
+        hip = np.zeros(count, np.uint32)
+        pip = np.zeros(count, np.uint32)
+        self._check(self._fn("dump_pods")(self._h, first, count, used.ctypes.data, phase.ctypes.data,
+                                          hip.ctypes.data, pip.ctypes.data), "dump_pods")
+        return used, phase, hip, pip
+
+
+class Engine(EngineBase):
+    """The MI355X engine (libkwok_engine.so)."""
+
+    PREFIX = "kwok_"
+
+    def __init__(self, cfg=None, **kw):
+        super().__init__(load_engine_lib(), cfg if cfg is not None else make_config(**kw))
+
+    def device_outputs(self):
+        v = abi.DeviceView()
+        self._check(self._lib.kwok_device_outputs(self._h, C.byref(v)), "device_outputs")
+        return v
+
+
+def comm_id() -> bytes:
+    lib = load_engine_lib()
+    b = C.create_string_buffer(abi.COMM_ID_BYTES)
+    rc = lib.kwok_comm_id(b)
+    if rc != 0:
+        raise KwokError(rc, "comm_id")
+    return b.raw
+
+
+def finalizer_patch() -> bytes:
+    lib = load_engine_lib()
+    n = C.c_size_t()
+    p = lib.kwok_finalizer_patch(C.byref(n))
+    return p[: n.value]

@@ -1,0 +1,1048 @@
+/*
+ * kwok_oracle.c - CPU ORACLE (test infrastructure only; never linked into or
+ * called by the product).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load it, as the checker / the CPU baseline.
+ *
+ * A plain, sequential C restatement of the reference's per-tick controller
+ * work (hezhizhen/kwok, paths relative to the reference repo root):
+ *   - ipPool Get/Put/Use/new            pkg/kwok/controllers/utils.go:52-117, addIP :37-50
+ *   - heartbeat patch                   node_controller.go:145-204,393-401 + templates/node.heartbeat.tpl
+ *   - node lock / init patch + A.5 test node_controller.go:301-391          + templates/node.status.tpl
+ *   - pod lock / patch + A.4 test       pod_controller.go:205-250,377-439    + templates/pod.status.tpl
+ *   - pod delete / finalizers / release pod_controller.go:155-202,306-343
+ *   - event routing                     node_controller.go:256-270, pod_controller.go:301-343
+ * rendered the way renderer.go:49-89 + sigs.k8s.io/yaml + encoding/json do
+ * for the default templates (sorted keys, compact, HTML-escaped strings).
+ * It uses its own data structures (string-keyed-equivalent hash sets for the
+ * pool, linear scans, libc gmtime_r/snprintf for formatting) and shares only
+ * the event record layout (include/kwok_engine.h) with the product.
+ *
+ * Parity pinning: this file is checked against the tests/golden JSON fixtures, which
+ * tests/golden/make_golden.py derives by executing the reference's own .tpl
+ * files through an independent text/template + YAML->JSON interpreter and the
+ * reference's renderer_test.go known answers (see DESIGN.md "Oracle").
+ *
+ * Deterministic choices where the reference is nondeterministic (DESIGN.md
+ * "Tick contract"): ipPool.Get reuses the LOWEST usable address (reference:
+ * random map order, utils.go:87-91); events are coalesced per tick; pods are
+ * evaluated and IPs assigned in canonical handle order.
+ */
+#include "kwok_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------------------- */
+/* small utilities                                                             */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    char* p;
+    size_t n, cap;
+} buf_t;
+
+static void buf_put(buf_t* b, const char* s, size_t n) {
+    if (b->n + n + 1 > b->cap) {
+        size_t c = b->cap ? b->cap : 4096;
+        while (c < b->n + n + 1) c *= 2;
+        b->p = (char*)realloc(b->p, c);
+        b->cap = c;
+    }
+    memcpy(b->p + b->n, s, n);
+    b->n += n;
+    b->p[b->n] = 0;
+}
+static void buf_s(buf_t* b, const char* s) { buf_put(b, s, strlen(s)); }
+
+/* encoding/json string encoding (HTML-safe, as json.Marshal) */
+static void buf_jstr(buf_t* b, const char* s, size_t n) {
+    static const char hex[] = "0123456789abcdef";
+    buf_put(b, "\"", 1);
+    for (size_t i = 0; i < n; i++) {
+        unsigned char c = (unsigned char)s[i];
+        if (c == '"') buf_s(b, "\\\"");
+        else if (c == '\\') buf_s(b, "\\\\");
+        else if (c == '\n') buf_s(b, "\\n");
+        else if (c == '\r') buf_s(b, "\\r");
+        else if (c == '\t') buf_s(b, "\\t");
+        else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+            char u[6] = {'\\', 'u', '0', '0', hex[c >> 4], hex[c & 15]};
+            buf_put(b, u, 6);
+        } else buf_put(b, (const char*)&c, 1);
+    }
+    buf_put(b, "\"", 1);
+}
+
+static char* xstrndup(const char* s, size_t n) {
+    char* r = (char*)malloc(n + 1);
+    memcpy(r, s, n);
+    r[n] = 0;
+    return r;
+}
+
+/* time.Format(time.RFC3339) of a UTC time (metav1.Time marshals UTC). */
+static void rfc3339(int64_t t, char out[32]) {
+    time_t tt = (time_t)t;
+    struct tm tm;
+    gmtime_r(&tt, &tm);
+    strftime(out, 32, "%Y-%m-%dT%H:%M:%SZ", &tm);
+}
+
+/* net.IP.String() of an IPv4 address */
+static void ip_str(uint32_t ip, char out[16]) {
+    snprintf(out, 16, "%u.%u.%u.%u", ip >> 24, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255);
+}
+
+/* net.ParseIP for canonical dotted quads; returns 0 on failure / empty */
+static int ip_parse(const char* s, size_t n, uint32_t* out) {
+    if (n == 0 || n > 15) return 0;
+    uint32_t v = 0;
+    int parts = 0;
+    size_t i = 0;
+    while (i < n) {
+        uint32_t x = 0;
+        size_t j = i;
+        while (j < n && s[j] >= '0' && s[j] <= '9') x = x * 10 + (uint32_t)(s[j++] - '0');
+        if (j == i || j - i > 3 || x > 255) return 0;
+        v = (v << 8) | x;
+        parts++;
+        if (j < n) {
+            if (s[j] != '.') return 0;
+            j++;
+        }
+        i = j;
+    }
+    if (parts != 4) return 0;
+    *out = v;
+    return 1;
+}
+
+static uint32_t fnv1a32(const char* s, size_t n) {
+    uint32_t h = 0x811C9DC5u;
+    for (size_t i = 0; i < n; i++) {
+        h ^= (unsigned char)s[i];
+        h *= 0x01000193u;
+    }
+    return h;
+}
+
+/* ------------------------------------------------------------------------- */
+/* ipPool (utils.go:52-117).  used/usable are sets of addresses; the          */
+/* reference keys them by the dotted string, which is 1:1 with the address.  */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    uint64_t* keys; /* 0 = empty, 1 = tombstone, addr+2 otherwise */
+    size_t cap, n, live;
+} hset_t;
+
+static size_t hs_slot(const hset_t* h, uint64_t k) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 17) & (h->cap - 1); }
+static int hs_has(const hset_t* h, uint64_t a) {
+    if (!h->cap) return 0;
+    uint64_t k = a + 2;
+    for (size_t i = hs_slot(h, k);; i = (i + 1) & (h->cap - 1)) {
+        if (h->keys[i] == 0) return 0;
+        if (h->keys[i] == k) return 1;
+    }
+}
+static void hs_add(hset_t* h, uint64_t a);
+static void hs_grow(hset_t* h) {
+    hset_t nh = {0};
+    nh.cap = h->cap ? h->cap * 2 : 64;
+    while (nh.cap < 4 * (h->live + 1)) nh.cap *= 2;
+    nh.keys = (uint64_t*)calloc(nh.cap, sizeof(uint64_t));
+    for (size_t i = 0; i < h->cap; i++)
+        if (h->keys[i] > 1) hs_add(&nh, h->keys[i] - 2);
+    free(h->keys);
+    *h = nh;
+}
+static void hs_add(hset_t* h, uint64_t a) {
+    if (hs_has(h, a)) return;
+    if (2 * (h->n + 1) > h->cap) hs_grow(h);
+    uint64_t k = a + 2;
+    size_t i = hs_slot(h, k);
+    while (h->keys[i] > 1) i = (i + 1) & (h->cap - 1);
+    if (h->keys[i] == 0) h->n++;
+    h->keys[i] = k;
+    h->live++;
+}
+static void hs_del(hset_t* h, uint64_t a) {
+    if (!h->cap) return;
+    uint64_t k = a + 2;
+    for (size_t i = hs_slot(h, k);; i = (i + 1) & (h->cap - 1)) {
+        if (h->keys[i] == 0) return;
+        if (h->keys[i] == k) {
+            h->keys[i] = 1;
+            h->live--;
+            return;
+        }
+    }
+}
+
+typedef struct {
+    uint32_t base;       /* parseCIDR keeps the host address of the CIDR string (utils.go:28-35) */
+    uint32_t net, mask;  /* ipnet.Mask */
+    uint64_t index;      /* ipPool.index */
+    hset_t used, usable; /* ipPool.used / ipPool.usable */
+    /* min-heap over usable (lazy deletion) for the lowest-address reuse rule */
+    uint64_t* heap;
+    size_t hn, hcap;
+} pool_t;
+
+static int cidr_contains(const pool_t* p, uint64_t a) { return a <= 0xFFFFFFFFull && ((uint32_t)a & p->mask) == p->net; }
+
+static void heap_push(pool_t* p, uint64_t a) {
+    if (p->hn == p->hcap) {
+        p->hcap = p->hcap ? p->hcap * 2 : 64;
+        p->heap = (uint64_t*)realloc(p->heap, p->hcap * sizeof(uint64_t));
+    }
+    size_t i = p->hn++;
+    p->heap[i] = a;
+    while (i && p->heap[(i - 1) / 2] > p->heap[i]) {
+        uint64_t t = p->heap[i];
+        p->heap[i] = p->heap[(i - 1) / 2];
+        p->heap[(i - 1) / 2] = t;
+        i = (i - 1) / 2;
+    }
+}
+static uint64_t heap_pop(pool_t* p) {
+    uint64_t top = p->heap[0];
+    p->heap[0] = p->heap[--p->hn];
+    size_t i = 0;
+    for (;;) {
+        size_t l = 2 * i + 1, r = l + 1, m = i;
+        if (l < p->hn && p->heap[l] < p->heap[m]) m = l;
+        if (r < p->hn && p->heap[r] < p->heap[m]) m = r;
+        if (m == i) break;
+        uint64_t t = p->heap[i];
+        p->heap[i] = p->heap[m];
+        p->heap[m] = t;
+        i = m;
+    }
+    return top;
+}
+static void usable_add(pool_t* p, uint64_t a) {
+    if (!hs_has(&p->usable, a)) {
+        hs_add(&p->usable, a);
+        heap_push(p, a);
+    }
+}
+
+/* ipPool.new (utils.go:68-81): sequential from base, skip addresses in used */
+static uint64_t pool_new(pool_t* p) {
+    for (;;) {
+        uint64_t ip = (uint64_t)p->base + p->index; /* addIP(cidr.IP, index) */
+        p->index++;
+        if (hs_has(&p->used, ip)) continue;
+        hs_add(&p->used, ip);
+        usable_add(p, ip);
+        return ip;
+    }
+}
+/* ipPool.Get (utils.go:83-98) with the lowest-usable-first reuse rule */
+static uint64_t pool_get(pool_t* p) {
+    uint64_t ip = 0;
+    int have = 0;
+    while (p->usable.live && p->hn) {
+        uint64_t a = heap_pop(p);
+        if (hs_has(&p->usable, a)) {
+            ip = a;
+            have = 1;
+            break;
+        }
+    }
+    if (!have) ip = pool_new(p);
+    hs_del(&p->usable, ip);
+    hs_add(&p->used, ip);
+    return ip;
+}
+/* ipPool.Put (utils.go:100-108) */
+static void pool_put(pool_t* p, uint64_t ip) {
+    if (!cidr_contains(p, ip)) return;
+    hs_del(&p->used, ip);
+    usable_add(p, ip);
+}
+/* ipPool.Use (utils.go:110-117) */
+static void pool_use(pool_t* p, uint64_t ip) {
+    if (!cidr_contains(p, ip)) return;
+    hs_add(&p->used, ip);
+}
+
+/* ------------------------------------------------------------------------- */
+/* engine state                                                                */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int used, exists, managed, lockable, event_lock, conforms, refs, phase;
+    char* name;
+    size_t name_len;
+    char* addresses;   /* compact JSON or NULL */
+    char* allocatable;
+    char* capacity;
+    char* info[KWOK_NI_COUNT];
+} onode_t;
+
+typedef struct {
+    int used, disregard, deleting, status_nonempty, conforms, has_fin, phase, event, delete_pending;
+    int32_t node, spec;
+    int64_t creation;
+    uint32_t host_ip, pod_ip;
+} opod_t;
+
+typedef struct {
+    char** cname;
+    char** cimage;
+    uint32_t nc;
+    char** iname;
+    char** iimage;
+    uint32_t ni;
+    char** gates;
+    uint32_t ng;
+} ospec_t;
+
+struct kwok_oracle {
+    kwok_config cfg;
+    char cidr[64], node_ip_s[16];
+    uint32_t node_ip;
+    uint32_t B, cn, cp, b_lo, b_hi;
+    onode_t* nodes;
+    opod_t* pods;
+    ospec_t* specs;
+    uint32_t n_specs;
+    pool_t pool;
+    char start_s[32];
+    char err[256];
+    /* outputs of the last tick */
+    buf_t arena;
+    int32_t *hb, *ini, *pp, *del;
+    uint64_t *ini_off, *pp_off;
+    uint32_t *ini_len, *pp_len;
+    uint8_t* del_fin;
+    uint32_t n_hb, n_ini, n_pp, n_del, hb_len;
+    uint64_t hb_off;
+};
+
+static int owns(const kwok_oracle* o, uint32_t b) { return b >= o->b_lo && b < o->b_hi; }
+
+int kwok_oracle_create(const kwok_config* cfg, kwok_oracle** out) {
+    *out = NULL;
+    if (!cfg || cfg->abi_version != KWOK_ABI_VERSION || cfg->enable_cni || cfg->custom_templates) return KWOK_EINVAL;
+    if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || !cfg->node_slots_per_bucket || !cfg->pod_slots_per_bucket)
+        return KWOK_EINVAL;
+    int W = cfg->world_size > 0 ? cfg->world_size : 1;
+    if (W > 1 && !cfg->allgather) return KWOK_EINVAL;
+    kwok_oracle* o = (kwok_oracle*)calloc(1, sizeof(*o));
+    o->cfg = *cfg;
+    o->cfg.world_size = W;
+    o->B = cfg->buckets;
+    o->cn = cfg->node_slots_per_bucket;
+    o->cp = cfg->pod_slots_per_bucket;
+    o->b_lo = (uint32_t)((uint64_t)cfg->rank * o->B / W);
+    o->b_hi = (uint32_t)((uint64_t)(cfg->rank + 1) * o->B / W);
+    /* parseCIDR (utils.go:28-35): net.ParseCIDR, then ipnet.IP = the parsed host IP */
+    const char* slash = strchr(cfg->cidr, '/');
+    uint32_t base;
+    if (!slash || !ip_parse(cfg->cidr, (size_t)(slash - cfg->cidr), &base)) {
+        free(o);
+        return KWOK_EDOMAIN;
+    }
+    int plen = atoi(slash + 1);
+    if (plen < 0 || plen > 32) {
+        free(o);
+        return KWOK_EDOMAIN;
+    }
+    o->pool.mask = plen == 0 ? 0 : (uint32_t)(0xFFFFFFFFull << (32 - plen));
+    o->pool.net = base & o->pool.mask;
+    o->pool.base = base;
+    if (!ip_parse(cfg->node_ip, strlen(cfg->node_ip), &o->node_ip)) {
+        free(o);
+        return KWOK_EDOMAIN;
+    }
+    ip_str(o->node_ip, o->node_ip_s);
+    rfc3339(cfg->start_time_unix, o->start_s);
+    o->nodes = (onode_t*)calloc((size_t)o->B * o->cn, sizeof(onode_t));
+    o->pods = (opod_t*)calloc((size_t)o->B * o->cp, sizeof(opod_t));
+    o->specs = (ospec_t*)calloc(cfg->max_pod_specs ? cfg->max_pod_specs : 1024, sizeof(ospec_t));
+    *out = o;
+    return KWOK_OK;
+}
+
+static void free_node_status(onode_t* n) {
+    free(n->addresses);
+    free(n->allocatable);
+    free(n->capacity);
+    n->addresses = n->allocatable = n->capacity = NULL;
+    for (int i = 0; i < KWOK_NI_COUNT; i++) {
+        free(n->info[i]);
+        n->info[i] = NULL;
+    }
+}
+
+void kwok_oracle_destroy(kwok_oracle* o) {
+    if (!o) return;
+    for (size_t i = 0; i < (size_t)o->B * o->cn; i++) {
+        free_node_status(&o->nodes[i]);
+        free(o->nodes[i].name);
+    }
+    for (uint32_t s = 0; s < o->n_specs; s++) {
+        ospec_t* sp = &o->specs[s];
+        for (uint32_t i = 0; i < sp->nc; i++) free(sp->cname[i]), free(sp->cimage[i]);
+        for (uint32_t i = 0; i < sp->ni; i++) free(sp->iname[i]), free(sp->iimage[i]);
+        for (uint32_t i = 0; i < sp->ng; i++) free(sp->gates[i]);
+        free(sp->cname), free(sp->cimage), free(sp->iname), free(sp->iimage), free(sp->gates);
+    }
+    free(o->specs);
+    free(o->nodes);
+    free(o->pods);
+    free(o->pool.used.keys);
+    free(o->pool.usable.keys);
+    free(o->pool.heap);
+    free(o->arena.p);
+    free(o->hb), free(o->ini), free(o->pp), free(o->del);
+    free(o->ini_off), free(o->pp_off), free(o->ini_len), free(o->pp_len), free(o->del_fin);
+    free(o);
+}
+
+const char* kwok_oracle_last_error(const kwok_oracle* o) { return o ? o->err : "null oracle"; }
+
+static char* dupstr(const char* arena, kwok_str s) { return s.len ? xstrndup(arena + s.off, s.len) : NULL; }
+static int streq(const char* a, const char* b) { return strcmp(a ? a : "", b ? b : "") == 0; }
+
+int kwok_oracle_register_pod_spec(kwok_oracle* o, const kwok_pod_spec* s, const char* arena, size_t arena_len,
+                                  int32_t* out_id) {
+    (void)arena_len;
+    ospec_t sp = {0};
+    sp.nc = s->n_containers;
+    sp.ni = s->n_init_containers;
+    sp.ng = s->n_readiness_gates;
+    sp.cname = (char**)calloc(sp.nc + 1, sizeof(char*));
+    sp.cimage = (char**)calloc(sp.nc + 1, sizeof(char*));
+    sp.iname = (char**)calloc(sp.ni + 1, sizeof(char*));
+    sp.iimage = (char**)calloc(sp.ni + 1, sizeof(char*));
+    sp.gates = (char**)calloc(sp.ng + 1, sizeof(char*));
+    for (uint32_t i = 0; i < sp.nc; i++) {
+        sp.cname[i] = xstrndup(arena + s->containers[i].name.off, s->containers[i].name.len);
+        sp.cimage[i] = xstrndup(arena + s->containers[i].image.off, s->containers[i].image.len);
+    }
+    for (uint32_t i = 0; i < sp.ni; i++) {
+        sp.iname[i] = xstrndup(arena + s->init_containers[i].name.off, s->init_containers[i].name.len);
+        sp.iimage[i] = xstrndup(arena + s->init_containers[i].image.off, s->init_containers[i].image.len);
+    }
+    for (uint32_t i = 0; i < sp.ng; i++) sp.gates[i] = xstrndup(arena + s->readiness_gates[i].off, s->readiness_gates[i].len);
+    /* dedupe */
+    for (uint32_t k = 0; k < o->n_specs; k++) {
+        ospec_t* t = &o->specs[k];
+        int same = t->nc == sp.nc && t->ni == sp.ni && t->ng == sp.ng;
+        for (uint32_t i = 0; same && i < sp.nc; i++) same = streq(t->cname[i], sp.cname[i]) && streq(t->cimage[i], sp.cimage[i]);
+        for (uint32_t i = 0; same && i < sp.ni; i++) same = streq(t->iname[i], sp.iname[i]) && streq(t->iimage[i], sp.iimage[i]);
+        for (uint32_t i = 0; same && i < sp.ng; i++) same = streq(t->gates[i], sp.gates[i]);
+        if (same) {
+            for (uint32_t i = 0; i < sp.nc; i++) free(sp.cname[i]), free(sp.cimage[i]);
+            for (uint32_t i = 0; i < sp.ni; i++) free(sp.iname[i]), free(sp.iimage[i]);
+            for (uint32_t i = 0; i < sp.ng; i++) free(sp.gates[i]);
+            free(sp.cname), free(sp.cimage), free(sp.iname), free(sp.iimage), free(sp.gates);
+            *out_id = (int32_t)k;
+            return KWOK_OK;
+        }
+    }
+    uint32_t cap = o->cfg.max_pod_specs ? o->cfg.max_pod_specs : 1024;
+    if (o->n_specs >= cap) return KWOK_EFULL;
+    o->specs[o->n_specs] = sp;
+    *out_id = (int32_t)o->n_specs++;
+    return KWOK_OK;
+}
+
+/* node entry lookup: entries live in bucket fnv1a32(name) & (B-1) */
+static int32_t node_find(kwok_oracle* o, const char* name, size_t n) {
+    uint32_t b = fnv1a32(name, n) & (o->B - 1);
+    for (uint32_t i = 0; i < o->cn; i++) {
+        onode_t* e = &o->nodes[(size_t)b * o->cn + i];
+        if (e->used && e->name_len == n && memcmp(e->name, name, n) == 0) return (int32_t)(b * o->cn + i);
+    }
+    return -1;
+}
+static int32_t node_entry(kwok_oracle* o, const char* name, size_t n, int* st) {
+    int32_t h = node_find(o, name, n);
+    if (h >= 0) return h;
+    uint32_t b = fnv1a32(name, n) & (o->B - 1);
+    if (!owns(o, b)) {
+        *st = KWOK_ENOTMINE;
+        return -1;
+    }
+    for (uint32_t i = 0; i < o->cn; i++) {
+        onode_t* e = &o->nodes[(size_t)b * o->cn + i];
+        if (!e->used) {
+            memset(e, 0, sizeof(*e));
+            e->used = 1;
+            e->name = xstrndup(name, n);
+            e->name_len = n;
+            return (int32_t)(b * o->cn + i);
+        }
+    }
+    *st = KWOK_EFULL;
+    return -1;
+}
+static void node_maybe_free(kwok_oracle* o, int32_t h) {
+    onode_t* e = &o->nodes[h];
+    if (!e->exists && e->refs == 0) {
+        free_node_status(e);
+        free(e->name);
+        memset(e, 0, sizeof(*e));
+    }
+}
+
+/* A.5: configureNode's merge is a no-op iff all template defaults are in place */
+static int node_conforms(const onode_t* n) {
+    const char* ni_arch = n->info[KWOK_NI_ARCHITECTURE];
+    return n->addresses && n->allocatable && n->capacity && n->phase == KWOK_PHASE_RUNNING && ni_arch &&
+           n->info[KWOK_NI_KUBE_PROXY_VERSION] && n->info[KWOK_NI_KUBELET_VERSION] &&
+           n->info[KWOK_NI_OPERATING_SYSTEM] && streq(n->info[KWOK_NI_SYSTEM_UUID], n->info[KWOK_NI_OS_IMAGE]);
+}
+
+int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
+                             int32_t* out_handles, int32_t* out_status) {
+    (void)arena_len;
+    int rejected = 0;
+    for (size_t i = 0; i < n; i++) {
+        const kwok_node_event* e = &ev[i];
+        const char* name = arena + e->name.off;
+        int st = KWOK_OK;
+        int32_t h;
+        if (e->op == KWOK_OP_DELETE) {
+            /* node_controller.go:265-269: Deleted -> nodesSets.Delete */
+            h = node_find(o, name, e->name.len);
+            if (h < 0) {
+                uint32_t b = fnv1a32(name, e->name.len) & (o->B - 1);
+                st = owns(o, b) ? KWOK_ENOTFOUND : KWOK_ENOTMINE;
+            } else {
+                onode_t* nd = &o->nodes[h];
+                nd->exists = nd->managed = nd->event_lock = 0;
+                free_node_status(nd);
+                node_maybe_free(o, h);
+            }
+        } else {
+            h = node_entry(o, name, e->name.len, &st);
+            if (h >= 0) {
+                onode_t* nd = &o->nodes[h];
+                free_node_status(nd);
+                nd->addresses = dupstr(arena, e->addresses);
+                nd->allocatable = dupstr(arena, e->allocatable);
+                nd->capacity = dupstr(arena, e->capacity);
+                for (int k = 0; k < KWOK_NI_COUNT; k++) nd->info[k] = dupstr(arena, e->node_info[k]);
+                nd->phase = e->phase;
+                nd->exists = 1;
+                /* node_controller.go:257-264: needHeartbeat -> Put; needLockNode -> lock */
+                if (e->managed) {
+                    nd->managed = 1;
+                    if (e->lockable) nd->event_lock = 1;
+                }
+                nd->lockable = e->lockable ? 1 : 0;
+                nd->conforms = node_conforms(nd);
+            }
+        }
+        if (out_handles) out_handles[i] = h;
+        if (out_status) out_status[i] = st;
+        if (st != KWOK_OK) rejected++;
+    }
+    return rejected;
+}
+
+int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
+                            int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
+    (void)arena_len;
+    int rejected = 0;
+    for (size_t i = 0; i < n; i++) {
+        const kwok_pod_event* e = &ev[i];
+        int st = KWOK_OK;
+        int32_t h = e->handle;
+        if (out_released) out_released[i] = 0;
+        if (e->op == KWOK_OP_DELETE) {
+            if (h < 0 || (uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
+                st = KWOK_ENOTFOUND;
+            } else {
+                opod_t* p = &o->pods[h];
+                int32_t nh = p->node;
+                uint32_t ip = 0;
+                /* pod_controller.go:329-336: release the event's podIP if the node is managed */
+                if (o->nodes[nh].managed && ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &ip) &&
+                    cidr_contains(&o->pool, ip)) {
+                    pool_put(&o->pool, ip);
+                    if (out_released) out_released[i] = ip;
+                }
+                memset(p, 0, sizeof(*p));
+                o->nodes[nh].refs--;
+                node_maybe_free(o, nh);
+            }
+        } else {
+            opod_t* p;
+            if (h < 0) {
+                int32_t nh = e->node_handle >= 0 ? e->node_handle
+                                                 : node_entry(o, arena + e->node_name.off, e->node_name.len, &st);
+                if (nh >= 0) {
+                    uint32_t b = (uint32_t)nh / o->cn;
+                    h = -1;
+                    for (uint32_t k = 0; k < o->cp; k++)
+                        if (!o->pods[(size_t)b * o->cp + k].used) {
+                            h = (int32_t)(b * o->cp + k);
+                            break;
+                        }
+                    if (h < 0) st = KWOK_EFULL;
+                    else {
+                        memset(&o->pods[h], 0, sizeof(opod_t));
+                        o->pods[h].used = 1;
+                        o->pods[h].node = nh;
+                        o->nodes[nh].refs++;
+                    }
+                }
+            } else if ((uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
+                st = KWOK_ENOTFOUND;
+                h = -1;
+            }
+            if (h >= 0) {
+                p = &o->pods[h];
+                p->disregard = !!(e->flags & KWOK_POD_DISREGARD);
+                p->deleting = !!(e->flags & KWOK_POD_DELETING);
+                p->status_nonempty = !!(e->flags & KWOK_POD_STATUS_NONEMPTY);
+                p->conforms = !!(e->flags & KWOK_POD_CONFORMS);
+                p->has_fin = !!(e->flags & KWOK_POD_HAS_FINALIZERS);
+                p->phase = e->phase;
+                p->spec = e->spec_id;
+                p->creation = e->creation_unix;
+                p->host_ip = p->pod_ip = 0;
+                ip_parse(arena + e->host_ip.off, e->host_ip.len, &p->host_ip);
+                ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &p->pod_ip);
+                int managed = o->nodes[p->node].managed;
+                if (p->deleting) {
+                    if (managed) p->delete_pending = 1; /* pod_controller.go:306-308 */
+                } else if (managed && !p->disregard) {
+                    p->event = 1; /* needLockPod (:252-269) -> lockChan (:318-319) */
+                }
+            }
+        }
+        if (out_handles) out_handles[i] = h;
+        if (out_status) out_status[i] = st;
+        if (st != KWOK_OK) rejected++;
+    }
+    return rejected;
+}
+
+int kwok_oracle_pool_put(kwok_oracle* o, const uint32_t* ips, size_t n) {
+    for (size_t i = 0; i < n; i++) pool_put(&o->pool, ips[i]);
+    return KWOK_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* renderers: the default .tpl files -> YAML -> JSON, for the default templates       */
+/* ------------------------------------------------------------------------- */
+/* node.heartbeat.tpl:1-31: five conditions, keys in sorted JSON order */
+static void render_conditions(buf_t* b, const char* now, const char* start) {
+    static const char* c[5][4] = {
+        {"kubelet is posting ready status", "KubeletReady", "True", "Ready"},
+        {"kubelet has sufficient disk space available", "KubeletHasSufficientDisk", "False", "OutOfDisk"},
+        {"kubelet has sufficient memory available", "KubeletHasSufficientMemory", "False", "MemoryPressure"},
+        {"kubelet has no disk pressure", "KubeletHasNoDiskPressure", "False", "DiskPressure"},
+        {"RouteController created a route", "RouteCreated", "False", "NetworkUnavailable"},
+    };
+    buf_s(b, "[");
+    for (int i = 0; i < 5; i++) {
+        if (i) buf_s(b, ",");
+        buf_s(b, "{\"lastHeartbeatTime\":");
+        buf_jstr(b, now, strlen(now));
+        buf_s(b, ",\"lastTransitionTime\":");
+        buf_jstr(b, start, strlen(start));
+        buf_s(b, ",\"message\":");
+        buf_jstr(b, c[i][0], strlen(c[i][0]));
+        buf_s(b, ",\"reason\":");
+        buf_jstr(b, c[i][1], strlen(c[i][1]));
+        buf_s(b, ",\"status\":");
+        buf_jstr(b, c[i][2], strlen(c[i][2]));
+        buf_s(b, ",\"type\":");
+        buf_jstr(b, c[i][3], strlen(c[i][3]));
+        buf_s(b, "}");
+    }
+    buf_s(b, "]");
+}
+
+/* configureHeartbeatNode (node_controller.go:393-401) */
+static void render_heartbeat(buf_t* b, const char* now, const char* start) {
+    buf_s(b, "{\"status\":{\"conditions\":");
+    render_conditions(b, now, start);
+    buf_s(b, "}}");
+}
+
+/* configureNode patch (node_controller.go:356-391), node.status.tpl + "\n" + node.heartbeat.tpl */
+static void render_node_init(kwok_oracle* o, buf_t* b, const onode_t* n, const char* now) {
+    static const char* dflt[KWOK_NI_COUNT] = {"amd64", "", "", "", "fake", "fake", "", "linux", "", ""};
+    static const char* key[KWOK_NI_COUNT] = {"architecture", "bootID", "containerRuntimeVersion", "kernelVersion",
+                                             "kubeProxyVersion", "kubeletVersion", "machineID", "operatingSystem",
+                                             "osImage", "systemUUID"};
+    static const char* dres = "{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}";
+    buf_s(b, "{\"status\":{\"addresses\":");
+    if (n->addresses) buf_s(b, n->addresses); /* {{ YAML . 1 }} echo: JSON -> YAML -> JSON identity */
+    else {
+        buf_s(b, "[{\"address\":");
+        buf_jstr(b, o->node_ip_s, strlen(o->node_ip_s));
+        buf_s(b, ",\"type\":\"InternalIP\"}]");
+    }
+    buf_s(b, ",\"allocatable\":");
+    buf_s(b, n->allocatable ? n->allocatable : dres);
+    buf_s(b, ",\"capacity\":");
+    buf_s(b, n->capacity ? n->capacity : dres);
+    buf_s(b, ",\"conditions\":");
+    render_conditions(b, now, o->start_s);
+    /* `with .nodeInfo` is always true: NodeSystemInfo is a struct, never omitted */
+    buf_s(b, ",\"nodeInfo\":{");
+    for (int k = 0; k < KWOK_NI_COUNT; k++) {
+        /* node.status.tpl:40: systemUUID is rendered from `with .osImage` */
+        const char* v = n->info[k == KWOK_NI_SYSTEM_UUID ? KWOK_NI_OS_IMAGE : k];
+        if (!v) v = dflt[k];
+        if (k) buf_s(b, ",");
+        buf_jstr(b, key[k], strlen(key[k]));
+        buf_s(b, ":");
+        buf_jstr(b, v, strlen(v));
+    }
+    buf_s(b, "},\"phase\":\"Running\"}}");
+}
+
+/* computePatchData render of pod.status.tpl (pod_controller.go:404-408) */
+static void render_pod(kwok_oracle* o, buf_t* b, const opod_t* p, uint32_t pod_ip) {
+    char st[32], ip[16];
+    rfc3339(p->creation, st); /* $startTime := .metadata.creationTimestamp */
+    const ospec_t* s = &o->specs[p->spec];
+    buf_s(b, "{\"status\":{\"conditions\":[");
+    static const char* ctypes[3] = {"Initialized", "Ready", "ContainersReady"};
+    for (uint32_t i = 0; i < 3 + s->ng; i++) {
+        const char* t = i < 3 ? ctypes[i] : s->gates[i - 3];
+        if (i) buf_s(b, ",");
+        buf_s(b, "{\"lastTransitionTime\":");
+        buf_jstr(b, st, strlen(st));
+        buf_s(b, ",\"status\":\"True\",\"type\":");
+        buf_jstr(b, t, strlen(t));
+        buf_s(b, "}");
+    }
+    buf_s(b, "],\"containerStatuses\":");
+    if (!s->nc) buf_s(b, "null"); /* empty `range` leaves `containerStatuses:` -> null */
+    else {
+        buf_s(b, "[");
+        for (uint32_t i = 0; i < s->nc; i++) {
+            if (i) buf_s(b, ",");
+            buf_s(b, "{\"image\":");
+            buf_jstr(b, s->cimage[i], strlen(s->cimage[i]));
+            buf_s(b, ",\"name\":");
+            buf_jstr(b, s->cname[i], strlen(s->cname[i]));
+            buf_s(b, ",\"ready\":true,\"restartCount\":0,\"state\":{\"running\":{\"startedAt\":");
+            buf_jstr(b, st, strlen(st));
+            buf_s(b, "}}}");
+        }
+        buf_s(b, "]");
+    }
+    if (p->status_nonempty) { /* {{ with .status }} hostIP / podIP */
+        ip_str(p->host_ip ? p->host_ip : o->node_ip, ip);
+        buf_s(b, ",\"hostIP\":");
+        buf_jstr(b, ip, strlen(ip));
+    }
+    buf_s(b, ",\"initContainerStatuses\":");
+    if (!s->ni) buf_s(b, "null");
+    else {
+        buf_s(b, "[");
+        for (uint32_t i = 0; i < s->ni; i++) {
+            if (i) buf_s(b, ",");
+            buf_s(b, "{\"image\":");
+            buf_jstr(b, s->iimage[i], strlen(s->iimage[i]));
+            buf_s(b, ",\"name\":");
+            buf_jstr(b, s->iname[i], strlen(s->iname[i]));
+            buf_s(b, ",\"ready\":true,\"restartCount\":0,\"state\":{\"terminated\":{\"exitCode\":0,\"finishedAt\":");
+            buf_jstr(b, st, strlen(st));
+            buf_s(b, ",\"reason\":\"Completed\",\"startedAt\":");
+            buf_jstr(b, st, strlen(st));
+            buf_s(b, "}}}");
+        }
+        buf_s(b, "]");
+    }
+    buf_s(b, ",\"phase\":\"Running\"");
+    if (p->status_nonempty) {
+        ip_str(pod_ip, ip);
+        buf_s(b, ",\"podIP\":");
+        buf_jstr(b, ip, strlen(ip));
+    }
+    buf_s(b, ",\"startTime\":");
+    buf_jstr(b, st, strlen(st));
+    buf_s(b, "}}");
+}
+
+/* ------------------------------------------------------------------------- */
+/* tick                                                                        */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    uint32_t* v;
+    size_t n, cap;
+} u32vec;
+static void vpush(u32vec* a, uint32_t x) {
+    if (a->n == a->cap) {
+        a->cap = a->cap ? a->cap * 2 : 64;
+        a->v = (uint32_t*)realloc(a->v, a->cap * sizeof(uint32_t));
+    }
+    a->v[a->n++] = x;
+}
+
+#define GROW(ptr, n) ptr = realloc(ptr, ((n) + 1) * sizeof(*(ptr)))
+
+/* exchange header (sharded mode); lists follow */
+typedef struct {
+    uint64_t alloc, n_use, n_rel;
+    uint64_t counters[KWOK_COUNTER_COUNT];
+} xhdr_t;
+
+int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
+    const size_t NN = (size_t)o->B * o->cn, NP = (size_t)o->B * o->cp;
+    char now[32];
+    rfc3339(now_unix, now);
+    uint64_t cnt[KWOK_COUNTER_COUNT] = {0};
+    o->arena.n = 0;
+    o->n_hb = o->n_ini = o->n_pp = o->n_del = 0;
+    u32vec rel = {0}, use = {0}, evals = {0}, locks = {0};
+
+    /* 1. deletions (DeletePods/DeletePod :155-202); the Deleted event releases the IP */
+    for (size_t h = 0; h < NP; h++) {
+        opod_t* p = &o->pods[h];
+        if (!p->used || !p->delete_pending) continue;
+        GROW(o->del, o->n_del);
+        GROW(o->del_fin, o->n_del);
+        o->del[o->n_del] = (int32_t)h;
+        o->del_fin[o->n_del++] = (uint8_t)p->has_fin;
+        cnt[KWOK_CNT_DELETE]++;
+        int32_t nh = p->node;
+        if (o->nodes[nh].managed && p->pod_ip && cidr_contains(&o->pool, p->pod_ip)) vpush(&rel, p->pod_ip);
+        memset(p, 0, sizeof(*p));
+        o->nodes[nh].refs--;
+        node_maybe_free(o, nh);
+    }
+    cnt[KWOK_CNT_RELEASE] = rel.n;
+    /* lock set: heartbeat feedback (every managed lockable node) + event locks */
+    for (size_t h = 0; h < NN; h++) {
+        onode_t* n = &o->nodes[h];
+        if (n->used && n->exists && ((n->managed && n->lockable) || n->event_lock)) vpush(&locks, (uint32_t)h);
+    }
+    /* pods to evaluate: lock events + LockPodsOnNode of locked managed nodes */
+    for (size_t h = 0; h < NP; h++) {
+        opod_t* p = &o->pods[h];
+        if (!p->used) continue;
+        onode_t* n = &o->nodes[p->node];
+        int relock = n->exists && n->managed && ((n->managed && n->lockable) || n->event_lock) && !p->disregard;
+        if (p->event || relock) vpush(&evals, (uint32_t)h);
+    }
+    uint64_t alloc_local = 0;
+    for (size_t i = 0; i < evals.n; i++) {
+        opod_t* p = &o->pods[evals.v[i]];
+        if (p->pod_ip && cidr_contains(&o->pool, p->pod_ip)) vpush(&use, p->pod_ip); /* configurePod :378-382 */
+        if (p->status_nonempty && !p->pod_ip) alloc_local++;
+    }
+    /* counters known before emission (the exchange needs them) */
+    for (size_t h = 0; h < NN; h++) {
+        onode_t* n = &o->nodes[h];
+        if (!n->used) continue;
+        if (n->managed) cnt[KWOK_CNT_HEARTBEAT]++, cnt[KWOK_CNT_NODES_MANAGED]++;
+    }
+    for (size_t i = 0; i < locks.n; i++) {
+        onode_t* n = &o->nodes[locks.v[i]];
+        cnt[KWOK_CNT_LOCK_CHECKED]++;
+        if (!n->conforms) cnt[KWOK_CNT_NODE_INIT]++;
+    }
+    for (size_t h = 0; h < NN; h++) {
+        onode_t* n = &o->nodes[h];
+        int locked = n->used && n->exists && ((n->managed && n->lockable) || n->event_lock);
+        if (n->used && n->managed && (n->conforms || locked)) cnt[KWOK_CNT_NODES_READY]++;
+    }
+    cnt[KWOK_CNT_EVALUATED] = evals.n;
+    cnt[KWOK_CNT_ALLOC] = alloc_local;
+    uint8_t* patched = (uint8_t*)calloc(NP + 1, 1);
+    for (size_t i = 0; i < evals.n; i++) {
+        opod_t* p = &o->pods[evals.v[i]];
+        if (p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip) {
+            cnt[KWOK_CNT_POD_PATCH]++;
+            patched[evals.v[i]] = 1;
+        }
+    }
+    for (size_t h = 0; h < NP; h++) {
+        opod_t* p = &o->pods[h];
+        if (!p->used) continue;
+        cnt[KWOK_CNT_PODS_TOTAL]++;
+        int ph = patched[h] ? KWOK_PHASE_RUNNING : p->phase;
+        if (ph == KWOK_PHASE_PENDING) cnt[KWOK_CNT_PODS_PENDING]++;
+        if (ph == KWOK_PHASE_RUNNING) cnt[KWOK_CNT_PODS_RUNNING]++;
+    }
+    free(patched);
+
+    /* 2. exchange (sharded mode) and the pool phases: Uses, then Puts */
+    uint64_t alloc_before = 0, alloc_after = 0;
+    uint64_t fleet[KWOK_COUNTER_COUNT];
+    memcpy(fleet, cnt, sizeof(fleet));
+    int W = o->cfg.world_size;
+    if (W > 1) {
+        size_t my_bytes = sizeof(xhdr_t) + 4 * (use.n + rel.n);
+        /* step 1: headers (sizes); step 2: padded lists */
+        xhdr_t hdr = {alloc_local, use.n, rel.n, {0}};
+        memcpy(hdr.counters, cnt, sizeof(cnt));
+        xhdr_t* all = (xhdr_t*)calloc((size_t)W, sizeof(xhdr_t));
+        if (o->cfg.allgather(o->cfg.allgather_user, &hdr, sizeof(hdr), all)) return KWOK_ECOMM;
+        size_t maxl = 0;
+        for (int r = 0; r < W; r++) {
+            size_t l = all[r].n_use + all[r].n_rel;
+            if (l > maxl) maxl = l;
+        }
+        (void)my_bytes;
+        uint32_t* mine = (uint32_t*)calloc(maxl + 1, 4);
+        memcpy(mine, use.v, 4 * use.n);
+        memcpy(mine + use.n, rel.v, 4 * rel.n);
+        uint32_t* lists = (uint32_t*)calloc((size_t)W * (maxl + 1), 4);
+        if (o->cfg.allgather(o->cfg.allgather_user, mine, 4 * (maxl + 1), lists)) return KWOK_ECOMM;
+        memset(fleet, 0, sizeof(fleet));
+        for (int r = 0; r < W; r++) {
+            for (int k = 0; k < KWOK_COUNTER_COUNT; k++) fleet[k] += all[r].counters[k];
+            if (r < o->cfg.rank) alloc_before += all[r].alloc;
+            if (r > o->cfg.rank) alloc_after += all[r].alloc;
+        }
+        for (int r = 0; r < W; r++)
+            for (uint64_t k = 0; k < all[r].n_use; k++) pool_use(&o->pool, lists[(size_t)r * (maxl + 1) + k]);
+        for (int r = 0; r < W; r++)
+            for (uint64_t k = 0; k < all[r].n_rel; k++)
+                pool_put(&o->pool, lists[(size_t)r * (maxl + 1) + all[r].n_use + k]);
+        free(all), free(mine), free(lists);
+    } else {
+        for (size_t i = 0; i < use.n; i++) pool_use(&o->pool, use.v[i]);
+        for (size_t i = 0; i < rel.n; i++) pool_put(&o->pool, rel.v[i]);
+    }
+
+    /* 3. heartbeat: every managed node (canonical order), identical bodies */
+    buf_t hbb = {0};
+    render_heartbeat(&hbb, now, o->start_s);
+    o->hb_len = (uint32_t)hbb.n;
+    o->hb_off = o->arena.n;
+    for (size_t h = 0; h < NN; h++) {
+        onode_t* n = &o->nodes[h];
+        if (!n->used || !n->managed) continue;
+        GROW(o->hb, o->n_hb);
+        o->hb[o->n_hb++] = (int32_t)h;
+        buf_put(&o->arena, hbb.p, hbb.n);
+    }
+    free(hbb.p);
+
+    /* 4. node lock (LockNode / configureNode) */
+    for (size_t i = 0; i < locks.n; i++) {
+        onode_t* n = &o->nodes[locks.v[i]];
+        if (!n->conforms) {
+            GROW(o->ini, o->n_ini);
+            GROW(o->ini_off, o->n_ini);
+            GROW(o->ini_len, o->n_ini);
+            size_t off = o->arena.n;
+            render_node_init(o, &o->arena, n, now);
+            o->ini[o->n_ini] = (int32_t)locks.v[i];
+            o->ini_off[o->n_ini] = off;
+            o->ini_len[o->n_ini++] = (uint32_t)(o->arena.n - off);
+            /* the apiserver applies the patch: defaults now in place */
+            static const char* dflt[KWOK_NI_COUNT] = {"amd64", "", "", "", "fake", "fake", "", "linux", "", ""};
+            for (int k = 0; k < KWOK_NI_COUNT; k++)
+                if (!n->info[k] && dflt[k][0]) n->info[k] = xstrndup(dflt[k], strlen(dflt[k]));
+            free(n->info[KWOK_NI_SYSTEM_UUID]);
+            n->info[KWOK_NI_SYSTEM_UUID] =
+                n->info[KWOK_NI_OS_IMAGE] ? xstrndup(n->info[KWOK_NI_OS_IMAGE], strlen(n->info[KWOK_NI_OS_IMAGE])) : NULL;
+            if (!n->addresses) {
+                buf_t a = {0};
+                buf_s(&a, "[{\"address\":");
+                buf_jstr(&a, o->node_ip_s, strlen(o->node_ip_s));
+                buf_s(&a, ",\"type\":\"InternalIP\"}]");
+                n->addresses = a.p;
+            }
+            if (!n->allocatable) n->allocatable = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
+            if (!n->capacity) n->capacity = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
+            n->phase = KWOK_PHASE_RUNNING;
+            n->conforms = 1;
+        }
+    }
+    for (size_t h = 0; h < NN; h++) o->nodes[h].event_lock = 0;
+
+    /* 5. pod lock in canonical order; Gets of lower ranks come first */
+    for (uint64_t k = 0; k < alloc_before; k++) (void)pool_get(&o->pool);
+    for (size_t i = 0; i < evals.n; i++) {
+        opod_t* p = &o->pods[evals.v[i]];
+        uint32_t ip = p->pod_ip;
+        /* `{{ with .podIP }} . {{ else }} PodIP {{ end }}` inside `{{ with .status }}` */
+        if (p->status_nonempty && !p->pod_ip) ip = (uint32_t)pool_get(&o->pool);
+        int need = p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip;
+        if (need) {
+            GROW(o->pp, o->n_pp);
+            GROW(o->pp_off, o->n_pp);
+            GROW(o->pp_len, o->n_pp);
+            size_t off = o->arena.n;
+            render_pod(o, &o->arena, p, ip);
+            o->pp[o->n_pp] = (int32_t)evals.v[i];
+            o->pp_off[o->n_pp] = off;
+            o->pp_len[o->n_pp++] = (uint32_t)(o->arena.n - off);
+            if (p->status_nonempty) {
+                if (!p->host_ip) p->host_ip = o->node_ip;
+                p->pod_ip = ip;
+            }
+            p->phase = KWOK_PHASE_RUNNING;
+            p->conforms = 1;
+            p->status_nonempty = 1;
+        }
+    }
+    for (uint64_t k = 0; k < alloc_after; k++) (void)pool_get(&o->pool);
+    for (size_t h = 0; h < NP; h++) o->pods[h].event = 0, o->pods[h].delete_pending &= o->pods[h].used;
+
+    free(rel.v), free(use.v), free(evals.v), free(locks.v);
+    if (res) {
+        memset(res, 0, sizeof(*res));
+        res->n_heartbeat = o->n_hb;
+        res->heartbeat_len = o->hb_len;
+        res->heartbeat_stride = o->hb_len;
+        res->n_node_init = o->n_ini;
+        res->n_pod_patch = o->n_pp;
+        res->n_delete = o->n_del;
+        res->arena_bytes = o->arena.n;
+        memcpy(res->counters, fleet, sizeof(fleet));
+        memcpy(res->local_counters, cnt, sizeof(cnt));
+    }
+    return KWOK_OK;
+}
+
+int kwok_oracle_read_outputs(kwok_oracle* o, kwok_outputs* out) {
+    if (out->heartbeat_nodes) memcpy(out->heartbeat_nodes, o->hb, 4 * o->n_hb);
+    out->heartbeat_off = o->hb_off;
+    if (out->node_init_nodes) memcpy(out->node_init_nodes, o->ini, 4 * o->n_ini);
+    if (out->node_init_off) memcpy(out->node_init_off, o->ini_off, 8 * o->n_ini);
+    if (out->node_init_len) memcpy(out->node_init_len, o->ini_len, 4 * o->n_ini);
+    if (out->pod_patch_pods) memcpy(out->pod_patch_pods, o->pp, 4 * o->n_pp);
+    if (out->pod_patch_off) memcpy(out->pod_patch_off, o->pp_off, 8 * o->n_pp);
+    if (out->pod_patch_len) memcpy(out->pod_patch_len, o->pp_len, 4 * o->n_pp);
+    if (out->delete_pods) memcpy(out->delete_pods, o->del, 4 * o->n_del);
+    if (out->delete_has_finalizers) memcpy(out->delete_has_finalizers, o->del_fin, o->n_del);
+    if (out->arena) {
+        if (out->arena_cap < o->arena.n) return KWOK_EINVAL;
+        memcpy(out->arena, o->arena.p, o->arena.n);
+    }
+    return KWOK_OK;
+}
+
+int kwok_oracle_node_has(kwok_oracle* o, const char* name, size_t len) {
+    int32_t h = node_find(o, name, len);
+    return h >= 0 && o->nodes[h].managed;
+}
+
+uint64_t kwok_oracle_node_size(kwok_oracle* o) {
+    uint64_t n = 0;
+    for (size_t h = 0; h < (size_t)o->B * o->cn; h++) n += o->nodes[h].used && o->nodes[h].managed;
+    return n;
+}
+
+int kwok_oracle_dump_pods(kwok_oracle* o, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase,
+                          uint32_t* host_ip, uint32_t* pod_ip) {
+    for (uint32_t i = 0; i < count; i++) {
+        size_t h = (size_t)first + i;
+        const opod_t* p = h < (size_t)o->B * o->cp ? &o->pods[h] : NULL;
+        if (used) used[i] = p ? (uint8_t)p->used : 0;
+        if (phase) phase[i] = p && p->used ? (uint8_t)p->phase : 0;
+        if (host_ip) host_ip[i] = p && p->used ? p->host_ip : 0;
+        if (pod_ip) pod_ip[i] = p && p->used ? p->pod_ip : 0;
+    }
+    return KWOK_OK;
+}
