@@ -1,0 +1,986 @@
+// engine.cpp - host runtime behind include/kwok_engine.h.
+//
+// Owns one GPU: device SoA state, the output arena, the replicated ipPool
+// bitmaps and (multi-rank) an RCCL communicator.  Host-side it keeps only what
+// the slot policy needs (names -> node slots, slot occupancy, refcounts); all
+// per-object status lives in HBM and is advanced by the kernels of one tick.
+//
+// Reference interfaces replaced (hezhizhen/kwok, pkg/kwok/controllers):
+//   NewController / NewNodeController / NewPodController  controller.go:80-152,
+//                                                          node_controller.go:79-117, pod_controller.go:84-128
+//   WatchNodes/ListNodes, WatchPods/ListPods event switch node_controller.go:256-295, pod_controller.go:301-367
+//   KeepNodeHeartbeat, LockNodes, LockPods, DeletePods    node_controller.go:175-204,301-354, pod_controller.go:155-250
+//   ipPool                                                utils.go:52-117
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kwok_engine.h"
+#include "device.h"
+#include "kernels.h"
+#include "templates.h"
+
+using namespace kwok;
+
+namespace {
+
+uint32_t fnv1a32(const char* s, size_t n) {
+    uint32_t h = 0x811C9DC5u;
+    for (size_t i = 0; i < n; i++) {
+        h ^= (unsigned char)s[i];
+        h *= 0x01000193u;
+    }
+    return h;
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct kwok_engine {
+    kwok_config cfg{};
+    std::string err;
+    int W = 1, rank = 0, dev = 0;
+    uint32_t B = 0, Cn = 0, Cp = 0, b_lo = 0, b_hi = 0, nb = 0, NL = 0, PL = 0;
+    PoolGeom pool{};
+    uint32_t node_ip = 0;
+    std::string node_ip_s;
+    int64_t start = 0;
+    hipStream_t st = nullptr;
+    DevState S{};
+
+    // ---- host mirrors (slot policy) ----
+    struct HNode {
+        std::string name;
+        uint8_t used = 0, exists = 0, managed = 0, lockable = 0;
+        uint32_t refs = 0;
+    };
+    std::vector<HNode> nodes;                        // [NL]
+    std::unordered_map<std::string, uint32_t> node_by_name;  // -> local slot
+    std::vector<uint64_t> node_bits;                 // occupancy bitset per bucket
+    uint64_t n_managed = 0;
+    std::vector<uint8_t> pod_used, pod_delpend;      // [PL]
+    std::vector<uint16_t> pod_node;                  // [PL] local node index in bucket
+    std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
+    std::vector<uint32_t> pending_del;
+
+    // ---- batch staging ----
+    std::vector<NodeOp> nops;
+    std::vector<PodOp> pops;
+    std::vector<uint32_t> node_stamp, pod_stamp, node_opi, pod_opi;
+    uint32_t gen = 0;
+    std::vector<uint32_t> puts;
+    void* pinned = nullptr;
+    size_t pinned_cap = 0;
+    void* d_ops = nullptr;
+    size_t d_ops_cap = 0;
+
+    // ---- specs / blobs ----
+    std::unordered_map<std::string, int32_t> spec_ids;
+    std::vector<SpecDesc> specs_h;
+    std::string spec_bytes_h, spec_kinds_h;
+    DevBuf<SpecDesc> d_specs;
+    DevBuf<uint8_t> d_spec_bytes, d_spec_kinds;
+    uint32_t max_pod_len = 0;
+    std::unordered_map<std::string, uint64_t> blob_ids;
+    std::string blob_h;
+    DevBuf<uint8_t> d_blob;
+    uint32_t max_init_len = 0;
+
+    // ---- tick ----
+    TickHdr* hdr_h = nullptr;  // pinned
+    bool have_tick = false;
+    ListDesc* d_ld_local = nullptr;
+    ListDesc* d_ld = nullptr;  // [W] or scratch
+    ncclComm_t comm = nullptr;
+    XMsg* d_xall = nullptr;
+    XMsg* h_xall = nullptr;  // pinned
+    uint32_t* d_xsend = nullptr;
+    uint32_t* d_xrecv = nullptr;
+    size_t xlist_cap = 0;
+    uint32_t hb_grid = 2048;
+
+    int fail(int code, const char* fmt, ...) {
+        char b[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(b, sizeof b, fmt, ap);
+        va_end(ap);
+        err = b;
+        return code;
+    }
+    bool owns(uint32_t bucket) const { return bucket >= b_lo && bucket < b_hi; }
+};
+
+#define HIPCHK(e, x)                                                                              \
+    do {                                                                                          \
+        hipError_t _r = (x);                                                                      \
+        if (_r != hipSuccess) return (e)->fail(KWOK_EDEVICE, "%s: %s", #x, hipGetErrorString(_r)); \
+    } while (0)
+
+namespace {
+
+template <class T>
+int dalloc(kwok_engine* e, T** p, size_t n) {
+    size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    hipError_t r = hipMalloc((void**)p, bytes);
+    if (r != hipSuccess) return e->fail(KWOK_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(r));
+    r = hipMemsetAsync(*p, 0, bytes, e->st);
+    if (r != hipSuccess) return e->fail(KWOK_EDEVICE, "hipMemset: %s", hipGetErrorString(r));
+    return KWOK_OK;
+}
+
+// grow a device buffer to hold `bytes` (keeps contents)
+template <class T>
+int dgrow(kwok_engine* e, DevBuf<T>& b, size_t n) {
+    if (n <= b.n) return KWOK_OK;
+    size_t cap = std::max<size_t>(n, b.n * 2 + 64);
+    T* p = nullptr;
+    if (hipMalloc((void**)&p, cap * sizeof(T)) != hipSuccess) return e->fail(KWOK_ENOMEM, "grow %zu", cap * sizeof(T));
+    if (b.p) {
+        HIPCHK(e, hipMemcpyAsync(p, b.p, b.n * sizeof(T), hipMemcpyDeviceToDevice, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+        (void)hipFree(b.p);
+    }
+    b.p = p;
+    b.n = cap;
+    return KWOK_OK;
+}
+
+int ensure_pinned(kwok_engine* e, size_t bytes) {
+    if (bytes <= e->pinned_cap) return KWOK_OK;
+    if (e->pinned) (void)hipHostFree(e->pinned);
+    e->pinned_cap = std::max(bytes, e->pinned_cap * 2);
+    if (hipHostMalloc(&e->pinned, e->pinned_cap, hipHostMallocDefault) != hipSuccess)
+        return e->fail(KWOK_ENOMEM, "pinned %zu", e->pinned_cap);
+    if (e->d_ops_cap < e->pinned_cap) {
+        if (e->d_ops) (void)hipFree(e->d_ops);
+        e->d_ops_cap = e->pinned_cap;
+        if (hipMalloc(&e->d_ops, e->d_ops_cap) != hipSuccess) return e->fail(KWOK_ENOMEM, "ops %zu", e->d_ops_cap);
+    }
+    return KWOK_OK;
+}
+
+// first free slot in a bucket's occupancy bitset (lowest index: canonical policy)
+int32_t first_free(std::vector<uint64_t>& bits, uint32_t bucket_local, uint32_t cap) {
+    uint32_t wpb = (cap + 63) / 64;
+    uint64_t* w = bits.data() + (size_t)bucket_local * wpb;
+    for (uint32_t i = 0; i < wpb; i++) {
+        uint64_t free = ~w[i];
+        if (i == wpb - 1 && (cap & 63)) free &= (1ull << (cap & 63)) - 1;
+        if (free) return (int32_t)(i * 64 + __builtin_ctzll(free));
+    }
+    return -1;
+}
+void set_bit(std::vector<uint64_t>& bits, uint32_t cap, uint32_t bucket_local, uint32_t idx, bool v) {
+    uint32_t wpb = (cap + 63) / 64;
+    uint64_t& w = bits[(size_t)bucket_local * wpb + idx / 64];
+    if (v) w |= 1ull << (idx & 63);
+    else w &= ~(1ull << (idx & 63));
+}
+
+// ---- per-batch op coalescing: ops for the same slot compose in order ----
+void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
+    if (e->node_stamp[slot] == e->gen) {
+        NodeOp& o = e->nops[e->node_opi[slot]];
+        o.or_bits = (uint8_t)((o.or_bits & and_mask) | or_bits);
+        o.and_mask = (uint8_t)(o.and_mask & and_mask);
+        if (set_blob) o.set_blob = 1, o.blob = blob;
+        return;
+    }
+    e->node_stamp[slot] = e->gen;
+    e->node_opi[slot] = (uint32_t)e->nops.size();
+    NodeOp o{};
+    o.slot = slot;
+    o.and_mask = and_mask;
+    o.or_bits = or_bits;
+    o.set_blob = set_blob;
+    o.blob = blob;
+    e->nops.push_back(o);
+}
+void pod_op(kwok_engine* e, const PodOp& in) {
+    uint32_t slot = in.slot;
+    if (e->pod_stamp[slot] == e->gen) {
+        PodOp& o = e->pops[e->pod_opi[slot]];
+        o.bits = (uint16_t)((o.bits & in.keep_mask) | in.bits);
+        o.keep_mask = (uint16_t)(o.keep_mask & in.keep_mask);
+        if (in.set_fields) {
+            o.set_fields = 1;
+            o.node = in.node, o.spec = in.spec, o.ctime = in.ctime, o.host_ip = in.host_ip, o.pod_ip = in.pod_ip;
+        }
+        return;
+    }
+    e->pod_stamp[slot] = e->gen;
+    e->pod_opi[slot] = (uint32_t)e->pops.size();
+    e->pops.push_back(in);
+}
+
+int flush_ops(kwok_engine* e) {
+    size_t nb = e->nops.size() * sizeof(NodeOp), pb = e->pops.size() * sizeof(PodOp), ub = e->puts.size() * 4;
+    size_t total = ((nb + 255) & ~(size_t)255) + ((pb + 255) & ~(size_t)255) + ub + 256;
+    int rc = ensure_pinned(e, total);
+    if (rc) return rc;
+    char* h = (char*)e->pinned;
+    size_t po = (nb + 255) & ~(size_t)255, uo = po + ((pb + 255) & ~(size_t)255);
+    memcpy(h, e->nops.data(), nb);
+    memcpy(h + po, e->pops.data(), pb);
+    memcpy(h + uo, e->puts.data(), ub);
+    char* d = (char*)e->d_ops;
+    HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
+    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)e->nops.size(), (const PodOp*)(d + po),
+                     (uint32_t)e->pops.size(), e->st);
+    if (!e->puts.empty()) {
+        // ingest-time Puts (Deleted events, pod_controller.go:329-336)
+        ListDesc ld{};
+        ld.rel = (const uint32_t*)(d + uo);
+        ld.n_rel = (uint32_t)e->puts.size();
+        HIPCHK(e, hipMemcpyAsync(e->d_ld, &ld, sizeof ld, hipMemcpyHostToDevice, e->st));
+        launch_pool_lists(e->S, e->d_ld, 1, false, ld.n_rel, e->st);
+    }
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    e->nops.clear();
+    e->pops.clear();
+    e->puts.clear();
+    return KWOK_OK;
+}
+
+int upload_specs(kwok_engine* e) {
+    int rc;
+    if ((rc = dgrow(e, e->d_specs, e->specs_h.size()))) return rc;
+    if ((rc = dgrow(e, e->d_spec_bytes, e->spec_bytes_h.size()))) return rc;
+    if ((rc = dgrow(e, e->d_spec_kinds, e->spec_kinds_h.size()))) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->d_specs.p, e->specs_h.data(), e->specs_h.size() * sizeof(SpecDesc),
+                             hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->d_spec_bytes.p, e->spec_bytes_h.data(), e->spec_bytes_h.size(), hipMemcpyHostToDevice,
+                             e->st));
+    HIPCHK(e, hipMemcpyAsync(e->d_spec_kinds.p, e->spec_kinds_h.data(), e->spec_kinds_h.size(),
+                             hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    e->S.specs = e->d_specs.p;
+    e->S.spec_bytes = e->d_spec_bytes.p;
+    e->S.spec_kinds = e->d_spec_kinds.p;
+    return KWOK_OK;
+}
+
+// the output arena must hold the worst case of one tick
+int size_arena(kwok_engine* e) {
+    uint64_t need = (uint64_t)e->NL * HB_STRIDE + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
+                    (uint64_t)e->PL * e->max_pod_len + 256;
+    if (need <= e->S.arena_cap) return KWOK_OK;
+    need = std::max<uint64_t>(need, e->S.arena_cap + e->S.arena_cap / 2);
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    if (e->S.arena) (void)hipFree(e->S.arena);
+    e->S.arena = nullptr;
+    e->S.arena_cap = 0;
+    if (hipMalloc((void**)&e->S.arena, need) != hipSuccess) return e->fail(KWOK_ENOMEM, "arena %llu", (unsigned long long)need);
+    e->S.arena_cap = need;
+    return KWOK_OK;
+}
+
+uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
+    std::string key = b.pre + '\x01' + b.post;
+    auto it = e->blob_ids.find(key);
+    if (it != e->blob_ids.end()) return it->second;
+    if (b.pre.size() > 0xFFFF || b.post.size() > 0xFFFF || e->blob_h.size() > 0xFFFFFFFFull - 0x20000) {
+        *rc = KWOK_EDOMAIN;
+        return 0;
+    }
+    uint64_t off = e->blob_h.size();
+    e->blob_h += b.pre;
+    e->blob_h += b.post;
+    uint64_t word = off | ((uint64_t)b.pre.size() << 32) | ((uint64_t)b.post.size() << 48);
+    e->blob_ids.emplace(key, word);
+    uint32_t ilen = 11u + (uint32_t)b.pre.size() + 14u + CONDS_LEN + 1u + (uint32_t)b.post.size() + 2u;
+    e->max_init_len = std::max(e->max_init_len, ilen);
+    size_t old = e->d_blob.n;
+    if ((*rc = dgrow(e, e->d_blob, e->blob_h.size()))) return 0;
+    (void)old;
+    (void)hipMemcpyAsync(e->d_blob.p + off, e->blob_h.data() + off, b.pre.size() + b.post.size(), hipMemcpyHostToDevice,
+                   e->st);
+    e->S.blob = e->d_blob.p;
+    return word;
+}
+
+bool node_conforms(const kwok_node_event& ev, const std::string info[10]) {
+    // A.5: configureNode's merged status equals the original iff no default applies
+    return ev.addresses.len && ev.allocatable.len && ev.capacity.len && ev.phase == KWOK_PHASE_RUNNING &&
+           !info[KWOK_NI_ARCHITECTURE].empty() && !info[KWOK_NI_KUBE_PROXY_VERSION].empty() &&
+           !info[KWOK_NI_KUBELET_VERSION].empty() && !info[KWOK_NI_OPERATING_SYSTEM].empty() &&
+           info[KWOK_NI_SYSTEM_UUID] == info[KWOK_NI_OS_IMAGE];
+}
+
+void free_node_if_unused(kwok_engine* e, uint32_t slot) {
+    auto& n = e->nodes[slot];
+    if (n.used && !n.exists && n.refs == 0) {
+        e->node_by_name.erase(n.name);
+        set_bit(e->node_bits, e->Cn, slot / e->Cn, slot % e->Cn, false);
+        n = kwok_engine::HNode();
+        node_op(e, slot, 0, 0, true, 0);
+    }
+}
+
+// find (or create a placeholder for) the node entry of `name`
+int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_t* out) {
+    std::string key(name, len);
+    auto it = e->node_by_name.find(key);
+    if (it != e->node_by_name.end()) {
+        *out = it->second;
+        return KWOK_OK;
+    }
+    uint32_t b = fnv1a32(name, len) & (e->B - 1);
+    if (!e->owns(b)) return KWOK_ENOTMINE;
+    if (!create) return KWOK_ENOTFOUND;
+    int32_t idx = first_free(e->node_bits, b - e->b_lo, e->Cn);
+    if (idx < 0) return KWOK_EFULL;
+    uint32_t slot = (b - e->b_lo) * e->Cn + (uint32_t)idx;
+    set_bit(e->node_bits, e->Cn, b - e->b_lo, (uint32_t)idx, true);
+    auto& n = e->nodes[slot];
+    n = kwok_engine::HNode();
+    n.used = 1;
+    n.name = key;
+    e->node_by_name.emplace(key, slot);
+    *out = slot;
+    return KWOK_OK;
+}
+
+int parse_opt_ip(const char* arena, kwok_str s, uint32_t* ip) {
+    *ip = 0;
+    if (!s.len) return KWOK_OK;
+    if (!parse_ipv4(arena + s.off, s.len, ip) || *ip == 0) return KWOK_EDOMAIN;
+    return KWOK_OK;
+}
+
+int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
+    if (e->comm) {
+        ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, e->comm, e->st);
+        if (r != ncclSuccess) return e->fail(KWOK_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
+        return KWOK_OK;
+    }
+    // host-memory exchange through the caller's allgather
+    std::vector<char> hs(bytes), hr(bytes * e->W);
+    HIPCHK(e, hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    if (e->cfg.allgather(e->cfg.allgather_user, hs.data(), bytes, hr.data()))
+        return e->fail(KWOK_ECOMM, "allgather callback failed");
+    HIPCHK(e, hipMemcpyAsync(recv, hr.data(), bytes * e->W, hipMemcpyHostToDevice, e->st));
+    return KWOK_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+uint32_t kwok_abi_version(void) { return KWOK_ABI_VERSION; }
+
+int kwok_comm_id(uint8_t out[KWOK_COMM_ID_BYTES]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return KWOK_ECOMM;
+    static_assert(sizeof(id) <= KWOK_COMM_ID_BYTES, "comm id size");
+    memset(out, 0, KWOK_COMM_ID_BYTES);
+    memcpy(out, &id, sizeof(id));
+    return KWOK_OK;
+}
+
+const char* kwok_finalizer_patch(size_t* len) {
+    static const char p[] = "{\"metadata\":{\"finalizers\":null}}";  // pod_controller.go:45
+    if (len) *len = sizeof(p) - 1;
+    return p;
+}
+
+uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets) { return fnv1a32(name, len) & (buckets - 1); }
+int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world) {
+    return (int32_t)(((uint64_t)bucket * (uint64_t)world) / buckets);
+}
+
+const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+void kwok_engine_destroy(kwok_engine* e) {
+    if (!e) return;
+    if (e->st) (void)hipStreamSynchronize(e->st);
+    void* ptrs[] = {e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
+                    e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
+                    e->S.pool_blk, e->S.pool_blk_base, e->S.alloc_addr, (void*)e->S.hb_static,
+                    (void*)e->S.hb_kind, e->S.hb_tmpl, e->S.tiles, e->S.tile_base, e->S.hdr, e->S.xmsg,
+                    e->S.use_list, e->S.rel_list, e->S.arena, e->S.hb_nodes, e->S.init_nodes, e->S.init_off,
+                    e->S.init_len, e->S.pp_pods, e->S.pp_off, e->S.pp_len, e->S.del_pods, e->S.del_fin,
+                    e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops, e->d_ld_local,
+                    e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (e->hdr_h) (void)hipHostFree(e->hdr_h);
+    if (e->h_xall) (void)hipHostFree(e->h_xall);
+    if (e->pinned) (void)hipHostFree(e->pinned);
+    if (e->comm) ncclCommDestroy(e->comm);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    delete e;
+}
+
+int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
+    if (!out) return KWOK_EINVAL;
+    *out = nullptr;
+    if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
+    if (cfg->enable_cni || cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates, no CNI
+    if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
+        !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
+        !cfg->pod_slots_per_bucket)
+        return KWOK_EINVAL;
+    int W = cfg->world_size > 0 ? cfg->world_size : 1;
+    if (cfg->rank < 0 || cfg->rank >= W || (W > 1 && !cfg->comm_id && !cfg->allgather) || (uint32_t)W > cfg->buckets)
+        return KWOK_EINVAL;
+    kwok_engine* e = new kwok_engine();
+    e->cfg = *cfg;
+    e->W = W;
+    e->rank = cfg->rank;
+    e->dev = cfg->device;
+    e->B = cfg->buckets;
+    e->Cn = cfg->node_slots_per_bucket;
+    e->Cp = cfg->pod_slots_per_bucket;
+    e->b_lo = (uint32_t)((uint64_t)cfg->rank * e->B / W);
+    e->b_hi = (uint32_t)((uint64_t)(cfg->rank + 1) * e->B / W);
+    // kwok_rank_of_bucket must agree with [b_lo, b_hi)
+    e->nb = e->b_hi - e->b_lo;
+    e->NL = e->nb * e->Cn;
+    e->PL = e->nb * e->Cp;
+    e->start = cfg->start_time_unix;
+    auto bail = [&](int rc) {
+        kwok_engine_destroy(e);
+        return rc;
+    };
+    // parseCIDR (utils.go:28-35): keep the host IP of the CIDR string as the pool base
+    if (!cfg->cidr || !cfg->node_ip) return bail(KWOK_EINVAL);
+    const char* slash = strchr(cfg->cidr, '/');
+    uint32_t base = 0;
+    if (!slash || !parse_ipv4(cfg->cidr, (size_t)(slash - cfg->cidr), &base)) return bail(KWOK_EDOMAIN);
+    int plen = atoi(slash + 1);
+    if (plen < 8 || plen > 32) return bail(KWOK_EDOMAIN);  // pool bitmaps sized for >= /8
+    uint32_t mask = plen == 32 ? 0xFFFFFFFFu : (uint32_t)(0xFFFFFFFFull << (32 - plen));
+    e->pool.net = base & mask;
+    e->pool.base = base;
+    e->pool.size = 1ull << (32 - plen);
+    e->pool.words = (e->pool.size + 63) / 64;
+    if (!parse_ipv4(cfg->node_ip, strlen(cfg->node_ip), &e->node_ip) || !e->node_ip) return bail(KWOK_EDOMAIN);
+    e->node_ip_s = format_ipv4(e->node_ip);
+    if (cfg->start_time_unix < 0 || cfg->start_time_unix > 0xFFFFFFFFll) return bail(KWOK_EDOMAIN);
+
+    if (hipSetDevice(e->dev) != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "hipSetDevice(%d)", e->dev));
+    if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return bail(KWOK_EDEVICE);
+    DevState& S = e->S;
+    S.n_node_slots = e->NL;
+    S.n_pod_slots = e->PL;
+    S.node_tiles = (e->NL + NODE_TILE - 1) / NODE_TILE;
+    S.pod_tiles = (e->PL + POD_TILE - 1) / POD_TILE;
+    S.cn = e->Cn;
+    S.cp = e->Cp;
+    S.node_handle_base = (int32_t)(e->b_lo * e->Cn);
+    S.pod_handle_base = (int32_t)(e->b_lo * e->Cp);
+    S.pool = e->pool;
+    S.node_ip = e->node_ip;
+    const uint32_t T = S.node_tiles + S.pod_tiles;
+    const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
+    // node/pod tiles round NL/PL up: allocate whole tiles so vector loads stay in bounds
+    const size_t NLa = (size_t)S.node_tiles * NODE_TILE, PLa = (size_t)S.pod_tiles * POD_TILE;
+    int rc = 0;
+    if ((rc = dalloc(e, &S.node_state, NLa)) || (rc = dalloc(e, &S.node_blob, NLa)) ||
+        (rc = dalloc(e, &S.node_tick, NLa)) || (rc = dalloc(e, &S.pod_state, PLa)) ||
+        (rc = dalloc(e, &S.pod_node, PLa)) || (rc = dalloc(e, &S.pod_spec, PLa)) ||
+        (rc = dalloc(e, &S.pod_ctime, PLa)) || (rc = dalloc(e, &S.pod_ip, PLa)) ||
+        (rc = dalloc(e, &S.host_ip, PLa)) || (rc = dalloc(e, &S.used_bm, e->pool.words)) ||
+        (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.pool_index, 1)) ||
+        (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.pool_blk_base, 2 * (size_t)nblk)) ||
+        (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
+        (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) || (rc = dalloc(e, &S.hb_tmpl, HB_STRIDE)) ||
+        (rc = dalloc(e, &S.tiles, (size_t)T * TF_STRIDE)) || (rc = dalloc(e, &S.tile_base, (size_t)T * 4)) ||
+        (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
+        (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &S.hb_nodes, NLa)) ||
+        (rc = dalloc(e, &S.init_nodes, NLa)) || (rc = dalloc(e, &S.init_off, NLa)) ||
+        (rc = dalloc(e, &S.init_len, NLa)) || (rc = dalloc(e, &S.pp_pods, PLa)) || (rc = dalloc(e, &S.pp_off, PLa)) ||
+        (rc = dalloc(e, &S.pp_len, PLa)) || (rc = dalloc(e, &S.del_pods, PLa)) || (rc = dalloc(e, &S.del_fin, PLa)) ||
+        (rc = dalloc(e, &e->d_ld_local, 1)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))))
+        return bail(rc);
+    // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
+    {
+        HeartbeatTemplate hb = build_heartbeat_template();
+        if (hb.bytes.size() != (size_t)HB_LEN) return bail(e->fail(KWOK_EINVAL, "heartbeat template %zu", hb.bytes.size()));
+        std::vector<uint8_t> bytes(HB_STRIDE, 0), kind(HB_STRIDE, 0xFF);
+        memcpy(bytes.data(), hb.bytes.data(), HB_LEN);
+        for (uint16_t o : hb.now_slots)
+            for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)i;
+        for (uint16_t o : hb.start_slots)
+            for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)(TS_LEN + i);
+        if (hipMemcpy((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(KWOK_EDEVICE);
+    }
+    {
+        ListDesc ld{};
+        ld.use = S.use_list;
+        ld.rel = S.rel_list;
+        ld.count_from_hdr = 1;
+        if (hipMemcpy(e->d_ld_local, &ld, sizeof ld, hipMemcpyHostToDevice) != hipSuccess) return bail(KWOK_EDEVICE);
+    }
+    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
+    if (W > 1) {
+        if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
+        if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
+            return bail(KWOK_ENOMEM);
+        if (cfg->comm_id) {
+            ncclUniqueId id;
+            memcpy(&id, cfg->comm_id, sizeof(id));
+            ncclResult_t r = ncclCommInitRank(&e->comm, W, id, e->rank);
+            if (r != ncclSuccess) return bail(e->fail(KWOK_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+        }
+    }
+    // host mirrors
+    e->nodes.resize(e->NL);
+    e->node_bits.assign((size_t)e->nb * ((e->Cn + 63) / 64), 0);
+    e->pod_used.assign(e->PL, 0);
+    e->pod_delpend.assign(e->PL, 0);
+    e->pod_node.assign(e->PL, 0);
+    e->pod_bits.assign((size_t)e->nb * ((e->Cp + 63) / 64), 0);
+    e->node_stamp.assign(e->NL, 0);
+    e->node_opi.assign(e->NL, 0);
+    e->pod_stamp.assign(e->PL, 0);
+    e->pod_opi.assign(e->PL, 0);
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->dev);
+    e->hb_grid = (uint32_t)std::max(1, dev_cus) * 8;
+    e->max_init_len = 0;
+    if ((rc = size_arena(e))) return bail(rc);
+    if (hipStreamSynchronize(e->st) != hipSuccess) return bail(KWOK_EDEVICE);
+    *out = e;
+    return KWOK_OK;
+}
+
+int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
+                           int32_t* out_id) {
+    if (!e || !spec || !out_id) return KWOK_EINVAL;
+    auto get = [&](kwok_str s, std::string& o) {
+        if ((size_t)s.off + s.len > arena_len) return false;
+        o.assign(arena + s.off, s.len);
+        return safe_string(o.data(), o.size());
+    };
+    std::vector<Container> cs(spec->n_containers), ics(spec->n_init_containers);
+    std::vector<std::string> gates(spec->n_readiness_gates);
+    for (uint32_t i = 0; i < spec->n_containers; i++)
+        if (!get(spec->containers[i].name, cs[i].name) || !get(spec->containers[i].image, cs[i].image))
+            return e->fail(KWOK_EDOMAIN, "container %u: not a safe string", i);
+    for (uint32_t i = 0; i < spec->n_init_containers; i++)
+        if (!get(spec->init_containers[i].name, ics[i].name) || !get(spec->init_containers[i].image, ics[i].image))
+            return e->fail(KWOK_EDOMAIN, "init container %u: not a safe string", i);
+    for (uint32_t i = 0; i < spec->n_readiness_gates; i++)
+        if (!get(spec->readiness_gates[i], gates[i])) return e->fail(KWOK_EDOMAIN, "readiness gate %u: not a safe string", i);
+    SpecProgram p = build_spec_program(cs, ics, gates);
+    if (p.max_len > 0xFFFF) return e->fail(KWOK_EDOMAIN, "pod patch longer than 64 KiB");
+    std::string key = p.a + '\x01' + p.ka + '\x01' + p.b + '\x01' + p.kb + '\x01' + p.c + '\x01' + p.kc;
+    auto it = e->spec_ids.find(key);
+    if (it != e->spec_ids.end()) {
+        *out_id = it->second;
+        return KWOK_OK;
+    }
+    uint32_t cap = e->cfg.max_pod_specs ? std::min<uint32_t>(e->cfg.max_pod_specs, 65535) : 1024;
+    if (e->specs_h.size() >= cap) return e->fail(KWOK_EFULL, "max_pod_specs reached");
+    SpecDesc d{};
+    d.off = (uint32_t)e->spec_bytes_h.size();
+    d.len_a = (uint16_t)p.a.size();
+    d.len_b = (uint16_t)p.b.size();
+    d.len_c = (uint16_t)p.c.size();
+    d.max_len = (uint16_t)p.max_len;
+    e->spec_bytes_h += p.a + p.b + p.c;
+    e->spec_kinds_h += p.ka + p.kb + p.kc;
+    e->specs_h.push_back(d);
+    int rc = upload_specs(e);
+    if (rc) return rc;
+    e->max_pod_len = std::max(e->max_pod_len, p.max_len);
+    if ((rc = size_arena(e))) return rc;
+    *out_id = (int32_t)(e->specs_h.size() - 1);
+    e->spec_ids.emplace(key, *out_id);
+    return KWOK_OK;
+}
+
+int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
+                      int32_t* out_handles, int32_t* out_status) {
+    if (!e || (n && !ev)) return KWOK_EINVAL;
+    e->gen++;
+    int rejected = 0;
+    for (size_t i = 0; i < n; i++) {
+        const kwok_node_event& x = ev[i];
+        int st = KWOK_OK;
+        int32_t handle = -1;
+        auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+        if (!x.name.len || x.name.len > 253 || !in_arena(x.name)) st = KWOK_EDOMAIN;
+        const char* name = arena + x.name.off;
+        uint32_t slot = 0;
+        if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
+            // node_controller.go:265-269: Deleted -> nodesSets.Delete
+            st = node_slot(e, name, x.name.len, false, &slot);
+            if (st == KWOK_OK) {
+                auto& hn = e->nodes[slot];
+                if (hn.managed) e->n_managed--;
+                hn.exists = hn.managed = 0;
+                node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
+                        false, 0);
+                handle = (int32_t)(e->b_lo * e->Cn + slot);
+                free_node_if_unused(e, slot);
+            }
+        } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
+            std::string info[KWOK_NI_COUNT];
+            for (int k = 0; k < KWOK_NI_COUNT && st == KWOK_OK; k++) {
+                if (!in_arena(x.node_info[k])) st = KWOK_EDOMAIN;
+                else if (x.node_info[k].len) {
+                    info[k].assign(arena + x.node_info[k].off, x.node_info[k].len);
+                    if (!safe_string(info[k].data(), info[k].size())) st = KWOK_EDOMAIN;
+                }
+            }
+            std::string js[3];
+            const kwok_str* jr[3] = {&x.addresses, &x.allocatable, &x.capacity};
+            for (int k = 0; k < 3 && st == KWOK_OK; k++) {
+                if (!in_arena(*jr[k])) st = KWOK_EDOMAIN;
+                else if (jr[k]->len) {
+                    js[k].assign(arena + jr[k]->off, jr[k]->len);
+                    if (!valid_json_blob(js[k].data(), js[k].size(), k == 0 ? '[' : '{')) st = KWOK_EDOMAIN;
+                }
+            }
+            if (st == KWOK_OK) st = node_slot(e, name, x.name.len, true, &slot);
+            if (st == KWOK_OK) {
+                NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
+                int brc = KWOK_OK;
+                uint64_t blob = intern_blob(e, nb, &brc);
+                if (brc) st = brc;
+                else {
+                    auto& hn = e->nodes[slot];
+                    hn.exists = 1;
+                    if (x.managed && !hn.managed) hn.managed = 1, e->n_managed++;  // never cleared but by Delete
+                    hn.lockable = x.lockable ? 1 : 0;
+                    bool ev_lock = x.managed && x.lockable;
+                    uint8_t bits = (uint8_t)(NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
+                                             (node_conforms(x, info) ? NS_CONFORMS : 0) | (ev_lock ? NS_EVENT_LOCK : 0));
+                    node_op(e, slot, ev_lock ? 0 : NS_EVENT_LOCK, bits, true, blob);
+                    handle = (int32_t)(e->b_lo * e->Cn + slot);
+                }
+            }
+        } else if (st == KWOK_OK) {
+            st = KWOK_EINVAL;
+        }
+        if (out_handles) out_handles[i] = handle;
+        if (out_status) out_status[i] = st;
+        if (st != KWOK_OK) rejected++;
+    }
+    int rc = size_arena(e);
+    if (rc) return rc;
+    rc = flush_ops(e);
+    return rc ? rc : rejected;
+}
+
+int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
+                     int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
+    if (!e || (n && !ev)) return KWOK_EINVAL;
+    e->gen++;
+    int rejected = 0;
+    const int32_t pbase = (int32_t)(e->b_lo * e->Cp);
+    for (size_t i = 0; i < n; i++) {
+        const kwok_pod_event& x = ev[i];
+        int st = KWOK_OK;
+        int32_t handle = -1;
+        if (out_released) out_released[i] = 0;
+        auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) st = KWOK_EDOMAIN;
+        uint32_t slot = 0;
+        bool existing = x.handle >= 0;
+        if (st == KWOK_OK && existing) {
+            int64_t l = (int64_t)x.handle - pbase;
+            if (l < 0 || l >= (int64_t)e->PL) {
+                uint32_t gb = (uint32_t)x.handle / e->Cp;
+                st = (x.handle >= 0 && gb < e->B) ? KWOK_ENOTMINE : KWOK_ENOTFOUND;
+            } else if (!e->pod_used[(uint32_t)l]) st = KWOK_ENOTFOUND;
+            else slot = (uint32_t)l;
+        }
+        if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
+            if (!existing) st = KWOK_EINVAL;
+            else {
+                uint32_t nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
+                auto& hn = e->nodes[nslot];
+                uint32_t ip = 0;
+                // pod_controller.go:329-336: release the event object's podIP if the node is managed
+                if (hn.managed && x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip) &&
+                    (uint64_t)(ip - e->pool.net) < e->pool.size && ip >= e->pool.net) {
+                    e->puts.push_back(ip);
+                    if (out_released) out_released[i] = ip;
+                }
+                PodOp o{};
+                o.slot = slot;
+                pod_op(e, o);  // state = 0
+                e->pod_used[slot] = 0;
+                e->pod_delpend[slot] = 0;
+                set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
+                hn.refs--;
+                free_node_if_unused(e, nslot);
+                handle = pbase + (int32_t)slot;
+            }
+        } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
+            uint32_t hip = 0, pip = 0;
+            if (parse_opt_ip(arena, x.host_ip, &hip) || parse_opt_ip(arena, x.pod_ip, &pip)) st = KWOK_EDOMAIN;
+            else if (x.spec_id < 0 || (size_t)x.spec_id >= e->specs_h.size()) st = KWOK_EINVAL;
+            else if (x.phase > KWOK_PHASE_UNKNOWN) st = KWOK_EINVAL;
+            else if (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll) st = KWOK_EDOMAIN;
+            uint32_t nslot = 0;
+            if (st == KWOK_OK && !existing) {
+                if (x.node_handle >= 0) {
+                    int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
+                    if (l < 0 || l >= (int64_t)e->NL) st = KWOK_ENOTMINE;
+                    else if (!e->nodes[(uint32_t)l].used) st = KWOK_ENOTFOUND;
+                    else nslot = (uint32_t)l;
+                } else if (!x.node_name.len || x.node_name.len > 253) {
+                    st = KWOK_EDOMAIN;
+                } else {
+                    st = node_slot(e, arena + x.node_name.off, x.node_name.len, true, &nslot);
+                }
+                if (st == KWOK_OK) {
+                    uint32_t bl = nslot / e->Cn;
+                    int32_t idx = first_free(e->pod_bits, bl, e->Cp);
+                    if (idx < 0) {
+                        st = KWOK_EFULL;
+                        free_node_if_unused(e, nslot);
+                    } else {
+                        slot = bl * e->Cp + (uint32_t)idx;
+                        set_bit(e->pod_bits, e->Cp, bl, (uint32_t)idx, true);
+                        e->pod_used[slot] = 1;
+                        e->pod_node[slot] = (uint16_t)(nslot % e->Cn);
+                        e->nodes[nslot].refs++;
+                    }
+                }
+            } else if (st == KWOK_OK) {
+                nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
+            }
+            if (st == KWOK_OK) {
+                const auto& hn = e->nodes[nslot];
+                uint16_t bits = (uint16_t)(PS_USED | ((uint16_t)x.phase << PS_PHASE_SHIFT));
+                if (x.flags & KWOK_POD_DISREGARD) bits |= PS_DISREGARD;
+                if (x.flags & KWOK_POD_HAS_FINALIZERS) bits |= PS_HAS_FIN;
+                if (x.flags & KWOK_POD_STATUS_NONEMPTY) bits |= PS_STATUS_NONEMPTY;
+                if (x.flags & KWOK_POD_CONFORMS) bits |= PS_CONFORMS;
+                if (hip) bits |= PS_HAS_HOST_IP;
+                if (x.flags & KWOK_POD_DELETING) {
+                    if (hn.managed) {  // pod_controller.go:306-308 -> deletePodChan
+                        bits |= PS_DELETE_PENDING;
+                        if (!e->pod_delpend[slot]) e->pending_del.push_back(slot);
+                        e->pod_delpend[slot] = 1;
+                    }
+                } else if (hn.managed && !(x.flags & KWOK_POD_DISREGARD)) {
+                    bits |= PS_EVENT;  // needLockPod (:252-269) -> lockPodChan
+                }
+                PodOp o{};
+                o.slot = slot;
+                o.keep_mask = existing ? (uint16_t)(PS_EVENT | PS_DELETE_PENDING) : 0;
+                o.bits = bits;
+                o.set_fields = 1;
+                o.node = e->pod_node[slot];
+                o.spec = (uint16_t)x.spec_id;
+                o.ctime = (uint32_t)x.creation_unix;
+                o.host_ip = hip;
+                o.pod_ip = pip;
+                pod_op(e, o);
+                handle = pbase + (int32_t)slot;
+            }
+        } else if (st == KWOK_OK) {
+            st = KWOK_EINVAL;
+        }
+        if (out_handles) out_handles[i] = handle;
+        if (out_status) out_status[i] = st;
+        if (st != KWOK_OK) rejected++;
+    }
+    int rc = flush_ops(e);
+    return rc ? rc : rejected;
+}
+
+int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
+    if (!e || (n && !ips)) return KWOK_EINVAL;
+    e->gen++;
+    e->puts.assign(ips, ips + n);
+    return flush_ops(e);
+}
+
+int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
+    if (!e) return KWOK_EINVAL;
+    if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
+    DevState& S = e->S;
+    hipStream_t st = e->st;
+    launch_tick_front(S, (uint64_t)now_unix, (uint64_t)e->start, e->W, st);
+    if (e->W == 1) {
+        launch_pool_lists(S, e->d_ld_local, 1, true, 0, st);
+        launch_pool_lists(S, e->d_ld_local, 1, false, 0, st);
+    } else {
+        // one allgather of the fixed-size exchange message; a second one for
+        // lists that did not fit inline (sizes known after the first)
+        int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
+        if (rc) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        uint64_t maxl = 0, maxu = 0, maxr = 0;
+        for (int r = 0; r < e->W; r++) {
+            maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
+            maxu = std::max<uint64_t>(maxu, e->h_xall[r].n_use);
+            maxr = std::max<uint64_t>(maxr, e->h_xall[r].n_rel);
+        }
+        std::vector<ListDesc> ld(e->W);
+        if (maxl <= (uint64_t)XINLINE) {
+            for (int r = 0; r < e->W; r++) {
+                ld[r].use = e->d_xall[r].ips;
+                ld[r].rel = e->d_xall[r].ips + e->h_xall[r].n_use;
+            }
+        } else {
+            if (maxl > e->xlist_cap) {
+                if (e->d_xsend) (void)hipFree(e->d_xsend);
+                if (e->d_xrecv) (void)hipFree(e->d_xrecv);
+                e->xlist_cap = maxl;
+                if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
+                    hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
+                    return e->fail(KWOK_ENOMEM, "exchange lists");
+            }
+            const XMsg& me = e->h_xall[e->rank];
+            HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
+            rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
+            if (rc) return rc;
+            for (int r = 0; r < e->W; r++) {
+                ld[r].use = e->d_xrecv + (size_t)r * maxl;
+                ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
+            }
+        }
+        for (int r = 0; r < e->W; r++) {
+            ld[r].n_use = (uint32_t)e->h_xall[r].n_use;
+            ld[r].n_rel = (uint32_t)e->h_xall[r].n_rel;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
+        launch_xreduce(S, e->d_xall, e->W, e->rank, st);
+        // Uses from every rank, then Puts from every rank
+        launch_pool_lists(S, e->d_ld, e->W, true, (uint32_t)maxu, st);
+        launch_pool_lists(S, e->d_ld, e->W, false, (uint32_t)maxr, st);
+    }
+    launch_pool_alloc(S, st);
+    launch_emit(S, st);
+    launch_hb_fill(S, e->hb_grid, st);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemcpyAsync(e->hdr_h, S.hdr, sizeof(TickHdr), hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    const TickHdr& H = *e->hdr_h;
+    if (H.overflow) return e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes);
+    // host mirror: pods deleted by the tick (DeletePod) free their slots
+    for (uint32_t slot : e->pending_del) {
+        if (!e->pod_delpend[slot] || !e->pod_used[slot]) continue;
+        uint32_t nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
+        e->pod_used[slot] = 0;
+        e->pod_delpend[slot] = 0;
+        set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
+        e->nodes[nslot].refs--;
+        if (e->nodes[nslot].used && !e->nodes[nslot].exists && e->nodes[nslot].refs == 0) {
+            e->gen++;
+            free_node_if_unused(e, nslot);
+        }
+    }
+    e->pending_del.clear();
+    if (!e->nops.empty()) {
+        int rc = flush_ops(e);
+        if (rc) return rc;
+    }
+    e->have_tick = true;
+    if (res) {
+        memset(res, 0, sizeof(*res));
+        res->n_heartbeat = H.n_hb;
+        res->heartbeat_len = HB_LEN;
+        res->heartbeat_stride = HB_STRIDE;
+        res->n_node_init = H.n_init;
+        res->n_pod_patch = H.n_pp;
+        res->n_delete = H.n_del;
+        res->arena_bytes = H.arena_bytes;
+        for (int k = 0; k < KWOK_COUNTER_COUNT; k++) {
+            res->counters[k] = H.counters[k];
+            res->local_counters[k] = H.local_counters[k];
+        }
+    }
+    return KWOK_OK;
+}
+
+int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
+    if (!e || !o) return KWOK_EINVAL;
+    if (!e->have_tick) return e->fail(KWOK_EINVAL, "no tick yet");
+    const TickHdr& H = *e->hdr_h;
+    DevState& S = e->S;
+    hipStream_t st = e->st;
+    auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        if (!dst || !bytes) return hipSuccess;
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    };
+    o->heartbeat_off = H.hb_base;
+    HIPCHK(e, cp(o->heartbeat_nodes, S.hb_nodes, (size_t)H.n_hb * 4));
+    HIPCHK(e, cp(o->node_init_nodes, S.init_nodes, (size_t)H.n_init * 4));
+    HIPCHK(e, cp(o->node_init_off, S.init_off, (size_t)H.n_init * 8));
+    HIPCHK(e, cp(o->node_init_len, S.init_len, (size_t)H.n_init * 4));
+    HIPCHK(e, cp(o->pod_patch_pods, S.pp_pods, (size_t)H.n_pp * 4));
+    HIPCHK(e, cp(o->pod_patch_off, S.pp_off, (size_t)H.n_pp * 8));
+    HIPCHK(e, cp(o->pod_patch_len, S.pp_len, (size_t)H.n_pp * 4));
+    HIPCHK(e, cp(o->delete_pods, S.del_pods, (size_t)H.n_del * 4));
+    HIPCHK(e, cp(o->delete_has_finalizers, S.del_fin, (size_t)H.n_del));
+    if (o->arena) {
+        if (o->arena_cap < H.arena_bytes) return e->fail(KWOK_EINVAL, "arena_cap < %llu", (unsigned long long)H.arena_bytes);
+        HIPCHK(e, cp(o->arena, S.arena, H.arena_bytes));
+    }
+    HIPCHK(e, hipStreamSynchronize(st));
+    return KWOK_OK;
+}
+
+int kwok_device_outputs(kwok_engine* e, kwok_device_view* v) {
+    if (!e || !v) return KWOK_EINVAL;
+    v->arena = e->S.arena;
+    v->heartbeat_nodes = e->S.hb_nodes;
+    v->pod_patch_pods = e->S.pp_pods;
+    v->pod_patch_off = e->S.pp_off;
+    v->pod_patch_len = e->S.pp_len;
+    v->stream = e->st;
+    return KWOK_OK;
+}
+
+int kwok_node_has(kwok_engine* e, const char* name, size_t len) {
+    if (!e || !name) return 0;
+    auto it = e->node_by_name.find(std::string(name, len));
+    return it != e->node_by_name.end() && e->nodes[it->second].managed;
+}
+
+uint64_t kwok_node_size(kwok_engine* e) { return e ? e->n_managed : 0; }
+
+int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase, uint32_t* host_ip,
+                   uint32_t* pod_ip) {
+    if (!e) return KWOK_EINVAL;
+    std::vector<uint16_t> sth(e->PL);
+    std::vector<uint32_t> hh(e->PL), ph(e->PL);
+    HIPCHK(e, hipMemcpyAsync(sth.data(), e->S.pod_state, (size_t)e->PL * 2, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(hh.data(), e->S.host_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(ph.data(), e->S.pod_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    const int64_t pbase = (int64_t)e->b_lo * e->Cp;
+    for (uint32_t i = 0; i < count; i++) {
+        int64_t l = (int64_t)first + i - pbase;
+        bool ok = l >= 0 && l < (int64_t)e->PL && (sth[(size_t)l] & PS_USED);
+        if (used) used[i] = ok;
+        if (phase) phase[i] = ok ? (uint8_t)((sth[(size_t)l] & PS_PHASE_MASK) >> PS_PHASE_SHIFT) : 0;
+        if (host_ip) host_ip[i] = ok && (sth[(size_t)l] & PS_HAS_HOST_IP) ? hh[(size_t)l] : 0;
+        if (pod_ip) pod_ip[i] = ok ? ph[(size_t)l] : 0;
+    }
+    return KWOK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// kernels.h - device state handle + launchers (host side of kernels.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device.h"
+
+namespace kwok {
+
+struct ListDesc {
+    const uint32_t* use;
+    const uint32_t* rel;
+    uint32_t n_use, n_rel;
+    uint32_t count_from_hdr;  // single rank: counts live in TickHdr
+    uint32_t pad;
+};
+
+// Everything a kernel needs, passed by value (pointers into HBM).
+struct DevState {
+    // nodes (local slots)
+    uint8_t* node_state;
+    uint64_t* node_blob;
+    uint8_t* node_tick;
+    uint32_t n_node_slots, node_tiles;
+    // pods (local slots)
+    uint16_t* pod_state;
+    uint16_t* pod_node;
+    uint16_t* pod_spec;
+    uint32_t* pod_ctime;
+    uint32_t* pod_ip;
+    uint32_t* host_ip;
+    uint32_t n_pod_slots, pod_tiles;
+    uint32_t cn, cp;
+    int32_t node_handle_base, pod_handle_base;
+    // pool replica
+    uint64_t* used_bm;
+    uint64_t* usable_bm;
+    uint64_t* pool_index;    // ipPool.index (persistent)
+    uint32_t* pool_blk;      // per word-block counts
+    uint64_t* pool_blk_base;
+    uint32_t* alloc_addr;    // this rank's allocated addresses, by local ordinal
+    PoolGeom pool;
+    // pod spec programs / node blobs
+    const SpecDesc* specs;
+    const uint8_t* spec_bytes;
+    const uint8_t* spec_kinds;
+    const uint8_t* blob;
+    // heartbeat template
+    const uint8_t* hb_static;
+    const uint8_t* hb_kind;
+    uint8_t* hb_tmpl;
+    // per tick
+    uint32_t* tiles;
+    uint64_t* tile_base;
+    TickHdr* hdr;
+    XMsg* xmsg;
+    uint32_t* use_list;
+    uint32_t* rel_list;
+    uint8_t* arena;
+    uint64_t arena_cap;
+    int32_t* hb_nodes;
+    int32_t* init_nodes;
+    uint64_t* init_off;
+    uint32_t* init_len;
+    int32_t* pp_pods;
+    uint64_t* pp_off;
+    uint32_t* pp_len;
+    int32_t* del_pods;
+    uint8_t* del_fin;
+    uint32_t node_ip;
+};
+
+void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
+                      hipStream_t st);
+void launch_tick_front(const DevState& S, uint64_t now, uint64_t start, int world, hipStream_t st);
+void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st);
+void launch_pool_lists(const DevState& S, const ListDesc* ld, int nranks, bool uses, uint32_t max_n,
+                       hipStream_t st);
+void launch_pool_alloc(const DevState& S, hipStream_t st);
+void launch_emit(const DevState& S, hipStream_t st);
+void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st);
+
+}  // namespace kwok

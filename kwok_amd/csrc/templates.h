@@ -1,0 +1,49 @@
+// templates.h - fixed-layout byte programs for the reference's three default
+// templates (pkg/kwok/controllers/templates/{node.heartbeat,node.status,
+// pod.status}.tpl) as they come out of renderer.go:49-89 (text/template ->
+// sigs.k8s.io/yaml.YAMLToJSON -> json.Marshal: sorted keys, compact) and the
+// {"status": ...} wrapper (node_controller.go:388,398; pod_controller.go:399).
+// The kernels only fill timestamp/IP slots and splice per-object blobs.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace kwok {
+
+constexpr uint8_t KIND_LIT = 0xFF;  // literal byte; otherwise an index into a 20-byte timestamp
+
+struct HeartbeatTemplate {
+    std::string bytes;              // HB_LEN bytes, timestamp slots zero-filled
+    std::vector<uint16_t> now_slots;   // offsets of lastHeartbeatTime values (Now)
+    std::vector<uint16_t> start_slots; // offsets of lastTransitionTime values (StartTime)
+};
+HeartbeatTemplate build_heartbeat_template();
+
+struct SpecProgram {
+    std::string a, b, c;           // segments (timestamp slots zero-filled)
+    std::string ka, kb, kc;        // per-byte kind (KIND_LIT or 0..19)
+    uint32_t max_len;              // a+b+c + 53 (hostIP/podIP pieces at 15-char IPs)
+};
+struct Container {
+    std::string name, image;
+};
+SpecProgram build_spec_program(const std::vector<Container>& containers, const std::vector<Container>& init,
+                               const std::vector<std::string>& gates);
+
+// node init blob: pre = "addresses":..,"allocatable":..,"capacity":..  post = "nodeInfo":{..},"phase":"Running"
+struct NodeBlob {
+    std::string pre, post;
+};
+NodeBlob build_node_blob(const std::string& addresses_json, const std::string& allocatable_json,
+                         const std::string& capacity_json, const std::string info[10], const std::string& node_ip);
+
+// domain checks (DESIGN.md "Supported domain")
+bool safe_string(const char* s, size_t n);
+bool valid_json_blob(const char* s, size_t n, char open);
+bool parse_ipv4(const char* s, size_t n, uint32_t* out);  // canonical dotted quad only
+std::string format_ipv4(uint32_t ip);
+void json_string(std::string& out, const std::string& s);
+
+}  // namespace kwok
