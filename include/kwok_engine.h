@@ -264,6 +264,13 @@ typedef struct kwok_device_view {
 } kwok_device_view;
 int kwok_device_outputs(kwok_engine* e, kwok_device_view* view);
 
+/* Diagnostics: device time per tick phase, measured with HIP events recorded
+ * on the engine's stream around each phase (enable resets the accumulators). */
+enum { KWOK_T_FRONT = 0 /* classify + scan */, KWOK_T_POOL /* ipPool kernels */, KWOK_T_EMIT,
+       KWOK_T_HB_FILL /* heartbeat emission */, KWOK_T_COUNT };
+int kwok_profile_enable(kwok_engine* e, int on);
+int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* ticks);
+
 /* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);
 int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world_size);

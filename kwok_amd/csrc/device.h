@@ -48,7 +48,7 @@ constexpr int HB_NSLOTS = 10;    // 5 x (lastHeartbeatTime, lastTransitionTime)
 // per-tile aggregates written by the classify kernel
 enum TileField {
     TF_HB = 0, TF_INIT, TF_INIT_BYTES, TF_LOCK, TF_MANAGED, TF_READY,   // node tiles
-    TF_DEL, TF_EVAL, TF_ALLOC, TF_PP, TF_PP_BYTES, TF_TOTAL, TF_PENDING, TF_RUNNING, // pod tiles
+    TF_DEL, TF_EVAL, TF_ALLOC, TF_PP, TF_PP_BYTES, TF_TOTAL, TF_PENDING, TF_RUNNING, TF_REL, // pod tiles
     TF_COUNT
 };
 constexpr int TF_STRIDE = 16;
@@ -66,6 +66,7 @@ struct TickHdr {
     // pool (post exchange)
     uint64_t alloc_total, alloc_base, usable_total, take_usable, fresh_in, fresh_out_start;
     uint64_t cursor_index;       // ipPool.index after the tick
+    uint64_t rel_total;          // releases this tick, all ranks (pending in rel_bm)
 };
 
 // exchange message, one per rank (allgather)

@@ -31,6 +31,8 @@ using namespace kwok;
 
 namespace {
 
+thread_local std::string g_create_err;  // kwok_last_error(NULL) after a failed create
+
 uint32_t fnv1a32(const char* s, size_t n) {
     uint32_t h = 0x811C9DC5u;
     for (size_t i = 0; i < n; i++) {
@@ -57,7 +59,9 @@ struct kwok_engine {
     uint32_t node_ip = 0;
     std::string node_ip_s;
     int64_t start = 0;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;   // tick pipeline
+    hipStream_t st2 = nullptr;  // heartbeat stream (k_hb_fill), overlaps pool + emit
+    hipEvent_t ev_front = nullptr, ev_hb = nullptr;
     DevState S{};
 
     // ---- host mirrors (slot policy) ----
@@ -101,7 +105,6 @@ struct kwok_engine {
     // ---- tick ----
     TickHdr* hdr_h = nullptr;  // pinned
     bool have_tick = false;
-    ListDesc* d_ld_local = nullptr;
     ListDesc* d_ld = nullptr;  // [W] or scratch
     ncclComm_t comm = nullptr;
     XMsg* d_xall = nullptr;
@@ -110,6 +113,12 @@ struct kwok_engine {
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
     uint32_t hb_grid = 2048;
+    // diagnostics
+    bool prof = false;
+    hipEvent_t pev[KWOK_T_COUNT + 1] = {};
+    hipEvent_t pev_hb[2] = {};  // hb_fill runs on st2
+    double prof_ms[KWOK_T_COUNT] = {};
+    uint64_t prof_ticks = 0;
 
     int fail(int code, const char* fmt, ...) {
         char b[512];
@@ -240,14 +249,8 @@ int flush_ops(kwok_engine* e) {
     HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
     launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)e->nops.size(), (const PodOp*)(d + po),
                      (uint32_t)e->pops.size(), e->st);
-    if (!e->puts.empty()) {
-        // ingest-time Puts (Deleted events, pod_controller.go:329-336)
-        ListDesc ld{};
-        ld.rel = (const uint32_t*)(d + uo);
-        ld.n_rel = (uint32_t)e->puts.size();
-        HIPCHK(e, hipMemcpyAsync(e->d_ld, &ld, sizeof ld, hipMemcpyHostToDevice, e->st));
-        launch_pool_lists(e->S, e->d_ld, 1, false, ld.n_rel, e->st);
-    }
+    if (!e->puts.empty())  // ingest-time Puts (Deleted events, pod_controller.go:329-336)
+        launch_pool_puts_now(e->S, (const uint32_t*)(d + uo), (uint32_t)e->puts.size(), e->st);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->nops.clear();
@@ -407,18 +410,18 @@ int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world) {
     return (int32_t)(((uint64_t)bucket * (uint64_t)world) / buckets);
 }
 
-const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : "null engine"; }
+const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : g_create_err.c_str(); }
 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->st) (void)hipStreamSynchronize(e->st);
     void* ptrs[] = {e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
-                    e->S.pool_blk, e->S.pool_blk_base, e->S.alloc_addr, (void*)e->S.hb_static,
+                    e->S.pool_blk, e->S.pool_blk_base, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.hb_tmpl, e->S.tiles, e->S.tile_base, e->S.hdr, e->S.xmsg,
                     e->S.use_list, e->S.rel_list, e->S.arena, e->S.hb_nodes, e->S.init_nodes, e->S.init_off,
                     e->S.init_len, e->S.pp_pods, e->S.pp_off, e->S.pp_len, e->S.del_pods, e->S.del_fin,
-                    e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops, e->d_ld_local,
+                    e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -426,6 +429,13 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->comm) ncclCommDestroy(e->comm);
+    for (auto& ev : e->pev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : e->pev_hb)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->ev_front) (void)hipEventDestroy(e->ev_front);
+    if (e->ev_hb) (void)hipEventDestroy(e->ev_hb);
+    if (e->st2) (void)hipStreamDestroy(e->st2);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
 }
@@ -458,6 +468,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->PL = e->nb * e->Cp;
     e->start = cfg->start_time_unix;
     auto bail = [&](int rc) {
+        g_create_err = e->err.empty() ? std::string("create failed (") + std::to_string(rc) + ")" : e->err;
         kwok_engine_destroy(e);
         return rc;
     };
@@ -477,8 +488,17 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->node_ip_s = format_ipv4(e->node_ip);
     if (cfg->start_time_unix < 0 || cfg->start_time_unix > 0xFFFFFFFFll) return bail(KWOK_EDOMAIN);
 
-    if (hipSetDevice(e->dev) != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "hipSetDevice(%d)", e->dev));
-    if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return bail(KWOK_EDEVICE);
+    {
+        hipError_t r = hipSetDevice(e->dev);
+        if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "hipSetDevice(%d): %s", e->dev, hipGetErrorString(r)));
+    }
+    {
+        hipError_t r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_front, hipEventDisableTiming);
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_hb, hipEventDisableTiming);
+        if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "stream/event create: %s", hipGetErrorString(r)));
+    }
     DevState& S = e->S;
     S.n_node_slots = e->NL;
     S.n_pod_slots = e->PL;
@@ -490,6 +510,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pod_handle_base = (int32_t)(e->b_lo * e->Cp);
     S.pool = e->pool;
     S.node_ip = e->node_ip;
+    S.world = W;
     const uint32_t T = S.node_tiles + S.pod_tiles;
     const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
     // node/pod tiles round NL/PL up: allocate whole tiles so vector loads stay in bounds
@@ -500,7 +521,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.pod_node, PLa)) || (rc = dalloc(e, &S.pod_spec, PLa)) ||
         (rc = dalloc(e, &S.pod_ctime, PLa)) || (rc = dalloc(e, &S.pod_ip, PLa)) ||
         (rc = dalloc(e, &S.host_ip, PLa)) || (rc = dalloc(e, &S.used_bm, e->pool.words)) ||
-        (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.pool_index, 1)) ||
+        (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.rel_bm, e->pool.words)) ||
+        (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &S.pool_index, 1)) ||
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.pool_blk_base, 2 * (size_t)nblk)) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) || (rc = dalloc(e, &S.hb_tmpl, HB_STRIDE)) ||
@@ -510,7 +532,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.init_nodes, NLa)) || (rc = dalloc(e, &S.init_off, NLa)) ||
         (rc = dalloc(e, &S.init_len, NLa)) || (rc = dalloc(e, &S.pp_pods, PLa)) || (rc = dalloc(e, &S.pp_off, PLa)) ||
         (rc = dalloc(e, &S.pp_len, PLa)) || (rc = dalloc(e, &S.del_pods, PLa)) || (rc = dalloc(e, &S.del_fin, PLa)) ||
-        (rc = dalloc(e, &e->d_ld_local, 1)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))))
+        (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
     {
@@ -522,16 +544,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)i;
         for (uint16_t o : hb.start_slots)
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)(TS_LEN + i);
-        if (hipMemcpy((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice) != hipSuccess)
-            return bail(KWOK_EDEVICE);
-    }
-    {
-        ListDesc ld{};
-        ld.use = S.use_list;
-        ld.rel = S.rel_list;
-        ld.count_from_hdr = 1;
-        if (hipMemcpy(e->d_ld_local, &ld, sizeof ld, hipMemcpyHostToDevice) != hipSuccess) return bail(KWOK_EDEVICE);
+        hipError_t r = hipMemcpy((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice);
+        if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
+        if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
     if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
     if (W > 1) {
@@ -561,7 +576,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->hb_grid = (uint32_t)std::max(1, dev_cus) * 8;
     e->max_init_len = 0;
     if ((rc = size_arena(e))) return bail(rc);
-    if (hipStreamSynchronize(e->st) != hipSuccess) return bail(KWOK_EDEVICE);
+    {
+        hipError_t r = hipStreamSynchronize(e->st);
+        if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "create sync: %s", hipGetErrorString(r)));
+    }
     *out = e;
     return KWOK_OK;
 }
@@ -819,23 +837,28 @@ int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
     if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
     DevState& S = e->S;
     hipStream_t st = e->st;
+    auto mark = [&](int i) {
+        if (e->prof) (void)hipEventRecord(e->pev[i], st);
+    };
+    mark(0);
     launch_tick_front(S, (uint64_t)now_unix, (uint64_t)e->start, e->W, st);
-    if (e->W == 1) {
-        launch_pool_lists(S, e->d_ld_local, 1, true, 0, st);
-        launch_pool_lists(S, e->d_ld_local, 1, false, 0, st);
-    } else {
+    // heartbeat emission only needs the scan (count + per-tick template): run it
+    // on the second stream, overlapped with the exchange, the pool and emit
+    HIPCHK(e, hipEventRecord(e->ev_front, st));
+    HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_front, 0));
+    if (e->prof) (void)hipEventRecord(e->pev_hb[0], e->st2);
+    launch_hb_fill(S, e->hb_grid, e->st2);
+    if (e->prof) (void)hipEventRecord(e->pev_hb[1], e->st2);
+    HIPCHK(e, hipEventRecord(e->ev_hb, e->st2));
+    if (e->W > 1) {
         // one allgather of the fixed-size exchange message; a second one for
         // lists that did not fit inline (sizes known after the first)
         int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
         if (rc) return rc;
         HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipStreamSynchronize(st));
-        uint64_t maxl = 0, maxu = 0, maxr = 0;
-        for (int r = 0; r < e->W; r++) {
-            maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
-            maxu = std::max<uint64_t>(maxu, e->h_xall[r].n_use);
-            maxr = std::max<uint64_t>(maxr, e->h_xall[r].n_rel);
-        }
+        uint64_t maxl = 0;
+        for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
         std::vector<ListDesc> ld(e->W);
         if (maxl <= (uint64_t)XINLINE) {
             for (int r = 0; r < e->W; r++) {
@@ -867,17 +890,28 @@ int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
         }
         HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
         launch_xreduce(S, e->d_xall, e->W, e->rank, st);
-        // Uses from every rank, then Puts from every rank
-        launch_pool_lists(S, e->d_ld, e->W, true, (uint32_t)maxu, st);
-        launch_pool_lists(S, e->d_ld, e->W, false, (uint32_t)maxr, st);
+        launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
     }
+    mark(1);  // (multi-rank: includes the exchange)
     launch_pool_alloc(S, st);
+    mark(2);
     launch_emit(S, st);
-    launch_hb_fill(S, e->hb_grid, st);
+    mark(3);
+    HIPCHK(e, hipStreamWaitEvent(st, e->ev_hb, 0));
+    mark(4);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipMemcpyAsync(e->hdr_h, S.hdr, sizeof(TickHdr), hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
     const TickHdr& H = *e->hdr_h;
+    if (e->prof) {
+        for (int i = 0; i < KWOK_T_COUNT; i++) {
+            float ms = 0;
+            if (i == KWOK_T_HB_FILL) (void)hipEventElapsedTime(&ms, e->pev_hb[0], e->pev_hb[1]);
+            else (void)hipEventElapsedTime(&ms, e->pev[i], e->pev[i + 1]);
+            e->prof_ms[i] += ms;
+        }
+        e->prof_ticks++;
+    }
     if (H.overflow) return e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes);
     // host mirror: pods deleted by the tick (DeletePod) free their slots
     for (uint32_t slot : e->pending_del) {
@@ -951,6 +985,25 @@ int kwok_device_outputs(kwok_engine* e, kwok_device_view* v) {
     v->pod_patch_off = e->S.pp_off;
     v->pod_patch_len = e->S.pp_len;
     v->stream = e->st;
+    return KWOK_OK;
+}
+
+int kwok_profile_enable(kwok_engine* e, int on) {
+    if (!e) return KWOK_EINVAL;
+    for (auto& ev : e->pev)
+        if (!ev) HIPCHK(e, hipEventCreate(&ev));
+    for (auto& ev : e->pev_hb)
+        if (!ev) HIPCHK(e, hipEventCreate(&ev));
+    e->prof = on != 0;
+    memset(e->prof_ms, 0, sizeof e->prof_ms);
+    e->prof_ticks = 0;
+    return KWOK_OK;
+}
+
+int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* ticks) {
+    if (!e) return KWOK_EINVAL;
+    if (ms_sum) memcpy(ms_sum, e->prof_ms, sizeof e->prof_ms);
+    if (ticks) *ticks = e->prof_ticks;
     return KWOK_OK;
 }
 

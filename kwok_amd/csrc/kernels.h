@@ -34,6 +34,7 @@ struct DevState {
     // pool replica
     uint64_t* used_bm;
     uint64_t* usable_bm;
+    uint64_t* rel_bm;        // Puts of this tick, folded into used/usable by k_pool_prep
     uint64_t* pool_index;    // ipPool.index (persistent)
     uint32_t* pool_blk;      // per word-block counts
     uint64_t* pool_blk_base;
@@ -53,8 +54,10 @@ struct DevState {
     uint64_t* tile_base;
     TickHdr* hdr;
     XMsg* xmsg;
-    uint32_t* use_list;
+    uint32_t* use_list;      // multi-rank exchange lists
     uint32_t* rel_list;
+    uint32_t* list_counts;   // [2]: n_use, n_rel (reset by k_emit)
+    int world;
     uint8_t* arena;
     uint64_t arena_cap;
     int32_t* hb_nodes;
@@ -73,8 +76,8 @@ void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const 
                       hipStream_t st);
 void launch_tick_front(const DevState& S, uint64_t now, uint64_t start, int world, hipStream_t st);
 void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st);
-void launch_pool_lists(const DevState& S, const ListDesc* ld, int nranks, bool uses, uint32_t max_n,
-                       hipStream_t st);
+void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
+void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
 void launch_pool_alloc(const DevState& S, hipStream_t st);
 void launch_emit(const DevState& S, hipStream_t st);
 void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st);

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
     }
     const uint32_t ptile = tile - S.node_tiles;
     const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    uint32_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running
+    uint32_t f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running, rel
     const bool live = first < S.n_pod_slots;
     uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = make_uint4(0, 0, 0, 0), ipa = make_uint4(0, 0, 0, 0),
           ipb = make_uint4(0, 0, 0, 0);
@@ -282,8 +282,17 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
         // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
         // addresses not already in `used` change the pool
         bool use = c.eval && ip && in_cidr(S.pool, ip) && !bm_test(S.used_bm, ip - S.pool.net);
-        wave_append(rel, ip, S.rel_list, &S.hdr->n_rel);
-        wave_append(use, ip, S.use_list, &S.hdr->n_use);
+        if (S.world == 1) {
+            // single rank: Use() in place; the Put of a released address waits in rel_bm
+            // and is folded by k_pool_prep, after every Use of this tick (Use -> Put order)
+            const uint64_t bit = ip - S.pool.net;
+            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
+            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+        } else {
+            wave_append(rel, ip, S.rel_list, &S.list_counts[1]);
+            wave_append(use, ip, S.use_list, &S.list_counts[0]);
+        }
+        f[8] += rel;
         if (c.need) {
             f[3]++;
             f[4] += S.specs[S.pod_spec[first + k]].max_len;
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
         f[6] += total && !c.need && c.phase == PHASE_PENDING;
         f[7] += total && (c.need || c.phase == PHASE_RUNNING);
     }
-    block_sum<8>(f);
+    block_sum<9>(f);
     if (t == 0) {
         uint32_t* o = S.tiles + (size_t)tile * TF_STRIDE;
         o[TF_DEL] = f[0];
@@ -304,74 +313,91 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
         o[TF_TOTAL] = f[5];
         o[TF_PENDING] = f[6];
         o[TF_RUNNING] = f[7];
+        o[TF_REL] = f[8];
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_scan: one block of 1024 threads.  Exclusive scan of the tile counts ->
-// tile bases; arena layout; counters; per-tick heartbeat template.
+// tile bases; arena layout; counters; per-tick heartbeat template.  Wave
+// shuffles inside each wave, one LDS exchange across the 16 waves.
 // ---------------------------------------------------------------------------
 constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_WAVES = SCAN_THREADS / 64;
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
+    const int l = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned long long y = __shfl_up((unsigned long long)x, off, 64);
+        if (l >= off) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor((unsigned long long)x, off, 64);
+    return x;
+}
+
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t now_unix, uint64_t start_unix,
                                                         int world_size) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, l = lane_id(), w = wave_id();
     const uint32_t T = S.node_tiles + S.pod_tiles;
     const uint32_t per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint32_t lo = min(T, t * per), hi = min(T, lo + per);
-    // fields scanned: hb, init, init_bytes (nodes); del, pp, pp_bytes, alloc (pods)
-    constexpr int NS = 7;
-    const int fld[NS] = {TF_HB, TF_INIT, TF_INIT_BYTES, TF_DEL, TF_PP, TF_PP_BYTES, TF_ALLOC};
-    uint64_t sum[NS] = {0, 0, 0, 0, 0, 0, 0};
-    uint64_t cnt[6] = {0, 0, 0, 0, 0, 0};  // lock, managed, ready, eval, total, pending+running packed below
-    uint64_t pend = 0, run = 0;
+    // scanned: hb, init, init_bytes (node tiles); del, pp, pp_bytes, alloc (pod tiles)
+    constexpr int NS = 7, NC = 8;
+    uint64_t sc[NS] = {0, 0, 0, 0, 0, 0, 0};
+    // reduced: lock, managed, ready (nodes); eval, total, pending, running, rel (pods)
+    uint64_t cn[NC] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t i = lo; i < hi; i++) {
         const uint32_t* o = S.tiles + (size_t)i * TF_STRIDE;
-        bool node = i < S.node_tiles;
-#pragma unroll
-        for (int f = 0; f < NS; f++) sum[f] += (node == (f < 3)) ? o[fld[f]] : 0u;
-        if (node) {
-            cnt[0] += o[TF_LOCK];
-            cnt[1] += o[TF_MANAGED];
-            cnt[2] += o[TF_READY];
+        if (i < S.node_tiles) {
+            sc[0] += o[TF_HB];
+            sc[1] += o[TF_INIT];
+            sc[2] += o[TF_INIT_BYTES];
+            cn[0] += o[TF_LOCK];
+            cn[1] += o[TF_MANAGED];
+            cn[2] += o[TF_READY];
         } else {
-            cnt[3] += o[TF_EVAL];
-            cnt[4] += o[TF_TOTAL];
-            pend += o[TF_PENDING];
-            run += o[TF_RUNNING];
+            sc[3] += o[TF_DEL];
+            sc[4] += o[TF_PP];
+            sc[5] += o[TF_PP_BYTES];
+            sc[6] += o[TF_ALLOC];
+            cn[3] += o[TF_EVAL];
+            cn[4] += o[TF_TOTAL];
+            cn[5] += o[TF_PENDING];
+            cn[6] += o[TF_RUNNING];
+            cn[7] += o[TF_REL];
         }
     }
-    // block scan (u64) through LDS, Hillis-Steele over 1024 entries
-    __shared__ uint64_t sh[SCAN_THREADS];
-    uint64_t excl[NS];
-    uint64_t total[NS];
+    __shared__ uint64_t wtot[SCAN_WAVES][NS];
+    __shared__ uint64_t wcnt[SCAN_WAVES][NC];
+    uint64_t incl[NS];
+#pragma unroll
     for (int f = 0; f < NS; f++) {
-        sh[t] = sum[f];
-        __syncthreads();
-        for (int off = 1; off < SCAN_THREADS; off <<= 1) {
-            uint64_t y = t >= off ? sh[t - off] : 0;
-            __syncthreads();
-            sh[t] += y;
-            __syncthreads();
-        }
-        excl[f] = sh[t] - sum[f];
-        total[f] = sh[SCAN_THREADS - 1];
-        __syncthreads();
+        incl[f] = wave_incl_scan64(sc[f]);
+        if (l == 63) wtot[w][f] = incl[f];
     }
-    // reductions of the plain counters
-    uint64_t red[8] = {cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], pend, run, 0};
-    for (int f = 0; f < 7; f++) {
-        sh[t] = red[f];
-        __syncthreads();
-        for (int s = SCAN_THREADS / 2; s > 0; s >>= 1) {
-            if (t < s) sh[t] += sh[t + s];
-            __syncthreads();
-        }
-        red[f] = sh[0];
-        __syncthreads();
+#pragma unroll
+    for (int f = 0; f < NC; f++) {
+        uint64_t r = wave_sum64(cn[f]);
+        if (l == 0) wcnt[w][f] = r;
     }
-    // second pass: per-tile bases
-    uint64_t run_b[NS];
-    for (int f = 0; f < NS; f++) run_b[f] = excl[f];
+    __syncthreads();
+    uint64_t run_b[NS], total[NS];
+#pragma unroll
+    for (int f = 0; f < NS; f++) {
+        uint64_t pre = 0, tot = 0;
+        for (int k = 0; k < SCAN_WAVES; k++) {
+            uint64_t v = wtot[k][f];
+            pre += k < w ? v : 0;
+            tot += v;
+        }
+        run_b[f] = pre + incl[f] - sc[f];
+        total[f] = tot;
+    }
     for (uint32_t i = lo; i < hi; i++) {
         const uint32_t* o = S.tiles + (size_t)i * TF_STRIDE;
         uint64_t* b = S.tile_base + (size_t)i * 4;
@@ -395,6 +421,11 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t now_
     }
     TickHdr* H = S.hdr;
     if (t == 0) {
+        uint64_t red[NC];
+        for (int f = 0; f < NC; f++) {
+            red[f] = 0;
+            for (int k = 0; k < SCAN_WAVES; k++) red[f] += wcnt[k][f];
+        }
         H->n_hb = (uint32_t)total[0];
         H->n_init = (uint32_t)total[1];
         H->init_bytes = total[2];
@@ -404,45 +435,47 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t now_
         H->n_alloc_local = (uint32_t)total[6];
         H->n_lock = (uint32_t)red[0];
         H->n_eval = (uint32_t)red[3];
+        H->n_rel = (uint32_t)red[7];
+        H->n_use = world_size > 1 ? S.list_counts[0] : 0;
         H->hb_base = 0;
         H->init_base = total[0] * (uint64_t)HB_STRIDE;
         H->pod_base = H->init_base + total[2];
         H->arena_bytes = H->pod_base + total[5];
         H->overflow = H->arena_bytes > S.arena_cap;
         uint64_t* L = H->local_counters;
-        L[0] = total[0];         // heartbeat
-        L[1] = total[1];         // node_init
-        L[2] = total[4];         // pod_patch
-        L[3] = total[3];         // delete
-        L[4] = total[6];         // alloc
-        L[5] = H->n_rel;         // release
-        L[6] = red[3];           // evaluated
-        L[7] = red[0];           // lock_checked
-        L[8] = red[1];           // nodes_managed
-        L[9] = red[2];           // nodes_ready
-        L[10] = red[4];          // pods_total
-        L[11] = red[5];          // pods_pending
-        L[12] = red[6];          // pods_running
+        L[0] = total[0];  // heartbeat
+        L[1] = total[1];  // node_init
+        L[2] = total[4];  // pod_patch
+        L[3] = total[3];  // delete
+        L[4] = total[6];  // alloc
+        L[5] = red[7];    // release
+        L[6] = red[3];    // evaluated
+        L[7] = red[0];    // lock_checked
+        L[8] = red[1];    // nodes_managed
+        L[9] = red[2];    // nodes_ready
+        L[10] = red[4];   // pods_total
+        L[11] = red[5];   // pods_pending
+        L[12] = red[6];   // pods_running
+        for (int k = 13; k < 16; k++) L[k] = 0;
         if (world_size == 1) {
             for (int k = 0; k < 16; k++) H->counters[k] = L[k];
             H->alloc_total = total[6];
             H->alloc_base = 0;
+            H->rel_total = red[7];
+        } else {
+            XMsg* X = S.xmsg;
+            X->alloc = total[6];
+            X->n_use = S.list_counts[0];
+            X->n_rel = S.list_counts[1];
+            for (int k = 0; k < 16; k++) X->counters[k] = L[k];
         }
     }
-    // exchange message (multi-rank): header + inline lists
+    // exchange message lists (multi-rank), inline when they fit
     if (world_size > 1) {
-        __syncthreads();
-        XMsg* X = S.xmsg;
-        uint32_t nu = H->n_use, nr = H->n_rel;
-        if (t == 0) {
-            X->alloc = total[6];
-            X->n_use = nu;
-            X->n_rel = nr;
-            for (int k = 0; k < 16; k++) X->counters[k] = H->local_counters[k];
-        }
+        const uint32_t nu = S.list_counts[0], nr = S.list_counts[1];
         if (nu + nr <= (uint32_t)XINLINE) {
-            for (uint32_t i = t; i < nu; i += SCAN_THREADS) X->ips[i] = S.use_list[i];
-            for (uint32_t i = t; i < nr; i += SCAN_THREADS) X->ips[nu + i] = S.rel_list[i];
+            for (uint32_t i = t; i < nu; i += SCAN_THREADS) S.xmsg->ips[i] = S.use_list[i];
+            for (uint32_t i = t; i < nr; i += SCAN_THREADS) S.xmsg->ips[nu + i] = S.rel_list[i];
         }
     }
     // per-tick heartbeat template: static bytes + Now / StartTime in the 10 slots
@@ -472,46 +505,53 @@ __global__ void k_xreduce(DevState S, const XMsg* all, int world_size, int rank)
     }
     H->alloc_total = tot;
     H->alloc_base = base;
+    uint64_t rel = 0;
+    for (int r = 0; r < world_size; r++) rel += all[r].n_rel;
+    H->rel_total = rel;
 }
 
 // ---------------------------------------------------------------------------
 // ipPool kernels on the replicated bitmaps
+//
+// Order inside a tick (DESIGN.md "Tick contract"): every Use (configurePod,
+// pod_controller.go:378-382) -> every Put of this tick's deletions
+// (pod_controller.go:329-336 / utils.go:100-108) -> the Gets (utils.go:83-98)
+// in canonical order.  Uses set `used` directly; Puts accumulate in rel_bm
+// (atomic ORs commute with the Uses) and k_pool_prep folds them:
+//   used &= ~rel, usable |= rel.
 // ---------------------------------------------------------------------------
-// Use (utils.go:110-117): set `used` for every listed in-CIDR address
-__global__ void k_pool_uses(DevState S, const ListDesc* ld, int nranks) {
-    for (int r = 0; r < nranks; r++) {
-        uint32_t n = nranks == 1 && ld[0].count_from_hdr ? S.hdr->n_use : ld[r].n_use;
-        const uint32_t* ips = ld[r].use;
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-            uint32_t ip = ips[i];
-            if (!in_cidr(S.pool, ip)) continue;
-            uint64_t b = ip - S.pool.net;
-            atomicOr((unsigned long long*)&S.used_bm[b >> 6], 1ull << (b & 63));
-        }
+// ingest-time Put (a Deleted watch event), applied immediately
+__global__ void k_pool_puts_now(DevState S, const uint32_t* ips, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t ip = ips[i];
+        if (!in_cidr(S.pool, ip)) continue;
+        uint64_t b = ip - S.pool.net;
+        atomicAnd((unsigned long long*)&S.used_bm[b >> 6], ~(1ull << (b & 63)));
+        atomicOr((unsigned long long*)&S.usable_bm[b >> 6], 1ull << (b & 63));
     }
 }
-// Put (utils.go:100-108): delete from used, add to usable
-__global__ void k_pool_puts(DevState S, const ListDesc* ld, int nranks) {
+// multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm
+__global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
     for (int r = 0; r < nranks; r++) {
-        uint32_t n = nranks == 1 && ld[0].count_from_hdr ? S.hdr->n_rel : ld[r].n_rel;
-        const uint32_t* ips = ld[r].rel;
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-            uint32_t ip = ips[i];
+        const ListDesc d = ld[r];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_use + d.n_rel; i += gridDim.x * blockDim.x) {
+            bool use = i < d.n_use;
+            uint32_t ip = use ? d.use[i] : d.rel[i - d.n_use];
             if (!in_cidr(S.pool, ip)) continue;
             uint64_t b = ip - S.pool.net;
-            atomicAnd((unsigned long long*)&S.used_bm[b >> 6], ~(1ull << (b & 63)));
-            atomicOr((unsigned long long*)&S.usable_bm[b >> 6], 1ull << (b & 63));
+            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
         }
     }
 }
 
-// free bits of `used` at or after the fresh cursor (ipPool.new skips used)
-__device__ __forceinline__ uint64_t free_mask(const DevState& S, uint64_t w, uint64_t cursor_bit) {
+// free bits for ipPool.new at or after the fresh cursor.  Addresses still
+// usable this tick are excluded: fresh allocation only happens once Get's
+// reuse branch has taken every usable address (take = U whenever F > 0).
+__device__ __forceinline__ uint64_t free_mask(const DevState& S, uint64_t w, uint64_t used, uint64_t usable,
+                                              uint64_t cursor_bit) {
     uint64_t lo = w * 64;
     if (lo + 64 <= cursor_bit) return 0;
-    // ipPool.new skips `used`; addresses still usable this tick are all taken
-    // by Get's reuse branch before any fresh allocation happens (take = U when F > 0)
-    uint64_t m = ~S.used_bm[w] & ~S.usable_bm[w];
+    uint64_t m = ~used & ~usable;
     if (cursor_bit > lo) m &= ~0ull << (cursor_bit - lo);
     if (lo + 64 > S.pool.size) m &= (S.pool.size - lo >= 64) ? ~0ull : ((1ull << (S.pool.size - lo)) - 1);
     return m;
@@ -521,20 +561,34 @@ __device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
     return a >= S.pool.net ? a - S.pool.net : 0;
 }
 
-constexpr int POOL_WPB = BLOCK * 4;  // bitmap words per block
+constexpr int POOL_WPT = 4;                  // bitmap words per thread
+constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per block
 
-// K1: per-block counts of usable bits and free bits (from cursor)
-__global__ __launch_bounds__(BLOCK) void k_pool_count(DevState S) {
-    if (S.hdr->alloc_total == 0) return;
+// fold this tick's Puts, then count usable / free bits per block for the plan
+__global__ __launch_bounds__(BLOCK) void k_pool_prep(DevState S) {
+    const TickHdr* H = S.hdr;
+    const bool fold = H->rel_total != 0, count = H->alloc_total != 0;
+    if (!fold && !count) return;
     const uint64_t cb = cursor_bit(S);
     uint32_t f[2] = {0, 0};
-    for (int k = 0; k < 4; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * 4 + k;
-        if (w < S.pool.words) {
-            f[0] += __popcll(S.usable_bm[w]);
-            f[1] += __popcll(free_mask(S, w, cb));
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
+        if (w >= S.pool.words) break;
+        uint64_t used = S.used_bm[w], usable = S.usable_bm[w];
+        if (fold) {
+            uint64_t r = S.rel_bm[w];
+            if (r) {
+                used &= ~r;
+                usable |= r;
+                S.used_bm[w] = used;
+                S.usable_bm[w] = usable;
+                S.rel_bm[w] = 0;
+            }
         }
+        f[0] += __popcll(usable);
+        f[1] += __popcll(free_mask(S, w, used, usable, cb));
     }
+    if (!count) return;
     block_sum<2>(f);
     if (threadIdx.x == 0) {
         S.pool_blk[2 * blockIdx.x] = f[0];
@@ -542,79 +596,59 @@ __global__ __launch_bounds__(BLOCK) void k_pool_count(DevState S) {
     }
 }
 
-// K2: one thread-block: scan block sums; plan = take `take_usable` lowest
-// usable addresses (the build's deterministic reuse rule), then fresh ones.
-__global__ __launch_bounds__(SCAN_THREADS) void k_pool_plan(DevState S, uint32_t nblk) {
+// select + commit.  Allocation ordinal g (global, canonical order):
+//   g < take                -> g-th lowest usable address (the build's reuse rule)
+//   g < take + fresh_in     -> (g-take)-th free in-CIDR address from the cursor
+//   otherwise               -> fresh_out_start + (g - take - fresh_in)  (beyond the CIDR)
+// Every rank commits ALL allocations to its replica; it records the addresses
+// of its own ordinals [alloc_base, alloc_base + n_alloc_local).  Each block
+// derives the plan from the per-block counts itself (no separate launch).
+__global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S, uint32_t nblk) {
     TickHdr* H = S.hdr;
-    if (H->alloc_total == 0) return;
-    __shared__ uint64_t su[SCAN_THREADS], sf[SCAN_THREADS];
-    const int t = threadIdx.x;
-    const uint32_t per = (nblk + SCAN_THREADS - 1) / SCAN_THREADS;
-    const uint32_t lo = min(nblk, t * per), hi = min(nblk, lo + per);
-    uint64_t u = 0, fr = 0;
-    for (uint32_t i = lo; i < hi; i++) u += S.pool_blk[2 * i], fr += S.pool_blk[2 * i + 1];
-    su[t] = u;
-    sf[t] = fr;
+    const uint64_t A = H->alloc_total;
+    if (A == 0) return;
+    __shared__ uint64_t sh[4];  // U, Fin, block base usable, block base free
+    if (threadIdx.x < 64) {
+        uint64_t u = 0, fr = 0, bu = 0, bf = 0;
+        for (uint32_t i = threadIdx.x; i < nblk; i += 64) {
+            uint64_t a = S.pool_blk[2 * i], c = S.pool_blk[2 * i + 1];
+            u += a;
+            fr += c;
+            if (i < blockIdx.x) bu += a, bf += c;
+        }
+        u = wave_sum64(u);
+        fr = wave_sum64(fr);
+        bu = wave_sum64(bu);
+        bf = wave_sum64(bf);
+        if (threadIdx.x == 0) sh[0] = u, sh[1] = fr, sh[2] = bu, sh[3] = bf;
+    }
     __syncthreads();
-    for (int off = 1; off < SCAN_THREADS; off <<= 1) {
-        uint64_t a = t >= off ? su[t - off] : 0, b = t >= off ? sf[t - off] : 0;
-        __syncthreads();
-        su[t] += a;
-        sf[t] += b;
-        __syncthreads();
-    }
-    uint64_t eu = su[t] - u, ef = sf[t] - fr;
-    for (uint32_t i = lo; i < hi; i++) {
-        S.pool_blk_base[2 * i] = eu;
-        S.pool_blk_base[2 * i + 1] = ef;
-        eu += S.pool_blk[2 * i];
-        ef += S.pool_blk[2 * i + 1];
-    }
-    if (t == 0) {
-        uint64_t U = su[SCAN_THREADS - 1], Fin = sf[SCAN_THREADS - 1];
-        uint64_t A = H->alloc_total;
-        uint64_t take = A < U ? A : U;
-        uint64_t F = A - take;
-        uint64_t fin = F < Fin ? F : Fin;
-        uint64_t fout = F - fin;
-        uint64_t cur = (uint64_t)S.pool.base + *S.pool_index;
-        uint64_t end = (uint64_t)S.pool.net + S.pool.size;
+    const uint64_t U = sh[0], Fin = sh[1];
+    const uint64_t take = A < U ? A : U, F = A - take, fin = F < Fin ? F : Fin, fout = F - fin;
+    const uint64_t cur = (uint64_t)S.pool.base + *S.pool_index;
+    const uint64_t end = (uint64_t)S.pool.net + S.pool.size;
+    const uint64_t fout0 = cur > end ? cur : end;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         H->usable_total = U;
         H->take_usable = take;
         H->fresh_in = fin;
-        H->fresh_out_start = cur > end ? cur : end;
-        // index after the last fresh address; committed to pool_index by k_emit
-        H->cursor_index = fout ? H->fresh_out_start + fout - S.pool.base : *S.pool_index;
-        // (fin > 0 && fout == 0: k_pool_select sets it)
+        H->fresh_out_start = fout0;
+        // ipPool.index after the last fresh address (k_emit commits it);
+        // fin > 0 && fout == 0: the thread that selects the last one sets it below
+        if (fout) H->cursor_index = fout0 + fout - S.pool.base;
+        else if (fin == 0) H->cursor_index = *S.pool_index;
     }
-}
-
-__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t k) {
-    // position of the k-th (0-based) set bit of m
-    for (uint32_t i = 0; i < k; i++) m &= m - 1;
-    return (uint32_t)(__ffsll((unsigned long long)m) - 1);
-}
-
-// K3: select + commit.  Allocation ordinal g (global, canonical order):
-//   g < take_usable           -> g-th lowest usable address
-//   g < take_usable+fresh_in  -> (g-take)-th free in-CIDR address from the cursor
-//   otherwise                 -> fresh_out_start + (g - take - fresh_in)   (beyond the CIDR)
-// Every rank commits ALL A allocations to its pool replica; it records the
-// addresses of its own range [alloc_base, alloc_base + n_alloc_local).
-__global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S) {
-    TickHdr* H = S.hdr;
-    if (H->alloc_total == 0) return;
-    const uint64_t take = H->take_usable, fin = H->fresh_in;
     const uint64_t lo_g = H->alloc_base, hi_g = lo_g + H->n_alloc_local;
     const uint64_t cb = cursor_bit(S);
-    const bool advance = fin > 0 && H->alloc_total == take + fin;
-    uint32_t c[2][4];
-    uint64_t wu[4], wf[4];
+    const bool advance = fin > 0 && fout == 0;
+    uint32_t c[2][POOL_WPT];
+    uint64_t wu[POOL_WPT], wf[POOL_WPT];
     uint32_t v[2] = {0, 0};
-    for (int k = 0; k < 4; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * 4 + k;
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
+        uint64_t used = w < S.pool.words ? S.used_bm[w] : ~0ull;
         wu[k] = w < S.pool.words ? S.usable_bm[w] : 0;
-        wf[k] = w < S.pool.words ? free_mask(S, w, cb) : 0;
+        wf[k] = w < S.pool.words ? free_mask(S, w, used, wu[k], cb) : 0;
         c[0][k] = __popcll(wu[k]);
         c[1][k] = __popcll(wf[k]);
         v[0] += c[0][k];
@@ -622,12 +656,11 @@ __global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S) {
     }
     uint32_t tot[2];
     block_excl_scan<2>(v, tot);
-    uint64_t ru = S.pool_blk_base[2 * blockIdx.x] + v[0];
-    uint64_t rf = S.pool_blk_base[2 * blockIdx.x + 1] + v[1];
-    for (int k = 0; k < 4; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * 4 + k;
+    uint64_t ru = sh[2] + v[0];
+    uint64_t rf = sh[3] + v[1];
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
         if (w >= S.pool.words) break;
-        // usable bits with rank < take
         if (ru < take && wu[k]) {
             uint64_t n = take - ru < c[0][k] ? take - ru : c[0][k];
             uint64_t m = wu[k], sel = 0;
@@ -638,8 +671,8 @@ __global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S) {
                 uint64_t g = ru + j;
                 if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
             }
-            S.usable_bm[w] &= ~sel;  // ipPool.Get: delete(usable) ...
-            S.used_bm[w] |= sel;     // ... used[ip] = struct{}{}  (one thread owns word w)
+            S.usable_bm[w] &= ~sel;  // ipPool.Get: delete(usable, ip) ...
+            S.used_bm[w] |= sel;     // ... used[ip]   (one thread owns word w)
         }
         ru += c[0][k];
         if (rf < fin && wf[k]) {
@@ -653,7 +686,7 @@ __global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S) {
                 uint64_t g = take + rf + j;
                 if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
             }
-            S.used_bm[w] |= sel;  // ipPool.new: used[ip] (usable set/unset nets to unchanged)
+            S.used_bm[w] |= sel;  // ipPool.new: used[ip]  (usable add + Get delete net to nothing)
             if (advance && rf + n == fin) H->cursor_index = (uint64_t)S.pool.net + w * 64 + b + 1 - S.pool.base;
         }
         rf += c[1][k];
@@ -759,7 +792,11 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevState S) {
     const uint32_t tile = blockIdx.x;
     const int t = threadIdx.x;
     const TickHdr* H = S.hdr;
-    if (tile == 0 && t == 0 && H->alloc_total) *S.pool_index = H->cursor_index;
+    if (tile == 0 && t == 0) {
+        if (H->alloc_total) *S.pool_index = H->cursor_index;
+        S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
+        S.list_counts[1] = 0;
+    }
     __shared__ PodJob jobs[POD_TILE];  // 32 KiB (node tiles reuse it for InitJob)
     if (tile < S.node_tiles) {
         const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
@@ -963,12 +1000,6 @@ __global__ void k_apply_pod_ops(DevState S, const PodOp* ops, uint32_t n) {
         S.pod_ip[o.slot] = o.pod_ip;
     }
 }
-__global__ void k_reset_lists(DevState S) {
-    if (threadIdx.x == 0) {
-        S.hdr->n_use = 0;
-        S.hdr->n_rel = 0;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // host-side launchers
@@ -981,16 +1012,19 @@ void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const 
     if (np) hipLaunchKernelGGL(k_apply_pod_ops, dim3(cdiv(np, 256)), dim3(256), 0, st, S, pops, np);
 }
 
-void launch_pool_lists(const DevState& S, const ListDesc* ld, int nranks, bool uses, uint32_t max_n,
-                       hipStream_t st) {
-    uint32_t g = max_n ? cdiv(max_n, 256) : 1024;
-    if (g > 2048) g = 2048;
-    if (uses) hipLaunchKernelGGL(k_pool_uses, dim3(g), dim3(256), 0, st, S, ld, nranks);
-    else hipLaunchKernelGGL(k_pool_puts, dim3(g), dim3(256), 0, st, S, ld, nranks);
+void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st) {
+    uint32_t g = n ? cdiv(n, 256) : 1;
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pool_puts_now, dim3(g), dim3(256), 0, st, S, ips, n);
+}
+
+void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st) {
+    uint32_t g = max_n ? cdiv(max_n, 256) : 1;
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
 void launch_tick_front(const DevState& S, uint64_t now, uint64_t start, int world, hipStream_t st) {
-    hipLaunchKernelGGL(k_reset_lists, dim3(1), dim3(64), 0, st, S);
     hipLaunchKernelGGL(k_classify, dim3(S.node_tiles + S.pod_tiles), dim3(BLOCK), 0, st, S);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, st, S, now, start, world);
 }
@@ -1001,9 +1035,8 @@ void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hip
 
 void launch_pool_alloc(const DevState& S, hipStream_t st) {
     uint32_t nblk = cdiv(S.pool.words, POOL_WPB);
-    hipLaunchKernelGGL(k_pool_count, dim3(nblk), dim3(BLOCK), 0, st, S);
-    hipLaunchKernelGGL(k_pool_plan, dim3(1), dim3(SCAN_THREADS), 0, st, S, nblk);
-    hipLaunchKernelGGL(k_pool_select, dim3(nblk), dim3(BLOCK), 0, st, S);
+    hipLaunchKernelGGL(k_pool_prep, dim3(nblk), dim3(BLOCK), 0, st, S);
+    hipLaunchKernelGGL(k_pool_select, dim3(nblk), dim3(BLOCK), 0, st, S, nblk);
 }
 
 void launch_emit(const DevState& S, hipStream_t st) {

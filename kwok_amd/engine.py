@@ -75,6 +75,8 @@ def declare(lib, pre):
             "device_outputs": (C.c_int, [VP, P(abi.DeviceView)]),
             "bucket_of": (U32, [C.c_char_p, SZ, U32]),
             "rank_of_bucket": (I32, [U32, U32, I32]),
+            "profile_enable": (C.c_int, [VP, C.c_int]),
+            "profile_read": (C.c_int, [VP, VP, VP]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name)
@@ -139,7 +141,8 @@ class EngineBase:
         create = self._fn("engine_create" if self.PREFIX == "kwok_" else "create")
         rc = create(C.byref(cfg), C.byref(h))
         if rc != 0:
-            raise KwokError(rc, "create")
+            msg = self._fn("last_error")(None)
+            raise KwokError(rc, "create: %s" % (msg or b"").decode())
         self._h = h
         self.last = None
 
@@ -265,6 +268,17 @@ class Engine(EngineBase):
 
     def __init__(self, cfg=None, **kw):
         super().__init__(load_engine_lib(), cfg if cfg is not None else make_config(**kw))
+
+    PHASES = ("front", "pool", "emit", "hb_fill")
+
+    def profile_enable(self, on=True):
+        self._check(self._lib.kwok_profile_enable(self._h, 1 if on else 0), "profile_enable")
+
+    def profile_read(self):
+        ms = (C.c_double * 4)()
+        n = C.c_uint64()
+        self._check(self._lib.kwok_profile_read(self._h, ms, C.byref(n)), "profile_read")
+        return dict(zip(self.PHASES, list(ms))), n.value
 
     def device_outputs(self):
         v = abi.DeviceView()

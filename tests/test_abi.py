@@ -42,7 +42,7 @@ def test_oracle_library_exports():
         if f in ("kwok_engine_create", "kwok_engine_destroy"):
             name = name.replace("engine_", "")
         if f in ("kwok_abi_version", "kwok_comm_id", "kwok_finalizer_patch", "kwok_device_outputs",
-                 "kwok_bucket_of", "kwok_rank_of_bucket"):
+                 "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read"):
             continue
         assert hasattr(lib, name), name
 
