@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -113,6 +114,13 @@ struct kwok_engine {
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
     uint32_t hb_grid = 2048;
+    // single-rank tick as a captured hipGraph (re-captured when device pointers move)
+    uint64_t* now_h = nullptr;  // pinned: Now() of the tick, copied by the graph's first node
+    uint64_t* d_now = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    DevState graph_S{};
+    bool graph_prof = false, use_graph = true;
     // diagnostics
     bool prof = false;
     hipEvent_t pev[KWOK_T_COUNT + 1] = {};
@@ -433,6 +441,10 @@ void kwok_engine_destroy(kwok_engine* e) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : e->pev_hb)
         if (ev) (void)hipEventDestroy(ev);
+    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    if (e->now_h) (void)hipHostFree(e->now_h);
+    if (e->d_now) (void)hipFree(e->d_now);
     if (e->ev_front) (void)hipEventDestroy(e->ev_front);
     if (e->ev_hb) (void)hipEventDestroy(e->ev_hb);
     if (e->st2) (void)hipStreamDestroy(e->st2);
@@ -548,7 +560,15 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
-    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
+    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->now_h, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+        return bail(KWOK_ENOMEM);
+    if ((rc = dalloc(e, &e->d_now, 1))) return bail(rc);
+    S.tick_now = e->d_now;
+    {
+        const char* ng = getenv("KWOK_NO_GRAPH");
+        e->use_graph = !(ng && ng[0] == '1');
+    }
     if (W > 1) {
         if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
         if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
@@ -832,16 +852,18 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     return flush_ops(e);
 }
 
-int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
-    if (!e) return KWOK_EINVAL;
-    if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
+namespace {
+// Enqueue one tick on e->st (+ e->st2).  Single rank: no host synchronisation,
+// so the whole sequence is captured once as a hipGraph and replayed.
+int enqueue_tick(kwok_engine* e) {
     DevState& S = e->S;
     hipStream_t st = e->st;
     auto mark = [&](int i) {
         if (e->prof) (void)hipEventRecord(e->pev[i], st);
     };
     mark(0);
-    launch_tick_front(S, (uint64_t)now_unix, (uint64_t)e->start, e->W, st);
+    HIPCHK(e, hipMemcpyAsync(e->d_now, e->now_h, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    launch_tick_front(S, (uint64_t)e->start, e->W, st);
     // heartbeat emission only needs the scan (count + per-tick template): run it
     // on the second stream, overlapped with the exchange, the pool and emit
     HIPCHK(e, hipEventRecord(e->ev_front, st));
@@ -901,6 +923,43 @@ int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
     mark(4);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipMemcpyAsync(e->hdr_h, S.hdr, sizeof(TickHdr), hipMemcpyDeviceToHost, st));
+    return KWOK_OK;
+}
+
+int capture_tick_graph(kwok_engine* e) {
+    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
+    if (e->graph) (void)hipGraphDestroy(e->graph);
+    e->graph_exec = nullptr;
+    e->graph = nullptr;
+    HIPCHK(e, hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_tick(e);
+    hipGraph_t g = nullptr;
+    hipError_t r = hipStreamEndCapture(e->st, &g);
+    if (rc) return rc;
+    if (r != hipSuccess) return e->fail(KWOK_EDEVICE, "hipStreamEndCapture: %s", hipGetErrorString(r));
+    e->graph = g;
+    HIPCHK(e, hipGraphInstantiate(&e->graph_exec, g, nullptr, nullptr, 0));
+    e->graph_S = e->S;
+    e->graph_prof = e->prof;
+    return KWOK_OK;
+}
+}  // namespace
+
+extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
+    if (!e) return KWOK_EINVAL;
+    if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
+    hipStream_t st = e->st;
+    *e->now_h = (uint64_t)now_unix;
+    if (e->W == 1 && e->use_graph) {
+        if (!e->graph_exec || e->graph_prof != e->prof || memcmp(&e->graph_S, &e->S, sizeof(DevState)) != 0) {
+            int rc = capture_tick_graph(e);
+            if (rc) return rc;
+        }
+        HIPCHK(e, hipGraphLaunch(e->graph_exec, st));
+    } else {
+        int rc = enqueue_tick(e);
+        if (rc) return rc;
+    }
     HIPCHK(e, hipStreamSynchronize(st));
     const TickHdr& H = *e->hdr_h;
     if (e->prof) {

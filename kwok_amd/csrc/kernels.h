@@ -70,11 +70,12 @@ struct DevState {
     int32_t* del_pods;
     uint8_t* del_fin;
     uint32_t node_ip;
+    const uint64_t* tick_now;  // Now() of the current tick (device scalar)
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
                       hipStream_t st);
-void launch_tick_front(const DevState& S, uint64_t now, uint64_t start, int world, hipStream_t st);
+void launch_tick_front(const DevState& S, uint64_t start, int world, hipStream_t st);
 void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st);
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);

@@ -318,11 +318,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: one block of 1024 threads.  Exclusive scan of the tile counts ->
+// k_scan: one block of 256 threads.  Exclusive scan of the tile counts ->
 // tile bases; arena layout; counters; per-tick heartbeat template.  Wave
 // shuffles inside each wave, one LDS exchange across the 16 waves.
 // ---------------------------------------------------------------------------
-constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_THREADS = 256;  // 4 waves: u64 partials stay in registers (no scratch)
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;
 
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
@@ -340,8 +340,8 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
     return x;
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t now_unix, uint64_t start_unix,
-                                                        int world_size) {
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t start_unix, int world_size) {
+    const uint64_t now_unix = *S.tick_now;  // written by the tick's (graph-captured) H2D copy
     const int t = threadIdx.x, l = lane_id(), w = wave_id();
     const uint32_t T = S.node_tiles + S.pod_tiles;
     const uint32_t per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
@@ -1024,9 +1024,9 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
-void launch_tick_front(const DevState& S, uint64_t now, uint64_t start, int world, hipStream_t st) {
+void launch_tick_front(const DevState& S, uint64_t start, int world, hipStream_t st) {
     hipLaunchKernelGGL(k_classify, dim3(S.node_tiles + S.pod_tiles), dim3(BLOCK), 0, st, S);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, st, S, now, start, world);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, st, S, start, world);
 }
 
 void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st) {

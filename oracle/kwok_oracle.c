@@ -506,8 +506,10 @@ int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n
         const kwok_node_event* e = &ev[i];
         const char* name = arena + e->name.off;
         int st = KWOK_OK;
-        int32_t h;
-        if (e->op == KWOK_OP_DELETE) {
+        int32_t h = -1;
+        if (e->name.len == 0 || e->name.len > 253) {
+            st = KWOK_EDOMAIN;
+        } else if (e->op == KWOK_OP_DELETE) {
             /* node_controller.go:265-269: Deleted -> nodesSets.Delete */
             h = node_find(o, name, e->name.len);
             if (h < 0) {
@@ -575,8 +577,10 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
         } else {
             opod_t* p;
             if (h < 0) {
-                int32_t nh = e->node_handle >= 0 ? e->node_handle
-                                                 : node_entry(o, arena + e->node_name.off, e->node_name.len, &st);
+                int32_t nh;
+                if (e->node_handle >= 0) nh = e->node_handle;
+                else if (e->node_name.len == 0 || e->node_name.len > 253) nh = -1, st = KWOK_EDOMAIN;
+                else nh = node_entry(o, arena + e->node_name.off, e->node_name.len, &st);
                 if (nh >= 0) {
                     uint32_t b = (uint32_t)nh / o->cn;
                     h = -1;

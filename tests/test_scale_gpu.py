@@ -197,8 +197,9 @@ def test_churn_parity(seed, cidr):
     d = Driver(kw, seed)
     rng = d.rng
     names = ["node-%07d" % i for i in range(1000)]
-    nh, _ = d.nodes(names, managed=(rng.random(1000) < 0.9).astype(np.uint8),
-                    lockable=(rng.random(1000) < 0.95).astype(np.uint8))
+    nh, st = d.nodes(names, managed=(rng.random(1000) < 0.9).astype(np.uint8),
+                     lockable=(rng.random(1000) < 0.95).astype(np.uint8))
+    assert (st == 0).all()
     net = ipaddress.IPv4Network(cidr, strict=False)
     ip_range = (int(net.network_address), int(net.network_address) + min(net.num_addresses, 4096))
     ev, ar = new_pods(rng, nh, 20_000, d.spec, 0.02, ip_range)
@@ -226,14 +227,16 @@ def test_partial_management_flap_parity():
     """C5-style: ManageAllNodes=false with a selector on 50% of the nodes, a
     disregard annotation on 0.1%, and 1% of the managed nodes deleted and
     re-created per tick."""
-    kw = dict(cidr="10.0.0.1/12", node_ip="10.1.2.3", buckets=1024, node_slots_per_bucket=32,
-              pod_slots_per_bucket=320)
+    cn, cp = workload.slots_for(20_000, 1024, 12)
+    kw = dict(cidr="10.0.0.1/12", node_ip="10.1.2.3", buckets=1024, node_slots_per_bucket=cn,
+              pod_slots_per_bucket=cp)
     d = Driver(kw, 7)
     rng = d.rng
     names = ["node-%07d" % i for i in range(20_000)]
     managed = (rng.random(len(names)) < 0.5).astype(np.uint8)
     lockable = (rng.random(len(names)) >= 0.001).astype(np.uint8)
-    nh, _ = d.nodes(names, managed, lockable)
+    nh, st = d.nodes(names, managed, lockable)
+    assert (st == 0).all()
     ev, ar = new_pods(rng, nh, 100_000, d.spec)
     d.pods(ev, ar)
     d.tick("c5 tick 0")
