@@ -1,0 +1,10 @@
+#!/bin/bash
+# PMC passes (counters in their own runs, kernel-trace only): FETCH_SIZE, WRITE_SIZE
+set -o pipefail
+TAG=${1:-x}
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline 0 > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || exit $?
+done
+ls -R $R/gpurun_out/pmc_${TAG}_FETCH_SIZE | head
