@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--nodes-per-rank", type=int, default=NODES_PER_RANK)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
     ap.add_argument("--cpu-nodes", type=int, default=NODES_PER_RANK)
-    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-ticks", type=int, default=20)
     return ap.parse_args()
 
 
@@ -103,7 +103,6 @@ def main():
             first = dict(zip(keng.abi.COUNTERS, list(r.counters)))
         now += 30
 
-    e.profile_enable(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -125,13 +124,24 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
+    # roofline pass: the same ticks replayed eagerly with HIP events around each
+    # phase on the stream it runs on (k_hb_fill: the heartbeat stream)
+    e.profile_enable(True)
+    for k in range(a.roofline_ticks):
+        e.tick(now, read=False)
+        now += 30
     phases, nt = e.profile_read()
+    e.profile_enable(False)
 
     if rank == 0:
         hb_ms = phases["hb_fill"] / max(nt, 1)
         n_hb_local = last.local_counters[0]
         achieved = HB_BYTES * n_hb_local / (hb_ms * 1e-3) / 1e9 if hb_ms > 0 else 0.0
-        tick_bytes = None
+        traffic, traffic_src = None, None
+        pmc = os.path.join(ROOT, "profiles", "r1_pmc_c2.json")
+        if os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK:
+            traffic = json.load(open(pmc))["kernels"]["k_hb_fill"]["hbm_bytes"]
+            traffic_src = "profiles/r1_pmc_c2.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same config)"
         out = {
             "metric": "state transitions/sec at 1M nodes/10M pods, 1-8 MI355X; % HBM roofline",
             "value": trans / dt,
@@ -156,7 +166,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_hb_fill", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "bytes_per_launch": HB_BYTES * n_hb_local, "avg_launch_ms": hb_ms,
-                         "traffic": tick_bytes},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "timing": "HIP events on the heartbeat stream, eager replay of %d ticks" % nt},
         }
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_nodes)

@@ -78,6 +78,9 @@ struct kwok_engine {
     std::vector<uint8_t> pod_used, pod_delpend;      // [PL]
     std::vector<uint16_t> pod_node;                  // [PL] local node index in bucket
     std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
+    std::vector<uint16_t> pod_fill;                  // per bucket: upper bound of used slots (only grows)
+    bool pod_fill_dirty = false;
+    uint16_t* d_pod_fill = nullptr;
     std::vector<uint32_t> pending_del;
 
     // ---- batch staging ----
@@ -116,7 +119,6 @@ struct kwok_engine {
     uint32_t hb_grid = 2048;
     // single-rank tick as a captured hipGraph (re-captured when device pointers move)
     uint64_t* now_h = nullptr;  // pinned: Now() of the tick, copied by the graph's first node
-    uint64_t* d_now = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     DevState graph_S{};
@@ -255,6 +257,11 @@ int flush_ops(kwok_engine* e) {
     memcpy(h + uo, e->puts.data(), ub);
     char* d = (char*)e->d_ops;
     HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
+    if (e->pod_fill_dirty) {  // before the ops that fill the new slots are visible to a tick
+        HIPCHK(e, hipMemcpyAsync(e->d_pod_fill, e->pod_fill.data(), e->pod_fill.size() * 2, hipMemcpyHostToDevice,
+                                 e->st));
+        e->pod_fill_dirty = false;
+    }
     launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)e->nops.size(), (const PodOp*)(d + po),
                      (uint32_t)e->pops.size(), e->st);
     if (!e->puts.empty())  // ingest-time Puts (Deleted events, pod_controller.go:329-336)
@@ -444,7 +451,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
     if (e->graph) (void)hipGraphDestroy(e->graph);
     if (e->now_h) (void)hipHostFree(e->now_h);
-    if (e->d_now) (void)hipFree(e->d_now);
+    if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
     if (e->ev_front) (void)hipEventDestroy(e->ev_front);
     if (e->ev_hb) (void)hipEventDestroy(e->ev_hb);
     if (e->st2) (void)hipStreamDestroy(e->st2);
@@ -534,7 +541,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.pod_ctime, PLa)) || (rc = dalloc(e, &S.pod_ip, PLa)) ||
         (rc = dalloc(e, &S.host_ip, PLa)) || (rc = dalloc(e, &S.used_bm, e->pool.words)) ||
         (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.rel_bm, e->pool.words)) ||
-        (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &S.pool_index, 1)) ||
+        (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &e->d_pod_fill, e->nb)) || (rc = dalloc(e, &S.pool_index, 1)) ||
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.pool_blk_base, 2 * (size_t)nblk)) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) || (rc = dalloc(e, &S.hb_tmpl, HB_STRIDE)) ||
@@ -563,8 +570,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&e->now_h, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
         return bail(KWOK_ENOMEM);
-    if ((rc = dalloc(e, &e->d_now, 1))) return bail(rc);
-    S.tick_now = e->d_now;
+    S.tick_now = e->now_h;   // zero-copy: k_scan reads the clock from pinned host memory
+    S.hdr_host = e->hdr_h;   // zero-copy: k_emit_pods publishes the header
+    S.pod_fill = e->d_pod_fill;
     {
         const char* ng = getenv("KWOK_NO_GRAPH");
         e->use_graph = !(ng && ng[0] == '1');
@@ -587,6 +595,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->pod_delpend.assign(e->PL, 0);
     e->pod_node.assign(e->PL, 0);
     e->pod_bits.assign((size_t)e->nb * ((e->Cp + 63) / 64), 0);
+    e->pod_fill.assign(e->nb, 0);
     e->node_stamp.assign(e->NL, 0);
     e->node_opi.assign(e->NL, 0);
     e->pod_stamp.assign(e->PL, 0);
@@ -796,6 +805,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                     } else {
                         slot = bl * e->Cp + (uint32_t)idx;
                         set_bit(e->pod_bits, e->Cp, bl, (uint32_t)idx, true);
+                        if ((uint32_t)idx + 1 > e->pod_fill[bl]) {
+                            e->pod_fill[bl] = (uint16_t)std::min<uint32_t>(e->Cp, ((uint32_t)idx + 8) & ~7u);
+                            e->pod_fill_dirty = true;
+                        }
                         e->pod_used[slot] = 1;
                         e->pod_node[slot] = (uint16_t)(nslot % e->Cn);
                         e->nodes[nslot].refs++;
@@ -862,15 +875,15 @@ int enqueue_tick(kwok_engine* e) {
         if (e->prof) (void)hipEventRecord(e->pev[i], st);
     };
     mark(0);
-    HIPCHK(e, hipMemcpyAsync(e->d_now, e->now_h, sizeof(uint64_t), hipMemcpyHostToDevice, st));
     launch_tick_front(S, (uint64_t)e->start, e->W, st);
-    // heartbeat emission only needs the scan (count + per-tick template): run it
-    // on the second stream, overlapped with the exchange, the pool and emit
+    // the node side (heartbeat stream + node list / node-init patches) only needs
+    // the scan: run it on the second stream, overlapped with the exchange, the
+    // pool and the pod side
     HIPCHK(e, hipEventRecord(e->ev_front, st));
     HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_front, 0));
-    if (e->prof) (void)hipEventRecord(e->pev_hb[0], e->st2);
-    launch_hb_fill(S, e->hb_grid, e->st2);
-    if (e->prof) (void)hipEventRecord(e->pev_hb[1], e->st2);
+    if (e->prof) launch_hb_fill(S, e->hb_grid, e->st2, e->pev_hb[0], e->pev_hb[1]);
+    else launch_hb_fill(S, e->hb_grid, e->st2);
+    launch_emit_nodes(S, e->st2);
     HIPCHK(e, hipEventRecord(e->ev_hb, e->st2));
     if (e->W > 1) {
         // one allgather of the fixed-size exchange message; a second one for
@@ -917,12 +930,11 @@ int enqueue_tick(kwok_engine* e) {
     mark(1);  // (multi-rank: includes the exchange)
     launch_pool_alloc(S, st);
     mark(2);
-    launch_emit(S, st);
+    launch_emit_pods(S, st);
     mark(3);
     HIPCHK(e, hipStreamWaitEvent(st, e->ev_hb, 0));
     mark(4);
     HIPCHK(e, hipGetLastError());
-    HIPCHK(e, hipMemcpyAsync(e->hdr_h, S.hdr, sizeof(TickHdr), hipMemcpyDeviceToHost, st));
     return KWOK_OK;
 }
 
@@ -950,7 +962,7 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
     if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
     hipStream_t st = e->st;
     *e->now_h = (uint64_t)now_unix;
-    if (e->W == 1 && e->use_graph) {
+    if (e->W == 1 && e->use_graph && !e->prof) {  // graph event nodes do not time: profile eagerly
         if (!e->graph_exec || e->graph_prof != e->prof || memcmp(&e->graph_S, &e->S, sizeof(DevState)) != 0) {
             int rc = capture_tick_graph(e);
             if (rc) return rc;

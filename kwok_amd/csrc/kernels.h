@@ -70,7 +70,9 @@ struct DevState {
     int32_t* del_pods;
     uint8_t* del_fin;
     uint32_t node_ip;
-    const uint64_t* tick_now;  // Now() of the current tick (device scalar)
+    const uint64_t* tick_now;  // Now() of the current tick (pinned host scalar, zero-copy)
+    TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
+    const uint16_t* pod_fill;  // per owned bucket: upper bound of used pod slots (host-maintained)
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
@@ -80,7 +82,9 @@ void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hip
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
 void launch_pool_alloc(const DevState& S, hipStream_t st);
-void launch_emit(const DevState& S, hipStream_t st);
-void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st);
+void launch_emit_nodes(const DevState& S, hipStream_t st);
+void launch_emit_pods(const DevState& S, hipStream_t st);
+void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st, hipEvent_t t0 = nullptr,
+                    hipEvent_t t1 = nullptr);
 
 }  // namespace kwok

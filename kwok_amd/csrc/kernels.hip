@@ -17,6 +17,7 @@
 //   k_hb_fill    the dominant kernel: n_managed identical 1059-byte heartbeat
 //                patches streamed from an LDS-staged template with 16-byte
 //                stores                                   (node_controller.go:145-204,393-401)
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "device.h"
@@ -250,16 +251,15 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
     const uint32_t ptile = tile - S.node_tiles;
     const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
     uint32_t f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running, rel
-    const bool live = first < S.n_pod_slots;
+    // slots at or above the bucket's fill mark are known empty: no loads
+    const bool live = first < S.n_pod_slots && (first % S.cp) < S.pod_fill[first / S.cp];
     uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = make_uint4(0, 0, 0, 0), ipa = make_uint4(0, 0, 0, 0),
           ipb = make_uint4(0, 0, 0, 0);
     if (live) {
         st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
-        if (st4.x | st4.y | st4.z | st4.w) {
-            nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
-            ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
-            ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
-        }
+        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
+        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
+        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
     }
     const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
     const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
 // tile bases; arena layout; counters; per-tick heartbeat template.  Wave
 // shuffles inside each wave, one LDS exchange across the 16 waves.
 // ---------------------------------------------------------------------------
-constexpr int SCAN_THREADS = 256;  // 4 waves: u64 partials stay in registers (no scratch)
+constexpr int SCAN_THREADS = 512;  // 256-VGPR budget: partials stay in registers
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;
 
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
@@ -340,45 +340,54 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
     return x;
 }
 
+// tile record -> the 7 scanned fields and 8 reduced fields
+struct TileVals {
+    uint32_t sc[7], cn[8];
+};
+__device__ __forceinline__ void load_tile(const DevState& S, uint32_t i, TileVals& v) {
+    const uint4* o = reinterpret_cast<const uint4*>(S.tiles + (size_t)i * TF_STRIDE);
+    const uint4 a = o[0], b = o[1], c = o[2], d = o[3];
+    const uint32_t f[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    if (i < S.node_tiles) {
+        v.sc[0] = f[TF_HB], v.sc[1] = f[TF_INIT], v.sc[2] = f[TF_INIT_BYTES];
+        v.sc[3] = v.sc[4] = v.sc[5] = v.sc[6] = 0;
+        v.cn[0] = f[TF_LOCK], v.cn[1] = f[TF_MANAGED], v.cn[2] = f[TF_READY];
+        v.cn[3] = v.cn[4] = v.cn[5] = v.cn[6] = v.cn[7] = 0;
+    } else {
+        v.sc[0] = v.sc[1] = v.sc[2] = 0;
+        v.sc[3] = f[TF_DEL], v.sc[4] = f[TF_PP], v.sc[5] = f[TF_PP_BYTES], v.sc[6] = f[TF_ALLOC];
+        v.cn[0] = v.cn[1] = v.cn[2] = 0;
+        v.cn[3] = f[TF_EVAL], v.cn[4] = f[TF_TOTAL], v.cn[5] = f[TF_PENDING], v.cn[6] = f[TF_RUNNING];
+        v.cn[7] = f[TF_REL];
+    }
+}
+
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t start_unix, int world_size) {
-    const uint64_t now_unix = *S.tick_now;  // written by the tick's (graph-captured) H2D copy
+    const uint64_t now_unix = *(volatile const uint64_t*)S.tick_now;  // pinned host scalar
     const int t = threadIdx.x, l = lane_id(), w = wave_id();
     const uint32_t T = S.node_tiles + S.pod_tiles;
     const uint32_t per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint32_t lo = min(T, t * per), hi = min(T, lo + per);
     // scanned: hb, init, init_bytes (node tiles); del, pp, pp_bytes, alloc (pod tiles)
-    constexpr int NS = 7, NC = 8;
-    uint64_t sc[NS] = {0, 0, 0, 0, 0, 0, 0};
     // reduced: lock, managed, ready (nodes); eval, total, pending, running, rel (pods)
-    uint64_t cn[NC] = {0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr int NS = 7, NC = 8;
+    uint32_t sc[NS] = {0, 0, 0, 0, 0, 0, 0}, cn[NC] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t i = lo; i < hi; i++) {
-        const uint32_t* o = S.tiles + (size_t)i * TF_STRIDE;
-        if (i < S.node_tiles) {
-            sc[0] += o[TF_HB];
-            sc[1] += o[TF_INIT];
-            sc[2] += o[TF_INIT_BYTES];
-            cn[0] += o[TF_LOCK];
-            cn[1] += o[TF_MANAGED];
-            cn[2] += o[TF_READY];
-        } else {
-            sc[3] += o[TF_DEL];
-            sc[4] += o[TF_PP];
-            sc[5] += o[TF_PP_BYTES];
-            sc[6] += o[TF_ALLOC];
-            cn[3] += o[TF_EVAL];
-            cn[4] += o[TF_TOTAL];
-            cn[5] += o[TF_PENDING];
-            cn[6] += o[TF_RUNNING];
-            cn[7] += o[TF_REL];
-        }
+        TileVals v;
+        load_tile(S, i, v);
+#pragma unroll
+        for (int f = 0; f < NS; f++) sc[f] += v.sc[f];
+#pragma unroll
+        for (int f = 0; f < NC; f++) cn[f] += v.cn[f];
     }
     __shared__ uint64_t wtot[SCAN_WAVES][NS];
     __shared__ uint64_t wcnt[SCAN_WAVES][NC];
-    uint64_t incl[NS];
+    uint64_t ex[NS];
 #pragma unroll
     for (int f = 0; f < NS; f++) {
-        incl[f] = wave_incl_scan64(sc[f]);
-        if (l == 63) wtot[w][f] = incl[f];
+        uint64_t inc = wave_incl_scan64(sc[f]);
+        ex[f] = inc - sc[f];
+        if (l == 63) wtot[w][f] = inc;
     }
 #pragma unroll
     for (int f = 0; f < NC; f++) {
@@ -386,38 +395,30 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t star
         if (l == 0) wcnt[w][f] = r;
     }
     __syncthreads();
-    uint64_t run_b[NS], total[NS];
+    uint64_t total[NS];
 #pragma unroll
     for (int f = 0; f < NS; f++) {
         uint64_t pre = 0, tot = 0;
+#pragma unroll
         for (int k = 0; k < SCAN_WAVES; k++) {
             uint64_t v = wtot[k][f];
             pre += k < w ? v : 0;
             tot += v;
         }
-        run_b[f] = pre + incl[f] - sc[f];
+        ex[f] += pre;
         total[f] = tot;
     }
     for (uint32_t i = lo; i < hi; i++) {
-        const uint32_t* o = S.tiles + (size_t)i * TF_STRIDE;
+        TileVals v;
+        load_tile(S, i, v);
         uint64_t* b = S.tile_base + (size_t)i * 4;
         if (i < S.node_tiles) {
-            b[0] = run_b[0];
-            b[1] = run_b[1];
-            b[2] = run_b[2];
-            run_b[0] += o[TF_HB];
-            run_b[1] += o[TF_INIT];
-            run_b[2] += o[TF_INIT_BYTES];
+            b[0] = ex[0], b[1] = ex[1], b[2] = ex[2];
         } else {
-            b[0] = run_b[3];
-            b[1] = run_b[4];
-            b[2] = run_b[5];
-            b[3] = run_b[6];
-            run_b[3] += o[TF_DEL];
-            run_b[4] += o[TF_PP];
-            run_b[5] += o[TF_PP_BYTES];
-            run_b[6] += o[TF_ALLOC];
+            b[0] = ex[3], b[1] = ex[4], b[2] = ex[5], b[3] = ex[6];
         }
+#pragma unroll
+        for (int f = 0; f < NS; f++) ex[f] += v.sc[f];
     }
     TickHdr* H = S.hdr;
     if (t == 0) {
@@ -788,17 +789,13 @@ __device__ void write_init_patch(const DevState& S, uint64_t blob, uint8_t* out)
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_emit(DevState S) {
+// node tiles: heartbeat list, node-init patches, node state (runs on the heartbeat stream)
+__global__ __launch_bounds__(BLOCK) void k_emit_nodes(DevState S) {
     const uint32_t tile = blockIdx.x;
     const int t = threadIdx.x;
     const TickHdr* H = S.hdr;
-    if (tile == 0 && t == 0) {
-        if (H->alloc_total) *S.pool_index = H->cursor_index;
-        S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
-        S.list_counts[1] = 0;
-    }
-    __shared__ PodJob jobs[POD_TILE];  // 32 KiB (node tiles reuse it for InitJob)
-    if (tile < S.node_tiles) {
+    __shared__ InitJob ijobs[NODE_TILE];
+    {
         const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
         const uint64_t* base = S.tile_base + (size_t)tile * 4;
         uint32_t packed = 0;
@@ -822,7 +819,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevState S) {
         }
         uint32_t tot[3];
         block_excl_scan<3>(v, tot);
-        InitJob* ij = reinterpret_cast<InitJob*>(jobs);
+        InitJob* ij = ijobs;
         uint32_t newpacked = 0;
         uint32_t ji = v[1];
 #pragma unroll
@@ -852,13 +849,32 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevState S) {
             InitJob jb = ij[j];
             write_init_patch(S, S.node_blob[jb.slot], S.arena + tile_bytes + jb.off);
         }
-        return;
     }
-    // ---- pods ----
-    const uint32_t ptile = tile - S.node_tiles;
+}
+
+// pod tiles: delete list, IP assignment, pod patches, pod state; publishes the
+// tick header to pinned host memory
+__global__ __launch_bounds__(BLOCK) void k_emit_pods(DevState S) {
+    const uint32_t ptile = blockIdx.x;
+    const uint32_t tile = S.node_tiles + ptile;
+    const int t = threadIdx.x;
+    const TickHdr* H = S.hdr;
+    if (ptile == 0 && t < 64) {
+        // the header is final here (scan, pool plan): publish it zero-copy
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(H);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
+        for (int i = t; i < (int)(sizeof(TickHdr) / 8); i += 64) dst[i] = src[i];
+        if (t == 0) {
+            if (H->alloc_total) *S.pool_index = H->cursor_index;
+            S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
+            S.list_counts[1] = 0;
+        }
+        __threadfence_system();
+    }
+    __shared__ PodJob jobs[POD_TILE];  // 32 KiB
     const uint64_t* base = S.tile_base + (size_t)tile * 4;  // del, pp, pp_bytes, alloc
     const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    const bool live = first < S.n_pod_slots;
+    const bool live = first < S.n_pod_slots && (first % S.cp) < S.pod_fill[first / S.cp];
     uint16_t st[POD_PER_THREAD];
     uint32_t ip[POD_PER_THREAD];
     PodCls c[POD_PER_THREAD];
@@ -869,11 +885,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevState S) {
               ipb = make_uint4(0, 0, 0, 0);
         if (live) {
             st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
-            if (st4.x | st4.y | st4.z | st4.w) {
-                nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
-                ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
-                ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
-            }
+            nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
+            ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
+            ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
         }
         const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
         const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
@@ -965,13 +979,16 @@ __global__ __launch_bounds__(BLOCK) void k_hb_fill(DevState S) {
     if (threadIdx.x < HB_CHUNKS) tmpl[threadIdx.x] = reinterpret_cast<const uint4*>(S.hb_tmpl)[threadIdx.x];
     __syncthreads();
     const uint64_t nchunks = (uint64_t)S.hdr->n_hb * HB_CHUNKS;
-    uint4* dst = reinterpret_cast<uint4*>(S.arena + S.hdr->hb_base);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* dst = reinterpret_cast<u32x4*>(S.arena + S.hdr->hb_base);
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
     uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     uint32_t m = (uint32_t)(i % HB_CHUNKS);
     const uint32_t dm = (uint32_t)(stride % HB_CHUNKS);
     for (; i < nchunks; i += stride) {
-        dst[i] = tmpl[m];
+        const uint4 v = tmpl[m];
+        u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, &dst[i]);  // write-once stream: do not keep in L2
         m += dm;
         if (m >= HB_CHUNKS) m -= HB_CHUNKS;
     }
@@ -1039,12 +1056,17 @@ void launch_pool_alloc(const DevState& S, hipStream_t st) {
     hipLaunchKernelGGL(k_pool_select, dim3(nblk), dim3(BLOCK), 0, st, S, nblk);
 }
 
-void launch_emit(const DevState& S, hipStream_t st) {
-    hipLaunchKernelGGL(k_emit, dim3(S.node_tiles + S.pod_tiles), dim3(BLOCK), 0, st, S);
+void launch_emit_nodes(const DevState& S, hipStream_t st) {
+    hipLaunchKernelGGL(k_emit_nodes, dim3(S.node_tiles), dim3(BLOCK), 0, st, S);
 }
 
-void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_hb_fill, dim3(grid), dim3(BLOCK), 0, st, S);
+void launch_emit_pods(const DevState& S, hipStream_t st) {
+    hipLaunchKernelGGL(k_emit_pods, dim3(S.pod_tiles), dim3(BLOCK), 0, st, S);
+}
+
+void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+    if (t0) hipExtLaunchKernelGGL(k_hb_fill, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S);  // kernel-exact timing
+    else hipLaunchKernelGGL(k_hb_fill, dim3(grid), dim3(BLOCK), 0, st, S);
 }
 
 }  // namespace kwok
