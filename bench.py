@@ -41,7 +41,14 @@ keng.load_engine_lib()
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NODES_PER_RANK = 100_000
-HB_BYTES = 1059  # algorithmic bytes written per heartbeat patch (k_hb_fill)
+# algorithmic HBM bytes of one tick (SURVEY.md §8(d) byte model):
+# per managed node a heartbeat (1 B flags + 4 B hb-time + 4 B out-index + the
+# 1059-byte materialised patch = 1068 B) and a no-op re-lock check (9 B); per
+# live pod a no-op re-check (10 B)
+HB_BYTES = 1059
+NODE_BYTES = 1068 + 9
+POD_BYTES = 10
+PMC_FILE = "r1_pmc_tick.json"
 
 
 def parse():
@@ -106,6 +113,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    e.profile_host(reset=True)
     t0 = time.perf_counter()
     trans = evald = 0
     last = None
@@ -124,8 +132,9 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
-    # roofline pass: the same ticks replayed eagerly with HIP events around each
-    # phase on the stream it runs on (k_hb_fill: the heartbeat stream)
+    host_ms, host_n = e.profile_host(reset=True)
+    # roofline pass: the same ticks with HIP events around each k_tick launch
+    # (kernel-exact hipExtLaunchKernelGGL events) and the kernel's phase stamps
     e.profile_enable(True)
     for k in range(a.roofline_ticks):
         e.tick(now, read=False)
@@ -134,14 +143,15 @@ def main():
     e.profile_enable(False)
 
     if rank == 0:
-        hb_ms = phases["hb_fill"] / max(nt, 1)
-        n_hb_local = last.local_counters[0]
-        achieved = HB_BYTES * n_hb_local / (hb_ms * 1e-3) / 1e9 if hb_ms > 0 else 0.0
+        kern_ms = phases["kernel"] / max(nt, 1)
+        lc = last.local_counters
+        alg_bytes = NODE_BYTES * lc[8] + POD_BYTES * lc[10]  # nodes_managed, pods_total (this rank)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", "r1_pmc_c2.json")
+        pmc = os.path.join(ROOT, "profiles", PMC_FILE)
         if os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK:
-            traffic = json.load(open(pmc))["kernels"]["k_hb_fill"]["hbm_bytes"]
-            traffic_src = "profiles/r1_pmc_c2.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same config)"
+            traffic = json.load(open(pmc))["kernels"]["k_tick"]["hbm_bytes"]
+            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE + WRITE_SIZE per launch, same config)" % PMC_FILE
         out = {
             "metric": "state transitions/sec at 1M nodes/10M pods, 1-8 MI355X; % HBM roofline",
             "value": trans / dt,
@@ -161,13 +171,14 @@ def main():
                        "cidr": workload.CIDR, "buckets": workload.BUCKETS, "parallelism": "bucket-sharded x%d" % world},
             "objects_evaluated_per_s": evald / dt,
             "phase_ms_per_tick": {k: v / max(nt, 1) for k, v in phases.items()},
+            "host_ms_per_tick": {k: v / max(host_n, 1) for k, v in host_ms.items()},
             "initial_tick_counters": first,
             "setup_s": setup_s,
-            "roofline": {"bound": "hbm", "kernel": "k_hb_fill", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_tick", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "bytes_per_launch": HB_BYTES * n_hb_local, "avg_launch_ms": hb_ms,
+                         "bytes_per_launch": alg_bytes, "avg_launch_ms": kern_ms,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "timing": "HIP events on the heartbeat stream, eager replay of %d ticks" % nt},
+                         "timing": "HIP events around each k_tick launch (hipExtLaunchKernelGGL), %d ticks" % nt},
         }
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_nodes)

@@ -264,12 +264,21 @@ typedef struct kwok_device_view {
 } kwok_device_view;
 int kwok_device_outputs(kwok_engine* e, kwok_device_view* view);
 
-/* Diagnostics: device time per tick phase, measured with HIP events recorded
- * on the engine's stream around each phase (enable resets the accumulators). */
-enum { KWOK_T_FRONT = 0 /* classify + scan */, KWOK_T_POOL /* ipPool kernels */, KWOK_T_EMIT,
-       KWOK_T_HB_FILL /* heartbeat emission */, KWOK_T_COUNT };
+/* Diagnostics: device time per tick (enable resets the accumulators).
+ * KERNEL is the tick kernel's launch duration(s) from HIP events; the phase
+ * split comes from the kernel's own clock stamps: CLASSIFY = first block start
+ * to last block done classifying, BARRIER = from there until the grid barrier
+ * releases, BASES = output bases / header, EXCHANGE = between the two launches
+ * of a multi-rank tick (allgather + pool apply), POOL = ipPool phase, EMIT =
+ * the rest of the launch (patch bytes, lists, heartbeat stream). */
+enum { KWOK_T_CLASSIFY = 0, KWOK_T_BARRIER, KWOK_T_BASES, KWOK_T_EXCHANGE, KWOK_T_POOL, KWOK_T_EMIT,
+       KWOK_T_KERNEL, KWOK_T_COUNT };
 int kwok_profile_enable(kwok_engine* e, int on);
 int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* ticks);
+/* Host-side wall time of kwok_tick (always measured): enqueue,
+ * waiting for the device, host bookkeeping after the wait, whole call. */
+enum { KWOK_H_ENQUEUE = 0, KWOK_H_WAIT, KWOK_H_POST, KWOK_H_TOTAL, KWOK_H_COUNT };
+int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], uint64_t* ticks);
 
 /* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);

@@ -45,13 +45,18 @@ constexpr int CONDS_LEN = HB_LEN - HB_PREFIX - 2;  // the conditions list "[...]
 constexpr int TS_LEN = 20;       // RFC3339 UTC "YYYY-MM-DDTHH:MM:SSZ"
 constexpr int HB_NSLOTS = 10;    // 5 x (lastHeartbeatTime, lastTransitionTime)
 
-// per-tile aggregates written by the classify kernel
-enum TileField {
-    TF_HB = 0, TF_INIT, TF_INIT_BYTES, TF_LOCK, TF_MANAGED, TF_READY,   // node tiles
-    TF_DEL, TF_EVAL, TF_ALLOC, TF_PP, TF_PP_BYTES, TF_TOTAL, TF_PENDING, TF_RUNNING, TF_REL, // pod tiles
-    TF_COUNT
+// per-tile and per-block aggregates of the classify phase.  The first
+// AG_NSCAN fields are exclusive-scanned into output ordinals / offsets (BYTES:
+// node-init bytes for node tiles, pod-patch bytes for pod tiles; node tiles
+// precede pod tiles, so one scan lays out [inits | pod patches]); the rest are
+// only summed.
+enum AggField {
+    AG_HB = 0, AG_INIT, AG_DEL, AG_PP, AG_BYTES, AG_ALLOC,                  // scanned
+    AG_INIT_BYTES, AG_LOCK, AG_MANAGED, AG_READY, AG_EVAL, AG_TOTAL, AG_PENDING, AG_RUNNING, AG_REL,
+    AG_COUNT
 };
-constexpr int TF_STRIDE = 16;
+constexpr int AG_NSCAN = 6;
+constexpr int AG_STRIDE = 16;
 
 // per-tick header: written on device, copied back to the host
 struct TickHdr {
@@ -67,6 +72,31 @@ struct TickHdr {
     uint64_t alloc_total, alloc_base, usable_total, take_usable, fresh_in, fresh_out_start;
     uint64_t cursor_index;       // ipPool.index after the tick
     uint64_t rel_total;          // releases this tick, all ranks (pending in rel_bm)
+    // s_memrealtime (100 MHz) stamps, CLK_* (block 0; the last two only in profiled ticks)
+    uint64_t clk[8];
+    // host-visible only (not published): TICK_ERR_* set by a timed-out grid barrier
+    uint32_t err, pad2;
+};
+
+constexpr uint32_t TICK_ERR_BARRIER = 1;  // a grid barrier timed out
+constexpr uint32_t TICK_ERR_LAYOUT = 2;   // device heartbeat count != the host's managed-node count
+enum : int {
+    CLK_ENTRY = 0,   // block 0 starts the FRONT phases
+    CLK_P1,          // block 0 done classifying
+    CLK_BAR,         // block 0 leaves the first grid barrier
+    CLK_BASES,       // block 0 done with bases / header
+    CLK_BACK,        // block 0 starts the BACK phases
+    CLK_POOL,        // block 0 done with the pool phase (emission starts)
+    CLK_ENTRY_MIN,   // earliest block start          (profiled ticks)
+    CLK_P1_MAX,      // latest block done classifying (profiled ticks)
+};
+
+// grid-barrier state of the persistent tick kernel (device memory, zeroed once):
+// generation, top counter and 8 group counters, each on its own 128-byte line
+constexpr int BAR_LINE = 32, BAR_GEN = 0, BAR_TOP = BAR_LINE, BAR_GRP = 2 * BAR_LINE;
+struct GridBar {
+    uint32_t w[(2 + 8) * BAR_LINE];
+    unsigned long long neg_entry_max, p1_max;  // profiled ticks: max(~entry), max(phase-1 end)
 };
 
 // exchange message, one per rank (allgather)

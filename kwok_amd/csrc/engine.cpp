@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -61,8 +62,6 @@ struct kwok_engine {
     std::string node_ip_s;
     int64_t start = 0;
     hipStream_t st = nullptr;   // tick pipeline
-    hipStream_t st2 = nullptr;  // heartbeat stream (k_hb_fill), overlaps pool + emit
-    hipEvent_t ev_front = nullptr, ev_hb = nullptr;
     DevState S{};
 
     // ---- host mirrors (slot policy) ----
@@ -116,19 +115,19 @@ struct kwok_engine {
     uint32_t* d_xsend = nullptr;
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
-    uint32_t hb_grid = 2048;
-    // single-rank tick as a captured hipGraph (re-captured when device pointers move)
-    uint64_t* now_h = nullptr;  // pinned: Now() of the tick, copied by the graph's first node
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
-    DevState graph_S{};
-    bool graph_prof = false, use_graph = true;
+    uint32_t tick_grid = 0;     // k_tick blocks: CUs x resident blocks per CU (all co-resident)
+    bool hb_first = false;      // KWOK_TICK_HB_FIRST=1: heartbeat stream before classification
     // diagnostics
     bool prof = false;
-    hipEvent_t pev[KWOK_T_COUNT + 1] = {};
-    hipEvent_t pev_hb[2] = {};  // hb_fill runs on st2
+    hipEvent_t pev[4] = {};  // k_tick launch start/stop: FRONT(+BACK) launch, BACK launch
     double prof_ms[KWOK_T_COUNT] = {};
     uint64_t prof_ticks = 0;
+    double host_ms[KWOK_H_COUNT] = {};
+    // KWOK_TICK_TRACE=1: per-block phase stamps, summarised on stderr at destroy
+    std::vector<uint64_t> trace_h;
+    double trace_sum[8][3] = {};
+    uint64_t trace_ticks = 0, trace_seen = 0;
+    uint64_t host_ticks = 0;
 
     int fail(int code, const char* fmt, ...) {
         char b[512];
@@ -429,11 +428,20 @@ const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : 
 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
+    if (e->trace_ticks) {
+        static const char* names[8] = {"entry", "p1-done", "barrier-out", "front-done",
+                                       "emit-start", "tiles-classified", "tiles-done", "reclassified"};
+        fprintf(stderr, "[kwok trace] grid %u, %llu ticks, us after first block start (min / median / max block)\n",
+                e->tick_grid, (unsigned long long)e->trace_ticks);
+        for (int k = 0; k < 8; k++)
+            fprintf(stderr, "[kwok trace] %-12s %8.2f %8.2f %8.2f\n", names[k], e->trace_sum[k][0] / e->trace_ticks,
+                    e->trace_sum[k][1] / e->trace_ticks, e->trace_sum[k][2] / e->trace_ticks);
+    }
     if (e->st) (void)hipStreamSynchronize(e->st);
-    void* ptrs[] = {e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
+    void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
-                    e->S.pool_blk, e->S.pool_blk_base, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.hb_tmpl, e->S.tiles, e->S.tile_base, e->S.hdr, e->S.xmsg,
+                    e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.tiles, e->S.hdr, e->S.xmsg,
                     e->S.use_list, e->S.rel_list, e->S.arena, e->S.hb_nodes, e->S.init_nodes, e->S.init_off,
                     e->S.init_len, e->S.pp_pods, e->S.pp_off, e->S.pp_len, e->S.del_pods, e->S.del_fin,
                     e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
@@ -446,15 +454,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->comm) ncclCommDestroy(e->comm);
     for (auto& ev : e->pev)
         if (ev) (void)hipEventDestroy(ev);
-    for (auto& ev : e->pev_hb)
-        if (ev) (void)hipEventDestroy(ev);
-    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
-    if (e->graph) (void)hipGraphDestroy(e->graph);
-    if (e->now_h) (void)hipHostFree(e->now_h);
     if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
-    if (e->ev_front) (void)hipEventDestroy(e->ev_front);
-    if (e->ev_hb) (void)hipEventDestroy(e->ev_hb);
-    if (e->st2) (void)hipStreamDestroy(e->st2);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
 }
@@ -513,10 +513,19 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     {
         hipError_t r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
-        if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking);
-        if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_front, hipEventDisableTiming);
-        if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_hb, hipEventDisableTiming);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "stream/event create: %s", hipGetErrorString(r)));
+    }
+    {
+        // k_tick's grid: every block must be resident at once (grid barriers).
+        // Blocks per CU = min(occupancy, KWOK_TICK_BLOCKS_PER_CU or 2); lower it
+        // when several engines share one GPU (their grids must fit together).
+        int cus = 0, occ = tick_occupancy(), want = 2;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->dev);
+        if (const char* v = getenv("KWOK_TICK_BLOCKS_PER_CU")) want = std::max(1, atoi(v));
+        if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
+        e->tick_grid = (uint32_t)(cus * std::min(occ, want));
+        const char* hf = getenv("KWOK_TICK_HB_FIRST");
+        e->hb_first = hf && hf[0] == '1';
     }
     DevState& S = e->S;
     S.n_node_slots = e->NL;
@@ -531,6 +540,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.node_ip = e->node_ip;
     S.world = W;
     const uint32_t T = S.node_tiles + S.pod_tiles;
+    if ((T + e->tick_grid - 1) / e->tick_grid > (uint32_t)MAX_TILES_PER_BLOCK)
+        return bail(e->fail(KWOK_EDOMAIN, "%u tiles exceed %u per k_tick block on %u blocks: shard over more GPUs", T,
+                            (unsigned)MAX_TILES_PER_BLOCK, e->tick_grid));
     const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
     // node/pod tiles round NL/PL up: allocate whole tiles so vector loads stay in bounds
     const size_t NLa = (size_t)S.node_tiles * NODE_TILE, PLa = (size_t)S.pod_tiles * POD_TILE;
@@ -542,10 +554,12 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.host_ip, PLa)) || (rc = dalloc(e, &S.used_bm, e->pool.words)) ||
         (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.rel_bm, e->pool.words)) ||
         (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &e->d_pod_fill, e->nb)) || (rc = dalloc(e, &S.pool_index, 1)) ||
-        (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.pool_blk_base, 2 * (size_t)nblk)) ||
+        (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
+        (rc = dalloc(e, &S.blockagg, (size_t)e->tick_grid * AG_STRIDE)) ||
+        (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)e->tick_grid * 8))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
-        (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) || (rc = dalloc(e, &S.hb_tmpl, HB_STRIDE)) ||
-        (rc = dalloc(e, &S.tiles, (size_t)T * TF_STRIDE)) || (rc = dalloc(e, &S.tile_base, (size_t)T * 4)) ||
+        (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) ||
+        (rc = dalloc(e, &S.tiles, (size_t)T * AG_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
         (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &S.hb_nodes, NLa)) ||
         (rc = dalloc(e, &S.init_nodes, NLa)) || (rc = dalloc(e, &S.init_off, NLa)) ||
@@ -567,16 +581,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
-    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&e->now_h, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess)
         return bail(KWOK_ENOMEM);
-    S.tick_now = e->now_h;   // zero-copy: k_scan reads the clock from pinned host memory
-    S.hdr_host = e->hdr_h;   // zero-copy: k_emit_pods publishes the header
+    S.hdr_host = e->hdr_h;   // zero-copy: k_tick's last block publishes the header
     S.pod_fill = e->d_pod_fill;
-    {
-        const char* ng = getenv("KWOK_NO_GRAPH");
-        e->use_graph = !(ng && ng[0] == '1');
-    }
     if (W > 1) {
         if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
         if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
@@ -600,9 +608,6 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->node_opi.assign(e->NL, 0);
     e->pod_stamp.assign(e->PL, 0);
     e->pod_opi.assign(e->PL, 0);
-    int dev_cus = 256;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->dev);
-    e->hb_grid = (uint32_t)std::max(1, dev_cus) * 8;
     e->max_init_len = 0;
     if ((rc = size_arena(e))) return bail(rc);
     {
@@ -866,121 +871,131 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
 }
 
 namespace {
-// Enqueue one tick on e->st (+ e->st2).  Single rank: no host synchronisation,
-// so the whole sequence is captured once as a hipGraph and replayed.
-int enqueue_tick(kwok_engine* e) {
+// Enqueue one tick on e->st.  Single rank: ONE persistent k_tick launch (no host
+// synchronisation, no graph needed).  Multi-rank: k_tick FRONT (classify, bases,
+// exchange message) -> allgather -> xreduce + pool_apply -> k_tick BACK (pool,
+// emission).
+int enqueue_tick(kwok_engine* e, uint64_t now) {
     DevState& S = e->S;
     hipStream_t st = e->st;
-    auto mark = [&](int i) {
-        if (e->prof) (void)hipEventRecord(e->pev[i], st);
-    };
-    mark(0);
-    launch_tick_front(S, (uint64_t)e->start, e->W, st);
-    // the node side (heartbeat stream + node list / node-init patches) only needs
-    // the scan: run it on the second stream, overlapped with the exchange, the
-    // pool and the pod side
-    HIPCHK(e, hipEventRecord(e->ev_front, st));
-    HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_front, 0));
-    if (e->prof) launch_hb_fill(S, e->hb_grid, e->st2, e->pev_hb[0], e->pev_hb[1]);
-    else launch_hb_fill(S, e->hb_grid, e->st2);
-    launch_emit_nodes(S, e->st2);
-    HIPCHK(e, hipEventRecord(e->ev_hb, e->st2));
-    if (e->W > 1) {
-        // one allgather of the fixed-size exchange message; a second one for
-        // lists that did not fit inline (sizes known after the first)
-        int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
-        if (rc) return rc;
-        HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipStreamSynchronize(st));
-        uint64_t maxl = 0;
-        for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
-        std::vector<ListDesc> ld(e->W);
-        if (maxl <= (uint64_t)XINLINE) {
-            for (int r = 0; r < e->W; r++) {
-                ld[r].use = e->d_xall[r].ips;
-                ld[r].rel = e->d_xall[r].ips + e->h_xall[r].n_use;
-            }
-        } else {
-            if (maxl > e->xlist_cap) {
-                if (e->d_xsend) (void)hipFree(e->d_xsend);
-                if (e->d_xrecv) (void)hipFree(e->d_xrecv);
-                e->xlist_cap = maxl;
-                if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
-                    hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
-                    return e->fail(KWOK_ENOMEM, "exchange lists");
-            }
-            const XMsg& me = e->h_xall[e->rank];
-            HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
-            HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
-            rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
-            if (rc) return rc;
-            for (int r = 0; r < e->W; r++) {
-                ld[r].use = e->d_xrecv + (size_t)r * maxl;
-                ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
-            }
-        }
-        for (int r = 0; r < e->W; r++) {
-            ld[r].n_use = (uint32_t)e->h_xall[r].n_use;
-            ld[r].n_rel = (uint32_t)e->h_xall[r].n_rel;
-        }
-        HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
-        launch_xreduce(S, e->d_xall, e->W, e->rank, st);
-        launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
+    hipEvent_t* ev = e->prof ? e->pev : nullptr;
+    const uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
+    const int order = e->hb_first ? TICK_HB_FIRST : 0;
+    if (e->W == 1) {
+        launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | order | (ev ? TICK_PROF : 0), st, ev ? ev[0] : nullptr,
+                    ev ? ev[1] : nullptr);
+        HIPCHK(e, hipGetLastError());
+        return KWOK_OK;
     }
-    mark(1);  // (multi-rank: includes the exchange)
-    launch_pool_alloc(S, st);
-    mark(2);
-    launch_emit_pods(S, st);
-    mark(3);
-    HIPCHK(e, hipStreamWaitEvent(st, e->ev_hb, 0));
-    mark(4);
+    launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_FRONT | order | (ev ? TICK_PROF : 0), st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+    // one allgather of the fixed-size exchange message; a second one for
+    // lists that did not fit inline (sizes known after the first)
+    int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
+    if (rc) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    uint64_t maxl = 0;
+    for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
+    std::vector<ListDesc> ld(e->W);
+    if (maxl <= (uint64_t)XINLINE) {
+        for (int r = 0; r < e->W; r++) {
+            ld[r].use = e->d_xall[r].ips;
+            ld[r].rel = e->d_xall[r].ips + e->h_xall[r].n_use;
+        }
+    } else {
+        if (maxl > e->xlist_cap) {
+            if (e->d_xsend) (void)hipFree(e->d_xsend);
+            if (e->d_xrecv) (void)hipFree(e->d_xrecv);
+            e->xlist_cap = maxl;
+            if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
+                hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
+                return e->fail(KWOK_ENOMEM, "exchange lists");
+        }
+        const XMsg& me = e->h_xall[e->rank];
+        HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
+        rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
+        if (rc) return rc;
+        for (int r = 0; r < e->W; r++) {
+            ld[r].use = e->d_xrecv + (size_t)r * maxl;
+            ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
+        }
+    }
+    for (int r = 0; r < e->W; r++) {
+        ld[r].n_use = (uint32_t)e->h_xall[r].n_use;
+        ld[r].n_rel = (uint32_t)e->h_xall[r].n_rel;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
+    launch_xreduce(S, e->d_xall, e->W, e->rank, st);
+    launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
+    launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_BACK, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
     HIPCHK(e, hipGetLastError());
     return KWOK_OK;
 }
-
-int capture_tick_graph(kwok_engine* e) {
-    if (e->graph_exec) (void)hipGraphExecDestroy(e->graph_exec);
-    if (e->graph) (void)hipGraphDestroy(e->graph);
-    e->graph_exec = nullptr;
-    e->graph = nullptr;
-    HIPCHK(e, hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_tick(e);
-    hipGraph_t g = nullptr;
-    hipError_t r = hipStreamEndCapture(e->st, &g);
-    if (rc) return rc;
-    if (r != hipSuccess) return e->fail(KWOK_EDEVICE, "hipStreamEndCapture: %s", hipGetErrorString(r));
-    e->graph = g;
-    HIPCHK(e, hipGraphInstantiate(&e->graph_exec, g, nullptr, nullptr, 0));
-    e->graph_S = e->S;
-    e->graph_prof = e->prof;
-    return KWOK_OK;
-}
 }  // namespace
+
+static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && e->W == 1; }
+
+// per stamp k: earliest / median / latest block, microseconds after the earliest block start
+static void trace_tick(kwok_engine* e) {
+    const size_t G = e->tick_grid;
+    if (++e->trace_seen <= 5) return;  // skip the initial (bulk) ticks
+    e->trace_h.resize(G * 8);
+    if (hipMemcpy(e->trace_h.data(), e->S.trace, G * 8 * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t t0 = ~0ull;
+    for (size_t b = 0; b < G; b++) t0 = std::min(t0, e->trace_h[b * 8]);
+    std::vector<double> v(G);
+    for (int k = 0; k < 8; k++) {
+        for (size_t b = 0; b < G; b++) v[b] = (double)(e->trace_h[b * 8 + k] - t0) * 0.01;
+        std::sort(v.begin(), v.end());
+        e->trace_sum[k][0] += v[0];
+        e->trace_sum[k][1] += v[G / 2];
+        e->trace_sum[k][2] += v[G - 1];
+    }
+    e->trace_ticks++;
+}
 
 extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
     if (!e) return KWOK_EINVAL;
     if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
     hipStream_t st = e->st;
-    *e->now_h = (uint64_t)now_unix;
-    if (e->W == 1 && e->use_graph && !e->prof) {  // graph event nodes do not time: profile eagerly
-        if (!e->graph_exec || e->graph_prof != e->prof || memcmp(&e->graph_S, &e->S, sizeof(DevState)) != 0) {
-            int rc = capture_tick_graph(e);
-            if (rc) return rc;
-        }
-        HIPCHK(e, hipGraphLaunch(e->graph_exec, st));
-    } else {
-        int rc = enqueue_tick(e);
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    {
+        int rc = enqueue_tick(e, (uint64_t)now_unix);
         if (rc) return rc;
     }
+    const auto t1 = clk::now();
     HIPCHK(e, hipStreamSynchronize(st));
+    const auto t2 = clk::now();
     const TickHdr& H = *e->hdr_h;
+    if (trace_enabled(e)) trace_tick(e);
+    if (H.err) {
+        const uint32_t err = H.err;
+        e->hdr_h->err = 0;
+        if (err & TICK_ERR_BARRIER)
+            return e->fail(KWOK_EDEVICE, "k_tick grid barrier timed out (grid %u not co-resident?)", e->tick_grid);
+        return e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
+                       (unsigned long long)e->n_managed);
+    }
     if (e->prof) {
-        for (int i = 0; i < KWOK_T_COUNT; i++) {
-            float ms = 0;
-            if (i == KWOK_T_HB_FILL) (void)hipEventElapsedTime(&ms, e->pev_hb[0], e->pev_hb[1]);
-            else (void)hipEventElapsedTime(&ms, e->pev[i], e->pev[i + 1]);
-            e->prof_ms[i] += ms;
-        }
+        // kernel time from the launch events; the phase split from the kernel's
+        // s_memrealtime stamps (100 MHz)
+        float k0 = 0, k1 = 0;
+        (void)hipEventElapsedTime(&k0, e->pev[0], e->pev[1]);
+        if (e->W > 1) (void)hipEventElapsedTime(&k1, e->pev[2], e->pev[3]);
+        const double kern = (double)k0 + k1;
+        auto span = [&](int a, int b) { return H.clk[b] > H.clk[a] ? (double)(H.clk[b] - H.clk[a]) * 1e-5 : 0.0; };
+        const double classify = span(CLK_ENTRY_MIN, CLK_P1_MAX), barrier = span(CLK_P1_MAX, CLK_BAR);
+        const double bases = span(CLK_BAR, CLK_BASES), pool = span(CLK_BACK, CLK_POOL);
+        e->prof_ms[KWOK_T_CLASSIFY] += classify;
+        e->prof_ms[KWOK_T_BARRIER] += barrier;
+        e->prof_ms[KWOK_T_BASES] += bases;
+        e->prof_ms[KWOK_T_EXCHANGE] += e->W > 1 ? span(CLK_BASES, CLK_BACK) : 0.0;
+        e->prof_ms[KWOK_T_POOL] += pool;
+        // emission runs to the end of the launch
+        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, kern - classify - barrier - bases - pool);
+        e->prof_ms[KWOK_T_KERNEL] += kern;
         e->prof_ticks++;
     }
     if (H.overflow) return e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes);
@@ -1003,6 +1018,15 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         if (rc) return rc;
     }
     e->have_tick = true;
+    {
+        const auto t3 = clk::now();
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        e->host_ms[KWOK_H_ENQUEUE] += ms(t0, t1);
+        e->host_ms[KWOK_H_WAIT] += ms(t1, t2);
+        e->host_ms[KWOK_H_POST] += ms(t2, t3);
+        e->host_ms[KWOK_H_TOTAL] += ms(t0, t3);
+        e->host_ticks++;
+    }
     if (res) {
         memset(res, 0, sizeof(*res));
         res->n_heartbeat = H.n_hb;
@@ -1063,8 +1087,6 @@ int kwok_profile_enable(kwok_engine* e, int on) {
     if (!e) return KWOK_EINVAL;
     for (auto& ev : e->pev)
         if (!ev) HIPCHK(e, hipEventCreate(&ev));
-    for (auto& ev : e->pev_hb)
-        if (!ev) HIPCHK(e, hipEventCreate(&ev));
     e->prof = on != 0;
     memset(e->prof_ms, 0, sizeof e->prof_ms);
     e->prof_ticks = 0;
@@ -1075,6 +1097,17 @@ int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* tic
     if (!e) return KWOK_EINVAL;
     if (ms_sum) memcpy(ms_sum, e->prof_ms, sizeof e->prof_ms);
     if (ticks) *ticks = e->prof_ticks;
+    return KWOK_OK;
+}
+
+int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], uint64_t* ticks) {
+    if (!e) return KWOK_EINVAL;
+    if (ms_sum) memcpy(ms_sum, e->host_ms, sizeof e->host_ms);
+    if (ticks) *ticks = e->host_ticks;
+    if (reset) {
+        memset(e->host_ms, 0, sizeof e->host_ms);
+        e->host_ticks = 0;
+    }
     return KWOK_OK;
 }
 

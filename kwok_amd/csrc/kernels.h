@@ -36,8 +36,7 @@ struct DevState {
     uint64_t* usable_bm;
     uint64_t* rel_bm;        // Puts of this tick, folded into used/usable by k_pool_prep
     uint64_t* pool_index;    // ipPool.index (persistent)
-    uint32_t* pool_blk;      // per word-block counts
-    uint64_t* pool_blk_base;
+    uint32_t* pool_blk;      // per word-block counts (usable, free)
     uint32_t* alloc_addr;    // this rank's allocated addresses, by local ordinal
     PoolGeom pool;
     // pod spec programs / node blobs
@@ -48,10 +47,8 @@ struct DevState {
     // heartbeat template
     const uint8_t* hb_static;
     const uint8_t* hb_kind;
-    uint8_t* hb_tmpl;
     // per tick
-    uint32_t* tiles;
-    uint64_t* tile_base;
+    uint32_t* tiles;           // [tiles][AG_STRIDE] per-tile aggregates (multi-rank BACK launch)
     TickHdr* hdr;
     XMsg* xmsg;
     uint32_t* use_list;      // multi-rank exchange lists
@@ -70,21 +67,24 @@ struct DevState {
     int32_t* del_pods;
     uint8_t* del_fin;
     uint32_t node_ip;
-    const uint64_t* tick_now;  // Now() of the current tick (pinned host scalar, zero-copy)
     TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
     const uint16_t* pod_fill;  // per owned bucket: upper bound of used pod slots (host-maintained)
+    GridBar* bar;              // persistent-kernel barrier state
+    uint32_t* blockagg;        // [grid][AG_STRIDE] per-block aggregates of the classify phase
+    uint64_t* trace;           // [grid][8] per-block phase stamps (KWOK_TICK_TRACE=1), else null
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
                       hipStream_t st);
-void launch_tick_front(const DevState& S, uint64_t start, int world, hipStream_t st);
 void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st);
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
-void launch_pool_alloc(const DevState& S, hipStream_t st);
-void launch_emit_nodes(const DevState& S, hipStream_t st);
-void launch_emit_pods(const DevState& S, hipStream_t st);
-void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st, hipEvent_t t0 = nullptr,
-                    hipEvent_t t1 = nullptr);
+
+// the persistent tick kernel; `grid` blocks must be co-resident (tick_occupancy)
+constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_HB_FIRST = 8;
+constexpr int MAX_TILES_PER_BLOCK = 32;
+void launch_tick(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
+                 hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+int tick_occupancy();  // resident k_tick blocks per CU
 
 }  // namespace kwok

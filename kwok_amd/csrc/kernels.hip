@@ -1,24 +1,25 @@
-// kernels.hip - gfx950 kernels of one kwok controller tick (see DESIGN.md).
+// kernels.hip - gfx950 kernels of one kwok controller tick (see DESIGN.md §5).
 //
 // A tick is a fixed pipeline of memory-bound sweeps over struct-of-arrays
-// state in HBM; nothing here is a dense contraction, so there is no MFMA:
+// state in HBM; nothing here is a dense contraction, so there is no MFMA.
+// The whole single-rank tick is ONE persistent launch (k_tick): per-tick
+// launch and inter-kernel gaps dominated the multi-kernel version (~70 us of
+// fixed cost per tick on MI355X), while the work itself is ~20 us of HBM
+// traffic.  Phases are separated by XCD-safe grid barriers.
 //
-//   k_classify   one pass over node + pod slots: per-tile counts, pool
-//                use/release candidate lists            (node_controller.go:206-223,
-//                                                        pod_controller.go:252-269,306-343,377-439)
-//   k_scan       one block: exclusive scan of tile counts -> output layout,
-//                fleet counters, per-tick heartbeat template (Now/StartTime)
-//   k_pool_*     ipPool Use / Put / Get-plan / select+commit on replicated
-//                used/usable bitmaps                      (utils.go:52-117)
-//   k_emit       second pass: compaction (wave ballots + block scans) of
-//                heartbeat / node-init / pod-patch / delete lists, byte
-//                emission of node-init and pod patches (wave per patch),
-//                state transitions
-//   k_hb_fill    the dominant kernel: n_managed identical 1059-byte heartbeat
-//                patches streamed from an LDS-staged template with 16-byte
-//                stores                                   (node_controller.go:145-204,393-401)
+//   classify    node + pod predicates, per-tile counts, pool Use/Put bits
+//                 (node_controller.go:206-223,356-391; pod_controller.go:252-269,306-343,377-439)
+//   bases       per-block output bases from per-block aggregates (no scan kernel)
+//   pool        ipPool Put fold / plan / select+commit on replicated bitmaps
+//                 (utils.go:52-117), only in ticks with Gets or Puts
+//   emit        compaction of heartbeat / node-init / pod-patch / delete lists
+//               (wave ballots + block scans), byte emission (wave per patch),
+//               state transitions, and the heartbeat stream: n_managed
+//               identical 1059-byte patches from an LDS template with
+//               16-byte non-temporal stores (node_controller.go:145-204,393-401)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 
 #include "device.h"
 #include "kernels.h"
@@ -31,15 +32,44 @@ namespace kwok {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-// wave-wide inclusive scan (64 lanes)
+// wave-wide inclusive scan (64 lanes) with DPP row shifts and row broadcasts:
+// six VALU adds with a cross-lane source operand, no LDS round trip (a
+// __shfl_up is a ds_bpermute, ~100+ cycles each, six of them dependent).
+// Every lane of the wave must be active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t x) {
+    // lanes whose source lies outside the row / rows outside ROW_MASK read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xF, false);
+}
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
-        if (l >= off) x += y;
-    }
+    x += dpp_src<0x111, 0xF>(x);  // row_shr:1
+    x += dpp_src<0x112, 0xF>(x);  // row_shr:2
+    x += dpp_src<0x114, 0xF>(x);  // row_shr:4
+    x += dpp_src<0x118, 0xF>(x);  // row_shr:8   -> inclusive within each row of 16
+    x += dpp_src<0x142, 0xA>(x);  // row_bcast:15 (lane 15 of row r into row r+1, rows 1 and 3)
+    x += dpp_src<0x143, 0xC>(x);  // row_bcast:31 (lane 31 into rows 2 and 3)
     return x;
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_src64(uint64_t x) {
+    const uint32_t lo = dpp_src<CTRL, ROW_MASK>((uint32_t)x), hi = dpp_src<CTRL, ROW_MASK>((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
+    x += dpp_src64<0x111, 0xF>(x);
+    x += dpp_src64<0x112, 0xF>(x);
+    x += dpp_src64<0x114, 0xF>(x);
+    x += dpp_src64<0x118, 0xF>(x);
+    x += dpp_src64<0x142, 0xA>(x);
+    x += dpp_src64<0x143, 0xC>(x);
+    return x;
+}
+// wave total, uniform (scalar) result
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+    x = wave_incl_scan64(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // block-wide exclusive scan of NF u32 fields; returns totals.  BLOCK=256.
@@ -85,7 +115,7 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* lis
     const int l = lane_id();
     int leader = __ffsll((unsigned long long)m) - 1;
     if (l == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
     if (pred) list[base + __popcll(m & ((1ull << l) - 1))] = x;
 }
 
@@ -209,493 +239,9 @@ __device__ __forceinline__ uint32_t init_patch_len(uint64_t blob) {
     return 11u + pre + 14u + (uint32_t)CONDS_LEN + 1u + post + 2u;
 }
 
-// ---------------------------------------------------------------------------
-// k_classify
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_classify(DevState S) {
-    const uint32_t tile = blockIdx.x;
-    const int t = threadIdx.x;
-    if (tile < S.node_tiles) {
-        const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
-        uint32_t f[6] = {0, 0, 0, 0, 0, 0};  // hb, init, init_bytes, lock, managed, ready
-        uint32_t packed = 0;
-        if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
-        uint32_t tick = 0;
-#pragma unroll
-        for (int k = 0; k < NODE_PER_THREAD; k++) {
-            uint8_t s = (uint8_t)(packed >> (8 * k));
-            NodeCls c = classify_node(s);
-            f[0] += c.hb;
-            f[3] += c.lock;
-            f[4] += c.managed;
-            f[5] += c.ready;
-            if (c.init) {
-                f[1]++;
-                f[2] += (init_patch_len(S.node_blob[first + k]) + 15u) & ~15u;
-            }
-            tick |= (uint32_t)node_tick_flags(s) << (8 * k);
-        }
-        if (first < S.n_node_slots) *reinterpret_cast<uint32_t*>(S.node_tick + first) = tick;
-        block_sum<6>(f);
-        if (t == 0) {
-            uint32_t* o = S.tiles + (size_t)tile * TF_STRIDE;
-            o[TF_HB] = f[0];
-            o[TF_INIT] = f[1];
-            o[TF_INIT_BYTES] = f[2];
-            o[TF_LOCK] = f[3];
-            o[TF_MANAGED] = f[4];
-            o[TF_READY] = f[5];
-        }
-        return;
-    }
-    const uint32_t ptile = tile - S.node_tiles;
-    const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    uint32_t f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running, rel
-    // slots at or above the bucket's fill mark are known empty: no loads
-    const bool live = first < S.n_pod_slots && (first % S.cp) < S.pod_fill[first / S.cp];
-    uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = make_uint4(0, 0, 0, 0), ipa = make_uint4(0, 0, 0, 0),
-          ipb = make_uint4(0, 0, 0, 0);
-    if (live) {
-        st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
-        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
-        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
-        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
-    }
-    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
-    const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
-    const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
-    const uint32_t bucket_local = first / S.cp;  // 8 slots never straddle a bucket (cp % 8 == 0)
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        uint16_t st = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
-        uint16_t nl = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
-        uint32_t ip = ips[k];
-        uint8_t ns = 0;
-        if (st & PS_USED) ns = S.node_state[bucket_local * S.cn + nl];
-        uint8_t ntf = node_tick_flags(ns);
-        PodCls c = classify_pod(st, ntf, ip);
-        f[0] += c.del;
-        f[1] += c.eval;
-        f[2] += c.alloc;
-        // the Deleted event of a pod we delete: release if the node is managed and the IP in CIDR
-        bool rel = c.del && (ntf & NT_MANAGED) && ip && in_cidr(S.pool, ip);
-        // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
-        // addresses not already in `used` change the pool
-        bool use = c.eval && ip && in_cidr(S.pool, ip) && !bm_test(S.used_bm, ip - S.pool.net);
-        if (S.world == 1) {
-            // single rank: Use() in place; the Put of a released address waits in rel_bm
-            // and is folded by k_pool_prep, after every Use of this tick (Use -> Put order)
-            const uint64_t bit = ip - S.pool.net;
-            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
-            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
-        } else {
-            wave_append(rel, ip, S.rel_list, &S.list_counts[1]);
-            wave_append(use, ip, S.use_list, &S.list_counts[0]);
-        }
-        f[8] += rel;
-        if (c.need) {
-            f[3]++;
-            f[4] += S.specs[S.pod_spec[first + k]].max_len;
-        }
-        bool total = c.used && !c.del;
-        f[5] += total;
-        f[6] += total && !c.need && c.phase == PHASE_PENDING;
-        f[7] += total && (c.need || c.phase == PHASE_RUNNING);
-    }
-    block_sum<9>(f);
-    if (t == 0) {
-        uint32_t* o = S.tiles + (size_t)tile * TF_STRIDE;
-        o[TF_DEL] = f[0];
-        o[TF_EVAL] = f[1];
-        o[TF_ALLOC] = f[2];
-        o[TF_PP] = f[3];
-        o[TF_PP_BYTES] = f[4];
-        o[TF_TOTAL] = f[5];
-        o[TF_PENDING] = f[6];
-        o[TF_RUNNING] = f[7];
-        o[TF_REL] = f[8];
-    }
-}
 
 // ---------------------------------------------------------------------------
-// k_scan: one block of 256 threads.  Exclusive scan of the tile counts ->
-// tile bases; arena layout; counters; per-tick heartbeat template.  Wave
-// shuffles inside each wave, one LDS exchange across the 16 waves.
-// ---------------------------------------------------------------------------
-constexpr int SCAN_THREADS = 512;  // 256-VGPR budget: partials stay in registers
-constexpr int SCAN_WAVES = SCAN_THREADS / 64;
-
-__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        unsigned long long y = __shfl_up((unsigned long long)x, off, 64);
-        if (l >= off) x += y;
-    }
-    return x;
-}
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor((unsigned long long)x, off, 64);
-    return x;
-}
-
-// tile record -> the 7 scanned fields and 8 reduced fields
-struct TileVals {
-    uint32_t sc[7], cn[8];
-};
-__device__ __forceinline__ void load_tile(const DevState& S, uint32_t i, TileVals& v) {
-    const uint4* o = reinterpret_cast<const uint4*>(S.tiles + (size_t)i * TF_STRIDE);
-    const uint4 a = o[0], b = o[1], c = o[2], d = o[3];
-    const uint32_t f[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-    if (i < S.node_tiles) {
-        v.sc[0] = f[TF_HB], v.sc[1] = f[TF_INIT], v.sc[2] = f[TF_INIT_BYTES];
-        v.sc[3] = v.sc[4] = v.sc[5] = v.sc[6] = 0;
-        v.cn[0] = f[TF_LOCK], v.cn[1] = f[TF_MANAGED], v.cn[2] = f[TF_READY];
-        v.cn[3] = v.cn[4] = v.cn[5] = v.cn[6] = v.cn[7] = 0;
-    } else {
-        v.sc[0] = v.sc[1] = v.sc[2] = 0;
-        v.sc[3] = f[TF_DEL], v.sc[4] = f[TF_PP], v.sc[5] = f[TF_PP_BYTES], v.sc[6] = f[TF_ALLOC];
-        v.cn[0] = v.cn[1] = v.cn[2] = 0;
-        v.cn[3] = f[TF_EVAL], v.cn[4] = f[TF_TOTAL], v.cn[5] = f[TF_PENDING], v.cn[6] = f[TF_RUNNING];
-        v.cn[7] = f[TF_REL];
-    }
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan(DevState S, uint64_t start_unix, int world_size) {
-    const uint64_t now_unix = *(volatile const uint64_t*)S.tick_now;  // pinned host scalar
-    const int t = threadIdx.x, l = lane_id(), w = wave_id();
-    const uint32_t T = S.node_tiles + S.pod_tiles;
-    const uint32_t per = (T + SCAN_THREADS - 1) / SCAN_THREADS;
-    const uint32_t lo = min(T, t * per), hi = min(T, lo + per);
-    // scanned: hb, init, init_bytes (node tiles); del, pp, pp_bytes, alloc (pod tiles)
-    // reduced: lock, managed, ready (nodes); eval, total, pending, running, rel (pods)
-    constexpr int NS = 7, NC = 8;
-    uint32_t sc[NS] = {0, 0, 0, 0, 0, 0, 0}, cn[NC] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = lo; i < hi; i++) {
-        TileVals v;
-        load_tile(S, i, v);
-#pragma unroll
-        for (int f = 0; f < NS; f++) sc[f] += v.sc[f];
-#pragma unroll
-        for (int f = 0; f < NC; f++) cn[f] += v.cn[f];
-    }
-    __shared__ uint64_t wtot[SCAN_WAVES][NS];
-    __shared__ uint64_t wcnt[SCAN_WAVES][NC];
-    uint64_t ex[NS];
-#pragma unroll
-    for (int f = 0; f < NS; f++) {
-        uint64_t inc = wave_incl_scan64(sc[f]);
-        ex[f] = inc - sc[f];
-        if (l == 63) wtot[w][f] = inc;
-    }
-#pragma unroll
-    for (int f = 0; f < NC; f++) {
-        uint64_t r = wave_sum64(cn[f]);
-        if (l == 0) wcnt[w][f] = r;
-    }
-    __syncthreads();
-    uint64_t total[NS];
-#pragma unroll
-    for (int f = 0; f < NS; f++) {
-        uint64_t pre = 0, tot = 0;
-#pragma unroll
-        for (int k = 0; k < SCAN_WAVES; k++) {
-            uint64_t v = wtot[k][f];
-            pre += k < w ? v : 0;
-            tot += v;
-        }
-        ex[f] += pre;
-        total[f] = tot;
-    }
-    for (uint32_t i = lo; i < hi; i++) {
-        TileVals v;
-        load_tile(S, i, v);
-        uint64_t* b = S.tile_base + (size_t)i * 4;
-        if (i < S.node_tiles) {
-            b[0] = ex[0], b[1] = ex[1], b[2] = ex[2];
-        } else {
-            b[0] = ex[3], b[1] = ex[4], b[2] = ex[5], b[3] = ex[6];
-        }
-#pragma unroll
-        for (int f = 0; f < NS; f++) ex[f] += v.sc[f];
-    }
-    TickHdr* H = S.hdr;
-    if (t == 0) {
-        uint64_t red[NC];
-        for (int f = 0; f < NC; f++) {
-            red[f] = 0;
-            for (int k = 0; k < SCAN_WAVES; k++) red[f] += wcnt[k][f];
-        }
-        H->n_hb = (uint32_t)total[0];
-        H->n_init = (uint32_t)total[1];
-        H->init_bytes = total[2];
-        H->n_del = (uint32_t)total[3];
-        H->n_pp = (uint32_t)total[4];
-        H->pp_bytes = total[5];
-        H->n_alloc_local = (uint32_t)total[6];
-        H->n_lock = (uint32_t)red[0];
-        H->n_eval = (uint32_t)red[3];
-        H->n_rel = (uint32_t)red[7];
-        H->n_use = world_size > 1 ? S.list_counts[0] : 0;
-        H->hb_base = 0;
-        H->init_base = total[0] * (uint64_t)HB_STRIDE;
-        H->pod_base = H->init_base + total[2];
-        H->arena_bytes = H->pod_base + total[5];
-        H->overflow = H->arena_bytes > S.arena_cap;
-        uint64_t* L = H->local_counters;
-        L[0] = total[0];  // heartbeat
-        L[1] = total[1];  // node_init
-        L[2] = total[4];  // pod_patch
-        L[3] = total[3];  // delete
-        L[4] = total[6];  // alloc
-        L[5] = red[7];    // release
-        L[6] = red[3];    // evaluated
-        L[7] = red[0];    // lock_checked
-        L[8] = red[1];    // nodes_managed
-        L[9] = red[2];    // nodes_ready
-        L[10] = red[4];   // pods_total
-        L[11] = red[5];   // pods_pending
-        L[12] = red[6];   // pods_running
-        for (int k = 13; k < 16; k++) L[k] = 0;
-        if (world_size == 1) {
-            for (int k = 0; k < 16; k++) H->counters[k] = L[k];
-            H->alloc_total = total[6];
-            H->alloc_base = 0;
-            H->rel_total = red[7];
-        } else {
-            XMsg* X = S.xmsg;
-            X->alloc = total[6];
-            X->n_use = S.list_counts[0];
-            X->n_rel = S.list_counts[1];
-            for (int k = 0; k < 16; k++) X->counters[k] = L[k];
-        }
-    }
-    // exchange message lists (multi-rank), inline when they fit
-    if (world_size > 1) {
-        const uint32_t nu = S.list_counts[0], nr = S.list_counts[1];
-        if (nu + nr <= (uint32_t)XINLINE) {
-            for (uint32_t i = t; i < nu; i += SCAN_THREADS) S.xmsg->ips[i] = S.use_list[i];
-            for (uint32_t i = t; i < nr; i += SCAN_THREADS) S.xmsg->ips[nu + i] = S.rel_list[i];
-        }
-    }
-    // per-tick heartbeat template: static bytes + Now / StartTime in the 10 slots
-    Ts now = format_ts(now_unix), st = format_ts(start_unix);
-    for (int i = t; i < HB_STRIDE; i += SCAN_THREADS) {
-        uint8_t k = S.hb_kind[i];
-        uint32_t b;
-        if (k == 0xFF) b = S.hb_static[i];
-        else if (k < TS_LEN) b = ts_byte(now, k);
-        else b = ts_byte(st, k - TS_LEN);
-        S.hb_tmpl[i] = (uint8_t)b;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_xreduce (multi-rank): fold the gathered exchange headers
-// ---------------------------------------------------------------------------
-__global__ void k_xreduce(DevState S, const XMsg* all, int world_size, int rank) {
-    if (threadIdx.x != 0) return;
-    TickHdr* H = S.hdr;
-    uint64_t tot = 0, base = 0;
-    for (int k = 0; k < 16; k++) H->counters[k] = 0;
-    for (int r = 0; r < world_size; r++) {
-        if (r < rank) base += all[r].alloc;
-        tot += all[r].alloc;
-        for (int k = 0; k < 16; k++) H->counters[k] += all[r].counters[k];
-    }
-    H->alloc_total = tot;
-    H->alloc_base = base;
-    uint64_t rel = 0;
-    for (int r = 0; r < world_size; r++) rel += all[r].n_rel;
-    H->rel_total = rel;
-}
-
-// ---------------------------------------------------------------------------
-// ipPool kernels on the replicated bitmaps
-//
-// Order inside a tick (DESIGN.md "Tick contract"): every Use (configurePod,
-// pod_controller.go:378-382) -> every Put of this tick's deletions
-// (pod_controller.go:329-336 / utils.go:100-108) -> the Gets (utils.go:83-98)
-// in canonical order.  Uses set `used` directly; Puts accumulate in rel_bm
-// (atomic ORs commute with the Uses) and k_pool_prep folds them:
-//   used &= ~rel, usable |= rel.
-// ---------------------------------------------------------------------------
-// ingest-time Put (a Deleted watch event), applied immediately
-__global__ void k_pool_puts_now(DevState S, const uint32_t* ips, uint32_t n) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        uint32_t ip = ips[i];
-        if (!in_cidr(S.pool, ip)) continue;
-        uint64_t b = ip - S.pool.net;
-        atomicAnd((unsigned long long*)&S.used_bm[b >> 6], ~(1ull << (b & 63)));
-        atomicOr((unsigned long long*)&S.usable_bm[b >> 6], 1ull << (b & 63));
-    }
-}
-// multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm
-__global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
-    for (int r = 0; r < nranks; r++) {
-        const ListDesc d = ld[r];
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_use + d.n_rel; i += gridDim.x * blockDim.x) {
-            bool use = i < d.n_use;
-            uint32_t ip = use ? d.use[i] : d.rel[i - d.n_use];
-            if (!in_cidr(S.pool, ip)) continue;
-            uint64_t b = ip - S.pool.net;
-            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
-        }
-    }
-}
-
-// free bits for ipPool.new at or after the fresh cursor.  Addresses still
-// usable this tick are excluded: fresh allocation only happens once Get's
-// reuse branch has taken every usable address (take = U whenever F > 0).
-__device__ __forceinline__ uint64_t free_mask(const DevState& S, uint64_t w, uint64_t used, uint64_t usable,
-                                              uint64_t cursor_bit) {
-    uint64_t lo = w * 64;
-    if (lo + 64 <= cursor_bit) return 0;
-    uint64_t m = ~used & ~usable;
-    if (cursor_bit > lo) m &= ~0ull << (cursor_bit - lo);
-    if (lo + 64 > S.pool.size) m &= (S.pool.size - lo >= 64) ? ~0ull : ((1ull << (S.pool.size - lo)) - 1);
-    return m;
-}
-__device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
-    uint64_t a = (uint64_t)S.pool.base + *S.pool_index;  // ipPool.new: addIP(cidr.IP, index)
-    return a >= S.pool.net ? a - S.pool.net : 0;
-}
-
-constexpr int POOL_WPT = 4;                  // bitmap words per thread
-constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per block
-
-// fold this tick's Puts, then count usable / free bits per block for the plan
-__global__ __launch_bounds__(BLOCK) void k_pool_prep(DevState S) {
-    const TickHdr* H = S.hdr;
-    const bool fold = H->rel_total != 0, count = H->alloc_total != 0;
-    if (!fold && !count) return;
-    const uint64_t cb = cursor_bit(S);
-    uint32_t f[2] = {0, 0};
-    for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        if (w >= S.pool.words) break;
-        uint64_t used = S.used_bm[w], usable = S.usable_bm[w];
-        if (fold) {
-            uint64_t r = S.rel_bm[w];
-            if (r) {
-                used &= ~r;
-                usable |= r;
-                S.used_bm[w] = used;
-                S.usable_bm[w] = usable;
-                S.rel_bm[w] = 0;
-            }
-        }
-        f[0] += __popcll(usable);
-        f[1] += __popcll(free_mask(S, w, used, usable, cb));
-    }
-    if (!count) return;
-    block_sum<2>(f);
-    if (threadIdx.x == 0) {
-        S.pool_blk[2 * blockIdx.x] = f[0];
-        S.pool_blk[2 * blockIdx.x + 1] = f[1];
-    }
-}
-
-// select + commit.  Allocation ordinal g (global, canonical order):
-//   g < take                -> g-th lowest usable address (the build's reuse rule)
-//   g < take + fresh_in     -> (g-take)-th free in-CIDR address from the cursor
-//   otherwise               -> fresh_out_start + (g - take - fresh_in)  (beyond the CIDR)
-// Every rank commits ALL allocations to its replica; it records the addresses
-// of its own ordinals [alloc_base, alloc_base + n_alloc_local).  Each block
-// derives the plan from the per-block counts itself (no separate launch).
-__global__ __launch_bounds__(BLOCK) void k_pool_select(DevState S, uint32_t nblk) {
-    TickHdr* H = S.hdr;
-    const uint64_t A = H->alloc_total;
-    if (A == 0) return;
-    __shared__ uint64_t sh[4];  // U, Fin, block base usable, block base free
-    if (threadIdx.x < 64) {
-        uint64_t u = 0, fr = 0, bu = 0, bf = 0;
-        for (uint32_t i = threadIdx.x; i < nblk; i += 64) {
-            uint64_t a = S.pool_blk[2 * i], c = S.pool_blk[2 * i + 1];
-            u += a;
-            fr += c;
-            if (i < blockIdx.x) bu += a, bf += c;
-        }
-        u = wave_sum64(u);
-        fr = wave_sum64(fr);
-        bu = wave_sum64(bu);
-        bf = wave_sum64(bf);
-        if (threadIdx.x == 0) sh[0] = u, sh[1] = fr, sh[2] = bu, sh[3] = bf;
-    }
-    __syncthreads();
-    const uint64_t U = sh[0], Fin = sh[1];
-    const uint64_t take = A < U ? A : U, F = A - take, fin = F < Fin ? F : Fin, fout = F - fin;
-    const uint64_t cur = (uint64_t)S.pool.base + *S.pool_index;
-    const uint64_t end = (uint64_t)S.pool.net + S.pool.size;
-    const uint64_t fout0 = cur > end ? cur : end;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        H->usable_total = U;
-        H->take_usable = take;
-        H->fresh_in = fin;
-        H->fresh_out_start = fout0;
-        // ipPool.index after the last fresh address (k_emit commits it);
-        // fin > 0 && fout == 0: the thread that selects the last one sets it below
-        if (fout) H->cursor_index = fout0 + fout - S.pool.base;
-        else if (fin == 0) H->cursor_index = *S.pool_index;
-    }
-    const uint64_t lo_g = H->alloc_base, hi_g = lo_g + H->n_alloc_local;
-    const uint64_t cb = cursor_bit(S);
-    const bool advance = fin > 0 && fout == 0;
-    uint32_t c[2][POOL_WPT];
-    uint64_t wu[POOL_WPT], wf[POOL_WPT];
-    uint32_t v[2] = {0, 0};
-    for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        uint64_t used = w < S.pool.words ? S.used_bm[w] : ~0ull;
-        wu[k] = w < S.pool.words ? S.usable_bm[w] : 0;
-        wf[k] = w < S.pool.words ? free_mask(S, w, used, wu[k], cb) : 0;
-        c[0][k] = __popcll(wu[k]);
-        c[1][k] = __popcll(wf[k]);
-        v[0] += c[0][k];
-        v[1] += c[1][k];
-    }
-    uint32_t tot[2];
-    block_excl_scan<2>(v, tot);
-    uint64_t ru = sh[2] + v[0];
-    uint64_t rf = sh[3] + v[1];
-    for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)blockIdx.x * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        if (w >= S.pool.words) break;
-        if (ru < take && wu[k]) {
-            uint64_t n = take - ru < c[0][k] ? take - ru : c[0][k];
-            uint64_t m = wu[k], sel = 0;
-            for (uint64_t j = 0; j < n; j++) {
-                uint32_t b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-                m &= m - 1;
-                sel |= 1ull << b;
-                uint64_t g = ru + j;
-                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
-            }
-            S.usable_bm[w] &= ~sel;  // ipPool.Get: delete(usable, ip) ...
-            S.used_bm[w] |= sel;     // ... used[ip]   (one thread owns word w)
-        }
-        ru += c[0][k];
-        if (rf < fin && wf[k]) {
-            uint64_t n = fin - rf < c[1][k] ? fin - rf : c[1][k];
-            uint64_t m = wf[k], sel = 0;
-            uint32_t b = 0;
-            for (uint64_t j = 0; j < n; j++) {
-                b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-                m &= m - 1;
-                sel |= 1ull << b;
-                uint64_t g = take + rf + j;
-                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
-            }
-            S.used_bm[w] |= sel;  // ipPool.new: used[ip]  (usable add + Get delete net to nothing)
-            if (advance && rf + n == fin) H->cursor_index = (uint64_t)S.pool.net + w * 64 + b + 1 - S.pool.base;
-        }
-        rf += c[1][k];
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_emit: compaction + byte emission + state transitions
+// patch writers (one wave per patch)
 // ---------------------------------------------------------------------------
 struct PodJob {
     uint32_t slot;   // local slot
@@ -761,11 +307,11 @@ __device__ void write_pod_patch(const DevState& S, const PodJob& j, uint8_t* out
 }
 
 // one wave writes one node init patch: {"status":{ pre ,"conditions": CONDS , post }}
-__device__ void write_init_patch(const DevState& S, uint64_t blob, uint8_t* out) {
+__device__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl, uint8_t* out) {
     const uint32_t boff = (uint32_t)blob, pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
     const uint32_t len = init_patch_len(blob);
     const uint8_t* bb = S.blob + boff;
-    const uint8_t* conds = S.hb_tmpl + HB_PREFIX;
+    const uint8_t* conds = hb_tmpl + HB_PREFIX;
     const char* p0 = "{\"status\":{";
     const char* p1 = ",\"conditions\":";
     for (uint32_t q0 = lane_id() * 4u; q0 < len; q0 += 256u) {
@@ -789,145 +335,479 @@ __device__ void write_init_patch(const DevState& S, uint64_t blob, uint8_t* out)
     }
 }
 
-// node tiles: heartbeat list, node-init patches, node state (runs on the heartbeat stream)
-__global__ __launch_bounds__(BLOCK) void k_emit_nodes(DevState S) {
-    const uint32_t tile = blockIdx.x;
+// ---------------------------------------------------------------------------
+// grid barrier for the persistent tick kernel (MI355X_MICROARCH.md "Workgroup
+// dispatch ... inter-workgroup visibility" and the barrier-xcd price row;
+// cdna_hip_programming.md §6 G16).  Producer side: every wave drains its
+// stores, block barrier, lane-0 agent release + vmcnt(0).  Arrival is two-level
+// (8 group counters on their own lines, then one top counter) so no single
+// address takes 512 serialized atomics; all counters are monotonic (a group's
+// last arriver is the one whose count reaches a multiple of the group size), so
+// nothing is reset between barriers or ticks.  Consumers poll the generation
+// relaxed with s_sleep, then one agent acquire + vmcnt(0) + block barrier.
+// Spins are bounded (2 s of s_memrealtime): a timeout flags the tick as failed
+// in the host-visible header instead of hanging the GPU.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void grid_barrier(GridBar* bar, TickHdr* hdr_host) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t* w = bar->w;
+        const uint32_t G = gridDim.x, g = blockIdx.x & 7;
+        const uint32_t gsize = (G - g + 7) / 8, ngroups = G < 8 ? G : 8;
+        const uint32_t gen = __hip_atomic_load(&w[BAR_GEN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bool released = false;
+        const uint32_t ga =
+            __hip_atomic_fetch_add(&w[BAR_GRP + BAR_LINE * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (ga % gsize == 0) {
+            const uint32_t ta = __hip_atomic_fetch_add(&w[BAR_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            if (ta % ngroups == 0) {
+                __hip_atomic_fetch_add(&w[BAR_GEN], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                released = true;
+            }
+        }
+        if (!released) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(&w[BAR_GEN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+                    __hip_atomic_store(&hdr_host->err, TICK_ERR_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// tile classification (phase 1): predicates A.4/A.5, per-tile counts,
+// in-place Use / pending Put bits (single rank) or exchange lists (multi rank).
+// Loads are issued in two independent rounds (state words, then node state +
+// pool word + spec ids) so a tile costs two HBM round trips, not four.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void classify_node_tile(const DevState& S, uint32_t tile, uint32_t (&ag)[AG_STRIDE]) {
     const int t = threadIdx.x;
-    const TickHdr* H = S.hdr;
-    __shared__ InitJob ijobs[NODE_TILE];
-    {
-        const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
-        const uint64_t* base = S.tile_base + (size_t)tile * 4;
-        uint32_t packed = 0;
-        if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
-        NodeCls c[NODE_PER_THREAD];
-        uint32_t v[3] = {0, 0, 0};  // hb, init, init bytes
-        uint32_t ilen[NODE_PER_THREAD];
-        uint64_t blob[NODE_PER_THREAD];
+    const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
+    uint32_t f[6] = {0, 0, 0, 0, 0, 0};  // hb, init, init_bytes, lock, managed, ready
+    uint32_t packed = 0;
+    if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
+    uint32_t tick = 0;
 #pragma unroll
-        for (int k = 0; k < NODE_PER_THREAD; k++) {
-            c[k] = classify_node((uint8_t)(packed >> (8 * k)));
-            v[0] += c[k].hb;
-            ilen[k] = 0;
-            blob[k] = 0;
-            if (c[k].init) {
-                blob[k] = S.node_blob[first + k];
-                ilen[k] = init_patch_len(blob[k]);
-                v[1]++;
-                v[2] += (ilen[k] + 15u) & ~15u;
+    for (int k = 0; k < NODE_PER_THREAD; k++) {
+        uint8_t s = (uint8_t)(packed >> (8 * k));
+        NodeCls c = classify_node(s);
+        f[0] += c.hb;
+        f[3] += c.lock;
+        f[4] += c.managed;
+        f[5] += c.ready;
+        if (c.init) {
+            f[1]++;
+            f[2] += (init_patch_len(S.node_blob[first + k]) + 15u) & ~15u;
+        }
+        tick |= (uint32_t)node_tick_flags(s) << (8 * k);
+    }
+    if (first < S.n_node_slots) *reinterpret_cast<uint32_t*>(S.node_tick + first) = tick;
+    block_sum<6>(f);
+    for (int i = 0; i < AG_STRIDE; i++) ag[i] = 0;
+    ag[AG_HB] = f[0];
+    ag[AG_INIT] = f[1];
+    ag[AG_BYTES] = f[2];
+    ag[AG_INIT_BYTES] = f[2];
+    ag[AG_LOCK] = f[3];
+    ag[AG_MANAGED] = f[4];
+    ag[AG_READY] = f[5];
+}
+
+// the first round of a pod tile: state, node index, podIP and spec id words of
+// this thread's 8 slots; slots at or above the bucket's fill mark read as empty
+struct PodQuad {
+    uint16_t st[POD_PER_THREAD], nl[POD_PER_THREAD];
+    uint32_t ip[POD_PER_THREAD];
+    bool live;
+};
+__device__ __forceinline__ void load_pod_quad(const DevState& S, uint32_t first, PodQuad& q) {
+    uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
+    uint32_t fill = 0;
+    if (first < S.n_pod_slots) {  // all five loads in flight together
+        fill = S.pod_fill[first / S.cp];
+        st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
+        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
+        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
+        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
+    }
+    q.live = first < S.n_pod_slots && (first % S.cp) < fill;
+    if (!q.live) st4 = make_uint4(0, 0, 0, 0);
+    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
+    const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
+    const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        q.st[k] = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
+        q.nl[k] = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
+        q.ip[k] = ips[k];
+    }
+}
+// could this pod need a patch (computePatchData), given it is evaluated?
+__device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
+    const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
+    return (st & PS_USED) && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ip == 0);
+}
+// spec ids of this thread's 8 slots, loaded only when one of them may need a patch
+__device__ __forceinline__ void load_spec_ids(const DevState& S, uint32_t first, const PodQuad& q, uint16_t (&sp)[8]) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(q.st[k], q.ip[k]);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (any) v = *reinterpret_cast<const uint4*>(S.pod_spec + first);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) sp[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
+}
+
+__device__ __forceinline__ void classify_pod_tile(const DevState& S, uint32_t ptile, uint32_t (&ag)[AG_STRIDE]) {
+    const int t = threadIdx.x;
+    const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
+    uint32_t f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running, rel
+    PodQuad q;
+    load_pod_quad(S, first, q);
+    const uint32_t bucket_local = first / S.cp;  // 8 slots never straddle a bucket (cp % 8 == 0)
+    // round 2: node state, the pool word of the podIP (speculative) and the spec ids
+    uint8_t ns[POD_PER_THREAD];
+    uint64_t uw[POD_PER_THREAD];
+    uint16_t sp[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        ns[k] = (q.st[k] & PS_USED) ? S.node_state[bucket_local * S.cn + q.nl[k]] : 0;
+        const bool inc = (q.st[k] & PS_USED) && q.ip[k] && in_cidr(S.pool, q.ip[k]);
+        uw[k] = inc ? S.used_bm[(q.ip[k] - S.pool.net) >> 6] : ~0ull;
+    }
+    load_spec_ids(S, first, q, sp);
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint16_t st = q.st[k];
+        const uint32_t ip = q.ip[k];
+        const uint8_t ntf = node_tick_flags(ns[k]);
+        PodCls c = classify_pod(st, ntf, ip);
+        f[0] += c.del;
+        f[1] += c.eval;
+        f[2] += c.alloc;
+        const bool inc = ip && in_cidr(S.pool, ip);
+        const uint64_t bit = ip - S.pool.net;
+        // the Deleted event of a pod we delete: release if the node is managed and the IP in CIDR
+        bool rel = c.del && (ntf & NT_MANAGED) && inc;
+        // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
+        // addresses not already in `used` change the pool
+        bool use = c.eval && inc && !((uw[k] >> (bit & 63)) & 1);
+        if (S.world == 1) {
+            // single rank: Use() in place; the Put of a released address waits in rel_bm
+            // and is folded in the pool phase, after every Use of this tick (Use -> Put)
+            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
+            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+        } else {
+            wave_append(rel, ip, S.rel_list, &S.list_counts[1]);
+            wave_append(use, ip, S.use_list, &S.list_counts[0]);
+        }
+        f[8] += rel;
+        if (c.need) {
+            f[3]++;
+            f[4] += S.specs[sp[k]].max_len;
+        }
+        bool total = c.used && !c.del;
+        f[5] += total;
+        f[6] += total && !c.need && c.phase == PHASE_PENDING;
+        f[7] += total && (c.need || c.phase == PHASE_RUNNING);
+    }
+    block_sum<9>(f);
+    for (int i = 0; i < AG_STRIDE; i++) ag[i] = 0;
+    ag[AG_DEL] = f[0];
+    ag[AG_EVAL] = f[1];
+    ag[AG_ALLOC] = f[2];
+    ag[AG_PP] = f[3];
+    ag[AG_BYTES] = f[4];
+    ag[AG_TOTAL] = f[5];
+    ag[AG_PENDING] = f[6];
+    ag[AG_RUNNING] = f[7];
+    ag[AG_REL] = f[8];
+}
+
+// ---------------------------------------------------------------------------
+// ipPool phase (only in ticks with Gets or Puts)
+//
+// Order inside a tick (DESIGN.md "Tick contract"): every Use (configurePod,
+// pod_controller.go:378-382) -> every Put of this tick's deletions
+// (pod_controller.go:329-336 / utils.go:100-108) -> the Gets (utils.go:83-98)
+// in canonical order.  Uses set `used` directly; Puts accumulate in rel_bm
+// (atomic ORs commute with the Uses) and the prep step folds them:
+//   used &= ~rel, usable |= rel.
+// ---------------------------------------------------------------------------
+// free bits for ipPool.new at or after the fresh cursor.  Addresses still
+// usable this tick are excluded: fresh allocation only happens once Get's
+// reuse branch has taken every usable address (take = U whenever F > 0).
+__device__ __forceinline__ uint64_t free_mask(const DevState& S, uint64_t w, uint64_t used, uint64_t usable,
+                                              uint64_t cursor_bit) {
+    uint64_t lo = w * 64;
+    if (lo + 64 <= cursor_bit) return 0;
+    uint64_t m = ~used & ~usable;
+    if (cursor_bit > lo) m &= ~0ull << (cursor_bit - lo);
+    if (lo + 64 > S.pool.size) m &= (S.pool.size - lo >= 64) ? ~0ull : ((1ull << (S.pool.size - lo)) - 1);
+    return m;
+}
+__device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
+    uint64_t a = (uint64_t)S.pool.base + *S.pool_index;  // ipPool.new: addIP(cidr.IP, index)
+    return a >= S.pool.net ? a - S.pool.net : 0;
+}
+
+constexpr int POOL_WPT = 4;                  // bitmap words per thread
+constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per word-block
+
+// fold this tick's Puts, count usable / free bits of word-block wb
+__device__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count) {
+    const uint64_t cb = cursor_bit(S);
+    uint32_t f[2] = {0, 0};
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
+        if (w >= S.pool.words) break;
+        uint64_t used = S.used_bm[w], usable = S.usable_bm[w];
+        if (fold) {
+            uint64_t r = S.rel_bm[w];
+            if (r) {
+                used &= ~r;
+                usable |= r;
+                S.used_bm[w] = used;
+                S.usable_bm[w] = usable;
+                S.rel_bm[w] = 0;
             }
         }
-        uint32_t tot[3];
-        block_excl_scan<3>(v, tot);
-        InitJob* ij = ijobs;
-        uint32_t newpacked = 0;
-        uint32_t ji = v[1];
-#pragma unroll
-        for (int k = 0; k < NODE_PER_THREAD; k++) {
-            const int32_t handle = S.node_handle_base + (int32_t)(first + k);
-            if (c[k].hb) S.hb_nodes[base[0] + v[0]++] = handle;
-            uint8_t s = (uint8_t)(packed >> (8 * k));
-            if (c[k].init) {
-                uint64_t ord = base[1] + ji;
-                uint64_t off = H->init_base + base[2] + v[2];
-                S.init_nodes[ord] = handle;
-                S.init_off[ord] = off;
-                S.init_len[ord] = ilen[k];
-                ij[ji].slot = first + k;
-                ij[ji].off = v[2];
-                ji++;
-                v[2] += (ilen[k] + 15u) & ~15u;
-                s |= NS_CONFORMS;  // the apiserver applied the init patch
-            }
-            s &= (uint8_t)~NS_EVENT_LOCK;
-            newpacked |= (uint32_t)s << (8 * k);
-        }
-        if (first < S.n_node_slots) *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
-        __syncthreads();
-        const uint64_t tile_bytes = H->init_base + base[2];
-        for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64) {
-            InitJob jb = ij[j];
-            write_init_patch(S, S.node_blob[jb.slot], S.arena + tile_bytes + jb.off);
-        }
+        f[0] += __popcll(usable);
+        f[1] += __popcll(free_mask(S, w, used, usable, cb));
+    }
+    block_sum<2>(f);
+    if (threadIdx.x == 0 && count) {
+        S.pool_blk[2 * wb] = f[0];
+        S.pool_blk[2 * wb + 1] = f[1];
     }
 }
 
-// pod tiles: delete list, IP assignment, pod patches, pod state; publishes the
-// tick header to pinned host memory
-__global__ __launch_bounds__(BLOCK) void k_emit_pods(DevState S) {
-    const uint32_t ptile = blockIdx.x;
-    const uint32_t tile = S.node_tiles + ptile;
-    const int t = threadIdx.x;
-    const TickHdr* H = S.hdr;
-    if (ptile == 0 && t < 64) {
-        // the header is final here (scan, pool plan): publish it zero-copy
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(H);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
-        for (int i = t; i < (int)(sizeof(TickHdr) / 8); i += 64) dst[i] = src[i];
-        if (t == 0) {
-            if (H->alloc_total) *S.pool_index = H->cursor_index;
-            S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
-            S.list_counts[1] = 0;
+struct PoolPlan {
+    uint64_t U, Fin, take, fin, fout, fout0;
+};
+// every block derives the same plan from the per-word-block counts
+__device__ PoolPlan pool_plan(const DevState& S, uint64_t A, uint32_t nwb, uint32_t upto, uint64_t* bu, uint64_t* bf) {
+    __shared__ uint64_t sh[4];
+    if (threadIdx.x < 64) {
+        uint64_t u = 0, fr = 0, pu = 0, pf = 0;
+        for (uint32_t i = threadIdx.x; i < nwb; i += 64) {
+            uint64_t a = S.pool_blk[2 * i], c = S.pool_blk[2 * i + 1];
+            u += a;
+            fr += c;
+            if (i < upto) pu += a, pf += c;
         }
-        __threadfence_system();
+        u = wave_sum64(u);
+        fr = wave_sum64(fr);
+        pu = wave_sum64(pu);
+        pf = wave_sum64(pf);
+        if (threadIdx.x == 0) sh[0] = u, sh[1] = fr, sh[2] = pu, sh[3] = pf;
     }
-    __shared__ PodJob jobs[POD_TILE];  // 32 KiB
-    const uint64_t* base = S.tile_base + (size_t)tile * 4;  // del, pp, pp_bytes, alloc
+    __syncthreads();
+    PoolPlan p;
+    p.U = sh[0];
+    p.Fin = sh[1];
+    *bu = sh[2];
+    *bf = sh[3];
+    __syncthreads();
+    p.take = A < p.U ? A : p.U;
+    const uint64_t F = A - p.take;
+    p.fin = F < p.Fin ? F : p.Fin;
+    p.fout = F - p.fin;
+    const uint64_t cur = (uint64_t)S.pool.base + *S.pool_index;
+    const uint64_t end = (uint64_t)S.pool.net + S.pool.size;
+    p.fout0 = cur > end ? cur : end;
+    return p;
+}
+
+// select + commit for word-block wb.  Allocation ordinal g (global, canonical order):
+//   g < take            -> g-th lowest usable address (the build's reuse rule)
+//   g < take + fin      -> (g-take)-th free in-CIDR address from the cursor
+//   otherwise           -> fout0 + (g - take - fin)          (beyond the CIDR)
+// Every rank commits ALL allocations to its replica; it records the addresses
+// of its own ordinals [alloc_base, alloc_base + n_alloc_local).
+__device__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
+                                   uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out) {
+    const uint64_t take = p.take, fin = p.fin;
+    const uint64_t cb = cursor_bit(S);
+    const bool advance = fin > 0 && p.fout == 0;
+    uint32_t c[2][POOL_WPT];
+    uint64_t wu[POOL_WPT], wf[POOL_WPT];
+    uint32_t v[2] = {0, 0};
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
+        uint64_t used = w < S.pool.words ? S.used_bm[w] : ~0ull;
+        wu[k] = w < S.pool.words ? S.usable_bm[w] : 0;
+        wf[k] = w < S.pool.words ? free_mask(S, w, used, wu[k], cb) : 0;
+        c[0][k] = __popcll(wu[k]);
+        c[1][k] = __popcll(wf[k]);
+        v[0] += c[0][k];
+        v[1] += c[1][k];
+    }
+    uint32_t tot[2];
+    block_excl_scan<2>(v, tot);
+    uint64_t ru = base_u + v[0];
+    uint64_t rf = base_f + v[1];
+    for (int k = 0; k < POOL_WPT; k++) {
+        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
+        if (w >= S.pool.words) break;
+        if (ru < take && wu[k]) {
+            uint64_t n = take - ru < c[0][k] ? take - ru : c[0][k];
+            uint64_t m = wu[k], sel = 0;
+            for (uint64_t j = 0; j < n; j++) {
+                uint32_t b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+                m &= m - 1;
+                sel |= 1ull << b;
+                uint64_t g = ru + j;
+                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
+            }
+            S.usable_bm[w] &= ~sel;  // ipPool.Get: delete(usable, ip) ...
+            S.used_bm[w] |= sel;     // ... used[ip]   (one thread owns word w)
+        }
+        ru += c[0][k];
+        if (rf < fin && wf[k]) {
+            uint64_t n = fin - rf < c[1][k] ? fin - rf : c[1][k];
+            uint64_t m = wf[k], sel = 0;
+            uint32_t b = 0;
+            for (uint64_t j = 0; j < n; j++) {
+                b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+                m &= m - 1;
+                sel |= 1ull << b;
+                uint64_t g = take + rf + j;
+                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
+            }
+            S.used_bm[w] |= sel;  // ipPool.new: used[ip]  (usable add + Get delete net to nothing)
+            if (advance && rf + n == fin) *cursor_out = (uint64_t)S.pool.net + w * 64 + b + 1 - S.pool.base;
+        }
+        rf += c[1][k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// emission: compaction of the output lists, byte emission, state transitions
+// ---------------------------------------------------------------------------
+// a tile's exclusive prefix of the AG_NSCAN scanned fields (passed by value)
+struct Bases {
+    uint64_t v[AG_NSCAN];
+};
+struct Layout {
+    uint64_t patch_base;  // arena offset of [node inits | pod patches] (= n_hb x HB_STRIDE)
+    uint64_t alloc_base;  // this rank's first global allocation ordinal
+    PoolPlan plan;
+};
+
+// base: this tile's exclusive prefix of the AG_NSCAN scanned fields
+__device__ __forceinline__ void emit_node_tile(const DevState& S, uint32_t tile, const Bases bs, const Layout& L,
+                                               const uint8_t* hb_tmpl, InitJob* ij) {
+    const uint64_t* base = bs.v;
+    const int t = threadIdx.x;
+    const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
+    uint32_t packed = 0;
+    if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
+    NodeCls c[NODE_PER_THREAD];
+    uint32_t v[3] = {0, 0, 0};  // hb, init, init bytes
+    uint32_t ilen[NODE_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < NODE_PER_THREAD; k++) {
+        c[k] = classify_node((uint8_t)(packed >> (8 * k)));
+        v[0] += c[k].hb;
+        ilen[k] = 0;
+        if (c[k].init) {
+            ilen[k] = init_patch_len(S.node_blob[first + k]);
+            v[1]++;
+            v[2] += (ilen[k] + 15u) & ~15u;
+        }
+    }
+    uint32_t tot[3];
+    block_excl_scan<3>(v, tot);
+    uint32_t newpacked = 0;
+    uint32_t ji = v[1];
+    const uint64_t tile_bytes = L.patch_base + base[AG_BYTES];
+#pragma unroll
+    for (int k = 0; k < NODE_PER_THREAD; k++) {
+        const int32_t handle = S.node_handle_base + (int32_t)(first + k);
+        if (c[k].hb) S.hb_nodes[base[AG_HB] + v[0]++] = handle;  // PatchStatus(name, heartbeat body)
+        uint8_t s = (uint8_t)(packed >> (8 * k));
+        if (c[k].init) {
+            uint64_t ord = base[AG_INIT] + ji;
+            S.init_nodes[ord] = handle;
+            S.init_off[ord] = tile_bytes + v[2];
+            S.init_len[ord] = ilen[k];
+            ij[ji].slot = first + k;
+            ij[ji].off = v[2];
+            ji++;
+            v[2] += (ilen[k] + 15u) & ~15u;
+            s |= NS_CONFORMS;  // the apiserver applied the init patch
+        }
+        s &= (uint8_t)~NS_EVENT_LOCK;
+        newpacked |= (uint32_t)s << (8 * k);
+    }
+    if (first < S.n_node_slots && newpacked != packed)
+        *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
+    __syncthreads();
+    for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64)
+        write_init_patch(S, S.node_blob[ij[j].slot], hb_tmpl, S.arena + tile_bytes + ij[j].off);
+    __syncthreads();
+}
+
+__device__ __forceinline__ void emit_pod_tile(const DevState& S, uint32_t ptile, const Bases bs, const Layout& L,
+                                              PodJob* jobs) {
+    const uint64_t* base = bs.v;
+    const int t = threadIdx.x;
     const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    const bool live = first < S.n_pod_slots && (first % S.cp) < S.pod_fill[first / S.cp];
-    uint16_t st[POD_PER_THREAD];
-    uint32_t ip[POD_PER_THREAD];
+    PodQuad q;
+    load_pod_quad(S, first, q);
+    const uint32_t bucket_local = first / S.cp;
+    uint8_t ntf[POD_PER_THREAD];
+    uint16_t sp[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++)
+        ntf[k] = (q.st[k] & PS_USED) ? S.node_tick[bucket_local * S.cn + q.nl[k]] : 0;
+    load_spec_ids(S, first, q, sp);
     PodCls c[POD_PER_THREAD];
     uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
-    const uint32_t bucket_local = first / S.cp;
-    {
-        uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = make_uint4(0, 0, 0, 0), ipa = make_uint4(0, 0, 0, 0),
-              ipb = make_uint4(0, 0, 0, 0);
-        if (live) {
-            st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
-            nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
-            ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
-            ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
-        }
-        const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
-        const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
-        const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
 #pragma unroll
-        for (int k = 0; k < POD_PER_THREAD; k++) {
-            st[k] = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
-            uint16_t nl = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
-            ip[k] = ips[k];
-            uint8_t ntf = (st[k] & PS_USED) ? S.node_tick[bucket_local * S.cn + nl] : 0;
-            c[k] = classify_pod(st[k], ntf, ip[k]);
-            v[0] += c[k].del;
-            if (c[k].need) {
-                v[1]++;
-                v[2] += S.specs[S.pod_spec[first + k]].max_len;
-            }
-            v[3] += c[k].alloc;
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        c[k] = classify_pod(q.st[k], ntf[k], q.ip[k]);
+        v[0] += c[k].del;
+        if (c[k].need) {
+            v[1]++;
+            v[2] += S.specs[sp[k]].max_len;
         }
+        v[3] += c[k].alloc;
     }
     uint32_t tot[4];
     block_excl_scan<4>(v, tot);
-    const uint64_t take = H->take_usable, fin = H->fresh_in, fout0 = H->fresh_out_start, abase = H->alloc_base;
+    const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0, abase = L.alloc_base;
+    const uint64_t tile_bytes = L.patch_base + base[AG_BYTES];
     uint32_t jl = v[1];
     bool dirty = false;
+    uint16_t nst[POD_PER_THREAD];
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
         const uint32_t slot = first + k;
         const int32_t handle = S.pod_handle_base + (int32_t)slot;
-        uint16_t s = st[k];
+        uint16_t s = q.st[k];
         if (c[k].del) {
-            uint64_t ord = base[0] + v[0]++;
+            uint64_t ord = base[AG_DEL] + v[0]++;
             S.del_pods[ord] = handle;
             S.del_fin[ord] = (s & PS_HAS_FIN) ? 1 : 0;
             s = 0;  // DeletePod -> Delete(grace 0): the object is gone
-            dirty = true;
         }
         if (c[k].eval) {
-            uint32_t pip = ip[k];
+            uint32_t pip = q.ip[k];
             if (c[k].alloc) {
-                uint64_t o = base[3] + v[3]++;
+                uint64_t o = base[AG_ALLOC] + v[3]++;
                 uint64_t g = abase + o;
                 pip = g < take + fin ? S.alloc_addr[o] : (uint32_t)(fout0 + (g - take - fin));
             }
@@ -937,55 +817,52 @@ __global__ __launch_bounds__(BLOCK) void k_emit_pods(DevState S) {
                 if (stat) {
                     hip = (s & PS_HAS_HOST_IP) ? S.host_ip[slot] : S.node_ip;
                     if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
-                    if (pip != ip[k]) S.pod_ip[slot] = pip;
+                    if (pip != q.ip[k]) S.pod_ip[slot] = pip;
                 }
-                uint64_t ord = base[1] + jl;
-                const SpecDesc& sd = S.specs[S.pod_spec[slot]];
+                uint64_t ord = base[AG_PP] + jl;
+                const SpecDesc& sd = S.specs[sp[k]];
                 uint32_t len = sd.len_a + sd.len_b + sd.len_c + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
                 S.pp_pods[ord] = handle;
-                S.pp_off[ord] = H->pod_base + base[2] + v[2];
+                S.pp_off[ord] = tile_bytes + v[2];
                 S.pp_len[ord] = len;
                 jobs[jl] = PodJob{slot, v[2], stat ? pip : 0u, hip};
                 jl++;
-                v[2] += S.specs[S.pod_spec[slot]].max_len;
+                v[2] += sd.max_len;
                 // the apiserver applied the patch
                 s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
                                PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
             }
             s &= (uint16_t)~PS_EVENT;
-            dirty = true;
         }
-        st[k] = s;
+        dirty |= s != q.st[k];  // steady-state re-checks leave the state word untouched
+        nst[k] = s;
     }
-    if (live && dirty) {
+    if (q.live && dirty) {
         uint4 o;
-        o.x = st[0] | (uint32_t)st[1] << 16;
-        o.y = st[2] | (uint32_t)st[3] << 16;
-        o.z = st[4] | (uint32_t)st[5] << 16;
-        o.w = st[6] | (uint32_t)st[7] << 16;
+        o.x = nst[0] | (uint32_t)nst[1] << 16;
+        o.y = nst[2] | (uint32_t)nst[3] << 16;
+        o.z = nst[4] | (uint32_t)nst[5] << 16;
+        o.w = nst[6] | (uint32_t)nst[7] << 16;
         *reinterpret_cast<uint4*>(S.pod_state + first) = o;
     }
     __syncthreads();
-    uint8_t* tile_out = S.arena + H->pod_base + base[2];
-    for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64) write_pod_patch(S, jobs[j], tile_out + jobs[j].off);
+    uint8_t* out = S.arena + tile_bytes;
+    for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64) write_pod_patch(S, jobs[j], out + jobs[j].off);
+    __syncthreads();
 }
 
-// ---------------------------------------------------------------------------
-// k_hb_fill: the n_hb heartbeat patches, 67 x 16 B each, from LDS
-// ---------------------------------------------------------------------------
+// this block's share of the n_hb identical heartbeat patches: 67 x 16 B each,
+// non-temporal 16-byte stores from the LDS template (node_controller.go:145-157)
 constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
-__global__ __launch_bounds__(BLOCK) void k_hb_fill(DevState S) {
-    __shared__ uint4 tmpl[HB_CHUNKS];
-    if (threadIdx.x < HB_CHUNKS) tmpl[threadIdx.x] = reinterpret_cast<const uint4*>(S.hb_tmpl)[threadIdx.x];
-    __syncthreads();
-    const uint64_t nchunks = (uint64_t)S.hdr->n_hb * HB_CHUNKS;
+__device__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4* dst = reinterpret_cast<u32x4*>(S.arena + S.hdr->hb_base);
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t nchunks = n_hb * HB_CHUNKS;
+    const uint64_t lo = nchunks * blockIdx.x / gridDim.x, hi = nchunks * (blockIdx.x + 1) / gridDim.x;
+    u32x4* dst = reinterpret_cast<u32x4*>(S.arena);  // heartbeat region starts at arena offset 0
+    uint64_t i = lo + threadIdx.x;
     uint32_t m = (uint32_t)(i % HB_CHUNKS);
-    const uint32_t dm = (uint32_t)(stride % HB_CHUNKS);
-    for (; i < nchunks; i += stride) {
+    constexpr uint32_t dm = BLOCK % HB_CHUNKS;
+    for (; i < hi; i += BLOCK) {
         const uint4 v = tmpl[m];
         u32x4 w = {v.x, v.y, v.z, v.w};
         __builtin_nontemporal_store(w, &dst[i]);  // write-once stream: do not keep in L2
@@ -994,9 +871,335 @@ __global__ __launch_bounds__(BLOCK) void k_hb_fill(DevState S) {
     }
 }
 
+// per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
+__device__ void build_hb_template(const DevState& S, uint8_t* tmpl, uint64_t now_unix, uint64_t start_unix) {
+    const Ts now = format_ts(now_unix), st = format_ts(start_unix);
+    for (int i = threadIdx.x; i < HB_STRIDE; i += BLOCK) {
+        const uint8_t k = S.hb_kind[i];
+        uint32_t b;
+        if (k == 0xFF) b = S.hb_static[i];
+        else if (k < TS_LEN) b = ts_byte(now, k);
+        else b = ts_byte(st, k - TS_LEN);
+        tmpl[i] = (uint8_t)b;
+    }
+    __syncthreads();
+}
+
+// block-wide sums of N u64 partials (every thread gets the totals)
+template <int N>
+__device__ __forceinline__ void block_sum64(uint64_t (&v)[N]) {
+    __shared__ uint64_t part[BLOCK / 64][N];
+#pragma unroll
+    for (int f = 0; f < N; f++) {
+        const uint64_t s = wave_sum64(v[f]);
+        if (lane_id() == 0) part[wave_id()][f] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < N; f++) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) s += part[w][f];
+        v[f] = s;
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
-// ingest + utility kernels
+// k_tick: one controller tick as ONE persistent launch (single rank) or two
+// launches around the exchange (multi-rank: FRONT, then BACK).  Block b owns
+// the contiguous tile range [T*b/G, T*(b+1)/G) (node tiles, then pod tiles).
+//
+//   phase 1  heartbeat template (LDS); classify own tiles; this block's share
+//            of the heartbeat stream (its length n_hb is the host's managed-node
+//            count: the bandwidth-bound stream overlaps the latency-bound
+//            classification and the barrier wait); per-block aggregate
+//                                                              [grid barrier]
+//   phase 2  prefix / totals of the per-block aggregates (one parallel read);
+//            block 0: tick header / exchange message; n_hb checked
+//   phase 3  (only with Gets or Puts) fold Puts + count [barrier], plan +
+//            select + commit [barrier]
+//   phase 4  block 0 publishes the (final) header zero-copy; every block:
+//            emission of its node / pod tiles
 // ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
+                                                   uint32_t n_hb, int phases) {
+    const int t = threadIdx.x;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t T = S.node_tiles + S.pod_tiles;
+    const uint32_t t_lo = (uint32_t)((uint64_t)T * b / G), t_hi = (uint32_t)((uint64_t)T * (b + 1) / G);
+    TickHdr* H = S.hdr;
+    __shared__ union {
+        PodJob pod[POD_TILE];
+        InitJob node[NODE_TILE];
+    } jobs;
+    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
+    __shared__ uint32_t sh_tagg[MAX_TILES_PER_BLOCK][AG_NSCAN];  // own tiles' scanned fields
+    __shared__ Layout sh_L;
+    uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
+    // diagnostics: per-block phase stamps
+#define TSTAMP(k)                                                                               \
+    do {                                                                                        \
+        if (S.trace && t == 0) S.trace[(size_t)b * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    TSTAMP(0);
+    build_hb_template(S, hb_tmpl, now_unix, start_unix);
+
+    if (phases & TICK_FRONT) {
+        if (t == 0) {
+            const uint64_t c = __builtin_amdgcn_s_memrealtime();
+            if (b == 0) H->clk[CLK_ENTRY] = c;
+            if (phases & TICK_PROF) atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)c);
+        }
+        // ---- phase 1: classify own tiles, then the heartbeat share ----------------
+        // odd blocks stream their heartbeat share first, even blocks classify first:
+        // the two resident blocks of a CU overlap bandwidth- and latency-bound work
+        const bool hb_first = (phases & TICK_HB_FIRST) && (b & 1);
+        if (hb_first) hb_fill_share(S, hb_tmpl4, n_hb);
+        uint32_t acc[AG_STRIDE];
+        for (int f = 0; f < AG_STRIDE; f++) acc[f] = 0;
+        for (uint32_t tile = t_lo; tile < t_hi; tile++) {
+            uint32_t ag[AG_STRIDE];
+            if (tile < S.node_tiles) classify_node_tile(S, tile, ag);
+            else classify_pod_tile(S, tile - S.node_tiles, ag);
+            for (int f = 0; f < AG_STRIDE; f++) acc[f] += ag[f];
+            if (t == 0)
+                for (int f = 0; f < AG_NSCAN; f++) sh_tagg[tile - t_lo][f] = ag[f];
+            if (S.world > 1 && t == 0) {  // the BACK launch re-reads the tile records
+                uint4* o = reinterpret_cast<uint4*>(S.tiles + (size_t)tile * AG_STRIDE);
+                for (int i = 0; i < AG_STRIDE / 4; i++) o[i] = make_uint4(ag[4 * i], ag[4 * i + 1], ag[4 * i + 2], ag[4 * i + 3]);
+            }
+        }
+        if (t == 0) {
+            uint4* o = reinterpret_cast<uint4*>(S.blockagg + (size_t)b * AG_STRIDE);
+            for (int i = 0; i < AG_STRIDE / 4; i++) o[i] = make_uint4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+        TSTAMP(5);
+        if (!hb_first) hb_fill_share(S, hb_tmpl4, n_hb);
+        if (t == 0) {
+            const uint64_t c = __builtin_amdgcn_s_memrealtime();
+            if (b == 0) H->clk[CLK_P1] = c;
+            if (phases & TICK_PROF) atomicMax(&S.bar->p1_max, (unsigned long long)c);
+        }
+        TSTAMP(1);
+        grid_barrier(S.bar, S.hdr_host);
+        TSTAMP(2);
+        if (b == 0 && t == 0) H->clk[CLK_BAR] = __builtin_amdgcn_s_memrealtime();
+    } else if (t < AG_NSCAN) {  // BACK launch: own tiles' records from the FRONT launch
+        for (uint32_t tile = t_lo; tile < t_hi; tile++) sh_tagg[tile - t_lo][t] = S.tiles[(size_t)tile * AG_STRIDE + t];
+    }
+
+    // ---- phase 2: prefix of the blocks before this one, totals ---------------------
+    // every block: prefix of the scanned fields + alloc / rel totals; block 0: all totals
+    uint64_t red[AG_NSCAN + AG_COUNT];  // [0, NSCAN): prefix; then totals
+    for (int f = 0; f < AG_NSCAN + AG_COUNT; f++) red[f] = 0;
+    for (uint32_t j = t; j < G; j += BLOCK) {
+        const uint4* r = reinterpret_cast<const uint4*>(S.blockagg + (size_t)j * AG_STRIDE);
+        const uint4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3];
+        const uint32_t a[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+        for (int f = 0; f < AG_NSCAN; f++) red[f] += j < b ? a[f] : 0u;
+#pragma unroll
+        for (int f = 0; f < AG_COUNT; f++) red[AG_NSCAN + f] += a[f];
+    }
+    block_sum64<AG_NSCAN + AG_COUNT>(red);
+    const uint64_t* pre = red;
+    const uint64_t* tot = red + AG_NSCAN;
+    const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+    if (b == 0 && t == 0) {
+        if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
+            __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (phases & TICK_FRONT) {
+            H->n_hb = (uint32_t)tot[AG_HB];
+            H->n_init = (uint32_t)tot[AG_INIT];
+            H->init_bytes = tot[AG_INIT_BYTES];
+            H->n_del = (uint32_t)tot[AG_DEL];
+            H->n_pp = (uint32_t)tot[AG_PP];
+            H->pp_bytes = tot[AG_BYTES] - tot[AG_INIT_BYTES];
+            H->n_alloc_local = (uint32_t)tot[AG_ALLOC];
+            H->n_lock = (uint32_t)tot[AG_LOCK];
+            H->n_eval = (uint32_t)tot[AG_EVAL];
+            H->n_rel = (uint32_t)tot[AG_REL];
+            H->n_use = S.world > 1 ? S.list_counts[0] : 0;
+            H->hb_base = 0;
+            H->init_base = patch_base;
+            H->pod_base = patch_base + tot[AG_INIT_BYTES];
+            H->arena_bytes = patch_base + tot[AG_BYTES];
+            H->overflow = H->arena_bytes > S.arena_cap;
+            uint64_t* C = H->local_counters;
+            C[0] = tot[AG_HB];        // heartbeat
+            C[1] = tot[AG_INIT];      // node_init
+            C[2] = tot[AG_PP];        // pod_patch
+            C[3] = tot[AG_DEL];       // delete
+            C[4] = tot[AG_ALLOC];     // alloc
+            C[5] = tot[AG_REL];       // release
+            C[6] = tot[AG_EVAL];      // evaluated
+            C[7] = tot[AG_LOCK];      // lock_checked
+            C[8] = tot[AG_MANAGED];   // nodes_managed
+            C[9] = tot[AG_READY];     // nodes_ready
+            C[10] = tot[AG_TOTAL];    // pods_total
+            C[11] = tot[AG_PENDING];  // pods_pending
+            C[12] = tot[AG_RUNNING];  // pods_running
+            for (int k = 13; k < 16; k++) C[k] = 0;
+            if (S.world == 1) {
+                for (int k = 0; k < 16; k++) H->counters[k] = C[k];
+                H->alloc_total = tot[AG_ALLOC];
+                H->alloc_base = 0;
+                H->rel_total = tot[AG_REL];
+            } else {
+                XMsg* X = S.xmsg;
+                X->alloc = tot[AG_ALLOC];
+                X->n_use = S.list_counts[0];
+                X->n_rel = S.list_counts[1];
+                for (int k = 0; k < 16; k++) X->counters[k] = C[k];
+            }
+            H->clk[CLK_BASES] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    if (b == 0 && S.world > 1 && (phases & TICK_FRONT)) {  // exchange lists inline when they fit
+        const uint32_t nu = S.list_counts[0], nr = S.list_counts[1];
+        if (nu + nr <= (uint32_t)XINLINE) {
+            for (uint32_t i = t; i < nu; i += BLOCK) S.xmsg->ips[i] = S.use_list[i];
+            for (uint32_t i = t; i < nr; i += BLOCK) S.xmsg->ips[nu + i] = S.rel_list[i];
+        }
+    }
+    TSTAMP(3);
+    if (!(phases & TICK_BACK)) return;
+
+    // ---- phase 3: ipPool (only in ticks with Gets or Puts) ---------------------
+    uint64_t A, rel_total, alloc_base, n_alloc_local;
+    if (phases & TICK_FRONT) {  // same launch: the totals are this tick's
+        A = tot[AG_ALLOC];
+        rel_total = tot[AG_REL];
+        alloc_base = 0;
+        n_alloc_local = tot[AG_ALLOC];
+    } else {  // after the exchange: fleet totals from k_xreduce
+        A = H->alloc_total;
+        rel_total = H->rel_total;
+        alloc_base = H->alloc_base;
+        n_alloc_local = H->n_alloc_local;
+    }
+    if (b == 0 && t == 0) H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
+    PoolPlan plan{};
+    if (A || rel_total) {
+        const uint32_t nwb = (uint32_t)((S.pool.words + POOL_WPB - 1) / POOL_WPB);
+        for (uint32_t wb = b; wb < nwb; wb += G) pool_prep_wblock(S, wb, rel_total != 0, A != 0);
+        grid_barrier(S.bar, S.hdr_host);
+        if (A) {
+            uint64_t cursor = ~0ull;
+            for (uint32_t wb = b; wb < nwb; wb += G) {
+                uint64_t bu, bf;
+                plan = pool_plan(S, A, nwb, wb, &bu, &bf);
+                pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor);
+            }
+            if (b >= nwb) {
+                uint64_t bu, bf;
+                plan = pool_plan(S, A, nwb, 0, &bu, &bf);
+            }
+            // ipPool.index after the last fresh address (committed after the barrier)
+            if (cursor != ~0ull) H->cursor_index = cursor;
+            if (b == 0 && t == 0) {
+                H->usable_total = plan.U;
+                H->take_usable = plan.take;
+                H->fresh_in = plan.fin;
+                H->fresh_out_start = plan.fout0;
+                if (plan.fout) H->cursor_index = plan.fout0 + plan.fout - S.pool.base;
+                else if (plan.fin == 0) H->cursor_index = *S.pool_index;
+            }
+            grid_barrier(S.bar, S.hdr_host);
+        }
+    }
+
+    // ---- phase 4: emission ------------------------------------------------------
+    if (t == 0) {
+        sh_L.patch_base = patch_base;
+        sh_L.alloc_base = alloc_base;
+        sh_L.plan = plan;
+    }
+    if (b == 0) {
+        // the header is final here (bases, pool plan and cursor: all written before
+        // the last grid barrier, or by this block): commit the cursor, reset the
+        // exchange lists, and publish the header zero-copy.  Every other block has
+        // read pool_index and list_counts before that barrier.
+        if (t == 0) {
+            H->clk[CLK_POOL] = __builtin_amdgcn_s_memrealtime();
+            if ((phases & TICK_PROF) && (phases & TICK_FRONT)) {  // every block stamped before the barrier
+                H->clk[CLK_ENTRY_MIN] = ~S.bar->neg_entry_max;
+                H->clk[CLK_P1_MAX] = S.bar->p1_max;
+                S.bar->neg_entry_max = 0;
+                S.bar->p1_max = 0;
+            }
+            if (A) *S.pool_index = H->cursor_index;
+            S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
+            S.list_counts[1] = 0;
+        }
+        __syncthreads();
+        if (t < 64) {
+            const uint64_t* src = reinterpret_cast<const uint64_t*>(H);
+            uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
+            for (int i = t; i < (int)(offsetof(TickHdr, err) / 8); i += 64) dst[i] = src[i];
+            __threadfence_system();
+        }
+    }
+    __syncthreads();
+    TSTAMP(4);
+    const Layout L = sh_L;
+    Bases run;
+    for (int f = 0; f < AG_NSCAN; f++) run.v[f] = pre[f];
+    for (uint32_t tile = t_lo; tile < t_hi; tile++) {
+        if (tile < S.node_tiles) emit_node_tile(S, tile, run, L, hb_tmpl, jobs.node);
+        else emit_pod_tile(S, tile - S.node_tiles, run, L, jobs.pod);
+        for (int f = 0; f < AG_NSCAN; f++) run.v[f] += sh_tagg[tile - t_lo][f];
+    }
+    TSTAMP(6);
+#undef TSTAMP
+}
+
+// ---------------------------------------------------------------------------
+// k_xreduce (multi-rank): fold the gathered exchange headers
+// ---------------------------------------------------------------------------
+__global__ void k_xreduce(DevState S, const XMsg* all, int world_size, int rank) {
+    if (threadIdx.x != 0) return;
+    TickHdr* H = S.hdr;
+    uint64_t tot = 0, base = 0, rel = 0;
+    for (int k = 0; k < 16; k++) H->counters[k] = 0;
+    for (int r = 0; r < world_size; r++) {
+        if (r < rank) base += all[r].alloc;
+        tot += all[r].alloc;
+        rel += all[r].n_rel;
+        for (int k = 0; k < 16; k++) H->counters[k] += all[r].counters[k];
+    }
+    H->alloc_total = tot;
+    H->alloc_base = base;
+    H->rel_total = rel;
+}
+
+// ingest-time Put (a Deleted watch event), applied immediately
+__global__ void k_pool_puts_now(DevState S, const uint32_t* ips, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t ip = ips[i];
+        if (!in_cidr(S.pool, ip)) continue;
+        uint64_t b = ip - S.pool.net;
+        atomicAnd((unsigned long long*)&S.used_bm[b >> 6], ~(1ull << (b & 63)));
+        atomicOr((unsigned long long*)&S.usable_bm[b >> 6], 1ull << (b & 63));
+    }
+}
+// multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm
+__global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
+    for (int r = 0; r < nranks; r++) {
+        const ListDesc d = ld[r];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_use + d.n_rel; i += gridDim.x * blockDim.x) {
+            bool use = i < d.n_use;
+            uint32_t ip = use ? d.use[i] : d.rel[i - d.n_use];
+            if (!in_cidr(S.pool, ip)) continue;
+            uint64_t b = ip - S.pool.net;
+            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
+        }
+    }
+}
+
 __global__ void k_apply_node_ops(DevState S, const NodeOp* ops, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1041,32 +1244,20 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
-void launch_tick_front(const DevState& S, uint64_t start, int world, hipStream_t st) {
-    hipLaunchKernelGGL(k_classify, dim3(S.node_tiles + S.pod_tiles), dim3(BLOCK), 0, st, S);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, st, S, start, world);
-}
-
 void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st) {
     hipLaunchKernelGGL(k_xreduce, dim3(1), dim3(64), 0, st, S, all, world, rank);
 }
 
-void launch_pool_alloc(const DevState& S, hipStream_t st) {
-    uint32_t nblk = cdiv(S.pool.words, POOL_WPB);
-    hipLaunchKernelGGL(k_pool_prep, dim3(nblk), dim3(BLOCK), 0, st, S);
-    hipLaunchKernelGGL(k_pool_select, dim3(nblk), dim3(BLOCK), 0, st, S, nblk);
+void launch_tick(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
+                 hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+    if (t0) hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases);
+    else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases);
 }
 
-void launch_emit_nodes(const DevState& S, hipStream_t st) {
-    hipLaunchKernelGGL(k_emit_nodes, dim3(S.node_tiles), dim3(BLOCK), 0, st, S);
-}
-
-void launch_emit_pods(const DevState& S, hipStream_t st) {
-    hipLaunchKernelGGL(k_emit_pods, dim3(S.pod_tiles), dim3(BLOCK), 0, st, S);
-}
-
-void launch_hb_fill(const DevState& S, uint32_t grid, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
-    if (t0) hipExtLaunchKernelGGL(k_hb_fill, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S);  // kernel-exact timing
-    else hipLaunchKernelGGL(k_hb_fill, dim3(grid), dim3(BLOCK), 0, st, S);
+int tick_occupancy() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tick, BLOCK, 0) != hipSuccess) return 0;
+    return n;
 }
 
 }  // namespace kwok

@@ -77,6 +77,7 @@ def declare(lib, pre):
             "rank_of_bucket": (I32, [U32, U32, I32]),
             "profile_enable": (C.c_int, [VP, C.c_int]),
             "profile_read": (C.c_int, [VP, VP, VP]),
+            "profile_host": (C.c_int, [VP, C.c_int, VP, VP]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name)
@@ -269,16 +270,23 @@ class Engine(EngineBase):
     def __init__(self, cfg=None, **kw):
         super().__init__(load_engine_lib(), cfg if cfg is not None else make_config(**kw))
 
-    PHASES = ("front", "pool", "emit", "hb_fill")
+    PHASES = ("classify", "barrier", "bases", "exchange", "pool", "emit", "kernel")  # KWOK_T_* order
+    HOST = ("enqueue", "wait", "post", "total")  # KWOK_H_* order
 
     def profile_enable(self, on=True):
         self._check(self._lib.kwok_profile_enable(self._h, 1 if on else 0), "profile_enable")
 
     def profile_read(self):
-        ms = (C.c_double * 4)()
+        ms = (C.c_double * len(self.PHASES))()
         n = C.c_uint64()
         self._check(self._lib.kwok_profile_read(self._h, ms, C.byref(n)), "profile_read")
         return dict(zip(self.PHASES, list(ms))), n.value
+
+    def profile_host(self, reset=False):
+        ms = (C.c_double * len(self.HOST))()
+        n = C.c_uint64()
+        self._check(self._lib.kwok_profile_host(self._h, 1 if reset else 0, ms, C.byref(n)), "profile_host")
+        return dict(zip(self.HOST, list(ms))), n.value
 
     def device_outputs(self):
         v = abi.DeviceView()

@@ -42,7 +42,7 @@ def test_oracle_library_exports():
         if f in ("kwok_engine_create", "kwok_engine_destroy"):
             name = name.replace("engine_", "")
         if f in ("kwok_abi_version", "kwok_comm_id", "kwok_finalizer_patch", "kwok_device_outputs",
-                 "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read"):
+                 "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host"):
             continue
         assert hasattr(lib, name), name
 
@@ -108,3 +108,16 @@ def test_create_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(engine.KwokError):
         engine.Engine(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8)
+
+
+def test_profile_enums_match_python_mirrors():
+    """The diagnostic buffers Engine passes are sized from these tuples: they
+    must list exactly the KWOK_T_* / KWOK_H_* entries of the header, in order."""
+    from kwok_amd.engine import Engine
+    hdr = open(os.path.join(ROOT, "include", "kwok_engine.h")).read()
+    for prefix, names in (("KWOK_T_", Engine.PHASES), ("KWOK_H_", Engine.HOST)):
+        body = re.search(r"enum\s*\{\s*(%s\w+[^}]*)\}" % prefix, hdr).group(1)
+        ents = [re.sub(r"\s*=.*", "", x).strip() for x in re.sub(r"/\*.*?\*/", "", body).split(",")]
+        ents = [x for x in ents if x]
+        assert ents[-1] == prefix + "COUNT"
+        assert [x[len(prefix):].lower() for x in ents[:-1]] == list(names)

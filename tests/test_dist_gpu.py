@@ -20,7 +20,8 @@ def _worker(rank, world, port, outdir):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # two engines share one GPU: each persistent tick grid must fit beside the other
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KWOK_TICK_BLOCKS_PER_CU="1")
     import torch.distributed as dist
     import dist_common as dc2
     from kwok_amd.engine import Engine
