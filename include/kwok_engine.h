@@ -266,12 +266,13 @@ int kwok_device_outputs(kwok_engine* e, kwok_device_view* view);
 
 /* Diagnostics: device time per tick (enable resets the accumulators).
  * KERNEL is the tick kernel's launch duration(s) from HIP events; the phase
- * split comes from the kernel's own clock stamps: CLASSIFY = first block start
- * to last block done classifying, BARRIER = from there until the grid barrier
- * releases, BASES = output bases / header, EXCHANGE = between the two launches
- * of a multi-rank tick (allgather + pool apply), POOL = ipPool phase, EMIT =
- * the rest of the launch (patch bytes, lists, heartbeat stream). */
-enum { KWOK_T_CLASSIFY = 0, KWOK_T_BARRIER, KWOK_T_BASES, KWOK_T_EXCHANGE, KWOK_T_POOL, KWOK_T_EMIT,
+ * split comes from the kernel's own clock stamps: CLASSIFY = first chain block
+ * start to the last chain block's arrival, STREAM = first chain block start to
+ * the last heartbeat streamer's exit, HEADER = the last arriver's reduction and
+ * header publication, EXCHANGE = between the two launches of a multi-rank tick
+ * (allgather + pool apply), POOL = ipPool phase (ticks with Gets / Puts),
+ * EMIT = the rest of the launch beyond the longer of chain and stream. */
+enum { KWOK_T_CLASSIFY = 0, KWOK_T_STREAM, KWOK_T_HEADER, KWOK_T_EXCHANGE, KWOK_T_POOL, KWOK_T_EMIT,
        KWOK_T_KERNEL, KWOK_T_COUNT };
 int kwok_profile_enable(kwok_engine* e, int on);
 int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* ticks);

@@ -30,12 +30,20 @@ constexpr int PS_PHASE_SHIFT = 8;
 constexpr uint16_t PS_PHASE_MASK = 7u << PS_PHASE_SHIFT;
 constexpr uint32_t PHASE_PENDING = 1, PHASE_RUNNING = 2;
 
-// ---- tile geometry -----------------------------------------------------------
+// ---- k_tick geometry ----------------------------------------------------------
+// Chain block b owns the contiguous bucket range [nb*b/Gc, nb*(b+1)/Gc) of the
+// rank: its node slots and its live pod slots (each bucket's pods below the
+// host-maintained fill mark, in 8-slot groups).  Node chunk = 1024 node slots,
+// pod chunk = 256 live groups (2048 pod slots); emission works chunk by chunk.
 constexpr int BLOCK = 256;          // 4 waves of 64
-constexpr int NODE_PER_THREAD = 4;  // node tile = 1024 slots
-constexpr int POD_PER_THREAD = 8;   // pod tile  = 2048 slots
-constexpr int NODE_TILE = BLOCK * NODE_PER_THREAD;
-constexpr int POD_TILE = BLOCK * POD_PER_THREAD;
+constexpr int NODE_PER_THREAD = 4;
+constexpr int POD_PER_THREAD = 8;   // one 8-slot group per thread per chunk
+constexpr int NODE_CHUNK = BLOCK * NODE_PER_THREAD;
+constexpr int POD_CHUNK = BLOCK * POD_PER_THREAD;
+constexpr int MAX_BPB = 64;               // buckets per chain block
+constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS node flags)
+constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
+constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
 
 // ---- fixed template geometry (default templates) -----------------------------
 constexpr int HB_LEN = 1059;     // {"status":{"conditions":[5 conditions]}} with 20-byte T/S
@@ -45,14 +53,13 @@ constexpr int CONDS_LEN = HB_LEN - HB_PREFIX - 2;  // the conditions list "[...]
 constexpr int TS_LEN = 20;       // RFC3339 UTC "YYYY-MM-DDTHH:MM:SSZ"
 constexpr int HB_NSLOTS = 10;    // 5 x (lastHeartbeatTime, lastTransitionTime)
 
-// per-tile and per-block aggregates of the classify phase.  The first
-// AG_NSCAN fields are exclusive-scanned into output ordinals / offsets (BYTES:
-// node-init bytes for node tiles, pod-patch bytes for pod tiles; node tiles
-// precede pod tiles, so one scan lays out [inits | pod patches]); the rest are
-// only summed.
+// per-chain-block record of the classify phase (16 x u32, one 64-byte line).
+// The first AG_NSCAN fields are exclusive-scanned over blocks into output
+// ordinals / byte offsets; the rest are only summed.  DIRTY = 1 when the block
+// has anything to emit or a state word to rewrite (else it skips emission).
 enum AggField {
-    AG_HB = 0, AG_INIT, AG_DEL, AG_PP, AG_BYTES, AG_ALLOC,                  // scanned
-    AG_INIT_BYTES, AG_LOCK, AG_MANAGED, AG_READY, AG_EVAL, AG_TOTAL, AG_PENDING, AG_RUNNING, AG_REL,
+    AG_INIT = 0, AG_INIT_BYTES, AG_DEL, AG_PP, AG_PP_BYTES, AG_ALLOC,  // scanned
+    AG_HB, AG_LOCK, AG_MANAGED, AG_READY, AG_EVAL, AG_TOTAL, AG_PENDING, AG_RUNNING, AG_REL, AG_DIRTY,
     AG_COUNT
 };
 constexpr int AG_NSCAN = 6;
@@ -72,31 +79,33 @@ struct TickHdr {
     uint64_t alloc_total, alloc_base, usable_total, take_usable, fresh_in, fresh_out_start;
     uint64_t cursor_index;       // ipPool.index after the tick
     uint64_t rel_total;          // releases this tick, all ranks (pending in rel_bm)
-    // s_memrealtime (100 MHz) stamps, CLK_* (block 0; the last two only in profiled ticks)
+    // s_memrealtime (100 MHz) stamps, CLK_*
     uint64_t clk[8];
-    // host-visible only (not published): TICK_ERR_* set by a timed-out grid barrier
+    // host-visible only (not published): TICK_ERR_* set by a timed-out wait
     uint32_t err, pad2;
 };
 
-constexpr uint32_t TICK_ERR_BARRIER = 1;  // a grid barrier timed out
+constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
 constexpr uint32_t TICK_ERR_LAYOUT = 2;   // device heartbeat count != the host's managed-node count
 enum : int {
-    CLK_ENTRY = 0,   // block 0 starts the FRONT phases
-    CLK_P1,          // block 0 done classifying
-    CLK_BAR,         // block 0 leaves the first grid barrier
-    CLK_BASES,       // block 0 done with bases / header
-    CLK_BACK,        // block 0 starts the BACK phases
-    CLK_POOL,        // block 0 done with the pool phase (emission starts)
-    CLK_ENTRY_MIN,   // earliest block start          (profiled ticks)
-    CLK_P1_MAX,      // latest block done classifying (profiled ticks)
+    CLK_ENTRY = 0,   // block 0 starts the tick (FRONT launch)
+    CLK_P1_MAX,      // the last chain block arrives (classification complete)
+    CLK_HDR,         // the last arriver has published the header / exchange message
+    CLK_BACK,        // BACK phases start (multi-rank: BACK launch, block 0)
+    CLK_POOL,        // pool phase done (pool leader)
+    CLK_ENTRY_MIN,   // earliest chain block start       (profiled ticks)
+    CLK_STREAM_END,  // latest heartbeat streamer exit   (profiled ticks, read by the host)
+    CLK_RSVD,
 };
 
-// grid-barrier state of the persistent tick kernel (device memory, zeroed once):
-// generation, top counter and 8 group counters, each on its own 128-byte line
-constexpr int BAR_LINE = 32, BAR_GEN = 0, BAR_TOP = BAR_LINE, BAR_GRP = 2 * BAR_LINE;
+// cross-block state of the tick kernel (device memory, zeroed at create and
+// after a failed tick), every word on its own 128-byte line
 struct GridBar {
-    uint32_t w[(2 + 8) * BAR_LINE];
-    unsigned long long neg_entry_max, p1_max;  // profiled ticks: max(~entry), max(phase-1 end)
+    unsigned long long arrive;  // monotonic: one add per chain block per FRONT launch
+    unsigned long long pad0[15];
+    uint32_t pcnt, pad1[31];    // pool-phase barrier: arrivals of the current instance
+    uint32_t pgen, pad2[31];    //                     generation
+    unsigned long long neg_entry_max, p1_max, stream_end_max, pad3[13];  // profiled ticks
 };
 
 // exchange message, one per rank (allgather)

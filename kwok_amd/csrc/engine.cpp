@@ -74,6 +74,10 @@ struct kwok_engine {
     std::unordered_map<std::string, uint32_t> node_by_name;  // -> local slot
     std::vector<uint64_t> node_bits;                 // occupancy bitset per bucket
     uint64_t n_managed = 0;
+    std::vector<uint32_t> mb_count;                  // [nb] managed nodes per owned bucket
+    bool hb_pre_dirty = true;                        // the per-chain-block heartbeat bases need an upload
+    uint32_t* hb_pre_h = nullptr;                    // pinned [n_chain + 1]
+    uint32_t* d_hb_pre = nullptr;
     std::vector<uint8_t> pod_used, pod_delpend;      // [PL]
     std::vector<uint16_t> pod_node;                  // [PL] local node index in bucket
     std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
@@ -115,8 +119,7 @@ struct kwok_engine {
     uint32_t* d_xsend = nullptr;
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
-    uint32_t tick_grid = 0;     // k_tick blocks: CUs x resident blocks per CU (all co-resident)
-    bool hb_first = false;      // KWOK_TICK_HB_FIRST=1: heartbeat stream before classification
+    uint32_t n_stream = 0;      // k_tick heartbeat streamer blocks (the chain blocks: S.n_chain)
     // diagnostics
     bool prof = false;
     hipEvent_t pev[4] = {};  // k_tick launch start/stop: FRONT(+BACK) launch, BACK launch
@@ -125,7 +128,7 @@ struct kwok_engine {
     double host_ms[KWOK_H_COUNT] = {};
     // KWOK_TICK_TRACE=1: per-block phase stamps, summarised on stderr at destroy
     std::vector<uint64_t> trace_h;
-    double trace_sum[8][3] = {};
+    double trace_sum[10][3] = {};  // chain stamps 0..7, streamer entry / exit
     uint64_t trace_ticks = 0, trace_seen = 0;
     uint64_t host_ticks = 0;
 
@@ -429,19 +432,26 @@ const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->trace_ticks) {
-        static const char* names[8] = {"entry", "p1-done", "barrier-out", "front-done",
-                                       "emit-start", "tiles-classified", "tiles-done", "reclassified"};
-        fprintf(stderr, "[kwok trace] grid %u, %llu ticks, us after first block start (min / median / max block)\n",
-                e->tick_grid, (unsigned long long)e->trace_ticks);
+        static const char* names[8] = {"entry", "nodes-done", "pods-done", "arrived",
+                                       "-", "pool-done", "exit", "-"};
+        fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
+                        "start (min / median / max block)\n",
+                e->S.n_chain, e->n_stream, (unsigned long long)e->trace_ticks);
         for (int k = 0; k < 8; k++)
-            fprintf(stderr, "[kwok trace] %-12s %8.2f %8.2f %8.2f\n", names[k], e->trace_sum[k][0] / e->trace_ticks,
-                    e->trace_sum[k][1] / e->trace_ticks, e->trace_sum[k][2] / e->trace_ticks);
+            if (names[k][0] != '-')
+                fprintf(stderr, "[kwok trace] chain    %-11s %8.2f %8.2f %8.2f\n", names[k],
+                        e->trace_sum[k][0] / e->trace_ticks, e->trace_sum[k][1] / e->trace_ticks,
+                        e->trace_sum[k][2] / e->trace_ticks);
+        for (int k = 0; k < 2; k++)
+            fprintf(stderr, "[kwok trace] streamer %-11s %8.2f %8.2f %8.2f\n", k ? "exit" : "entry",
+                    e->trace_sum[8 + k][0] / e->trace_ticks, e->trace_sum[8 + k][1] / e->trace_ticks,
+                    e->trace_sum[8 + k][2] / e->trace_ticks);
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.tiles, e->S.hdr, e->S.xmsg,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
                     e->S.use_list, e->S.rel_list, e->S.arena, e->S.hb_nodes, e->S.init_nodes, e->S.init_off,
                     e->S.init_len, e->S.pp_pods, e->S.pp_off, e->S.pp_len, e->S.del_pods, e->S.del_fin,
                     e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
@@ -449,6 +459,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (e->hdr_h) (void)hipHostFree(e->hdr_h);
+    if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->comm) ncclCommDestroy(e->comm);
@@ -515,23 +526,23 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         hipError_t r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "stream/event create: %s", hipGetErrorString(r)));
     }
+    DevState& S = e->S;
     {
-        // k_tick's grid: every block must be resident at once (grid barriers).
-        // Blocks per CU = min(occupancy, KWOK_TICK_BLOCKS_PER_CU or 2); lower it
-        // when several engines share one GPU (their grids must fit together).
-        int cus = 0, occ = tick_occupancy(), want = 2;
+        // k_tick's grid: chain blocks (KWOK_TICK_BLOCKS_PER_CU per CU, default 1)
+        // must be co-resident (dirty ticks wait on each other); streamer blocks
+        // (KWOK_TICK_STREAMERS_PER_CU, default 1) only stream and exit.  Lower
+        // both when several engines share one GPU (their grids must fit together).
+        int cus = 0, occ = tick_occupancy(), want = 1, wants = 1;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->dev);
         if (const char* v = getenv("KWOK_TICK_BLOCKS_PER_CU")) want = std::max(1, atoi(v));
+        if (const char* v = getenv("KWOK_TICK_STREAMERS_PER_CU")) wants = std::max(1, atoi(v));
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
-        e->tick_grid = (uint32_t)(cus * std::min(occ, want));
-        const char* hf = getenv("KWOK_TICK_HB_FIRST");
-        e->hb_first = hf && hf[0] == '1';
+        S.n_chain = (uint32_t)(cus * std::min(occ, want));
+        e->n_stream = (uint32_t)(cus * wants);
     }
-    DevState& S = e->S;
     S.n_node_slots = e->NL;
     S.n_pod_slots = e->PL;
-    S.node_tiles = (e->NL + NODE_TILE - 1) / NODE_TILE;
-    S.pod_tiles = (e->PL + POD_TILE - 1) / POD_TILE;
+    S.nb = e->nb;
     S.cn = e->Cn;
     S.cp = e->Cp;
     S.node_handle_base = (int32_t)(e->b_lo * e->Cn);
@@ -539,13 +550,19 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pool = e->pool;
     S.node_ip = e->node_ip;
     S.world = W;
-    const uint32_t T = S.node_tiles + S.pod_tiles;
-    if ((T + e->tick_grid - 1) / e->tick_grid > (uint32_t)MAX_TILES_PER_BLOCK)
-        return bail(e->fail(KWOK_EDOMAIN, "%u tiles exceed %u per k_tick block on %u blocks: shard over more GPUs", T,
-                            (unsigned)MAX_TILES_PER_BLOCK, e->tick_grid));
+    {
+        // a chain block's bucket range must fit its LDS node flags and 64 pod chunks
+        const uint32_t bpb = (e->nb + S.n_chain - 1) / S.n_chain;
+        if (bpb > (uint32_t)MAX_BPB || (uint64_t)bpb * e->Cn > (uint64_t)NODE_LDS ||
+            (uint64_t)bpb * (e->Cp / POD_PER_THREAD) > (uint64_t)MAX_POD_CHUNKS * BLOCK)
+            return bail(e->fail(KWOK_EDOMAIN,
+                                "%u buckets x (%u node, %u pod slots) per k_tick chain block exceed its limits "
+                                "(%d buckets, %d node slots, %d pod groups): shard over more GPUs",
+                                bpb, e->Cn, e->Cp, MAX_BPB, NODE_LDS, MAX_POD_CHUNKS * BLOCK));
+    }
     const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
-    // node/pod tiles round NL/PL up: allocate whole tiles so vector loads stay in bounds
-    const size_t NLa = (size_t)S.node_tiles * NODE_TILE, PLa = (size_t)S.pod_tiles * POD_TILE;
+    // node / pod arrays: whole 16-byte vectors at the end (Cn % 4 == 0, Cp % 8 == 0)
+    const size_t NLa = (size_t)e->NL + 16, PLa = (size_t)e->PL + 16;
     int rc = 0;
     if ((rc = dalloc(e, &S.node_state, NLa)) || (rc = dalloc(e, &S.node_blob, NLa)) ||
         (rc = dalloc(e, &S.node_tick, NLa)) || (rc = dalloc(e, &S.pod_state, PLa)) ||
@@ -555,11 +572,11 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.usable_bm, e->pool.words)) || (rc = dalloc(e, &S.rel_bm, e->pool.words)) ||
         (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &e->d_pod_fill, e->nb)) || (rc = dalloc(e, &S.pool_index, 1)) ||
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
-        (rc = dalloc(e, &S.blockagg, (size_t)e->tick_grid * AG_STRIDE)) ||
-        (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)e->tick_grid * 8))) ||
+        (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
+        (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
+        (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * 8))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) ||
-        (rc = dalloc(e, &S.tiles, (size_t)T * AG_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
         (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &S.hb_nodes, NLa)) ||
         (rc = dalloc(e, &S.init_nodes, NLa)) || (rc = dalloc(e, &S.init_off, NLa)) ||
@@ -581,8 +598,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
-    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipHostMallocDefault) != hipSuccess)
         return bail(KWOK_ENOMEM);
+    S.hb_pre = e->d_hb_pre;
     S.hdr_host = e->hdr_h;   // zero-copy: k_tick's last block publishes the header
     S.pod_fill = e->d_pod_fill;
     if (W > 1) {
@@ -599,6 +618,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     // host mirrors
     e->nodes.resize(e->NL);
     e->node_bits.assign((size_t)e->nb * ((e->Cn + 63) / 64), 0);
+    e->mb_count.assign(e->nb, 0);
     e->pod_used.assign(e->PL, 0);
     e->pod_delpend.assign(e->PL, 0);
     e->pod_node.assign(e->PL, 0);
@@ -682,7 +702,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
             st = node_slot(e, name, x.name.len, false, &slot);
             if (st == KWOK_OK) {
                 auto& hn = e->nodes[slot];
-                if (hn.managed) e->n_managed--;
+                if (hn.managed) e->n_managed--, e->mb_count[slot / e->Cn]--, e->hb_pre_dirty = true;
                 hn.exists = hn.managed = 0;
                 node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
                         false, 0);
@@ -716,7 +736,12 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 else {
                     auto& hn = e->nodes[slot];
                     hn.exists = 1;
-                    if (x.managed && !hn.managed) hn.managed = 1, e->n_managed++;  // never cleared but by Delete
+                    if (x.managed && !hn.managed) {  // never cleared but by Delete
+                        hn.managed = 1;
+                        e->n_managed++;
+                        e->mb_count[slot / e->Cn]++;
+                        e->hb_pre_dirty = true;
+                    }
                     hn.lockable = x.lockable ? 1 : 0;
                     bool ev_lock = x.managed && x.lockable;
                     uint8_t bits = (uint8_t)(NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
@@ -880,14 +905,26 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
     hipStream_t st = e->st;
     hipEvent_t* ev = e->prof ? e->pev : nullptr;
     const uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
-    const int order = e->hb_first ? TICK_HB_FIRST : 0;
+    if (e->hb_pre_dirty) {
+        // heartbeat handles are written in node order at per-chain-block bases:
+        // managed nodes of the buckets before each block's range (host-maintained)
+        uint32_t acc = 0, bk = 0;
+        for (uint32_t b = 0; b <= S.n_chain; b++) {
+            const uint32_t lo = (uint32_t)((uint64_t)e->nb * b / S.n_chain);
+            for (; bk < lo; bk++) acc += e->mb_count[bk];
+            e->hb_pre_h[b] = acc;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_hb_pre, e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipMemcpyHostToDevice, st));
+        e->hb_pre_dirty = false;
+    }
+    const int prof = ev ? TICK_PROF : 0;
     if (e->W == 1) {
-        launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | order | (ev ? TICK_PROF : 0), st, ev ? ev[0] : nullptr,
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, st, ev ? ev[0] : nullptr,
                     ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
         return KWOK_OK;
     }
-    launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_FRONT | order | (ev ? TICK_PROF : 0), st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
     // one allgather of the fixed-size exchange message; a second one for
     // lists that did not fit inline (sizes known after the first)
     int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
@@ -928,7 +965,7 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
     HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
     launch_xreduce(S, e->d_xall, e->W, e->rank, st);
     launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
-    launch_tick(S, e->tick_grid, now, (uint64_t)e->start, nhb, TICK_BACK, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
     HIPCHK(e, hipGetLastError());
     return KWOK_OK;
 }
@@ -938,20 +975,27 @@ static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr &
 
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
 static void trace_tick(kwok_engine* e) {
-    const size_t G = e->tick_grid;
+    const size_t G = e->S.n_chain, N = G + e->n_stream;
     if (++e->trace_seen <= 5) return;  // skip the initial (bulk) ticks
-    e->trace_h.resize(G * 8);
-    if (hipMemcpy(e->trace_h.data(), e->S.trace, G * 8 * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    e->trace_h.assign(N * 8, 0);
+    if (hipMemcpy(e->trace_h.data(), e->S.trace, N * 8 * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    (void)hipMemset(e->S.trace, 0, N * 8 * 8);
     uint64_t t0 = ~0ull;
     for (size_t b = 0; b < G; b++) t0 = std::min(t0, e->trace_h[b * 8]);
-    std::vector<double> v(G);
-    for (int k = 0; k < 8; k++) {
-        for (size_t b = 0; b < G; b++) v[b] = (double)(e->trace_h[b * 8 + k] - t0) * 0.01;
+    // stamps a block did not reach this tick (a clean block skips the pool phase) are 0
+    auto summarise = [&](size_t lo, size_t hi, int k, double* out) {
+        std::vector<double> v;
+        for (size_t b = lo; b < hi; b++)
+            if (e->trace_h[b * 8 + k] >= t0) v.push_back((double)(e->trace_h[b * 8 + k] - t0) * 0.01);
+        if (v.empty()) return;
         std::sort(v.begin(), v.end());
-        e->trace_sum[k][0] += v[0];
-        e->trace_sum[k][1] += v[G / 2];
-        e->trace_sum[k][2] += v[G - 1];
-    }
+        out[0] += v[0];
+        out[1] += v[v.size() / 2];
+        out[2] += v[v.size() - 1];
+    };
+    for (int k = 0; k < 8; k++) summarise(0, G, k, e->trace_sum[k]);
+    summarise(G, N, 0, e->trace_sum[8]);
+    summarise(G, N, 6, e->trace_sum[9]);
     e->trace_ticks++;
 }
 
@@ -973,8 +1017,10 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
     if (H.err) {
         const uint32_t err = H.err;
         e->hdr_h->err = 0;
+        (void)hipMemset(e->S.bar, 0, sizeof(GridBar));  // the next tick starts from a clean count
         if (err & TICK_ERR_BARRIER)
-            return e->fail(KWOK_EDEVICE, "k_tick grid barrier timed out (grid %u not co-resident?)", e->tick_grid);
+            return e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
+                           e->S.n_chain);
         return e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
                        (unsigned long long)e->n_managed);
     }
@@ -986,15 +1032,20 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         if (e->W > 1) (void)hipEventElapsedTime(&k1, e->pev[2], e->pev[3]);
         const double kern = (double)k0 + k1;
         auto span = [&](int a, int b) { return H.clk[b] > H.clk[a] ? (double)(H.clk[b] - H.clk[a]) * 1e-5 : 0.0; };
-        const double classify = span(CLK_ENTRY_MIN, CLK_P1_MAX), barrier = span(CLK_P1_MAX, CLK_BAR);
-        const double bases = span(CLK_BAR, CLK_BASES), pool = span(CLK_BACK, CLK_POOL);
+        // the streamers' latest exit, kept on the device (they never touch the header)
+        unsigned long long send = 0;
+        (void)hipMemcpy(&send, &e->S.bar->stream_end_max, 8, hipMemcpyDeviceToHost);
+        (void)hipMemset(&e->S.bar->stream_end_max, 0, 8);
+        e->hdr_h->clk[CLK_STREAM_END] = send;
+        const double classify = span(CLK_ENTRY_MIN, CLK_P1_MAX), stream = span(CLK_ENTRY_MIN, CLK_STREAM_END);
+        const double header = span(CLK_P1_MAX, CLK_HDR), pool = span(CLK_BACK, CLK_POOL);
         e->prof_ms[KWOK_T_CLASSIFY] += classify;
-        e->prof_ms[KWOK_T_BARRIER] += barrier;
-        e->prof_ms[KWOK_T_BASES] += bases;
-        e->prof_ms[KWOK_T_EXCHANGE] += e->W > 1 ? span(CLK_BASES, CLK_BACK) : 0.0;
+        e->prof_ms[KWOK_T_STREAM] += stream;
+        e->prof_ms[KWOK_T_HEADER] += header;
+        e->prof_ms[KWOK_T_EXCHANGE] += e->W > 1 ? span(CLK_HDR, CLK_BACK) : 0.0;
         e->prof_ms[KWOK_T_POOL] += pool;
-        // emission runs to the end of the launch
-        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, kern - classify - barrier - bases - pool);
+        // what follows the header in the chain (pool, emission), beyond the stream
+        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, kern - std::max(classify + header + pool, stream));
         e->prof_ms[KWOK_T_KERNEL] += kern;
         e->prof_ticks++;
     }

@@ -20,7 +20,7 @@ struct DevState {
     uint8_t* node_state;
     uint64_t* node_blob;
     uint8_t* node_tick;
-    uint32_t n_node_slots, node_tiles;
+    uint32_t n_node_slots;
     // pods (local slots)
     uint16_t* pod_state;
     uint16_t* pod_node;
@@ -28,8 +28,10 @@ struct DevState {
     uint32_t* pod_ctime;
     uint32_t* pod_ip;
     uint32_t* host_ip;
-    uint32_t n_pod_slots, pod_tiles;
+    uint32_t n_pod_slots;
     uint32_t cn, cp;
+    uint32_t nb;               // owned buckets
+    uint32_t n_chain;          // k_tick chain blocks (own bucket ranges); streamer blocks follow them
     int32_t node_handle_base, pod_handle_base;
     // pool replica
     uint64_t* used_bm;
@@ -48,7 +50,6 @@ struct DevState {
     const uint8_t* hb_static;
     const uint8_t* hb_kind;
     // per tick
-    uint32_t* tiles;           // [tiles][AG_STRIDE] per-tile aggregates (multi-rank BACK launch)
     TickHdr* hdr;
     XMsg* xmsg;
     uint32_t* use_list;      // multi-rank exchange lists
@@ -69,8 +70,10 @@ struct DevState {
     uint32_t node_ip;
     TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
     const uint16_t* pod_fill;  // per owned bucket: upper bound of used pod slots (host-maintained)
-    GridBar* bar;              // persistent-kernel barrier state
-    uint32_t* blockagg;        // [grid][AG_STRIDE] per-block aggregates of the classify phase
+    const uint32_t* hb_pre;    // [n_chain + 1] managed nodes before each chain block (host-maintained)
+    GridBar* bar;              // cross-block state
+    uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
+    uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
     uint64_t* trace;           // [grid][8] per-block phase stamps (KWOK_TICK_TRACE=1), else null
 };
 
@@ -80,10 +83,11 @@ void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hip
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
 
-// the persistent tick kernel; `grid` blocks must be co-resident (tick_occupancy)
-constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_HB_FIRST = 8;
-constexpr int MAX_TILES_PER_BLOCK = 32;
-void launch_tick(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
+// the tick kernel: n_chain chain blocks (+ n_stream heartbeat streamers in
+// launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
+// with work to emit, so they must be co-resident (tick_occupancy).
+constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4;
+void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
 

@@ -1,22 +1,23 @@
 // kernels.hip - gfx950 kernels of one kwok controller tick.
 //
-// A tick is a fixed pipeline of memory-bound sweeps over struct-of-arrays
-// state in HBM; nothing here is a dense contraction, so there is no MFMA.
-// The whole single-rank tick is ONE persistent launch (k_tick): per-tick
-// launch and inter-kernel gaps dominated the multi-kernel version (~70 us of
-// fixed cost per tick on MI355X), while the work itself is ~20 us of HBM
-// traffic.  Phases are separated by XCD-safe grid barriers.
+// A tick is a set of memory-bound sweeps over struct-of-arrays state in HBM;
+// nothing here is a dense contraction, so there is no MFMA.  The single-rank
+// tick is ONE launch (k_tick) of two kinds of blocks:
 //
-//   classify    node + pod predicates, per-tile counts, pool Use/Put bits
-//                 (node_controller.go:206-223,356-391; pod_controller.go:252-269,306-343,377-439)
-//   bases       per-block output bases from per-block aggregates (no scan kernel)
-//   pool        ipPool Put fold / plan / select+commit on replicated bitmaps
-//                 (utils.go:52-117), only in ticks with Gets or Puts
-//   emit        compaction of heartbeat / node-init / pod-patch / delete lists
-//               (wave ballots + block scans), byte emission (wave per patch),
-//               state transitions, and the heartbeat stream: n_managed
-//               identical 1059-byte patches from an LDS template with
-//               16-byte non-temporal stores (node_controller.go:145-204,393-401)
+//   chain blocks     one per bucket range: classify nodes and live pod groups
+//                    (node_controller.go:206-223,356-391; pod_controller.go:
+//                    252-269,306-343,377-439), heartbeat handle list, Use/Put
+//                    bits; publish a record and arrive.  Only blocks with
+//                    something to emit go on: prefix over the records, the
+//                    ipPool phase (utils.go:52-117) in ticks with Gets or Puts,
+//                    compaction + byte emission of their dirty chunks.
+//   streamer blocks  the n_managed identical 1059-byte heartbeat patches
+//                    (node_controller.go:145-204,393-401) from an LDS template
+//                    with 16-byte non-temporal stores, overlapping the
+//                    latency-bound classification.
+//
+// In the steady state no block waits on another: the last chain block to
+// arrive reduces the records into the tick header.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -105,18 +106,6 @@ __device__ __forceinline__ void block_sum(uint32_t (&v)[NF]) {
     block_excl_scan<NF>(v, tot);
 #pragma unroll
     for (int f = 0; f < NF; f++) v[f] = tot[f];
-}
-
-// append x to a device list with one atomic per wave
-__device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* list, uint32_t* counter) {
-    uint64_t m = __ballot(pred);
-    if (!m) return;
-    uint32_t base = 0;
-    const int l = lane_id();
-    int leader = __ffsll((unsigned long long)m) - 1;
-    if (l == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-    if (pred) list[base + __popcll(m & ((1ull << l) - 1))] = x;
 }
 
 __device__ __forceinline__ bool in_cidr(const PoolGeom& g, uint32_t ip) {
@@ -255,7 +244,7 @@ struct InitJob {
 };
 
 // one wave writes one pod patch: A [+ "hostIP":"H",] B [+ "podIP":"P",] C
-__device__ void write_pod_patch(const DevState& S, const PodJob& j, uint8_t* out) {
+__device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob& j, uint8_t* out) {
     const SpecDesc sd = S.specs[S.pod_spec[j.slot]];
     const Ts ts = format_ts(S.pod_ctime[j.slot]);
     const bool st = j.host_ip != 0;
@@ -307,7 +296,7 @@ __device__ void write_pod_patch(const DevState& S, const PodJob& j, uint8_t* out
 }
 
 // one wave writes one node init patch: {"status":{ pre ,"conditions": CONDS , post }}
-__device__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl, uint8_t* out) {
+__device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl, uint8_t* out) {
     const uint32_t boff = (uint32_t)blob, pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
     const uint32_t len = init_patch_len(blob);
     const uint8_t* bb = S.blob + boff;
@@ -333,206 +322,6 @@ __device__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t
         }
         *reinterpret_cast<uint32_t*>(out + q0) = w;
     }
-}
-
-// ---------------------------------------------------------------------------
-// grid barrier for the persistent tick kernel (MI355X_MICROARCH.md "Workgroup
-// dispatch ... inter-workgroup visibility" and the barrier-xcd price row;
-// cdna_hip_programming.md §6 G16).  Producer side: every wave drains its
-// stores, block barrier, lane-0 agent release + vmcnt(0).  Arrival is two-level
-// (8 group counters on their own lines, then one top counter) so no single
-// address takes 512 serialized atomics; all counters are monotonic (a group's
-// last arriver is the one whose count reaches a multiple of the group size), so
-// nothing is reset between barriers or ticks.  Consumers poll the generation
-// relaxed with s_sleep, then one agent acquire + vmcnt(0) + block barrier.
-// Spins are bounded (2 s of s_memrealtime): a timeout flags the tick as failed
-// in the host-visible header instead of hanging the GPU.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void grid_barrier(GridBar* bar, TickHdr* hdr_host) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t* w = bar->w;
-        const uint32_t G = gridDim.x, g = blockIdx.x & 7;
-        const uint32_t gsize = (G - g + 7) / 8, ngroups = G < 8 ? G : 8;
-        const uint32_t gen = __hip_atomic_load(&w[BAR_GEN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bool released = false;
-        const uint32_t ga =
-            __hip_atomic_fetch_add(&w[BAR_GRP + BAR_LINE * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-        if (ga % gsize == 0) {
-            const uint32_t ta = __hip_atomic_fetch_add(&w[BAR_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-            if (ta % ngroups == 0) {
-                __hip_atomic_fetch_add(&w[BAR_GEN], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                released = true;
-            }
-        }
-        if (!released) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(&w[BAR_GEN], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-                    __hip_atomic_store(&hdr_host->err, TICK_ERR_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// tile classification (phase 1): predicates A.4/A.5, per-tile counts,
-// in-place Use / pending Put bits (single rank) or exchange lists (multi rank).
-// Loads are issued in two independent rounds (state words, then node state +
-// pool word + spec ids) so a tile costs two HBM round trips, not four.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void classify_node_tile(const DevState& S, uint32_t tile, uint32_t (&ag)[AG_STRIDE]) {
-    const int t = threadIdx.x;
-    const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
-    uint32_t f[6] = {0, 0, 0, 0, 0, 0};  // hb, init, init_bytes, lock, managed, ready
-    uint32_t packed = 0;
-    if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
-    uint32_t tick = 0;
-#pragma unroll
-    for (int k = 0; k < NODE_PER_THREAD; k++) {
-        uint8_t s = (uint8_t)(packed >> (8 * k));
-        NodeCls c = classify_node(s);
-        f[0] += c.hb;
-        f[3] += c.lock;
-        f[4] += c.managed;
-        f[5] += c.ready;
-        if (c.init) {
-            f[1]++;
-            f[2] += (init_patch_len(S.node_blob[first + k]) + 15u) & ~15u;
-        }
-        tick |= (uint32_t)node_tick_flags(s) << (8 * k);
-    }
-    if (first < S.n_node_slots) *reinterpret_cast<uint32_t*>(S.node_tick + first) = tick;
-    block_sum<6>(f);
-    for (int i = 0; i < AG_STRIDE; i++) ag[i] = 0;
-    ag[AG_HB] = f[0];
-    ag[AG_INIT] = f[1];
-    ag[AG_BYTES] = f[2];
-    ag[AG_INIT_BYTES] = f[2];
-    ag[AG_LOCK] = f[3];
-    ag[AG_MANAGED] = f[4];
-    ag[AG_READY] = f[5];
-}
-
-// the first round of a pod tile: state, node index, podIP and spec id words of
-// this thread's 8 slots; slots at or above the bucket's fill mark read as empty
-struct PodQuad {
-    uint16_t st[POD_PER_THREAD], nl[POD_PER_THREAD];
-    uint32_t ip[POD_PER_THREAD];
-    bool live;
-};
-__device__ __forceinline__ void load_pod_quad(const DevState& S, uint32_t first, PodQuad& q) {
-    uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
-    uint32_t fill = 0;
-    if (first < S.n_pod_slots) {  // all five loads in flight together
-        fill = S.pod_fill[first / S.cp];
-        st4 = *reinterpret_cast<const uint4*>(S.pod_state + first);
-        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + first);
-        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + first);
-        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + first + 4);
-    }
-    q.live = first < S.n_pod_slots && (first % S.cp) < fill;
-    if (!q.live) st4 = make_uint4(0, 0, 0, 0);
-    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
-    const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
-    const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        q.st[k] = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
-        q.nl[k] = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
-        q.ip[k] = ips[k];
-    }
-}
-// could this pod need a patch (computePatchData), given it is evaluated?
-__device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
-    const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
-    return (st & PS_USED) && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ip == 0);
-}
-// spec ids of this thread's 8 slots, loaded only when one of them may need a patch
-__device__ __forceinline__ void load_spec_ids(const DevState& S, uint32_t first, const PodQuad& q, uint16_t (&sp)[8]) {
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(q.st[k], q.ip[k]);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (any) v = *reinterpret_cast<const uint4*>(S.pod_spec + first);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) sp[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
-}
-
-__device__ __forceinline__ void classify_pod_tile(const DevState& S, uint32_t ptile, uint32_t (&ag)[AG_STRIDE]) {
-    const int t = threadIdx.x;
-    const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    uint32_t f[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // del, eval, alloc, pp, pp_bytes, total, pending, running, rel
-    PodQuad q;
-    load_pod_quad(S, first, q);
-    const uint32_t bucket_local = first / S.cp;  // 8 slots never straddle a bucket (cp % 8 == 0)
-    // round 2: node state, the pool word of the podIP (speculative) and the spec ids
-    uint8_t ns[POD_PER_THREAD];
-    uint64_t uw[POD_PER_THREAD];
-    uint16_t sp[POD_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        ns[k] = (q.st[k] & PS_USED) ? S.node_state[bucket_local * S.cn + q.nl[k]] : 0;
-        const bool inc = (q.st[k] & PS_USED) && q.ip[k] && in_cidr(S.pool, q.ip[k]);
-        uw[k] = inc ? S.used_bm[(q.ip[k] - S.pool.net) >> 6] : ~0ull;
-    }
-    load_spec_ids(S, first, q, sp);
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint16_t st = q.st[k];
-        const uint32_t ip = q.ip[k];
-        const uint8_t ntf = node_tick_flags(ns[k]);
-        PodCls c = classify_pod(st, ntf, ip);
-        f[0] += c.del;
-        f[1] += c.eval;
-        f[2] += c.alloc;
-        const bool inc = ip && in_cidr(S.pool, ip);
-        const uint64_t bit = ip - S.pool.net;
-        // the Deleted event of a pod we delete: release if the node is managed and the IP in CIDR
-        bool rel = c.del && (ntf & NT_MANAGED) && inc;
-        // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
-        // addresses not already in `used` change the pool
-        bool use = c.eval && inc && !((uw[k] >> (bit & 63)) & 1);
-        if (S.world == 1) {
-            // single rank: Use() in place; the Put of a released address waits in rel_bm
-            // and is folded in the pool phase, after every Use of this tick (Use -> Put)
-            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
-            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
-        } else {
-            wave_append(rel, ip, S.rel_list, &S.list_counts[1]);
-            wave_append(use, ip, S.use_list, &S.list_counts[0]);
-        }
-        f[8] += rel;
-        if (c.need) {
-            f[3]++;
-            f[4] += S.specs[sp[k]].max_len;
-        }
-        bool total = c.used && !c.del;
-        f[5] += total;
-        f[6] += total && !c.need && c.phase == PHASE_PENDING;
-        f[7] += total && (c.need || c.phase == PHASE_RUNNING);
-    }
-    block_sum<9>(f);
-    for (int i = 0; i < AG_STRIDE; i++) ag[i] = 0;
-    ag[AG_DEL] = f[0];
-    ag[AG_EVAL] = f[1];
-    ag[AG_ALLOC] = f[2];
-    ag[AG_PP] = f[3];
-    ag[AG_BYTES] = f[4];
-    ag[AG_TOTAL] = f[5];
-    ag[AG_PENDING] = f[6];
-    ag[AG_RUNNING] = f[7];
-    ag[AG_REL] = f[8];
 }
 
 // ---------------------------------------------------------------------------
@@ -566,7 +355,7 @@ constexpr int POOL_WPT = 4;                  // bitmap words per thread
 constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per word-block
 
 // fold this tick's Puts, count usable / free bits of word-block wb
-__device__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count) {
+__device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count) {
     const uint64_t cb = cursor_bit(S);
     uint32_t f[2] = {0, 0};
     for (int k = 0; k < POOL_WPT; k++) {
@@ -597,7 +386,7 @@ struct PoolPlan {
     uint64_t U, Fin, take, fin, fout, fout0;
 };
 // every block derives the same plan from the per-word-block counts
-__device__ PoolPlan pool_plan(const DevState& S, uint64_t A, uint32_t nwb, uint32_t upto, uint64_t* bu, uint64_t* bf) {
+__device__ __forceinline__ PoolPlan pool_plan(const DevState& S, uint64_t A, uint32_t nwb, uint32_t upto, uint64_t* bu, uint64_t* bf) {
     __shared__ uint64_t sh[4];
     if (threadIdx.x < 64) {
         uint64_t u = 0, fr = 0, pu = 0, pf = 0;
@@ -636,7 +425,7 @@ __device__ PoolPlan pool_plan(const DevState& S, uint64_t A, uint32_t nwb, uint3
 //   otherwise           -> fout0 + (g - take - fin)          (beyond the CIDR)
 // Every rank commits ALL allocations to its replica; it records the addresses
 // of its own ordinals [alloc_base, alloc_base + n_alloc_local).
-__device__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
+__device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
                                    uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out) {
     const uint64_t take = p.take, fin = p.fin;
     const uint64_t cb = cursor_bit(S);
@@ -694,193 +483,113 @@ __device__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPla
 }
 
 // ---------------------------------------------------------------------------
-// emission: compaction of the output lists, byte emission, state transitions
+// cross-block hand-offs (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement
+// & inter-workgroup visibility", valid forms; cdna_hip_programming.md §6 G16)
+//
+//   * per-block records: stored write-through (sc1) by wave 0, drained with
+//     vmcnt(0), then ONE returning agent-scope add on ONE arrival counter.  The
+//     block whose add completes the tick's count (the "last arriver") and the
+//     blocks that poll the counter (sc1 loads) read the records with sc1 loads.
+//   * the pool phase (ticks with Gets or Puts) uses a sense-reversal barrier
+//     among its participants: release fence -> arrive -> poll -> acquire fence.
+// Every spin is bounded (2 s of s_memrealtime) and flags the tick as failed.
 // ---------------------------------------------------------------------------
-// a tile's exclusive prefix of the AG_NSCAN scanned fields (passed by value)
-struct Bases {
-    uint64_t v[AG_NSCAN];
-};
-struct Layout {
-    uint64_t patch_base;  // arena offset of [node inits | pod patches] (= n_hb x HB_STRIDE)
-    uint64_t alloc_base;  // this rank's first global allocation ordinal
-    PoolPlan plan;
-};
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st32_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld32_sc1(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint64_t SPIN_LIMIT = 200000000ull;  // 2 s at 100 MHz
 
-// base: this tile's exclusive prefix of the AG_NSCAN scanned fields
-__device__ __forceinline__ void emit_node_tile(const DevState& S, uint32_t tile, const Bases bs, const Layout& L,
-                                               const uint8_t* hb_tmpl, InitJob* ij) {
-    const uint64_t* base = bs.v;
-    const int t = threadIdx.x;
-    const uint32_t first = tile * NODE_TILE + t * NODE_PER_THREAD;
-    uint32_t packed = 0;
-    if (first < S.n_node_slots) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
-    NodeCls c[NODE_PER_THREAD];
-    uint32_t v[3] = {0, 0, 0};  // hb, init, init bytes
-    uint32_t ilen[NODE_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < NODE_PER_THREAD; k++) {
-        c[k] = classify_node((uint8_t)(packed >> (8 * k)));
-        v[0] += c[k].hb;
-        ilen[k] = 0;
-        if (c[k].init) {
-            ilen[k] = init_patch_len(S.node_blob[first + k]);
-            v[1]++;
-            v[2] += (ilen[k] + 15u) & ~15u;
-        }
-    }
-    uint32_t tot[3];
-    block_excl_scan<3>(v, tot);
-    uint32_t newpacked = 0;
-    uint32_t ji = v[1];
-    const uint64_t tile_bytes = L.patch_base + base[AG_BYTES];
-#pragma unroll
-    for (int k = 0; k < NODE_PER_THREAD; k++) {
-        const int32_t handle = S.node_handle_base + (int32_t)(first + k);
-        if (c[k].hb) S.hb_nodes[base[AG_HB] + v[0]++] = handle;  // PatchStatus(name, heartbeat body)
-        uint8_t s = (uint8_t)(packed >> (8 * k));
-        if (c[k].init) {
-            uint64_t ord = base[AG_INIT] + ji;
-            S.init_nodes[ord] = handle;
-            S.init_off[ord] = tile_bytes + v[2];
-            S.init_len[ord] = ilen[k];
-            ij[ji].slot = first + k;
-            ij[ji].off = v[2];
-            ji++;
-            v[2] += (ilen[k] + 15u) & ~15u;
-            s |= NS_CONFORMS;  // the apiserver applied the init patch
-        }
-        s &= (uint8_t)~NS_EVENT_LOCK;
-        newpacked |= (uint32_t)s << (8 * k);
-    }
-    if (first < S.n_node_slots && newpacked != packed)
-        *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
+// append x to a device list with one atomic per wave; entries are stored
+// write-through: the FRONT launch's last arriver reads them (multi-rank)
+__device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* list, uint32_t* counter) {
+    uint64_t m = __ballot(pred);
+    if (!m) return;
+    uint32_t base = 0;
+    const int l = lane_id();
+    int leader = __ffsll((unsigned long long)m) - 1;
+    if (l == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (pred) st32_sc1(&list[base + __popcll(m & ((1ull << l) - 1))], x);
+}
+
+// publish this block's record and arrive; returns the arrival counter before
+// this block's add (uniform).  Every wave drains its stores and atomics first,
+// so the Use / Put atomics of the classify phase are performed before the add.
+__device__ __forceinline__ uint64_t publish_and_arrive(const DevState& S, uint32_t b, const uint32_t (&rec)[AG_STRIDE]) {
+    __shared__ unsigned long long sh_old;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64)
-        write_init_patch(S, S.node_blob[ij[j].slot], hb_tmpl, S.arena + tile_bytes + ij[j].off);
+    if (threadIdx.x < 64) {
+        const int l = lane_id();
+        if (l < AG_STRIDE / 2) {
+            uint64_t v = 0;
+#pragma unroll
+            for (int i = 0; i < AG_STRIDE / 2; i++)
+                if (l == i) v = (uint64_t)rec[2 * i] | (uint64_t)rec[2 * i + 1] << 32;
+            st_sc1(reinterpret_cast<uint64_t*>(S.blockagg + (size_t)b * AG_STRIDE) + l, v);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (l == 0)
+            sh_old = __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return sh_old;
+}
+
+// poll the arrival counter (sc1) until every chain block of this tick arrived,
+// then acquire (the pool phase reads bitmaps other blocks changed)
+__device__ __forceinline__ void wait_arrivals(const DevState& S, uint64_t target) {
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_sc1(&S.bar->arrive) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT) {
+                __hip_atomic_store(&S.hdr_host->err, TICK_ERR_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
 }
 
-__device__ __forceinline__ void emit_pod_tile(const DevState& S, uint32_t ptile, const Bases bs, const Layout& L,
-                                              PodJob* jobs) {
-    const uint64_t* base = bs.v;
-    const int t = threadIdx.x;
-    const uint32_t first = ptile * POD_TILE + t * POD_PER_THREAD;
-    PodQuad q;
-    load_pod_quad(S, first, q);
-    const uint32_t bucket_local = first / S.cp;
-    uint8_t ntf[POD_PER_THREAD];
-    uint16_t sp[POD_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++)
-        ntf[k] = (q.st[k] & PS_USED) ? S.node_tick[bucket_local * S.cn + q.nl[k]] : 0;
-    load_spec_ids(S, first, q, sp);
-    PodCls c[POD_PER_THREAD];
-    uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        c[k] = classify_pod(q.st[k], ntf[k], q.ip[k]);
-        v[0] += c[k].del;
-        if (c[k].need) {
-            v[1]++;
-            v[2] += S.specs[sp[k]].max_len;
-        }
-        v[3] += c[k].alloc;
-    }
-    uint32_t tot[4];
-    block_excl_scan<4>(v, tot);
-    const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0, abase = L.alloc_base;
-    const uint64_t tile_bytes = L.patch_base + base[AG_BYTES];
-    uint32_t jl = v[1];
-    bool dirty = false;
-    uint16_t nst[POD_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint32_t slot = first + k;
-        const int32_t handle = S.pod_handle_base + (int32_t)slot;
-        uint16_t s = q.st[k];
-        if (c[k].del) {
-            uint64_t ord = base[AG_DEL] + v[0]++;
-            S.del_pods[ord] = handle;
-            S.del_fin[ord] = (s & PS_HAS_FIN) ? 1 : 0;
-            s = 0;  // DeletePod -> Delete(grace 0): the object is gone
-        }
-        if (c[k].eval) {
-            uint32_t pip = q.ip[k];
-            if (c[k].alloc) {
-                uint64_t o = base[AG_ALLOC] + v[3]++;
-                uint64_t g = abase + o;
-                pip = g < take + fin ? S.alloc_addr[o] : (uint32_t)(fout0 + (g - take - fin));
-            }
-            if (c[k].need) {
-                const bool stat = s & PS_STATUS_NONEMPTY;
-                uint32_t hip = 0;
-                if (stat) {
-                    hip = (s & PS_HAS_HOST_IP) ? S.host_ip[slot] : S.node_ip;
-                    if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
-                    if (pip != q.ip[k]) S.pod_ip[slot] = pip;
+// sense-reversal barrier among the n blocks of the pool phase
+__device__ __forceinline__ void pool_barrier(const DevState& S, uint32_t n) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        GridBar* bar = S.bar;
+        const uint32_t gen = __hip_atomic_load(&bar->pgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t a = __hip_atomic_fetch_add(&bar->pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (a == n) {
+            __hip_atomic_store(&bar->pcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&bar->pgen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(&bar->pgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT) {
+                    __hip_atomic_store(&S.hdr_host->err, TICK_ERR_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
                 }
-                uint64_t ord = base[AG_PP] + jl;
-                const SpecDesc& sd = S.specs[sp[k]];
-                uint32_t len = sd.len_a + sd.len_b + sd.len_c + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
-                S.pp_pods[ord] = handle;
-                S.pp_off[ord] = tile_bytes + v[2];
-                S.pp_len[ord] = len;
-                jobs[jl] = PodJob{slot, v[2], stat ? pip : 0u, hip};
-                jl++;
-                v[2] += sd.max_len;
-                // the apiserver applied the patch
-                s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
-                               PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
             }
-            s &= (uint16_t)~PS_EVENT;
         }
-        dirty |= s != q.st[k];  // steady-state re-checks leave the state word untouched
-        nst[k] = s;
-    }
-    if (q.live && dirty) {
-        uint4 o;
-        o.x = nst[0] | (uint32_t)nst[1] << 16;
-        o.y = nst[2] | (uint32_t)nst[3] << 16;
-        o.z = nst[4] | (uint32_t)nst[5] << 16;
-        o.w = nst[6] | (uint32_t)nst[7] << 16;
-        *reinterpret_cast<uint4*>(S.pod_state + first) = o;
-    }
-    __syncthreads();
-    uint8_t* out = S.arena + tile_bytes;
-    for (uint32_t j = wave_id(); j < tot[1]; j += BLOCK / 64) write_pod_patch(S, jobs[j], out + jobs[j].off);
-    __syncthreads();
-}
-
-// this block's share of the n_hb identical heartbeat patches: 67 x 16 B each,
-// non-temporal 16-byte stores from the LDS template (node_controller.go:145-157)
-constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
-__device__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t nchunks = n_hb * HB_CHUNKS;
-    const uint64_t lo = nchunks * blockIdx.x / gridDim.x, hi = nchunks * (blockIdx.x + 1) / gridDim.x;
-    u32x4* dst = reinterpret_cast<u32x4*>(S.arena);  // heartbeat region starts at arena offset 0
-    uint64_t i = lo + threadIdx.x;
-    uint32_t m = (uint32_t)(i % HB_CHUNKS);
-    constexpr uint32_t dm = BLOCK % HB_CHUNKS;
-    for (; i < hi; i += BLOCK) {
-        const uint4 v = tmpl[m];
-        u32x4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, &dst[i]);  // write-once stream: do not keep in L2
-        m += dm;
-        if (m >= HB_CHUNKS) m -= HB_CHUNKS;
-    }
-}
-
-// per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
-__device__ void build_hb_template(const DevState& S, uint8_t* tmpl, uint64_t now_unix, uint64_t start_unix) {
-    const Ts now = format_ts(now_unix), st = format_ts(start_unix);
-    for (int i = threadIdx.x; i < HB_STRIDE; i += BLOCK) {
-        const uint8_t k = S.hb_kind[i];
-        uint32_t b;
-        if (k == 0xFF) b = S.hb_static[i];
-        else if (k < TS_LEN) b = ts_byte(now, k);
-        else b = ts_byte(st, k - TS_LEN);
-        tmpl[i] = (uint8_t)b;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 }
@@ -905,202 +614,712 @@ __device__ __forceinline__ void block_sum64(uint64_t (&v)[N]) {
     __syncthreads();
 }
 
-// ---------------------------------------------------------------------------
-// k_tick: one controller tick as ONE persistent launch (single rank) or two
-// launches around the exchange (multi-rank: FRONT, then BACK).  Block b owns
-// the contiguous tile range [T*b/G, T*(b+1)/G) (node tiles, then pod tiles).
-//
-//   phase 1  heartbeat template (LDS); classify own tiles; this block's share
-//            of the heartbeat stream (its length n_hb is the host's managed-node
-//            count: the bandwidth-bound stream overlaps the latency-bound
-//            classification and the barrier wait); per-block aggregate
-//                                                              [grid barrier]
-//   phase 2  prefix / totals of the per-block aggregates (one parallel read);
-//            block 0: tick header / exchange message; n_hb checked
-//   phase 3  (only with Gets or Puts) fold Puts + count [barrier], plan +
-//            select + commit [barrier]
-//   phase 4  block 0 publishes the (final) header zero-copy; every block:
-//            emission of its node / pod tiles
-// ---------------------------------------------------------------------------
+// prefix over chain blocks < b and totals over all chain blocks of the records
+// (sc1 loads: the records may have been published in this launch)
+struct Sums {
+    uint64_t pre[AG_STRIDE], tot[AG_STRIDE];
+};
+__device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, Sums& r) {
+    uint64_t red[2 * AG_STRIDE];
+#pragma unroll
+    for (int f = 0; f < 2 * AG_STRIDE; f++) red[f] = 0;
+    for (uint32_t j = threadIdx.x; j < S.n_chain; j += BLOCK) {
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(S.blockagg + (size_t)j * AG_STRIDE);
+        uint64_t q[AG_STRIDE / 2];
+#pragma unroll
+        for (int i = 0; i < AG_STRIDE / 2; i++) q[i] = ld_sc1(p + i);
+#pragma unroll
+        for (int i = 0; i < AG_STRIDE / 2; i++) {
+            const uint32_t lo = (uint32_t)q[i], hi = (uint32_t)(q[i] >> 32);
+            red[2 * i] += j < b ? lo : 0u;
+            red[2 * i + 1] += j < b ? hi : 0u;
+            red[AG_STRIDE + 2 * i] += lo;
+            red[AG_STRIDE + 2 * i + 1] += hi;
+        }
+    }
+    block_sum64<2 * AG_STRIDE>(red);
+#pragma unroll
+    for (int f = 0; f < AG_STRIDE; f++) {
+        r.pre[f] = red[f];
+        r.tot[f] = red[AG_STRIDE + f];
+    }
+}
 
+// ---------------------------------------------------------------------------
+// chain-block geometry: the block's bucket range, its live pod groups
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void block_range(const DevState& S, uint32_t b, uint32_t& bk0, uint32_t& nbk) {
+    bk0 = (uint32_t)((uint64_t)S.nb * b / S.n_chain);
+    nbk = (uint32_t)((uint64_t)S.nb * (b + 1) / S.n_chain) - bk0;
+}
+// gpre[j] = live 8-slot pod groups of the block's buckets before j (fill marks
+// are multiples of 8).  Wave 0 only; the caller synchronises.
+__device__ __forceinline__ void load_gpre(const DevState& S, uint32_t bk0, uint32_t nbk, uint32_t* gpre) {
+    if (threadIdx.x < 64) {
+        const int l = lane_id();
+        const uint32_t g = l < (int)nbk ? (uint32_t)S.pod_fill[bk0 + l] >> 3 : 0u;
+        gpre[l + 1] = wave_incl_scan(g);
+        if (l == 0) gpre[0] = 0;
+    }
+}
+// largest j with gpre[j] <= gi (a bucket that has groups)
+__device__ __forceinline__ uint32_t find_bucket(const uint32_t* gpre, uint32_t nbk, uint32_t gi) {
+    uint32_t lo = 0, hi = nbk;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gpre[mid] <= gi) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// one 8-slot pod group: state, node index and podIP words (one HBM round trip)
+struct PodGrp {
+    uint32_t slot;  // first local slot; ~0u when the group index is past the block's groups
+    uint32_t j;     // bucket within the block
+    uint16_t st[POD_PER_THREAD], nl[POD_PER_THREAD];
+    uint32_t ip[POD_PER_THREAD];
+};
+__device__ __forceinline__ void load_group(const DevState& S, const uint32_t* gpre, uint32_t bk0, uint32_t nbk,
+                                           uint32_t ng, uint32_t gi, PodGrp& g) {
+    uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
+    g.slot = ~0u;
+    g.j = 0;
+    if (gi < ng) {
+        const uint32_t j = find_bucket(gpre, nbk, gi);
+        g.j = j;
+        g.slot = (bk0 + j) * S.cp + (gi - gpre[j]) * (uint32_t)POD_PER_THREAD;
+        st4 = *reinterpret_cast<const uint4*>(S.pod_state + g.slot);
+        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + g.slot);
+        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
+        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
+    }
+    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
+    const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
+    const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        g.st[k] = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
+        g.nl[k] = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
+        g.ip[k] = ips[k];
+    }
+}
+// could this pod need a patch (computePatchData), given it is evaluated?
+__device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
+    const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
+    return (st & PS_USED) && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ip == 0);
+}
+// spec ids of a group, loaded only when one of its pods may need a patch
+__device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g, uint16_t (&sp)[POD_PER_THREAD]) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(g.st[k], g.ip[k]);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (any && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) sp[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
+}
+__device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uint8_t* nflags, const PodGrp& g, int k) {
+    return (g.st[k] & PS_USED) ? nflags[g.j * S.cn + g.nl[k]] : (uint8_t)0;
+}
+
+// ---------------------------------------------------------------------------
+// classify phase (FRONT): predicates A.4 / A.5 over the block's nodes and live
+// pod groups; Use / Put bits (single rank: in place; multi rank: exchange
+// lists); heartbeat handles at the host-maintained base; per-thread counts
+// ---------------------------------------------------------------------------
+// the used-bitmap words of a group's evaluated in-CIDR IPs.  Pods of one
+// bucket hold consecutive addresses (canonical allocation order), so a
+// group's 8 addresses usually fall in two adjacent words: load those two.
+__device__ __forceinline__ void load_used_words(const DevState& S, const PodGrp& g, const PodCls (&c)[POD_PER_THREAD],
+                                                uint64_t (&uw)[POD_PER_THREAD]) {
+    bool any = false, near = true;
+    uint64_t w0 = 0;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const bool inc = c[k].eval && g.ip[k] && in_cidr(S.pool, g.ip[k]);
+        if (inc) {
+            const uint64_t w = (uint64_t)(g.ip[k] - S.pool.net) >> 6;
+            if (!any) w0 = w, any = true;
+            near &= (w == w0 || w == w0 + 1);
+        }
+    }
+    if (!any) {
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) uw[k] = ~0ull;
+        return;
+    }
+    if (near) {
+        const uint64_t a = S.used_bm[w0], b = w0 + 1 < S.pool.words ? S.used_bm[w0 + 1] : 0ull;
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint64_t w = (uint64_t)(g.ip[k] - S.pool.net) >> 6;
+            uw[k] = w == w0 ? a : b;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const bool inc = c[k].eval && g.ip[k] && in_cidr(S.pool, g.ip[k]);
+            uw[k] = inc ? S.used_bm[(g.ip[k] - S.pool.net) >> 6] : ~0ull;
+        }
+    }
+}
+
+// classify one loaded group; returns true when emission must visit its chunk
+__device__ __forceinline__ bool classify_group(const DevState& S, const uint8_t* nflags, const PodGrp& g,
+                                               uint32_t (&f)[AG_STRIDE]) {
+    PodCls c[POD_PER_THREAD];  // an empty group (slot ~0u) reads as unused pods
+    uint8_t ntf[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        ntf[k] = group_node_flags(S, nflags, g, k);
+        c[k] = classify_pod(g.st[k], ntf[k], g.ip[k]);
+    }
+    uint64_t uw[POD_PER_THREAD];
+    load_used_words(S, g, c, uw);
+    uint16_t sp[POD_PER_THREAD];
+    load_spec_ids(S, g, sp);
+    bool dirty = false;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint16_t st = g.st[k];
+        const uint32_t ip = g.ip[k];
+        f[AG_DEL] += c[k].del;
+        f[AG_EVAL] += c[k].eval;
+        f[AG_ALLOC] += c[k].alloc;
+        const bool inc = ip && in_cidr(S.pool, ip);
+        const uint64_t bit = ip - S.pool.net;
+        // the Deleted event of a pod we delete: release if the node is managed and the IP in CIDR
+        const bool rel = c[k].del && (ntf[k] & NT_MANAGED) && inc;
+        // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
+        // addresses not already in `used` change the pool
+        const bool use = c[k].eval && inc && !((uw[k] >> (bit & 63)) & 1);
+        if (S.world == 1) {
+            // single rank: Use() in place; the Put of a released address waits in rel_bm
+            // and is folded in the pool phase, after every Use of this tick (Use -> Put)
+            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
+            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+        }
+        f[AG_REL] += rel;
+        if (c[k].need) {
+            f[AG_PP]++;
+            f[AG_PP_BYTES] += S.specs[sp[k]].max_len;
+        }
+        const bool total = c[k].used && !c[k].del;
+        f[AG_TOTAL] += total;
+        f[AG_PENDING] += total && !c[k].need && c[k].phase == PHASE_PENDING;
+        f[AG_RUNNING] += total && (c[k].need || c[k].phase == PHASE_RUNNING);
+        dirty |= c[k].del || c[k].need || (c[k].eval && (st & PS_EVENT));
+    }
+    if (S.world > 1) {  // wave-level appends (ballot over the active lanes)
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint32_t ip = g.ip[k];
+            const bool inc = ip && in_cidr(S.pool, ip);
+            const uint64_t bit = ip - S.pool.net;
+            wave_append(c[k].del && (ntf[k] & NT_MANAGED) && inc, ip, S.rel_list, &S.list_counts[1]);
+            wave_append(c[k].eval && inc && !((uw[k] >> (bit & 63)) & 1), ip, S.use_list, &S.list_counts[0]);
+        }
+    }
+    return dirty;
+}
+
+// ---------------------------------------------------------------------------
+// emission: compaction of the output lists, byte emission, state transitions.
+// Only chunks marked dirty by the classify phase are visited: a clean chunk
+// contributes nothing to any scanned field.
+// ---------------------------------------------------------------------------
+struct Layout {
+    uint64_t init_base;   // arena offset of the node-init patches (= n_hb x HB_STRIDE)
+    uint64_t pod_base;    // arena offset of the pod patches (after every init patch)
+    uint64_t alloc_base;  // this rank's first global allocation ordinal
+    PoolPlan plan;
+};
+struct Bases {
+    uint64_t v[AG_NSCAN];  // running prefix of the scanned fields
+};
+
+// node chunk at block-local node offset i0 (node slots nbase + [i0, i0 + 1024))
+__device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbase, uint32_t i0, uint32_t nn, Bases& run,
+                                const Layout& L, const uint8_t* hb_tmpl, InitJob* ij) {
+    const uint32_t i = i0 + threadIdx.x * NODE_PER_THREAD;
+    const uint32_t first = nbase + i;
+    uint32_t packed = 0;
+    if (i < nn) packed = *reinterpret_cast<const uint32_t*>(S.node_state + first);
+    NodeCls c[NODE_PER_THREAD];
+    uint32_t v[2] = {0, 0};  // init, init bytes
+    uint32_t ilen[NODE_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < NODE_PER_THREAD; k++) {
+        c[k] = classify_node((uint8_t)(packed >> (8 * k)));
+        ilen[k] = 0;
+        if (c[k].init) {
+            ilen[k] = init_patch_len(S.node_blob[first + k]);
+            v[0]++;
+            v[1] += (ilen[k] + 15u) & ~15u;
+        }
+    }
+    uint32_t tot[2];
+    block_excl_scan<2>(v, tot);
+    const uint64_t chunk_bytes = L.init_base + run.v[AG_INIT_BYTES];
+    uint32_t newpacked = 0, ji = v[0];
+#pragma unroll
+    for (int k = 0; k < NODE_PER_THREAD; k++) {
+        uint8_t s = (uint8_t)(packed >> (8 * k));
+        if (c[k].init) {
+            const uint64_t ord = run.v[AG_INIT] + ji;
+            S.init_nodes[ord] = S.node_handle_base + (int32_t)(first + k);
+            S.init_off[ord] = chunk_bytes + v[1];
+            S.init_len[ord] = ilen[k];
+            ij[ji].slot = first + k;
+            ij[ji].off = v[1];
+            ji++;
+            v[1] += (ilen[k] + 15u) & ~15u;
+            s |= NS_CONFORMS;  // the apiserver applied the init patch
+        }
+        s &= (uint8_t)~NS_EVENT_LOCK;
+        newpacked |= (uint32_t)s << (8 * k);
+    }
+    if (i < nn && newpacked != packed) *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
+    __syncthreads();
+    for (uint32_t q = wave_id(); q < tot[0]; q += BLOCK / 64)
+        write_init_patch(S, S.node_blob[ij[q].slot], hb_tmpl, S.arena + chunk_bytes + ij[q].off);
+    __syncthreads();
+    run.v[AG_INIT] += tot[0];
+    run.v[AG_INIT_BYTES] += tot[1];
+}
+
+// pod chunk c: the block's live groups [c*256, c*256 + 256)
+__device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
+                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, PodJob* jobs) {
+    PodGrp g;
+    load_group(S, gpre, bk0, nbk, ng, c * BLOCK + threadIdx.x, g);
+    uint16_t sp[POD_PER_THREAD];
+    load_spec_ids(S, g, sp);
+    PodCls cl[POD_PER_THREAD];
+    uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        cl[k] = classify_pod(g.st[k], group_node_flags(S, nflags, g, k), g.ip[k]);
+        v[0] += cl[k].del;
+        if (cl[k].need) {
+            v[1]++;
+            v[2] += S.specs[sp[k]].max_len;
+        }
+        v[3] += cl[k].alloc;
+    }
+    uint32_t tot[4];
+    block_excl_scan<4>(v, tot);
+    const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0;
+    const uint64_t chunk_bytes = L.pod_base + run.v[AG_PP_BYTES];
+    uint32_t jl = v[1];
+    bool dirty = false;
+    uint16_t nst[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint32_t slot = g.slot + k;
+        const int32_t handle = S.pod_handle_base + (int32_t)slot;
+        uint16_t s = g.st[k];
+        if (cl[k].del) {
+            const uint64_t ord = run.v[AG_DEL] + v[0]++;
+            S.del_pods[ord] = handle;
+            S.del_fin[ord] = (s & PS_HAS_FIN) ? 1 : 0;
+            s = 0;  // DeletePod -> Delete(grace 0): the object is gone
+        }
+        if (cl[k].eval) {
+            uint32_t pip = g.ip[k];
+            if (cl[k].alloc) {
+                const uint64_t o = run.v[AG_ALLOC] + v[3]++;
+                const uint64_t gidx = L.alloc_base + o;
+                pip = gidx < take + fin ? S.alloc_addr[o] : (uint32_t)(fout0 + (gidx - take - fin));
+            }
+            if (cl[k].need) {
+                const bool stat = s & PS_STATUS_NONEMPTY;
+                uint32_t hip = 0;
+                if (stat) {
+                    hip = (s & PS_HAS_HOST_IP) ? S.host_ip[slot] : S.node_ip;
+                    if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
+                    if (pip != g.ip[k]) S.pod_ip[slot] = pip;
+                }
+                const uint64_t ord = run.v[AG_PP] + jl;
+                const SpecDesc& sd = S.specs[sp[k]];
+                const uint32_t len = sd.len_a + sd.len_b + sd.len_c + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
+                S.pp_pods[ord] = handle;
+                S.pp_off[ord] = chunk_bytes + v[2];
+                S.pp_len[ord] = len;
+                jobs[jl] = PodJob{slot, v[2], stat ? pip : 0u, hip};
+                jl++;
+                v[2] += sd.max_len;
+                // the apiserver applied the patch
+                s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
+                               PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
+            }
+            s &= (uint16_t)~PS_EVENT;
+        }
+        dirty |= s != g.st[k];
+        nst[k] = s;
+    }
+    if (g.slot != ~0u && dirty) {
+        uint4 o;
+        o.x = nst[0] | (uint32_t)nst[1] << 16;
+        o.y = nst[2] | (uint32_t)nst[3] << 16;
+        o.z = nst[4] | (uint32_t)nst[5] << 16;
+        o.w = nst[6] | (uint32_t)nst[7] << 16;
+        *reinterpret_cast<uint4*>(S.pod_state + g.slot) = o;
+    }
+    __syncthreads();
+    uint8_t* out = S.arena + chunk_bytes;
+    for (uint32_t q = wave_id(); q < tot[1]; q += BLOCK / 64) write_pod_patch(S, jobs[q], out + jobs[q].off);
+    __syncthreads();
+    run.v[AG_DEL] += tot[0];
+    run.v[AG_PP] += tot[1];
+    run.v[AG_PP_BYTES] += tot[2];
+    run.v[AG_ALLOC] += tot[3];
+}
+
+// ---------------------------------------------------------------------------
+// heartbeat stream: n_hb identical 1059-byte patches, 67 x 16 B each, from an
+// LDS template with non-temporal 16-byte stores (node_controller.go:145-157)
+// ---------------------------------------------------------------------------
+constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
+__device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t nchunks = n_hb * HB_CHUNKS;
+    const uint64_t lo = nchunks * idx / cnt, hi = nchunks * (idx + 1) / cnt;
+    u32x4* dst = reinterpret_cast<u32x4*>(S.arena);  // heartbeat region starts at arena offset 0
+    uint64_t i = lo + threadIdx.x;
+    uint32_t m = (uint32_t)(i % HB_CHUNKS);
+    constexpr uint32_t dm = BLOCK % HB_CHUNKS;
+    for (; i < hi; i += BLOCK) {
+        const uint4 v = tmpl[m];
+        u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, &dst[i]);  // write-once stream: do not keep in L2
+        m += dm;
+        if (m >= HB_CHUNKS) m -= HB_CHUNKS;
+    }
+}
+
+// per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
+__device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tmpl, uint64_t now_unix, uint64_t start_unix) {
+    const Ts now = format_ts(now_unix), st = format_ts(start_unix);
+    for (int i = threadIdx.x; i < HB_STRIDE; i += BLOCK) {
+        const uint8_t k = S.hb_kind[i];
+        uint32_t b;
+        if (k == 0xFF) b = S.hb_static[i];
+        else if (k < TS_LEN) b = ts_byte(now, k);
+        else b = ts_byte(st, k - TS_LEN);
+        tmpl[i] = (uint8_t)b;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// header / exchange message (FRONT launch, written by the last arriver)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb) {
+    TickHdr* H = S.hdr;
+    const uint64_t* tot = r.tot;
+    const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+    if (threadIdx.x == 0) {
+        if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
+            __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        H->n_hb = (uint32_t)tot[AG_HB];
+        H->n_init = (uint32_t)tot[AG_INIT];
+        H->init_bytes = tot[AG_INIT_BYTES];
+        H->n_del = (uint32_t)tot[AG_DEL];
+        H->n_pp = (uint32_t)tot[AG_PP];
+        H->pp_bytes = tot[AG_PP_BYTES];
+        H->n_alloc_local = (uint32_t)tot[AG_ALLOC];
+        H->n_lock = (uint32_t)tot[AG_LOCK];
+        H->n_eval = (uint32_t)tot[AG_EVAL];
+        H->n_rel = (uint32_t)tot[AG_REL];
+        H->n_use = S.world > 1 ? ld32_sc1(&S.list_counts[0]) : 0;
+        H->hb_base = 0;
+        H->init_base = patch_base;
+        H->pod_base = patch_base + tot[AG_INIT_BYTES];
+        H->arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
+        H->overflow = H->arena_bytes > S.arena_cap;
+        uint64_t* C = H->local_counters;
+        C[0] = tot[AG_HB];        // heartbeat
+        C[1] = tot[AG_INIT];      // node_init
+        C[2] = tot[AG_PP];        // pod_patch
+        C[3] = tot[AG_DEL];       // delete
+        C[4] = tot[AG_ALLOC];     // alloc
+        C[5] = tot[AG_REL];       // release
+        C[6] = tot[AG_EVAL];      // evaluated
+        C[7] = tot[AG_LOCK];      // lock_checked
+        C[8] = tot[AG_MANAGED];   // nodes_managed
+        C[9] = tot[AG_READY];     // nodes_ready
+        C[10] = tot[AG_TOTAL];    // pods_total
+        C[11] = tot[AG_PENDING];  // pods_pending
+        C[12] = tot[AG_RUNNING];  // pods_running
+        for (int k = 13; k < 16; k++) C[k] = 0;
+        if (S.world > 1 || tot[AG_ALLOC] == 0) H->cursor_index = *S.pool_index;  // else: the pool phase
+        if (S.world == 1) {
+            for (int k = 0; k < 16; k++) H->counters[k] = C[k];
+            H->alloc_total = tot[AG_ALLOC];
+            H->alloc_base = 0;
+            H->rel_total = tot[AG_REL];
+            if (tot[AG_ALLOC] == 0) H->usable_total = H->take_usable = H->fresh_in = H->fresh_out_start = 0;
+        } else {
+            XMsg* X = S.xmsg;
+            X->alloc = tot[AG_ALLOC];
+            X->n_use = H->n_use;
+            X->n_rel = ld32_sc1(&S.list_counts[1]);
+            for (int k = 0; k < 16; k++) X->counters[k] = C[k];
+        }
+    }
+    if (S.world > 1) {  // exchange lists inline when they fit
+        const uint32_t nu = ld32_sc1(&S.list_counts[0]), nr = ld32_sc1(&S.list_counts[1]);
+        if (nu + nr <= (uint32_t)XINLINE) {
+            for (uint32_t i = threadIdx.x; i < nu; i += BLOCK) S.xmsg->ips[i] = ld32_sc1(&S.use_list[i]);
+            for (uint32_t i = threadIdx.x; i < nr; i += BLOCK) S.xmsg->ips[nu + i] = ld32_sc1(&S.rel_list[i]);
+        }
+    }
+}
+
+// copy the device header to the pinned host copy (zero-copy publication).
+// Single rank: the pool leader publishes the pool fields (skip_alloc: the Get
+// plan and cursor) and its phase stamps (skip_pool) itself, concurrently.
+__device__ __forceinline__ void publish_header(const DevState& S, bool skip_alloc, bool skip_pool) {
+    constexpr int A0 = offsetof(TickHdr, usable_total) / 8, A1 = offsetof(TickHdr, rel_total) / 8;
+    constexpr int C0 = offsetof(TickHdr, clk) / 8;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(S.hdr);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
+        for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += 64) {
+            if (skip_alloc && i >= A0 && i < A1) continue;
+            if (skip_pool && (i == C0 + CLK_BACK || i == C0 + CLK_POOL)) continue;
+            dst[i] = src[i];
+        }
+        __threadfence_system();
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// k_tick: one controller tick.  Single rank: ONE launch (FRONT | BACK).
+// Multi rank: FRONT launch -> exchange -> BACK launch.
+//
+// Blocks [0, n_chain) are chain blocks, each owning a contiguous bucket range;
+// blocks [n_chain, grid) (FRONT only) stream the heartbeat bodies and touch
+// nothing else, so the bandwidth-bound stream overlaps the latency-bound
+// classification.
+//
+//   FRONT  per chain block: node states -> heartbeat handles (host-maintained
+//          base), node flags into LDS; live pod groups -> predicates, Use /
+//          Put; one block record; arrive.  The LAST arriver reduces the records
+//          into the tick header (single rank) / exchange message (multi rank).
+//          A block with nothing to emit is done here (the steady state).
+//   BACK   per dirty chain block (single rank: after every block arrived):
+//          prefix over the records; the pool phase among the dirty blocks when
+//          the tick has Gets or Puts (multi rank: among all blocks); emission
+//          of the dirty chunks.
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
                                                    uint32_t n_hb, int phases) {
     const int t = threadIdx.x;
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t T = S.node_tiles + S.pod_tiles;
-    const uint32_t t_lo = (uint32_t)((uint64_t)T * b / G), t_hi = (uint32_t)((uint64_t)T * (b + 1) / G);
-    TickHdr* H = S.hdr;
+    const uint32_t b = blockIdx.x;
     __shared__ union {
-        PodJob pod[POD_TILE];
-        InitJob node[NODE_TILE];
+        PodJob pod[POD_CHUNK];
+        InitJob node[NODE_CHUNK];
     } jobs;
     __shared__ uint4 hb_tmpl4[HB_CHUNKS];
-    __shared__ uint32_t sh_tagg[MAX_TILES_PER_BLOCK][AG_NSCAN];  // own tiles' scanned fields
+    __shared__ uint32_t nflags32[NODE_LDS / 4];
+    __shared__ uint32_t gpre[MAX_BPB + 1];
+    __shared__ uint32_t sh_mask[3];  // pod chunk mask lo / hi, node chunk mask
     __shared__ Layout sh_L;
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
-    // diagnostics: per-block phase stamps
+    const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
 #define TSTAMP(k)                                                                               \
     do {                                                                                        \
         if (S.trace && t == 0) S.trace[(size_t)b * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
     TSTAMP(0);
-    build_hb_template(S, hb_tmpl, now_unix, start_unix);
+
+    // ---- heartbeat streamers ------------------------------------------------------
+    if (b >= S.n_chain) {
+        build_hb_template(S, hb_tmpl, now_unix, start_unix);
+        hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
+        if ((phases & TICK_PROF) && t == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+        TSTAMP(6);
+        return;
+    }
+
+    uint32_t bk0, nbk;
+    block_range(S, b, bk0, nbk);
+    const uint32_t nn = nbk * S.cn, nbase = bk0 * S.cn;
+    TickHdr* H = S.hdr;
+    uint64_t pod_mask = 0;
+    uint32_t node_mask = 0;
+    uint32_t my_init = 0;
+    bool have_sums = false;
+    Sums sums;
 
     if (phases & TICK_FRONT) {
         if (t == 0) {
-            const uint64_t c = __builtin_amdgcn_s_memrealtime();
-            if (b == 0) H->clk[CLK_ENTRY] = c;
-            if (phases & TICK_PROF) atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)c);
+            if (phases & TICK_PROF)
+                atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         }
-        // ---- phase 1: classify own tiles, then the heartbeat share ----------------
-        // odd blocks stream their heartbeat share first, even blocks classify first:
-        // the two resident blocks of a CU overlap bandwidth- and latency-bound work
-        const bool hb_first = (phases & TICK_HB_FIRST) && (b & 1);
-        if (hb_first) hb_fill_share(S, hb_tmpl4, n_hb);
-        uint32_t acc[AG_STRIDE];
-        for (int f = 0; f < AG_STRIDE; f++) acc[f] = 0;
-        for (uint32_t tile = t_lo; tile < t_hi; tile++) {
-            uint32_t ag[AG_STRIDE];
-            if (tile < S.node_tiles) classify_node_tile(S, tile, ag);
-            else classify_pod_tile(S, tile - S.node_tiles, ag);
-            for (int f = 0; f < AG_STRIDE; f++) acc[f] += ag[f];
-            if (t == 0)
-                for (int f = 0; f < AG_NSCAN; f++) sh_tagg[tile - t_lo][f] = ag[f];
-            if (S.world > 1 && t == 0) {  // the BACK launch re-reads the tile records
-                uint4* o = reinterpret_cast<uint4*>(S.tiles + (size_t)tile * AG_STRIDE);
-                for (int i = 0; i < AG_STRIDE / 4; i++) o[i] = make_uint4(ag[4 * i], ag[4 * i + 1], ag[4 * i + 2], ag[4 * i + 3]);
+        if (t < 3) sh_mask[t] = 0;
+        load_gpre(S, bk0, nbk, gpre);  // its loads are in flight with the node loads below
+        uint32_t f[AG_STRIDE];
+#pragma unroll
+        for (int i = 0; i < AG_STRIDE; i++) f[i] = 0;
+        // ---- nodes: KeepNodeHeartbeat handles, needLockNode / configureNode (A.5) ----
+        uint32_t hb_run = S.hb_pre[b];
+        uint32_t nmask = 0;
+        for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
+            const uint32_t i = i0 + t * NODE_PER_THREAD;
+            const uint32_t packed = i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u;
+            uint32_t tick = 0, hb[1] = {0}, hbm = 0;
+            bool dirty = false;
+#pragma unroll
+            for (int k = 0; k < NODE_PER_THREAD; k++) {
+                const uint8_t s = (uint8_t)(packed >> (8 * k));
+                const NodeCls c = classify_node(s);
+                f[AG_HB] += c.hb;
+                f[AG_LOCK] += c.lock;
+                f[AG_MANAGED] += c.managed;
+                f[AG_READY] += c.ready;
+                if (c.init) {
+                    f[AG_INIT]++;
+                    f[AG_INIT_BYTES] += (init_patch_len(S.node_blob[nbase + i + k]) + 15u) & ~15u;
+                }
+                dirty |= c.init || (s & NS_EVENT_LOCK);
+                tick |= (uint32_t)node_tick_flags(s) << (8 * k);
+                hb[0] += c.hb;
+                hbm |= (uint32_t)c.hb << k;
             }
+            if (i < nn) {
+                nflags32[i / 4] = tick;
+                if (S.world > 1) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
+            }
+            uint32_t tot[1];
+            block_excl_scan<1>(hb, tot);
+            uint32_t pos = hb_run + hb[0];
+#pragma unroll
+            for (int k = 0; k < NODE_PER_THREAD; k++)
+                if ((hbm >> k) & 1) {
+                    if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
+                    pos++;
+                }
+            hb_run += tot[0];
+            if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
         }
-        if (t == 0) {
-            uint4* o = reinterpret_cast<uint4*>(S.blockagg + (size_t)b * AG_STRIDE);
-            for (int i = 0; i < AG_STRIDE / 4; i++) o[i] = make_uint4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
-        }
-        TSTAMP(5);
-        if (!hb_first) hb_fill_share(S, hb_tmpl4, n_hb);
-        if (t == 0) {
-            const uint64_t c = __builtin_amdgcn_s_memrealtime();
-            if (b == 0) H->clk[CLK_P1] = c;
-            if (phases & TICK_PROF) atomicMax(&S.bar->p1_max, (unsigned long long)c);
-        }
+        __syncthreads();  // gpre and node flags
         TSTAMP(1);
-        grid_barrier(S.bar, S.hdr_host);
+        // ---- pods: two live groups per thread in flight ----------------------------
+        const uint32_t ng = gpre[nbk];
+        uint64_t pmask = 0;
+        for (uint32_t g0 = 0; g0 < ng; g0 += 2 * BLOCK) {
+            PodGrp G0, G1;
+            load_group(S, gpre, bk0, nbk, ng, g0 + t, G0);
+            load_group(S, gpre, bk0, nbk, ng, g0 + BLOCK + t, G1);
+            const uint32_t c0 = g0 / BLOCK;
+            if (classify_group(S, nflags, G0, f)) pmask |= 1ull << c0;
+            if (classify_group(S, nflags, G1, f)) pmask |= 1ull << (c0 + 1);
+        }
         TSTAMP(2);
-        if (b == 0 && t == 0) H->clk[CLK_BAR] = __builtin_amdgcn_s_memrealtime();
-    } else if (t < AG_NSCAN) {  // BACK launch: own tiles' records from the FRONT launch
-        for (uint32_t tile = t_lo; tile < t_hi; tile++) sh_tagg[tile - t_lo][t] = S.tiles[(size_t)tile * AG_STRIDE + t];
-    }
-
-    // ---- phase 2: prefix of the blocks before this one, totals ---------------------
-    // every block: prefix of the scanned fields + alloc / rel totals; block 0: all totals
-    uint64_t red[AG_NSCAN + AG_COUNT];  // [0, NSCAN): prefix; then totals
-    for (int f = 0; f < AG_NSCAN + AG_COUNT; f++) red[f] = 0;
-    for (uint32_t j = t; j < G; j += BLOCK) {
-        const uint4* r = reinterpret_cast<const uint4*>(S.blockagg + (size_t)j * AG_STRIDE);
-        const uint4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3];
-        const uint32_t a[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-#pragma unroll
-        for (int f = 0; f < AG_NSCAN; f++) red[f] += j < b ? a[f] : 0u;
-#pragma unroll
-        for (int f = 0; f < AG_COUNT; f++) red[AG_NSCAN + f] += a[f];
-    }
-    block_sum64<AG_NSCAN + AG_COUNT>(red);
-    const uint64_t* pre = red;
-    const uint64_t* tot = red + AG_NSCAN;
-    const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
-    if (b == 0 && t == 0) {
-        if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
-            __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (phases & TICK_FRONT) {
-            H->n_hb = (uint32_t)tot[AG_HB];
-            H->n_init = (uint32_t)tot[AG_INIT];
-            H->init_bytes = tot[AG_INIT_BYTES];
-            H->n_del = (uint32_t)tot[AG_DEL];
-            H->n_pp = (uint32_t)tot[AG_PP];
-            H->pp_bytes = tot[AG_BYTES] - tot[AG_INIT_BYTES];
-            H->n_alloc_local = (uint32_t)tot[AG_ALLOC];
-            H->n_lock = (uint32_t)tot[AG_LOCK];
-            H->n_eval = (uint32_t)tot[AG_EVAL];
-            H->n_rel = (uint32_t)tot[AG_REL];
-            H->n_use = S.world > 1 ? S.list_counts[0] : 0;
-            H->hb_base = 0;
-            H->init_base = patch_base;
-            H->pod_base = patch_base + tot[AG_INIT_BYTES];
-            H->arena_bytes = patch_base + tot[AG_BYTES];
-            H->overflow = H->arena_bytes > S.arena_cap;
-            uint64_t* C = H->local_counters;
-            C[0] = tot[AG_HB];        // heartbeat
-            C[1] = tot[AG_INIT];      // node_init
-            C[2] = tot[AG_PP];        // pod_patch
-            C[3] = tot[AG_DEL];       // delete
-            C[4] = tot[AG_ALLOC];     // alloc
-            C[5] = tot[AG_REL];       // release
-            C[6] = tot[AG_EVAL];      // evaluated
-            C[7] = tot[AG_LOCK];      // lock_checked
-            C[8] = tot[AG_MANAGED];   // nodes_managed
-            C[9] = tot[AG_READY];     // nodes_ready
-            C[10] = tot[AG_TOTAL];    // pods_total
-            C[11] = tot[AG_PENDING];  // pods_pending
-            C[12] = tot[AG_RUNNING];  // pods_running
-            for (int k = 13; k < 16; k++) C[k] = 0;
-            if (S.world == 1) {
-                for (int k = 0; k < 16; k++) H->counters[k] = C[k];
-                H->alloc_total = tot[AG_ALLOC];
-                H->alloc_base = 0;
-                H->rel_total = tot[AG_REL];
-            } else {
-                XMsg* X = S.xmsg;
-                X->alloc = tot[AG_ALLOC];
-                X->n_use = S.list_counts[0];
-                X->n_rel = S.list_counts[1];
-                for (int k = 0; k < 16; k++) X->counters[k] = C[k];
+        if (nmask) atomicOr(&sh_mask[2], nmask);
+        if (pmask) {
+            if ((uint32_t)pmask) atomicOr(&sh_mask[0], (uint32_t)pmask);
+            if ((uint32_t)(pmask >> 32)) atomicOr(&sh_mask[1], (uint32_t)(pmask >> 32));
+        }
+        block_sum<AG_STRIDE>(f);  // synchronises: the masks are complete
+        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
+        node_mask = sh_mask[2];
+        f[AG_DIRTY] = (pod_mask | node_mask) ? 1u : 0u;
+        my_init = f[AG_INIT];
+        if (S.world > 1 && t == 0) {
+            S.dmask[2 * b] = pod_mask;
+            S.dmask[2 * b + 1] = node_mask;
+        }
+        // ---- arrive; the last arriver writes the header / exchange message ---------
+        const uint64_t old = publish_and_arrive(S, b, f);
+        TSTAMP(3);
+        const bool last = (old + 1) % S.n_chain == 0;
+        if (last) {
+            const uint64_t c = __builtin_amdgcn_s_memrealtime();
+            reduce_records(S, b, sums);
+            have_sums = true;
+            if (t == 0) {
+                H->clk[CLK_P1_MAX] = c;
+                if (phases & TICK_PROF) {
+                    H->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
+                    __hip_atomic_store(&S.bar->neg_entry_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
-            H->clk[CLK_BASES] = __builtin_amdgcn_s_memrealtime();
+            write_front_header(S, sums, n_hb);
+            if (t == 0) H->clk[CLK_HDR] = __builtin_amdgcn_s_memrealtime();
+            if (S.world == 1) publish_header(S, sums.tot[AG_ALLOC] != 0, (sums.tot[AG_ALLOC] | sums.tot[AG_REL]) != 0);
         }
-    }
-    if (b == 0 && S.world > 1 && (phases & TICK_FRONT)) {  // exchange lists inline when they fit
-        const uint32_t nu = S.list_counts[0], nr = S.list_counts[1];
-        if (nu + nr <= (uint32_t)XINLINE) {
-            for (uint32_t i = t; i < nu; i += BLOCK) S.xmsg->ips[i] = S.use_list[i];
-            for (uint32_t i = t; i < nr; i += BLOCK) S.xmsg->ips[nu + i] = S.rel_list[i];
+        if (!(phases & TICK_BACK)) return;
+        // single rank: a clean block is done; a dirty one waits for every record
+        if (!(pod_mask | node_mask)) {
+            TSTAMP(6);
+            return;
         }
+        if (!last) {
+            wait_arrivals(S, (old / S.n_chain + 1) * S.n_chain);
+            reduce_records(S, b, sums);
+            have_sums = true;
+        }
+    } else {
+        // BACK launch (multi rank): this block's masks from the FRONT launch
+        if (t == 0) {
+            sh_mask[0] = (uint32_t)S.dmask[2 * b];
+            sh_mask[1] = (uint32_t)(S.dmask[2 * b] >> 32);
+            sh_mask[2] = (uint32_t)S.dmask[2 * b + 1];
+            if (b == 0) {
+                H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
+                S.list_counts[0] = 0;  // exchange lists for the next tick
+                S.list_counts[1] = 0;
+            }
+        }
+        __syncthreads();
+        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
+        node_mask = sh_mask[2];
+        my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
     }
-    TSTAMP(3);
-    if (!(phases & TICK_BACK)) return;
+    if (!have_sums) reduce_records(S, b, sums);
 
-    // ---- phase 3: ipPool (only in ticks with Gets or Puts) ---------------------
-    uint64_t A, rel_total, alloc_base, n_alloc_local;
-    if (phases & TICK_FRONT) {  // same launch: the totals are this tick's
-        A = tot[AG_ALLOC];
-        rel_total = tot[AG_REL];
-        alloc_base = 0;
-        n_alloc_local = tot[AG_ALLOC];
-    } else {  // after the exchange: fleet totals from k_xreduce
-        A = H->alloc_total;
-        rel_total = H->rel_total;
-        alloc_base = H->alloc_base;
-        n_alloc_local = H->n_alloc_local;
-    }
-    if (b == 0 && t == 0) H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
+    // ---- pool phase (ticks with Gets or Puts) -------------------------------------
+    const bool single = S.world == 1;
+    const uint64_t A = single ? sums.tot[AG_ALLOC] : H->alloc_total;
+    const uint64_t rel_total = single ? sums.tot[AG_REL] : H->rel_total;
+    const uint64_t alloc_base = single ? 0 : H->alloc_base;
+    const uint64_t n_alloc_local = sums.tot[AG_ALLOC];
+    // participants: single rank - the dirty blocks (every Get / Put belongs to one);
+    // multi rank - every block (each rank commits every rank's Gets to its replica)
+    const uint32_t np = single ? (uint32_t)sums.tot[AG_DIRTY] : S.n_chain;
+    const uint32_t pidx = single ? (uint32_t)sums.pre[AG_DIRTY] : b;
+    const bool dirty = (pod_mask | node_mask) != 0;
     PoolPlan plan{};
     if (A || rel_total) {
+        if (single && pidx == 0 && t == 0) H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
         const uint32_t nwb = (uint32_t)((S.pool.words + POOL_WPB - 1) / POOL_WPB);
-        for (uint32_t wb = b; wb < nwb; wb += G) pool_prep_wblock(S, wb, rel_total != 0, A != 0);
-        grid_barrier(S.bar, S.hdr_host);
+        for (uint32_t wb = pidx; wb < nwb; wb += np) pool_prep_wblock(S, wb, rel_total != 0, A != 0);
+        pool_barrier(S, np);
         if (A) {
             uint64_t cursor = ~0ull;
-            for (uint32_t wb = b; wb < nwb; wb += G) {
+            for (uint32_t wb = pidx; wb < nwb; wb += np) {
                 uint64_t bu, bf;
                 plan = pool_plan(S, A, nwb, wb, &bu, &bf);
                 pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor);
             }
-            if (b >= nwb) {
+            if (pidx >= nwb) {
                 uint64_t bu, bf;
                 plan = pool_plan(S, A, nwb, 0, &bu, &bf);
             }
             // ipPool.index after the last fresh address (committed after the barrier)
             if (cursor != ~0ull) H->cursor_index = cursor;
-            if (b == 0 && t == 0) {
+            if (pidx == 0 && t == 0) {
                 H->usable_total = plan.U;
                 H->take_usable = plan.take;
                 H->fresh_in = plan.fin;
@@ -1108,50 +1327,61 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 if (plan.fout) H->cursor_index = plan.fout0 + plan.fout - S.pool.base;
                 else if (plan.fin == 0) H->cursor_index = *S.pool_index;
             }
-            grid_barrier(S.bar, S.hdr_host);
+            pool_barrier(S, np);
+            if (pidx == 0 && t == 0) *S.pool_index = H->cursor_index;
         }
+        if (pidx == 0 && t == 0) {
+            H->clk[CLK_POOL] = __builtin_amdgcn_s_memrealtime();
+            if (single) {  // the last arriver published everything else (publish_header)
+                TickHdr* P = S.hdr_host;
+                if (A) {
+                    P->usable_total = H->usable_total;
+                    P->take_usable = H->take_usable;
+                    P->fresh_in = H->fresh_in;
+                    P->fresh_out_start = H->fresh_out_start;
+                    P->cursor_index = H->cursor_index;
+                }
+                P->clk[CLK_BACK] = H->clk[CLK_BACK];
+                P->clk[CLK_POOL] = H->clk[CLK_POOL];
+                __threadfence_system();
+            }
+        }
+        TSTAMP(5);
+    }
+    if (!single && b == 0) publish_header(S, false, false);  // multi rank: counts, exchange totals and pool fields
+    if (!dirty) {
+        TSTAMP(6);
+        return;
     }
 
-    // ---- phase 4: emission ------------------------------------------------------
+    // ---- emission of the dirty chunks ----------------------------------------------
+    if (!(phases & TICK_FRONT)) {  // BACK launch: the block's pod groups and node flags again
+        load_gpre(S, bk0, nbk, gpre);
+        if (pod_mask)
+            for (uint32_t i = t * 4; i < nn; i += NODE_CHUNK)
+                nflags32[i / 4] = *reinterpret_cast<const uint32_t*>(S.node_tick + nbase + i);
+        __syncthreads();
+    }
+    if (node_mask && my_init) build_hb_template(S, hb_tmpl, now_unix, start_unix);
     if (t == 0) {
-        sh_L.patch_base = patch_base;
+        const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+        sh_L.init_base = patch_base;
+        sh_L.pod_base = patch_base + sums.tot[AG_INIT_BYTES];
         sh_L.alloc_base = alloc_base;
         sh_L.plan = plan;
     }
-    if (b == 0) {
-        // the header is final here (bases, pool plan and cursor: all written before
-        // the last grid barrier, or by this block): commit the cursor, reset the
-        // exchange lists, and publish the header zero-copy.  Every other block has
-        // read pool_index and list_counts before that barrier.
-        if (t == 0) {
-            H->clk[CLK_POOL] = __builtin_amdgcn_s_memrealtime();
-            if ((phases & TICK_PROF) && (phases & TICK_FRONT)) {  // every block stamped before the barrier
-                H->clk[CLK_ENTRY_MIN] = ~S.bar->neg_entry_max;
-                H->clk[CLK_P1_MAX] = S.bar->p1_max;
-                S.bar->neg_entry_max = 0;
-                S.bar->p1_max = 0;
-            }
-            if (A) *S.pool_index = H->cursor_index;
-            S.list_counts[0] = 0;  // multi-rank exchange lists for the next tick
-            S.list_counts[1] = 0;
-        }
-        __syncthreads();
-        if (t < 64) {
-            const uint64_t* src = reinterpret_cast<const uint64_t*>(H);
-            uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
-            for (int i = t; i < (int)(offsetof(TickHdr, err) / 8); i += 64) dst[i] = src[i];
-            __threadfence_system();
-        }
-    }
     __syncthreads();
-    TSTAMP(4);
     const Layout L = sh_L;
     Bases run;
-    for (int f = 0; f < AG_NSCAN; f++) run.v[f] = pre[f];
-    for (uint32_t tile = t_lo; tile < t_hi; tile++) {
-        if (tile < S.node_tiles) emit_node_tile(S, tile, run, L, hb_tmpl, jobs.node);
-        else emit_pod_tile(S, tile - S.node_tiles, run, L, jobs.pod);
-        for (int f = 0; f < AG_NSCAN; f++) run.v[f] += sh_tagg[tile - t_lo][f];
+    for (int f = 0; f < AG_NSCAN; f++) run.v[f] = sums.pre[f];
+    for (uint32_t m = node_mask; m; m &= m - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctz(m);
+        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, hb_tmpl, jobs.node);
+    }
+    const uint32_t ng = gpre[nbk];
+    for (uint64_t m = pod_mask; m; m &= m - 1) {
+        const uint32_t c = (uint32_t)__builtin_ctzll(m);
+        emit_pod_chunk(S, gpre, nflags, bk0, nbk, ng, c, run, L, jobs.pod);
     }
     TSTAMP(6);
 #undef TSTAMP
@@ -1248,8 +1478,9 @@ void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hip
     hipLaunchKernelGGL(k_xreduce, dim3(1), dim3(64), 0, st, S, all, world, rank);
 }
 
-void launch_tick(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
+void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+    const uint32_t grid = S.n_chain + ((phases & TICK_FRONT) ? n_stream : 0u);
     if (t0) hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases);
     else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases);
 }

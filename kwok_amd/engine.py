@@ -270,7 +270,7 @@ class Engine(EngineBase):
     def __init__(self, cfg=None, **kw):
         super().__init__(load_engine_lib(), cfg if cfg is not None else make_config(**kw))
 
-    PHASES = ("classify", "barrier", "bases", "exchange", "pool", "emit", "kernel")  # KWOK_T_* order
+    PHASES = ("classify", "stream", "header", "exchange", "pool", "emit", "kernel")  # KWOK_T_* order
     HOST = ("enqueue", "wait", "post", "total")  # KWOK_H_* order
 
     def profile_enable(self, on=True):

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=${1:-x}
 R=$GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/tests_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
 trc=$?
 tail -15 gpurun_out/tests_$TAG.log
 [ $trc -eq 0 ] || [ $trc -eq 1 ] || exit $trc
