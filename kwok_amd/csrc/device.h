@@ -44,6 +44,7 @@ constexpr int MAX_BPB = 64;               // buckets per chain block
 constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS node flags)
 constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
 constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
+constexpr int TRACE_SLOTS = 16;           // KWOK_TICK_TRACE=1: per-block phase stamps
 
 // ---- fixed template geometry (default templates) -----------------------------
 constexpr int HB_LEN = 1059;     // {"status":{"conditions":[5 conditions]}} with 20-byte T/S

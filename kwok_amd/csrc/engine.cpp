@@ -120,6 +120,11 @@ struct kwok_engine {
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
     uint32_t n_stream = 0;      // k_tick heartbeat streamer blocks (the chain blocks: S.n_chain)
+    DevState* d_S = nullptr;    // S in device memory (the kernel's out-of-line phases read it there)
+    hipEvent_t done_ev = nullptr;  // tick completion (KWOK_SYNC=spin, the default)
+    bool sync_spin = true;
+    DevState* S_pin = nullptr;  // pinned staging for its upload
+    DevState S_up{};            // the copy last uploaded
     // diagnostics
     bool prof = false;
     hipEvent_t pev[4] = {};  // k_tick launch start/stop: FRONT(+BACK) launch, BACK launch
@@ -128,7 +133,7 @@ struct kwok_engine {
     double host_ms[KWOK_H_COUNT] = {};
     // KWOK_TICK_TRACE=1: per-block phase stamps, summarised on stderr at destroy
     std::vector<uint64_t> trace_h;
-    double trace_sum[10][3] = {};  // chain stamps 0..7, streamer entry / exit
+    double trace_sum[TRACE_SLOTS + 2][3] = {};  // chain stamps, streamer entry / exit
     uint64_t trace_ticks = 0, trace_seen = 0;
     uint64_t host_ticks = 0;
 
@@ -432,20 +437,21 @@ const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->trace_ticks) {
-        static const char* names[8] = {"entry", "nodes-done", "pods-done", "arrived",
-                                       "-", "pool-done", "exit", "-"};
+        static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "-", "pool-done",
+                                                 "exit", "header-done", "w:gpre", "w:pod-loads", "w:pods-classd",
+                                                 "w:block-sum", "w:masks", "w:used-words", "-", "-"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
                         "start (min / median / max block)\n",
                 e->S.n_chain, e->n_stream, (unsigned long long)e->trace_ticks);
-        for (int k = 0; k < 8; k++)
-            if (names[k][0] != '-')
+        for (int k = 0; k < TRACE_SLOTS; k++)
+            if (names[k][0] != '-' && e->trace_sum[k][2] > 0)
                 fprintf(stderr, "[kwok trace] chain    %-11s %8.2f %8.2f %8.2f\n", names[k],
                         e->trace_sum[k][0] / e->trace_ticks, e->trace_sum[k][1] / e->trace_ticks,
                         e->trace_sum[k][2] / e->trace_ticks);
         for (int k = 0; k < 2; k++)
             fprintf(stderr, "[kwok trace] streamer %-11s %8.2f %8.2f %8.2f\n", k ? "exit" : "entry",
-                    e->trace_sum[8 + k][0] / e->trace_ticks, e->trace_sum[8 + k][1] / e->trace_ticks,
-                    e->trace_sum[8 + k][2] / e->trace_ticks);
+                    e->trace_sum[TRACE_SLOTS + k][0] / e->trace_ticks, e->trace_sum[TRACE_SLOTS + k][1] / e->trace_ticks,
+                    e->trace_sum[TRACE_SLOTS + k][2] / e->trace_ticks);
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
@@ -460,6 +466,9 @@ void kwok_engine_destroy(kwok_engine* e) {
         if (p) (void)hipFree(p);
     if (e->hdr_h) (void)hipHostFree(e->hdr_h);
     if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
+    if (e->S_pin) (void)hipHostFree(e->S_pin);
+    if (e->done_ev) (void)hipEventDestroy(e->done_ev);
+    if (e->d_S) (void)hipFree(e->d_S);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->comm) ncclCommDestroy(e->comm);
@@ -574,7 +583,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
         (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
         (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
-        (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * 8))) ||
+        (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
@@ -598,7 +607,16 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
+    if ((rc = dalloc(e, &e->d_S, 1))) return bail(rc);
+    {
+        const char* sy = getenv("KWOK_SYNC");
+        e->sync_spin = !(sy && strcmp(sy, "block") == 0);
+        if (hipEventCreateWithFlags(&e->done_ev, hipEventDisableTiming) != hipSuccess)
+            return bail(e->fail(KWOK_EDEVICE, "event create"));
+    }
+    S.self = e->d_S;
     if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->S_pin, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipHostMallocDefault) != hipSuccess)
         return bail(KWOK_ENOMEM);
     S.hb_pre = e->d_hb_pre;
@@ -917,6 +935,11 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
         HIPCHK(e, hipMemcpyAsync(e->d_hb_pre, e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipMemcpyHostToDevice, st));
         e->hb_pre_dirty = false;
     }
+    if (memcmp(&e->S_up, &S, sizeof(DevState)) != 0) {  // pointers / sizes changed since the last upload
+        *e->S_pin = S;
+        HIPCHK(e, hipMemcpyAsync(e->d_S, e->S_pin, sizeof(DevState), hipMemcpyHostToDevice, st));
+        e->S_up = S;
+    }
     const int prof = ev ? TICK_PROF : 0;
     if (e->W == 1) {
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, st, ev ? ev[0] : nullptr,
@@ -977,25 +1000,26 @@ static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr &
 static void trace_tick(kwok_engine* e) {
     const size_t G = e->S.n_chain, N = G + e->n_stream;
     if (++e->trace_seen <= 5) return;  // skip the initial (bulk) ticks
-    e->trace_h.assign(N * 8, 0);
-    if (hipMemcpy(e->trace_h.data(), e->S.trace, N * 8 * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    (void)hipMemset(e->S.trace, 0, N * 8 * 8);
+    const size_t TS = TRACE_SLOTS;
+    e->trace_h.assign(N * TS, 0);
+    if (hipMemcpy(e->trace_h.data(), e->S.trace, N * TS * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    (void)hipMemset(e->S.trace, 0, N * TS * 8);
     uint64_t t0 = ~0ull;
-    for (size_t b = 0; b < G; b++) t0 = std::min(t0, e->trace_h[b * 8]);
+    for (size_t b = 0; b < G; b++) t0 = std::min(t0, e->trace_h[b * TS]);
     // stamps a block did not reach this tick (a clean block skips the pool phase) are 0
     auto summarise = [&](size_t lo, size_t hi, int k, double* out) {
         std::vector<double> v;
         for (size_t b = lo; b < hi; b++)
-            if (e->trace_h[b * 8 + k] >= t0) v.push_back((double)(e->trace_h[b * 8 + k] - t0) * 0.01);
+            if (e->trace_h[b * TS + k] >= t0) v.push_back((double)(e->trace_h[b * TS + k] - t0) * 0.01);
         if (v.empty()) return;
         std::sort(v.begin(), v.end());
         out[0] += v[0];
         out[1] += v[v.size() / 2];
         out[2] += v[v.size() - 1];
     };
-    for (int k = 0; k < 8; k++) summarise(0, G, k, e->trace_sum[k]);
-    summarise(G, N, 0, e->trace_sum[8]);
-    summarise(G, N, 6, e->trace_sum[9]);
+    for (int k = 0; k < TRACE_SLOTS; k++) summarise(0, G, k, e->trace_sum[k]);
+    summarise(G, N, 0, e->trace_sum[TRACE_SLOTS]);
+    summarise(G, N, 6, e->trace_sum[TRACE_SLOTS + 1]);
     e->trace_ticks++;
 }
 
@@ -1010,7 +1034,17 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         if (rc) return rc;
     }
     const auto t1 = clk::now();
-    HIPCHK(e, hipStreamSynchronize(st));
+    if (e->sync_spin) {
+        // spin on the tick's completion event: a blocking stream wait sleeps and
+        // pays the wake-up latency on every tick
+        HIPCHK(e, hipEventRecord(e->done_ev, st));
+        hipError_t q;
+        while ((q = hipEventQuery(e->done_ev)) == hipErrorNotReady) {
+        }
+        HIPCHK(e, q);
+    } else {
+        HIPCHK(e, hipStreamSynchronize(st));
+    }
     const auto t2 = clk::now();
     const TickHdr& H = *e->hdr_h;
     if (trace_enabled(e)) trace_tick(e);

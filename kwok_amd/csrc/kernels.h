@@ -74,7 +74,8 @@ struct DevState {
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
-    uint64_t* trace;           // [grid][8] per-block phase stamps (KWOK_TICK_TRACE=1), else null
+    uint64_t* trace;           // [grid][TRACE_SLOTS] per-block phase stamps (KWOK_TICK_TRACE=1), else null
+    const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,

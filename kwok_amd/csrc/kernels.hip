@@ -524,11 +524,11 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* lis
 }
 
 // publish this block's record and arrive; returns the arrival counter before
-// this block's add (uniform).  Every wave drains its stores and atomics first,
-// so the Use / Put atomics of the classify phase are performed before the add.
+// this block's add (uniform).  A wave that issued pool atomics or exchange-list
+// stores drained them in the classify slow path, before the barrier here; the
+// block's other stores (output lists) are issued after the arrival.
 __device__ __forceinline__ uint64_t publish_and_arrive(const DevState& S, uint32_t b, const uint32_t (&rec)[AG_STRIDE]) {
     __shared__ unsigned long long sh_old;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 64) {
         const int l = lane_id();
@@ -615,14 +615,22 @@ __device__ __forceinline__ void block_sum64(uint64_t (&v)[N]) {
 }
 
 // prefix over chain blocks < b and totals over all chain blocks of the records
-// (sc1 loads: the records may have been published in this launch)
+// (sc1 loads: the records may have been published in this launch).  The
+// records are transposed through LDS: thread (f, p) = (t / 16, t % 16) sums
+// field f of records p, p + 16, ... and a 16-lane DPP row reduction finishes.
+constexpr int MAX_CHAIN = 512;
+constexpr int REC_PITCH = AG_STRIDE + 1;  // conflict-free column reads
 struct Sums {
     uint64_t pre[AG_STRIDE], tot[AG_STRIDE];
 };
-__device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, Sums& r) {
-    uint64_t red[2 * AG_STRIDE];
-#pragma unroll
-    for (int f = 0; f < 2 * AG_STRIDE; f++) red[f] = 0;
+__device__ __forceinline__ uint64_t row_sum16(uint64_t x) {  // lane 15 of each 16-lane row: the row total
+    x += dpp_src64<0x111, 0xF>(x);
+    x += dpp_src64<0x112, 0xF>(x);
+    x += dpp_src64<0x114, 0xF>(x);
+    x += dpp_src64<0x118, 0xF>(x);
+    return x;
+}
+__device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, uint32_t* recs, Sums* out) {
     for (uint32_t j = threadIdx.x; j < S.n_chain; j += BLOCK) {
         const uint64_t* p = reinterpret_cast<const uint64_t*>(S.blockagg + (size_t)j * AG_STRIDE);
         uint64_t q[AG_STRIDE / 2];
@@ -630,19 +638,25 @@ __device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, Su
         for (int i = 0; i < AG_STRIDE / 2; i++) q[i] = ld_sc1(p + i);
 #pragma unroll
         for (int i = 0; i < AG_STRIDE / 2; i++) {
-            const uint32_t lo = (uint32_t)q[i], hi = (uint32_t)(q[i] >> 32);
-            red[2 * i] += j < b ? lo : 0u;
-            red[2 * i + 1] += j < b ? hi : 0u;
-            red[AG_STRIDE + 2 * i] += lo;
-            red[AG_STRIDE + 2 * i + 1] += hi;
+            recs[j * REC_PITCH + 2 * i] = (uint32_t)q[i];
+            recs[j * REC_PITCH + 2 * i + 1] = (uint32_t)(q[i] >> 32);
         }
     }
-    block_sum64<2 * AG_STRIDE>(red);
-#pragma unroll
-    for (int f = 0; f < AG_STRIDE; f++) {
-        r.pre[f] = red[f];
-        r.tot[f] = red[AG_STRIDE + f];
+    __syncthreads();
+    const uint32_t f = threadIdx.x >> 4, p = threadIdx.x & 15;
+    uint64_t tot = 0, pre = 0;
+    for (uint32_t j = p; j < S.n_chain; j += 16) {
+        const uint32_t v = recs[j * REC_PITCH + f];
+        tot += v;
+        pre += j < b ? v : 0u;
     }
+    tot = row_sum16(tot);
+    pre = row_sum16(pre);
+    if (p == 15) {
+        out->tot[f] = tot;
+        out->pre[f] = pre;
+    }
+    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -729,100 +743,178 @@ __device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uin
 // pod groups; Use / Put bits (single rank: in place; multi rank: exchange
 // lists); heartbeat handles at the host-maintained base; per-thread counts
 // ---------------------------------------------------------------------------
-// the used-bitmap words of a group's evaluated in-CIDR IPs.  Pods of one
-// bucket hold consecutive addresses (canonical allocation order), so a
-// group's 8 addresses usually fall in two adjacent words: load those two.
-__device__ __forceinline__ void load_used_words(const DevState& S, const PodGrp& g, const PodCls (&c)[POD_PER_THREAD],
-                                                uint64_t (&uw)[POD_PER_THREAD]) {
-    bool any = false, near = true;
-    uint64_t w0 = 0;
+// Per-group predicate masks (bit k = pod k of the 8-slot group), computed
+// branch-free from the packed state words: the steady state is a sweep of
+// ~20 VALU ops per pod.  Everything rare (a Use that changes the pool, a
+// release, a patch - whose byte count needs the spec) runs in a slow path
+// entered only when some lane of the wave needs it.
+struct GroupMasks {
+    uint32_t del, eval, alloc, need, rel, usec, total, pend, run, dirty;
+};
+__device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGrp& g, const uint8_t (&ntf)[POD_PER_THREAD]) {
+    GroupMasks m{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
-        const bool inc = c[k].eval && g.ip[k] && in_cidr(S.pool, g.ip[k]);
-        if (inc) {
-            const uint64_t w = (uint64_t)(g.ip[k] - S.pool.net) >> 6;
-            if (!any) w0 = w, any = true;
-            near &= (w == w0 || w == w0 + 1);
-        }
+        const uint32_t st = g.st[k], ip = g.ip[k], nf = ntf[k];
+        const uint32_t used = st & PS_USED;
+        const uint32_t del = used && (st & PS_DELETE_PENDING);
+        // needLockPod / heartbeat re-lock (pod_controller.go:252-269, node_controller.go:152)
+        const uint32_t eval = used && !del && ((st & PS_EVENT) || ((nf & NT_RELOCK) && !(st & PS_DISREGARD)));
+        const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
+        const uint32_t ipz = ip == 0;
+        // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47)
+        const uint32_t alloc = eval && (st & PS_STATUS_NONEMPTY) && ipz;
+        // computePatchData: Pending always patches; otherwise the strategic merge must change something
+        const uint32_t need = eval && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ipz);
+        const uint32_t inc = !ipz && (uint64_t)(ip - S.pool.net) < S.pool.size && ip >= S.pool.net;
+        const uint32_t total = used && !del;
+        m.del |= del << k;
+        m.eval |= eval << k;
+        m.alloc |= alloc << k;
+        m.need |= need << k;
+        m.rel |= (del && (nf & NT_MANAGED) && inc) << k;
+        m.usec |= (eval && inc) << k;
+        m.total |= total << k;
+        m.pend |= (total && !need && phase == PHASE_PENDING) << k;
+        m.run |= (total && (need || phase == PHASE_RUNNING)) << k;
+        m.dirty |= (del || need || (eval && (st & PS_EVENT))) << k;
     }
-    if (!any) {
+    return m;
+}
+
+// `used` bits of a group's Use candidates (bit k set = already in `used`).
+// Pods of one bucket hold consecutive addresses (canonical allocation order),
+// so a group's addresses usually fall in two adjacent words: load those two
+// (UsedWords); a group that straddles more is resolved word by word.
+struct UsedWords {
+    uint64_t w0, a, b;
+    bool near;
+};
+__device__ __forceinline__ UsedWords used_words(const DevState& S, const PodGrp& g, uint32_t usec) {
+    UsedWords u{0, 0, 0, true};
+    if (!usec) return u;
+    const uint32_t k0 = (uint32_t)__builtin_ctz(usec);
+    uint32_t ip0 = g.ip[0];
 #pragma unroll
-        for (int k = 0; k < POD_PER_THREAD; k++) uw[k] = ~0ull;
-        return;
+    for (int k = 1; k < POD_PER_THREAD; k++) ip0 = (uint32_t)k == k0 ? g.ip[k] : ip0;
+    u.w0 = (uint64_t)(ip0 - S.pool.net) >> 6;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint64_t w = (uint64_t)(g.ip[k] - S.pool.net) >> 6;
+        u.near &= !((usec >> k) & 1) || w == u.w0 || w == u.w0 + 1;
     }
-    if (near) {
-        const uint64_t a = S.used_bm[w0], b = w0 + 1 < S.pool.words ? S.used_bm[w0 + 1] : 0ull;
+    if (u.near) {
+        u.a = S.used_bm[u.w0];
+        u.b = u.w0 + 1 < S.pool.words ? S.used_bm[u.w0 + 1] : 0ull;
+    }
+    return u;
+}
+__device__ __forceinline__ uint32_t used_bits(const DevState& S, const PodGrp& g, uint32_t usec, const UsedWords& u) {
+    uint32_t bits = 0;
+    if (u.near) {
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
-            const uint64_t w = (uint64_t)(g.ip[k] - S.pool.net) >> 6;
-            uw[k] = w == w0 ? a : b;
+            const uint64_t bit = g.ip[k] - S.pool.net;
+            const uint64_t w = (bit >> 6) == u.w0 ? u.a : u.b;
+            bits |= (uint32_t)((w >> (bit & 63)) & 1) << k;
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < POD_PER_THREAD; k++) {
-            const bool inc = c[k].eval && g.ip[k] && in_cidr(S.pool, g.ip[k]);
-            uw[k] = inc ? S.used_bm[(g.ip[k] - S.pool.net) >> 6] : ~0ull;
-        }
+        for (int k = 0; k < POD_PER_THREAD; k++)
+            if ((usec >> k) & 1) {
+                const uint64_t bit = g.ip[k] - S.pool.net;
+                bits |= (uint32_t)((S.used_bm[bit >> 6] >> (bit & 63)) & 1) << k;
+            }
     }
+    return bits & usec;
 }
 
-// classify one loaded group; returns true when emission must visit its chunk
-__device__ __forceinline__ bool classify_group(const DevState& S, const uint8_t* nflags, const PodGrp& g,
-                                               uint32_t (&f)[AG_STRIDE]) {
-    PodCls c[POD_PER_THREAD];  // an empty group (slot ~0u) reads as unused pods
-    uint8_t ntf[POD_PER_THREAD];
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        ntf[k] = group_node_flags(S, nflags, g, k);
-        c[k] = classify_pod(g.st[k], ntf[k], g.ip[k]);
-    }
-    uint64_t uw[POD_PER_THREAD];
-    load_used_words(S, g, c, uw);
-    uint16_t sp[POD_PER_THREAD];
-    load_spec_ids(S, g, sp);
-    bool dirty = false;
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint16_t st = g.st[k];
-        const uint32_t ip = g.ip[k];
-        f[AG_DEL] += c[k].del;
-        f[AG_EVAL] += c[k].eval;
-        f[AG_ALLOC] += c[k].alloc;
-        const bool inc = ip && in_cidr(S.pool, ip);
-        const uint64_t bit = ip - S.pool.net;
-        // the Deleted event of a pod we delete: release if the node is managed and the IP in CIDR
-        const bool rel = c[k].del && (ntf[k] & NT_MANAGED) && inc;
-        // configurePod (pod_controller.go:378-382): Use() an existing in-CIDR IP; only
-        // addresses not already in `used` change the pool
-        const bool use = c[k].eval && inc && !((uw[k] >> (bit & 63)) & 1);
-        if (S.world == 1) {
-            // single rank: Use() in place; the Put of a released address waits in rel_bm
-            // and is folded in the pool phase, after every Use of this tick (Use -> Put)
-            if (use) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
-            if (rel) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
-        }
-        f[AG_REL] += rel;
-        if (c[k].need) {
-            f[AG_PP]++;
-            f[AG_PP_BYTES] += S.specs[sp[k]].max_len;
-        }
-        const bool total = c[k].used && !c[k].del;
-        f[AG_TOTAL] += total;
-        f[AG_PENDING] += total && !c[k].need && c[k].phase == PHASE_PENDING;
-        f[AG_RUNNING] += total && (c[k].need || c[k].phase == PHASE_RUNNING);
-        dirty |= c[k].del || c[k].need || (c[k].eval && (st & PS_EVENT));
-    }
-    if (S.world > 1) {  // wave-level appends (ballot over the active lanes)
+// count one group and run its slow path; returns true when emission must
+// visit its chunk
+__device__ __forceinline__ bool count_group(const DevState& S, const PodGrp& g, const GroupMasks& m, uint32_t use,
+                                            uint32_t (&f)[AG_STRIDE]) {
+    f[AG_DEL] += __popc(m.del);
+    f[AG_EVAL] += __popc(m.eval);
+    f[AG_ALLOC] += __popc(m.alloc);
+    f[AG_REL] += __popc(m.rel);
+    f[AG_PP] += __popc(m.need);
+    f[AG_TOTAL] += __popc(m.total);
+    f[AG_PENDING] += __popc(m.pend);
+    f[AG_RUNNING] += __popc(m.run);
+    if (__builtin_expect(__ballot((use | m.rel | m.need) != 0) != 0, 0)) {
+        // slow path (wave-uniform entry): pool bits / exchange lists, patch byte counts
+        uint16_t sp[POD_PER_THREAD];
+        load_spec_ids(S, g, sp);
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
             const uint32_t ip = g.ip[k];
-            const bool inc = ip && in_cidr(S.pool, ip);
             const uint64_t bit = ip - S.pool.net;
-            wave_append(c[k].del && (ntf[k] & NT_MANAGED) && inc, ip, S.rel_list, &S.list_counts[1]);
-            wave_append(c[k].eval && inc && !((uw[k] >> (bit & 63)) & 1), ip, S.use_list, &S.list_counts[0]);
+            const bool u = (use >> k) & 1, r = (m.rel >> k) & 1;
+            if (S.world == 1) {
+                // single rank: Use() in place; the Put of a released address waits in rel_bm
+                // and is folded in the pool phase, after every Use of this tick (Use -> Put)
+                if (u) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
+                if (r) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+            } else {  // ballots over every lane of the wave
+                wave_append(r, ip, S.rel_list, &S.list_counts[1]);
+                wave_append(u, ip, S.use_list, &S.list_counts[0]);
+            }
+            if ((m.need >> k) & 1) f[AG_PP_BYTES] += S.specs[sp[k]].max_len;
         }
+        // the atomics / list entries are performed before this block arrives
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    return dirty;
+    return m.dirty != 0;
+}
+
+// classify two loaded groups (their used-bitmap loads in flight together):
+// counts into f, dirty chunk bits c0 / c0 + 1 into pmask.  Uniform per wave up
+// to the lane masks (an empty group, slot ~0u, reads as unused pods).
+__device__ __forceinline__ void classify_groups(const DevState& S, const uint8_t* nflags, const PodGrp& g0,
+                                                const PodGrp& g1, uint32_t c0, uint32_t (&f)[AG_STRIDE],
+                                                uint64_t& pmask, bool trace) {
+    uint8_t n0[POD_PER_THREAD], n1[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        n0[k] = group_node_flags(S, nflags, g0, k);
+        n1[k] = group_node_flags(S, nflags, g1, k);
+    }
+    const GroupMasks m0 = group_masks(S, g0, n0), m1 = group_masks(S, g1, n1);
+    if (trace) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) S.trace[(size_t)blockIdx.x * TRACE_SLOTS + 12] = __builtin_amdgcn_s_memrealtime();
+    }
+    // configurePod (pod_controller.go:378-382): Use() every evaluated in-CIDR podIP;
+    // only addresses not already in `used` change the pool
+    const UsedWords u0 = used_words(S, g0, m0.usec), u1 = used_words(S, g1, m1.usec);
+    const uint32_t use0 = m0.usec & ~used_bits(S, g0, m0.usec, u0);
+    const uint32_t use1 = m1.usec & ~used_bits(S, g1, m1.usec, u1);
+    if (trace) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) S.trace[(size_t)blockIdx.x * TRACE_SLOTS + 13] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (count_group(S, g0, m0, use0, f)) pmask |= 1ull << c0;
+    if (count_group(S, g1, m1, use1, f)) pmask |= 1ull << (c0 + 1);
+}
+
+// block-wide totals of N u32 fields (every thread gets them; one barrier pair)
+template <int N>
+__device__ __forceinline__ void block_total(uint32_t (&v)[N]) {
+    __shared__ uint32_t part[BLOCK / 64][N];
+#pragma unroll
+    for (int f = 0; f < N; f++) {
+        const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v[f]), 63);
+        if (lane_id() == 0) part[wave_id()][f] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < N; f++) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) s += part[w][f];
+        v[f] = s;
+    }
+    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -980,7 +1072,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
 
 // ---------------------------------------------------------------------------
 // heartbeat stream: n_hb identical 1059-byte patches, 67 x 16 B each, from an
-// LDS template with non-temporal 16-byte stores (node_controller.go:145-157)
+// LDS template with 16-byte stores (node_controller.go:145-157)
 // ---------------------------------------------------------------------------
 constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
 __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
@@ -994,7 +1086,7 @@ __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tm
     for (; i < hi; i += BLOCK) {
         const uint4 v = tmpl[m];
         u32x4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, &dst[i]);  // write-once stream: do not keep in L2
+        dst[i] = w;  // plain stores: 7.4 TB/s vs 5.8 for nt on this fill (tools/micro/fill.hip)
         m += dm;
         if (m >= HB_CHUNKS) m -= HB_CHUNKS;
     }
@@ -1015,32 +1107,39 @@ __device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tm
 }
 
 // ---------------------------------------------------------------------------
-// header / exchange message (FRONT launch, written by the last arriver)
+// header / exchange message (FRONT launch, written by the last arriver).  The
+// header is assembled in LDS and stored with one coalesced pass to the device
+// copy and (single rank) the pinned host copy; the host reads it after the
+// launch completes.  Single rank: when a pool phase follows, its leader
+// publishes the Get plan / cursor (skip_alloc) and its stamps (skip_pool).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb) {
-    TickHdr* H = S.hdr;
+__device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb, uint64_t pool_index,
+                                                   TickHdr* L, uint64_t c_p1, bool prof) {
     const uint64_t* tot = r.tot;
     const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+    const bool single = S.world == 1;
     if (threadIdx.x == 0) {
         if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
             __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        H->n_hb = (uint32_t)tot[AG_HB];
-        H->n_init = (uint32_t)tot[AG_INIT];
-        H->init_bytes = tot[AG_INIT_BYTES];
-        H->n_del = (uint32_t)tot[AG_DEL];
-        H->n_pp = (uint32_t)tot[AG_PP];
-        H->pp_bytes = tot[AG_PP_BYTES];
-        H->n_alloc_local = (uint32_t)tot[AG_ALLOC];
-        H->n_lock = (uint32_t)tot[AG_LOCK];
-        H->n_eval = (uint32_t)tot[AG_EVAL];
-        H->n_rel = (uint32_t)tot[AG_REL];
-        H->n_use = S.world > 1 ? ld32_sc1(&S.list_counts[0]) : 0;
-        H->hb_base = 0;
-        H->init_base = patch_base;
-        H->pod_base = patch_base + tot[AG_INIT_BYTES];
-        H->arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
-        H->overflow = H->arena_bytes > S.arena_cap;
-        uint64_t* C = H->local_counters;
+        const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
+        L->n_hb = (uint32_t)tot[AG_HB];
+        L->n_init = (uint32_t)tot[AG_INIT];
+        L->n_pp = (uint32_t)tot[AG_PP];
+        L->n_del = (uint32_t)tot[AG_DEL];
+        L->n_use = nu;
+        L->n_rel = (uint32_t)tot[AG_REL];
+        L->n_alloc_local = (uint32_t)tot[AG_ALLOC];
+        L->n_eval = (uint32_t)tot[AG_EVAL];
+        L->n_lock = (uint32_t)tot[AG_LOCK];
+        L->init_bytes = tot[AG_INIT_BYTES];
+        L->pp_bytes = tot[AG_PP_BYTES];
+        L->hb_base = 0;
+        L->init_base = patch_base;
+        L->pod_base = patch_base + tot[AG_INIT_BYTES];
+        L->arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
+        L->overflow = L->arena_bytes > S.arena_cap;
+        L->pad0 = L->pad1 = 0;
+        uint64_t* C = L->local_counters;
         C[0] = tot[AG_HB];        // heartbeat
         C[1] = tot[AG_INIT];      // node_init
         C[2] = tot[AG_PP];        // pod_patch
@@ -1055,22 +1154,41 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
         C[11] = tot[AG_PENDING];  // pods_pending
         C[12] = tot[AG_RUNNING];  // pods_running
         for (int k = 13; k < 16; k++) C[k] = 0;
-        if (S.world > 1 || tot[AG_ALLOC] == 0) H->cursor_index = *S.pool_index;  // else: the pool phase
-        if (S.world == 1) {
-            for (int k = 0; k < 16; k++) H->counters[k] = C[k];
-            H->alloc_total = tot[AG_ALLOC];
-            H->alloc_base = 0;
-            H->rel_total = tot[AG_REL];
-            if (tot[AG_ALLOC] == 0) H->usable_total = H->take_usable = H->fresh_in = H->fresh_out_start = 0;
-        } else {
+        for (int k = 0; k < 16; k++) L->counters[k] = single ? C[k] : 0;
+        L->alloc_total = single ? tot[AG_ALLOC] : 0;
+        L->alloc_base = 0;
+        L->usable_total = L->take_usable = L->fresh_in = L->fresh_out_start = 0;
+        L->cursor_index = pool_index;  // the pool phase overwrites it when it allocates
+        L->rel_total = single ? tot[AG_REL] : 0;
+        for (int k = 0; k < 8; k++) L->clk[k] = 0;
+        L->clk[CLK_P1_MAX] = c_p1;
+        if (prof) {
+            L->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
+            __hip_atomic_store(&S.bar->neg_entry_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        L->clk[CLK_HDR] = __builtin_amdgcn_s_memrealtime();
+        if (!single) {
             XMsg* X = S.xmsg;
             X->alloc = tot[AG_ALLOC];
-            X->n_use = H->n_use;
-            X->n_rel = ld32_sc1(&S.list_counts[1]);
+            X->n_use = nu;
+            X->n_rel = nr;
             for (int k = 0; k < 16; k++) X->counters[k] = C[k];
         }
     }
-    if (S.world > 1) {  // exchange lists inline when they fit
+    __syncthreads();
+    constexpr int NW = offsetof(TickHdr, err) / 8;
+    constexpr int A0 = offsetof(TickHdr, usable_total) / 8, A1 = offsetof(TickHdr, rel_total) / 8;
+    constexpr int C0 = offsetof(TickHdr, clk) / 8;
+    const bool skip_alloc = single && tot[AG_ALLOC] != 0, skip_pool = single && (tot[AG_ALLOC] | tot[AG_REL]) != 0;
+    for (int i = threadIdx.x; i < NW; i += BLOCK) {
+        const uint64_t w = reinterpret_cast<const uint64_t*>(L)[i];
+        const bool pool_word = (i >= A0 && i < A1) || i == C0 + CLK_BACK || i == C0 + CLK_POOL;
+        // the pool leader may already have written its fields (it runs concurrently)
+        if (!(skip_pool && pool_word)) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
+        if (single && !(skip_alloc && i >= A0 && i < A1) && !(skip_pool && (i == C0 + CLK_BACK || i == C0 + CLK_POOL)))
+            reinterpret_cast<uint64_t*>(S.hdr_host)[i] = w;
+    }
+    if (!single) {  // exchange lists inline when they fit
         const uint32_t nu = ld32_sc1(&S.list_counts[0]), nr = ld32_sc1(&S.list_counts[1]);
         if (nu + nr <= (uint32_t)XINLINE) {
             for (uint32_t i = threadIdx.x; i < nu; i += BLOCK) S.xmsg->ips[i] = ld32_sc1(&S.use_list[i]);
@@ -1079,226 +1197,54 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
     }
 }
 
-// copy the device header to the pinned host copy (zero-copy publication).
-// Single rank: the pool leader publishes the pool fields (skip_alloc: the Get
-// plan and cursor) and its phase stamps (skip_pool) itself, concurrently.
-__device__ __forceinline__ void publish_header(const DevState& S, bool skip_alloc, bool skip_pool) {
-    constexpr int A0 = offsetof(TickHdr, usable_total) / 8, A1 = offsetof(TickHdr, rel_total) / 8;
-    constexpr int C0 = offsetof(TickHdr, clk) / 8;
+// multi rank (BACK launch, block 0): copy the device header to the pinned host copy
+__device__ __forceinline__ void publish_header(const DevState& S) {
     __syncthreads();
-    if (threadIdx.x < 64) {
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(S.hdr);
-        uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
-        for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += 64) {
-            if (skip_alloc && i >= A0 && i < A1) continue;
-            if (skip_pool && (i == C0 + CLK_BACK || i == C0 + CLK_POOL)) continue;
-            dst[i] = src[i];
-        }
-        __threadfence_system();
-    }
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(S.hdr);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
+    for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += BLOCK) dst[i] = src[i];
     __syncthreads();
 }
 
-// ---------------------------------------------------------------------------
-// k_tick: one controller tick.  Single rank: ONE launch (FRONT | BACK).
-// Multi rank: FRONT launch -> exchange -> BACK launch.
-//
-// Blocks [0, n_chain) are chain blocks, each owning a contiguous bucket range;
-// blocks [n_chain, grid) (FRONT only) stream the heartbeat bodies and touch
-// nothing else, so the bandwidth-bound stream overlaps the latency-bound
-// classification.
-//
-//   FRONT  per chain block: node states -> heartbeat handles (host-maintained
-//          base), node flags into LDS; live pod groups -> predicates, Use /
-//          Put; one block record; arrive.  The LAST arriver reduces the records
-//          into the tick header (single rank) / exchange message (multi rank).
-//          A block with nothing to emit is done here (the steady state).
-//   BACK   per dirty chain block (single rank: after every block arrived):
-//          prefix over the records; the pool phase among the dirty blocks when
-//          the tick has Gets or Puts (multi rank: among all blocks); emission
-//          of the dirty chunks.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
-                                                   uint32_t n_hb, int phases) {
+// pointers into k_tick's LDS for the out-of-line BACK phases
+struct TickLds {
+    uint32_t* recs;
+    PodJob* pod;
+    InitJob* node;
+    uint8_t* hb_tmpl;
+    uint32_t* nflags32;
+    uint32_t* gpre;
+    Sums* sums;
+    Layout* L;
+};
+
+// BACK phases of a chain block that has something to emit (and, multi rank,
+// every block when the pool phase runs): prefix over the records, ipPool phase,
+// emission.  Out of line so the steady-state path keeps its registers; the
+// device state is read through its copy in device memory (S.self).
+__device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l, uint32_t b, uint32_t bk0, uint32_t nbk,
+                                       uint64_t pod_mask, uint32_t node_mask, uint32_t my_init, bool have_sums,
+                                       int phases, uint32_t n_hb, uint64_t now_unix, uint64_t start_unix) {
+    const DevState& S = *G;
     const int t = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    __shared__ union {
-        PodJob pod[POD_CHUNK];
-        InitJob node[NODE_CHUNK];
-    } jobs;
-    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
-    __shared__ uint32_t nflags32[NODE_LDS / 4];
-    __shared__ uint32_t gpre[MAX_BPB + 1];
-    __shared__ uint32_t sh_mask[3];  // pod chunk mask lo / hi, node chunk mask
-    __shared__ Layout sh_L;
-    uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
-    const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
-#define TSTAMP(k)                                                                               \
-    do {                                                                                        \
-        if (S.trace && t == 0) S.trace[(size_t)b * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-    TSTAMP(0);
-
-    // ---- heartbeat streamers ------------------------------------------------------
-    if (b >= S.n_chain) {
-        build_hb_template(S, hb_tmpl, now_unix, start_unix);
-        hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
-        if ((phases & TICK_PROF) && t == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
-        TSTAMP(6);
-        return;
-    }
-
-    uint32_t bk0, nbk;
-    block_range(S, b, bk0, nbk);
-    const uint32_t nn = nbk * S.cn, nbase = bk0 * S.cn;
     TickHdr* H = S.hdr;
-    uint64_t pod_mask = 0;
-    uint32_t node_mask = 0;
-    uint32_t my_init = 0;
-    bool have_sums = false;
-    Sums sums;
-
-    if (phases & TICK_FRONT) {
-        if (t == 0) {
-            if (phases & TICK_PROF)
-                atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
-        if (t < 3) sh_mask[t] = 0;
-        load_gpre(S, bk0, nbk, gpre);  // its loads are in flight with the node loads below
-        uint32_t f[AG_STRIDE];
-#pragma unroll
-        for (int i = 0; i < AG_STRIDE; i++) f[i] = 0;
-        // ---- nodes: KeepNodeHeartbeat handles, needLockNode / configureNode (A.5) ----
-        uint32_t hb_run = S.hb_pre[b];
-        uint32_t nmask = 0;
-        for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
-            const uint32_t i = i0 + t * NODE_PER_THREAD;
-            const uint32_t packed = i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u;
-            uint32_t tick = 0, hb[1] = {0}, hbm = 0;
-            bool dirty = false;
-#pragma unroll
-            for (int k = 0; k < NODE_PER_THREAD; k++) {
-                const uint8_t s = (uint8_t)(packed >> (8 * k));
-                const NodeCls c = classify_node(s);
-                f[AG_HB] += c.hb;
-                f[AG_LOCK] += c.lock;
-                f[AG_MANAGED] += c.managed;
-                f[AG_READY] += c.ready;
-                if (c.init) {
-                    f[AG_INIT]++;
-                    f[AG_INIT_BYTES] += (init_patch_len(S.node_blob[nbase + i + k]) + 15u) & ~15u;
-                }
-                dirty |= c.init || (s & NS_EVENT_LOCK);
-                tick |= (uint32_t)node_tick_flags(s) << (8 * k);
-                hb[0] += c.hb;
-                hbm |= (uint32_t)c.hb << k;
-            }
-            if (i < nn) {
-                nflags32[i / 4] = tick;
-                if (S.world > 1) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
-            }
-            uint32_t tot[1];
-            block_excl_scan<1>(hb, tot);
-            uint32_t pos = hb_run + hb[0];
-#pragma unroll
-            for (int k = 0; k < NODE_PER_THREAD; k++)
-                if ((hbm >> k) & 1) {
-                    if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
-                    pos++;
-                }
-            hb_run += tot[0];
-            if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
-        }
-        __syncthreads();  // gpre and node flags
-        TSTAMP(1);
-        // ---- pods: two live groups per thread in flight ----------------------------
-        const uint32_t ng = gpre[nbk];
-        uint64_t pmask = 0;
-        for (uint32_t g0 = 0; g0 < ng; g0 += 2 * BLOCK) {
-            PodGrp G0, G1;
-            load_group(S, gpre, bk0, nbk, ng, g0 + t, G0);
-            load_group(S, gpre, bk0, nbk, ng, g0 + BLOCK + t, G1);
-            const uint32_t c0 = g0 / BLOCK;
-            if (classify_group(S, nflags, G0, f)) pmask |= 1ull << c0;
-            if (classify_group(S, nflags, G1, f)) pmask |= 1ull << (c0 + 1);
-        }
-        TSTAMP(2);
-        if (nmask) atomicOr(&sh_mask[2], nmask);
-        if (pmask) {
-            if ((uint32_t)pmask) atomicOr(&sh_mask[0], (uint32_t)pmask);
-            if ((uint32_t)(pmask >> 32)) atomicOr(&sh_mask[1], (uint32_t)(pmask >> 32));
-        }
-        block_sum<AG_STRIDE>(f);  // synchronises: the masks are complete
-        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
-        node_mask = sh_mask[2];
-        f[AG_DIRTY] = (pod_mask | node_mask) ? 1u : 0u;
-        my_init = f[AG_INIT];
-        if (S.world > 1 && t == 0) {
-            S.dmask[2 * b] = pod_mask;
-            S.dmask[2 * b + 1] = node_mask;
-        }
-        // ---- arrive; the last arriver writes the header / exchange message ---------
-        const uint64_t old = publish_and_arrive(S, b, f);
-        TSTAMP(3);
-        const bool last = (old + 1) % S.n_chain == 0;
-        if (last) {
-            const uint64_t c = __builtin_amdgcn_s_memrealtime();
-            reduce_records(S, b, sums);
-            have_sums = true;
-            if (t == 0) {
-                H->clk[CLK_P1_MAX] = c;
-                if (phases & TICK_PROF) {
-                    H->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
-                    __hip_atomic_store(&S.bar->neg_entry_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            write_front_header(S, sums, n_hb);
-            if (t == 0) H->clk[CLK_HDR] = __builtin_amdgcn_s_memrealtime();
-            if (S.world == 1) publish_header(S, sums.tot[AG_ALLOC] != 0, (sums.tot[AG_ALLOC] | sums.tot[AG_REL]) != 0);
-        }
-        if (!(phases & TICK_BACK)) return;
-        // single rank: a clean block is done; a dirty one waits for every record
-        if (!(pod_mask | node_mask)) {
-            TSTAMP(6);
-            return;
-        }
-        if (!last) {
-            wait_arrivals(S, (old / S.n_chain + 1) * S.n_chain);
-            reduce_records(S, b, sums);
-            have_sums = true;
-        }
-    } else {
-        // BACK launch (multi rank): this block's masks from the FRONT launch
-        if (t == 0) {
-            sh_mask[0] = (uint32_t)S.dmask[2 * b];
-            sh_mask[1] = (uint32_t)(S.dmask[2 * b] >> 32);
-            sh_mask[2] = (uint32_t)S.dmask[2 * b + 1];
-            if (b == 0) {
-                H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
-                S.list_counts[0] = 0;  // exchange lists for the next tick
-                S.list_counts[1] = 0;
-            }
-        }
-        __syncthreads();
-        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
-        node_mask = sh_mask[2];
-        my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
-    }
-    if (!have_sums) reduce_records(S, b, sums);
+    const uint32_t nn = nbk * S.cn, nbase = bk0 * S.cn;
+#define TSTAMP(k)                                                                                         \
+    do {                                                                                                  \
+        if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    if (!have_sums) reduce_records(S, b, l.recs, l.sums);
 
     // ---- pool phase (ticks with Gets or Puts) -------------------------------------
     const bool single = S.world == 1;
-    const uint64_t A = single ? sums.tot[AG_ALLOC] : H->alloc_total;
-    const uint64_t rel_total = single ? sums.tot[AG_REL] : H->rel_total;
+    const uint64_t A = single ? l.sums->tot[AG_ALLOC] : H->alloc_total;
+    const uint64_t rel_total = single ? l.sums->tot[AG_REL] : H->rel_total;
     const uint64_t alloc_base = single ? 0 : H->alloc_base;
-    const uint64_t n_alloc_local = sums.tot[AG_ALLOC];
+    const uint64_t n_alloc_local = l.sums->tot[AG_ALLOC];
     // participants: single rank - the dirty blocks (every Get / Put belongs to one);
     // multi rank - every block (each rank commits every rank's Gets to its replica)
-    const uint32_t np = single ? (uint32_t)sums.tot[AG_DIRTY] : S.n_chain;
-    const uint32_t pidx = single ? (uint32_t)sums.pre[AG_DIRTY] : b;
+    const uint32_t np = single ? (uint32_t)l.sums->tot[AG_DIRTY] : S.n_chain;
+    const uint32_t pidx = single ? (uint32_t)l.sums->pre[AG_DIRTY] : b;
     const bool dirty = (pod_mask | node_mask) != 0;
     PoolPlan plan{};
     if (A || rel_total) {
@@ -1348,7 +1294,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         }
         TSTAMP(5);
     }
-    if (!single && b == 0) publish_header(S, false, false);  // multi rank: counts, exchange totals and pool fields
+    if (!single && b == 0) publish_header(S);  // multi rank: counts, exchange totals and pool fields
     if (!dirty) {
         TSTAMP(6);
         return;
@@ -1356,35 +1302,245 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
 
     // ---- emission of the dirty chunks ----------------------------------------------
     if (!(phases & TICK_FRONT)) {  // BACK launch: the block's pod groups and node flags again
-        load_gpre(S, bk0, nbk, gpre);
+        load_gpre(S, bk0, nbk, l.gpre);
         if (pod_mask)
             for (uint32_t i = t * 4; i < nn; i += NODE_CHUNK)
-                nflags32[i / 4] = *reinterpret_cast<const uint32_t*>(S.node_tick + nbase + i);
+                l.nflags32[i / 4] = *reinterpret_cast<const uint32_t*>(S.node_tick + nbase + i);
         __syncthreads();
     }
-    if (node_mask && my_init) build_hb_template(S, hb_tmpl, now_unix, start_unix);
+    if (node_mask && my_init) build_hb_template(S, l.hb_tmpl, now_unix, start_unix);
     if (t == 0) {
         const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
-        sh_L.init_base = patch_base;
-        sh_L.pod_base = patch_base + sums.tot[AG_INIT_BYTES];
-        sh_L.alloc_base = alloc_base;
-        sh_L.plan = plan;
+        l.L->init_base = patch_base;
+        l.L->pod_base = patch_base + l.sums->tot[AG_INIT_BYTES];
+        l.L->alloc_base = alloc_base;
+        l.L->plan = plan;
     }
     __syncthreads();
-    const Layout L = sh_L;
+    const Layout L = *l.L;
     Bases run;
-    for (int f = 0; f < AG_NSCAN; f++) run.v[f] = sums.pre[f];
+    for (int f = 0; f < AG_NSCAN; f++) run.v[f] = l.sums->pre[f];
     for (uint32_t m = node_mask; m; m &= m - 1) {
         const uint32_t k = (uint32_t)__builtin_ctz(m);
-        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, hb_tmpl, jobs.node);
+        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, l.hb_tmpl, l.node);
     }
-    const uint32_t ng = gpre[nbk];
+    const uint32_t ng = l.gpre[nbk];
     for (uint64_t m = pod_mask; m; m &= m - 1) {
         const uint32_t c = (uint32_t)__builtin_ctzll(m);
-        emit_pod_chunk(S, gpre, nflags, bk0, nbk, ng, c, run, L, jobs.pod);
+        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.pod);
     }
     TSTAMP(6);
 #undef TSTAMP
+}
+
+// ---------------------------------------------------------------------------
+// k_tick: one controller tick.  Single rank: ONE launch (FRONT | BACK).
+// Multi rank: FRONT launch -> exchange -> BACK launch.
+//
+// Blocks [0, n_chain) are chain blocks, each owning a contiguous bucket range;
+// blocks [n_chain, grid) (FRONT only) stream the heartbeat bodies and touch
+// nothing else, so the bandwidth-bound stream overlaps the latency-bound
+// classification.
+//
+//   FRONT  per chain block: node states -> heartbeat handles (host-maintained
+//          base), node flags into LDS; live pod groups -> predicates, Use /
+//          Put; one block record; arrive.  The LAST arriver reduces the records
+//          into the tick header (single rank) / exchange message (multi rank).
+//          A block with nothing to emit is done here (the steady state).
+//   BACK   per dirty chain block (single rank: after every block arrived):
+//          prefix over the records; the pool phase among the dirty blocks when
+//          the tick has Gets or Puts (multi rank: among all blocks); emission
+//          of the dirty chunks.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
+                                                   uint32_t n_hb, int phases) {
+    const int t = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    __shared__ union {
+        PodJob pod[POD_CHUNK];
+        InitJob node[NODE_CHUNK];
+        uint32_t recs[MAX_CHAIN * REC_PITCH];  // reduce_records (before emission)
+    } jobs;
+    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
+    __shared__ uint32_t nflags32[NODE_LDS / 4];
+    __shared__ uint32_t gpre[MAX_BPB + 1];
+    __shared__ uint32_t sh_mask[3];  // pod chunk mask lo / hi, node chunk mask
+    __shared__ Sums sums;
+    __shared__ TickHdr sh_hdr;
+    __shared__ Layout sh_L;
+    uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
+    const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
+#define TSTAMP(k)                                                                                         \
+    do {                                                                                                  \
+        if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    // trace runs only: drain this wave's memory operations, then stamp (perturbs the overlap)
+#define TWAIT(k)                                                     \
+    do {                                                             \
+        if (S.trace) {                                               \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+            TSTAMP(k);                                               \
+        }                                                            \
+    } while (0)
+    TSTAMP(0);
+
+    // ---- heartbeat streamers ------------------------------------------------------
+    if (b >= S.n_chain) {
+        build_hb_template(S, hb_tmpl, now_unix, start_unix);
+        hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
+        if ((phases & TICK_PROF) && t == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+        TSTAMP(6);
+        return;
+    }
+
+    uint32_t bk0, nbk;
+    block_range(S, b, bk0, nbk);
+    const uint32_t nn = nbk * S.cn, nbase = bk0 * S.cn;
+    TickHdr* H = S.hdr;
+    uint64_t pod_mask = 0;
+    uint32_t node_mask = 0;
+    uint32_t my_init = 0;
+    bool have_sums = false;
+
+    if (phases & TICK_FRONT) {
+        if (t == 0 && (phases & TICK_PROF))
+            atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (t < 3) sh_mask[t] = 0;
+        const uint64_t pool_index = *S.pool_index;  // for the header, should this block arrive last
+        const uint32_t hb_base = S.hb_pre[b];
+        // round trip 1: the fill marks (-> live pod groups) and the first node chunk
+        load_gpre(S, bk0, nbk, gpre);
+        const uint32_t packed0 = (uint32_t)t * NODE_PER_THREAD < nn
+                                     ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + t * NODE_PER_THREAD)
+                                     : 0u;
+        __syncthreads();  // gpre
+        TWAIT(8);
+        // round trip 2 is issued now and lands while the nodes are classified
+        const uint32_t ng = gpre[nbk];
+        PodGrp G0, G1;
+        load_group(S, gpre, bk0, nbk, ng, t, G0);
+        load_group(S, gpre, bk0, nbk, ng, BLOCK + t, G1);
+        TWAIT(9);
+        uint32_t f[AG_STRIDE];
+#pragma unroll
+        for (int i = 0; i < AG_STRIDE; i++) f[i] = 0;
+        // ---- nodes: KeepNodeHeartbeat handles, needLockNode / configureNode (A.5) ----
+        uint32_t nmask = 0;
+        for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
+            const uint32_t i = i0 + t * NODE_PER_THREAD;
+            const uint32_t packed =
+                i0 == 0 ? packed0 : (i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u);
+            uint32_t tick = 0;
+            bool dirty = false;
+#pragma unroll
+            for (int k = 0; k < NODE_PER_THREAD; k++) {
+                const uint8_t s = (uint8_t)(packed >> (8 * k));
+                const NodeCls c = classify_node(s);
+                f[AG_HB] += c.hb;
+                f[AG_LOCK] += c.lock;
+                f[AG_MANAGED] += c.managed;
+                f[AG_READY] += c.ready;
+                if (c.init) {
+                    f[AG_INIT]++;
+                    f[AG_INIT_BYTES] += (init_patch_len(S.node_blob[nbase + i + k]) + 15u) & ~15u;
+                }
+                dirty |= c.init || (s & NS_EVENT_LOCK);
+                tick |= (uint32_t)node_tick_flags(s) << (8 * k);
+            }
+            if (i < nn) {
+                nflags32[i / 4] = tick;
+                if (S.world > 1) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
+            }
+            if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
+        }
+        __syncthreads();  // node flags
+        TSTAMP(1);
+        // ---- pods: two live groups per thread in flight ----------------------------
+        uint64_t pmask = 0;
+        classify_groups(S, nflags, G0, G1, 0, f, pmask, S.trace != nullptr);
+        TWAIT(10);
+        for (uint32_t g0 = 2 * BLOCK; g0 < ng; g0 += 2 * BLOCK) {
+            load_group(S, gpre, bk0, nbk, ng, g0 + t, G0);
+            load_group(S, gpre, bk0, nbk, ng, g0 + BLOCK + t, G1);
+            classify_groups(S, nflags, G0, G1, g0 / BLOCK, f, pmask, false);
+        }
+        TSTAMP(2);
+        if (nmask) atomicOr(&sh_mask[2], nmask);
+        if (pmask) {
+            if ((uint32_t)pmask) atomicOr(&sh_mask[0], (uint32_t)pmask);
+            if ((uint32_t)(pmask >> 32)) atomicOr(&sh_mask[1], (uint32_t)(pmask >> 32));
+        }
+        block_total<AG_STRIDE>(f);  // synchronises: the masks are complete
+        TWAIT(11);
+        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
+        node_mask = sh_mask[2];
+        f[AG_DIRTY] = (pod_mask | node_mask) ? 1u : 0u;
+        my_init = f[AG_INIT];
+        if (S.world > 1 && t == 0) {
+            S.dmask[2 * b] = pod_mask;
+            S.dmask[2 * b + 1] = node_mask;
+        }
+        // ---- arrive; the last arriver writes the header / exchange message ---------
+        const uint64_t old = publish_and_arrive(S, b, f);
+        TSTAMP(3);
+        // KeepNodeHeartbeat handles, in node order from the host-maintained base
+        // (node_controller.go:175-204), after the arrival: nothing waits on them
+        {
+            uint32_t hb_run = hb_base;
+            for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
+                const uint32_t i = i0 + t * NODE_PER_THREAD;
+                const uint32_t hbm = i < nn ? (nflags32[i / 4] >> 1) & 0x01010101u : 0u;  // NT_MANAGED of 4 nodes
+                uint32_t hb[1] = {(uint32_t)__popc(hbm)}, tot[1];
+                block_excl_scan<1>(hb, tot);
+                uint32_t pos = hb_run + hb[0];
+#pragma unroll
+                for (int k = 0; k < NODE_PER_THREAD; k++)
+                    if ((hbm >> (8 * k)) & 1) {
+                        if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
+                        pos++;
+                    }
+                hb_run += tot[0];
+            }
+        }
+        const bool last = (old + 1) % S.n_chain == 0;
+        if (last) {
+            const uint64_t c = __builtin_amdgcn_s_memrealtime();
+            reduce_records(S, b, jobs.recs, &sums);
+            have_sums = true;
+            write_front_header(S, sums, n_hb, pool_index, &sh_hdr, c, (phases & TICK_PROF) != 0);
+            TSTAMP(7);
+        }
+        if (!(phases & TICK_BACK)) return;
+        // single rank: a clean block is done; a dirty one waits for every record
+        if (!(pod_mask | node_mask)) {
+            TSTAMP(6);
+            return;
+        }
+        if (!last) wait_arrivals(S, (old / S.n_chain + 1) * S.n_chain);
+    } else {
+        // BACK launch (multi rank): this block's masks from the FRONT launch
+        if (t == 0) {
+            sh_mask[0] = (uint32_t)S.dmask[2 * b];
+            sh_mask[1] = (uint32_t)(S.dmask[2 * b] >> 32);
+            sh_mask[2] = (uint32_t)S.dmask[2 * b + 1];
+            if (b == 0) {
+                H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
+                S.list_counts[0] = 0;  // exchange lists for the next tick
+                S.list_counts[1] = 0;
+            }
+        }
+        __syncthreads();
+        pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
+        node_mask = sh_mask[2];
+        my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
+    }
+    tick_back(S.self, TickLds{jobs.recs, jobs.pod, jobs.node, hb_tmpl, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
+              pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix);
+#undef TSTAMP
+#undef TWAIT
 }
 
 // ---------------------------------------------------------------------------
