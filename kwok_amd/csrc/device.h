@@ -44,6 +44,7 @@ constexpr int MAX_BPB = 64;               // buckets per chain block
 constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS node flags)
 constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
 constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
+constexpr int SPEC_GROUPS = 3;            // pod groups per thread loaded before the fill marks land
 constexpr int TRACE_SLOTS = 16;           // KWOK_TICK_TRACE=1: per-block phase stamps
 
 // ---- fixed template geometry (default templates) -----------------------------
@@ -84,6 +85,9 @@ struct TickHdr {
     uint64_t clk[8];
     // host-visible only (not published): TICK_ERR_* set by a timed-out wait
     uint32_t err, pad2;
+    // single rank: the tick's field totals (AG_*), written by the chain block whose
+    // accumulator add completed each field; the host derives the header from them
+    uint64_t tot[16];
 };
 
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
@@ -107,7 +111,10 @@ struct GridBar {
     uint32_t pcnt, pad1[31];    // pool-phase barrier: arrivals of the current instance
     uint32_t pgen, pad2[31];    //                     generation
     unsigned long long neg_entry_max, p1_max, stream_end_max, pad3[13];  // profiled ticks
+    unsigned long long acc[16][16];  // single rank: field accumulators (arrivals << ACC_SHIFT | sum), one line each
 };
+constexpr int ACC_SHIFT = 54;  // arrivals in the top 10 bits (<= 1023 chain blocks), sums below
+constexpr unsigned long long ACC_MASK = (1ull << ACC_SHIFT) - 1;
 
 // exchange message, one per rank (allgather)
 constexpr int XINLINE = 2048;

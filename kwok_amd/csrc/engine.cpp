@@ -123,6 +123,10 @@ struct kwok_engine {
     DevState* d_S = nullptr;    // S in device memory (the kernel's out-of-line phases read it there)
     hipEvent_t done_ev = nullptr;  // tick completion (KWOK_SYNC=spin, the default)
     bool sync_spin = true;
+    bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
+    bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
+    uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
+    uint64_t front_launches = 0;  // FRONT launches since the cross-block state was last zeroed
     DevState* S_pin = nullptr;  // pinned staging for its upload
     DevState S_up{};            // the copy last uploaded
     // diagnostics
@@ -548,6 +552,12 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
         S.n_chain = (uint32_t)(cus * std::min(occ, want));
         e->n_stream = (uint32_t)(cus * wants);
+        if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
+        const char* pr = getenv("KWOK_TICK_PRIO");
+        e->chain_prio = pr && pr[0] == '1';
+        if (const char* v = getenv("KWOK_TICK_STREAM_DELAY_NS")) S.stream_delay = (uint32_t)std::max(0, atoi(v) / 10);
+        const char* ns = getenv("KWOK_TICK_NO_STREAM");
+        e->no_stream = ns && ns[0] == '1';
     }
     S.n_node_slots = e->NL;
     S.n_pod_slots = e->PL;
@@ -940,14 +950,17 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
         HIPCHK(e, hipMemcpyAsync(e->d_S, e->S_pin, sizeof(DevState), hipMemcpyHostToDevice, st));
         e->S_up = S;
     }
-    const int prof = ev ? TICK_PROF : 0;
+    const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
+    if (++e->tick_tag == 0) e->tick_tag = 1;
+    const uint64_t target = ++e->front_launches * S.n_chain;
     if (e->W == 1) {
-        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, st, ev ? ev[0] : nullptr,
-                    ev ? ev[1] : nullptr);
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, e->tick_tag, target, st,
+                    ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
         return KWOK_OK;
     }
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, e->tick_tag, target, st,
+                ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
     // one allgather of the fixed-size exchange message; a second one for
     // lists that did not fit inline (sizes known after the first)
     int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
@@ -988,11 +1001,41 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
     HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
     launch_xreduce(S, e->d_xall, e->W, e->rank, st);
     launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, e->tick_tag, target, st,
+                ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
     HIPCHK(e, hipGetLastError());
     return KWOK_OK;
 }
 }  // namespace
+
+// single rank: the kernel publishes the tick's field totals (TickHdr::tot); the
+// counts, output layout and counters follow from them
+static void derive_header(kwok_engine* e) {
+    TickHdr& H = *e->hdr_h;
+    const uint64_t* t = H.tot;
+    H.n_hb = (uint32_t)t[AG_HB];
+    H.n_init = (uint32_t)t[AG_INIT];
+    H.n_pp = (uint32_t)t[AG_PP];
+    H.n_del = (uint32_t)t[AG_DEL];
+    H.n_use = 0;
+    H.n_rel = (uint32_t)t[AG_REL];
+    H.n_alloc_local = (uint32_t)t[AG_ALLOC];
+    H.n_eval = (uint32_t)t[AG_EVAL];
+    H.n_lock = (uint32_t)t[AG_LOCK];
+    H.init_bytes = t[AG_INIT_BYTES];
+    H.pp_bytes = t[AG_PP_BYTES];
+    H.hb_base = 0;
+    H.init_base = (uint64_t)H.n_hb * HB_STRIDE;
+    H.pod_base = H.init_base + H.init_bytes;
+    H.arena_bytes = H.pod_base + H.pp_bytes;
+    H.overflow = H.arena_bytes > e->S.arena_cap;
+    const int map[13] = {AG_HB, AG_INIT, AG_PP, AG_DEL, AG_ALLOC, AG_REL, AG_EVAL,
+                         AG_LOCK, AG_MANAGED, AG_READY, AG_TOTAL, AG_PENDING, AG_RUNNING};
+    for (int k = 0; k < 16; k++) H.local_counters[k] = H.counters[k] = k < 13 ? t[map[k]] : 0;
+    H.alloc_total = t[AG_ALLOC];
+    H.alloc_base = 0;
+    H.rel_total = t[AG_REL];
+}
 
 static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && e->W == 1; }
 
@@ -1029,6 +1072,7 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
     hipStream_t st = e->st;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    memset(e->hdr_h->clk, 0, sizeof e->hdr_h->clk);  // this tick's stamps only (the launch orders it)
     {
         int rc = enqueue_tick(e, (uint64_t)now_unix);
         if (rc) return rc;
@@ -1046,12 +1090,14 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         HIPCHK(e, hipStreamSynchronize(st));
     }
     const auto t2 = clk::now();
+    if (e->W == 1) derive_header(e);
     const TickHdr& H = *e->hdr_h;
     if (trace_enabled(e)) trace_tick(e);
     if (H.err) {
         const uint32_t err = H.err;
         e->hdr_h->err = 0;
         (void)hipMemset(e->S.bar, 0, sizeof(GridBar));  // the next tick starts from a clean count
+        e->front_launches = 0;
         if (err & TICK_ERR_BARRIER)
             return e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
                            e->S.n_chain);

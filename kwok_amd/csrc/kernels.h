@@ -76,6 +76,7 @@ struct DevState {
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
     uint64_t* trace;           // [grid][TRACE_SLOTS] per-block phase stamps (KWOK_TICK_TRACE=1), else null
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
+    uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
@@ -87,9 +88,11 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
 // the tick kernel: n_chain chain blocks (+ n_stream heartbeat streamers in
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
 // with work to emit, so they must be co-resident (tick_occupancy).
-constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4;
+constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16;  // NOSTREAM: diagnostics only
+// tag: this tick's nonzero id (single-rank dirty records); arrive_target: the
+// arrival count at which every chain block of this FRONT launch has arrived
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
-                 hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+                 uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
 
 }  // namespace kwok

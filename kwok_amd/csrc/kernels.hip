@@ -630,16 +630,22 @@ __device__ __forceinline__ uint64_t row_sum16(uint64_t x) {  // lane 15 of each 
     x += dpp_src64<0x118, 0xF>(x);
     return x;
 }
-__device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, uint32_t* recs, Sums* out) {
+// tag != 0 (single rank): only dirty blocks publish records, marked with the
+// tick's tag in AG_DIRTY; any other record is stale and counts as zero (a clean
+// block has nothing in any scanned field).
+__device__ __forceinline__ void reduce_records(const DevState& S, uint32_t b, uint32_t tag, uint32_t* recs, Sums* out) {
     for (uint32_t j = threadIdx.x; j < S.n_chain; j += BLOCK) {
         const uint64_t* p = reinterpret_cast<const uint64_t*>(S.blockagg + (size_t)j * AG_STRIDE);
         uint64_t q[AG_STRIDE / 2];
 #pragma unroll
         for (int i = 0; i < AG_STRIDE / 2; i++) q[i] = ld_sc1(p + i);
+        const bool keep = !tag || (uint32_t)(q[AG_DIRTY / 2] >> (32 * (AG_DIRTY & 1))) == tag;
 #pragma unroll
         for (int i = 0; i < AG_STRIDE / 2; i++) {
-            recs[j * REC_PITCH + 2 * i] = (uint32_t)q[i];
-            recs[j * REC_PITCH + 2 * i + 1] = (uint32_t)(q[i] >> 32);
+            uint32_t lo = keep ? (uint32_t)q[i] : 0u, hi = keep ? (uint32_t)(q[i] >> 32) : 0u;
+            if (tag && 2 * i + 1 == AG_DIRTY) hi = keep ? 1u : 0u;
+            recs[j * REC_PITCH + 2 * i] = lo;
+            recs[j * REC_PITCH + 2 * i + 1] = hi;
         }
     }
     __syncthreads();
@@ -689,10 +695,12 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* gpre, uint32_t n
 
 // one 8-slot pod group: state, node index and podIP words (one HBM round trip)
 struct PodGrp {
-    uint32_t slot;  // first local slot; ~0u when the group index is past the block's groups
+    uint32_t slot;  // first local slot; ~0u when the group holds no pods
     uint32_t j;     // bucket within the block
-    uint16_t st[POD_PER_THREAD], nl[POD_PER_THREAD];
+    uint32_t stw[4], ndw[4];  // state / node-index words, two pods each (kept packed: registers)
     uint32_t ip[POD_PER_THREAD];
+    __device__ __forceinline__ uint32_t st(int k) const { return (stw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; }
+    __device__ __forceinline__ uint32_t nl(int k) const { return (ndw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; }
 };
 __device__ __forceinline__ void load_group(const DevState& S, const uint32_t* gpre, uint32_t bk0, uint32_t nbk,
                                            uint32_t ng, uint32_t gi, PodGrp& g) {
@@ -708,15 +716,10 @@ __device__ __forceinline__ void load_group(const DevState& S, const uint32_t* gp
         ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
         ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
     }
-    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w};
-    const uint32_t ndw[4] = {nd4.x, nd4.y, nd4.z, nd4.w};
-    const uint32_t ips[8] = {ipa.x, ipa.y, ipa.z, ipa.w, ipb.x, ipb.y, ipb.z, ipb.w};
-#pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        g.st[k] = (uint16_t)(stw[k >> 1] >> (16 * (k & 1)));
-        g.nl[k] = (uint16_t)(ndw[k >> 1] >> (16 * (k & 1)));
-        g.ip[k] = ips[k];
-    }
+    g.stw[0] = st4.x, g.stw[1] = st4.y, g.stw[2] = st4.z, g.stw[3] = st4.w;
+    g.ndw[0] = nd4.x, g.ndw[1] = nd4.y, g.ndw[2] = nd4.z, g.ndw[3] = nd4.w;
+    g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
+    g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
 }
 // could this pod need a patch (computePatchData), given it is evaluated?
 __device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
@@ -727,7 +730,7 @@ __device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
 __device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g, uint16_t (&sp)[POD_PER_THREAD]) {
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(g.st[k], g.ip[k]);
+    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(g.st(k), g.ip[k]);
     uint4 v = make_uint4(0, 0, 0, 0);
     if (any && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -735,7 +738,7 @@ __device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g
     for (int k = 0; k < POD_PER_THREAD; k++) sp[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
 }
 __device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uint8_t* nflags, const PodGrp& g, int k) {
-    return (g.st[k] & PS_USED) ? nflags[g.j * S.cn + g.nl[k]] : (uint8_t)0;
+    return (g.st(k) & PS_USED) ? nflags[g.j * S.cn + g.nl(k)] : (uint8_t)0;
 }
 
 // ---------------------------------------------------------------------------
@@ -752,32 +755,47 @@ struct GroupMasks {
     uint32_t del, eval, alloc, need, rel, usec, total, pend, run, dirty;
 };
 __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGrp& g, const uint8_t (&ntf)[POD_PER_THREAD]) {
+    // SWAR over the packed state words: each 32-bit op evaluates two pods (bit 0 and
+    // bit 16 of every plane); integer arithmetic keeps it all in VGPRs
+    static_assert(PS_USED == 1 && PS_DISREGARD == 2 && PS_DELETE_PENDING == 4 && PS_STATUS_NONEMPTY == 16 &&
+                      PS_CONFORMS == 32 && PS_EVENT == 64 && PS_HAS_HOST_IP == 128 && PS_PHASE_SHIFT == 8 &&
+                      NT_RELOCK == 1 && NT_MANAGED == 2 && PHASE_PENDING == 1 && PHASE_RUNNING == 2,
+                  "state bit layout");
+    constexpr uint32_t M = 0x00010001u;
+    // the CIDR spans at most 2^24 addresses (prefix >= 8): one u32 compare tests it
+    const uint32_t net = S.pool.net, size = (uint32_t)S.pool.size;
     GroupMasks m{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint32_t st = g.st[k], ip = g.ip[k], nf = ntf[k];
-        const uint32_t used = st & PS_USED;
-        const uint32_t del = used && (st & PS_DELETE_PENDING);
+    for (int w = 0; w < 4; w++) {
+        const uint32_t s = g.stw[w];
+        const uint32_t nf = (uint32_t)ntf[2 * w] | (uint32_t)ntf[2 * w + 1] << 16;
+        const uint32_t ia = g.ip[2 * w], ib = g.ip[2 * w + 1];
+        const uint32_t ipz = (ia == 0 ? 1u : 0u) | (ib == 0 ? M ^ 1u : 0u);
+        const uint32_t inc = ((ia - net < size ? 1u : 0u) | (ib - net < size ? M ^ 1u : 0u)) & ~ipz;
+        const uint32_t used = s & M, disr = (s >> 1) & M, del = used & (s >> 2);
+        const uint32_t nonempty = (s >> 4) & M, conf = (s >> 5) & M, event = (s >> 6) & M, hhost = (s >> 7) & M;
+        const uint32_t ph = (s >> 8) & (7u * M);
+        const uint32_t xr = ph ^ (PHASE_RUNNING * M), xp = ph ^ (PHASE_PENDING * M);
+        const uint32_t running = ~(xr | (xr >> 1) | (xr >> 2)) & M, pending = ~(xp | (xp >> 1) | (xp >> 2)) & M;
+        const uint32_t relock = nf & M, managed = (nf >> 1) & M;
+        const uint32_t live = used & ~del & M;
         // needLockPod / heartbeat re-lock (pod_controller.go:252-269, node_controller.go:152)
-        const uint32_t eval = used && !del && ((st & PS_EVENT) || ((nf & NT_RELOCK) && !(st & PS_DISREGARD)));
-        const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
-        const uint32_t ipz = ip == 0;
-        // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47)
-        const uint32_t alloc = eval && (st & PS_STATUS_NONEMPTY) && ipz;
+        const uint32_t eval = live & (event | (relock & ~disr));
         // computePatchData: Pending always patches; otherwise the strategic merge must change something
-        const uint32_t need = eval && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ipz);
-        const uint32_t inc = !ipz && (uint64_t)(ip - S.pool.net) < S.pool.size && ip >= S.pool.net;
-        const uint32_t total = used && !del;
-        m.del |= del << k;
-        m.eval |= eval << k;
-        m.alloc |= alloc << k;
-        m.need |= need << k;
-        m.rel |= (del && (nf & NT_MANAGED) && inc) << k;
-        m.usec |= (eval && inc) << k;
-        m.total |= total << k;
-        m.pend |= (total && !need && phase == PHASE_PENDING) << k;
-        m.run |= (total && (need || phase == PHASE_RUNNING)) << k;
-        m.dirty |= (del || need || (eval && (st & PS_EVENT))) << k;
+        const uint32_t need = eval & (((running & conf & hhost) ^ M) | ipz);
+        // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47)
+        const uint32_t alloc = eval & nonempty & ipz;
+        auto put = [w](uint32_t& mask, uint32_t plane) { mask |= ((plane & 1u) | ((plane >> 15) & 2u)) << (2 * w); };
+        put(m.del, del & M);
+        put(m.eval, eval);
+        put(m.alloc, alloc);
+        put(m.need, need);
+        put(m.rel, del & managed & inc);
+        put(m.usec, eval & inc);
+        put(m.total, live);
+        put(m.pend, live & ~need & pending);
+        put(m.run, live & (need | running));
+        put(m.dirty, (del & M) | need | (eval & event));
     }
     return m;
 }
@@ -829,9 +847,9 @@ __device__ __forceinline__ uint32_t used_bits(const DevState& S, const PodGrp& g
     return bits & usec;
 }
 
-// count one group and run its slow path; returns true when emission must
-// visit its chunk
-__device__ __forceinline__ bool count_group(const DevState& S, const PodGrp& g, const GroupMasks& m, uint32_t use,
+// counts of one group into f, and its rare pre-count work (wave-uniform entry):
+// the byte counts of patches (spec lengths) and the releases of deleted pods
+__device__ __forceinline__ void count_group(const DevState& S, const PodGrp& g, const GroupMasks& m,
                                             uint32_t (&f)[AG_STRIDE]) {
     f[AG_DEL] += __popc(m.del);
     f[AG_EVAL] += __popc(m.eval);
@@ -841,60 +859,76 @@ __device__ __forceinline__ bool count_group(const DevState& S, const PodGrp& g, 
     f[AG_TOTAL] += __popc(m.total);
     f[AG_PENDING] += __popc(m.pend);
     f[AG_RUNNING] += __popc(m.run);
-    if (__builtin_expect(__ballot((use | m.rel | m.need) != 0) != 0, 0)) {
-        // slow path (wave-uniform entry): pool bits / exchange lists, patch byte counts
+    if (__builtin_expect(__ballot((m.rel | m.need) != 0) != 0, 0)) {
         uint16_t sp[POD_PER_THREAD];
         load_spec_ids(S, g, sp);
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
             const uint32_t ip = g.ip[k];
             const uint64_t bit = ip - S.pool.net;
-            const bool u = (use >> k) & 1, r = (m.rel >> k) & 1;
+            const bool r = (m.rel >> k) & 1;
+            // the Deleted event of a pod we delete: Put if the node is managed and the IP in CIDR
+            // (pod_controller.go:329-336).  Single rank: the Put waits in rel_bm, folded in
+            // the pool phase after every Use of this tick (Use -> Put)
             if (S.world == 1) {
-                // single rank: Use() in place; the Put of a released address waits in rel_bm
-                // and is folded in the pool phase, after every Use of this tick (Use -> Put)
-                if (u) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
                 if (r) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
-            } else {  // ballots over every lane of the wave
-                wave_append(r, ip, S.rel_list, &S.list_counts[1]);
-                wave_append(u, ip, S.use_list, &S.list_counts[0]);
+            } else {
+                wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
             }
             if ((m.need >> k) & 1) f[AG_PP_BYTES] += S.specs[sp[k]].max_len;
         }
-        // the atomics / list entries are performed before this block arrives
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before this block arrives
     }
-    return m.dirty != 0;
 }
 
-// classify two loaded groups (their used-bitmap loads in flight together):
-// counts into f, dirty chunk bits c0 / c0 + 1 into pmask.  Uniform per wave up
-// to the lane masks (an empty group, slot ~0u, reads as unused pods).
-__device__ __forceinline__ void classify_groups(const DevState& S, const uint8_t* nflags, const PodGrp& g0,
-                                                const PodGrp& g1, uint32_t c0, uint32_t (&f)[AG_STRIDE],
-                                                uint64_t& pmask, bool trace) {
-    uint8_t n0[POD_PER_THREAD], n1[POD_PER_THREAD];
+// configurePod (pod_controller.go:378-382): Use() of the group's evaluated in-CIDR
+// podIPs that are not in `used` (wave-uniform entry; rare outside restarts)
+__device__ __forceinline__ void apply_uses(const DevState& S, const PodGrp& g, uint32_t use) {
+    if (__builtin_expect(__ballot(use != 0) != 0, 0)) {
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        n0[k] = group_node_flags(S, nflags, g0, k);
-        n1[k] = group_node_flags(S, nflags, g1, k);
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint32_t ip = g.ip[k];
+            const uint64_t bit = ip - S.pool.net;
+            const bool u = (use >> k) & 1;
+            if (S.world == 1) {
+                if (u) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
+            } else {
+                wave_append(u, ip, S.use_list, &S.list_counts[0]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before this block arrives
     }
-    const GroupMasks m0 = group_masks(S, g0, n0), m1 = group_masks(S, g1, n1);
-    if (trace) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (threadIdx.x == 0) S.trace[(size_t)blockIdx.x * TRACE_SLOTS + 12] = __builtin_amdgcn_s_memrealtime();
+}
+
+// one 8-slot group at a known slot (~0u: none), pods at or past `fill` read as empty
+__device__ __forceinline__ void load_group_at(const DevState& S, uint32_t slot, uint32_t j, PodGrp& g) {
+    uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
+    g.slot = slot;
+    g.j = j;
+    if (slot != ~0u) {
+        st4 = *reinterpret_cast<const uint4*>(S.pod_state + slot);
+        nd4 = *reinterpret_cast<const uint4*>(S.pod_node + slot);
+        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + slot);
+        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + slot + 4);
     }
-    // configurePod (pod_controller.go:378-382): Use() every evaluated in-CIDR podIP;
-    // only addresses not already in `used` change the pool
-    const UsedWords u0 = used_words(S, g0, m0.usec), u1 = used_words(S, g1, m1.usec);
-    const uint32_t use0 = m0.usec & ~used_bits(S, g0, m0.usec, u0);
-    const uint32_t use1 = m1.usec & ~used_bits(S, g1, m1.usec, u1);
-    if (trace) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (threadIdx.x == 0) S.trace[(size_t)blockIdx.x * TRACE_SLOTS + 13] = __builtin_amdgcn_s_memrealtime();
+    g.stw[0] = st4.x, g.stw[1] = st4.y, g.stw[2] = st4.z, g.stw[3] = st4.w;
+    g.ndw[0] = nd4.x, g.ndw[1] = nd4.y, g.ndw[2] = nd4.z, g.ndw[3] = nd4.w;
+    g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
+    g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
+}
+// a speculatively loaded group past its bucket's fill mark holds no pods
+__device__ __forceinline__ void clip_group(PodGrp& g, bool live) {
+    if (!live) {
+        g.slot = ~0u;
+#pragma unroll
+        for (int w = 0; w < 4; w++) g.stw[w] = 0;
     }
-    if (count_group(S, g0, m0, use0, f)) pmask |= 1ull << c0;
-    if (count_group(S, g1, m1, use1, f)) pmask |= 1ull << (c0 + 1);
+}
+__device__ __forceinline__ GroupMasks masks_of(const DevState& S, const uint8_t* nflags, const PodGrp& g) {
+    uint8_t n[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) n[k] = group_node_flags(S, nflags, g, k);
+    return group_masks(S, g, n);
 }
 
 // block-wide totals of N u32 fields (every thread gets them; one barrier pair)
@@ -993,7 +1027,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
-        cl[k] = classify_pod(g.st[k], group_node_flags(S, nflags, g, k), g.ip[k]);
+        cl[k] = classify_pod(g.st(k), group_node_flags(S, nflags, g, k), g.ip[k]);
         v[0] += cl[k].del;
         if (cl[k].need) {
             v[1]++;
@@ -1012,7 +1046,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     for (int k = 0; k < POD_PER_THREAD; k++) {
         const uint32_t slot = g.slot + k;
         const int32_t handle = S.pod_handle_base + (int32_t)slot;
-        uint16_t s = g.st[k];
+        uint16_t s = g.st(k);
         if (cl[k].del) {
             const uint64_t ord = run.v[AG_DEL] + v[0]++;
             S.del_pods[ord] = handle;
@@ -1049,7 +1083,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
             }
             s &= (uint16_t)~PS_EVENT;
         }
-        dirty |= s != g.st[k];
+        dirty |= s != g.st(k);
         nst[k] = s;
     }
     if (g.slot != ~0u && dirty) {
@@ -1075,10 +1109,9 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
 // LDS template with 16-byte stores (node_controller.go:145-157)
 // ---------------------------------------------------------------------------
 constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
-__device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
+// 16-byte units [lo, hi) of the heartbeat region
+__device__ __forceinline__ void hb_fill_units(const DevState& S, const uint4* tmpl, uint64_t lo, uint64_t hi) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t nchunks = n_hb * HB_CHUNKS;
-    const uint64_t lo = nchunks * idx / cnt, hi = nchunks * (idx + 1) / cnt;
     u32x4* dst = reinterpret_cast<u32x4*>(S.arena);  // heartbeat region starts at arena offset 0
     uint64_t i = lo + threadIdx.x;
     uint32_t m = (uint32_t)(i % HB_CHUNKS);
@@ -1090,6 +1123,12 @@ __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tm
         m += dm;
         if (m >= HB_CHUNKS) m -= HB_CHUNKS;
     }
+}
+
+// this streamer's share of the heartbeat stream (static, contiguous)
+__device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
+    const uint64_t units = n_hb * HB_CHUNKS;
+    hb_fill_units(S, tmpl, units * idx / cnt, units * (idx + 1) / cnt);
 }
 
 // per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
@@ -1113,87 +1152,93 @@ __device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tm
 // launch completes.  Single rank: when a pool phase follows, its leader
 // publishes the Get plan / cursor (skip_alloc) and its stamps (skip_pool).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb, uint64_t pool_index,
-                                                   TickHdr* L, uint64_t c_p1, bool prof) {
-    const uint64_t* tot = r.tot;
+// word i of the tick header (TickHdr as 61 x u64), computed by thread i
+__device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint32_t n_hb, uint32_t nu,
+                                                uint64_t pool_index, uint64_t arena_cap, bool single, const uint64_t* clk) {
+    constexpr int W_LC = offsetof(TickHdr, local_counters) / 8, W_C = offsetof(TickHdr, counters) / 8;
+    constexpr int W_CLK = offsetof(TickHdr, clk) / 8;
+    static_assert(offsetof(TickHdr, init_bytes) == 48 && offsetof(TickHdr, local_counters) == 96 &&
+                      offsetof(TickHdr, alloc_total) == 352 && offsetof(TickHdr, clk) == 416 &&
+                      offsetof(TickHdr, err) == 480,
+                  "TickHdr layout");
     const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+    const uint64_t arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
+    auto pair = [](uint64_t lo, uint64_t hi) { return (uint64_t)(uint32_t)lo | (uint64_t)(uint32_t)hi << 32; };
+    if (i >= W_LC && i < W_C + 16) {
+        // local_counters / counters: heartbeat, node_init, pod_patch, delete, alloc, release,
+        // evaluated, lock_checked, nodes_managed, nodes_ready, pods_total, pods_pending, pods_running
+        const int k = (i - W_LC) & 15;
+        constexpr uint64_t MAP = (uint64_t)AG_HB | (uint64_t)AG_INIT << 4 | (uint64_t)AG_PP << 8 | (uint64_t)AG_DEL << 12 |
+                                 (uint64_t)AG_ALLOC << 16 | (uint64_t)AG_REL << 20 | (uint64_t)AG_EVAL << 24 |
+                                 (uint64_t)AG_LOCK << 28 | (uint64_t)AG_MANAGED << 32 | (uint64_t)AG_READY << 36 |
+                                 (uint64_t)AG_TOTAL << 40 | (uint64_t)AG_PENDING << 44 | (uint64_t)AG_RUNNING << 48;
+        if (k >= 13 || (i >= W_C && !single)) return 0;  // fleet counters: k_xreduce (multi rank)
+        return tot[(MAP >> (4 * k)) & 15];
+    }
+    if (i >= W_CLK && i < W_CLK + 8) return clk[i - W_CLK];
+    switch (i) {
+        case 0: return pair(tot[AG_HB], tot[AG_INIT]);
+        case 1: return pair(tot[AG_PP], tot[AG_DEL]);
+        case 2: return pair(nu, tot[AG_REL]);
+        case 3: return pair(tot[AG_ALLOC], tot[AG_EVAL]);
+        case 4: return pair(tot[AG_LOCK], arena_bytes > arena_cap);
+        case 6: return tot[AG_INIT_BYTES];
+        case 7: return tot[AG_PP_BYTES];
+        case 9: return patch_base;                        // init_base (hb_base, word 8, is 0)
+        case 10: return patch_base + tot[AG_INIT_BYTES];  // pod_base
+        case 11: return arena_bytes;
+        case 44: return single ? tot[AG_ALLOC] : 0;       // alloc_total (alloc_base, word 45, is 0)
+        case 50: return pool_index;                       // cursor_index: the pool phase overwrites it
+        case 51: return single ? tot[AG_REL] : 0;         // rel_total
+        default: return 0;                                // pads, hb_base, alloc_base, the Get plan
+    }
+}
+
+// ---------------------------------------------------------------------------
+// header / exchange message (FRONT launch, written by the last arriver): one
+// header word per thread, stored to the device copy and (single rank) the
+// pinned host copy; the host reads it after the launch completes.  Single
+// rank: when a pool phase follows, its leader publishes the Get plan / cursor
+// (skip_alloc) and its stamps (skip_pool) itself, concurrently.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb, uint64_t pool_index,
+                                                   uint64_t c_p1, bool prof) {
+    const uint64_t* tot = r.tot;
     const bool single = S.world == 1;
-    if (threadIdx.x == 0) {
+    const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
+    uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    clk[CLK_P1_MAX] = c_p1;
+    if (prof) clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
+    clk[CLK_HDR] = __builtin_amdgcn_s_memrealtime();
+    constexpr int NW = offsetof(TickHdr, err) / 8;
+    constexpr int A0 = offsetof(TickHdr, usable_total) / 8, A1 = offsetof(TickHdr, rel_total) / 8;
+    constexpr int C0 = offsetof(TickHdr, clk) / 8;
+    const bool skip_alloc = single && tot[AG_ALLOC] != 0, skip_pool = single && (tot[AG_ALLOC] | tot[AG_REL]) != 0;
+    const int i = threadIdx.x;
+    if (i < NW) {
+        const uint64_t w = header_word(i, tot, n_hb, nu, pool_index, S.arena_cap, single, clk);
+        const bool pool_clk = i == C0 + CLK_BACK || i == C0 + CLK_POOL;
+        // the pool leader may already have written its fields (it runs concurrently)
+        if (!(skip_pool && (pool_clk || (i >= A0 && i < A1)))) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
+        if (single && !(skip_alloc && i >= A0 && i < A1) && !(skip_pool && pool_clk))
+            reinterpret_cast<uint64_t*>(S.hdr_host)[i] = w;
+    }
+    if (i == 0) {
         if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
             __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
-        L->n_hb = (uint32_t)tot[AG_HB];
-        L->n_init = (uint32_t)tot[AG_INIT];
-        L->n_pp = (uint32_t)tot[AG_PP];
-        L->n_del = (uint32_t)tot[AG_DEL];
-        L->n_use = nu;
-        L->n_rel = (uint32_t)tot[AG_REL];
-        L->n_alloc_local = (uint32_t)tot[AG_ALLOC];
-        L->n_eval = (uint32_t)tot[AG_EVAL];
-        L->n_lock = (uint32_t)tot[AG_LOCK];
-        L->init_bytes = tot[AG_INIT_BYTES];
-        L->pp_bytes = tot[AG_PP_BYTES];
-        L->hb_base = 0;
-        L->init_base = patch_base;
-        L->pod_base = patch_base + tot[AG_INIT_BYTES];
-        L->arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
-        L->overflow = L->arena_bytes > S.arena_cap;
-        L->pad0 = L->pad1 = 0;
-        uint64_t* C = L->local_counters;
-        C[0] = tot[AG_HB];        // heartbeat
-        C[1] = tot[AG_INIT];      // node_init
-        C[2] = tot[AG_PP];        // pod_patch
-        C[3] = tot[AG_DEL];       // delete
-        C[4] = tot[AG_ALLOC];     // alloc
-        C[5] = tot[AG_REL];       // release
-        C[6] = tot[AG_EVAL];      // evaluated
-        C[7] = tot[AG_LOCK];      // lock_checked
-        C[8] = tot[AG_MANAGED];   // nodes_managed
-        C[9] = tot[AG_READY];     // nodes_ready
-        C[10] = tot[AG_TOTAL];    // pods_total
-        C[11] = tot[AG_PENDING];  // pods_pending
-        C[12] = tot[AG_RUNNING];  // pods_running
-        for (int k = 13; k < 16; k++) C[k] = 0;
-        for (int k = 0; k < 16; k++) L->counters[k] = single ? C[k] : 0;
-        L->alloc_total = single ? tot[AG_ALLOC] : 0;
-        L->alloc_base = 0;
-        L->usable_total = L->take_usable = L->fresh_in = L->fresh_out_start = 0;
-        L->cursor_index = pool_index;  // the pool phase overwrites it when it allocates
-        L->rel_total = single ? tot[AG_REL] : 0;
-        for (int k = 0; k < 8; k++) L->clk[k] = 0;
-        L->clk[CLK_P1_MAX] = c_p1;
-        if (prof) {
-            L->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
-            __hip_atomic_store(&S.bar->neg_entry_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        L->clk[CLK_HDR] = __builtin_amdgcn_s_memrealtime();
+        if (prof) __hip_atomic_store(&S.bar->neg_entry_max, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!single) {
             XMsg* X = S.xmsg;
             X->alloc = tot[AG_ALLOC];
             X->n_use = nu;
             X->n_rel = nr;
-            for (int k = 0; k < 16; k++) X->counters[k] = C[k];
+            constexpr int LC = offsetof(TickHdr, local_counters) / 8;
+            for (int k = 0; k < 16; k++) X->counters[k] = header_word(LC + k, tot, n_hb, nu, pool_index, S.arena_cap, single, clk);
         }
     }
-    __syncthreads();
-    constexpr int NW = offsetof(TickHdr, err) / 8;
-    constexpr int A0 = offsetof(TickHdr, usable_total) / 8, A1 = offsetof(TickHdr, rel_total) / 8;
-    constexpr int C0 = offsetof(TickHdr, clk) / 8;
-    const bool skip_alloc = single && tot[AG_ALLOC] != 0, skip_pool = single && (tot[AG_ALLOC] | tot[AG_REL]) != 0;
-    for (int i = threadIdx.x; i < NW; i += BLOCK) {
-        const uint64_t w = reinterpret_cast<const uint64_t*>(L)[i];
-        const bool pool_word = (i >= A0 && i < A1) || i == C0 + CLK_BACK || i == C0 + CLK_POOL;
-        // the pool leader may already have written its fields (it runs concurrently)
-        if (!(skip_pool && pool_word)) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
-        if (single && !(skip_alloc && i >= A0 && i < A1) && !(skip_pool && (i == C0 + CLK_BACK || i == C0 + CLK_POOL)))
-            reinterpret_cast<uint64_t*>(S.hdr_host)[i] = w;
-    }
-    if (!single) {  // exchange lists inline when they fit
-        const uint32_t nu = ld32_sc1(&S.list_counts[0]), nr = ld32_sc1(&S.list_counts[1]);
-        if (nu + nr <= (uint32_t)XINLINE) {
-            for (uint32_t i = threadIdx.x; i < nu; i += BLOCK) S.xmsg->ips[i] = ld32_sc1(&S.use_list[i]);
-            for (uint32_t i = threadIdx.x; i < nr; i += BLOCK) S.xmsg->ips[nu + i] = ld32_sc1(&S.rel_list[i]);
-        }
+    if (!single && nu + nr <= (uint32_t)XINLINE) {  // exchange lists inline when they fit
+        for (uint32_t j = threadIdx.x; j < nu; j += BLOCK) S.xmsg->ips[j] = ld32_sc1(&S.use_list[j]);
+        for (uint32_t j = threadIdx.x; j < nr; j += BLOCK) S.xmsg->ips[nu + j] = ld32_sc1(&S.rel_list[j]);
     }
 }
 
@@ -1204,6 +1249,27 @@ __device__ __forceinline__ void publish_header(const DevState& S) {
     uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
     for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += BLOCK) dst[i] = src[i];
     __syncthreads();
+}
+
+// KeepNodeHeartbeat handles (node_controller.go:175-204): the block's managed
+// nodes in node order from the host-maintained base, after the block arrived
+// (nothing waits on them)
+__device__ __forceinline__ void write_hb_handles(const DevState& S, const uint32_t* nflags32, uint32_t nbase, uint32_t nn,
+                                                 uint32_t hb_run) {
+    for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
+        const uint32_t i = i0 + threadIdx.x * NODE_PER_THREAD;
+        const uint32_t hbm = i < nn ? (nflags32[i / 4] >> 1) & 0x01010101u : 0u;  // NT_MANAGED of 4 nodes
+        uint32_t hb[1] = {(uint32_t)__popc(hbm)}, tot[1];
+        block_excl_scan<1>(hb, tot);
+        uint32_t pos = hb_run + hb[0];
+#pragma unroll
+        for (int k = 0; k < NODE_PER_THREAD; k++)
+            if ((hbm >> (8 * k)) & 1) {
+                if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
+                pos++;
+            }
+        hb_run += tot[0];
+    }
 }
 
 // pointers into k_tick's LDS for the out-of-line BACK phases
@@ -1233,7 +1299,7 @@ __device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l
     do {                                                                                                  \
         if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-    if (!have_sums) reduce_records(S, b, l.recs, l.sums);
+    if (!have_sums) reduce_records(S, b, 0, l.recs, l.sums);
 
     // ---- pool phase (ticks with Gets or Puts) -------------------------------------
     const bool single = S.world == 1;
@@ -1353,7 +1419,7 @@ __device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l
 //          of the dirty chunks.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
-                                                   uint32_t n_hb, int phases) {
+                                                   uint32_t n_hb, int phases, uint32_t tag, uint64_t arrive_target) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     __shared__ union {
@@ -1364,9 +1430,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ uint4 hb_tmpl4[HB_CHUNKS];
     __shared__ uint32_t nflags32[NODE_LDS / 4];
     __shared__ uint32_t gpre[MAX_BPB + 1];
-    __shared__ uint32_t sh_mask[3];  // pod chunk mask lo / hi, node chunk mask
+    __shared__ uint32_t sh_mask[4];  // pod chunk mask lo / hi, node chunk mask, most groups in a bucket
     __shared__ Sums sums;
-    __shared__ TickHdr sh_hdr;
     __shared__ Layout sh_L;
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
@@ -1387,7 +1452,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     // ---- heartbeat streamers ------------------------------------------------------
     if (b >= S.n_chain) {
         build_hb_template(S, hb_tmpl, now_unix, start_unix);
-        hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
+        if (S.stream_delay) {  // diagnostics: hold the stream back while the chain's first round trips run
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < S.stream_delay) __builtin_amdgcn_s_sleep(4);
+        }
+        if (!(phases & TICK_NOSTREAM)) hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
         if ((phases & TICK_PROF) && t == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1396,6 +1465,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         return;
     }
 
+    if (phases & TICK_PRIO) __builtin_amdgcn_s_setprio(3);  // chain waves issue ahead of the streamers
     uint32_t bk0, nbk;
     block_range(S, b, bk0, nbk);
     const uint32_t nn = nbk * S.cn, nbase = bk0 * S.cn;
@@ -1409,25 +1479,32 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         if (t == 0 && (phases & TICK_PROF))
             atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (t < 3) sh_mask[t] = 0;
-        const uint64_t pool_index = *S.pool_index;  // for the header, should this block arrive last
+        const bool single = S.world == 1;
         const uint32_t hb_base = S.hb_pre[b];
-        // round trip 1: the fill marks (-> live pod groups) and the first node chunk
-        load_gpre(S, bk0, nbk, gpre);
+        // round trip 1, all loads independent: the fill marks, the node states and,
+        // speculatively, SPEC_GROUPS pod groups per thread at a static thread ->
+        // (bucket, group) map; groups past a bucket's fill mark are discarded when it
+        // lands (a bucket with more groups takes one more round trip per extra row)
+        const uint32_t tpb = BLOCK / (nbk ? nbk : 1u);  // threads per bucket
+        const uint32_t j = t / tpb, l = t - j * tpb;
+        const bool jv = j < nbk;
+        const uint32_t gcap = S.cp / POD_PER_THREAD;
+        const uint32_t fill = jv ? S.pod_fill[bk0 + j] : 0u;
+        PodGrp G[SPEC_GROUPS];
+#pragma unroll
+        for (int q = 0; q < SPEC_GROUPS; q++) {
+            const uint32_t a = l + q * tpb;
+            load_group_at(S, jv && a < gcap ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, G[q]);
+        }
         const uint32_t packed0 = (uint32_t)t * NODE_PER_THREAD < nn
                                      ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + t * NODE_PER_THREAD)
                                      : 0u;
-        __syncthreads();  // gpre
-        TWAIT(8);
-        // round trip 2 is issued now and lands while the nodes are classified
-        const uint32_t ng = gpre[nbk];
-        PodGrp G0, G1;
-        load_group(S, gpre, bk0, nbk, ng, t, G0);
-        load_group(S, gpre, bk0, nbk, ng, BLOCK + t, G1);
-        TWAIT(9);
+        const uint64_t pool_index = single ? 0 : *S.pool_index;  // multi rank: the header's default cursor
+        if (jv && l == 0) gpre[j + 1] = fill / POD_PER_THREAD;
         uint32_t f[AG_STRIDE];
 #pragma unroll
         for (int i = 0; i < AG_STRIDE; i++) f[i] = 0;
-        // ---- nodes: KeepNodeHeartbeat handles, needLockNode / configureNode (A.5) ----
+        // ---- nodes: needLockNode / configureNode (A.5), node flags for the pods -----
         uint32_t nmask = 0;
         for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
             const uint32_t i = i0 + t * NODE_PER_THREAD;
@@ -1452,20 +1529,49 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             }
             if (i < nn) {
                 nflags32[i / 4] = tick;
-                if (S.world > 1) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
+                if (!single) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
             }
             if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
         }
-        __syncthreads();  // node flags
+        __syncthreads();  // node flags, fill marks
+        if (t < 64) {     // gpre: live groups of the buckets before j; the block's largest bucket
+            const uint32_t g = t < (int)nbk ? gpre[t + 1] : 0u;
+            const uint32_t inc = wave_incl_scan(g);
+            uint32_t mx = g;
+            for (int o = 32; o; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+            gpre[t + 1] = inc;
+            if (t == 0) gpre[0] = 0, sh_mask[3] = mx;
+        }
+        __syncthreads();
         TSTAMP(1);
-        // ---- pods: two live groups per thread in flight ----------------------------
+        // ---- pods: the speculative groups, then any further rows (rare) ------------
         uint64_t pmask = 0;
-        classify_groups(S, nflags, G0, G1, 0, f, pmask, S.trace != nullptr);
-        TWAIT(10);
-        for (uint32_t g0 = 2 * BLOCK; g0 < ng; g0 += 2 * BLOCK) {
-            load_group(S, gpre, bk0, nbk, ng, g0 + t, G0);
-            load_group(S, gpre, bk0, nbk, ng, g0 + BLOCK + t, G1);
-            classify_groups(S, nflags, G0, G1, g0 / BLOCK, f, pmask, false);
+        uint32_t usec[SPEC_GROUPS];  // single rank: Use candidates, checked after the accumulator adds
+#pragma unroll
+        for (int q = 0; q < SPEC_GROUPS; q++) {
+            const uint32_t a = l + q * tpb;
+            clip_group(G[q], jv && a * POD_PER_THREAD < fill);
+            const GroupMasks m = masks_of(S, nflags, G[q]);
+            count_group(S, G[q], m, f);
+            // emission chunks are runs of 256 live groups in slot order (gpre)
+            if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+            usec[q] = m.usec;
+            if (!single) {  // multi rank: Use lists before the record (the exchange message carries them)
+                const UsedWords u = used_words(S, G[q], m.usec);
+                apply_uses(S, G[q], m.usec & ~used_bits(S, G[q], m.usec, u));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const uint32_t maxg = sh_mask[3];
+        for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += tpb) {
+            PodGrp H;
+            const uint32_t a = l + a0;
+            load_group_at(S, jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, H);
+            const GroupMasks m = masks_of(S, nflags, H);
+            count_group(S, H, m, f);
+            if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+            const UsedWords u = used_words(S, H, m.usec);
+            apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
         }
         TSTAMP(2);
         if (nmask) atomicOr(&sh_mask[2], nmask);
@@ -1474,52 +1580,84 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if ((uint32_t)(pmask >> 32)) atomicOr(&sh_mask[1], (uint32_t)(pmask >> 32));
         }
         block_total<AG_STRIDE>(f);  // synchronises: the masks are complete
-        TWAIT(11);
         pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
         node_mask = sh_mask[2];
-        f[AG_DIRTY] = (pod_mask | node_mask) ? 1u : 0u;
+        const bool dirty = (pod_mask | node_mask) != 0;
         my_init = f[AG_INIT];
-        if (S.world > 1 && t == 0) {
-            S.dmask[2 * b] = pod_mask;
-            S.dmask[2 * b + 1] = node_mask;
-        }
-        // ---- arrive; the last arriver writes the header / exchange message ---------
-        const uint64_t old = publish_and_arrive(S, b, f);
-        TSTAMP(3);
-        // KeepNodeHeartbeat handles, in node order from the host-maintained base
-        // (node_controller.go:175-204), after the arrival: nothing waits on them
-        {
-            uint32_t hb_run = hb_base;
-            for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
-                const uint32_t i = i0 + t * NODE_PER_THREAD;
-                const uint32_t hbm = i < nn ? (nflags32[i / 4] >> 1) & 0x01010101u : 0u;  // NT_MANAGED of 4 nodes
-                uint32_t hb[1] = {(uint32_t)__popc(hbm)}, tot[1];
-                block_excl_scan<1>(hb, tot);
-                uint32_t pos = hb_run + hb[0];
+        if (single) {
+            // ---- single rank: field accumulators; no block waits for another --------
+            // A dirty block first publishes its record (tagged with this tick) for the
+            // emission prefix of the dirty blocks after it.
+            f[AG_DIRTY] = dirty ? tag : 0u;
+            if (dirty && t < AG_STRIDE / 2) {
+                uint64_t w = 0;  // (selects, not f[2 * t]: a lane-indexed array would live in scratch)
 #pragma unroll
-                for (int k = 0; k < NODE_PER_THREAD; k++)
-                    if ((hbm >> (8 * k)) & 1) {
-                        if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
-                        pos++;
-                    }
-                hb_run += tot[0];
+                for (int i = 0; i < AG_STRIDE / 2; i++)
+                    w = t == i ? ((uint64_t)f[2 * i] | (uint64_t)f[2 * i + 1] << 32) : w;
+                st_sc1(reinterpret_cast<uint64_t*>(S.blockagg + (size_t)b * AG_STRIDE) + t, w);
             }
-        }
-        const bool last = (old + 1) % S.n_chain == 0;
-        if (last) {
-            const uint64_t c = __builtin_amdgcn_s_memrealtime();
-            reduce_records(S, b, jobs.recs, &sums);
+            // the Use checks of the speculative groups, in flight with the accumulator adds
+            UsedWords u[SPEC_GROUPS];
+#pragma unroll
+            for (int q = 0; q < SPEC_GROUPS; q++) u[q] = used_words(S, G[q], usec[q]);
+            if (t < AG_DIRTY) {
+                // lane t owns field t: one returning add of (one arrival | this block's
+                // value); the block whose add completes the count holds the tick's total
+                uint32_t v = 0;
+#pragma unroll
+                for (int i = 0; i < AG_DIRTY; i++) v = t == i ? f[i] : v;
+                unsigned long long* acc = &S.bar->acc[t][0];
+                const unsigned long long old = atomicAdd(acc, (1ull << ACC_SHIFT) | v);
+                if ((old >> ACC_SHIFT) == S.n_chain - 1u) {
+                    const uint64_t total = (old & ACC_MASK) + v;
+                    st_sc1(acc, 0ull);  // the next tick starts from zero
+                    S.hdr_host->tot[t] = total;
+                    if (t == AG_HB) {
+                        if (total != n_hb)  // the heartbeat stream was laid out for the host's count
+                            __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        S.hdr_host->clk[CLK_P1_MAX] = __builtin_amdgcn_s_memrealtime();
+                        if (phases & TICK_PROF) {
+                            S.hdr_host->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
+                            st_sc1(&S.bar->neg_entry_max, 0ull);
+                        }
+                        TSTAMP(7);
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPEC_GROUPS; q++) apply_uses(S, G[q], usec[q] & ~used_bits(S, G[q], usec[q], u[q]));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            // arrive (after this block's Uses and record): the dirty blocks count arrivals
+            if (t == 0) __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            TSTAMP(3);
+            write_hb_handles(S, nflags32, nbase, nn, hb_base);
+            if (!dirty) {
+                TSTAMP(6);
+                return;
+            }
+            wait_arrivals(S, arrive_target);
+            reduce_records(S, b, tag, jobs.recs, &sums);
             have_sums = true;
-            write_front_header(S, sums, n_hb, pool_index, &sh_hdr, c, (phases & TICK_PROF) != 0);
-            TSTAMP(7);
+        } else {
+            // ---- multi rank: records; the last arriver writes the exchange message -----
+            if (t == 0) {
+                S.dmask[2 * b] = pod_mask;
+                S.dmask[2 * b + 1] = node_mask;
+            }
+            f[AG_DIRTY] = dirty ? 1u : 0u;
+            const uint64_t old = publish_and_arrive(S, b, f);
+            TSTAMP(3);
+            if ((old + 1) % S.n_chain == 0) {
+                const uint64_t c = __builtin_amdgcn_s_memrealtime();
+                reduce_records(S, b, 0, jobs.recs, &sums);
+                write_front_header(S, sums, n_hb, pool_index, c, (phases & TICK_PROF) != 0);
+                TSTAMP(7);
+            }
+            write_hb_handles(S, nflags32, nbase, nn, hb_base);
+            return;  // the BACK launch follows the exchange
         }
-        if (!(phases & TICK_BACK)) return;
-        // single rank: a clean block is done; a dirty one waits for every record
-        if (!(pod_mask | node_mask)) {
-            TSTAMP(6);
-            return;
-        }
-        if (!last) wait_arrivals(S, (old / S.n_chain + 1) * S.n_chain);
     } else {
         // BACK launch (multi rank): this block's masks from the FRONT launch
         if (t == 0) {
@@ -1635,10 +1773,12 @@ void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hip
 }
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
-                 hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+                 uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const uint32_t grid = S.n_chain + ((phases & TICK_FRONT) ? n_stream : 0u);
-    if (t0) hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases);
-    else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases);
+    if (t0)
+        hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases, tag,
+                              arrive_target);
+    else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases, tag, arrive_target);
 }
 
 int tick_occupancy() {
