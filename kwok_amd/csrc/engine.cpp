@@ -125,6 +125,7 @@ struct kwok_engine {
     bool sync_spin = true;
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
+    int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
     uint64_t front_launches = 0;  // FRONT launches since the cross-block state was last zeroed
     DevState* S_pin = nullptr;  // pinned staging for its upload
@@ -556,6 +557,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         const char* pr = getenv("KWOK_TICK_PRIO");
         e->chain_prio = pr && pr[0] == '1';
         if (const char* v = getenv("KWOK_TICK_STREAM_DELAY_NS")) S.stream_delay = (uint32_t)std::max(0, atoi(v) / 10);
+        if (const char* v = getenv("KWOK_TICK_STREAM_SHARE")) e->share_env = std::min(1024, std::max(0, atoi(v)));
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
     }
@@ -945,6 +947,9 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
         HIPCHK(e, hipMemcpyAsync(e->d_hb_pre, e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipMemcpyHostToDevice, st));
         e->hb_pre_dirty = false;
     }
+    // a long heartbeat stream is shared with the chain blocks once they are done
+    // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
+    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)HB_STRIDE >= (32ull << 20) ? 921u : 1024u);
     if (memcmp(&e->S_up, &S, sizeof(DevState)) != 0) {  // pointers / sizes changed since the last upload
         *e->S_pin = S;
         HIPCHK(e, hipMemcpyAsync(e->d_S, e->S_pin, sizeof(DevState), hipMemcpyHostToDevice, st));

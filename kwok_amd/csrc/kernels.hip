@@ -1125,10 +1125,15 @@ __device__ __forceinline__ void hb_fill_units(const DevState& S, const uint4* tm
     }
 }
 
-// this streamer's share of the heartbeat stream (static, contiguous)
-__device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
+// static shares of the heartbeat stream: the streamer blocks split the first
+// stream_share/1024 of it, and every chain block writes an equal slice of the
+// rest once its own work is done (so the stream's tail overlaps nothing idle)
+__device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, bool streamer,
+                                              uint32_t idx, uint32_t cnt) {
     const uint64_t units = n_hb * HB_CHUNKS;
-    hb_fill_units(S, tmpl, units * idx / cnt, units * (idx + 1) / cnt);
+    const uint64_t cut = units * S.stream_share / 1024;
+    const uint64_t lo = streamer ? 0 : cut, n = streamer ? cut : units - cut;
+    hb_fill_units(S, tmpl, lo + n * idx / cnt, lo + n * (idx + 1) / cnt);
 }
 
 // per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
@@ -1456,7 +1461,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__builtin_amdgcn_s_memrealtime() - t0 < S.stream_delay) __builtin_amdgcn_s_sleep(4);
         }
-        if (!(phases & TICK_NOSTREAM)) hb_fill_share(S, hb_tmpl4, n_hb, b - S.n_chain, gridDim.x - S.n_chain);
+        if (!(phases & TICK_NOSTREAM)) hb_fill_share(S, hb_tmpl4, n_hb, true, b - S.n_chain, gridDim.x - S.n_chain);
         if ((phases & TICK_PROF) && t == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1633,6 +1638,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if (t == 0) __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             TSTAMP(3);
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
+            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
+                build_hb_template(S, hb_tmpl, now_unix, start_unix);
+                hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+            }
             if (!dirty) {
                 TSTAMP(6);
                 return;
@@ -1656,6 +1665,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 TSTAMP(7);
             }
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
+            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {
+                build_hb_template(S, hb_tmpl, now_unix, start_unix);
+                hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+            }
             return;  // the BACK launch follows the exchange
         }
     } else {
