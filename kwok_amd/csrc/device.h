@@ -88,6 +88,8 @@ struct TickHdr {
     // single rank: the tick's field totals (AG_*), written by the chain block whose
     // accumulator add completed each field; the host derives the header from them
     uint64_t tot[16];
+    // multi rank: a BACK launch found exchange lists too long to be inline
+    uint32_t xovf, pad3;
 };
 
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out

@@ -634,8 +634,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.hb_pre = e->d_hb_pre;
     S.hdr_host = e->hdr_h;   // zero-copy: k_tick's last block publishes the header
     S.pod_fill = e->d_pod_fill;
+    S.rank = e->rank;
     if (W > 1) {
         if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
+        S.xall = e->d_xall;
         if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
             return bail(KWOK_ENOMEM);
         if (cfg->comm_id) {
@@ -966,49 +968,53 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
     }
     launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, e->tick_tag, target, st,
                 ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
-    // one allgather of the fixed-size exchange message; a second one for
-    // lists that did not fit inline (sizes known after the first)
+    // one allgather of the fixed-size exchange message, then BACK: it folds the
+    // gathered messages and applies the inline lists itself (no host round trip).
+    // Lists too long to be inline: BACK flags it and the host finishes the tick
+    // with a second allgather (finish_long_lists).
     int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
     if (rc) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
-    HIPCHK(e, hipStreamSynchronize(st));
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, e->tick_tag, target, st,
+                ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    HIPCHK(e, hipGetLastError());
+    return KWOK_OK;
+}
+// multi rank, after a BACK launch that found lists too long to be inline (the
+// same on every rank: the flag comes from the gathered messages): gather the
+// lists, apply every rank's Uses and Puts, and run BACK again
+int finish_long_lists(kwok_engine* e, uint64_t now) {
+    DevState& S = e->S;
+    hipStream_t st = e->st;
+    e->hdr_h->xovf = 0;
+    HIPCHK(e, hipMemcpy(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost));
     uint64_t maxl = 0;
     for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
-    std::vector<ListDesc> ld(e->W);
-    if (maxl <= (uint64_t)XINLINE) {
-        for (int r = 0; r < e->W; r++) {
-            ld[r].use = e->d_xall[r].ips;
-            ld[r].rel = e->d_xall[r].ips + e->h_xall[r].n_use;
-        }
-    } else {
-        if (maxl > e->xlist_cap) {
-            if (e->d_xsend) (void)hipFree(e->d_xsend);
-            if (e->d_xrecv) (void)hipFree(e->d_xrecv);
-            e->xlist_cap = maxl;
-            if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
-                hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
-                return e->fail(KWOK_ENOMEM, "exchange lists");
-        }
-        const XMsg& me = e->h_xall[e->rank];
-        HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
-        HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
-        rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
-        if (rc) return rc;
-        for (int r = 0; r < e->W; r++) {
-            ld[r].use = e->d_xrecv + (size_t)r * maxl;
-            ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
-        }
+    if (maxl > e->xlist_cap) {
+        if (e->d_xsend) (void)hipFree(e->d_xsend);
+        if (e->d_xrecv) (void)hipFree(e->d_xrecv);
+        e->xlist_cap = maxl;
+        if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
+            hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
+            return e->fail(KWOK_ENOMEM, "exchange lists");
     }
+    const XMsg& me = e->h_xall[e->rank];
+    if (me.n_use) HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
+    if (me.n_rel) HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
+    int rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
+    if (rc) return rc;
+    std::vector<ListDesc> ld(e->W);
     for (int r = 0; r < e->W; r++) {
+        ld[r].use = e->d_xrecv + (size_t)r * maxl;
+        ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
         ld[r].n_use = (uint32_t)e->h_xall[r].n_use;
         ld[r].n_rel = (uint32_t)e->h_xall[r].n_rel;
     }
     HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
-    launch_xreduce(S, e->d_xall, e->W, e->rank, st);
     launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, e->tick_tag, target, st,
-                ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+    launch_tick(S, e->n_stream, now, (uint64_t)e->start, (uint32_t)e->n_managed, TICK_BACK | TICK_XLISTS, e->tick_tag,
+                e->front_launches * S.n_chain, st);
     HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(st));
     return KWOK_OK;
 }
 }  // namespace
@@ -1093,6 +1099,10 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         HIPCHK(e, q);
     } else {
         HIPCHK(e, hipStreamSynchronize(st));
+    }
+    if (e->W > 1 && e->hdr_h->xovf) {
+        int rc = finish_long_lists(e, (uint64_t)now_unix);
+        if (rc) return rc;
     }
     const auto t2 = clk::now();
     if (e->W == 1) derive_header(e);

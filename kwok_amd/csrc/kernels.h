@@ -56,6 +56,8 @@ struct DevState {
     uint32_t* rel_list;
     uint32_t* list_counts;   // [2]: n_use, n_rel (reset by k_emit)
     int world;
+    int rank;
+    const XMsg* xall;        // [world] gathered exchange messages (multi rank)
     uint8_t* arena;
     uint64_t arena_cap;
     int32_t* hb_nodes;
@@ -82,14 +84,14 @@ struct DevState {
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
                       hipStream_t st);
-void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st);
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
 
 // the tick kernel: n_chain chain blocks (+ n_stream heartbeat streamers in
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
 // with work to emit, so they must be co-resident (tick_occupancy).
-constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16;  // NOSTREAM: diagnostics only
+constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16,  // NOSTREAM: diagnostics only
+              TICK_XLISTS = 32;  // BACK: the exchange lists were applied by k_pool_apply
 // tag: this tick's nonzero id (single-rank dirty records); arrive_target: the
 // arrival count at which every chain block of this FRONT launch has arrived
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,

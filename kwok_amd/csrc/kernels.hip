@@ -1295,7 +1295,8 @@ struct TickLds {
 // device state is read through its copy in device memory (S.self).
 __device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l, uint32_t b, uint32_t bk0, uint32_t nbk,
                                        uint64_t pod_mask, uint32_t node_mask, uint32_t my_init, bool have_sums,
-                                       int phases, uint32_t n_hb, uint64_t now_unix, uint64_t start_unix) {
+                                       int phases, uint32_t n_hb, uint64_t now_unix, uint64_t start_unix, uint64_t xA,
+                                       uint64_t xrel, uint64_t xbase) {
     const DevState& S = *G;
     const int t = threadIdx.x;
     TickHdr* H = S.hdr;
@@ -1308,9 +1309,9 @@ __device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l
 
     // ---- pool phase (ticks with Gets or Puts) -------------------------------------
     const bool single = S.world == 1;
-    const uint64_t A = single ? l.sums->tot[AG_ALLOC] : H->alloc_total;
-    const uint64_t rel_total = single ? l.sums->tot[AG_REL] : H->rel_total;
-    const uint64_t alloc_base = single ? 0 : H->alloc_base;
+    const uint64_t A = single ? l.sums->tot[AG_ALLOC] : xA;
+    const uint64_t rel_total = single ? l.sums->tot[AG_REL] : xrel;
+    const uint64_t alloc_base = single ? 0 : xbase;
     const uint64_t n_alloc_local = l.sums->tot[AG_ALLOC];
     // participants: single rank - the dirty blocks (every Get / Put belongs to one);
     // multi rank - every block (each rank commits every rank's Gets to its replica)
@@ -1479,6 +1480,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     uint32_t node_mask = 0;
     uint32_t my_init = 0;
     bool have_sums = false;
+    uint64_t xA = 0, xrel = 0, xbase = 0;  // multi rank: fleet Gets / Puts, this rank's first Get ordinal
 
     if (phases & TICK_FRONT) {
         if (t == 0 && (phases & TICK_PROF))
@@ -1672,7 +1674,50 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             return;  // the BACK launch follows the exchange
         }
     } else {
-        // BACK launch (multi rank): this block's masks from the FRONT launch
+        // BACK launch (multi rank).  Every block folds the gathered exchange
+        // messages (W of them): the fleet's Gets, this rank's first ordinal, Puts
+        const XMsg* X = S.xall;
+        uint64_t base = 0;
+        uint32_t maxl = 0;
+        for (int r = 0; r < S.world; r++) {
+            const uint64_t al = X[r].alloc;
+            xA += al;
+            if (r < S.rank) base += al;
+            xrel += X[r].n_rel;
+            maxl = max(maxl, (uint32_t)(X[r].n_use + X[r].n_rel));
+        }
+        xbase = base;
+        if (!(phases & TICK_XLISTS)) {
+            if (maxl > (uint32_t)XINLINE) {
+                // lists that did not fit inline: the host runs the second allgather,
+                // applies them and launches BACK again (TICK_XLISTS)
+                if (b == 0 && t == 0) S.hdr_host->xovf = 1;
+                return;
+            }
+            // every rank's Uses into `used`, every rank's Puts into rel_bm (folded in
+            // the pool phase after all of them: Use -> Put), from the inline lists
+            for (int r = 0; r < S.world; r++) {
+                const uint32_t nu = (uint32_t)X[r].n_use, nl = nu + (uint32_t)X[r].n_rel;
+                for (uint32_t i = b * BLOCK + t; i < nl; i += S.n_chain * BLOCK) {
+                    const uint32_t ip = X[r].ips[i];
+                    if (!in_cidr(S.pool, ip)) continue;
+                    const uint64_t bit = ip - S.pool.net;
+                    atomicOr((unsigned long long*)&(i < nu ? S.used_bm : S.rel_bm)[bit >> 6], 1ull << (bit & 63));
+                }
+            }
+            if (xA || xrel) pool_barrier(S, S.n_chain);  // the pool phase reads every rank's bits
+        }
+        if (b == 0 && t < 16) {  // fleet counters
+            uint64_t c = 0;
+            for (int r = 0; r < S.world; r++) c += X[r].counters[t];
+            H->counters[t] = c;
+            if (t == 0) {
+                H->alloc_total = xA;
+                H->alloc_base = xbase;
+                H->rel_total = xrel;
+            }
+        }
+        // this block's masks from the FRONT launch
         if (t == 0) {
             sh_mask[0] = (uint32_t)S.dmask[2 * b];
             sh_mask[1] = (uint32_t)(S.dmask[2 * b] >> 32);
@@ -1689,28 +1734,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
     }
     tick_back(S.self, TickLds{jobs.recs, jobs.pod, jobs.node, hb_tmpl, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
-              pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix);
+              pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase);
 #undef TSTAMP
 #undef TWAIT
-}
-
-// ---------------------------------------------------------------------------
-// k_xreduce (multi-rank): fold the gathered exchange headers
-// ---------------------------------------------------------------------------
-__global__ void k_xreduce(DevState S, const XMsg* all, int world_size, int rank) {
-    if (threadIdx.x != 0) return;
-    TickHdr* H = S.hdr;
-    uint64_t tot = 0, base = 0, rel = 0;
-    for (int k = 0; k < 16; k++) H->counters[k] = 0;
-    for (int r = 0; r < world_size; r++) {
-        if (r < rank) base += all[r].alloc;
-        tot += all[r].alloc;
-        rel += all[r].n_rel;
-        for (int k = 0; k < 16; k++) H->counters[k] += all[r].counters[k];
-    }
-    H->alloc_total = tot;
-    H->alloc_base = base;
-    H->rel_total = rel;
 }
 
 // ingest-time Put (a Deleted watch event), applied immediately
@@ -1781,9 +1807,6 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
-void launch_xreduce(const DevState& S, const XMsg* all, int world, int rank, hipStream_t st) {
-    hipLaunchKernelGGL(k_xreduce, dim3(1), dim3(64), 0, st, S, all, world, rank);
-}
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {

@@ -16,6 +16,7 @@ from kwok_amd.engine import make_config
 
 BUCKETS, CN, CP = 64, 32, 512
 CIDR = "10.0.0.1/20"
+BIG_CIDR = "10.0.0.1/16"  # the "big" scenario: > 2048 releases per rank in one tick (exchange lists not inline)
 
 
 def free_port():
@@ -46,14 +47,16 @@ def gloo_allgather_fn():
     return fn
 
 
-def make(cls, rank, world, allgather=None, device=0):
-    cfg = make_config(cidr=CIDR, node_ip="196.168.0.1", buckets=BUCKETS, node_slots_per_bucket=CN,
+def make(cls, rank, world, allgather=None, device=0, big=False):
+    cfg = make_config(cidr=BIG_CIDR if big else CIDR, node_ip="196.168.0.1", buckets=BUCKETS, node_slots_per_bucket=CN,
                       pod_slots_per_bucket=CP, rank=rank, world_size=world, device=device, allgather=allgather)
     return cls(cfg)
 
 
-def scenario(seed=11, ticks=5):
-    """A deterministic list of per-tick event batches (dict form)."""
+def scenario(seed=11, ticks=5, big=False):
+    """A deterministic list of per-tick event batches (dict form).  big: 12000
+    pods, then 6000 deletions in one tick (every rank's release list is longer
+    than the inline exchange message holds)."""
     rng = np.random.default_rng(seed)
     names = ["node-%07d" % i for i in range(400)]
     out = []
@@ -65,13 +68,14 @@ def scenario(seed=11, ticks=5):
             for n in names:
                 nodes.append(dict(op="upsert", name=n, managed=bool(rng.random() < 0.9),
                                   lockable=bool(rng.random() < 0.95)))
-            k = 3000
+            k = 12000 if big else 3000
         else:
             k = 400
             for n in rng.choice(names, 4, replace=False):  # flaps
                 nodes.append(dict(op="delete", name=str(n)))
                 nodes.append(dict(op="upsert", name=str(n), managed=True, lockable=True))
-            for i in rng.choice(len(live), min(len(live), 300), replace=False):
+            ndel = 6000 if big and t == 2 else 300
+            for i in rng.choice(len(live), min(len(live), ndel), replace=False):
                 pods.append(dict(op="deleting", key=live[i], fin=bool(rng.random() < 0.5)))
             for i in rng.choice(len(live), 60, replace=False):
                 pods.append(dict(op="ext_delete", key=live[i]))

@@ -12,7 +12,7 @@ import torch.multiprocessing as mp
 import dist_common as dc
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, big=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -27,9 +27,9 @@ def _worker(rank, world, port, outdir):
         dist.all_gather_object(objs, mine)
         return [ip for r, l in enumerate(objs) if r != rank for ip in l]
 
-    o = dc2.make(Oracle, rank, world, allgather=dc2.gloo_allgather_fn())
+    o = dc2.make(Oracle, rank, world, allgather=dc2.gloo_allgather_fn(), big=big)
     run = dc2.Runner(o, world, rank, exchange_puts)
-    res = [dc2.summarize(run.run_tick(n, p)) for n, p in dc2.scenario()]
+    res = [dc2.summarize(run.run_tick(n, p)) for n, p in dc2.scenario(big=big, ticks=4 if big else 5)]
     with open(os.path.join(outdir, "r%d.pkl" % rank), "wb") as f:
         pickle.dump(res, f)
     o.close()
@@ -49,13 +49,13 @@ def merge(parts):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_oracle_matches_single(world):
+@pytest.mark.parametrize("world,big", [(2, False), (4, False), (2, True)])
+def test_sharded_oracle_matches_single(world, big):
     from oracle.oracle import Oracle
-    single = dc.Runner(dc.make(Oracle, 0, 1))
-    ref = [dc.summarize(single.run_tick(n, p)) for n, p in dc.scenario()]
+    single = dc.Runner(dc.make(Oracle, 0, 1, big=big))
+    ref = [dc.summarize(single.run_tick(n, p)) for n, p in dc.scenario(big=big, ticks=4 if big else 5)]
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, dc.free_port(), d), nprocs=world, start_method="spawn", join=True)
+        mp.start_processes(_worker, args=(world, dc.free_port(), d, big), nprocs=world, start_method="spawn", join=True)
         parts = [pickle.load(open(os.path.join(d, "r%d.pkl" % r), "rb")) for r in range(world)]
     got = merge(parts)
     assert len(got) == len(ref)

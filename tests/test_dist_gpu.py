@@ -16,7 +16,7 @@ from test_dist_cpu import merge
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, big=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -32,30 +32,34 @@ def _worker(rank, world, port, outdir):
         dist.all_gather_object(objs, mine)
         return [ip for r, l in enumerate(objs) if r != rank for ip in l]
 
-    e = dc2.make(Engine, rank, world, allgather=dc2.gloo_allgather_fn())
+    e = dc2.make(Engine, rank, world, allgather=dc2.gloo_allgather_fn(), big=big)
     run = dc2.Runner(e, world, rank, exchange_puts)
-    res = [dc2.summarize(run.run_tick(n, p)) for n, p in dc2.scenario()]
+    res = [dc2.summarize(run.run_tick(n, p)) for n, p in dc2.scenario(big=big, ticks=4 if big else 5)]
     with open(os.path.join(outdir, "r%d.pkl" % rank), "wb") as f:
         pickle.dump(res, f)
     e.close()
     dist.destroy_process_group()
 
 
-def test_two_rank_engine_matches_single_and_oracle():
+@pytest.mark.parametrize("big", [False, True], ids=["inline-lists", "long-lists"])
+def test_two_rank_engine_matches_single_and_oracle(big):
     from kwok_amd.engine import Engine
     from oracle.oracle import Oracle
-    single_o = dc.Runner(dc.make(Oracle, 0, 1))
-    ref = [dc.summarize(single_o.run_tick(n, p)) for n, p in dc.scenario()]
-    single_e = dc.Runner(dc.make(Engine, 0, 1))
-    eng = [dc.summarize(single_e.run_tick(n, p)) for n, p in dc.scenario()]
+    sc = dc.scenario(big=big, ticks=4 if big else 5)
+    single_o = dc.Runner(dc.make(Oracle, 0, 1, big=big))
+    ref = [dc.summarize(single_o.run_tick(n, p)) for n, p in sc]
+    single_e = dc.Runner(dc.make(Engine, 0, 1, big=big))
+    eng = [dc.summarize(single_e.run_tick(n, p)) for n, p in sc]
     for t, (g, r) in enumerate(zip(eng, ref)):
         for k in ("hb", "hb_body", "inits", "pods", "deletes", "counters"):
             assert g[k] == r[k], "single-rank engine tick %d %s" % (t, k)
     single_e.b.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, dc.free_port(), d), nprocs=2, start_method="spawn", join=True)
+        mp.start_processes(_worker, args=(2, dc.free_port(), d, big), nprocs=2, start_method="spawn", join=True)
         parts = [pickle.load(open(os.path.join(d, "r%d.pkl" % r), "rb")) for r in range(2)]
     got = merge(parts)
     for t, (g, r) in enumerate(zip(got, ref)):
         for k in ("hb", "hb_body", "inits", "pods", "deletes", "counters"):
             assert g[k] == r[k], "2-rank engine tick %d %s" % (t, k)
+    if big:  # the long-list exchange really ran: > 2 x 2048 releases in one tick
+        assert max(r["counters"]["release"] for r in ref) > 2 * 2048
