@@ -930,7 +930,7 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
 namespace {
 // Enqueue one tick on e->st.  Single rank: ONE persistent k_tick launch (no host
 // synchronisation, no graph needed).  Multi-rank: k_tick FRONT (classify, bases,
-// exchange message) -> allgather -> xreduce + pool_apply -> k_tick BACK (pool,
+// exchange message) -> allgather -> k_tick BACK (fold messages, lists, pool,
 // emission).
 int enqueue_tick(kwok_engine* e, uint64_t now) {
     DevState& S = e->S;

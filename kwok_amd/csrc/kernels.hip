@@ -1177,7 +1177,7 @@ __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint
                                  (uint64_t)AG_ALLOC << 16 | (uint64_t)AG_REL << 20 | (uint64_t)AG_EVAL << 24 |
                                  (uint64_t)AG_LOCK << 28 | (uint64_t)AG_MANAGED << 32 | (uint64_t)AG_READY << 36 |
                                  (uint64_t)AG_TOTAL << 40 | (uint64_t)AG_PENDING << 44 | (uint64_t)AG_RUNNING << 48;
-        if (k >= 13 || (i >= W_C && !single)) return 0;  // fleet counters: k_xreduce (multi rank)
+        if (k >= 13 || (i >= W_C && !single)) return 0;  // fleet counters: the BACK launch (multi rank)
         return tot[(MAP >> (4 * k)) & 15];
     }
     if (i >= W_CLK && i < W_CLK + 8) return clk[i - W_CLK];
