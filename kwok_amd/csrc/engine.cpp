@@ -301,6 +301,8 @@ int upload_specs(kwok_engine* e) {
     e->S.specs = e->d_specs.p;
     e->S.spec_bytes = e->d_spec_bytes.p;
     e->S.spec_kinds = e->d_spec_kinds.p;
+    e->S.n_specs = (uint32_t)e->specs_h.size();
+    e->S.spec_total = (uint32_t)e->spec_bytes_h.size();
     return KWOK_OK;
 }
 
@@ -340,6 +342,7 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     (void)hipMemcpyAsync(e->d_blob.p + off, e->blob_h.data() + off, b.pre.size() + b.post.size(), hipMemcpyHostToDevice,
                    e->st);
     e->S.blob = e->d_blob.p;
+    e->S.blob_total = (uint32_t)e->blob_h.size();
     return word;
 }
 
@@ -444,7 +447,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->trace_ticks) {
         static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "-", "pool-done",
                                                  "exit", "header-done", "w:gpre", "w:pod-loads", "w:pods-classd",
-                                                 "w:block-sum", "w:masks", "w:used-words", "-", "-"};
+                                                 "w:block-sum", "w:masks", "w:used-words", "nodes-emitted", "back-start"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
                         "start (min / median / max block)\n",
                 e->S.n_chain, e->n_stream, (unsigned long long)e->trace_ticks);
@@ -1053,7 +1056,8 @@ static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr &
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
 static void trace_tick(kwok_engine* e) {
     const size_t G = e->S.n_chain, N = G + e->n_stream;
-    if (++e->trace_seen <= 5) return;  // skip the initial (bulk) ticks
+    static const int skip = getenv("KWOK_TICK_TRACE_SKIP") ? atoi(getenv("KWOK_TICK_TRACE_SKIP")) : 5;
+    if ((int)++e->trace_seen <= skip) return;  // skip the initial (bulk) ticks
     const size_t TS = TRACE_SLOTS;
     e->trace_h.assign(N * TS, 0);
     if (hipMemcpy(e->trace_h.data(), e->S.trace, N * TS * 8, hipMemcpyDeviceToHost) != hipSuccess) return;

@@ -46,6 +46,8 @@ struct DevState {
     const uint8_t* spec_bytes;
     const uint8_t* spec_kinds;
     const uint8_t* blob;
+    uint32_t n_specs, spec_total;  // spec descriptors; bytes of the concatenated spec programs
+    uint32_t blob_total;           // bytes of the interned node blobs
     // heartbeat template
     const uint8_t* hb_static;
     const uint8_t* hb_kind;

@@ -181,7 +181,21 @@ __device__ __forceinline__ uint32_t ip_len(uint32_t ip) {
     return n;
 }
 
-__device__ __forceinline__ uint32_t lit_byte(const char* s, uint32_t i) { return (uint32_t)(uint8_t)s[i]; }
+// byte i (< 16) of a short literal, from two compile-time words (no memory access)
+struct Lit16 {
+    uint64_t lo, hi;
+};
+constexpr Lit16 lit16(const char* s) {
+    Lit16 r{0, 0};
+    for (int i = 0; i < 16 && s[i]; i++) {
+        if (i < 8) r.lo |= (uint64_t)(uint8_t)s[i] << (8 * i);
+        else r.hi |= (uint64_t)(uint8_t)s[i] << (8 * (i - 8));
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t lit_byte(Lit16 l, uint32_t i) {
+    return (uint32_t)((i < 8 ? l.lo >> (8 * i) : l.hi >> (8 * (i - 8))) & 0xFF);
+}
 
 // ---------------------------------------------------------------------------
 // per-object predicates (shared by k_classify and k_emit)
@@ -232,84 +246,139 @@ __device__ __forceinline__ uint32_t init_patch_len(uint64_t blob) {
 // ---------------------------------------------------------------------------
 // patch writers (one wave per patch)
 // ---------------------------------------------------------------------------
+// per-patch data gathered during compaction (LDS job lists), so a wave writing
+// a patch starts from registers / LDS only
 struct PodJob {
-    uint32_t slot;   // local slot
-    uint32_t off;    // byte offset within the tile's pod region
-    uint32_t pod_ip; // rendered podIP (0 = no status section)
+    uint32_t off;     // byte offset within the chunk's pod region
+    uint32_t pod_ip;  // rendered podIP (0 = no status section)
     uint32_t host_ip;
+    uint32_t ctime;   // creationTimestamp (unix seconds)
+    uint32_t spec;    // pod spec id
 };
 struct InitJob {
-    uint32_t slot;
     uint32_t off;
+    uint32_t pad;
+    uint64_t blob;    // node_blob word: off | pre_len << 32 | post_len << 48
 };
 
+// the spec programs and node blobs of the engine, staged in LDS once per
+// emitting block when they fit (the common case: a handful of specs / blobs);
+// otherwise the writers read them from global memory
+constexpr int SPEC_LDS_DESCS = 64, SPEC_LDS_PROG = 4096, BLOB_LDS = 4096;
+struct EmitCache {
+    uint32_t n_desc;                       // 0: not staged
+    uint32_t blob_ok;
+    SpecDesc desc[SPEC_LDS_DESCS];
+    uint16_t prog[SPEC_LDS_PROG];          // byte | kind << 8
+    uint8_t blob[BLOB_LDS];
+};
+__device__ __forceinline__ void stage_emit_cache(const DevState& S, EmitCache* c, bool pods, bool nodes) {
+    const bool sp = pods && S.n_specs <= (uint32_t)SPEC_LDS_DESCS && S.spec_total <= (uint32_t)SPEC_LDS_PROG;
+    const bool bl = nodes && S.blob_total <= (uint32_t)BLOB_LDS;
+    if (sp) {
+        for (uint32_t i = threadIdx.x; i < S.n_specs; i += BLOCK) c->desc[i] = S.specs[i];
+        for (uint32_t i = threadIdx.x; i < S.spec_total; i += BLOCK)
+            c->prog[i] = (uint16_t)(S.spec_bytes[i] | (uint32_t)S.spec_kinds[i] << 8);
+    }
+    if (bl)
+        for (uint32_t i = threadIdx.x; i < S.blob_total; i += BLOCK) c->blob[i] = S.blob[i];
+    if (threadIdx.x == 0) {
+        c->n_desc = sp ? S.n_specs : 0u;
+        c->blob_ok = bl ? 1u : 0u;
+    }
+    __syncthreads();
+}
+
+// Patches are assembled in a per-wave LDS buffer with lane-strided byte copies
+// (no per-byte control flow: every lane runs the same instructions), then
+// copied out 16 bytes per lane.  Longer patches than the buffer (specs with many
+// containers) take the direct per-byte path.
+constexpr uint32_t PATCH_BUF = 2048;
+
+// byte o of a spec's A|B|C template (timestamp slots from ts)
+__device__ __forceinline__ uint32_t tmpl_byte(const DevState& S, const EmitCache* c, bool cached, uint32_t off, const Ts& ts) {
+    const uint32_t v = cached ? c->prog[off] : (S.spec_bytes[off] | (uint32_t)S.spec_kinds[off] << 8);
+    const uint32_t kd = v >> 8;
+    return kd == 0xFF ? (v & 0xFF) : ts_byte(ts, kd);
+}
+// byte i of `"<key>":"<ip>",` (key: 10 bytes for hostIP, 9 for podIP)
+__device__ __forceinline__ uint32_t ipseg_byte(Lit16 key, uint32_t klen, const IpStr& ip, uint32_t i) {
+    return i < klen ? lit_byte(key, i) : i < klen + ip.len ? ip_byte(ip, i - klen) : (i == klen + ip.len ? '"' : ',');
+}
+
 // one wave writes one pod patch: A [+ "hostIP":"H",] B [+ "podIP":"P",] C
-__device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob& j, uint8_t* out) {
-    const SpecDesc sd = S.specs[S.pod_spec[j.slot]];
-    const Ts ts = format_ts(S.pod_ctime[j.slot]);
+__device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob& j, const EmitCache* c, uint8_t* buf,
+                                                uint8_t* out) {
+    const bool cached = c->n_desc != 0;
+    const SpecDesc sd = cached ? c->desc[j.spec] : S.specs[j.spec];
+    const Ts ts = format_ts(j.ctime);
     const bool st = j.host_ip != 0;
     const IpStr H = format_ip(j.host_ip), P = format_ip(j.pod_ip);
     const uint32_t la = sd.len_a, lb = sd.len_b, lc = sd.len_c;
     const uint32_t lh = st ? 10u + H.len + 2u : 0u, lp = st ? 9u + P.len + 2u : 0u;
     const uint32_t len = la + lh + lb + lp + lc;
-    const uint8_t* bytes = S.spec_bytes + sd.off;
-    const uint8_t* kinds = S.spec_kinds + sd.off;
-    const char* kh = "\"hostIP\":\"";
-    const char* kp = "\"podIP\":\"";
-    for (uint32_t q0 = lane_id() * 4u; q0 < len; q0 += 256u) {
-        uint32_t w = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            uint32_t q = q0 + k, b = 0;
-            if (q < len) {
-                uint32_t p = q;
-                uint32_t seg_off;  // offset into the concatenated spec bytes (A|B|C)
-                bool tmpl = false;
-                if (p < la) {
-                    tmpl = true;
-                    seg_off = p;
-                } else if ((p -= la) < lh) {
-                    if (p < 10u) b = lit_byte(kh, p);
-                    else if (p < 10u + H.len) b = ip_byte(H, p - 10u);
-                    else b = (p == 10u + H.len) ? '"' : ',';
-                } else if ((p -= lh) < lb) {
-                    tmpl = true;
-                    seg_off = la + p;
-                } else if ((p -= lb) < lp) {
-                    if (p < 9u) b = lit_byte(kp, p);
-                    else if (p < 9u + P.len) b = ip_byte(P, p - 9u);
-                    else b = (p == 9u + P.len) ? '"' : ',';
-                } else {
-                    p -= lp;
-                    tmpl = true;
-                    seg_off = la + lb + p;
-                }
-                if (tmpl) {
-                    uint8_t kd = kinds[seg_off];
-                    b = kd == 0xFF ? bytes[seg_off] : ts_byte(ts, kd);
-                }
+    constexpr Lit16 kh = lit16("\"hostIP\":\""), kp = lit16("\"podIP\":\"");
+    const uint32_t l = lane_id();
+    if (len <= PATCH_BUF) {
+        for (uint32_t i = l; i < la; i += 64) buf[i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + i, ts);
+        for (uint32_t i = l; i < lb; i += 64) buf[la + lh + i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + la + i, ts);
+        for (uint32_t i = l; i < lc; i += 64)
+            buf[la + lh + lb + lp + i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + la + lb + i, ts);
+        if (l < lh) buf[la + l] = (uint8_t)ipseg_byte(kh, 10, H, l);
+        if (l < lp) buf[la + lh + lb + l] = (uint8_t)ipseg_byte(kp, 9, P, l);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes before its reads
+        for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u)
+            *reinterpret_cast<uint4*>(out + q0) = *reinterpret_cast<const uint4*>(buf + q0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads complete before the next patch's writes
+        return;
+    }
+    for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u) {  // long patches: byte by byte
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16; k++) {
+            uint32_t p = q0 + k, b = 0;
+            if (p < len) {
+                if (p < la) b = tmpl_byte(S, c, cached, sd.off + p, ts);
+                else if ((p -= la) < lh) b = ipseg_byte(kh, 10, H, p);
+                else if ((p -= lh) < lb) b = tmpl_byte(S, c, cached, sd.off + la + p, ts);
+                else if ((p -= lb) < lp) b = ipseg_byte(kp, 9, P, p);
+                else b = tmpl_byte(S, c, cached, sd.off + la + lb + (p - lp), ts);
             }
-            w |= b << (8 * k);
+            w[k >> 2] |= b << (8 * (k & 3));
         }
-        *reinterpret_cast<uint32_t*>(out + q0) = w;
+        *reinterpret_cast<uint4*>(out + q0) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
 // one wave writes one node init patch: {"status":{ pre ,"conditions": CONDS , post }}
-__device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl, uint8_t* out) {
+__device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl,
+                                                 const EmitCache* c, uint8_t* buf, uint8_t* out) {
     const uint32_t boff = (uint32_t)blob, pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
     const uint32_t len = init_patch_len(blob);
-    const uint8_t* bb = S.blob + boff;
+    const uint8_t* bb = (c->blob_ok ? c->blob : S.blob) + boff;
     const uint8_t* conds = hb_tmpl + HB_PREFIX;
-    const char* p0 = "{\"status\":{";
-    const char* p1 = ",\"conditions\":";
-    for (uint32_t q0 = lane_id() * 4u; q0 < len; q0 += 256u) {
-        uint32_t w = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            uint32_t q = q0 + k, b = 0;
-            if (q < len) {
-                uint32_t p = q;
+    constexpr Lit16 p0 = lit16("{\"status\":{"), p1 = lit16(",\"conditions\":");
+    const uint32_t l = lane_id();
+    if (len <= PATCH_BUF) {
+        // layout: p0 (11) | pre | p1 (14) | CONDS | ',' | post | '}' '}'
+        if (l < 11) buf[l] = (uint8_t)lit_byte(p0, l);
+        for (uint32_t i = l; i < pre; i += 64) buf[11 + i] = bb[i];
+        if (l < 14) buf[11 + pre + l] = (uint8_t)lit_byte(p1, l);
+        for (uint32_t i = l; i < (uint32_t)CONDS_LEN; i += 64) buf[25 + pre + i] = conds[i];
+        const uint32_t o = 25 + pre + CONDS_LEN;
+        if (l == 0) buf[o] = ',';
+        for (uint32_t i = l; i < post; i += 64) buf[o + 1 + i] = bb[pre + i];
+        if (l < 2) buf[o + 1 + post + l] = '}';
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u)
+            *reinterpret_cast<uint4*>(out + q0) = *reinterpret_cast<const uint4*>(buf + q0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        return;
+    }
+    for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16; k++) {
+            uint32_t p = q0 + k, b = 0;
+            if (p < len) {
                 if (p < 11u) b = lit_byte(p0, p);
                 else if ((p -= 11u) < pre) b = bb[p];
                 else if ((p -= pre) < 14u) b = lit_byte(p1, p);
@@ -318,9 +387,9 @@ __device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blo
                 else if ((p -= 1u) < post) b = bb[pre + p];
                 else b = '}';
             }
-            w |= b << (8 * k);
+            w[k >> 2] |= b << (8 * (k & 3));
         }
-        *reinterpret_cast<uint32_t*>(out + q0) = w;
+        *reinterpret_cast<uint4*>(out + q0) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
@@ -968,7 +1037,8 @@ struct Bases {
 
 // node chunk at block-local node offset i0 (node slots nbase + [i0, i0 + 1024))
 __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbase, uint32_t i0, uint32_t nn, Bases& run,
-                                const Layout& L, const uint8_t* hb_tmpl, InitJob* ij) {
+                                const Layout& L, const uint8_t* hb_tmpl, InitJob* ij, const EmitCache* ec,
+                                uint8_t* pbuf) {
     const uint32_t i = i0 + threadIdx.x * NODE_PER_THREAD;
     const uint32_t first = nbase + i;
     uint32_t packed = 0;
@@ -976,12 +1046,15 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
     NodeCls c[NODE_PER_THREAD];
     uint32_t v[2] = {0, 0};  // init, init bytes
     uint32_t ilen[NODE_PER_THREAD];
+    uint64_t blob[NODE_PER_THREAD];
 #pragma unroll
     for (int k = 0; k < NODE_PER_THREAD; k++) {
         c[k] = classify_node((uint8_t)(packed >> (8 * k)));
         ilen[k] = 0;
+        blob[k] = 0;
         if (c[k].init) {
-            ilen[k] = init_patch_len(S.node_blob[first + k]);
+            blob[k] = S.node_blob[first + k];
+            ilen[k] = init_patch_len(blob[k]);
             v[0]++;
             v[1] += (ilen[k] + 15u) & ~15u;
         }
@@ -998,8 +1071,8 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
             S.init_nodes[ord] = S.node_handle_base + (int32_t)(first + k);
             S.init_off[ord] = chunk_bytes + v[1];
             S.init_len[ord] = ilen[k];
-            ij[ji].slot = first + k;
             ij[ji].off = v[1];
+            ij[ji].blob = blob[k];
             ji++;
             v[1] += (ilen[k] + 15u) & ~15u;
             s |= NS_CONFORMS;  // the apiserver applied the init patch
@@ -1010,7 +1083,7 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
     if (i < nn && newpacked != packed) *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
     __syncthreads();
     for (uint32_t q = wave_id(); q < tot[0]; q += BLOCK / 64)
-        write_init_patch(S, S.node_blob[ij[q].slot], hb_tmpl, S.arena + chunk_bytes + ij[q].off);
+        write_init_patch(S, ij[q].blob, hb_tmpl, ec, pbuf + wave_id() * PATCH_BUF, S.arena + chunk_bytes + ij[q].off);
     __syncthreads();
     run.v[AG_INIT] += tot[0];
     run.v[AG_INIT_BYTES] += tot[1];
@@ -1018,7 +1091,8 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
 
 // pod chunk c: the block's live groups [c*256, c*256 + 256)
 __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
-                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, PodJob* jobs) {
+                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, PodJob* jobs,
+                               const EmitCache* ec, uint8_t* pbuf) {
     PodGrp g;
     load_group(S, gpre, bk0, nbk, ng, c * BLOCK + threadIdx.x, g);
     uint16_t sp[POD_PER_THREAD];
@@ -1074,7 +1148,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
                 S.pp_pods[ord] = handle;
                 S.pp_off[ord] = chunk_bytes + v[2];
                 S.pp_len[ord] = len;
-                jobs[jl] = PodJob{slot, v[2], stat ? pip : 0u, hip};
+                jobs[jl] = PodJob{v[2], stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]};
                 jl++;
                 v[2] += sd.max_len;
                 // the apiserver applied the patch
@@ -1096,7 +1170,8 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     }
     __syncthreads();
     uint8_t* out = S.arena + chunk_bytes;
-    for (uint32_t q = wave_id(); q < tot[1]; q += BLOCK / 64) write_pod_patch(S, jobs[q], out + jobs[q].off);
+    for (uint32_t q = wave_id(); q < tot[1]; q += BLOCK / 64)
+        write_pod_patch(S, jobs[q], ec, pbuf + wave_id() * PATCH_BUF, out + jobs[q].off);
     __syncthreads();
     run.v[AG_DEL] += tot[0];
     run.v[AG_PP] += tot[1];
@@ -1279,6 +1354,8 @@ __device__ __forceinline__ void write_hb_handles(const DevState& S, const uint32
 
 // pointers into k_tick's LDS for the out-of-line BACK phases
 struct TickLds {
+    EmitCache* ec;
+    uint8_t* pbuf;  // [BLOCK / 64][PATCH_BUF] per-wave patch buffers
     uint32_t* recs;
     PodJob* pod;
     InitJob* node;
@@ -1293,7 +1370,7 @@ struct TickLds {
 // every block when the pool phase runs): prefix over the records, ipPool phase,
 // emission.  Out of line so the steady-state path keeps its registers; the
 // device state is read through its copy in device memory (S.self).
-__device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l, uint32_t b, uint32_t bk0, uint32_t nbk,
+__device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLds l, uint32_t b, uint32_t bk0, uint32_t nbk,
                                        uint64_t pod_mask, uint32_t node_mask, uint32_t my_init, bool have_sums,
                                        int phases, uint32_t n_hb, uint64_t now_unix, uint64_t start_unix, uint64_t xA,
                                        uint64_t xrel, uint64_t xbase) {
@@ -1392,14 +1469,18 @@ __device__ __noinline__ void tick_back(const DevState* __restrict__ G, TickLds l
     const Layout L = *l.L;
     Bases run;
     for (int f = 0; f < AG_NSCAN; f++) run.v[f] = l.sums->pre[f];
+    TSTAMP(15);
+    stage_emit_cache(S, l.ec, pod_mask != 0, node_mask != 0 && my_init != 0);
     for (uint32_t m = node_mask; m; m &= m - 1) {
         const uint32_t k = (uint32_t)__builtin_ctz(m);
-        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, l.hb_tmpl, l.node);
+        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, l.hb_tmpl, l.node, l.ec, l.pbuf);
     }
+    TSTAMP(14);
     const uint32_t ng = l.gpre[nbk];
     for (uint64_t m = pod_mask; m; m &= m - 1) {
         const uint32_t c = (uint32_t)__builtin_ctzll(m);
-        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.pod);
+        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.pod, l.ec,
+                       l.pbuf);
     }
     TSTAMP(6);
 #undef TSTAMP
@@ -1439,6 +1520,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ uint32_t sh_mask[4];  // pod chunk mask lo / hi, node chunk mask, most groups in a bucket
     __shared__ Sums sums;
     __shared__ Layout sh_L;
+    __shared__ EmitCache emit_cache;
+    __shared__ uint4 patch_buf4[BLOCK / 64 * PATCH_BUF / 16];
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
 #define TSTAMP(k)                                                                                         \
@@ -1733,7 +1816,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         node_mask = sh_mask[2];
         my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
     }
-    tick_back(S.self, TickLds{jobs.recs, jobs.pod, jobs.node, hb_tmpl, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
+    tick_back(S.self, TickLds{&emit_cache, reinterpret_cast<uint8_t*>(patch_buf4), jobs.recs, jobs.pod, jobs.node, hb_tmpl, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
               pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase);
 #undef TSTAMP
 #undef TWAIT
