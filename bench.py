@@ -6,10 +6,14 @@ Workload (N=1): configs[1] of BASELINE.json - 100k nodes x 1M pods, steady-state
 heartbeat + status ticks on one MI355X.  Weak scaling: every rank owns 100k
 nodes / 1M pods of a fleet of N x 100k nodes hashed into 4096 buckets
 (contiguous bucket ranges per rank), and ranks exchange pool/counter data over
-RCCL each tick.  A step = one kwok_tick (one heartbeat interval at a fixed
-clock): heartbeat patches for every managed node, lock checks for every node,
-re-evaluation of every pod, ipPool bookkeeping.  Warmup includes the initial
-tick (100k node-init patches + 1M Pending->Running patches with IP allocation).
+RCCL each tick.  A step = one tick (one heartbeat interval at a fixed clock):
+heartbeat patches for every managed node, lock checks for every node,
+re-evaluation of every pod, ipPool bookkeeping, and the host collecting the
+tick's result.  Steps are queued (kwok_tick_submit for tick k+1 before
+kwok_tick_collect of tick k, outputs double-buffered); --no-queue times one
+blocking kwok_tick per step, and that figure is always reported beside the
+queued one (ms_per_step_kwok_tick).  Warmup includes the initial tick (100k
+node-init patches + 1M Pending->Running patches with IP allocation).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -60,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
     ap.add_argument("--cpu-nodes", type=int, default=NODES_PER_RANK)
     ap.add_argument("--roofline-ticks", type=int, default=20)
+    ap.add_argument("--no-queue", dest="queue", action="store_false",
+                    help="time kwok_tick one at a time instead of queued submit/collect")
     return ap.parse_args()
 
 
@@ -117,12 +123,23 @@ def main():
     t0 = time.perf_counter()
     trans = evald = 0
     last = None
+    if a.queue:
+        # tick k+1 is submitted before tick k is collected (kwok_tick_submit /
+        # kwok_tick_collect): the next launch is queued while the host finishes a tick
+        e.tick_submit(now)
+        now += 30
     for k in range(a.steps):
-        r = e.tick(now, read=False)
+        if not a.queue:
+            r = e.tick(now, read=False)
+            now += 30
+        else:
+            if k + 1 < a.steps:
+                e.tick_submit(now)
+                now += 30
+            r = e.tick_collect(read=False)
         c = r.counters
         trans += c[0] + c[1] + c[2] + c[3] + c[5]
         evald += c[6] + c[7]
-        now += 30
         last = r
     torch.cuda.synchronize()
     if world > 1:
@@ -133,6 +150,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
     host_ms, host_n = e.profile_host(reset=True)
+    # the same steps one kwok_tick at a time (reported beside the queued figure)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for k in range(a.steps):
+        e.tick(now, read=False)
+        now += 30
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt_sync = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([dt_sync], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_sync = float(t[0])
     # roofline pass: the same ticks with HIP events around each k_tick launch
     # (kernel-exact hipExtLaunchKernelGGL events) and the kernel's phase stamps
     e.profile_enable(True)
@@ -169,6 +202,9 @@ def main():
                        "nodes": fl.total_nodes, "pods": fl.total_nodes * workload.PODS_PER_NODE,
                        "nodes_per_gpu": a.nodes_per_rank, "pods_per_node": workload.PODS_PER_NODE,
                        "cidr": workload.CIDR, "buckets": workload.BUCKETS, "parallelism": "bucket-sharded x%d" % world},
+            "tick_api": ("kwok_tick_submit/kwok_tick_collect, tick k+1 queued before tick k is collected"
+                         if a.queue else "kwok_tick"),
+            "ms_per_step_kwok_tick": dt_sync / a.steps * 1e3,  # the same steps, one blocking kwok_tick each
             "objects_evaluated_per_s": evald / dt,
             "phase_ms_per_tick": {k: v / max(nt, 1) for k, v in phases.items()},
             "host_ms_per_tick": {k: v / max(host_n, 1) for k, v in host_ms.items()},

@@ -61,8 +61,9 @@ enum {
     KWOK_EDEVICE = -5,    /* HIP runtime error */
     KWOK_ECOMM = -6,      /* RCCL / exchange error */
     KWOK_ENOTFOUND = -7,  /* unknown handle */
-    KWOK_ENOTMINE = -8    /* object hashes to a bucket owned by another rank (not an error
+    KWOK_ENOTMINE = -8,   /* object hashes to a bucket owned by another rank (not an error
                              for a sharded caller: route it to the owning rank) */
+    KWOK_EBUSY = -9       /* ticks outstanding (kwok_tick_submit / kwok_tick_collect order) */
 };
 
 enum { KWOK_OP_UPSERT = 1 /* watch.Added / watch.Modified / list item */, KWOK_OP_DELETE = 2 /* watch.Deleted */ };
@@ -238,8 +239,21 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n);
 
 /* Advance one heartbeat interval at fixed clock now_unix (the Now() template
- * func).  Blocks until the tick's outputs are ready. */
+ * func).  Blocks until the tick's outputs are ready.  = kwok_tick_submit +
+ * kwok_tick_collect; KWOK_EBUSY while submitted ticks are not collected. */
 int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res);
+/* The same tick in two halves, so that tick N+1 runs on the device while the
+ * caller collects and consumes tick N (at most two ticks outstanding):
+ *   kwok_tick_submit   enqueue the tick (returns without waiting).
+ *   kwok_tick_collect  wait for the oldest submitted tick and return its result;
+ *                      kwok_read_outputs / kwok_device_outputs then refer to it,
+ *                      until the next kwok_tick_submit.
+ * Results equal kwok_tick's for the same call sequence.  Ingest, spec
+ * registration, kwok_pool_put and kwok_dump_pods first finish every submitted
+ * tick on the host (their results stay collectable), so events apply after the
+ * ticks submitted before them. */
+int kwok_tick_submit(kwok_engine* e, int64_t now_unix);
+int kwok_tick_collect(kwok_engine* e, kwok_tick_result* res);
 int kwok_read_outputs(kwok_engine* e, kwok_outputs* out);
 
 /* The constant merge patch sent before Delete when a pod has finalizers
@@ -253,7 +267,8 @@ uint64_t kwok_node_size(kwok_engine* e);
 int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase,
                    uint32_t* host_ip, uint32_t* pod_ip);
 
-/* Device-resident outputs for zero-copy consumers (valid until the next tick). */
+/* Device-resident outputs of the last collected tick, for zero-copy consumers
+ * (valid until the next kwok_tick_submit / kwok_tick). */
 typedef struct kwok_device_view {
     const void* arena;
     const int32_t* heartbeat_nodes;

@@ -12,9 +12,9 @@ import numpy as np
 ABI_VERSION = 1
 COMM_ID_BYTES = 128
 
-OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE, EBUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8, -9
 ERRNAMES = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EDOMAIN", -4: "EFULL", -5: "EDEVICE",
-            -6: "ECOMM", -7: "ENOTFOUND", -8: "ENOTMINE"}
+            -6: "ECOMM", -7: "ENOTFOUND", -8: "ENOTMINE", -9: "EBUSY"}
 
 OP_UPSERT, OP_DELETE = 1, 2
 PHASE_NONE, PHASE_PENDING, PHASE_RUNNING, PHASE_SUCCEEDED, PHASE_FAILED, PHASE_UNKNOWN, PHASE_OTHER = range(7)

@@ -113,6 +113,7 @@ struct GridBar {
     uint32_t pcnt, pad1[31];    // pool-phase barrier: arrivals of the current instance
     uint32_t pgen, pad2[31];    //                     generation
     unsigned long long neg_entry_max, p1_max, stream_end_max, pad3[13];  // profiled ticks
+    uint32_t skip, pad4[31];    // multi rank: a BACK stopped for long lists; launches queued behind it skip
     unsigned long long acc[16][16];  // single rank: field accumulators (arrivals << ACC_SHIFT | sum), one line each
 };
 constexpr int ACC_SHIFT = 54;  // arrivals in the top 10 bits (<= 1023 chain blocks), sums below

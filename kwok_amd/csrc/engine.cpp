@@ -84,7 +84,7 @@ struct kwok_engine {
     std::vector<uint16_t> pod_fill;                  // per bucket: upper bound of used slots (only grows)
     bool pod_fill_dirty = false;
     uint16_t* d_pod_fill = nullptr;
-    std::vector<uint32_t> pending_del;
+    std::vector<uint32_t> pending_del;               // DeletePods routed since the last submit
 
     // ---- batch staging ----
     std::vector<NodeOp> nops;
@@ -110,8 +110,38 @@ struct kwok_engine {
     uint32_t max_init_len = 0;
 
     // ---- tick ----
-    TickHdr* hdr_h = nullptr;  // pinned
-    bool have_tick = false;
+    // A tick's outputs (header, lists, arena) live in one of two slots, so tick N+1
+    // can be queued while tick N is collected (kwok_tick_submit / _collect).  Slot 1
+    // is allocated on the first submit that finds slot 0 busy.
+    struct TickSlot {
+        TickHdr* hdr_h = nullptr;  // pinned: k_tick publishes the field totals here
+        uint8_t* arena = nullptr;
+        uint64_t arena_cap = 0;
+        int32_t *hb_nodes = nullptr, *init_nodes = nullptr, *pp_pods = nullptr, *del_pods = nullptr;
+        uint64_t *init_off = nullptr, *pp_off = nullptr;
+        uint32_t *init_len = nullptr, *pp_len = nullptr;
+        uint8_t* del_fin = nullptr;
+        DevState* d_S = nullptr;    // S with this slot's outputs, in device memory (out-of-line kernel phases)
+        DevState* S_pin = nullptr;  // pinned staging for its upload
+        DevState S_up{};            // the copy last uploaded
+        hipEvent_t done = nullptr;  // recorded after the tick's launches
+        hipEvent_t pev[4] = {};     // profiling: FRONT(+BACK) launch start/stop, BACK launch start/stop
+        bool alloc = false;
+        // the tick in the slot
+        int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
+        uint64_t now = 0, target = 0;
+        uint32_t tag = 0;
+        std::vector<uint32_t> pending_del;  // pods whose DeletePod this tick emits
+        int rc = 0;
+        std::string err;
+        kwok_tick_result res{};
+    };
+    TickSlot slots[2];
+    int queue[2] = {-1, -1};  // queued / done slots in submission order
+    int nq = 0;
+    int cur = -1;             // slot of the last collected tick (kwok_read_outputs)
+    size_t NLa = 0, PLa = 0;  // output list capacities
+    uint64_t arena_need = 0;  // worst-case output bytes of one tick
     ListDesc* d_ld = nullptr;  // [W] or scratch
     ncclComm_t comm = nullptr;
     XMsg* d_xall = nullptr;
@@ -120,19 +150,14 @@ struct kwok_engine {
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
     uint32_t n_stream = 0;      // k_tick heartbeat streamer blocks (the chain blocks: S.n_chain)
-    DevState* d_S = nullptr;    // S in device memory (the kernel's out-of-line phases read it there)
-    hipEvent_t done_ev = nullptr;  // tick completion (KWOK_SYNC=spin, the default)
-    bool sync_spin = true;
+    bool sync_spin = true;      // spin on a tick's completion event (KWOK_SYNC=spin, the default)
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
     uint64_t front_launches = 0;  // FRONT launches since the cross-block state was last zeroed
-    DevState* S_pin = nullptr;  // pinned staging for its upload
-    DevState S_up{};            // the copy last uploaded
     // diagnostics
     bool prof = false;
-    hipEvent_t pev[4] = {};  // k_tick launch start/stop: FRONT(+BACK) launch, BACK launch
     double prof_ms[KWOK_T_COUNT] = {};
     uint64_t prof_ticks = 0;
     double host_ms[KWOK_H_COUNT] = {};
@@ -306,18 +331,75 @@ int upload_specs(kwok_engine* e) {
     return KWOK_OK;
 }
 
-// the output arena must hold the worst case of one tick
+int drain(kwok_engine* e);  // finish every queued tick on the host (below)
+
+// the output arena must hold the worst case of one tick (grown per slot at submit)
 int size_arena(kwok_engine* e) {
-    uint64_t need = (uint64_t)e->NL * HB_STRIDE + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
+    e->arena_need = (uint64_t)e->NL * HB_STRIDE + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
                     (uint64_t)e->PL * e->max_pod_len + 256;
-    if (need <= e->S.arena_cap) return KWOK_OK;
-    need = std::max<uint64_t>(need, e->S.arena_cap + e->S.arena_cap / 2);
-    HIPCHK(e, hipStreamSynchronize(e->st));
-    if (e->S.arena) (void)hipFree(e->S.arena);
-    e->S.arena = nullptr;
-    e->S.arena_cap = 0;
-    if (hipMalloc((void**)&e->S.arena, need) != hipSuccess) return e->fail(KWOK_ENOMEM, "arena %llu", (unsigned long long)need);
-    e->S.arena_cap = need;
+    return KWOK_OK;
+}
+int grow_arena(kwok_engine* e, kwok_engine::TickSlot& T) {  // T holds no queued tick
+    if (e->arena_need <= T.arena_cap) return KWOK_OK;
+    const uint64_t need = std::max<uint64_t>(e->arena_need, T.arena_cap + T.arena_cap / 2);
+    if (T.arena) (void)hipFree(T.arena);
+    T.arena = nullptr;
+    T.arena_cap = 0;
+    if (hipMalloc((void**)&T.arena, need) != hipSuccess) return e->fail(KWOK_ENOMEM, "arena %llu", (unsigned long long)need);
+    T.arena_cap = need;
+    return KWOK_OK;
+}
+int alloc_slot(kwok_engine* e, int k) {
+    kwok_engine::TickSlot& T = e->slots[k];
+    int rc = 0;
+    if ((rc = dalloc(e, &T.hb_nodes, e->NLa)) || (rc = dalloc(e, &T.init_nodes, e->NLa)) ||
+        (rc = dalloc(e, &T.init_off, e->NLa)) || (rc = dalloc(e, &T.init_len, e->NLa)) ||
+        (rc = dalloc(e, &T.pp_pods, e->PLa)) || (rc = dalloc(e, &T.pp_off, e->PLa)) || (rc = dalloc(e, &T.pp_len, e->PLa)) ||
+        (rc = dalloc(e, &T.del_pods, e->PLa)) || (rc = dalloc(e, &T.del_fin, e->PLa)) || (rc = dalloc(e, &T.d_S, 1)))
+        return rc;
+    if (hipHostMalloc((void**)&T.hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&T.S_pin, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
+        return e->fail(KWOK_ENOMEM, "pinned tick header");
+    memset(T.hdr_h, 0, sizeof(TickHdr));
+    if (hipEventCreateWithFlags(&T.done, hipEventDisableTiming) != hipSuccess) return e->fail(KWOK_EDEVICE, "event create");
+    for (auto& ev : T.pev)
+        if (e->prof && !ev) HIPCHK(e, hipEventCreate(&ev));
+    T.alloc = true;
+    return KWOK_OK;
+}
+void free_slot(kwok_engine::TickSlot& T) {
+    void* ptrs[] = {T.arena, T.hb_nodes, T.init_nodes, T.init_off, T.init_len, T.pp_pods,
+                    T.pp_off, T.pp_len, T.del_pods, T.del_fin, T.d_S};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (T.hdr_h) (void)hipHostFree(T.hdr_h);
+    if (T.S_pin) (void)hipHostFree(T.S_pin);
+    if (T.done) (void)hipEventDestroy(T.done);
+    for (auto& ev : T.pev)
+        if (ev) (void)hipEventDestroy(ev);
+}
+// this slot's outputs into S (what launches read), uploaded to the slot's device copy if changed
+int bind_slot(kwok_engine* e, int k) {
+    kwok_engine::TickSlot& T = e->slots[k];
+    DevState& S = e->S;
+    S.arena = T.arena;
+    S.arena_cap = T.arena_cap;
+    S.hb_nodes = T.hb_nodes;
+    S.init_nodes = T.init_nodes;
+    S.init_off = T.init_off;
+    S.init_len = T.init_len;
+    S.pp_pods = T.pp_pods;
+    S.pp_off = T.pp_off;
+    S.pp_len = T.pp_len;
+    S.del_pods = T.del_pods;
+    S.del_fin = T.del_fin;
+    S.hdr_host = T.hdr_h;
+    S.self = T.d_S;
+    if (memcmp(&T.S_up, &S, sizeof(DevState)) != 0) {  // pointers / sizes changed since the last upload
+        *T.S_pin = S;  // the slot's previous upload has completed (its tick was collected)
+        HIPCHK(e, hipMemcpyAsync(T.d_S, T.S_pin, sizeof(DevState), hipMemcpyHostToDevice, e->st));
+        T.S_up = S;
+    }
     return KWOK_OK;
 }
 
@@ -466,22 +548,15 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
-                    e->S.use_list, e->S.rel_list, e->S.arena, e->S.hb_nodes, e->S.init_nodes, e->S.init_off,
-                    e->S.init_len, e->S.pp_pods, e->S.pp_off, e->S.pp_len, e->S.del_pods, e->S.del_fin,
-                    e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
+                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    if (e->hdr_h) (void)hipHostFree(e->hdr_h);
+    for (auto& T : e->slots) free_slot(T);
     if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
-    if (e->S_pin) (void)hipHostFree(e->S_pin);
-    if (e->done_ev) (void)hipEventDestroy(e->done_ev);
-    if (e->d_S) (void)hipFree(e->d_S);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->comm) ncclCommDestroy(e->comm);
-    for (auto& ev : e->pev)
-        if (ev) (void)hipEventDestroy(ev);
     if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
@@ -587,6 +662,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
     // node / pod arrays: whole 16-byte vectors at the end (Cn % 4 == 0, Cp % 8 == 0)
     const size_t NLa = (size_t)e->NL + 16, PLa = (size_t)e->PL + 16;
+    e->NLa = NLa;
+    e->PLa = PLa;
     int rc = 0;
     if ((rc = dalloc(e, &S.node_state, NLa)) || (rc = dalloc(e, &S.node_blob, NLa)) ||
         (rc = dalloc(e, &S.node_tick, NLa)) || (rc = dalloc(e, &S.pod_state, PLa)) ||
@@ -602,11 +679,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
-        (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &S.hb_nodes, NLa)) ||
-        (rc = dalloc(e, &S.init_nodes, NLa)) || (rc = dalloc(e, &S.init_off, NLa)) ||
-        (rc = dalloc(e, &S.init_len, NLa)) || (rc = dalloc(e, &S.pp_pods, PLa)) || (rc = dalloc(e, &S.pp_off, PLa)) ||
-        (rc = dalloc(e, &S.pp_len, PLa)) || (rc = dalloc(e, &S.del_pods, PLa)) || (rc = dalloc(e, &S.del_fin, PLa)) ||
-        (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))))
+        (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))) ||
+        (rc = alloc_slot(e, 0)))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
     {
@@ -622,20 +696,13 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
-    if ((rc = dalloc(e, &e->d_S, 1))) return bail(rc);
     {
         const char* sy = getenv("KWOK_SYNC");
         e->sync_spin = !(sy && strcmp(sy, "block") == 0);
-        if (hipEventCreateWithFlags(&e->done_ev, hipEventDisableTiming) != hipSuccess)
-            return bail(e->fail(KWOK_EDEVICE, "event create"));
     }
-    S.self = e->d_S;
-    if (hipHostMalloc((void**)&e->hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&e->S_pin, sizeof(DevState), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipHostMallocDefault) != hipSuccess)
         return bail(KWOK_ENOMEM);
     S.hb_pre = e->d_hb_pre;
-    S.hdr_host = e->hdr_h;   // zero-copy: k_tick's last block publishes the header
     S.pod_fill = e->d_pod_fill;
     S.rank = e->rank;
     if (W > 1) {
@@ -664,7 +731,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->pod_stamp.assign(e->PL, 0);
     e->pod_opi.assign(e->PL, 0);
     e->max_init_len = 0;
-    if ((rc = size_arena(e))) return bail(rc);
+    if ((rc = size_arena(e)) || (rc = grow_arena(e, e->slots[0]))) return bail(rc);
     {
         hipError_t r = hipStreamSynchronize(e->st);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "create sync: %s", hipGetErrorString(r)));
@@ -676,6 +743,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
 int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
                            int32_t* out_id) {
     if (!e || !spec || !out_id) return KWOK_EINVAL;
+    drain(e);  // the host mirrors reflect every submitted tick
     auto get = [&](kwok_str s, std::string& o) {
         if ((size_t)s.off + s.len > arena_len) return false;
         o.assign(arena + s.off, s.len);
@@ -722,6 +790,7 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
 int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
                       int32_t* out_handles, int32_t* out_status) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
+    drain(e);  // the host mirrors reflect every submitted tick
     e->gen++;
     int rejected = 0;
     for (size_t i = 0; i < n; i++) {
@@ -801,6 +870,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
+    drain(e);  // the host mirrors reflect every submitted tick
     e->gen++;
     int rejected = 0;
     const int32_t pbase = (int32_t)(e->b_lo * e->Cp);
@@ -925,24 +995,31 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
 
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     if (!e || (n && !ips)) return KWOK_EINVAL;
+    drain(e);  // the host mirrors reflect every submitted tick
     e->gen++;
     e->puts.assign(ips, ips + n);
     return flush_ops(e);
 }
 
 namespace {
-// Enqueue one tick on e->st.  Single rank: ONE persistent k_tick launch (no host
-// synchronisation, no graph needed).  Multi-rank: k_tick FRONT (classify, bases,
-// exchange message) -> allgather -> k_tick BACK (fold messages, lists, pool,
-// emission).
-int enqueue_tick(kwok_engine* e, uint64_t now) {
+enum { SLOT_FREE = 0, SLOT_QUEUED = 1, SLOT_DONE = 2 };
+
+// Enqueue one tick on e->st into slot k.  Single rank: ONE persistent k_tick
+// launch (no host synchronisation, no graph needed).  Multi-rank: k_tick FRONT
+// (classify, bases, exchange message) -> allgather -> k_tick BACK (fold
+// messages, lists, pool, emission).  requeue: the slot's tick was skipped on
+// the device (queued behind a tick that needed finish_long_lists) and runs
+// again with its own tag and arrival target.
+int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     DevState& S = e->S;
+    kwok_engine::TickSlot& T = e->slots[k];
     hipStream_t st = e->st;
-    hipEvent_t* ev = e->prof ? e->pev : nullptr;
+    hipEvent_t* ev = e->prof ? T.pev : nullptr;
     const uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
     if (e->hb_pre_dirty) {
         // heartbeat handles are written in node order at per-chain-block bases:
         // managed nodes of the buckets before each block's range (host-maintained)
+        HIPCHK(e, hipStreamSynchronize(st));  // hb_pre_h is pinned staging read by a queued copy
         uint32_t acc = 0, bk = 0;
         for (uint32_t b = 0; b <= S.n_chain; b++) {
             const uint32_t lo = (uint32_t)((uint64_t)e->nb * b / S.n_chain);
@@ -955,40 +1032,47 @@ int enqueue_tick(kwok_engine* e, uint64_t now) {
     // a long heartbeat stream is shared with the chain blocks once they are done
     // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)HB_STRIDE >= (32ull << 20) ? 921u : 1024u);
-    if (memcmp(&e->S_up, &S, sizeof(DevState)) != 0) {  // pointers / sizes changed since the last upload
-        *e->S_pin = S;
-        HIPCHK(e, hipMemcpyAsync(e->d_S, e->S_pin, sizeof(DevState), hipMemcpyHostToDevice, st));
-        e->S_up = S;
-    }
+    int rc = bind_slot(e, k);
+    if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
-    if (++e->tick_tag == 0) e->tick_tag = 1;
-    const uint64_t target = ++e->front_launches * S.n_chain;
+    if (!requeue) {
+        memset(T.hdr_h, 0, sizeof(TickHdr));  // the slot's previous tick was collected
+        if (++e->tick_tag == 0) e->tick_tag = 1;
+        T.tag = e->tick_tag;
+        T.target = ++e->front_launches * S.n_chain;
+    }
+    const uint64_t now = T.now;
     if (e->W == 1) {
-        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, e->tick_tag, target, st,
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
-        return KWOK_OK;
+    } else {
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, T.tag, T.target, st,
+                    ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+        // one allgather of the fixed-size exchange message, then BACK: it folds the
+        // gathered messages and applies the inline lists itself (no host round trip).
+        // Lists too long to be inline: BACK flags it and the host finishes the tick
+        // with a second allgather (finish_long_lists).
+        rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
+        if (rc) return rc;
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, T.tag, T.target, st,
+                    ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+        HIPCHK(e, hipGetLastError());
     }
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, e->tick_tag, target, st,
-                ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
-    // one allgather of the fixed-size exchange message, then BACK: it folds the
-    // gathered messages and applies the inline lists itself (no host round trip).
-    // Lists too long to be inline: BACK flags it and the host finishes the tick
-    // with a second allgather (finish_long_lists).
-    int rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
-    if (rc) return rc;
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, e->tick_tag, target, st,
-                ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
-    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(T.done, st));
     return KWOK_OK;
 }
-// multi rank, after a BACK launch that found lists too long to be inline (the
-// same on every rank: the flag comes from the gathered messages): gather the
-// lists, apply every rank's Uses and Puts, and run BACK again
-int finish_long_lists(kwok_engine* e, uint64_t now) {
+// multi rank, after the BACK launch of slot k's tick found lists too long to be
+// inline (the same on every rank: the flag comes from the gathered messages):
+// gather the lists, apply every rank's Uses and Puts, and run BACK again.  A tick
+// queued behind it skipped on the device (GridBar::skip) and is enqueued again.
+int finish_long_lists(kwok_engine* e, int k, int next) {
     DevState& S = e->S;
+    kwok_engine::TickSlot& T = e->slots[k];
     hipStream_t st = e->st;
-    e->hdr_h->xovf = 0;
+    T.hdr_h->xovf = 0;
+    // the skipped tick's allgather re-gathered the same messages (its FRONT did not run)
+    HIPCHK(e, hipStreamSynchronize(st));
     HIPCHK(e, hipMemcpy(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost));
     uint64_t maxl = 0;
     for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
@@ -1000,10 +1084,13 @@ int finish_long_lists(kwok_engine* e, uint64_t now) {
             hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
             return e->fail(KWOK_ENOMEM, "exchange lists");
     }
+    int rc = bind_slot(e, k);
+    if (rc) return rc;
+    HIPCHK(e, hipMemsetAsync(&S.bar->skip, 0, sizeof(uint32_t), st));
     const XMsg& me = e->h_xall[e->rank];
     if (me.n_use) HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
     if (me.n_rel) HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
-    int rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
+    rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
     if (rc) return rc;
     std::vector<ListDesc> ld(e->W);
     for (int r = 0; r < e->W; r++) {
@@ -1014,18 +1101,17 @@ int finish_long_lists(kwok_engine* e, uint64_t now) {
     }
     HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
     launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
-    launch_tick(S, e->n_stream, now, (uint64_t)e->start, (uint32_t)e->n_managed, TICK_BACK | TICK_XLISTS, e->tick_tag,
-                e->front_launches * S.n_chain, st);
+    launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed, TICK_BACK | TICK_XLISTS, T.tag,
+                T.target, st);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(st));
+    if (next >= 0) return enqueue_tick(e, next, true);
     return KWOK_OK;
 }
-}  // namespace
 
 // single rank: the kernel publishes the tick's field totals (TickHdr::tot); the
 // counts, output layout and counters follow from them
-static void derive_header(kwok_engine* e) {
-    TickHdr& H = *e->hdr_h;
+void derive_header(TickHdr& H, uint64_t arena_cap) {
     const uint64_t* t = H.tot;
     H.n_hb = (uint32_t)t[AG_HB];
     H.n_init = (uint32_t)t[AG_INIT];
@@ -1042,7 +1128,7 @@ static void derive_header(kwok_engine* e) {
     H.init_base = (uint64_t)H.n_hb * HB_STRIDE;
     H.pod_base = H.init_base + H.init_bytes;
     H.arena_bytes = H.pod_base + H.pp_bytes;
-    H.overflow = H.arena_bytes > e->S.arena_cap;
+    H.overflow = H.arena_bytes > arena_cap;
     const int map[13] = {AG_HB, AG_INIT, AG_PP, AG_DEL, AG_ALLOC, AG_REL, AG_EVAL,
                          AG_LOCK, AG_MANAGED, AG_READY, AG_TOTAL, AG_PENDING, AG_RUNNING};
     for (int k = 0; k < 16; k++) H.local_counters[k] = H.counters[k] = k < 13 ? t[map[k]] : 0;
@@ -1051,10 +1137,10 @@ static void derive_header(kwok_engine* e) {
     H.rel_total = t[AG_REL];
 }
 
-static bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && e->W == 1; }
+bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && e->W == 1; }
 
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
-static void trace_tick(kwok_engine* e) {
+void trace_tick(kwok_engine* e) {
     const size_t G = e->S.n_chain, N = G + e->n_stream;
     static const int skip = getenv("KWOK_TICK_TRACE_SKIP") ? atoi(getenv("KWOK_TICK_TRACE_SKIP")) : 5;
     if ((int)++e->trace_seen <= skip) return;  // skip the initial (bulk) ticks
@@ -1081,61 +1167,81 @@ static void trace_tick(kwok_engine* e) {
     e->trace_ticks++;
 }
 
-extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
-    if (!e) return KWOK_EINVAL;
-    if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
-    hipStream_t st = e->st;
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    memset(e->hdr_h->clk, 0, sizeof e->hdr_h->clk);  // this tick's stamps only (the launch orders it)
-    {
-        int rc = enqueue_tick(e, (uint64_t)now_unix);
-        if (rc) return rc;
-    }
+using clk = std::chrono::steady_clock;
+double ms_between(clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); }
+
+// Finish the oldest queued tick on the host: wait for it, complete a multi-rank
+// tick with long lists, derive the header, check errors, mirror DeletePods into
+// the host slot state.  The result stays in the slot until kwok_tick_collect.
+int retire(kwok_engine* e) {
+    int qi = -1;
+    for (int i = 0; i < e->nq; i++)
+        if (e->slots[e->queue[i]].state == SLOT_QUEUED) {
+            qi = i;
+            break;
+        }
+    if (qi < 0) return KWOK_OK;
+    const int k = e->queue[qi];
+    const int next = qi + 1 < e->nq ? e->queue[qi + 1] : -1;  // a tick queued behind this one
+    kwok_engine::TickSlot& T = e->slots[k];
+    T.state = SLOT_DONE;
+    T.rc = KWOK_OK;
+    auto failed = [&](int rc) {
+        T.rc = rc;
+        T.err = e->err;
+        return rc;
+    };
     const auto t1 = clk::now();
     if (e->sync_spin) {
-        // spin on the tick's completion event: a blocking stream wait sleeps and
-        // pays the wake-up latency on every tick
-        HIPCHK(e, hipEventRecord(e->done_ev, st));
+        // spin on the tick's completion event: a blocking wait sleeps and pays the
+        // wake-up latency on every tick
         hipError_t q;
-        while ((q = hipEventQuery(e->done_ev)) == hipErrorNotReady) {
+        while ((q = hipEventQuery(T.done)) == hipErrorNotReady) {
         }
-        HIPCHK(e, q);
-    } else {
-        HIPCHK(e, hipStreamSynchronize(st));
+        if (q != hipSuccess) return failed(e->fail(KWOK_EDEVICE, "tick: %s", hipGetErrorString(q)));
+    } else if (hipEventSynchronize(T.done) != hipSuccess) {
+        return failed(e->fail(KWOK_EDEVICE, "tick event sync"));
     }
-    if (e->W > 1 && e->hdr_h->xovf) {
-        int rc = finish_long_lists(e, (uint64_t)now_unix);
-        if (rc) return rc;
+    if (e->W > 1 && T.hdr_h->xovf) {
+        int rc = finish_long_lists(e, k, next);
+        if (rc) return failed(rc);
     }
     const auto t2 = clk::now();
-    if (e->W == 1) derive_header(e);
-    const TickHdr& H = *e->hdr_h;
+    if (e->W == 1) derive_header(*T.hdr_h, T.arena_cap);
+    const TickHdr& H = *T.hdr_h;
     if (trace_enabled(e)) trace_tick(e);
     if (H.err) {
         const uint32_t err = H.err;
-        e->hdr_h->err = 0;
+        // a tick queued behind a failed one ran on its state: fail it as well
+        (void)hipStreamSynchronize(e->st);
         (void)hipMemset(e->S.bar, 0, sizeof(GridBar));  // the next tick starts from a clean count
         e->front_launches = 0;
-        if (err & TICK_ERR_BARRIER)
-            return e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
-                           e->S.n_chain);
-        return e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
-                       (unsigned long long)e->n_managed);
+        int rc = (err & TICK_ERR_BARRIER)
+                     ? e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
+                               e->S.n_chain)
+                     : e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
+                               (unsigned long long)e->n_managed);
+        if (next >= 0) {
+            kwok_engine::TickSlot& U = e->slots[next];
+            U.state = SLOT_DONE;
+            U.rc = rc;
+            U.err = e->err;
+        }
+        return failed(rc);
     }
     if (e->prof) {
         // kernel time from the launch events; the phase split from the kernel's
         // s_memrealtime stamps (100 MHz)
         float k0 = 0, k1 = 0;
-        (void)hipEventElapsedTime(&k0, e->pev[0], e->pev[1]);
-        if (e->W > 1) (void)hipEventElapsedTime(&k1, e->pev[2], e->pev[3]);
+        (void)hipEventElapsedTime(&k0, T.pev[0], T.pev[1]);
+        if (e->W > 1) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
         const double kern = (double)k0 + k1;
-        auto span = [&](int a, int b) { return H.clk[b] > H.clk[a] ? (double)(H.clk[b] - H.clk[a]) * 1e-5 : 0.0; };
         // the streamers' latest exit, kept on the device (they never touch the header)
         unsigned long long send = 0;
         (void)hipMemcpy(&send, &e->S.bar->stream_end_max, 8, hipMemcpyDeviceToHost);
         (void)hipMemset(&e->S.bar->stream_end_max, 0, 8);
-        e->hdr_h->clk[CLK_STREAM_END] = send;
+        T.hdr_h->clk[CLK_STREAM_END] = send;
+        auto span = [&](int a, int b) { return H.clk[b] > H.clk[a] ? (double)(H.clk[b] - H.clk[a]) * 1e-5 : 0.0; };
         const double classify = span(CLK_ENTRY_MIN, CLK_P1_MAX), stream = span(CLK_ENTRY_MIN, CLK_STREAM_END);
         const double header = span(CLK_P1_MAX, CLK_HDR), pool = span(CLK_BACK, CLK_POOL);
         e->prof_ms[KWOK_T_CLASSIFY] += classify;
@@ -1148,9 +1254,9 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
         e->prof_ms[KWOK_T_KERNEL] += kern;
         e->prof_ticks++;
     }
-    if (H.overflow) return e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes);
+    if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));
     // host mirror: pods deleted by the tick (DeletePod) free their slots
-    for (uint32_t slot : e->pending_del) {
+    for (uint32_t slot : T.pending_del) {
         if (!e->pod_delpend[slot] || !e->pod_used[slot]) continue;
         uint32_t nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
         e->pod_used[slot] = 0;
@@ -1162,43 +1268,110 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
             free_node_if_unused(e, nslot);
         }
     }
-    e->pending_del.clear();
-    if (!e->nops.empty()) {
+    T.pending_del.clear();
+    // the slot-freeing ops of deleted nodes without pods: no tick reads such a
+    // node, so with a tick already queued they wait for the next flush
+    if (!e->nops.empty() && next < 0) {
         int rc = flush_ops(e);
-        if (rc) return rc;
+        if (rc) return failed(rc);
     }
-    e->have_tick = true;
-    {
-        const auto t3 = clk::now();
-        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        e->host_ms[KWOK_H_ENQUEUE] += ms(t0, t1);
-        e->host_ms[KWOK_H_WAIT] += ms(t1, t2);
-        e->host_ms[KWOK_H_POST] += ms(t2, t3);
-        e->host_ms[KWOK_H_TOTAL] += ms(t0, t3);
-        e->host_ticks++;
+    kwok_tick_result& r = T.res;
+    memset(&r, 0, sizeof(r));
+    r.n_heartbeat = H.n_hb;
+    r.heartbeat_len = HB_LEN;
+    r.heartbeat_stride = HB_STRIDE;
+    r.n_node_init = H.n_init;
+    r.n_pod_patch = H.n_pp;
+    r.n_delete = H.n_del;
+    r.arena_bytes = H.arena_bytes;
+    for (int c = 0; c < KWOK_COUNTER_COUNT; c++) {
+        r.counters[c] = H.counters[c];
+        r.local_counters[c] = H.local_counters[c];
     }
-    if (res) {
-        memset(res, 0, sizeof(*res));
-        res->n_heartbeat = H.n_hb;
-        res->heartbeat_len = HB_LEN;
-        res->heartbeat_stride = HB_STRIDE;
-        res->n_node_init = H.n_init;
-        res->n_pod_patch = H.n_pp;
-        res->n_delete = H.n_del;
-        res->arena_bytes = H.arena_bytes;
-        for (int k = 0; k < KWOK_COUNTER_COUNT; k++) {
-            res->counters[k] = H.counters[k];
-            res->local_counters[k] = H.local_counters[k];
-        }
-    }
+    const auto t3 = clk::now();
+    e->host_ms[KWOK_H_WAIT] += ms_between(t1, t2);
+    e->host_ms[KWOK_H_POST] += ms_between(t2, t3);
+    e->host_ms[KWOK_H_TOTAL] += ms_between(t1, t3);
+    e->host_ticks++;
     return KWOK_OK;
+}
+
+// every queued tick finished on the host (before anything that reads or changes
+// the host mirrors or device state outside the tick stream)
+int drain(kwok_engine* e) {
+    for (int i = 0; i < e->nq; i++)
+        if (e->slots[e->queue[i]].state == SLOT_QUEUED) retire(e);  // per-tick failures stay in the slots
+    return KWOK_OK;
+}
+}  // namespace
+
+extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
+    if (!e) return KWOK_EINVAL;
+    if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
+    if (e->nq >= 2) return e->fail(KWOK_EBUSY, "two ticks outstanding: collect one first");
+    if (e->nq >= 1 && (e->prof || trace_enabled(e)))
+        return e->fail(KWOK_EBUSY, "profiled / traced ticks are not queued behind each other");
+    const auto t0 = clk::now();
+    int k = -1;
+    for (int pass = 0; pass < 2 && k < 0; pass++)  // prefer keeping the last collected tick's outputs
+        for (int i = 0; i < 2 && k < 0; i++)
+            if (e->slots[i].alloc && e->slots[i].state == SLOT_FREE && (pass == 1 || i != e->cur)) k = i;
+    if (k < 0) {
+        int rc = alloc_slot(e, 1);
+        if (rc) return rc;
+        k = 1;
+    }
+    kwok_engine::TickSlot& T = e->slots[k];
+    int rc = grow_arena(e, T);
+    if (rc) return rc;
+    if (!e->nops.empty() && (rc = flush_ops(e))) return rc;  // deferred by retire
+    if (k == e->cur) e->cur = -1;  // its outputs are overwritten
+    T.now = (uint64_t)now_unix;
+    T.pending_del.swap(e->pending_del);
+    e->pending_del.clear();
+    rc = enqueue_tick(e, k, false);
+    if (rc) {
+        e->pending_del.swap(T.pending_del);
+        return rc;
+    }
+    T.state = SLOT_QUEUED;
+    e->queue[e->nq++] = k;
+    e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
+    e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
+    return KWOK_OK;
+}
+
+extern "C" int kwok_tick_collect(kwok_engine* e, kwok_tick_result* res) {
+    if (!e) return KWOK_EINVAL;
+    if (e->nq == 0) return e->fail(KWOK_EINVAL, "no tick submitted");
+    const int k = e->queue[0];
+    kwok_engine::TickSlot& T = e->slots[k];
+    if (T.state == SLOT_QUEUED) retire(e);
+    e->queue[0] = e->queue[1];
+    e->queue[1] = -1;
+    e->nq--;
+    T.state = SLOT_FREE;
+    if (T.rc) {
+        e->err = T.err;
+        return T.rc;
+    }
+    e->cur = k;
+    if (res) *res = T.res;
+    return KWOK_OK;
+}
+
+extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res) {
+    if (!e) return KWOK_EINVAL;
+    if (e->nq) return e->fail(KWOK_EBUSY, "ticks outstanding: kwok_tick_collect them first");
+    int rc = kwok_tick_submit(e, now_unix);
+    return rc ? rc : kwok_tick_collect(e, res);
 }
 
 int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     if (!e || !o) return KWOK_EINVAL;
-    if (!e->have_tick) return e->fail(KWOK_EINVAL, "no tick yet");
-    const TickHdr& H = *e->hdr_h;
-    DevState& S = e->S;
+    if (e->cur < 0) return e->fail(KWOK_EINVAL, "no collected tick (or its slot was reused by a submit)");
+    const kwok_engine::TickSlot& S = e->slots[e->cur];  // outputs of the last collected tick
+    const TickHdr& H = *S.hdr_h;
     hipStream_t st = e->st;
     auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
         if (!dst || !bytes) return hipSuccess;
@@ -1224,19 +1397,23 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
 
 int kwok_device_outputs(kwok_engine* e, kwok_device_view* v) {
     if (!e || !v) return KWOK_EINVAL;
-    v->arena = e->S.arena;
-    v->heartbeat_nodes = e->S.hb_nodes;
-    v->pod_patch_pods = e->S.pp_pods;
-    v->pod_patch_off = e->S.pp_off;
-    v->pod_patch_len = e->S.pp_len;
+    if (e->cur < 0) return e->fail(KWOK_EINVAL, "no collected tick (or its slot was reused by a submit)");
+    const kwok_engine::TickSlot& T = e->slots[e->cur];
+    v->arena = T.arena;
+    v->heartbeat_nodes = T.hb_nodes;
+    v->pod_patch_pods = T.pp_pods;
+    v->pod_patch_off = T.pp_off;
+    v->pod_patch_len = T.pp_len;
     v->stream = e->st;
     return KWOK_OK;
 }
 
 int kwok_profile_enable(kwok_engine* e, int on) {
     if (!e) return KWOK_EINVAL;
-    for (auto& ev : e->pev)
-        if (!ev) HIPCHK(e, hipEventCreate(&ev));
+    drain(e);
+    for (auto& T : e->slots)
+        for (auto& ev : T.pev)
+            if (T.alloc && !ev) HIPCHK(e, hipEventCreate(&ev));
     e->prof = on != 0;
     memset(e->prof_ms, 0, sizeof e->prof_ms);
     e->prof_ticks = 0;
@@ -1272,6 +1449,7 @@ uint64_t kwok_node_size(kwok_engine* e) { return e ? e->n_managed : 0; }
 int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase, uint32_t* host_ip,
                    uint32_t* pod_ip) {
     if (!e) return KWOK_EINVAL;
+    drain(e);
     std::vector<uint16_t> sth(e->PL);
     std::vector<uint32_t> hh(e->PL), ph(e->PL);
     HIPCHK(e, hipMemcpyAsync(sth.data(), e->S.pod_state, (size_t)e->PL * 2, hipMemcpyDeviceToHost, e->st));

@@ -1524,6 +1524,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ uint4 patch_buf4[BLOCK / 64 * PATCH_BUF / 16];
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
+    if (S.world > 1 && !(phases & TICK_XLISTS) &&
+        __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        return;  // queued behind a tick the host has not finished (long lists): re-launched later
 #define TSTAMP(k)                                                                                         \
     do {                                                                                                  \
         if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -1774,7 +1777,12 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if (maxl > (uint32_t)XINLINE) {
                 // lists that did not fit inline: the host runs the second allgather,
                 // applies them and launches BACK again (TICK_XLISTS)
-                if (b == 0 && t == 0) S.hdr_host->xovf = 1;
+                if (b == 0 && t == 0) {
+                    S.hdr_host->xovf = 1;
+                    // a tick already queued behind this one must not run before the
+                    // host finishes this one (kwok_tick_submit): its launches skip
+                    __hip_atomic_store(&S.bar->skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 return;
             }
             // every rank's Uses into `used`, every rank's Puts into rel_bm (folded in

@@ -78,6 +78,8 @@ def declare(lib, pre):
             "profile_enable": (C.c_int, [VP, C.c_int]),
             "profile_read": (C.c_int, [VP, VP, VP]),
             "profile_host": (C.c_int, [VP, C.c_int, VP, VP]),
+            "tick_submit": (C.c_int, [VP, C.c_int64]),
+            "tick_collect": (C.c_int, [VP, P(abi.TickResult)]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name)
@@ -269,6 +271,16 @@ class Engine(EngineBase):
 
     def __init__(self, cfg=None, **kw):
         super().__init__(load_engine_lib(), cfg if cfg is not None else make_config(**kw))
+
+    # kwok_tick in two halves: tick N+1 runs on the device while tick N is collected
+    def tick_submit(self, now_unix):
+        self._check(self._lib.kwok_tick_submit(self._h, now_unix), "tick_submit")
+
+    def tick_collect(self, read=True):
+        res = abi.TickResult()
+        self._check(self._lib.kwok_tick_collect(self._h, C.byref(res)), "tick_collect")
+        self.last = res
+        return self.read_outputs(res) if read else res
 
     PHASES = ("classify", "stream", "header", "exchange", "pool", "emit", "kernel")  # KWOK_T_* order
     HOST = ("enqueue", "wait", "post", "total")  # KWOK_H_* order

@@ -105,7 +105,7 @@ class Runner:
         self.state = {}    # pod key -> (phase, hostip, podip) as last seen
         self.now = 1704067230
 
-    def run_tick(self, nodes, pods):
+    def run_tick(self, nodes, pods, pair=False):
         if nodes:
             ar = abi.Arena()
             ev = np.zeros(len(nodes), abi.NODE_EVENT_DTYPE)
@@ -167,7 +167,19 @@ class Runner:
             others = self.exchange_puts(released)
             if others:
                 self.b.pool_put(np.array(others, np.uint32))
-        out = self.b.tick(self.now)
+        if not pair:
+            return self._done(self.b.tick(self.now))
+        # two ticks with no events between: queued back to back where the backend
+        # can (kwok_tick_submit / _collect), one after the other otherwise
+        if hasattr(self.b, "tick_submit"):
+            self.b.tick_submit(self.now)
+            self.b.tick_submit(self.now + 30)
+            first = self._done(self.b.tick_collect())
+            return [first, self._done(self.b.tick_collect())]
+        first = self._done(self.b.tick(self.now))
+        return [first, self._done(self.b.tick(self.now))]
+
+    def _done(self, out):
         self.now += 30
         for h, _ in out.deletes:
             for k in [k for k, v in self.handles.items() if v == h]:
@@ -177,6 +189,16 @@ class Runner:
     def state_of(self, h):
         used, phase, hip, pip = self.b.dump_pods(h, 1)
         return dict(phase=int(phase[0]), hostip=abi.ip4s(int(hip[0])), podip=abi.ip4s(int(pip[0])))
+
+
+def run_all(runner, sc, pair=False):
+    """Summaries of every tick of scenario sc (pair: each step is two ticks,
+    queued back to back on backends that can)."""
+    out = []
+    for n, p in sc:
+        r = runner.run_tick(n, p, pair=pair)
+        out += [summarize(x) for x in (r if pair else [r])]
+    return out
 
 
 def summarize(out):

@@ -123,6 +123,26 @@ def replay(fx, backend, check=True, on_tick=None):
     return True
 
 
+def replay_queued(fx, backend):
+    """Replay with every tick submitted before the previous one is collected
+    (kwok_tick_submit / _collect); outputs must equal the plain replay's."""
+    specs = SpecCache(backend)
+    prev = None
+    for ti, t in enumerate(fx["ticks"]):
+        if t["node_events"]:
+            recs, arena = node_batch(t["node_events"])
+            backend.ingest_nodes_raw(recs, arena)
+        if t["pod_events"]:
+            recs, arena = pod_batch(t["pod_events"], specs)
+            backend.ingest_pods_raw(recs, arena)
+        backend.tick_submit(t["now"])
+        if prev is not None:
+            compare_tick(fx["name"], prev, fx["ticks"][prev]["expect"], backend.tick_collect())
+        prev = ti
+    compare_tick(fx["name"], prev, fx["ticks"][prev]["expect"], backend.tick_collect())
+    return True
+
+
 def compare_tick(name, ti, exp, out):
     where = "%s tick %d" % (name, ti)
     assert [list(d) for d in out.deletes] == exp["deletes"], where + " deletes"

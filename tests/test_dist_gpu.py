@@ -16,7 +16,7 @@ from test_dist_cpu import merge
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, outdir, big=False):
+def _worker(rank, world, port, outdir, big=False, pair=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -34,28 +34,32 @@ def _worker(rank, world, port, outdir, big=False):
 
     e = dc2.make(Engine, rank, world, allgather=dc2.gloo_allgather_fn(), big=big)
     run = dc2.Runner(e, world, rank, exchange_puts)
-    res = [dc2.summarize(run.run_tick(n, p)) for n, p in dc2.scenario(big=big, ticks=4 if big else 5)]
+    res = dc2.run_all(run, dc2.scenario(big=big, ticks=4 if big else 5), pair)
     with open(os.path.join(outdir, "r%d.pkl" % rank), "wb") as f:
         pickle.dump(res, f)
     e.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("big", [False, True], ids=["inline-lists", "long-lists"])
-def test_two_rank_engine_matches_single_and_oracle(big):
+@pytest.mark.parametrize("big,pair", [(False, False), (True, False), (True, True)],
+                         ids=["inline-lists", "long-lists", "long-lists-queued"])
+def test_two_rank_engine_matches_single_and_oracle(big, pair):
+    """queued: every step is two ticks submitted back to back, so a tick queues
+    behind one whose lists are not inline (it skips on the device and is
+    launched again after the host finishes the first)."""
     from kwok_amd.engine import Engine
     from oracle.oracle import Oracle
     sc = dc.scenario(big=big, ticks=4 if big else 5)
     single_o = dc.Runner(dc.make(Oracle, 0, 1, big=big))
-    ref = [dc.summarize(single_o.run_tick(n, p)) for n, p in sc]
+    ref = dc.run_all(single_o, sc, pair)
     single_e = dc.Runner(dc.make(Engine, 0, 1, big=big))
-    eng = [dc.summarize(single_e.run_tick(n, p)) for n, p in sc]
+    eng = dc.run_all(single_e, sc, pair)
     for t, (g, r) in enumerate(zip(eng, ref)):
         for k in ("hb", "hb_body", "inits", "pods", "deletes", "counters"):
             assert g[k] == r[k], "single-rank engine tick %d %s" % (t, k)
     single_e.b.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(2, dc.free_port(), d, big), nprocs=2, start_method="spawn", join=True)
+        mp.start_processes(_worker, args=(2, dc.free_port(), d, big, pair), nprocs=2, start_method="spawn", join=True)
         parts = [pickle.load(open(os.path.join(d, "r%d.pkl" % r), "rb")) for r in range(2)]
     got = merge(parts)
     for t, (g, r) in enumerate(zip(got, ref)):

@@ -17,3 +17,11 @@ def test_engine_golden_trace(name):
     e = Engine(harness.config_for(fx))
     harness.replay(fx, e)
     e.close()
+
+
+@pytest.mark.parametrize("name", harness.TRACES)
+def test_engine_golden_trace_queued(name):
+    fx = harness.load_trace(name)
+    e = Engine(harness.config_for(fx))
+    harness.replay_queued(fx, e)
+    e.close()

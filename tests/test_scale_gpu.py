@@ -45,15 +45,20 @@ def compare_state(e, o, n_slots, where):
 
 def test_c2_full_parity_and_properties():
     """C2 at full size: initial tick (100k node inits, 1M Pending->Running with
-    IPs) and a steady tick, byte-exact against the oracle; IPs are exactly the
-    first 1M addresses of 10.0.0.1/8 in canonical (bucket, slot) order."""
+    IPs) and steady ticks, byte-exact against the oracle; IPs are exactly the
+    first 1M addresses of 10.0.0.1/8 in canonical (bucket, slot) order.  Ticks
+    0 and 1 are queued back to back (kwok_tick_submit x2, then collect), tick 2
+    is a plain kwok_tick."""
     e, fl, ph = workload.build_engine_fleet(Engine, 100_000)
     o, _, ph2 = workload.build_engine_fleet(Oracle, 100_000)
     assert (ph == ph2).all()
     n_slots = workload.BUCKETS * fl.cp
-    for t in range(2):
+    e.tick_submit(workload.S0 + 30)
+    e.tick_submit(workload.S0 + 60)
+    for t in range(3):
         now = workload.S0 + 30 * (t + 1)
-        eo, oo = e.tick(now), o.tick(now)
+        eo = e.tick_collect() if t < 2 else e.tick(now)
+        oo = o.tick(now)
         compare(eo, oo, "c2 tick %d" % t)
         if t == 0:
             assert eo.counters["pod_patch"] == 1_000_000 and eo.counters["node_init"] == 100_000
@@ -120,6 +125,16 @@ class Driver:
         compare(eo, oo, where)
         compare_state(self.e, self.o, self.n_slots, where)
         return eo
+
+    def tick_pair(self, where):
+        """two ticks queued back to back on the engine, one after the other on the oracle"""
+        self.e.tick_submit(self.now)
+        self.e.tick_submit(self.now + 30)
+        for k in range(2):
+            eo, oo = self.e.tick_collect(), self.o.tick(self.now)
+            self.now += 30
+            compare(eo, oo, "%s (queued %d)" % (where, k))
+        compare_state(self.e, self.o, self.n_slots, where)
 
     def live(self):
         used, phase, hip, pip = self.o.dump_pods(0, self.n_slots)
@@ -218,7 +233,10 @@ def test_churn_parity(seed, cidr):
             d.nodes(fl, managed=1, lockable=1)
         ev, ar = new_pods(rng, nh, 3000, d.spec, 0.02, ip_range)
         d.pods(ev, ar)
-        d.tick("churn seed %d tick %d" % (seed, t))
+        if t == 6:  # deletes, releases and Gets in the first of two queued ticks
+            d.tick_pair("churn seed %d tick %d" % (seed, t))
+        else:
+            d.tick("churn seed %d tick %d" % (seed, t))
     d.e.close()
     d.o.close()
 
