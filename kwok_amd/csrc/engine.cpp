@@ -357,11 +357,14 @@ int alloc_slot(kwok_engine* e, int k) {
         (rc = dalloc(e, &T.pp_pods, e->PLa)) || (rc = dalloc(e, &T.pp_off, e->PLa)) || (rc = dalloc(e, &T.pp_len, e->PLa)) ||
         (rc = dalloc(e, &T.del_pods, e->PLa)) || (rc = dalloc(e, &T.del_fin, e->PLa)) || (rc = dalloc(e, &T.d_S, 1)))
         return rc;
-    if (hipHostMalloc((void**)&T.hdr_h, sizeof(TickHdr), hipHostMallocDefault) != hipSuccess ||
+    // the header is coherent host memory written with system-scope stores, so the
+    // completion event needs no system-scope release (measured ~1.7 us per tick)
+    if (hipHostMalloc((void**)&T.hdr_h, sizeof(TickHdr), hipHostMallocCoherent) != hipSuccess ||
         hipHostMalloc((void**)&T.S_pin, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         return e->fail(KWOK_ENOMEM, "pinned tick header");
     memset(T.hdr_h, 0, sizeof(TickHdr));
-    if (hipEventCreateWithFlags(&T.done, hipEventDisableTiming) != hipSuccess) return e->fail(KWOK_EDEVICE, "event create");
+    if (hipEventCreateWithFlags(&T.done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+        return e->fail(KWOK_EDEVICE, "event create");
     for (auto& ev : T.pev)
         if (e->prof && !ev) HIPCHK(e, hipEventCreate(&ev));
     T.alloc = true;

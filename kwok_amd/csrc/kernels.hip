@@ -618,6 +618,14 @@ __device__ __forceinline__ uint64_t publish_and_arrive(const DevState& S, uint32
 
 // poll the arrival counter (sc1) until every chain block of this tick arrived,
 // then acquire (the pool phase reads bitmaps other blocks changed)
+// stores to the pinned host header: system scope (write-through to host memory),
+// so the host sees them once the tick's completion event fires (that event has no
+// system-scope release of its own)
+template <class T, class V>
+__device__ __forceinline__ void st_host(T* p, V v) {
+    __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void wait_arrivals(const DevState& S, uint64_t target) {
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1301,7 +1309,7 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
         // the pool leader may already have written its fields (it runs concurrently)
         if (!(skip_pool && (pool_clk || (i >= A0 && i < A1)))) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
         if (single && !(skip_alloc && i >= A0 && i < A1) && !(skip_pool && pool_clk))
-            reinterpret_cast<uint64_t*>(S.hdr_host)[i] = w;
+            st_host(reinterpret_cast<uint64_t*>(S.hdr_host) + i, w);
     }
     if (i == 0) {
         if (tot[AG_HB] != n_hb)  // the heartbeat stream was laid out for the host's count
@@ -1327,7 +1335,7 @@ __device__ __forceinline__ void publish_header(const DevState& S) {
     __syncthreads();
     const uint64_t* src = reinterpret_cast<const uint64_t*>(S.hdr);
     uint64_t* dst = reinterpret_cast<uint64_t*>(S.hdr_host);
-    for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += BLOCK) dst[i] = src[i];
+    for (int i = threadIdx.x; i < (int)(offsetof(TickHdr, err) / 8); i += BLOCK) st_host(dst + i, src[i]);
     __syncthreads();
 }
 
@@ -1430,14 +1438,14 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
             if (single) {  // the last arriver published everything else (publish_header)
                 TickHdr* P = S.hdr_host;
                 if (A) {
-                    P->usable_total = H->usable_total;
-                    P->take_usable = H->take_usable;
-                    P->fresh_in = H->fresh_in;
-                    P->fresh_out_start = H->fresh_out_start;
-                    P->cursor_index = H->cursor_index;
+                    st_host(&P->usable_total, H->usable_total);
+                    st_host(&P->take_usable, H->take_usable);
+                    st_host(&P->fresh_in, H->fresh_in);
+                    st_host(&P->fresh_out_start, H->fresh_out_start);
+                    st_host(&P->cursor_index, H->cursor_index);
                 }
-                P->clk[CLK_BACK] = H->clk[CLK_BACK];
-                P->clk[CLK_POOL] = H->clk[CLK_POOL];
+                st_host(&P->clk[CLK_BACK], H->clk[CLK_BACK]);
+                st_host(&P->clk[CLK_POOL], H->clk[CLK_POOL]);
                 __threadfence_system();
             }
         }
@@ -1689,46 +1697,46 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                     w = t == i ? ((uint64_t)f[2 * i] | (uint64_t)f[2 * i + 1] << 32) : w;
                 st_sc1(reinterpret_cast<uint64_t*>(S.blockagg + (size_t)b * AG_STRIDE) + t, w);
             }
-            // the Use checks of the speculative groups, in flight with the accumulator adds
+            // the Use checks of the speculative groups
             UsedWords u[SPEC_GROUPS];
 #pragma unroll
             for (int q = 0; q < SPEC_GROUPS; q++) u[q] = used_words(S, G[q], usec[q]);
-            if (t < AG_DIRTY) {
-                // lane t owns field t: one returning add of (one arrival | this block's
-                // value); the block whose add completes the count holds the tick's total
-                uint32_t v = 0;
+            uint32_t acc_v = 0;  // lane t < AG_DIRTY: this block's value of field t
 #pragma unroll
-                for (int i = 0; i < AG_DIRTY; i++) v = t == i ? f[i] : v;
-                unsigned long long* acc = &S.bar->acc[t][0];
-                const unsigned long long old = atomicAdd(acc, (1ull << ACC_SHIFT) | v);
-                if ((old >> ACC_SHIFT) == S.n_chain - 1u) {
-                    const uint64_t total = (old & ACC_MASK) + v;
-                    st_sc1(acc, 0ull);  // the next tick starts from zero
-                    S.hdr_host->tot[t] = total;
-                    if (t == AG_HB) {
-                        if (total != n_hb)  // the heartbeat stream was laid out for the host's count
-                            __hip_atomic_store(&S.hdr_host->err, TICK_ERR_LAYOUT, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                        S.hdr_host->clk[CLK_P1_MAX] = __builtin_amdgcn_s_memrealtime();
-                        if (phases & TICK_PROF) {
-                            S.hdr_host->clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
-                            st_sc1(&S.bar->neg_entry_max, 0ull);
-                        }
-                        TSTAMP(7);
-                    }
-                }
-            }
+            for (int i = 0; i < AG_DIRTY; i++) acc_v = t == i ? f[i] : acc_v;
 #pragma unroll
             for (int q = 0; q < SPEC_GROUPS; q++) apply_uses(S, G[q], usec[q] & ~used_bits(S, G[q], usec[q], u[q]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             // arrive (after this block's Uses and record): the dirty blocks count arrivals
             if (t == 0) __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // lane t owns field t: one returning add of (one arrival | this block's
+            // value); the block whose add completes the count holds the tick's total.
+            // The adds queue behind each other (~2 us for 256 blocks): their results are
+            // looked at only after this block's slice of the stream.
+            unsigned long long acc_old = 0;
+            const uint64_t c_arrive = __builtin_amdgcn_s_memrealtime();
+            if (t < AG_DIRTY) acc_old = atomicAdd(&S.bar->acc[t][0], (1ull << ACC_SHIFT) | acc_v);
             TSTAMP(3);
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
                 hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+            }
+            if (t < AG_DIRTY && (acc_old >> ACC_SHIFT) == S.n_chain - 1u) {
+                const uint64_t total = (acc_old & ACC_MASK) + acc_v;
+                st_sc1(&S.bar->acc[t][0], 0ull);  // the next tick starts from zero
+                st_host(&S.hdr_host->tot[t], total);
+                if (t == AG_HB) {
+                    if (total != n_hb)  // the heartbeat stream was laid out for the host's count
+                        st_host(&S.hdr_host->err, TICK_ERR_LAYOUT);
+                    st_host(&S.hdr_host->clk[CLK_P1_MAX], c_arrive);  // the last arrival
+                    if (phases & TICK_PROF) {
+                        st_host(&S.hdr_host->clk[CLK_ENTRY_MIN], ~ld_sc1(&S.bar->neg_entry_max));
+                        st_sc1(&S.bar->neg_entry_max, 0ull);
+                    }
+                    TSTAMP(7);
+                }
             }
             if (!dirty) {
                 TSTAMP(6);
@@ -1778,7 +1786,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 // lists that did not fit inline: the host runs the second allgather,
                 // applies them and launches BACK again (TICK_XLISTS)
                 if (b == 0 && t == 0) {
-                    S.hdr_host->xovf = 1;
+                    st_host(&S.hdr_host->xovf, 1u);
                     // a tick already queued behind this one must not run before the
                     // host finishes this one (kwok_tick_submit): its launches skip
                     __hip_atomic_store(&S.bar->skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
