@@ -531,8 +531,8 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->trace_ticks) {
         static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "-", "pool-done",
-                                                 "exit", "header-done", "w:gpre", "w:pod-loads", "w:pods-classd",
-                                                 "w:block-sum", "w:masks", "w:used-words", "nodes-emitted", "back-start"};
+                                                 "exit", "header-done", "node-flags", "w:pod-loads", "block-sum",
+                                                 "drained", "hb-handles", "share-done", "nodes-emitted", "back-start"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
                         "start (min / median / max block)\n",
                 e->S.n_chain, e->n_stream, (unsigned long long)e->trace_ticks);

@@ -1192,19 +1192,37 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
 // LDS template with 16-byte stores (node_controller.go:145-157)
 // ---------------------------------------------------------------------------
 constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
-// 16-byte units [lo, hi) of the heartbeat region
-__device__ __forceinline__ void hb_fill_units(const DevState& S, const uint4* tmpl, uint64_t lo, uint64_t hi) {
+// The stream is written in groups of 4 slots (4 x 67 = 268 units of 16 B): lane l
+// of a wave writes units 64k + l (k = 0..4) of a group, which are always the same
+// template units, so a wave keeps its 5 template units in registers and the loop
+// is 5 plain 16-byte stores per group (no LDS read per store).
+constexpr uint32_t HB_GROUP_SLOTS = 4, HB_GROUP_UNITS = HB_GROUP_SLOTS * HB_CHUNKS;  // 268
+static_assert(HB_GROUP_UNITS > 256 && HB_GROUP_UNITS <= 320, "5 stores of a wave per group");
+// groups [g0, g1) of the heartbeat region (units past n_hb slots are not written)
+__device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint64_t g0,
+                                               uint64_t g1) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t l = lane_id(), w = wave_id();
+    u32x4 r[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = tmpl[(64u * k + l) % HB_CHUNKS];
+        r[k] = u32x4{v.x, v.y, v.z, v.w};
+    }
+    const uint64_t units = n_hb * HB_CHUNKS;
     u32x4* dst = reinterpret_cast<u32x4*>(S.arena);  // heartbeat region starts at arena offset 0
-    uint64_t i = lo + threadIdx.x;
-    uint32_t m = (uint32_t)(i % HB_CHUNKS);
-    constexpr uint32_t dm = BLOCK % HB_CHUNKS;
-    for (; i < hi; i += BLOCK) {
-        const uint4 v = tmpl[m];
-        u32x4 w = {v.x, v.y, v.z, v.w};
-        dst[i] = w;  // plain stores: 7.4 TB/s vs 5.8 for nt on this fill (tools/micro/fill.hip)
-        m += dm;
-        if (m >= HB_CHUNKS) m -= HB_CHUNKS;
+    for (uint64_t g = g0 + w; g < g1; g += BLOCK / 64) {
+        const uint64_t u0 = g * HB_GROUP_UNITS + l;
+        u32x4* p = dst + u0;
+        if (u0 + 256u < units) {  // a whole group (every group but possibly the last)
+#pragma unroll
+            for (int k = 0; k < 4; k++) p[64 * k] = r[k];  // plain stores: 7.5 TB/s (tools/micro/fill.hip)
+            if (l < HB_GROUP_UNITS - 256u) p[256] = r[4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if (64u * k + l < HB_GROUP_UNITS && u0 + 64u * k < units) p[64 * k] = r[k];
+        }
     }
 }
 
@@ -1213,10 +1231,10 @@ __device__ __forceinline__ void hb_fill_units(const DevState& S, const uint4* tm
 // rest once its own work is done (so the stream's tail overlaps nothing idle)
 __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, bool streamer,
                                               uint32_t idx, uint32_t cnt) {
-    const uint64_t units = n_hb * HB_CHUNKS;
-    const uint64_t cut = units * S.stream_share / 1024;
-    const uint64_t lo = streamer ? 0 : cut, n = streamer ? cut : units - cut;
-    hb_fill_units(S, tmpl, lo + n * idx / cnt, lo + n * (idx + 1) / cnt);
+    const uint64_t groups = (n_hb + HB_GROUP_SLOTS - 1) / HB_GROUP_SLOTS;
+    const uint64_t cut = groups * S.stream_share / 1024;
+    const uint64_t lo = streamer ? 0 : cut, n = streamer ? cut : groups - cut;
+    hb_fill_groups(S, tmpl, n_hb, lo + n * idx / cnt, lo + n * (idx + 1) / cnt);
 }
 
 // per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
@@ -1635,6 +1653,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
         }
         __syncthreads();  // node flags, fill marks
+        TSTAMP(8);
         if (t < 64) {     // gpre: live groups of the buckets before j; the block's largest bucket
             const uint32_t g = t < (int)nbk ? gpre[t + 1] : 0u;
             const uint32_t inc = wave_incl_scan(g);
@@ -1645,6 +1664,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         }
         __syncthreads();
         TSTAMP(1);
+        TWAIT(9);
         // ---- pods: the speculative groups, then any further rows (rare) ------------
         uint64_t pmask = 0;
         uint32_t usec[SPEC_GROUPS];  // single rank: Use candidates, checked after the accumulator adds
@@ -1681,6 +1701,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if ((uint32_t)(pmask >> 32)) atomicOr(&sh_mask[1], (uint32_t)(pmask >> 32));
         }
         block_total<AG_STRIDE>(f);  // synchronises: the masks are complete
+        TSTAMP(10);
         pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
         node_mask = sh_mask[2];
         const bool dirty = (pod_mask | node_mask) != 0;
@@ -1708,6 +1729,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             for (int q = 0; q < SPEC_GROUPS; q++) apply_uses(S, G[q], usec[q] & ~used_bits(S, G[q], usec[q], u[q]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            TSTAMP(11);
             // arrive (after this block's Uses and record): the dirty blocks count arrivals
             if (t == 0) __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // lane t owns field t: one returning add of (one arrival | this block's
@@ -1719,10 +1741,12 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if (t < AG_DIRTY) acc_old = atomicAdd(&S.bar->acc[t][0], (1ull << ACC_SHIFT) | acc_v);
             TSTAMP(3);
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
+            TSTAMP(12);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
                 hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
             }
+            TSTAMP(13);
             if (t < AG_DIRTY && (acc_old >> ACC_SHIFT) == S.n_chain - 1u) {
                 const uint64_t total = (acc_old & ACC_MASK) + acc_v;
                 st_sc1(&S.bar->acc[t][0], 0ull);  // the next tick starts from zero

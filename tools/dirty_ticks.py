@@ -22,16 +22,18 @@ now = workload.S0 + 30
 
 def tick(label):
     global now
+    e.profile_host(reset=True)
     t0 = time.perf_counter()
     r = e.tick(now, read=False)
     dt = time.perf_counter() - t0
+    hm, _ = e.profile_host(reset=True)
     now += 30
     phases, n = e.profile_read()
     e.profile_enable(True)
     c = dict(zip(abi.COUNTERS, r.counters))
     print("%-10s wall %8.3f ms  kernel %8.3f ms  pp %8d del %8d init %7d alloc %8d rel %8d" % (
         label, dt * 1e3, phases["kernel"], c["pod_patch"], c["delete"], c["node_init"], c["alloc"], c["release"]),
-        {k: round(v, 3) for k, v in phases.items() if v})
+        {k: round(v, 3) for k, v in phases.items() if v}, "host", {k: round(v, 3) for k, v in hm.items()})
 
 
 tick("initial")
@@ -48,6 +50,8 @@ for k in range(3):
         rng.random(len(sel)) < 0.5, abi.POD_HAS_FINALIZERS, 0).astype(ev["flags"].dtype)
     ev["spec_id"] = 0
     ev["creation_unix"] = workload.S0 - 60
+    t0 = time.perf_counter()
     hs, st, _ = e.ingest_pods_raw(ev, b"")
+    print("ingest of %d deleting pods: %.3f ms" % (len(ev), (time.perf_counter() - t0) * 1e3))
     tick("churn-del")
     ph = np.delete(ph, sel)

@@ -20,9 +20,35 @@ __global__ void k_fill(u32x4* dst, uint64_t n_hb, unsigned long long* clk) {
         u32x4 w = {v.x, v.y, v.z, v.w};
         if (MODE == 0) __builtin_nontemporal_store(w, &dst[i]);
         else if (MODE == 1) dst[i] = w;
-        else __hip_atomic_store(reinterpret_cast<uint64_t*>(&dst[i]), (uint64_t)v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (MODE == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(&dst[i]), "v"(w) : "memory");
+        else if (MODE == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(&dst[i]), "v"(w) : "memory");
+        else asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(&dst[i]), "v"(w) : "memory");
         m += dm;
         if (m >= 67) m -= 67;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t0; clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); }
+}
+// 4-slot groups (268 chunks): lane l writes chunks 64k+l (k = 0..4) of every group,
+// always the same template chunks -> 5 template values in registers, no LDS in the loop
+__global__ void k_fill_reg(u32x4* dst, uint64_t n_hb, unsigned long long* clk, int unroll2) {
+    __shared__ uint4 tmpl[67];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x < 67) tmpl[threadIdx.x] = make_uint4(threadIdx.x, 1, 2, 3);
+    __syncthreads();
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    u32x4 r[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = tmpl[(64 * k + l) % 67];
+        r[k] = u32x4{v.x, v.y, v.z, v.w};
+    }
+    const uint64_t ng = n_hb / 4, g0 = ng * blockIdx.x / gridDim.x, g1 = ng * (blockIdx.x + 1) / gridDim.x;
+    for (uint64_t g = g0 + w; g < g1; g += nw) {
+        u32x4* p = dst + g * 268 + l;
+#pragma unroll
+        for (int k = 0; k < 4; k++) p[64 * k] = r[k];
+        if (l < 12) p[256] = r[4];
     }
     __syncthreads();
     if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t0; clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); }
@@ -34,12 +60,18 @@ int main() {
     std::vector<unsigned long long> hc(2 * 4096);
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     const char* names[3] = {"nt", "plain", "sc1(8B)"};
-    for (int mode = 0; mode < 2; mode++)
-        for (int threads : {256, 512, 1024})
-            for (int grid : {256, 512, 1024, 2048}) {
+    const char* names2[5] = {"nt", "plain", "sc1", "sc0sc1", "nt-sc1"};
+    for (int mode = 0; mode < 5; mode++)
+        for (int threads : {256})
+            for (int grid : {256, 512}) {
                 auto launch = [&] {
-                    if (mode == 0) hipLaunchKernelGGL(k_fill<0>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk);
-                    else hipLaunchKernelGGL(k_fill<1>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk);
+                    switch (mode) {
+                        case 0: hipLaunchKernelGGL(k_fill<0>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk); break;
+                        case 1: hipLaunchKernelGGL(k_fill<1>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk); break;
+                        case 2: hipLaunchKernelGGL(k_fill<2>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk); break;
+                        case 3: hipLaunchKernelGGL(k_fill<3>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk); break;
+                        default: hipLaunchKernelGGL(k_fill<4>, dim3(grid), dim3(threads), 0, 0, dst, n_hb, clk); break;
+                    }
                 };
                 for (int w = 0; w < 5; w++) launch();
                 (void)hipDeviceSynchronize();
@@ -52,7 +84,16 @@ int main() {
                     for (int b = 0; b < grid; b++) { mn = std::min(mn, hc[2 * b]); mx = std::max(mx, hc[2 * b + 1]); }
                     span_best = std::min(span_best, (mx - mn) * 0.01);
                 }
-                printf("%-6s threads %4d grid %5d: event %.2f us  span %.2f us  -> %.2f TB/s (span)\n", names[mode], threads, grid,
+                {
+                    (void)hipEventRecord(e0);
+                    for (int r = 0; r < 20; r++) launch();
+                    (void)hipEventRecord(e1);
+                    (void)hipEventSynchronize(e1);
+                    float ms;
+                    (void)hipEventElapsedTime(&ms, e0, e1);
+                    printf("   back-to-back: %.2f us per launch\n", ms * 1e3 / 20);
+                }
+                printf("%-6s threads %4d grid %5d: event %.2f us  span %.2f us  -> %.2f TB/s (span)\n", names2[mode], threads, grid,
                        best * 1e3, span_best, n_hb * 1072 / (span_best * 1e-6) / 1e12);
             }
     return 0;
