@@ -154,6 +154,8 @@ struct SpecDesc {
     uint32_t off;             // into spec byte/kind arrays
     uint16_t len_a, len_b, len_c;
     uint16_t max_len;         // 16-aligned arena reservation
+    uint32_t ts_first;        // its timestamp slots: spec_ts[ts_first, + n_ts) (offsets into A|B|C)
+    uint16_t n_ts, pad;
 };
 
 }  // namespace kwok

@@ -103,6 +103,8 @@ struct kwok_engine {
     std::string spec_bytes_h, spec_kinds_h;
     DevBuf<SpecDesc> d_specs;
     DevBuf<uint8_t> d_spec_bytes, d_spec_kinds;
+    std::vector<uint16_t> spec_ts_h;  // timestamp slot offsets of every spec
+    DevBuf<uint16_t> d_spec_ts;
     uint32_t max_pod_len = 0;
     std::unordered_map<std::string, uint64_t> blob_ids;
     std::string blob_h;
@@ -125,7 +127,11 @@ struct kwok_engine {
         DevState* S_pin = nullptr;  // pinned staging for its upload
         DevState S_up{};            // the copy last uploaded
         hipEvent_t done = nullptr;  // recorded after the tick's launches
-        hipEvent_t pev[4] = {};     // profiling: FRONT(+BACK) launch start/stop, BACK launch start/stop
+        hipEvent_t pev[6] = {};     // profiling: FRONT(+BACK) launch start/stop, BACK launch start/stop, k_emit
+        uint4* pp_job = nullptr;    // k_tick -> k_emit job records
+        uint64_t* init_job = nullptr;
+        uint32_t* emit_n = nullptr;
+        bool emit_queued = false;   // k_emit was enqueued behind the tick's launches
         bool alloc = false;
         // the tick in the slot
         int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
@@ -150,6 +156,8 @@ struct kwok_engine {
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
     uint32_t n_stream = 0;      // k_tick heartbeat streamer blocks (the chain blocks: S.n_chain)
+    uint32_t emit_grid = 0;     // k_emit blocks
+    bool emit_hint = true;      // events were ingested since the last submit: the tick likely emits patches
     bool sync_spin = true;      // spin on a tick's completion event (KWOK_SYNC=spin, the default)
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
@@ -314,18 +322,25 @@ int flush_ops(kwok_engine* e) {
 int upload_specs(kwok_engine* e) {
     int rc;
     if ((rc = dgrow(e, e->d_specs, e->specs_h.size()))) return rc;
-    if ((rc = dgrow(e, e->d_spec_bytes, e->spec_bytes_h.size()))) return rc;
+    // the kernels read the spec bytes as 32-bit words, up to 64 bytes past the end
+    std::string bytes = e->spec_bytes_h;
+    bytes.resize(((bytes.size() + 3) & ~(size_t)3) + 64, '\0');
+    if ((rc = dgrow(e, e->d_spec_bytes, bytes.size()))) return rc;
+    if ((rc = dgrow(e, e->d_spec_ts, std::max<size_t>(e->spec_ts_h.size(), 1)))) return rc;
     if ((rc = dgrow(e, e->d_spec_kinds, e->spec_kinds_h.size()))) return rc;
     HIPCHK(e, hipMemcpyAsync(e->d_specs.p, e->specs_h.data(), e->specs_h.size() * sizeof(SpecDesc),
                              hipMemcpyHostToDevice, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->d_spec_bytes.p, e->spec_bytes_h.data(), e->spec_bytes_h.size(), hipMemcpyHostToDevice,
-                             e->st));
+    HIPCHK(e, hipMemcpyAsync(e->d_spec_bytes.p, bytes.data(), bytes.size(), hipMemcpyHostToDevice, e->st));
+    if (!e->spec_ts_h.empty())
+        HIPCHK(e, hipMemcpyAsync(e->d_spec_ts.p, e->spec_ts_h.data(), e->spec_ts_h.size() * 2, hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipMemcpyAsync(e->d_spec_kinds.p, e->spec_kinds_h.data(), e->spec_kinds_h.size(),
                              hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->S.specs = e->d_specs.p;
     e->S.spec_bytes = e->d_spec_bytes.p;
     e->S.spec_kinds = e->d_spec_kinds.p;
+    e->S.spec_ts = e->d_spec_ts.p;
+    e->S.ts_total = (uint32_t)e->spec_ts_h.size();
     e->S.n_specs = (uint32_t)e->specs_h.size();
     e->S.spec_total = (uint32_t)e->spec_bytes_h.size();
     return KWOK_OK;
@@ -355,7 +370,8 @@ int alloc_slot(kwok_engine* e, int k) {
     if ((rc = dalloc(e, &T.hb_nodes, e->NLa)) || (rc = dalloc(e, &T.init_nodes, e->NLa)) ||
         (rc = dalloc(e, &T.init_off, e->NLa)) || (rc = dalloc(e, &T.init_len, e->NLa)) ||
         (rc = dalloc(e, &T.pp_pods, e->PLa)) || (rc = dalloc(e, &T.pp_off, e->PLa)) || (rc = dalloc(e, &T.pp_len, e->PLa)) ||
-        (rc = dalloc(e, &T.del_pods, e->PLa)) || (rc = dalloc(e, &T.del_fin, e->PLa)) || (rc = dalloc(e, &T.d_S, 1)))
+        (rc = dalloc(e, &T.del_pods, e->PLa)) || (rc = dalloc(e, &T.del_fin, e->PLa)) || (rc = dalloc(e, &T.d_S, 1)) ||
+        (rc = dalloc(e, &T.pp_job, e->PLa)) || (rc = dalloc(e, &T.init_job, e->NLa)) || (rc = dalloc(e, &T.emit_n, 2)))
         return rc;
     // the header is coherent host memory written with system-scope stores, so the
     // completion event needs no system-scope release (measured ~1.7 us per tick)
@@ -372,7 +388,7 @@ int alloc_slot(kwok_engine* e, int k) {
 }
 void free_slot(kwok_engine::TickSlot& T) {
     void* ptrs[] = {T.arena, T.hb_nodes, T.init_nodes, T.init_off, T.init_len, T.pp_pods,
-                    T.pp_off, T.pp_len, T.del_pods, T.del_fin, T.d_S};
+                    T.pp_off, T.pp_len, T.del_pods, T.del_fin, T.d_S, T.pp_job, T.init_job, T.emit_n};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (T.hdr_h) (void)hipHostFree(T.hdr_h);
@@ -398,6 +414,9 @@ int bind_slot(kwok_engine* e, int k) {
     S.del_fin = T.del_fin;
     S.hdr_host = T.hdr_h;
     S.self = T.d_S;
+    S.pp_job = T.pp_job;
+    S.init_job = T.init_job;
+    S.emit_n = T.emit_n;
     if (memcmp(&T.S_up, &S, sizeof(DevState)) != 0) {  // pointers / sizes changed since the last upload
         *T.S_pin = S;  // the slot's previous upload has completed (its tick was collected)
         HIPCHK(e, hipMemcpyAsync(T.d_S, T.S_pin, sizeof(DevState), hipMemcpyHostToDevice, e->st));
@@ -530,7 +549,7 @@ const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->trace_ticks) {
-        static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "-", "pool-done",
+        static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "pod-jobs", "pool-done",
                                                  "exit", "header-done", "node-flags", "w:pod-loads", "block-sum",
                                                  "drained", "hb-handles", "share-done", "nodes-emitted", "back-start"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
@@ -551,7 +570,7 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
-                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_blob.p, e->d_ops,
+                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_spec_ts.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -634,6 +653,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
         S.n_chain = (uint32_t)(cus * std::min(occ, want));
         e->n_stream = (uint32_t)(cus * wants);
+        e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
         const char* pr = getenv("KWOK_TICK_PRIO");
         e->chain_prio = pr && pr[0] == '1';
@@ -778,8 +798,12 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     d.len_b = (uint16_t)p.b.size();
     d.len_c = (uint16_t)p.c.size();
     d.max_len = (uint16_t)p.max_len;
+    d.ts_first = (uint32_t)e->spec_ts_h.size();
+    const std::string kinds = p.ka + p.kb + p.kc;
+    for (size_t i = 0; i < kinds.size(); i++)  // slot starts (kinds 0..19 in a row)
+        if (kinds[i] == 0) e->spec_ts_h.push_back((uint16_t)i), d.n_ts++;
     e->spec_bytes_h += p.a + p.b + p.c;
-    e->spec_kinds_h += p.ka + p.kb + p.kc;
+    e->spec_kinds_h += kinds;
     e->specs_h.push_back(d);
     int rc = upload_specs(e);
     if (rc) return rc;
@@ -794,6 +818,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                       int32_t* out_handles, int32_t* out_status) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
     drain(e);  // the host mirrors reflect every submitted tick
+    e->emit_hint = true;
     e->gen++;
     int rejected = 0;
     for (size_t i = 0; i < n; i++) {
@@ -874,6 +899,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
     drain(e);  // the host mirrors reflect every submitted tick
+    e->emit_hint = true;
     e->gen++;
     int rejected = 0;
     const int32_t pbase = (int32_t)(e->b_lo * e->Cp);
@@ -1007,6 +1033,17 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
 namespace {
 enum { SLOT_FREE = 0, SLOT_QUEUED = 1, SLOT_DONE = 2 };
 
+// k_emit for slot k's tick (S bound to slot k), behind its k_tick launch(es)
+int enqueue_emit(kwok_engine* e, int k) {
+    kwok_engine::TickSlot& T = e->slots[k];
+    if (e->prof) HIPCHK(e, hipEventRecord(T.pev[4], e->st));
+    launch_emit(e->S, e->emit_grid, T.now, (uint64_t)e->start, e->st);
+    HIPCHK(e, hipGetLastError());
+    if (e->prof) HIPCHK(e, hipEventRecord(T.pev[5], e->st));
+    T.emit_queued = true;
+    return KWOK_OK;
+}
+
 // Enqueue one tick on e->st into slot k.  Single rank: ONE persistent k_tick
 // launch (no host synchronisation, no graph needed).  Multi-rank: k_tick FRONT
 // (classify, bases, exchange message) -> allgather -> k_tick BACK (fold
@@ -1062,6 +1099,9 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
                     ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
         HIPCHK(e, hipGetLastError());
     }
+    // the patch bytes, when events since the last tick make jobs likely (otherwise
+    // retire launches k_emit if the tick turns out to have jobs)
+    if (T.emit_queued && (rc = enqueue_emit(e, k))) return rc;
     HIPCHK(e, hipEventRecord(T.done, st));
     return KWOK_OK;
 }
@@ -1107,6 +1147,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed, TICK_BACK | TICK_XLISTS, T.tag,
                 T.target, st);
     HIPCHK(e, hipGetLastError());
+    if ((rc = enqueue_emit(e, k))) return rc;  // this launch built the jobs
     HIPCHK(e, hipStreamSynchronize(st));
     if (next >= 0) return enqueue_tick(e, next, true);
     return KWOK_OK;
@@ -1167,6 +1208,14 @@ void trace_tick(kwok_engine* e) {
     for (int k = 0; k < TRACE_SLOTS; k++) summarise(0, G, k, e->trace_sum[k]);
     summarise(G, N, 0, e->trace_sum[TRACE_SLOTS]);
     summarise(G, N, 6, e->trace_sum[TRACE_SLOTS + 1]);
+    if (getenv("KWOK_TICK_TRACE_RAW")) {  // the last block's 16 stamps (ad-hoc kernel probes), us after t0
+        fprintf(stderr, "[kwok trace raw]");
+        for (size_t k = 0; k < TS; k++) {
+            const uint64_t v = e->trace_h[(N - 1) * TS + k];
+            fprintf(stderr, " %.3f", k == 8 ? (double)v : v >= t0 ? (double)(v - t0) * 0.01 : -1.0);
+        }
+        fprintf(stderr, "\n");
+    }
     e->trace_ticks++;
 }
 
@@ -1212,6 +1261,14 @@ int retire(kwok_engine* e) {
     const auto t2 = clk::now();
     if (e->W == 1) derive_header(*T.hdr_h, T.arena_cap);
     const TickHdr& H = *T.hdr_h;
+    if (!H.err && (H.n_pp || H.n_init) && !T.emit_queued) {
+        // jobs nobody expected (no events since the previous tick): their bytes now
+        int rc = bind_slot(e, k);
+        if (!rc) rc = enqueue_emit(e, k);
+        if (rc) return failed(rc);
+        if (hipEventRecord(T.done, e->st) != hipSuccess || hipEventSynchronize(T.done) != hipSuccess)
+            return failed(e->fail(KWOK_EDEVICE, "k_emit"));
+    }
     if (trace_enabled(e)) trace_tick(e);
     if (H.err) {
         const uint32_t err = H.err;
@@ -1238,7 +1295,9 @@ int retire(kwok_engine* e) {
         float k0 = 0, k1 = 0;
         (void)hipEventElapsedTime(&k0, T.pev[0], T.pev[1]);
         if (e->W > 1) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
-        const double kern = (double)k0 + k1;
+        float k2 = 0;
+        if (T.emit_queued) (void)hipEventElapsedTime(&k2, T.pev[4], T.pev[5]);
+        const double kern = (double)k0 + k1 + k2;
         // the streamers' latest exit, kept on the device (they never touch the header)
         unsigned long long send = 0;
         (void)hipMemcpy(&send, &e->S.bar->stream_end_max, 8, hipMemcpyDeviceToHost);
@@ -1252,8 +1311,8 @@ int retire(kwok_engine* e) {
         e->prof_ms[KWOK_T_HEADER] += header;
         e->prof_ms[KWOK_T_EXCHANGE] += e->W > 1 ? span(CLK_HDR, CLK_BACK) : 0.0;
         e->prof_ms[KWOK_T_POOL] += pool;
-        // what follows the header in the chain (pool, emission), beyond the stream
-        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, kern - std::max(classify + header + pool, stream));
+        // what follows the header in the chain (pool, job lists) beyond the stream, and k_emit
+        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2;
         e->prof_ms[KWOK_T_KERNEL] += kern;
         e->prof_ticks++;
     }
@@ -1330,6 +1389,8 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     if (!e->nops.empty() && (rc = flush_ops(e))) return rc;  // deferred by retire
     if (k == e->cur) e->cur = -1;  // its outputs are overwritten
     T.now = (uint64_t)now_unix;
+    T.emit_queued = e->emit_hint;
+    e->emit_hint = false;
     T.pending_del.swap(e->pending_del);
     e->pending_del.clear();
     rc = enqueue_tick(e, k, false);

@@ -46,7 +46,9 @@ struct DevState {
     const uint8_t* spec_bytes;
     const uint8_t* spec_kinds;
     const uint8_t* blob;
+    const uint16_t* spec_ts;       // timestamp slot offsets of every spec (SpecDesc::ts_first)
     uint32_t n_specs, spec_total;  // spec descriptors; bytes of the concatenated spec programs
+    uint32_t ts_total;             // entries of spec_ts
     uint32_t blob_total;           // bytes of the interned node blobs
     // heartbeat template
     const uint8_t* hb_static;
@@ -69,6 +71,9 @@ struct DevState {
     int32_t* pp_pods;
     uint64_t* pp_off;
     uint32_t* pp_len;
+    uint4* pp_job;             // per pod patch: podIP (0: no status section), hostIP, creationTimestamp, spec (k_emit)
+    uint64_t* init_job;        // per node init: its blob (k_emit)
+    uint32_t* emit_n;          // [2]: pod patches, node inits whose bytes k_emit writes
     int32_t* del_pods;
     uint8_t* del_fin;
     uint32_t node_ip;
@@ -99,5 +104,8 @@ constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
+// the patch bytes of the tick's jobs (after its k_tick launch(es), on the same stream)
+void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st);
+int emit_occupancy();  // resident k_emit blocks per CU
 
 }  // namespace kwok

@@ -151,20 +151,34 @@ struct IpStr {
     uint32_t len;
 };
 __device__ __forceinline__ IpStr format_ip(uint32_t ip) {
-    IpStr r{0, 0, 0};
-    auto put = [&](uint32_t ch) {
-        if (r.len < 8) r.lo |= (uint64_t)ch << (8 * r.len);
-        else r.hi |= (uint64_t)ch << (8 * (r.len - 8));
-        r.len++;
-    };
+    // branch-free: each octet's digits packed (1-3 bytes) and its '.', appended
+    // to a 128-bit little-endian accumulator at the running length
+    uint64_t lo = 0, hi = 0;
+    uint32_t n = 0;
 #pragma unroll
     for (int k = 3; k >= 0; k--) {
-        uint32_t o = (ip >> (8 * k)) & 255u;
-        if (o >= 100u) put('0' + o / 100u);
-        if (o >= 10u) put('0' + (o / 10u) % 10u);
-        put('0' + o % 10u);
-        if (k) put('.');
+        const uint32_t o = (ip >> (8 * k)) & 255u;
+        const uint32_t d2 = o / 100u, d1 = (o / 10u) % 10u, d0 = o % 10u;
+        const uint32_t w = o >= 100u ? 3u : (o >= 10u ? 2u : 1u);
+        uint32_t v = o >= 100u ? ('0' + d2) | ('0' + d1) << 8 | ('0' + d0) << 16
+                                : (o >= 10u ? ('0' + d1) | ('0' + d0) << 8 : ('0' + d0));
+        uint32_t m = w;
+        if (k) {
+            v |= (uint32_t)'.' << (8 * w);
+            m++;
+        }
+        // append the m (<= 4) bytes of v at byte n (< 16)
+        const uint64_t x = v;
+        const uint32_t sh = 8u * (n & 7u);
+        const uint64_t part_lo = x << sh, spill = sh ? x >> (64u - sh) : 0ull;
+        lo |= n < 8u ? part_lo : 0ull;
+        hi |= n < 8u ? spill : part_lo;
+        n += m;
     }
+    IpStr r;
+    r.lo = lo;
+    r.hi = hi;
+    r.len = n;
     return r;
 }
 __device__ __forceinline__ uint32_t ip_byte(const IpStr& s, uint32_t i) {
@@ -244,41 +258,37 @@ __device__ __forceinline__ uint32_t init_patch_len(uint64_t blob) {
 
 
 // ---------------------------------------------------------------------------
-// patch writers (one wave per patch)
+// patch writers (one wave per patch; kernel k_emit)
 // ---------------------------------------------------------------------------
-// per-patch data gathered during compaction (LDS job lists), so a wave writing
-// a patch starts from registers / LDS only
+// a pod patch job (k_tick writes it as a uint4 into S.pp_job; k_emit writes the bytes)
 struct PodJob {
-    uint32_t off;     // byte offset within the chunk's pod region
     uint32_t pod_ip;  // rendered podIP (0 = no status section)
     uint32_t host_ip;
     uint32_t ctime;   // creationTimestamp (unix seconds)
     uint32_t spec;    // pod spec id
 };
-struct InitJob {
-    uint32_t off;
-    uint32_t pad;
-    uint64_t blob;    // node_blob word: off | pre_len << 32 | post_len << 48
-};
 
 // the spec programs and node blobs of the engine, staged in LDS once per
 // emitting block when they fit (the common case: a handful of specs / blobs);
 // otherwise the writers read them from global memory
-constexpr int SPEC_LDS_DESCS = 64, SPEC_LDS_PROG = 4096, BLOB_LDS = 4096;
+constexpr int SPEC_LDS_DESCS = 64, SPEC_LDS_PROG = 4096, SPEC_LDS_TS = 256, BLOB_LDS = 4096;
 struct EmitCache {
     uint32_t n_desc;                       // 0: not staged
     uint32_t blob_ok;
     SpecDesc desc[SPEC_LDS_DESCS];
-    uint16_t prog[SPEC_LDS_PROG];          // byte | kind << 8
+    uint32_t prog32[SPEC_LDS_PROG / 4 + 16];  // the spec bytes (timestamp slots zero), readable 64 bytes past the end
+    uint16_t ts[SPEC_LDS_TS];                // timestamp slot offsets of the specs (spec-relative)
     uint8_t blob[BLOB_LDS];
 };
 __device__ __forceinline__ void stage_emit_cache(const DevState& S, EmitCache* c, bool pods, bool nodes) {
-    const bool sp = pods && S.n_specs <= (uint32_t)SPEC_LDS_DESCS && S.spec_total <= (uint32_t)SPEC_LDS_PROG;
+    const bool sp = pods && S.n_specs <= (uint32_t)SPEC_LDS_DESCS && S.spec_total <= (uint32_t)SPEC_LDS_PROG &&
+                    S.ts_total <= (uint32_t)SPEC_LDS_TS;
     const bool bl = nodes && S.blob_total <= (uint32_t)BLOB_LDS;
     if (sp) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.spec_bytes);  // padded by the host
         for (uint32_t i = threadIdx.x; i < S.n_specs; i += BLOCK) c->desc[i] = S.specs[i];
-        for (uint32_t i = threadIdx.x; i < S.spec_total; i += BLOCK)
-            c->prog[i] = (uint16_t)(S.spec_bytes[i] | (uint32_t)S.spec_kinds[i] << 8);
+        for (uint32_t i = threadIdx.x; i < (S.spec_total + 3) / 4 + 16; i += BLOCK) c->prog32[i] = w[i];
+        for (uint32_t i = threadIdx.x; i < S.ts_total; i += BLOCK) c->ts[i] = S.spec_ts[i];
     }
     if (bl)
         for (uint32_t i = threadIdx.x; i < S.blob_total; i += BLOCK) c->blob[i] = S.blob[i];
@@ -289,43 +299,75 @@ __device__ __forceinline__ void stage_emit_cache(const DevState& S, EmitCache* c
     __syncthreads();
 }
 
-// Patches are assembled in a per-wave LDS buffer with lane-strided byte copies
-// (no per-byte control flow: every lane runs the same instructions), then
-// copied out 16 bytes per lane.  Longer patches than the buffer (specs with many
-// containers) take the direct per-byte path.
+// Patches are assembled in a per-wave LDS buffer, then copied out 16 bytes per
+// lane.  Longer patches than the buffer (specs with many containers) take the
+// direct per-byte path.
 constexpr uint32_t PATCH_BUF = 2048;
 
-// byte o of a spec's A|B|C template (timestamp slots from ts)
-__device__ __forceinline__ uint32_t tmpl_byte(const DevState& S, const EmitCache* c, bool cached, uint32_t off, const Ts& ts) {
-    const uint32_t v = cached ? c->prog[off] : (S.spec_bytes[off] | (uint32_t)S.spec_kinds[off] << 8);
-    const uint32_t kd = v >> 8;
-    return kd == 0xFF ? (v & 0xFF) : ts_byte(ts, kd);
+// bytes [o, o + 4) / byte o of the spec programs (words w: LDS copy or the padded global array;
+// pass 1 below reads up to 60 bytes past a spec's end for the words the IP pieces replace)
+__device__ __forceinline__ uint32_t tmpl_word(const uint32_t* w, uint32_t o) {
+    const uint32_t i = o >> 2;
+    return __builtin_amdgcn_alignbyte(w[i + 1], w[i], o & 3u);
+}
+__device__ __forceinline__ uint32_t tmpl_byte8(const uint32_t* w, uint32_t o) { return (w[o >> 2] >> (8u * (o & 3u))) & 0xFFu; }
+// byte o of a spec's A|B|C template with its timestamp slots filled (global arrays)
+__device__ __forceinline__ uint32_t tmpl_byte(const DevState& S, uint32_t off, const Ts& ts) {
+    const uint32_t kd = S.spec_kinds[off];
+    return kd == 0xFF ? S.spec_bytes[off] : ts_byte(ts, kd);
 }
 // byte i of `"<key>":"<ip>",` (key: 10 bytes for hostIP, 9 for podIP)
 __device__ __forceinline__ uint32_t ipseg_byte(Lit16 key, uint32_t klen, const IpStr& ip, uint32_t i) {
     return i < klen ? lit_byte(key, i) : i < klen + ip.len ? ip_byte(ip, i - klen) : (i == klen + ip.len ? '"' : ',');
 }
 
-// one wave writes one pod patch: A [+ "hostIP":"H",] B [+ "podIP":"P",] C
+// One wave writes one pod patch: A [+ "hostIP":"H",] B [+ "podIP":"P",] C
+// (pod_controller.go:404-439 over pod.status.tpl).  The job's fields are
+// wave-uniform (scalar formatting of the timestamp and the two IPs).  Pass 1
+// writes the template 4 bytes per lane, each word shifted to its segment's
+// output position (two aligned reads + alignbyte); pass 2 rewrites, byte by
+// byte, the hostIP / podIP pieces with the words they straddle, then the
+// timestamp slots.
+template <bool cached>  // the spec programs staged in LDS (EmitCache) or read from global memory
 __device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob& j, const EmitCache* c, uint8_t* buf,
                                                 uint8_t* out) {
-    const bool cached = c->n_desc != 0;
-    const SpecDesc sd = cached ? c->desc[j.spec] : S.specs[j.spec];
-    const Ts ts = format_ts(j.ctime);
-    const bool st = j.host_ip != 0;
-    const IpStr H = format_ip(j.host_ip), P = format_ip(j.pod_ip);
+    const uint32_t spec = __builtin_amdgcn_readfirstlane(j.spec);
+    const SpecDesc sd = cached ? c->desc[spec] : S.specs[spec];
+    const Ts ts = format_ts(__builtin_amdgcn_readfirstlane(j.ctime));
+    const uint32_t hip = __builtin_amdgcn_readfirstlane(j.host_ip), pip = __builtin_amdgcn_readfirstlane(j.pod_ip);
+    const bool st = hip != 0;
+    const IpStr H = format_ip(hip), P = format_ip(pip);
     const uint32_t la = sd.len_a, lb = sd.len_b, lc = sd.len_c;
     const uint32_t lh = st ? 10u + H.len + 2u : 0u, lp = st ? 9u + P.len + 2u : 0u;
-    const uint32_t len = la + lh + lb + lp + lc;
+    const uint32_t eA = la + lh, eB = eA + lb, eP = eB + lp;  // output starts of B, the podIP piece, C
+    const uint32_t len = eP + lc;
     constexpr Lit16 kh = lit16("\"hostIP\":\""), kp = lit16("\"podIP\":\"");
     const uint32_t l = lane_id();
     if (len <= PATCH_BUF) {
-        for (uint32_t i = l; i < la; i += 64) buf[i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + i, ts);
-        for (uint32_t i = l; i < lb; i += 64) buf[la + lh + i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + la + i, ts);
-        for (uint32_t i = l; i < lc; i += 64)
-            buf[la + lh + lb + lp + i] = (uint8_t)tmpl_byte(S, c, cached, sd.off + la + lb + i, ts);
-        if (l < lh) buf[la + l] = (uint8_t)ipseg_byte(kh, 10, H, l);
-        if (l < lp) buf[la + lh + lb + l] = (uint8_t)ipseg_byte(kp, 9, P, l);
+        const uint32_t* W = cached ? c->prog32 : reinterpret_cast<const uint32_t*>(S.spec_bytes);
+        const uint32_t base = sd.off;
+        for (uint32_t p = 4u * l; p < len; p += 256u) {
+            const uint32_t sh = p < eA ? 0u : (p < eP ? lh : lh + lp);
+            *reinterpret_cast<uint32_t*>(buf + p) = tmpl_word(W, base + p - sh);
+        }
+        if (st) {  // the IP pieces and the B / C bytes of the words they end in
+            const uint32_t n1 = min(len, (eA + 3u) & ~3u) - la, n2 = min(len, (eP + 3u) & ~3u) - eB;
+            if (l < n1 + n2) {
+                const uint32_t p = l < n1 ? la + l : eB + (l - n1);
+                uint32_t b;
+                if (p < eA) b = ipseg_byte(kh, 10, H, p - la);
+                else if (p < eB) b = tmpl_byte8(W, base + p - lh);
+                else if (p < eP) b = ipseg_byte(kp, 9, P, p - eB);
+                else b = tmpl_byte8(W, base + p - lh - lp);
+                buf[p] = (uint8_t)b;
+            }
+        }
+        const uint32_t nts = sd.n_ts * (uint32_t)TS_LEN;  // timestamp slots (never across a segment end)
+        for (uint32_t i = l; i < nts; i += 64u) {
+            const uint32_t k = i / (uint32_t)TS_LEN, bi = i - k * (uint32_t)TS_LEN;
+            const uint32_t t = (cached ? c->ts[sd.ts_first + k] : S.spec_ts[sd.ts_first + k]) + bi;
+            buf[t < la ? t : (t < la + lb ? t + lh : t + lh + lp)] = (uint8_t)ts_byte(ts, bi);
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes before its reads
         for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u)
             *reinterpret_cast<uint4*>(out + q0) = *reinterpret_cast<const uint4*>(buf + q0);
@@ -337,11 +379,11 @@ __device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob&
         for (uint32_t k = 0; k < 16; k++) {
             uint32_t p = q0 + k, b = 0;
             if (p < len) {
-                if (p < la) b = tmpl_byte(S, c, cached, sd.off + p, ts);
+                if (p < la) b = tmpl_byte(S, sd.off + p, ts);
                 else if ((p -= la) < lh) b = ipseg_byte(kh, 10, H, p);
-                else if ((p -= lh) < lb) b = tmpl_byte(S, c, cached, sd.off + la + p, ts);
+                else if ((p -= lh) < lb) b = tmpl_byte(S, sd.off + la + p, ts);
                 else if ((p -= lb) < lp) b = ipseg_byte(kp, 9, P, p);
-                else b = tmpl_byte(S, c, cached, sd.off + la + lb + (p - lp), ts);
+                else b = tmpl_byte(S, sd.off + la + lb + (p - lp), ts);
             }
             w[k >> 2] |= b << (8 * (k & 3));
         }
@@ -350,11 +392,12 @@ __device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob&
 }
 
 // one wave writes one node init patch: {"status":{ pre ,"conditions": CONDS , post }}
+template <bool cached>  // the node blobs staged in LDS (EmitCache) or read from global memory
 __device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl,
                                                  const EmitCache* c, uint8_t* buf, uint8_t* out) {
     const uint32_t boff = (uint32_t)blob, pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
     const uint32_t len = init_patch_len(blob);
-    const uint8_t* bb = (c->blob_ok ? c->blob : S.blob) + boff;
+    const uint8_t* bb = (cached ? c->blob : S.blob) + boff;
     const uint8_t* conds = hb_tmpl + HB_PREFIX;
     constexpr Lit16 p0 = lit16("{\"status\":{"), p1 = lit16(",\"conditions\":");
     const uint32_t l = lane_id();
@@ -1045,8 +1088,7 @@ struct Bases {
 
 // node chunk at block-local node offset i0 (node slots nbase + [i0, i0 + 1024))
 __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbase, uint32_t i0, uint32_t nn, Bases& run,
-                                const Layout& L, const uint8_t* hb_tmpl, InitJob* ij, const EmitCache* ec,
-                                uint8_t* pbuf) {
+                                const Layout& L) {
     const uint32_t i = i0 + threadIdx.x * NODE_PER_THREAD;
     const uint32_t first = nbase + i;
     uint32_t packed = 0;
@@ -1079,8 +1121,7 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
             S.init_nodes[ord] = S.node_handle_base + (int32_t)(first + k);
             S.init_off[ord] = chunk_bytes + v[1];
             S.init_len[ord] = ilen[k];
-            ij[ji].off = v[1];
-            ij[ji].blob = blob[k];
+            S.init_job[ord] = blob[k];  // the patch bytes: k_emit
             ji++;
             v[1] += (ilen[k] + 15u) & ~15u;
             s |= NS_CONFORMS;  // the apiserver applied the init patch
@@ -1090,17 +1131,13 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
     }
     if (i < nn && newpacked != packed) *reinterpret_cast<uint32_t*>(S.node_state + first) = newpacked;
     __syncthreads();
-    for (uint32_t q = wave_id(); q < tot[0]; q += BLOCK / 64)
-        write_init_patch(S, ij[q].blob, hb_tmpl, ec, pbuf + wave_id() * PATCH_BUF, S.arena + chunk_bytes + ij[q].off);
-    __syncthreads();
     run.v[AG_INIT] += tot[0];
     run.v[AG_INIT_BYTES] += tot[1];
 }
 
 // pod chunk c: the block's live groups [c*256, c*256 + 256)
 __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
-                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, PodJob* jobs,
-                               const EmitCache* ec, uint8_t* pbuf) {
+                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L) {
     PodGrp g;
     load_group(S, gpre, bk0, nbk, ng, c * BLOCK + threadIdx.x, g);
     uint16_t sp[POD_PER_THREAD];
@@ -1156,7 +1193,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
                 S.pp_pods[ord] = handle;
                 S.pp_off[ord] = chunk_bytes + v[2];
                 S.pp_len[ord] = len;
-                jobs[jl] = PodJob{v[2], stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]};
+                S.pp_job[ord] = make_uint4(stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]);  // the bytes: k_emit
                 jl++;
                 v[2] += sd.max_len;
                 // the apiserver applied the patch
@@ -1176,10 +1213,6 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
         o.w = nst[6] | (uint32_t)nst[7] << 16;
         *reinterpret_cast<uint4*>(S.pod_state + g.slot) = o;
     }
-    __syncthreads();
-    uint8_t* out = S.arena + chunk_bytes;
-    for (uint32_t q = wave_id(); q < tot[1]; q += BLOCK / 64)
-        write_pod_patch(S, jobs[q], ec, pbuf + wave_id() * PATCH_BUF, out + jobs[q].off);
     __syncthreads();
     run.v[AG_DEL] += tot[0];
     run.v[AG_PP] += tot[1];
@@ -1380,12 +1413,7 @@ __device__ __forceinline__ void write_hb_handles(const DevState& S, const uint32
 
 // pointers into k_tick's LDS for the out-of-line BACK phases
 struct TickLds {
-    EmitCache* ec;
-    uint8_t* pbuf;  // [BLOCK / 64][PATCH_BUF] per-wave patch buffers
     uint32_t* recs;
-    PodJob* pod;
-    InitJob* node;
-    uint8_t* hb_tmpl;
     uint32_t* nflags32;
     uint32_t* gpre;
     Sums* sums;
@@ -1483,7 +1511,6 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
                 l.nflags32[i / 4] = *reinterpret_cast<const uint32_t*>(S.node_tick + nbase + i);
         __syncthreads();
     }
-    if (node_mask && my_init) build_hb_template(S, l.hb_tmpl, now_unix, start_unix);
     if (t == 0) {
         const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
         l.L->init_base = patch_base;
@@ -1496,17 +1523,15 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     Bases run;
     for (int f = 0; f < AG_NSCAN; f++) run.v[f] = l.sums->pre[f];
     TSTAMP(15);
-    stage_emit_cache(S, l.ec, pod_mask != 0, node_mask != 0 && my_init != 0);
     for (uint32_t m = node_mask; m; m &= m - 1) {
         const uint32_t k = (uint32_t)__builtin_ctz(m);
-        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L, l.hb_tmpl, l.node, l.ec, l.pbuf);
+        emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L);
     }
     TSTAMP(14);
     const uint32_t ng = l.gpre[nbk];
     for (uint64_t m = pod_mask; m; m &= m - 1) {
         const uint32_t c = (uint32_t)__builtin_ctzll(m);
-        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.pod, l.ec,
-                       l.pbuf);
+        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L);
     }
     TSTAMP(6);
 #undef TSTAMP
@@ -1535,19 +1560,13 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                                                    uint32_t n_hb, int phases, uint32_t tag, uint64_t arrive_target) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
-    __shared__ union {
-        PodJob pod[POD_CHUNK];
-        InitJob node[NODE_CHUNK];
-        uint32_t recs[MAX_CHAIN * REC_PITCH];  // reduce_records (before emission)
-    } jobs;
+    __shared__ uint32_t recs[MAX_CHAIN * REC_PITCH];  // reduce_records
     __shared__ uint4 hb_tmpl4[HB_CHUNKS];
     __shared__ uint32_t nflags32[NODE_LDS / 4];
     __shared__ uint32_t gpre[MAX_BPB + 1];
     __shared__ uint32_t sh_mask[4];  // pod chunk mask lo / hi, node chunk mask, most groups in a bucket
     __shared__ Sums sums;
     __shared__ Layout sh_L;
-    __shared__ EmitCache emit_cache;
-    __shared__ uint4 patch_buf4[BLOCK / 64 * PATCH_BUF / 16];
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
     if (S.world > 1 && !(phases & TICK_XLISTS) &&
@@ -1751,6 +1770,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 const uint64_t total = (acc_old & ACC_MASK) + acc_v;
                 st_sc1(&S.bar->acc[t][0], 0ull);  // the next tick starts from zero
                 st_host(&S.hdr_host->tot[t], total);
+                if (t == AG_PP) S.emit_n[0] = (uint32_t)total;  // for k_emit, which runs after this launch
+                if (t == AG_INIT) S.emit_n[1] = (uint32_t)total;
                 if (t == AG_HB) {
                     if (total != n_hb)  // the heartbeat stream was laid out for the host's count
                         st_host(&S.hdr_host->err, TICK_ERR_LAYOUT);
@@ -1767,7 +1788,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 return;
             }
             wait_arrivals(S, arrive_target);
-            reduce_records(S, b, tag, jobs.recs, &sums);
+            reduce_records(S, b, tag, recs, &sums);
             have_sums = true;
         } else {
             // ---- multi rank: records; the last arriver writes the exchange message -----
@@ -1780,8 +1801,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             TSTAMP(3);
             if ((old + 1) % S.n_chain == 0) {
                 const uint64_t c = __builtin_amdgcn_s_memrealtime();
-                reduce_records(S, b, 0, jobs.recs, &sums);
+                reduce_records(S, b, 0, recs, &sums);
                 write_front_header(S, sums, n_hb, pool_index, c, (phases & TICK_PROF) != 0);
+                if (t < 2) S.emit_n[t] = 0u;  // set by BACK once it builds the jobs
                 TSTAMP(7);
             }
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
@@ -1830,6 +1852,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             }
             if (xA || xrel) pool_barrier(S, S.n_chain);  // the pool phase reads every rank's bits
         }
+        if (b == 0 && t < 2) S.emit_n[t] = t ? H->n_init : H->n_pp;  // this launch builds k_emit's jobs
         if (b == 0 && t < 16) {  // fleet counters
             uint64_t c = 0;
             for (int r = 0; r < S.world; r++) c += X[r].counters[t];
@@ -1856,7 +1879,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         node_mask = sh_mask[2];
         my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
     }
-    tick_back(S.self, TickLds{&emit_cache, reinterpret_cast<uint8_t*>(patch_buf4), jobs.recs, jobs.pod, jobs.node, hb_tmpl, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
+    tick_back(S.self, TickLds{recs, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
               pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase);
 #undef TSTAMP
 #undef TWAIT
@@ -1938,6 +1961,54 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
         hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases, tag,
                               arrive_target);
     else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases, tag, arrive_target);
+}
+
+// ---------------------------------------------------------------------------
+// k_emit: the patch bytes of a tick's node inits and pod patches, from the job
+// records k_tick wrote (S.init_job / S.pp_job at the ordinals of init_off /
+// pp_off).  A kernel of its own because patch assembly is latency-bound per
+// wave: k_tick runs one chain wave per SIMD, this grid runs up to 8.  Launched
+// after the tick's k_tick on the same stream (only for ticks with jobs).
+// ---------------------------------------------------------------------------
+constexpr int EMIT_BLOCK = 256;
+static_assert(EMIT_BLOCK == BLOCK, "stage_emit_cache / build_hb_template stride by BLOCK");
+__global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
+    __shared__ EmitCache ec;
+    __shared__ uint4 pbuf4[EMIT_BLOCK / 64 * PATCH_BUF / 16];
+    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
+    if (S.world > 1 && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        return;  // the tick's launches were skipped (queued behind one the host has not finished)
+    const uint32_t n_pp = S.emit_n[0], n_init = S.emit_n[1];
+    if (n_pp == 0 && n_init == 0) return;
+    stage_emit_cache(S, &ec, n_pp != 0, n_init != 0);
+    uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
+    if (n_init) build_hb_template(S, hb_tmpl, now_unix, start_unix);
+    uint8_t* buf = reinterpret_cast<uint8_t*>(pbuf4) + wave_id() * PATCH_BUF;
+    const uint32_t w0 = blockIdx.x * (EMIT_BLOCK / 64) + wave_id(), nw = gridDim.x * (EMIT_BLOCK / 64);
+    if (ec.blob_ok) {
+        for (uint32_t q = w0; q < n_init; q += nw) write_init_patch<true>(S, S.init_job[q], hb_tmpl, &ec, buf, S.arena + S.init_off[q]);
+    } else {
+        for (uint32_t q = w0; q < n_init; q += nw) write_init_patch<false>(S, S.init_job[q], hb_tmpl, &ec, buf, S.arena + S.init_off[q]);
+    }
+    auto job = [&](uint32_t q) {
+        const uint4 r = S.pp_job[q];
+        return PodJob{r.x, r.y, r.z, r.w};
+    };
+    if (ec.n_desc) {
+        for (uint32_t q = w0; q < n_pp; q += nw) write_pod_patch<true>(S, job(q), &ec, buf, S.arena + S.pp_off[q]);
+    } else {
+        for (uint32_t q = w0; q < n_pp; q += nw) write_pod_patch<false>(S, job(q), &ec, buf, S.arena + S.pp_off[q]);
+    }
+}
+
+void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st) {
+    hipLaunchKernelGGL(k_emit, dim3(grid), dim3(EMIT_BLOCK), 0, st, S, now, start);
+}
+
+int emit_occupancy() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_emit, EMIT_BLOCK, 0) != hipSuccess) return 0;
+    return n;
 }
 
 int tick_occupancy() {

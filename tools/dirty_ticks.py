@@ -37,6 +37,9 @@ def tick(label):
 
 
 tick("initial")
+if len(sys.argv) > 3 and sys.argv[3] == "initial":
+    e.close()
+    sys.exit(0)
 tick("steady")
 rng = np.random.default_rng(1)
 for k in range(3):
