@@ -52,7 +52,7 @@ NODES_PER_RANK = 100_000
 HB_BYTES = 1059
 NODE_BYTES = 1068 + 9
 POD_BYTES = 10
-PMC_FILE = "r1_pmc_tick.json"
+PMC_FILE = "r1e_pmc_tick.json"
 
 
 def parse():
