@@ -300,6 +300,55 @@ int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], ui
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);
 int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world_size);
 
+/* ---- watch-event ingest codec (host only, no device calls) ----
+ * Decodes one Kubernetes Node / Pod JSON document (as a watch event or list
+ * item carries it) into the record kwok_ingest_nodes / kwok_ingest_pods take,
+ * evaluating the controller's selectors and the pod template's no-op test on
+ * the host:
+ *   kwok_codec_create   the selector half of controllers.NewController
+ *                       controller.go:80-101, labelsParse utils.go:205-210
+ *   kwok_decode_node    WatchNodes / ListNodes per-object work before Put/lock
+ *                       (needHeartbeat, needLockNode) node_controller.go:206-223,256-270
+ *   kwok_decode_pod     WatchPods / ListPods per-object work (needLockPod's selectors,
+ *                       deletionTimestamp, finalizers) pod_controller.go:252-269,301-343,
+ *                       plus computePatchData's SMP no-op test   pod_controller.go:404-439
+ * kwok_str refs point into the caller's arena (the document); node status
+ * blobs are canonicalised in place, so the arena is written.  The record's
+ * op is UPSERT and handle / spec_id / node_handle are -1: the caller sets op
+ * for watch.Deleted, and registers the pod spec (kwok_register_pod_spec) from
+ * the decoded containers / init containers / readiness gates. */
+typedef struct kwok_codec_config {
+    int32_t manage_all_nodes;                          /* Config.ManageAllNodes */
+    const char* manage_nodes_with_annotation_selector; /* Config.ManageNodesWithAnnotationSelector */
+    const char* manage_nodes_with_label_selector;      /* ...WithLabelSelector: applied as the list/watch filter */
+    const char* disregard_status_with_annotation_selector;
+    const char* disregard_status_with_label_selector;
+} kwok_codec_config;
+
+#define KWOK_DOC_MAX_CONTAINERS 32u
+#define KWOK_DOC_MAX_GATES 16u
+
+typedef struct kwok_pod_doc {
+    kwok_pod_event ev;
+    kwok_str name;        /* metadata.name */
+    kwok_str namespace_;  /* metadata.namespace */
+    uint32_t n_containers, n_init_containers, n_readiness_gates, reserved0;
+    kwok_container containers[KWOK_DOC_MAX_CONTAINERS];
+    kwok_container init_containers[KWOK_DOC_MAX_CONTAINERS];
+    kwok_str readiness_gates[KWOK_DOC_MAX_GATES];
+} kwok_pod_doc;
+
+typedef struct kwok_codec kwok_codec;
+int kwok_codec_create(const kwok_codec_config* cfg, kwok_codec** out);
+void kwok_codec_destroy(kwok_codec* c);
+const char* kwok_codec_last_error(void); /* this thread's last codec error */
+/* labels.Parse(selector).Matches(json_map) (json_map: a JSON object of strings or null) */
+int kwok_selector_matches(const char* selector, const char* json_map, size_t len, int32_t* out);
+int kwok_decode_node(const kwok_codec* c, char* arena, size_t arena_len, size_t doc_off, size_t doc_len,
+                     kwok_node_event* ev);
+int kwok_decode_pod(const kwok_codec* c, char* arena, size_t arena_len, size_t doc_off, size_t doc_len,
+                    kwok_pod_doc* out);
+
 #ifdef __cplusplus
 }
 #endif

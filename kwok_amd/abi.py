@@ -59,6 +59,23 @@ class PodSpec(C.Structure):
                 ("readiness_gates", C.POINTER(KwokStr)), ("n_readiness_gates", C.c_uint32)]
 
 
+DOC_MAX_CONTAINERS, DOC_MAX_GATES = 32, 16
+
+
+class CodecConfig(C.Structure):
+    _fields_ = [("manage_all_nodes", C.c_int32), ("manage_nodes_with_annotation_selector", C.c_char_p),
+                ("manage_nodes_with_label_selector", C.c_char_p),
+                ("disregard_status_with_annotation_selector", C.c_char_p),
+                ("disregard_status_with_label_selector", C.c_char_p)]
+
+
+class PodDoc(C.Structure):
+    _fields_ = [("ev", PodEvent), ("name", KwokStr), ("namespace_", KwokStr), ("n_containers", C.c_uint32),
+                ("n_init_containers", C.c_uint32), ("n_readiness_gates", C.c_uint32), ("reserved0", C.c_uint32),
+                ("containers", Container * DOC_MAX_CONTAINERS), ("init_containers", Container * DOC_MAX_CONTAINERS),
+                ("readiness_gates", KwokStr * DOC_MAX_GATES)]
+
+
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 

@@ -80,6 +80,12 @@ def declare(lib, pre):
             "profile_host": (C.c_int, [VP, C.c_int, VP, VP]),
             "tick_submit": (C.c_int, [VP, C.c_int64]),
             "tick_collect": (C.c_int, [VP, P(abi.TickResult)]),
+            "codec_create": (C.c_int, [P(abi.CodecConfig), P(VP)]),
+            "codec_destroy": (None, [VP]),
+            "codec_last_error": (C.c_char_p, []),
+            "selector_matches": (C.c_int, [C.c_char_p, C.c_char_p, SZ, P(I32)]),
+            "decode_node": (C.c_int, [VP, VP, SZ, SZ, SZ, P(abi.NodeEvent)]),
+            "decode_pod": (C.c_int, [VP, VP, SZ, SZ, SZ, P(abi.PodDoc)]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name)

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import json
 import os
+import time
 
 import numpy as np
 
@@ -85,6 +86,127 @@ def pod_batch(events, specs: SpecCache):
     return recs, bytes(ar.buf)
 
 
+# ---- the same events as Kubernetes JSON objects, decoded by the host codec
+# (kwok_decode_node / kwok_decode_pod) instead of being written as records
+MANAGE = "kwok.x-k8s.io/node=fake"        # ManageNodesWithAnnotationSelector
+DISREGARD = "kwok.x-k8s.io/status=custom"  # DisregardStatusWithAnnotationSelector
+
+
+def rfc3339(t):
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
+
+
+def pod_status_like_template(ev, creation):
+    """The status pod.status.tpl renders, as the apiserver stores it."""
+    st = rfc3339(creation)
+    spec = ev["spec"]
+    conds = [{"lastProbeTime": None, "lastTransitionTime": st, "status": "True", "type": t}
+             for t in ["Initialized", "Ready", "ContainersReady"] + list(spec["gates"])]
+    cs = [{"image": i, "name": n, "ready": True, "restartCount": 0, "imageID": "", "lastState": {},
+           "state": {"running": {"startedAt": st}}} for n, i in spec["containers"]]
+    ics = [{"image": i, "name": n, "ready": True, "restartCount": 0,
+            "state": {"terminated": {"exitCode": 0, "finishedAt": st, "reason": "Completed", "startedAt": st}}}
+           for n, i in spec["init"]]
+    out = {"conditions": conds, "startTime": st, "qosClass": "BestEffort"}
+    if cs:
+        out["containerStatuses"] = cs
+    if ics:
+        out["initContainerStatuses"] = ics
+    return out
+
+
+def pod_doc(ev):
+    md = {"name": ev["key"], "namespace": "default", "creationTimestamp": rfc3339(ev["creation"]),
+          "uid": "u-" + ev["key"]}
+    if ev["disregard"]:
+        md["annotations"] = {"kwok.x-k8s.io/status": "custom", "other": "x"}
+    else:
+        md["labels"] = {"app": "fake"}
+    if ev["deleting"]:
+        md["deletionTimestamp"] = rfc3339(ev["creation"] + 5)
+    if ev["finalizers"]:
+        md["finalizers"] = ["kwok.x-k8s.io/fake"] * ev["finalizers"]
+    spec = {"nodeName": ev["node"], "containers": [{"name": n, "image": i} for n, i in ev["spec"]["containers"]]}
+    if ev["spec"]["init"]:
+        spec["initContainers"] = [{"name": n, "image": i} for n, i in ev["spec"]["init"]]
+    if ev["spec"]["gates"]:
+        spec["readinessGates"] = [{"conditionType": g} for g in ev["spec"]["gates"]]
+    status = {}
+    if ev["conforms"]:
+        status = pod_status_like_template(ev, ev["creation"])
+    elif ev["status_nonempty"]:
+        status = {"qosClass": "BestEffort"}
+    if ev["phase"]:
+        status["phase"] = ev["phase"]
+    if ev["hostIP"]:
+        status["hostIP"] = ev["hostIP"]
+    if ev["podIP"]:
+        status["podIP"] = ev["podIP"]
+        status["podIPs"] = [{"ip": ev["podIP"]}]
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec, "status": status}
+
+
+def node_doc(ev):
+    md = {"name": ev["name"], "annotations": {}}
+    if ev["managed"]:
+        md["annotations"]["kwok.x-k8s.io/node"] = "fake"
+    if not ev["lockable"]:
+        md["annotations"]["kwok.x-k8s.io/status"] = "custom"
+    status = {"daemonEndpoints": {"kubeletEndpoint": {"Port": 0}}, "nodeInfo": dict(ev["nodeInfo"])}
+    for k in ("addresses", "allocatable", "capacity"):
+        if ev[k]:
+            status[k] = ev[k]
+    if ev["phase"]:
+        status["phase"] = ev["phase"]
+    return {"apiVersion": "v1", "kind": "Node", "metadata": md, "spec": {}, "status": status}
+
+
+def json_node_batch(events, codec):
+    """node_batch, but every upsert goes through JSON and the codec."""
+    ups = [e for e in events if e["op"] != "delete"]
+    b = codec.decode_nodes([json.dumps(node_doc(e), indent=1).encode() for e in ups])
+    ar = abi.Arena()
+    ar.buf = bytearray(b.buf)
+    recs = np.zeros(len(events), abi.NODE_EVENT_DTYPE)
+    k = 0
+    for i, ev in enumerate(events):
+        if ev["op"] == "delete":
+            recs[i]["op"] = abi.OP_DELETE
+            recs[i]["name"] = ar.ref(ev["name"])
+        else:
+            recs[i] = np.frombuffer(bytes(b.nodes[k]), abi.NODE_EVENT_DTYPE)[0]
+            k += 1
+    return recs, bytes(ar.buf)
+
+
+def json_pod_batch(events, specs: SpecCache, codec):
+    ups = [e for e in events if e["op"] != "delete"]
+    b = codec.decode_pods([json.dumps(pod_doc(e)).encode() for e in ups])
+    ar = abi.Arena()
+    ar.buf = bytearray(b.buf)
+    recs = np.zeros(len(events), abi.POD_EVENT_DTYPE)
+    k = 0
+    for i, ev in enumerate(events):
+        if ev["op"] == "delete":  # watch.Deleted carries the last state: same record as pod_batch
+            one, one_ar = pod_batch([ev], specs)
+            base = len(ar.buf)
+            ar.buf += one_ar
+            for f in ("node_name", "host_ip", "pod_ip"):
+                if one[0][f]["len"]:
+                    one[0][f]["off"] += base
+            recs[i] = one[0]
+            continue
+        d = b.pods[k]
+        k += 1
+        recs[i] = np.frombuffer(bytes(d.ev), abi.POD_EVENT_DTYPE)[0]
+        recs[i]["handle"] = ev.get("handle", -1)  # the caller's object -> handle map
+        spec = {"containers": [[b.text(c.name), b.text(c.image)] for c in d.containers[:d.n_containers]],
+                "init": [[b.text(c.name), b.text(c.image)] for c in d.init_containers[:d.n_init_containers]],
+                "gates": [b.text(g) for g in d.readiness_gates[:d.n_readiness_gates]]}
+        recs[i]["spec_id"] = specs.get(spec)
+    return recs, bytes(ar.buf)
+
+
 def config_for(fx, **kw):
     c = fx["config"]
     return make_config(cidr=c["cidr"], node_ip=c["node_ip"], start_time=c["start_time"], buckets=c["buckets"],
@@ -92,18 +214,19 @@ def config_for(fx, **kw):
                        pod_slots_per_bucket=c["pod_slots_per_bucket"], **kw)
 
 
-def replay(fx, backend, check=True, on_tick=None):
-    """Replay a fixture through backend; assert equality tick by tick."""
+def replay(fx, backend, check=True, on_tick=None, codec=None):
+    """Replay a fixture through backend; assert equality tick by tick.  With a
+    codec, events travel as Kubernetes JSON objects decoded by the host codec."""
     specs = SpecCache(backend)
     for ti, t in enumerate(fx["ticks"]):
         if t["node_events"]:
-            recs, arena = node_batch(t["node_events"])
+            recs, arena = json_node_batch(t["node_events"], codec) if codec else node_batch(t["node_events"])
             hs, st = backend.ingest_nodes_raw(recs, arena)
             if check:
                 assert list(st) == [0] * len(st), (ti, list(st))
                 assert list(hs) == [e["expect_handle"] for e in t["node_events"]], ti
         if t["pod_events"]:
-            recs, arena = pod_batch(t["pod_events"], specs)
+            recs, arena = json_pod_batch(t["pod_events"], specs, codec) if codec else pod_batch(t["pod_events"], specs)
             hs, st, _rel = backend.ingest_pods_raw(recs, arena)
             if check:
                 assert list(st) == [0] * len(st), (ti, list(st))

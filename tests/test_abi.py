@@ -43,7 +43,9 @@ def test_oracle_library_exports():
             name = name.replace("engine_", "")
         if f in ("kwok_abi_version", "kwok_comm_id", "kwok_finalizer_patch", "kwok_device_outputs",
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
-                 "kwok_tick_submit", "kwok_tick_collect"):  # engine only: queued ticks (the oracle is sequential)
+                 "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
+                 "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
+                 "kwok_decode_node", "kwok_decode_pod"):  # host codec: feeds both, lives in the engine library
             continue
         assert hasattr(lib, name), name
 
@@ -64,6 +66,12 @@ STRUCTS = {
     "kwok_outputs": (abi.Outputs, ["heartbeat_nodes", "heartbeat_off", "node_init_nodes", "node_init_off",
                                    "node_init_len", "pod_patch_pods", "pod_patch_off", "pod_patch_len",
                                    "delete_pods", "delete_has_finalizers", "arena", "arena_cap"]),
+    "kwok_codec_config": (abi.CodecConfig, ["manage_all_nodes", "manage_nodes_with_annotation_selector",
+                                            "manage_nodes_with_label_selector",
+                                            "disregard_status_with_annotation_selector",
+                                            "disregard_status_with_label_selector"]),
+    "kwok_pod_doc": (abi.PodDoc, ["ev", "name", "namespace_", "n_containers", "n_init_containers",
+                                  "n_readiness_gates", "containers", "init_containers", "readiness_gates"]),
     "kwok_device_view": (abi.DeviceView, ["arena", "heartbeat_nodes", "pod_patch_pods", "pod_patch_off",
                                           "pod_patch_len", "stream"]),
 }

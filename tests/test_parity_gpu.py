@@ -20,6 +20,19 @@ def test_engine_golden_trace(name):
 
 
 @pytest.mark.parametrize("name", harness.TRACES)
+def test_engine_golden_trace_via_json(name):
+    """Events as Kubernetes JSON objects through the host codec
+    (kwok_decode_node / kwok_decode_pod) into the HIP engine: same goldens."""
+    from kwok_amd.codec import Codec
+    fx = harness.load_trace(name)
+    codec = Codec(manage_all_nodes=False, manage_nodes_with_annotation_selector=harness.MANAGE,
+                  disregard_status_with_annotation_selector=harness.DISREGARD)
+    e = Engine(harness.config_for(fx))
+    harness.replay(fx, e, codec=codec)
+    e.close()
+
+
+@pytest.mark.parametrize("name", harness.TRACES)
 def test_engine_golden_trace_queued(name):
     fx = harness.load_trace(name)
     e = Engine(harness.config_for(fx))
