@@ -348,6 +348,13 @@ int kwok_decode_node(const kwok_codec* c, char* arena, size_t arena_len, size_t 
                      kwok_node_event* ev);
 int kwok_decode_pod(const kwok_codec* c, char* arena, size_t arena_len, size_t doc_off, size_t doc_len,
                     kwok_pod_doc* out);
+/* Batches over documents at doc_off[i] / doc_len[i] of one arena, decoded by
+ * `threads` host threads (documents must not overlap).  status[i] (optional)
+ * gets each document's code; returns the number of rejected documents. */
+int kwok_decode_nodes(const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                      const uint32_t* doc_len, size_t n, int threads, kwok_node_event* ev, int32_t* status);
+int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                     const uint32_t* doc_len, size_t n, int threads, kwok_pod_doc* out, int32_t* status);
 
 #ifdef __cplusplus
 }

@@ -73,27 +73,31 @@ class Codec:
         except Exception:
             pass
 
-    def _decode(self, kind, docs, strict):
+    def _decode(self, kind, docs, strict, threads=1):
         b = Batch()
-        spans = []
+        offs, lens = [], []
         for d in docs:
             raw = d if isinstance(d, (bytes, bytearray)) else json.dumps(d).encode()
-            spans.append((len(b.buf), len(raw)))
+            offs.append(len(b.buf))
+            lens.append(len(raw))
             b.buf += raw
+        n = len(offs)
         cbuf = C.create_string_buffer(bytes(b.buf) or b"\0", max(1, len(b.buf)))
-        fn = self._lib.kwok_decode_node if kind == "node" else self._lib.kwok_decode_pod
-        for off, n in spans:
-            rec = abi.NodeEvent() if kind == "node" else abi.PodDoc()
-            rc = fn(self._h, cbuf, len(b.buf), off, n, C.byref(rec))
-            if rc and strict:
-                raise KwokError(rc, "decode_%s: %s" % (kind, self._lib.kwok_codec_last_error().decode()))
-            b.status.append(rc)
-            (b.nodes if kind == "node" else b.pods).append(rec)
+        off_a, len_a = (C.c_uint64 * max(1, n))(*offs), (C.c_uint32 * max(1, n))(*lens)
+        recs = ((abi.NodeEvent if kind == "node" else abi.PodDoc) * max(1, n))()
+        st = (C.c_int32 * max(1, n))()
+        fn = self._lib.kwok_decode_nodes if kind == "node" else self._lib.kwok_decode_pods
+        bad = fn(self._h, cbuf, len(b.buf), off_a, len_a, n, threads, recs, st)
+        if bad < 0 or (bad and strict):
+            raise KwokError(bad if bad < 0 else st[[x for x in range(n) if st[x]][0]],
+                            "decode_%ss: %s" % (kind, self._lib.kwok_codec_last_error().decode()))
+        b.status = list(st[:n])
+        (b.nodes if kind == "node" else b.pods).extend(recs[:n])
         b.buf = bytearray(cbuf.raw[:len(b.buf)])  # node blobs were canonicalised in place
         return b
 
-    def decode_nodes(self, docs, strict=True) -> Batch:
-        return self._decode("node", docs, strict)
+    def decode_nodes(self, docs, strict=True, threads=1) -> Batch:
+        return self._decode("node", docs, strict, threads)
 
-    def decode_pods(self, docs, strict=True) -> Batch:
-        return self._decode("pod", docs, strict)
+    def decode_pods(self, docs, strict=True, threads=1) -> Batch:
+        return self._decode("pod", docs, strict, threads)

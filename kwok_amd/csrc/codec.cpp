@@ -29,6 +29,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kwok_engine.h"
@@ -744,6 +745,45 @@ int kwok_decode_pod(const kwok_codec* c, char* arena, size_t arena_len, size_t d
     if (conforms && (!stt || stt->t != JV::STR || stt->s != st_time)) conforms = false;
     if (conforms) ev.flags |= KWOK_POD_CONFORMS;
     return KWOK_OK;
+}
+
+}  // extern "C"
+
+namespace {
+template <class F>
+int batch(size_t n, int threads, int32_t* status, F&& one) {
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > n) threads = (int)(n ? n : 1);
+    std::vector<int> bad(threads, 0);
+    auto run = [&](int t) {
+        for (size_t i = t; i < n; i += threads) {  // strided: similar-size documents spread evenly
+            int rc = one(i);
+            if (status) status[i] = rc;
+            if (rc) bad[t]++;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(run, t);
+    run(0);
+    for (auto& th : pool) th.join();
+    int total = 0;
+    for (int b : bad) total += b;
+    return total;
+}
+}  // namespace
+
+extern "C" {
+
+int kwok_decode_nodes(const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                      const uint32_t* doc_len, size_t n, int threads, kwok_node_event* ev, int32_t* status) {
+    if (!c || (n && (!doc_off || !doc_len || !ev))) return fail(KWOK_EINVAL, "null argument");
+    return batch(n, threads, status, [&](size_t i) { return kwok_decode_node(c, arena, arena_len, doc_off[i], doc_len[i], &ev[i]); });
+}
+
+int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                     const uint32_t* doc_len, size_t n, int threads, kwok_pod_doc* out, int32_t* status) {
+    if (!c || (n && (!doc_off || !doc_len || !out))) return fail(KWOK_EINVAL, "null argument");
+    return batch(n, threads, status, [&](size_t i) { return kwok_decode_pod(c, arena, arena_len, doc_off[i], doc_len[i], &out[i]); });
 }
 
 }  // extern "C"

@@ -86,6 +86,8 @@ def declare(lib, pre):
             "selector_matches": (C.c_int, [C.c_char_p, C.c_char_p, SZ, P(I32)]),
             "decode_node": (C.c_int, [VP, VP, SZ, SZ, SZ, P(abi.NodeEvent)]),
             "decode_pod": (C.c_int, [VP, VP, SZ, SZ, SZ, P(abi.PodDoc)]),
+            "decode_nodes": (C.c_int, [VP, VP, SZ, VP, VP, SZ, C.c_int, VP, VP]),
+            "decode_pods": (C.c_int, [VP, VP, SZ, VP, VP, SZ, C.c_int, VP, VP]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name)

@@ -269,3 +269,22 @@ def test_trace_via_json_codec_matches_golden_on_oracle(name):
     o = Oracle(harness.config_for(fx))
     harness.replay(fx, o, codec=codec)
     o.close()
+
+
+def test_threaded_batch_equals_serial():
+    """kwok_decode_pods / _nodes with several host threads give the records
+    (and in-place canonical blobs) of the one-thread decode."""
+    import harness
+    fx = harness.load_trace("churn")
+    pods = [e for t in fx["ticks"] for e in t["pod_events"] if e["op"] == "upsert"]
+    nodes = [e for t in fx["ticks"] for e in t["node_events"] if e["op"] == "upsert"]
+    rng = random.Random(3)
+    pdocs = [scramble(pod_doc(e), rng) for e in pods]
+    ndocs = [scramble(node_doc(e), rng) for e in nodes]
+    codec = Codec(manage_all_nodes=False, manage_nodes_with_annotation_selector=MANAGE,
+                  disregard_status_with_annotation_selector=DISREGARD)
+    for kind, docs in (("pods", pdocs), ("nodes", ndocs)):
+        one = getattr(codec, "decode_" + kind)(docs, threads=1)
+        many = getattr(codec, "decode_" + kind)(docs, threads=5)
+        recs = lambda b: [bytes(r) for r in (b.pods if kind == "pods" else b.nodes)]
+        assert recs(one) == recs(many) and one.buf == many.buf and one.status == many.status
