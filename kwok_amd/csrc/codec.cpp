@@ -27,8 +27,9 @@
 // longer for the accepted domain), so the arena must be writable.
 #include <algorithm>
 #include <cstring>
-#include <map>
+#include <deque>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <vector>
 
@@ -49,12 +50,12 @@ struct JV {
     enum T { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
     bool b = false;
     bool escaped = false;   // STR: the source held an escape (span is not the value)
-    std::string s;          // STR value / NUM text
+    std::string_view s;     // STR value / NUM text (a view of the source, or of the Doc's store)
     uint32_t off = 0, len = 0;  // source span of the value (STR: inside the quotes)
     std::vector<JV> a;
-    std::vector<std::pair<std::string, JV>> o;
+    std::vector<std::pair<std::string_view, JV>> o;
 
-    const JV* get(const char* k) const {
+    const JV* get(std::string_view k) const {
         if (t != OBJ) return nullptr;
         for (auto& kv : o)
             if (kv.first == k) return &kv.second;
@@ -67,8 +68,9 @@ struct Parser {
     const char* p;
     size_t n, i = 0;
     size_t base;
-    std::string err;
-    Parser(const char* arena, size_t off, size_t len) : p(arena + off), n(len), base(off) {}
+    std::deque<std::string>* store;  // decoded text of escaped strings (stable addresses)
+    Parser(const char* arena, size_t off, size_t len, std::deque<std::string>* st)
+        : p(arena + off), n(len), base(off), store(st) {}
 
     void ws() {
         while (i < n && (p[i] == ' ' || p[i] == '\t' || p[i] == '\n' || p[i] == '\r')) i++;
@@ -105,22 +107,31 @@ struct Parser {
         v.t = JV::STR;
         v.off = (uint32_t)(base + i);
         size_t start = i;
+        std::string* buf = nullptr;
         while (i < n && p[i] != '"') {
             unsigned char c = (unsigned char)p[i];
             if (c < 0x20) return false;
-            if (c != '\\') { v.s += (char)c; i++; continue; }
-            v.escaped = true;
+            if (c != '\\') {
+                if (buf) *buf += (char)c;
+                i++;
+                continue;
+            }
+            if (!buf) {
+                store->emplace_back(p + start, i - start);
+                buf = &store->back();
+                v.escaped = true;
+            }
             if (++i >= n) return false;
             char e = p[i++];
             switch (e) {
-                case '"': v.s += '"'; break;
-                case '\\': v.s += '\\'; break;
-                case '/': v.s += '/'; break;
-                case 'b': v.s += '\b'; break;
-                case 'f': v.s += '\f'; break;
-                case 'n': v.s += '\n'; break;
-                case 'r': v.s += '\r'; break;
-                case 't': v.s += '\t'; break;
+                case '"': *buf += '"'; break;
+                case '\\': *buf += '\\'; break;
+                case '/': *buf += '/'; break;
+                case 'b': *buf += '\b'; break;
+                case 'f': *buf += '\f'; break;
+                case 'n': *buf += '\n'; break;
+                case 'r': *buf += '\r'; break;
+                case 't': *buf += '\t'; break;
                 case 'u': {
                     uint32_t c1;
                     if (!hex4(&c1)) return false;
@@ -130,7 +141,7 @@ struct Parser {
                         if (!hex4(&c2) || c2 < 0xDC00 || c2 >= 0xE000) return false;
                         c1 = 0x10000 + ((c1 - 0xD800) << 10) + (c2 - 0xDC00);
                     }
-                    put_utf8(v.s, c1);
+                    put_utf8(*buf, c1);
                     break;
                 }
                 default: return false;
@@ -138,6 +149,7 @@ struct Parser {
         }
         if (i >= n) return false;
         v.len = (uint32_t)(i - start);
+        v.s = buf ? std::string_view(*buf) : std::string_view(p + start, i - start);
         i++;
         return true;
     }
@@ -149,7 +161,7 @@ struct Parser {
             i++;
         if (i == s) return false;
         v.t = JV::NUM;
-        v.s.assign(p + s, i - s);
+        v.s = std::string_view(p + s, i - s);
         return true;
     }
     bool value(JV& v, int depth) {
@@ -163,6 +175,7 @@ struct Parser {
             v.t = JV::OBJ;
             i++;
             ws();
+            v.o.reserve(8);
             if (i < n && p[i] == '}') { i++; ok = true; }
             else {
                 ok = false;
@@ -214,7 +227,7 @@ struct Parser {
 };
 
 // Go encoding/json string escaping (HTML-safe, as json.Marshal does)
-bool go_string(std::string& out, const std::string& s) {
+bool go_string(std::string& out, std::string_view s) {
     static const char* hx = "0123456789abcdef";
     out += '"';
     for (size_t k = 0; k < s.size(); k++) {
@@ -237,7 +250,7 @@ bool go_string(std::string& out, const std::string& s) {
     return true;
 }
 
-bool plain_int(const std::string& t) {
+bool plain_int(std::string_view t) {
     size_t k = t[0] == '-' ? 1 : 0;
     if (k >= t.size()) return false;
     if (t[k] == '0' && t.size() > k + 1) return false;
@@ -267,7 +280,7 @@ bool canon(std::string& out, const JV& v) {
             out += ']';
             return true;
         case JV::OBJ: {
-            std::vector<const std::pair<std::string, JV>*> kv;
+            std::vector<const std::pair<std::string_view, JV>*> kv;
             for (auto& e : v.o) kv.push_back(&e);
             std::stable_sort(kv.begin(), kv.end(), [](auto* x, auto* y) { return x->first < y->first; });
             for (size_t k = 1; k < kv.size(); k++)
@@ -319,23 +332,26 @@ bool norm_equal(const JV& x, const JV& y) {
             return true;
         case JV::OBJ: {
             for (auto& kv : x.o) {
-                const JV* o = y.get(kv.first.c_str());
+                const JV* o = y.get(kv.first);
                 if (o ? !norm_equal(kv.second, *o) : !zeroish(kv.second)) return false;
             }
             for (auto& kv : y.o)
-                if (!x.get(kv.first.c_str()) && !zeroish(kv.second)) return false;
+                if (!x.get(kv.first) && !zeroish(kv.second)) return false;
             return true;
         }
     }
     return false;
 }
 
-JV jstr(const std::string& s) { JV v; v.t = JV::STR; v.s = s; return v; }
+JV jstr(std::string_view s) { JV v; v.t = JV::STR; v.s = s; return v; }
 JV jbool(bool b) { JV v; v.t = JV::BOOL; v.b = b; return v; }
 JV jnum(const char* s) { JV v; v.t = JV::NUM; v.s = s; return v; }
-JV jobj(std::vector<std::pair<std::string, JV>> o) { JV v; v.t = JV::OBJ; v.o = std::move(o); return v; }
+JV jobj(std::vector<std::pair<std::string_view, JV>> o) { JV v; v.t = JV::OBJ; v.o = std::move(o); return v; }
 
 // ---------------------------------------------------------------- selectors
+// labels.Set as decoded from the object: (key, value) views into the document
+using SMap = std::vector<std::pair<std::string_view, std::string_view>>;
+
 struct Req {
     enum Op { IN, NOTIN, EXISTS, NOTEXISTS } op;
     std::string key;
@@ -346,11 +362,13 @@ struct Selector {
     bool set = false;  // false = nil selector (never matches / not configured)
     std::vector<Req> reqs;  // empty + set = labels.Everything()
 
-    bool matches(const std::map<std::string, std::string>& m) const {
+    bool matches(const SMap& m) const {
         for (auto& r : reqs) {
-            auto it = m.find(r.key);
-            bool has = it != m.end();
-            bool in = has && std::find(r.vals.begin(), r.vals.end(), it->second) != r.vals.end();
+            const std::string_view* val = nullptr;
+            for (auto& kv : m)
+                if (kv.first == r.key) val = &kv.second;  // last duplicate wins, as a Go map decode
+            bool has = val != nullptr;
+            bool in = has && std::find(r.vals.begin(), r.vals.end(), *val) != r.vals.end();
             switch (r.op) {
                 case Req::IN: if (!in) return false; break;
                 case Req::NOTIN: if (in) return false; break;
@@ -456,13 +474,13 @@ int parse_selector(const char* text, Selector* out) {
     return KWOK_OK;
 }
 
-int string_map(const JV* v, std::map<std::string, std::string>* m) {
+int string_map(const JV* v, SMap* m) {
     m->clear();
     if (!v || v->is_null()) return KWOK_OK;
     if (v->t != JV::OBJ) return fail(KWOK_EDOMAIN, "labels/annotations is not an object");
     for (auto& kv : v->o) {
         if (kv.second.t != JV::STR) return fail(KWOK_EDOMAIN, "label/annotation value is not a string");
-        (*m)[kv.first] = kv.second.s;
+        m->emplace_back(kv.first, kv.second.s);
     }
     return KWOK_OK;
 }
@@ -478,7 +496,7 @@ int ref(const JV* v, kwok_str* out, const char* what) {
 }
 
 // RFC3339 "YYYY-MM-DDTHH:MM:SSZ" (metav1.Time's wire form) -> unix seconds
-bool parse_time(const std::string& s, int64_t* out) {
+bool parse_time(std::string_view s, int64_t* out) {
     if (s.size() != 20 || s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':' || s[16] != ':' || s[19] != 'Z')
         return false;
     auto d = [&](int a, int n, int* v) {
@@ -503,7 +521,7 @@ bool parse_time(const std::string& s, int64_t* out) {
     return true;
 }
 
-uint8_t pod_phase(const std::string& s) {
+uint8_t pod_phase(std::string_view s) {
     if (s.empty()) return KWOK_PHASE_NONE;
     if (s == "Pending") return KWOK_PHASE_PENDING;
     if (s == "Running") return KWOK_PHASE_RUNNING;
@@ -514,13 +532,14 @@ uint8_t pod_phase(const std::string& s) {
 }
 
 struct Doc {
+    std::deque<std::string> store;
     JV root;
 };
 
 int parse_doc(const char* arena, size_t arena_len, size_t off, size_t len, Doc* d) {
     if (!arena || off > arena_len || len > arena_len - off || arena_len > 0xFFFFFFFFull)
         return fail(KWOK_EINVAL, "document span outside the arena (or arena > 4 GiB)");
-    Parser ps(arena, off, len);
+    Parser ps(arena, off, len, &d->store);
     if (!ps.document(d->root) || d->root.t != JV::OBJ) return fail(KWOK_EDOMAIN, "malformed JSON object document");
     return KWOK_OK;
 }
@@ -567,9 +586,10 @@ int kwok_selector_matches(const char* selector, const char* json_map, size_t len
     int rc = parse_selector(selector, &s);
     if (rc) return rc;
     JV v;
-    Parser ps(json_map, 0, len);
+    std::deque<std::string> store;
+    Parser ps(json_map, 0, len, &store);
     if (!ps.document(v) || (v.t != JV::OBJ && v.t != JV::NUL)) return fail(KWOK_EINVAL, "bad label map JSON");
-    std::map<std::string, std::string> m;
+    SMap m;
     if ((rc = string_map(&v, &m))) return rc;
     *out = s.set && s.matches(m) ? 1 : 0;
     return KWOK_OK;
@@ -587,7 +607,7 @@ int kwok_decode_node(const kwok_codec* c, char* arena, size_t arena_len, size_t 
     if (!md || md->t != JV::OBJ) return fail(KWOK_EDOMAIN, "node without metadata");
     if ((rc = ref(md->get("name"), &ev->name, "metadata.name"))) return rc;
     if (!ev->name.len) return fail(KWOK_EDOMAIN, "node without a name");
-    std::map<std::string, std::string> ann, lab;
+    SMap ann, lab;
     if ((rc = string_map(md->get("annotations"), &ann)) || (rc = string_map(md->get("labels"), &lab))) return rc;
     // needHeartbeat = nodeSelectorFunc (controller.go:83-98); with a label selector the
     // apiserver filters the list/watch, so an object that reaches the codec is managed iff it matches
@@ -654,8 +674,8 @@ int kwok_decode_pod(const kwok_codec* c, char* arena, size_t arena_len, size_t d
     const JV* ct = md->get("creationTimestamp");
     if (!ct || ct->t != JV::STR || !parse_time(ct->s, &ev.creation_unix))
         return fail(KWOK_EDOMAIN, "metadata.creationTimestamp missing or not YYYY-MM-DDTHH:MM:SSZ");
-    const std::string& st_time = ct->s;
-    std::map<std::string, std::string> ann, lab;
+    std::string_view st_time = ct->s;
+    SMap ann, lab;
     if ((rc = string_map(md->get("annotations"), &ann)) || (rc = string_map(md->get("labels"), &lab))) return rc;
     // needLockPod selectors (pod_controller.go:257-267): empty maps never match
     if ((c->disregard_ann.set && !ann.empty() && c->disregard_ann.matches(ann)) ||
@@ -704,10 +724,10 @@ int kwok_decode_pod(const kwok_codec* c, char* arena, size_t arena_len, size_t d
         return rc;
 
     // CONFORMS: SMP(status, rendered) == status for the template's list/time fields (A.4)
-    auto sv = [&](const kwok_str& s) { return std::string(arena + s.off, s.len); };
+    auto sv = [&](const kwok_str& s) { return std::string_view(arena + s.off, s.len); };
     bool conforms = true;
     // conditions: merge key `type`; each rendered condition must already be present with equal fields
-    std::vector<std::string> types = {"Initialized", "Ready", "ContainersReady"};
+    std::vector<std::string_view> types = {"Initialized", "Ready", "ContainersReady"};
     for (uint32_t k = 0; k < out->n_readiness_gates; k++) types.push_back(sv(out->readiness_gates[k]));
     const JV* conds = st->get("conditions");
     for (auto& t : types) {
