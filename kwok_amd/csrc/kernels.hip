@@ -1972,6 +1972,38 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
 // ---------------------------------------------------------------------------
 constexpr int EMIT_BLOCK = 256;
 static_assert(EMIT_BLOCK == BLOCK, "stage_emit_cache / build_hb_template stride by BLOCK");
+// A wave takes chunks of 64 consecutive jobs: one coalesced load brings the 64
+// job records and arena offsets into its lanes, then the wave writes the 64
+// patches with the job read out of lane k.  With the spec programs / blobs in
+// LDS the patch loop issues no global loads, so its stores never have to
+// drain before the next patch starts (a per-patch job load waited on every
+// earlier store: the vmcnt counter is shared).
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); }
+template <bool pods, bool cached>
+__device__ __forceinline__ void emit_chunks(const DevState& S, const EmitCache* c, const uint8_t* hb_tmpl, uint8_t* buf,
+                                            uint32_t w0, uint32_t nw, uint32_t n) {
+    const uint32_t l = lane_id();
+    for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
+        const uint32_t q = ch * 64u + l, cnt = min(64u, n - ch * 64u);
+        uint4 r = make_uint4(0u, 0u, 0u, 0u);
+        uint64_t off = 0;
+        if (q < n) {
+            if (pods) r = S.pp_job[q];
+            else {
+                const uint64_t b = S.init_job[q];
+                r.x = (uint32_t)b;
+                r.y = (uint32_t)(b >> 32);
+            }
+            off = pods ? S.pp_off[q] : S.init_off[q];
+        }
+        const uint32_t olo = (uint32_t)off, ohi = (uint32_t)(off >> 32);
+        for (uint32_t k = 0; k < cnt; k++) {
+            uint8_t* out = S.arena + (((uint64_t)rdlane(ohi, k) << 32) | rdlane(olo, k));
+            if (pods) write_pod_patch<cached>(S, PodJob{rdlane(r.x, k), rdlane(r.y, k), rdlane(r.z, k), rdlane(r.w, k)}, c, buf, out);
+            else write_init_patch<cached>(S, ((uint64_t)rdlane(r.y, k) << 32) | rdlane(r.x, k), hb_tmpl, c, buf, out);
+        }
+    }
+}
 __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
     __shared__ EmitCache ec;
     __shared__ uint4 pbuf4[EMIT_BLOCK / 64 * PATCH_BUF / 16];
@@ -1985,20 +2017,10 @@ __global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevState S, uint64_t now_un
     if (n_init) build_hb_template(S, hb_tmpl, now_unix, start_unix);
     uint8_t* buf = reinterpret_cast<uint8_t*>(pbuf4) + wave_id() * PATCH_BUF;
     const uint32_t w0 = blockIdx.x * (EMIT_BLOCK / 64) + wave_id(), nw = gridDim.x * (EMIT_BLOCK / 64);
-    if (ec.blob_ok) {
-        for (uint32_t q = w0; q < n_init; q += nw) write_init_patch<true>(S, S.init_job[q], hb_tmpl, &ec, buf, S.arena + S.init_off[q]);
-    } else {
-        for (uint32_t q = w0; q < n_init; q += nw) write_init_patch<false>(S, S.init_job[q], hb_tmpl, &ec, buf, S.arena + S.init_off[q]);
-    }
-    auto job = [&](uint32_t q) {
-        const uint4 r = S.pp_job[q];
-        return PodJob{r.x, r.y, r.z, r.w};
-    };
-    if (ec.n_desc) {
-        for (uint32_t q = w0; q < n_pp; q += nw) write_pod_patch<true>(S, job(q), &ec, buf, S.arena + S.pp_off[q]);
-    } else {
-        for (uint32_t q = w0; q < n_pp; q += nw) write_pod_patch<false>(S, job(q), &ec, buf, S.arena + S.pp_off[q]);
-    }
+    if (ec.blob_ok) emit_chunks<false, true>(S, &ec, hb_tmpl, buf, w0, nw, n_init);
+    else emit_chunks<false, false>(S, &ec, hb_tmpl, buf, w0, nw, n_init);
+    if (ec.n_desc) emit_chunks<true, true>(S, &ec, hb_tmpl, buf, w0, nw, n_pp);
+    else emit_chunks<true, false>(S, &ec, hb_tmpl, buf, w0, nw, n_pp);
 }
 
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st) {
