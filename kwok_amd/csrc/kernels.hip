@@ -2004,7 +2004,7 @@ __device__ __forceinline__ void emit_chunks(const DevState& S, const EmitCache* 
         }
     }
 }
-__global__ __launch_bounds__(EMIT_BLOCK) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
+__global__ __launch_bounds__(EMIT_BLOCK, 8) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
     __shared__ EmitCache ec;
     __shared__ uint4 pbuf4[EMIT_BLOCK / 64 * PATCH_BUF / 16];
     __shared__ uint4 hb_tmpl4[HB_CHUNKS];
