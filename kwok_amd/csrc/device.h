@@ -151,11 +151,14 @@ struct PodOp {
 
 // spec descriptor: A | B | C segments of the pod patch (see templates.cpp)
 struct SpecDesc {
-    uint32_t off;             // into spec byte/kind arrays
+    uint32_t off;             // into the spec byte array (timestamp slots zero)
     uint16_t len_a, len_b, len_c;
     uint16_t max_len;         // 16-aligned arena reservation
-    uint32_t ts_first;        // its timestamp slots: spec_ts[ts_first, + n_ts) (offsets into A|B|C)
+    uint32_t nxt_off;         // its timestamp lookup: spec_nxt[nxt_off + d] (build_ts_lookup)
     uint16_t n_ts, pad;
 };
+// byte padding around the spec / blob arrays the emitter reads 4-byte words of
+// (a 16-byte window reads up to 15 bytes before a segment and 20 past it)
+constexpr int SRC_PAD_FRONT = 16, SRC_PAD_BACK = 64;
 
 }  // namespace kwok

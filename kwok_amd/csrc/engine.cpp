@@ -100,11 +100,11 @@ struct kwok_engine {
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
     std::vector<SpecDesc> specs_h;
-    std::string spec_bytes_h, spec_kinds_h;
+    std::string spec_bytes_h;
     DevBuf<SpecDesc> d_specs;
-    DevBuf<uint8_t> d_spec_bytes, d_spec_kinds;
-    std::vector<uint16_t> spec_ts_h;  // timestamp slot offsets of every spec
-    DevBuf<uint16_t> d_spec_ts;
+    DevBuf<uint8_t> d_spec_bytes;
+    std::vector<uint16_t> spec_nxt_h;  // timestamp lookups of every spec (build_ts_lookup)
+    DevBuf<uint16_t> d_spec_nxt;
     uint32_t max_pod_len = 0;
     std::unordered_map<std::string, uint64_t> blob_ids;
     std::string blob_h;
@@ -322,25 +322,23 @@ int flush_ops(kwok_engine* e) {
 int upload_specs(kwok_engine* e) {
     int rc;
     if ((rc = dgrow(e, e->d_specs, e->specs_h.size()))) return rc;
-    // the kernels read the spec bytes as 32-bit words, up to 64 bytes past the end
-    std::string bytes = e->spec_bytes_h;
-    bytes.resize(((bytes.size() + 3) & ~(size_t)3) + 64, '\0');
+    // the kernels read the spec bytes as 32-bit words, up to SRC_PAD_FRONT bytes
+    // before a segment and SRC_PAD_BACK past the end
+    std::string bytes(SRC_PAD_FRONT, '\0');
+    bytes += e->spec_bytes_h;
+    bytes.resize(((bytes.size() + 3) & ~(size_t)3) + SRC_PAD_BACK, '\0');
     if ((rc = dgrow(e, e->d_spec_bytes, bytes.size()))) return rc;
-    if ((rc = dgrow(e, e->d_spec_ts, std::max<size_t>(e->spec_ts_h.size(), 1)))) return rc;
-    if ((rc = dgrow(e, e->d_spec_kinds, e->spec_kinds_h.size()))) return rc;
+    if ((rc = dgrow(e, e->d_spec_nxt, std::max<size_t>(e->spec_nxt_h.size(), 1)))) return rc;
     HIPCHK(e, hipMemcpyAsync(e->d_specs.p, e->specs_h.data(), e->specs_h.size() * sizeof(SpecDesc),
                              hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipMemcpyAsync(e->d_spec_bytes.p, bytes.data(), bytes.size(), hipMemcpyHostToDevice, e->st));
-    if (!e->spec_ts_h.empty())
-        HIPCHK(e, hipMemcpyAsync(e->d_spec_ts.p, e->spec_ts_h.data(), e->spec_ts_h.size() * 2, hipMemcpyHostToDevice, e->st));
-    HIPCHK(e, hipMemcpyAsync(e->d_spec_kinds.p, e->spec_kinds_h.data(), e->spec_kinds_h.size(),
-                             hipMemcpyHostToDevice, e->st));
+    if (!e->spec_nxt_h.empty())
+        HIPCHK(e, hipMemcpyAsync(e->d_spec_nxt.p, e->spec_nxt_h.data(), e->spec_nxt_h.size() * 2, hipMemcpyHostToDevice, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->S.specs = e->d_specs.p;
-    e->S.spec_bytes = e->d_spec_bytes.p;
-    e->S.spec_kinds = e->d_spec_kinds.p;
-    e->S.spec_ts = e->d_spec_ts.p;
-    e->S.ts_total = (uint32_t)e->spec_ts_h.size();
+    e->S.spec_bytes = e->d_spec_bytes.p + SRC_PAD_FRONT;
+    e->S.spec_nxt = e->d_spec_nxt.p;
+    e->S.nxt_total = (uint32_t)e->spec_nxt_h.size();
     e->S.n_specs = (uint32_t)e->specs_h.size();
     e->S.spec_total = (uint32_t)e->spec_bytes_h.size();
     return KWOK_OK;
@@ -429,7 +427,8 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     std::string key = b.pre + '\x01' + b.post;
     auto it = e->blob_ids.find(key);
     if (it != e->blob_ids.end()) return it->second;
-    if (b.pre.size() > 0xFFFF || b.post.size() > 0xFFFF || e->blob_h.size() > 0xFFFFFFFFull - 0x20000) {
+    // k_emit keeps patch positions in 16 bits
+    if (b.pre.size() + CONDS_LEN + b.post.size() > 0xFFF0 || e->blob_h.size() > 0xFFFFFFFFull - 0x20000) {
         *rc = KWOK_EDOMAIN;
         return 0;
     }
@@ -438,14 +437,29 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     e->blob_h += b.post;
     uint64_t word = off | ((uint64_t)b.pre.size() << 32) | ((uint64_t)b.post.size() << 48);
     e->blob_ids.emplace(key, word);
-    uint32_t ilen = 11u + (uint32_t)b.pre.size() + 14u + CONDS_LEN + 1u + (uint32_t)b.post.size() + 2u;
+    uint32_t ilen = (uint32_t)b.pre.size() + CONDS_LEN + (uint32_t)b.post.size();
     e->max_init_len = std::max(e->max_init_len, ilen);
-    size_t old = e->d_blob.n;
-    if ((*rc = dgrow(e, e->d_blob, e->blob_h.size()))) return 0;
-    (void)old;
-    (void)hipMemcpyAsync(e->d_blob.p + off, e->blob_h.data() + off, b.pre.size() + b.post.size(), hipMemcpyHostToDevice,
-                   e->st);
-    e->S.blob = e->d_blob.p;
+    // device copy: SRC_PAD_FRONT zero bytes, the blobs, SRC_PAD_BACK zero bytes (k_emit reads around them)
+    const size_t padded = ((SRC_PAD_FRONT + e->blob_h.size() + 3) & ~(size_t)3) + SRC_PAD_BACK;
+    if (padded > e->d_blob.n) {
+        uint8_t* p = nullptr;
+        const size_t cap = std::max<size_t>(padded, 2 * e->d_blob.n);
+        if (hipMalloc((void**)&p, cap) != hipSuccess) {
+            *rc = e->fail(KWOK_ENOMEM, "blob %zu", cap);
+            return 0;
+        }
+        (void)hipMemsetAsync(p, 0, cap, e->st);
+        if (e->d_blob.p) {
+            (void)hipMemcpyAsync(p, e->d_blob.p, SRC_PAD_FRONT + off, hipMemcpyDeviceToDevice, e->st);
+            (void)hipStreamSynchronize(e->st);
+            (void)hipFree(e->d_blob.p);
+        }
+        e->d_blob.p = p;
+        e->d_blob.n = cap;
+    }
+    (void)hipMemcpyAsync(e->d_blob.p + SRC_PAD_FRONT + off, e->blob_h.data() + off, b.pre.size() + b.post.size(),
+                         hipMemcpyHostToDevice, e->st);
+    e->S.blob = e->d_blob.p + SRC_PAD_FRONT;
     e->S.blob_total = (uint32_t)e->blob_h.size();
     return word;
 }
@@ -570,7 +584,7 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
-                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_kinds.p, e->d_spec_ts.p, e->d_blob.p, e->d_ops,
+                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -783,7 +797,9 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     for (uint32_t i = 0; i < spec->n_readiness_gates; i++)
         if (!get(spec->readiness_gates[i], gates[i])) return e->fail(KWOK_EDOMAIN, "readiness gate %u: not a safe string", i);
     SpecProgram p = build_spec_program(cs, ics, gates);
-    if (p.max_len > 0xFFFF) return e->fail(KWOK_EDOMAIN, "pod patch longer than 64 KiB");
+    if (p.max_len > 0xFFF0) return e->fail(KWOK_EDOMAIN, "pod patch longer than 64 KiB");
+    std::vector<uint16_t> nxt;
+    if (!build_ts_lookup(p, nxt)) return e->fail(KWOK_EDOMAIN, "pod patch layout outside the emitter's domain");
     std::string key = p.a + '\x01' + p.ka + '\x01' + p.b + '\x01' + p.kb + '\x01' + p.c + '\x01' + p.kc;
     auto it = e->spec_ids.find(key);
     if (it != e->spec_ids.end()) {
@@ -798,12 +814,12 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     d.len_b = (uint16_t)p.b.size();
     d.len_c = (uint16_t)p.c.size();
     d.max_len = (uint16_t)p.max_len;
-    d.ts_first = (uint32_t)e->spec_ts_h.size();
+    d.nxt_off = (uint32_t)e->spec_nxt_h.size();
     const std::string kinds = p.ka + p.kb + p.kc;
     for (size_t i = 0; i < kinds.size(); i++)  // slot starts (kinds 0..19 in a row)
-        if (kinds[i] == 0) e->spec_ts_h.push_back((uint16_t)i), d.n_ts++;
+        if (kinds[i] == 0) d.n_ts++;
+    e->spec_nxt_h.insert(e->spec_nxt_h.end(), nxt.begin(), nxt.end());
     e->spec_bytes_h += p.a + p.b + p.c;
-    e->spec_kinds_h += kinds;
     e->specs_h.push_back(d);
     int rc = upload_specs(e);
     if (rc) return rc;

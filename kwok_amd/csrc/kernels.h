@@ -43,12 +43,11 @@ struct DevState {
     PoolGeom pool;
     // pod spec programs / node blobs
     const SpecDesc* specs;
-    const uint8_t* spec_bytes;
-    const uint8_t* spec_kinds;
-    const uint8_t* blob;
-    const uint16_t* spec_ts;       // timestamp slot offsets of every spec (SpecDesc::ts_first)
+    const uint8_t* spec_bytes;     // SRC_PAD_FRONT bytes into a padded device array
+    const uint8_t* blob;           // (likewise) framed node init blobs: pre | post
+    const uint16_t* spec_nxt;      // timestamp lookups of every spec (SpecDesc::nxt_off)
     uint32_t n_specs, spec_total;  // spec descriptors; bytes of the concatenated spec programs
-    uint32_t ts_total;             // entries of spec_ts
+    uint32_t nxt_total;            // entries of spec_nxt
     uint32_t blob_total;           // bytes of the interned node blobs
     // heartbeat template
     const uint8_t* hb_static;

@@ -207,9 +207,6 @@ constexpr Lit16 lit16(const char* s) {
     }
     return r;
 }
-__device__ __forceinline__ uint32_t lit_byte(Lit16 l, uint32_t i) {
-    return (uint32_t)((i < 8 ? l.lo >> (8 * i) : l.hi >> (8 * (i - 8))) & 0xFF);
-}
 
 // ---------------------------------------------------------------------------
 // per-object predicates (shared by k_classify and k_emit)
@@ -251,189 +248,10 @@ __device__ __forceinline__ PodCls classify_pod(uint16_t st, uint8_t ntf, uint32_
     return c;
 }
 
+// framed blob (templates.cpp build_node_blob): pre | heartbeat conditions | post
 __device__ __forceinline__ uint32_t init_patch_len(uint64_t blob) {
-    uint32_t pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
-    return 11u + pre + 14u + (uint32_t)CONDS_LEN + 1u + post + 2u;
-}
-
-
-// ---------------------------------------------------------------------------
-// patch writers (one wave per patch; kernel k_emit)
-// ---------------------------------------------------------------------------
-// a pod patch job (k_tick writes it as a uint4 into S.pp_job; k_emit writes the bytes)
-struct PodJob {
-    uint32_t pod_ip;  // rendered podIP (0 = no status section)
-    uint32_t host_ip;
-    uint32_t ctime;   // creationTimestamp (unix seconds)
-    uint32_t spec;    // pod spec id
-};
-
-// the spec programs and node blobs of the engine, staged in LDS once per
-// emitting block when they fit (the common case: a handful of specs / blobs);
-// otherwise the writers read them from global memory
-constexpr int SPEC_LDS_DESCS = 64, SPEC_LDS_PROG = 4096, SPEC_LDS_TS = 256, BLOB_LDS = 4096;
-struct EmitCache {
-    uint32_t n_desc;                       // 0: not staged
-    uint32_t blob_ok;
-    SpecDesc desc[SPEC_LDS_DESCS];
-    uint32_t prog32[SPEC_LDS_PROG / 4 + 16];  // the spec bytes (timestamp slots zero), readable 64 bytes past the end
-    uint16_t ts[SPEC_LDS_TS];                // timestamp slot offsets of the specs (spec-relative)
-    uint8_t blob[BLOB_LDS];
-};
-__device__ __forceinline__ void stage_emit_cache(const DevState& S, EmitCache* c, bool pods, bool nodes) {
-    const bool sp = pods && S.n_specs <= (uint32_t)SPEC_LDS_DESCS && S.spec_total <= (uint32_t)SPEC_LDS_PROG &&
-                    S.ts_total <= (uint32_t)SPEC_LDS_TS;
-    const bool bl = nodes && S.blob_total <= (uint32_t)BLOB_LDS;
-    if (sp) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.spec_bytes);  // padded by the host
-        for (uint32_t i = threadIdx.x; i < S.n_specs; i += BLOCK) c->desc[i] = S.specs[i];
-        for (uint32_t i = threadIdx.x; i < (S.spec_total + 3) / 4 + 16; i += BLOCK) c->prog32[i] = w[i];
-        for (uint32_t i = threadIdx.x; i < S.ts_total; i += BLOCK) c->ts[i] = S.spec_ts[i];
-    }
-    if (bl)
-        for (uint32_t i = threadIdx.x; i < S.blob_total; i += BLOCK) c->blob[i] = S.blob[i];
-    if (threadIdx.x == 0) {
-        c->n_desc = sp ? S.n_specs : 0u;
-        c->blob_ok = bl ? 1u : 0u;
-    }
-    __syncthreads();
-}
-
-// Patches are assembled in a per-wave LDS buffer, then copied out 16 bytes per
-// lane.  Longer patches than the buffer (specs with many containers) take the
-// direct per-byte path.
-constexpr uint32_t PATCH_BUF = 2048;
-
-// bytes [o, o + 4) / byte o of the spec programs (words w: LDS copy or the padded global array;
-// pass 1 below reads up to 60 bytes past a spec's end for the words the IP pieces replace)
-__device__ __forceinline__ uint32_t tmpl_word(const uint32_t* w, uint32_t o) {
-    const uint32_t i = o >> 2;
-    return __builtin_amdgcn_alignbyte(w[i + 1], w[i], o & 3u);
-}
-__device__ __forceinline__ uint32_t tmpl_byte8(const uint32_t* w, uint32_t o) { return (w[o >> 2] >> (8u * (o & 3u))) & 0xFFu; }
-// byte o of a spec's A|B|C template with its timestamp slots filled (global arrays)
-__device__ __forceinline__ uint32_t tmpl_byte(const DevState& S, uint32_t off, const Ts& ts) {
-    const uint32_t kd = S.spec_kinds[off];
-    return kd == 0xFF ? S.spec_bytes[off] : ts_byte(ts, kd);
-}
-// byte i of `"<key>":"<ip>",` (key: 10 bytes for hostIP, 9 for podIP)
-__device__ __forceinline__ uint32_t ipseg_byte(Lit16 key, uint32_t klen, const IpStr& ip, uint32_t i) {
-    return i < klen ? lit_byte(key, i) : i < klen + ip.len ? ip_byte(ip, i - klen) : (i == klen + ip.len ? '"' : ',');
-}
-
-// One wave writes one pod patch: A [+ "hostIP":"H",] B [+ "podIP":"P",] C
-// (pod_controller.go:404-439 over pod.status.tpl).  The job's fields are
-// wave-uniform (scalar formatting of the timestamp and the two IPs).  Pass 1
-// writes the template 4 bytes per lane, each word shifted to its segment's
-// output position (two aligned reads + alignbyte); pass 2 rewrites, byte by
-// byte, the hostIP / podIP pieces with the words they straddle, then the
-// timestamp slots.
-template <bool cached>  // the spec programs staged in LDS (EmitCache) or read from global memory
-__device__ __forceinline__ void write_pod_patch(const DevState& S, const PodJob& j, const EmitCache* c, uint8_t* buf,
-                                                uint8_t* out) {
-    const uint32_t spec = __builtin_amdgcn_readfirstlane(j.spec);
-    const SpecDesc sd = cached ? c->desc[spec] : S.specs[spec];
-    const Ts ts = format_ts(__builtin_amdgcn_readfirstlane(j.ctime));
-    const uint32_t hip = __builtin_amdgcn_readfirstlane(j.host_ip), pip = __builtin_amdgcn_readfirstlane(j.pod_ip);
-    const bool st = hip != 0;
-    const IpStr H = format_ip(hip), P = format_ip(pip);
-    const uint32_t la = sd.len_a, lb = sd.len_b, lc = sd.len_c;
-    const uint32_t lh = st ? 10u + H.len + 2u : 0u, lp = st ? 9u + P.len + 2u : 0u;
-    const uint32_t eA = la + lh, eB = eA + lb, eP = eB + lp;  // output starts of B, the podIP piece, C
-    const uint32_t len = eP + lc;
-    constexpr Lit16 kh = lit16("\"hostIP\":\""), kp = lit16("\"podIP\":\"");
-    const uint32_t l = lane_id();
-    if (len <= PATCH_BUF) {
-        const uint32_t* W = cached ? c->prog32 : reinterpret_cast<const uint32_t*>(S.spec_bytes);
-        const uint32_t base = sd.off;
-        for (uint32_t p = 4u * l; p < len; p += 256u) {
-            const uint32_t sh = p < eA ? 0u : (p < eP ? lh : lh + lp);
-            *reinterpret_cast<uint32_t*>(buf + p) = tmpl_word(W, base + p - sh);
-        }
-        if (st) {  // the IP pieces and the B / C bytes of the words they end in
-            const uint32_t n1 = min(len, (eA + 3u) & ~3u) - la, n2 = min(len, (eP + 3u) & ~3u) - eB;
-            if (l < n1 + n2) {
-                const uint32_t p = l < n1 ? la + l : eB + (l - n1);
-                uint32_t b;
-                if (p < eA) b = ipseg_byte(kh, 10, H, p - la);
-                else if (p < eB) b = tmpl_byte8(W, base + p - lh);
-                else if (p < eP) b = ipseg_byte(kp, 9, P, p - eB);
-                else b = tmpl_byte8(W, base + p - lh - lp);
-                buf[p] = (uint8_t)b;
-            }
-        }
-        const uint32_t nts = sd.n_ts * (uint32_t)TS_LEN;  // timestamp slots (never across a segment end)
-        for (uint32_t i = l; i < nts; i += 64u) {
-            const uint32_t k = i / (uint32_t)TS_LEN, bi = i - k * (uint32_t)TS_LEN;
-            const uint32_t t = (cached ? c->ts[sd.ts_first + k] : S.spec_ts[sd.ts_first + k]) + bi;
-            buf[t < la ? t : (t < la + lb ? t + lh : t + lh + lp)] = (uint8_t)ts_byte(ts, bi);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes before its reads
-        for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u)
-            *reinterpret_cast<uint4*>(out + q0) = *reinterpret_cast<const uint4*>(buf + q0);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads complete before the next patch's writes
-        return;
-    }
-    for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u) {  // long patches: byte by byte
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (uint32_t k = 0; k < 16; k++) {
-            uint32_t p = q0 + k, b = 0;
-            if (p < len) {
-                if (p < la) b = tmpl_byte(S, sd.off + p, ts);
-                else if ((p -= la) < lh) b = ipseg_byte(kh, 10, H, p);
-                else if ((p -= lh) < lb) b = tmpl_byte(S, sd.off + la + p, ts);
-                else if ((p -= lb) < lp) b = ipseg_byte(kp, 9, P, p);
-                else b = tmpl_byte(S, sd.off + la + lb + (p - lp), ts);
-            }
-            w[k >> 2] |= b << (8 * (k & 3));
-        }
-        *reinterpret_cast<uint4*>(out + q0) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
-// one wave writes one node init patch: {"status":{ pre ,"conditions": CONDS , post }}
-template <bool cached>  // the node blobs staged in LDS (EmitCache) or read from global memory
-__device__ __forceinline__ void write_init_patch(const DevState& S, uint64_t blob, const uint8_t* hb_tmpl,
-                                                 const EmitCache* c, uint8_t* buf, uint8_t* out) {
-    const uint32_t boff = (uint32_t)blob, pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
-    const uint32_t len = init_patch_len(blob);
-    const uint8_t* bb = (cached ? c->blob : S.blob) + boff;
-    const uint8_t* conds = hb_tmpl + HB_PREFIX;
-    constexpr Lit16 p0 = lit16("{\"status\":{"), p1 = lit16(",\"conditions\":");
-    const uint32_t l = lane_id();
-    if (len <= PATCH_BUF) {
-        // layout: p0 (11) | pre | p1 (14) | CONDS | ',' | post | '}' '}'
-        if (l < 11) buf[l] = (uint8_t)lit_byte(p0, l);
-        for (uint32_t i = l; i < pre; i += 64) buf[11 + i] = bb[i];
-        if (l < 14) buf[11 + pre + l] = (uint8_t)lit_byte(p1, l);
-        for (uint32_t i = l; i < (uint32_t)CONDS_LEN; i += 64) buf[25 + pre + i] = conds[i];
-        const uint32_t o = 25 + pre + CONDS_LEN;
-        if (l == 0) buf[o] = ',';
-        for (uint32_t i = l; i < post; i += 64) buf[o + 1 + i] = bb[pre + i];
-        if (l < 2) buf[o + 1 + post + l] = '}';
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u)
-            *reinterpret_cast<uint4*>(out + q0) = *reinterpret_cast<const uint4*>(buf + q0);
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        return;
-    }
-    for (uint32_t q0 = l * 16u; q0 < len; q0 += 1024u) {
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (uint32_t k = 0; k < 16; k++) {
-            uint32_t p = q0 + k, b = 0;
-            if (p < len) {
-                if (p < 11u) b = lit_byte(p0, p);
-                else if ((p -= 11u) < pre) b = bb[p];
-                else if ((p -= pre) < 14u) b = lit_byte(p1, p);
-                else if ((p -= 14u) < (uint32_t)CONDS_LEN) b = conds[p];
-                else if ((p -= CONDS_LEN) < 1u) b = ',';
-                else if ((p -= 1u) < post) b = bb[pre + p];
-                else b = '}';
-            }
-            w[k >> 2] |= b << (8 * (k & 3));
-        }
-        *reinterpret_cast<uint4*>(out + q0) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+    const uint32_t pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
+    return pre + (uint32_t)CONDS_LEN + post;
 }
 
 // ---------------------------------------------------------------------------
@@ -1966,61 +1784,292 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
 // ---------------------------------------------------------------------------
 // k_emit: the patch bytes of a tick's node inits and pod patches, from the job
 // records k_tick wrote (S.init_job / S.pp_job at the ordinals of init_off /
-// pp_off).  A kernel of its own because patch assembly is latency-bound per
-// wave: k_tick runs one chain wave per SIMD, this grid runs up to 8.  Launched
-// after the tick's k_tick on the same stream (only for ticks with jobs).
+// pp_off; pod_controller.go:404-439 over pod.status.tpl, node_controller.go:
+// 356-391 over node.status.tpl + node.heartbeat.tpl).  Launched after the
+// tick's k_tick on the same stream (only for ticks with jobs).
+//
+// The work unit is 16 output bytes, assembled in registers and written with
+// one 16-byte store.  A patch is a sequence of regions, each >= 16 bytes:
+//   pod, status non-empty:  A | "hostIP":"H", | B | "podIP":"P", | C
+//   pod, status empty:      A B C                  (one region)
+//   node init:              pre | CONDS | post     (framed blob; the tick's
+//                                                   heartbeat conditions)
+// so a unit spans at most two regions, and (pods) overlaps at most one
+// 20-byte creationTimestamp slot of the template (build_ts_lookup).  A wave
+// takes 64 consecutive jobs at a time:
+//   phase 1  lane j <- job j: the job's timestamp and hostIP / podIP pieces
+//            into the wave's LDS record, its region bounds, its unit count;
+//            a DPP scan gives the units' job-relative numbering;
+//   phase 2  the chunk's units, 64 per pass (one per lane): the lane's job
+//            (a uniform walk over the few jobs a pass touches), two 16-byte
+//            source windows (5 dword reads + alignbyte each), a byte-mask
+//            merge at the region boundary, the timestamp overlay, the store.
+// Sources (spec programs, blobs, the heartbeat conditions, the job records)
+// are read from LDS; a spec set or blob set too large for the block's cache
+// is read from global memory instead (same code, generic pointers).
 // ---------------------------------------------------------------------------
 constexpr int EMIT_BLOCK = 256;
-static_assert(EMIT_BLOCK == BLOCK, "stage_emit_cache / build_hb_template stride by BLOCK");
-// A wave takes chunks of 64 consecutive jobs: one coalesced load brings the 64
-// job records and arena offsets into its lanes, then the wave writes the 64
-// patches with the job read out of lane k.  With the spec programs / blobs in
-// LDS the patch loop issues no global loads, so its stores never have to
-// drain before the next patch starts (a per-patch job load waited on every
-// earlier store: the vmcnt counter is shared).
+static_assert(EMIT_BLOCK == BLOCK, "build_hb_template strides by BLOCK");
+constexpr int EC_DESC = 64, EC_PROG = 4096, EC_NXT = 1280, EC_BLOB = 2048;
+constexpr uint32_t SEG_STRIDE = 56;  // per job: "hostIP":"H", (28 bytes) | "podIP":"P", (28 bytes)
+constexpr uint32_t TS_STRIDE = 36;   // per job: its 20-byte timestamp, then 16 zero bytes
+constexpr uint32_t TS_FIRST = 16;    // 16 zero bytes before job 0's timestamp
+constexpr uint32_t TS_ZERO = TS_FIRST + 64 * TS_STRIDE;  // 20+ zero bytes (a unit with no slot)
+constexpr uint32_t TS_AREA = TS_ZERO + 32;
+struct EmitWave {
+    uint32_t out_lo[64], out_hi[64];  // arena offset of each job's patch
+    uint32_t e12[64], e34[64];        // region starts 1..4 (u16 pairs; 0xFFFF: no such region)
+    uint32_t aux[64];                 // pods: spec id; inits: blob offset
+    uint8_t seg[SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_BACK];
+    uint8_t ts[TS_AREA];
+};
+struct EmitLds {
+    SpecDesc desc[EC_DESC];
+    uint16_t nxt[EC_NXT];
+    uint8_t prog[SRC_PAD_FRONT + EC_PROG + SRC_PAD_BACK];
+    uint8_t blob[SRC_PAD_FRONT + EC_BLOB + SRC_PAD_BACK];
+    uint8_t hb[HB_STRIDE + SRC_PAD_BACK];  // the tick's heartbeat template; CONDS at HB_PREFIX
+    uint32_t spec_ok, blob_ok;
+    EmitWave w[EMIT_BLOCK / 64];
+};
+static_assert(sizeof(EmitLds) <= 40960, "four k_emit blocks per CU");
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); }
-template <bool pods, bool cached>
-__device__ __forceinline__ void emit_chunks(const DevState& S, const EmitCache* c, const uint8_t* hb_tmpl, uint8_t* buf,
-                                            uint32_t w0, uint32_t nw, uint32_t n) {
-    const uint32_t l = lane_id();
-    for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
-        const uint32_t q = ch * 64u + l, cnt = min(64u, n - ch * 64u);
-        uint4 r = make_uint4(0u, 0u, 0u, 0u);
-        uint64_t off = 0;
-        if (q < n) {
-            if (pods) r = S.pp_job[q];
-            else {
-                const uint64_t b = S.init_job[q];
-                r.x = (uint32_t)b;
-                r.y = (uint32_t)(b >> 32);
-            }
-            off = pods ? S.pp_off[q] : S.init_off[q];
-        }
-        const uint32_t olo = (uint32_t)off, ohi = (uint32_t)(off >> 32);
-        for (uint32_t k = 0; k < cnt; k++) {
-            uint8_t* out = S.arena + (((uint64_t)rdlane(ohi, k) << 32) | rdlane(olo, k));
-            if (pods) write_pod_patch<cached>(S, PodJob{rdlane(r.x, k), rdlane(r.y, k), rdlane(r.z, k), rdlane(r.w, k)}, c, buf, out);
-            else write_init_patch<cached>(S, ((uint64_t)rdlane(r.y, k) << 32) | rdlane(r.x, k), hb_tmpl, c, buf, out);
-        }
+
+// 16 bytes at byte offset `off` of a 4-byte aligned source (LDS or global)
+__device__ __forceinline__ uint4 ext16(const uint8_t* base, uint32_t off) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(base) + (off >> 2);
+    const uint32_t sh = off & 3u;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+// `"<key>":"<ip>",` as 7 dwords (key: KLEN bytes, 10 for hostIP, 9 for podIP)
+template <int KLEN>
+__device__ __forceinline__ void write_seg(uint8_t* dst, Lit16 key, const IpStr& ip) {
+    uint32_t d[6] = {(uint32_t)ip.lo, (uint32_t)(ip.lo >> 32), (uint32_t)ip.hi, (uint32_t)(ip.hi >> 32), 0u, 0u};
+    const uint64_t tail = 0x2C22ull << (8u * (ip.len & 3u));  // '"' ',' after the address
+    const uint32_t m = ip.len >> 2;
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) d[k] |= (m == k ? (uint32_t)tail : 0u) | (m + 1u == k ? (uint32_t)(tail >> 32) : 0u);
+    const uint32_t kw[4] = {(uint32_t)key.lo, (uint32_t)(key.lo >> 32), (uint32_t)key.hi, (uint32_t)(key.hi >> 32)};
+    uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        const int b = 4 * i - KLEN;  // offset into `<ip>",` of this dword's first byte
+        uint32_t v = i < 4 ? kw[i] : 0u;
+        if (b >= 0) v |= __builtin_amdgcn_alignbyte(d[(b >> 2) + 1], d[b >> 2], (uint32_t)(b & 3));
+        else if (b > -4) v |= d[0] << (8 * -b);
+        o[i] = v;
     }
 }
-__global__ __launch_bounds__(EMIT_BLOCK, 8) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
-    __shared__ EmitCache ec;
-    __shared__ uint4 pbuf4[EMIT_BLOCK / 64 * PATCH_BUF / 16];
-    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
+
+// the block's sources in LDS (when they fit), the tick's heartbeat template,
+// zeroed job records
+__device__ __forceinline__ void stage_emit(const DevState& S, EmitLds* L, bool pods, bool nodes, uint64_t now_unix,
+                                           uint64_t start_unix) {
+    const uint32_t t = threadIdx.x;
+    const bool sp = pods && S.n_specs <= (uint32_t)EC_DESC && S.spec_total <= (uint32_t)EC_PROG &&
+                    S.nxt_total <= (uint32_t)EC_NXT;
+    const bool bl = nodes && S.blob_total <= (uint32_t)EC_BLOB;
+    if (sp) {
+        for (uint32_t i = t; i < S.n_specs; i += BLOCK) L->desc[i] = S.specs[i];
+        for (uint32_t i = t; i < S.nxt_total; i += BLOCK) L->nxt[i] = S.spec_nxt[i];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(S.spec_bytes - SRC_PAD_FRONT);  // the padded array
+        uint32_t* dst = reinterpret_cast<uint32_t*>(L->prog);
+        for (uint32_t i = t; i < (SRC_PAD_FRONT + S.spec_total + 3) / 4 + SRC_PAD_BACK / 4; i += BLOCK) dst[i] = src[i];
+    }
+    if (bl) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(S.blob - SRC_PAD_FRONT);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(L->blob);
+        for (uint32_t i = t; i < (SRC_PAD_FRONT + S.blob_total + 3) / 4 + SRC_PAD_BACK / 4; i += BLOCK) dst[i] = src[i];
+    }
+    uint32_t* z = reinterpret_cast<uint32_t*>(L->w);
+    for (uint32_t i = t; i < sizeof(L->w) / 4; i += BLOCK) z[i] = 0u;
+    for (uint32_t i = HB_STRIDE + t; i < HB_STRIDE + SRC_PAD_BACK; i += BLOCK) L->hb[i] = 0;
+    if (t == 0) {
+        L->spec_ok = sp ? 1u : 0u;
+        L->blob_ok = bl ? 1u : 0u;
+    }
+    if (nodes) build_hb_template(S, L->hb, now_unix, start_unix);  // synchronises
+    __syncthreads();
+}
+
+// phase 1: lane l <- job q; returns its number of 16-byte units
+template <bool POD, bool CACHED>
+__device__ __forceinline__ uint32_t emit_phase1(const DevState& S, const EmitLds* L, EmitWave* W, uint32_t q, uint32_t n) {
+    const uint32_t l = lane_id();
+    uint32_t nu = 0, olo = 0, ohi = 0, e12 = 0xFFFFFFFFu, e34 = 0xFFFFFFFFu, aux = 0;
+    if (q < n) {
+        uint64_t off;
+        uint32_t len;
+        if (POD) {
+            const uint4 j = S.pp_job[q];  // podIP (0: no status section), hostIP, creationTimestamp, spec
+            off = S.pp_off[q];
+            len = S.pp_len[q];
+            aux = j.w;
+            const Ts ts = format_ts(j.z);
+            uint32_t* tw = reinterpret_cast<uint32_t*>(W->ts + TS_FIRST + l * TS_STRIDE);
+            tw[0] = (uint32_t)ts.w0;
+            tw[1] = (uint32_t)(ts.w0 >> 32);
+            tw[2] = (uint32_t)ts.w1;
+            tw[3] = (uint32_t)(ts.w1 >> 32);
+            tw[4] = (uint32_t)ts.w2;
+            if (j.y != 0) {  // `{{ with .status }}`: hostIP / podIP (pod.status.tpl:44-47)
+                const SpecDesc sd = CACHED ? L->desc[j.w] : S.specs[j.w];
+                const IpStr H = format_ip(j.y), P = format_ip(j.x);
+                uint8_t* sg = W->seg + SRC_PAD_FRONT + l * SEG_STRIDE;
+                write_seg<10>(sg, lit16("\"hostIP\":\""), H);
+                write_seg<9>(sg + 28, lit16("\"podIP\":\""), P);
+                const uint32_t e1 = sd.len_a, e2 = e1 + 12u + H.len, e3 = e2 + sd.len_b, e4 = e3 + 11u + P.len;
+                e12 = e1 | e2 << 16;
+                e34 = e3 | e4 << 16;
+            }
+        } else {
+            const uint64_t b = S.init_job[q];
+            off = S.init_off[q];
+            len = S.init_len[q];
+            aux = (uint32_t)b;
+            const uint32_t pre = (uint32_t)(b >> 32) & 0xFFFFu;
+            e12 = pre | (pre + (uint32_t)CONDS_LEN) << 16;
+        }
+        olo = (uint32_t)off;
+        ohi = (uint32_t)(off >> 32);
+        nu = (len + 15u) >> 4;
+    }
+    W->out_lo[l] = olo;
+    W->out_hi[l] = ohi;
+    W->e12[l] = e12;
+    W->e34[l] = e34;
+    W->aux[l] = aux;
+    return nu;
+}
+
+// phase 2: the units of the chunk's cnt jobs (ustart: lane j = job j's first unit)
+template <bool POD, bool CACHED>
+__device__ __forceinline__ void emit_phase2(const DevState& S, const EmitLds* L, const EmitWave* W, uint32_t cnt,
+                                            uint32_t ustart, uint32_t utot) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t l = lane_id();
+    const uint8_t* lds = reinterpret_cast<const uint8_t*>(L);
+    const uint32_t o_seg = (uint32_t)((const uint8_t*)W->seg - lds) + SRC_PAD_FRONT;
+    const uint32_t o_ts = (uint32_t)((const uint8_t*)W->ts - lds);
+    const uint32_t o_prog = (uint32_t)offsetof(EmitLds, prog) + SRC_PAD_FRONT;
+    const uint32_t o_blob = (uint32_t)offsetof(EmitLds, blob) + SRC_PAD_FRONT;
+    const uint32_t o_conds = (uint32_t)offsetof(EmitLds, hb) + HB_PREFIX;
+    // the template source: the LDS cache, else the global array
+    const uint8_t* tbase = CACHED ? lds : (POD ? S.spec_bytes : S.blob);
+    const uint32_t o_tmpl = CACHED ? (POD ? o_prog : o_blob) : 0u;
+    uint32_t kcur = 0;
+    for (uint32_t u0 = 0; u0 < utot; u0 += 64u) {
+        const uint32_t u = u0 + l;
+        // the lane's job: the last job of the pass whose first unit is <= u
+        uint32_t k = kcur, sk = rdlane(ustart, kcur);
+        for (uint32_t j = kcur + 1; j < cnt; j++) {
+            const uint32_t s = rdlane(ustart, j);
+            if (s > u0 + 63u) break;
+            if (u >= s) k = j, sk = s;
+        }
+        kcur = rdlane(k, 63);
+        if (u >= utot) continue;
+        const uint32_t x = (u - sk) << 4;  // the unit's first byte in its patch
+        const uint32_t e12 = W->e12[k], e34 = W->e34[k], aux = W->aux[k];
+        const uint64_t obase = ((uint64_t)W->out_hi[k] << 32) | W->out_lo[k];
+        const uint32_t e1 = e12 & 0xFFFFu, e2 = e12 >> 16, e3 = e34 & 0xFFFFu, e4 = e34 >> 16;
+        auto region = [&](uint32_t p) {
+            return (uint32_t)(p >= e1) + (uint32_t)(p >= e2) + (uint32_t)(p >= e3) + (uint32_t)(p >= e4);
+        };
+        auto rstart = [&](uint32_t r) { return r == 0 ? 0u : r == 1 ? e1 : r == 2 ? e2 : r == 3 ? e3 : e4; };
+        const uint32_t r1 = region(x), r2 = region(x + 15u);
+        const uint32_t s1 = rstart(r1), s2 = rstart(r2);
+        const uint32_t n = r1 == r2 ? 16u : s2 - x;  // bytes of the unit in region r1
+        SpecDesc sd{};
+        if (POD) sd = CACHED ? L->desc[aux] : S.specs[aux];
+        // template coordinate of region r's first byte (pods: the A|B|C offset of a
+        // template region; inits: the blob offset of pre / post)
+        auto tstart = [&](uint32_t r) {
+            if (POD) return r == 0 ? 0u : r == 2 ? e1 : e1 + e3 - e2;
+            return r == 0 ? 0u : e1;
+        };
+        // byte source of region r at output position x (a window may start before
+        // its region: the source arrays are padded)
+        auto src = [&](uint32_t r, uint32_t s, const uint8_t*& base) -> uint32_t {
+            if (POD) {
+                if (r & 1u) {
+                    base = lds;
+                    return o_seg + k * SEG_STRIDE + (r == 3 ? 28u : 0u) + x - s;
+                }
+                base = tbase;
+                return o_tmpl + sd.off + tstart(r) + x - s;
+            }
+            if (r == 1) {
+                base = lds;
+                return o_conds + x - s;
+            }
+            base = tbase;
+            return o_tmpl + aux + tstart(r) + x - s;
+        };
+        const uint8_t *b1, *b2;
+        const uint32_t a1 = src(r1, s1, b1), a2 = src(r2, s2, b2);
+        const uint4 v1 = ext16(b1, a1), v2 = ext16(b2, a2);
+        uint32_t o[4];
+        const uint32_t vv1[4] = {v1.x, v1.y, v1.z, v1.w}, vv2[4] = {v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int c = min(max((int)n - 4 * d, 0), 4);  // bytes of dword d from region r1
+            const uint32_t m = c == 4 ? 0xFFFFFFFFu : (1u << (8 * c)) - 1u;
+            o[d] = (vv1[d] & m) | (vv2[d] & ~m);
+        }
+        if (POD) {
+            // the timestamp slot (at most one) inside the unit's template region
+            const uint32_t rt = (r1 & 1u) ? r2 : r1;
+            const uint32_t st = rt == r1 ? s1 : s2, tst = tstart(rt);
+            const uint32_t w0 = rt == r1 ? x : s2, w1 = rt == r2 ? x + 16u : s2;
+            const uint32_t tw0 = tst + w0 - st, tw1 = tst + w1 - st;
+            const uint32_t ni = sd.nxt_off + (tw0 >> 2);
+            const uint32_t s = (rt & 1u) ? 0xFFFFu : (uint32_t)(CACHED ? L->nxt[ni] : S.spec_nxt[ni]);
+            const bool ov = s < tw1 && s + (uint32_t)TS_LEN > tw0;
+            const uint32_t so = s - tst + st;  // output position of the slot
+            const uint4 t4 = ext16(lds, o_ts + (ov ? TS_FIRST + k * TS_STRIDE + x - so : TS_ZERO));
+            o[0] |= t4.x;
+            o[1] |= t4.y;
+            o[2] |= t4.z;
+            o[3] |= t4.w;
+        }
+        *reinterpret_cast<u32x4*>(S.arena + obase + x) = u32x4{o[0], o[1], o[2], o[3]};
+    }
+}
+
+template <bool POD, bool CACHED>
+__device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_t w0, uint32_t nw, uint32_t n) {
+    EmitWave* W = &L->w[wave_id()];
+    for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
+        const uint32_t cnt = min(64u, n - ch * 64u);
+        const uint32_t nu = emit_phase1<POD, CACHED>(S, L, W, ch * 64u + lane_id(), n);
+        const uint32_t incl = wave_incl_scan(nu);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the records before phase 2 reads them
+        emit_phase2<POD, CACHED>(S, L, W, cnt, incl - nu, rdlane(incl, 63));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // phase 2's reads before the next records
+    }
+}
+
+__global__ __launch_bounds__(EMIT_BLOCK, 4) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
+    __shared__ EmitLds L;
     if (S.world > 1 && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return;  // the tick's launches were skipped (queued behind one the host has not finished)
     const uint32_t n_pp = S.emit_n[0], n_init = S.emit_n[1];
     if (n_pp == 0 && n_init == 0) return;
-    stage_emit_cache(S, &ec, n_pp != 0, n_init != 0);
-    uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
-    if (n_init) build_hb_template(S, hb_tmpl, now_unix, start_unix);
-    uint8_t* buf = reinterpret_cast<uint8_t*>(pbuf4) + wave_id() * PATCH_BUF;
+    stage_emit(S, &L, n_pp != 0, n_init != 0, now_unix, start_unix);
     const uint32_t w0 = blockIdx.x * (EMIT_BLOCK / 64) + wave_id(), nw = gridDim.x * (EMIT_BLOCK / 64);
-    if (ec.blob_ok) emit_chunks<false, true>(S, &ec, hb_tmpl, buf, w0, nw, n_init);
-    else emit_chunks<false, false>(S, &ec, hb_tmpl, buf, w0, nw, n_init);
-    if (ec.n_desc) emit_chunks<true, true>(S, &ec, hb_tmpl, buf, w0, nw, n_pp);
-    else emit_chunks<true, false>(S, &ec, hb_tmpl, buf, w0, nw, n_pp);
+    if (n_init) {
+        if (L.blob_ok) emit_jobs<false, true>(S, &L, w0, nw, n_init);
+        else emit_jobs<false, false>(S, &L, w0, nw, n_init);
+    }
+    if (n_pp) {
+        if (L.spec_ok) emit_jobs<true, true>(S, &L, w0, nw, n_pp);
+        else emit_jobs<true, false>(S, &L, w0, nw, n_pp);
+    }
 }
 
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st) {

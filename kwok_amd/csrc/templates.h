@@ -32,12 +32,17 @@ struct Container {
 SpecProgram build_spec_program(const std::vector<Container>& containers, const std::vector<Container>& init,
                                const std::vector<std::string>& gates);
 
-// node init blob: pre = "addresses":..,"allocatable":..,"capacity":..  post = "nodeInfo":{..},"phase":"Running"
+// node init blob, framed so the init patch is pre + conditions + post:
+//   pre  = {"status":{"addresses":..,"allocatable":..,"capacity":..,"conditions":
+//   post = ,"nodeInfo":{..},"phase":"Running"}}
 struct NodeBlob {
     std::string pre, post;
 };
 NodeBlob build_node_blob(const std::string& addresses_json, const std::string& allocatable_json,
                          const std::string& capacity_json, const std::string info[10], const std::string& node_ip);
+
+// k_emit's timestamp-slot lookup of a spec (false: layout outside what it handles)
+bool build_ts_lookup(const SpecProgram& p, std::vector<uint16_t>& out);
 
 // domain checks (DESIGN.md "Supported domain")
 bool safe_string(const char* s, size_t n);

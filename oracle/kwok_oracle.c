@@ -94,27 +94,85 @@ static void ip_str(uint32_t ip, char out[16]) {
     snprintf(out, 16, "%u.%u.%u.%u", ip >> 24, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255);
 }
 
-/* net.ParseIP for canonical dotted quads; returns 0 on failure / empty */
+/* net.ParseIP (Go 1.19) of a dotted quad: four decimal fields 0..255 split by
+ * single dots, no leading zeros (rejected since Go 1.17), nothing else.
+ * Returns 0 on failure / empty.  IPv6 forms are outside the supported domain. */
 static int ip_parse(const char* s, size_t n, uint32_t* out) {
-    if (n == 0 || n > 15) return 0;
     uint32_t v = 0;
-    int parts = 0;
     size_t i = 0;
-    while (i < n) {
-        uint32_t x = 0;
-        size_t j = i;
-        while (j < n && s[j] >= '0' && s[j] <= '9') x = x * 10 + (uint32_t)(s[j++] - '0');
-        if (j == i || j - i > 3 || x > 255) return 0;
-        v = (v << 8) | x;
-        parts++;
-        if (j < n) {
-            if (s[j] != '.') return 0;
-            j++;
+    for (int field = 0; field < 4; field++) {
+        if (field) {
+            if (i >= n || s[i] != '.') return 0;
+            i++;
         }
-        i = j;
+        size_t d = 0;
+        uint32_t x = 0;
+        while (i + d < n && s[i + d] >= '0' && s[i + d] <= '9' && d < 4) x = x * 10 + (uint32_t)(s[i + d++] - '0');
+        if (d == 0 || d > 3 || x > 255 || (d > 1 && s[i] == '0')) return 0;
+        v = v << 8 | x;
+        i += d;
     }
-    if (parts != 4) return 0;
+    if (i != n) return 0;
     *out = v;
+    return 1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* supported input domain: the engine rejects what it cannot   */
+/* emit verbatim, and so does this oracle (KWOK_EDOMAIN)                     */
+/* ------------------------------------------------------------------------- */
+/* Does `v`, rendered as `key: {{ . }}` into the template's YAML, come back out
+ * of sigs.k8s.io/yaml (over gopkg.in/yaml.v2 v2.4.0 resolve.go, [ext]) as the
+ * same JSON string?  One plain scalar: alnum first, [A-Za-z0-9._/:@+-] and
+ * spaces, no ": ", no trailing ':' / space.  Resolves to !!str: not a bool/null
+ * spelling of resolveMap; a digit-led value, '_' removed, is neither an integer
+ * literal (0x / 0o / 0b / decimal digits: ParseInt/ParseUint base 0) nor a
+ * yamlStyleFloat (out-of-range literals are rejected as well). */
+static int yaml_plain_string(const char* v, size_t n) {
+    static const char* const resolve_map[] = {"y", "Y", "yes", "Yes", "YES", "true", "True", "TRUE", "on", "On", "ON",
+                                              "n", "N", "no", "No", "NO", "false", "False", "FALSE", "off", "Off", "OFF",
+                                              "null", "Null", "NULL"};
+    if (n < 1 || n > 253) return 0;
+    for (size_t i = 0; i < n; i++) {
+        char c = v[i];
+        int ok = (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c && strchr("._/:@+- ", c));
+        if (!ok) return 0;
+        if (i == 0 && !((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'))) return 0;
+        if (c == ':' && (i + 1 == n || v[i + 1] == ' ')) return 0;
+    }
+    if (v[n - 1] == ' ') return 0;
+    for (size_t k = 0; k < sizeof(resolve_map) / sizeof(resolve_map[0]); k++)
+        if (strlen(resolve_map[k]) == n && memcmp(resolve_map[k], v, n) == 0) return 0;
+    if (v[0] < '0' || v[0] > '9') return 1;
+    char p[256];
+    size_t m = 0;
+    for (size_t i = 0; i < n; i++)
+        if (v[i] != '_') p[m++] = v[i];
+    p[m] = 0;
+    /* integer literals */
+    const char* digits = "0123456789";
+    size_t from = 0;
+    if (m > 2 && p[0] == '0' && (p[1] == 'x' || p[1] == 'X')) digits = "0123456789abcdefABCDEF", from = 2;
+    else if (m > 2 && p[0] == '0' && (p[1] == 'o' || p[1] == 'O')) digits = "01234567", from = 2;
+    else if (m > 2 && p[0] == '0' && (p[1] == 'b' || p[1] == 'B')) digits = "01", from = 2;
+    if (from < m && strspn(p + from, digits) == m - from) return 0;
+    /* yamlStyleFloat, digit-led: [0-9]+(\.[0-9]*)?([eE][-+]?[0-9]+)? */
+    size_t i = strspn(p, "0123456789");
+    if (p[i] == '.') i += 1 + strspn(p + i + 1, "0123456789");
+    if (p[i] == 'e' || p[i] == 'E') {
+        size_t j = i + 1 + (p[i + 1] == '+' || p[i + 1] == '-');
+        size_t d = strspn(p + j, "0123456789");
+        if (d) i = j + d;
+    }
+    return p[i] != 0; /* the whole value matched: a float */
+}
+
+/* status.addresses / allocatable / capacity as compact JSON (json.Marshal of
+ * the object): a list / an object without control characters */
+static int json_blob_ok(const char* s, size_t n, char open) {
+    if (n < 2 || s[0] != open || s[n - 1] != (open == '[' ? ']' : '}')) return 0;
+    for (size_t i = 0; i < n; i++)
+        if ((unsigned char)s[i] < 0x20) return 0;
     return 1;
 }
 
@@ -409,7 +467,15 @@ static int streq(const char* a, const char* b) { return strcmp(a ? a : "", b ? b
 
 int kwok_oracle_register_pod_spec(kwok_oracle* o, const kwok_pod_spec* s, const char* arena, size_t arena_len,
                                   int32_t* out_id) {
-    (void)arena_len;
+    /* every value pod.status.tpl renders with {{ . }} must stay a string */
+#define SAFE(ks) ((size_t)(ks).off + (ks).len <= arena_len && yaml_plain_string(arena + (ks).off, (ks).len))
+    for (uint32_t i = 0; i < s->n_containers; i++)
+        if (!SAFE(s->containers[i].name) || !SAFE(s->containers[i].image)) return KWOK_EDOMAIN;
+    for (uint32_t i = 0; i < s->n_init_containers; i++)
+        if (!SAFE(s->init_containers[i].name) || !SAFE(s->init_containers[i].image)) return KWOK_EDOMAIN;
+    for (uint32_t i = 0; i < s->n_readiness_gates; i++)
+        if (!SAFE(s->readiness_gates[i])) return KWOK_EDOMAIN;
+#undef SAFE
     ospec_t sp = {0};
     sp.nc = s->n_containers;
     sp.ni = s->n_init_containers;
@@ -522,7 +588,16 @@ int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n
                 node_maybe_free(o, h);
             }
         } else {
-            h = node_entry(o, name, e->name.len, &st);
+            /* node.status.tpl renders nodeInfo values with {{ . }} and echoes the
+             * JSON of addresses / allocatable / capacity */
+            for (int k = 0; k < KWOK_NI_COUNT && st == KWOK_OK; k++)
+                if (e->node_info[k].len && !yaml_plain_string(arena + e->node_info[k].off, e->node_info[k].len))
+                    st = KWOK_EDOMAIN;
+            const kwok_str* blobs[3] = {&e->addresses, &e->allocatable, &e->capacity};
+            for (int k = 0; k < 3 && st == KWOK_OK; k++)
+                if (blobs[k]->len && !json_blob_ok(arena + blobs[k]->off, blobs[k]->len, k == 0 ? '[' : '{'))
+                    st = KWOK_EDOMAIN;
+            if (st == KWOK_OK) h = node_entry(o, name, e->name.len, &st);
             if (h >= 0) {
                 onode_t* nd = &o->nodes[h];
                 free_node_status(nd);
@@ -558,7 +633,9 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
         int32_t h = e->handle;
         if (out_released) out_released[i] = 0;
         if (e->op == KWOK_OP_DELETE) {
-            if (h < 0 || (uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
+            if (h < 0) {
+                st = KWOK_EINVAL; /* a Deleted event names an object the caller ingested */
+            } else if ((uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
                 st = KWOK_ENOTFOUND;
             } else {
                 opod_t* p = &o->pods[h];
@@ -576,10 +653,27 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
             }
         } else {
             opod_t* p;
-            if (h < 0) {
+            uint32_t hip = 0, pip = 0;
+            if (h >= 0 && ((uint32_t)h >= o->B * o->cp || !o->pods[h].used)) {
+                st = KWOK_ENOTFOUND;
+                h = -1;
+            } else if ((e->host_ip.len && (!ip_parse(arena + e->host_ip.off, e->host_ip.len, &hip) || !hip)) ||
+                       (e->pod_ip.len && (!ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &pip) || !pip))) {
+                st = KWOK_EDOMAIN; /* IPv4 dotted quads only */
+                h = -1;
+            } else if (e->spec_id < 0 || (uint32_t)e->spec_id >= o->n_specs || e->phase > KWOK_PHASE_UNKNOWN) {
+                st = KWOK_EINVAL;
+                h = -1;
+            } else if (e->creation_unix < 0 || e->creation_unix > 0xFFFFFFFFll) {
+                st = KWOK_EDOMAIN; /* creationTimestamp between 1970 and 2106 */
+                h = -1;
+            } else if (h < 0) {
                 int32_t nh;
-                if (e->node_handle >= 0) nh = e->node_handle;
-                else if (e->node_name.len == 0 || e->node_name.len > 253) nh = -1, st = KWOK_EDOMAIN;
+                if (e->node_handle >= 0) {
+                    nh = e->node_handle;
+                    if ((uint32_t)nh < o->b_lo * o->cn || (uint32_t)nh >= o->b_hi * o->cn) nh = -1, st = KWOK_ENOTMINE;
+                    else if (!o->nodes[nh].used) nh = -1, st = KWOK_ENOTFOUND;
+                } else if (e->node_name.len == 0 || e->node_name.len > 253) nh = -1, st = KWOK_EDOMAIN;
                 else nh = node_entry(o, arena + e->node_name.off, e->node_name.len, &st);
                 if (nh >= 0) {
                     uint32_t b = (uint32_t)nh / o->cn;
@@ -589,17 +683,16 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                             h = (int32_t)(b * o->cp + k);
                             break;
                         }
-                    if (h < 0) st = KWOK_EFULL;
-                    else {
+                    if (h < 0) {
+                        st = KWOK_EFULL;
+                        node_maybe_free(o, nh);
+                    } else {
                         memset(&o->pods[h], 0, sizeof(opod_t));
                         o->pods[h].used = 1;
                         o->pods[h].node = nh;
                         o->nodes[nh].refs++;
                     }
                 }
-            } else if ((uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
-                st = KWOK_ENOTFOUND;
-                h = -1;
             }
             if (h >= 0) {
                 p = &o->pods[h];
@@ -611,9 +704,8 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                 p->phase = e->phase;
                 p->spec = e->spec_id;
                 p->creation = e->creation_unix;
-                p->host_ip = p->pod_ip = 0;
-                ip_parse(arena + e->host_ip.off, e->host_ip.len, &p->host_ip);
-                ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &p->pod_ip);
+                p->host_ip = hip;
+                p->pod_ip = pip;
                 int managed = o->nodes[p->node].managed;
                 if (p->deleting) {
                     if (managed) p->delete_pending = 1; /* pod_controller.go:306-308 */

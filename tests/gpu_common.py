@@ -1,0 +1,178 @@
+"""Shared helpers of the GPU parity tests: the HIP engine and the CPU oracle
+driven with the same event batches, compared output by output (handles, patch
+bytes, deletes, counters) and on the full pod state."""
+import numpy as np
+
+from kwok_amd import abi
+from kwok_amd.engine import Engine, make_config
+from oracle.oracle import Oracle
+
+
+def compare(e_out, o_out, where):
+    assert list(e_out.heartbeat_nodes) == list(o_out.heartbeat_nodes), where + " heartbeat handles"
+    n = len(e_out.heartbeat_nodes)
+    if n:
+        hb = o_out.heartbeat_body(0)
+        a = np.frombuffer(e_out.arena, np.uint8)[e_out.heartbeat_off:e_out.heartbeat_off + n * e_out.heartbeat_stride]
+        a = a.reshape(n, e_out.heartbeat_stride)[:, :e_out.heartbeat_len]
+        assert (a == np.frombuffer(hb, np.uint8)[None, :]).all(), where + " heartbeat bytes"
+        ob = np.frombuffer(o_out.arena, np.uint8)[o_out.heartbeat_off:o_out.heartbeat_off + n * len(hb)]
+        assert (ob.reshape(n, len(hb)) == np.frombuffer(hb, np.uint8)[None, :]).all()
+    assert [h for h, _ in e_out.node_inits] == [h for h, _ in o_out.node_inits], where + " node-init handles"
+    assert [b for _, b in e_out.node_inits] == [b for _, b in o_out.node_inits], where + " node-init bytes"
+    assert [h for h, _ in e_out.pod_patches] == [h for h, _ in o_out.pod_patches], where + " pod-patch handles"
+    bad = [h for (h, b), (_, c) in zip(e_out.pod_patches, o_out.pod_patches) if b != c]
+    assert not bad, where + " pod-patch bytes differ for %d pods, first %d" % (len(bad), bad[0])
+    assert e_out.deletes == o_out.deletes, where + " deletes"
+    assert e_out.counters == o_out.counters, where + " counters"
+
+
+def compare_state(e, o, n_slots, where):
+    eu, ep, eh, ei = e.dump_pods(0, n_slots)
+    ou, op, oh, oi = o.dump_pods(0, n_slots)
+    assert (eu == ou).all(), where + " pod slots"
+    assert (ep == op).all(), where + " phases"
+    assert (eh == oh).all(), where + " hostIPs"
+    assert (ei == oi).all(), where + " podIPs"
+
+
+class Driver:
+    """Applies the same random event batches to engine and oracle."""
+
+    DEFAULT_SPECS = [([("fake-pod", "fake")], [], []),
+                     ([("a", "img-a"), ("b", "img/b:v2")], [("init", "busybox")], ["g.io/x"])]
+
+    def __init__(self, cfg_kw, seed, specs=None):
+        self.e = Engine(make_config(**cfg_kw))
+        self.o = Oracle(make_config(**cfg_kw))
+        self.rng = np.random.default_rng(seed)
+        self.cfg = cfg_kw
+        self.spec = [self.e.register_pod_spec(*sp) for sp in (specs or self.DEFAULT_SPECS)]
+        assert self.spec == [self.o.register_pod_spec(*sp) for sp in (specs or self.DEFAULT_SPECS)]
+        self.n_slots = cfg_kw["buckets"] * cfg_kw["pod_slots_per_bucket"]
+        self.spec_of = np.zeros(self.n_slots, np.int32)   # immutable pod fields, by handle
+        self.ctime_of = np.zeros(self.n_slots, np.int64)
+        self.now = 1704067230
+
+    def nodes(self, names, managed, lockable, op=abi.OP_UPSERT, phase=abi.PHASE_NONE, status=None):
+        """status: optional per-node dicts {addresses, allocatable, capacity (JSON
+        strings), nodeInfo {key: value}} as the codec would decode them"""
+        ar = abi.Arena()
+        ev = np.zeros(len(names), abi.NODE_EVENT_DTYPE)
+        ev["op"] = op
+        ev["managed"] = managed
+        ev["lockable"] = lockable
+        ev["phase"] = phase
+        for i, n in enumerate(names):
+            ev[i]["name"] = ar.ref(n)
+            if status is not None and status[i]:
+                st = status[i]
+                for f in ("addresses", "allocatable", "capacity"):
+                    ev[i][f] = ar.ref(st.get(f, ""))
+                for k, key in enumerate(abi.NODEINFO_KEYS):
+                    ev[i]["node_info"][k] = ar.ref(st.get("nodeInfo", {}).get(key, ""))
+        a = bytes(ar.buf)
+        h1, s1 = self.e.ingest_nodes_raw(ev, a)
+        h2, s2 = self.o.ingest_nodes_raw(ev, a)
+        assert (h1 == h2).all() and (s1 == s2).all()
+        return h1, s1
+
+    def pods(self, ev, arena=b""):
+        h1, s1, r1 = self.e.ingest_pods_raw(ev, arena)
+        h2, s2, r2 = self.o.ingest_pods_raw(ev, arena)
+        assert (h1 == h2).all() and (s1 == s2).all() and (r1 == r2).all()
+        new = (ev["op"] == abi.OP_UPSERT) & (ev["handle"] < 0) & (s1 == 0)
+        self.spec_of[h1[new]] = ev["spec_id"][new]
+        self.ctime_of[h1[new]] = ev["creation_unix"][new]
+        return h1, s1, r1
+
+    def tick(self, where):
+        eo, oo = self.e.tick(self.now), self.o.tick(self.now)
+        self.now += 30
+        compare(eo, oo, where)
+        compare_state(self.e, self.o, self.n_slots, where)
+        return eo
+
+    def tick_pair(self, where):
+        """two ticks queued back to back on the engine, one after the other on the oracle"""
+        self.e.tick_submit(self.now)
+        self.e.tick_submit(self.now + 30)
+        for k in range(2):
+            eo, oo = self.e.tick_collect(), self.o.tick(self.now)
+            self.now += 30
+            compare(eo, oo, "%s (queued %d)" % (where, k))
+        compare_state(self.e, self.o, self.n_slots, where)
+
+    def live(self):
+        used, phase, hip, pip = self.o.dump_pods(0, self.n_slots)
+        idx = np.nonzero(used)[0]
+        return idx, phase[idx], hip[idx], pip[idx]
+
+
+def new_pods(rng, node_handles, n, spec_ids, with_ip_frac=0.0, ip_range=None, host_ips=(), host_ip_frac=0.0,
+             years=0):
+    """Pending / empty-status pods on random nodes; optionally with existing
+    podIPs from ip_range, existing hostIPs drawn from host_ips, and creation
+    times spread over `years` years (timestamp formatting)."""
+    ev = np.zeros(n, abi.POD_EVENT_DTYPE)
+    ev["op"] = abi.OP_UPSERT
+    ev["handle"] = -1
+    ev["node_handle"] = rng.choice(node_handles, n)
+    ev["spec_id"] = rng.choice(spec_ids, n)
+    ev["creation_unix"] = 1704067200 - rng.integers(0, max(10 ** 6, years * 31_557_600), n)
+    ph = rng.choice([abi.PHASE_PENDING, abi.PHASE_PENDING, abi.PHASE_NONE], n)
+    ev["phase"] = ph
+    fl = np.where(ph == abi.PHASE_PENDING, abi.POD_STATUS_NONEMPTY, 0)
+    fl |= np.where(rng.random(n) < 0.3, abi.POD_HAS_FINALIZERS, 0)
+    fl |= np.where(rng.random(n) < 0.03, abi.POD_DISREGARD, 0)
+    ev["flags"] = fl
+    arena = b""
+    if (with_ip_frac and ip_range) or (host_ip_frac and host_ips):
+        ar = abi.Arena()
+        if with_ip_frac and ip_range:
+            lo, hi = ip_range
+            for i in np.nonzero(rng.random(n) < with_ip_frac)[0]:
+                ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(rng.integers(lo, hi))))
+                ev[i]["flags"] |= abi.POD_STATUS_NONEMPTY
+        if host_ip_frac and host_ips:
+            for i in np.nonzero(rng.random(n) < host_ip_frac)[0]:
+                ev[i]["host_ip"] = ar.ref(host_ips[int(rng.integers(0, len(host_ips)))])
+                ev[i]["flags"] |= abi.POD_STATUS_NONEMPTY
+        arena = bytes(ar.buf)
+    return ev, arena
+
+
+def mark_deleting(rng, d, handles):
+    """Modified events with a deletionTimestamp for existing pods (state kept)."""
+    idx, phase, hip, pip = d.live()
+    pos = np.searchsorted(idx, handles)
+    ar = abi.Arena()
+    ev = np.zeros(len(handles), abi.POD_EVENT_DTYPE)
+    ev["op"] = abi.OP_UPSERT
+    ev["handle"] = handles
+    ev["node_handle"] = -1
+    ev["spec_id"] = d.spec_of[handles]
+    ev["phase"] = phase[pos]
+    ev["creation_unix"] = d.ctime_of[handles]
+    fl = abi.POD_DELETING | np.where(rng.random(len(handles)) < 0.5, abi.POD_HAS_FINALIZERS, 0)
+    fl |= np.where(phase[pos] == abi.PHASE_RUNNING, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
+    ev["flags"] = fl
+    for i in range(len(handles)):
+        if hip[pos[i]]:
+            ev[i]["host_ip"] = ar.ref(abi.ip4s(int(hip[pos[i]])))
+        if pip[pos[i]]:
+            ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[pos[i]])))
+    return ev, bytes(ar.buf)
+
+
+def external_deletes(d, handles):
+    idx, phase, hip, pip = d.live()
+    pos = np.searchsorted(idx, handles)
+    ar = abi.Arena()
+    ev = np.zeros(len(handles), abi.POD_EVENT_DTYPE)
+    ev["op"] = abi.OP_DELETE
+    ev["handle"] = handles
+    for i in range(len(handles)):
+        if pip[pos[i]]:
+            ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[pos[i]])))
+    return ev, bytes(ar.buf)

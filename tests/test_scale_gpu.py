@@ -8,39 +8,12 @@ import ipaddress
 import numpy as np
 import pytest
 
+from gpu_common import Driver, compare, compare_state, external_deletes, mark_deleting, new_pods
 from kwok_amd import abi, workload
 from kwok_amd.engine import Engine, make_config
 from oracle.oracle import Oracle
 
 pytestmark = pytest.mark.gpu
-
-
-def compare(e_out, o_out, where):
-    assert list(e_out.heartbeat_nodes) == list(o_out.heartbeat_nodes), where + " heartbeat handles"
-    n = len(e_out.heartbeat_nodes)
-    if n:
-        hb = o_out.heartbeat_body(0)
-        a = np.frombuffer(e_out.arena, np.uint8)[e_out.heartbeat_off:e_out.heartbeat_off + n * e_out.heartbeat_stride]
-        a = a.reshape(n, e_out.heartbeat_stride)[:, :e_out.heartbeat_len]
-        assert (a == np.frombuffer(hb, np.uint8)[None, :]).all(), where + " heartbeat bytes"
-        ob = np.frombuffer(o_out.arena, np.uint8)[o_out.heartbeat_off:o_out.heartbeat_off + n * len(hb)]
-        assert (ob.reshape(n, len(hb)) == np.frombuffer(hb, np.uint8)[None, :]).all()
-    assert [h for h, _ in e_out.node_inits] == [h for h, _ in o_out.node_inits], where + " node-init handles"
-    assert [b for _, b in e_out.node_inits] == [b for _, b in o_out.node_inits], where + " node-init bytes"
-    assert [h for h, _ in e_out.pod_patches] == [h for h, _ in o_out.pod_patches], where + " pod-patch handles"
-    bad = [h for (h, b), (_, c) in zip(e_out.pod_patches, o_out.pod_patches) if b != c]
-    assert not bad, where + " pod-patch bytes differ for %d pods, first %d" % (len(bad), bad[0])
-    assert e_out.deletes == o_out.deletes, where + " deletes"
-    assert e_out.counters == o_out.counters, where + " counters"
-
-
-def compare_state(e, o, n_slots, where):
-    eu, ep, eh, ei = e.dump_pods(0, n_slots)
-    ou, op, oh, oi = o.dump_pods(0, n_slots)
-    assert (eu == ou).all(), where + " pod slots"
-    assert (ep == op).all(), where + " phases"
-    assert (eh == oh).all(), where + " hostIPs"
-    assert (ei == oi).all(), where + " podIPs"
 
 
 def test_c2_full_parity_and_properties():
@@ -75,131 +48,6 @@ def test_c2_full_parity_and_properties():
     compare_state(e, o, n_slots, "c2")
     e.close()
     o.close()
-
-
-class Driver:
-    """Applies the same random event batches to engine and oracle."""
-
-    def __init__(self, cfg_kw, seed):
-        self.e = Engine(make_config(**cfg_kw))
-        self.o = Oracle(make_config(**cfg_kw))
-        self.rng = np.random.default_rng(seed)
-        self.cfg = cfg_kw
-        self.spec = [self.e.register_pod_spec([("fake-pod", "fake")]),
-                     self.e.register_pod_spec([("a", "img-a"), ("b", "img/b:v2")], [("init", "busybox")], ["g.io/x"])]
-        assert self.spec == [self.o.register_pod_spec([("fake-pod", "fake")]),
-                             self.o.register_pod_spec([("a", "img-a"), ("b", "img/b:v2")], [("init", "busybox")],
-                                                      ["g.io/x"])]
-        self.n_slots = cfg_kw["buckets"] * cfg_kw["pod_slots_per_bucket"]
-        self.spec_of = np.zeros(self.n_slots, np.int32)   # immutable pod fields, by handle
-        self.ctime_of = np.zeros(self.n_slots, np.int64)
-        self.now = 1704067230
-
-    def nodes(self, names, managed, lockable, op=abi.OP_UPSERT, phase=abi.PHASE_NONE):
-        ar = abi.Arena()
-        ev = np.zeros(len(names), abi.NODE_EVENT_DTYPE)
-        ev["op"] = op
-        ev["managed"] = managed
-        ev["lockable"] = lockable
-        ev["phase"] = phase
-        for i, n in enumerate(names):
-            ev[i]["name"] = ar.ref(n)
-        a = bytes(ar.buf)
-        h1, s1 = self.e.ingest_nodes_raw(ev, a)
-        h2, s2 = self.o.ingest_nodes_raw(ev, a)
-        assert (h1 == h2).all() and (s1 == s2).all()
-        return h1, s1
-
-    def pods(self, ev, arena=b""):
-        h1, s1, r1 = self.e.ingest_pods_raw(ev, arena)
-        h2, s2, r2 = self.o.ingest_pods_raw(ev, arena)
-        assert (h1 == h2).all() and (s1 == s2).all() and (r1 == r2).all()
-        new = (ev["op"] == abi.OP_UPSERT) & (ev["handle"] < 0) & (s1 == 0)
-        self.spec_of[h1[new]] = ev["spec_id"][new]
-        self.ctime_of[h1[new]] = ev["creation_unix"][new]
-        return h1, s1, r1
-
-    def tick(self, where):
-        eo, oo = self.e.tick(self.now), self.o.tick(self.now)
-        self.now += 30
-        compare(eo, oo, where)
-        compare_state(self.e, self.o, self.n_slots, where)
-        return eo
-
-    def tick_pair(self, where):
-        """two ticks queued back to back on the engine, one after the other on the oracle"""
-        self.e.tick_submit(self.now)
-        self.e.tick_submit(self.now + 30)
-        for k in range(2):
-            eo, oo = self.e.tick_collect(), self.o.tick(self.now)
-            self.now += 30
-            compare(eo, oo, "%s (queued %d)" % (where, k))
-        compare_state(self.e, self.o, self.n_slots, where)
-
-    def live(self):
-        used, phase, hip, pip = self.o.dump_pods(0, self.n_slots)
-        idx = np.nonzero(used)[0]
-        return idx, phase[idx], hip[idx], pip[idx]
-
-
-def new_pods(rng, node_handles, n, spec_ids, with_ip_frac=0.0, ip_range=None):
-    ev = np.zeros(n, abi.POD_EVENT_DTYPE)
-    ev["op"] = abi.OP_UPSERT
-    ev["handle"] = -1
-    ev["node_handle"] = rng.choice(node_handles, n)
-    ev["spec_id"] = rng.choice(spec_ids, n)
-    ev["creation_unix"] = 1704067200 - rng.integers(0, 10 ** 6, n)
-    ph = rng.choice([abi.PHASE_PENDING, abi.PHASE_PENDING, abi.PHASE_NONE], n)
-    ev["phase"] = ph
-    fl = np.where(ph == abi.PHASE_PENDING, abi.POD_STATUS_NONEMPTY, 0)
-    fl |= np.where(rng.random(n) < 0.3, abi.POD_HAS_FINALIZERS, 0)
-    fl |= np.where(rng.random(n) < 0.03, abi.POD_DISREGARD, 0)
-    ev["flags"] = fl
-    arena = b""
-    if with_ip_frac and ip_range:
-        ar = abi.Arena()
-        lo, hi = ip_range
-        for i in np.nonzero(rng.random(n) < with_ip_frac)[0]:
-            ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(rng.integers(lo, hi))))
-            ev[i]["flags"] |= abi.POD_STATUS_NONEMPTY
-        arena = bytes(ar.buf)
-    return ev, arena
-
-
-def mark_deleting(rng, d, handles):
-    """Modified events with a deletionTimestamp for existing pods (state kept)."""
-    idx, phase, hip, pip = d.live()
-    pos = np.searchsorted(idx, handles)
-    ar = abi.Arena()
-    ev = np.zeros(len(handles), abi.POD_EVENT_DTYPE)
-    ev["op"] = abi.OP_UPSERT
-    ev["handle"] = handles
-    ev["node_handle"] = -1
-    ev["spec_id"] = d.spec_of[handles]
-    ev["phase"] = phase[pos]
-    ev["creation_unix"] = d.ctime_of[handles]
-    fl = abi.POD_DELETING | np.where(rng.random(len(handles)) < 0.5, abi.POD_HAS_FINALIZERS, 0)
-    fl |= np.where(phase[pos] == abi.PHASE_RUNNING, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
-    ev["flags"] = fl
-    for i in range(len(handles)):
-        if hip[pos[i]]:
-            ev[i]["host_ip"] = ar.ref(abi.ip4s(int(hip[pos[i]])))
-        if pip[pos[i]]:
-            ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[pos[i]])))
-    return ev, bytes(ar.buf)
-
-
-def external_deletes(d, handles):
-    idx, phase, hip, pip = d.live()
-    pos = np.searchsorted(idx, handles)
-    ar = abi.Arena()
-    ev = np.zeros(len(handles), abi.POD_EVENT_DTYPE)
-    ev["op"] = abi.OP_DELETE
-    ev["handle"] = handles
-    for i in range(len(handles)):
-        if pip[pos[i]]:
-            ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[pos[i]])))
-    return ev, bytes(ar.buf)
 
 
 @pytest.mark.parametrize("seed,cidr", [(1, "10.0.0.1/16"), (2, "10.0.0.1/20"), (3, "172.16.3.9/22")])
@@ -269,31 +117,23 @@ def test_partial_management_flap_parity():
     d.o.close()
 
 
+def test_domain_table_engine():
+    """The engine accepts / rejects exactly the domain table the oracle does
+    (tests/domain_cases.py, tests/test_domain.py): yaml.v2-typed strings, IPv4
+    dotted quads as Go 1.19 parses them."""
+    from test_domain import KW, check_backend
+    check_backend(lambda: Engine(make_config(**KW)))
+
+
 def test_domain_rejections():
-    """Values outside the supported domain are rejected, never emulated:
-    YAML-typed strings (yaml.v2 would turn `y` / `1.5` / `null` into bool /
-    float / null), IPv6 / non-canonical IPs, custom templates, EnableCNI."""
-    e = Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8))
-    for bad in ("y", "on", "null", "1.5", "0x1F", "-x", "a b", ""):
-        with pytest.raises(Exception):
-            e.register_pod_spec([("c", bad)])
-    e.register_pod_spec([("c", "nginx:1.25")])
-    ar = abi.Arena()
-    ev = np.zeros(2, abi.POD_EVENT_DTYPE)
-    ev["op"] = abi.OP_UPSERT
-    ev["handle"] = -1
-    ev["node_handle"] = -1
-    ev[0]["node_name"] = ar.ref("n")
-    ev[1]["node_name"] = ar.ref("n")
-    ev[0]["pod_ip"] = ar.ref("010.0.0.1")
-    ev[1]["pod_ip"] = ar.ref("fe80::1")
-    _, st, _ = e.ingest_pods_raw(ev, bytes(ar.buf))
-    assert list(st) == [abi.EDOMAIN, abi.EDOMAIN]
-    e.close()
-    for kw in (dict(cidr="fe80::1/64"), dict(cidr="10.0.0.1/4")):
+    """Configurations outside the supported domain are rejected, never
+    emulated: IPv6 / non-canonical CIDRs, prefixes shorter than /8, custom
+    templates, EnableCNI."""
+    for kw in (dict(cidr="fe80::1/64"), dict(cidr="10.0.0.1/4"), dict(cidr="010.0.0.1/8")):
         with pytest.raises(Exception):
             Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, **kw))
-    cfg = make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8)
-    cfg.custom_templates = 1
-    with pytest.raises(Exception):
-        Engine(cfg)
+    for field in ("custom_templates", "enable_cni"):
+        cfg = make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8)
+        setattr(cfg, field, 1)
+        with pytest.raises(Exception):
+            Engine(cfg)
