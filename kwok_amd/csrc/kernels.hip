@@ -31,7 +31,7 @@ namespace kwok {
 // small device helpers
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }  // uniform
 
 // wave-wide inclusive scan (64 lanes) with DPP row shifts and row broadcasts:
 // six VALU adds with a cross-lane source operand, no LDS round trip (a
@@ -1810,25 +1810,25 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
 // ---------------------------------------------------------------------------
 constexpr int EMIT_BLOCK = 256;
 static_assert(EMIT_BLOCK == BLOCK, "build_hb_template strides by BLOCK");
-constexpr int EC_DESC = 64, EC_PROG = 4096, EC_NXT = 1280, EC_BLOB = 2048;
+constexpr int EC_PROG = 4096, EC_NXT = 1152, EC_BLOB = 2048;
 constexpr uint32_t SEG_STRIDE = 56;  // per job: "hostIP":"H", (28 bytes) | "podIP":"P", (28 bytes)
 constexpr uint32_t TS_STRIDE = 36;   // per job: its 20-byte timestamp, then 16 zero bytes
 constexpr uint32_t TS_FIRST = 16;    // 16 zero bytes before job 0's timestamp
 constexpr uint32_t TS_ZERO = TS_FIRST + 64 * TS_STRIDE;  // 20+ zero bytes (a unit with no slot)
 constexpr uint32_t TS_AREA = TS_ZERO + 32;
+constexpr uint32_t HB_LDS = 1104;    // the heartbeat template: CONDS at HB_PREFIX, read up to 32 bytes around it
+static_assert(HB_LDS >= HB_STRIDE && HB_LDS >= ((HB_PREFIX + CONDS_LEN + 15) & ~15) + 32, "heartbeat template in LDS");
 struct EmitWave {
-    uint32_t out_lo[64], out_hi[64];  // arena offset of each job's patch
-    uint32_t e12[64], e34[64];        // region starts 1..4 (u16 pairs; 0xFFFF: no such region)
-    uint32_t aux[64];                 // pods: spec id; inits: blob offset
+    uint4 rec[64];   // per job: arena offset / 16, region starts 1|2 and 3|4 (u16; 0xFFFF: none), template offset
+    uint32_t nxt[64];  // pods: the spec's timestamp lookup offset
     uint8_t seg[SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_BACK];
     uint8_t ts[TS_AREA];
 };
 struct EmitLds {
-    SpecDesc desc[EC_DESC];
     uint16_t nxt[EC_NXT];
     uint8_t prog[SRC_PAD_FRONT + EC_PROG + SRC_PAD_BACK];
     uint8_t blob[SRC_PAD_FRONT + EC_BLOB + SRC_PAD_BACK];
-    uint8_t hb[HB_STRIDE + SRC_PAD_BACK];  // the tick's heartbeat template; CONDS at HB_PREFIX
+    uint8_t hb[HB_LDS];  // the tick's heartbeat template
     uint32_t spec_ok, blob_ok;
     EmitWave w[EMIT_BLOCK / 64];
 };
@@ -1870,11 +1870,9 @@ __device__ __forceinline__ void write_seg(uint8_t* dst, Lit16 key, const IpStr& 
 __device__ __forceinline__ void stage_emit(const DevState& S, EmitLds* L, bool pods, bool nodes, uint64_t now_unix,
                                            uint64_t start_unix) {
     const uint32_t t = threadIdx.x;
-    const bool sp = pods && S.n_specs <= (uint32_t)EC_DESC && S.spec_total <= (uint32_t)EC_PROG &&
-                    S.nxt_total <= (uint32_t)EC_NXT;
+    const bool sp = pods && S.spec_total <= (uint32_t)EC_PROG && S.nxt_total <= (uint32_t)EC_NXT;
     const bool bl = nodes && S.blob_total <= (uint32_t)EC_BLOB;
     if (sp) {
-        for (uint32_t i = t; i < S.n_specs; i += BLOCK) L->desc[i] = S.specs[i];
         for (uint32_t i = t; i < S.nxt_total; i += BLOCK) L->nxt[i] = S.spec_nxt[i];
         const uint32_t* src = reinterpret_cast<const uint32_t*>(S.spec_bytes - SRC_PAD_FRONT);  // the padded array
         uint32_t* dst = reinterpret_cast<uint32_t*>(L->prog);
@@ -1887,7 +1885,7 @@ __device__ __forceinline__ void stage_emit(const DevState& S, EmitLds* L, bool p
     }
     uint32_t* z = reinterpret_cast<uint32_t*>(L->w);
     for (uint32_t i = t; i < sizeof(L->w) / 4; i += BLOCK) z[i] = 0u;
-    for (uint32_t i = HB_STRIDE + t; i < HB_STRIDE + SRC_PAD_BACK; i += BLOCK) L->hb[i] = 0;
+    for (uint32_t i = HB_STRIDE + t; i < HB_LDS; i += BLOCK) L->hb[i] = 0;
     if (t == 0) {
         L->spec_ok = sp ? 1u : 0u;
         L->blob_ok = bl ? 1u : 0u;
@@ -1897,10 +1895,10 @@ __device__ __forceinline__ void stage_emit(const DevState& S, EmitLds* L, bool p
 }
 
 // phase 1: lane l <- job q; returns its number of 16-byte units
-template <bool POD, bool CACHED>
-__device__ __forceinline__ uint32_t emit_phase1(const DevState& S, const EmitLds* L, EmitWave* W, uint32_t q, uint32_t n) {
+template <bool POD>
+__device__ __forceinline__ uint32_t emit_phase1(const DevState& S, EmitWave* W, uint32_t q, uint32_t n) {
     const uint32_t l = lane_id();
-    uint32_t nu = 0, olo = 0, ohi = 0, e12 = 0xFFFFFFFFu, e34 = 0xFFFFFFFFu, aux = 0;
+    uint32_t nu = 0, o16 = 0, e12 = 0xFFFFFFFFu, e34 = 0xFFFFFFFFu, toff = 0, nxo = 0;
     if (q < n) {
         uint64_t off;
         uint32_t len;
@@ -1908,7 +1906,9 @@ __device__ __forceinline__ uint32_t emit_phase1(const DevState& S, const EmitLds
             const uint4 j = S.pp_job[q];  // podIP (0: no status section), hostIP, creationTimestamp, spec
             off = S.pp_off[q];
             len = S.pp_len[q];
-            aux = j.w;
+            const SpecDesc sd = S.specs[j.w];
+            toff = sd.off;
+            nxo = sd.nxt_off;
             const Ts ts = format_ts(j.z);
             uint32_t* tw = reinterpret_cast<uint32_t*>(W->ts + TS_FIRST + l * TS_STRIDE);
             tw[0] = (uint32_t)ts.w0;
@@ -1917,7 +1917,6 @@ __device__ __forceinline__ uint32_t emit_phase1(const DevState& S, const EmitLds
             tw[3] = (uint32_t)(ts.w1 >> 32);
             tw[4] = (uint32_t)ts.w2;
             if (j.y != 0) {  // `{{ with .status }}`: hostIP / podIP (pod.status.tpl:44-47)
-                const SpecDesc sd = CACHED ? L->desc[j.w] : S.specs[j.w];
                 const IpStr H = format_ip(j.y), P = format_ip(j.x);
                 uint8_t* sg = W->seg + SRC_PAD_FRONT + l * SEG_STRIDE;
                 write_seg<10>(sg, lit16("\"hostIP\":\""), H);
@@ -1930,114 +1929,118 @@ __device__ __forceinline__ uint32_t emit_phase1(const DevState& S, const EmitLds
             const uint64_t b = S.init_job[q];
             off = S.init_off[q];
             len = S.init_len[q];
-            aux = (uint32_t)b;
+            toff = (uint32_t)b;
             const uint32_t pre = (uint32_t)(b >> 32) & 0xFFFFu;
             e12 = pre | (pre + (uint32_t)CONDS_LEN) << 16;
         }
-        olo = (uint32_t)off;
-        ohi = (uint32_t)(off >> 32);
+        o16 = (uint32_t)(off >> 4);
         nu = (len + 15u) >> 4;
     }
-    W->out_lo[l] = olo;
-    W->out_hi[l] = ohi;
-    W->e12[l] = e12;
-    W->e34[l] = e34;
-    W->aux[l] = aux;
+    W->rec[l] = make_uint4(o16, e12, e34, toff);
+    W->nxt[l] = nxo;
     return nu;
 }
 
-// phase 2: the units of the chunk's cnt jobs (ustart: lane j = job j's first unit)
+// phase 2: the units of the chunk's cnt jobs (ustart: lane j = job j's first unit).
+// Every region's bytes sit at (output position + delta(region)) of its source:
+//   pods:  A: tmpl          H: seg(k) - e1      B: tmpl - (e2 - e1)
+//          P: seg(k)+28 - e3                    C: tmpl - (e2 - e1) - (e4 - e3)
+//   inits: pre: blob        CONDS: hb + 24 - e1  post: blob + e1 - e2
+// (tmpl / blob: the job's template offset in the spec / blob array).
+struct EmitSrc {
+    const uint8_t* lds;
+    const uint8_t* tbase;  // template source: the LDS cache, else the global array (flat reads)
+    uint32_t o_seg, o_ts, o_tmpl;
+};
+// unit x (byte offset, a multiple of 16) of job k: its 16 bytes and arena offset
+template <bool POD, bool CACHED>
+__device__ __forceinline__ uint4 emit_unit(const DevState& S, const EmitLds* L, const EmitWave* W, const EmitSrc& E,
+                                           uint32_t k, uint32_t x, uint64_t& dst) {
+    const uint4 R = W->rec[k];
+    const uint32_t e1 = R.y & 0xFFFFu, e2 = R.y >> 16, e3 = R.z & 0xFFFFu, e4 = R.z >> 16, toff = R.w;
+    const uint32_t y = x + 15u;
+    // region deltas (see above) and starts, selected by the region bits of x and y
+    const uint32_t seg_k = E.o_seg + k * SEG_STRIDE;
+    const uint32_t d0 = E.o_tmpl + toff;
+    const uint32_t d1 = POD ? seg_k - e1 : (uint32_t)offsetof(EmitLds, hb) + HB_PREFIX - e1;
+    const uint32_t d2 = POD ? d0 - (e2 - e1) : d0 + e1 - e2;
+    const uint32_t d3 = seg_k + 28u - e3;
+    const uint32_t d4 = d2 - (e4 - e3);
+    const bool x1 = x >= e1, x2 = x >= e2, x3 = x >= e3, x4 = x >= e4;
+    const bool y1 = y >= e1, y2 = y >= e2, y3 = y >= e3, y4 = y >= e4;
+    uint32_t dx = d0, dy = d0, sy = 0;
+    dx = x1 ? d1 : dx, dx = x2 ? d2 : dx, dx = x3 ? d3 : dx, dx = x4 ? d4 : dx;
+    dy = y1 ? d1 : dy, dy = y2 ? d2 : dy, dy = y3 ? d3 : dy, dy = y4 ? d4 : dy;
+    sy = y1 ? e1 : sy, sy = y2 ? e2 : sy, sy = y3 ? e3 : sy, sy = y4 ? e4 : sy;
+    const uint32_t rx = (uint32_t)x1 + x2 + x3 + x4, ry = (uint32_t)y1 + y2 + y3 + y4;
+    const uint32_t n = rx == ry ? 16u : sy - x;  // bytes of the unit in x's region
+    // template regions: pods 0, 2, 4; inits 0, 2
+    const bool tx = POD ? !(rx & 1u) : rx != 1u, ty = POD ? !(ry & 1u) : ry != 1u;
+    const uint8_t* bx = (CACHED || !tx) ? E.lds : E.tbase;
+    const uint8_t* by = (CACHED || !ty) ? E.lds : E.tbase;
+    const uint4 v1 = ext16(bx, x + dx), v2 = ext16(by, x + dy);
+    uint32_t o[4];
+    const uint32_t vv1[4] = {v1.x, v1.y, v1.z, v1.w}, vv2[4] = {v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int c = min(max((int)n - 4 * d, 0), 4);  // bytes of dword d from x's region
+        const uint32_t m = c == 4 ? 0xFFFFFFFFu : (1u << (8 * c)) - 1u;
+        o[d] = (vv1[d] & m) | (vv2[d] & ~m);
+    }
+    if (POD) {
+        // the timestamp slot (at most one) in the unit's template region; template
+        // coordinate of output position p in a template region: p + delta - d0
+        const bool tt = tx || ty;
+        const uint32_t dT = tx ? dx : dy;
+        const uint32_t w0 = tx ? x : sy, w1 = (tx && rx != ry) ? sy : x + 16u;
+        const uint32_t tw0 = w0 + dT - d0, tw1 = w1 + dT - d0;
+        const uint32_t ni = tt ? W->nxt[k] + (tw0 >> 2) : 0u;
+        const uint32_t s = CACHED ? (uint32_t)L->nxt[ni] : (uint32_t)S.spec_nxt[ni];
+        const bool ov = tt && s < tw1 && s + (uint32_t)TS_LEN > tw0;
+        const uint32_t so = s + d0 - dT;  // output position of the slot
+        const uint4 t4 = ext16(E.lds, E.o_ts + (ov ? TS_FIRST + k * TS_STRIDE + x - so : TS_ZERO));
+        o[0] |= t4.x;
+        o[1] |= t4.y;
+        o[2] |= t4.z;
+        o[3] |= t4.w;
+    }
+    dst = ((uint64_t)R.x << 4) + x;
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// two units per lane per pass (u and u + 64): two independent LDS chains in flight
 template <bool POD, bool CACHED>
 __device__ __forceinline__ void emit_phase2(const DevState& S, const EmitLds* L, const EmitWave* W, uint32_t cnt,
                                             uint32_t ustart, uint32_t utot) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t l = lane_id();
-    const uint8_t* lds = reinterpret_cast<const uint8_t*>(L);
-    const uint32_t o_seg = (uint32_t)((const uint8_t*)W->seg - lds) + SRC_PAD_FRONT;
-    const uint32_t o_ts = (uint32_t)((const uint8_t*)W->ts - lds);
-    const uint32_t o_prog = (uint32_t)offsetof(EmitLds, prog) + SRC_PAD_FRONT;
-    const uint32_t o_blob = (uint32_t)offsetof(EmitLds, blob) + SRC_PAD_FRONT;
-    const uint32_t o_conds = (uint32_t)offsetof(EmitLds, hb) + HB_PREFIX;
-    // the template source: the LDS cache, else the global array
-    const uint8_t* tbase = CACHED ? lds : (POD ? S.spec_bytes : S.blob);
-    const uint32_t o_tmpl = CACHED ? (POD ? o_prog : o_blob) : 0u;
+    EmitSrc E;
+    E.lds = reinterpret_cast<const uint8_t*>(L);
+    E.o_seg = (uint32_t)((const uint8_t*)W->seg - E.lds) + SRC_PAD_FRONT;
+    E.o_ts = (uint32_t)((const uint8_t*)W->ts - E.lds);
+    E.tbase = CACHED ? E.lds : (POD ? S.spec_bytes : S.blob);
+    E.o_tmpl = CACHED ? (uint32_t)(POD ? offsetof(EmitLds, prog) : offsetof(EmitLds, blob)) + SRC_PAD_FRONT : 0u;
     uint32_t kcur = 0;
-    for (uint32_t u0 = 0; u0 < utot; u0 += 64u) {
-        const uint32_t u = u0 + l;
-        // the lane's job: the last job of the pass whose first unit is <= u
-        uint32_t k = kcur, sk = rdlane(ustart, kcur);
+    for (uint32_t u0 = 0; u0 < utot; u0 += 128u) {
+        // past the chunk's units a lane redoes its last unit and does not store it
+        const uint32_t ua = min(u0 + l, utot - 1u), ub = min(u0 + 64u + l, utot - 1u);
+        // each unit's job: the last job of the pass whose first unit is <= it
+        uint32_t ka = kcur, kb = kcur, sa = rdlane(ustart, kcur), sb = sa;
         for (uint32_t j = kcur + 1; j < cnt; j++) {
             const uint32_t s = rdlane(ustart, j);
-            if (s > u0 + 63u) break;
-            if (u >= s) k = j, sk = s;
+            if (s > u0 + 127u) break;
+            const bool ga = ua >= s, gb = ub >= s;
+            ka = ga ? j : ka;
+            sa = ga ? s : sa;
+            kb = gb ? j : kb;
+            sb = gb ? s : sb;
         }
-        kcur = rdlane(k, 63);
-        if (u >= utot) continue;
-        const uint32_t x = (u - sk) << 4;  // the unit's first byte in its patch
-        const uint32_t e12 = W->e12[k], e34 = W->e34[k], aux = W->aux[k];
-        const uint64_t obase = ((uint64_t)W->out_hi[k] << 32) | W->out_lo[k];
-        const uint32_t e1 = e12 & 0xFFFFu, e2 = e12 >> 16, e3 = e34 & 0xFFFFu, e4 = e34 >> 16;
-        auto region = [&](uint32_t p) {
-            return (uint32_t)(p >= e1) + (uint32_t)(p >= e2) + (uint32_t)(p >= e3) + (uint32_t)(p >= e4);
-        };
-        auto rstart = [&](uint32_t r) { return r == 0 ? 0u : r == 1 ? e1 : r == 2 ? e2 : r == 3 ? e3 : e4; };
-        const uint32_t r1 = region(x), r2 = region(x + 15u);
-        const uint32_t s1 = rstart(r1), s2 = rstart(r2);
-        const uint32_t n = r1 == r2 ? 16u : s2 - x;  // bytes of the unit in region r1
-        SpecDesc sd{};
-        if (POD) sd = CACHED ? L->desc[aux] : S.specs[aux];
-        // template coordinate of region r's first byte (pods: the A|B|C offset of a
-        // template region; inits: the blob offset of pre / post)
-        auto tstart = [&](uint32_t r) {
-            if (POD) return r == 0 ? 0u : r == 2 ? e1 : e1 + e3 - e2;
-            return r == 0 ? 0u : e1;
-        };
-        // byte source of region r at output position x (a window may start before
-        // its region: the source arrays are padded)
-        auto src = [&](uint32_t r, uint32_t s, const uint8_t*& base) -> uint32_t {
-            if (POD) {
-                if (r & 1u) {
-                    base = lds;
-                    return o_seg + k * SEG_STRIDE + (r == 3 ? 28u : 0u) + x - s;
-                }
-                base = tbase;
-                return o_tmpl + sd.off + tstart(r) + x - s;
-            }
-            if (r == 1) {
-                base = lds;
-                return o_conds + x - s;
-            }
-            base = tbase;
-            return o_tmpl + aux + tstart(r) + x - s;
-        };
-        const uint8_t *b1, *b2;
-        const uint32_t a1 = src(r1, s1, b1), a2 = src(r2, s2, b2);
-        const uint4 v1 = ext16(b1, a1), v2 = ext16(b2, a2);
-        uint32_t o[4];
-        const uint32_t vv1[4] = {v1.x, v1.y, v1.z, v1.w}, vv2[4] = {v2.x, v2.y, v2.z, v2.w};
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            const int c = min(max((int)n - 4 * d, 0), 4);  // bytes of dword d from region r1
-            const uint32_t m = c == 4 ? 0xFFFFFFFFu : (1u << (8 * c)) - 1u;
-            o[d] = (vv1[d] & m) | (vv2[d] & ~m);
-        }
-        if (POD) {
-            // the timestamp slot (at most one) inside the unit's template region
-            const uint32_t rt = (r1 & 1u) ? r2 : r1;
-            const uint32_t st = rt == r1 ? s1 : s2, tst = tstart(rt);
-            const uint32_t w0 = rt == r1 ? x : s2, w1 = rt == r2 ? x + 16u : s2;
-            const uint32_t tw0 = tst + w0 - st, tw1 = tst + w1 - st;
-            const uint32_t ni = sd.nxt_off + (tw0 >> 2);
-            const uint32_t s = (rt & 1u) ? 0xFFFFu : (uint32_t)(CACHED ? L->nxt[ni] : S.spec_nxt[ni]);
-            const bool ov = s < tw1 && s + (uint32_t)TS_LEN > tw0;
-            const uint32_t so = s - tst + st;  // output position of the slot
-            const uint4 t4 = ext16(lds, o_ts + (ov ? TS_FIRST + k * TS_STRIDE + x - so : TS_ZERO));
-            o[0] |= t4.x;
-            o[1] |= t4.y;
-            o[2] |= t4.z;
-            o[3] |= t4.w;
-        }
-        *reinterpret_cast<u32x4*>(S.arena + obase + x) = u32x4{o[0], o[1], o[2], o[3]};
+        kcur = rdlane(kb, 63);
+        uint64_t da, db;
+        const uint4 va = emit_unit<POD, CACHED>(S, L, W, E, ka, (ua - sa) << 4, da);
+        const uint4 vb = emit_unit<POD, CACHED>(S, L, W, E, kb, (ub - sb) << 4, db);
+        if (u0 + l < utot) *reinterpret_cast<u32x4*>(S.arena + da) = u32x4{va.x, va.y, va.z, va.w};
+        if (u0 + 64u + l < utot) *reinterpret_cast<u32x4*>(S.arena + db) = u32x4{vb.x, vb.y, vb.z, vb.w};
     }
 }
 
@@ -2046,7 +2049,7 @@ __device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_
     EmitWave* W = &L->w[wave_id()];
     for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
         const uint32_t cnt = min(64u, n - ch * 64u);
-        const uint32_t nu = emit_phase1<POD, CACHED>(S, L, W, ch * 64u + lane_id(), n);
+        const uint32_t nu = emit_phase1<POD>(S, W, ch * 64u + lane_id(), n);
         const uint32_t incl = wave_incl_scan(nu);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the records before phase 2 reads them
         emit_phase2<POD, CACHED>(S, L, W, cnt, incl - nu, rdlane(incl, 63));
