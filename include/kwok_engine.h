@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KWOK_ABI_VERSION 1u
+#define KWOK_ABI_VERSION 2u
 #define KWOK_COMM_ID_BYTES 128u
 
 /* ---- status codes (int return values; per-record codes in out_status) ---- */
@@ -188,11 +188,22 @@ typedef struct kwok_tick_result {
     uint32_t n_node_init;
     uint32_t n_pod_patch;
     uint32_t n_delete;
-    uint32_t reserved0;
+    uint32_t heartbeat_epoch;   /* changes whenever the heartbeat handle list changes (the
+                                   managed set, node_controller.go:259-269); a caller that
+                                   kept the list of an earlier tick with the same epoch
+                                   need not read it again */
     uint64_t arena_bytes;       /* bytes of the output arena in use */
     uint64_t counters[KWOK_COUNTER_COUNT];       /* fleet-wide (all ranks) */
     uint64_t local_counters[KWOK_COUNTER_COUNT]; /* this rank */
 } kwok_tick_result;
+
+/* kwok_outputs.flags */
+enum {
+    /* the host arena receives ONE heartbeat body (all heartbeat patches of a tick
+       are identical, node_controller.go:393-401) followed by the node-init / pod
+       patch region: host offset = arena offset - arena_shift */
+    KWOK_READ_HEARTBEAT_ONCE = 1u
+};
 
 /* Host buffers the caller provides to kwok_read_outputs (NULL = skip). */
 typedef struct kwok_outputs {
@@ -208,6 +219,11 @@ typedef struct kwok_outputs {
     uint8_t* delete_has_finalizers; /* [n_delete] 1 = send kwok_finalizer_patch() first */
     uint8_t* arena;                 /* [arena_cap] copy of the output arena */
     uint64_t arena_cap;
+    uint32_t flags;                 /* KWOK_READ_* */
+    uint32_t reserved0;
+    uint64_t arena_shift;           /* out: node_init_off / pod_patch_off - arena_shift = the
+                                       offset in the host arena (0 without HEARTBEAT_ONCE) */
+    uint64_t arena_copied;          /* out: bytes written to the host arena */
 } kwok_outputs;
 
 typedef struct kwok_engine kwok_engine;

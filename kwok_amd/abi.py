@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 COMM_ID_BYTES = 128
 
 OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE, EBUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8, -9
@@ -91,7 +91,7 @@ class Config(C.Structure):
 class TickResult(C.Structure):
     _fields_ = [("n_heartbeat", C.c_uint32), ("heartbeat_len", C.c_uint32), ("heartbeat_stride", C.c_uint64),
                 ("n_node_init", C.c_uint32), ("n_pod_patch", C.c_uint32), ("n_delete", C.c_uint32),
-                ("reserved0", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("heartbeat_epoch", C.c_uint32), ("arena_bytes", C.c_uint64),
                 ("counters", C.c_uint64 * COUNTER_COUNT), ("local_counters", C.c_uint64 * COUNTER_COUNT)]
 
 
@@ -100,7 +100,10 @@ class Outputs(C.Structure):
                 ("node_init_nodes", C.c_void_p), ("node_init_off", C.c_void_p), ("node_init_len", C.c_void_p),
                 ("pod_patch_pods", C.c_void_p), ("pod_patch_off", C.c_void_p), ("pod_patch_len", C.c_void_p),
                 ("delete_pods", C.c_void_p), ("delete_has_finalizers", C.c_void_p),
-                ("arena", C.c_void_p), ("arena_cap", C.c_uint64)]
+                ("arena", C.c_void_p), ("arena_cap", C.c_uint64), ("flags", C.c_uint32), ("reserved0", C.c_uint32),
+                ("arena_shift", C.c_uint64), ("arena_copied", C.c_uint64)]
+
+READ_HEARTBEAT_ONCE = 1
 
 
 class DeviceView(C.Structure):

@@ -76,6 +76,7 @@ struct kwok_engine {
     uint64_t n_managed = 0;
     std::vector<uint32_t> mb_count;                  // [nb] managed nodes per owned bucket
     bool hb_pre_dirty = true;                        // the per-chain-block heartbeat bases need an upload
+    uint32_t hb_epoch = 0;                           // kwok_tick_result.heartbeat_epoch: bumped when the managed set changes
     uint32_t* hb_pre_h = nullptr;                    // pinned [n_chain + 1]
     uint32_t* d_hb_pre = nullptr;
     std::vector<uint8_t> pod_used, pod_delpend;      // [PL]
@@ -137,6 +138,7 @@ struct kwok_engine {
         int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
         uint64_t now = 0, target = 0;
         uint32_t tag = 0;
+        uint32_t epoch = 0;         // heartbeat_epoch of the tick
         std::vector<uint32_t> pending_del;  // pods whose DeletePod this tick emits
         int rc = 0;
         std::string err;
@@ -850,7 +852,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
             st = node_slot(e, name, x.name.len, false, &slot);
             if (st == KWOK_OK) {
                 auto& hn = e->nodes[slot];
-                if (hn.managed) e->n_managed--, e->mb_count[slot / e->Cn]--, e->hb_pre_dirty = true;
+                if (hn.managed) e->n_managed--, e->mb_count[slot / e->Cn]--, e->hb_pre_dirty = true, e->hb_epoch++;
                 hn.exists = hn.managed = 0;
                 node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
                         false, 0);
@@ -889,6 +891,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                         e->n_managed++;
                         e->mb_count[slot / e->Cn]++;
                         e->hb_pre_dirty = true;
+                        e->hb_epoch++;
                     }
                     hn.lockable = x.lockable ? 1 : 0;
                     bool ev_lock = x.managed && x.lockable;
@@ -1361,6 +1364,7 @@ int retire(kwok_engine* e) {
     r.n_node_init = H.n_init;
     r.n_pod_patch = H.n_pp;
     r.n_delete = H.n_del;
+    r.heartbeat_epoch = T.epoch;
     r.arena_bytes = H.arena_bytes;
     for (int c = 0; c < KWOK_COUNTER_COUNT; c++) {
         r.counters[c] = H.counters[c];
@@ -1405,6 +1409,7 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     if (!e->nops.empty() && (rc = flush_ops(e))) return rc;  // deferred by retire
     if (k == e->cur) e->cur = -1;  // its outputs are overwritten
     T.now = (uint64_t)now_unix;
+    T.epoch = e->hb_epoch;
     T.emit_queued = e->emit_hint;
     e->emit_hint = false;
     T.pending_del.swap(e->pending_del);
@@ -1467,9 +1472,24 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     HIPCHK(e, cp(o->pod_patch_len, S.pp_len, (size_t)H.n_pp * 4));
     HIPCHK(e, cp(o->delete_pods, S.del_pods, (size_t)H.n_del * 4));
     HIPCHK(e, cp(o->delete_has_finalizers, S.del_fin, (size_t)H.n_del));
+    o->arena_shift = 0;
+    o->arena_copied = 0;
     if (o->arena) {
-        if (o->arena_cap < H.arena_bytes) return e->fail(KWOK_EINVAL, "arena_cap < %llu", (unsigned long long)H.arena_bytes);
-        HIPCHK(e, cp(o->arena, S.arena, H.arena_bytes));
+        if (o->flags & KWOK_READ_HEARTBEAT_ONCE) {
+            // one heartbeat body, then the node-init / pod patch region (init_base..)
+            const uint64_t hb = H.n_hb ? (uint64_t)HB_STRIDE : 0, patches = H.arena_bytes - H.init_base;
+            if (o->arena_cap < hb + patches)
+                return e->fail(KWOK_EINVAL, "arena_cap < %llu", (unsigned long long)(hb + patches));
+            HIPCHK(e, cp(o->arena, S.arena, hb));
+            HIPCHK(e, cp(o->arena + hb, S.arena + H.init_base, patches));
+            o->arena_shift = H.init_base - hb;
+            o->arena_copied = hb + patches;
+        } else {
+            if (o->arena_cap < H.arena_bytes)
+                return e->fail(KWOK_EINVAL, "arena_cap < %llu", (unsigned long long)H.arena_bytes);
+            HIPCHK(e, cp(o->arena, S.arena, H.arena_bytes));
+            o->arena_copied = H.arena_bytes;
+        }
     }
     HIPCHK(e, hipStreamSynchronize(st));
     return KWOK_OK;

@@ -227,7 +227,10 @@ class EngineBase:
             return res
         return self.read_outputs(res)
 
-    def read_outputs(self, res=None):
+    def read_outputs(self, res=None, heartbeat_once=False):
+        """The tick's outputs on the host.  heartbeat_once: the arena holds ONE
+        heartbeat body (kwok_outputs KWOK_READ_HEARTBEAT_ONCE) - what a caller
+        that sends the same body to every node needs."""
         res = res or self.last
         hb = np.empty(res.n_heartbeat, np.int32)
         ini = np.empty(res.n_node_init, np.int32)
@@ -241,16 +244,18 @@ class EngineBase:
         arena = np.empty(max(1, res.arena_bytes), np.uint8)
         out = abi.Outputs(hb.ctypes.data, 0, ini.ctypes.data, ini_off.ctypes.data, ini_len.ctypes.data,
                           pp.ctypes.data, pp_off.ctypes.data, pp_len.ctypes.data, dl.ctypes.data, dlf.ctypes.data,
-                          arena.ctypes.data, arena.nbytes)
+                          arena.ctypes.data, arena.nbytes, abi.READ_HEARTBEAT_ONCE if heartbeat_once else 0)
         self._check(self._fn("read_outputs")(self._h, C.byref(out)), "read_outputs")
-        ab = arena.tobytes()
+        ab = arena[:out.arena_copied].tobytes()
+        sh = out.arena_shift
         return TickOutput(
             counters=dict(zip(abi.COUNTERS, list(res.counters))),
             local_counters=dict(zip(abi.COUNTERS, list(res.local_counters))),
-            heartbeat_nodes=hb, heartbeat_len=res.heartbeat_len, heartbeat_stride=res.heartbeat_stride,
+            heartbeat_nodes=hb, heartbeat_len=res.heartbeat_len,
+            heartbeat_stride=0 if heartbeat_once else res.heartbeat_stride,
             heartbeat_off=out.heartbeat_off,
-            node_inits=[(int(h), ab[o:o + n]) for h, o, n in zip(ini, ini_off, ini_len)],
-            pod_patches=[(int(h), ab[o:o + n]) for h, o, n in zip(pp, pp_off, pp_len)],
+            node_inits=[(int(h), ab[o - sh:o - sh + n]) for h, o, n in zip(ini, ini_off, ini_len)],
+            pod_patches=[(int(h), ab[o - sh:o - sh + n]) for h, o, n in zip(pp, pp_off, pp_len)],
             deletes=[(int(h), int(f)) for h, f in zip(dl, dlf)],
             arena=ab)
 

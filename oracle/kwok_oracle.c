@@ -33,6 +33,12 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#define OMP_TID() omp_get_thread_num()
+#else
+#define OMP_TID() 0
+#endif
 
 /* ------------------------------------------------------------------------- */
 /* small utilities                                                             */
@@ -376,6 +382,8 @@ struct kwok_oracle {
     uint32_t *ini_len, *pp_len;
     uint8_t* del_fin;
     uint32_t n_hb, n_ini, n_pp, n_del, hb_len;
+    uint32_t hb_epoch; /* bumped when the managed set changes */
+    int threads;       /* host threads of the tick's sweeps (kwok_oracle_set_threads) */
     uint64_t hb_off;
 };
 
@@ -583,6 +591,7 @@ int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n
                 st = owns(o, b) ? KWOK_ENOTFOUND : KWOK_ENOTMINE;
             } else {
                 onode_t* nd = &o->nodes[h];
+                if (nd->managed) o->hb_epoch++;
                 nd->exists = nd->managed = nd->event_lock = 0;
                 free_node_status(nd);
                 node_maybe_free(o, h);
@@ -609,6 +618,7 @@ int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n
                 nd->exists = 1;
                 /* node_controller.go:257-264: needHeartbeat -> Put; needLockNode -> lock */
                 if (e->managed) {
+                    if (!nd->managed) o->hb_epoch++;
                     nd->managed = 1;
                     if (e->lockable) nd->event_lock = 1;
                 }
@@ -867,17 +877,190 @@ static void render_pod(kwok_oracle* o, buf_t* b, const opod_t* p, uint32_t pod_i
 
 /* ------------------------------------------------------------------------- */
 /* tick                                                                        */
+/*                                                                             */
+/* The per-object sweeps run on o->threads host threads (OpenMP, when built  */
+/* with it; kwok_oracle_set_threads).  Every sweep splits its index range     */
+/* into contiguous per-thread pieces whose results are concatenated in thread */
+/* order, and everything order-dependent on shared state (DeletePod          */
+/* bookkeeping, ipPool Use / Put / Get) stays sequential, so the outputs are  */
+/* the same for any thread count (tests/test_oracle_golden.py).              */
 /* ------------------------------------------------------------------------- */
 typedef struct {
     uint32_t* v;
     size_t n, cap;
 } u32vec;
-static void vpush(u32vec* a, uint32_t x) {
-    if (a->n == a->cap) {
-        a->cap = a->cap ? a->cap * 2 : 64;
-        a->v = (uint32_t*)realloc(a->v, a->cap * sizeof(uint32_t));
+static void vreserve(u32vec* a, size_t n) {
+    if (a->n + n > a->cap) {
+        size_t c = a->cap ? a->cap : 64;
+        while (c < a->n + n) c *= 2;
+        a->v = (uint32_t*)realloc(a->v, c * sizeof(uint32_t));
+        a->cap = c;
     }
+}
+static void vpush(u32vec* a, uint32_t x) {
+    vreserve(a, 1);
     a->v[a->n++] = x;
+}
+
+static int nthr(const kwok_oracle* o) { return o->threads > 0 ? o->threads : 1; }
+int kwok_oracle_set_threads(kwok_oracle* o, int n) {
+#ifdef _OPENMP
+    o->threads = n > 0 ? n : omp_get_max_threads();
+#else
+    o->threads = 1;
+    (void)n;
+#endif
+    return o->threads;
+}
+
+/* the indices i in [0, n) with KEEP(o, i), ascending (a macro: the predicate
+ * is inlined into the sweep) */
+#define PFILTER(o, n, KEEP, out)                                                  \
+    do {                                                                          \
+        const int T_ = nthr(o);                                                   \
+        const size_t n_ = (n);                                                    \
+        u32vec* part_ = (u32vec*)calloc((size_t)T_, sizeof(u32vec));              \
+        _Pragma("omp parallel num_threads(T_)") {                                 \
+            const int t_ = OMP_TID();                                             \
+            for (size_t i_ = n_ * t_ / T_, hi_ = n_ * (t_ + 1) / T_; i_ < hi_; i_++) \
+                if (KEEP(o, i_)) vpush(&part_[t_], (uint32_t)i_);                  \
+        }                                                                         \
+        pconcat(part_, T_, out);                                                  \
+    } while (0)
+static void pconcat(u32vec* part, int T, u32vec* out) {
+    size_t tot = 0;
+    for (int t = 0; t < T; t++) tot += part[t].n;
+    vreserve(out, tot);
+    for (int t = 0; t < T; t++) {
+        memcpy(out->v + out->n, part[t].v, part[t].n * sizeof(uint32_t));
+        out->n += part[t].n;
+        free(part[t].v);
+    }
+    free(part);
+}
+
+/* LockNode set: heartbeat feedback (every managed lockable node) + event locks */
+static int node_locked(const onode_t* n) { return n->used && n->exists && ((n->managed && n->lockable) || n->event_lock); }
+static inline int keep_del(const kwok_oracle* o, size_t h) { return o->pods[h].used && o->pods[h].delete_pending; }
+static inline int keep_lock(const kwok_oracle* o, size_t h) { return node_locked(&o->nodes[h]); }
+static inline int keep_managed(const kwok_oracle* o, size_t h) { return o->nodes[h].used && o->nodes[h].managed; }
+/* LockPods: lock events + LockPodsOnNode of every locked managed node */
+static inline int keep_eval(const kwok_oracle* o, size_t h) {
+    const opod_t* p = &o->pods[h];
+    if (!p->used) return 0;
+    const onode_t* n = &o->nodes[p->node];
+    return p->event || (node_locked(n) && n->managed && !p->disregard);
+}
+static int pod_needs_patch(const opod_t* p) {
+    return p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip;
+}
+
+static void arena_reserve(buf_t* b, size_t n) {
+    if (b->n + n + 1 > b->cap) {
+        size_t c = b->cap ? b->cap : 4096;
+        while (c < b->n + n + 1) c *= 2;
+        b->p = (char*)realloc(b->p, c);
+        b->cap = c;
+    }
+}
+
+/* render items [0, n) of a list in parallel (render(o, buf, i) appends item i's
+ * patch, or nothing) and append them to the arena in list order; off / len get
+ * each rendered item's arena offset and length (compacted: k-th rendered) */
+typedef int (*render_fn)(kwok_oracle* o, buf_t* b, size_t i, const char* now);
+static size_t prender(kwok_oracle* o, size_t n, render_fn render, const char* now, uint64_t* off, uint32_t* len,
+                      size_t* which) {
+    const int T = nthr(o);
+    buf_t* bufs = (buf_t*)calloc((size_t)T, sizeof(buf_t));
+    size_t* cnt = (size_t*)calloc((size_t)T + 1, sizeof(size_t));
+    size_t* first = (size_t*)calloc((size_t)T + 1, sizeof(size_t));
+    size_t* loc = (size_t*)calloc(n + 1, sizeof(size_t)); /* per rendered item: offset in its thread buffer */
+    uint32_t* lens = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
+    size_t* idx = (size_t*)calloc(n + 1, sizeof(size_t));
+    /* pass 1: count per thread (rendered items are those that produce bytes) */
+#pragma omp parallel num_threads(T)
+    {
+        const int t = OMP_TID();
+        size_t k = 0;
+        for (size_t i = n * t / T, hi = n * (t + 1) / T; i < hi; i++) {
+            const size_t before = bufs[t].n;
+            if (render(o, &bufs[t], i, now)) {
+                loc[n * t / T + k] = before;
+                lens[n * t / T + k] = (uint32_t)(bufs[t].n - before);
+                idx[n * t / T + k] = i;
+                k++;
+            }
+        }
+        cnt[t] = k;
+    }
+    size_t tot = 0, bytes = 0;
+    for (int t = 0; t < T; t++) {
+        first[t] = bytes;
+        bytes += bufs[t].n;
+        tot += cnt[t];
+    }
+    const size_t base = o->arena.n;
+    arena_reserve(&o->arena, bytes);
+    size_t k = 0;
+    for (int t = 0; t < T; t++) {
+        for (size_t j = 0; j < cnt[t]; j++, k++) {
+            const size_t s = n * t / T + j;
+            off[k] = base + first[t] + loc[s];
+            len[k] = lens[s];
+            if (which) which[k] = idx[s];
+        }
+    }
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+    for (int t = 0; t < T; t++) {
+        if (bufs[t].n) memcpy(o->arena.p + base + first[t], bufs[t].p, bufs[t].n);
+        free(bufs[t].p);
+    }
+    o->arena.n = base + bytes;
+    o->arena.p[o->arena.n] = 0;
+    free(bufs), free(cnt), free(first), free(loc), free(lens), free(idx);
+    return tot;
+}
+
+/* per-tick scratch of the renderers */
+typedef struct {
+    const uint32_t* list; /* locks / evals */
+    const uint32_t* ip;   /* evals: the podIP each pod renders */
+} rctx_t;
+static rctx_t g_rctx; /* set around each prender call (the oracle is not re-entrant) */
+
+static int render_init_item(kwok_oracle* o, buf_t* b, size_t i, const char* now) {
+    const onode_t* n = &o->nodes[g_rctx.list[i]];
+    if (n->conforms) return 0;
+    render_node_init(o, b, n, now);
+    return 1;
+}
+static int render_pod_item(kwok_oracle* o, buf_t* b, size_t i, const char* now) {
+    (void)now;
+    const opod_t* p = &o->pods[g_rctx.list[i]];
+    if (!pod_needs_patch(p)) return 0;
+    render_pod(o, b, p, g_rctx.ip[i]);
+    return 1;
+}
+
+/* the apiserver applies a node init patch: defaults now in place */
+static void node_apply_init(kwok_oracle* o, onode_t* n) {
+    static const char* dflt[KWOK_NI_COUNT] = {"amd64", "", "", "", "fake", "fake", "", "linux", "", ""};
+    for (int k = 0; k < KWOK_NI_COUNT; k++)
+        if (!n->info[k] && dflt[k][0]) n->info[k] = xstrndup(dflt[k], strlen(dflt[k]));
+    free(n->info[KWOK_NI_SYSTEM_UUID]);
+    n->info[KWOK_NI_SYSTEM_UUID] =
+        n->info[KWOK_NI_OS_IMAGE] ? xstrndup(n->info[KWOK_NI_OS_IMAGE], strlen(n->info[KWOK_NI_OS_IMAGE])) : NULL;
+    if (!n->addresses) {
+        buf_t a = {0};
+        buf_s(&a, "[{\"address\":");
+        buf_jstr(&a, o->node_ip_s, strlen(o->node_ip_s));
+        buf_s(&a, ",\"type\":\"InternalIP\"}]");
+        n->addresses = a.p;
+    }
+    if (!n->allocatable) n->allocatable = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
+    if (!n->capacity) n->capacity = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
+    n->phase = KWOK_PHASE_RUNNING;
+    n->conforms = 1;
 }
 
 #define GROW(ptr, n) ptr = realloc(ptr, ((n) + 1) * sizeof(*(ptr)))
@@ -890,19 +1073,21 @@ typedef struct {
 
 int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
     const size_t NN = (size_t)o->B * o->cn, NP = (size_t)o->B * o->cp;
+    const int T = nthr(o);
     char now[32];
     rfc3339(now_unix, now);
     uint64_t cnt[KWOK_COUNTER_COUNT] = {0};
     o->arena.n = 0;
     o->n_hb = o->n_ini = o->n_pp = o->n_del = 0;
-    u32vec rel = {0}, use = {0}, evals = {0}, locks = {0};
+    u32vec rel = {0}, use = {0}, evals = {0}, locks = {0}, dels = {0}, hbl = {0};
 
     /* 1. deletions (DeletePods/DeletePod :155-202); the Deleted event releases the IP */
-    for (size_t h = 0; h < NP; h++) {
+    PFILTER(o, NP, keep_del, &dels);
+    GROW(o->del, dels.n);
+    GROW(o->del_fin, dels.n);
+    for (size_t i = 0; i < dels.n; i++) {
+        const size_t h = dels.v[i];
         opod_t* p = &o->pods[h];
-        if (!p->used || !p->delete_pending) continue;
-        GROW(o->del, o->n_del);
-        GROW(o->del_fin, o->n_del);
         o->del[o->n_del] = (int32_t)h;
         o->del_fin[o->n_del++] = (uint8_t)p->has_fin;
         cnt[KWOK_CNT_DELETE]++;
@@ -913,60 +1098,64 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
         node_maybe_free(o, nh);
     }
     cnt[KWOK_CNT_RELEASE] = rel.n;
-    /* lock set: heartbeat feedback (every managed lockable node) + event locks */
-    for (size_t h = 0; h < NN; h++) {
-        onode_t* n = &o->nodes[h];
-        if (n->used && n->exists && ((n->managed && n->lockable) || n->event_lock)) vpush(&locks, (uint32_t)h);
-    }
-    /* pods to evaluate: lock events + LockPodsOnNode of locked managed nodes */
-    for (size_t h = 0; h < NP; h++) {
-        opod_t* p = &o->pods[h];
-        if (!p->used) continue;
-        onode_t* n = &o->nodes[p->node];
-        int relock = n->exists && n->managed && ((n->managed && n->lockable) || n->event_lock) && !p->disregard;
-        if (p->event || relock) vpush(&evals, (uint32_t)h);
-    }
-    uint64_t alloc_local = 0;
-    for (size_t i = 0; i < evals.n; i++) {
-        opod_t* p = &o->pods[evals.v[i]];
-        if (p->pod_ip && cidr_contains(&o->pool, p->pod_ip)) vpush(&use, p->pod_ip); /* configurePod :378-382 */
-        if (p->status_nonempty && !p->pod_ip) alloc_local++;
+    PFILTER(o, NN, keep_lock, &locks);
+    PFILTER(o, NP, keep_eval, &evals);
+    /* configurePod (:378-382): Use of every evaluated in-CIDR podIP.  Use of an
+     * address already in `used` changes nothing, so only the others are listed. */
+    {
+        uint8_t* fresh = (uint8_t*)calloc(evals.n + 1, 1);
+        uint64_t alloc_local = 0;
+#pragma omp parallel for num_threads(T) reduction(+ : alloc_local)
+        for (size_t i = 0; i < evals.n; i++) {
+            const opod_t* p = &o->pods[evals.v[i]];
+            if (p->pod_ip && cidr_contains(&o->pool, p->pod_ip) && !hs_has(&o->pool.used, p->pod_ip)) fresh[i] = 1;
+            if (p->status_nonempty && !p->pod_ip) alloc_local++;
+        }
+        for (size_t i = 0; i < evals.n; i++)
+            if (fresh[i]) vpush(&use, o->pods[evals.v[i]].pod_ip);
+        free(fresh);
+        cnt[KWOK_CNT_ALLOC] = alloc_local;
     }
     /* counters known before emission (the exchange needs them) */
-    for (size_t h = 0; h < NN; h++) {
-        onode_t* n = &o->nodes[h];
-        if (!n->used) continue;
-        if (n->managed) cnt[KWOK_CNT_HEARTBEAT]++, cnt[KWOK_CNT_NODES_MANAGED]++;
-    }
-    for (size_t i = 0; i < locks.n; i++) {
-        onode_t* n = &o->nodes[locks.v[i]];
-        cnt[KWOK_CNT_LOCK_CHECKED]++;
-        if (!n->conforms) cnt[KWOK_CNT_NODE_INIT]++;
-    }
-    for (size_t h = 0; h < NN; h++) {
-        onode_t* n = &o->nodes[h];
-        int locked = n->used && n->exists && ((n->managed && n->lockable) || n->event_lock);
-        if (n->used && n->managed && (n->conforms || locked)) cnt[KWOK_CNT_NODES_READY]++;
-    }
-    cnt[KWOK_CNT_EVALUATED] = evals.n;
-    cnt[KWOK_CNT_ALLOC] = alloc_local;
-    uint8_t* patched = (uint8_t*)calloc(NP + 1, 1);
-    for (size_t i = 0; i < evals.n; i++) {
-        opod_t* p = &o->pods[evals.v[i]];
-        if (p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip) {
-            cnt[KWOK_CNT_POD_PATCH]++;
-            patched[evals.v[i]] = 1;
+    {
+        uint64_t hb = 0, ready = 0, init = 0, pp = 0, total = 0, pend = 0, run = 0;
+#pragma omp parallel for num_threads(T) reduction(+ : hb, ready)
+        for (size_t h = 0; h < NN; h++) {
+            const onode_t* n = &o->nodes[h];
+            if (n->used && n->managed) {
+                hb++;
+                if (n->conforms || node_locked(n)) ready++;
+            }
         }
+#pragma omp parallel for num_threads(T) reduction(+ : init)
+        for (size_t i = 0; i < locks.n; i++) init += !o->nodes[locks.v[i]].conforms;
+        uint8_t* patched = (uint8_t*)calloc(NP + 1, 1);
+#pragma omp parallel for num_threads(T) reduction(+ : pp)
+        for (size_t i = 0; i < evals.n; i++)
+            if (pod_needs_patch(&o->pods[evals.v[i]])) {
+                pp++;
+                patched[evals.v[i]] = 1;
+            }
+#pragma omp parallel for num_threads(T) reduction(+ : total, pend, run)
+        for (size_t h = 0; h < NP; h++) {
+            const opod_t* p = &o->pods[h];
+            if (!p->used) continue;
+            total++;
+            const int ph = patched[h] ? KWOK_PHASE_RUNNING : p->phase;
+            pend += ph == KWOK_PHASE_PENDING;
+            run += ph == KWOK_PHASE_RUNNING;
+        }
+        free(patched);
+        cnt[KWOK_CNT_HEARTBEAT] = cnt[KWOK_CNT_NODES_MANAGED] = hb;
+        cnt[KWOK_CNT_NODES_READY] = ready;
+        cnt[KWOK_CNT_LOCK_CHECKED] = locks.n;
+        cnt[KWOK_CNT_NODE_INIT] = init;
+        cnt[KWOK_CNT_EVALUATED] = evals.n;
+        cnt[KWOK_CNT_POD_PATCH] = pp;
+        cnt[KWOK_CNT_PODS_TOTAL] = total;
+        cnt[KWOK_CNT_PODS_PENDING] = pend;
+        cnt[KWOK_CNT_PODS_RUNNING] = run;
     }
-    for (size_t h = 0; h < NP; h++) {
-        opod_t* p = &o->pods[h];
-        if (!p->used) continue;
-        cnt[KWOK_CNT_PODS_TOTAL]++;
-        int ph = patched[h] ? KWOK_PHASE_RUNNING : p->phase;
-        if (ph == KWOK_PHASE_PENDING) cnt[KWOK_CNT_PODS_PENDING]++;
-        if (ph == KWOK_PHASE_RUNNING) cnt[KWOK_CNT_PODS_RUNNING]++;
-    }
-    free(patched);
 
     /* 2. exchange (sharded mode) and the pool phases: Uses, then Puts */
     uint64_t alloc_before = 0, alloc_after = 0;
@@ -974,9 +1163,8 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
     memcpy(fleet, cnt, sizeof(fleet));
     int W = o->cfg.world_size;
     if (W > 1) {
-        size_t my_bytes = sizeof(xhdr_t) + 4 * (use.n + rel.n);
         /* step 1: headers (sizes); step 2: padded lists */
-        xhdr_t hdr = {alloc_local, use.n, rel.n, {0}};
+        xhdr_t hdr = {cnt[KWOK_CNT_ALLOC], use.n, rel.n, {0}};
         memcpy(hdr.counters, cnt, sizeof(cnt));
         xhdr_t* all = (xhdr_t*)calloc((size_t)W, sizeof(xhdr_t));
         if (o->cfg.allgather(o->cfg.allgather_user, &hdr, sizeof(hdr), all)) return KWOK_ECOMM;
@@ -985,10 +1173,9 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
             size_t l = all[r].n_use + all[r].n_rel;
             if (l > maxl) maxl = l;
         }
-        (void)my_bytes;
         uint32_t* mine = (uint32_t*)calloc(maxl + 1, 4);
-        memcpy(mine, use.v, 4 * use.n);
-        memcpy(mine + use.n, rel.v, 4 * rel.n);
+        if (use.n) memcpy(mine, use.v, 4 * use.n);
+        if (rel.n) memcpy(mine + use.n, rel.v, 4 * rel.n);
         uint32_t* lists = (uint32_t*)calloc((size_t)W * (maxl + 1), 4);
         if (o->cfg.allgather(o->cfg.allgather_user, mine, 4 * (maxl + 1), lists)) return KWOK_ECOMM;
         memset(fleet, 0, sizeof(fleet));
@@ -1009,83 +1196,77 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
     }
 
     /* 3. heartbeat: every managed node (canonical order), identical bodies */
-    buf_t hbb = {0};
-    render_heartbeat(&hbb, now, o->start_s);
-    o->hb_len = (uint32_t)hbb.n;
-    o->hb_off = o->arena.n;
-    for (size_t h = 0; h < NN; h++) {
-        onode_t* n = &o->nodes[h];
-        if (!n->used || !n->managed) continue;
-        GROW(o->hb, o->n_hb);
-        o->hb[o->n_hb++] = (int32_t)h;
-        buf_put(&o->arena, hbb.p, hbb.n);
+    {
+        buf_t hbb = {0};
+        render_heartbeat(&hbb, now, o->start_s);
+        o->hb_len = (uint32_t)hbb.n;
+        o->hb_off = o->arena.n;
+        PFILTER(o, NN, keep_managed, &hbl);
+        GROW(o->hb, hbl.n);
+        memcpy(o->hb, hbl.v, hbl.n * sizeof(int32_t));
+        o->n_hb = (uint32_t)hbl.n;
+        arena_reserve(&o->arena, (size_t)o->n_hb * hbb.n);
+        char* dst = o->arena.p + o->arena.n;
+#pragma omp parallel for num_threads(T)
+        for (size_t i = 0; i < o->n_hb; i++) memcpy(dst + i * hbb.n, hbb.p, hbb.n);
+        o->arena.n += (size_t)o->n_hb * hbb.n;
+        o->arena.p[o->arena.n] = 0;
+        free(hbb.p);
     }
-    free(hbb.p);
 
-    /* 4. node lock (LockNode / configureNode) */
-    for (size_t i = 0; i < locks.n; i++) {
-        onode_t* n = &o->nodes[locks.v[i]];
-        if (!n->conforms) {
-            GROW(o->ini, o->n_ini);
-            GROW(o->ini_off, o->n_ini);
-            GROW(o->ini_len, o->n_ini);
-            size_t off = o->arena.n;
-            render_node_init(o, &o->arena, n, now);
-            o->ini[o->n_ini] = (int32_t)locks.v[i];
-            o->ini_off[o->n_ini] = off;
-            o->ini_len[o->n_ini++] = (uint32_t)(o->arena.n - off);
-            /* the apiserver applies the patch: defaults now in place */
-            static const char* dflt[KWOK_NI_COUNT] = {"amd64", "", "", "", "fake", "fake", "", "linux", "", ""};
-            for (int k = 0; k < KWOK_NI_COUNT; k++)
-                if (!n->info[k] && dflt[k][0]) n->info[k] = xstrndup(dflt[k], strlen(dflt[k]));
-            free(n->info[KWOK_NI_SYSTEM_UUID]);
-            n->info[KWOK_NI_SYSTEM_UUID] =
-                n->info[KWOK_NI_OS_IMAGE] ? xstrndup(n->info[KWOK_NI_OS_IMAGE], strlen(n->info[KWOK_NI_OS_IMAGE])) : NULL;
-            if (!n->addresses) {
-                buf_t a = {0};
-                buf_s(&a, "[{\"address\":");
-                buf_jstr(&a, o->node_ip_s, strlen(o->node_ip_s));
-                buf_s(&a, ",\"type\":\"InternalIP\"}]");
-                n->addresses = a.p;
-            }
-            if (!n->allocatable) n->allocatable = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
-            if (!n->capacity) n->capacity = xstrndup("{\"cpu\":\"1k\",\"memory\":\"1Ti\",\"pods\":\"1M\"}", 39);
-            n->phase = KWOK_PHASE_RUNNING;
-            n->conforms = 1;
-        }
+    /* 4. node lock (LockNode / configureNode): init patches, then the apiserver applies them */
+    {
+        GROW(o->ini, locks.n);
+        GROW(o->ini_off, locks.n);
+        GROW(o->ini_len, locks.n);
+        size_t* which = (size_t*)calloc(locks.n + 1, sizeof(size_t));
+        g_rctx.list = locks.v;
+        o->n_ini = cnt[KWOK_CNT_NODE_INIT] ? (uint32_t)prender(o, locks.n, render_init_item, now, o->ini_off, o->ini_len, which) : 0;
+        for (uint32_t k = 0; k < o->n_ini; k++) o->ini[k] = (int32_t)locks.v[which[k]];
+#pragma omp parallel for num_threads(T)
+        for (uint32_t k = 0; k < o->n_ini; k++) node_apply_init(o, &o->nodes[o->ini[k]]);
+        free(which);
     }
+#pragma omp parallel for num_threads(T)
     for (size_t h = 0; h < NN; h++) o->nodes[h].event_lock = 0;
 
     /* 5. pod lock in canonical order; Gets of lower ranks come first */
-    for (uint64_t k = 0; k < alloc_before; k++) (void)pool_get(&o->pool);
-    for (size_t i = 0; i < evals.n; i++) {
-        opod_t* p = &o->pods[evals.v[i]];
-        uint32_t ip = p->pod_ip;
-        /* `{{ with .podIP }} . {{ else }} PodIP {{ end }}` inside `{{ with .status }}` */
-        if (p->status_nonempty && !p->pod_ip) ip = (uint32_t)pool_get(&o->pool);
-        int need = p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip;
-        if (need) {
-            GROW(o->pp, o->n_pp);
-            GROW(o->pp_off, o->n_pp);
-            GROW(o->pp_len, o->n_pp);
-            size_t off = o->arena.n;
-            render_pod(o, &o->arena, p, ip);
-            o->pp[o->n_pp] = (int32_t)evals.v[i];
-            o->pp_off[o->n_pp] = off;
-            o->pp_len[o->n_pp++] = (uint32_t)(o->arena.n - off);
+    {
+        uint32_t* ip = (uint32_t*)calloc(evals.n + 1, sizeof(uint32_t));
+        for (uint64_t k = 0; k < alloc_before; k++) (void)pool_get(&o->pool);
+        for (size_t i = 0; i < evals.n; i++) {
+            const opod_t* p = &o->pods[evals.v[i]];
+            /* `{{ with .podIP }} . {{ else }} PodIP {{ end }}` inside `{{ with .status }}` */
+            ip[i] = (p->status_nonempty && !p->pod_ip) ? (uint32_t)pool_get(&o->pool) : p->pod_ip;
+        }
+        for (uint64_t k = 0; k < alloc_after; k++) (void)pool_get(&o->pool);
+        GROW(o->pp, evals.n);
+        GROW(o->pp_off, evals.n);
+        GROW(o->pp_len, evals.n);
+        size_t* which = (size_t*)calloc(evals.n + 1, sizeof(size_t));
+        g_rctx.list = evals.v;
+        g_rctx.ip = ip;
+        o->n_pp = cnt[KWOK_CNT_POD_PATCH] ? (uint32_t)prender(o, evals.n, render_pod_item, now, o->pp_off, o->pp_len, which) : 0;
+        for (uint32_t k = 0; k < o->n_pp; k++) o->pp[k] = (int32_t)evals.v[which[k]];
+        /* the apiserver applies each patch */
+#pragma omp parallel for num_threads(T)
+        for (uint32_t k = 0; k < o->n_pp; k++) {
+            opod_t* p = &o->pods[o->pp[k]];
             if (p->status_nonempty) {
                 if (!p->host_ip) p->host_ip = o->node_ip;
-                p->pod_ip = ip;
+                p->pod_ip = ip[which[k]];
             }
             p->phase = KWOK_PHASE_RUNNING;
             p->conforms = 1;
             p->status_nonempty = 1;
         }
+        free(which);
+        free(ip);
     }
-    for (uint64_t k = 0; k < alloc_after; k++) (void)pool_get(&o->pool);
+#pragma omp parallel for num_threads(T)
     for (size_t h = 0; h < NP; h++) o->pods[h].event = 0, o->pods[h].delete_pending &= o->pods[h].used;
 
-    free(rel.v), free(use.v), free(evals.v), free(locks.v);
+    free(rel.v), free(use.v), free(evals.v), free(locks.v), free(dels.v), free(hbl.v);
     if (res) {
         memset(res, 0, sizeof(*res));
         res->n_heartbeat = o->n_hb;
@@ -1094,6 +1275,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
         res->n_node_init = o->n_ini;
         res->n_pod_patch = o->n_pp;
         res->n_delete = o->n_del;
+        res->heartbeat_epoch = o->hb_epoch;
         res->arena_bytes = o->arena.n;
         memcpy(res->counters, fleet, sizeof(fleet));
         memcpy(res->local_counters, cnt, sizeof(cnt));
@@ -1112,9 +1294,21 @@ int kwok_oracle_read_outputs(kwok_oracle* o, kwok_outputs* out) {
     if (out->pod_patch_len) memcpy(out->pod_patch_len, o->pp_len, 4 * o->n_pp);
     if (out->delete_pods) memcpy(out->delete_pods, o->del, 4 * o->n_del);
     if (out->delete_has_finalizers) memcpy(out->delete_has_finalizers, o->del_fin, o->n_del);
+    out->arena_shift = 0;
+    out->arena_copied = 0;
     if (out->arena) {
-        if (out->arena_cap < o->arena.n) return KWOK_EINVAL;
-        memcpy(out->arena, o->arena.p, o->arena.n);
+        if (out->flags & KWOK_READ_HEARTBEAT_ONCE) { /* one body, then the patches */
+            size_t hb = o->n_hb ? o->hb_len : 0, first = (size_t)o->n_hb * o->hb_len, rest = o->arena.n - first;
+            if (out->arena_cap < hb + rest) return KWOK_EINVAL;
+            memcpy(out->arena, o->arena.p, hb);
+            memcpy(out->arena + hb, o->arena.p + first, rest);
+            out->arena_shift = first - hb;
+            out->arena_copied = hb + rest;
+        } else {
+            if (out->arena_cap < o->arena.n) return KWOK_EINVAL;
+            memcpy(out->arena, o->arena.p, o->arena.n);
+            out->arena_copied = o->arena.n;
+        }
     }
     return KWOK_OK;
 }

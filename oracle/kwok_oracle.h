@@ -19,6 +19,8 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                             int32_t* out_handles, int32_t* out_status, uint32_t* out_released);
 int kwok_oracle_pool_put(kwok_oracle* o, const uint32_t* ips, size_t n);
 int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res);
+/* host threads of the tick's per-object sweeps (<= 0: all; 1: sequential); returns the count */
+int kwok_oracle_set_threads(kwok_oracle* o, int n);
 int kwok_oracle_read_outputs(kwok_oracle* o, kwok_outputs* out);
 int kwok_oracle_node_has(kwok_oracle* o, const char* name, size_t len);
 uint64_t kwok_oracle_node_size(kwok_oracle* o);

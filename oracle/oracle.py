@@ -28,11 +28,20 @@ def load():
             build()
         _lib = C.CDLL(LIB)
         _eng.declare(_lib, "kwok_oracle_")
+        _lib.kwok_oracle_set_threads.restype = C.c_int
+        _lib.kwok_oracle_set_threads.argtypes = [C.c_void_p, C.c_int]
     return _lib
 
 
 class Oracle(_eng.EngineBase):
     PREFIX = "kwok_oracle_"
 
-    def __init__(self, cfg=None, **kw):
+    def __init__(self, cfg=None, threads=1, **kw):
         super().__init__(load(), cfg if cfg is not None else _eng.make_config(**kw))
+        self.threads = self.set_threads(threads)
+
+    def set_threads(self, n):
+        """host threads of the tick's sweeps (OpenMP; <= 0: all cores); the
+        outputs are the same for every count"""
+        self.threads = self._lib.kwok_oracle_set_threads(self._h, n)
+        return self.threads

@@ -62,10 +62,12 @@ STRUCTS = {
                                  "max_pod_specs", "rank", "world_size", "device", "comm_id", "allgather",
                                  "allgather_user"]),
     "kwok_tick_result": (abi.TickResult, ["n_heartbeat", "heartbeat_len", "heartbeat_stride", "n_node_init",
-                                          "n_pod_patch", "n_delete", "arena_bytes", "counters", "local_counters"]),
+                                          "n_pod_patch", "n_delete", "heartbeat_epoch", "arena_bytes", "counters",
+                                          "local_counters"]),
     "kwok_outputs": (abi.Outputs, ["heartbeat_nodes", "heartbeat_off", "node_init_nodes", "node_init_off",
                                    "node_init_len", "pod_patch_pods", "pod_patch_off", "pod_patch_len",
-                                   "delete_pods", "delete_has_finalizers", "arena", "arena_cap"]),
+                                   "delete_pods", "delete_has_finalizers", "arena", "arena_cap", "flags",
+                                   "arena_shift", "arena_copied"]),
     "kwok_codec_config": (abi.CodecConfig, ["manage_all_nodes", "manage_nodes_with_annotation_selector",
                                             "manage_nodes_with_label_selector",
                                             "disregard_status_with_annotation_selector",
@@ -130,3 +132,19 @@ def test_profile_enums_match_python_mirrors():
         ents = [x for x in ents if x]
         assert ents[-1] == prefix + "COUNT"
         assert [x[len(prefix):].lower() for x in ents[:-1]] == list(names)
+
+
+def test_compact_readout_oracle():
+    """KWOK_READ_HEARTBEAT_ONCE: one heartbeat body, then the patch region at
+    offsets shifted by arena_shift - the same patches as the full copy"""
+    import harness
+    from oracle.oracle import Oracle
+    fx = harness.load_trace("specs")
+    o = Oracle(harness.config_for(fx))
+    seen = []
+    harness.replay(fx, o, on_tick=lambda ti, t, out: seen.append(ti))
+    full = o.read_outputs()
+    once = o.read_outputs(heartbeat_once=True)
+    assert once.node_inits == full.node_inits and once.pod_patches == full.pod_patches
+    assert once.heartbeat_body(0) == full.heartbeat_body(0) and len(full.heartbeat_nodes) > 1
+    assert len(once.arena) == len(full.arena) - (len(full.heartbeat_nodes) - 1) * full.heartbeat_len

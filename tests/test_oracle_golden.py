@@ -107,3 +107,65 @@ def test_ippool_cases():
                     now += 30
                 got.append(None)
         assert got == c["results"], c
+
+
+@pytest.mark.parametrize("name", harness.TRACES)
+def test_oracle_threads_golden(name):
+    """the OpenMP sweeps (the all-core CPU baseline) reproduce the goldens too"""
+    fx = harness.load_trace(name)
+    o = Oracle(harness.config_for(fx), threads=8)
+    harness.replay(fx, o)
+
+
+def test_oracle_threads_match_sequential_at_scale():
+    """8 threads vs 1 thread on a churning fleet (deletions with and without
+    finalizers, IP release and reuse, new pods): identical outputs and state"""
+    import numpy as np
+    from kwok_amd import abi, workload
+    outs = []
+    for th in (1, 8):
+        o, fl, ph = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=th), 3000, buckets=256)
+        assert o.threads == th
+        rng = np.random.default_rng(5)
+        seq = []
+        for t in range(3):
+            if t:
+                used, phase, hip, pip = o.dump_pods(0, 256 * fl.cp)
+                idx = np.nonzero(used)[0]
+                dl = np.sort(rng.choice(idx, 500, replace=False)).astype(np.int32)
+                ar = abi.Arena()
+                ev = np.zeros(len(dl), abi.POD_EVENT_DTYPE)
+                ev["op"] = abi.OP_UPSERT
+                ev["handle"] = dl
+                ev["phase"] = abi.PHASE_RUNNING
+                ev["creation_unix"] = workload.S0 - 60
+                ev["flags"] = (abi.POD_DELETING | abi.POD_STATUS_NONEMPTY | abi.POD_CONFORMS |
+                               np.where(np.arange(len(dl)) % 2, abi.POD_HAS_FINALIZERS, 0))
+                for i, h in enumerate(dl):
+                    ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[h])))
+                    ev[i]["host_ip"] = ar.ref(abi.ip4s(int(hip[h])))
+                _, st, _ = o.ingest_pods_raw(ev, bytes(ar.buf))
+                assert (st == 0).all()
+                names = fl.names[rng.choice(len(fl.names), 700)]
+                new = np.zeros(len(names), abi.POD_EVENT_DTYPE)
+                new["op"] = abi.OP_UPSERT
+                new["handle"] = -1
+                new["node_handle"] = -1
+                new["phase"] = abi.PHASE_PENDING
+                new["flags"] = abi.POD_STATUS_NONEMPTY
+                new["creation_unix"] = workload.S0 + t
+                new["node_name"]["off"] = np.arange(len(names), dtype=np.uint32) * 12
+                new["node_name"]["len"] = 12
+                _, st, _ = o.ingest_pods_raw(new, names.tobytes())
+                assert (st == 0).all()
+            out = o.tick(workload.S0 + 30 * (t + 1))
+            seq.append((list(out.heartbeat_nodes), out.node_inits, out.pod_patches, out.deletes, out.counters))
+        assert seq[1][3] and seq[1][2]  # deletes and new pods' patches happened
+        seq.append(o.dump_pods(0, 256 * fl.cp))
+        outs.append(seq)
+        o.close()
+    a, b = outs
+    for x, y in zip(a[:-1], b[:-1]):
+        assert x == y
+    for x, y in zip(a[-1], b[-1]):
+        assert (x == y).all()
