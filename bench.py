@@ -1,19 +1,28 @@
 #!/usr/bin/env python3
 """bench.py - kwok fake-kubelet tick on MI355X (BASELINE.json metric:
-state transitions/sec, % of HBM roofline).
+"state transitions/sec at 1M nodes/10M pods, 1-8 MI355X; % HBM roofline").
 
-Workload (N=1): configs[1] of BASELINE.json - 100k nodes x 1M pods, steady-state
-heartbeat + status ticks on one MI355X.  Weak scaling: every rank owns 100k
-nodes / 1M pods of a fleet of N x 100k nodes hashed into 4096 buckets
-(contiguous bucket ranges per rank), and ranks exchange pool/counter data over
-RCCL each tick.  A step = one tick (one heartbeat interval at a fixed clock):
-heartbeat patches for every managed node, lock checks for every node,
-re-evaluation of every pod, ipPool bookkeeping, and the host collecting the
-tick's result.  Steps are queued (kwok_tick_submit for tick k+1 before
-kwok_tick_collect of tick k, outputs double-buffered); --no-queue times one
-blocking kwok_tick per step, and that figure is always reported beside the
-queued one (ms_per_step_kwok_tick).  Warmup includes the initial tick (100k
-node-init patches + 1M Pending->Running patches with IP allocation).
+Workload (N=1): the metric's configuration - 1M nodes x 10M pods (10 pods per
+node, the reference benchmark's pod shape) stepped per tick on one MI355X:
+steady-state heartbeat + status ticks (BASELINE configs[1]'s tick at the
+metric's size).  Weak scaling: every rank owns 1M nodes / 10M pods of a fleet
+of N x 1M nodes hashed into 4096 buckets (contiguous bucket ranges per rank);
+ranks exchange pool / counter data over RCCL every tick.  The CIDR is
+10.0.0.1/8 (/4 once the fleet has more than 16M pods) so that every fresh IP
+lies in the CIDR.
+
+A step = one tick (one heartbeat interval at a fixed clock): the heartbeat patch
+of every managed node, the lock check of every node, the re-evaluation of
+every pod, ipPool bookkeeping and the host collecting the tick's result, with
+all state resident in HBM.  Steps are queued (kwok_tick_submit for tick k+1
+before kwok_tick_collect of tick k).  Reported beside `value`:
+  * the same steps one blocking kwok_tick each;
+  * the same steps with the per-tick hand-off a Go caller consumes
+    (kwok_read_outputs, KWOK_READ_HEARTBEAT_ONCE: one heartbeat body + the
+    patch region + the delete list; the heartbeat handle list only when its
+    epoch changes) - PCIe-inclusive;
+  * the initial tick (1M node-init patches + 10M Pending->Running patches with
+    IP allocation), timed on its own, with its own roofline (k_emit).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -21,6 +30,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -33,26 +43,32 @@ sys.path.insert(0, ROOT)
 # it first so that libkwok_engine.so binds the SAME runtime (its NEEDED
 # sonames resolve to the already-loaded copies): one runtime per process, and
 # torch.cuda.synchronize() covers the engine's stream.
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
 
+from kwok_amd import abi  # noqa: E402
 from kwok_amd import engine as keng  # noqa: E402
 from kwok_amd import workload  # noqa: E402
 
 keng.load_engine_lib()
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-NODES_PER_RANK = 100_000
-# algorithmic HBM bytes of one tick (SURVEY.md §8(d) byte model):
-# per managed node a heartbeat (1 B flags + 4 B hb-time + 4 B out-index + the
-# 1059-byte materialised patch = 1068 B) and a no-op re-lock check (9 B); per
-# live pod a no-op re-check (10 B)
-HB_BYTES = 1059
+NODES_PER_RANK = 1_000_000
+# algorithmic HBM bytes (SURVEY.md §8(d) byte model):
+#   steady tick, per managed node: heartbeat 1 B flags + 4 B hb-time + 4 B
+#   out-index + the 1059-byte patch = 1068 B, plus a no-op re-lock check 9 B;
+#   per live pod a no-op re-check 10 B
 NODE_BYTES = 1068 + 9
 POD_BYTES = 10
-PMC_FILE = "r1e_pmc_tick.json"
+NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only line)
+#   initial tick, per node init 1471 B (9 B check + 4 B index + 1458 B patch), per
+#   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
+INIT_BYTES = 1471
+POD_PATCH_BYTES = 577
+PMC_FILE = "r2_pmc_1M.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
 
 
 def parse():
@@ -61,33 +77,86 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nodes-per-rank", type=int, default=NODES_PER_RANK)
-    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 (N=1)")
-    ap.add_argument("--cpu-nodes", type=int, default=NODES_PER_RANK)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement on rank 0 (N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-core leg (0: all cores)")
+    ap.add_argument("--cpu-ticks", type=int, default=5)
     ap.add_argument("--roofline-ticks", type=int, default=20)
-    ap.add_argument("--no-queue", dest="queue", action="store_false",
-                    help="time kwok_tick one at a time instead of queued submit/collect")
     return ap.parse_args()
 
 
-def cpu_baseline(nodes, ticks=5):
-    """The C oracle (a sequential restatement of the reference controllers)
-    on one host core, same workload shape, bounded to a few steady ticks."""
+def cidr_for(total_pods):
+    return "10.0.0.1/8" if total_pods <= (1 << 24) - 16 else "10.0.0.1/4"
+
+
+def transitions(c):
+    # heartbeat + node init + pod patch + delete + release
+    return c[0] + c[1] + c[2] + c[3] + c[5]
+
+
+def cpu_baseline(nodes, threads, ticks):
+    """The C restatement (oracle/kwok_oracle.c, test infrastructure) on the same
+    fleet: built and initial-ticked with all threads, then `ticks` steady ticks
+    on `threads` threads (its OpenMP sweeps) and on one thread."""
     from oracle.oracle import Oracle  # test infrastructure: baseline only
     t0 = time.perf_counter()
-    o, _, _ = workload.build_engine_fleet(Oracle, nodes)
+    o, _, _ = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=threads), nodes,
+                                          cidr=cidr_for(nodes * workload.PODS_PER_NODE))
+    cores = o.threads
     o.tick(workload.S0 + 30, read=False)  # initial tick (locks + Pending->Running)
     t_init = time.perf_counter() - t0
-    t1 = time.perf_counter()
-    trans = 0
-    for k in range(ticks):
-        r = o.tick(workload.S0 + 60 + 30 * k, read=False)
-        trans += r.counters[0] + r.counters[1] + r.counters[2] + r.counters[3] + r.counters[5]
-    dt = time.perf_counter() - t1
+    legs = {}
+    now = workload.S0 + 60
+    for th in (cores, 1):
+        o.set_threads(th)
+        trans = 0
+        t1 = time.perf_counter()
+        for _ in range(ticks if th > 1 else max(2, ticks // 2)):
+            r = o.tick(now, read=False)
+            now += 30
+            trans += transitions(r.counters)
+        dt = time.perf_counter() - t1
+        legs[th] = (trans / dt, dt / (ticks if th > 1 else max(2, ticks // 2)) * 1e3)
     o.close()
-    return {"value": trans / dt, "unit": "transitions/s", "cores": 1, "kind": "port",
-            "sample": "oracle (C restatement), %d nodes x %d pods, %d steady ticks after the initial tick "
-                      "(setup+initial tick %.1fs)" % (nodes, nodes * 10, ticks, t_init),
-            "ms_per_step": dt / ticks * 1e3}
+    return {"value": legs[cores][0], "unit": "transitions/s", "cores": cores, "kind": "port",
+            "ms_per_step": legs[cores][1],
+            "single_core": {"value": legs[1][0], "cores": 1, "ms_per_step": legs[1][1]},
+            "sample": "oracle/kwok_oracle.c (the C restatement, OpenMP sweeps), the same %d nodes x %d pods "
+                      "fleet, steady ticks after the initial tick (setup + initial tick %.1fs on %d threads); "
+                      "the reference Go controllers cannot run here (no Go toolchain)"
+                      % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
+
+
+class Handoff:
+    """The per-tick hand-off a Go caller consumes: compact
+    arena (one heartbeat body + the patch region), patch / delete lists, and the
+    heartbeat handle list only when its epoch changed."""
+
+    def __init__(self, e):
+        self.e = e
+        self.epoch = None
+        self.bufs = {}
+
+    def buf(self, name, n, dt):
+        b = self.bufs.get(name)
+        if b is None or b.size < n:
+            b = self.bufs[name] = np.empty(max(n, 1), dt)
+        return b
+
+    def read(self, res):
+        hb = self.buf("hb", res.n_heartbeat, np.int32) if res.heartbeat_epoch != self.epoch else None
+        self.epoch = res.heartbeat_epoch
+        arena = self.buf("arena", res.arena_bytes - (res.n_heartbeat - 1) * res.heartbeat_stride
+                         if res.n_heartbeat else res.arena_bytes, np.uint8)
+        p = lambda name, n, dt: self.buf(name, n, dt).ctypes.data  # noqa: E731
+        out = abi.Outputs(hb.ctypes.data if hb is not None else None, 0,
+                          p("ini", res.n_node_init, np.int32), p("ini_off", res.n_node_init, np.uint64),
+                          p("ini_len", res.n_node_init, np.uint32),
+                          p("pp", res.n_pod_patch, np.int32), p("pp_off", res.n_pod_patch, np.uint64),
+                          p("pp_len", res.n_pod_patch, np.uint32),
+                          p("dl", res.n_delete, np.int32), p("dlf", res.n_delete, np.uint8),
+                          arena.ctypes.data, arena.nbytes, abi.READ_HEARTBEAT_ONCE)
+        self.e._check(self.e._lib.kwok_read_outputs(self.e._h, C.byref(out)), "read_outputs")
+        return out.arena_copied
 
 
 def main():
@@ -103,71 +172,88 @@ def main():
         obj = [keng.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = obj[0]
+    total_pods = a.nodes_per_rank * world * workload.PODS_PER_NODE
+    cidr = cidr_for(total_pods)
     t0 = time.perf_counter()
     e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes_per_rank, rank=rank, world=world, device=local,
-                                              comm_id=comm)
+                                              comm_id=comm, cidr=cidr)
     setup_s = time.perf_counter() - t0
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    # ---- initial tick (untimed warmup step 0, measured on its own) ----------
     now = workload.S0 + 30
-    first = None
-    for w in range(a.warmup):
-        r = e.tick(now, read=False)
-        if w == 0:
-            first = dict(zip(keng.abi.COUNTERS, list(r.counters)))
+    barrier()
+    e.profile_enable(True)
+    t1 = time.perf_counter()
+    r0 = e.tick(now, read=False)
+    init_wall = max_over_ranks(time.perf_counter() - t1)
+    ph0, _ = e.profile_read()
+    e.profile_enable(False)
+    first = dict(zip(abi.COUNTERS, list(r0.counters)))
+    now += 30
+    for w in range(1, a.warmup):
+        e.tick(now, read=False)
         now += 30
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    # ---- timed steps: queued submit / collect ----------------------------------
+    barrier()
     e.profile_host(reset=True)
     t0 = time.perf_counter()
     trans = evald = 0
     last = None
-    if a.queue:
-        # tick k+1 is submitted before tick k is collected (kwok_tick_submit /
-        # kwok_tick_collect): the next launch is queued while the host finishes a tick
-        e.tick_submit(now)
-        now += 30
+    e.tick_submit(now)
+    now += 30
     for k in range(a.steps):
-        if not a.queue:
-            r = e.tick(now, read=False)
+        if k + 1 < a.steps:
+            e.tick_submit(now)
             now += 30
-        else:
-            if k + 1 < a.steps:
-                e.tick_submit(now)
-                now += 30
-            r = e.tick_collect(read=False)
+        r = e.tick_collect(read=False)
         c = r.counters
-        trans += c[0] + c[1] + c[2] + c[3] + c[5]
+        trans += transitions(c)
         evald += c[6] + c[7]
         last = r
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
     host_ms, host_n = e.profile_host(reset=True)
-    # the same steps one kwok_tick at a time (reported beside the queued figure)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+
+    # ---- the same steps, one blocking kwok_tick each ---------------------------
+    barrier()
     t1 = time.perf_counter()
     for k in range(a.steps):
         e.tick(now, read=False)
         now += 30
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt_sync = time.perf_counter() - t1
-    if world > 1:
-        t = torch.tensor([dt_sync], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt_sync = float(t[0])
-    # roofline pass: the same ticks with HIP events around each k_tick launch
-    # (kernel-exact hipExtLaunchKernelGGL events) and the kernel's phase stamps
+    barrier()
+    dt_sync = max_over_ranks(time.perf_counter() - t1)
+
+    # ---- the same steps with the per-tick hand-off (queued) --------------------
+    ho = Handoff(e)
+    copied = trans_read = 0
+    barrier()
+    t1 = time.perf_counter()
+    e.tick_submit(now)
+    now += 30
+    for k in range(a.steps):
+        if k + 1 < a.steps:
+            e.tick_submit(now)
+            now += 30
+        r = e.tick_collect(read=False)
+        trans_read += transitions(r.counters)
+        copied += ho.read(r)
+    barrier()
+    dt_read = max_over_ranks(time.perf_counter() - t1)
+
+    # ---- roofline pass: HIP events around each k_tick launch ------------------
     e.profile_enable(True)
     for k in range(a.roofline_ticks):
         e.tick(now, read=False)
@@ -178,13 +264,18 @@ def main():
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
         lc = last.local_counters
-        alg_bytes = NODE_BYTES * lc[8] + POD_BYTES * lc[10]  # nodes_managed, pods_total (this rank)
+        n_nodes, n_pods = lc[8], lc[10]  # nodes_managed, pods_total (this rank)
+        alg_bytes = NODE_BYTES * n_nodes + POD_BYTES * n_pods
+        state_bytes = NODE_STATE_BYTES * n_nodes + POD_BYTES * n_pods
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", PMC_FILE)
         if os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK:
             traffic = json.load(open(pmc))["kernels"]["k_tick"]["hbm_bytes"]
-            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE + WRITE_SIZE per launch, same config)" % PMC_FILE
+            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch, same config)" % PMC_FILE
+        ilc = r0.local_counters
+        init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
+        emit_ms = ph0["emit_kernel"]
         out = {
             "metric": "state transitions/sec at 1M nodes/10M pods, 1-8 MI355X; % HBM roofline",
             "value": trans / dt,
@@ -198,26 +289,44 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": "C2 steady-state heartbeat + status ticks (configs[1])",
+            "config": {"workload": "metric configuration: 1M nodes x 10M pods per GPU, steady-state heartbeat + "
+                                   "status ticks (configs[1]'s tick at the metric's size)",
                        "nodes": fl.total_nodes, "pods": fl.total_nodes * workload.PODS_PER_NODE,
                        "nodes_per_gpu": a.nodes_per_rank, "pods_per_node": workload.PODS_PER_NODE,
-                       "cidr": workload.CIDR, "buckets": workload.BUCKETS, "parallelism": "bucket-sharded x%d" % world},
-            "tick_api": ("kwok_tick_submit/kwok_tick_collect, tick k+1 queued before tick k is collected"
-                         if a.queue else "kwok_tick"),
-            "ms_per_step_kwok_tick": dt_sync / a.steps * 1e3,  # the same steps, one blocking kwok_tick each
+                       "cidr": cidr, "buckets": workload.BUCKETS, "parallelism": "bucket-sharded x%d" % world},
+            "tick_api": "kwok_tick_submit/kwok_tick_collect, tick k+1 queued before tick k is collected",
+            "ms_per_step_kwok_tick": dt_sync / a.steps * 1e3,
+            "ms_per_step_with_handoff": dt_read / a.steps * 1e3,
+            "handoff": {"transitions_per_s": trans_read / dt_read,
+                        "bytes_to_host_per_step": copied / a.steps,
+                        "what": "kwok_read_outputs with KWOK_READ_HEARTBEAT_ONCE (one heartbeat body + patch "
+                                "region + lists; heartbeat handles only when the epoch changes), pageable host "
+                                "buffers, queued ticks"},
             "objects_evaluated_per_s": evald / dt,
             "phase_ms_per_tick": {k: v / max(nt, 1) for k, v in phases.items()},
             "host_ms_per_tick": {k: v / max(host_n, 1) for k, v in host_ms.items()},
-            "initial_tick_counters": first,
+            "initial_tick": {"wall_ms": init_wall * 1e3, "kernel_ms": ph0["kernel"], "k_emit_ms": emit_ms,
+                             "transitions": transitions(r0.counters),
+                             "transitions_per_s": transitions(r0.counters) / init_wall,
+                             "counters": first,
+                             "emit_roofline": {"bound": "hbm", "kernel": "k_emit", "bytes": init_bytes,
+                                               "achieved": init_bytes / (emit_ms * 1e-3) / 1e9 if emit_ms else None,
+                                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                               "frac": init_bytes / (emit_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                               if emit_ms else None}},
             "setup_s": setup_s,
             "roofline": {"bound": "hbm", "kernel": "k_tick", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "bytes_per_launch": alg_bytes, "avg_launch_ms": kern_ms,
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_launch": alg_bytes, "avg_launch_ms": kern_ms, "traffic_source": traffic_src,
                          "timing": "HIP events around each k_tick launch (hipExtLaunchKernelGGL), %d ticks" % nt},
+            "state_only": {"bytes_per_tick": state_bytes,
+                           "achieved": state_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0,
+                           "unit": "GB/s", "classify_ms": phases["classify"] / max(nt, 1),
+                           "note": "SoA state read + written per tick without the materialised heartbeat "
+                                   "bodies, over the same k_tick launch time"},
         }
         if world == 1 and a.cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a.cpu_nodes)
+            out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
         print(json.dumps(out))
     e.close()
     if world > 1:

@@ -638,7 +638,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     uint32_t base = 0;
     if (!slash || !parse_ipv4(cfg->cidr, (size_t)(slash - cfg->cidr), &base)) return bail(KWOK_EDOMAIN);
     int plen = atoi(slash + 1);
-    if (plen < 8 || plen > 32) return bail(KWOK_EDOMAIN);  // pool bitmaps sized for >= /8
+    if (plen < 4 || plen > 32) return bail(KWOK_EDOMAIN);  // pool bitmaps: <= 2^28 addresses (32 MiB each)
     uint32_t mask = plen == 32 ? 0xFFFFFFFFu : (uint32_t)(0xFFFFFFFFull << (32 - plen));
     e->pool.net = base & mask;
     e->pool.base = base;
@@ -1333,6 +1333,7 @@ int retire(kwok_engine* e) {
         // what follows the header in the chain (pool, job lists) beyond the stream, and k_emit
         e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2;
         e->prof_ms[KWOK_T_KERNEL] += kern;
+        e->prof_ms[KWOK_T_EMIT_KERNEL] += k2;
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));

@@ -700,7 +700,7 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
                       NT_RELOCK == 1 && NT_MANAGED == 2 && PHASE_PENDING == 1 && PHASE_RUNNING == 2,
                   "state bit layout");
     constexpr uint32_t M = 0x00010001u;
-    // the CIDR spans at most 2^24 addresses (prefix >= 8): one u32 compare tests it
+    // the CIDR spans at most 2^28 addresses (prefix >= 4): one u32 compare tests it
     const uint32_t net = S.pool.net, size = (uint32_t)S.pool.size;
     GroupMasks m{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll

@@ -259,6 +259,35 @@ class EngineBase:
             deletes=[(int(h), int(f)) for h, f in zip(dl, dlf)],
             arena=ab)
 
+    def read_arrays(self, res=None, heartbeat_once=False):
+        """The tick's outputs as numpy arrays (no per-patch Python objects): for
+        fleets of millions of objects.  Offsets index `arena` directly."""
+        res = res or self.last
+        a = {"heartbeat_nodes": np.empty(res.n_heartbeat, np.int32),
+             "node_init_nodes": np.empty(res.n_node_init, np.int32),
+             "node_init_off": np.empty(res.n_node_init, np.uint64),
+             "node_init_len": np.empty(res.n_node_init, np.uint32),
+             "pod_patch_pods": np.empty(res.n_pod_patch, np.int32),
+             "pod_patch_off": np.empty(res.n_pod_patch, np.uint64),
+             "pod_patch_len": np.empty(res.n_pod_patch, np.uint32),
+             "delete_pods": np.empty(res.n_delete, np.int32),
+             "delete_has_finalizers": np.empty(res.n_delete, np.uint8)}
+        arena = np.empty(max(1, res.arena_bytes), np.uint8)
+        out = abi.Outputs(*[a[k].ctypes.data if k != "heartbeat_off" else 0 for k in
+                            ("heartbeat_nodes", "heartbeat_off", "node_init_nodes", "node_init_off", "node_init_len",
+                             "pod_patch_pods", "pod_patch_off", "pod_patch_len", "delete_pods",
+                             "delete_has_finalizers")],
+                          arena.ctypes.data, arena.nbytes, abi.READ_HEARTBEAT_ONCE if heartbeat_once else 0)
+        self._check(self._fn("read_outputs")(self._h, C.byref(out)), "read_outputs")
+        a["arena"] = arena[:out.arena_copied]
+        a["node_init_off"] -= np.uint64(out.arena_shift)
+        a["pod_patch_off"] -= np.uint64(out.arena_shift)
+        a["heartbeat_off"] = out.heartbeat_off
+        a["heartbeat_len"] = res.heartbeat_len
+        a["heartbeat_stride"] = 0 if heartbeat_once else res.heartbeat_stride
+        a["counters"] = dict(zip(abi.COUNTERS, list(res.counters)))
+        return a
+
     # -- queries ----------------------------------------------------------------
     def node_has(self, name: str) -> bool:
         b = name.encode()
@@ -295,7 +324,7 @@ class Engine(EngineBase):
         self.last = res
         return self.read_outputs(res) if read else res
 
-    PHASES = ("classify", "stream", "header", "exchange", "pool", "emit", "kernel")  # KWOK_T_* order
+    PHASES = ("classify", "stream", "header", "exchange", "pool", "emit", "kernel", "emit_kernel")  # KWOK_T_* order
     HOST = ("enqueue", "wait", "post", "total")  # KWOK_H_* order
 
     def profile_enable(self, on=True):

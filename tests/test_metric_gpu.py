@@ -1,0 +1,84 @@
+"""GPU parity at the metric's own configuration (BASELINE.json metric "at 1M
+nodes/10M pods", north_star "1M simulated nodes / 10M pods stepped per tick"):
+1M nodes x 10M pods on one MI355X against the CPU restatement (its OpenMP
+sweeps), byte for byte on the initial tick (1M node-init patches, 10M
+Pending->Running patches with IP allocation) and on a steady tick (1M
+heartbeats), plus size-independent properties of the allocation.  The
+comparison is vectorised (numpy views over both arenas): the per-patch
+Python objects of the small-trace tests would not fit."""
+import ipaddress
+
+import numpy as np
+import pytest
+from numpy.lib.stride_tricks import as_strided
+
+from kwok_amd import workload
+from kwok_amd.engine import Engine
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+NODES = 1_000_000
+
+
+def rows(arena, off, length):
+    """arena[off[i] : off[i] + length] for every i, as one (n, length) array"""
+    v = as_strided(arena, (arena.size - length + 1, length), (1, 1))
+    return v[off.astype(np.int64)]
+
+
+def compare_patches(ea, eo, el, oa, oo, ol, what):
+    assert (el == ol).all(), what + " lengths"
+    for L in np.unique(el):
+        sel = np.nonzero(el == L)[0]
+        for part in np.array_split(sel, max(1, len(sel) // 1_000_000)):
+            a, b = rows(ea, eo[part], int(L)), rows(oa, oo[part], int(L))
+            bad = np.nonzero((a != b).any(axis=1))[0]
+            assert len(bad) == 0, "%s: %d patches of length %d differ, first at #%d" % (what, len(bad), L, part[bad[0]])
+
+
+def compare_tick(e, o, where):
+    E, O = e.read_arrays(), o.read_arrays()
+    assert E["counters"] == O["counters"], where
+    assert (E["heartbeat_nodes"] == O["heartbeat_nodes"]).all(), where + " heartbeat handles"
+    n = len(E["heartbeat_nodes"])
+    if n:
+        body = O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]
+        hb = E["arena"][E["heartbeat_off"]:E["heartbeat_off"] + n * E["heartbeat_stride"]]
+        hb = hb.reshape(n, E["heartbeat_stride"])[:, :E["heartbeat_len"]]
+        assert (hb == body[None, :]).all(), where + " heartbeat bodies"
+    for k in ("node_init_nodes", "pod_patch_pods", "delete_pods", "delete_has_finalizers"):
+        assert (E[k] == O[k]).all(), where + " " + k
+    compare_patches(E["arena"], E["node_init_off"], E["node_init_len"], O["arena"], O["node_init_off"],
+                    O["node_init_len"], where + " node inits")
+    compare_patches(E["arena"], E["pod_patch_off"], E["pod_patch_len"], O["arena"], O["pod_patch_off"],
+                    O["pod_patch_len"], where + " pod patches")
+    return E["counters"]
+
+
+@pytest.mark.timeout(900)
+def test_metric_config_1m_nodes_10m_pods():
+    e, fl, ph = workload.build_engine_fleet(Engine, NODES)
+    o, _, ph2 = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=0), NODES)
+    assert (ph == ph2).all() and len(ph) == 10 * NODES
+    n_slots = workload.BUCKETS * fl.cp
+    e.tick(workload.S0 + 30, read=False)
+    o.tick(workload.S0 + 30, read=False)
+    c = compare_tick(e, o, "1M tick 0")
+    assert c["pod_patch"] == 10 * NODES and c["node_init"] == NODES and c["alloc"] == 10 * NODES
+    used, phase, hip, pip = e.dump_pods(0, n_slots)
+    live = used.astype(bool)
+    ips = pip[live]
+    base = int(ipaddress.IPv4Address("10.0.0.1"))
+    # ipPool.new hands out base, base+1, ... in canonical (bucket, slot) order (utils.go:68-81)
+    assert (ips == base + np.arange(10 * NODES, dtype=np.uint32)).all()
+    assert (phase[live] == 2).all() and (hip[live] == int(ipaddress.IPv4Address("196.168.0.1"))).all()
+    ou, op, oh, oi = o.dump_pods(0, n_slots)
+    assert (ou == used).all() and (op == phase).all() and (oh == hip).all() and (oi == pip).all()
+    # a steady tick: 1M identical heartbeats, every pod re-checked, nothing patched
+    e.tick(workload.S0 + 60, read=False)
+    o.tick(workload.S0 + 60, read=False)
+    c = compare_tick(e, o, "1M tick 1")
+    assert c["heartbeat"] == NODES and c["pod_patch"] == 0 and c["evaluated"] == 10 * NODES
+    e.close()
+    o.close()

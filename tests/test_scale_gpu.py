@@ -127,9 +127,9 @@ def test_domain_table_engine():
 
 def test_domain_rejections():
     """Configurations outside the supported domain are rejected, never
-    emulated: IPv6 / non-canonical CIDRs, prefixes shorter than /8, custom
+    emulated: IPv6 / non-canonical CIDRs, prefixes shorter than /4, custom
     templates, EnableCNI."""
-    for kw in (dict(cidr="fe80::1/64"), dict(cidr="10.0.0.1/4"), dict(cidr="010.0.0.1/8")):
+    for kw in (dict(cidr="fe80::1/64"), dict(cidr="10.0.0.1/3"), dict(cidr="010.0.0.1/8")):
         with pytest.raises(Exception):
             Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, **kw))
     for field in ("custom_templates", "enable_cni"):
