@@ -62,6 +62,7 @@ struct kwok_engine {
     std::string node_ip_s;
     int64_t start = 0;
     hipStream_t st = nullptr;   // tick pipeline
+    hipEvent_t fence = nullptr; // recorded (system-scope release) before device -> host copies of kernel output
     DevState S{};
 
     // ---- host mirrors (slot policy) ----
@@ -362,6 +363,8 @@ int grow_arena(kwok_engine* e, kwok_engine::TickSlot& T) {  // T holds no queued
     T.arena_cap = 0;
     if (hipMalloc((void**)&T.arena, need) != hipSuccess) return e->fail(KWOK_ENOMEM, "arena %llu", (unsigned long long)need);
     T.arena_cap = need;
+    if (getenv("KWOK_DEBUG_POISON"))  // diagnostics: bytes no kernel writes read as 0xEE, not as stale data
+        HIPCHK(e, hipMemsetAsync(T.arena, 0xEE, need, e->st));
     return KWOK_OK;
 }
 int alloc_slot(kwok_engine* e, int k) {
@@ -515,6 +518,15 @@ int parse_opt_ip(const char* arena, kwok_str s, uint32_t* ip) {
     return KWOK_OK;
 }
 
+// Tick completion events skip the system-scope release (the tick header is
+// written with system-scope stores), so before a copy engine reads what the
+// kernels wrote, record an event that performs it: the kernels' dirty L2 lines
+// (per XCD, not coherent with the copy engine) are written back first.
+int release_for_host(kwok_engine* e) {
+    HIPCHK(e, hipEventRecord(e->fence, e->st));
+    return KWOK_OK;
+}
+
 int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
     if (e->comm) {
         ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, e->comm, e->st);
@@ -523,6 +535,7 @@ int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
     }
     // host-memory exchange through the caller's allgather
     std::vector<char> hs(bytes), hr(bytes * e->W);
+    if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     if (e->cfg.allgather(e->cfg.allgather_user, hs.data(), bytes, hr.data()))
@@ -596,6 +609,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
+    if (e->fence) (void)hipEventDestroy(e->fence);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
 }
@@ -654,6 +668,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     {
         hipError_t r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipEventCreateWithFlags(&e->fence, hipEventDisableTiming);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "stream/event create: %s", hipGetErrorString(r)));
     }
     DevState& S = e->S;
@@ -1134,6 +1149,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     hipStream_t st = e->st;
     T.hdr_h->xovf = 0;
     // the skipped tick's allgather re-gathered the same messages (its FRONT did not run)
+    if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, hipStreamSynchronize(st));
     HIPCHK(e, hipMemcpy(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost));
     uint64_t maxl = 0;
@@ -1464,6 +1480,7 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     };
     o->heartbeat_off = H.hb_base;
+    if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, cp(o->heartbeat_nodes, S.hb_nodes, (size_t)H.n_hb * 4));
     HIPCHK(e, cp(o->node_init_nodes, S.init_nodes, (size_t)H.n_init * 4));
     HIPCHK(e, cp(o->node_init_off, S.init_off, (size_t)H.n_init * 8));
@@ -1553,6 +1570,7 @@ int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used,
     drain(e);
     std::vector<uint16_t> sth(e->PL);
     std::vector<uint32_t> hh(e->PL), ph(e->PL);
+    if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, hipMemcpyAsync(sth.data(), e->S.pod_state, (size_t)e->PL * 2, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(hh.data(), e->S.host_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(ph.data(), e->S.pod_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));

@@ -15,7 +15,12 @@ def compare(e_out, o_out, where):
         hb = o_out.heartbeat_body(0)
         a = np.frombuffer(e_out.arena, np.uint8)[e_out.heartbeat_off:e_out.heartbeat_off + n * e_out.heartbeat_stride]
         a = a.reshape(n, e_out.heartbeat_stride)[:, :e_out.heartbeat_len]
-        assert (a == np.frombuffer(hb, np.uint8)[None, :]).all(), where + " heartbeat bytes"
+        ok = (a == np.frombuffer(hb, np.uint8)[None, :])
+        if not ok.all():
+            bad = np.nonzero(~ok.all(axis=1))[0]
+            pos = np.nonzero(~ok[bad[0]])[0]
+            raise AssertionError("%s heartbeat bytes: %d of %d bodies differ (first #%d at bytes %s); got %r want %r" % (
+                where, len(bad), n, bad[0], list(pos[:8]), bytes(a[bad[0]][pos[0]:pos[0] + 24]), hb[pos[0]:pos[0] + 24]))
         ob = np.frombuffer(o_out.arena, np.uint8)[o_out.heartbeat_off:o_out.heartbeat_off + n * len(hb)]
         assert (ob.reshape(n, len(hb)) == np.frombuffer(hb, np.uint8)[None, :]).all()
     assert [h for h, _ in e_out.node_inits] == [h for h, _ in o_out.node_inits], where + " node-init handles"
