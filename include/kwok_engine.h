@@ -267,7 +267,15 @@ int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res);
  * Results equal kwok_tick's for the same call sequence.  Ingest, spec
  * registration, kwok_pool_put and kwok_dump_pods first finish every submitted
  * tick on the host (their results stay collectable), so events apply after the
- * ticks submitted before them. */
+ * ticks submitted before them.
+ * Multi rank (world_size > 1): every rank must tick the same sequence of ticks
+ * (the exchange messages carry the tick's sequence number; ranks out of step
+ * fail the tick with KWOK_ECOMM), and kwok_tick_submit first finishes the
+ * previous tick on the host, so each rank issues its collectives in the same
+ * order whatever its submit / collect pattern.
+ * A failed tick (KWOK_EDEVICE / KWOK_ECOMM from collect) leaves the device
+ * and host state out of step: every later call fails with KWOK_EDEVICE until the
+ * engine is destroyed and recreated (state rebuilt from a List, as on restart). */
 int kwok_tick_submit(kwok_engine* e, int64_t now_unix);
 int kwok_tick_collect(kwok_engine* e, kwok_tick_result* res);
 int kwok_read_outputs(kwok_engine* e, kwok_outputs* out);

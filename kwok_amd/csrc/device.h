@@ -94,6 +94,7 @@ struct TickHdr {
 
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
 constexpr uint32_t TICK_ERR_LAYOUT = 2;   // device heartbeat count != the host's managed-node count
+constexpr uint32_t TICK_ERR_SEQ = 4;      // multi rank: the gathered messages are of different ticks
 enum : int {
     CLK_ENTRY = 0,   // block 0 starts the tick (FRONT launch)
     CLK_P1_MAX,      // the last chain block arrives (classification complete)
@@ -118,11 +119,14 @@ struct GridBar {
 };
 constexpr int ACC_SHIFT = 54;  // arrivals in the top 10 bits (<= 1023 chain blocks), sums below
 constexpr unsigned long long ACC_MASK = (1ull << ACC_SHIFT) - 1;
+constexpr int MAX_CHAIN = 512;  // k_tick chain blocks (reduce_records' LDS; engine_create clamps to it)
+static_assert(MAX_CHAIN < (1 << (64 - ACC_SHIFT)), "the accumulators count arrivals of every chain block");
 
 // exchange message, one per rank (allgather)
 constexpr int XINLINE = 2048;
 struct XMsg {
-    uint64_t alloc, n_use, n_rel, pad;
+    uint64_t alloc, n_use, n_rel;
+    uint64_t seq;  // the FRONT launch's tick tag: equal on every rank that ticks in step
     uint64_t counters[16];
     uint32_t ips[XINLINE];  // uses then releases (when they fit)
 };

@@ -63,6 +63,7 @@ struct kwok_engine {
     int64_t start = 0;
     hipStream_t st = nullptr;   // tick pipeline
     hipEvent_t fence = nullptr; // recorded (system-scope release) before device -> host copies of kernel output
+    hipStream_t rst = nullptr;  // kwok_read_outputs: copies of a collected tick, beside the next tick's kernels
     DevState S{};
 
     // ---- host mirrors (slot policy) ----
@@ -177,6 +178,10 @@ struct kwok_engine {
     double trace_sum[TRACE_SLOTS + 2][3] = {};  // chain stamps, streamer entry / exit
     uint64_t trace_ticks = 0, trace_seen = 0;
     uint64_t host_ticks = 0;
+    // a failed tick leaves device and host state out of step: every later call
+    // fails with KWOK_EDEVICE (destroy and recreate the engine, re-ingest by List)
+    bool poisoned = false;
+    uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
     int fail(int code, const char* fmt, ...) {
         char b[512];
@@ -348,6 +353,10 @@ int upload_specs(kwok_engine* e) {
 }
 
 int drain(kwok_engine* e);  // finish every queued tick on the host (below)
+int poisoned(kwok_engine* e) {
+    return e->fail(KWOK_EDEVICE, "a failed tick left the engine out of step with the device: destroy it and "
+                                 "recreate it (re-ingest by List)");
+}
 
 // the output arena must hold the worst case of one tick (grown per slot at submit)
 int size_arena(kwok_engine* e) {
@@ -610,6 +619,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
     if (e->fence) (void)hipEventDestroy(e->fence);
+    if (e->rst) (void)hipStreamDestroy(e->rst);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
 }
@@ -621,6 +631,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (cfg->enable_cni || cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates, no CNI
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
         !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
+        cfg->pod_slots_per_bucket > 65528 /* fill marks are u16 */ ||
         !cfg->pod_slots_per_bucket)
         return KWOK_EINVAL;
     int W = cfg->world_size > 0 ? cfg->world_size : 1;
@@ -669,6 +680,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     {
         hipError_t r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
         if (r == hipSuccess) r = hipEventCreateWithFlags(&e->fence, hipEventDisableTiming);
+        if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->rst, hipStreamNonBlocking);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "stream/event create: %s", hipGetErrorString(r)));
     }
     DevState& S = e->S;
@@ -682,7 +694,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_BLOCKS_PER_CU")) want = std::max(1, atoi(v));
         if (const char* v = getenv("KWOK_TICK_STREAMERS_PER_CU")) wants = std::max(1, atoi(v));
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
-        S.n_chain = (uint32_t)(cus * std::min(occ, want));
+        S.n_chain = std::min<uint32_t>((uint32_t)(cus * std::min(occ, want)), (uint32_t)MAX_CHAIN);
         e->n_stream = (uint32_t)(cus * wants);
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
@@ -690,6 +702,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->chain_prio = pr && pr[0] == '1';
         if (const char* v = getenv("KWOK_TICK_STREAM_DELAY_NS")) S.stream_delay = (uint32_t)std::max(0, atoi(v) / 10);
         if (const char* v = getenv("KWOK_TICK_STREAM_SHARE")) e->share_env = std::min(1024, std::max(0, atoi(v)));
+        if (const char* v = getenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")) e->debug_fault_tick = strtoull(v, nullptr, 10);
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
     }
@@ -797,7 +810,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
 int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
                            int32_t* out_id) {
     if (!e || !spec || !out_id) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
+    if (e->poisoned) return poisoned(e);
     auto get = [&](kwok_str s, std::string& o) {
         if ((size_t)s.off + s.len > arena_len) return false;
         o.assign(arena + s.off, s.len);
@@ -850,7 +865,9 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
 int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
                       int32_t* out_handles, int32_t* out_status) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
+    if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     e->gen++;
     int rejected = 0;
@@ -932,7 +949,9 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
     if (!e || (n && !ev)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
+    if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     e->gen++;
     int rejected = 0;
@@ -1058,7 +1077,9 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
 
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     if (!e || (n && !ips)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
+    if (e->poisoned) return poisoned(e);
     e->gen++;
     e->puts.assign(ips, ips + n);
     return flush_ops(e);
@@ -1089,7 +1110,8 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     kwok_engine::TickSlot& T = e->slots[k];
     hipStream_t st = e->st;
     hipEvent_t* ev = e->prof ? T.pev : nullptr;
-    const uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
+    uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
+    if (e->debug_fault_tick && e->front_launches + 1 == e->debug_fault_tick && !requeue) nhb++;  // tests: TICK_ERR_LAYOUT
     if (e->hb_pre_dirty) {
         // heartbeat handles are written in node order at per-chain-block bases:
         // managed nodes of the buckets before each block's range (host-maintained)
@@ -1314,8 +1336,11 @@ int retire(kwok_engine* e) {
         int rc = (err & TICK_ERR_BARRIER)
                      ? e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
                                e->S.n_chain)
+                 : (err & TICK_ERR_SEQ)
+                     ? e->fail(KWOK_ECOMM, "ranks out of step: the gathered exchange messages are of different ticks")
                      : e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
                                (unsigned long long)e->n_managed);
+        e->poisoned = true;
         if (next >= 0) {
             kwok_engine::TickSlot& U = e->slots[next];
             U.state = SLOT_DONE;
@@ -1406,11 +1431,16 @@ int drain(kwok_engine* e) {
 
 extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     if (!e) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
     if (e->nq >= 2) return e->fail(KWOK_EBUSY, "two ticks outstanding: collect one first");
     if (e->nq >= 1 && (e->prof || trace_enabled(e)))
         return e->fail(KWOK_EBUSY, "profiled / traced ticks are not queued behind each other");
     const auto t0 = clk::now();
+    // multi rank: the previous tick is finished (its long-list allgather, if any,
+    // included) before this one's collectives are enqueued, so every rank issues
+    // its collectives in the same order whatever its submit / collect pattern
+    if (e->W > 1) drain(e);
     int k = -1;
     for (int pass = 0; pass < 2 && k < 0; pass++)  // prefer keeping the last collected tick's outputs
         for (int i = 0; i < 2 && k < 0; i++)
@@ -1471,16 +1501,21 @@ extern "C" int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res
 
 int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     if (!e || !o) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     if (e->cur < 0) return e->fail(KWOK_EINVAL, "no collected tick (or its slot was reused by a submit)");
     const kwok_engine::TickSlot& S = e->slots[e->cur];  // outputs of the last collected tick
     const TickHdr& H = *S.hdr_h;
-    hipStream_t st = e->st;
+    // the copies run on their own stream once the tick is done, so they overlap a
+    // tick already queued behind it (kwok_tick_submit before kwok_read_outputs);
+    // the fence event there writes the kernels' L2 lines back for the copy engine
+    hipStream_t st = e->rst;
+    HIPCHK(e, hipStreamWaitEvent(st, S.done, 0));
+    HIPCHK(e, hipEventRecord(e->fence, st));
     auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
         if (!dst || !bytes) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     };
     o->heartbeat_off = H.hb_base;
-    if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, cp(o->heartbeat_nodes, S.hb_nodes, (size_t)H.n_hb * 4));
     HIPCHK(e, cp(o->node_init_nodes, S.init_nodes, (size_t)H.n_init * 4));
     HIPCHK(e, cp(o->node_init_off, S.init_off, (size_t)H.n_init * 8));
@@ -1567,6 +1602,7 @@ uint64_t kwok_node_size(kwok_engine* e) { return e ? e->n_managed : 0; }
 int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase, uint32_t* host_ip,
                    uint32_t* pod_ip) {
     if (!e) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
     drain(e);
     std::vector<uint16_t> sth(e->PL);
     std::vector<uint32_t> hh(e->PL), ph(e->PL);

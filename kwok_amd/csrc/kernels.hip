@@ -556,7 +556,6 @@ __device__ __forceinline__ void block_sum64(uint64_t (&v)[N]) {
 // (sc1 loads: the records may have been published in this launch).  The
 // records are transposed through LDS: thread (f, p) = (t / 16, t % 16) sums
 // field f of records p, p + 16, ... and a 16-lane DPP row reduction finishes.
-constexpr int MAX_CHAIN = 512;
 constexpr int REC_PITCH = AG_STRIDE + 1;  // conflict-free column reads
 struct Sums {
     uint64_t pre[AG_STRIDE], tot[AG_STRIDE];
@@ -1159,7 +1158,7 @@ __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint
 // (skip_alloc) and its stamps (skip_pool) itself, concurrently.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb, uint64_t pool_index,
-                                                   uint64_t c_p1, bool prof) {
+                                                   uint64_t c_p1, bool prof, uint32_t tag) {
     const uint64_t* tot = r.tot;
     const bool single = S.world == 1;
     const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
@@ -1187,6 +1186,7 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
         if (!single) {
             XMsg* X = S.xmsg;
             X->alloc = tot[AG_ALLOC];
+            X->seq = tag;
             X->n_use = nu;
             X->n_rel = nr;
             constexpr int LC = offsetof(TickHdr, local_counters) / 8;
@@ -1620,7 +1620,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if ((old + 1) % S.n_chain == 0) {
                 const uint64_t c = __builtin_amdgcn_s_memrealtime();
                 reduce_records(S, b, 0, recs, &sums);
-                write_front_header(S, sums, n_hb, pool_index, c, (phases & TICK_PROF) != 0);
+                write_front_header(S, sums, n_hb, pool_index, c, (phases & TICK_PROF) != 0, tag);
                 if (t < 2) S.emit_n[t] = 0u;  // set by BACK once it builds the jobs
                 TSTAMP(7);
             }
@@ -1637,13 +1637,16 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         const XMsg* X = S.xall;
         uint64_t base = 0;
         uint32_t maxl = 0;
+        bool step = true;
         for (int r = 0; r < S.world; r++) {
             const uint64_t al = X[r].alloc;
             xA += al;
             if (r < S.rank) base += al;
             xrel += X[r].n_rel;
             maxl = max(maxl, (uint32_t)(X[r].n_use + X[r].n_rel));
+            step &= X[r].seq == tag;
         }
+        if (!step && b == 0 && t == 0) st_host(&S.hdr_host->err, TICK_ERR_SEQ);  // ranks out of step: results void
         xbase = base;
         if (!(phases & TICK_XLISTS)) {
             if (maxl > (uint32_t)XINLINE) {

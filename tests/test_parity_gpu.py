@@ -61,3 +61,34 @@ def test_engine_compact_readout(name):
         if e0 == e1:
             assert h0 == h1
     e.close()
+
+
+def test_failed_tick_poisons_engine(monkeypatch):
+    """A tick that fails on the device (here a forced heartbeat-layout mismatch,
+    KWOK_DEBUG_LAYOUT_FAULT_TICK) is reported by collect, and every later call
+    fails with KWOK_EDEVICE instead of running on host mirrors that no longer
+    match the device (destroy / recreate is the recovery)."""
+    from kwok_amd.engine import KwokError
+    fx = harness.load_trace("churn")
+    monkeypatch.setenv("KWOK_DEBUG_LAYOUT_FAULT_TICK", "2")
+    e = Engine(harness.config_for(fx))
+    monkeypatch.delenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")
+    specs = harness.SpecCache(e)
+    t = fx["ticks"]
+    recs, ar = harness.node_batch(t[0]["node_events"])
+    e.ingest_nodes_raw(recs, ar)
+    recs, ar = harness.pod_batch(t[0]["pod_events"], specs)
+    e.ingest_pods_raw(recs, ar)
+    e.tick(t[0]["now"])
+    with pytest.raises(KwokError) as ex:
+        e.tick(t[1]["now"])
+    assert ex.value.code == abi.EDEVICE
+    for call in (lambda: e.tick(t[1]["now"] + 30), lambda: e.ingest_nodes_raw(*harness.node_batch(t[0]["node_events"])),
+                 lambda: e.dump_pods(0, 8)):
+        with pytest.raises(KwokError) as ex:
+            call()
+        assert ex.value.code == abi.EDEVICE and "recreate" in str(ex.value)
+    e.close()
+    e = Engine(harness.config_for(fx))  # a fresh engine replays the trace
+    harness.replay(fx, e)
+    e.close()
