@@ -759,8 +759,11 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)i;
         for (uint16_t o : hb.start_slots)
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)(TS_LEN + i);
-        hipError_t r = hipMemcpy((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice);
-        if (r == hipSuccess) r = hipMemcpy((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice);
+        // on the engine's stream, after dalloc's zero fills (a null-stream copy is
+        // not ordered with a non-blocking stream: the fill could land after it)
+        hipError_t r = hipMemcpyAsync((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice, e->st);
+        if (r == hipSuccess) r = hipMemcpyAsync((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice, e->st);
+        if (r == hipSuccess) r = hipStreamSynchronize(e->st);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
     {
@@ -1173,7 +1176,8 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     // the skipped tick's allgather re-gathered the same messages (its FRONT did not run)
     if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, hipStreamSynchronize(st));
-    HIPCHK(e, hipMemcpy(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
     uint64_t maxl = 0;
     for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
     if (maxl > e->xlist_cap) {
@@ -1247,8 +1251,9 @@ void trace_tick(kwok_engine* e) {
     if ((int)++e->trace_seen <= skip) return;  // skip the initial (bulk) ticks
     const size_t TS = TRACE_SLOTS;
     e->trace_h.assign(N * TS, 0);
-    if (hipMemcpy(e->trace_h.data(), e->S.trace, N * TS * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    (void)hipMemset(e->S.trace, 0, N * TS * 8);
+    if (release_for_host(e) || hipMemcpyAsync(e->trace_h.data(), e->S.trace, N * TS * 8, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+        hipMemsetAsync(e->S.trace, 0, N * TS * 8, e->st) != hipSuccess || hipStreamSynchronize(e->st) != hipSuccess)
+        return;
     uint64_t t0 = ~0ull;
     for (size_t b = 0; b < G; b++) t0 = std::min(t0, e->trace_h[b * TS]);
     // stamps a block did not reach this tick (a clean block skips the pool phase) are 0
@@ -1331,7 +1336,8 @@ int retire(kwok_engine* e) {
         const uint32_t err = H.err;
         // a tick queued behind a failed one ran on its state: fail it as well
         (void)hipStreamSynchronize(e->st);
-        (void)hipMemset(e->S.bar, 0, sizeof(GridBar));  // the next tick starts from a clean count
+        (void)hipMemsetAsync(e->S.bar, 0, sizeof(GridBar), e->st);  // the next tick starts from a clean count
+        (void)hipStreamSynchronize(e->st);
         e->front_launches = 0;
         int rc = (err & TICK_ERR_BARRIER)
                      ? e->fail(KWOK_EDEVICE, "k_tick cross-block wait timed out (%u chain blocks not co-resident?)",
@@ -1360,8 +1366,10 @@ int retire(kwok_engine* e) {
         const double kern = (double)k0 + k1 + k2;
         // the streamers' latest exit, kept on the device (they never touch the header)
         unsigned long long send = 0;
-        (void)hipMemcpy(&send, &e->S.bar->stream_end_max, 8, hipMemcpyDeviceToHost);
-        (void)hipMemset(&e->S.bar->stream_end_max, 0, 8);
+        (void)release_for_host(e);
+        (void)hipMemcpyAsync(&send, &e->S.bar->stream_end_max, 8, hipMemcpyDeviceToHost, e->st);
+        (void)hipMemsetAsync(&e->S.bar->stream_end_max, 0, 8, e->st);
+        (void)hipStreamSynchronize(e->st);
         T.hdr_h->clk[CLK_STREAM_END] = send;
         auto span = [&](int a, int b) { return H.clk[b] > H.clk[a] ? (double)(H.clk[b] - H.clk[a]) * 1e-5 : 0.0; };
         const double classify = span(CLK_ENTRY_MIN, CLK_P1_MAX), stream = span(CLK_ENTRY_MIN, CLK_STREAM_END);
