@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-core leg (0: all cores)")
     ap.add_argument("--cpu-ticks", type=int, default=5)
     ap.add_argument("--roofline-ticks", type=int, default=20)
+    ap.add_argument("--churn-ticks", type=int, default=5, help="C4 churn ticks after the steady legs (N=1; 0: skip)")
+    ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
+                                                         "metric size: 2M create/delete per tick)")
     return ap.parse_args()
 
 
@@ -124,6 +127,57 @@ def cpu_baseline(nodes, threads, ticks):
                       "fleet, steady ticks after the initial tick (setup + initial tick %.1fs on %d threads); "
                       "the reference Go controllers cannot run here (no Go toolchain)"
                       % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
+
+
+def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
+    """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
+    for deletion (Modified events with their status, half with finalizers) and
+    n_churn new Pending pods on the same nodes (workload.Churn).  A step =
+    kwok_ingest_pods of that batch (2 x n_churn records, host threads + H2D +
+    apply kernel) + one kwok_tick (1M deletes + releases, 1M Pending->Running
+    patches reusing the released IPs).  Event generation (which reads the pod
+    IPs back) sits between the timed steps.  The first step is warmup."""
+    n_handles = workload.BUCKETS * fl.cp
+    ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=7)
+    dump = lambda: e.dump_pods(0, n_handles)  # noqa: E731
+    ing = tck = 0.0
+    trans = recs = 0
+    kern = emit = 0.0
+    last = None
+    for k in range(ticks + 1):
+        ev, ar = ch.batch(dump, now)
+        torch.cuda.synchronize()
+        if k:
+            e.profile_enable(True)
+        t0 = time.perf_counter()
+        hs, st, _ = e.ingest_pods_raw(ev, ar)
+        t1 = time.perf_counter()
+        r = e.tick(now, read=False)
+        t2 = time.perf_counter()
+        ch.applied(hs, st)
+        now += 30
+        if k:
+            ph, nt = e.profile_read()
+            e.profile_enable(False)
+            kern += ph["kernel"]
+            emit += ph["emit_kernel"]
+            ing += t1 - t0
+            tck += t2 - t1
+            trans += transitions(r.counters)
+            recs += len(ev)
+            last = dict(zip(abi.COUNTERS, list(r.counters)))
+    return now, {
+        "workload": "C4 pod churn storm (BASELINE configs[3]) on the metric fleet: %d deletion-marked pods (50%% with "
+                    "finalizers) + %d creates per tick" % (n_churn, n_churn),
+        "ticks": ticks, "records_per_tick": recs // max(ticks, 1),
+        "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
+        "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
+        "ingest_records_per_s": recs / ing if ing else None,
+        "tick_transitions_per_s": trans / tck if tck else None,
+        "kernel_ms": kern / ticks, "k_emit_ms": emit / ticks,
+        "counters_last_tick": last,
+        "note": "ingest = kwok_ingest_pods (record validation, IP parsing, slot policy on host threads, "
+                "H2D of the coalesced ops, k_apply_pod_ops); event generation between steps untimed"}
 
 
 class Handoff:
@@ -261,6 +315,10 @@ def main():
     phases, nt = e.profile_read()
     e.profile_enable(False)
 
+    churn = None
+    if world == 1 and a.churn_ticks > 0:
+        now, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank)
+
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
         lc = last.local_counters
@@ -325,6 +383,8 @@ def main():
                            "note": "SoA state read + written per tick without the materialised heartbeat "
                                    "bodies, over the same k_tick launch time"},
         }
+        if churn is not None:
+            out["churn"] = churn
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
         print(json.dumps(out))

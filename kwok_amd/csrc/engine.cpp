@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -73,7 +74,7 @@ struct kwok_engine {
         uint32_t refs = 0;
     };
     std::vector<HNode> nodes;                        // [NL]
-    std::unordered_map<std::string, uint32_t> node_by_name;  // -> local slot
+    std::vector<std::unordered_map<std::string, uint32_t>> node_by_name;  // [nb] per owned bucket: name -> local slot
     std::vector<uint64_t> node_bits;                 // occupancy bitset per bucket
     uint64_t n_managed = 0;
     std::vector<uint32_t> mb_count;                  // [nb] managed nodes per owned bucket
@@ -81,20 +82,40 @@ struct kwok_engine {
     uint32_t hb_epoch = 0;                           // kwok_tick_result.heartbeat_epoch: bumped when the managed set changes
     uint32_t* hb_pre_h = nullptr;                    // pinned [n_chain + 1]
     uint32_t* d_hb_pre = nullptr;
-    std::vector<uint8_t> pod_used, pod_delpend;      // [PL]
-    std::vector<uint16_t> pod_node;                  // [PL] local node index in bucket
+    struct HPod {  // one cache line fetch per pod record
+        uint16_t node;    // local node index in the bucket
+        uint8_t used, delpend;
+        uint32_t stamp, opi;  // op coalescing: the op of the unflushed batch (stamp == gen) at stage index opi
+    };
+    std::vector<HPod> pods;                          // [PL]
     std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
     std::vector<uint16_t> pod_fill;                  // per bucket: upper bound of used slots (only grows)
-    bool pod_fill_dirty = false;
     uint16_t* d_pod_fill = nullptr;
-    std::vector<uint32_t> pending_del;               // DeletePods routed since the last submit
 
-    // ---- batch staging ----
-    std::vector<NodeOp> nops;
-    std::vector<PodOp> pops;
-    std::vector<uint32_t> node_stamp, pod_stamp, node_opi, pod_opi;
-    uint32_t gen = 0;
-    std::vector<uint32_t> puts;
+    // ---- batch staging, one Stage per ingest partition ----
+    // Partition p owns the bucket range [p*nb/n_part, (p+1)*nb/n_part): every op on
+    // a slot of those buckets is staged (and coalesced) in stage[p], so partitions
+    // run on their own host threads with no shared writes.  Slot policy, op
+    // coalescing and event order are per bucket, so results do not depend on
+    // n_part.
+    struct Stage {
+        std::vector<NodeOp> nops;
+        std::vector<PodOp> pops;
+        std::vector<uint32_t> puts;         // ingest-time Puts (Deleted events)
+        std::vector<uint32_t> pending_del;  // DeletePods routed since the last submit
+        bool fill_dirty = false;            // a pod fill mark of the partition grew
+        int rejected = 0;
+    };
+    std::vector<Stage> stage;
+    int n_part = 1;
+    std::vector<uint32_t> node_stamp, node_opi;  // opi: index in the slot's stage
+    uint32_t gen = 1;  // ops of the unflushed batch carry stamp == gen (flush_ops advances it)
+    // threaded-ingest scratch, kept between calls (fresh allocations would page-fault
+    // on first touch, from every thread at once)
+    std::vector<uint32_t> ing_bkt;
+    std::vector<uint64_t> ing_res;
+    std::vector<std::vector<uint32_t>> ing_order;  // [n_part]
+    Stage& stage_of(uint32_t bucket_local) { return stage[(size_t)((uint64_t)bucket_local * n_part / nb)]; }
     void* pinned = nullptr;
     size_t pinned_cap = 0;
     void* d_ops = nullptr;
@@ -141,7 +162,7 @@ struct kwok_engine {
         uint64_t now = 0, target = 0;
         uint32_t tag = 0;
         uint32_t epoch = 0;         // heartbeat_epoch of the tick
-        std::vector<uint32_t> pending_del;  // pods whose DeletePod this tick emits
+        std::vector<std::vector<uint32_t>> pending_del;  // [n_part] pods whose DeletePod this tick emits
         int rc = 0;
         std::string err;
         kwok_tick_result res{};
@@ -181,6 +202,7 @@ struct kwok_engine {
     // a failed tick leaves device and host state out of step: every later call
     // fails with KWOK_EDEVICE (destroy and recreate the engine, re-ingest by List)
     bool poisoned = false;
+    bool iprof = false;  // KWOK_INGEST_PROF=1: host ingest / retire phase times on stderr
     uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
     int fail(int code, const char* fmt, ...) {
@@ -262,29 +284,46 @@ void set_bit(std::vector<uint64_t>& bits, uint32_t cap, uint32_t bucket_local, u
     else w &= ~(1ull << (idx & 63));
 }
 
+// Run f(p) for every ingest partition p: on n_part host threads when the batch
+// is large enough to pay for them, else in order on the caller's thread.
+template <class F>
+void run_parts(kwok_engine* e, bool parallel, F&& f) {
+    if (!parallel || e->n_part == 1) {
+        for (int p = 0; p < e->n_part; p++) f(p);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)e->n_part - 1);
+    for (int p = 1; p < e->n_part; p++) th.emplace_back([&f, p] { f(p); });
+    f(0);
+    for (auto& t : th) t.join();
+}
+constexpr size_t PAR_MIN = 32768;  // records (or deletes) per call before the partitions get threads
+
 // ---- per-batch op coalescing: ops for the same slot compose in order ----
 void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
+    auto& g = e->stage_of(slot / e->Cn);
     if (e->node_stamp[slot] == e->gen) {
-        NodeOp& o = e->nops[e->node_opi[slot]];
+        NodeOp& o = g.nops[e->node_opi[slot]];
         o.or_bits = (uint8_t)((o.or_bits & and_mask) | or_bits);
         o.and_mask = (uint8_t)(o.and_mask & and_mask);
         if (set_blob) o.set_blob = 1, o.blob = blob;
         return;
     }
     e->node_stamp[slot] = e->gen;
-    e->node_opi[slot] = (uint32_t)e->nops.size();
+    e->node_opi[slot] = (uint32_t)g.nops.size();
     NodeOp o{};
     o.slot = slot;
     o.and_mask = and_mask;
     o.or_bits = or_bits;
     o.set_blob = set_blob;
     o.blob = blob;
-    e->nops.push_back(o);
+    g.nops.push_back(o);
 }
-void pod_op(kwok_engine* e, const PodOp& in) {
-    uint32_t slot = in.slot;
-    if (e->pod_stamp[slot] == e->gen) {
-        PodOp& o = e->pops[e->pod_opi[slot]];
+void pod_op(kwok_engine* e, kwok_engine::Stage& g, const PodOp& in) {
+    auto& hp = e->pods[in.slot];
+    if (hp.stamp == e->gen) {
+        PodOp& o = g.pops[hp.opi];
         o.bits = (uint16_t)((o.bits & in.keep_mask) | in.bits);
         o.keep_mask = (uint16_t)(o.keep_mask & in.keep_mask);
         if (in.set_fields) {
@@ -293,37 +332,65 @@ void pod_op(kwok_engine* e, const PodOp& in) {
         }
         return;
     }
-    e->pod_stamp[slot] = e->gen;
-    e->pod_opi[slot] = (uint32_t)e->pops.size();
-    e->pops.push_back(in);
+    hp.stamp = e->gen;
+    hp.opi = (uint32_t)g.pops.size();
+    g.pops.push_back(in);
+}
+bool node_ops_pending(const kwok_engine* e) {
+    for (const auto& g : e->stage)
+        if (!g.nops.empty()) return true;
+    return false;
 }
 
+// Every partition's staged ops -> one host-to-device copy -> the apply kernels.
+// Each slot has at most one op per batch (coalesced), so the kernels apply them
+// in any order.
 int flush_ops(kwok_engine* e) {
-    size_t nb = e->nops.size() * sizeof(NodeOp), pb = e->pops.size() * sizeof(PodOp), ub = e->puts.size() * 4;
-    size_t total = ((nb + 255) & ~(size_t)255) + ((pb + 255) & ~(size_t)255) + ub + 256;
-    int rc = ensure_pinned(e, total);
+    size_t nn = 0, np = 0, nu = 0;
+    bool fill = false;
+    for (const auto& g : e->stage) nn += g.nops.size(), np += g.pops.size(), nu += g.puts.size(), fill |= g.fill_dirty;
+    const size_t nb = nn * sizeof(NodeOp), pb = np * sizeof(PodOp), ub = nu * 4;
+    const size_t po = (nb + 255) & ~(size_t)255, uo = po + ((pb + 255) & ~(size_t)255);
+    int rc = ensure_pinned(e, uo + ub + 256);
     if (rc) return rc;
     char* h = (char*)e->pinned;
-    size_t po = (nb + 255) & ~(size_t)255, uo = po + ((pb + 255) & ~(size_t)255);
-    memcpy(h, e->nops.data(), nb);
-    memcpy(h + po, e->pops.data(), pb);
-    memcpy(h + uo, e->puts.data(), ub);
+    std::vector<size_t> at(3 * (size_t)e->n_part);  // each partition's first node op / pod op / put
+    for (size_t p = 0, a = 0, b = 0, c = 0; p < (size_t)e->n_part; p++) {
+        at[3 * p] = a, at[3 * p + 1] = b, at[3 * p + 2] = c;
+        a += e->stage[p].nops.size(), b += e->stage[p].pops.size(), c += e->stage[p].puts.size();
+    }
+    run_parts(e, np + nn >= PAR_MIN, [&](int p) {  // pinned memcpy: ~2 GB/s per thread
+        auto& g = e->stage[(size_t)p];
+        if (!g.nops.empty()) memcpy(h + at[3 * p] * sizeof(NodeOp), g.nops.data(), g.nops.size() * sizeof(NodeOp));
+        if (!g.pops.empty()) memcpy(h + po + at[3 * p + 1] * sizeof(PodOp), g.pops.data(), g.pops.size() * sizeof(PodOp));
+        if (!g.puts.empty()) memcpy(h + uo + at[3 * p + 2] * 4, g.puts.data(), g.puts.size() * 4);
+    });
+    const auto tf0 = std::chrono::steady_clock::now();
     char* d = (char*)e->d_ops;
     HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
-    if (e->pod_fill_dirty) {  // before the ops that fill the new slots are visible to a tick
+    if (fill) {  // before the ops that fill the new slots are visible to a tick
         HIPCHK(e, hipMemcpyAsync(e->d_pod_fill, e->pod_fill.data(), e->pod_fill.size() * 2, hipMemcpyHostToDevice,
                                  e->st));
-        e->pod_fill_dirty = false;
     }
-    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)e->nops.size(), (const PodOp*)(d + po),
-                     (uint32_t)e->pops.size(), e->st);
-    if (!e->puts.empty())  // ingest-time Puts (Deleted events, pod_controller.go:329-336)
-        launch_pool_puts_now(e->S, (const uint32_t*)(d + uo), (uint32_t)e->puts.size(), e->st);
+    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)nn, (const PodOp*)(d + po), (uint32_t)np, e->st);
+    if (nu)  // ingest-time Puts (Deleted events, pod_controller.go:329-336)
+        launch_pool_puts_now(e->S, (const uint32_t*)(d + uo), (uint32_t)nu, e->st);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->st));
-    e->nops.clear();
-    e->pops.clear();
-    e->puts.clear();
+    if (e->iprof && np + nn > 1000)
+        fprintf(stderr, "[kwok flush] %zu node + %zu pod ops, %zu puts: %.2f MB, device copy + apply %.2f ms\n", nn, np,
+                nu, (uo + ub) / 1e6, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
+    for (auto& g : e->stage) {
+        g.nops.clear();
+        g.pops.clear();
+        g.puts.clear();
+        g.fill_dirty = false;
+    }
+    if (++e->gen == 0) {  // stamps wrapped: forget them all
+        std::fill(e->node_stamp.begin(), e->node_stamp.end(), 0u);
+        for (auto& hp : e->pods) hp.stamp = 0;
+        e->gen = 1;
+    }
     return KWOK_OK;
 }
 
@@ -489,7 +556,7 @@ bool node_conforms(const kwok_node_event& ev, const std::string info[10]) {
 void free_node_if_unused(kwok_engine* e, uint32_t slot) {
     auto& n = e->nodes[slot];
     if (n.used && !n.exists && n.refs == 0) {
-        e->node_by_name.erase(n.name);
+        e->node_by_name[slot / e->Cn].erase(n.name);
         set_bit(e->node_bits, e->Cn, slot / e->Cn, slot % e->Cn, false);
         n = kwok_engine::HNode();
         node_op(e, slot, 0, 0, true, 0);
@@ -498,14 +565,15 @@ void free_node_if_unused(kwok_engine* e, uint32_t slot) {
 
 // find (or create a placeholder for) the node entry of `name`
 int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_t* out) {
+    const uint32_t b = fnv1a32(name, len) & (e->B - 1);
+    if (!e->owns(b)) return KWOK_ENOTMINE;
+    auto& byname = e->node_by_name[b - e->b_lo];
     std::string key(name, len);
-    auto it = e->node_by_name.find(key);
-    if (it != e->node_by_name.end()) {
+    auto it = byname.find(key);
+    if (it != byname.end()) {
         *out = it->second;
         return KWOK_OK;
     }
-    uint32_t b = fnv1a32(name, len) & (e->B - 1);
-    if (!e->owns(b)) return KWOK_ENOTMINE;
     if (!create) return KWOK_ENOTFOUND;
     int32_t idx = first_free(e->node_bits, b - e->b_lo, e->Cn);
     if (idx < 0) return KWOK_EFULL;
@@ -515,7 +583,7 @@ int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_
     n = kwok_engine::HNode();
     n.used = 1;
     n.name = key;
-    e->node_by_name.emplace(key, slot);
+    byname.emplace(std::move(key), slot);
     *out = slot;
     return KWOK_OK;
 }
@@ -703,6 +771,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_STREAM_DELAY_NS")) S.stream_delay = (uint32_t)std::max(0, atoi(v) / 10);
         if (const char* v = getenv("KWOK_TICK_STREAM_SHARE")) e->share_env = std::min(1024, std::max(0, atoi(v)));
         if (const char* v = getenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")) e->debug_fault_tick = strtoull(v, nullptr, 10);
+        e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
     }
@@ -791,15 +860,21 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->nodes.resize(e->NL);
     e->node_bits.assign((size_t)e->nb * ((e->Cn + 63) / 64), 0);
     e->mb_count.assign(e->nb, 0);
-    e->pod_used.assign(e->PL, 0);
-    e->pod_delpend.assign(e->PL, 0);
-    e->pod_node.assign(e->PL, 0);
+    e->node_by_name.resize(e->nb);
+    e->pods.assign(e->PL, kwok_engine::HPod{0, 0, 0, 0, 0});
+    {
+        // host ingest partitions (threads): KWOK_INGEST_THREADS, else up to 16
+        unsigned hw = std::thread::hardware_concurrency();
+        int np = (int)std::min(16u, hw ? hw : 1u);
+        if (const char* v = getenv("KWOK_INGEST_THREADS")) np = atoi(v);
+        e->n_part = std::max(1, std::min(np, (int)std::min<uint32_t>(e->nb, 64)));
+        e->stage.resize((size_t)e->n_part);
+        for (auto& T : e->slots) T.pending_del.resize((size_t)e->n_part);
+    }
     e->pod_bits.assign((size_t)e->nb * ((e->Cp + 63) / 64), 0);
     e->pod_fill.assign(e->nb, 0);
     e->node_stamp.assign(e->NL, 0);
     e->node_opi.assign(e->NL, 0);
-    e->pod_stamp.assign(e->PL, 0);
-    e->pod_opi.assign(e->PL, 0);
     e->max_init_len = 0;
     if ((rc = size_arena(e)) || (rc = grow_arena(e, e->slots[0]))) return bail(rc);
     {
@@ -872,7 +947,6 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
-    e->gen++;
     int rejected = 0;
     for (size_t i = 0; i < n; i++) {
         const kwok_node_event& x = ev[i];
@@ -951,48 +1025,70 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
 
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
-    if (!e || (n && !ev)) return KWOK_EINVAL;
+    if (!e || (n && !ev) || n > 0xFFFFFFFFull) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
-    e->gen++;
-    int rejected = 0;
     const int32_t pbase = (int32_t)(e->b_lo * e->Cp);
-    for (size_t i = 0; i < n; i++) {
+    auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+    // The bucket (owned, local) whose slots a record changes, or -1 when it changes
+    // nothing but its own out_status (it is rejected).  A record's partition
+    // processes it; records of one bucket keep their batch order.
+    auto bucket_of_record = [&](const kwok_pod_event& x) -> int64_t {
+        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) return -1;
+        if (x.handle >= 0) {
+            const int64_t l = (int64_t)x.handle - pbase;
+            return l >= 0 && l < (int64_t)e->PL ? l / e->Cp : -1;
+        }
+        if (x.op != KWOK_OP_UPSERT) return -1;
+        if (x.node_handle >= 0) {
+            const int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
+            return l >= 0 && l < (int64_t)e->NL ? l / e->Cn : -1;
+        }
+        if (!x.node_name.len || x.node_name.len > 253) return -1;
+        const uint32_t b = fnv1a32(arena + x.node_name.off, x.node_name.len) & (e->B - 1);
+        return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
+    };
+    // WatchPods / ListPods event switch (pod_controller.go:301-343) for one record
+    struct Res {
+        int32_t handle, st;
+        uint32_t released;
+    };
+    auto ingest_one = [&](size_t i, kwok_engine::Stage& g) -> Res {
         const kwok_pod_event& x = ev[i];
         int st = KWOK_OK;
         int32_t handle = -1;
-        if (out_released) out_released[i] = 0;
-        auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+        uint32_t released = 0;
         if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) st = KWOK_EDOMAIN;
         uint32_t slot = 0;
-        bool existing = x.handle >= 0;
+        const bool existing = x.handle >= 0;
         if (st == KWOK_OK && existing) {
             int64_t l = (int64_t)x.handle - pbase;
             if (l < 0 || l >= (int64_t)e->PL) {
                 uint32_t gb = (uint32_t)x.handle / e->Cp;
                 st = (x.handle >= 0 && gb < e->B) ? KWOK_ENOTMINE : KWOK_ENOTFOUND;
-            } else if (!e->pod_used[(uint32_t)l]) st = KWOK_ENOTFOUND;
+            } else if (!e->pods[(uint32_t)l].used) st = KWOK_ENOTFOUND;
             else slot = (uint32_t)l;
         }
         if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
             if (!existing) st = KWOK_EINVAL;
             else {
-                uint32_t nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
+                auto& hp = e->pods[slot];
+                uint32_t nslot = (slot / e->Cp) * e->Cn + hp.node;
                 auto& hn = e->nodes[nslot];
                 uint32_t ip = 0;
                 // pod_controller.go:329-336: release the event object's podIP if the node is managed
                 if (hn.managed && x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip) &&
                     (uint64_t)(ip - e->pool.net) < e->pool.size && ip >= e->pool.net) {
-                    e->puts.push_back(ip);
-                    if (out_released) out_released[i] = ip;
+                    g.puts.push_back(ip);
+                    released = ip;
                 }
                 PodOp o{};
                 o.slot = slot;
-                pod_op(e, o);  // state = 0
-                e->pod_used[slot] = 0;
-                e->pod_delpend[slot] = 0;
+                pod_op(e, g, o);  // state = 0
+                hp.used = 0;
+                hp.delpend = 0;
                 set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
                 hn.refs--;
                 free_node_if_unused(e, nslot);
@@ -1027,18 +1123,19 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                         set_bit(e->pod_bits, e->Cp, bl, (uint32_t)idx, true);
                         if ((uint32_t)idx + 1 > e->pod_fill[bl]) {
                             e->pod_fill[bl] = (uint16_t)std::min<uint32_t>(e->Cp, ((uint32_t)idx + 8) & ~7u);
-                            e->pod_fill_dirty = true;
+                            g.fill_dirty = true;
                         }
-                        e->pod_used[slot] = 1;
-                        e->pod_node[slot] = (uint16_t)(nslot % e->Cn);
+                        e->pods[slot].used = 1;
+                        e->pods[slot].node = (uint16_t)(nslot % e->Cn);
                         e->nodes[nslot].refs++;
                     }
                 }
             } else if (st == KWOK_OK) {
-                nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
+                nslot = (slot / e->Cp) * e->Cn + e->pods[slot].node;
             }
             if (st == KWOK_OK) {
                 const auto& hn = e->nodes[nslot];
+                auto& hp = e->pods[slot];
                 uint16_t bits = (uint16_t)(PS_USED | ((uint16_t)x.phase << PS_PHASE_SHIFT));
                 if (x.flags & KWOK_POD_DISREGARD) bits |= PS_DISREGARD;
                 if (x.flags & KWOK_POD_HAS_FINALIZERS) bits |= PS_HAS_FIN;
@@ -1048,8 +1145,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 if (x.flags & KWOK_POD_DELETING) {
                     if (hn.managed) {  // pod_controller.go:306-308 -> deletePodChan
                         bits |= PS_DELETE_PENDING;
-                        if (!e->pod_delpend[slot]) e->pending_del.push_back(slot);
-                        e->pod_delpend[slot] = 1;
+                        if (!hp.delpend) g.pending_del.push_back(slot);
+                        hp.delpend = 1;
                     }
                 } else if (hn.managed && !(x.flags & KWOK_POD_DISREGARD)) {
                     bits |= PS_EVENT;  // needLockPod (:252-269) -> lockPodChan
@@ -1059,22 +1156,128 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 o.keep_mask = existing ? (uint16_t)(PS_EVENT | PS_DELETE_PENDING) : 0;
                 o.bits = bits;
                 o.set_fields = 1;
-                o.node = e->pod_node[slot];
+                o.node = hp.node;
                 o.spec = (uint16_t)x.spec_id;
                 o.ctime = (uint32_t)x.creation_unix;
                 o.host_ip = hip;
                 o.pod_ip = pip;
-                pod_op(e, o);
+                pod_op(e, g, o);
                 handle = pbase + (int32_t)slot;
             }
         } else if (st == KWOK_OK) {
             st = KWOK_EINVAL;
         }
-        if (out_handles) out_handles[i] = handle;
-        if (out_status) out_status[i] = st;
-        if (st != KWOK_OK) rejected++;
+        if (st != KWOK_OK) g.rejected++;
+        return Res{handle, st, released};
+    };
+    auto put = [&](size_t i, const Res& r) {
+        if (out_handles) out_handles[i] = r.handle;
+        if (out_status) out_status[i] = r.st;
+        if (out_released) out_released[i] = r.released;
+    };
+    for (auto& g : e->stage) g.rejected = 0;
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto tp1 = tp0;
+    if (n < PAR_MIN || e->n_part == 1) {
+        for (size_t i = 0; i < n; i++) {
+            const int64_t bl = bucket_of_record(ev[i]);
+            put(i, ingest_one(i, bl < 0 ? e->stage[0] : e->stage_of((uint32_t)bl)));
+        }
+    } else {
+        // Bucket of every record (chunks in parallel).  Then each partition gathers
+        // its records in bucket order (a stable counting sort: per bucket, batch
+        // order is kept, and nothing orders records of different buckets), so one
+        // bucket's slot state, bitmap and nodes stay in cache while its records
+        // are ingested.  Results land in `all` and are copied out per contiguous
+        // record range.
+        const int P = e->n_part;
+        constexpr uint32_t NONE = 0xFFFFFFFFu;
+        if (e->ing_bkt.size() < n) e->ing_bkt.resize(n);
+        if (e->ing_res.size() < n) e->ing_res.resize(n);
+        e->ing_order.resize((size_t)P);
+        uint32_t* bkt = e->ing_bkt.data();
+        uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
+        run_parts(e, true, [&](int p) {
+            const size_t lo = n * (size_t)p / (size_t)P, hi = n * (size_t)(p + 1) / (size_t)P;
+            for (size_t i = lo; i < hi; i++) {
+                const int64_t bl = bucket_of_record(ev[i]);
+                bkt[i] = bl < 0 ? NONE : (uint32_t)bl;
+            }
+        });
+        tp1 = std::chrono::steady_clock::now();
+        run_parts(e, true, [&](int p) {
+            auto& g = e->stage[(size_t)p];
+            // partition p owns buckets [first, last): those with bl * P / nb == p
+            const uint32_t first = (uint32_t)(((uint64_t)p * e->nb + P - 1) / P);
+            const uint32_t last = (uint32_t)(((uint64_t)(p + 1) * e->nb + P - 1) / P);
+            const uint32_t nbk = last - first;
+            std::vector<uint32_t> off(nbk + 2, 0);  // [0]: records that change nothing (partition 0)
+            const uint32_t* bk = bkt;
+            for (size_t i = 0; i < n; i++) {
+                const uint32_t b = bk[i];
+                if (b == NONE) off[1] += p == 0;
+                else if (b - first < nbk) off[b - first + 2]++;
+            }
+            for (uint32_t k = 1; k < nbk + 2; k++) off[k] += off[k - 1];
+            auto& order = e->ing_order[(size_t)p];
+            if (order.size() < off[nbk + 1]) order.resize(off[nbk + 1] + off[nbk + 1] / 8);
+            const uint32_t n_mine = off[nbk + 1];
+            for (size_t i = 0; i < n; i++) {
+                const uint32_t b = bk[i];
+                if (b == NONE) {
+                    if (p == 0) order[off[0]++] = (uint32_t)i;
+                } else if (b - first < nbk) {
+                    order[off[b - first + 1]++] = (uint32_t)i;
+                }
+            }
+            // records come in bucket order, i.e. from all over the batch: prefetch
+            // each record (PF ahead), then its IP strings and result word (PF/2
+            // ahead), so that their cache misses overlap
+            constexpr uint32_t PF = 16;
+            for (uint32_t k = 0; k < n_mine; k++) {
+                if (k + PF < n_mine) {
+                    const char* q = (const char*)&ev[order[k + PF]];
+                    __builtin_prefetch(q);
+                    __builtin_prefetch(q + sizeof(kwok_pod_event) - 1);
+                }
+                if (k + PF / 2 < n_mine) {
+                    const uint32_t j = order[k + PF / 2];
+                    const kwok_pod_event& y = ev[j];
+                    if (y.pod_ip.len && (size_t)y.pod_ip.off < arena_len) __builtin_prefetch(arena + y.pod_ip.off);
+                    if (y.host_ip.len && (size_t)y.host_ip.off < arena_len) __builtin_prefetch(arena + y.host_ip.off);
+                    __builtin_prefetch(&all[j], 1);
+                    const int64_t ps = (int64_t)y.handle - pbase;
+                    if (ps >= 0 && ps < (int64_t)e->PL) __builtin_prefetch(&e->pods[(size_t)ps], 1);
+                    const int64_t ns = (int64_t)y.node_handle - (int64_t)e->b_lo * e->Cn;
+                    if (y.handle < 0 && ns >= 0 && ns < (int64_t)e->NL) __builtin_prefetch(&e->nodes[(size_t)ns], 1);
+                }
+                const uint32_t i = order[k];
+                const Res r = ingest_one(i, g);
+                all[i] = (uint32_t)r.handle | (uint64_t)(uint32_t)r.st << 32;
+                // released IPs only come from DELETE records: theirs here, the rest zeroed below
+                if (out_released && ev[i].op == KWOK_OP_DELETE) out_released[i] = r.released;
+            }
+        });
+        run_parts(e, true, [&](int t) {
+            const size_t lo = n * (size_t)t / (size_t)P, hi = n * (size_t)(t + 1) / (size_t)P;
+            for (size_t i = lo; i < hi; i++) {
+                if (out_handles) out_handles[i] = (int32_t)(uint32_t)all[i];
+                if (out_status) out_status[i] = (int32_t)(all[i] >> 32);
+                if (out_released && ev[i].op != KWOK_OP_DELETE) out_released[i] = 0;
+            }
+        });
     }
+    int rejected = 0;
+    for (auto& g : e->stage) rejected += g.rejected;
+    const auto tp2 = std::chrono::steady_clock::now();
     int rc = flush_ops(e);
+    if (e->iprof) {
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "[kwok ingest] %zu pod records, %d partitions: route %.2f ms, records %.2f ms, flush %.2f ms\n",
+                n, e->n_part, ms(tp0, tp1), ms(tp1, tp2), ms(tp2, std::chrono::steady_clock::now()));
+    }
     return rc ? rc : rejected;
 }
 
@@ -1083,8 +1286,7 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
-    e->gen++;
-    e->puts.assign(ips, ips + n);
+    e->stage[0].puts.insert(e->stage[0].puts.end(), ips, ips + n);
     return flush_ops(e);
 }
 
@@ -1386,23 +1588,9 @@ int retire(kwok_engine* e) {
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));
-    // host mirror: pods deleted by the tick (DeletePod) free their slots
-    for (uint32_t slot : T.pending_del) {
-        if (!e->pod_delpend[slot] || !e->pod_used[slot]) continue;
-        uint32_t nslot = (slot / e->Cp) * e->Cn + e->pod_node[slot];
-        e->pod_used[slot] = 0;
-        e->pod_delpend[slot] = 0;
-        set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
-        e->nodes[nslot].refs--;
-        if (e->nodes[nslot].used && !e->nodes[nslot].exists && e->nodes[nslot].refs == 0) {
-            e->gen++;
-            free_node_if_unused(e, nslot);
-        }
-    }
-    T.pending_del.clear();
     // the slot-freeing ops of deleted nodes without pods: no tick reads such a
     // node, so with a tick already queued they wait for the next flush
-    if (!e->nops.empty() && next < 0) {
+    if (node_ops_pending(e) && next < 0) {
         int rc = flush_ops(e);
         if (rc) return failed(rc);
     }
@@ -1426,6 +1614,33 @@ int retire(kwok_engine* e) {
     e->host_ms[KWOK_H_TOTAL] += ms_between(t1, t3);
     e->host_ticks++;
     return KWOK_OK;
+}
+
+// Host mirror of the DeletePods a just-enqueued tick performs: every pod it
+// deletes frees its slot (each partition its own list, routed at ingest).  Run
+// right after the enqueue, so it overlaps the tick on the device; nothing reads
+// the mirrors before the tick is retired (ingest and dumps drain first).
+void free_deleted(kwok_engine* e, kwok_engine::TickSlot& T) {
+    size_t n_del = 0;
+    for (const auto& l : T.pending_del) n_del += l.size();
+    if (!n_del) return;
+    const auto td0 = clk::now();
+    run_parts(e, n_del >= PAR_MIN, [&](int p) {
+        auto& list = T.pending_del[(size_t)p];
+        for (uint32_t slot : list) {
+            auto& hp = e->pods[slot];
+            if (!hp.delpend || !hp.used) continue;
+            uint32_t nslot = (slot / e->Cp) * e->Cn + hp.node;
+            hp.used = 0;
+            hp.delpend = 0;
+            set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
+            e->nodes[nslot].refs--;
+            free_node_if_unused(e, nslot);
+        }
+        list.clear();
+    });
+    if (e->iprof)
+        fprintf(stderr, "[kwok submit] %zu deleted pods freed in %.2f ms\n", n_del, ms_between(td0, clk::now()));
 }
 
 // every queued tick finished on the host (before anything that reads or changes
@@ -1461,19 +1676,22 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     kwok_engine::TickSlot& T = e->slots[k];
     int rc = grow_arena(e, T);
     if (rc) return rc;
-    if (!e->nops.empty() && (rc = flush_ops(e))) return rc;  // deferred by retire
+    if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;  // deferred by retire
     if (k == e->cur) e->cur = -1;  // its outputs are overwritten
     T.now = (uint64_t)now_unix;
     T.epoch = e->hb_epoch;
     T.emit_queued = e->emit_hint;
     e->emit_hint = false;
-    T.pending_del.swap(e->pending_del);
-    e->pending_del.clear();
+    for (int p = 0; p < e->n_part; p++) {
+        T.pending_del[(size_t)p].swap(e->stage[(size_t)p].pending_del);
+        e->stage[(size_t)p].pending_del.clear();
+    }
     rc = enqueue_tick(e, k, false);
     if (rc) {
-        e->pending_del.swap(T.pending_del);
+        for (int p = 0; p < e->n_part; p++) e->stage[(size_t)p].pending_del.swap(T.pending_del[(size_t)p]);
         return rc;
     }
+    free_deleted(e, T);
     T.state = SLOT_QUEUED;
     e->queue[e->nq++] = k;
     e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
@@ -1601,8 +1819,8 @@ int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], ui
 
 int kwok_node_has(kwok_engine* e, const char* name, size_t len) {
     if (!e || !name) return 0;
-    auto it = e->node_by_name.find(std::string(name, len));
-    return it != e->node_by_name.end() && e->nodes[it->second].managed;
+    uint32_t slot = 0;
+    return node_slot(e, name, len, false, &slot) == KWOK_OK && e->nodes[slot].managed;
 }
 
 uint64_t kwok_node_size(kwok_engine* e) { return e ? e->n_managed : 0; }

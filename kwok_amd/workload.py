@@ -61,6 +61,7 @@ class Fleet:
     arena: bytes
     cn: int
     cp: int
+    node_handles: np.ndarray = None  # set by build_engine_fleet
 
 
 def make_fleet(nodes_per_rank: int, rank: int = 0, world: int = 1, buckets: int = BUCKETS) -> Fleet:
@@ -112,8 +113,107 @@ def build_engine_fleet(engine_cls, nodes_per_rank, rank=0, world=1, device=0, ci
     hs, st = e.ingest_nodes_raw(fl.node_events, fl.arena)
     if (st != 0).any():
         raise RuntimeError("node ingest rejected %d records (first code %d)" % ((st != 0).sum(), st[st != 0][0]))
+    fl.node_handles = hs
     pods = pod_events(hs, spec, pods_per_node)
     ph, pst, _ = e.ingest_pods_raw(pods, b"")
     if (pst != 0).any():
         raise RuntimeError("pod ingest rejected %d records (first code %d)" % ((pst != 0).sum(), pst[pst != 0][0]))
     return e, fl, ph
+
+
+def ip_strings(ips: np.ndarray, base: int = 0):
+    """Dotted quads (net.IP.String()) of IPv4 addresses, vectorised: one byte
+    arena plus (off, len) per address; off counts from `base`."""
+    ips = np.asarray(ips, np.uint32)
+    n = ips.shape[0]
+    octs = [((ips >> np.uint32(s)) & np.uint32(255)).astype(np.int64) for s in (24, 16, 8, 0)]
+    lens = [1 + (o >= 10) + (o >= 100) for o in octs]
+    total = lens[0] + lens[1] + lens[2] + lens[3] + 3
+    off = np.zeros(n, np.int64)
+    if n:
+        off[1:] = np.cumsum(total)[:-1]
+    buf = np.zeros(int(total.sum()) if n else 0, np.uint8)
+    pos = off.copy()
+    for k, (o, ln) in enumerate(zip(octs, lens)):
+        m3 = ln == 3
+        buf[pos[m3]] = 48 + o[m3] // 100
+        m2 = ln >= 2
+        buf[(pos + (ln == 3))[m2]] = 48 + (o[m2] // 10) % 10
+        buf[pos + ln - 1] = 48 + o % 10
+        pos += ln
+        if k < 3:
+            buf[pos] = ord(".")
+            pos += 1
+    return buf, (off + base).astype(np.uint32), total.astype(np.uint32)
+
+
+class Churn:
+    """BASELINE configs[3], the pod churn storm, as watch events (the shapes
+    WatchPods sees, pod_controller.go:301-343).  Every tick, the `n_churn`
+    oldest live pods get a deletionTimestamp: a Modified event carrying the
+    pod's Running status (hostIP = NodeIP, its podIP), half of them with
+    finalizers; the engine's tick deletes them (DeletePod, :155-202) and
+    releases their IPs.  As many new Pending pods are created on the same nodes
+    (so per-node pod counts stay fixed), and take IPs in the same tick (reuse of
+    the released addresses, utils.go:83-108).  The later Deleted events of the
+    deleted pods are not sent: the engine already freed those handles and the
+    shim drops them.
+
+    `dump` returns (used, phase, host_ip, pod_ip) over all pod handles
+    [0, n_handles) of a single-rank engine (or the oracle)."""
+
+    def __init__(self, pod_handles, node_of_pod, spec_id, n_handles, n_churn, seed=0, node_ip=NODE_IP,
+                 creation=S0 - 60):
+        self.live = np.asarray(pod_handles, np.int32).copy()  # FIFO: oldest first
+        self.node_of = np.zeros(n_handles, np.int32)
+        self.node_of[self.live] = node_of_pod
+        self.ctime = np.zeros(n_handles, np.int64)
+        self.ctime[self.live] = creation
+        self.spec = spec_id
+        self.n = n_churn
+        self.rng = np.random.default_rng(seed)
+        self.node_ip = node_ip.encode()
+
+    def batch(self, dump, now):
+        """(events, arena): n_churn deletion-marked pods, then n_churn new pods"""
+        D = min(self.n, self.live.shape[0])
+        dead = self.live[:D]
+        used, phase, _, pip = dump()
+        assert used[dead].all(), "churn: a live pod is missing from the engine"
+        ip_buf, ip_off, ip_len = ip_strings(pip[dead], base=len(self.node_ip))
+        arena = self.node_ip + ip_buf.tobytes()
+        ev = np.zeros(2 * D, abi.POD_EVENT_DTYPE)
+        d = ev[:D]
+        d["op"] = abi.OP_UPSERT
+        d["handle"] = dead
+        d["node_handle"] = -1
+        d["spec_id"] = self.spec
+        d["phase"] = phase[dead]
+        d["creation_unix"] = self.ctime[dead]
+        fin = np.where(self.rng.random(D) < 0.5, abi.POD_HAS_FINALIZERS, 0)
+        running = phase[dead] == abi.PHASE_RUNNING
+        d["flags"] = (abi.POD_DELETING | fin | np.where(running, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
+                      | np.where(pip[dead] != 0, abi.POD_STATUS_NONEMPTY, 0))
+        d["host_ip"]["off"] = 0
+        d["host_ip"]["len"] = np.where(running, len(self.node_ip), 0)
+        d["pod_ip"]["off"] = ip_off
+        d["pod_ip"]["len"] = np.where(pip[dead] != 0, ip_len, 0)
+        c = ev[D:]
+        c["op"] = abi.OP_UPSERT
+        c["handle"] = -1
+        c["node_handle"] = self.rng.permutation(self.node_of[dead])
+        c["spec_id"] = self.spec
+        c["phase"] = abi.PHASE_PENDING
+        c["flags"] = abi.POD_STATUS_NONEMPTY
+        c["creation_unix"] = now - 5
+        self._pending = (D, c["node_handle"].copy(), now - 5)
+        return ev, arena
+
+    def applied(self, handles, status):
+        """account the ingest result of the last batch"""
+        D, nodes, ct = self._pending
+        assert (status == 0).all(), "churn batch rejected: %s" % np.unique(status[status != 0])
+        new = handles[D:]
+        self.node_of[new] = nodes
+        self.ctime[new] = ct
+        self.live = np.concatenate([self.live[D:], new])

@@ -2,6 +2,7 @@
 driven with the same event batches, compared output by output (handles, patch
 bytes, deletes, counters) and on the full pod state."""
 import numpy as np
+from numpy.lib.stride_tricks import as_strided
 
 from kwok_amd import abi
 from kwok_amd.engine import Engine, make_config
@@ -181,3 +182,39 @@ def external_deletes(d, handles):
         if pip[pos[i]]:
             ev[i]["pod_ip"] = ar.ref(abi.ip4s(int(pip[pos[i]])))
     return ev, bytes(ar.buf)
+
+
+# ---- vectorised comparison for fleets of millions of objects ----------------
+def rows(arena, off, length):
+    """arena[off[i] : off[i] + length] for every i, as one (n, length) array"""
+    v = as_strided(arena, (arena.size - length + 1, length), (1, 1))
+    return v[off.astype(np.int64)]
+
+
+def compare_patches(ea, eo, el, oa, oo, ol, what):
+    assert (el == ol).all(), what + " lengths"
+    for L in np.unique(el):
+        sel = np.nonzero(el == L)[0]
+        for part in np.array_split(sel, max(1, len(sel) // 1_000_000)):
+            a, b = rows(ea, eo[part], int(L)), rows(oa, oo[part], int(L))
+            bad = np.nonzero((a != b).any(axis=1))[0]
+            assert len(bad) == 0, "%s: %d patches of length %d differ, first at #%d" % (what, len(bad), L, part[bad[0]])
+
+
+def compare_tick(e, o, where):
+    E, O = e.read_arrays(), o.read_arrays()
+    assert E["counters"] == O["counters"], where
+    assert (E["heartbeat_nodes"] == O["heartbeat_nodes"]).all(), where + " heartbeat handles"
+    n = len(E["heartbeat_nodes"])
+    if n:
+        body = O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]
+        hb = E["arena"][E["heartbeat_off"]:E["heartbeat_off"] + n * E["heartbeat_stride"]]
+        hb = hb.reshape(n, E["heartbeat_stride"])[:, :E["heartbeat_len"]]
+        assert (hb == body[None, :]).all(), where + " heartbeat bodies"
+    for k in ("node_init_nodes", "pod_patch_pods", "delete_pods", "delete_has_finalizers"):
+        assert (E[k] == O[k]).all(), where + " " + k
+    compare_patches(E["arena"], E["node_init_off"], E["node_init_len"], O["arena"], O["node_init_off"],
+                    O["node_init_len"], where + " node inits")
+    compare_patches(E["arena"], E["pod_patch_off"], E["pod_patch_len"], O["arena"], O["pod_patch_off"],
+                    O["pod_patch_len"], where + " pod patches")
+    return E["counters"]
