@@ -82,6 +82,7 @@ def parse():
     ap.add_argument("--cpu-ticks", type=int, default=5)
     ap.add_argument("--roofline-ticks", type=int, default=20)
     ap.add_argument("--churn-ticks", type=int, default=5, help="C4 churn ticks after the steady legs (N=1; 0: skip)")
+    ap.add_argument("--flap-ticks", type=int, default=5, help="C5 flap ticks on a partially managed fleet (N=1; 0: skip)")
     ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
                                                          "metric size: 2M create/delete per tick)")
     return ap.parse_args()
@@ -144,10 +145,12 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
     trans = recs = 0
     kern = emit = 0.0
     last = None
-    for k in range(ticks + 1):
+    steps = []
+    for k in range(ticks + 2):
         ev, ar = ch.batch(dump, now)
         torch.cuda.synchronize()
-        if k:
+        prof = k == ticks + 1  # one more step, profiled (HIP events), for the kernel times only
+        if prof:
             e.profile_enable(True)
         t0 = time.perf_counter()
         hs, st, _ = e.ingest_pods_raw(ev, ar)
@@ -156,13 +159,14 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
         t2 = time.perf_counter()
         ch.applied(hs, st)
         now += 30
-        if k:
+        if prof:
             ph, nt = e.profile_read()
             e.profile_enable(False)
-            kern += ph["kernel"]
-            emit += ph["emit_kernel"]
+            kern, emit = ph["kernel"] * ticks, ph["emit_kernel"] * ticks
+        elif k:
             ing += t1 - t0
             tck += t2 - t1
+            steps.append((t1 - t0, t2 - t1))
             trans += transitions(r.counters)
             recs += len(ev)
             last = dict(zip(abi.COUNTERS, list(r.counters)))
@@ -172,12 +176,54 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
         "ticks": ticks, "records_per_tick": recs // max(ticks, 1),
         "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
         "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
+        "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
+                      "ingest": float(np.median([a for a, _ in steps])) * 1e3,
+                      "tick": float(np.median([b for _, b in steps])) * 1e3},
         "ingest_records_per_s": recs / ing if ing else None,
         "tick_transitions_per_s": trans / tck if tck else None,
         "kernel_ms": kern / ticks, "k_emit_ms": emit / ticks,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods (record validation, IP parsing, slot policy on host threads, "
-                "H2D of the coalesced ops, k_apply_pod_ops); event generation between steps untimed"}
+                "H2D of the coalesced ops, k_apply_pod_ops); event generation between steps untimed (the GPU idles "
+                "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
+
+
+def flap_leg(nodes, ticks):
+    """BASELINE configs[4] (C5): a fleet of `nodes` nodes x 10 pods with
+    ManageAllNodes=false (annotation selector on 50% of the nodes, disregard
+    annotation on 0.1%); per tick 1% of the managed nodes are deleted and
+    created again (workload.Flap).  A step = kwok_ingest_nodes of that batch +
+    one kwok_tick (heartbeats of the managed half, the flapped nodes' init
+    patches, re-evaluation of the managed nodes' pods).  First step warmup."""
+    e, fl, _ = workload.build_engine_fleet(keng.Engine, nodes, managed_frac=0.5, lockable_frac=0.999, seed=5)
+    now = workload.S0 + 30
+    e.tick(now, read=False)
+    f = workload.Flap(fl, 0.01, seed=6)
+    ing = tck = 0.0
+    trans = 0
+    last = None
+    for k in range(ticks + 1):
+        now += 30
+        ev, ar = f.batch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.ingest_nodes_raw(ev, ar)
+        t1 = time.perf_counter()
+        r = e.tick(now, read=False)
+        t2 = time.perf_counter()
+        if k:
+            ing += t1 - t0
+            tck += t2 - t1
+            trans += transitions(r.counters)
+            last = dict(zip(abi.COUNTERS, list(r.counters)))
+    e.close()
+    return {"workload": "C5 node flap under partial management (BASELINE configs[4]): %d nodes x %d pods, "
+                        "annotation selector on 50%%, 1%% of the managed nodes deleted + re-added per tick"
+                        % (nodes, nodes * workload.PODS_PER_NODE),
+            "ticks": ticks, "flapped_nodes_per_tick": f.k,
+            "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
+            "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
+            "counters_last_tick": last}
 
 
 class Handoff:
@@ -319,6 +365,9 @@ def main():
     if world == 1 and a.churn_ticks > 0:
         now, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank)
 
+    e.close()
+    flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
+
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
         lc = last.local_counters
@@ -385,10 +434,11 @@ def main():
         }
         if churn is not None:
             out["churn"] = churn
+        if flap is not None:
+            out["flap"] = flap
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
         print(json.dumps(out))
-    e.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

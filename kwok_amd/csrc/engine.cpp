@@ -20,6 +20,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -49,6 +52,63 @@ template <class T>
 struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
+};
+
+// Persistent host worker threads for the ingest partitions (started on first
+// use): run(n, f) calls f(0) on the caller and f(1..n-1) on the workers, and
+// returns when all are done.
+class WorkPool {
+  public:
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int n, const std::function<void(int)>& f) {
+        while ((int)th_.size() < n - 1) {
+            const int id = (int)th_.size() + 1;
+            th_.emplace_back([this, id] { loop(id); });
+        }
+        {
+            std::lock_guard<std::mutex> l(m_);
+            job_ = &f;
+            width_ = n;
+            left_ = n - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [&] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(int id) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> l(m_);
+        for (;;) {
+            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            if (id >= width_) continue;  // this run uses fewer workers
+            const std::function<void(int)>* f = job_;
+            l.unlock();
+            (*f)(id);
+            l.lock();
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int width_ = 0, left_ = 0;
+    bool stop_ = false;
 };
 
 }  // namespace
@@ -131,6 +191,8 @@ struct kwok_engine {
     DevBuf<uint16_t> d_spec_nxt;
     uint32_t max_pod_len = 0;
     std::unordered_map<std::string, uint64_t> blob_ids;
+    uint64_t empty_blob = 0;      // the blob of a node with an empty status (every status field absent)
+    bool has_empty_blob = false;
     std::string blob_h;
     DevBuf<uint8_t> d_blob;
     uint32_t max_init_len = 0;
@@ -202,7 +264,8 @@ struct kwok_engine {
     // a failed tick leaves device and host state out of step: every later call
     // fails with KWOK_EDEVICE (destroy and recreate the engine, re-ingest by List)
     bool poisoned = false;
-    bool iprof = false;  // KWOK_INGEST_PROF=1: host ingest / retire phase times on stderr
+    bool iprof = false;
+    WorkPool workers;  // host threads of the ingest partitions  // KWOK_INGEST_PROF=1: host ingest / retire phase times on stderr
     uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
     int fail(int code, const char* fmt, ...) {
@@ -292,11 +355,8 @@ void run_parts(kwok_engine* e, bool parallel, F&& f) {
         for (int p = 0; p < e->n_part; p++) f(p);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve((size_t)e->n_part - 1);
-    for (int p = 1; p < e->n_part; p++) th.emplace_back([&f, p] { f(p); });
-    f(0);
-    for (auto& t : th) t.join();
+    const std::function<void(int)> fn = [&f](int p) { f(p); };
+    e->workers.run(e->n_part, fn);
 }
 constexpr size_t PAR_MIN = 32768;  // records (or deletes) per call before the partitions get threads
 
@@ -351,8 +411,11 @@ int flush_ops(kwok_engine* e) {
     for (const auto& g : e->stage) nn += g.nops.size(), np += g.pops.size(), nu += g.puts.size(), fill |= g.fill_dirty;
     const size_t nb = nn * sizeof(NodeOp), pb = np * sizeof(PodOp), ub = nu * 4;
     const size_t po = (nb + 255) & ~(size_t)255, uo = po + ((pb + 255) & ~(size_t)255);
+    const auto tfm0 = std::chrono::steady_clock::now();
     int rc = ensure_pinned(e, uo + ub + 256);
     if (rc) return rc;
+    const auto tfm = std::chrono::steady_clock::now();
+    const double t_pin = std::chrono::duration<double, std::milli>(tfm - tfm0).count();
     char* h = (char*)e->pinned;
     std::vector<size_t> at(3 * (size_t)e->n_part);  // each partition's first node op / pod op / put
     for (size_t p = 0, a = 0, b = 0, c = 0; p < (size_t)e->n_part; p++) {
@@ -366,6 +429,7 @@ int flush_ops(kwok_engine* e) {
         if (!g.puts.empty()) memcpy(h + uo + at[3 * p + 2] * 4, g.puts.data(), g.puts.size() * 4);
     });
     const auto tf0 = std::chrono::steady_clock::now();
+    const double t_copy = std::chrono::duration<double, std::milli>(tf0 - tfm).count();
     char* d = (char*)e->d_ops;
     HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
     if (fill) {  // before the ops that fill the new slots are visible to a tick
@@ -378,8 +442,9 @@ int flush_ops(kwok_engine* e) {
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->st));
     if (e->iprof && np + nn > 1000)
-        fprintf(stderr, "[kwok flush] %zu node + %zu pod ops, %zu puts: %.2f MB, device copy + apply %.2f ms\n", nn, np,
-                nu, (uo + ub) / 1e6, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
+        fprintf(stderr, "[kwok flush] %zu node + %zu pod ops, %zu puts: %.2f MB, pinned alloc %.2f ms, staging %.2f ms, "
+                        "device copy + apply %.2f ms\n", nn, np, nu, (uo + ub) / 1e6, t_pin, t_copy,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
     for (auto& g : e->stage) {
         g.nops.clear();
         g.pops.clear();
@@ -948,6 +1013,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     int rejected = 0;
+    const auto tn0 = std::chrono::steady_clock::now();
     for (size_t i = 0; i < n; i++) {
         const kwok_node_event& x = ev[i];
         int st = KWOK_OK;
@@ -988,9 +1054,19 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
             }
             if (st == KWOK_OK) st = node_slot(e, name, x.name.len, true, &slot);
             if (st == KWOK_OK) {
-                NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
+                // a Node created with an empty status (kwok's own fleets) renders the
+                // one default blob: built once
+                bool empty = js[0].empty() && js[1].empty() && js[2].empty();
+                for (int k = 0; k < KWOK_NI_COUNT; k++) empty = empty && info[k].empty();
                 int brc = KWOK_OK;
-                uint64_t blob = intern_blob(e, nb, &brc);
+                uint64_t blob = 0;
+                if (empty && e->has_empty_blob) {
+                    blob = e->empty_blob;
+                } else {
+                    NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
+                    blob = intern_blob(e, nb, &brc);
+                    if (empty && !brc) e->empty_blob = blob, e->has_empty_blob = true;
+                }
                 if (brc) st = brc;
                 else {
                     auto& hn = e->nodes[slot];
@@ -1017,9 +1093,14 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         if (out_status) out_status[i] = st;
         if (st != KWOK_OK) rejected++;
     }
+    const auto tn1 = std::chrono::steady_clock::now();
     int rc = size_arena(e);
     if (rc) return rc;
     rc = flush_ops(e);
+    if (e->iprof)
+        fprintf(stderr, "[kwok ingest] %zu node records: records %.2f ms, flush %.2f ms\n", n,
+                std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tn1).count());
     return rc ? rc : rejected;
 }
 
@@ -1184,25 +1265,51 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             put(i, ingest_one(i, bl < 0 ? e->stage[0] : e->stage_of((uint32_t)bl)));
         }
     } else {
-        // Bucket of every record (chunks in parallel).  Then each partition gathers
-        // its records in bucket order (a stable counting sort: per bucket, batch
-        // order is kept, and nothing orders records of different buckets), so one
-        // bucket's slot state, bitmap and nodes stay in cache while its records
-        // are ingested.  Results land in `all` and are copied out per contiguous
+        // Bucket of every record and a stable scatter of the record indices by
+        // partition (both in parallel, chunk by chunk).  Then each partition sorts
+        // its records by bucket (a stable counting sort: per bucket, batch order is
+        // kept, and nothing orders records of different buckets), so one bucket's
+        // slot state, bitmap and nodes stay in cache while its records are
+        // ingested.  Results land in `all` and are copied out per contiguous
         // record range.
         const int P = e->n_part;
         constexpr uint32_t NONE = 0xFFFFFFFFu;
-        if (e->ing_bkt.size() < n) e->ing_bkt.resize(n);
+        if (e->ing_bkt.size() < 2 * n) e->ing_bkt.resize(2 * n);
         if (e->ing_res.size() < n) e->ing_res.resize(n);
         e->ing_order.resize((size_t)P);
         uint32_t* bkt = e->ing_bkt.data();
+        uint32_t* plist = bkt + n;          // record indices grouped by partition
         uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
-        run_parts(e, true, [&](int p) {
-            const size_t lo = n * (size_t)p / (size_t)P, hi = n * (size_t)(p + 1) / (size_t)P;
+        auto owner = [&](uint32_t b) { return b == NONE ? 0 : (int)((uint64_t)b * (uint64_t)P / e->nb); };
+        std::vector<size_t> cnt((size_t)P * P + 1, 0);  // [chunk][partition], then scatter positions
+        run_parts(e, true, [&](int c) {
+            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
+            size_t k[64] = {};  // local: neighbouring chunks' counters share cache lines
             for (size_t i = lo; i < hi; i++) {
                 const int64_t bl = bucket_of_record(ev[i]);
                 bkt[i] = bl < 0 ? NONE : (uint32_t)bl;
+                k[owner(bkt[i])]++;
             }
+            std::copy(k, k + P, &cnt[(size_t)c * P]);
+        });
+        std::vector<size_t> pstart((size_t)P + 1, 0);
+        {
+            size_t acc = 0;
+            for (int p = 0; p < P; p++) {
+                pstart[(size_t)p] = acc;
+                for (int c = 0; c < P; c++) {
+                    const size_t v = cnt[(size_t)c * P + p];
+                    cnt[(size_t)c * P + p] = acc;
+                    acc += v;
+                }
+            }
+            pstart[(size_t)P] = acc;
+        }
+        run_parts(e, true, [&](int c) {
+            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
+            size_t k[64];
+            std::copy(&cnt[(size_t)c * P], &cnt[(size_t)c * P] + P, k);
+            for (size_t i = lo; i < hi; i++) plist[k[owner(bkt[i])]++] = (uint32_t)i;
         });
         tp1 = std::chrono::steady_clock::now();
         run_parts(e, true, [&](int p) {
@@ -1211,24 +1318,19 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const uint32_t first = (uint32_t)(((uint64_t)p * e->nb + P - 1) / P);
             const uint32_t last = (uint32_t)(((uint64_t)(p + 1) * e->nb + P - 1) / P);
             const uint32_t nbk = last - first;
-            std::vector<uint32_t> off(nbk + 2, 0);  // [0]: records that change nothing (partition 0)
-            const uint32_t* bk = bkt;
-            for (size_t i = 0; i < n; i++) {
-                const uint32_t b = bk[i];
-                if (b == NONE) off[1] += p == 0;
-                else if (b - first < nbk) off[b - first + 2]++;
+            const uint32_t* mine = plist + pstart[(size_t)p];
+            const uint32_t n_mine = (uint32_t)(pstart[(size_t)p + 1] - pstart[(size_t)p]);
+            std::vector<uint32_t> off(nbk + 2, 0);  // [0]: records that change nothing (partition 0 only)
+            for (uint32_t k = 0; k < n_mine; k++) {
+                const uint32_t b = bkt[mine[k]];
+                off[b == NONE ? 1 : b - first + 2]++;
             }
             for (uint32_t k = 1; k < nbk + 2; k++) off[k] += off[k - 1];
             auto& order = e->ing_order[(size_t)p];
-            if (order.size() < off[nbk + 1]) order.resize(off[nbk + 1] + off[nbk + 1] / 8);
-            const uint32_t n_mine = off[nbk + 1];
-            for (size_t i = 0; i < n; i++) {
-                const uint32_t b = bk[i];
-                if (b == NONE) {
-                    if (p == 0) order[off[0]++] = (uint32_t)i;
-                } else if (b - first < nbk) {
-                    order[off[b - first + 1]++] = (uint32_t)i;
-                }
+            if (order.size() < n_mine) order.resize(n_mine + n_mine / 8);
+            for (uint32_t k = 0; k < n_mine; k++) {
+                const uint32_t i = mine[k], b = bkt[i];
+                order[off[b == NONE ? 0 : b - first + 1]++] = i;
             }
             // records come in bucket order, i.e. from all over the batch: prefetch
             // each record (PF ahead), then its IP strings and result word (PF/2
@@ -1609,6 +1711,8 @@ int retire(kwok_engine* e) {
         r.local_counters[c] = H.local_counters[c];
     }
     const auto t3 = clk::now();
+    if (e->iprof && (H.n_pp || H.n_del || H.n_init))
+        fprintf(stderr, "[kwok retire] wait %.3f ms, post %.3f ms\n", ms_between(t1, t2), ms_between(t2, t3));
     e->host_ms[KWOK_H_WAIT] += ms_between(t1, t2);
     e->host_ms[KWOK_H_POST] += ms_between(t2, t3);
     e->host_ms[KWOK_H_TOTAL] += ms_between(t1, t3);
@@ -1691,9 +1795,12 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
         for (int p = 0; p < e->n_part; p++) e->stage[(size_t)p].pending_del.swap(T.pending_del[(size_t)p]);
         return rc;
     }
+    const auto te = clk::now();
     free_deleted(e, T);
     T.state = SLOT_QUEUED;
     e->queue[e->nq++] = k;
+    if (e->iprof)
+        fprintf(stderr, "[kwok submit] enqueue %.3f ms, mirror %.3f ms\n", ms_between(t0, te), ms_between(te, clk::now()));
     e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
     e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
     return KWOK_OK;

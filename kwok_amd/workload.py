@@ -64,20 +64,29 @@ class Fleet:
     node_handles: np.ndarray = None  # set by build_engine_fleet
 
 
-def make_fleet(nodes_per_rank: int, rank: int = 0, world: int = 1, buckets: int = BUCKETS) -> Fleet:
+def make_fleet(nodes_per_rank: int, rank: int = 0, world: int = 1, buckets: int = BUCKETS,
+               managed_frac: float = 1.0, lockable_frac: float = 1.0, seed: int = 0) -> Fleet:
     """Weak scaling: the fleet has nodes_per_rank * world nodes; this rank owns
-    the nodes whose bucket falls in its contiguous bucket range."""
+    the nodes whose bucket falls in its contiguous bucket range.
+    managed_frac < 1: ManageAllNodes=false with an annotation selector that
+    matches that fraction of the nodes (needHeartbeat, node_controller.go:206);
+    lockable_frac < 1: the rest carry a disregard annotation (needLockNode
+    false, :210-223).  Both drawn per node name index with `seed`."""
     total = nodes_per_rank * world
     names = node_names(0, total)
     b = fnv1a32_rows(names) & np.uint32(buckets - 1)
     lo = rank * buckets // world
     hi = (rank + 1) * buckets // world
-    mine = names[(b >= lo) & (b < hi)]
+    sel = (b >= lo) & (b < hi)
+    mine = names[sel]
     n = mine.shape[0]
+    rng = np.random.default_rng(seed)
+    managed = rng.random(total) < managed_frac if managed_frac < 1 else np.ones(total, bool)
+    lockable = rng.random(total) < lockable_frac if lockable_frac < 1 else np.ones(total, bool)
     ev = np.zeros(n, abi.NODE_EVENT_DTYPE)
     ev["op"] = abi.OP_UPSERT
-    ev["managed"] = 1
-    ev["lockable"] = 1
+    ev["managed"] = managed[sel]
+    ev["lockable"] = lockable[sel]
     ev["name"]["off"] = np.arange(n, dtype=np.uint32) * 12
     ev["name"]["len"] = 12
     cn, cp = slots_for(total, buckets)
@@ -100,11 +109,12 @@ def pod_events(node_handles: np.ndarray, spec_id: int, pods_per_node: int = PODS
 
 
 def build_engine_fleet(engine_cls, nodes_per_rank, rank=0, world=1, device=0, cidr=CIDR, node_ip=NODE_IP,
-                       start=S0, buckets=BUCKETS, pods_per_node=PODS_PER_NODE, **cfg_kw):
+                       start=S0, buckets=BUCKETS, pods_per_node=PODS_PER_NODE, managed_frac=1.0, lockable_frac=1.0,
+                       seed=0, **cfg_kw):
     """Create an engine (or oracle) for this rank and ingest its share of the
     fleet.  Returns (engine, fleet, pod_handles)."""
     from .engine import make_config
-    fl = make_fleet(nodes_per_rank, rank, world, buckets)
+    fl = make_fleet(nodes_per_rank, rank, world, buckets, managed_frac, lockable_frac, seed)
     cfg = make_config(cidr=cidr, node_ip=node_ip, start_time=start, buckets=buckets,
                       node_slots_per_bucket=fl.cn, pod_slots_per_bucket=fl.cp, rank=rank, world_size=world,
                       device=device, **cfg_kw)
@@ -217,3 +227,27 @@ class Churn:
         self.node_of[new] = nodes
         self.ctime[new] = ct
         self.live = np.concatenate([self.live[D:], new])
+
+
+class Flap:
+    """BASELINE configs[4], node failure / flap injection under partial
+    management: every tick, `frac` of the managed nodes are deleted and created
+    again (watch Deleted then Added of a Node with an empty status and the same
+    name, node_controller.go:256-270): they drop out of and rejoin the managed
+    set (heartbeat handle list epoch), are locked again and get the node-init
+    patch (configureNode, :356-391); their pods stay and are re-evaluated."""
+
+    def __init__(self, fleet, frac=0.01, seed=0):
+        ev = fleet.node_events
+        self.idx = np.nonzero(ev["managed"] != 0)[0]
+        self.fleet = fleet
+        self.k = max(1, int(len(self.idx) * frac))
+        self.rng = np.random.default_rng(seed)
+
+    def batch(self):
+        """(events, arena): k Deleted records, then k Added records"""
+        pick = self.rng.choice(self.idx, self.k, replace=False)
+        src = self.fleet.node_events[pick]
+        ev = np.concatenate([src, src])
+        ev["op"][:self.k] = abi.OP_DELETE
+        return ev, self.fleet.arena

@@ -12,6 +12,6 @@ cat gpurun_out/bench_$TAG.json
 timeout -k 10 300 python bench.py --nodes-per-rank 1000 --cpu-baseline 0 --roofline-ticks 10 > gpurun_out/bench_${TAG}_floor.json 2>/dev/null && cut -c1-400 gpurun_out/bench_${TAG}_floor.json
 if [ "$2" = "prof" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 > $R/gpurun_out/bench_${TAG}_prof.json 2>&1 || exit 4
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 > $R/gpurun_out/bench_${TAG}_prof.json 2>&1 || exit 4
 fi
 exit $trc
