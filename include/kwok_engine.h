@@ -36,6 +36,8 @@
  *   kwok_node_has / _size    NodeController.Has / Size        node_controller.go:403-409
  *   kwok_pool_put            ipPool.Put (replicating an ingest-time release
  *                            to the other ranks' pool replicas) utils.go:100-108
+ *   kwok_cni_pending /       EnableCNI: the pods configurePod would call cni.Setup
+ *   kwok_cni_assign          for, and the IPs it returned    pod_controller.go:383-389
  */
 #ifndef KWOK_ENGINE_H
 #define KWOK_ENGINE_H
@@ -56,7 +58,7 @@ enum {
     KWOK_EINVAL = -1,     /* bad argument / config */
     KWOK_ENOMEM = -2,     /* host or device allocation failed */
     KWOK_EDOMAIN = -3,    /* input outside the supported domain (e.g. not a "safe string",
-                             IPv6, custom templates, EnableCNI) - rejected, never emulated */
+                             IPv6, custom templates) - rejected, never emulated */
     KWOK_EFULL = -4,      /* bucket slot capacity exhausted */
     KWOK_EDEVICE = -5,    /* HIP runtime error */
     KWOK_ECOMM = -6,      /* RCCL / exchange error */
@@ -149,7 +151,8 @@ typedef struct kwok_config {
     const char* cidr;              /* Config.CIDR,   e.g. "10.0.0.1/24" (controller.go:72) */
     const char* node_ip;           /* Config.NodeIP, e.g. "196.168.0.1" (controller.go:73) */
     int64_t start_time_unix;       /* the StartTime() template func (controller.go:39-41) */
-    int32_t enable_cni;            /* Config.EnableCNI: must be 0 */
+    int32_t enable_cni;            /* Config.EnableCNI: pod IPs come from the caller's CNI plugin
+                                      (kwok_cni_pending / kwok_cni_assign); the ipPool is unused */
     int32_t custom_templates;      /* must be 0: only templates.Default* are supported */
     uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
     uint32_t node_slots_per_bucket;
@@ -253,6 +256,23 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                      size_t arena_len, int32_t* out_handles, int32_t* out_status,
                      uint32_t* out_released);
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n);
+
+/* EnableCNI (kwok_config.enable_cni = 1).  The reference calls cni.Setup inside
+ * configurePod for an evaluated pod without a podIP and renders the patch with
+ * the IP it returns (pod_controller.go:383-389); a Deleted event calls
+ * cni.Remove instead of ipPool.Put (:337-342).  With the engine:
+ *   before a tick, kwok_cni_pending lists (canonical order) the pods that tick
+ *   will evaluate that hold no podIP; the caller runs cni.Setup for each and
+ *   hands the first IPs back with kwok_cni_assign; the tick then patches them
+ *   with those IPs.  A pod still without an IP is not patched (as a failed
+ *   cni.Setup).  The ipPool is never used: no Get, Use or Put; the caller runs
+ *   cni.Remove on Deleted events (the engine's own deletions included).
+ * kwok_cni_pending: *n_out = the number of pending pods; KWOK_EINVAL (n_out set)
+ * when cap is smaller.  kwok_cni_assign: out_status[i] per record (KWOK_OK,
+ * KWOK_ENOTFOUND, KWOK_ENOTMINE, KWOK_EDOMAIN for IP 0); returns the number of
+ * rejected records or a negative error. */
+int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out);
+int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips, size_t n, int32_t* out_status);
 
 /* Advance one heartbeat interval at fixed clock now_unix (the Now() template
  * func).  Blocks until the tick's outputs are ready.  = kwok_tick_submit +

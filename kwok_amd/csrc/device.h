@@ -150,7 +150,7 @@ struct PodOp {
     uint16_t keep_mask, bits;  // state = (state & keep_mask) | bits
     uint16_t node, spec;
     uint32_t ctime, host_ip, pod_ip;
-    uint32_t set_fields;       // overwrite node/spec/ctime/IPs
+    uint32_t set_fields;       // 1: overwrite node/spec/ctime/IPs; 2: podIP only (kwok_cni_assign)
 };
 
 // spec descriptor: A | B | C segments of the pod patch (see templates.cpp)

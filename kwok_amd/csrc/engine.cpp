@@ -386,9 +386,12 @@ void pod_op(kwok_engine* e, kwok_engine::Stage& g, const PodOp& in) {
         PodOp& o = g.pops[hp.opi];
         o.bits = (uint16_t)((o.bits & in.keep_mask) | in.bits);
         o.keep_mask = (uint16_t)(o.keep_mask & in.keep_mask);
-        if (in.set_fields) {
+        if (in.set_fields == 1) {
             o.set_fields = 1;
             o.node = in.node, o.spec = in.spec, o.ctime = in.ctime, o.host_ip = in.host_ip, o.pod_ip = in.pod_ip;
+        } else if (in.set_fields == 2) {  // podIP only (kwok_cni_assign)
+            o.pod_ip = in.pod_ip;
+            if (!o.set_fields) o.set_fields = 2;
         }
         return;
     }
@@ -761,7 +764,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!out) return KWOK_EINVAL;
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
-    if (cfg->enable_cni || cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates, no CNI
+    if (cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
         !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
         cfg->pod_slots_per_bucket > 65528 /* fill marks are u16 */ ||
@@ -850,6 +853,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pool = e->pool;
     S.node_ip = e->node_ip;
     S.world = W;
+    S.cni = cfg->enable_cni ? 1u : 0u;
     {
         // a chain block's bucket range must fit its LDS node flags and 64 pod chunks
         const uint32_t bpb = (e->nb + S.n_chain - 1) / S.n_chain;
@@ -1160,7 +1164,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 auto& hn = e->nodes[nslot];
                 uint32_t ip = 0;
                 // pod_controller.go:329-336: release the event object's podIP if the node is managed
-                if (hn.managed && x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip) &&
+                // (EnableCNI: cni.Remove on the caller's side instead, :337-342)
+                if (!e->S.cni && hn.managed && x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip) &&
                     (uint64_t)(ip - e->pool.net) < e->pool.size && ip >= e->pool.net) {
                     g.puts.push_back(ip);
                     released = ip;
@@ -1220,7 +1225,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 uint16_t bits = (uint16_t)(PS_USED | ((uint16_t)x.phase << PS_PHASE_SHIFT));
                 if (x.flags & KWOK_POD_DISREGARD) bits |= PS_DISREGARD;
                 if (x.flags & KWOK_POD_HAS_FINALIZERS) bits |= PS_HAS_FIN;
-                if (x.flags & KWOK_POD_STATUS_NONEMPTY) bits |= PS_STATUS_NONEMPTY;
+                // a status that holds an IP is not empty (`{{ with .status }}`)
+                if ((x.flags & KWOK_POD_STATUS_NONEMPTY) || hip || pip) bits |= PS_STATUS_NONEMPTY;
                 if (x.flags & KWOK_POD_CONFORMS) bits |= PS_CONFORMS;
                 if (hip) bits |= PS_HAS_HOST_IP;
                 if (x.flags & KWOK_POD_DELETING) {
@@ -1380,6 +1386,67 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         fprintf(stderr, "[kwok ingest] %zu pod records, %d partitions: route %.2f ms, records %.2f ms, flush %.2f ms\n",
                 n, e->n_part, ms(tp0, tp1), ms(tp1, tp2), ms(tp2, std::chrono::steady_clock::now()));
     }
+    return rc ? rc : rejected;
+}
+
+int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {
+    if (!e || !n_out || (cap && !out)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    if (!e->S.cni) return e->fail(KWOK_EINVAL, "kwok_cni_pending: the engine was created without enable_cni");
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    if (node_ops_pending(e))
+        if (int rc = flush_ops(e)) return rc;
+    // scratch: the exchange list buffer (multi-rank ticks only, none in flight) and its counter
+    HIPCHK(e, hipMemsetAsync(e->S.list_counts, 0, 4, e->st));
+    launch_cni_pending(e->S, (int32_t*)e->S.use_list, e->S.list_counts, e->st);
+    HIPCHK(e, hipGetLastError());
+    uint32_t cnt = 0;
+    if (int rc = release_for_host(e)) return rc;
+    HIPCHK(e, hipMemcpyAsync(&cnt, e->S.list_counts, 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    std::vector<int32_t> h(cnt);
+    if (cnt) {
+        HIPCHK(e, hipMemcpyAsync(h.data(), e->S.use_list, (size_t)cnt * 4, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    (void)hipMemsetAsync(e->S.list_counts, 0, 8, e->st);
+    std::sort(h.begin(), h.end());  // canonical order
+    *n_out = cnt;
+    if (cap < cnt) return e->fail(KWOK_EINVAL, "kwok_cni_pending: %u pods pending, buffer holds %zu", cnt, cap);
+    if (cnt) memcpy(out, h.data(), (size_t)cnt * 4);
+    return KWOK_OK;
+}
+
+int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips, size_t n, int32_t* out_status) {
+    if (!e || (n && (!handles || !ips))) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    if (!e->S.cni) return e->fail(KWOK_EINVAL, "kwok_cni_assign: the engine was created without enable_cni");
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    const int64_t pbase = (int64_t)e->b_lo * e->Cp;
+    int rejected = 0;
+    for (size_t i = 0; i < n; i++) {
+        const int64_t l = (int64_t)handles[i] - pbase;
+        int st = KWOK_OK;
+        if (l < 0 || l >= (int64_t)e->PL) st = handles[i] >= 0 && (uint32_t)handles[i] / e->Cp < e->B ? KWOK_ENOTMINE : KWOK_ENOTFOUND;
+        else if (!e->pods[(size_t)l].used) st = KWOK_ENOTFOUND;
+        else if (!ips[i]) st = KWOK_EDOMAIN;
+        if (st == KWOK_OK) {
+            // configurePod: pod.Status.PodIP = ips[0] (pod_controller.go:388), so the status is not empty
+            PodOp o{};
+            o.slot = (uint32_t)l;
+            o.keep_mask = 0xFFFF;
+            o.bits = PS_STATUS_NONEMPTY;
+            o.set_fields = 2;
+            o.pod_ip = ips[i];
+            pod_op(e, e->stage_of((uint32_t)l / e->Cp), o);
+        } else {
+            rejected++;
+        }
+        if (out_status) out_status[i] = st;
+    }
+    int rc = flush_ops(e);
     return rc ? rc : rejected;
 }
 

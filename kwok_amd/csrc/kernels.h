@@ -86,12 +86,16 @@ struct DevState {
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)
+    uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
 };
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
                       hipStream_t st);
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
+// EnableCNI: handles of the pods the next tick evaluates that hold no podIP
+// (configurePod's cni.Setup set), appended in any order at out[*count]
+void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStream_t st);
 
 // the tick kernel: n_chain chain blocks (+ n_stream heartbeat streamers in
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks

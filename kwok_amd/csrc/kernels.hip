@@ -235,16 +235,19 @@ struct PodCls {
     bool used, del, eval, alloc, need;
     uint32_t phase;
 };
-__device__ __forceinline__ PodCls classify_pod(uint16_t st, uint8_t ntf, uint32_t pod_ip) {
+__device__ __forceinline__ PodCls classify_pod(uint16_t st, uint8_t ntf, uint32_t pod_ip, bool cni) {
     PodCls c;
     c.used = st & PS_USED;
     c.del = c.used && (st & PS_DELETE_PENDING);
     c.eval = c.used && !c.del && ((st & PS_EVENT) || ((ntf & NT_RELOCK) && !(st & PS_DISREGARD)));
     c.phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
-    // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47)
-    c.alloc = c.eval && (st & PS_STATUS_NONEMPTY) && pod_ip == 0;
-    // computePatchData: Pending always patches; otherwise the strategic merge must change something
-    c.need = c.eval && (c.phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || pod_ip == 0);
+    // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47);
+    // EnableCNI: the podIP comes from cni.Setup instead (pod_controller.go:383-389)
+    c.alloc = !cni && c.eval && (st & PS_STATUS_NONEMPTY) && pod_ip == 0;
+    // computePatchData: Pending always patches; otherwise the strategic merge must change something.
+    // EnableCNI: a pod without an IP is waiting for cni.Setup (configurePod fails: no patch)
+    c.need = c.eval && (cni ? pod_ip != 0 && (c.phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP))
+                            : (c.phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || pod_ip == 0));
     return c;
 }
 
@@ -708,7 +711,7 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
         const uint32_t nf = (uint32_t)ntf[2 * w] | (uint32_t)ntf[2 * w + 1] << 16;
         const uint32_t ia = g.ip[2 * w], ib = g.ip[2 * w + 1];
         const uint32_t ipz = (ia == 0 ? 1u : 0u) | (ib == 0 ? M ^ 1u : 0u);
-        const uint32_t inc = ((ia - net < size ? 1u : 0u) | (ib - net < size ? M ^ 1u : 0u)) & ~ipz;
+        const uint32_t inc_pool = ((ia - net < size ? 1u : 0u) | (ib - net < size ? M ^ 1u : 0u)) & ~ipz;
         const uint32_t used = s & M, disr = (s >> 1) & M, del = used & (s >> 2);
         const uint32_t nonempty = (s >> 4) & M, conf = (s >> 5) & M, event = (s >> 6) & M, hhost = (s >> 7) & M;
         const uint32_t ph = (s >> 8) & (7u * M);
@@ -719,9 +722,13 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
         // needLockPod / heartbeat re-lock (pod_controller.go:252-269, node_controller.go:152)
         const uint32_t eval = live & (event | (relock & ~disr));
         // computePatchData: Pending always patches; otherwise the strategic merge must change something
-        const uint32_t need = eval & (((running & conf & hhost) ^ M) | ipz);
-        // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47)
-        const uint32_t alloc = eval & nonempty & ipz;
+        // (EnableCNI: not before cni.Setup gave the pod an IP)
+        const uint32_t stale = (running & conf & hhost) ^ M;
+        const uint32_t need = S.cni ? eval & stale & ~ipz : eval & (stale | ipz);
+        // `{{ with .status }} ... {{ with .podIP }} . {{ else }} {{ PodIP }}` (pod.status.tpl:44-47);
+        // EnableCNI: no ipPool (no Get, Use or Put)
+        const uint32_t alloc = S.cni ? 0u : eval & nonempty & ipz;
+        const uint32_t inc = S.cni ? 0u : inc_pool;
         auto put = [w](uint32_t& mask, uint32_t plane) { mask |= ((plane & 1u) | ((plane >> 15) & 2u)) << (2 * w); };
         put(m.del, del & M);
         put(m.eval, eval);
@@ -963,7 +970,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
-        cl[k] = classify_pod(g.st(k), group_node_flags(S, nflags, g, k), g.ip[k]);
+        cl[k] = classify_pod(g.st(k), group_node_flags(S, nflags, g, k), g.ip[k], S.cni != 0);
         v[0] += cl[k].del;
         if (cl[k].need) {
             v[1]++;
@@ -1716,6 +1723,18 @@ __global__ void k_pool_puts_now(DevState S, const uint32_t* ips, uint32_t n) {
         atomicOr((unsigned long long*)&S.usable_bm[b >> 6], 1ull << (b & 63));
     }
 }
+// EnableCNI: the pods the next tick evaluates (the eval predicate of
+// classify_pod over the current node states) that hold no podIP
+__global__ void k_cni_pending(DevState S, int32_t* out, uint32_t* count) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < S.n_pod_slots; i += gridDim.x * blockDim.x) {
+        const uint16_t st = S.pod_state[i];
+        if (!(st & PS_USED)) continue;
+        const uint32_t b = i / S.cp;
+        const uint8_t ntf = node_tick_flags(S.node_state[(size_t)b * S.cn + S.pod_node[i]]);
+        const PodCls c = classify_pod(st, ntf, S.pod_ip[i], true);
+        if (c.eval && S.pod_ip[i] == 0) out[atomicAdd(count, 1u)] = S.pod_handle_base + (int32_t)i;
+    }
+}
 // multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm
 __global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
     for (int r = 0; r < nranks; r++) {
@@ -1742,11 +1761,13 @@ __global__ void k_apply_pod_ops(DevState S, const PodOp* ops, uint32_t n) {
     if (i >= n) return;
     PodOp o = ops[i];
     S.pod_state[o.slot] = (uint16_t)((S.pod_state[o.slot] & o.keep_mask) | o.bits);
-    if (o.set_fields) {  // add / modify carry the whole decoded object
+    if (o.set_fields == 1) {  // add / modify carry the whole decoded object
         S.pod_node[o.slot] = o.node;
         S.pod_spec[o.slot] = o.spec;
         S.pod_ctime[o.slot] = o.ctime;
         S.host_ip[o.slot] = o.host_ip;
+        S.pod_ip[o.slot] = o.pod_ip;
+    } else if (o.set_fields == 2) {  // kwok_cni_assign: the podIP cni.Setup returned
         S.pod_ip[o.slot] = o.pod_ip;
     }
 }
@@ -1766,6 +1787,12 @@ void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hi
     uint32_t g = n ? cdiv(n, 256) : 1;
     if (g > 1024) g = 1024;
     hipLaunchKernelGGL(k_pool_puts_now, dim3(g), dim3(256), 0, st, S, ips, n);
+}
+
+void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStream_t st) {
+    uint32_t g = cdiv(S.n_pod_slots, 256);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_cni_pending, dim3(g ? g : 1), dim3(256), 0, st, S, out, count);
 }
 
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st) {

@@ -61,6 +61,8 @@ def declare(lib, pre):
         "ingest_nodes": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP]),
         "ingest_pods": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP, VP]),
         "pool_put": (C.c_int, [VP, VP, SZ]),
+        "cni_pending": (C.c_int, [VP, VP, SZ, P(SZ)]),
+        "cni_assign": (C.c_int, [VP, VP, VP, SZ, VP]),
         "tick": (C.c_int, [VP, C.c_int64, P(abi.TickResult)]),
         "read_outputs": (C.c_int, [VP, P(abi.Outputs)]),
         "node_has": (C.c_int, [VP, C.c_char_p, SZ]),
@@ -115,7 +117,7 @@ class TickOutput:
 
 def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200, buckets=4096,
                 node_slots_per_bucket=64, pod_slots_per_bucket=512, max_pod_specs=1024, rank=0, world_size=1,
-                device=0, comm_id=None, allgather=None):
+                device=0, comm_id=None, allgather=None, enable_cni=False):
     cfg = abi.Config()
     cfg.abi_version = abi.ABI_VERSION
     cfg.cidr = cidr.encode()
@@ -126,6 +128,7 @@ def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200
     cfg.pod_slots_per_bucket = pod_slots_per_bucket
     cfg.max_pod_specs = max_pod_specs
     cfg.rank, cfg.world_size, cfg.device = rank, world_size, device
+    cfg.enable_cni = 1 if enable_cni else 0
     keep = []
     if comm_id is not None:
         b = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
@@ -213,6 +216,24 @@ class EngineBase:
     def pool_put(self, ips):
         a = np.ascontiguousarray(ips, dtype=np.uint32)
         self._check(self._fn("pool_put")(self._h, a.ctypes.data, len(a)), "pool_put")
+
+    # -- EnableCNI (configurePod's cni.Setup, pod_controller.go:383-389) --------
+    def cni_pending(self):
+        """handles (canonical order) of the pods the next tick evaluates without a podIP"""
+        n = C.c_size_t()
+        rc = self._fn("cni_pending")(self._h, None, 0, C.byref(n))
+        if rc != 0 and n.value == 0:
+            self._check(rc, "cni_pending")
+        out = np.empty(max(1, n.value), np.int32)
+        self._check(self._fn("cni_pending")(self._h, out.ctypes.data, out.size, C.byref(n)), "cni_pending")
+        return out[:n.value]
+
+    def cni_assign(self, handles, ips):
+        h = np.ascontiguousarray(handles, dtype=np.int32)
+        a = np.ascontiguousarray(ips, dtype=np.uint32)
+        st = np.empty(len(h), np.int32)
+        self._check(self._fn("cni_assign")(self._h, h.ctypes.data, a.ctypes.data, len(h), st.ctypes.data), "cni_assign")
+        return st
 
     # -- tick -------------------------------------------------------------------
     def tick_raw(self, now_unix):

@@ -385,19 +385,21 @@ struct kwok_oracle {
     uint32_t hb_epoch; /* bumped when the managed set changes */
     int threads;       /* host threads of the tick's sweeps (kwok_oracle_set_threads) */
     uint64_t hb_off;
+    int cni;           /* Config.EnableCNI: IPs from cni.Setup (kwok_oracle_cni_assign), no ipPool */
 };
 
 static int owns(const kwok_oracle* o, uint32_t b) { return b >= o->b_lo && b < o->b_hi; }
 
 int kwok_oracle_create(const kwok_config* cfg, kwok_oracle** out) {
     *out = NULL;
-    if (!cfg || cfg->abi_version != KWOK_ABI_VERSION || cfg->enable_cni || cfg->custom_templates) return KWOK_EINVAL;
+    if (!cfg || cfg->abi_version != KWOK_ABI_VERSION || cfg->custom_templates) return KWOK_EINVAL;
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || !cfg->node_slots_per_bucket || !cfg->pod_slots_per_bucket)
         return KWOK_EINVAL;
     int W = cfg->world_size > 0 ? cfg->world_size : 1;
     if (W > 1 && !cfg->allgather) return KWOK_EINVAL;
     kwok_oracle* o = (kwok_oracle*)calloc(1, sizeof(*o));
     o->cfg = *cfg;
+    o->cni = cfg->enable_cni != 0;
     o->cfg.world_size = W;
     o->B = cfg->buckets;
     o->cn = cfg->node_slots_per_bucket;
@@ -651,8 +653,9 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                 opod_t* p = &o->pods[h];
                 int32_t nh = p->node;
                 uint32_t ip = 0;
-                /* pod_controller.go:329-336: release the event's podIP if the node is managed */
-                if (o->nodes[nh].managed && ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &ip) &&
+                /* pod_controller.go:329-336: release the event's podIP if the node is managed
+                 * (EnableCNI: cni.Remove on the caller's side, :337-342) */
+                if (!o->cni && o->nodes[nh].managed && ip_parse(arena + e->pod_ip.off, e->pod_ip.len, &ip) &&
                     cidr_contains(&o->pool, ip)) {
                     pool_put(&o->pool, ip);
                     if (out_released) out_released[i] = ip;
@@ -708,7 +711,7 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                 p = &o->pods[h];
                 p->disregard = !!(e->flags & KWOK_POD_DISREGARD);
                 p->deleting = !!(e->flags & KWOK_POD_DELETING);
-                p->status_nonempty = !!(e->flags & KWOK_POD_STATUS_NONEMPTY);
+                p->status_nonempty = !!(e->flags & KWOK_POD_STATUS_NONEMPTY) || hip || pip; /* an IP is status */
                 p->conforms = !!(e->flags & KWOK_POD_CONFORMS);
                 p->has_fin = !!(e->flags & KWOK_POD_HAS_FINALIZERS);
                 p->phase = e->phase;
@@ -727,6 +730,38 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
         if (out_handles) out_handles[i] = h;
         if (out_status) out_status[i] = st;
         if (st != KWOK_OK) rejected++;
+    }
+    return rejected;
+}
+
+static inline int keep_eval(const kwok_oracle* o, size_t h);
+/* EnableCNI: the pods the next tick evaluates without a podIP (configurePod's
+ * cni.Setup set, pod_controller.go:383-389), canonical order */
+int kwok_oracle_cni_pending(kwok_oracle* o, int32_t* out, size_t cap, size_t* n_out) {
+    if (!o->cni || !n_out) return KWOK_EINVAL;
+    size_t n = 0;
+    for (size_t h = 0; h < (size_t)o->B * o->cp; h++)
+        if (!o->pods[h].delete_pending && keep_eval(o, h) && !o->pods[h].pod_ip) {
+            if (n < cap) out[n] = (int32_t)h;
+            n++;
+        }
+    *n_out = n;
+    return n <= cap ? KWOK_OK : KWOK_EINVAL;
+}
+/* ... and the IPs cni.Setup returned: pod.Status.PodIP = ips[0] (:388) */
+int kwok_oracle_cni_assign(kwok_oracle* o, const int32_t* handles, const uint32_t* ips, size_t n, int32_t* out_status) {
+    if (!o->cni) return KWOK_EINVAL;
+    int rejected = 0;
+    for (size_t i = 0; i < n; i++) {
+        int st = KWOK_OK;
+        if (handles[i] < 0 || (uint32_t)handles[i] >= o->B * o->cp || !o->pods[handles[i]].used) st = KWOK_ENOTFOUND;
+        else if (!ips[i]) st = KWOK_EDOMAIN;
+        else {
+            o->pods[handles[i]].pod_ip = ips[i];
+            o->pods[handles[i]].status_nonempty = 1;
+        }
+        if (out_status) out_status[i] = st;
+        rejected += st != KWOK_OK;
     }
     return rejected;
 }
@@ -951,7 +986,10 @@ static inline int keep_eval(const kwok_oracle* o, size_t h) {
     const onode_t* n = &o->nodes[p->node];
     return p->event || (node_locked(n) && n->managed && !p->disregard);
 }
-static int pod_needs_patch(const opod_t* p) {
+/* computePatchData (pod_controller.go:404-439); EnableCNI: configurePod fails
+ * (no patch) while cni.Setup has not given the pod an IP (:383-389) */
+static int pod_needs_patch(const kwok_oracle* o, const opod_t* p) {
+    if (o->cni) return p->pod_ip && (p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip);
     return p->phase != KWOK_PHASE_RUNNING || !p->conforms || !p->host_ip || !p->pod_ip;
 }
 
@@ -1037,7 +1075,7 @@ static int render_init_item(kwok_oracle* o, buf_t* b, size_t i, const char* now)
 static int render_pod_item(kwok_oracle* o, buf_t* b, size_t i, const char* now) {
     (void)now;
     const opod_t* p = &o->pods[g_rctx.list[i]];
-    if (!pod_needs_patch(p)) return 0;
+    if (!pod_needs_patch(o, p)) return 0;
     render_pod(o, b, p, g_rctx.ip[i]);
     return 1;
 }
@@ -1092,7 +1130,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
         o->del_fin[o->n_del++] = (uint8_t)p->has_fin;
         cnt[KWOK_CNT_DELETE]++;
         int32_t nh = p->node;
-        if (o->nodes[nh].managed && p->pod_ip && cidr_contains(&o->pool, p->pod_ip)) vpush(&rel, p->pod_ip);
+        if (!o->cni && o->nodes[nh].managed && p->pod_ip && cidr_contains(&o->pool, p->pod_ip)) vpush(&rel, p->pod_ip);
         memset(p, 0, sizeof(*p));
         o->nodes[nh].refs--;
         node_maybe_free(o, nh);
@@ -1108,6 +1146,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
 #pragma omp parallel for num_threads(T) reduction(+ : alloc_local)
         for (size_t i = 0; i < evals.n; i++) {
             const opod_t* p = &o->pods[evals.v[i]];
+            if (o->cni) continue; /* EnableCNI: no ipPool.Use / Get (pod_controller.go:378-389) */
             if (p->pod_ip && cidr_contains(&o->pool, p->pod_ip) && !hs_has(&o->pool.used, p->pod_ip)) fresh[i] = 1;
             if (p->status_nonempty && !p->pod_ip) alloc_local++;
         }
@@ -1132,7 +1171,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
         uint8_t* patched = (uint8_t*)calloc(NP + 1, 1);
 #pragma omp parallel for num_threads(T) reduction(+ : pp)
         for (size_t i = 0; i < evals.n; i++)
-            if (pod_needs_patch(&o->pods[evals.v[i]])) {
+            if (pod_needs_patch(o, &o->pods[evals.v[i]])) {
                 pp++;
                 patched[evals.v[i]] = 1;
             }
@@ -1237,7 +1276,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res) {
         for (size_t i = 0; i < evals.n; i++) {
             const opod_t* p = &o->pods[evals.v[i]];
             /* `{{ with .podIP }} . {{ else }} PodIP {{ end }}` inside `{{ with .status }}` */
-            ip[i] = (p->status_nonempty && !p->pod_ip) ? (uint32_t)pool_get(&o->pool) : p->pod_ip;
+            ip[i] = (!o->cni && p->status_nonempty && !p->pod_ip) ? (uint32_t)pool_get(&o->pool) : p->pod_ip;
         }
         for (uint64_t k = 0; k < alloc_after; k++) (void)pool_get(&o->pool);
         GROW(o->pp, evals.n);

@@ -18,6 +18,8 @@ int kwok_oracle_ingest_nodes(kwok_oracle* o, const kwok_node_event* ev, size_t n
 int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                             int32_t* out_handles, int32_t* out_status, uint32_t* out_released);
 int kwok_oracle_pool_put(kwok_oracle* o, const uint32_t* ips, size_t n);
+int kwok_oracle_cni_pending(kwok_oracle* o, int32_t* out, size_t cap, size_t* n_out);
+int kwok_oracle_cni_assign(kwok_oracle* o, const int32_t* handles, const uint32_t* ips, size_t n, int32_t* out_status);
 int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res);
 /* host threads of the tick's per-object sweeps (<= 0: all; 1: sequential); returns the count */
 int kwok_oracle_set_threads(kwok_oracle* o, int n);

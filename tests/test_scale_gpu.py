@@ -128,12 +128,12 @@ def test_domain_table_engine():
 def test_domain_rejections():
     """Configurations outside the supported domain are rejected, never
     emulated: IPv6 / non-canonical CIDRs, prefixes shorter than /4, custom
-    templates, EnableCNI."""
+    templates.  EnableCNI is accepted (kwok_cni_pending / kwok_cni_assign)."""
     for kw in (dict(cidr="fe80::1/64"), dict(cidr="10.0.0.1/3"), dict(cidr="010.0.0.1/8")):
         with pytest.raises(Exception):
             Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, **kw))
-    for field in ("custom_templates", "enable_cni"):
-        cfg = make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8)
-        setattr(cfg, field, 1)
-        with pytest.raises(Exception):
-            Engine(cfg)
+    cfg = make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8)
+    cfg.custom_templates = 1
+    with pytest.raises(Exception):
+        Engine(cfg)
+    Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, enable_cni=True)).close()
