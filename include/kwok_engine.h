@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KWOK_ABI_VERSION 2u
+#define KWOK_ABI_VERSION 3u
 #define KWOK_COMM_ID_BYTES 128u
 
 /* ---- status codes (int return values; per-record codes in out_status) ---- */
@@ -156,7 +156,8 @@ typedef struct kwok_config {
     int32_t custom_templates;      /* must be 0: only templates.Default* are supported */
     uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
     uint32_t node_slots_per_bucket;
-    uint32_t pod_slots_per_bucket;
+    uint32_t pod_slots_per_bucket; /* initial pod capacity of a bucket (multiple of 8); grows up to
+                                      pod_handle_stride when a bucket fills */
     uint32_t max_pod_specs;
     int32_t rank;                  /* this engine owns buckets [rank*B/W, (rank+1)*B/W) */
     int32_t world_size;
@@ -164,6 +165,11 @@ typedef struct kwok_config {
     const uint8_t* comm_id;        /* KWOK_COMM_ID_BYTES from kwok_comm_id(): RCCL exchange */
     kwok_allgather_fn allgather;   /* alternative host-memory exchange (used when comm_id == NULL) */
     void* allgather_user;
+    uint32_t pod_handle_stride;    /* pod handle = bucket * pod_handle_stride + slot in the bucket:
+                                      the most pods one bucket can hold (multiple of 8, <= 65528;
+                                      0 = pod_slots_per_bucket, i.e. no growth).  Handles stay valid
+                                      when a bucket's capacity grows (KWOK_EFULL only past it). */
+    uint32_t reserved0;
 } kwok_config;
 
 /* fleet counters (kwok_tick_result.counters, summed over ranks) */

@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 COMM_ID_BYTES = 128
 
 OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE, EBUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8, -9
@@ -85,7 +85,8 @@ class Config(C.Structure):
                 ("buckets", C.c_uint32), ("node_slots_per_bucket", C.c_uint32),
                 ("pod_slots_per_bucket", C.c_uint32), ("max_pod_specs", C.c_uint32),
                 ("rank", C.c_int32), ("world_size", C.c_int32), ("device", C.c_int32),
-                ("comm_id", C.c_void_p), ("allgather", ALLGATHER_FN), ("allgather_user", C.c_void_p)]
+                ("comm_id", C.c_void_p), ("allgather", ALLGATHER_FN), ("allgather_user", C.c_void_p),
+                ("pod_handle_stride", C.c_uint32), ("reserved0", C.c_uint32)]
 
 
 class TickResult(C.Structure):

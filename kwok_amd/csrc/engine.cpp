@@ -118,6 +118,7 @@ struct kwok_engine {
     std::string err;
     int W = 1, rank = 0, dev = 0;
     uint32_t B = 0, Cn = 0, Cp = 0, b_lo = 0, b_hi = 0, nb = 0, NL = 0, PL = 0;
+    uint32_t Hs = 0;  // pod handle stride: handle = bucket * Hs + slot in the bucket; Cp grows up to it
     PoolGeom pool{};
     uint32_t node_ip = 0;
     std::string node_ip_s;
@@ -150,6 +151,7 @@ struct kwok_engine {
     std::vector<HPod> pods;                          // [PL]
     std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
     std::vector<uint16_t> pod_fill;                  // per bucket: upper bound of used slots (only grows)
+    std::vector<uint32_t> pod_cnt;                   // per bucket: live pods
     uint16_t* d_pod_fill = nullptr;
 
     // ---- batch staging, one Stage per ingest partition ----
@@ -278,6 +280,17 @@ struct kwok_engine {
         return code;
     }
     bool owns(uint32_t bucket) const { return bucket >= b_lo && bucket < b_hi; }
+    // pod handle <-> local slot (bucket_local * Cp + index)
+    int32_t pod_handle(uint32_t slot) const { return (int32_t)((b_lo + slot / Cp) * Hs + slot % Cp); }
+    // KWOK_OK (slot set), KWOK_ENOTMINE (another rank's bucket) or KWOK_ENOTFOUND
+    int pod_slot(int64_t h, uint32_t* slot) const {
+        if (h < 0 || h / Hs >= B) return KWOK_ENOTFOUND;
+        const uint32_t b = (uint32_t)(h / Hs), i = (uint32_t)(h % Hs);
+        if (!owns(b)) return KWOK_ENOTMINE;
+        if (i >= Cp) return KWOK_ENOTFOUND;
+        *slot = (b - b_lo) * Cp + i;
+        return KWOK_OK;
+    }
 };
 
 #define HIPCHK(e, x)                                                                              \
@@ -689,6 +702,83 @@ int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
     return KWOK_OK;
 }
 
+// Grow every bucket's pod capacity to new_cp (<= the handle stride): the device
+// pod arrays and the host mirrors are re-laid out bucket by bucket (a bucket's
+// pods keep their index, so handles, canonical order and IP order are
+// unchanged); per-slot lists are reallocated.  Runs between ticks (drained),
+// with no pod ops staged.
+int grow_pods(kwok_engine* e, uint32_t new_cp) {
+    const uint32_t old = e->Cp, nb = e->nb;
+    if (new_cp <= old) return KWOK_OK;
+    hipStream_t st = e->st;
+    DevState& S = e->S;
+    const size_t PL2 = (size_t)nb * new_cp, PLa2 = PL2 + 16;
+    auto relayout = [&](auto*& p) -> int {
+        using T = std::remove_reference_t<decltype(*p)>;
+        T* q = nullptr;
+        if (hipMalloc((void**)&q, PLa2 * sizeof(T)) != hipSuccess) return e->fail(KWOK_ENOMEM, "grow pods");
+        HIPCHK(e, hipMemsetAsync(q, 0, PLa2 * sizeof(T), st));
+        HIPCHK(e, hipMemcpy2DAsync(q, (size_t)new_cp * sizeof(T), p, (size_t)old * sizeof(T), (size_t)old * sizeof(T), nb,
+                                   hipMemcpyDeviceToDevice, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        (void)hipFree(p);
+        p = q;
+        return KWOK_OK;
+    };
+    auto resize = [&](auto*& p, bool keep) -> int {  // per-ordinal lists: contents kept (the last tick's outputs)
+        using T = std::remove_reference_t<decltype(*p)>;
+        T* q = nullptr;
+        if (hipMalloc((void**)&q, PLa2 * sizeof(T)) != hipSuccess) return e->fail(KWOK_ENOMEM, "grow pod lists");
+        HIPCHK(e, hipMemsetAsync(q, 0, PLa2 * sizeof(T), st));
+        if (keep && p) HIPCHK(e, hipMemcpyAsync(q, p, e->PLa * sizeof(T), hipMemcpyDeviceToDevice, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        if (p) (void)hipFree(p);
+        p = q;
+        return KWOK_OK;
+    };
+    int rc = 0;
+    if ((rc = relayout(S.pod_state)) || (rc = relayout(S.pod_node)) || (rc = relayout(S.pod_spec)) ||
+        (rc = relayout(S.pod_ctime)) || (rc = relayout(S.pod_ip)) || (rc = relayout(S.host_ip)) ||
+        (rc = resize(S.alloc_addr, false)) || (rc = resize(S.use_list, false)) || (rc = resize(S.rel_list, false)))
+        return rc;
+    for (auto& T : e->slots) {
+        if (!T.alloc) continue;
+        if ((rc = resize(T.pp_pods, true)) || (rc = resize(T.pp_off, true)) || (rc = resize(T.pp_len, true)) ||
+            (rc = resize(T.del_pods, true)) || (rc = resize(T.del_fin, true)) || (rc = resize(T.pp_job, true)))
+            return rc;
+    }
+    // host mirrors
+    std::vector<kwok_engine::HPod> pods(PL2, kwok_engine::HPod{0, 0, 0, 0, 0});
+    const uint32_t w_old = (old + 63) / 64, w_new = (new_cp + 63) / 64;
+    std::vector<uint64_t> bits((size_t)nb * w_new, 0);
+    for (uint32_t b = 0; b < nb; b++) {
+        std::copy(e->pods.begin() + (size_t)b * old, e->pods.begin() + (size_t)(b + 1) * old, pods.begin() + (size_t)b * new_cp);
+        std::copy(e->pod_bits.begin() + (size_t)b * w_old, e->pod_bits.begin() + (size_t)(b + 1) * w_old,
+                  bits.begin() + (size_t)b * w_new);
+    }
+    e->pods.swap(pods);
+    e->pod_bits.swap(bits);
+    auto remap = [&](uint32_t slot) { return (slot / old) * new_cp + slot % old; };
+    for (auto& g : e->stage)
+        for (auto& s : g.pending_del) s = remap(s);
+    for (auto& T : e->slots)
+        for (auto& l : T.pending_del)
+            for (auto& s : l) s = remap(s);
+    e->Cp = new_cp;
+    e->PL = (uint32_t)PL2;
+    e->PLa = PLa2;
+    S.cp = new_cp;
+    S.n_pod_slots = e->PL;
+    return size_arena(e);
+}
+
+// The largest pod capacity a chain block's pod chunks cover (engine_create's limit)
+uint32_t max_pod_capacity(const kwok_engine* e) {
+    const uint64_t bpb = (e->nb + e->S.n_chain - 1) / e->S.n_chain;
+    const uint64_t lim = (uint64_t)MAX_POD_CHUNKS * BLOCK * POD_PER_THREAD / bpb;
+    return (uint32_t)std::min<uint64_t>(e->Hs, lim & ~7ull);
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -765,10 +855,11 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
     if (cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates
+    const uint32_t hs = cfg->pod_handle_stride ? cfg->pod_handle_stride : cfg->pod_slots_per_bucket;
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
         !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
-        cfg->pod_slots_per_bucket > 65528 /* fill marks are u16 */ ||
-        !cfg->pod_slots_per_bucket)
+        !cfg->pod_slots_per_bucket || hs % 8 || hs < cfg->pod_slots_per_bucket ||
+        hs > 65528 /* fill marks are u16 */ || (uint64_t)cfg->buckets * hs > 0x7FFFFFFFull /* int32 handles */)
         return KWOK_EINVAL;
     int W = cfg->world_size > 0 ? cfg->world_size : 1;
     if (cfg->rank < 0 || cfg->rank >= W || (W > 1 && !cfg->comm_id && !cfg->allgather) || (uint32_t)W > cfg->buckets)
@@ -781,6 +872,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     e->B = cfg->buckets;
     e->Cn = cfg->node_slots_per_bucket;
     e->Cp = cfg->pod_slots_per_bucket;
+    e->Hs = hs;
     e->b_lo = (uint32_t)((uint64_t)cfg->rank * e->B / W);
     e->b_hi = (uint32_t)((uint64_t)(cfg->rank + 1) * e->B / W);
     // kwok_rank_of_bucket must agree with [b_lo, b_hi)
@@ -849,7 +941,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.cn = e->Cn;
     S.cp = e->Cp;
     S.node_handle_base = (int32_t)(e->b_lo * e->Cn);
-    S.pod_handle_base = (int32_t)(e->b_lo * e->Cp);
+    S.pod_handle_base = 0;  // pod handles: pod_handle_of (stride)
+    S.b_lo = e->b_lo;
+    S.pod_stride = e->Hs;
     S.pool = e->pool;
     S.node_ip = e->node_ip;
     S.world = W;
@@ -942,6 +1036,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     e->pod_bits.assign((size_t)e->nb * ((e->Cp + 63) / 64), 0);
     e->pod_fill.assign(e->nb, 0);
+    e->pod_cnt.assign(e->nb, 0);
     e->node_stamp.assign(e->NL, 0);
     e->node_opi.assign(e->NL, 0);
     e->max_init_len = 0;
@@ -1115,7 +1210,6 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
-    const int32_t pbase = (int32_t)(e->b_lo * e->Cp);
     auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
     // The bucket (owned, local) whose slots a record changes, or -1 when it changes
     // nothing but its own out_status (it is rejected).  A record's partition
@@ -1123,8 +1217,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     auto bucket_of_record = [&](const kwok_pod_event& x) -> int64_t {
         if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) return -1;
         if (x.handle >= 0) {
-            const int64_t l = (int64_t)x.handle - pbase;
-            return l >= 0 && l < (int64_t)e->PL ? l / e->Cp : -1;
+            uint32_t sl = 0;
+            return e->pod_slot(x.handle, &sl) == KWOK_OK ? (int64_t)(sl / e->Cp) : -1;
         }
         if (x.op != KWOK_OP_UPSERT) return -1;
         if (x.node_handle >= 0) {
@@ -1149,12 +1243,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         uint32_t slot = 0;
         const bool existing = x.handle >= 0;
         if (st == KWOK_OK && existing) {
-            int64_t l = (int64_t)x.handle - pbase;
-            if (l < 0 || l >= (int64_t)e->PL) {
-                uint32_t gb = (uint32_t)x.handle / e->Cp;
-                st = (x.handle >= 0 && gb < e->B) ? KWOK_ENOTMINE : KWOK_ENOTFOUND;
-            } else if (!e->pods[(uint32_t)l].used) st = KWOK_ENOTFOUND;
-            else slot = (uint32_t)l;
+            st = e->pod_slot(x.handle, &slot);
+            if (st == KWOK_OK && !e->pods[slot].used) st = KWOK_ENOTFOUND;
         }
         if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
             if (!existing) st = KWOK_EINVAL;
@@ -1176,9 +1266,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 hp.used = 0;
                 hp.delpend = 0;
                 set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
+                e->pod_cnt[slot / e->Cp]--;
                 hn.refs--;
                 free_node_if_unused(e, nslot);
-                handle = pbase + (int32_t)slot;
+                handle = e->pod_handle(slot);
             }
         } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
             uint32_t hip = 0, pip = 0;
@@ -1207,6 +1298,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                     } else {
                         slot = bl * e->Cp + (uint32_t)idx;
                         set_bit(e->pod_bits, e->Cp, bl, (uint32_t)idx, true);
+                        e->pod_cnt[bl]++;
                         if ((uint32_t)idx + 1 > e->pod_fill[bl]) {
                             e->pod_fill[bl] = (uint16_t)std::min<uint32_t>(e->Cp, ((uint32_t)idx + 8) & ~7u);
                             g.fill_dirty = true;
@@ -1249,7 +1341,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 o.host_ip = hip;
                 o.pod_ip = pip;
                 pod_op(e, g, o);
-                handle = pbase + (int32_t)slot;
+                handle = e->pod_handle(slot);
             }
         } else if (st == KWOK_OK) {
             st = KWOK_EINVAL;
@@ -1263,9 +1355,35 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         if (out_released) out_released[i] = r.released;
     };
     for (auto& g : e->stage) g.rejected = 0;
+    // A bucket that this batch's creates would fill grows first (every bucket to a
+    // larger capacity, up to the handle stride): creates[bl] counts them, ignoring
+    // the slots this batch's deletes free (an upper bound)
+    auto is_create = [](const kwok_pod_event& x) { return x.op == KWOK_OP_UPSERT && x.handle < 0; };
+    auto grow_for = [&](const std::vector<uint32_t>& creates) -> int {
+        uint64_t need = 0;
+        for (uint32_t b = 0; b < e->nb; b++)
+            if (creates[b]) need = std::max<uint64_t>(need, (uint64_t)e->pod_cnt[b] + creates[b]);
+        if (need <= e->Cp) return KWOK_OK;
+        const uint32_t cap = max_pod_capacity(e);
+        if (cap <= e->Cp) return KWOK_OK;  // at the stride (or the chain blocks' limit): EFULL per record
+        const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>((need + 7) & ~7ull, 2ull * e->Cp));
+        if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
+        return grow_pods(e, want);
+    };
     const auto tp0 = std::chrono::steady_clock::now();
     auto tp1 = tp0;
     if (n < PAR_MIN || e->n_part == 1) {
+        {
+            std::vector<uint32_t> creates(e->nb, 0);
+            bool any = false;
+            for (size_t i = 0; i < n; i++)
+                if (is_create(ev[i])) {
+                    const int64_t bl = bucket_of_record(ev[i]);
+                    if (bl >= 0) creates[(size_t)bl]++, any = true;
+                }
+            if (any)
+                if (int rc = grow_for(creates)) return rc;
+        }
         for (size_t i = 0; i < n; i++) {
             const int64_t bl = bucket_of_record(ev[i]);
             put(i, ingest_one(i, bl < 0 ? e->stage[0] : e->stage_of((uint32_t)bl)));
@@ -1288,16 +1406,23 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
         auto owner = [&](uint32_t b) { return b == NONE ? 0 : (int)((uint64_t)b * (uint64_t)P / e->nb); };
         std::vector<size_t> cnt((size_t)P * P + 1, 0);  // [chunk][partition], then scatter positions
+        std::vector<std::vector<uint32_t>> creates((size_t)P);
         run_parts(e, true, [&](int c) {
             const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
             size_t k[64] = {};  // local: neighbouring chunks' counters share cache lines
+            auto& cr = creates[(size_t)c];
+            cr.assign(e->nb, 0);
             for (size_t i = lo; i < hi; i++) {
                 const int64_t bl = bucket_of_record(ev[i]);
                 bkt[i] = bl < 0 ? NONE : (uint32_t)bl;
                 k[owner(bkt[i])]++;
+                if (bl >= 0 && is_create(ev[i])) cr[(size_t)bl]++;
             }
             std::copy(k, k + P, &cnt[(size_t)c * P]);
         });
+        for (int c = 1; c < P; c++)
+            for (uint32_t b = 0; b < e->nb; b++) creates[0][b] += creates[(size_t)c][b];
+        if (int rc = grow_for(creates[0])) return rc;
         std::vector<size_t> pstart((size_t)P + 1, 0);
         {
             size_t acc = 0;
@@ -1354,8 +1479,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                     if (y.pod_ip.len && (size_t)y.pod_ip.off < arena_len) __builtin_prefetch(arena + y.pod_ip.off);
                     if (y.host_ip.len && (size_t)y.host_ip.off < arena_len) __builtin_prefetch(arena + y.host_ip.off);
                     __builtin_prefetch(&all[j], 1);
-                    const int64_t ps = (int64_t)y.handle - pbase;
-                    if (ps >= 0 && ps < (int64_t)e->PL) __builtin_prefetch(&e->pods[(size_t)ps], 1);
+                    uint32_t ps = 0;
+                    if (y.handle >= 0 && e->pod_slot(y.handle, &ps) == KWOK_OK) __builtin_prefetch(&e->pods[ps], 1);
                     const int64_t ns = (int64_t)y.node_handle - (int64_t)e->b_lo * e->Cn;
                     if (y.handle < 0 && ns >= 0 && ns < (int64_t)e->NL) __builtin_prefetch(&e->nodes[(size_t)ns], 1);
                 }
@@ -1424,14 +1549,12 @@ int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips,
     if (!e->S.cni) return e->fail(KWOK_EINVAL, "kwok_cni_assign: the engine was created without enable_cni");
     drain(e);
     if (e->poisoned) return poisoned(e);
-    const int64_t pbase = (int64_t)e->b_lo * e->Cp;
     int rejected = 0;
     for (size_t i = 0; i < n; i++) {
-        const int64_t l = (int64_t)handles[i] - pbase;
-        int st = KWOK_OK;
-        if (l < 0 || l >= (int64_t)e->PL) st = handles[i] >= 0 && (uint32_t)handles[i] / e->Cp < e->B ? KWOK_ENOTMINE : KWOK_ENOTFOUND;
-        else if (!e->pods[(size_t)l].used) st = KWOK_ENOTFOUND;
-        else if (!ips[i]) st = KWOK_EDOMAIN;
+        uint32_t l = 0;
+        int st = e->pod_slot(handles[i], &l);
+        if (st == KWOK_OK && !e->pods[l].used) st = KWOK_ENOTFOUND;
+        else if (st == KWOK_OK && !ips[i]) st = KWOK_EDOMAIN;
         if (st == KWOK_OK) {
             // configurePod: pod.Status.PodIP = ips[0] (pod_controller.go:388), so the status is not empty
             PodOp o{};
@@ -1440,7 +1563,7 @@ int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips,
             o.bits = PS_STATUS_NONEMPTY;
             o.set_fields = 2;
             o.pod_ip = ips[i];
-            pod_op(e, e->stage_of((uint32_t)l / e->Cp), o);
+            pod_op(e, e->stage_of(l / e->Cp), o);
         } else {
             rejected++;
         }
@@ -1805,6 +1928,7 @@ void free_deleted(kwok_engine* e, kwok_engine::TickSlot& T) {
             hp.used = 0;
             hp.delpend = 0;
             set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
+            e->pod_cnt[slot / e->Cp]--;
             e->nodes[nslot].refs--;
             free_node_if_unused(e, nslot);
         }
@@ -2011,10 +2135,9 @@ int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used,
     HIPCHK(e, hipMemcpyAsync(hh.data(), e->S.host_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(ph.data(), e->S.pod_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
-    const int64_t pbase = (int64_t)e->b_lo * e->Cp;
     for (uint32_t i = 0; i < count; i++) {
-        int64_t l = (int64_t)first + i - pbase;
-        bool ok = l >= 0 && l < (int64_t)e->PL && (sth[(size_t)l] & PS_USED);
+        uint32_t l = 0;
+        bool ok = e->pod_slot((int64_t)first + i, &l) == KWOK_OK && (sth[l] & PS_USED);
         if (used) used[i] = ok;
         if (phase) phase[i] = ok ? (uint8_t)((sth[(size_t)l] & PS_PHASE_MASK) >> PS_PHASE_SHIFT) : 0;
         if (host_ip) host_ip[i] = ok && (sth[(size_t)l] & PS_HAS_HOST_IP) ? hh[(size_t)l] : 0;

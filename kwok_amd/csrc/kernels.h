@@ -87,7 +87,13 @@ struct DevState {
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
+    uint32_t b_lo;             // first owned bucket
+    uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
 };
+
+__device__ __host__ inline int32_t pod_handle_of(const DevState& S, uint32_t slot) {
+    return (int32_t)((S.b_lo + slot / S.cp) * S.pod_stride + slot % S.cp);
+}
 
 void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const PodOp* pops, uint32_t np,
                       hipStream_t st);

@@ -988,7 +988,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
         const uint32_t slot = g.slot + k;
-        const int32_t handle = S.pod_handle_base + (int32_t)slot;
+        const int32_t handle = pod_handle_of(S, slot);
         uint16_t s = g.st(k);
         if (cl[k].del) {
             const uint64_t ord = run.v[AG_DEL] + v[0]++;
@@ -1732,7 +1732,7 @@ __global__ void k_cni_pending(DevState S, int32_t* out, uint32_t* count) {
         const uint32_t b = i / S.cp;
         const uint8_t ntf = node_tick_flags(S.node_state[(size_t)b * S.cn + S.pod_node[i]]);
         const PodCls c = classify_pod(st, ntf, S.pod_ip[i], true);
-        if (c.eval && S.pod_ip[i] == 0) out[atomicAdd(count, 1u)] = S.pod_handle_base + (int32_t)i;
+        if (c.eval && S.pod_ip[i] == 0) out[atomicAdd(count, 1u)] = pod_handle_of(S, i);
     }
 }
 // multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm

@@ -403,7 +403,9 @@ int kwok_oracle_create(const kwok_config* cfg, kwok_oracle** out) {
     o->cfg.world_size = W;
     o->B = cfg->buckets;
     o->cn = cfg->node_slots_per_bucket;
-    o->cp = cfg->pod_slots_per_bucket;
+    /* handles are bucket * stride + slot: the oracle holds every bucket at its
+     * largest capacity (the engine grows to it) */
+    o->cp = cfg->pod_handle_stride ? cfg->pod_handle_stride : cfg->pod_slots_per_bucket;
     o->b_lo = (uint32_t)((uint64_t)cfg->rank * o->B / W);
     o->b_hi = (uint32_t)((uint64_t)(cfg->rank + 1) * o->B / W);
     /* parseCIDR (utils.go:28-35): net.ParseCIDR, then ipnet.IP = the parsed host IP */

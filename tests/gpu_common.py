@@ -55,7 +55,7 @@ class Driver:
         self.cfg = cfg_kw
         self.spec = [self.e.register_pod_spec(*sp) for sp in (specs or self.DEFAULT_SPECS)]
         assert self.spec == [self.o.register_pod_spec(*sp) for sp in (specs or self.DEFAULT_SPECS)]
-        self.n_slots = cfg_kw["buckets"] * cfg_kw["pod_slots_per_bucket"]
+        self.n_slots = cfg_kw["buckets"] * (cfg_kw.get("pod_handle_stride") or cfg_kw["pod_slots_per_bucket"])
         self.spec_of = np.zeros(self.n_slots, np.int32)   # immutable pod fields, by handle
         self.ctime_of = np.zeros(self.n_slots, np.int64)
         self.now = 1704067230
