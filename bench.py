@@ -47,7 +47,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+# KWOK_BENCH_REHEARSAL=1: every rank on GPU 0 and the exchange over the host
+# allgather hook (gloo) instead of RCCL - rehearses the N>1 bench on a one-GPU
+# box (RCCL refuses two ranks on one GPU); never used for reported numbers
+REHEARSAL = os.environ.get("KWOK_BENCH_REHEARSAL") == "1"
+torch.cuda.set_device(0 if REHEARSAL else int(os.environ.get("LOCAL_RANK", "0")))
 
 from kwok_amd import abi  # noqa: E402
 from kwok_amd import engine as keng  # noqa: E402
@@ -263,12 +267,19 @@ def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if REHEARSAL else int(os.environ.get("LOCAL_RANK", "0"))
+    if REHEARSAL:
+        os.environ.setdefault("KWOK_TICK_BLOCKS_PER_CU", "1")
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; the data path uses the engine's RCCL comm
 
     comm = None
-    if world > 1:
+    gather = None
+    if world > 1 and REHEARSAL:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from dist_common import gloo_allgather_fn  # rehearsal only: host-memory exchange
+        gather = gloo_allgather_fn()
+    elif world > 1:
         obj = [keng.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = obj[0]
@@ -276,7 +287,7 @@ def main():
     cidr = cidr_for(total_pods)
     t0 = time.perf_counter()
     e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes_per_rank, rank=rank, world=world, device=local,
-                                              comm_id=comm, cidr=cidr)
+                                              comm_id=comm, allgather=gather, cidr=cidr)
     setup_s = time.perf_counter() - t0
 
     def barrier():
@@ -432,6 +443,8 @@ def main():
                            "note": "SoA state read + written per tick without the materialised heartbeat "
                                    "bodies, over the same k_tick launch time"},
         }
+        if REHEARSAL:
+            out["rehearsal"] = "all ranks on GPU 0, host allgather instead of RCCL: not a reported measurement"
         if churn is not None:
             out["churn"] = churn
         if flap is not None:
