@@ -153,7 +153,8 @@ typedef struct kwok_config {
     int64_t start_time_unix;       /* the StartTime() template func (controller.go:39-41) */
     int32_t enable_cni;            /* Config.EnableCNI: pod IPs come from the caller's CNI plugin
                                       (kwok_cni_pending / kwok_cni_assign); the ipPool is unused */
-    int32_t custom_templates;      /* must be 0: only templates.Default* are supported */
+    int32_t custom_templates;      /* 0: templates.Default*; 1: pod_status_template below (the node
+                                      templates stay the defaults) */
     uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
     uint32_t node_slots_per_bucket;
     uint32_t pod_slots_per_bucket; /* initial pod capacity of a bucket (multiple of 8); grows up to
@@ -170,6 +171,10 @@ typedef struct kwok_config {
                                       0 = pod_slots_per_bucket, i.e. no growth).  Handles stay valid
                                       when a bucket's capacity grows (KWOK_EFULL only past it). */
     uint32_t reserved0;
+    const char* pod_status_template; /* custom_templates = 1: Config.PodStatusTemplate (controller.go:76),
+                                        compiled per registered pod spec into the kernels' byte
+                                        program; KWOK_EDOMAIN when its output does not fit that
+                                        program (see kwok_template_render) */
 } kwok_config;
 
 /* fleet counters (kwok_tick_result.counters, summed over ranks) */
@@ -346,6 +351,27 @@ int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* tic
  * waiting for the device, host bookkeeping after the wait, whole call. */
 enum { KWOK_H_ENQUEUE = 0, KWOK_H_WAIT, KWOK_H_POST, KWOK_H_TOTAL, KWOK_H_COUNT };
 int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], uint64_t* ticks);
+
+/* Host only (no device): renderer.renderToJSON (renderer.go:49-89) - the
+ * covered subset of Go text/template, then sigs.k8s.io/yaml.YAMLToJSON - of
+ * template `tpl` over the JSON document `doc` (the object as json.Marshal gives
+ * it), with template funcs given as a JSON object of strings ({"Now": "...",
+ * "NodeIP": "...", ...}; YAML is built in).  This is the renderer custom pod
+ * status templates are compiled with.  *out_len = the output length
+ * (KWOK_EINVAL when cap is smaller); KWOK_EDOMAIN for a template, document or
+ * YAML outside the covered subset, with the reason in kwok_template_last_error(). */
+int kwok_template_render(const char* tpl, size_t tpl_len, const char* doc, size_t doc_len, const char* funcs,
+                         size_t funcs_len, char* out, size_t cap, size_t* out_len);
+const char* kwok_template_last_error(void);
+/* Host only: a custom pod status template compiled for one pod spec (as
+ * kwok_register_pod_spec does with custom_templates = 1), then assembled on the
+ * host exactly as the kernels assemble it: the patch bytes of a pod with that
+ * spec, creationTimestamp, hostIP (0: NodeIP), podIP and status emptiness.
+ * KWOK_EDOMAIN (reason in kwok_template_last_error) when the template does not
+ * compile to the kernels' program. */
+int kwok_pod_template_patch(const char* tpl, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
+                            int64_t start_unix, const char* node_ip, int64_t creation_unix, uint32_t host_ip,
+                            uint32_t pod_ip, int32_t status_nonempty, char* out, size_t cap, size_t* out_len);
 
 /* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);

@@ -16,6 +16,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 
 #include <algorithm>
@@ -30,6 +31,7 @@
 
 #include "../../include/kwok_engine.h"
 #include "device.h"
+#include "gotemplate.h"
 #include "kernels.h"
 #include "templates.h"
 
@@ -185,6 +187,8 @@ struct kwok_engine {
 
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
+    bool custom_pod = false;      // Config.PodStatusTemplate in use (compiled per spec)
+    std::string pod_tpl, start_s; // its text; StartTime() (RFC3339 of start_time_unix)
     std::vector<SpecDesc> specs_h;
     std::string spec_bytes_h;
     DevBuf<SpecDesc> d_specs;
@@ -804,6 +808,84 @@ const char* kwok_finalizer_patch(size_t* len) {
 }
 
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets) { return fnv1a32(name, len) & (buckets - 1); }
+
+namespace {
+thread_local std::string g_tpl_err;
+}
+const char* kwok_template_last_error(void) { return g_tpl_err.c_str(); }
+
+int kwok_pod_template_patch(const char* tpl, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
+                            int64_t start_unix, const char* node_ip, int64_t creation_unix, uint32_t host_ip,
+                            uint32_t pod_ip, int32_t status_nonempty, char* out, size_t cap, size_t* out_len) {
+    if (!tpl || !spec || !node_ip || !out_len || (cap && !out)) return KWOK_EINVAL;
+    g_tpl_err.clear();
+    auto get = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len ? std::string(arena + s.off, s.len) : std::string(); };
+    std::vector<Container> cs, ics;
+    std::vector<std::string> gates;
+    for (uint32_t i = 0; i < spec->n_containers; i++) cs.push_back({get(spec->containers[i].name), get(spec->containers[i].image)});
+    for (uint32_t i = 0; i < spec->n_init_containers; i++)
+        ics.push_back({get(spec->init_containers[i].name), get(spec->init_containers[i].image)});
+    for (uint32_t i = 0; i < spec->n_readiness_gates; i++) gates.push_back(get(spec->readiness_gates[i]));
+    auto rfc3339 = [](int64_t u) {
+        time_t t = (time_t)u;
+        struct tm tm;
+        gmtime_r(&t, &tm);
+        char b[32];
+        strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);
+        return std::string(b);
+    };
+    SpecProgram p;
+    if (!compile_pod_template(tpl, cs, ics, gates, rfc3339(start_unix), p, g_tpl_err)) return KWOK_EDOMAIN;
+    const std::string ts = rfc3339(creation_unix);
+    auto fill = [&](const std::string& seg, const std::string& kind) {
+        std::string o = seg;
+        for (size_t i = 0; i < o.size(); i++)
+            if ((uint8_t)kind[i] != KIND_LIT) o[i] = ts[(uint8_t)kind[i]];
+        return o;
+    };
+    std::string o = fill(p.a, p.ka);
+    if (status_nonempty) {  // the kernels' `{{ with .status }}` pieces (k_emit)
+        uint32_t nip = 0;
+        parse_ipv4(node_ip, strlen(node_ip), &nip);
+        o += "\"hostIP\":\"" + format_ipv4(host_ip ? host_ip : nip) + "\",";
+        o += fill(p.b, p.kb);
+        o += "\"podIP\":\"" + format_ipv4(pod_ip) + "\",";
+    } else {
+        o += fill(p.b, p.kb);
+    }
+    o += fill(p.c, p.kc);
+    *out_len = o.size();
+    if (o.size() > cap) return KWOK_EINVAL;
+    memcpy(out, o.data(), o.size());
+    return KWOK_OK;
+}
+
+int kwok_template_render(const char* tpl, size_t tpl_len, const char* doc, size_t doc_len, const char* funcs,
+                         size_t funcs_len, char* out, size_t cap, size_t* out_len) {
+    using namespace kwok::gotpl;
+    if (!tpl || !doc || !out_len || (cap && !out)) return KWOK_EINVAL;
+    g_tpl_err.clear();
+    VPtr d, f;
+    if (!parse_json(std::string(doc, doc_len), d, g_tpl_err)) return KWOK_EDOMAIN;
+    Env env;
+    if (funcs && funcs_len) {
+        if (!parse_json(std::string(funcs, funcs_len), f, g_tpl_err)) return KWOK_EDOMAIN;
+        if (f->kind != Value::MAP) {
+            g_tpl_err = "funcs must be a JSON object of strings";
+            return KWOK_EINVAL;
+        }
+        for (auto& kv : f->map) {
+            const std::string v = kv.second->s;
+            env.funcs[kv.first] = [v] { return v; };
+        }
+    }
+    std::string o;
+    if (!render_to_json(std::string(tpl, tpl_len), d, env, o, g_tpl_err)) return KWOK_EDOMAIN;
+    *out_len = o.size();
+    if (o.size() > cap) return KWOK_EINVAL;
+    memcpy(out, o.data(), o.size());
+    return KWOK_OK;
+}
 int32_t kwok_rank_of_bucket(uint32_t bucket, uint32_t buckets, int32_t world) {
     return (int32_t)(((uint64_t)bucket * (uint64_t)world) / buckets);
 }
@@ -854,7 +936,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!out) return KWOK_EINVAL;
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
-    if (cfg->custom_templates) return KWOK_EDOMAIN;  // only the default templates
+    if (cfg->custom_templates && (cfg->custom_templates != 1 || !cfg->pod_status_template))
+        return KWOK_EINVAL;  // 1 = a custom pod status template (the node templates stay the defaults)
     const uint32_t hs = cfg->pod_handle_stride ? cfg->pod_handle_stride : cfg->pod_slots_per_bucket;
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
         !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
@@ -900,6 +983,24 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!parse_ipv4(cfg->node_ip, strlen(cfg->node_ip), &e->node_ip) || !e->node_ip) return bail(KWOK_EDOMAIN);
     e->node_ip_s = format_ipv4(e->node_ip);
     if (cfg->start_time_unix < 0 || cfg->start_time_unix > 0xFFFFFFFFll) return bail(KWOK_EDOMAIN);
+    {
+        time_t t = (time_t)cfg->start_time_unix;
+        struct tm tm;
+        gmtime_r(&t, &tm);
+        char b[32];
+        strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);  // time.RFC3339 in UTC
+        e->start_s = b;
+    }
+    if (cfg->custom_templates) {
+        // compiled per spec at kwok_register_pod_spec; a trial spec rejects a template
+        // outside the covered subset here already
+        e->custom_pod = true;
+        e->pod_tpl = cfg->pod_status_template;
+        SpecProgram p;
+        std::string why;
+        if (!compile_pod_template(e->pod_tpl, {Container{"c", "img"}}, {}, {}, e->start_s, p, why))
+            return bail(e->fail(KWOK_EDOMAIN, "pod status template: %s", why.c_str()));
+    }
 
     {
         hipError_t r = hipSetDevice(e->dev);
@@ -1070,7 +1171,14 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
             return e->fail(KWOK_EDOMAIN, "init container %u: not a safe string", i);
     for (uint32_t i = 0; i < spec->n_readiness_gates; i++)
         if (!get(spec->readiness_gates[i], gates[i])) return e->fail(KWOK_EDOMAIN, "readiness gate %u: not a safe string", i);
-    SpecProgram p = build_spec_program(cs, ics, gates);
+    SpecProgram p;
+    if (e->custom_pod) {
+        std::string why;
+        if (!compile_pod_template(e->pod_tpl, cs, ics, gates, e->start_s, p, why))
+            return e->fail(KWOK_EDOMAIN, "pod status template: %s", why.c_str());
+    } else {
+        p = build_spec_program(cs, ics, gates);
+    }
     if (p.max_len > 0xFFF0) return e->fail(KWOK_EDOMAIN, "pod patch longer than 64 KiB");
     std::vector<uint16_t> nxt;
     if (!build_ts_lookup(p, nxt)) return e->fail(KWOK_EDOMAIN, "pod patch layout outside the emitter's domain");
@@ -1319,7 +1427,9 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 if (x.flags & KWOK_POD_HAS_FINALIZERS) bits |= PS_HAS_FIN;
                 // a status that holds an IP is not empty (`{{ with .status }}`)
                 if ((x.flags & KWOK_POD_STATUS_NONEMPTY) || hip || pip) bits |= PS_STATUS_NONEMPTY;
-                if (x.flags & KWOK_POD_CONFORMS) bits |= PS_CONFORMS;
+                // the caller's digest is of the default template; with a custom one a pod
+                // conforms once the engine has patched it (an extra, idempotent patch at most)
+                if ((x.flags & KWOK_POD_CONFORMS) && !e->custom_pod) bits |= PS_CONFORMS;
                 if (hip) bits |= PS_HAS_HOST_IP;
                 if (x.flags & KWOK_POD_DELETING) {
                     if (hn.managed) {  // pod_controller.go:306-308 -> deletePodChan

@@ -41,6 +41,16 @@ struct NodeBlob {
 NodeBlob build_node_blob(const std::string& addresses_json, const std::string& allocatable_json,
                          const std::string& capacity_json, const std::string info[10], const std::string& node_ip);
 
+// A custom pod status template (Config.PodStatusTemplate, controller.go:76)
+// compiled into the same program: rendered (gotemplate.h) over symbolic pod
+// documents of this spec - every status shape the engine emits, two sets of
+// sentinel timestamps / IPs - and accepted only if the outputs prove the
+// A | "hostIP":"H", | B | "podIP":"P", | C layout with creationTimestamp slots.
+// false + err: outside what the kernels emit (the caller's KWOK_EDOMAIN).
+bool compile_pod_template(const std::string& tpl, const std::vector<Container>& containers,
+                          const std::vector<Container>& init, const std::vector<std::string>& gates,
+                          const std::string& start_time, SpecProgram& out, std::string& err);
+
 // k_emit's timestamp-slot lookup of a spec (false: layout outside what it handles)
 bool build_ts_lookup(const SpecProgram& p, std::vector<uint16_t>& out);
 

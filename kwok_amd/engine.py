@@ -83,6 +83,10 @@ def declare(lib, pre):
             "tick_submit": (C.c_int, [VP, C.c_int64]),
             "tick_collect": (C.c_int, [VP, P(abi.TickResult)]),
             "codec_create": (C.c_int, [P(abi.CodecConfig), P(VP)]),
+            "template_render": (C.c_int, [C.c_char_p, SZ, C.c_char_p, SZ, C.c_char_p, SZ, VP, SZ, P(SZ)]),
+            "template_last_error": (C.c_char_p, []),
+            "pod_template_patch": (C.c_int, [C.c_char_p, P(abi.PodSpec), C.c_char_p, SZ, C.c_int64, C.c_char_p,
+                                             C.c_int64, U32, U32, I32, VP, SZ, P(SZ)]),
             "codec_destroy": (None, [VP]),
             "codec_last_error": (C.c_char_p, []),
             "selector_matches": (C.c_int, [C.c_char_p, C.c_char_p, SZ, P(I32)]),
@@ -117,7 +121,8 @@ class TickOutput:
 
 def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200, buckets=4096,
                 node_slots_per_bucket=64, pod_slots_per_bucket=512, max_pod_specs=1024, rank=0, world_size=1,
-                device=0, comm_id=None, allgather=None, enable_cni=False, pod_handle_stride=0):
+                device=0, comm_id=None, allgather=None, enable_cni=False, pod_handle_stride=0,
+                pod_status_template=None):
     cfg = abi.Config()
     cfg.abi_version = abi.ABI_VERSION
     cfg.cidr = cidr.encode()
@@ -131,6 +136,11 @@ def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200
     cfg.enable_cni = 1 if enable_cni else 0
     cfg.pod_handle_stride = pod_handle_stride
     keep = []
+    if pod_status_template is not None:
+        b = C.create_string_buffer(pod_status_template.encode())
+        keep.append(b)
+        cfg.custom_templates = 1
+        cfg.pod_status_template = C.cast(b, C.c_char_p)
     if comm_id is not None:
         b = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
         keep.append(b)
@@ -384,3 +394,46 @@ def finalizer_patch() -> bytes:
     n = C.c_size_t()
     p = lib.kwok_finalizer_patch(C.byref(n))
     return p[: n.value]
+
+
+def template_render(tpl: str, doc, funcs=None) -> str:
+    """kwok_template_render: renderToJSON of `tpl` over the document (a JSON
+    string or a JSON-able value) with zero-argument template funcs
+    {"Now": "...", ...}.  Host only."""
+    import json as _json
+    lib = load_engine_lib()
+    t = tpl.encode()
+    d = (doc if isinstance(doc, str) else _json.dumps(doc)).encode()
+    f = _json.dumps(funcs or {}).encode()
+    n = C.c_size_t()
+    cap = 1 << 16
+    while True:
+        out = C.create_string_buffer(cap)
+        rc = lib.kwok_template_render(t, len(t), d, len(d), f, len(f), out, cap, C.byref(n))
+        if rc == abi.EINVAL and n.value > cap:
+            cap = n.value + 1
+            continue
+        if rc != 0:
+            raise KwokError(rc, (lib.kwok_template_last_error() or b"").decode())
+        return out.raw[:n.value].decode()
+
+
+def pod_template_patch(tpl: str, containers=(), init_containers=(), readiness_gates=(), start=1704067200,
+                       node_ip="196.168.0.1", creation=1704067140, host_ip=0, pod_ip=0, status_nonempty=True) -> bytes:
+    """kwok_pod_template_patch: the patch the engine emits for a pod with this
+    spec under the custom pod status template (compiled + assembled on the host)."""
+    lib = load_engine_lib()
+    ar = abi.Arena()
+    cs = (abi.Container * max(1, len(containers)))(*[abi.Container(ar.kstr(n), ar.kstr(i)) for n, i in containers])
+    ics = (abi.Container * max(1, len(init_containers)))(
+        *[abi.Container(ar.kstr(n), ar.kstr(i)) for n, i in init_containers])
+    gs = (abi.KwokStr * max(1, len(readiness_gates)))(*[ar.kstr(g) for g in readiness_gates])
+    spec = abi.PodSpec(cs, len(containers), ics, len(init_containers), gs, len(readiness_gates))
+    buf, n = ar.cbuf()
+    out = C.create_string_buffer(1 << 16)
+    m = C.c_size_t()
+    rc = lib.kwok_pod_template_patch(tpl.encode(), C.byref(spec), buf, n, start, node_ip.encode(), creation, host_ip,
+                                     pod_ip, 1 if status_nonempty else 0, out, 1 << 16, C.byref(m))
+    if rc != 0:
+        raise KwokError(rc, (lib.kwok_template_last_error() or b"").decode())
+    return out.raw[:m.value]

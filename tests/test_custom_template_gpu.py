@@ -1,0 +1,98 @@
+"""GPU: custom pod status templates (Config.PodStatusTemplate, controller.go:76;
+SURVEY §8(f) rank 3).  The engine compiles the template per registered pod
+spec into the kernels' A | hostIP | B | podIP | C program; every pod patch
+k_emit writes must equal the host assembly of that program
+(kwok_pod_template_patch, checked against tests/golden/gotmpl.py in
+tests/test_template_cpu.py) and, for a sample, gotmpl.py itself.  Who is
+patched, IP allocation, deletes and counters do not depend on the template:
+they must equal the oracle's (default template) on the same events."""
+import ipaddress
+
+import numpy as np
+import pytest
+
+from gpu_common import compare_state, new_pods
+from kwok_amd import abi, engine
+from kwok_amd.engine import Engine, make_config
+from oracle.oracle import Oracle
+from test_template_cpu import expected_patch, tpl
+
+pytestmark = pytest.mark.gpu
+
+SPECS = [([("fake-pod", "fake")], [], []),
+         ([("a", "img-a"), ("b", "img/b:v2")], [("init", "busybox")], ["g.io/x"]),
+         ([], [("i0", "registry.k8s.io/pause:3.9"), ("i1", "busybox:1.36")], ["g.io/a", "g.io/b"])]
+
+
+@pytest.mark.parametrize("name", ["pod_a.tpl", "pod_b.tpl"])
+def test_custom_pod_template_engine(name):
+    text = tpl(name)
+    kw = dict(cidr="10.0.0.1/16", node_ip="196.168.0.1", buckets=256, node_slots_per_bucket=16,
+              pod_slots_per_bucket=256)
+    e = Engine(make_config(pod_status_template=text, **kw))
+    o = Oracle(make_config(**kw))
+    spec = [e.register_pod_spec(*s) for s in SPECS]
+    assert spec == [o.register_pod_spec(*s) for s in SPECS]
+    rng = np.random.default_rng(5)
+    ar = abi.Arena()
+    names = ["node-%04d" % i for i in range(300)]
+    ev = np.zeros(len(names), abi.NODE_EVENT_DTYPE)
+    ev["op"] = abi.OP_UPSERT
+    ev["managed"] = 1
+    ev["lockable"] = 1
+    for i, n in enumerate(names):
+        ev[i]["name"] = ar.ref(n)
+    nh, st = e.ingest_nodes_raw(ev, bytes(ar.buf))
+    assert (o.ingest_nodes_raw(ev, bytes(ar.buf))[0] == nh).all()
+    n_slots = 256 * 256
+    meta = {}  # handle -> (spec index, creation, original hostIP, status non-empty)
+    now = 1704067230
+    for t in range(3):
+        pods, par = new_pods(rng, nh, 4000, spec, host_ips=("10.9.8.7", "172.16.0.1"), host_ip_frac=0.3,
+                             years=40)
+        pods["flags"] &= ~abi.POD_DISREGARD
+        h1, s1, _ = e.ingest_pods_raw(pods, par)
+        h2, s2, _ = o.ingest_pods_raw(pods, par)
+        assert (h1 == h2).all() and (s1 == s2).all()
+        for i, h in enumerate(h1):
+            hip = 0
+            if pods[i]["host_ip"]["len"]:
+                off = int(pods[i]["host_ip"]["off"])
+                hip = int(ipaddress.IPv4Address(par[off:off + int(pods[i]["host_ip"]["len"])].decode()))
+            meta[int(h)] = (spec.index(int(pods[i]["spec_id"])), int(pods[i]["creation_unix"]), hip,
+                            bool(pods[i]["flags"] & abi.POD_STATUS_NONEMPTY))
+        if t:  # deletions: IP release and reuse in the same tick
+            live = np.array(sorted(meta), np.int32)
+            dead = rng.choice(live, 500, replace=False)
+            d = np.zeros(len(dead), abi.POD_EVENT_DTYPE)
+            d["op"] = abi.OP_DELETE
+            d["handle"] = dead
+            assert (e.ingest_pods_raw(d, b"")[1] == o.ingest_pods_raw(d, b"")[1]).all()
+            for h in dead:
+                meta.pop(int(h))
+        E, O = e.tick(now), o.tick(now)
+        now += 30
+        assert E.counters == O.counters, t
+        assert [h for h, _ in E.pod_patches] == [h for h, _ in O.pod_patches], t
+        assert E.deletes == O.deletes and list(E.heartbeat_nodes) == list(O.heartbeat_nodes)
+        compare_state(e, o, n_slots, "custom template tick %d" % t)
+        used, phase, hips, pips = e.dump_pods(0, n_slots)
+        for k, (h, got) in enumerate(E.pod_patches):
+            si, ct, hip, ne = meta[h]
+            cs, ics, gates = SPECS[si]
+            want = engine.pod_template_patch(text, cs, ics, gates, 1704067200, "196.168.0.1", ct, hip,
+                                             int(pips[h]), ne)
+            assert got == want, "tick %d pod %d" % (t, h)
+            if k % 97 == 0:
+                assert got == expected_patch(text, cs, ics, gates, ct, hip, int(pips[h]), ne)
+        for h, _ in E.pod_patches:  # applied: the status is no longer empty
+            si, ct, hip, _ = meta[h]
+            meta[h] = (si, ct, hip, True)
+    e.close()
+    o.close()
+
+
+def test_custom_template_rejected_at_create():
+    with pytest.raises(engine.KwokError):
+        Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8,
+                           pod_status_template="conditions: []\nstartTime: {{ Now }}\n"))
