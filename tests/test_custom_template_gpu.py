@@ -50,7 +50,7 @@ def test_custom_pod_template_engine(name):
     for t in range(3):
         pods, par = new_pods(rng, nh, 4000, spec, host_ips=("10.9.8.7", "172.16.0.1"), host_ip_frac=0.3,
                              years=40)
-        pods["flags"] &= ~abi.POD_DISREGARD
+        pods["flags"] &= np.uint8(0xFF & ~abi.POD_DISREGARD)
         h1, s1, _ = e.ingest_pods_raw(pods, par)
         h2, s2, _ = o.ingest_pods_raw(pods, par)
         assert (h1 == h2).all() and (s1 == s2).all()
