@@ -153,8 +153,9 @@ typedef struct kwok_config {
     int64_t start_time_unix;       /* the StartTime() template func (controller.go:39-41) */
     int32_t enable_cni;            /* Config.EnableCNI: pod IPs come from the caller's CNI plugin
                                       (kwok_cni_pending / kwok_cni_assign); the ipPool is unused */
-    int32_t custom_templates;      /* 0: templates.Default*; 1: pod_status_template below (the node
-                                      templates stay the defaults) */
+    int32_t custom_templates;      /* bit mask: 0 = templates.Default*; KWOK_TPL_POD: pod_status_template
+                                      below, KWOK_TPL_NODE_INIT: node_init_template below (the
+                                      heartbeat template is always the default) */
     uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
     uint32_t node_slots_per_bucket;
     uint32_t pod_slots_per_bucket; /* initial pod capacity of a bucket (multiple of 8); grows up to
@@ -171,11 +172,15 @@ typedef struct kwok_config {
                                       0 = pod_slots_per_bucket, i.e. no growth).  Handles stay valid
                                       when a bucket's capacity grows (KWOK_EFULL only past it). */
     uint32_t reserved0;
-    const char* pod_status_template; /* custom_templates = 1: Config.PodStatusTemplate (controller.go:76),
+    const char* pod_status_template; /* KWOK_TPL_POD: Config.PodStatusTemplate (controller.go:76),
                                         compiled per registered pod spec into the kernels' byte
                                         program; KWOK_EDOMAIN when its output does not fit that
-                                        program (see kwok_template_render) */
+                                        program (see kwok_pod_template_patch) */
+    const char* node_init_template;  /* KWOK_TPL_NODE_INIT: Config.NodeInitializationTemplate
+                                        (controller.go:75), compiled per distinct node status into
+                                        the node's init blob (see kwok_node_template_patch) */
 } kwok_config;
+enum { KWOK_TPL_POD = 1, KWOK_TPL_NODE_INIT = 2 };
 
 /* fleet counters (kwok_tick_result.counters, summed over ranks) */
 enum {
@@ -372,6 +377,12 @@ const char* kwok_template_last_error(void);
 int kwok_pod_template_patch(const char* tpl, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
                             int64_t start_unix, const char* node_ip, int64_t creation_unix, uint32_t host_ip,
                             uint32_t pod_ip, int32_t status_nonempty, char* out, size_t cap, size_t* out_len);
+/* Host only: the init patch (LockNode / configureNode) of the node in `ev` under
+ * a custom node initialization template, at heartbeat time now_unix, as the
+ * engine compiles and the kernels assemble it. */
+int kwok_node_template_patch(const char* tpl, const kwok_node_event* ev, const char* arena, size_t arena_len,
+                             int64_t start_unix, const char* node_ip, int64_t now_unix, char* out, size_t cap,
+                             size_t* out_len);
 
 /* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);

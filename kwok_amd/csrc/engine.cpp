@@ -188,7 +188,9 @@ struct kwok_engine {
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
     bool custom_pod = false;      // Config.PodStatusTemplate in use (compiled per spec)
-    std::string pod_tpl, start_s; // its text; StartTime() (RFC3339 of start_time_unix)
+    bool custom_node = false;     // Config.NodeInitializationTemplate in use (compiled per node status)
+    std::string pod_tpl, node_tpl, start_s;  // their texts; StartTime() (RFC3339 of start_time_unix)
+    std::unordered_map<std::string, uint64_t> node_tpl_blobs;  // node status fields -> compiled blob
     std::vector<SpecDesc> specs_h;
     std::string spec_bytes_h;
     DevBuf<SpecDesc> d_specs;
@@ -814,6 +816,33 @@ thread_local std::string g_tpl_err;
 }
 const char* kwok_template_last_error(void) { return g_tpl_err.c_str(); }
 
+int kwok_node_template_patch(const char* tpl, const kwok_node_event* ev, const char* arena, size_t arena_len,
+                             int64_t start_unix, const char* node_ip, int64_t now_unix, char* out, size_t cap,
+                             size_t* out_len) {
+    if (!tpl || !ev || !node_ip || !out_len || (cap && !out)) return KWOK_EINVAL;
+    g_tpl_err.clear();
+    auto get = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len ? std::string(arena + s.off, s.len) : std::string(); };
+    std::string info[KWOK_NI_COUNT];
+    for (int k = 0; k < KWOK_NI_COUNT; k++) info[k] = get(ev->node_info[k]);
+    auto rfc3339 = [](int64_t u) {
+        time_t t = (time_t)u;
+        struct tm tm;
+        gmtime_r(&t, &tm);
+        char b[32];
+        strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);
+        return std::string(b);
+    };
+    NodeBlob nb;
+    if (!compile_node_template(tpl, get(ev->addresses), get(ev->allocatable), get(ev->capacity), info, ev->phase, node_ip,
+                               rfc3339(start_unix), nb, g_tpl_err))
+        return KWOK_EDOMAIN;
+    const std::string o = nb.pre + heartbeat_conditions(rfc3339(now_unix), rfc3339(start_unix)) + nb.post;
+    *out_len = o.size();
+    if (o.size() > cap) return KWOK_EINVAL;
+    memcpy(out, o.data(), o.size());
+    return KWOK_OK;
+}
+
 int kwok_pod_template_patch(const char* tpl, const kwok_pod_spec* spec, const char* arena, size_t arena_len,
                             int64_t start_unix, const char* node_ip, int64_t creation_unix, uint32_t host_ip,
                             uint32_t pod_ip, int32_t status_nonempty, char* out, size_t cap, size_t* out_len) {
@@ -936,8 +965,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!out) return KWOK_EINVAL;
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
-    if (cfg->custom_templates && (cfg->custom_templates != 1 || !cfg->pod_status_template))
-        return KWOK_EINVAL;  // 1 = a custom pod status template (the node templates stay the defaults)
+    if ((cfg->custom_templates & ~(KWOK_TPL_POD | KWOK_TPL_NODE_INIT)) ||
+        ((cfg->custom_templates & KWOK_TPL_POD) && !cfg->pod_status_template) ||
+        ((cfg->custom_templates & KWOK_TPL_NODE_INIT) && !cfg->node_init_template))
+        return KWOK_EINVAL;
     const uint32_t hs = cfg->pod_handle_stride ? cfg->pod_handle_stride : cfg->pod_slots_per_bucket;
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
         !cfg->node_slots_per_bucket || cfg->node_slots_per_bucket > 65536 || cfg->pod_slots_per_bucket % 8 ||
@@ -991,7 +1022,16 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);  // time.RFC3339 in UTC
         e->start_s = b;
     }
-    if (cfg->custom_templates) {
+    if (cfg->custom_templates & KWOK_TPL_NODE_INIT) {
+        // compiled per node status at ingest; a trial node rejects a template outside the subset here
+        e->custom_node = true;
+        e->node_tpl = cfg->node_init_template;
+        NodeBlob b;
+        std::string why, info[KWOK_NI_COUNT];
+        if (!compile_node_template(e->node_tpl, "", "", "", info, KWOK_PHASE_NONE, e->node_ip_s, e->start_s, b, why))
+            return bail(e->fail(KWOK_EDOMAIN, "node initialization template: %s", why.c_str()));
+    }
+    if (cfg->custom_templates & KWOK_TPL_POD) {
         // compiled per spec at kwok_register_pod_spec; a trial spec rejects a template
         // outside the covered subset here already
         e->custom_pod = true;
@@ -1267,7 +1307,26 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 for (int k = 0; k < KWOK_NI_COUNT; k++) empty = empty && info[k].empty();
                 int brc = KWOK_OK;
                 uint64_t blob = 0;
-                if (empty && e->has_empty_blob) {
+                if (e->custom_node) {
+                    // one compile per distinct status (the fields the template may read)
+                    std::string key = std::to_string(x.phase);
+                    for (int k = 0; k < 3; k++) key += '\x01' + js[k];
+                    for (int k = 0; k < KWOK_NI_COUNT; k++) key += '\x01' + info[k];
+                    auto it = e->node_tpl_blobs.find(key);
+                    if (it != e->node_tpl_blobs.end()) {
+                        blob = it->second;
+                    } else {
+                        NodeBlob nb;
+                        std::string why;
+                        if (!compile_node_template(e->node_tpl, js[0], js[1], js[2], info, x.phase, e->node_ip_s,
+                                                   e->start_s, nb, why)) {
+                            brc = KWOK_EDOMAIN;
+                        } else {
+                            blob = intern_blob(e, nb, &brc);
+                            if (!brc) e->node_tpl_blobs.emplace(std::move(key), blob);
+                        }
+                    }
+                } else if (empty && e->has_empty_blob) {
                     blob = e->empty_blob;
                 } else {
                     NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
@@ -1288,7 +1347,8 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                     hn.lockable = x.lockable ? 1 : 0;
                     bool ev_lock = x.managed && x.lockable;
                     uint8_t bits = (uint8_t)(NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
-                                             (node_conforms(x, info) ? NS_CONFORMS : 0) | (ev_lock ? NS_EVENT_LOCK : 0));
+                                             (!e->custom_node && node_conforms(x, info) ? NS_CONFORMS : 0) |
+                                             (ev_lock ? NS_EVENT_LOCK : 0));
                     node_op(e, slot, ev_lock ? 0 : NS_EVENT_LOCK, bits, true, blob);
                     handle = (int32_t)(e->b_lo * e->Cn + slot);
                 }

@@ -295,6 +295,15 @@ struct Exec {
     std::vector<std::pair<std::string, VPtr>> vars;
     std::string out;
 
+    bool allowed(const std::string& p) const {
+        for (const std::string& a : *env.allowed_paths) {
+            if (a == p) return true;
+            if (a.size() >= 2 && a.compare(a.size() - 2, 2, ".*") == 0 && p.size() > a.size() - 2 &&
+                p.compare(0, a.size() - 2, a, 0, a.size() - 2) == 0 && (p[a.size() - 2] == '.' || p[a.size() - 2] == '['))
+                return true;
+        }
+        return false;
+    }
     VPtr field(VPtr v, const std::string& chain) {  // ".a.b" (or "" for v)
         size_t i = 0;
         while (i < chain.size()) {
@@ -306,9 +315,7 @@ struct Exec {
             if (name.empty()) continue;
             if (v->kind != Value::MAP) fail("field ." + name + " of a non-map value is outside the subset");
             const std::string p = v->path + "." + name;
-            if (env.allowed_paths &&
-                std::find(env.allowed_paths->begin(), env.allowed_paths->end(), p) == env.allowed_paths->end())
-                fail("the template reads " + p + ", which the engine does not hold per pod spec");
+            if (env.allowed_paths && !allowed(p)) fail("the template reads " + p + ", which the engine does not hold");
             auto it = std::lower_bound(v->map.begin(), v->map.end(), name,
                                        [](const auto& kv, const std::string& k) { return kv.first < k; });
             v = (it != v->map.end() && it->first == name) ? it->second : make_noval(p);
@@ -981,8 +988,9 @@ bool parse_json(const std::string& s, VPtr& out, std::string& err) {
     }
 }
 
-bool yaml_to_json(const std::string& yaml, std::string& out, std::string& err) {
-    try {
+namespace {
+VPtr yaml_tree(const std::string& yaml) {
+    {
         YamlParser p;
         size_t pos = 0;
         bool started = false;
@@ -1008,8 +1016,20 @@ bool yaml_to_json(const std::string& yaml, std::string& out, std::string& err) {
         }
         VPtr v = p.lines.empty() ? make_null() : p.node(p.lines[0].indent);
         if (p.at != p.lines.size()) fail("unparsed YAML from: " + p.lines[p.at].s);
-        out.clear();
-        json_emit(out, v);
+        return v;
+    }
+}
+}  // namespace
+
+std::string to_json(const VPtr& v) {
+    std::string o;
+    json_emit(o, v);
+    return o;
+}
+
+bool yaml_to_json(const std::string& yaml, std::string& out, std::string& err) {
+    try {
+        out = to_json(yaml_tree(yaml));
         return true;
     } catch (const Fail& f) {
         err = f.msg;
@@ -1017,7 +1037,7 @@ bool yaml_to_json(const std::string& yaml, std::string& out, std::string& err) {
     }
 }
 
-bool render_to_json(const std::string& tpl, const VPtr& doc, const Env& env, std::string& out, std::string& err) {
+bool execute_template(const std::string& tpl, const VPtr& doc, const Env& env, std::string& text, std::string& err) {
     try {
         size_t a = 0, b = tpl.size();  // strings.TrimSpace
         while (a < b && isspace((unsigned char)tpl[a])) a++;
@@ -1026,11 +1046,36 @@ bool render_to_json(const std::string& tpl, const VPtr& doc, const Env& env, std
         Exec x{env, {}, {}};
         x.vars.push_back({"$", doc});
         x.run(nodes, doc);
-        return yaml_to_json(x.out, out, err);
+        text = std::move(x.out);
+        return true;
     } catch (const Fail& f) {
         err = f.msg;
         return false;
     }
+}
+
+bool render_to_tree(const std::string& tpl, const VPtr& doc, const Env& env, VPtr& out, std::string& err) {
+    try {
+        size_t a = 0, b = tpl.size();  // strings.TrimSpace
+        while (a < b && isspace((unsigned char)tpl[a])) a++;
+        while (b > a && isspace((unsigned char)tpl[b - 1])) b--;
+        std::vector<Node> nodes = parse_template(tpl.substr(a, b - a));
+        Exec x{env, {}, {}};
+        x.vars.push_back({"$", doc});
+        x.run(nodes, doc);
+        out = yaml_tree(x.out);
+        return true;
+    } catch (const Fail& f) {
+        err = f.msg;
+        return false;
+    }
+}
+
+bool render_to_json(const std::string& tpl, const VPtr& doc, const Env& env, std::string& out, std::string& err) {
+    VPtr t;
+    if (!render_to_tree(tpl, doc, env, t, err)) return false;
+    out = to_json(t);
+    return true;
 }
 
 }  // namespace gotpl

@@ -40,13 +40,18 @@ VPtr with_paths(const VPtr& v, const std::string& path);
 struct Env {
     // template funcs by name (zero-argument funcs return a string)
     std::map<std::string, std::function<std::string()>> funcs;
-    // nullptr: any field may be read; else only paths in the set
+    // nullptr: any field may be read; else only paths in the set ("$.a.*": $.a's subtree)
     const std::vector<std::string>* allowed_paths = nullptr;
 };
 
 // renderToJSON: TrimSpace, parse, execute over doc, YAMLToJSON.  false + err on
 // anything outside the covered subset (or a Go template / YAML error).
 bool render_to_json(const std::string& tpl, const VPtr& doc, const Env& env, std::string& out, std::string& err);
+// the same, stopping at the YAML tree (a null value for an empty output)
+bool render_to_tree(const std::string& tpl, const VPtr& doc, const Env& env, VPtr& out, std::string& err);
+std::string to_json(const VPtr& v);  // encoding/json.Marshal
+// template execution alone (the text YAMLToJSON would read)
+bool execute_template(const std::string& tpl, const VPtr& doc, const Env& env, std::string& text, std::string& err);
 
 // helpers exposed for tests (kwok_template_render) and the compiler
 bool parse_json(const std::string& s, VPtr& out, std::string& err);

@@ -51,6 +51,19 @@ bool compile_pod_template(const std::string& tpl, const std::vector<Container>& 
                           const std::vector<Container>& init, const std::vector<std::string>& gates,
                           const std::string& start_time, SpecProgram& out, std::string& err);
 
+// A custom node initialization template (Config.NodeInitializationTemplate,
+// controller.go:75) for one node's status fields, compiled into the framed
+// blob: NewNodeController renders it followed by the heartbeat template
+// (node_controller.go:101), so the init patch is pre | the heartbeat's
+// conditions list (the kernels' CONDS, with Now / StartTime) | post.
+// phase: KWOK_PHASE_NONE / RUNNING / OTHER of the node event.
+bool compile_node_template(const std::string& tpl, const std::string& addresses_json,
+                           const std::string& allocatable_json, const std::string& capacity_json,
+                           const std::string info[10], int phase, const std::string& node_ip,
+                           const std::string& start_time, NodeBlob& out, std::string& err);
+// the heartbeat conditions list (CONDS) rendered at now / start (RFC3339)
+std::string heartbeat_conditions(const std::string& now, const std::string& start);
+
 // k_emit's timestamp-slot lookup of a spec (false: layout outside what it handles)
 bool build_ts_lookup(const SpecProgram& p, std::vector<uint16_t>& out);
 

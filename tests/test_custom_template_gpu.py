@@ -96,3 +96,36 @@ def test_custom_template_rejected_at_create():
     with pytest.raises(engine.KwokError):
         Engine(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8,
                            pod_status_template="conditions: []\nstartTime: {{ Now }}\n"))
+
+
+def test_custom_node_init_template_engine():
+    """node_a.tpl for the init patches (compiled per distinct node status into
+    the node's blob; the heartbeat conditions spliced in by k_emit)"""
+    from test_template_cpu import NODES, node_record
+    text = tpl("node_a.tpl")
+    kw = dict(cidr="10.0.0.1/16", node_ip="196.168.0.1", buckets=64, node_slots_per_bucket=16,
+              pod_slots_per_bucket=64)
+    e = Engine(make_config(node_init_template=text, pod_status_template=tpl("pod_b.tpl"), **kw))
+    o = Oracle(make_config(**kw))
+    recs = {}
+    for i in range(300):
+        ev, ar = node_record(NODES[i % len(NODES)], "node-%04d" % i)
+        h1, s1 = e.ingest_nodes_raw(ev, ar)
+        h2, s2 = o.ingest_nodes_raw(ev, ar)
+        assert s1[0] == 0 and h1[0] == h2[0]
+        recs[int(h1[0])] = (ev, ar)
+    now = 1704067230
+    for t in range(2):
+        E, O = e.tick(now), o.tick(now)
+        assert list(E.heartbeat_nodes) == list(O.heartbeat_nodes)
+        assert E.heartbeat_body(0) == O.heartbeat_body(0)
+        if t == 0:
+            assert sorted(h for h, _ in E.node_inits) == sorted(recs)  # every node is initialised once
+        else:
+            assert E.node_inits == []  # the engine applied its patches: the nodes conform now
+        for h, got in E.node_inits:
+            ev, ar = recs[h]
+            assert got == engine.node_template_patch(text, ev[0], ar, 1704067200, "196.168.0.1", now), h
+        now += 30
+    e.close()
+    o.close()

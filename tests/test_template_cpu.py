@@ -157,3 +157,87 @@ def test_comments_trim_markers_else_if():
     for bad in ("k: {{ printf \"%d\" 1 }}", "k: {{ .b", "{{ if .a }}x", "k: |\n  block\n", "k: 0x10\n"):
         with pytest.raises(KwokError):
             engine.template_render(bad, doc)
+
+
+# ---- custom node initialization templates ----------------------------------
+NODES = [
+    {},
+    {"addresses": '[{"address":"10.9.9.9","type":"InternalIP"}]',
+     "allocatable": '{"cpu":"4","memory":"8Gi","pods":"110"}', "capacity": '{"cpu":"4","memory":"8Gi","pods":"110"}',
+     "nodeInfo": {"architecture": "arm64", "osImage": "ubuntu", "kubeletVersion": "v1.26.0"}, "phase": 2},
+    {"allocatable": '{"cpu":"1","pods":"8"}', "nodeInfo": {"kernelVersion": "6.1.0"}},
+]
+
+
+def node_record(n, name="n0"):
+    from kwok_amd import abi
+    ar = abi.Arena()
+    ev = np.zeros(1, abi.NODE_EVENT_DTYPE)
+    ev["op"] = abi.OP_UPSERT
+    ev["managed"] = 1
+    ev["lockable"] = 1
+    ev["phase"] = n.get("phase", 0)
+    ev[0]["name"] = ar.ref(name)
+    for f in ("addresses", "allocatable", "capacity"):
+        ev[0][f] = ar.ref(n.get(f, ""))
+    for k, key in enumerate(abi.NODEINFO_KEYS):
+        ev[0]["node_info"][k] = ar.ref(n.get("nodeInfo", {}).get(key, ""))
+    return ev, bytes(ar.buf)
+
+
+def node_doc(n):
+    st = {"daemonEndpoints": {"kubeletEndpoint": {"Port": 0}},
+          "nodeInfo": {k: n.get("nodeInfo", {}).get(k, "") for k in
+                       __import__("kwok_amd.abi", fromlist=["x"]).NODEINFO_KEYS}}
+    for f in ("addresses", "allocatable", "capacity"):
+        if n.get(f):
+            st[f] = json.loads(n[f])
+    if n.get("phase") == 2:
+        st["phase"] = "Running"
+    return {"metadata": {"name": "n0"}, "spec": {}, "status": st}
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_TPL), reason="reference templates not present")
+@pytest.mark.parametrize("which", ["reference", "node_a.tpl"])
+def test_node_templates_compile_and_match_gotmpl(which):
+    rd = lambda f: open(os.path.join(REF_TPL, f)).read()  # noqa: E731
+    text = rd("node.status.tpl") if which == "reference" else tpl(which)
+    full = text + "\n" + rd("node.heartbeat.tpl")  # node_controller.go:101
+    now = START + 30
+    funcs = {"NodeIP": lambda: NODE_IP, "Now": lambda: rfc3339(now), "StartTime": lambda: rfc3339(START)}
+    for n in NODES:
+        ev, ar = node_record(n)
+        got = engine.node_template_patch(text, ev[0], ar, START, NODE_IP, now)
+        want = ('{"status":%s}' % gotmpl.render_to_json(full, node_doc(n), funcs)).encode()
+        assert got == want, n
+
+
+def test_node_templates_outside_the_blob_are_rejected():
+    """a node template must leave the conditions to the heartbeat template and
+    read only the status fields the engine holds"""
+    bad = "conditions: []\nphase: Running\n"
+    ev, ar = node_record({})
+    with pytest.raises(KwokError):
+        engine.node_template_patch(bad, ev[0], ar)
+    with pytest.raises(KwokError):  # Now outside the conditions varies per tick
+        engine.node_template_patch("phase: Running\nx: {{ Now }}\n", ev[0], ar)
+    with pytest.raises(KwokError):  # a field the engine does not hold
+        engine.node_template_patch("phase: {{ .metadata.name }}\n", ev[0], ar)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_TPL), reason="reference templates not present")
+def test_reference_node_template_compiles_to_the_default_blob():
+    """the generic compiler, fed the reference's node.status.tpl, gives the init
+    patch the built-in default path gives (the oracle's, pinned by the goldens)"""
+    from kwok_amd.engine import make_config
+    from oracle.oracle import Oracle
+    text = open(os.path.join(REF_TPL, "node.status.tpl")).read()
+    for n in NODES:
+        o = Oracle(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, node_ip=NODE_IP,
+                               start_time=START))
+        ev, ar = node_record(n)
+        o.ingest_nodes_raw(ev, ar)
+        out = o.tick(START + 30)
+        assert len(out.node_inits) == 1
+        assert engine.node_template_patch(text, ev[0], ar, START, NODE_IP, START + 30) == out.node_inits[0][1], n
+        o.close()
