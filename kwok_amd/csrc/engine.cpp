@@ -378,6 +378,7 @@ void run_parts(kwok_engine* e, bool parallel, F&& f) {
     e->workers.run(e->n_part, fn);
 }
 constexpr size_t PAR_MIN = 32768;  // records (or deletes) per call before the partitions get threads
+constexpr size_t NODE_PAR_MIN = 2048;  // node records (the per-record work is heavier)
 
 // ---- per-batch op coalescing: ops for the same slot compose in order ----
 void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
@@ -1259,13 +1260,16 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
-    int rejected = 0;
-    const auto tn0 = std::chrono::steady_clock::now();
-    for (size_t i = 0; i < n; i++) {
+    auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+    // per partition: managed-set changes (applied after the batch)
+    std::vector<int64_t> d_managed((size_t)e->n_part, 0);
+    std::vector<uint8_t> set_changed((size_t)e->n_part, 0);
+    std::mutex blob_mu;  // blob interning (host string + device upload) and the template cache
+    // WatchNodes / ListNodes event switch (node_controller.go:256-270) for one record
+    auto ingest_one = [&](size_t i, int part) {
         const kwok_node_event& x = ev[i];
         int st = KWOK_OK;
         int32_t handle = -1;
-        auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
         if (!x.name.len || x.name.len > 253 || !in_arena(x.name)) st = KWOK_EDOMAIN;
         const char* name = arena + x.name.off;
         uint32_t slot = 0;
@@ -1274,7 +1278,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
             st = node_slot(e, name, x.name.len, false, &slot);
             if (st == KWOK_OK) {
                 auto& hn = e->nodes[slot];
-                if (hn.managed) e->n_managed--, e->mb_count[slot / e->Cn]--, e->hb_pre_dirty = true, e->hb_epoch++;
+                if (hn.managed) d_managed[(size_t)part]--, e->mb_count[slot / e->Cn]--, set_changed[(size_t)part] = 1;
                 hn.exists = hn.managed = 0;
                 node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
                         false, 0);
@@ -1307,6 +1311,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 for (int k = 0; k < KWOK_NI_COUNT; k++) empty = empty && info[k].empty();
                 int brc = KWOK_OK;
                 uint64_t blob = 0;
+                std::lock_guard<std::mutex> lock(blob_mu);
                 if (e->custom_node) {
                     // one compile per distinct status (the fields the template may read)
                     std::string key = std::to_string(x.phase);
@@ -1339,10 +1344,9 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                     hn.exists = 1;
                     if (x.managed && !hn.managed) {  // never cleared but by Delete
                         hn.managed = 1;
-                        e->n_managed++;
+                        d_managed[(size_t)part]++;
                         e->mb_count[slot / e->Cn]++;
-                        e->hb_pre_dirty = true;
-                        e->hb_epoch++;
+                        set_changed[(size_t)part] = 1;
                     }
                     hn.lockable = x.lockable ? 1 : 0;
                     bool ev_lock = x.managed && x.lockable;
@@ -1358,8 +1362,49 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         }
         if (out_handles) out_handles[i] = handle;
         if (out_status) out_status[i] = st;
-        if (st != KWOK_OK) rejected++;
+        return st != KWOK_OK;
+    };
+    // the bucket (owned, local) a record changes, or -1 (rejected / another rank's)
+    auto bucket_of_record = [&](const kwok_node_event& x) -> int64_t {
+        if (!x.name.len || x.name.len > 253 || !in_arena(x.name)) return -1;
+        const uint32_t b = fnv1a32(arena + x.name.off, x.name.len) & (e->B - 1);
+        return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
+    };
+    const auto tn0 = std::chrono::steady_clock::now();
+    std::vector<int> rej((size_t)e->n_part, 0);
+    if (n < NODE_PAR_MIN || e->n_part == 1) {
+        for (size_t i = 0; i < n; i++) {
+            const int64_t bl = bucket_of_record(ev[i]);
+            const int part = bl < 0 ? 0 : (int)((uint64_t)bl * e->n_part / e->nb);
+            rej[(size_t)part] += ingest_one(i, part);
+        }
+    } else {
+        // partitions own bucket ranges (as for pods); each takes its records in batch order
+        std::vector<uint8_t> part(n);
+        const int P = e->n_part;
+        run_parts(e, true, [&](int c) {
+            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
+            for (size_t i = lo; i < hi; i++) {
+                const int64_t bl = bucket_of_record(ev[i]);
+                part[i] = (uint8_t)(bl < 0 ? 0 : (uint64_t)bl * (uint64_t)P / e->nb);
+            }
+        });
+        run_parts(e, true, [&](int p) {
+            for (size_t i = 0; i < n; i++)
+                if (part[i] == (uint8_t)p) rej[(size_t)p] += ingest_one(i, p);
+        });
     }
+    int rejected = 0;
+    for (int p = 0; p < e->n_part; p++) {
+        rejected += rej[(size_t)p];
+        e->n_managed = (uint64_t)((int64_t)e->n_managed + d_managed[(size_t)p]);
+        if (set_changed[(size_t)p]) e->hb_pre_dirty = true;
+    }
+    for (uint8_t c : set_changed)
+        if (c) {
+            e->hb_epoch++;  // the managed set changed in this batch
+            break;
+        }
     const auto tn1 = std::chrono::steady_clock::now();
     int rc = size_arena(e);
     if (rc) return rc;
