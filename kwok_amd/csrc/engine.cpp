@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -200,7 +201,7 @@ struct kwok_engine {
     uint32_t max_pod_len = 0;
     std::unordered_map<std::string, uint64_t> blob_ids;
     uint64_t empty_blob = 0;      // the blob of a node with an empty status (every status field absent)
-    bool has_empty_blob = false;
+    std::atomic<bool> has_empty_blob{false};
     std::string blob_h;
     DevBuf<uint8_t> d_blob;
     uint32_t max_init_len = 0;
@@ -1311,8 +1312,14 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 for (int k = 0; k < KWOK_NI_COUNT; k++) empty = empty && info[k].empty();
                 int brc = KWOK_OK;
                 uint64_t blob = 0;
-                std::lock_guard<std::mutex> lock(blob_mu);
-                if (e->custom_node) {
+                // the empty-status blob, once built, is read without the lock (it is
+                // written only under it, before any thread can see has_empty_blob)
+                const bool fast = !e->custom_node && empty && e->has_empty_blob.load(std::memory_order_acquire);
+                std::unique_lock<std::mutex> lock(blob_mu, std::defer_lock);
+                if (!fast) lock.lock();
+                if (fast) {
+                    blob = e->empty_blob;
+                } else if (e->custom_node) {
                     // one compile per distinct status (the fields the template may read)
                     std::string key = std::to_string(x.phase);
                     for (int k = 0; k < 3; k++) key += '\x01' + js[k];
@@ -1331,12 +1338,15 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                             if (!brc) e->node_tpl_blobs.emplace(std::move(key), blob);
                         }
                     }
-                } else if (empty && e->has_empty_blob) {
+                } else if (empty && e->has_empty_blob.load(std::memory_order_acquire)) {
                     blob = e->empty_blob;
                 } else {
                     NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
                     blob = intern_blob(e, nb, &brc);
-                    if (empty && !brc) e->empty_blob = blob, e->has_empty_blob = true;
+                    if (empty && !brc) {
+                        e->empty_blob = blob;
+                        e->has_empty_blob.store(true, std::memory_order_release);
+                    }
                 }
                 if (brc) st = brc;
                 else {
