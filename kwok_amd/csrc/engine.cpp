@@ -1623,11 +1623,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         // record range.
         const int P = e->n_part;
         constexpr uint32_t NONE = 0xFFFFFFFFu;
-        if (e->ing_bkt.size() < 2 * n) e->ing_bkt.resize(2 * n);
-        if (e->ing_res.size() < n) e->ing_res.resize(n);
+        if (e->ing_bkt.size() < n) e->ing_bkt.resize(n);
+        if (e->ing_res.size() < 2 * n) e->ing_res.resize(2 * n);
         e->ing_order.resize((size_t)P);
         uint32_t* bkt = e->ing_bkt.data();
-        uint32_t* plist = bkt + n;          // record indices grouped by partition
+        uint64_t* plist = e->ing_res.data() + n;  // (bucket << 32 | record) grouped by partition
         uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
         auto owner = [&](uint32_t b) { return b == NONE ? 0 : (int)((uint64_t)b * (uint64_t)P / e->nb); };
         std::vector<size_t> cnt((size_t)P * P + 1, 0);  // [chunk][partition], then scatter positions
@@ -1665,7 +1665,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
             size_t k[64];
             std::copy(&cnt[(size_t)c * P], &cnt[(size_t)c * P] + P, k);
-            for (size_t i = lo; i < hi; i++) plist[k[owner(bkt[i])]++] = (uint32_t)i;
+            for (size_t i = lo; i < hi; i++) plist[k[owner(bkt[i])]++] = (uint64_t)bkt[i] << 32 | (uint32_t)i;
         });
         tp1 = std::chrono::steady_clock::now();
         run_parts(e, true, [&](int p) {
@@ -1674,18 +1674,18 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const uint32_t first = (uint32_t)(((uint64_t)p * e->nb + P - 1) / P);
             const uint32_t last = (uint32_t)(((uint64_t)(p + 1) * e->nb + P - 1) / P);
             const uint32_t nbk = last - first;
-            const uint32_t* mine = plist + pstart[(size_t)p];
+            const uint64_t* mine = plist + pstart[(size_t)p];  // read in order: no random bkt[] reads
             const uint32_t n_mine = (uint32_t)(pstart[(size_t)p + 1] - pstart[(size_t)p]);
             std::vector<uint32_t> off(nbk + 2, 0);  // [0]: records that change nothing (partition 0 only)
             for (uint32_t k = 0; k < n_mine; k++) {
-                const uint32_t b = bkt[mine[k]];
+                const uint32_t b = (uint32_t)(mine[k] >> 32);
                 off[b == NONE ? 1 : b - first + 2]++;
             }
             for (uint32_t k = 1; k < nbk + 2; k++) off[k] += off[k - 1];
             auto& order = e->ing_order[(size_t)p];
             if (order.size() < n_mine) order.resize(n_mine + n_mine / 8);
             for (uint32_t k = 0; k < n_mine; k++) {
-                const uint32_t i = mine[k], b = bkt[i];
+                const uint32_t i = (uint32_t)mine[k], b = (uint32_t)(mine[k] >> 32);
                 order[off[b == NONE ? 0 : b - first + 1]++] = i;
             }
             // records come in bucket order, i.e. from all over the batch: prefetch
