@@ -250,6 +250,7 @@ std::vector<Node> parse_template(const std::string& text) {
             f.block->has_else = true;
             f.list = &f.block->else_body;
             if (toks.size() > 1) {  // else if / else with: a nested block that ends with this one
+                if (st.size() > 64) fail("template blocks nested deeper than the covered subset");
                 if (toks[1].k != T_IDENT || (toks[1].v != "if" && toks[1].v != "with")) fail("unsupported else clause");
                 Node b{toks[1].v == "if" ? Node::IF : Node::WITH, "", make_pipe({toks.begin() + 2, toks.end()}), {}, {}, false};
                 f.list->push_back(std::move(b));
@@ -257,6 +258,7 @@ std::vector<Node> parse_template(const std::string& text) {
                 st.push_back({&nb->body, nb, true});
             }
         } else if (head.k == T_IDENT && (head.v == "if" || head.v == "with" || head.v == "range")) {
+            if (st.size() > 64) fail("template blocks nested deeper than the covered subset");
             Node b{head.v == "if" ? Node::IF : head.v == "with" ? Node::WITH : Node::RANGE, "",
                    make_pipe({toks.begin() + 1, toks.end()}), {}, {}, false};
             st.back().list->push_back(std::move(b));
@@ -685,7 +687,7 @@ std::string sq_unescape(const std::string& s, size_t& i) {  // s[i] == '\''
 }
 
 // flow collection / scalar inside flow context, from s[i]
-VPtr flow(const std::string& s, size_t& i);
+VPtr flow(const std::string& s, size_t& i, int depth = 0);
 void skip_ws(const std::string& s, size_t& i) {
     while (i < s.size() && (s[i] == ' ' || s[i] == '\t')) i++;
 }
@@ -700,7 +702,8 @@ VPtr flow_scalar(const std::string& s, size_t& i, bool key) {
     i = j;
     return plain_scalar(t);
 }
-VPtr flow(const std::string& s, size_t& i) {
+VPtr flow(const std::string& s, size_t& i, int depth) {
+    if (depth > 64) fail("flow collection nested deeper than the covered subset");
     skip_ws(s, i);
     if (i >= s.size()) fail("truncated flow collection");
     if (s[i] == '[') {
@@ -712,7 +715,7 @@ VPtr flow(const std::string& s, size_t& i) {
             return make_list(items);
         }
         while (true) {
-            items.push_back(flow(s, i));
+            items.push_back(flow(s, i, depth + 1));
             skip_ws(s, i);
             if (i < s.size() && s[i] == ',') {
                 i++;
@@ -739,7 +742,7 @@ VPtr flow(const std::string& s, size_t& i) {
             skip_ws(s, i);
             if (i >= s.size() || s[i] != ':') fail("bad flow mapping");
             i++;
-            kv.push_back({k->s, flow(s, i)});
+            kv.push_back({k->s, flow(s, i, depth + 1)});
             skip_ws(s, i);
             if (i < s.size() && s[i] == ',') {
                 i++;
@@ -794,12 +797,20 @@ size_t key_colon(const std::string& s) {
     return std::string::npos;
 }
 
+constexpr int MAX_DEPTH = 64;  // nesting of YAML / JSON collections and template blocks
+
 struct YamlParser {
     std::vector<Line> lines;
     size_t at = 0;
+    int depth = 0;
 
     VPtr node(int min_indent) {
         if (at >= lines.size() || lines[at].indent < min_indent) return make_null();
+        if (++depth > MAX_DEPTH) fail("YAML nested deeper than the covered subset");
+        struct Up {
+            int& d;
+            ~Up() { d--; }
+        } up{depth};
         const Line& l = lines[at];
         if (l.s == "-" || l.s.compare(0, 2, "- ") == 0) return seq(l.indent);
         if (key_colon(l.s) != std::string::npos) return mapping(l.indent);
@@ -904,12 +915,18 @@ void json_emit(std::string& o, const VPtr& v) {
 struct JsonParser {
     const std::string& s;
     size_t i = 0;
+    int depth = 0;
     void ws() {
         while (i < s.size() && isspace((unsigned char)s[i])) i++;
     }
     VPtr value() {
         ws();
         if (i >= s.size()) fail("truncated JSON");
+        if (++depth > 64) fail("JSON nested deeper than the covered subset");
+        struct Up {
+            int& d;
+            ~Up() { d--; }
+        } up{depth};
         const char c = s[i];
         if (c == '{') {
             std::vector<std::pair<std::string, VPtr>> kv;
