@@ -154,8 +154,8 @@ typedef struct kwok_config {
     int32_t enable_cni;            /* Config.EnableCNI: pod IPs come from the caller's CNI plugin
                                       (kwok_cni_pending / kwok_cni_assign); the ipPool is unused */
     int32_t custom_templates;      /* bit mask: 0 = templates.Default*; KWOK_TPL_POD: pod_status_template
-                                      below, KWOK_TPL_NODE_INIT: node_init_template below (the
-                                      heartbeat template is always the default) */
+                                      below, KWOK_TPL_NODE_INIT: node_init_template, KWOK_TPL_HEARTBEAT:
+                                      node_heartbeat_template */
     uint32_t buckets;              /* power of two; node -> bucket = fnv1a32(name) & (buckets-1) */
     uint32_t node_slots_per_bucket;
     uint32_t pod_slots_per_bucket; /* initial pod capacity of a bucket (multiple of 8); grows up to
@@ -179,8 +179,11 @@ typedef struct kwok_config {
     const char* node_init_template;  /* KWOK_TPL_NODE_INIT: Config.NodeInitializationTemplate
                                         (controller.go:75), compiled per distinct node status into
                                         the node's init blob (see kwok_node_template_patch) */
+    const char* node_heartbeat_template; /* KWOK_TPL_HEARTBEAT: Config.NodeHeartbeatTemplate
+                                        (controller.go:77): must render the same conditions list for
+                                        every node, <= 1280 bytes (see kwok_heartbeat_template_patch) */
 } kwok_config;
-enum { KWOK_TPL_POD = 1, KWOK_TPL_NODE_INIT = 2 };
+enum { KWOK_TPL_POD = 1, KWOK_TPL_NODE_INIT = 2, KWOK_TPL_HEARTBEAT = 4 };
 
 /* fleet counters (kwok_tick_result.counters, summed over ranks) */
 enum {
@@ -380,9 +383,13 @@ int kwok_pod_template_patch(const char* tpl, const kwok_pod_spec* spec, const ch
 /* Host only: the init patch (LockNode / configureNode) of the node in `ev` under
  * a custom node initialization template, at heartbeat time now_unix, as the
  * engine compiles and the kernels assemble it. */
-int kwok_node_template_patch(const char* tpl, const kwok_node_event* ev, const char* arena, size_t arena_len,
-                             int64_t start_unix, const char* node_ip, int64_t now_unix, char* out, size_t cap,
-                             size_t* out_len);
+int kwok_node_template_patch(const char* tpl, const char* heartbeat_tpl, const kwok_node_event* ev, const char* arena,
+                             size_t arena_len, int64_t start_unix, const char* node_ip, int64_t now_unix, char* out,
+                             size_t cap, size_t* out_len);
+/* Host only: the heartbeat patch (configureHeartbeatNode) under a custom
+ * heartbeat template (NULL: the default) at now_unix. */
+int kwok_heartbeat_template_patch(const char* tpl, int64_t start_unix, const char* node_ip, int64_t now_unix, char* out,
+                                  size_t cap, size_t* out_len);
 
 /* Bucket of a node name (fnv1a32 & (buckets-1)) and its owning rank. */
 uint32_t kwok_bucket_of(const char* name, size_t len, uint32_t buckets);

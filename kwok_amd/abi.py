@@ -87,7 +87,8 @@ class Config(C.Structure):
                 ("rank", C.c_int32), ("world_size", C.c_int32), ("device", C.c_int32),
                 ("comm_id", C.c_void_p), ("allgather", ALLGATHER_FN), ("allgather_user", C.c_void_p),
                 ("pod_handle_stride", C.c_uint32), ("reserved0", C.c_uint32),
-                ("pod_status_template", C.c_char_p), ("node_init_template", C.c_char_p)]
+                ("pod_status_template", C.c_char_p), ("node_init_template", C.c_char_p),
+                ("node_heartbeat_template", C.c_char_p)]
 
 
 class TickResult(C.Structure):

@@ -54,6 +54,10 @@ constexpr int HB_PREFIX = 24;    // {"status":{"conditions":
 constexpr int CONDS_LEN = HB_LEN - HB_PREFIX - 2;  // the conditions list "[...]"
 constexpr int TS_LEN = 20;       // RFC3339 UTC "YYYY-MM-DDTHH:MM:SSZ"
 constexpr int HB_NSLOTS = 10;    // 5 x (lastHeartbeatTime, lastTransitionTime)
+// a custom heartbeat template (KWOK_TPL_HEARTBEAT) may render up to this many bytes;
+// the geometry of the default one above is the streamer's fast path
+constexpr int HB_MAX_STRIDE = 1280;
+constexpr int HB_MAX_UNITS = HB_MAX_STRIDE / 16;
 
 // per-chain-block record of the classify phase (16 x u32, one 64-byte line).
 // The first AG_NSCAN fields are exclusive-scanned over blocks into output

@@ -188,6 +188,10 @@ struct kwok_engine {
 
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
+    uint32_t hb_len = HB_LEN, hb_stride = HB_STRIDE;  // heartbeat patch bytes / arena stride (16-aligned)
+    HeartbeatTemplate hb_tpl;     // the heartbeat template (default or compiled from Config.NodeHeartbeatTemplate)
+    bool custom_hb = false;
+    std::string hb_tpl_text;
     bool custom_pod = false;      // Config.PodStatusTemplate in use (compiled per spec)
     bool custom_node = false;     // Config.NodeInitializationTemplate in use (compiled per node status)
     std::string pod_tpl, node_tpl, start_s;  // their texts; StartTime() (RFC3339 of start_time_unix)
@@ -516,7 +520,7 @@ int poisoned(kwok_engine* e) {
 
 // the output arena must hold the worst case of one tick (grown per slot at submit)
 int size_arena(kwok_engine* e) {
-    e->arena_need = (uint64_t)e->NL * HB_STRIDE + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
+    e->arena_need = (uint64_t)e->NL * e->hb_stride + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
                     (uint64_t)e->PL * e->max_pod_len + 256;
     return KWOK_OK;
 }
@@ -598,7 +602,7 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     auto it = e->blob_ids.find(key);
     if (it != e->blob_ids.end()) return it->second;
     // k_emit keeps patch positions in 16 bits
-    if (b.pre.size() + CONDS_LEN + b.post.size() > 0xFFF0 || e->blob_h.size() > 0xFFFFFFFFull - 0x20000) {
+    if (b.pre.size() + e->hb_tpl.conds_len + b.post.size() > 0xFFF0 || e->blob_h.size() > 0xFFFFFFFFull - 0x20000) {
         *rc = KWOK_EDOMAIN;
         return 0;
     }
@@ -607,7 +611,7 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     e->blob_h += b.post;
     uint64_t word = off | ((uint64_t)b.pre.size() << 32) | ((uint64_t)b.post.size() << 48);
     e->blob_ids.emplace(key, word);
-    uint32_t ilen = (uint32_t)b.pre.size() + CONDS_LEN + (uint32_t)b.post.size();
+    uint32_t ilen = (uint32_t)b.pre.size() + e->hb_tpl.conds_len + (uint32_t)b.post.size();
     e->max_init_len = std::max(e->max_init_len, ilen);
     // device copy: SRC_PAD_FRONT zero bytes, the blobs, SRC_PAD_BACK zero bytes (k_emit reads around them)
     const size_t padded = ((SRC_PAD_FRONT + e->blob_h.size() + 3) & ~(size_t)3) + SRC_PAD_BACK;
@@ -818,9 +822,30 @@ thread_local std::string g_tpl_err;
 }
 const char* kwok_template_last_error(void) { return g_tpl_err.c_str(); }
 
-int kwok_node_template_patch(const char* tpl, const kwok_node_event* ev, const char* arena, size_t arena_len,
-                             int64_t start_unix, const char* node_ip, int64_t now_unix, char* out, size_t cap,
-                             size_t* out_len) {
+int kwok_heartbeat_template_patch(const char* tpl, int64_t start_unix, const char* node_ip, int64_t now_unix, char* out,
+                                  size_t cap, size_t* out_len) {
+    if (!node_ip || !out_len || (cap && !out)) return KWOK_EINVAL;
+    g_tpl_err.clear();
+    auto rfc3339 = [](int64_t u) {
+        time_t t = (time_t)u;
+        struct tm tm;
+        gmtime_r(&t, &tm);
+        char b[32];
+        strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);
+        return std::string(b);
+    };
+    HeartbeatTemplate hb = build_heartbeat_template();
+    if (tpl && !compile_heartbeat_template(tpl, rfc3339(start_unix), node_ip, hb, g_tpl_err)) return KWOK_EDOMAIN;
+    const std::string o = heartbeat_patch(hb, rfc3339(now_unix), rfc3339(start_unix));
+    *out_len = o.size();
+    if (o.size() > cap) return KWOK_EINVAL;
+    memcpy(out, o.data(), o.size());
+    return KWOK_OK;
+}
+
+int kwok_node_template_patch(const char* tpl, const char* heartbeat_tpl, const kwok_node_event* ev, const char* arena,
+                             size_t arena_len, int64_t start_unix, const char* node_ip, int64_t now_unix, char* out,
+                             size_t cap, size_t* out_len) {
     if (!tpl || !ev || !node_ip || !out_len || (cap && !out)) return KWOK_EINVAL;
     g_tpl_err.clear();
     auto get = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len ? std::string(arena + s.off, s.len) : std::string(); };
@@ -834,11 +859,14 @@ int kwok_node_template_patch(const char* tpl, const kwok_node_event* ev, const c
         strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);
         return std::string(b);
     };
+    HeartbeatTemplate hb = build_heartbeat_template();
+    if (heartbeat_tpl && !compile_heartbeat_template(heartbeat_tpl, rfc3339(start_unix), node_ip, hb, g_tpl_err))
+        return KWOK_EDOMAIN;
     NodeBlob nb;
     if (!compile_node_template(tpl, get(ev->addresses), get(ev->allocatable), get(ev->capacity), info, ev->phase, node_ip,
-                               rfc3339(start_unix), nb, g_tpl_err))
+                               rfc3339(start_unix), hb, nb, g_tpl_err))
         return KWOK_EDOMAIN;
-    const std::string o = nb.pre + heartbeat_conditions(rfc3339(now_unix), rfc3339(start_unix)) + nb.post;
+    const std::string o = nb.pre + heartbeat_conditions(hb, rfc3339(now_unix), rfc3339(start_unix)) + nb.post;
     *out_len = o.size();
     if (o.size() > cap) return KWOK_EINVAL;
     memcpy(out, o.data(), o.size());
@@ -967,9 +995,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!out) return KWOK_EINVAL;
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
-    if ((cfg->custom_templates & ~(KWOK_TPL_POD | KWOK_TPL_NODE_INIT)) ||
+    if ((cfg->custom_templates & ~(KWOK_TPL_POD | KWOK_TPL_NODE_INIT | KWOK_TPL_HEARTBEAT)) ||
         ((cfg->custom_templates & KWOK_TPL_POD) && !cfg->pod_status_template) ||
-        ((cfg->custom_templates & KWOK_TPL_NODE_INIT) && !cfg->node_init_template))
+        ((cfg->custom_templates & KWOK_TPL_NODE_INIT) && !cfg->node_init_template) ||
+        ((cfg->custom_templates & KWOK_TPL_HEARTBEAT) && !cfg->node_heartbeat_template))
         return KWOK_EINVAL;
     const uint32_t hs = cfg->pod_handle_stride ? cfg->pod_handle_stride : cfg->pod_slots_per_bucket;
     if (!cfg->buckets || (cfg->buckets & (cfg->buckets - 1)) || cfg->node_slots_per_bucket % 4 ||
@@ -1024,13 +1053,25 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%SZ", &tm);  // time.RFC3339 in UTC
         e->start_s = b;
     }
+    // the heartbeat template first: its conditions list is part of every node init patch
+    e->hb_tpl = build_heartbeat_template();
+    if (cfg->custom_templates & KWOK_TPL_HEARTBEAT) {
+        e->custom_hb = true;
+        e->hb_tpl_text = cfg->node_heartbeat_template;
+        std::string why;
+        if (!compile_heartbeat_template(e->hb_tpl_text, e->start_s, e->node_ip_s, e->hb_tpl, why))
+            return bail(e->fail(KWOK_EDOMAIN, "node heartbeat template: %s", why.c_str()));
+    }
+    e->hb_len = (uint32_t)e->hb_tpl.bytes.size();
+    e->hb_stride = (e->hb_len + 15u) & ~15u;
     if (cfg->custom_templates & KWOK_TPL_NODE_INIT) {
         // compiled per node status at ingest; a trial node rejects a template outside the subset here
         e->custom_node = true;
         e->node_tpl = cfg->node_init_template;
         NodeBlob b;
         std::string why, info[KWOK_NI_COUNT];
-        if (!compile_node_template(e->node_tpl, "", "", "", info, KWOK_PHASE_NONE, e->node_ip_s, e->start_s, b, why))
+        if (!compile_node_template(e->node_tpl, "", "", "", info, KWOK_PHASE_NONE, e->node_ip_s, e->start_s, e->hb_tpl, b,
+                                   why))
             return bail(e->fail(KWOK_EDOMAIN, "node initialization template: %s", why.c_str()));
     }
     if (cfg->custom_templates & KWOK_TPL_POD) {
@@ -1085,6 +1126,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.cp = e->Cp;
     S.node_handle_base = (int32_t)(e->b_lo * e->Cn);
     S.pod_handle_base = 0;  // pod handles: pod_handle_of (stride)
+    S.hb_units = e->hb_stride / 16;
+    S.conds_off = e->hb_tpl.conds_off;
+    S.conds_len = e->hb_tpl.conds_len;
     S.b_lo = e->b_lo;
     S.pod_stride = e->Hs;
     S.pool = e->pool;
@@ -1118,26 +1162,25 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
         (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
-        (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_STRIDE)) ||
-        (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_STRIDE)) ||
+        (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_MAX_STRIDE)) ||
+        (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
         (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))) ||
         (rc = alloc_slot(e, 0)))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
     {
-        HeartbeatTemplate hb = build_heartbeat_template();
-        if (hb.bytes.size() != (size_t)HB_LEN) return bail(e->fail(KWOK_EINVAL, "heartbeat template %zu", hb.bytes.size()));
-        std::vector<uint8_t> bytes(HB_STRIDE, 0), kind(HB_STRIDE, 0xFF);
-        memcpy(bytes.data(), hb.bytes.data(), HB_LEN);
+        const HeartbeatTemplate& hb = e->hb_tpl;
+        std::vector<uint8_t> bytes(HB_MAX_STRIDE, 0), kind(HB_MAX_STRIDE, 0xFF);
+        memcpy(bytes.data(), hb.bytes.data(), hb.bytes.size());
         for (uint16_t o : hb.now_slots)
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)i;
         for (uint16_t o : hb.start_slots)
             for (int i = 0; i < TS_LEN; i++) kind[o + i] = (uint8_t)(TS_LEN + i);
         // on the engine's stream, after dalloc's zero fills (a null-stream copy is
         // not ordered with a non-blocking stream: the fill could land after it)
-        hipError_t r = hipMemcpyAsync((void*)S.hb_static, bytes.data(), HB_STRIDE, hipMemcpyHostToDevice, e->st);
-        if (r == hipSuccess) r = hipMemcpyAsync((void*)S.hb_kind, kind.data(), HB_STRIDE, hipMemcpyHostToDevice, e->st);
+        hipError_t r = hipMemcpyAsync((void*)S.hb_static, bytes.data(), HB_MAX_STRIDE, hipMemcpyHostToDevice, e->st);
+        if (r == hipSuccess) r = hipMemcpyAsync((void*)S.hb_kind, kind.data(), HB_MAX_STRIDE, hipMemcpyHostToDevice, e->st);
         if (r == hipSuccess) r = hipStreamSynchronize(e->st);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "template upload: %s", hipGetErrorString(r)));
     }
@@ -1331,7 +1374,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                         NodeBlob nb;
                         std::string why;
                         if (!compile_node_template(e->node_tpl, js[0], js[1], js[2], info, x.phase, e->node_ip_s,
-                                                   e->start_s, nb, why)) {
+                                                   e->start_s, e->hb_tpl, nb, why)) {
                             brc = KWOK_EDOMAIN;
                         } else {
                             blob = intern_blob(e, nb, &brc);
@@ -1849,7 +1892,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     }
     // a long heartbeat stream is shared with the chain blocks once they are done
     // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
-    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)HB_STRIDE >= (32ull << 20) ? 921u : 1024u);
+    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)e->hb_stride >= (32ull << 20) ? 921u : 1024u);
     int rc = bind_slot(e, k);
     if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
@@ -1935,7 +1978,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
 
 // single rank: the kernel publishes the tick's field totals (TickHdr::tot); the
 // counts, output layout and counters follow from them
-void derive_header(TickHdr& H, uint64_t arena_cap) {
+void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride) {
     const uint64_t* t = H.tot;
     H.n_hb = (uint32_t)t[AG_HB];
     H.n_init = (uint32_t)t[AG_INIT];
@@ -1949,7 +1992,7 @@ void derive_header(TickHdr& H, uint64_t arena_cap) {
     H.init_bytes = t[AG_INIT_BYTES];
     H.pp_bytes = t[AG_PP_BYTES];
     H.hb_base = 0;
-    H.init_base = (uint64_t)H.n_hb * HB_STRIDE;
+    H.init_base = (uint64_t)H.n_hb * hb_stride;
     H.pod_base = H.init_base + H.init_bytes;
     H.arena_bytes = H.pod_base + H.pp_bytes;
     H.overflow = H.arena_bytes > arena_cap;
@@ -2040,7 +2083,7 @@ int retire(kwok_engine* e) {
         if (rc) return failed(rc);
     }
     const auto t2 = clk::now();
-    if (e->W == 1) derive_header(*T.hdr_h, T.arena_cap);
+    if (e->W == 1) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride);
     const TickHdr& H = *T.hdr_h;
     if (!H.err && (H.n_pp || H.n_init) && !T.emit_queued) {
         // jobs nobody expected (no events since the previous tick): their bytes now
@@ -2114,8 +2157,8 @@ int retire(kwok_engine* e) {
     kwok_tick_result& r = T.res;
     memset(&r, 0, sizeof(r));
     r.n_heartbeat = H.n_hb;
-    r.heartbeat_len = HB_LEN;
-    r.heartbeat_stride = HB_STRIDE;
+    r.heartbeat_len = e->hb_len;
+    r.heartbeat_stride = e->hb_stride;
     r.n_node_init = H.n_init;
     r.n_pod_patch = H.n_pp;
     r.n_delete = H.n_del;
@@ -2279,7 +2322,7 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     if (o->arena) {
         if (o->flags & KWOK_READ_HEARTBEAT_ONCE) {
             // one heartbeat body, then the node-init / pod patch region (init_base..)
-            const uint64_t hb = H.n_hb ? (uint64_t)HB_STRIDE : 0, patches = H.arena_bytes - H.init_base;
+            const uint64_t hb = H.n_hb ? (uint64_t)e->hb_stride : 0, patches = H.arena_bytes - H.init_base;
             if (o->arena_cap < hb + patches)
                 return e->fail(KWOK_EINVAL, "arena_cap < %llu", (unsigned long long)(hb + patches));
             HIPCHK(e, cp(o->arena, S.arena, hb));

@@ -89,6 +89,9 @@ struct DevState {
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
+    // heartbeat geometry (default: HB_STRIDE / 16, HB_PREFIX, CONDS_LEN; a custom template's otherwise)
+    uint32_t hb_units;         // 16-byte units per heartbeat slot (arena stride = 16 x hb_units)
+    uint32_t conds_off, conds_len;  // the conditions list inside the heartbeat (spliced into node inits)
 };
 
 __device__ __host__ inline int32_t pod_handle_of(const DevState& S, uint32_t slot) {

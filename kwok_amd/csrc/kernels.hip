@@ -252,9 +252,9 @@ __device__ __forceinline__ PodCls classify_pod(uint16_t st, uint8_t ntf, uint32_
 }
 
 // framed blob (templates.cpp build_node_blob): pre | heartbeat conditions | post
-__device__ __forceinline__ uint32_t init_patch_len(uint64_t blob) {
+__device__ __forceinline__ uint32_t init_patch_len(const DevState& S, uint64_t blob) {
     const uint32_t pre = (uint32_t)(blob >> 32) & 0xFFFF, post = (uint32_t)(blob >> 48);
-    return pre + (uint32_t)CONDS_LEN + post;
+    return pre + S.conds_len + post;
 }
 
 // ---------------------------------------------------------------------------
@@ -928,7 +928,7 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
         blob[k] = 0;
         if (c[k].init) {
             blob[k] = S.node_blob[first + k];
-            ilen[k] = init_patch_len(blob[k]);
+            ilen[k] = init_patch_len(S, blob[k]);
             v[0]++;
             v[1] += (ilen[k] + 15u) & ~15u;
         }
@@ -1055,9 +1055,36 @@ constexpr int HB_CHUNKS = HB_STRIDE / 16;  // 67
 // is 5 plain 16-byte stores per group (no LDS read per store).
 constexpr uint32_t HB_GROUP_SLOTS = 4, HB_GROUP_UNITS = HB_GROUP_SLOTS * HB_CHUNKS;  // 268
 static_assert(HB_GROUP_UNITS > 256 && HB_GROUP_UNITS <= 320, "5 stores of a wave per group");
+static_assert(HB_GROUP_SLOTS * HB_MAX_UNITS <= 320, "custom heartbeats: still 5 stores of a wave per group");
+// A custom heartbeat (any 16-byte unit count up to HB_MAX_UNITS): the same
+// group walk with the unit count a launch argument, every store predicated.
+__device__ __noinline__ void hb_fill_groups_any(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint64_t g0,
+                                                uint64_t g1) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t l = lane_id(), w = wave_id(), U = S.hb_units, GU = HB_GROUP_SLOTS * U;
+    u32x4 r[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = tmpl[(64u * k + l) % U];
+        r[k] = u32x4{v.x, v.y, v.z, v.w};
+    }
+    const uint64_t units = n_hb * U;
+    u32x4* dst = reinterpret_cast<u32x4*>(S.arena);
+    for (uint64_t g = g0 + w; g < g1; g += BLOCK / 64) {
+        const uint64_t u0 = g * GU + l;
+        u32x4* p = dst + u0;
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (64u * k + l < GU && u0 + 64u * k < units) p[64 * k] = r[k];
+    }
+}
 // groups [g0, g1) of the heartbeat region (units past n_hb slots are not written)
 __device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint64_t g0,
                                                uint64_t g1) {
+    if (S.hb_units != (uint32_t)HB_CHUNKS) {  // wave-uniform: a custom heartbeat template
+        hb_fill_groups_any(S, tmpl, n_hb, g0, g1);
+        return;
+    }
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t l = lane_id(), w = wave_id();
     u32x4 r[5];
@@ -1097,7 +1124,7 @@ __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tm
 // per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
 __device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tmpl, uint64_t now_unix, uint64_t start_unix) {
     const Ts now = format_ts(now_unix), st = format_ts(start_unix);
-    for (int i = threadIdx.x; i < HB_STRIDE; i += BLOCK) {
+    for (int i = threadIdx.x; i < (int)(16u * S.hb_units); i += BLOCK) {
         const uint8_t k = S.hb_kind[i];
         uint32_t b;
         if (k == 0xFF) b = S.hb_static[i];
@@ -1116,7 +1143,7 @@ __device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tm
 // publishes the Get plan / cursor (skip_alloc) and its stamps (skip_pool).
 // ---------------------------------------------------------------------------
 // word i of the tick header (TickHdr as 61 x u64), computed by thread i
-__device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint32_t n_hb, uint32_t nu,
+__device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint32_t n_hb, uint32_t hb_stride, uint32_t nu,
                                                 uint64_t pool_index, uint64_t arena_cap, bool single, const uint64_t* clk) {
     constexpr int W_LC = offsetof(TickHdr, local_counters) / 8, W_C = offsetof(TickHdr, counters) / 8;
     constexpr int W_CLK = offsetof(TickHdr, clk) / 8;
@@ -1124,7 +1151,7 @@ __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint
                       offsetof(TickHdr, alloc_total) == 352 && offsetof(TickHdr, clk) == 416 &&
                       offsetof(TickHdr, err) == 480,
                   "TickHdr layout");
-    const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+    const uint64_t patch_base = (uint64_t)n_hb * hb_stride;
     const uint64_t arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
     auto pair = [](uint64_t lo, uint64_t hi) { return (uint64_t)(uint32_t)lo | (uint64_t)(uint32_t)hi << 32; };
     if (i >= W_LC && i < W_C + 16) {
@@ -1179,7 +1206,7 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
     const bool skip_alloc = single && tot[AG_ALLOC] != 0, skip_pool = single && (tot[AG_ALLOC] | tot[AG_REL]) != 0;
     const int i = threadIdx.x;
     if (i < NW) {
-        const uint64_t w = header_word(i, tot, n_hb, nu, pool_index, S.arena_cap, single, clk);
+        const uint64_t w = header_word(i, tot, n_hb, 16u * S.hb_units, nu, pool_index, S.arena_cap, single, clk);
         const bool pool_clk = i == C0 + CLK_BACK || i == C0 + CLK_POOL;
         // the pool leader may already have written its fields (it runs concurrently)
         if (!(skip_pool && (pool_clk || (i >= A0 && i < A1)))) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
@@ -1197,7 +1224,8 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
             X->n_use = nu;
             X->n_rel = nr;
             constexpr int LC = offsetof(TickHdr, local_counters) / 8;
-            for (int k = 0; k < 16; k++) X->counters[k] = header_word(LC + k, tot, n_hb, nu, pool_index, S.arena_cap, single, clk);
+            for (int k = 0; k < 16; k++)
+                X->counters[k] = header_word(LC + k, tot, n_hb, 16u * S.hb_units, nu, pool_index, S.arena_cap, single, clk);
         }
     }
     if (!single && nu + nr <= (uint32_t)XINLINE) {  // exchange lists inline when they fit
@@ -1337,7 +1365,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
         __syncthreads();
     }
     if (t == 0) {
-        const uint64_t patch_base = (uint64_t)n_hb * HB_STRIDE;
+        const uint64_t patch_base = (uint64_t)n_hb * (16u * S.hb_units);
         l.L->init_base = patch_base;
         l.L->pod_base = patch_base + l.sums->tot[AG_INIT_BYTES];
         l.L->alloc_base = alloc_base;
@@ -1386,7 +1414,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     __shared__ uint32_t recs[MAX_CHAIN * REC_PITCH];  // reduce_records
-    __shared__ uint4 hb_tmpl4[HB_CHUNKS];
+    __shared__ uint4 hb_tmpl4[HB_MAX_UNITS];
     __shared__ uint32_t nflags32[NODE_LDS / 4];
     __shared__ uint32_t gpre[MAX_BPB + 1];
     __shared__ uint32_t sh_mask[4];  // pod chunk mask lo / hi, node chunk mask, most groups in a bucket
@@ -1485,7 +1513,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 f[AG_READY] += c.ready;
                 if (c.init) {
                     f[AG_INIT]++;
-                    f[AG_INIT_BYTES] += (init_patch_len(S.node_blob[nbase + i + k]) + 15u) & ~15u;
+                    f[AG_INIT_BYTES] += (init_patch_len(S, S.node_blob[nbase + i + k]) + 15u) & ~15u;
                 }
                 dirty |= c.init || (s & NS_EVENT_LOCK);
                 tick |= (uint32_t)node_tick_flags(s) << (8 * k);
@@ -1846,7 +1874,7 @@ constexpr uint32_t TS_STRIDE = 36;   // per job: its 20-byte timestamp, then 16 
 constexpr uint32_t TS_FIRST = 16;    // 16 zero bytes before job 0's timestamp
 constexpr uint32_t TS_ZERO = TS_FIRST + 64 * TS_STRIDE;  // 20+ zero bytes (a unit with no slot)
 constexpr uint32_t TS_AREA = TS_ZERO + 32;
-constexpr uint32_t HB_LDS = 1104;    // the heartbeat template: CONDS at HB_PREFIX, read up to 32 bytes around it
+constexpr uint32_t HB_LDS = HB_MAX_STRIDE + 32;  // the heartbeat template: CONDS at conds_off, read up to 32 bytes around it
 static_assert(HB_LDS >= HB_STRIDE && HB_LDS >= ((HB_PREFIX + CONDS_LEN + 15) & ~15) + 32, "heartbeat template in LDS");
 struct EmitWave {
     uint4 rec[64];   // per job: arena offset / 16, region starts 1|2 and 3|4 (u16; 0xFFFF: none), template offset
@@ -1915,7 +1943,7 @@ __device__ __forceinline__ void stage_emit(const DevState& S, EmitLds* L, bool p
     }
     uint32_t* z = reinterpret_cast<uint32_t*>(L->w);
     for (uint32_t i = t; i < sizeof(L->w) / 4; i += BLOCK) z[i] = 0u;
-    for (uint32_t i = HB_STRIDE + t; i < HB_LDS; i += BLOCK) L->hb[i] = 0;
+    for (uint32_t i = 16u * S.hb_units + t; i < HB_LDS; i += BLOCK) L->hb[i] = 0;
     if (t == 0) {
         L->spec_ok = sp ? 1u : 0u;
         L->blob_ok = bl ? 1u : 0u;
@@ -1961,7 +1989,7 @@ __device__ __forceinline__ uint32_t emit_phase1(const DevState& S, EmitWave* W, 
             len = S.init_len[q];
             toff = (uint32_t)b;
             const uint32_t pre = (uint32_t)(b >> 32) & 0xFFFFu;
-            e12 = pre | (pre + (uint32_t)CONDS_LEN) << 16;
+            e12 = pre | (pre + S.conds_len) << 16;
         }
         o16 = (uint32_t)(off >> 4);
         nu = (len + 15u) >> 4;
@@ -1992,7 +2020,7 @@ __device__ __forceinline__ uint4 emit_unit(const DevState& S, const EmitLds* L, 
     // region deltas (see above) and starts, selected by the region bits of x and y
     const uint32_t seg_k = E.o_seg + k * SEG_STRIDE;
     const uint32_t d0 = E.o_tmpl + toff;
-    const uint32_t d1 = POD ? seg_k - e1 : (uint32_t)offsetof(EmitLds, hb) + HB_PREFIX - e1;
+    const uint32_t d1 = POD ? seg_k - e1 : (uint32_t)offsetof(EmitLds, hb) + S.conds_off - e1;
     const uint32_t d2 = POD ? d0 - (e2 - e1) : d0 + e1 - e2;
     const uint32_t d3 = seg_k + 28u - e3;
     const uint32_t d4 = d2 - (e4 - e3);

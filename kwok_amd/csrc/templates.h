@@ -15,11 +15,18 @@ namespace kwok {
 constexpr uint8_t KIND_LIT = 0xFF;  // literal byte; otherwise an index into a 20-byte timestamp
 
 struct HeartbeatTemplate {
-    std::string bytes;              // HB_LEN bytes, timestamp slots zero-filled
-    std::vector<uint16_t> now_slots;   // offsets of lastHeartbeatTime values (Now)
-    std::vector<uint16_t> start_slots; // offsets of lastTransitionTime values (StartTime)
+    std::string bytes;              // the patch (HB_LEN bytes by default), timestamp slots zero-filled
+    std::vector<uint16_t> now_slots;   // offsets of Now values (lastHeartbeatTime)
+    std::vector<uint16_t> start_slots; // offsets of StartTime values (lastTransitionTime)
+    uint32_t conds_off = 0, conds_len = 0;  // the conditions list (spliced into node init patches)
 };
 HeartbeatTemplate build_heartbeat_template();
+// A custom heartbeat template (Config.NodeHeartbeatTemplate, controller.go:77):
+// rendered with sentinel Now values (StartTime and NodeIP are fixed), it must
+// be {"status":{"conditions":[...]}} of at most HB_MAX_STRIDE bytes, the same
+// for every node (it may read no node field); every Now becomes a slot.
+bool compile_heartbeat_template(const std::string& tpl, const std::string& start_time, const std::string& node_ip,
+                                HeartbeatTemplate& out, std::string& err);
 
 struct SpecProgram {
     std::string a, b, c;           // segments (timestamp slots zero-filled)
@@ -60,9 +67,11 @@ bool compile_pod_template(const std::string& tpl, const std::vector<Container>& 
 bool compile_node_template(const std::string& tpl, const std::string& addresses_json,
                            const std::string& allocatable_json, const std::string& capacity_json,
                            const std::string info[10], int phase, const std::string& node_ip,
-                           const std::string& start_time, NodeBlob& out, std::string& err);
-// the heartbeat conditions list (CONDS) rendered at now / start (RFC3339)
-std::string heartbeat_conditions(const std::string& now, const std::string& start);
+                           const std::string& start_time, const HeartbeatTemplate& hb, NodeBlob& out,
+                           std::string& err);
+// the heartbeat patch / its conditions list (CONDS) at now / start (RFC3339)
+std::string heartbeat_patch(const HeartbeatTemplate& hb, const std::string& now, const std::string& start);
+std::string heartbeat_conditions(const HeartbeatTemplate& hb, const std::string& now, const std::string& start);
 
 // k_emit's timestamp-slot lookup of a spec (false: layout outside what it handles)
 bool build_ts_lookup(const SpecProgram& p, std::vector<uint16_t>& out);

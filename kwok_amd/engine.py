@@ -87,8 +87,9 @@ def declare(lib, pre):
             "template_last_error": (C.c_char_p, []),
             "pod_template_patch": (C.c_int, [C.c_char_p, P(abi.PodSpec), C.c_char_p, SZ, C.c_int64, C.c_char_p,
                                              C.c_int64, U32, U32, I32, VP, SZ, P(SZ)]),
-            "node_template_patch": (C.c_int, [C.c_char_p, P(abi.NodeEvent), C.c_char_p, SZ, C.c_int64, C.c_char_p,
-                                              C.c_int64, VP, SZ, P(SZ)]),
+            "node_template_patch": (C.c_int, [C.c_char_p, C.c_char_p, P(abi.NodeEvent), C.c_char_p, SZ, C.c_int64,
+                                              C.c_char_p, C.c_int64, VP, SZ, P(SZ)]),
+            "heartbeat_template_patch": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, VP, SZ, P(SZ)]),
             "codec_destroy": (None, [VP]),
             "codec_last_error": (C.c_char_p, []),
             "selector_matches": (C.c_int, [C.c_char_p, C.c_char_p, SZ, P(I32)]),
@@ -124,7 +125,7 @@ class TickOutput:
 def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200, buckets=4096,
                 node_slots_per_bucket=64, pod_slots_per_bucket=512, max_pod_specs=1024, rank=0, world_size=1,
                 device=0, comm_id=None, allgather=None, enable_cni=False, pod_handle_stride=0,
-                pod_status_template=None, node_init_template=None):
+                pod_status_template=None, node_init_template=None, node_heartbeat_template=None):
     cfg = abi.Config()
     cfg.abi_version = abi.ABI_VERSION
     cfg.cidr = cidr.encode()
@@ -148,6 +149,11 @@ def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200
         keep.append(b)
         cfg.custom_templates |= 2
         cfg.node_init_template = C.cast(b, C.c_char_p)
+    if node_heartbeat_template is not None:
+        b = C.create_string_buffer(node_heartbeat_template.encode())
+        keep.append(b)
+        cfg.custom_templates |= 4
+        cfg.node_heartbeat_template = C.cast(b, C.c_char_p)
     if comm_id is not None:
         b = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
         keep.append(b)
@@ -447,15 +453,29 @@ def pod_template_patch(tpl: str, containers=(), init_containers=(), readiness_ga
 
 
 def node_template_patch(tpl: str, event, arena: bytes, start=1704067200, node_ip="196.168.0.1",
-                        now=1704067230) -> bytes:
+                        now=1704067230, heartbeat_tpl=None) -> bytes:
     """kwok_node_template_patch: the init patch of the node record `event` (a
     NODE_EVENT_DTYPE row) under a custom node initialization template."""
     lib = load_engine_lib()
     ev = np.ascontiguousarray(np.asarray([event], dtype=abi.NODE_EVENT_DTYPE))
     out = C.create_string_buffer(1 << 16)
     m = C.c_size_t()
-    rc = lib.kwok_node_template_patch(tpl.encode(), C.cast(ev.ctypes.data, C.POINTER(abi.NodeEvent)), arena or b"\0",
+    rc = lib.kwok_node_template_patch(tpl.encode(), heartbeat_tpl.encode() if heartbeat_tpl else None,
+                                      C.cast(ev.ctypes.data, C.POINTER(abi.NodeEvent)), arena or b"\0",
                                       len(arena), start, node_ip.encode(), now, out, 1 << 16, C.byref(m))
+    if rc != 0:
+        raise KwokError(rc, (lib.kwok_template_last_error() or b"").decode())
+    return out.raw[:m.value]
+
+
+def heartbeat_template_patch(tpl=None, start=1704067200, node_ip="196.168.0.1", now=1704067230) -> bytes:
+    """kwok_heartbeat_template_patch: the heartbeat body under a custom heartbeat
+    template (None: the default)."""
+    lib = load_engine_lib()
+    out = C.create_string_buffer(1 << 16)
+    m = C.c_size_t()
+    rc = lib.kwok_heartbeat_template_patch(tpl.encode() if tpl else None, start, node_ip.encode(), now, out, 1 << 16,
+                                           C.byref(m))
     if rc != 0:
         raise KwokError(rc, (lib.kwok_template_last_error() or b"").decode())
     return out.raw[:m.value]

@@ -47,7 +47,7 @@ def test_oracle_library_exports():
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
                  "kwok_decode_node", "kwok_decode_pod", "kwok_decode_nodes", "kwok_decode_pods",  # host codec: feeds both, lives in the engine library
                  "kwok_template_render", "kwok_template_last_error", "kwok_pod_template_patch",
-                 "kwok_node_template_patch"):  # host template compiler (engine library)
+                 "kwok_node_template_patch", "kwok_heartbeat_template_patch"):  # host template compiler (engine library)
             continue
         assert hasattr(lib, name), name
 
@@ -63,7 +63,7 @@ STRUCTS = {
                                  "custom_templates", "buckets", "node_slots_per_bucket", "pod_slots_per_bucket",
                                  "max_pod_specs", "rank", "world_size", "device", "comm_id", "allgather",
                                  "allgather_user", "pod_handle_stride", "reserved0", "pod_status_template",
-                                 "node_init_template"]),
+                                 "node_init_template", "node_heartbeat_template"]),
     "kwok_tick_result": (abi.TickResult, ["n_heartbeat", "heartbeat_len", "heartbeat_stride", "n_node_init",
                                           "n_pod_patch", "n_delete", "heartbeat_epoch", "arena_bytes", "counters",
                                           "local_counters"]),

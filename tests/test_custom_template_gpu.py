@@ -129,3 +129,43 @@ def test_custom_node_init_template_engine():
         now += 30
     e.close()
     o.close()
+
+
+@pytest.mark.parametrize("hb", ["heartbeat_a.tpl", "heartbeat_b.tpl"])
+def test_custom_heartbeat_template_engine(hb):
+    """a custom heartbeat (1254 B: 79 units per slot, near the 80-unit limit; and
+    a short 165 B one): the stream writes the compiled body for every managed
+    node through the general group walk, node inits splice its conditions"""
+    from test_template_cpu import NODES, node_record
+    htext, ntext = tpl(hb), tpl("node_a.tpl")
+    kw = dict(cidr="10.0.0.1/16", node_ip="196.168.0.1", buckets=256, node_slots_per_bucket=64,
+              pod_slots_per_bucket=64)
+    e = Engine(make_config(node_heartbeat_template=htext, node_init_template=ntext, **kw))
+    o = Oracle(make_config(**kw))
+    recs = {}
+    for i in range(5003):  # not a multiple of the 4-slot stream group
+        ev, ar = node_record(NODES[i % len(NODES)], "node-%05d" % i)
+        h1, s1 = e.ingest_nodes_raw(ev, ar)
+        h2, _ = o.ingest_nodes_raw(ev, ar)
+        assert s1[0] == 0 and h1[0] == h2[0]
+        recs[int(h1[0])] = (ev, ar)
+    now = 1704067230
+    for t in range(3):
+        E, O = e.tick(now), o.tick(now)
+        assert list(E.heartbeat_nodes) == list(O.heartbeat_nodes)
+        body = engine.heartbeat_template_patch(htext, 1704067200, "196.168.0.1", now)
+        n = len(E.heartbeat_nodes)
+        assert E.heartbeat_len == len(body) and E.heartbeat_stride == (len(body) + 15) // 16 * 16
+        a = np.frombuffer(E.arena, np.uint8)[E.heartbeat_off:E.heartbeat_off + n * E.heartbeat_stride]
+        a = a.reshape(n, E.heartbeat_stride)[:, :E.heartbeat_len]
+        assert (a == np.frombuffer(body, np.uint8)[None, :]).all(), "tick %d heartbeat bodies" % t
+        assert len(E.node_inits) == (len(recs) if t == 0 else 0)
+        for h, got in E.node_inits:
+            ev, ar = recs[h]
+            assert got == engine.node_template_patch(ntext, ev[0], ar, 1704067200, "196.168.0.1", now,
+                                                     heartbeat_tpl=htext), h
+        out = e.read_outputs(heartbeat_once=True)  # the compact hand-off carries one body
+        assert out.heartbeat_body(0) == body
+        now += 30
+    e.close()
+    o.close()

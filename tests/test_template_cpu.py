@@ -241,3 +241,42 @@ def test_reference_node_template_compiles_to_the_default_blob():
         assert len(out.node_inits) == 1
         assert engine.node_template_patch(text, ev[0], ar, START, NODE_IP, START + 30) == out.node_inits[0][1], n
         o.close()
+
+
+# ---- custom heartbeat templates --------------------------------------------
+@pytest.mark.parametrize("name", ["heartbeat_a.tpl", "heartbeat_b.tpl"])
+def test_heartbeat_templates_match_gotmpl(name):
+    text = tpl(name)
+    for now in (START + 30, START + 86400 * 365 + 7):
+        funcs = {"NodeIP": lambda: NODE_IP, "Now": lambda: rfc3339(now), "StartTime": lambda: rfc3339(START)}
+        want = ('{"status":%s}' % gotmpl.render_to_json(text, {"metadata": {}, "spec": {}, "status": {}}, funcs)).encode()
+        assert engine.heartbeat_template_patch(text, START, NODE_IP, now) == want
+    # node inits splice the custom conditions: node_controller.go:101 appends the heartbeat template text
+    full = tpl("node_a.tpl") + "\n" + text
+    for n in NODES:
+        ev, ar = node_record(n)
+        funcs = {"NodeIP": lambda: NODE_IP, "Now": lambda: rfc3339(START + 30), "StartTime": lambda: rfc3339(START)}
+        want = ('{"status":%s}' % gotmpl.render_to_json(full, node_doc(n), funcs)).encode()
+        assert engine.node_template_patch(tpl("node_a.tpl"), ev[0], ar, START, NODE_IP, START + 30, heartbeat_tpl=text) == want
+
+
+def test_default_heartbeat_equals_the_oracle_body():
+    from kwok_amd.engine import make_config
+    from oracle.oracle import Oracle
+    o = Oracle(make_config(buckets=16, node_slots_per_bucket=4, pod_slots_per_bucket=8, node_ip=NODE_IP, start_time=START))
+    ev, ar = node_record({})
+    o.ingest_nodes_raw(ev, ar)
+    out = o.tick(START + 30)
+    assert engine.heartbeat_template_patch(None, START, NODE_IP, START + 30) == out.heartbeat_body(0)
+    if os.path.isdir(REF_TPL):  # the reference's own template compiles to the same body
+        ref = open(os.path.join(REF_TPL, "node.heartbeat.tpl")).read()
+        assert engine.heartbeat_template_patch(ref, START, NODE_IP, START + 30) == out.heartbeat_body(0)
+    o.close()
+
+
+@pytest.mark.parametrize("bad", ["conditions: []\nphase: Running\n",          # a second key
+                                 "conditions:\n- type: {{ .metadata.name }}\n",  # a per-node field
+                                 "conditions:\n" + "- message: %s\n  type: T\n" % ("x" * 1300)])  # too long
+def test_heartbeat_templates_outside_the_stream_are_rejected(bad):
+    with pytest.raises(KwokError):
+        engine.heartbeat_template_patch(bad)
