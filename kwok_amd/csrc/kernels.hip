@@ -1078,10 +1078,13 @@ __device__ __noinline__ void hb_fill_groups_any(const DevState& S, const uint4* 
             if (64u * k + l < GU && u0 + 64u * k < units) p[64 * k] = r[k];
     }
 }
-// groups [g0, g1) of the heartbeat region (units past n_hb slots are not written)
+// groups [g0, g1) of the heartbeat region (units past n_hb slots are not written).
+// GEN: a custom heartbeat geometry (k_tick<true>); the default one compiles
+// without the general walk so its register allocation is untouched.
+template <bool GEN>
 __device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* tmpl, uint64_t n_hb, uint64_t g0,
                                                uint64_t g1) {
-    if (S.hb_units != (uint32_t)HB_CHUNKS) {  // wave-uniform: a custom heartbeat template
+    if (GEN) {
         hb_fill_groups_any(S, tmpl, n_hb, g0, g1);
         return;
     }
@@ -1113,12 +1116,13 @@ __device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* t
 // static shares of the heartbeat stream: the streamer blocks split the first
 // stream_share/1024 of it, and every chain block writes an equal slice of the
 // rest once its own work is done (so the stream's tail overlaps nothing idle)
+template <bool GEN>
 __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, bool streamer,
                                               uint32_t idx, uint32_t cnt) {
     const uint64_t groups = (n_hb + HB_GROUP_SLOTS - 1) / HB_GROUP_SLOTS;
     const uint64_t cut = groups * S.stream_share / 1024;
     const uint64_t lo = streamer ? 0 : cut, n = streamer ? cut : groups - cut;
-    hb_fill_groups(S, tmpl, n_hb, lo + n * idx / cnt, lo + n * (idx + 1) / cnt);
+    hb_fill_groups<GEN>(S, tmpl, n_hb, lo + n * idx / cnt, lo + n * (idx + 1) / cnt);
 }
 
 // per-tick heartbeat template in LDS: static bytes + Now / StartTime slots
@@ -1409,6 +1413,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
 //          the tick has Gets or Puts (multi rank: among all blocks); emission
 //          of the dirty chunks.
 // ---------------------------------------------------------------------------
+template <bool GEN_HB>
 __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix, uint64_t start_unix,
                                                    uint32_t n_hb, int phases, uint32_t tag, uint64_t arrive_target) {
     const int t = threadIdx.x;
@@ -1446,7 +1451,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__builtin_amdgcn_s_memrealtime() - t0 < S.stream_delay) __builtin_amdgcn_s_sleep(4);
         }
-        if (!(phases & TICK_NOSTREAM)) hb_fill_share(S, hb_tmpl4, n_hb, true, b - S.n_chain, gridDim.x - S.n_chain);
+        if (!(phases & TICK_NOSTREAM)) hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, true, b - S.n_chain, gridDim.x - S.n_chain);
         if ((phases & TICK_PROF) && t == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1616,7 +1621,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             TSTAMP(12);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
-                hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+                hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, false, b, S.n_chain);
             }
             TSTAMP(13);
             if (t < AG_DIRTY && (acc_old >> ACC_SHIFT) == S.n_chain - 1u) {
@@ -1662,7 +1667,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
-                hb_fill_share(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+                hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, false, b, S.n_chain);
             }
             return;  // the BACK launch follows the exchange
         }
@@ -1833,10 +1838,11 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const uint32_t grid = S.n_chain + ((phases & TICK_FRONT) ? n_stream : 0u);
+    auto kern = S.hb_units == (uint32_t)HB_CHUNKS ? k_tick<false> : k_tick<true>;
     if (t0)
-        hipExtLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases, tag,
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases, tag,
                               arrive_target);
-    else hipLaunchKernelGGL(k_tick, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases, tag, arrive_target);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, st, S, now, start, n_hb, phases, tag, arrive_target);
 }
 
 // ---------------------------------------------------------------------------
@@ -2144,9 +2150,10 @@ int emit_occupancy() {
 }
 
 int tick_occupancy() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tick, BLOCK, 0) != hipSuccess) return 0;
-    return n;
+    int n = 0, m = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_tick<false>, BLOCK, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_tick<true>, BLOCK, 0) != hipSuccess) return 0;
+    return std::min(n, m);
 }
 
 }  // namespace kwok
