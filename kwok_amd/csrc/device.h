@@ -164,7 +164,25 @@ struct SpecDesc {
     uint16_t max_len;         // 16-aligned arena reservation
     uint32_t nxt_off;         // its timestamp lookup: spec_nxt[nxt_off + d] (build_ts_lookup)
     uint16_t n_ts, pad;
+    uint32_t tab_off;         // its unit tables (build_unit_tables), NO_TAB: the general emitter only
 };
+constexpr uint32_t NO_TAB = 0xFFFFFFFFu;
+
+// ---- k_emit's table-driven pod path ------------------------------------------
+// A pod patch's byte layout depends only on its spec and status shape: empty
+// status (shape 0), or the lengths h, p (7..15) of its hostIP / podIP strings
+// (shape 1 + (h-7)*9 + (p-7)).  Per spec and shape the host tabulates every
+// 16-byte unit of the patch: its static bytes (zero at the creationTimestamp
+// slots and the IP digits) and up to two overlays, each a byte offset into the
+// job's value row (a 16-byte window of it lands on the unit).  Value row, per
+// job, VROW_STRIDE bytes in LDS: the timestamp at VROW_TS, the hostIP string at
+// VROW_H, the podIP string at VROW_P, zeros elsewhere; the 16 bytes before a
+// row are the previous row's zero tail (or a zero lead pad).  An overlay
+// offset is stored biased by VROW_BIAS (0: no overlay, a zero window).
+constexpr int EMIT_SHAPES = 82;
+constexpr int VROW_STRIDE = 100, VROW_TS = 0, VROW_H = 36, VROW_P = 68, VROW_BIAS = 16;
+constexpr uint32_t MAX_TAB_UNITS = 1u << 22;  // all specs' tables (64 MiB of static bytes)
+constexpr inline uint32_t emit_shape(uint32_t h, uint32_t p) { return 1u + (h - 7u) * 9u + (p - 7u); }
 // byte padding around the spec / blob arrays the emitter reads 4-byte words of
 // (a 16-byte window reads up to 15 bytes before a segment and 20 past it)
 constexpr int SRC_PAD_FRONT = 16, SRC_PAD_BACK = 64;

@@ -202,6 +202,9 @@ struct kwok_engine {
     DevBuf<uint8_t> d_spec_bytes;
     std::vector<uint16_t> spec_nxt_h;  // timestamp lookups of every spec (build_ts_lookup)
     DevBuf<uint16_t> d_spec_nxt;
+    DevBuf<uint8_t> d_unit_tab;      // k_emit's unit tables (16 bytes per unit), appended per spec
+    DevBuf<uint16_t> d_unit_desc;
+    uint32_t tab_units = 0;
     uint32_t max_pod_len = 0;
     std::unordered_map<std::string, uint64_t> blob_ids;
     uint64_t empty_blob = 0;      // the blob of a node with an empty status (every status field absent)
@@ -975,7 +978,7 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
-                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_blob.p, e->d_ops,
+                    e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1267,6 +1270,9 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     if (p.max_len > 0xFFF0) return e->fail(KWOK_EDOMAIN, "pod patch longer than 64 KiB");
     std::vector<uint16_t> nxt;
     if (!build_ts_lookup(p, nxt)) return e->fail(KWOK_EDOMAIN, "pod patch layout outside the emitter's domain");
+    std::string tab;
+    std::vector<uint16_t> tdesc;
+    const bool tabled = build_unit_tables(p, tab, tdesc);  // else: the general emitter path only
     std::string key = p.a + '\x01' + p.ka + '\x01' + p.b + '\x01' + p.kb + '\x01' + p.c + '\x01' + p.kc;
     auto it = e->spec_ids.find(key);
     if (it != e->spec_ids.end()) {
@@ -1282,6 +1288,23 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     d.len_c = (uint16_t)p.c.size();
     d.max_len = (uint16_t)p.max_len;
     d.nxt_off = (uint32_t)e->spec_nxt_h.size();
+    d.tab_off = NO_TAB;
+    // KWOK_EMIT_TAB_UNITS caps the table units (tests: 0 = the general emitter only, small = mixed chunks)
+    const char* cap_env = getenv("KWOK_EMIT_TAB_UNITS");
+    const size_t tab_cap = cap_env ? (size_t)strtoull(cap_env, nullptr, 10) : (size_t)MAX_TAB_UNITS;
+    if (tabled && e->tab_units + tdesc.size() <= std::min(tab_cap, (size_t)MAX_TAB_UNITS)) {
+        const size_t n = e->tab_units + tdesc.size();
+        int rc;
+        if ((rc = dgrow(e, e->d_unit_tab, n * 16)) || (rc = dgrow(e, e->d_unit_desc, n))) return rc;
+        HIPCHK(e, hipMemcpyAsync(e->d_unit_tab.p + (size_t)e->tab_units * 16, tab.data(), tab.size(),
+                                 hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipMemcpyAsync(e->d_unit_desc.p + e->tab_units, tdesc.data(), tdesc.size() * 2,
+                                 hipMemcpyHostToDevice, e->st));
+        d.tab_off = e->tab_units;
+        e->tab_units = (uint32_t)n;
+        e->S.unit_tab = reinterpret_cast<const uint4*>(e->d_unit_tab.p);
+        e->S.unit_desc = e->d_unit_desc.p;
+    }
     const std::string kinds = p.ka + p.kb + p.kc;
     for (size_t i = 0; i < kinds.size(); i++)  // slot starts (kinds 0..19 in a row)
         if (kinds[i] == 0) d.n_ts++;

@@ -46,6 +46,8 @@ struct DevState {
     const uint8_t* spec_bytes;     // SRC_PAD_FRONT bytes into a padded device array
     const uint8_t* blob;           // (likewise) framed node init blobs: pre | post
     const uint16_t* spec_nxt;      // timestamp lookups of every spec (SpecDesc::nxt_off)
+    const uint4* unit_tab;         // unit tables of every spec (SpecDesc::tab_off, build_unit_tables)
+    const uint16_t* unit_desc;     //   and their overlay words
     uint32_t n_specs, spec_total;  // spec descriptors; bytes of the concatenated spec programs
     uint32_t nxt_total;            // entries of spec_nxt
     uint32_t blob_total;           // bytes of the interned node blobs

@@ -1873,6 +1873,15 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
 // is read from global memory instead (same code, generic pointers).
 // ---------------------------------------------------------------------------
 constexpr int EMIT_BLOCK = 256;
+#ifndef EMIT_TAB_G
+#define EMIT_TAB_G 8  // table path: lanes per job
+#endif
+#ifndef EMIT_FLAT_UNR
+#define EMIT_FLAT_UNR 4  // one-spec chunks: 1 KiB stores per lane step
+#endif
+#ifndef EMIT_TAB_UNR
+#define EMIT_TAB_UNR 5  // table path: units per lane per step (G * UNR = 40: a default pod patch)
+#endif
 static_assert(EMIT_BLOCK == BLOCK, "build_hb_template strides by BLOCK");
 constexpr int EC_PROG = 4096, EC_NXT = 1152, EC_BLOB = 2048;
 constexpr uint32_t SEG_STRIDE = 56;  // per job: "hostIP":"H", (28 bytes) | "podIP":"P", (28 bytes)
@@ -1882,12 +1891,24 @@ constexpr uint32_t TS_ZERO = TS_FIRST + 64 * TS_STRIDE;  // 20+ zero bytes (a un
 constexpr uint32_t TS_AREA = TS_ZERO + 32;
 constexpr uint32_t HB_LDS = HB_MAX_STRIDE + 32;  // the heartbeat template: CONDS at conds_off, read up to 32 bytes around it
 static_assert(HB_LDS >= HB_STRIDE && HB_LDS >= ((HB_PREFIX + CONDS_LEN + 15) & ~15) + 32, "heartbeat template in LDS");
+// the table path's value rows (device.h) alias seg / ts (a chunk takes one path)
+constexpr uint32_t VROW_AREA = VROW_BIAS + 64 * VROW_STRIDE + 4;  // lead pad, rows, the last window's 5th dword
+constexpr uint32_t EMIT_GEN_AREA = SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_BACK + TS_AREA;
 struct EmitWave {
     uint4 rec[64];   // per job: arena offset / 16, region starts 1|2 and 3|4 (u16; 0xFFFF: none), template offset
+                     // (table path: arena offset / 16, table unit base, unit count)
     uint32_t nxt[64];  // pods: the spec's timestamp lookup offset
     uint8_t seg[SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_BACK];
     uint8_t ts[TS_AREA];
+    uint8_t vx[VROW_AREA > EMIT_GEN_AREA ? ((VROW_AREA - EMIT_GEN_AREA + 3) & ~3u) : 4];
 };
+static_assert(offsetof(EmitWave, ts) == offsetof(EmitWave, seg) + sizeof(EmitWave::seg) &&
+                  offsetof(EmitWave, vx) == offsetof(EmitWave, ts) + sizeof(EmitWave::ts) &&
+                  sizeof(EmitWave::seg) + sizeof(EmitWave::ts) + sizeof(EmitWave::vx) >= VROW_AREA,
+              "value rows fit over seg | ts | vx");
+static_assert(VROW_STRIDE % 4 == 0 && (VROW_STRIDE / 4) % 2 == 1, "rows: whole dwords, an odd count (banks)");
+static_assert(VROW_TS == 0 && VROW_H == 36 && VROW_P == 68 && VROW_STRIDE == 100,
+              "emit_phase1_tab writes the row as 25 dwords: TS 0-4, H 9-12, P 17-20");
 struct EmitLds {
     uint16_t nxt[EC_NXT];
     uint8_t prog[SRC_PAD_FRONT + EC_PROG + SRC_PAD_BACK];
@@ -2108,14 +2129,269 @@ __device__ __forceinline__ void emit_phase2(const DevState& S, const EmitLds* L,
     }
 }
 
+// ---- table-driven pod path (device.h): lane l <- job q of the chunk --------
+struct TabJob {
+    uint32_t o16, tb, nu, mu;  // mu: the spec's reservation in units (max_len / 16)
+    bool ok;  // the job's spec has unit tables (or q >= n)
+    Ts ts;
+    IpStr h, p;
+};
+__device__ __forceinline__ TabJob emit_job_tab(const DevState& S, uint32_t q, uint32_t n) {
+    TabJob J;
+    J.o16 = J.tb = J.nu = J.mu = 0;
+    J.ok = true;
+    J.h.lo = J.h.hi = J.p.lo = J.p.hi = 0;
+    J.ts.w0 = J.ts.w1 = J.ts.w2 = 0;
+    if (q < n) {
+        const uint4 j = S.pp_job[q];  // podIP (0: no status section), hostIP, creationTimestamp, spec
+        const SpecDesc sd = S.specs[j.w];
+        J.ok = sd.tab_off != NO_TAB;
+        J.ts = format_ts(j.z);
+        uint32_t shape = 0;
+        if (j.y != 0) {  // `{{ with .status }}`: hostIP / podIP (pod.status.tpl:44-47)
+            J.h = format_ip(j.y);
+            J.p = format_ip(j.x);
+            shape = emit_shape(J.h.len, J.p.len);
+        }
+        J.mu = (uint32_t)sd.max_len >> 4;
+        J.tb = sd.tab_off + shape * J.mu;
+        J.o16 = (uint32_t)(S.pp_off[q] >> 4);
+        J.nu = (S.pp_len[q] + 15u) >> 4;
+    }
+    return J;
+}
+// the job's value row (25 dwords: TS, zeros, H, zeros, P, zeros) and record
+__device__ __forceinline__ void emit_row_tab(EmitWave* W, const TabJob& J) {
+    const uint32_t l = lane_id();
+    uint32_t* r = reinterpret_cast<uint32_t*>(W->seg + VROW_BIAS + l * VROW_STRIDE);
+    const uint32_t v[25] = {(uint32_t)J.ts.w0, (uint32_t)(J.ts.w0 >> 32), (uint32_t)J.ts.w1, (uint32_t)(J.ts.w1 >> 32),
+                            (uint32_t)J.ts.w2, 0u, 0u, 0u, 0u,
+                            (uint32_t)J.h.lo, (uint32_t)(J.h.lo >> 32), (uint32_t)J.h.hi, (uint32_t)(J.h.hi >> 32),
+                            0u, 0u, 0u, 0u,
+                            (uint32_t)J.p.lo, (uint32_t)(J.p.lo >> 32), (uint32_t)J.p.hi, (uint32_t)(J.p.hi >> 32),
+                            0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 25; i++) r[i] = v[i];
+    if (l < 4) reinterpret_cast<uint32_t*>(W->seg)[l] = 0u;  // the lead pad (row 0's zero window)
+    W->rec[l] = make_uint4(J.o16, J.tb, J.nu, 0u);
+}
+// G lanes per job, G * UNR units of it per step (unit li + G * i for lane li).
+// Steps are (job pass, unit step) pairs, software-pipelined: the next step's
+// record and table loads are issued before this step's value-row reads and
+// stores, so the table round trip hides behind a step of stores.
+template <int UNR>
+struct TabStep {
+    uint4 t[UNR];
+    uint32_t d[UNR];
+    uint32_t o16, nu, k, u0;
+};
+template <int G, int UNR>
+__device__ __forceinline__ TabStep<UNR> tab_load(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t item,
+                                                 uint32_t nsteps) {
+    const uint32_t l = lane_id(), li = l % G;
+    const uint32_t pass = item / nsteps, step = item - pass * nsteps;  // wave-uniform
+    TabStep<UNR> T;
+    T.k = pass * (64 / G) + l / G;
+    T.u0 = step * (G * UNR) + li;
+    uint32_t tb = 0;
+    T.nu = 0, T.o16 = 0;
+    if (T.k < cnt) {
+        const uint4 R = W->rec[T.k];
+        T.o16 = R.x, tb = R.y, T.nu = R.z;
+    }
+#pragma unroll
+    for (int i = 0; i < UNR; i++) {  // past the job's units: reload its last unit (no store)
+        const uint32_t u = T.nu ? min(T.u0 + G * i, T.nu - 1u) : 0u;
+        T.t[i] = S.unit_tab[tb + u];
+        T.d[i] = S.unit_desc[tb + u];
+    }
+    return T;
+}
+template <int G, int UNR>
+__device__ __forceinline__ void tab_store(const DevState& S, const EmitWave* W, const TabStep<UNR>& T) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint8_t* row = W->seg + T.k * VROW_STRIDE;  // biased: row k starts VROW_BIAS bytes in
+    uint32_t dor = 0;
+#pragma unroll
+    for (int i = 0; i < UNR; i++) dor |= T.d[i];
+    uint4 v[UNR];
+#pragma unroll
+    for (int i = 0; i < UNR; i++) v[i] = ext16(row, T.d[i] & 0xFFu);
+    if (__builtin_expect(dor >> 8, 0)) {  // a second field in a unit
+#pragma unroll
+        for (int i = 0; i < UNR; i++) {
+            const uint4 w = ext16(row, T.d[i] >> 8);
+            v[i].x |= w.x, v[i].y |= w.y, v[i].z |= w.z, v[i].w |= w.w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < UNR; i++) {
+        const uint32_t u = T.u0 + G * i;
+        if (u < T.nu)
+            *reinterpret_cast<u32x4*>(S.arena + ((uint64_t)(T.o16 + u) << 4)) =
+                u32x4{T.t[i].x | v[i].x, T.t[i].y | v[i].y, T.t[i].z | v[i].z, T.t[i].w | v[i].w};
+    }
+}
+// maxnu: the chunk's largest unit count (wave-uniform)
+template <int G, int UNR>
+__device__ __forceinline__ void emit_phase2_tab(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t maxnu) {
+    const uint32_t nsteps = (maxnu + G * UNR - 1) / (G * UNR);
+    const uint32_t items = ((cnt + 64 / G - 1) / (64 / G)) * nsteps;
+    if (items == 0) return;
+    TabStep<UNR> cur = tab_load<G, UNR>(S, W, cnt, 0, nsteps);
+    for (uint32_t it = 0; it < items; it++) {
+        TabStep<UNR> nxt;
+        if (it + 1 < items) nxt = tab_load<G, UNR>(S, W, cnt, it + 1, nsteps);
+        tab_store<G, UNR>(S, W, cur);
+        cur = nxt;
+    }
+}
+
+// Chunks of one spec (every job reserves the same max_len = MU units, so the
+// chunk's patches are one contiguous run of cnt * MU units): lane l takes units
+// l + 64 i of the run, so every store is a whole 1 KiB of the arena.  A unit's
+// job / unit index advance incrementally; units of a job's reservation past its
+// patch are not stored.  Software-pipelined like the G-lane path.
+template <int UNR>
+struct FlatStep {
+    uint4 t[UNR];
+    uint32_t d[UNR], k[UNR], ok[UNR];
+};
+template <int UNR>
+__device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const EmitWave* W, uint32_t& k, uint32_t& u,
+                                                   uint32_t dk, uint32_t du, uint32_t mu, uint32_t cnt) {
+    FlatStep<UNR> F;
+#pragma unroll
+    for (int i = 0; i < UNR; i++) {
+        const bool live = k < cnt;
+        const uint4 R = W->rec[live ? k : 0u];  // arena offset / 16, table unit base, unit count
+        F.k[i] = k;
+        F.ok[i] = live && u < R.z;
+        const uint32_t uu = F.ok[i] ? u : 0u;
+#ifdef EMIT_DIAG_NO_TAB  // timing builds only: no table loads
+        F.t[i] = make_uint4(uu, R.y, 0u, 0u);
+        F.d[i] = uu & 63u;
+#else
+        F.t[i] = S.unit_tab[R.y + uu];
+        F.d[i] = S.unit_desc[R.y + uu];
+#endif
+        k += dk, u += du;
+        if (u >= mu) u -= mu, k++;
+    }
+    return F;
+}
+template <int UNR>
+__device__ __forceinline__ void flat_store(const DevState& S, const EmitWave* W, const FlatStep<UNR>& F, uint64_t o16,
+                                           uint32_t g) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t dor = 0;
+#pragma unroll
+    for (int i = 0; i < UNR; i++) dor |= F.d[i];
+    uint4 v[UNR];
+#pragma unroll
+    for (int i = 0; i < UNR; i++) v[i] = ext16(W->seg + F.k[i] * VROW_STRIDE, F.d[i] & 0xFFu);
+    if (__builtin_expect(dor >> 8, 0)) {  // a second field in a unit
+#pragma unroll
+        for (int i = 0; i < UNR; i++) {
+            const uint4 w = ext16(W->seg + F.k[i] * VROW_STRIDE, F.d[i] >> 8);
+            v[i].x |= w.x, v[i].y |= w.y, v[i].z |= w.z, v[i].w |= w.w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < UNR; i++)
+        if (F.ok[i])
+            *reinterpret_cast<u32x4*>(S.arena + ((o16 + g + 64u * i) << 4)) =
+                u32x4{F.t[i].x | v[i].x, F.t[i].y | v[i].y, F.t[i].z | v[i].z, F.t[i].w | v[i].w};
+}
+template <int UNR>
+__device__ __forceinline__ void emit_phase2_flat(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t mu) {
+    const uint32_t l = lane_id();
+    const uint64_t o16 = W->rec[0].x;
+    const uint32_t total = cnt * mu;
+    uint32_t k = l / mu, u = l - (l / mu) * mu;
+    const uint32_t dk = 64u / mu, du = 64u - dk * mu;
+    FlatStep<UNR> cur = flat_load<UNR>(S, W, k, u, dk, du, mu, cnt);
+    for (uint32_t g0 = 0; g0 < total; g0 += 64u * UNR) {
+        FlatStep<UNR> nxt;
+        if (g0 + 64u * UNR < total) nxt = flat_load<UNR>(S, W, k, u, dk, du, mu, cnt);
+        flat_store<UNR>(S, W, cur, o16, g0 + l);
+        cur = nxt;
+    }
+}
+
+// ---- node inits of one blob (the common case: nodes created alike) --------
+// When every job of a chunk frames the same blob, its init patches are all the
+// same bytes: the wave renders the patch once into LDS (seg | ts | vx) with the
+// general unit emitter, then streams cnt copies of it with aligned 16-byte LDS
+// reads (the jobs sit back to back in the arena, init_patch_len rounded to 16).
+constexpr uint32_t INIT_RENDER_MAX = (SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_BACK + TS_AREA) & ~15u;
+
+// the chunk's cnt init jobs, all of one blob, nu units each (records in W->rec)
+template <bool CACHED>
+__device__ __forceinline__ void emit_init_copies(const DevState& S, const EmitLds* L, EmitWave* W, uint32_t cnt,
+                                                 uint32_t nu) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t l = lane_id();
+    EmitSrc E;
+    E.lds = reinterpret_cast<const uint8_t*>(L);
+    E.o_seg = 0, E.o_ts = 0;
+    E.tbase = CACHED ? E.lds : S.blob;
+    E.o_tmpl = CACHED ? (uint32_t)offsetof(EmitLds, blob) + SRC_PAD_FRONT : 0u;
+    uint4* img = reinterpret_cast<uint4*>(W->seg);  // 16-byte aligned
+    for (uint32_t u = l; u < nu; u += 64) {  // render job 0's patch
+        uint64_t dst;
+        img[u] = emit_unit<false, CACHED>(S, L, W, E, 0, u << 4, dst);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t o16 = W->rec[0].x;  // the chunk's jobs are contiguous from job 0's offset
+    const uint32_t total = cnt * nu;
+    uint32_t u = l % nu;
+    const uint32_t step = 64u % nu;
+    for (uint32_t g = l; g < total; g += 64) {
+        const uint4 v = img[u];
+        *reinterpret_cast<u32x4*>(S.arena + ((o16 + g) << 4)) = u32x4{v.x, v.y, v.z, v.w};
+        u += step;
+        u = u >= nu ? u - nu : u;
+    }
+}
+
 template <bool POD, bool CACHED>
 __device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_t w0, uint32_t nw, uint32_t n) {
     EmitWave* W = &L->w[wave_id()];
     for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
         const uint32_t cnt = min(64u, n - ch * 64u);
+        if (POD) {
+            const TabJob J = emit_job_tab(S, ch * 64u + lane_id(), n);
+            if (__ballot(!J.ok) == 0) {  // every job of the chunk has tables
+                emit_row_tab(W, J);
+                uint32_t mx = J.nu;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+                const uint32_t mu = __builtin_amdgcn_readfirstlane(J.mu);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rows before phase 2 reads them
+                if (__ballot(ch * 64u + lane_id() < n && J.mu != mu) == 0)
+                    emit_phase2_flat<EMIT_FLAT_UNR>(S, W, cnt, mu);
+                else
+                    emit_phase2_tab<EMIT_TAB_G, EMIT_TAB_UNR>(S, W, cnt, __builtin_amdgcn_readfirstlane(mx));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // phase 2's reads before the next rows
+                continue;
+            }
+        }
         const uint32_t nu = emit_phase1<POD>(S, W, ch * 64u + lane_id(), n);
         const uint32_t incl = wave_incl_scan(nu);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the records before phase 2 reads them
+        if (!POD) {
+            const uint64_t q = (uint64_t)ch * 64u + lane_id();
+            const uint64_t blob = q < n ? S.init_job[q] : 0ull;
+            const uint64_t b0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(blob >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)blob);
+            const uint32_t nu0 = __builtin_amdgcn_readfirstlane(nu);
+            if (__ballot(q < n && blob != b0) == 0 && nu0 * 16u <= INIT_RENDER_MAX) {
+                emit_init_copies<CACHED>(S, L, W, cnt, nu0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                continue;
+            }
+        }
         emit_phase2<POD, CACHED>(S, L, W, cnt, incl - nu, rdlane(incl, 63));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // phase 2's reads before the next records
     }
@@ -2129,11 +2405,19 @@ __global__ __launch_bounds__(EMIT_BLOCK, 4) void k_emit(DevState S, uint64_t now
     if (n_pp == 0 && n_init == 0) return;
     stage_emit(S, &L, n_pp != 0, n_init != 0, now_unix, start_unix);
     const uint32_t w0 = blockIdx.x * (EMIT_BLOCK / 64) + wave_id(), nw = gridDim.x * (EMIT_BLOCK / 64);
+#ifdef EMIT_DIAG_NO_INITS  // timing builds only (tools/build_variant.sh): one job kind skipped
+    if (false) {
+#else
     if (n_init) {
+#endif
         if (L.blob_ok) emit_jobs<false, true>(S, &L, w0, nw, n_init);
         else emit_jobs<false, false>(S, &L, w0, nw, n_init);
     }
+#ifdef EMIT_DIAG_NO_PODS
+    if (false) {
+#else
     if (n_pp) {
+#endif
         if (L.spec_ok) emit_jobs<true, true>(S, &L, w0, nw, n_pp);
         else emit_jobs<true, false>(S, &L, w0, nw, n_pp);
     }

@@ -75,6 +75,10 @@ std::string heartbeat_conditions(const HeartbeatTemplate& hb, const std::string&
 
 // k_emit's timestamp-slot lookup of a spec (false: layout outside what it handles)
 bool build_ts_lookup(const SpecProgram& p, std::vector<uint16_t>& out);
+// k_emit's unit tables of a spec (device.h, "table-driven pod path"):
+// EMIT_SHAPES x (max_len / 16) units, 16 static bytes each (tab) and an overlay
+// word (desc: offset | offset << 8).  false: a unit needs more than two overlays.
+bool build_unit_tables(const SpecProgram& p, std::string& tab, std::vector<uint16_t>& desc);
 
 // domain checks (DESIGN.md "Supported domain")
 bool safe_string(const char* s, size_t n);

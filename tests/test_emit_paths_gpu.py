@@ -1,8 +1,10 @@
 """GPU parity of every k_emit source path against the CPU oracle.
 
-k_emit assembles each 16-byte output unit from at most two source regions
-(kernels.hip "k_emit"); the spec programs and node blobs come from the
-block's LDS cache when they fit and from global memory otherwise.  These
+k_emit writes a pod patch from its spec's per-shape unit tables (static bytes
+plus value-row overlays) or, for specs without tables, assembles each 16-byte
+unit from at most two source regions (kernels.hip "k_emit"); the spec programs
+and node blobs come from the block's LDS cache when they fit and from global
+memory otherwise.  Every test runs with the tables, without them, and mixed.  These
 tests drive both paths for pod patches (pod_controller.go:404-439 over
 pod.status.tpl) and node-init patches (node_controller.go:356-391 over
 node.status.tpl), in the same tick and separately, with patches far past
@@ -15,6 +17,18 @@ from gpu_common import Driver, new_pods
 from kwok_amd import abi
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["table", "general", "mixed"])
+def emit_path(request, monkeypatch):
+    """pod patches from the per-shape unit tables, from the general region
+    emitter (KWOK_EMIT_TAB_UNITS=0), or both (a cap that tables only the first
+    specs registered, so chunks mix the two and fall back as a whole)"""
+    if request.param == "general":
+        monkeypatch.setenv("KWOK_EMIT_TAB_UNITS", "0")
+    elif request.param == "mixed":
+        monkeypatch.setenv("KWOK_EMIT_TAB_UNITS", "20000")
+    return request.param
 
 HOST_IPS = ["1.2.3.4", "10.20.30.40", "100.100.100.100", "192.168.100.200", "255.255.255.255", "9.99.9.99"]
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build an engine library variant with extra kernel defines, for A/B runs
+# (KWOK_ENGINE_LIB=...).  Usage: build_variant.sh NAME "-DFOO=1 -DBAR=2"
+set -e
+cd "$(dirname "$0")/../kwok_amd"
+make -s lib/libkwok_engine.so
+mkdir -p lib/var
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -g -fPIC -std=c++17 -Wall -Wno-unused-function $2 \
+  -c csrc/kernels.hip -o lib/var/kernels_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/var/libkwok_engine_$1.so lib/engine.o lib/templates.o \
+  lib/codec.o lib/gotemplate.o lib/var/kernels_$1.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+echo lib/var/libkwok_engine_$1.so
