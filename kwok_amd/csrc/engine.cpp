@@ -120,6 +120,7 @@ struct kwok_engine {
     kwok_config cfg{};
     std::string err;
     int W = 1, rank = 0, dev = 0;
+    bool multi = false;  // the FRONT / exchange / BACK tick (W > 1, or KWOK_FORCE_MULTI with one rank)
     uint32_t B = 0, Cn = 0, Cp = 0, b_lo = 0, b_hi = 0, nb = 0, NL = 0, PL = 0;
     uint32_t Hs = 0;  // pod handle stride: handle = bucket * Hs + slot in the bucket; Cp grows up to it
     PoolGeom pool{};
@@ -264,6 +265,7 @@ struct kwok_engine {
     bool sync_spin = true;      // spin on a tick's completion event (KWOK_SYNC=spin, the default)
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
+    int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
     uint64_t front_launches = 0;  // FRONT launches since the cross-block state was last zeroed
@@ -1015,6 +1017,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     kwok_engine* e = new kwok_engine();
     e->cfg = *cfg;
     e->W = W;
+    // KWOK_FORCE_MULTI=1 (tests): one rank through the multi-rank tick, so the exchange
+    // (RCCL with comm_id, else the allgather callback) runs on a single GPU
+    e->multi = W > 1 || (getenv("KWOK_FORCE_MULTI") && (cfg->comm_id || cfg->allgather));
     e->rank = cfg->rank;
     e->dev = cfg->device;
     e->B = cfg->buckets;
@@ -1117,6 +1122,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->chain_prio = pr && pr[0] == '1';
         if (const char* v = getenv("KWOK_TICK_STREAM_DELAY_NS")) S.stream_delay = (uint32_t)std::max(0, atoi(v) / 10);
         if (const char* v = getenv("KWOK_TICK_STREAM_SHARE")) e->share_env = std::min(1024, std::max(0, atoi(v)));
+        if (const char* v = getenv("KWOK_HB_NT")) e->nt_env = atoi(v) != 0;
         if (const char* v = getenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")) e->debug_fault_tick = strtoull(v, nullptr, 10);
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
@@ -1137,6 +1143,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pool = e->pool;
     S.node_ip = e->node_ip;
     S.world = W;
+    S.multi = e->multi ? 1 : 0;
     S.cni = cfg->enable_cni ? 1u : 0u;
     {
         // a chain block's bucket range must fit its LDS node flags and 64 pod chunks
@@ -1196,7 +1203,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.hb_pre = e->d_hb_pre;
     S.pod_fill = e->d_pod_fill;
     S.rank = e->rank;
-    if (W > 1) {
+    if (e->multi) {
         if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
         S.xall = e->d_xall;
         if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
@@ -1916,6 +1923,11 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // a long heartbeat stream is shared with the chain blocks once they are done
     // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)e->hb_stride >= (32ull << 20) ? 921u : 1024u);
+    // a stream that fits the 256 MB Infinity Cache is rewritten from it every tick
+    // (plain stores); a larger one (1M nodes: 1.07 GB) is written non-temporally:
+    // 239 -> 216 us per 1M x 10M tick (no L2 pollution under the chain's reads,
+    // no dirty L2 left for the kernel-end write-back)
+    S.hb_nt = e->nt_env >= 0 ? (uint32_t)e->nt_env : (nhb * (uint64_t)e->hb_stride >= (256ull << 20) ? 1u : 0u);
     int rc = bind_slot(e, k);
     if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
@@ -1926,7 +1938,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         T.target = ++e->front_launches * S.n_chain;
     }
     const uint64_t now = T.now;
-    if (e->W == 1) {
+    if (!e->multi) {
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
@@ -2027,7 +2039,7 @@ void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride) {
     H.rel_total = t[AG_REL];
 }
 
-bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && e->W == 1; }
+bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && !e->multi; }
 
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
 void trace_tick(kwok_engine* e) {
@@ -2101,12 +2113,12 @@ int retire(kwok_engine* e) {
     } else if (hipEventSynchronize(T.done) != hipSuccess) {
         return failed(e->fail(KWOK_EDEVICE, "tick event sync"));
     }
-    if (e->W > 1 && T.hdr_h->xovf) {
+    if (e->multi && T.hdr_h->xovf) {
         int rc = finish_long_lists(e, k, next);
         if (rc) return failed(rc);
     }
     const auto t2 = clk::now();
-    if (e->W == 1) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride);
+    if (!e->multi) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride);
     const TickHdr& H = *T.hdr_h;
     if (!H.err && (H.n_pp || H.n_init) && !T.emit_queued) {
         // jobs nobody expected (no events since the previous tick): their bytes now
@@ -2145,7 +2157,7 @@ int retire(kwok_engine* e) {
         // s_memrealtime stamps (100 MHz)
         float k0 = 0, k1 = 0;
         (void)hipEventElapsedTime(&k0, T.pev[0], T.pev[1]);
-        if (e->W > 1) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
+        if (e->multi) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
         float k2 = 0;
         if (T.emit_queued) (void)hipEventElapsedTime(&k2, T.pev[4], T.pev[5]);
         const double kern = (double)k0 + k1 + k2;
@@ -2162,7 +2174,7 @@ int retire(kwok_engine* e) {
         e->prof_ms[KWOK_T_CLASSIFY] += classify;
         e->prof_ms[KWOK_T_STREAM] += stream;
         e->prof_ms[KWOK_T_HEADER] += header;
-        e->prof_ms[KWOK_T_EXCHANGE] += e->W > 1 ? span(CLK_HDR, CLK_BACK) : 0.0;
+        e->prof_ms[KWOK_T_EXCHANGE] += e->multi ? span(CLK_HDR, CLK_BACK) : 0.0;
         e->prof_ms[KWOK_T_POOL] += pool;
         // what follows the header in the chain (pool, job lists) beyond the stream, and k_emit
         e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2;
@@ -2249,7 +2261,7 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     // multi rank: the previous tick is finished (its long-list allgather, if any,
     // included) before this one's collectives are enqueued, so every rank issues
     // its collectives in the same order whatever its submit / collect pattern
-    if (e->W > 1) drain(e);
+    if (e->multi) drain(e);
     int k = -1;
     for (int pass = 0; pass < 2 && k < 0; pass++)  // prefer keeping the last collected tick's outputs
         for (int i = 0; i < 2 && k < 0; i++)

@@ -61,6 +61,7 @@ struct DevState {
     uint32_t* rel_list;
     uint32_t* list_counts;   // [2]: n_use, n_rel (reset by k_emit)
     int world;
+    int multi;               // FRONT / exchange / BACK ticks (world > 1, or forced for tests)
     int rank;
     const XMsg* xall;        // [world] gathered exchange messages (multi rank)
     uint8_t* arena;
@@ -88,6 +89,7 @@ struct DevState {
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)
+    uint32_t hb_nt;            // heartbeat stores non-temporal (streams larger than the Infinity Cache)
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp

@@ -814,7 +814,7 @@ __device__ __forceinline__ void count_group(const DevState& S, const PodGrp& g, 
             // the Deleted event of a pod we delete: Put if the node is managed and the IP in CIDR
             // (pod_controller.go:329-336).  Single rank: the Put waits in rel_bm, folded in
             // the pool phase after every Use of this tick (Use -> Put)
-            if (S.world == 1) {
+            if (!S.multi) {
                 if (r) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
             } else {
                 wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
@@ -834,7 +834,7 @@ __device__ __forceinline__ void apply_uses(const DevState& S, const PodGrp& g, u
             const uint32_t ip = g.ip[k];
             const uint64_t bit = ip - S.pool.net;
             const bool u = (use >> k) & 1;
-            if (S.world == 1) {
+            if (!S.multi) {
                 if (u) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
             } else {
                 wave_append(u, ip, S.use_list, &S.list_counts[0]);
@@ -1073,9 +1073,15 @@ __device__ __noinline__ void hb_fill_groups_any(const DevState& S, const uint4* 
     for (uint64_t g = g0 + w; g < g1; g += BLOCK / 64) {
         const uint64_t u0 = g * GU + l;
         u32x4* p = dst + u0;
+        if (S.hb_nt) {
 #pragma unroll
-        for (int k = 0; k < 5; k++)
-            if (64u * k + l < GU && u0 + 64u * k < units) p[64 * k] = r[k];
+            for (int k = 0; k < 5; k++)
+                if (64u * k + l < GU && u0 + 64u * k < units) __builtin_nontemporal_store(r[k], p + 64 * k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if (64u * k + l < GU && u0 + 64u * k < units) p[64 * k] = r[k];
+        }
     }
 }
 // groups [g0, g1) of the heartbeat region (units past n_hb slots are not written).
@@ -1101,7 +1107,11 @@ __device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* t
     for (uint64_t g = g0 + w; g < g1; g += BLOCK / 64) {
         const uint64_t u0 = g * HB_GROUP_UNITS + l;
         u32x4* p = dst + u0;
-        if (u0 + 256u < units) {  // a whole group (every group but possibly the last)
+        if (S.hb_nt && u0 + 256u < units) {  // a whole group, non-temporal (S.hb_nt: uniform)
+#pragma unroll
+            for (int k = 0; k < 4; k++) __builtin_nontemporal_store(r[k], p + 64 * k);
+            if (l < HB_GROUP_UNITS - 256u) __builtin_nontemporal_store(r[4], p + 256);
+        } else if (u0 + 256u < units) {  // a whole group (every group but possibly the last)
 #pragma unroll
             for (int k = 0; k < 4; k++) p[64 * k] = r[k];  // plain stores: 7.5 TB/s (tools/micro/fill.hip)
             if (l < HB_GROUP_UNITS - 256u) p[256] = r[4];
@@ -1198,7 +1208,7 @@ __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint
 __device__ __forceinline__ void write_front_header(const DevState& S, const Sums& r, uint32_t n_hb, uint64_t pool_index,
                                                    uint64_t c_p1, bool prof, uint32_t tag) {
     const uint64_t* tot = r.tot;
-    const bool single = S.world == 1;
+    const bool single = !S.multi;
     const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
     uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     clk[CLK_P1_MAX] = c_p1;
@@ -1296,7 +1306,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     if (!have_sums) reduce_records(S, b, 0, l.recs, l.sums);
 
     // ---- pool phase (ticks with Gets or Puts) -------------------------------------
-    const bool single = S.world == 1;
+    const bool single = !S.multi;
     const uint64_t A = single ? l.sums->tot[AG_ALLOC] : xA;
     const uint64_t rel_total = single ? l.sums->tot[AG_REL] : xrel;
     const uint64_t alloc_base = single ? 0 : xbase;
@@ -1427,7 +1437,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ Layout sh_L;
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
-    if (S.world > 1 && !(phases & TICK_XLISTS) &&
+    if (S.multi && !(phases & TICK_XLISTS) &&
         __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return;  // queued behind a tick the host has not finished (long lists): re-launched later
 #define TSTAMP(k)                                                                                         \
@@ -1475,7 +1485,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         if (t == 0 && (phases & TICK_PROF))
             atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (t < 3) sh_mask[t] = 0;
-        const bool single = S.world == 1;
+        const bool single = !S.multi;
         const uint32_t hb_base = S.hb_pre[b];
         // round trip 1, all loads independent: the fill marks, the node states and,
         // speculatively, SPEC_GROUPS pod groups per thread at a static thread ->
@@ -1919,6 +1929,16 @@ struct EmitLds {
 };
 static_assert(sizeof(EmitLds) <= 40960, "four k_emit blocks per CU");
 
+// a 16-byte unit of patch output, non-temporal (written once, read by the host's
+// copy engine): 1M x 10M initial k_emit 1.70 -> 1.62 ms against plain stores
+__device__ __forceinline__ void emit_st(uint8_t* arena, uint64_t off, uint4 v) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifdef EMIT_PLAIN  // A/B builds
+    *reinterpret_cast<u32x4*>(arena + off) = u32x4{v.x, v.y, v.z, v.w};
+#else
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(arena + off));
+#endif
+}
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); }
 
 // 16 bytes at byte offset `off` of a 4-byte aligned source (LDS or global)
@@ -2097,7 +2117,6 @@ __device__ __forceinline__ uint4 emit_unit(const DevState& S, const EmitLds* L, 
 template <bool POD, bool CACHED>
 __device__ __forceinline__ void emit_phase2(const DevState& S, const EmitLds* L, const EmitWave* W, uint32_t cnt,
                                             uint32_t ustart, uint32_t utot) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t l = lane_id();
     EmitSrc E;
     E.lds = reinterpret_cast<const uint8_t*>(L);
@@ -2124,8 +2143,8 @@ __device__ __forceinline__ void emit_phase2(const DevState& S, const EmitLds* L,
         uint64_t da, db;
         const uint4 va = emit_unit<POD, CACHED>(S, L, W, E, ka, (ua - sa) << 4, da);
         const uint4 vb = emit_unit<POD, CACHED>(S, L, W, E, kb, (ub - sb) << 4, db);
-        if (u0 + l < utot) *reinterpret_cast<u32x4*>(S.arena + da) = u32x4{va.x, va.y, va.z, va.w};
-        if (u0 + 64u + l < utot) *reinterpret_cast<u32x4*>(S.arena + db) = u32x4{vb.x, vb.y, vb.z, vb.w};
+        if (u0 + l < utot) emit_st(S.arena, da, va);
+        if (u0 + 64u + l < utot) emit_st(S.arena, db, vb);
     }
 }
 
@@ -2209,7 +2228,6 @@ __device__ __forceinline__ TabStep<UNR> tab_load(const DevState& S, const EmitWa
 }
 template <int G, int UNR>
 __device__ __forceinline__ void tab_store(const DevState& S, const EmitWave* W, const TabStep<UNR>& T) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint8_t* row = W->seg + T.k * VROW_STRIDE;  // biased: row k starts VROW_BIAS bytes in
     uint32_t dor = 0;
 #pragma unroll
@@ -2228,8 +2246,8 @@ __device__ __forceinline__ void tab_store(const DevState& S, const EmitWave* W, 
     for (int i = 0; i < UNR; i++) {
         const uint32_t u = T.u0 + G * i;
         if (u < T.nu)
-            *reinterpret_cast<u32x4*>(S.arena + ((uint64_t)(T.o16 + u) << 4)) =
-                u32x4{T.t[i].x | v[i].x, T.t[i].y | v[i].y, T.t[i].z | v[i].z, T.t[i].w | v[i].w};
+            emit_st(S.arena, (uint64_t)(T.o16 + u) << 4,
+                    make_uint4(T.t[i].x | v[i].x, T.t[i].y | v[i].y, T.t[i].z | v[i].z, T.t[i].w | v[i].w));
     }
 }
 // maxnu: the chunk's largest unit count (wave-uniform)
@@ -2283,7 +2301,6 @@ __device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const Emit
 template <int UNR>
 __device__ __forceinline__ void flat_store(const DevState& S, const EmitWave* W, const FlatStep<UNR>& F, uint64_t o16,
                                            uint32_t g) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t dor = 0;
 #pragma unroll
     for (int i = 0; i < UNR; i++) dor |= F.d[i];
@@ -2300,8 +2317,8 @@ __device__ __forceinline__ void flat_store(const DevState& S, const EmitWave* W,
 #pragma unroll
     for (int i = 0; i < UNR; i++)
         if (F.ok[i])
-            *reinterpret_cast<u32x4*>(S.arena + ((o16 + g + 64u * i) << 4)) =
-                u32x4{F.t[i].x | v[i].x, F.t[i].y | v[i].y, F.t[i].z | v[i].z, F.t[i].w | v[i].w};
+            emit_st(S.arena, (o16 + g + 64u * i) << 4,
+                    make_uint4(F.t[i].x | v[i].x, F.t[i].y | v[i].y, F.t[i].z | v[i].z, F.t[i].w | v[i].w));
 }
 template <int UNR>
 __device__ __forceinline__ void emit_phase2_flat(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t mu) {
@@ -2330,7 +2347,6 @@ constexpr uint32_t INIT_RENDER_MAX = (SRC_PAD_FRONT + 64 * SEG_STRIDE + SRC_PAD_
 template <bool CACHED>
 __device__ __forceinline__ void emit_init_copies(const DevState& S, const EmitLds* L, EmitWave* W, uint32_t cnt,
                                                  uint32_t nu) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t l = lane_id();
     EmitSrc E;
     E.lds = reinterpret_cast<const uint8_t*>(L);
@@ -2348,8 +2364,7 @@ __device__ __forceinline__ void emit_init_copies(const DevState& S, const EmitLd
     uint32_t u = l % nu;
     const uint32_t step = 64u % nu;
     for (uint32_t g = l; g < total; g += 64) {
-        const uint4 v = img[u];
-        *reinterpret_cast<u32x4*>(S.arena + ((o16 + g) << 4)) = u32x4{v.x, v.y, v.z, v.w};
+        emit_st(S.arena, (o16 + g) << 4, img[u]);
         u += step;
         u = u >= nu ? u - nu : u;
     }
@@ -2399,7 +2414,7 @@ __device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_
 
 __global__ __launch_bounds__(EMIT_BLOCK, 4) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
     __shared__ EmitLds L;
-    if (S.world > 1 && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    if (S.multi && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return;  // the tick's launches were skipped (queued behind one the host has not finished)
     const uint32_t n_pp = S.emit_n[0], n_init = S.emit_n[1];
     if (n_pp == 0 && n_init == 0) return;

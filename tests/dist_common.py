@@ -47,9 +47,10 @@ def gloo_allgather_fn():
     return fn
 
 
-def make(cls, rank, world, allgather=None, device=0, big=False):
+def make(cls, rank, world, allgather=None, device=0, big=False, comm_id=None):
     cfg = make_config(cidr=BIG_CIDR if big else CIDR, node_ip="196.168.0.1", buckets=BUCKETS, node_slots_per_bucket=CN,
-                      pod_slots_per_bucket=CP, rank=rank, world_size=world, device=device, allgather=allgather)
+                      pod_slots_per_bucket=CP, rank=rank, world_size=world, device=device, allgather=allgather,
+                      comm_id=comm_id)
     return cls(cfg)
 
 
