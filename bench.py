@@ -389,8 +389,12 @@ def main():
         traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", PMC_FILE)
         if os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK:
-            traffic = json.load(open(pmc))["kernels"]["k_tick"]["hbm_bytes"]
-            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch, same config)" % PMC_FILE
+            ks = json.load(open(pmc))["kernels"]
+            # the default-geometry kernel: "k_tick" (older builds) or "void k_tick<false>"
+            kt = [k for k in ks if k == "k_tick" or k.startswith("void k_tick<false>")]
+            if kt:
+                traffic = ks[kt[0]]["hbm_bytes"]
+                traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch, same config)" % PMC_FILE
         ilc = r0.local_counters
         init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
         emit_ms = ph0["emit_kernel"]
