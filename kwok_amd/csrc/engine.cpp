@@ -1922,12 +1922,17 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     }
     // a long heartbeat stream is shared with the chain blocks once they are done
     // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
-    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env : (nhb * (uint64_t)e->hb_stride >= (32ull << 20) ? 921u : 1024u);
     // a stream that fits the 256 MB Infinity Cache is rewritten from it every tick
     // (plain stores); a larger one (1M nodes: 1.07 GB) is written non-temporally:
     // 239 -> 216 us per 1M x 10M tick (no L2 pollution under the chain's reads,
     // no dirty L2 left for the kernel-end write-back)
-    S.hb_nt = e->nt_env >= 0 ? (uint32_t)e->nt_env : (nhb * (uint64_t)e->hb_stride >= (256ull << 20) ? 1u : 0u);
+    const uint64_t hb_bytes = nhb * (uint64_t)e->hb_stride;
+    S.hb_nt = e->nt_env >= 0 ? (uint32_t)e->nt_env : (hb_bytes >= (256ull << 20) ? 1u : 0u);
+    // the streamers' share: with the non-temporal stream the chain blocks finish
+    // sooner (1M x 10M: classification 172 -> 122 us) and take more of the tail
+    // (tools/share_sweep2.sh: 921 -> 860 /1024, 217 -> 208 us per tick)
+    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
+                                       : (hb_bytes < (32ull << 20) ? 1024u : (S.hb_nt ? 860u : 921u));
     int rc = bind_slot(e, k);
     if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
