@@ -265,6 +265,11 @@ class Handoff:
 
 def main():
     a = parse()
+    # stdout carries exactly one JSON line: libraries that print banners to the C
+    # stdout (RCCL prints "RCCL version ..." at communicator init) go to stderr
+    sys.stdout.flush()
+    json_out = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if REHEARSAL else int(os.environ.get("LOCAL_RANK", "0"))
@@ -283,6 +288,8 @@ def main():
         obj = [keng.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm = obj[0]
+    elif os.environ.get("KWOK_FORCE_MULTI"):  # diagnostics: one rank through FRONT / RCCL exchange / BACK
+        comm = keng.comm_id()
     total_pods = a.nodes_per_rank * world * workload.PODS_PER_NODE
     cidr = cidr_for(total_pods)
     t0 = time.perf_counter()
@@ -455,7 +462,8 @@ def main():
             out["flap"] = flap
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
-        print(json.dumps(out))
+        sys.stdout.flush()
+        os.write(json_out, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
