@@ -1,0 +1,315 @@
+//go:build kwok_mi355x
+
+// engine_cgo.go - the cgo binding of the MI355X engine (include/kwok_engine.h)
+// for pkg/kwok/controllers.  Copy this directory's files into the reference's
+// pkg/kwok/controllers and build with `-tags kwok_mi355x`; libkwok_engine.so
+// and kwok_engine.h are expected under third_party/kwok_amd (INTEGRATION.md).
+//
+// Not compiled in this repository: the image has no Go toolchain.  Every C
+// entry point called here is exercised through the same ABI by the ctypes
+// tests (tests/test_abi.py and the GPU parity tests).
+
+package controllers
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../third_party/kwok_amd/include
+#cgo LDFLAGS: -L${SRCDIR}/../../../third_party/kwok_amd/lib -lkwok_engine -Wl,-rpath,${SRCDIR}/../../../third_party/kwok_amd/lib
+#include <stdlib.h>
+#include "kwok_engine.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+
+	"sigs.k8s.io/kwok/pkg/kwok/controllers/templates"
+)
+
+// output kinds handed to the apply callback of tick
+const (
+	kindHeartbeat = iota
+	kindNodeInit
+	kindPodPatch
+	kindDelete // | 1: the pod has finalizers (kwok_finalizer_patch first)
+)
+
+func boolToC(b bool) C.int32_t {
+	if b {
+		return 1
+	}
+	return 0
+}
+
+type gpuEngine struct {
+	h       *C.kwok_engine
+	hb      []int32 // heartbeat handle list of heartbeat epoch hbEpoch
+	hbEpoch uint32
+}
+
+func (g *gpuEngine) lastError() string { return C.GoString(C.kwok_last_error(g.h)) }
+
+// newGPUEngine replaces the per-object work of NewNodeController /
+// NewPodController (node_controller.go:79-117, pod_controller.go:84-128) for
+// one GPU.  startUnix is the StartTime() template value (controller.go:33).
+func newGPUEngine(conf Config, startUnix int64, rank, world int, commID []byte) (*gpuEngine, error) {
+	cidr, nodeIP := C.CString(conf.CIDR), C.CString(conf.NodeIP)
+	defer C.free(unsafe.Pointer(cidr))
+	defer C.free(unsafe.Pointer(nodeIP))
+	// custom pod status / node initialization / heartbeat templates are compiled by
+	// the engine (KWOK_EDOMAIN with the reason when one does not fit the kernels' programs)
+	var custom C.int32_t
+	podTpl, nodeTpl := C.CString(conf.PodStatusTemplate), C.CString(conf.NodeInitializationTemplate)
+	hbTpl := C.CString(conf.NodeHeartbeatTemplate)
+	defer C.free(unsafe.Pointer(podTpl))
+	defer C.free(unsafe.Pointer(nodeTpl))
+	defer C.free(unsafe.Pointer(hbTpl))
+	if conf.PodStatusTemplate != templates.DefaultPodStatusTemplate {
+		custom |= C.KWOK_TPL_POD
+	}
+	if conf.NodeInitializationTemplate != templates.DefaultNodeStatusTemplate {
+		custom |= C.KWOK_TPL_NODE_INIT
+	}
+	if conf.NodeHeartbeatTemplate != templates.DefaultNodeHeartbeatTemplate {
+		custom |= C.KWOK_TPL_HEARTBEAT
+	}
+	cfg := C.kwok_config{
+		abi_version:             C.KWOK_ABI_VERSION,
+		cidr:                    cidr,
+		node_ip:                 nodeIP,
+		start_time_unix:         C.int64_t(startUnix),
+		enable_cni:              boolToC(conf.EnableCNI), // IPs from cni.Setup: INTEGRATION.md "EnableCNI"
+		custom_templates:        custom,
+		pod_status_template:     podTpl,
+		node_init_template:      nodeTpl,
+		node_heartbeat_template: hbTpl,
+		buckets:                 4096,
+		node_slots_per_bucket:   64,
+		pod_slots_per_bucket:    640,   // initial capacity; a bucket grows when a batch would fill it ...
+		pod_handle_stride:       65528, // ... up to this many pods (e.g. 1000+ pods on one node)
+		max_pod_specs:           4096,
+		rank:                    C.int32_t(rank),
+		world_size:              C.int32_t(world),
+		device:                  C.int32_t(rank),
+	}
+	if world > 1 {
+		if len(commID) != C.KWOK_COMM_ID_BYTES {
+			return nil, fmt.Errorf("kwok: %d ranks need a %d-byte communicator id (kwokCommID on rank 0)", world, C.KWOK_COMM_ID_BYTES)
+		}
+		id := C.CBytes(commID)
+		defer C.free(id)
+		cfg.comm_id = (*C.uint8_t)(id)
+	}
+	var h *C.kwok_engine
+	if rc := C.kwok_engine_create(&cfg, &h); rc != C.KWOK_OK {
+		return nil, fmt.Errorf("kwok_engine_create: %d: %s", int(rc), C.GoString(C.kwok_last_error(nil)))
+	}
+	return &gpuEngine{h: h}, nil
+}
+
+// kwokCommID: the RCCL communicator id rank 0 creates and sends to the other ranks.
+func kwokCommID() ([]byte, error) {
+	buf := make([]byte, C.KWOK_COMM_ID_BYTES)
+	if rc := C.kwok_comm_id((*C.uint8_t)(unsafe.Pointer(&buf[0]))); rc != C.KWOK_OK {
+		return nil, fmt.Errorf("kwok_comm_id: %d", int(rc))
+	}
+	return buf, nil
+}
+
+func (g *gpuEngine) close() {
+	if g.h != nil {
+		C.kwok_engine_destroy(g.h)
+		g.h = nil
+	}
+}
+
+func arenaPtr(arena []byte) *C.char {
+	if len(arena) == 0 {
+		return nil
+	}
+	return (*C.char)(unsafe.Pointer(&arena[0]))
+}
+
+// registerPodSpec: the spec id of a decoded pod's containers / init containers /
+// readiness gates (their strings are kwok_str refs into arena).
+func (g *gpuEngine) registerPodSpec(doc *C.kwok_pod_doc, arena []byte) (int32, error) {
+	spec := C.kwok_pod_spec{
+		containers:        &doc.containers[0],
+		n_containers:      doc.n_containers,
+		init_containers:   &doc.init_containers[0],
+		n_init_containers: doc.n_init_containers,
+		readiness_gates:   &doc.readiness_gates[0],
+		n_readiness_gates: doc.n_readiness_gates,
+	}
+	var id C.int32_t
+	if rc := C.kwok_register_pod_spec(g.h, &spec, arenaPtr(arena), C.size_t(len(arena)), &id); rc != C.KWOK_OK {
+		return -1, fmt.Errorf("kwok_register_pod_spec: %d: %s", int(rc), g.lastError())
+	}
+	return int32(id), nil
+}
+
+// ingestNodes / ingestPods: one batch of watch records in event order; per
+// record the handle and status (KWOK_OK, KWOK_EDOMAIN, ...).
+func (g *gpuEngine) ingestNodes(ev []C.kwok_node_event, arena []byte) (handles, status []int32, err error) {
+	handles, status = make([]int32, len(ev)), make([]int32, len(ev))
+	if len(ev) == 0 {
+		return
+	}
+	rc := C.kwok_ingest_nodes(g.h, &ev[0], C.size_t(len(ev)), arenaPtr(arena), C.size_t(len(arena)),
+		(*C.int32_t)(&handles[0]), (*C.int32_t)(&status[0]))
+	if rc < 0 {
+		err = fmt.Errorf("kwok_ingest_nodes: %d: %s", int(rc), g.lastError())
+	}
+	return
+}
+
+func (g *gpuEngine) ingestPods(ev []C.kwok_pod_event, arena []byte) (handles, status []int32, released []uint32, err error) {
+	handles, status, released = make([]int32, len(ev)), make([]int32, len(ev)), make([]uint32, len(ev))
+	if len(ev) == 0 {
+		return
+	}
+	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(len(ev)), arenaPtr(arena), C.size_t(len(arena)),
+		(*C.int32_t)(&handles[0]), (*C.int32_t)(&status[0]), (*C.uint32_t)(&released[0]))
+	if rc < 0 {
+		err = fmt.Errorf("kwok_ingest_pods: %d: %s", int(rc), g.lastError())
+	}
+	return
+}
+
+// poolPut replicates IPs another rank released at ingest time (multi-GPU).
+func (g *gpuEngine) poolPut(ips []uint32) error {
+	if len(ips) == 0 {
+		return nil
+	}
+	if rc := C.kwok_pool_put(g.h, (*C.uint32_t)(&ips[0]), C.size_t(len(ips))); rc != C.KWOK_OK {
+		return fmt.Errorf("kwok_pool_put: %s", g.lastError())
+	}
+	return nil
+}
+
+func finalizerPatch() []byte {
+	var n C.size_t
+	p := C.kwok_finalizer_patch(&n)
+	return C.GoBytes(unsafe.Pointer(p), C.int(n))
+}
+
+// tick runs one heartbeat interval and hands every body to apply.  The host
+// copy holds ONE heartbeat body (all bodies of a tick are identical,
+// node_controller.go:393-401) and the node-init / pod patch region: a steady
+// tick at 1M nodes moves ~1 KB over PCIe, not 1 GB.  The heartbeat handle
+// list is read only when its epoch changed.  The body slices stay valid after
+// tick returns (they alias one Go buffer).
+func (g *gpuEngine) tick(nowUnix int64, apply func(kind int, handle int32, body []byte)) error {
+	var res C.kwok_tick_result
+	if rc := C.kwok_tick(g.h, C.int64_t(nowUnix), &res); rc != C.KWOK_OK {
+		return fmt.Errorf("kwok_tick: %s", g.lastError())
+	}
+	newEpoch := g.hb == nil || uint32(res.heartbeat_epoch) != g.hbEpoch
+	if newEpoch {
+		g.hb = make([]int32, res.n_heartbeat) // filled by kwok_read_outputs below
+	}
+	ini := make([]int32, res.n_node_init)
+	iniOff := make([]uint64, res.n_node_init)
+	iniLen := make([]uint32, res.n_node_init)
+	pp := make([]int32, res.n_pod_patch)
+	ppOff := make([]uint64, res.n_pod_patch)
+	ppLen := make([]uint32, res.n_pod_patch)
+	del := make([]int32, res.n_delete)
+	delFin := make([]uint8, res.n_delete)
+	need := uint64(res.arena_bytes)
+	if res.n_heartbeat > 1 {
+		need -= uint64(res.n_heartbeat-1) * uint64(res.heartbeat_stride)
+	}
+	arena := C.malloc(C.size_t(need) + 1) // C memory: the engine copies into it
+	defer C.free(arena)
+	out := C.kwok_outputs{arena: (*C.uint8_t)(arena), arena_cap: C.uint64_t(need), flags: C.KWOK_READ_HEARTBEAT_ONCE}
+	if len(g.hb) > 0 && newEpoch {
+		out.heartbeat_nodes = (*C.int32_t)(&g.hb[0])
+	}
+	if len(ini) > 0 {
+		out.node_init_nodes, out.node_init_off, out.node_init_len =
+			(*C.int32_t)(&ini[0]), (*C.uint64_t)(&iniOff[0]), (*C.uint32_t)(&iniLen[0])
+	}
+	if len(pp) > 0 {
+		out.pod_patch_pods, out.pod_patch_off, out.pod_patch_len =
+			(*C.int32_t)(&pp[0]), (*C.uint64_t)(&ppOff[0]), (*C.uint32_t)(&ppLen[0])
+	}
+	if len(del) > 0 {
+		out.delete_pods, out.delete_has_finalizers = (*C.int32_t)(&del[0]), (*C.uint8_t)(&delFin[0])
+	}
+	if rc := C.kwok_read_outputs(g.h, &out); rc != C.KWOK_OK {
+		return fmt.Errorf("kwok_read_outputs: %s", g.lastError())
+	}
+	g.hbEpoch = uint32(res.heartbeat_epoch)
+	buf := C.GoBytes(arena, C.int(out.arena_copied))
+	shift := uint64(out.arena_shift)
+	if res.n_heartbeat > 0 {
+		body := buf[:res.heartbeat_len] // the heartbeat body, sent to every managed node
+		for _, h := range g.hb {
+			apply(kindHeartbeat, h, body)
+		}
+	}
+	for i, h := range ini {
+		apply(kindNodeInit, h, buf[iniOff[i]-shift:iniOff[i]-shift+uint64(iniLen[i])])
+	}
+	for i, h := range pp {
+		apply(kindPodPatch, h, buf[ppOff[i]-shift:ppOff[i]-shift+uint64(ppLen[i])])
+	}
+	for i, h := range del { // Patch(removeFinalizers) if delFin[i], then Delete(grace 0)
+		apply(kindDelete|int(delFin[i]), h, nil)
+	}
+	return nil
+}
+
+// ---- host codec: watch objects as JSON -> records (kwok_decode_*) ----------
+
+type gpuCodec struct{ c *C.kwok_codec }
+
+func newGPUCodec(conf Config) (*gpuCodec, error) {
+	cs := []*C.char{
+		C.CString(conf.ManageNodesWithAnnotationSelector), C.CString(conf.ManageNodesWithLabelSelector),
+		C.CString(conf.DisregardStatusWithAnnotationSelector), C.CString(conf.DisregardStatusWithLabelSelector),
+	}
+	defer func() {
+		for _, p := range cs {
+			C.free(unsafe.Pointer(p))
+		}
+	}()
+	cfg := C.kwok_codec_config{
+		manage_all_nodes:                          boolToC(conf.ManageAllNodes),
+		manage_nodes_with_annotation_selector:     cs[0],
+		manage_nodes_with_label_selector:          cs[1],
+		disregard_status_with_annotation_selector: cs[2],
+		disregard_status_with_label_selector:      cs[3],
+	}
+	var c *C.kwok_codec
+	if rc := C.kwok_codec_create(&cfg, &c); rc != C.KWOK_OK { // labels.Parse errors surface here
+		return nil, fmt.Errorf("kwok_codec_create: %s", C.GoString(C.kwok_codec_last_error()))
+	}
+	return &gpuCodec{c: c}, nil
+}
+
+func (d *gpuCodec) close() { C.kwok_codec_destroy(d.c) }
+
+// decodeNodes / decodePods: objects at offs[i] / lens[i] of arena (their JSON,
+// concatenated) -> records whose strings point into the same arena (node status
+// blobs are re-serialised in place).  status[i] != KWOK_OK: outside the domain.
+func (d *gpuCodec) decodeNodes(arena []byte, offs []uint64, lens []uint32, threads int) ([]C.kwok_node_event, []int32) {
+	ev, st := make([]C.kwok_node_event, len(offs)), make([]int32, len(offs))
+	if len(offs) > 0 {
+		C.kwok_decode_nodes(d.c, arenaPtr(arena), C.size_t(len(arena)), (*C.uint64_t)(&offs[0]),
+			(*C.uint32_t)(&lens[0]), C.size_t(len(offs)), C.int(threads), &ev[0], (*C.int32_t)(&st[0]))
+	}
+	return ev, st
+}
+
+func (d *gpuCodec) decodePods(arena []byte, offs []uint64, lens []uint32, threads int) ([]C.kwok_pod_doc, []int32) {
+	docs, st := make([]C.kwok_pod_doc, len(offs)), make([]int32, len(offs))
+	if len(offs) > 0 {
+		C.kwok_decode_pods(d.c, arenaPtr(arena), C.size_t(len(arena)), (*C.uint64_t)(&offs[0]),
+			(*C.uint32_t)(&lens[0]), C.size_t(len(offs)), C.int(threads), &docs[0], (*C.int32_t)(&st[0]))
+	}
+	return docs, st
+}
+
+func str(arena []byte, s C.kwok_str) string { return string(arena[s.off : s.off+s.len]) }

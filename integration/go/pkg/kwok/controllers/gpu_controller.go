@@ -1,0 +1,367 @@
+//go:build kwok_mi355x
+
+// gpu_controller.go - the client-go side of the drop-in: watch events are
+// batched as object JSON, decoded by the engine's host codec and ingested
+// before each tick; every body the tick returns is applied through the
+// clientset with the reference's 16-wide task pools (utils.go:119-161).
+// NewController builds this in place of NodeController + PodController when
+// the package is built with -tags kwok_mi355x (controller_mi355x.go).
+//
+// Not compiled in this repository (no Go toolchain in the image).
+
+package controllers
+
+/*
+#include "kwok_engine.h"
+*/
+import "C"
+
+import (
+	"context"
+	"encoding/json"
+	"fmt"
+	"runtime"
+	"sync"
+	"time"
+
+	corev1 "k8s.io/api/core/v1"
+	apierrors "k8s.io/apimachinery/pkg/api/errors"
+	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
+	"k8s.io/apimachinery/pkg/types"
+	"k8s.io/apimachinery/pkg/watch"
+
+	"sigs.k8s.io/kwok/pkg/log"
+)
+
+// objBatch: watch objects since the last tick, as concatenated JSON
+type objBatch struct {
+	arena []byte
+	offs  []uint64
+	lens  []uint32
+	del   []bool
+	uids  []types.UID
+}
+
+func (b *objBatch) add(obj interface{}, uid types.UID, deleted bool) error {
+	raw, err := json.Marshal(obj)
+	if err != nil {
+		return err
+	}
+	b.offs = append(b.offs, uint64(len(b.arena)))
+	b.lens = append(b.lens, uint32(len(raw)))
+	b.arena = append(b.arena, raw...)
+	b.del = append(b.del, deleted)
+	b.uids = append(b.uids, uid)
+	return nil
+}
+
+// GPUController: one engine (one GPU) behind the reference's Controller API.
+type GPUController struct {
+	conf      Config
+	eng       *gpuEngine
+	codec     *gpuCodec
+	interval  time.Duration
+	finalizer []byte
+
+	mu    sync.Mutex // guards the batches (watch goroutines append, the tick loop swaps)
+	nodes objBatch
+	pods  objBatch
+
+	// tick loop only
+	nodeName map[int32]string // node handle -> name
+	podByUID map[types.UID]int32
+	podRef   map[int32]types.NamespacedName
+}
+
+func newGPUController(conf Config, interval time.Duration) (*GPUController, error) {
+	st, err := time.Parse(time.RFC3339, startTime) // the StartTime() value (controller.go:33)
+	if err != nil {
+		return nil, err
+	}
+	eng, err := newGPUEngine(conf, st.Unix(), 0, 1, nil)
+	if err != nil {
+		return nil, err
+	}
+	codec, err := newGPUCodec(conf)
+	if err != nil {
+		eng.close()
+		return nil, err
+	}
+	return &GPUController{
+		conf: conf, eng: eng, codec: codec, interval: interval, finalizer: finalizerPatch(),
+		nodeName: map[int32]string{}, podByUID: map[types.UID]int32{}, podRef: map[int32]types.NamespacedName{},
+	}, nil
+}
+
+// Start: the node and pod watches of NodeController.Start / PodController.Start
+// (node_controller.go:119-143, pod_controller.go:130-153) feed the batches; the
+// tick loop replaces KeepNodeHeartbeat, LockNodes, LockPods and DeletePods.
+func (c *GPUController) Start(ctx context.Context) error {
+	nodeOpt := metav1.ListOptions{LabelSelector: c.conf.ManageNodesWithLabelSelector}
+	podOpt := metav1.ListOptions{FieldSelector: podFieldSelector}
+	if err := c.watch(ctx, true, nodeOpt); err != nil {
+		return fmt.Errorf("failed to watch nodes: %w", err)
+	}
+	if err := c.watch(ctx, false, podOpt); err != nil {
+		return fmt.Errorf("failed to watch pods: %w", err)
+	}
+	go c.loop(ctx)
+	return nil
+}
+
+// watch from the current state (a watch without resourceVersion first sends an
+// Added event per existing object, as ListNodes / ListPods would), re-opened
+// when the server closes it, like WatchNodes / WatchPods
+func (c *GPUController) watch(ctx context.Context, nodes bool, opt metav1.ListOptions) error {
+	open := func() (watch.Interface, error) {
+		if nodes {
+			return c.conf.ClientSet.CoreV1().Nodes().Watch(ctx, opt)
+		}
+		return c.conf.ClientSet.CoreV1().Pods(corev1.NamespaceAll).Watch(ctx, opt)
+	}
+	w, err := open()
+	if err != nil {
+		return err
+	}
+	logger := log.FromContext(ctx)
+	go func() {
+		rc := w.ResultChan()
+		for {
+			select {
+			case <-ctx.Done():
+				w.Stop()
+				return
+			case ev, ok := <-rc:
+				if !ok {
+					for {
+						if w, err = open(); err == nil {
+							rc = w.ResultChan()
+							break
+						}
+						logger.Error("Failed to re-watch", err)
+						select {
+						case <-ctx.Done():
+							return
+						case <-time.After(time.Second * 5):
+						}
+					}
+					continue
+				}
+				c.onEvent(ctx, nodes, ev)
+			}
+		}
+	}()
+	return nil
+}
+
+func (c *GPUController) onEvent(ctx context.Context, nodes bool, ev watch.Event) {
+	if ev.Type != watch.Added && ev.Type != watch.Modified && ev.Type != watch.Deleted {
+		return
+	}
+	var err error
+	c.mu.Lock()
+	switch obj := ev.Object.(type) {
+	case *corev1.Node:
+		if nodes {
+			err = c.nodes.add(obj, obj.UID, ev.Type == watch.Deleted)
+		}
+	case *corev1.Pod:
+		if !nodes {
+			err = c.pods.add(obj, obj.UID, ev.Type == watch.Deleted)
+		}
+	}
+	c.mu.Unlock()
+	if err != nil {
+		log.FromContext(ctx).Error("Failed to encode watch object", err)
+	}
+}
+
+func (c *GPUController) loop(ctx context.Context) {
+	logger := log.FromContext(ctx)
+	tasks := newParallelTasks(16) // the reference's heartbeat / lock / delete parallelism
+	t := time.NewTimer(c.interval)
+	defer func() {
+		t.Stop()
+		tasks.Wait()
+		c.codec.close()
+		c.eng.close()
+	}()
+	for {
+		select {
+		case <-ctx.Done():
+			return
+		case <-t.C:
+			start := time.Now()
+			n, err := c.step(ctx, tasks, start.Unix())
+			tasks.Wait()
+			if err != nil {
+				logger.Error("Failed to tick", err)
+			}
+			logger.Info("Tick", "bodies", n, "elapsed", time.Since(start))
+			t.Reset(c.interval)
+		}
+	}
+}
+
+// step: ingest the batches (nodes first, so new pods find their node), run the
+// tick, hand every body to the task pool
+func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int64) (int, error) {
+	c.mu.Lock()
+	nb, pb := c.nodes, c.pods
+	c.nodes, c.pods = objBatch{}, objBatch{}
+	c.mu.Unlock()
+	if err := c.flushNodes(ctx, nb); err != nil {
+		return 0, err
+	}
+	if err := c.flushPods(ctx, pb); err != nil {
+		return 0, err
+	}
+	logger := log.FromContext(ctx)
+	nodesAPI := c.conf.ClientSet.CoreV1().Nodes()
+	var gone []int32
+	n := 0
+	err := c.eng.tick(now, func(kind int, h int32, body []byte) {
+		n++
+		switch kind {
+		case kindHeartbeat, kindNodeInit: // configureHeartbeatNode / configureNode bodies
+			name := c.nodeName[h]
+			tasks.Add(func() {
+				if _, err := nodesAPI.PatchStatus(ctx, name, body); err != nil {
+					logger.Error("Failed to patch node status", err, "node", name)
+				}
+			})
+		case kindPodPatch: // LockPod (pod_controller.go:205-231)
+			ref := c.podRef[h]
+			tasks.Add(func() {
+				_, err := c.conf.ClientSet.CoreV1().Pods(ref.Namespace).Patch(ctx, ref.Name,
+					types.StrategicMergePatchType, body, metav1.PatchOptions{}, "status")
+				if err != nil && !apierrors.IsNotFound(err) {
+					logger.Error("Failed to lock pod", err, "pod", ref.String())
+				}
+			})
+		default: // DeletePod (pod_controller.go:155-183); the engine freed the handle
+			ref, fin := c.podRef[h], kind&1 != 0
+			gone = append(gone, h)
+			tasks.Add(func() {
+				pods := c.conf.ClientSet.CoreV1().Pods(ref.Namespace)
+				if fin {
+					if _, err := pods.Patch(ctx, ref.Name, types.MergePatchType, c.finalizer, metav1.PatchOptions{}); err != nil {
+						if !apierrors.IsNotFound(err) {
+							logger.Error("Failed to patch pod finalizers", err, "pod", ref.String())
+						}
+						return
+					}
+				}
+				if err := pods.Delete(ctx, ref.Name, deleteOpt); err != nil && !apierrors.IsNotFound(err) {
+					logger.Error("Failed to delete pod", err, "pod", ref.String())
+				}
+			})
+		}
+	})
+	for _, h := range gone { // the later Deleted watch event finds no handle and is dropped
+		for uid, hh := range c.podByUID {
+			if hh == h {
+				delete(c.podByUID, uid)
+				break
+			}
+		}
+		delete(c.podRef, h)
+	}
+	return n, err
+}
+
+func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
+	if len(b.offs) == 0 {
+		return nil
+	}
+	logger := log.FromContext(ctx)
+	ev, st := c.codec.decodeNodes(b.arena, b.offs, b.lens, runtime.NumCPU())
+	keep := make([]C.kwok_node_event, 0, len(ev))
+	names := make([]string, 0, len(ev))
+	for i := range ev {
+		if st[i] != C.KWOK_OK { // outside the engine's domain: not simulated (DESIGN.md §2)
+			logger.Warn("Node outside the supported domain", fmt.Errorf("kwok status %d", st[i]))
+			continue
+		}
+		ev[i].op = C.KWOK_OP_UPSERT
+		if b.del[i] {
+			ev[i].op = C.KWOK_OP_DELETE
+		}
+		keep = append(keep, ev[i])
+		names = append(names, str(b.arena, ev[i].name))
+	}
+	hs, ss, err := c.eng.ingestNodes(keep, b.arena)
+	if err != nil {
+		return err
+	}
+	for i := range keep {
+		if ss[i] != C.KWOK_OK {
+			continue
+		}
+		if keep[i].op == C.KWOK_OP_DELETE {
+			delete(c.nodeName, hs[i])
+		} else {
+			c.nodeName[hs[i]] = names[i]
+		}
+	}
+	return nil
+}
+
+func (c *GPUController) flushPods(ctx context.Context, b objBatch) error {
+	if len(b.offs) == 0 {
+		return nil
+	}
+	logger := log.FromContext(ctx)
+	docs, st := c.codec.decodePods(b.arena, b.offs, b.lens, runtime.NumCPU())
+	evs := make([]C.kwok_pod_event, 0, len(docs))
+	uids := make([]types.UID, 0, len(docs))
+	refs := make([]types.NamespacedName, 0, len(docs))
+	for i := range docs {
+		if st[i] != C.KWOK_OK {
+			logger.Warn("Pod outside the supported domain", fmt.Errorf("kwok status %d", st[i]))
+			continue
+		}
+		d := &docs[i]
+		h, known := c.podByUID[b.uids[i]]
+		if b.del[i] {
+			if !known { // never ingested, or already deleted by the engine
+				continue
+			}
+			d.ev.op = C.KWOK_OP_DELETE // releases status.podIP (pod_controller.go:329-336)
+			d.ev.handle = C.int32_t(h)
+		} else {
+			id, err := c.eng.registerPodSpec(d, b.arena)
+			if err != nil {
+				logger.Warn("Pod spec outside the supported domain", err)
+				continue
+			}
+			d.ev.op = C.KWOK_OP_UPSERT
+			d.ev.handle = -1
+			if known {
+				d.ev.handle = C.int32_t(h)
+			}
+			d.ev.spec_id = C.int32_t(id)
+			d.ev.node_handle = -1
+		}
+		evs = append(evs, d.ev)
+		uids = append(uids, b.uids[i])
+		refs = append(refs, types.NamespacedName{Namespace: str(b.arena, d.namespace_), Name: str(b.arena, d.name)})
+	}
+	hs, ss, _, err := c.eng.ingestPods(evs, b.arena)
+	if err != nil {
+		return err
+	}
+	for i := range evs {
+		if ss[i] != C.KWOK_OK {
+			continue
+		}
+		if evs[i].op == C.KWOK_OP_DELETE {
+			delete(c.podByUID, uids[i])
+			delete(c.podRef, hs[i])
+		} else {
+			c.podByUID[uids[i]] = hs[i]
+			c.podRef[hs[i]] = refs[i]
+		}
+	}
+	return nil
+}
