@@ -2155,16 +2155,34 @@ struct TabJob {
     Ts ts;
     IpStr h, p;
 };
-__device__ __forceinline__ TabJob emit_job_tab(const DevState& S, uint32_t q, uint32_t n) {
+// a job's records (loaded one chunk ahead) and the lane's last spec descriptor
+struct JobRaw {
+    uint4 j;  // podIP (0: no status section), hostIP, creationTimestamp, spec
+    uint64_t off;
+    uint32_t len;
+};
+__device__ __forceinline__ JobRaw job_raw(const DevState& S, uint64_t q, uint32_t n) {
+    JobRaw R;
+    R.j = make_uint4(0u, 0u, 0u, 0u), R.off = 0, R.len = 0;
+    if (q < n) R.j = S.pp_job[q], R.off = S.pp_off[q], R.len = S.pp_len[q];
+    return R;
+}
+struct SpecCache {
+    uint32_t id, tab_off, max_len;
+};
+__device__ __forceinline__ TabJob emit_job_tab(const DevState& S, const JobRaw& R, bool live, SpecCache& sc) {
     TabJob J;
     J.o16 = J.tb = J.nu = J.mu = 0;
     J.ok = true;
     J.h.lo = J.h.hi = J.p.lo = J.p.hi = 0;
     J.ts.w0 = J.ts.w1 = J.ts.w2 = 0;
-    if (q < n) {
-        const uint4 j = S.pp_job[q];  // podIP (0: no status section), hostIP, creationTimestamp, spec
-        const SpecDesc sd = S.specs[j.w];
-        J.ok = sd.tab_off != NO_TAB;
+    if (live) {
+        const uint4 j = R.j;
+        if (j.w != sc.id) {  // usually every job of a wave shares one spec: one load per lane
+            const SpecDesc& sd = S.specs[j.w];
+            sc.id = j.w, sc.tab_off = sd.tab_off, sc.max_len = sd.max_len;
+        }
+        J.ok = sc.tab_off != NO_TAB;
         J.ts = format_ts(j.z);
         uint32_t shape = 0;
         if (j.y != 0) {  // `{{ with .status }}`: hostIP / podIP (pod.status.tpl:44-47)
@@ -2172,10 +2190,10 @@ __device__ __forceinline__ TabJob emit_job_tab(const DevState& S, uint32_t q, ui
             J.p = format_ip(j.x);
             shape = emit_shape(J.h.len, J.p.len);
         }
-        J.mu = (uint32_t)sd.max_len >> 4;
-        J.tb = sd.tab_off + shape * J.mu;
-        J.o16 = (uint32_t)(S.pp_off[q] >> 4);
-        J.nu = (S.pp_len[q] + 15u) >> 4;
+        J.mu = sc.max_len >> 4;
+        J.tb = sc.tab_off + shape * J.mu;
+        J.o16 = (uint32_t)(R.off >> 4);
+        J.nu = (R.len + 15u) >> 4;
     }
     return J;
 }
@@ -2373,10 +2391,15 @@ __device__ __forceinline__ void emit_init_copies(const DevState& S, const EmitLd
 template <bool POD, bool CACHED>
 __device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_t w0, uint32_t nw, uint32_t n) {
     EmitWave* W = &L->w[wave_id()];
+    SpecCache sc{0xFFFFFFFFu, NO_TAB, 0u};
+    JobRaw nxt;
+    if (POD) nxt = job_raw(S, (uint64_t)w0 * 64u + lane_id(), n);
     for (uint32_t ch = w0; ch * 64u < n; ch += nw) {
         const uint32_t cnt = min(64u, n - ch * 64u);
         if (POD) {
-            const TabJob J = emit_job_tab(S, ch * 64u + lane_id(), n);
+            const JobRaw cur = nxt;
+            nxt = job_raw(S, (uint64_t)(ch + nw) * 64u + lane_id(), n);  // the wave's next chunk, in flight
+            const TabJob J = emit_job_tab(S, cur, ch * 64u + lane_id() < n, sc);
             if (__ballot(!J.ok) == 0) {  // every job of the chunk has tables
                 emit_row_tab(W, J);
                 uint32_t mx = J.nu;
