@@ -2050,7 +2050,9 @@ bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && !e->m
 void trace_tick(kwok_engine* e) {
     const size_t G = e->S.n_chain, N = G + e->n_stream;
     static const int skip = getenv("KWOK_TICK_TRACE_SKIP") ? atoi(getenv("KWOK_TICK_TRACE_SKIP")) : 5;
+    static const uint64_t only = getenv("KWOK_TICK_TRACE_COUNT") ? strtoull(getenv("KWOK_TICK_TRACE_COUNT"), nullptr, 10) : 0;
     if ((int)++e->trace_seen <= skip) return;  // skip the initial (bulk) ticks
+    if (only && e->trace_ticks >= only) return;  // KWOK_TICK_TRACE_COUNT: summarise only the first traced ticks
     const size_t TS = TRACE_SLOTS;
     e->trace_h.assign(N * TS, 0);
     if (release_for_host(e) || hipMemcpyAsync(e->trace_h.data(), e->S.trace, N * TS * 8, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
