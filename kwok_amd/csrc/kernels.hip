@@ -960,8 +960,15 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
 }
 
 // pod chunk c: the block's live groups [c*256, c*256 + 256)
+constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs x (record + offset)
+// A thread's jobs take consecutive ordinals (thread-major canonical order), so a
+// wave's jobs are one contiguous ordinal range: their 16-byte k_emit records and
+// 8-byte arena offsets are staged in LDS (`stage`, 12 KiB per wave: up to 512
+// jobs) and written out as whole rows instead of one cache line per lane per
+// pod (the initial 1M x 10M tick's job stores: ~270 of its ~510 us of pod
+// emission).
 __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
-                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L) {
+                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, uint32_t* stage) {
     PodGrp g;
     load_group(S, gpre, bk0, nbk, ng, c * BLOCK + threadIdx.x, g);
     uint16_t sp[POD_PER_THREAD];
@@ -983,6 +990,9 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0;
     const uint64_t chunk_bytes = L.pod_base + run.v[AG_PP_BYTES];
     uint32_t jl = v[1];
+    const uint32_t wpre = (uint32_t)__shfl((int)v[1], 0);  // the wave's first job (block-chunk relative)
+    uint4* stg = reinterpret_cast<uint4*>(stage + (threadIdx.x >> 6) * POD_STAGE_WORDS);
+    uint64_t* stg_off = reinterpret_cast<uint64_t*>(stg + 512);
     bool dirty = false;
     uint16_t nst[POD_PER_THREAD];
 #pragma unroll
@@ -1015,9 +1025,9 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
                 const SpecDesc& sd = S.specs[sp[k]];
                 const uint32_t len = sd.len_a + sd.len_b + sd.len_c + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
                 S.pp_pods[ord] = handle;
-                S.pp_off[ord] = chunk_bytes + v[2];
+                stg_off[jl - wpre] = chunk_bytes + v[2];
                 S.pp_len[ord] = len;
-                S.pp_job[ord] = make_uint4(stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]);  // the bytes: k_emit
+                stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]);  // the bytes: k_emit
                 jl++;
                 v[2] += sd.max_len;
                 // the apiserver applied the patch
@@ -1028,6 +1038,12 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
         }
         dirty |= s != g.st(k);
         nst[k] = s;
+    }
+    {  // the wave's staged records -> pp_job[run + wpre, run + wend)
+        const uint32_t wend = (uint32_t)__shfl((int)jl, 63);
+        uint4* dst = S.pp_job + run.v[AG_PP] + wpre;
+        uint64_t* dst_off = S.pp_off + run.v[AG_PP] + wpre;
+        for (uint32_t i = lane_id(); i < wend - wpre; i += 64) dst[i] = stg[i], dst_off[i] = stg_off[i];
     }
     if (g.slot != ~0u && dirty) {
         uint4 o;
@@ -1398,7 +1414,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     const uint32_t ng = l.gpre[nbk];
     for (uint64_t m = pod_mask; m; m &= m - 1) {
         const uint32_t c = (uint32_t)__builtin_ctzll(m);
-        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L);
+        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.recs);
     }
     TSTAMP(6);
 #undef TSTAMP
@@ -1428,7 +1444,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                                                    uint32_t n_hb, int phases, uint32_t tag, uint64_t arrive_target) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
-    __shared__ uint32_t recs[MAX_CHAIN * REC_PITCH];  // reduce_records
+    // reduce_records; then emit_pod_chunk's staging (two k_tick blocks per CU still fit)
+    __shared__ uint32_t recs[MAX_CHAIN * REC_PITCH > (BLOCK / 64) * POD_STAGE_WORDS ? MAX_CHAIN * REC_PITCH
+                                                                                   : (BLOCK / 64) * POD_STAGE_WORDS];
     __shared__ uint4 hb_tmpl4[HB_MAX_UNITS];
     __shared__ uint32_t nflags32[NODE_LDS / 4];
     __shared__ uint32_t gpre[MAX_BPB + 1];
