@@ -24,7 +24,7 @@ SPECS = [([("fake-pod", "fake")], [], []),
          ([], [("i0", "registry.k8s.io/pause:3.9"), ("i1", "busybox:1.36")], ["g.io/a", "g.io/b"])]
 
 
-@pytest.mark.parametrize("name", ["pod_a.tpl", "pod_b.tpl"])
+@pytest.mark.parametrize("name", ["pod_a.tpl", "pod_b.tpl", "pod_c.tpl"])
 def test_custom_pod_template_engine(name):
     text = tpl(name)
     kw = dict(cidr="10.0.0.1/16", node_ip="196.168.0.1", buckets=256, node_slots_per_bucket=16,

@@ -113,7 +113,7 @@ def test_reference_pod_template_compiles_to_the_default_program():
             assert got == expected_patch(text, cs, ics, gates, START - 60 - k, hip, pip, ne), (k, hip, ne)
 
 
-@pytest.mark.parametrize("name", ["pod_a.tpl", "pod_b.tpl"])
+@pytest.mark.parametrize("name", ["pod_a.tpl", "pod_b.tpl", "pod_c.tpl"])
 def test_custom_pod_templates_compile_and_match_gotmpl(name):
     text = tpl(name)
     for k, (cs, ics, gates) in enumerate(random_specs(3, 30)):
