@@ -164,7 +164,9 @@ struct kwok_engine {
     // run on their own host threads with no shared writes.  Slot policy, op
     // coalescing and event order are per bucket, so results do not depend on
     // n_part.
-    struct Stage {
+    // one cache-line pair per partition: every staged op moves a vector's end
+    // pointer, and partitions run on different threads
+    struct alignas(128) Stage {
         std::vector<NodeOp> nops;
         std::vector<PodOp> pops;
         std::vector<uint32_t> puts;         // ingest-time Puts (Deleted events)
@@ -178,9 +180,10 @@ struct kwok_engine {
     uint32_t gen = 1;  // ops of the unflushed batch carry stamp == gen (flush_ops advances it)
     // threaded-ingest scratch, kept between calls (fresh allocations would page-fault
     // on first touch, from every thread at once)
-    std::vector<uint32_t> ing_bkt;
     std::vector<uint64_t> ing_res;
-    std::vector<std::vector<uint32_t>> ing_order;  // [n_part]
+    // pod records, validated and parsed in batch order (PodPrep, below), grouped by
+    // partition, then by bucket inside each partition
+    std::vector<unsigned char> ing_prep, ing_sorted;
     Stage& stage_of(uint32_t bucket_local) { return stage[(size_t)((uint64_t)bucket_local * n_part / nb)]; }
     void* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -389,6 +392,23 @@ void run_parts(kwok_engine* e, bool parallel, F&& f) {
 }
 constexpr size_t PAR_MIN = 32768;  // records (or deletes) per call before the partitions get threads
 constexpr size_t NODE_PAR_MIN = 2048;  // node records (the per-record work is heavier)
+
+// A pod record after the checks that depend only on the record itself (arena
+// bounds, IP strings, spec id, phase, creation time), done once in batch order
+// with sequential reads of the records and their strings.  The threaded ingest
+// groups these by partition and bucket, so the slot-policy pass reads them in
+// order instead of gathering the caller's records from all over the batch.
+struct PodPrep {
+    uint32_t idx, bkt;      // record index; owned local bucket (NO_BUCKET: the record changes no slot)
+    int32_t handle, node_handle, spec_id;
+    uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: pip = the parsed podIP
+    uint32_t ctime;
+    uint8_t op, phase, flags, chk;  // chk: PREP_*
+    int32_t fst;            // UPSERT: the first failing field check (KWOK_OK: none)
+    kwok_str node_name;
+};
+enum : uint8_t { PREP_ARENA_BAD = 1, PREP_DEL_IP = 2 };
+constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 
 // ---- per-batch op coalescing: ops for the same slot compose in order ----
 void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
@@ -1507,35 +1527,58 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
-    // The bucket (owned, local) whose slots a record changes, or -1 when it changes
-    // nothing but its own out_status (it is rejected).  A record's partition
-    // processes it; records of one bucket keep their batch order.
-    auto bucket_of_record = [&](const kwok_pod_event& x) -> int64_t {
-        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) return -1;
+    const size_t n_specs = e->specs_h.size();
+    // The record-local checks and parses (batch order), and the bucket (owned,
+    // local) whose slots the record changes, or NO_BUCKET when it changes nothing
+    // but its own out_status (it is rejected).  A record's partition processes
+    // it; records of one bucket keep their batch order.
+    auto prep = [&](size_t i, PodPrep& r) {
+        const kwok_pod_event& x = ev[i];
+        r.idx = (uint32_t)i;
+        r.handle = x.handle, r.node_handle = x.node_handle, r.spec_id = x.spec_id;
+        r.op = x.op, r.phase = x.phase, r.flags = x.flags, r.chk = 0;
+        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK;
+        r.node_name = x.node_name;
+        r.bkt = NO_BUCKET;
+        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
+            r.chk = PREP_ARENA_BAD;
+            return;
+        }
+        if (x.op == KWOK_OP_DELETE) {
+            uint32_t ip = 0;
+            if (x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip)) r.pip = ip, r.chk |= PREP_DEL_IP;
+        } else if (x.op == KWOK_OP_UPSERT) {
+            if (parse_opt_ip(arena, x.host_ip, &r.hip) || parse_opt_ip(arena, x.pod_ip, &r.pip)) r.fst = KWOK_EDOMAIN;
+            else if (x.spec_id < 0 || (size_t)x.spec_id >= n_specs) r.fst = KWOK_EINVAL;
+            else if (x.phase > KWOK_PHASE_UNKNOWN) r.fst = KWOK_EINVAL;
+            else if (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll) r.fst = KWOK_EDOMAIN;
+            else r.ctime = (uint32_t)x.creation_unix;
+        }
         if (x.handle >= 0) {
             uint32_t sl = 0;
-            return e->pod_slot(x.handle, &sl) == KWOK_OK ? (int64_t)(sl / e->Cp) : -1;
+            if (e->pod_slot(x.handle, &sl) == KWOK_OK) r.bkt = sl / e->Cp;
+            return;
         }
-        if (x.op != KWOK_OP_UPSERT) return -1;
+        if (x.op != KWOK_OP_UPSERT) return;
         if (x.node_handle >= 0) {
             const int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
-            return l >= 0 && l < (int64_t)e->NL ? l / e->Cn : -1;
+            if (l >= 0 && l < (int64_t)e->NL) r.bkt = (uint32_t)(l / e->Cn);
+            return;
         }
-        if (!x.node_name.len || x.node_name.len > 253) return -1;
+        if (!x.node_name.len || x.node_name.len > 253) return;
         const uint32_t b = fnv1a32(arena + x.node_name.off, x.node_name.len) & (e->B - 1);
-        return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
+        if (e->owns(b)) r.bkt = b - e->b_lo;
     };
     // WatchPods / ListPods event switch (pod_controller.go:301-343) for one record
     struct Res {
         int32_t handle, st;
         uint32_t released;
     };
-    auto ingest_one = [&](size_t i, kwok_engine::Stage& g) -> Res {
-        const kwok_pod_event& x = ev[i];
+    auto ingest_one = [&](const PodPrep& x, kwok_engine::Stage& g) -> Res {
         int st = KWOK_OK;
         int32_t handle = -1;
         uint32_t released = 0;
-        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) st = KWOK_EDOMAIN;
+        if (x.chk & PREP_ARENA_BAD) st = KWOK_EDOMAIN;
         uint32_t slot = 0;
         const bool existing = x.handle >= 0;
         if (st == KWOK_OK && existing) {
@@ -1548,11 +1591,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 auto& hp = e->pods[slot];
                 uint32_t nslot = (slot / e->Cp) * e->Cn + hp.node;
                 auto& hn = e->nodes[nslot];
-                uint32_t ip = 0;
+                const uint32_t ip = x.pip;
                 // pod_controller.go:329-336: release the event object's podIP if the node is managed
                 // (EnableCNI: cni.Remove on the caller's side instead, :337-342)
-                if (!e->S.cni && hn.managed && x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip) &&
-                    (uint64_t)(ip - e->pool.net) < e->pool.size && ip >= e->pool.net) {
+                if (!e->S.cni && hn.managed && (x.chk & PREP_DEL_IP) && (uint64_t)(ip - e->pool.net) < e->pool.size &&
+                    ip >= e->pool.net) {
                     g.puts.push_back(ip);
                     released = ip;
                 }
@@ -1568,11 +1611,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 handle = e->pod_handle(slot);
             }
         } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
-            uint32_t hip = 0, pip = 0;
-            if (parse_opt_ip(arena, x.host_ip, &hip) || parse_opt_ip(arena, x.pod_ip, &pip)) st = KWOK_EDOMAIN;
-            else if (x.spec_id < 0 || (size_t)x.spec_id >= e->specs_h.size()) st = KWOK_EINVAL;
-            else if (x.phase > KWOK_PHASE_UNKNOWN) st = KWOK_EINVAL;
-            else if (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll) st = KWOK_EDOMAIN;
+            const uint32_t hip = x.hip, pip = x.pip;
+            st = x.fst;
             uint32_t nslot = 0;
             if (st == KWOK_OK && !existing) {
                 if (x.node_handle >= 0) {
@@ -1635,7 +1675,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 o.set_fields = 1;
                 o.node = hp.node;
                 o.spec = (uint16_t)x.spec_id;
-                o.ctime = (uint32_t)x.creation_unix;
+                o.ctime = x.ctime;
                 o.host_ip = hip;
                 o.pod_ip = pip;
                 pod_op(e, g, o);
@@ -1656,7 +1696,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     // A bucket that this batch's creates would fill grows first (every bucket to a
     // larger capacity, up to the handle stride): creates[bl] counts them, ignoring
     // the slots this batch's deletes free (an upper bound)
-    auto is_create = [](const kwok_pod_event& x) { return x.op == KWOK_OP_UPSERT && x.handle < 0; };
+    auto is_create = [](const PodPrep& x) { return x.op == KWOK_OP_UPSERT && x.handle < 0 && x.bkt != NO_BUCKET; };
     auto grow_for = [&](const std::vector<uint32_t>& creates) -> int {
         uint64_t need = 0;
         for (uint32_t b = 0; b < e->nb; b++)
@@ -1674,119 +1714,116 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         {
             std::vector<uint32_t> creates(e->nb, 0);
             bool any = false;
-            for (size_t i = 0; i < n; i++)
-                if (is_create(ev[i])) {
-                    const int64_t bl = bucket_of_record(ev[i]);
-                    if (bl >= 0) creates[(size_t)bl]++, any = true;
-                }
+            PodPrep r;
+            for (size_t i = 0; i < n; i++) {
+                prep(i, r);
+                if (is_create(r)) creates[r.bkt]++, any = true;
+            }
             if (any)
                 if (int rc = grow_for(creates)) return rc;
         }
+        // (the bucket mapping of handles is read again: a growth changed Cp)
+        PodPrep r;
         for (size_t i = 0; i < n; i++) {
-            const int64_t bl = bucket_of_record(ev[i]);
-            put(i, ingest_one(i, bl < 0 ? e->stage[0] : e->stage_of((uint32_t)bl)));
+            prep(i, r);
+            put(i, ingest_one(r, r.bkt == NO_BUCKET ? e->stage[0] : e->stage_of(r.bkt)));
         }
     } else {
-        // Bucket of every record and a stable scatter of the record indices by
-        // partition (both in parallel, chunk by chunk).  Then each partition sorts
-        // its records by bucket (a stable counting sort: per bucket, batch order is
-        // kept, and nothing orders records of different buckets), so one bucket's
-        // slot state, bitmap and nodes stay in cache while its records are
-        // ingested.  Results land in `all` and are copied out per contiguous
-        // record range.
+        // Pass 1 (chunks in parallel): each record's checks and parses, in batch
+        // order, and per-chunk counts of its bucket.  Pass 2: one stable scatter
+        // of the prepared records by bucket (per bucket, batch order is kept, and
+        // nothing orders records of different buckets).  Pass 3 (per partition):
+        // the partition's buckets are one contiguous run of the sorted records,
+        // read in order, so one bucket's slot state, bitmap and nodes stay in
+        // cache while its records are ingested.  Results land in `all` and are
+        // copied out per contiguous record range.
         const int P = e->n_part;
-        constexpr uint32_t NONE = 0xFFFFFFFFu;
-        if (e->ing_bkt.size() < n) e->ing_bkt.resize(n);
-        if (e->ing_res.size() < 2 * n) e->ing_res.resize(2 * n);
-        e->ing_order.resize((size_t)P);
-        uint32_t* bkt = e->ing_bkt.data();
-        uint64_t* plist = e->ing_res.data() + n;  // (bucket << 32 | record) grouped by partition
+        const uint32_t NB1 = e->nb + 1;  // key 0: records that change nothing; key b + 1: bucket b
+        if (e->ing_res.size() < n) e->ing_res.resize(n);
+        if (e->ing_prep.size() < n * sizeof(PodPrep)) e->ing_prep.resize(n * sizeof(PodPrep) + n * sizeof(PodPrep) / 8);
+        if (e->ing_sorted.size() < n * sizeof(PodPrep)) e->ing_sorted.resize(n * sizeof(PodPrep) + n * sizeof(PodPrep) / 8);
+        PodPrep* pre = reinterpret_cast<PodPrep*>(e->ing_prep.data());    // pass 1 output (batch order)
+        PodPrep* srt = reinterpret_cast<PodPrep*>(e->ing_sorted.data());  // pass 2 output (by bucket)
         uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
-        auto owner = [&](uint32_t b) { return b == NONE ? 0 : (int)((uint64_t)b * (uint64_t)P / e->nb); };
-        std::vector<size_t> cnt((size_t)P * P + 1, 0);  // [chunk][partition], then scatter positions
-        std::vector<std::vector<uint32_t>> creates((size_t)P);
+        auto key = [](uint32_t b) { return b == NO_BUCKET ? 0u : b + 1u; };
+        std::vector<uint32_t> cnt((size_t)P * NB1, 0);  // [chunk][key], then scatter positions
+        std::vector<std::vector<uint32_t>> creates((size_t)P);  // per chunk: creates per bucket
         run_parts(e, true, [&](int c) {
             const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-            size_t k[64] = {};  // local: neighbouring chunks' counters share cache lines
+            uint32_t* k = &cnt[(size_t)c * NB1];
             auto& cr = creates[(size_t)c];
             cr.assign(e->nb, 0);
             for (size_t i = lo; i < hi; i++) {
-                const int64_t bl = bucket_of_record(ev[i]);
-                bkt[i] = bl < 0 ? NONE : (uint32_t)bl;
-                k[owner(bkt[i])]++;
-                if (bl >= 0 && is_create(ev[i])) cr[(size_t)bl]++;
+                PodPrep& r = pre[i];
+                prep(i, r);
+                k[key(r.bkt)]++;
+                if (is_create(r)) cr[r.bkt]++;
             }
-            std::copy(k, k + P, &cnt[(size_t)c * P]);
         });
         for (int c = 1; c < P; c++)
             for (uint32_t b = 0; b < e->nb; b++) creates[0][b] += creates[(size_t)c][b];
-        if (int rc = grow_for(creates[0])) return rc;
-        std::vector<size_t> pstart((size_t)P + 1, 0);
+        {
+            const uint32_t cp0 = e->Cp;
+            if (int rc = grow_for(creates[0])) return rc;
+            if (e->Cp != cp0)  // handles past the old capacity may name a slot now: re-map them
+                run_parts(e, true, [&](int c) {
+                    const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
+                    uint32_t* k = &cnt[(size_t)c * NB1];
+                    for (size_t i = lo; i < hi; i++) {
+                        uint32_t sl = 0;
+                        PodPrep& r = pre[i];
+                        if (r.handle < 0 || (r.chk & PREP_ARENA_BAD)) continue;
+                        const uint32_t nbk = e->pod_slot(r.handle, &sl) == KWOK_OK ? sl / e->Cp : NO_BUCKET;
+                        k[key(r.bkt)]--;
+                        r.bkt = nbk;
+                        k[key(r.bkt)]++;
+                    }
+                });
+        }
+        // key-major, chunk-minor exclusive scan: the chunks' positions per key
+        std::vector<size_t> kstart((size_t)NB1 + 1, 0);
         {
             size_t acc = 0;
-            for (int p = 0; p < P; p++) {
-                pstart[(size_t)p] = acc;
+            for (uint32_t b = 0; b < NB1; b++) {
+                kstart[b] = acc;
                 for (int c = 0; c < P; c++) {
-                    const size_t v = cnt[(size_t)c * P + p];
-                    cnt[(size_t)c * P + p] = acc;
+                    const uint32_t v = cnt[(size_t)c * NB1 + b];
+                    cnt[(size_t)c * NB1 + b] = (uint32_t)acc;
                     acc += v;
                 }
             }
-            pstart[(size_t)P] = acc;
+            kstart[NB1] = acc;
         }
         run_parts(e, true, [&](int c) {
             const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-            size_t k[64];
-            std::copy(&cnt[(size_t)c * P], &cnt[(size_t)c * P] + P, k);
-            for (size_t i = lo; i < hi; i++) plist[k[owner(bkt[i])]++] = (uint64_t)bkt[i] << 32 | (uint32_t)i;
+            uint32_t* k = &cnt[(size_t)c * NB1];
+            for (size_t i = lo; i < hi; i++) srt[k[key(pre[i].bkt)]++] = pre[i];
         });
         tp1 = std::chrono::steady_clock::now();
         run_parts(e, true, [&](int p) {
             auto& g = e->stage[(size_t)p];
             // partition p owns buckets [first, last): those with bl * P / nb == p
+            // (partition 0 also takes the records that change nothing, key 0)
             const uint32_t first = (uint32_t)(((uint64_t)p * e->nb + P - 1) / P);
             const uint32_t last = (uint32_t)(((uint64_t)(p + 1) * e->nb + P - 1) / P);
-            const uint32_t nbk = last - first;
-            const uint64_t* mine = plist + pstart[(size_t)p];  // read in order: no random bkt[] reads
-            const uint32_t n_mine = (uint32_t)(pstart[(size_t)p + 1] - pstart[(size_t)p]);
-            std::vector<uint32_t> off(nbk + 2, 0);  // [0]: records that change nothing (partition 0 only)
-            for (uint32_t k = 0; k < n_mine; k++) {
-                const uint32_t b = (uint32_t)(mine[k] >> 32);
-                off[b == NONE ? 1 : b - first + 2]++;
-            }
-            for (uint32_t k = 1; k < nbk + 2; k++) off[k] += off[k - 1];
-            auto& order = e->ing_order[(size_t)p];
-            if (order.size() < n_mine) order.resize(n_mine + n_mine / 8);
-            for (uint32_t k = 0; k < n_mine; k++) {
-                const uint32_t i = (uint32_t)mine[k], b = (uint32_t)(mine[k] >> 32);
-                order[off[b == NONE ? 0 : b - first + 1]++] = i;
-            }
-            // records come in bucket order, i.e. from all over the batch: prefetch
-            // each record (PF ahead), then its IP strings and result word (PF/2
-            // ahead), so that their cache misses overlap
-            constexpr uint32_t PF = 16;
-            for (uint32_t k = 0; k < n_mine; k++) {
-                if (k + PF < n_mine) {
-                    const char* q = (const char*)&ev[order[k + PF]];
-                    __builtin_prefetch(q);
-                    __builtin_prefetch(q + sizeof(kwok_pod_event) - 1);
+            const size_t k0 = kstart[p == 0 ? 0 : first + 1], k1 = kstart[last + 1];
+            // records are read in order; prefetch the pod mirror of existing handles
+            // and the result word (records come from all over the batch)
+            constexpr size_t PF = 8;
+            for (size_t k = k0; k < k1; k++) {
+                if (k + PF < k1) {
+                    const PodPrep& y = srt[k + PF];
+                    __builtin_prefetch(&all[y.idx], 1);
+                    if (y.bkt != NO_BUCKET && y.handle >= 0) {
+                        uint32_t ps = 0;
+                        if (e->pod_slot(y.handle, &ps) == KWOK_OK) __builtin_prefetch(&e->pods[ps], 1);
+                    }
                 }
-                if (k + PF / 2 < n_mine) {
-                    const uint32_t j = order[k + PF / 2];
-                    const kwok_pod_event& y = ev[j];
-                    if (y.pod_ip.len && (size_t)y.pod_ip.off < arena_len) __builtin_prefetch(arena + y.pod_ip.off);
-                    if (y.host_ip.len && (size_t)y.host_ip.off < arena_len) __builtin_prefetch(arena + y.host_ip.off);
-                    __builtin_prefetch(&all[j], 1);
-                    uint32_t ps = 0;
-                    if (y.handle >= 0 && e->pod_slot(y.handle, &ps) == KWOK_OK) __builtin_prefetch(&e->pods[ps], 1);
-                    const int64_t ns = (int64_t)y.node_handle - (int64_t)e->b_lo * e->Cn;
-                    if (y.handle < 0 && ns >= 0 && ns < (int64_t)e->NL) __builtin_prefetch(&e->nodes[(size_t)ns], 1);
-                }
-                const uint32_t i = order[k];
-                const Res r = ingest_one(i, g);
-                all[i] = (uint32_t)r.handle | (uint64_t)(uint32_t)r.st << 32;
+                const PodPrep& x = srt[k];
+                const Res r = ingest_one(x, g);
+                all[x.idx] = (uint32_t)r.handle | (uint64_t)(uint32_t)r.st << 32;
                 // released IPs only come from DELETE records: theirs here, the rest zeroed below
-                if (out_released && ev[i].op == KWOK_OP_DELETE) out_released[i] = r.released;
+                if (out_released && x.op == KWOK_OP_DELETE) out_released[x.idx] = r.released;
             }
         });
         run_parts(e, true, [&](int t) {
