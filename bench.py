@@ -313,9 +313,11 @@ def main():
     now = workload.S0 + 30
     barrier()
     e.profile_enable(True)
+    e.profile_host(reset=True)
     t1 = time.perf_counter()
     r0 = e.tick(now, read=False)
     init_wall = max_over_ranks(time.perf_counter() - t1)
+    init_host, _ = e.profile_host(reset=True)
     ph0, _ = e.profile_read()
     e.profile_enable(False)
     first = dict(zip(abi.COUNTERS, list(r0.counters)))
@@ -435,6 +437,7 @@ def main():
             "phase_ms_per_tick": {k: v / max(nt, 1) for k, v in phases.items()},
             "host_ms_per_tick": {k: v / max(host_n, 1) for k, v in host_ms.items()},
             "initial_tick": {"wall_ms": init_wall * 1e3, "kernel_ms": ph0["kernel"], "k_emit_ms": emit_ms,
+                             "host_ms": init_host,
                              "transitions": transitions(r0.counters),
                              "transitions_per_s": transitions(r0.counters) / init_wall,
                              "counters": first,

@@ -543,10 +543,22 @@ int poisoned(kwok_engine* e) {
                                  "recreate it (re-ingest by List)");
 }
 
-// the output arena must hold the worst case of one tick (grown per slot at submit)
+// the output arena must hold the worst case of one tick.  It changes when the
+// capacity, the specs or the node blobs do (ingest, registration), and is
+// reserved then for the slots the next submit may take (a free slot whose outputs
+// the caller is not reading), not inside that tick: the 1M x 10M fleet's first
+// tick would otherwise reallocate ~8 GB (~0.7 ms of its enqueue).  A slot still
+// queued grows at its next submit.
+enum { SLOT_FREE = 0, SLOT_QUEUED = 1, SLOT_DONE = 2 };
+int grow_arena(kwok_engine* e, kwok_engine::TickSlot& T);
 int size_arena(kwok_engine* e) {
     e->arena_need = (uint64_t)e->NL * e->hb_stride + (uint64_t)e->NL * ((e->max_init_len + 15u) & ~15u) +
                     (uint64_t)e->PL * e->max_pod_len + 256;
+    for (int i = 0; i < 2; i++) {
+        kwok_engine::TickSlot& T = e->slots[i];
+        if (T.alloc && T.state == SLOT_FREE && i != e->cur)
+            if (int rc = grow_arena(e, T)) return rc;
+    }
     return KWOK_OK;
 }
 int grow_arena(kwok_engine* e, kwok_engine::TickSlot& T) {  // T holds no queued tick
@@ -1918,7 +1930,6 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
 }
 
 namespace {
-enum { SLOT_FREE = 0, SLOT_QUEUED = 1, SLOT_DONE = 2 };
 
 // k_emit for slot k's tick (S bound to slot k), behind its k_tick launch(es)
 int enqueue_emit(kwok_engine* e, int k) {
