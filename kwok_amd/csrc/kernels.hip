@@ -974,20 +974,65 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     uint16_t sp[POD_PER_THREAD];
     load_spec_ids(S, g, sp);
     PodCls cl[POD_PER_THREAD];
+    // every global input of the emission loop below is loaded here, before the
+    // scan, as one batch of independent loads (inside the loop, each pod's spec
+    // descriptor / reused address was a dependent round trip of its own):
+    // the spec lengths (one descriptor when the group's pods share a spec, the
+    // usual case), the pods' creation times and held host IPs
+    uint32_t sd_len[POD_PER_THREAD], sd_max[POD_PER_THREAD], ctm[POD_PER_THREAD], hipk[POD_PER_THREAD];
     uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
+    bool any_need = false, one_spec = true;
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
         cl[k] = classify_pod(g.st(k), group_node_flags(S, nflags, g, k), g.ip[k], S.cni != 0);
+        any_need |= cl[k].need;
+        one_spec &= sp[k] == sp[0];
+    }
+    if (any_need) {
+        if (one_spec) {
+            const SpecDesc& sd = S.specs[sp[0]];
+            const uint32_t ln = (uint32_t)sd.len_a + sd.len_b + sd.len_c, mx = sd.max_len;
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) sd_len[k] = ln, sd_max[k] = mx;
+        } else {
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) {
+                const SpecDesc& sd = S.specs[sp[k]];
+                sd_len[k] = (uint32_t)sd.len_a + sd.len_b + sd.len_c;
+                sd_max[k] = sd.max_len;
+            }
+        }
+        const uint4 ta = *reinterpret_cast<const uint4*>(S.pod_ctime + g.slot);
+        const uint4 tb = *reinterpret_cast<const uint4*>(S.pod_ctime + g.slot + 4);
+        const uint4 ha = *reinterpret_cast<const uint4*>(S.host_ip + g.slot);
+        const uint4 hb = *reinterpret_cast<const uint4*>(S.host_ip + g.slot + 4);
+        ctm[0] = ta.x, ctm[1] = ta.y, ctm[2] = ta.z, ctm[3] = ta.w, ctm[4] = tb.x, ctm[5] = tb.y, ctm[6] = tb.z, ctm[7] = tb.w;
+        hipk[0] = ha.x, hipk[1] = ha.y, hipk[2] = ha.z, hipk[3] = ha.w, hipk[4] = hb.x, hipk[5] = hb.y, hipk[6] = hb.z,
+        hipk[7] = hb.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) sd_len[k] = sd_max[k] = ctm[k] = hipk[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
         v[0] += cl[k].del;
         if (cl[k].need) {
             v[1]++;
-            v[2] += S.specs[sp[k]].max_len;
+            v[2] += sd_max[k];
         }
         v[3] += cl[k].alloc;
     }
+    const uint32_t my_alloc = v[3];
     uint32_t tot[4];
     block_excl_scan<4>(v, tot);
     const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0;
+    // the thread's reused / in-bitmap addresses: ordinals [run + v[3], + my_alloc), one batch
+    uint32_t areuse[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint64_t o = run.v[AG_ALLOC] + v[3] + (uint32_t)k;
+        areuse[k] = ((uint32_t)k < my_alloc && L.alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
+    }
     const uint64_t chunk_bytes = L.pod_base + run.v[AG_PP_BYTES];
     uint32_t jl = v[1];
     const uint32_t wpre = (uint32_t)__shfl((int)v[1], 0);  // the wave's first job (block-chunk relative)
@@ -995,6 +1040,7 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
     uint64_t* stg_off = reinterpret_cast<uint64_t*>(stg + 512);
     bool dirty = false;
     uint16_t nst[POD_PER_THREAD];
+    uint32_t ai = 0;
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) {
         const uint32_t slot = g.slot + k;
@@ -1009,27 +1055,30 @@ __device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t
         if (cl[k].eval) {
             uint32_t pip = g.ip[k];
             if (cl[k].alloc) {
-                const uint64_t o = run.v[AG_ALLOC] + v[3]++;
+                const uint32_t a = ai++;  // the thread's a-th allocation
+                const uint64_t o = run.v[AG_ALLOC] + v[3] + a;
                 const uint64_t gidx = L.alloc_base + o;
-                pip = gidx < take + fin ? S.alloc_addr[o] : (uint32_t)(fout0 + (gidx - take - fin));
+                uint32_t r = areuse[0];
+#pragma unroll
+                for (int q = 1; q < POD_PER_THREAD; q++) r = a == (uint32_t)q ? areuse[q] : r;
+                pip = gidx < take + fin ? r : (uint32_t)(fout0 + (gidx - take - fin));
             }
             if (cl[k].need) {
                 const bool stat = s & PS_STATUS_NONEMPTY;
                 uint32_t hip = 0;
                 if (stat) {
-                    hip = (s & PS_HAS_HOST_IP) ? S.host_ip[slot] : S.node_ip;
+                    hip = (s & PS_HAS_HOST_IP) ? hipk[k] : S.node_ip;
                     if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
                     if (pip != g.ip[k]) S.pod_ip[slot] = pip;
                 }
                 const uint64_t ord = run.v[AG_PP] + jl;
-                const SpecDesc& sd = S.specs[sp[k]];
-                const uint32_t len = sd.len_a + sd.len_b + sd.len_c + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
+                const uint32_t len = sd_len[k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
                 S.pp_pods[ord] = handle;
                 stg_off[jl - wpre] = chunk_bytes + v[2];
                 S.pp_len[ord] = len;
-                stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, S.pod_ctime[slot], sp[k]);  // the bytes: k_emit
+                stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, ctm[k], sp[k]);  // the bytes: k_emit
                 jl++;
-                v[2] += sd.max_len;
+                v[2] += sd_max[k];
                 // the apiserver applied the patch
                 s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
                                PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
