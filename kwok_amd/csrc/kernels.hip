@@ -352,66 +352,100 @@ __device__ __forceinline__ PoolPlan pool_plan(const DevState& S, uint64_t A, uin
     return p;
 }
 
+// the n-th (0-indexed) set bit of m (m has more than n set bits): a popcount
+// binary search, branch-free
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t n) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int wd = 32; wd >= 1; wd >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(m & ((1ull << wd) - 1ull));
+        const bool up = n >= c;
+        n = up ? n - c : n;
+        m = up ? m >> wd : m;
+        pos += up ? (uint32_t)wd : 0u;
+    }
+    return pos;
+}
+// the lowest n of the cnt set bits of m
+__device__ __forceinline__ uint64_t lowest_bits(uint64_t m, uint32_t n, uint32_t cnt) {
+    if (n >= cnt) return m;
+    if (n == 0) return 0;
+    return m & ((1ull << nth_set_bit(m, n)) - 1ull);
+}
+// The wave's selections as alloc_addr entries, written coalesced.  Lane l took
+// the lowest n of the set bits of m (word wl = w0 + l); the wave's selections
+// are the ordinals [g0, g0 + total) in lane order.  Output p = lane + 64 q: its
+// owner lane (the first whose inclusive count exceeds p, a binary search over
+// the counts in LDS) and the (p - owner's exclusive count)-th set bit of the
+// owner's word.  Only this rank's ordinals [lo_g, hi_g) are recorded.
+__device__ __forceinline__ void wave_write_addrs(const DevState& S, uint32_t* sh_in, uint64_t* sh_m, uint64_t g0, uint32_t n,
+                                                 uint64_t m, uint64_t w0, uint64_t lo_g, uint64_t hi_g) {
+    const uint32_t l = lane_id();
+    const uint32_t incl = wave_incl_scan(n);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (total == 0) return;
+    if (g0 >= hi_g || g0 + total <= lo_g) return;
+    sh_in[l] = incl;
+    sh_m[l] = m;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (uint32_t p = l; p < total; p += 64) {
+        uint32_t o = 0;
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1) o = sh_in[o + st - 1] <= p ? o + st : o;
+        const uint32_t ex = o ? sh_in[o - 1] : 0u;
+        const uint32_t bit = nth_set_bit(sh_m[o], p - ex);
+        const uint64_t g = g0 + p;
+        if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)((w0 + o) * 64 + bit);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads before the next list's writes
+}
+
 // select + commit for word-block wb.  Allocation ordinal g (global, canonical order):
 //   g < take            -> g-th lowest usable address (the build's reuse rule)
 //   g < take + fin      -> (g-take)-th free in-CIDR address from the cursor
 //   otherwise           -> fout0 + (g - take - fin)          (beyond the CIDR)
 // Every rank commits ALL allocations to its replica; it records the addresses
 // of its own ordinals [alloc_base, alloc_base + n_alloc_local).
+// Words are taken k-major (pass k: words wb * POOL_WPB + k * BLOCK + thread), so
+// a pass's words are consecutive across the block and its selections are one
+// contiguous ordinal range per wave: each lane commits its word's selections
+// as two masks, and the wave writes their addresses coalesced (one alloc_addr
+// entry per lane per store, instead of a serial bit walk per lane with one
+// scattered store per address: the 1M x 10M initial tick's 10M fresh Gets).
 __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
                                    uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out) {
+    __shared__ uint32_t sh_in[BLOCK / 64][64];
+    __shared__ uint64_t sh_m[BLOCK / 64][64];
     const uint64_t take = p.take, fin = p.fin;
     const uint64_t cb = cursor_bit(S);
     const bool advance = fin > 0 && p.fout == 0;
-    uint32_t c[2][POOL_WPT];
-    uint64_t wu[POOL_WPT], wf[POOL_WPT];
-    uint32_t v[2] = {0, 0};
+    const uint32_t wv = threadIdx.x >> 6;
     for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        uint64_t used = w < S.pool.words ? S.used_bm[w] : ~0ull;
-        wu[k] = w < S.pool.words ? S.usable_bm[w] : 0;
-        wf[k] = w < S.pool.words ? free_mask(S, w, used, wu[k], cb) : 0;
-        c[0][k] = __popcll(wu[k]);
-        c[1][k] = __popcll(wf[k]);
-        v[0] += c[0][k];
-        v[1] += c[1][k];
-    }
-    uint32_t tot[2];
-    block_excl_scan<2>(v, tot);
-    uint64_t ru = base_u + v[0];
-    uint64_t rf = base_f + v[1];
-    for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        if (w >= S.pool.words) break;
-        if (ru < take && wu[k]) {
-            uint64_t n = take - ru < c[0][k] ? take - ru : c[0][k];
-            uint64_t m = wu[k], sel = 0;
-            for (uint64_t j = 0; j < n; j++) {
-                uint32_t b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-                m &= m - 1;
-                sel |= 1ull << b;
-                uint64_t g = ru + j;
-                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
-            }
-            S.usable_bm[w] &= ~sel;  // ipPool.Get: delete(usable, ip) ...
-            S.used_bm[w] |= sel;     // ... used[ip]   (one thread owns word w)
-        }
-        ru += c[0][k];
-        if (rf < fin && wf[k]) {
-            uint64_t n = fin - rf < c[1][k] ? fin - rf : c[1][k];
-            uint64_t m = wf[k], sel = 0;
-            uint32_t b = 0;
-            for (uint64_t j = 0; j < n; j++) {
-                b = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-                m &= m - 1;
-                sel |= 1ull << b;
-                uint64_t g = take + rf + j;
-                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w * 64 + b);
-            }
-            S.used_bm[w] |= sel;  // ipPool.new: used[ip]  (usable add + Get delete net to nothing)
-            if (advance && rf + n == fin) *cursor_out = (uint64_t)S.pool.net + w * 64 + b + 1 - S.pool.base;
-        }
-        rf += c[1][k];
+        const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
+        const bool valid = w < S.pool.words;
+        const uint64_t used = valid ? S.used_bm[w] : ~0ull;
+        const uint64_t wu = valid ? S.usable_bm[w] : 0ull;
+        const uint64_t wf = valid ? free_mask(S, w, used, wu, cb) : 0ull;
+        const uint32_t cu = (uint32_t)__popcll(wu), cf = (uint32_t)__popcll(wf);
+        uint32_t v[2] = {cu, cf}, tot[2];
+        block_excl_scan<2>(v, tot);
+        const uint64_t ru = base_u + v[0], rf = base_f + v[1];
+        const uint32_t nu = ru < take ? (uint32_t)min((uint64_t)cu, take - ru) : 0u;
+        const uint32_t nf = rf < fin ? (uint32_t)min((uint64_t)cf, fin - rf) : 0u;
+        const uint64_t selu = lowest_bits(wu, nu, cu), self = lowest_bits(wf, nf, cf);
+        if (selu) S.usable_bm[w] = wu & ~selu;  // ipPool.Get: delete(usable, ip) ...
+        if (selu | self) S.used_bm[w] = used | selu | self;  // ... used[ip]; ipPool.new: used[ip]  (one thread owns word w)
+        if (advance && nf && rf + nf == fin)
+            *cursor_out = (uint64_t)S.pool.net + w * 64 + nth_set_bit(wf, nf - 1) + 1 - S.pool.base;
+        const uint64_t w0 = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + (threadIdx.x & ~63u);
+        const uint64_t gu0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ru) |
+                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ru >> 32)) << 32);
+        const uint64_t gf0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)rf) |
+                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rf >> 32)) << 32);
+        wave_write_addrs(S, sh_in[wv], sh_m[wv], gu0, nu, wu, w0, lo_g, hi_g);
+        wave_write_addrs(S, sh_in[wv], sh_m[wv], take + gf0, nf, wf, w0, lo_g, hi_g);
+        base_u += tot[0];
+        base_f += tot[1];
     }
 }
 
