@@ -1001,146 +1001,187 @@ constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs 
 // jobs) and written out as whole rows instead of one cache line per lane per
 // pod (the initial 1M x 10M tick's job stores: ~270 of its ~510 us of pod
 // emission).
-__device__ __forceinline__ void emit_pod_chunk(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
-                               uint32_t nbk, uint32_t ng, uint32_t c, Bases& run, const Layout& L, uint32_t* stage) {
-    PodGrp g;
-    load_group(S, gpre, bk0, nbk, ng, c * BLOCK + threadIdx.x, g);
-    uint16_t sp[POD_PER_THREAD];
-    load_spec_ids(S, g, sp);
-    PodCls cl[POD_PER_THREAD];
+// NC dirty chunks at a time (cs[0] < cs[1] in canonical order): their loads,
+// classification and scans overlap, and the block synchronises once per NC
+// chunks.  A chunk costs ~9 us of mostly fixed latency (group loads ~2, scan ~1,
+// emission with its reused-address loads ~3.6, the closing barrier ~2.3: trace
+// of the 1M x 10M churn tick, which visits all 19 chunks of every block).
+template <int NC>
+__device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
+                                                uint32_t nbk, uint32_t ng, const uint32_t (&cs)[NC], Bases& run,
+                                                const Layout& L, uint32_t* stage) {
+    PodGrp g[NC];
+    uint16_t sp[NC][POD_PER_THREAD];
+#pragma unroll
+    for (int i = 0; i < NC; i++) load_group(S, gpre, bk0, nbk, ng, cs[i] * BLOCK + threadIdx.x, g[i]);
+#pragma unroll
+    for (int i = 0; i < NC; i++) load_spec_ids(S, g[i], sp[i]);
+    PodCls cl[NC][POD_PER_THREAD];
     // every global input of the emission loop below is loaded here, before the
     // scan, as one batch of independent loads (inside the loop, each pod's spec
     // descriptor / reused address was a dependent round trip of its own):
     // the spec lengths (one descriptor when the group's pods share a spec, the
     // usual case), the pods' creation times and held host IPs
-    uint32_t sd_len[POD_PER_THREAD], sd_max[POD_PER_THREAD], ctm[POD_PER_THREAD], hipk[POD_PER_THREAD];
-    uint32_t v[4] = {0, 0, 0, 0};  // del, pp, pp bytes, alloc
-    bool any_need = false, one_spec = true;
+    uint32_t sd_len[NC][POD_PER_THREAD], sd_max[NC][POD_PER_THREAD], ctm[NC][POD_PER_THREAD], hipk[NC][POD_PER_THREAD];
+    uint32_t v[4 * NC];  // per chunk: del, pp, pp bytes, alloc
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        cl[k] = classify_pod(g.st(k), group_node_flags(S, nflags, g, k), g.ip[k], S.cni != 0);
-        any_need |= cl[k].need;
-        one_spec &= sp[k] == sp[0];
-    }
-    if (any_need) {
-        if (one_spec) {
-            const SpecDesc& sd = S.specs[sp[0]];
-            const uint32_t ln = (uint32_t)sd.len_a + sd.len_b + sd.len_c, mx = sd.max_len;
+    for (int i = 0; i < NC; i++) {
+        bool any_need = false, one_spec = true;
 #pragma unroll
-            for (int k = 0; k < POD_PER_THREAD; k++) sd_len[k] = ln, sd_max[k] = mx;
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            cl[i][k] = classify_pod(g[i].st(k), group_node_flags(S, nflags, g[i], k), g[i].ip[k], S.cni != 0);
+            any_need |= cl[i][k].need;
+            one_spec &= sp[i][k] == sp[i][0];
+        }
+        if (any_need) {
+            if (one_spec) {
+                const SpecDesc& sd = S.specs[sp[i][0]];
+                const uint32_t ln = (uint32_t)sd.len_a + sd.len_b + sd.len_c, mx = sd.max_len;
+#pragma unroll
+                for (int k = 0; k < POD_PER_THREAD; k++) sd_len[i][k] = ln, sd_max[i][k] = mx;
+            } else {
+#pragma unroll
+                for (int k = 0; k < POD_PER_THREAD; k++) {
+                    const SpecDesc& sd = S.specs[sp[i][k]];
+                    sd_len[i][k] = (uint32_t)sd.len_a + sd.len_b + sd.len_c;
+                    sd_max[i][k] = sd.max_len;
+                }
+            }
+            const uint4 ta = *reinterpret_cast<const uint4*>(S.pod_ctime + g[i].slot);
+            const uint4 tb = *reinterpret_cast<const uint4*>(S.pod_ctime + g[i].slot + 4);
+            const uint4 ha = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot);
+            const uint4 hb = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot + 4);
+            ctm[i][0] = ta.x, ctm[i][1] = ta.y, ctm[i][2] = ta.z, ctm[i][3] = ta.w;
+            ctm[i][4] = tb.x, ctm[i][5] = tb.y, ctm[i][6] = tb.z, ctm[i][7] = tb.w;
+            hipk[i][0] = ha.x, hipk[i][1] = ha.y, hipk[i][2] = ha.z, hipk[i][3] = ha.w;
+            hipk[i][4] = hb.x, hipk[i][5] = hb.y, hipk[i][6] = hb.z, hipk[i][7] = hb.w;
         } else {
 #pragma unroll
-            for (int k = 0; k < POD_PER_THREAD; k++) {
-                const SpecDesc& sd = S.specs[sp[k]];
-                sd_len[k] = (uint32_t)sd.len_a + sd.len_b + sd.len_c;
-                sd_max[k] = sd.max_len;
+            for (int k = 0; k < POD_PER_THREAD; k++) sd_len[i][k] = sd_max[i][k] = ctm[i][k] = hipk[i][k] = 0;
+        }
+        v[4 * i] = v[4 * i + 1] = v[4 * i + 2] = v[4 * i + 3] = 0;
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            v[4 * i] += cl[i][k].del;
+            if (cl[i][k].need) {
+                v[4 * i + 1]++;
+                v[4 * i + 2] += sd_max[i][k];
             }
+            v[4 * i + 3] += cl[i][k].alloc;
         }
-        const uint4 ta = *reinterpret_cast<const uint4*>(S.pod_ctime + g.slot);
-        const uint4 tb = *reinterpret_cast<const uint4*>(S.pod_ctime + g.slot + 4);
-        const uint4 ha = *reinterpret_cast<const uint4*>(S.host_ip + g.slot);
-        const uint4 hb = *reinterpret_cast<const uint4*>(S.host_ip + g.slot + 4);
-        ctm[0] = ta.x, ctm[1] = ta.y, ctm[2] = ta.z, ctm[3] = ta.w, ctm[4] = tb.x, ctm[5] = tb.y, ctm[6] = tb.z, ctm[7] = tb.w;
-        hipk[0] = ha.x, hipk[1] = ha.y, hipk[2] = ha.z, hipk[3] = ha.w, hipk[4] = hb.x, hipk[5] = hb.y, hipk[6] = hb.z,
-        hipk[7] = hb.w;
-    } else {
-#pragma unroll
-        for (int k = 0; k < POD_PER_THREAD; k++) sd_len[k] = sd_max[k] = ctm[k] = hipk[k] = 0;
     }
+    uint32_t my_alloc[NC];
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        v[0] += cl[k].del;
-        if (cl[k].need) {
-            v[1]++;
-            v[2] += sd_max[k];
+    for (int i = 0; i < NC; i++) my_alloc[i] = v[4 * i + 3];
+    uint32_t tot[4 * NC];
+    block_excl_scan<4 * NC>(v, tot);
+    // chunk i's bases: the running prefix plus the totals of the chunks before it
+    Bases rb[NC];
+#pragma unroll
+    for (int i = 0; i < NC; i++) {
+        rb[i] = run;
+#pragma unroll
+        for (int j = 0; j < i; j++) {
+            rb[i].v[AG_DEL] += tot[4 * j];
+            rb[i].v[AG_PP] += tot[4 * j + 1];
+            rb[i].v[AG_PP_BYTES] += tot[4 * j + 2];
+            rb[i].v[AG_ALLOC] += tot[4 * j + 3];
         }
-        v[3] += cl[k].alloc;
     }
-    const uint32_t my_alloc = v[3];
-    uint32_t tot[4];
-    block_excl_scan<4>(v, tot);
     const uint64_t take = L.plan.take, fin = L.plan.fin, fout0 = L.plan.fout0;
-    // the thread's reused / in-bitmap addresses: ordinals [run + v[3], + my_alloc), one batch
-    uint32_t areuse[POD_PER_THREAD];
+    // the thread's reused / in-bitmap addresses: ordinals [base + v[3], + my_alloc), one batch
+    uint32_t areuse[NC][POD_PER_THREAD];
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint64_t o = run.v[AG_ALLOC] + v[3] + (uint32_t)k;
-        areuse[k] = ((uint32_t)k < my_alloc && L.alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
-    }
-    const uint64_t chunk_bytes = L.pod_base + run.v[AG_PP_BYTES];
-    uint32_t jl = v[1];
-    const uint32_t wpre = (uint32_t)__shfl((int)v[1], 0);  // the wave's first job (block-chunk relative)
+    for (int i = 0; i < NC; i++)
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint64_t o = rb[i].v[AG_ALLOC] + v[4 * i + 3] + (uint32_t)k;
+            areuse[i][k] = ((uint32_t)k < my_alloc[i] && L.alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
+        }
     uint4* stg = reinterpret_cast<uint4*>(stage + (threadIdx.x >> 6) * POD_STAGE_WORDS);
     uint64_t* stg_off = reinterpret_cast<uint64_t*>(stg + 512);
-    bool dirty = false;
-    uint16_t nst[POD_PER_THREAD];
-    uint32_t ai = 0;
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) {
-        const uint32_t slot = g.slot + k;
-        const int32_t handle = pod_handle_of(S, slot);
-        uint16_t s = g.st(k);
-        if (cl[k].del) {
-            const uint64_t ord = run.v[AG_DEL] + v[0]++;
-            S.del_pods[ord] = handle;
-            S.del_fin[ord] = (s & PS_HAS_FIN) ? 1 : 0;
-            s = 0;  // DeletePod -> Delete(grace 0): the object is gone
-        }
-        if (cl[k].eval) {
-            uint32_t pip = g.ip[k];
-            if (cl[k].alloc) {
-                const uint32_t a = ai++;  // the thread's a-th allocation
-                const uint64_t o = run.v[AG_ALLOC] + v[3] + a;
-                const uint64_t gidx = L.alloc_base + o;
-                uint32_t r = areuse[0];
+    for (int i = 0; i < NC; i++) {
+        const Bases& r = rb[i];
+        const PodGrp& gi = g[i];
+        const uint64_t chunk_bytes = L.pod_base + r.v[AG_PP_BYTES];
+        uint32_t vdel = v[4 * i], jl = v[4 * i + 1], vbytes = v[4 * i + 2];
+        const uint32_t va = v[4 * i + 3];
+        const uint32_t wpre = (uint32_t)__shfl((int)jl, 0);  // the wave's first job (block-chunk relative)
+        bool dirty = false;
+        uint16_t nst[POD_PER_THREAD];
+        uint32_t ai = 0;
 #pragma unroll
-                for (int q = 1; q < POD_PER_THREAD; q++) r = a == (uint32_t)q ? areuse[q] : r;
-                pip = gidx < take + fin ? r : (uint32_t)(fout0 + (gidx - take - fin));
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint32_t slot = gi.slot + k;
+            const int32_t handle = pod_handle_of(S, slot);
+            uint16_t s = gi.st(k);
+            if (cl[i][k].del) {
+                const uint64_t ord = r.v[AG_DEL] + vdel++;
+                S.del_pods[ord] = handle;
+                S.del_fin[ord] = (s & PS_HAS_FIN) ? 1 : 0;
+                s = 0;  // DeletePod -> Delete(grace 0): the object is gone
             }
-            if (cl[k].need) {
-                const bool stat = s & PS_STATUS_NONEMPTY;
-                uint32_t hip = 0;
-                if (stat) {
-                    hip = (s & PS_HAS_HOST_IP) ? hipk[k] : S.node_ip;
-                    if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
-                    if (pip != g.ip[k]) S.pod_ip[slot] = pip;
+            if (cl[i][k].eval) {
+                uint32_t pip = gi.ip[k];
+                if (cl[i][k].alloc) {
+                    const uint32_t a = ai++;  // the thread's a-th allocation
+                    const uint64_t o = r.v[AG_ALLOC] + va + a;
+                    const uint64_t gidx = L.alloc_base + o;
+                    uint32_t ra = areuse[i][0];
+#pragma unroll
+                    for (int q = 1; q < POD_PER_THREAD; q++) ra = a == (uint32_t)q ? areuse[i][q] : ra;
+                    pip = gidx < take + fin ? ra : (uint32_t)(fout0 + (gidx - take - fin));
                 }
-                const uint64_t ord = run.v[AG_PP] + jl;
-                const uint32_t len = sd_len[k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
-                S.pp_pods[ord] = handle;
-                stg_off[jl - wpre] = chunk_bytes + v[2];
-                S.pp_len[ord] = len;
-                stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, ctm[k], sp[k]);  // the bytes: k_emit
-                jl++;
-                v[2] += sd_max[k];
-                // the apiserver applied the patch
-                s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
-                               PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
+                if (cl[i][k].need) {
+                    const bool stat = s & PS_STATUS_NONEMPTY;
+                    uint32_t hip = 0;
+                    if (stat) {
+                        hip = (s & PS_HAS_HOST_IP) ? hipk[i][k] : S.node_ip;
+                        if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
+                        if (pip != gi.ip[k]) S.pod_ip[slot] = pip;
+                    }
+                    const uint64_t ord = r.v[AG_PP] + jl;
+                    const uint32_t len = sd_len[i][k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
+                    S.pp_pods[ord] = handle;
+                    stg_off[jl - wpre] = chunk_bytes + vbytes;
+                    S.pp_len[ord] = len;
+                    stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, ctm[i][k], sp[i][k]);  // the bytes: k_emit
+                    jl++;
+                    vbytes += sd_max[i][k];
+                    // the apiserver applied the patch
+                    s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
+                                   PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
+                }
+                s &= (uint16_t)~PS_EVENT;
             }
-            s &= (uint16_t)~PS_EVENT;
+            dirty |= s != gi.st(k);
+            nst[k] = s;
         }
-        dirty |= s != g.st(k);
-        nst[k] = s;
-    }
-    {  // the wave's staged records -> pp_job[run + wpre, run + wend)
-        const uint32_t wend = (uint32_t)__shfl((int)jl, 63);
-        uint4* dst = S.pp_job + run.v[AG_PP] + wpre;
-        uint64_t* dst_off = S.pp_off + run.v[AG_PP] + wpre;
-        for (uint32_t i = lane_id(); i < wend - wpre; i += 64) dst[i] = stg[i], dst_off[i] = stg_off[i];
-    }
-    if (g.slot != ~0u && dirty) {
-        uint4 o;
-        o.x = nst[0] | (uint32_t)nst[1] << 16;
-        o.y = nst[2] | (uint32_t)nst[3] << 16;
-        o.z = nst[4] | (uint32_t)nst[5] << 16;
-        o.w = nst[6] | (uint32_t)nst[7] << 16;
-        *reinterpret_cast<uint4*>(S.pod_state + g.slot) = o;
+        {  // the wave's staged records -> pp_job[base + wpre, base + wend); the wave's
+           // LDS operations run in order, so the next chunk's staging follows these reads
+            const uint32_t wend = (uint32_t)__shfl((int)jl, 63);
+            uint4* dst = S.pp_job + r.v[AG_PP] + wpre;
+            uint64_t* dst_off = S.pp_off + r.v[AG_PP] + wpre;
+            for (uint32_t q = lane_id(); q < wend - wpre; q += 64) dst[q] = stg[q], dst_off[q] = stg_off[q];
+        }
+        if (gi.slot != ~0u && dirty) {
+            uint4 o;
+            o.x = nst[0] | (uint32_t)nst[1] << 16;
+            o.y = nst[2] | (uint32_t)nst[3] << 16;
+            o.z = nst[4] | (uint32_t)nst[5] << 16;
+            o.w = nst[6] | (uint32_t)nst[7] << 16;
+            *reinterpret_cast<uint4*>(S.pod_state + gi.slot) = o;
+        }
     }
     __syncthreads();
-    run.v[AG_DEL] += tot[0];
-    run.v[AG_PP] += tot[1];
-    run.v[AG_PP_BYTES] += tot[2];
-    run.v[AG_ALLOC] += tot[3];
+#pragma unroll
+    for (int i = 0; i < NC; i++) {
+        run.v[AG_DEL] += tot[4 * i];
+        run.v[AG_PP] += tot[4 * i + 1];
+        run.v[AG_PP_BYTES] += tot[4 * i + 2];
+        run.v[AG_ALLOC] += tot[4 * i + 3];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1495,9 +1536,17 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     }
     TSTAMP(14);
     const uint32_t ng = l.gpre[nbk];
-    for (uint64_t m = pod_mask; m; m &= m - 1) {
-        const uint32_t c = (uint32_t)__builtin_ctzll(m);
-        emit_pod_chunk(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, c, run, L, l.recs);
+    for (uint64_t m = pod_mask; m;) {  // dirty chunks two at a time, in canonical order
+        const uint32_t c0 = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        if (m) {
+            const uint32_t cs[2] = {c0, (uint32_t)__builtin_ctzll(m)};
+            m &= m - 1;
+            emit_pod_chunks<2>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, cs, run, L, l.recs);
+        } else {
+            const uint32_t cs[1] = {c0};
+            emit_pod_chunks<1>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, cs, run, L, l.recs);
+        }
     }
     TSTAMP(6);
 #undef TSTAMP
