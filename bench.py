@@ -322,9 +322,16 @@ def main():
     e.profile_enable(False)
     first = dict(zip(abi.COUNTERS, list(r0.counters)))
     now += 30
-    for w in range(1, a.warmup):
-        e.tick(now, read=False)
+    # the remaining warmup steps take the timed steps' path (queued two deep), so
+    # the second tick slot (its lists and ~8 GB arena) is allocated before timing
+    if a.warmup > 1:
+        e.tick_submit(now)
         now += 30
+        for w in range(1, a.warmup):
+            if w + 1 < a.warmup:
+                e.tick_submit(now)
+                now += 30
+            e.tick_collect(read=False)
 
     # ---- timed steps: queued submit / collect ----------------------------------
     barrier()
