@@ -403,8 +403,10 @@ struct PodPrep {
     int32_t handle, node_handle, spec_id;
     uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: pip = the parsed podIP
     uint32_t ctime;
+    uint32_t slot;          // handle >= 0: its local slot (bkt * Cp + index), when pst == KWOK_OK
     uint8_t op, phase, flags, chk;  // chk: PREP_*
-    int32_t fst;            // UPSERT: the first failing field check (KWOK_OK: none)
+    int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
+    int8_t pst;             // handle >= 0: pod_slot's status
     kwok_str node_name;
 };
 enum : uint8_t { PREP_ARENA_BAD = 1, PREP_DEL_IP = 2 };
@@ -1549,7 +1551,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         r.idx = (uint32_t)i;
         r.handle = x.handle, r.node_handle = x.node_handle, r.spec_id = x.spec_id;
         r.op = x.op, r.phase = x.phase, r.flags = x.flags, r.chk = 0;
-        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK;
+        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK, r.slot = 0, r.pst = KWOK_OK;
         r.node_name = x.node_name;
         r.bkt = NO_BUCKET;
         if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
@@ -1567,8 +1569,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             else r.ctime = (uint32_t)x.creation_unix;
         }
         if (x.handle >= 0) {
-            uint32_t sl = 0;
-            if (e->pod_slot(x.handle, &sl) == KWOK_OK) r.bkt = sl / e->Cp;
+            r.pst = (int8_t)e->pod_slot(x.handle, &r.slot);
+            if (r.pst == KWOK_OK) r.bkt = r.slot / e->Cp;
             return;
         }
         if (x.op != KWOK_OP_UPSERT) return;
@@ -1593,15 +1595,21 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         if (x.chk & PREP_ARENA_BAD) st = KWOK_EDOMAIN;
         uint32_t slot = 0;
         const bool existing = x.handle >= 0;
+        // existing handles: bkt = slot / Cp (prep); no divisions below
+        const uint32_t bl0 = x.bkt;
         if (st == KWOK_OK && existing) {
-            st = e->pod_slot(x.handle, &slot);
+            st = x.pst;
+            slot = x.slot;
             if (st == KWOK_OK && !e->pods[slot].used) st = KWOK_ENOTFOUND;
         }
+        auto handle_of = [&](uint32_t bl, uint32_t sl) {
+            return (int32_t)((e->b_lo + bl) * e->Hs + (sl - bl * e->Cp));
+        };
         if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
             if (!existing) st = KWOK_EINVAL;
             else {
                 auto& hp = e->pods[slot];
-                uint32_t nslot = (slot / e->Cp) * e->Cn + hp.node;
+                uint32_t nslot = bl0 * e->Cn + hp.node;
                 auto& hn = e->nodes[nslot];
                 const uint32_t ip = x.pip;
                 // pod_controller.go:329-336: release the event object's podIP if the node is managed
@@ -1616,14 +1624,15 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 pod_op(e, g, o);  // state = 0
                 hp.used = 0;
                 hp.delpend = 0;
-                set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
-                e->pod_cnt[slot / e->Cp]--;
+                set_bit(e->pod_bits, e->Cp, bl0, slot - bl0 * e->Cp, false);
+                e->pod_cnt[bl0]--;
                 hn.refs--;
                 free_node_if_unused(e, nslot);
-                handle = e->pod_handle(slot);
+                handle = handle_of(bl0, slot);
             }
         } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
             const uint32_t hip = x.hip, pip = x.pip;
+            uint32_t bl = bl0;
             st = x.fst;
             uint32_t nslot = 0;
             if (st == KWOK_OK && !existing) {
@@ -1638,7 +1647,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                     st = node_slot(e, arena + x.node_name.off, x.node_name.len, true, &nslot);
                 }
                 if (st == KWOK_OK) {
-                    uint32_t bl = nslot / e->Cn;
+                    bl = x.bkt != NO_BUCKET ? x.bkt : nslot / e->Cn;  // the node's bucket (prep)
                     int32_t idx = first_free(e->pod_bits, bl, e->Cp);
                     if (idx < 0) {
                         st = KWOK_EFULL;
@@ -1652,12 +1661,12 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                             g.fill_dirty = true;
                         }
                         e->pods[slot].used = 1;
-                        e->pods[slot].node = (uint16_t)(nslot % e->Cn);
+                        e->pods[slot].node = (uint16_t)(nslot - bl * e->Cn);
                         e->nodes[nslot].refs++;
                     }
                 }
             } else if (st == KWOK_OK) {
-                nslot = (slot / e->Cp) * e->Cn + e->pods[slot].node;
+                nslot = bl * e->Cn + e->pods[slot].node;
             }
             if (st == KWOK_OK) {
                 const auto& hn = e->nodes[nslot];
@@ -1691,7 +1700,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 o.host_ip = hip;
                 o.pod_ip = pip;
                 pod_op(e, g, o);
-                handle = e->pod_handle(slot);
+                handle = handle_of(bl, slot);
             }
         } else if (st == KWOK_OK) {
             st = KWOK_EINVAL;
@@ -1785,7 +1794,9 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                         uint32_t sl = 0;
                         PodPrep& r = pre[i];
                         if (r.handle < 0 || (r.chk & PREP_ARENA_BAD)) continue;
-                        const uint32_t nbk = e->pod_slot(r.handle, &sl) == KWOK_OK ? sl / e->Cp : NO_BUCKET;
+                        r.pst = (int8_t)e->pod_slot(r.handle, &sl);
+                        r.slot = sl;
+                        const uint32_t nbk = r.pst == KWOK_OK ? sl / e->Cp : NO_BUCKET;
                         k[key(r.bkt)]--;
                         r.bkt = nbk;
                         k[key(r.bkt)]++;
@@ -1826,10 +1837,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 if (k + PF < k1) {
                     const PodPrep& y = srt[k + PF];
                     __builtin_prefetch(&all[y.idx], 1);
-                    if (y.bkt != NO_BUCKET && y.handle >= 0) {
-                        uint32_t ps = 0;
-                        if (e->pod_slot(y.handle, &ps) == KWOK_OK) __builtin_prefetch(&e->pods[ps], 1);
-                    }
+                    if (y.bkt != NO_BUCKET && y.handle >= 0) __builtin_prefetch(&e->pods[y.slot], 1);
                 }
                 const PodPrep& x = srt[k];
                 const Res r = ingest_one(x, g);
