@@ -373,31 +373,38 @@ __device__ __forceinline__ uint64_t lowest_bits(uint64_t m, uint32_t n, uint32_t
     return m & ((1ull << nth_set_bit(m, n)) - 1ull);
 }
 // The wave's selections as alloc_addr entries, written coalesced.  Lane l took
-// the lowest n of the set bits of m (word wl = w0 + l); the wave's selections
-// are the ordinals [g0, g0 + total) in lane order.  Output p = lane + 64 q: its
-// owner lane (the first whose inclusive count exceeds p, a binary search over
-// the counts in LDS) and the (p - owner's exclusive count)-th set bit of the
-// owner's word.  Only this rank's ordinals [lo_g, hi_g) are recorded.
-__device__ __forceinline__ void wave_write_addrs(const DevState& S, uint32_t* sh_in, uint64_t* sh_m, uint64_t g0, uint32_t n,
-                                                 uint64_t m, uint64_t w0, uint64_t lo_g, uint64_t hi_g) {
+// the lowest n of the set bits of m (word w0 + l); the wave's selections are the
+// ordinals [g0, g0 + total) in lane order.  Every word taken whole (a fresh
+// fleet's run of free words): the addresses are the words' bits in order, one
+// entry per lane per store.  Otherwise lane by lane (a uniform walk over the
+// lanes that took bits): the wave writes lane j's selections together, lane l
+// its (l)-th set bit.  Only this rank's ordinals [lo_g, hi_g) are recorded.
+__device__ __forceinline__ void wave_write_addrs(const DevState& S, uint64_t g0, uint32_t n, uint64_t m, uint64_t w0,
+                                                 uint64_t lo_g, uint64_t hi_g) {
     const uint32_t l = lane_id();
     const uint32_t incl = wave_incl_scan(n);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total == 0) return;
     if (g0 >= hi_g || g0 + total <= lo_g) return;
-    sh_in[l] = incl;
-    sh_m[l] = m;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (uint32_t p = l; p < total; p += 64) {
-        uint32_t o = 0;
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1) o = sh_in[o + st - 1] <= p ? o + st : o;
-        const uint32_t ex = o ? sh_in[o - 1] : 0u;
-        const uint32_t bit = nth_set_bit(sh_m[o], p - ex);
-        const uint64_t g = g0 + p;
-        if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)((w0 + o) * 64 + bit);
+    if (__ballot(n != 64u) == 0) {
+        for (uint32_t p = l; p < total; p += 64) {
+            const uint64_t g = g0 + p;
+            if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)(w0 * 64 + p);
+        }
+        return;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reads before the next list's writes
+    const uint32_t ex = incl - n;
+    for (uint64_t act = __ballot(n != 0); act; act &= act - 1) {
+        const int j = (int)__builtin_ctzll(act);
+        const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
+        const uint32_t exj = (uint32_t)__builtin_amdgcn_readlane((int)ex, j);
+        const uint64_t mj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, j) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), j) << 32);
+        if (l < nj) {
+            const uint64_t g = g0 + exj + l;
+            if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)((w0 + (uint32_t)j) * 64 + nth_set_bit(mj, l));
+        }
+    }
 }
 
 // select + commit for word-block wb.  Allocation ordinal g (global, canonical order):
@@ -414,12 +421,9 @@ __device__ __forceinline__ void wave_write_addrs(const DevState& S, uint32_t* sh
 // scattered store per address: the 1M x 10M initial tick's 10M fresh Gets).
 __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
                                    uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out) {
-    __shared__ uint32_t sh_in[BLOCK / 64][64];
-    __shared__ uint64_t sh_m[BLOCK / 64][64];
     const uint64_t take = p.take, fin = p.fin;
     const uint64_t cb = cursor_bit(S);
     const bool advance = fin > 0 && p.fout == 0;
-    const uint32_t wv = threadIdx.x >> 6;
     for (int k = 0; k < POOL_WPT; k++) {
         const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
         const bool valid = w < S.pool.words;
@@ -442,8 +446,8 @@ __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t w
                              ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ru >> 32)) << 32);
         const uint64_t gf0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)rf) |
                              ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rf >> 32)) << 32);
-        wave_write_addrs(S, sh_in[wv], sh_m[wv], gu0, nu, wu, w0, lo_g, hi_g);
-        wave_write_addrs(S, sh_in[wv], sh_m[wv], take + gf0, nf, wf, w0, lo_g, hi_g);
+        wave_write_addrs(S, gu0, nu, wu, w0, lo_g, hi_g);
+        wave_write_addrs(S, take + gf0, nf, wf, w0, lo_g, hi_g);
         base_u += tot[0];
         base_f += tot[1];
     }
