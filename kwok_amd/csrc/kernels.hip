@@ -1115,10 +1115,13 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
         bool dirty = false;
         uint16_t nst[POD_PER_THREAD];
         uint32_t ai = 0;
+        // the group's 8 slots share a bucket (bk0 + j): handles without a division
+        const uint32_t gb = bk0 + gi.j;
+        const int32_t h0 = (int32_t)((S.b_lo + gb) * S.pod_stride + (gi.slot - gb * S.cp));
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
             const uint32_t slot = gi.slot + k;
-            const int32_t handle = pod_handle_of(S, slot);
+            const int32_t handle = h0 + k;
             uint16_t s = gi.st(k);
             if (cl[i][k].del) {
                 const uint64_t ord = r.v[AG_DEL] + vdel++;
