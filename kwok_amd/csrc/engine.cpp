@@ -404,18 +404,19 @@ constexpr size_t NODE_PAR_MIN = 2048;  // node records (the per-record work is h
 // with sequential reads of the records and their strings.  The threaded ingest
 // groups these by partition and bucket, so the slot-policy pass reads them in
 // order instead of gathering the caller's records from all over the batch.
-struct PodPrep {
+struct PodPrep {  // 32 bytes: the scatter and the slot-policy pass move these
     uint32_t idx, bkt;      // record index; owned local bucket (NO_BUCKET: the record changes no slot)
-    int32_t handle, node_handle, spec_id;
     uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: pip = the parsed podIP
     uint32_t ctime;
-    uint32_t slot;          // handle >= 0: its local slot (bkt * Cp + index), when pst == KWOK_OK
+    uint32_t slot;          // PREP_EXISTING: the handle's local pod slot (bkt * Cp + index);
+                            // a create by node handle: the node's local slot (when pst == KWOK_OK)
+    uint16_t spec;          // UPSERT with fst == KWOK_OK: the spec id
     uint8_t op, phase, flags, chk;  // chk: PREP_*
     int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
-    int8_t pst;             // handle >= 0: pod_slot's status
-    kwok_str node_name;
+    int8_t pst;             // PREP_EXISTING: pod_slot's status; create by node handle: KWOK_ENOTMINE or OK
 };
-enum : uint8_t { PREP_ARENA_BAD = 1, PREP_DEL_IP = 2 };
+static_assert(sizeof(PodPrep) == 32, "prepared pod records are 32 bytes");
+enum : uint8_t { PREP_ARENA_BAD = 1, PREP_DEL_IP = 2, PREP_EXISTING = 4, PREP_BY_NAME = 8 };
 constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 
 // ---- per-batch op coalescing: ops for the same slot compose in order ----
@@ -1594,10 +1595,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     auto prep = [&](size_t i, PodPrep& r) {
         const kwok_pod_event& x = ev[i];
         r.idx = (uint32_t)i;
-        r.handle = x.handle, r.node_handle = x.node_handle, r.spec_id = x.spec_id;
         r.op = x.op, r.phase = x.phase, r.flags = x.flags, r.chk = 0;
-        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK, r.slot = 0, r.pst = KWOK_OK;
-        r.node_name = x.node_name;
+        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK, r.slot = 0, r.pst = KWOK_OK, r.spec = 0;
         r.bkt = NO_BUCKET;
         if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
             r.chk = PREP_ARENA_BAD;
@@ -1611,9 +1610,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             else if (x.spec_id < 0 || (size_t)x.spec_id >= n_specs) r.fst = KWOK_EINVAL;
             else if (x.phase > KWOK_PHASE_UNKNOWN) r.fst = KWOK_EINVAL;
             else if (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll) r.fst = KWOK_EDOMAIN;
-            else r.ctime = (uint32_t)x.creation_unix;
+            else r.ctime = (uint32_t)x.creation_unix, r.spec = (uint16_t)x.spec_id;  // max_pod_specs <= 65535
         }
         if (x.handle >= 0) {
+            r.chk |= PREP_EXISTING;
             r.pst = (int8_t)e->pod_slot(x.handle, &r.slot);
             if (r.pst == KWOK_OK) r.bkt = r.slot / e->Cp;
             return;
@@ -1621,9 +1621,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         if (x.op != KWOK_OP_UPSERT) return;
         if (x.node_handle >= 0) {
             const int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
-            if (l >= 0 && l < (int64_t)e->NL) r.bkt = (uint32_t)(l / e->Cn);
+            if (l >= 0 && l < (int64_t)e->NL) r.bkt = (uint32_t)(l / e->Cn), r.slot = (uint32_t)l;
+            else r.pst = KWOK_ENOTMINE;
             return;
         }
+        r.chk |= PREP_BY_NAME;  // the name is read again from the record (rare: callers pass node handles)
         if (!x.node_name.len || x.node_name.len > 253) return;
         const uint32_t b = fnv1a32(arena + x.node_name.off, x.node_name.len) & (e->B - 1);
         if (e->owns(b)) r.bkt = b - e->b_lo;
@@ -1639,7 +1641,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         uint32_t released = 0;
         if (x.chk & PREP_ARENA_BAD) st = KWOK_EDOMAIN;
         uint32_t slot = 0;
-        const bool existing = x.handle >= 0;
+        const bool existing = x.chk & PREP_EXISTING;
         // existing handles: bkt = slot / Cp (prep); no divisions below
         const uint32_t bl0 = x.bkt;
         if (st == KWOK_OK && existing) {
@@ -1681,15 +1683,14 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             st = x.fst;
             uint32_t nslot = 0;
             if (st == KWOK_OK && !existing) {
-                if (x.node_handle >= 0) {
-                    int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
-                    if (l < 0 || l >= (int64_t)e->NL) st = KWOK_ENOTMINE;
-                    else if (!e->nodes[(uint32_t)l].used) st = KWOK_ENOTFOUND;
-                    else nslot = (uint32_t)l;
-                } else if (!x.node_name.len || x.node_name.len > 253) {
-                    st = KWOK_EDOMAIN;
+                if (!(x.chk & PREP_BY_NAME)) {
+                    st = x.pst;  // KWOK_ENOTMINE: another rank's (or no) node slot
+                    if (st == KWOK_OK && !e->nodes[x.slot].used) st = KWOK_ENOTFOUND;
+                    else nslot = x.slot;
                 } else {
-                    st = node_slot(e, arena + x.node_name.off, x.node_name.len, true, &nslot);
+                    const kwok_str nm = ev[x.idx].node_name;
+                    if (!nm.len || nm.len > 253) st = KWOK_EDOMAIN;
+                    else st = node_slot(e, arena + nm.off, nm.len, true, &nslot);
                 }
                 if (st == KWOK_OK) {
                     bl = x.bkt != NO_BUCKET ? x.bkt : nslot / e->Cn;  // the node's bucket (prep)
@@ -1740,7 +1741,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 o.bits = bits;
                 o.set_fields = 1;
                 o.node = hp.node;
-                o.spec = (uint16_t)x.spec_id;
+                o.spec = x.spec;
                 o.ctime = x.ctime;
                 o.host_ip = hip;
                 o.pod_ip = pip;
@@ -1762,7 +1763,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     // A bucket that this batch's creates would fill grows first (every bucket to a
     // larger capacity, up to the handle stride): creates[bl] counts them, ignoring
     // the slots this batch's deletes free (an upper bound)
-    auto is_create = [](const PodPrep& x) { return x.op == KWOK_OP_UPSERT && x.handle < 0 && x.bkt != NO_BUCKET; };
+    auto is_create = [](const PodPrep& x) { return x.op == KWOK_OP_UPSERT && !(x.chk & PREP_EXISTING) && x.bkt != NO_BUCKET; };
     auto grow_for = [&](const std::vector<uint32_t>& creates) -> int {
         uint64_t need = 0;
         for (uint32_t b = 0; b < e->nb; b++)
@@ -1838,8 +1839,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                     for (size_t i = lo; i < hi; i++) {
                         uint32_t sl = 0;
                         PodPrep& r = pre[i];
-                        if (r.handle < 0 || (r.chk & PREP_ARENA_BAD)) continue;
-                        r.pst = (int8_t)e->pod_slot(r.handle, &sl);
+                        if (!(r.chk & PREP_EXISTING)) continue;
+                        r.pst = (int8_t)e->pod_slot(ev[r.idx].handle, &sl);
                         r.slot = sl;
                         const uint32_t nbk = r.pst == KWOK_OK ? sl / e->Cp : NO_BUCKET;
                         k[key(r.bkt)]--;
@@ -1882,7 +1883,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
                 if (k + PF < k1) {
                     const PodPrep& y = srt[k + PF];
                     __builtin_prefetch(&all[y.idx], 1);
-                    if (y.bkt != NO_BUCKET && y.handle >= 0) __builtin_prefetch(&e->pods[y.slot], 1);
+                    if (y.bkt != NO_BUCKET && (y.chk & PREP_EXISTING)) __builtin_prefetch(&e->pods[y.slot], 1);
                 }
                 const PodPrep& x = srt[k];
                 const Res r = ingest_one(x, g);
