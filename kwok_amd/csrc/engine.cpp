@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <time.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -50,6 +51,33 @@ uint32_t fnv1a32(const char* s, size_t n) {
     }
     return h;
 }
+
+// Host scratch on 2 MiB pages where the kernel grants them (madvise): the
+// threaded ingest scatters records over ~4k bucket runs of tens of MB, and with
+// 4 KiB pages each run is a TLB miss
+struct HugeBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    HugeBuf() = default;
+    HugeBuf(const HugeBuf&) = delete;
+    HugeBuf& operator=(const HugeBuf&) = delete;
+    ~HugeBuf() { free(p); }
+    void* get(size_t need) {
+        if (need <= n) return p;
+        free(p);
+        const size_t huge = (size_t)2 << 20;
+        const size_t sz = (need + need / 8 + huge - 1) & ~(huge - 1);
+        p = aligned_alloc(huge, sz);
+        if (!p) {
+            n = 0;
+            return nullptr;
+        }
+        (void)madvise(p, sz, MADV_HUGEPAGE);
+        memset(p, 0, sz);  // first touch here, not inside a batch's passes
+        n = sz;
+        return p;
+    }
+};
 
 template <class T>
 struct DevBuf {
@@ -186,10 +214,10 @@ struct kwok_engine {
     uint32_t gen = 1;  // ops of the unflushed batch carry stamp == gen (flush_ops advances it)
     // threaded-ingest scratch, kept between calls (fresh allocations would page-fault
     // on first touch, from every thread at once)
-    std::vector<uint64_t> ing_res;
+    HugeBuf ing_res;
     // pod records, validated and parsed in batch order (PodPrep, below), grouped by
     // partition, then by bucket inside each partition
-    std::vector<unsigned char> ing_prep, ing_sorted;
+    HugeBuf ing_prep, ing_sorted;
     Stage& stage_of(uint32_t bucket_local) { return stage[(size_t)((uint64_t)bucket_local * n_part / nb)]; }
     void* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -1806,12 +1834,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         // copied out per contiguous record range.
         const int P = e->n_part;
         const uint32_t NB1 = e->nb + 1;  // key 0: records that change nothing; key b + 1: bucket b
-        if (e->ing_res.size() < n) e->ing_res.resize(n);
-        if (e->ing_prep.size() < n * sizeof(PodPrep)) e->ing_prep.resize(n * sizeof(PodPrep) + n * sizeof(PodPrep) / 8);
-        if (e->ing_sorted.size() < n * sizeof(PodPrep)) e->ing_sorted.resize(n * sizeof(PodPrep) + n * sizeof(PodPrep) / 8);
-        PodPrep* pre = reinterpret_cast<PodPrep*>(e->ing_prep.data());    // pass 1 output (batch order)
-        PodPrep* srt = reinterpret_cast<PodPrep*>(e->ing_sorted.data());  // pass 2 output (by bucket)
-        uint64_t* all = e->ing_res.data();  // per record: handle | status << 32 (released: below)
+        PodPrep* pre = static_cast<PodPrep*>(e->ing_prep.get(n * sizeof(PodPrep)));    // pass 1 output (batch order)
+        PodPrep* srt = static_cast<PodPrep*>(e->ing_sorted.get(n * sizeof(PodPrep)));  // pass 2 output (by bucket)
+        uint64_t* all = static_cast<uint64_t*>(e->ing_res.get(n * sizeof(uint64_t)));  // per record: handle | status << 32
+        if (!pre || !srt || !all) return e->fail(KWOK_ENOMEM, "ingest scratch for %zu records", n);
         auto key = [](uint32_t b) { return b == NO_BUCKET ? 0u : b + 1u; };
         std::vector<uint32_t> cnt((size_t)P * NB1, 0);  // [chunk][key], then scatter positions
         std::vector<std::vector<uint32_t>> creates((size_t)P);  // per chunk: creates per bucket
