@@ -134,25 +134,34 @@ def cpu_baseline(nodes, threads, ticks):
                       % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
 
 
-def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
+def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
     kwok_ingest_pods of that batch (2 x n_churn records, host threads + H2D +
     apply kernel) + one kwok_tick (1M deletes + releases, 1M Pending->Running
     patches reusing the released IPs).  Event generation (which reads the pod
-    IPs back) sits between the timed steps.  The first step is warmup."""
-    n_handles = workload.BUCKETS * fl.cp
-    ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=7)
-    dump = lambda: e.dump_pods(0, n_handles)  # noqa: E731
+    IPs back) sits between the timed steps.  The first step is warmup.
+    world > 1: every rank churns n_churn of its own pods per tick (weak
+    scaling); the releases of all ranks cross the exchange (their lists are
+    longer than the inline message: the second allgather), and each step is
+    timed between barriers, max over ranks."""
+    barrier = barrier or torch.cuda.synchronize
+    max_over_ranks = max_over_ranks or (lambda x: x)
+    lo = rank * workload.BUCKETS // world
+    hi = (rank + 1) * workload.BUCKETS // world
+    n_handles = (hi - lo) * fl.cp
+    ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=7,
+                        first=lo * fl.cp)
+    dump = lambda: e.dump_pods(lo * fl.cp, n_handles)  # noqa: E731
     ing = tck = 0.0
     trans = recs = 0
-    kern = emit = 0.0
+    kern = emit = xch = 0.0
     last = None
     steps = []
     for k in range(ticks + 2):
         ev, ar = ch.batch(dump, now)
-        torch.cuda.synchronize()
+        barrier()
         prof = k == ticks + 1  # one more step, profiled (HIP events), for the kernel times only
         if prof:
             e.profile_enable(True)
@@ -161,31 +170,38 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn):
         t1 = time.perf_counter()
         r = e.tick(now, read=False)
         t2 = time.perf_counter()
+        if world > 1:
+            barrier()
+            t2 = time.perf_counter()
         ch.applied(hs, st)
         now += 30
         if prof:
             ph, nt = e.profile_read()
             e.profile_enable(False)
-            kern, emit = ph["kernel"] * ticks, ph["emit_kernel"] * ticks
+            kern, emit, xch = ph["kernel"] * ticks, ph["emit_kernel"] * ticks, ph["exchange"] * ticks
         elif k:
-            ing += t1 - t0
-            tck += t2 - t1
-            steps.append((t1 - t0, t2 - t1))
+            a, b = max_over_ranks(t1 - t0), max_over_ranks(t2 - t0)
+            ing += a
+            tck += b - a
+            steps.append((a, b - a))
             trans += transitions(r.counters)
             recs += len(ev)
             last = dict(zip(abi.COUNTERS, list(r.counters)))
     return now, {
         "workload": "C4 pod churn storm (BASELINE configs[3]) on the metric fleet: %d deletion-marked pods (50%% with "
-                    "finalizers) + %d creates per tick" % (n_churn, n_churn),
-        "ticks": ticks, "records_per_tick": recs // max(ticks, 1),
+                    "finalizers) + %d creates per tick%s" % (n_churn, n_churn, " per rank" if world > 1 else ""),
+        "ticks": ticks, "records_per_tick": recs // max(ticks, 1) * world,
         "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
         "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
         "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
                       "ingest": float(np.median([a for a, _ in steps])) * 1e3,
                       "tick": float(np.median([b for _, b in steps])) * 1e3},
-        "ingest_records_per_s": recs / ing if ing else None,
+        "ingest_records_per_s": recs * world / ing if ing else None,
         "tick_transitions_per_s": trans / tck if tck else None,
         "kernel_ms": kern / ticks, "k_emit_ms": emit / ticks,
+        # multi-rank tick: the FRONT header to the (last) BACK launch's start -
+        # allgather, and for long lists the host round trip, second allgather, k_pool_apply
+        "exchange_ms": xch / ticks if (world > 1 or os.environ.get("KWOK_FORCE_MULTI")) else None,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods (record validation, IP parsing, slot policy on host threads, "
                 "H2D of the coalesced ops, k_apply_pod_ops); event generation between steps untimed (the GPU idles "
@@ -389,8 +405,9 @@ def main():
     e.profile_enable(False)
 
     churn = None
-    if world == 1 and a.churn_ticks > 0:
-        now, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank)
+    if a.churn_ticks > 0:
+        now, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, rank, world, barrier,
+                               max_over_ranks)
 
     e.close()
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None

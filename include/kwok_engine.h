@@ -318,6 +318,14 @@ int kwok_tick(kwok_engine* e, int64_t now_unix, kwok_tick_result* res);
 int kwok_tick_submit(kwok_engine* e, int64_t now_unix);
 int kwok_tick_collect(kwok_engine* e, kwok_tick_result* res);
 int kwok_read_outputs(kwok_engine* e, kwok_outputs* out);
+/* Bytes [off, off + len) of the last collected tick's output arena (the arena
+ * offsets kwok_read_outputs reports without KWOK_READ_HEARTBEAT_ONCE:
+ * heartbeat_off, node_init_off[i], pod_patch_off[i]) copied into dst.  For
+ * callers that read the patches in bounded pieces: the initial tick of a
+ * 1M-node / 10M-pod fleet is ~7 GB of patches (a cgo caller must not size one
+ * copy with a C int).  The patches lie in increasing offset order (node inits,
+ * then pod patches, each in canonical order).  KWOK_EINVAL outside the arena. */
+int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst);
 
 /* The constant merge patch sent before Delete when a pod has finalizers
  * (removeFinalizers, pod_controller.go:45). */

@@ -28,11 +28,16 @@ import (
 
 // output kinds handed to the apply callback of tick
 const (
-	kindHeartbeat = iota
-	kindNodeInit
-	kindPodPatch
-	kindDelete // | 1: the pod has finalizers (kwok_finalizer_patch first)
+	kindHeartbeat = iota // configureHeartbeatNode body (node_controller.go:393-401)
+	kindNodeInit         // configureNode body (node_controller.go:356-391)
+	kindPodPatch         // configurePod body (pod_controller.go:377-402)
+	kindDelete           // DeletePod of a pod without finalizers: Delete(grace 0) (pod_controller.go:155-183)
+	kindDeleteFin        // DeletePod of a pod with finalizers: kwok_finalizer_patch, then Delete
 )
+
+// readChunk bounds one kwok_read_arena copy: the initial tick of a 1M-node /
+// 10M-pod fleet is ~7 GB of patches, read and handed out piece by piece
+const readChunk = 64 << 20
 
 func boolToC(b bool) C.int32_t {
 	if b {
@@ -193,12 +198,14 @@ func finalizerPatch() []byte {
 	return C.GoBytes(unsafe.Pointer(p), C.int(n))
 }
 
-// tick runs one heartbeat interval and hands every body to apply.  The host
-// copy holds ONE heartbeat body (all bodies of a tick are identical,
-// node_controller.go:393-401) and the node-init / pod patch region: a steady
-// tick at 1M nodes moves ~1 KB over PCIe, not 1 GB.  The heartbeat handle
-// list is read only when its epoch changed.  The body slices stay valid after
-// tick returns (they alias one Go buffer).
+// tick runs one heartbeat interval and hands every body to apply.  The lists
+// come first (kwok_read_outputs without an arena); then ONE heartbeat body (all
+// bodies of a tick are identical, node_controller.go:393-401) and the node-init
+// / pod patches in bounded pieces (kwok_read_arena, 64-bit offsets), each copied
+// once, straight into Go memory (the engine keeps no pointer past the call).  A
+// steady tick at 1M nodes moves ~1 KB over PCIe, not 1 GB.  The heartbeat handle
+// list is read only when its epoch changed.  Body slices stay valid after tick
+// returns (each aliases its piece's buffer).
 func (g *gpuEngine) tick(nowUnix int64, apply func(kind int, handle int32, body []byte)) error {
 	var res C.kwok_tick_result
 	if rc := C.kwok_tick(g.h, C.int64_t(nowUnix), &res); rc != C.KWOK_OK {
@@ -216,13 +223,7 @@ func (g *gpuEngine) tick(nowUnix int64, apply func(kind int, handle int32, body 
 	ppLen := make([]uint32, res.n_pod_patch)
 	del := make([]int32, res.n_delete)
 	delFin := make([]uint8, res.n_delete)
-	need := uint64(res.arena_bytes)
-	if res.n_heartbeat > 1 {
-		need -= uint64(res.n_heartbeat-1) * uint64(res.heartbeat_stride)
-	}
-	arena := C.malloc(C.size_t(need) + 1) // C memory: the engine copies into it
-	defer C.free(arena)
-	out := C.kwok_outputs{arena: (*C.uint8_t)(arena), arena_cap: C.uint64_t(need), flags: C.KWOK_READ_HEARTBEAT_ONCE}
+	var out C.kwok_outputs // no arena: the bytes follow through kwok_read_arena
 	if len(g.hb) > 0 && newEpoch {
 		out.heartbeat_nodes = (*C.int32_t)(&g.hb[0])
 	}
@@ -241,25 +242,105 @@ func (g *gpuEngine) tick(nowUnix int64, apply func(kind int, handle int32, body 
 		return fmt.Errorf("kwok_read_outputs: %s", g.lastError())
 	}
 	g.hbEpoch = uint32(res.heartbeat_epoch)
-	buf := C.GoBytes(arena, C.int(out.arena_copied))
-	shift := uint64(out.arena_shift)
 	if res.n_heartbeat > 0 {
-		body := buf[:res.heartbeat_len] // the heartbeat body, sent to every managed node
+		body := make([]byte, res.heartbeat_len) // the heartbeat body, sent to every managed node
+		if err := g.readArena(uint64(out.heartbeat_off), body); err != nil {
+			return err
+		}
 		for _, h := range g.hb {
 			apply(kindHeartbeat, h, body)
 		}
 	}
-	for i, h := range ini {
-		apply(kindNodeInit, h, buf[iniOff[i]-shift:iniOff[i]-shift+uint64(iniLen[i])])
+	if err := g.applyPatches(kindNodeInit, ini, iniOff, iniLen, apply); err != nil {
+		return err
 	}
-	for i, h := range pp {
-		apply(kindPodPatch, h, buf[ppOff[i]-shift:ppOff[i]-shift+uint64(ppLen[i])])
+	if err := g.applyPatches(kindPodPatch, pp, ppOff, ppLen, apply); err != nil {
+		return err
 	}
-	for i, h := range del { // Patch(removeFinalizers) if delFin[i], then Delete(grace 0)
-		apply(kindDelete|int(delFin[i]), h, nil)
+	for i, h := range del { // Patch(removeFinalizers) if the pod has finalizers, then Delete(grace 0)
+		if delFin[i] != 0 {
+			apply(kindDeleteFin, h, nil)
+		} else {
+			apply(kindDelete, h, nil)
+		}
 	}
 	return nil
 }
+
+// applyPatches: the patches at offs[i] / lens[i] (increasing offsets), read in
+// pieces of at most readChunk bytes (a single larger patch is one piece)
+func (g *gpuEngine) applyPatches(kind int, hs []int32, offs []uint64, lens []uint32,
+	apply func(kind int, handle int32, body []byte)) error {
+	for i := 0; i < len(hs); {
+		lo := offs[i]
+		j := i + 1
+		for j < len(hs) && offs[j]+uint64(lens[j])-lo <= readChunk {
+			j++
+		}
+		buf := make([]byte, offs[j-1]+uint64(lens[j-1])-lo)
+		if err := g.readArena(lo, buf); err != nil {
+			return err
+		}
+		for k := i; k < j; k++ {
+			apply(kind, hs[k], buf[offs[k]-lo:offs[k]-lo+uint64(lens[k])])
+		}
+		i = j
+	}
+	return nil
+}
+
+// readArena copies arena bytes [off, off+len(buf)) of the collected tick into buf
+func (g *gpuEngine) readArena(off uint64, buf []byte) error {
+	if len(buf) == 0 {
+		return nil
+	}
+	if rc := C.kwok_read_arena(g.h, C.uint64_t(off), C.uint64_t(len(buf)), unsafe.Pointer(&buf[0])); rc != C.KWOK_OK {
+		return fmt.Errorf("kwok_read_arena: %s", g.lastError())
+	}
+	return nil
+}
+
+// ---- EnableCNI: configurePod's cni.Setup (pod_controller.go:383-389) ----------
+
+// cniPending: the pods the next tick evaluates that hold no podIP, canonical order
+func (g *gpuEngine) cniPending() ([]int32, error) {
+	var n C.size_t
+	if rc := C.kwok_cni_pending(g.h, nil, 0, &n); rc != C.KWOK_OK && n == 0 {
+		return nil, fmt.Errorf("kwok_cni_pending: %s", g.lastError())
+	}
+	hs := make([]int32, n)
+	if n == 0 {
+		return hs, nil
+	}
+	if rc := C.kwok_cni_pending(g.h, (*C.int32_t)(&hs[0]), C.size_t(len(hs)), &n); rc != C.KWOK_OK {
+		return nil, fmt.Errorf("kwok_cni_pending: %s", g.lastError())
+	}
+	return hs[:n], nil
+}
+
+// cniAssign: the first IP cni.Setup returned per pod (IPv4, host order)
+func (g *gpuEngine) cniAssign(hs []int32, ips []uint32) error {
+	if len(hs) == 0 {
+		return nil
+	}
+	st := make([]int32, len(hs))
+	if rc := C.kwok_cni_assign(g.h, (*C.int32_t)(&hs[0]), (*C.uint32_t)(&ips[0]), C.size_t(len(hs)),
+		(*C.int32_t)(&st[0])); rc < 0 {
+		return fmt.Errorf("kwok_cni_assign: %s", g.lastError())
+	}
+	return nil
+}
+
+// nodeHas / nodeSize: NodeController.Has / Size (node_controller.go:403-409)
+func (g *gpuEngine) nodeHas(name string) bool {
+	if name == "" {
+		return false
+	}
+	b := []byte(name)
+	return C.kwok_node_has(g.h, (*C.char)(unsafe.Pointer(&b[0])), C.size_t(len(b))) != 0
+}
+
+func (g *gpuEngine) nodeSize() int { return int(C.kwok_node_size(g.h)) }
 
 // ---- host codec: watch objects as JSON -> records (kwok_decode_*) ----------
 

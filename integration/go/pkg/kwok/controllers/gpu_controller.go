@@ -18,8 +18,10 @@ import "C"
 
 import (
 	"context"
+	"encoding/binary"
 	"encoding/json"
 	"fmt"
+	"net"
 	"runtime"
 	"sync"
 	"time"
@@ -30,6 +32,7 @@ import (
 	"k8s.io/apimachinery/pkg/types"
 	"k8s.io/apimachinery/pkg/watch"
 
+	"sigs.k8s.io/kwok/pkg/cni"
 	"sigs.k8s.io/kwok/pkg/log"
 )
 
@@ -70,6 +73,7 @@ type GPUController struct {
 	// tick loop only
 	nodeName map[int32]string // node handle -> name
 	podByUID map[types.UID]int32
+	podUID   map[int32]types.UID // pod handle -> UID (the reverse of podByUID)
 	podRef   map[int32]types.NamespacedName
 }
 
@@ -89,7 +93,8 @@ func newGPUController(conf Config, interval time.Duration) (*GPUController, erro
 	}
 	return &GPUController{
 		conf: conf, eng: eng, codec: codec, interval: interval, finalizer: finalizerPatch(),
-		nodeName: map[int32]string{}, podByUID: map[types.UID]int32{}, podRef: map[int32]types.NamespacedName{},
+		nodeName: map[int32]string{}, podByUID: map[types.UID]int32{}, podUID: map[int32]types.UID{},
+		podRef: map[int32]types.NamespacedName{},
 	}, nil
 }
 
@@ -203,8 +208,14 @@ func (c *GPUController) loop(ctx context.Context) {
 	}
 }
 
-// step: ingest the batches (nodes first, so new pods find their node), run the
-// tick, hand every body to the task pool
+// Has / Size: NodeController.Has / Size (node_controller.go:403-409) of the
+// engine's managed-node set
+func (c *GPUController) Has(nodeName string) bool { return c.eng.nodeHas(nodeName) }
+func (c *GPUController) Size() int               { return c.eng.nodeSize() }
+
+// step: ingest the batches (nodes first, so new pods find their node), give
+// the tick's pending pods their CNI IPs (EnableCNI), run the tick, hand every
+// body to the task pool
 func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int64) (int, error) {
 	c.mu.Lock()
 	nb, pb := c.nodes, c.pods
@@ -213,8 +224,13 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 	if err := c.flushNodes(ctx, nb); err != nil {
 		return 0, err
 	}
-	if err := c.flushPods(ctx, pb); err != nil {
+	if err := c.flushPods(ctx, tasks, pb); err != nil {
 		return 0, err
+	}
+	if c.conf.EnableCNI {
+		if err := c.setupCNI(ctx, tasks); err != nil {
+			return 0, err
+		}
 	}
 	logger := log.FromContext(ctx)
 	nodesAPI := c.conf.ClientSet.CoreV1().Nodes()
@@ -239,12 +255,12 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 					logger.Error("Failed to lock pod", err, "pod", ref.String())
 				}
 			})
-		default: // DeletePod (pod_controller.go:155-183); the engine freed the handle
-			ref, fin := c.podRef[h], kind&1 != 0
+		case kindDelete, kindDeleteFin: // DeletePod (pod_controller.go:155-183); the engine freed the handle
+			ref, fin := c.podRef[h], kind == kindDeleteFin
 			gone = append(gone, h)
 			tasks.Add(func() {
 				pods := c.conf.ClientSet.CoreV1().Pods(ref.Namespace)
-				if fin {
+				if fin { // only pods with finalizers (len(pod.Finalizers) != 0, :161)
 					if _, err := pods.Patch(ctx, ref.Name, types.MergePatchType, c.finalizer, metav1.PatchOptions{}); err != nil {
 						if !apierrors.IsNotFound(err) {
 							logger.Error("Failed to patch pod finalizers", err, "pod", ref.String())
@@ -258,16 +274,46 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 			})
 		}
 	})
-	for _, h := range gone { // the later Deleted watch event finds no handle and is dropped
-		for uid, hh := range c.podByUID {
-			if hh == h {
-				delete(c.podByUID, uid)
-				break
-			}
-		}
+	for _, h := range gone { // the later Deleted watch event finds no handle (CNI: it still runs cni.Remove)
+		delete(c.podByUID, c.podUID[h])
+		delete(c.podUID, h)
 		delete(c.podRef, h)
 	}
 	return n, err
+}
+
+// setupCNI: configurePod's cni.Setup for the pods the next tick evaluates that
+// hold no podIP (pod_controller.go:383-389), 16 at a time; the engine patches
+// them with the first returned IP.  A failed Setup leaves the pod unpatched
+// this tick, as configurePod's error does.
+func (c *GPUController) setupCNI(ctx context.Context, tasks *parallelTasks) error {
+	hs, err := c.eng.cniPending()
+	if err != nil || len(hs) == 0 {
+		return err
+	}
+	logger := log.FromContext(ctx)
+	ips := make([]uint32, len(hs))
+	for i, h := range hs {
+		i, uid, ref := i, c.podUID[h], c.podRef[h]
+		tasks.Add(func() {
+			got, err := cni.Setup(ctx, string(uid), ref.Name, ref.Namespace)
+			if err != nil {
+				logger.Error("cni setup", err, "pod", ref.String())
+				return
+			}
+			if ip := net.ParseIP(got[0]).To4(); ip != nil {
+				ips[i] = binary.BigEndian.Uint32(ip)
+			}
+		})
+	}
+	tasks.Wait()
+	keep, kept := hs[:0], ips[:0]
+	for i := range hs {
+		if ips[i] != 0 {
+			keep, kept = append(keep, hs[i]), append(kept, ips[i])
+		}
+	}
+	return c.eng.cniAssign(keep, kept)
 }
 
 func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
@@ -307,61 +353,104 @@ func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
 	return nil
 }
 
-func (c *GPUController) flushPods(ctx context.Context, b objBatch) error {
+// flushPods ingests the batch in event order.  A pod's first event in the
+// batch may create it (handle -1); its later events need that handle, so the
+// batch is cut into runs in which no new pod appears twice: run k+1 is
+// ingested after run k, once run k's handles are known.  (Added then Modified,
+// or Added then Deleted, within one interval: one slot, then its update or its
+// Deleted event with the pod's podIP release, pod_controller.go:329-336.)
+func (c *GPUController) flushPods(ctx context.Context, tasks *parallelTasks, b objBatch) error {
 	if len(b.offs) == 0 {
 		return nil
 	}
 	logger := log.FromContext(ctx)
 	docs, st := c.codec.decodePods(b.arena, b.offs, b.lens, runtime.NumCPU())
-	evs := make([]C.kwok_pod_event, 0, len(docs))
-	uids := make([]types.UID, 0, len(docs))
-	refs := make([]types.NamespacedName, 0, len(docs))
+	type rec struct {
+		i   int // index in the batch
+		ref types.NamespacedName
+	}
+	var run []rec
+	created := map[types.UID]bool{} // new pods of the current run
+	flush := func() error {
+		evs := make([]C.kwok_pod_event, 0, len(run))
+		keep := run[:0]
+		for _, r := range run {
+			d := &docs[r.i]
+			h, known := c.podByUID[b.uids[r.i]]
+			if b.del[r.i] {
+				// EnableCNI: cni.Remove for a pod on a managed node (pod_controller.go:337-342),
+				// also when the engine deleted it already (its handle is gone)
+				if c.conf.EnableCNI && c.eng.nodeHas(str(b.arena, d.ev.node_name)) {
+					uid, ref := b.uids[r.i], r.ref
+					tasks.Add(func() {
+						if err := cni.Remove(context.Background(), string(uid), ref.Name, ref.Namespace); err != nil {
+							logger.Error("cni remove", err)
+						}
+					})
+				}
+				if !known { // never ingested, or already deleted by the engine
+					continue
+				}
+				d.ev.op = C.KWOK_OP_DELETE // releases status.podIP (pod_controller.go:329-336)
+				d.ev.handle = C.int32_t(h)
+			} else {
+				id, err := c.eng.registerPodSpec(d, b.arena)
+				if err != nil {
+					logger.Warn("Pod spec outside the supported domain", err)
+					continue
+				}
+				d.ev.op = C.KWOK_OP_UPSERT
+				d.ev.handle = -1
+				if known {
+					d.ev.handle = C.int32_t(h)
+				}
+				d.ev.spec_id = C.int32_t(id)
+				d.ev.node_handle = -1
+			}
+			evs = append(evs, d.ev)
+			keep = append(keep, r)
+		}
+		run = run[:0]
+		for k := range created {
+			delete(created, k)
+		}
+		hs, ss, _, err := c.eng.ingestPods(evs, b.arena)
+		if err != nil {
+			return err
+		}
+		for k, r := range keep {
+			if ss[k] != C.KWOK_OK {
+				continue
+			}
+			uid := b.uids[r.i]
+			if evs[k].op == C.KWOK_OP_DELETE {
+				delete(c.podByUID, uid)
+				delete(c.podUID, hs[k])
+				delete(c.podRef, hs[k])
+			} else {
+				c.podByUID[uid] = hs[k]
+				c.podUID[hs[k]] = uid
+				c.podRef[hs[k]] = r.ref
+			}
+		}
+		return nil
+	}
 	for i := range docs {
 		if st[i] != C.KWOK_OK {
 			logger.Warn("Pod outside the supported domain", fmt.Errorf("kwok status %d", st[i]))
 			continue
 		}
+		uid := b.uids[i]
+		if created[uid] { // its handle comes from the run before
+			if err := flush(); err != nil {
+				return err
+			}
+		}
+		if _, known := c.podByUID[uid]; !known && !b.del[i] {
+			created[uid] = true
+		}
 		d := &docs[i]
-		h, known := c.podByUID[b.uids[i]]
-		if b.del[i] {
-			if !known { // never ingested, or already deleted by the engine
-				continue
-			}
-			d.ev.op = C.KWOK_OP_DELETE // releases status.podIP (pod_controller.go:329-336)
-			d.ev.handle = C.int32_t(h)
-		} else {
-			id, err := c.eng.registerPodSpec(d, b.arena)
-			if err != nil {
-				logger.Warn("Pod spec outside the supported domain", err)
-				continue
-			}
-			d.ev.op = C.KWOK_OP_UPSERT
-			d.ev.handle = -1
-			if known {
-				d.ev.handle = C.int32_t(h)
-			}
-			d.ev.spec_id = C.int32_t(id)
-			d.ev.node_handle = -1
-		}
-		evs = append(evs, d.ev)
-		uids = append(uids, b.uids[i])
-		refs = append(refs, types.NamespacedName{Namespace: str(b.arena, d.namespace_), Name: str(b.arena, d.name)})
+		run = append(run, rec{i, types.NamespacedName{Namespace: str(b.arena, d.namespace_), Name: str(b.arena, d.name)}})
 	}
-	hs, ss, _, err := c.eng.ingestPods(evs, b.arena)
-	if err != nil {
-		return err
-	}
-	for i := range evs {
-		if ss[i] != C.KWOK_OK {
-			continue
-		}
-		if evs[i].op == C.KWOK_OP_DELETE {
-			delete(c.podByUID, uids[i])
-			delete(c.podRef, hs[i])
-		} else {
-			c.podByUID[uids[i]] = hs[i]
-			c.podRef[hs[i]] = refs[i]
-		}
-	}
-	return nil
+	return flush()
 }

@@ -248,6 +248,7 @@ struct kwok_engine {
     uint64_t empty_blob = 0;      // the blob of a node with an empty status (every status field absent)
     std::atomic<bool> has_empty_blob{false};
     std::string blob_h;
+    size_t blob_up_lo = SIZE_MAX;  // blob_h bytes from here on are not on the device yet (upload_blobs)
     DevBuf<uint8_t> d_blob;
     uint32_t max_init_len = 0;
 
@@ -687,29 +688,36 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     e->blob_ids.emplace(key, word);
     uint32_t ilen = (uint32_t)b.pre.size() + e->hb_tpl.conds_len + (uint32_t)b.post.size();
     e->max_init_len = std::max(e->max_init_len, ilen);
-    // device copy: SRC_PAD_FRONT zero bytes, the blobs, SRC_PAD_BACK zero bytes (k_emit reads around them)
+    e->blob_up_lo = std::min<size_t>(e->blob_up_lo, off);  // uploaded once per batch (upload_blobs)
+    return word;
+}
+
+// The blobs interned since the last upload -> the device copy (SRC_PAD_FRONT
+// zero bytes, the blobs, SRC_PAD_BACK zero bytes: k_emit reads around them).
+// Once per node batch, after every ingest thread is done appending to blob_h,
+// and synchronised before return: blob_h (pageable) may grow at the next batch.
+int upload_blobs(kwok_engine* e) {
+    if (e->blob_up_lo >= e->blob_h.size()) return KWOK_OK;
+    const size_t lo = e->blob_up_lo;
     const size_t padded = ((SRC_PAD_FRONT + e->blob_h.size() + 3) & ~(size_t)3) + SRC_PAD_BACK;
     if (padded > e->d_blob.n) {
         uint8_t* p = nullptr;
         const size_t cap = std::max<size_t>(padded, 2 * e->d_blob.n);
-        if (hipMalloc((void**)&p, cap) != hipSuccess) {
-            *rc = e->fail(KWOK_ENOMEM, "blob %zu", cap);
-            return 0;
-        }
-        (void)hipMemsetAsync(p, 0, cap, e->st);
-        if (e->d_blob.p) {
-            (void)hipMemcpyAsync(p, e->d_blob.p, SRC_PAD_FRONT + off, hipMemcpyDeviceToDevice, e->st);
-            (void)hipStreamSynchronize(e->st);
-            (void)hipFree(e->d_blob.p);
-        }
+        if (hipMalloc((void**)&p, cap) != hipSuccess) return e->fail(KWOK_ENOMEM, "blob %zu", cap);
+        HIPCHK(e, hipMemsetAsync(p, 0, cap, e->st));
+        if (e->d_blob.p) HIPCHK(e, hipMemcpyAsync(p, e->d_blob.p, SRC_PAD_FRONT + lo, hipMemcpyDeviceToDevice, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+        if (e->d_blob.p) (void)hipFree(e->d_blob.p);
         e->d_blob.p = p;
         e->d_blob.n = cap;
     }
-    (void)hipMemcpyAsync(e->d_blob.p + SRC_PAD_FRONT + off, e->blob_h.data() + off, b.pre.size() + b.post.size(),
-                         hipMemcpyHostToDevice, e->st);
+    HIPCHK(e, hipMemcpyAsync(e->d_blob.p + SRC_PAD_FRONT + lo, e->blob_h.data() + lo, e->blob_h.size() - lo,
+                             hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    e->blob_up_lo = SIZE_MAX;
     e->S.blob = e->d_blob.p + SRC_PAD_FRONT;
     e->S.blob_total = (uint32_t)e->blob_h.size();
-    return word;
+    return KWOK_OK;
 }
 
 bool node_conforms(const kwok_node_event& ev, const std::string info[10]) {
@@ -1218,6 +1226,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_STREAMERS_PER_CU")) wants = std::max(1, atoi(v));
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
         S.n_chain = std::min<uint32_t>((uint32_t)(cus * std::min(occ, want)), (uint32_t)MAX_CHAIN);
+        // KWOK_TICK_CHAIN_BLOCKS: fewer chain blocks, so that the grids of many engines
+        // sharing one GPU (the 8-rank C3 test) are co-resident together
+        if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
         e->n_stream = (uint32_t)(cus * wants);
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
@@ -1597,8 +1608,9 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
             break;
         }
     const auto tn1 = std::chrono::steady_clock::now();
-    int rc = size_arena(e);
+    int rc = upload_blobs(e);
     if (rc) return rc;
+    if ((rc = size_arena(e))) return rc;
     rc = flush_ops(e);
     if (e->iprof)
         fprintf(stderr, "[kwok ingest] %zu node records: records %.2f ms, flush %.2f ms\n", n,
@@ -2232,9 +2244,20 @@ int retire(kwok_engine* e) {
     kwok_engine::TickSlot& T = e->slots[k];
     T.state = SLOT_DONE;
     T.rc = KWOK_OK;
+    // every failure here leaves the device state (advanced by the kernels) and the
+    // host mirrors / the caller's view out of step: the engine is poisoned, and a
+    // tick queued behind this one (it ran on that state) fails with it
     auto failed = [&](int rc) {
         T.rc = rc;
         T.err = e->err;
+        e->poisoned = true;
+        if (next >= 0 && e->slots[next].state == SLOT_QUEUED) {
+            kwok_engine::TickSlot& U = e->slots[next];
+            (void)hipStreamSynchronize(e->st);
+            U.state = SLOT_DONE;
+            U.rc = rc;
+            U.err = e->err;
+        }
         return rc;
     };
     const auto t1 = clk::now();
@@ -2397,6 +2420,7 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     // included) before this one's collectives are enqueued, so every rank issues
     // its collectives in the same order whatever its submit / collect pattern
     if (e->multi) drain(e);
+    if (e->poisoned) return poisoned(e);  // the drained tick failed (its error stays collectable)
     int k = -1;
     for (int pass = 0; pass < 2 && k < 0; pass++)  // prefer keeping the last collected tick's outputs
         for (int i = 0; i < 2 && k < 0; i++)
@@ -2506,6 +2530,24 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
             o->arena_copied = H.arena_bytes;
         }
     }
+    HIPCHK(e, hipStreamSynchronize(st));
+    return KWOK_OK;
+}
+
+int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {
+    if (!e || (len && !dst)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    if (e->cur < 0) return e->fail(KWOK_EINVAL, "no collected tick (or its slot was reused by a submit)");
+    const kwok_engine::TickSlot& S = e->slots[e->cur];
+    const uint64_t total = S.hdr_h->arena_bytes;
+    if (off > total || len > total - off)
+        return e->fail(KWOK_EINVAL, "arena range [%llu, +%llu) outside the tick's %llu bytes", (unsigned long long)off,
+                       (unsigned long long)len, (unsigned long long)total);
+    if (!len) return KWOK_OK;
+    hipStream_t st = e->rst;  // beside a tick queued behind the collected one (as kwok_read_outputs)
+    HIPCHK(e, hipStreamWaitEvent(st, S.done, 0));
+    HIPCHK(e, hipEventRecord(e->fence, st));
+    HIPCHK(e, hipMemcpyAsync(dst, S.arena + off, len, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
     return KWOK_OK;
 }

@@ -65,6 +65,7 @@ def declare(lib, pre):
         "cni_assign": (C.c_int, [VP, VP, VP, SZ, VP]),
         "tick": (C.c_int, [VP, C.c_int64, P(abi.TickResult)]),
         "read_outputs": (C.c_int, [VP, P(abi.Outputs)]),
+        "read_arena": (C.c_int, [VP, U64, U64, VP]),
         "node_has": (C.c_int, [VP, C.c_char_p, SZ]),
         "node_size": (U64, [VP]),
         "dump_pods": (C.c_int, [VP, I32, U32, VP, VP, VP, VP]),
@@ -334,6 +335,13 @@ class EngineBase:
         a["heartbeat_stride"] = 0 if heartbeat_once else res.heartbeat_stride
         a["counters"] = dict(zip(abi.COUNTERS, list(res.counters)))
         return a
+
+    def read_arena(self, off, n, out=None):
+        """kwok_read_arena: bytes [off, off + n) of the collected tick's arena
+        (the offsets read_outputs reports without heartbeat_once)"""
+        buf = out if out is not None else np.empty(max(1, n), np.uint8)
+        self._check(self._fn("read_arena")(self._h, off, n, buf.ctypes.data), "read_arena")
+        return buf[:n]
 
     # -- queries ----------------------------------------------------------------
     def node_has(self, name: str) -> bool:

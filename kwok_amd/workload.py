@@ -169,16 +169,18 @@ class Churn:
     deleted pods are not sent: the engine already freed those handles and the
     shim drops them.
 
-    `dump` returns (used, phase, host_ip, pod_ip) over all pod handles
-    [0, n_handles) of a single-rank engine (or the oracle)."""
+    `dump` returns (used, phase, host_ip, pod_ip) over the pod handles
+    [first, first + n_handles): every handle of a single-rank engine (or the
+    oracle), or one rank's bucket range of a sharded one."""
 
     def __init__(self, pod_handles, node_of_pod, spec_id, n_handles, n_churn, seed=0, node_ip=NODE_IP,
-                 creation=S0 - 60):
+                 creation=S0 - 60, first=0):
+        self.first = first
         self.live = np.asarray(pod_handles, np.int32).copy()  # FIFO: oldest first
         self.node_of = np.zeros(n_handles, np.int32)
-        self.node_of[self.live] = node_of_pod
+        self.node_of[self.live - first] = node_of_pod
         self.ctime = np.zeros(n_handles, np.int64)
-        self.ctime[self.live] = creation
+        self.ctime[self.live - first] = creation
         self.spec = spec_id
         self.n = n_churn
         self.rng = np.random.default_rng(seed)
@@ -188,9 +190,10 @@ class Churn:
         """(events, arena): n_churn deletion-marked pods, then n_churn new pods"""
         D = min(self.n, self.live.shape[0])
         dead = self.live[:D]
+        loc = dead - self.first
         used, phase, _, pip = dump()
-        assert used[dead].all(), "churn: a live pod is missing from the engine"
-        ip_buf, ip_off, ip_len = ip_strings(pip[dead], base=len(self.node_ip))
+        assert used[loc].all(), "churn: a live pod is missing from the engine"
+        ip_buf, ip_off, ip_len = ip_strings(pip[loc], base=len(self.node_ip))
         arena = self.node_ip + ip_buf.tobytes()
         ev = np.zeros(2 * D, abi.POD_EVENT_DTYPE)
         d = ev[:D]
@@ -198,20 +201,20 @@ class Churn:
         d["handle"] = dead
         d["node_handle"] = -1
         d["spec_id"] = self.spec
-        d["phase"] = phase[dead]
-        d["creation_unix"] = self.ctime[dead]
+        d["phase"] = phase[loc]
+        d["creation_unix"] = self.ctime[loc]
         fin = np.where(self.rng.random(D) < 0.5, abi.POD_HAS_FINALIZERS, 0)
-        running = phase[dead] == abi.PHASE_RUNNING
+        running = phase[loc] == abi.PHASE_RUNNING
         d["flags"] = (abi.POD_DELETING | fin | np.where(running, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
-                      | np.where(pip[dead] != 0, abi.POD_STATUS_NONEMPTY, 0))
+                      | np.where(pip[loc] != 0, abi.POD_STATUS_NONEMPTY, 0))
         d["host_ip"]["off"] = 0
         d["host_ip"]["len"] = np.where(running, len(self.node_ip), 0)
         d["pod_ip"]["off"] = ip_off
-        d["pod_ip"]["len"] = np.where(pip[dead] != 0, ip_len, 0)
+        d["pod_ip"]["len"] = np.where(pip[loc] != 0, ip_len, 0)
         c = ev[D:]
         c["op"] = abi.OP_UPSERT
         c["handle"] = -1
-        c["node_handle"] = self.rng.permutation(self.node_of[dead])
+        c["node_handle"] = self.rng.permutation(self.node_of[loc])
         c["spec_id"] = self.spec
         c["phase"] = abi.PHASE_PENDING
         c["flags"] = abi.POD_STATUS_NONEMPTY
@@ -224,8 +227,8 @@ class Churn:
         D, nodes, ct = self._pending
         assert (status == 0).all(), "churn batch rejected: %s" % np.unique(status[status != 0])
         new = handles[D:]
-        self.node_of[new] = nodes
-        self.ctime[new] = ct
+        self.node_of[new - self.first] = nodes
+        self.ctime[new - self.first] = ct
         self.live = np.concatenate([self.live[D:], new])
 
 

@@ -1354,6 +1354,12 @@ int kwok_oracle_read_outputs(kwok_oracle* o, kwok_outputs* out) {
     return KWOK_OK;
 }
 
+int kwok_oracle_read_arena(kwok_oracle* o, uint64_t off, uint64_t len, void* dst) {
+    if (off > o->arena.n || len > o->arena.n - off || (len && !dst)) return KWOK_EINVAL;
+    if (len) memcpy(dst, o->arena.p + off, len);
+    return KWOK_OK;
+}
+
 int kwok_oracle_node_has(kwok_oracle* o, const char* name, size_t len) {
     int32_t h = node_find(o, name, len);
     return h >= 0 && o->nodes[h].managed;

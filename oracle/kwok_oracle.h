@@ -24,6 +24,7 @@ int kwok_oracle_tick(kwok_oracle* o, int64_t now_unix, kwok_tick_result* res);
 /* host threads of the tick's per-object sweeps (<= 0: all; 1: sequential); returns the count */
 int kwok_oracle_set_threads(kwok_oracle* o, int n);
 int kwok_oracle_read_outputs(kwok_oracle* o, kwok_outputs* out);
+int kwok_oracle_read_arena(kwok_oracle* o, uint64_t off, uint64_t len, void* dst);
 int kwok_oracle_node_has(kwok_oracle* o, const char* name, size_t len);
 uint64_t kwok_oracle_node_size(kwok_oracle* o);
 int kwok_oracle_dump_pods(kwok_oracle* o, int32_t first, uint32_t count, uint8_t* used, uint8_t* phase,

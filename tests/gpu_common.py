@@ -201,6 +201,68 @@ def compare_patches(ea, eo, el, oa, oo, ol, what):
             assert len(bad) == 0, "%s: %d patches of length %d differ, first at #%d" % (what, len(bad), L, part[bad[0]])
 
 
+def patch_digests(arena, off, length):
+    """A 64-bit digest per patch (a random linear form of its bytes, the same
+    weights in every process): compares patch bytes across processes without
+    moving them."""
+    out = np.zeros(len(off), np.uint64)
+    length = np.asarray(length)
+    for L in np.unique(length):
+        sel = np.nonzero(length == L)[0]
+        w = np.random.default_rng(int(L)).integers(1, 1 << 62, int(L), dtype=np.uint64) | np.uint64(1)
+        for part in np.array_split(sel, max(1, len(sel) // 50_000)):
+            r = rows(arena, np.asarray(off)[part], int(L)).astype(np.uint64)
+            out[part] = (r * w[None, :]).sum(axis=1, dtype=np.uint64)
+    return out
+
+
+def shim_read_check(e, O, res, chunk=64 << 20):
+    """The Go drop-in's read sequence (integration/go/.../engine_cgo.go tick /
+    applyPatches), replayed through ctypes on the engine's collected tick and
+    checked byte for byte against the oracle's outputs O (read_arrays):
+    kwok_read_outputs without an arena (the lists), kwok_read_arena of ONE
+    heartbeat body, then the node-init and pod patches in pieces of at most
+    `chunk` bytes, 64-bit offsets.  Returns (pieces, bytes read)."""
+    import ctypes as C
+    n = {k: getattr(res, k) for k in ("n_heartbeat", "n_node_init", "n_pod_patch", "n_delete")}
+    L = {"hb": np.empty(n["n_heartbeat"], np.int32),
+         "ini": np.empty(n["n_node_init"], np.int32), "ini_off": np.empty(n["n_node_init"], np.uint64),
+         "ini_len": np.empty(n["n_node_init"], np.uint32),
+         "pp": np.empty(n["n_pod_patch"], np.int32), "pp_off": np.empty(n["n_pod_patch"], np.uint64),
+         "pp_len": np.empty(n["n_pod_patch"], np.uint32),
+         "dl": np.empty(n["n_delete"], np.int32), "dlf": np.empty(n["n_delete"], np.uint8)}
+    p = lambda k: L[k].ctypes.data if L[k].size else None  # noqa: E731
+    out = abi.Outputs(p("hb"), 0, p("ini"), p("ini_off"), p("ini_len"), p("pp"), p("pp_off"), p("pp_len"),
+                      p("dl"), p("dlf"), None, 0, 0)
+    e._check(e._fn("read_outputs")(e._h, C.byref(out)), "read_outputs (lists only)")
+    assert out.arena_copied == 0
+    for a, b in (("hb", "heartbeat_nodes"), ("ini", "node_init_nodes"), ("pp", "pod_patch_pods"),
+                 ("dl", "delete_pods"), ("dlf", "delete_has_finalizers")):
+        assert (L[a] == O[b]).all(), b
+    total = pieces = 0
+    if n["n_heartbeat"]:
+        body = e.read_arena(out.heartbeat_off, res.heartbeat_len)
+        total += body.size
+        assert (body == O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]).all(), "heartbeat body"
+    for hs, offs, lens, oo, ol, what in ((L["ini"], L["ini_off"], L["ini_len"], O["node_init_off"], O["node_init_len"],
+                                         "node inits"),
+                                        (L["pp"], L["pp_off"], L["pp_len"], O["pod_patch_off"], O["pod_patch_len"],
+                                         "pod patches")):
+        ends = offs.astype(np.int64) + lens
+        assert (np.diff(offs.astype(np.int64)) > 0).all(), what + ": offsets increase"
+        i = 0
+        while i < len(hs):
+            lo = int(offs[i])
+            j = max(i + 1, int(np.searchsorted(ends, lo + chunk, side="right")))  # the shim's greedy piece
+            buf = e.read_arena(lo, int(ends[j - 1]) - lo)
+            assert buf.size <= chunk or j == i + 1
+            compare_patches(buf, offs[i:j] - np.uint64(lo), lens[i:j], O["arena"], oo[i:j], ol[i:j], what)
+            total += buf.size
+            pieces += 1
+            i = j
+    return pieces, total
+
+
 def compare_tick(e, o, where):
     E, O = e.read_arrays(), o.read_arrays()
     assert E["counters"] == O["counters"], where

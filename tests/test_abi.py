@@ -151,3 +151,21 @@ def test_compact_readout_oracle():
     assert once.node_inits == full.node_inits and once.pod_patches == full.pod_patches
     assert once.heartbeat_body(0) == full.heartbeat_body(0) and len(full.heartbeat_nodes) > 1
     assert len(once.arena) == len(full.arena) - (len(full.heartbeat_nodes) - 1) * full.heartbeat_len
+
+
+def test_shim_read_sequence_oracle():
+    """The Go drop-in's read sequence (lists without an arena, kwok_read_arena of
+    one heartbeat body, the patches in bounded pieces) over the oracle's ABI:
+    the same bytes as the one-copy read (gpu_common.shim_read_check, which the
+    GPU test runs on the 1M x 10M initial tick)"""
+    import harness
+    from gpu_common import shim_read_check
+    from oracle.oracle import Oracle
+    fx = harness.load_trace("specs")
+    o = Oracle(harness.config_for(fx))
+    got = []
+    harness.replay(fx, o, on_tick=lambda ti, t, out: got.append(shim_read_check(o, o.read_arrays(), o.last, 2048)))
+    assert sum(p for p, _ in got) > 4 and sum(n for _, n in got) > 4096, got
+    with pytest.raises(engine.KwokError):  # outside the arena
+        o.read_arena(o.last.arena_bytes - 4, 8)
+    o.close()

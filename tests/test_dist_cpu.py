@@ -63,3 +63,11 @@ def test_sharded_oracle_matches_single(world, big):
         for k in ("hb", "hb_body", "inits", "pods", "deletes", "counters"):
             assert g[k] == r[k], "tick %d %s" % (t, k)
     assert sum(len(r["pods"]) for r in ref) > 3000 and sum(len(r["deletes"]) for r in ref) > 500
+
+
+def test_eight_oracle_shards_c3_churn():
+    """W = 8 oracle shards over gloo on the C3 protocol (tests/c3_common.py):
+    20k nodes x 200k pods, then 20k deletes + 20k creates in one tick, so every
+    shard's release list (~2.5k) is longer than the inline exchange message"""
+    from c3_common import run_c3
+    run_c3(8, 20_000, 20_000, "oracle")

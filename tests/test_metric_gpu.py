@@ -10,7 +10,7 @@ import ipaddress
 
 import numpy as np
 import pytest
-from gpu_common import compare_tick
+from gpu_common import compare_tick, shim_read_check
 from kwok_amd import workload
 from kwok_amd.engine import Engine
 from oracle.oracle import Oracle
@@ -26,10 +26,15 @@ def test_metric_config_1m_nodes_10m_pods():
     o, _, ph2 = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=0), NODES)
     assert (ph == ph2).all() and len(ph) == 10 * NODES
     n_slots = workload.BUCKETS * fl.cp
-    e.tick(workload.S0 + 30, read=False)
+    r0 = e.tick(workload.S0 + 30, read=False)
     o.tick(workload.S0 + 30, read=False)
     c = compare_tick(e, o, "1M tick 0")
     assert c["pod_patch"] == 10 * NODES and c["node_init"] == NODES and c["alloc"] == 10 * NODES
+    # the Go drop-in's hand-off (lists, one heartbeat body, the ~7 GB of patches in
+    # 64 MiB pieces through kwok_read_arena): every byte against the oracle
+    assert r0.arena_bytes > 1 << 32
+    pieces, nbytes = shim_read_check(e, o.read_arrays(), r0)
+    assert pieces > 64 and nbytes > 1 << 32, (pieces, nbytes)
     used, phase, hip, pip = e.dump_pods(0, n_slots)
     live = used.astype(bool)
     ips = pip[live]

@@ -46,3 +46,41 @@ def test_one_rank_multi_path_matches_oracle(monkeypatch, transport, big, pair):
             assert g[k] == r[k], "%s one-rank multi path, tick %d %s" % (transport, t, k)
     if big:  # the long-list exchange really ran: > 2048 Uses + releases in one tick
         assert max(r["counters"]["release"] for r in ref) > 2048
+
+
+@pytest.mark.parametrize("pair", [False, True], ids=["blocking", "queued"])
+def test_failed_exchange_poisons_engine(monkeypatch, pair):
+    """A tick whose host-side exchange fails (the second allgather of long
+    lists, in kwok_tick_collect's retire) is reported as KWOK_ECOMM, a tick
+    queued behind it fails with it, and every later call fails with
+    KWOK_EDEVICE: the device state went on without the host."""
+    from kwok_amd import abi
+    from kwok_amd import engine as keng
+    calls = {"long": 0}
+
+    def gather(user, send, nbytes, recv):
+        if nbytes != 8 * 4 + 16 * 8 + 2048 * 4:  # not the fixed-size message: the long-list exchange
+            calls["long"] += 1
+            return 1
+        C.memmove(recv, send, nbytes)
+        return 0
+
+    monkeypatch.setenv("KWOK_FORCE_MULTI", "1")
+    e = dc.make(keng.Engine, 0, 1, big=True, allgather=gather)
+    run = dc.Runner(e)
+    with pytest.raises(keng.KwokError) as ex:
+        for n, p in dc.scenario(big=True, ticks=4):
+            run.run_tick(n, p, pair=pair)
+    assert calls["long"] == 1, calls
+    if pair:
+        # multi rank: the second submit first finishes the previous tick on the host,
+        # which fails; the submit refuses, and collect reports the failed tick
+        assert ex.value.code == abi.EDEVICE and "recreate" in str(ex.value), ex.value
+        with pytest.raises(keng.KwokError) as ex:
+            e.tick_collect(read=False)
+    assert ex.value.code == abi.ECOMM, ex.value
+    for call in (lambda: e.tick(1704070000, read=False), lambda: e.dump_pods(0, 8)):
+        with pytest.raises(keng.KwokError) as ex:
+            call()
+        assert ex.value.code == abi.EDEVICE and "recreate" in str(ex.value)
+    e.close()
