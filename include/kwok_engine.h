@@ -274,6 +274,15 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena,
                      size_t arena_len, int32_t* out_handles, int32_t* out_status,
                      uint32_t* out_released);
+/* Page-locked host memory for ingest batches.  kwok_ingest_pods copies its
+ * records, string arena and per-record results between host and GPU (the pod
+ * event switch runs on the device); buffers from kwok_host_alloc move by DMA at
+ * the link's rate, pageable ones through the runtime's staging copies (2-8x
+ * slower for a 2M-record batch, and noisier).  A caller that decodes watch
+ * events straight into such buffers (the codec's output, a cgo slice over C
+ * memory) pays no extra host copy.  NULL on failure; kwok_host_free releases. */
+void* kwok_host_alloc(size_t bytes);
+void kwok_host_free(void* p);
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n);
 
 /* EnableCNI (kwok_config.enable_cni = 1).  The reference calls cni.Setup inside

@@ -13,6 +13,8 @@ enum : uint8_t {
     NS_LOCKABLE = 4,    // needLockNode on its latest event (:210-223)
     NS_CONFORMS = 8,    // configureNode would return nil (A.5)
     NS_EVENT_LOCK = 16, // a watch/list event queued it for LockNode (:261-263)
+    NS_SLOT = 32,       // the slot holds a node entry (an existing node, or one that pods still
+                        // reference: deleted, or a placeholder named by a pod's spec.nodeName)
 };
 
 // ---- pod state word (d_pod_state): flags in bits 0..7, phase in 8..10 -------
@@ -155,6 +157,43 @@ struct PodOp {
     uint16_t node, spec;
     uint32_t ctime, host_ip, pod_ip;
     uint32_t set_fields;       // 1: overwrite node/spec/ctime/IPs; 2: podIP only (kwok_cni_assign)
+};
+
+// ---- GPU pod ingest (ingest.hip) ---------------------------------------------
+// A pod record after the checks that depend only on the record itself (arena
+// bounds, IPv4 strings, spec id, phase, creation time, handle -> bucket),
+// written by k_ing_prep at the record's batch index.  The per-bucket apply
+// pass reads these in bucket order (a stable sort of the batch by bucket).
+struct PodRec {             // 32 bytes
+    uint32_t bucket;        // owned local bucket whose slots the record may change (REC_NONE: none)
+    uint32_t pos;           // existing: the handle's index in its bucket; create: the node's index
+    uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: the parsed podIP
+    uint32_t ctime;
+    uint16_t spec;          // UPSERT with fst == KWOK_OK: the spec id
+    uint8_t op, phase, flags, chk;  // chk: REC_*
+    int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
+    int8_t pst;             // existing: the handle lookup's status
+    uint8_t pad[4];
+};
+static_assert(sizeof(PodRec) == 32, "prepared pod records are 32 bytes");
+constexpr uint32_t REC_NONE = 0xFFFFFFFFu;
+enum : uint8_t {
+    REC_EXISTING = 1,  // handle >= 0
+    REC_DEL_IP = 2,    // DELETE: the event's podIP parsed
+    REC_BY_NAME = 4,   // create naming its node by spec.nodeName: the host resolves it (pos)
+    REC_HARD = 8,      // by name, and the node entry could be freed before the record in event order:
+                       // the apply pass stops at it until the host resolves it
+    REC_RESOLVED = 16, // pos holds the node the host resolved
+    REC_FINAL = 32,    // the host gave the record its status (the apply pass skips it)
+};
+// per-batch counters of the GPU ingest (device memory, read back by the host)
+struct IngSummary {
+    uint32_t n_byname;      // owned by-name creates listed for host resolution
+    uint32_t rejected;      // records with a status other than KWOK_OK
+    uint32_t n_freed;       // node slots the apply pass freed (deleted / placeholder nodes no pod references)
+    uint32_t n_stopped;     // buckets whose apply pass stopped at an unresolved REC_HARD record
+    uint32_t need;          // max over buckets with creates: live pods + creates (growth check)
+    uint32_t pad[3];
 };
 
 // spec descriptor: A | B | C segments of the pod patch (see templates.cpp)

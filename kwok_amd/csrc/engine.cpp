@@ -42,6 +42,8 @@ using namespace kwok;
 namespace {
 
 thread_local std::string g_create_err;  // kwok_last_error(NULL) after a failed create
+using clk = std::chrono::steady_clock;
+double ms_between(clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); }
 
 uint32_t fnv1a32(const char* s, size_t n) {
     uint32_t h = 0x811C9DC5u;
@@ -51,33 +53,6 @@ uint32_t fnv1a32(const char* s, size_t n) {
     }
     return h;
 }
-
-// Host scratch on 2 MiB pages where the kernel grants them (madvise): the
-// threaded ingest scatters records over ~4k bucket runs of tens of MB, and with
-// 4 KiB pages each run is a TLB miss
-struct HugeBuf {
-    void* p = nullptr;
-    size_t n = 0;
-    HugeBuf() = default;
-    HugeBuf(const HugeBuf&) = delete;
-    HugeBuf& operator=(const HugeBuf&) = delete;
-    ~HugeBuf() { free(p); }
-    void* get(size_t need) {
-        if (need <= n) return p;
-        free(p);
-        const size_t huge = (size_t)2 << 20;
-        const size_t sz = (need + need / 8 + huge - 1) & ~(huge - 1);
-        p = aligned_alloc(huge, sz);
-        if (!p) {
-            n = 0;
-            return nullptr;
-        }
-        (void)madvise(p, sz, MADV_HUGEPAGE);
-        memset(p, 0, sz);  // first touch here, not inside a batch's passes
-        n = sz;
-        return p;
-    }
-};
 
 template <class T>
 struct DevBuf {
@@ -164,8 +139,9 @@ struct kwok_engine {
     struct HNode {
         std::string name;
         uint8_t used = 0, exists = 0, managed = 0, lockable = 0;
-        uint32_t refs = 0;
-        uint32_t hash = 0;  // fnv1a32(name): bucket (low bits) and name-table home
+        uint8_t zombie = 0;  // used && !exists: a deleted node (or a placeholder) pods may still reference;
+                             // the entry is freed once none does (the device knows the references)
+        uint32_t hash = 0;   // fnv1a32(name): bucket (low bits) and name-table home
     };
     std::vector<HNode> nodes;                        // [NL]
     // name -> node slot: per owned bucket, an open-addressing table (linear probing,
@@ -181,48 +157,56 @@ struct kwok_engine {
     uint32_t hb_epoch = 0;                           // kwok_tick_result.heartbeat_epoch: bumped when the managed set changes
     uint32_t* hb_pre_h = nullptr;                    // pinned [n_chain + 1]
     uint32_t* d_hb_pre = nullptr;
-    struct HPod {  // one cache line fetch per pod record
-        uint16_t node;    // local node index in the bucket
-        uint8_t used, delpend;
-        uint32_t stamp, opi;  // op coalescing: the op of the unflushed batch (stamp == gen) at stage index opi
-    };
-    std::vector<HPod> pods;                          // [PL]
-    std::vector<uint64_t> pod_bits;                  // occupancy bitset per bucket
-    std::vector<uint16_t> pod_fill;                  // per bucket: upper bound of used slots (only grows)
-    std::vector<uint32_t> pod_cnt;                   // per bucket: live pods
+    std::vector<uint32_t> zb_count;                  // [nb] zombie node entries per owned bucket
+    // pods: no host mirror.  The device's pod_state (USED = slot occupancy),
+    // pod_node and node_state (NS_SLOT) are the state the GPU ingest pass
+    // (ingest.hip) applies batches to; pod_fill is its per-bucket fill mark.
     uint16_t* d_pod_fill = nullptr;
 
-    // ---- batch staging, one Stage per ingest partition ----
+    // ---- node batch staging, one Stage per ingest partition ----
     // Partition p owns the bucket range [p*nb/n_part, (p+1)*nb/n_part): every op on
-    // a slot of those buckets is staged (and coalesced) in stage[p], so partitions
-    // run on their own host threads with no shared writes.  Slot policy, op
-    // coalescing and event order are per bucket, so results do not depend on
-    // n_part.
-    // one cache-line pair per partition: every staged op moves a vector's end
-    // pointer, and partitions run on different threads
+    // a node slot of those buckets is staged (and coalesced) in stage[p], so
+    // partitions run on their own host threads with no shared writes.  Slot policy,
+    // op coalescing and event order are per bucket, so results do not depend on
+    // n_part.  One cache-line pair per partition: every staged op moves a vector's
+    // end pointer, and partitions run on different threads.
     struct alignas(128) Stage {
         std::vector<NodeOp> nops;
-        std::vector<PodOp> pops;
-        std::vector<uint32_t> puts;         // ingest-time Puts (Deleted events)
-        std::vector<uint32_t> pending_del;  // DeletePods routed since the last submit
-        bool fill_dirty = false;            // a pod fill mark of the partition grew
+        std::vector<uint32_t> puts;         // kwok_pool_put (other ranks' ingest-time releases)
         int rejected = 0;
     };
     std::vector<Stage> stage;
     int n_part = 1;
     std::vector<uint32_t> node_stamp, node_opi;  // opi: index in the slot's stage
     uint32_t gen = 1;  // ops of the unflushed batch carry stamp == gen (flush_ops advances it)
-    // threaded-ingest scratch, kept between calls (fresh allocations would page-fault
-    // on first touch, from every thread at once)
-    HugeBuf ing_res;
-    // pod records, validated and parsed in batch order (PodPrep, below), grouped by
-    // partition, then by bucket inside each partition
-    HugeBuf ing_prep, ing_sorted;
     Stage& stage_of(uint32_t bucket_local) { return stage[(size_t)((uint64_t)bucket_local * n_part / nb)]; }
     void* pinned = nullptr;
     size_t pinned_cap = 0;
     void* d_ops = nullptr;
     size_t d_ops_cap = 0;
+
+    // ---- GPU pod ingest (ingest.hip) ----
+    struct Ingest {
+        size_t cap = 0;          // records the per-record buffers hold
+        size_t arena_cap = 0;
+        size_t sort_bytes = 0;
+        void* d_ev = nullptr;
+        uint8_t* d_arena = nullptr;
+        PodRec* rec = nullptr;
+        uint32_t *keys = nullptr, *keys_sorted = nullptr, *idx_sorted = nullptr;
+        int32_t *out_handle = nullptr, *out_status = nullptr;
+        uint32_t* out_released = nullptr;
+        uint32_t* byname = nullptr;
+        uint32_t* fix = nullptr;  // [2 * cap] (batch index, code) pairs
+        void* sort_tmp = nullptr;
+        // per bucket / per node slot (allocated once)
+        uint32_t *creates = nullptr, *dels = nullptr, *beg = nullptr, *end = nullptr, *stopped = nullptr;
+        uint32_t* freed = nullptr;
+        uint32_t* refs_q = nullptr;   // [NL] node slots to count references of / their counts
+        uint32_t* refs_out = nullptr;
+        IngSummary* sum = nullptr;
+        IngSummary* sum_h = nullptr;  // pinned
+    } ing;
 
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
@@ -279,7 +263,6 @@ struct kwok_engine {
         uint64_t now = 0, target = 0;
         uint32_t tag = 0;
         uint32_t epoch = 0;         // heartbeat_epoch of the tick
-        std::vector<std::vector<uint32_t>> pending_del;  // [n_part] pods whose DeletePod this tick emits
         int rc = 0;
         std::string err;
         kwok_tick_result res{};
@@ -425,28 +408,7 @@ void run_parts(kwok_engine* e, bool parallel, F&& f) {
     const std::function<void(int)> fn = [&f](int p) { f(p); };
     e->workers.run(e->n_part, fn);
 }
-constexpr size_t PAR_MIN = 32768;  // records (or deletes) per call before the partitions get threads
 constexpr size_t NODE_PAR_MIN = 2048;  // node records (the per-record work is heavier)
-
-// A pod record after the checks that depend only on the record itself (arena
-// bounds, IP strings, spec id, phase, creation time), done once in batch order
-// with sequential reads of the records and their strings.  The threaded ingest
-// groups these by partition and bucket, so the slot-policy pass reads them in
-// order instead of gathering the caller's records from all over the batch.
-struct PodPrep {  // 32 bytes: the scatter and the slot-policy pass move these
-    uint32_t idx, bkt;      // record index; owned local bucket (NO_BUCKET: the record changes no slot)
-    uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: pip = the parsed podIP
-    uint32_t ctime;
-    uint32_t slot;          // PREP_EXISTING: the handle's local pod slot (bkt * Cp + index);
-                            // a create by node handle: the node's local slot (when pst == KWOK_OK)
-    uint16_t spec;          // UPSERT with fst == KWOK_OK: the spec id
-    uint8_t op, phase, flags, chk;  // chk: PREP_*
-    int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
-    int8_t pst;             // PREP_EXISTING: pod_slot's status; create by node handle: KWOK_ENOTMINE or OK
-};
-static_assert(sizeof(PodPrep) == 32, "prepared pod records are 32 bytes");
-enum : uint8_t { PREP_ARENA_BAD = 1, PREP_DEL_IP = 2, PREP_EXISTING = 4, PREP_BY_NAME = 8 };
-constexpr uint32_t NO_BUCKET = 0xFFFFFFFFu;
 
 // ---- per-batch op coalescing: ops for the same slot compose in order ----
 void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
@@ -468,83 +430,41 @@ void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, b
     o.blob = blob;
     g.nops.push_back(o);
 }
-void pod_op(kwok_engine* e, kwok_engine::Stage& g, const PodOp& in) {
-    auto& hp = e->pods[in.slot];
-    if (hp.stamp == e->gen) {
-        PodOp& o = g.pops[hp.opi];
-        o.bits = (uint16_t)((o.bits & in.keep_mask) | in.bits);
-        o.keep_mask = (uint16_t)(o.keep_mask & in.keep_mask);
-        if (in.set_fields == 1) {
-            o.set_fields = 1;
-            o.node = in.node, o.spec = in.spec, o.ctime = in.ctime, o.host_ip = in.host_ip, o.pod_ip = in.pod_ip;
-        } else if (in.set_fields == 2) {  // podIP only (kwok_cni_assign)
-            o.pod_ip = in.pod_ip;
-            if (!o.set_fields) o.set_fields = 2;
-        }
-        return;
-    }
-    hp.stamp = e->gen;
-    hp.opi = (uint32_t)g.pops.size();
-    g.pops.push_back(in);
-}
 bool node_ops_pending(const kwok_engine* e) {
     for (const auto& g : e->stage)
         if (!g.nops.empty()) return true;
     return false;
 }
 
-// Every partition's staged ops -> one host-to-device copy -> the apply kernels.
-// Each slot has at most one op per batch (coalesced), so the kernels apply them
-// in any order.
+// Every partition's staged node ops (and Puts) -> one host-to-device copy -> the
+// apply kernels.  Each slot has at most one op per batch (coalesced), so the
+// kernels apply them in any order.
 int flush_ops(kwok_engine* e) {
-    size_t nn = 0, np = 0, nu = 0;
-    bool fill = false;
-    for (const auto& g : e->stage) nn += g.nops.size(), np += g.pops.size(), nu += g.puts.size(), fill |= g.fill_dirty;
-    const size_t nb = nn * sizeof(NodeOp), pb = np * sizeof(PodOp), ub = nu * 4;
-    const size_t po = (nb + 255) & ~(size_t)255, uo = po + ((pb + 255) & ~(size_t)255);
-    const auto tfm0 = std::chrono::steady_clock::now();
-    int rc = ensure_pinned(e, uo + ub + 256);
-    if (rc) return rc;
-    const auto tfm = std::chrono::steady_clock::now();
-    const double t_pin = std::chrono::duration<double, std::milli>(tfm - tfm0).count();
+    size_t nn = 0, nu = 0;
+    for (const auto& g : e->stage) nn += g.nops.size(), nu += g.puts.size();
+    const size_t nb = nn * sizeof(NodeOp), ub = nu * 4;
+    const size_t uo = (nb + 255) & ~(size_t)255;
+    if (int rc = ensure_pinned(e, uo + ub + 256)) return rc;
     char* h = (char*)e->pinned;
-    std::vector<size_t> at(3 * (size_t)e->n_part);  // each partition's first node op / pod op / put
-    for (size_t p = 0, a = 0, b = 0, c = 0; p < (size_t)e->n_part; p++) {
-        at[3 * p] = a, at[3 * p + 1] = b, at[3 * p + 2] = c;
-        a += e->stage[p].nops.size(), b += e->stage[p].pops.size(), c += e->stage[p].puts.size();
+    for (size_t p = 0, a = 0, c = 0; p < (size_t)e->n_part; p++) {
+        auto& g = e->stage[p];
+        if (!g.nops.empty()) memcpy(h + a * sizeof(NodeOp), g.nops.data(), g.nops.size() * sizeof(NodeOp));
+        if (!g.puts.empty()) memcpy(h + uo + c * 4, g.puts.data(), g.puts.size() * 4);
+        a += g.nops.size(), c += g.puts.size();
     }
-    run_parts(e, np + nn >= PAR_MIN, [&](int p) {  // pinned memcpy: ~2 GB/s per thread
-        auto& g = e->stage[(size_t)p];
-        if (!g.nops.empty()) memcpy(h + at[3 * p] * sizeof(NodeOp), g.nops.data(), g.nops.size() * sizeof(NodeOp));
-        if (!g.pops.empty()) memcpy(h + po + at[3 * p + 1] * sizeof(PodOp), g.pops.data(), g.pops.size() * sizeof(PodOp));
-        if (!g.puts.empty()) memcpy(h + uo + at[3 * p + 2] * 4, g.puts.data(), g.puts.size() * 4);
-    });
-    const auto tf0 = std::chrono::steady_clock::now();
-    const double t_copy = std::chrono::duration<double, std::milli>(tf0 - tfm).count();
     char* d = (char*)e->d_ops;
-    HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
-    if (fill) {  // before the ops that fill the new slots are visible to a tick
-        HIPCHK(e, hipMemcpyAsync(e->d_pod_fill, e->pod_fill.data(), e->pod_fill.size() * 2, hipMemcpyHostToDevice,
-                                 e->st));
-    }
-    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)nn, (const PodOp*)(d + po), (uint32_t)np, e->st);
-    if (nu)  // ingest-time Puts (Deleted events, pod_controller.go:329-336)
+    if (nn || nu) HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
+    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)nn, nullptr, 0, e->st);
+    if (nu)  // kwok_pool_put: ingest-time releases of other ranks (pod_controller.go:329-336)
         launch_pool_puts_now(e->S, (const uint32_t*)(d + uo), (uint32_t)nu, e->st);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->st));
-    if (e->iprof && np + nn > 1000)
-        fprintf(stderr, "[kwok flush] %zu node + %zu pod ops, %zu puts: %.2f MB, pinned alloc %.2f ms, staging %.2f ms, "
-                        "device copy + apply %.2f ms\n", nn, np, nu, (uo + ub) / 1e6, t_pin, t_copy,
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count());
     for (auto& g : e->stage) {
         g.nops.clear();
-        g.pops.clear();
         g.puts.clear();
-        g.fill_dirty = false;
     }
     if (++e->gen == 0) {  // stamps wrapped: forget them all
         std::fill(e->node_stamp.begin(), e->node_stamp.end(), 0u);
-        for (auto& hp : e->pods) hp.stamp = 0;
         e->gen = 1;
     }
     return KWOK_OK;
@@ -692,6 +612,29 @@ uint64_t intern_blob(kwok_engine* e, const NodeBlob& b, int* rc) {
     return word;
 }
 
+// Tick completion events skip the system-scope release (the tick header is
+// written with system-scope stores), so before a copy engine reads what the
+// kernels wrote, record an event that performs it: the kernels' dirty L2 lines
+// (per XCD, not coherent with the copy engine) are written back first.
+int release_for_host(kwok_engine* e) {
+    HIPCHK(e, hipEventRecord(e->fence, e->st));
+    return KWOK_OK;
+}
+
+// live pods referencing each node slot of `slots` (drained: nothing else runs)
+int node_refs(kwok_engine* e, const std::vector<uint32_t>& slots, std::vector<uint32_t>& out) {
+    out.assign(slots.size(), 0);
+    if (slots.empty()) return KWOK_OK;
+    if (slots.size() > e->NL) return e->fail(KWOK_EINVAL, "node_refs: %zu slots", slots.size());
+    HIPCHK(e, hipMemcpyAsync(e->ing.refs_q, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, e->st));
+    launch_node_refs(e->S, e->ing.refs_q, (uint32_t)slots.size(), e->ing.refs_out, e->st);
+    HIPCHK(e, hipGetLastError());
+    if (int rc = release_for_host(e)) return rc;
+    HIPCHK(e, hipMemcpyAsync(out.data(), e->ing.refs_out, slots.size() * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KWOK_OK;
+}
+
 // The blobs interned since the last upload -> the device copy (SRC_PAD_FRONT
 // zero bytes, the blobs, SRC_PAD_BACK zero bytes: k_emit reads around them).
 // Once per node batch, after every ingest thread is done appending to blob_h,
@@ -757,14 +700,23 @@ void name_erase(kwok_engine* e, uint32_t bl, uint32_t idx, uint32_t h) {
     tab[i] = 0;
 }
 
-void free_node_if_unused(kwok_engine* e, uint32_t slot) {
+// a node entry's zombie mark (used && !exists: pods may still reference it)
+void set_zombie(kwok_engine* e, uint32_t slot, bool z) {
     auto& n = e->nodes[slot];
-    if (n.used && !n.exists && n.refs == 0) {
-        name_erase(e, slot / e->Cn, slot % e->Cn, n.hash);
-        set_bit(e->node_bits, e->Cn, slot / e->Cn, slot % e->Cn, false);
-        n = kwok_engine::HNode();
-        node_op(e, slot, 0, 0, true, 0);
-    }
+    if (n.zombie == (uint8_t)z) return;
+    n.zombie = z;
+    e->zb_count[slot / e->Cn] += z ? 1u : (uint32_t)-1;
+}
+// drop node entry `slot` from the host side (name table, occupancy); the device
+// entry is cleared by the staged op (dev_cleared: the device already did it)
+void free_node(kwok_engine* e, uint32_t slot, bool dev_cleared) {
+    auto& n = e->nodes[slot];
+    if (!n.used) return;
+    name_erase(e, slot / e->Cn, slot % e->Cn, n.hash);
+    set_bit(e->node_bits, e->Cn, slot / e->Cn, slot % e->Cn, false);
+    set_zombie(e, slot, false);
+    n = kwok_engine::HNode();
+    if (!dev_cleared) node_op(e, slot, 0, 0, true, 0);
 }
 
 // find (or create a placeholder for) the node entry of `name`
@@ -804,15 +756,6 @@ int parse_opt_ip(const char* arena, kwok_str s, uint32_t* ip) {
     return KWOK_OK;
 }
 
-// Tick completion events skip the system-scope release (the tick header is
-// written with system-scope stores), so before a copy engine reads what the
-// kernels wrote, record an event that performs it: the kernels' dirty L2 lines
-// (per XCD, not coherent with the copy engine) are written back first.
-int release_for_host(kwok_engine* e) {
-    HIPCHK(e, hipEventRecord(e->fence, e->st));
-    return KWOK_OK;
-}
-
 int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
     if (e->comm) {
         ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, e->comm, e->st);
@@ -831,10 +774,9 @@ int exchange(kwok_engine* e, void* send, size_t bytes, void* recv) {
 }
 
 // Grow every bucket's pod capacity to new_cp (<= the handle stride): the device
-// pod arrays and the host mirrors are re-laid out bucket by bucket (a bucket's
-// pods keep their index, so handles, canonical order and IP order are
-// unchanged); per-slot lists are reallocated.  Runs between ticks (drained),
-// with no pod ops staged.
+// pod arrays are re-laid out bucket by bucket (a bucket's pods keep their index,
+// so handles, canonical order and IP order are unchanged); per-slot lists are
+// reallocated.  Runs between ticks (drained), before a batch's apply pass.
 int grow_pods(kwok_engine* e, uint32_t new_cp) {
     const uint32_t old = e->Cp, nb = e->nb;
     if (new_cp <= old) return KWOK_OK;
@@ -875,29 +817,116 @@ int grow_pods(kwok_engine* e, uint32_t new_cp) {
             (rc = resize(T.del_pods, true)) || (rc = resize(T.del_fin, true)) || (rc = resize(T.pp_job, true)))
             return rc;
     }
-    // host mirrors
-    std::vector<kwok_engine::HPod> pods(PL2, kwok_engine::HPod{0, 0, 0, 0, 0});
-    const uint32_t w_old = (old + 63) / 64, w_new = (new_cp + 63) / 64;
-    std::vector<uint64_t> bits((size_t)nb * w_new, 0);
-    for (uint32_t b = 0; b < nb; b++) {
-        std::copy(e->pods.begin() + (size_t)b * old, e->pods.begin() + (size_t)(b + 1) * old, pods.begin() + (size_t)b * new_cp);
-        std::copy(e->pod_bits.begin() + (size_t)b * w_old, e->pod_bits.begin() + (size_t)(b + 1) * w_old,
-                  bits.begin() + (size_t)b * w_new);
-    }
-    e->pods.swap(pods);
-    e->pod_bits.swap(bits);
-    auto remap = [&](uint32_t slot) { return (slot / old) * new_cp + slot % old; };
-    for (auto& g : e->stage)
-        for (auto& s : g.pending_del) s = remap(s);
-    for (auto& T : e->slots)
-        for (auto& l : T.pending_del)
-            for (auto& s : l) s = remap(s);
     e->Cp = new_cp;
     e->PL = (uint32_t)PL2;
     e->PLa = PLa2;
     S.cp = new_cp;
     S.n_pod_slots = e->PL;
     return size_arena(e);
+}
+
+// ---- GPU pod ingest: host side -------------------------------------------------
+uint32_t sort_bits(const kwok_engine* e) {  // sort keys are local buckets 0..nb (nb: nothing to apply)
+    uint32_t b = 1;
+    while ((1ull << b) <= e->nb) b++;
+    return b;
+}
+// per-record device buffers for batches of n records (grown with headroom)
+int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
+    auto& G = e->ing;
+    if (n > G.cap) {
+        const size_t cap = std::max<size_t>(n + n / 4, 4096);
+        void* ptrs[] = {G.d_ev, G.rec, G.keys, G.keys_sorted, G.idx_sorted, G.out_handle, G.out_status,
+                        G.out_released, G.byname, G.fix, G.sort_tmp};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        G.d_ev = G.sort_tmp = nullptr;
+        G.rec = nullptr;
+        G.keys = G.keys_sorted = G.idx_sorted = G.out_released = G.byname = G.fix = nullptr;
+        G.out_handle = G.out_status = nullptr;
+        G.cap = G.sort_bytes = 0;
+        int rc = 0;
+        if ((rc = dalloc(e, (uint8_t**)&G.d_ev, cap * sizeof(kwok_pod_event))) || (rc = dalloc(e, &G.rec, cap)) ||
+            (rc = dalloc(e, &G.keys, cap)) || (rc = dalloc(e, &G.keys_sorted, cap)) || (rc = dalloc(e, &G.idx_sorted, cap)) ||
+            (rc = dalloc(e, &G.out_handle, cap)) || (rc = dalloc(e, &G.out_status, cap)) ||
+            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.byname, cap)) || (rc = dalloc(e, &G.fix, 2 * cap)))
+            return rc;
+        G.sort_bytes = ingest_sort_bytes((uint32_t)cap, 32);
+        if ((rc = dalloc(e, (uint8_t**)&G.sort_tmp, G.sort_bytes))) return rc;
+        G.cap = cap;
+    }
+    if (arena_len > G.arena_cap) {
+        if (G.d_arena) (void)hipFree(G.d_arena);
+        G.d_arena = nullptr;
+        G.arena_cap = 0;
+        const size_t cap = std::max<size_t>(arena_len + arena_len / 4, 1 << 16);
+        if (int rc = dalloc(e, &G.d_arena, cap)) return rc;
+        G.arena_cap = cap;
+    }
+    return KWOK_OK;
+}
+IngestBatch ingest_batch(kwok_engine* e, uint32_t n, size_t arena_len) {
+    auto& G = e->ing;
+    IngestBatch I{};
+    I.ev = G.d_ev;
+    I.n = n;
+    I.n_specs = (uint32_t)e->specs_h.size();
+    I.arena = G.d_arena;
+    I.arena_len = arena_len;
+    I.rec = G.rec;
+    I.keys = G.keys;
+    I.keys_sorted = G.keys_sorted;
+    I.idx_sorted = G.idx_sorted;
+    I.out_handle = G.out_handle;
+    I.out_status = G.out_status;
+    I.out_released = G.out_released;
+    I.creates = G.creates;
+    I.dels = G.dels;
+    I.byname = G.byname;
+    I.beg = G.beg;
+    I.end = G.end;
+    I.stopped = G.stopped;
+    I.freed = G.freed;
+    I.sum = G.sum;
+    return I;
+}
+// the batch summary -> pinned host memory (waits for the stream)
+int read_summary(kwok_engine* e) {
+    if (int rc = release_for_host(e)) return rc;
+    HIPCHK(e, hipMemcpyAsync(e->ing.sum_h, e->ing.sum, sizeof(IngSummary), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KWOK_OK;
+}
+// host resolutions -> the prepared records (REC_RESOLVED / REC_HARD / a final status)
+int apply_fixes(kwok_engine* e, const IngestBatch& I, const std::vector<uint32_t>& fix) {
+    if (fix.empty()) return KWOK_OK;
+    HIPCHK(e, hipMemcpyAsync(e->ing.fix, fix.data(), fix.size() * 4, hipMemcpyHostToDevice, e->st));
+    launch_ingest_fix(e->S, I, e->ing.fix, (uint32_t)(fix.size() / 2), e->st);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(e->st));  // `fix` is pageable and reused
+    return KWOK_OK;
+}
+// a pod names a node without an entry: a placeholder entry (node_slot), which the
+// pod references until it goes; the fix code of the record
+uint32_t resolve_placeholder(kwok_engine* e, const char* name, size_t len) {
+    uint32_t slot = 0;
+    const int st = node_slot(e, name, len, true, &slot);
+    if (st != KWOK_OK) return 0x80000000u | (uint8_t)(int8_t)st;
+    if (!e->nodes[slot].exists) {
+        node_op(e, slot, 0xFF, NS_SLOT, false, 0);
+        set_zombie(e, slot, true);
+    }
+    return slot % e->Cn;
+}
+// node entries the apply pass freed (the device cleared them) -> the host side
+int free_device_freed(kwok_engine* e) {
+    const uint32_t nf = e->ing.sum_h->n_freed;
+    if (!nf) return KWOK_OK;
+    std::vector<uint32_t> fr(nf);
+    HIPCHK(e, hipMemcpyAsync(fr.data(), e->ing.freed, (size_t)nf * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    for (uint32_t s : fr) free_node(e, s, true);
+    return KWOK_OK;
 }
 
 // The largest pod capacity a chain block's pod chunks cover (engine_create's limit)
@@ -1096,6 +1125,15 @@ void kwok_engine_destroy(kwok_engine* e) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& T : e->slots) free_slot(T);
+    {
+        auto& g = e->ing;
+        void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
+                      g.out_released, g.byname, g.fix, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.stopped,
+                      g.freed, g.refs_q, g.refs_out, g.sum};
+        for (void* p : ip)
+            if (p) (void)hipFree(p);
+        if (g.sum_h) (void)hipHostFree(g.sum_h);
+    }
     if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
@@ -1259,6 +1297,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.world = W;
     S.multi = e->multi ? 1 : 0;
     S.cni = cfg->enable_cni ? 1u : 0u;
+    S.custom_pod = (cfg->custom_templates & KWOK_TPL_POD) ? 1u : 0u;
+    S.buckets = e->B;
     {
         // a chain block's bucket range must fit its LDS node flags and 64 pod chunks
         const uint32_t bpb = (e->nb + S.n_chain - 1) / S.n_chain;
@@ -1339,19 +1379,23 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->name_mask = t - 1;
         e->name_tab.assign((size_t)e->nb * t, 0);
     }
-    e->pods.assign(e->PL, kwok_engine::HPod{0, 0, 0, 0, 0});
     {
-        // host ingest partitions (threads): KWOK_INGEST_THREADS, else up to 16
+        // host ingest partitions of node batches (threads): KWOK_INGEST_THREADS, else up to 16
         unsigned hw = std::thread::hardware_concurrency();
         int np = (int)std::min(16u, hw ? hw : 1u);
         if (const char* v = getenv("KWOK_INGEST_THREADS")) np = atoi(v);
         e->n_part = std::max(1, std::min(np, (int)std::min<uint32_t>(e->nb, 64)));
         e->stage.resize((size_t)e->n_part);
-        for (auto& T : e->slots) T.pending_del.resize((size_t)e->n_part);
     }
-    e->pod_bits.assign((size_t)e->nb * ((e->Cp + 63) / 64), 0);
-    e->pod_fill.assign(e->nb, 0);
-    e->pod_cnt.assign(e->nb, 0);
+    e->zb_count.assign(e->nb, 0);
+    {  // GPU pod ingest: per-bucket / per-node-slot scratch and the batch summary
+        auto& g = e->ing;
+        if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.dels, e->nb)) || (rc = dalloc(e, &g.beg, e->nb)) ||
+            (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.stopped, e->nb)) || (rc = dalloc(e, &g.freed, e->NL)) ||
+            (rc = dalloc(e, &g.refs_q, e->NL)) || (rc = dalloc(e, &g.refs_out, e->NL)) || (rc = dalloc(e, &g.sum, 1)))
+            return bail(rc);
+        if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
+    }
     e->node_stamp.assign(e->NL, 0);
     e->node_opi.assign(e->NL, 0);
     e->max_init_len = 0;
@@ -1454,6 +1498,30 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
+    const auto tq0 = clk::now();
+    // a deleted node's entry lives while pods reference it (the pods' node refs,
+    // pod_controller.go routes by spec.nodeName): the references of the nodes this
+    // batch deletes, counted on the device (no pod changes during a node batch)
+    std::unordered_map<uint32_t, uint32_t> refs;
+    {
+        std::vector<uint32_t> del;
+        for (size_t i = 0; i < n; i++) {
+            const kwok_node_event& x = ev[i];
+            uint32_t slot = 0;
+            if (x.op == KWOK_OP_DELETE && x.name.len && x.name.len <= 253 && in_arena(x.name) &&
+                node_slot(e, arena + x.name.off, x.name.len, false, &slot) == KWOK_OK)
+                del.push_back(slot);
+        }
+        if (!del.empty()) {
+            std::vector<uint32_t> cnt;
+            if (int rc = node_refs(e, del, cnt)) return rc;
+            for (size_t k = 0; k < del.size(); k++) refs[del[k]] = cnt[k];
+        }
+    }
+    auto refs_of = [&](uint32_t slot) {  // a node created in this batch has none
+        auto it = refs.find(slot);
+        return it == refs.end() ? 0u : it->second;
+    };
     // per partition: managed-set changes (applied after the batch)
     std::vector<int64_t> d_managed((size_t)e->n_part, 0);
     std::vector<uint8_t> set_changed((size_t)e->n_part, 0);
@@ -1476,7 +1544,8 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
                         false, 0);
                 handle = (int32_t)(e->b_lo * e->Cn + slot);
-                free_node_if_unused(e, slot);
+                if (refs_of(slot) == 0) free_node(e, slot, false);
+                else set_zombie(e, slot, true);  // freed when its last pod goes (ingest / tick)
             }
         } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
             std::string info[KWOK_NI_COUNT];
@@ -1544,6 +1613,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                 else {
                     auto& hn = e->nodes[slot];
                     hn.exists = 1;
+                    set_zombie(e, slot, false);
                     if (x.managed && !hn.managed) {  // never cleared but by Delete
                         hn.managed = 1;
                         d_managed[(size_t)part]++;
@@ -1552,7 +1622,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                     }
                     hn.lockable = x.lockable ? 1 : 0;
                     bool ev_lock = x.managed && x.lockable;
-                    uint8_t bits = (uint8_t)(NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
+                    uint8_t bits = (uint8_t)(NS_SLOT | NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
                                              (!e->custom_node && node_conforms(x, info) ? NS_CONFORMS : 0) |
                                              (ev_lock ? NS_EVENT_LOCK : 0));
                     node_op(e, slot, ev_lock ? 0 : NS_EVENT_LOCK, bits, true, blob);
@@ -1574,7 +1644,9 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     };
     const auto tn0 = std::chrono::steady_clock::now();
     std::vector<int> rej((size_t)e->n_part, 0);
-    if (n < NODE_PAR_MIN || e->n_part == 1) {
+    static const size_t par_min = getenv("KWOK_NODE_PAR_MIN") ? strtoull(getenv("KWOK_NODE_PAR_MIN"), nullptr, 10)
+                                                             : NODE_PAR_MIN;
+    if (n < par_min || e->n_part == 1) {
         for (size_t i = 0; i < n; i++) {
             const int64_t bl = bucket_of_record(ev[i]);
             const int part = bl < 0 ? 0 : (int)((uint64_t)bl * e->n_part / e->nb);
@@ -1613,344 +1685,131 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     if ((rc = size_arena(e))) return rc;
     rc = flush_ops(e);
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu node records: records %.2f ms, flush %.2f ms\n", n,
-                std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
+        fprintf(stderr, "[kwok ingest] %zu node records: refs %.2f ms, records %.2f ms, flush %.2f ms\n", n,
+                ms_between(tq0, tn0), std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tn1).count());
     return rc ? rc : rejected;
 }
 
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
-    if (!e || (n && !ev) || n > 0xFFFFFFFFull) return KWOK_EINVAL;
+    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
-    drain(e);  // the host mirrors reflect every submitted tick
+    drain(e);  // the device state reflects every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
-    auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
-    const size_t n_specs = e->specs_h.size();
-    // The record-local checks and parses (batch order), and the bucket (owned,
-    // local) whose slots the record changes, or NO_BUCKET when it changes nothing
-    // but its own out_status (it is rejected).  A record's partition processes
-    // it; records of one bucket keep their batch order.
-    auto prep = [&](size_t i, PodPrep& r) {
-        const kwok_pod_event& x = ev[i];
-        r.idx = (uint32_t)i;
-        r.op = x.op, r.phase = x.phase, r.flags = x.flags, r.chk = 0;
-        r.hip = r.pip = 0, r.ctime = 0, r.fst = KWOK_OK, r.slot = 0, r.pst = KWOK_OK, r.spec = 0;
-        r.bkt = NO_BUCKET;
-        if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
-            r.chk = PREP_ARENA_BAD;
-            return;
-        }
-        if (x.op == KWOK_OP_DELETE) {
-            uint32_t ip = 0;
-            if (x.pod_ip.len && parse_ipv4(arena + x.pod_ip.off, x.pod_ip.len, &ip)) r.pip = ip, r.chk |= PREP_DEL_IP;
-        } else if (x.op == KWOK_OP_UPSERT) {
-            if (parse_opt_ip(arena, x.host_ip, &r.hip) || parse_opt_ip(arena, x.pod_ip, &r.pip)) r.fst = KWOK_EDOMAIN;
-            else if (x.spec_id < 0 || (size_t)x.spec_id >= n_specs) r.fst = KWOK_EINVAL;
-            else if (x.phase > KWOK_PHASE_UNKNOWN) r.fst = KWOK_EINVAL;
-            else if (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll) r.fst = KWOK_EDOMAIN;
-            else r.ctime = (uint32_t)x.creation_unix, r.spec = (uint16_t)x.spec_id;  // max_pod_specs <= 65535
-        }
-        if (x.handle >= 0) {
-            r.chk |= PREP_EXISTING;
-            r.pst = (int8_t)e->pod_slot(x.handle, &r.slot);
-            if (r.pst == KWOK_OK) r.bkt = r.slot / e->Cp;
-            return;
-        }
-        if (x.op != KWOK_OP_UPSERT) return;
-        if (x.node_handle >= 0) {
-            const int64_t l = (int64_t)x.node_handle - (int64_t)e->b_lo * e->Cn;
-            if (l >= 0 && l < (int64_t)e->NL) r.bkt = (uint32_t)(l / e->Cn), r.slot = (uint32_t)l;
-            else r.pst = KWOK_ENOTMINE;
-            return;
-        }
-        r.chk |= PREP_BY_NAME;  // the name is read again from the record (rare: callers pass node handles)
-        if (!x.node_name.len || x.node_name.len > 253) return;
-        const uint32_t b = fnv1a32(arena + x.node_name.off, x.node_name.len) & (e->B - 1);
-        if (e->owns(b)) r.bkt = b - e->b_lo;
-    };
-    // WatchPods / ListPods event switch (pod_controller.go:301-343) for one record
-    struct Res {
-        int32_t handle, st;
-        uint32_t released;
-    };
-    auto ingest_one = [&](const PodPrep& x, kwok_engine::Stage& g) -> Res {
-        int st = KWOK_OK;
-        int32_t handle = -1;
-        uint32_t released = 0;
-        if (x.chk & PREP_ARENA_BAD) st = KWOK_EDOMAIN;
-        uint32_t slot = 0;
-        const bool existing = x.chk & PREP_EXISTING;
-        // existing handles: bkt = slot / Cp (prep); no divisions below
-        const uint32_t bl0 = x.bkt;
-        if (st == KWOK_OK && existing) {
-            st = x.pst;
-            slot = x.slot;
-            if (st == KWOK_OK && !e->pods[slot].used) st = KWOK_ENOTFOUND;
-        }
-        auto handle_of = [&](uint32_t bl, uint32_t sl) {
-            return (int32_t)((e->b_lo + bl) * e->Hs + (sl - bl * e->Cp));
-        };
-        if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
-            if (!existing) st = KWOK_EINVAL;
-            else {
-                auto& hp = e->pods[slot];
-                uint32_t nslot = bl0 * e->Cn + hp.node;
-                auto& hn = e->nodes[nslot];
-                const uint32_t ip = x.pip;
-                // pod_controller.go:329-336: release the event object's podIP if the node is managed
-                // (EnableCNI: cni.Remove on the caller's side instead, :337-342)
-                if (!e->S.cni && hn.managed && (x.chk & PREP_DEL_IP) && (uint64_t)(ip - e->pool.net) < e->pool.size &&
-                    ip >= e->pool.net) {
-                    g.puts.push_back(ip);
-                    released = ip;
-                }
-                PodOp o{};
-                o.slot = slot;
-                pod_op(e, g, o);  // state = 0
-                hp.used = 0;
-                hp.delpend = 0;
-                set_bit(e->pod_bits, e->Cp, bl0, slot - bl0 * e->Cp, false);
-                e->pod_cnt[bl0]--;
-                hn.refs--;
-                free_node_if_unused(e, nslot);
-                handle = handle_of(bl0, slot);
-            }
-        } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
-            const uint32_t hip = x.hip, pip = x.pip;
-            uint32_t bl = bl0;
-            st = x.fst;
-            uint32_t nslot = 0;
-            if (st == KWOK_OK && !existing) {
-                if (!(x.chk & PREP_BY_NAME)) {
-                    st = x.pst;  // KWOK_ENOTMINE: another rank's (or no) node slot
-                    if (st == KWOK_OK && !e->nodes[x.slot].used) st = KWOK_ENOTFOUND;
-                    else nslot = x.slot;
-                } else {
-                    const kwok_str nm = ev[x.idx].node_name;
-                    if (!nm.len || nm.len > 253) st = KWOK_EDOMAIN;
-                    else st = node_slot(e, arena + nm.off, nm.len, true, &nslot);
-                }
-                if (st == KWOK_OK) {
-                    bl = x.bkt != NO_BUCKET ? x.bkt : nslot / e->Cn;  // the node's bucket (prep)
-                    int32_t idx = first_free(e->pod_bits, bl, e->Cp);
-                    if (idx < 0) {
-                        st = KWOK_EFULL;
-                        free_node_if_unused(e, nslot);
-                    } else {
-                        slot = bl * e->Cp + (uint32_t)idx;
-                        set_bit(e->pod_bits, e->Cp, bl, (uint32_t)idx, true);
-                        e->pod_cnt[bl]++;
-                        if ((uint32_t)idx + 1 > e->pod_fill[bl]) {
-                            e->pod_fill[bl] = (uint16_t)std::min<uint32_t>(e->Cp, ((uint32_t)idx + 8) & ~7u);
-                            g.fill_dirty = true;
-                        }
-                        e->pods[slot].used = 1;
-                        e->pods[slot].node = (uint16_t)(nslot - bl * e->Cn);
-                        e->nodes[nslot].refs++;
-                    }
-                }
-            } else if (st == KWOK_OK) {
-                nslot = bl * e->Cn + e->pods[slot].node;
-            }
-            if (st == KWOK_OK) {
-                const auto& hn = e->nodes[nslot];
-                auto& hp = e->pods[slot];
-                uint16_t bits = (uint16_t)(PS_USED | ((uint16_t)x.phase << PS_PHASE_SHIFT));
-                if (x.flags & KWOK_POD_DISREGARD) bits |= PS_DISREGARD;
-                if (x.flags & KWOK_POD_HAS_FINALIZERS) bits |= PS_HAS_FIN;
-                // a status that holds an IP is not empty (`{{ with .status }}`)
-                if ((x.flags & KWOK_POD_STATUS_NONEMPTY) || hip || pip) bits |= PS_STATUS_NONEMPTY;
-                // the caller's digest is of the default template; with a custom one a pod
-                // conforms once the engine has patched it (an extra, idempotent patch at most)
-                if ((x.flags & KWOK_POD_CONFORMS) && !e->custom_pod) bits |= PS_CONFORMS;
-                if (hip) bits |= PS_HAS_HOST_IP;
-                if (x.flags & KWOK_POD_DELETING) {
-                    if (hn.managed) {  // pod_controller.go:306-308 -> deletePodChan
-                        bits |= PS_DELETE_PENDING;
-                        if (!hp.delpend) g.pending_del.push_back(slot);
-                        hp.delpend = 1;
-                    }
-                } else if (hn.managed && !(x.flags & KWOK_POD_DISREGARD)) {
-                    bits |= PS_EVENT;  // needLockPod (:252-269) -> lockPodChan
-                }
-                PodOp o{};
-                o.slot = slot;
-                o.keep_mask = existing ? (uint16_t)(PS_EVENT | PS_DELETE_PENDING) : 0;
-                o.bits = bits;
-                o.set_fields = 1;
-                o.node = hp.node;
-                o.spec = x.spec;
-                o.ctime = x.ctime;
-                o.host_ip = hip;
-                o.pod_ip = pip;
-                pod_op(e, g, o);
-                handle = handle_of(bl, slot);
-            }
-        } else if (st == KWOK_OK) {
-            st = KWOK_EINVAL;
-        }
-        if (st != KWOK_OK) g.rejected++;
-        return Res{handle, st, released};
-    };
-    auto put = [&](size_t i, const Res& r) {
-        if (out_handles) out_handles[i] = r.handle;
-        if (out_status) out_status[i] = r.st;
-        if (out_released) out_released[i] = r.released;
-    };
-    for (auto& g : e->stage) g.rejected = 0;
-    // A bucket that this batch's creates would fill grows first (every bucket to a
-    // larger capacity, up to the handle stride): creates[bl] counts them, ignoring
-    // the slots this batch's deletes free (an upper bound)
-    auto is_create = [](const PodPrep& x) { return x.op == KWOK_OP_UPSERT && !(x.chk & PREP_EXISTING) && x.bkt != NO_BUCKET; };
-    auto grow_for = [&](const std::vector<uint32_t>& creates) -> int {
-        uint64_t need = 0;
-        for (uint32_t b = 0; b < e->nb; b++)
-            if (creates[b]) need = std::max<uint64_t>(need, (uint64_t)e->pod_cnt[b] + creates[b]);
-        if (need <= e->Cp) return KWOK_OK;
+    if (!n) return 0;
+    const auto t0 = clk::now();
+    // node ops an earlier call deferred (retire's frees) land before the pass reads node states
+    if (node_ops_pending(e))
+        if (int rc = flush_ops(e)) return rc;
+    int rc = ingest_reserve(e, n, arena_len);
+    if (rc) return rc;
+    auto& G = e->ing;
+    hipStream_t st = e->st;
+    IngestBatch I = ingest_batch(e, (uint32_t)n, arena_len);
+    // the records and their strings -> HBM; prep; the growth need
+    HIPCHK(e, hipMemsetAsync(G.sum, 0, sizeof(IngSummary), st));
+    HIPCHK(e, hipMemsetAsync(G.dels, 0, (size_t)e->nb * 4, st));
+    HIPCHK(e, hipMemcpyAsync(G.d_ev, ev, n * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
+    if (arena_len) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    launch_ingest_prep(e->S, I, st);
+    launch_ingest_need(e->S, I, st);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = read_summary(e))) return rc;
+    const auto t1 = clk::now();
+    IngSummary sum = *G.sum_h;
+    // growth: every bucket to a larger capacity (up to the handle stride) when the
+    // batch's creates could fill one
+    bool efull_possible = false;
+    if (sum.need > e->Cp) {
         const uint32_t cap = max_pod_capacity(e);
-        if (cap <= e->Cp) return KWOK_OK;  // at the stride (or the chain blocks' limit): EFULL per record
-        const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>((need + 7) & ~7ull, 2ull * e->Cp));
-        if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
-        return grow_pods(e, want);
-    };
-    const auto tp0 = std::chrono::steady_clock::now();
-    auto tp1 = tp0;
-    if (n < PAR_MIN || e->n_part == 1) {
-        {
-            std::vector<uint32_t> creates(e->nb, 0);
-            bool any = false;
-            PodPrep r;
-            for (size_t i = 0; i < n; i++) {
-                prep(i, r);
-                if (is_create(r)) creates[r.bkt]++, any = true;
-            }
-            if (any)
-                if (int rc = grow_for(creates)) return rc;
+        if (cap > e->Cp) {
+            const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(((uint64_t)sum.need + 7) & ~7ull, 2ull * e->Cp));
+            if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
+            if ((rc = grow_pods(e, want))) return rc;
+            I = ingest_batch(e, (uint32_t)n, arena_len);
         }
-        // (the bucket mapping of handles is read again: a growth changed Cp)
-        PodPrep r;
-        for (size_t i = 0; i < n; i++) {
-            prep(i, r);
-            put(i, ingest_one(r, r.bkt == NO_BUCKET ? e->stage[0] : e->stage_of(r.bkt)));
-        }
-    } else {
-        // Pass 1 (chunks in parallel): each record's checks and parses, in batch
-        // order, and per-chunk counts of its bucket.  Pass 2: one stable scatter
-        // of the prepared records by bucket (per bucket, batch order is kept, and
-        // nothing orders records of different buckets).  Pass 3 (per partition):
-        // the partition's buckets are one contiguous run of the sorted records,
-        // read in order, so one bucket's slot state, bitmap and nodes stay in
-        // cache while its records are ingested.  Results land in `all` and are
-        // copied out per contiguous record range.
-        const int P = e->n_part;
-        const uint32_t NB1 = e->nb + 1;  // key 0: records that change nothing; key b + 1: bucket b
-        PodPrep* pre = static_cast<PodPrep*>(e->ing_prep.get(n * sizeof(PodPrep)));    // pass 1 output (batch order)
-        PodPrep* srt = static_cast<PodPrep*>(e->ing_sorted.get(n * sizeof(PodPrep)));  // pass 2 output (by bucket)
-        uint64_t* all = static_cast<uint64_t*>(e->ing_res.get(n * sizeof(uint64_t)));  // per record: handle | status << 32
-        if (!pre || !srt || !all) return e->fail(KWOK_ENOMEM, "ingest scratch for %zu records", n);
-        auto key = [](uint32_t b) { return b == NO_BUCKET ? 0u : b + 1u; };
-        std::vector<uint32_t> cnt((size_t)P * NB1, 0);  // [chunk][key], then scatter positions
-        std::vector<std::vector<uint32_t>> creates((size_t)P);  // per chunk: creates per bucket
-        run_parts(e, true, [&](int c) {
-            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-            uint32_t* k = &cnt[(size_t)c * NB1];
-            auto& cr = creates[(size_t)c];
-            cr.assign(e->nb, 0);
-            for (size_t i = lo; i < hi; i++) {
-                PodPrep& r = pre[i];
-                prep(i, r);
-                k[key(r.bkt)]++;
-                if (is_create(r)) cr[r.bkt]++;
-            }
-        });
-        for (int c = 1; c < P; c++)
-            for (uint32_t b = 0; b < e->nb; b++) creates[0][b] += creates[(size_t)c][b];
-        {
-            const uint32_t cp0 = e->Cp;
-            if (int rc = grow_for(creates[0])) return rc;
-            if (e->Cp != cp0)  // handles past the old capacity may name a slot now: re-map them
-                run_parts(e, true, [&](int c) {
-                    const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-                    uint32_t* k = &cnt[(size_t)c * NB1];
-                    for (size_t i = lo; i < hi; i++) {
-                        uint32_t sl = 0;
-                        PodPrep& r = pre[i];
-                        if (!(r.chk & PREP_EXISTING)) continue;
-                        r.pst = (int8_t)e->pod_slot(ev[r.idx].handle, &sl);
-                        r.slot = sl;
-                        const uint32_t nbk = r.pst == KWOK_OK ? sl / e->Cp : NO_BUCKET;
-                        k[key(r.bkt)]--;
-                        r.bkt = nbk;
-                        k[key(r.bkt)]++;
-                    }
-                });
-        }
-        // key-major, chunk-minor exclusive scan: the chunks' positions per key
-        std::vector<size_t> kstart((size_t)NB1 + 1, 0);
-        {
-            size_t acc = 0;
-            for (uint32_t b = 0; b < NB1; b++) {
-                kstart[b] = acc;
-                for (int c = 0; c < P; c++) {
-                    const uint32_t v = cnt[(size_t)c * NB1 + b];
-                    cnt[(size_t)c * NB1 + b] = (uint32_t)acc;
-                    acc += v;
-                }
-            }
-            kstart[NB1] = acc;
-        }
-        run_parts(e, true, [&](int c) {
-            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-            uint32_t* k = &cnt[(size_t)c * NB1];
-            for (size_t i = lo; i < hi; i++) srt[k[key(pre[i].bkt)]++] = pre[i];
-        });
-        tp1 = std::chrono::steady_clock::now();
-        run_parts(e, true, [&](int p) {
-            auto& g = e->stage[(size_t)p];
-            // partition p owns buckets [first, last): those with bl * P / nb == p
-            // (partition 0 also takes the records that change nothing, key 0)
-            const uint32_t first = (uint32_t)(((uint64_t)p * e->nb + P - 1) / P);
-            const uint32_t last = (uint32_t)(((uint64_t)(p + 1) * e->nb + P - 1) / P);
-            const size_t k0 = kstart[p == 0 ? 0 : first + 1], k1 = kstart[last + 1];
-            // records are read in order; prefetch the pod mirror of existing handles
-            // and the result word (records come from all over the batch)
-            constexpr size_t PF = 8;
-            for (size_t k = k0; k < k1; k++) {
-                if (k + PF < k1) {
-                    const PodPrep& y = srt[k + PF];
-                    __builtin_prefetch(&all[y.idx], 1);
-                    if (y.bkt != NO_BUCKET && (y.chk & PREP_EXISTING)) __builtin_prefetch(&e->pods[y.slot], 1);
-                }
-                const PodPrep& x = srt[k];
-                const Res r = ingest_one(x, g);
-                all[x.idx] = (uint32_t)r.handle | (uint64_t)(uint32_t)r.st << 32;
-                // released IPs only come from DELETE records: theirs here, the rest zeroed below
-                if (out_released && x.op == KWOK_OP_DELETE) out_released[x.idx] = r.released;
-            }
-        });
-        run_parts(e, true, [&](int t) {
-            const size_t lo = n * (size_t)t / (size_t)P, hi = n * (size_t)(t + 1) / (size_t)P;
-            for (size_t i = lo; i < hi; i++) {
-                if (out_handles) out_handles[i] = (int32_t)(uint32_t)all[i];
-                if (out_status) out_status[i] = (int32_t)(all[i] >> 32);
-                if (out_released && ev[i].op != KWOK_OP_DELETE) out_released[i] = 0;
-            }
-        });
+        efull_possible = sum.need > e->Cp;  // at the stride (or the chain blocks' limit): EFULL per record
     }
-    int rejected = 0;
-    for (auto& g : e->stage) rejected += g.rejected;
-    const auto tp2 = std::chrono::steady_clock::now();
-    int rc = flush_ops(e);
-    if (e->iprof) {
-        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-            return std::chrono::duration<double, std::milli>(b - a).count();
-        };
-        fprintf(stderr, "[kwok ingest] %zu pod records, %d partitions: route %.2f ms, records %.2f ms, flush %.2f ms\n",
-                n, e->n_part, ms(tp0, tp1), ms(tp1, tp2), ms(tp2, std::chrono::steady_clock::now()));
+    // by-name creates (spec.nodeName): resolved on the host, in event order
+    std::vector<uint32_t> fix;
+    if (sum.n_byname) {
+        std::vector<uint32_t> idx(sum.n_byname), dels(e->nb);
+        HIPCHK(e, hipMemcpyAsync(idx.data(), G.byname, idx.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipMemcpyAsync(dels.data(), G.dels, dels.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        std::sort(idx.begin(), idx.end());
+        const std::vector<uint32_t> zb0 = e->zb_count;  // zombie entries at the batch's start
+        // A node entry can only be freed during the batch in a bucket that deletes pods
+        // at ingest, holds zombie entries, or may run out of pod slots: there a name
+        // that is missing or a zombie is resolved when the apply pass reaches it
+        // (REC_HARD).  Elsewhere every lookup (and placeholder) is the one event
+        // order would give.
+        for (uint32_t i : idx) {
+            const kwok_str nm = ev[i].node_name;
+            const uint32_t bl = (fnv1a32(arena + nm.off, nm.len) & (e->B - 1)) - e->b_lo;
+            const bool dirty = efull_possible || dels[bl] || zb0[bl];
+            uint32_t slot = 0;
+            int s0 = node_slot(e, arena + nm.off, nm.len, false, &slot);
+            if (s0 == KWOK_OK && !(dirty && e->nodes[slot].zombie)) {
+                fix.push_back(i), fix.push_back(slot % e->Cn);
+            } else if (dirty) {
+                fix.push_back(i), fix.push_back(0x40000000u);  // REC_HARD
+            } else {
+                fix.push_back(i);
+                fix.push_back(resolve_placeholder(e, arena + nm.off, nm.len));
+            }
+        }
     }
-    return rc ? rc : rejected;
+    if ((rc = apply_fixes(e, I, fix))) return rc;
+    if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;  // placeholders' NS_SLOT
+    // stable sort by bucket; the apply pass, one wave per bucket, in event order
+    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
+    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
+    if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
+        return e->fail(KWOK_EDEVICE, "ingest sort");
+    const auto t2 = clk::now();
+    int rounds = 0;
+    for (;;) {
+        launch_ingest_apply(e->S, I, st);
+        HIPCHK(e, hipGetLastError());
+        if ((rc = read_summary(e))) return rc;
+        rounds++;
+        if ((rc = free_device_freed(e))) return rc;  // node entries the pass freed
+        if (!G.sum_h->n_stopped) break;
+        // buckets stopped at a REC_HARD record: resolve it now (after the frees so far)
+        const uint32_t ns = G.sum_h->n_stopped;
+        std::vector<uint32_t> bk(ns), pos(ns), ix(ns);
+        HIPCHK(e, hipMemcpyAsync(bk.data(), G.stopped, ns * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&pos[k], G.beg + bk[k], 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&ix[k], G.idx_sorted + pos[k], 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        fix.clear();
+        for (uint32_t i : ix) {
+            const kwok_str nm = ev[i].node_name;
+            uint32_t slot = 0;
+            if (node_slot(e, arena + nm.off, nm.len, false, &slot) == KWOK_OK) fix.push_back(i), fix.push_back(slot % e->Cn);
+            else fix.push_back(i), fix.push_back(resolve_placeholder(e, arena + nm.off, nm.len));
+        }
+        if ((rc = apply_fixes(e, I, fix))) return rc;
+        if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;
+        HIPCHK(e, hipMemsetAsync(&G.sum->n_stopped, 0, 4, st));
+        HIPCHK(e, hipMemsetAsync(&G.sum->n_freed, 0, 4, st));
+    }
+    const auto t3 = clk::now();
+    // per-record results -> the caller's arrays
+    if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles, G.out_handle, n * 4, hipMemcpyDeviceToHost, st));
+    if (out_status) HIPCHK(e, hipMemcpyAsync(out_status, G.out_status, n * 4, hipMemcpyDeviceToHost, st));
+    if (out_released) HIPCHK(e, hipMemcpyAsync(out_released, G.out_released, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    if (e->iprof)
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU): copy + prep %.2f ms, resolve + sort %.2f ms, apply %.2f ms "
+                        "(%d rounds), results %.2f ms\n", n, ms_between(t0, t1), ms_between(t1, t2), ms_between(t2, t3),
+                rounds, ms_between(t3, clk::now()));
+    return (int)G.sum_h->rejected;
 }
 
 int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {
@@ -1983,33 +1842,38 @@ int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {
 }
 
 int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips, size_t n, int32_t* out_status) {
-    if (!e || (n && (!handles || !ips))) return KWOK_EINVAL;
+    if (!e || (n && (!handles || !ips)) || n > 0x7FFFFFF0ull) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
     if (!e->S.cni) return e->fail(KWOK_EINVAL, "kwok_cni_assign: the engine was created without enable_cni");
     drain(e);
     if (e->poisoned) return poisoned(e);
-    int rejected = 0;
-    for (size_t i = 0; i < n; i++) {
-        uint32_t l = 0;
-        int st = e->pod_slot(handles[i], &l);
-        if (st == KWOK_OK && !e->pods[l].used) st = KWOK_ENOTFOUND;
-        else if (st == KWOK_OK && !ips[i]) st = KWOK_EDOMAIN;
-        if (st == KWOK_OK) {
-            // configurePod: pod.Status.PodIP = ips[0] (pod_controller.go:388), so the status is not empty
-            PodOp o{};
-            o.slot = (uint32_t)l;
-            o.keep_mask = 0xFFFF;
-            o.bits = PS_STATUS_NONEMPTY;
-            o.set_fields = 2;
-            o.pod_ip = ips[i];
-            pod_op(e, e->stage_of(l / e->Cp), o);
-        } else {
-            rejected++;
-        }
-        if (out_status) out_status[i] = st;
+    if (!n) return 0;
+    // a handle assigned twice keeps its last valid IP (configurePod runs once per tick)
+    std::vector<uint8_t> wr(n, 0);
+    {
+        std::unordered_map<int32_t, size_t> last;
+        for (size_t i = 0; i < n; i++)
+            if (ips[i]) last[handles[i]] = i;
+        for (const auto& kv : last) wr[kv.second] = 1;
     }
-    int rc = flush_ops(e);
-    return rc ? rc : rejected;
+    int rc = ingest_reserve(e, n, 0);
+    if (rc) return rc;
+    auto& G = e->ing;
+    hipStream_t st = e->st;
+    // scratch: the ingest buffers (handles, IPs, write flags, statuses)
+    HIPCHK(e, hipMemsetAsync(G.sum, 0, sizeof(IngSummary), st));
+    HIPCHK(e, hipMemcpyAsync(G.keys, handles, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(G.keys_sorted, ips, n * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(G.idx_sorted, wr.data(), n, hipMemcpyHostToDevice, st));
+    launch_cni_assign(e->S, (const int32_t*)G.keys, G.keys_sorted, (const uint8_t*)G.idx_sorted, (uint32_t)n,
+                      G.out_status, &G.sum->rejected, st);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = read_summary(e))) return rc;
+    if (out_status) {
+        HIPCHK(e, hipMemcpyAsync(out_status, G.out_status, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+    }
+    return (int)G.sum_h->rejected;
 }
 
 int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
@@ -2225,8 +2089,8 @@ void trace_tick(kwok_engine* e) {
     e->trace_ticks++;
 }
 
-using clk = std::chrono::steady_clock;
-double ms_between(clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); }
+
+int free_zombies(kwok_engine* e);  // (below)
 
 // Finish the oldest queued tick on the host: wait for it, complete a multi-rank
 // tick with long lists, derive the header, check errors, mirror DeletePods into
@@ -2341,6 +2205,8 @@ int retire(kwok_engine* e) {
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));
+    if (H.n_del)  // deleted nodes whose last pod this tick deleted
+        if (int rc = free_zombies(e)) return failed(rc);
     // the slot-freeing ops of deleted nodes without pods: no tick reads such a
     // node, so with a tick already queued they wait for the next flush
     if (node_ops_pending(e) && next < 0) {
@@ -2371,32 +2237,21 @@ int retire(kwok_engine* e) {
     return KWOK_OK;
 }
 
-// Host mirror of the DeletePods a just-enqueued tick performs: every pod it
-// deletes frees its slot (each partition its own list, routed at ingest).  Run
-// right after the enqueue, so it overlaps the tick on the device; nothing reads
-// the mirrors before the tick is retired (ingest and dumps drain first).
-void free_deleted(kwok_engine* e, kwok_engine::TickSlot& T) {
-    size_t n_del = 0;
-    for (const auto& l : T.pending_del) n_del += l.size();
-    if (!n_del) return;
-    const auto td0 = clk::now();
-    run_parts(e, n_del >= PAR_MIN, [&](int p) {
-        auto& list = T.pending_del[(size_t)p];
-        for (uint32_t slot : list) {
-            auto& hp = e->pods[slot];
-            if (!hp.delpend || !hp.used) continue;
-            uint32_t nslot = (slot / e->Cp) * e->Cn + hp.node;
-            hp.used = 0;
-            hp.delpend = 0;
-            set_bit(e->pod_bits, e->Cp, slot / e->Cp, slot % e->Cp, false);
-            e->pod_cnt[slot / e->Cp]--;
-            e->nodes[nslot].refs--;
-            free_node_if_unused(e, nslot);
-        }
-        list.clear();
-    });
-    if (e->iprof)
-        fprintf(stderr, "[kwok submit] %zu deleted pods freed in %.2f ms\n", n_del, ms_between(td0, clk::now()));
+// After a tick that deleted pods (DeletePods): the entries of deleted nodes
+// (zombies) no pod references any more are freed, as the last pod's removal
+// frees them at ingest (the device counts the references).
+int free_zombies(kwok_engine* e) {
+    std::vector<uint32_t> z;
+    for (uint32_t bl = 0; bl < e->nb; bl++)
+        if (e->zb_count[bl])
+            for (uint32_t i = 0; i < e->Cn; i++)
+                if (e->nodes[(size_t)bl * e->Cn + i].zombie) z.push_back(bl * e->Cn + i);
+    if (z.empty()) return KWOK_OK;
+    std::vector<uint32_t> refs;
+    if (int rc = node_refs(e, z, refs)) return rc;
+    for (size_t k = 0; k < z.size(); k++)
+        if (!refs[k]) free_node(e, z[k], false);
+    return KWOK_OK;
 }
 
 // every queued tick finished on the host (before anything that reads or changes
@@ -2439,21 +2294,11 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     T.epoch = e->hb_epoch;
     T.emit_queued = e->emit_hint;
     e->emit_hint = false;
-    for (int p = 0; p < e->n_part; p++) {
-        T.pending_del[(size_t)p].swap(e->stage[(size_t)p].pending_del);
-        e->stage[(size_t)p].pending_del.clear();
-    }
     rc = enqueue_tick(e, k, false);
-    if (rc) {
-        for (int p = 0; p < e->n_part; p++) e->stage[(size_t)p].pending_del.swap(T.pending_del[(size_t)p]);
-        return rc;
-    }
-    const auto te = clk::now();
-    free_deleted(e, T);
+    if (rc) return rc;
     T.state = SLOT_QUEUED;
     e->queue[e->nq++] = k;
-    if (e->iprof)
-        fprintf(stderr, "[kwok submit] enqueue %.3f ms, mirror %.3f ms\n", ms_between(t0, te), ms_between(te, clk::now()));
+    if (e->iprof) fprintf(stderr, "[kwok submit] enqueue %.3f ms\n", ms_between(t0, clk::now()));
     e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
     e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
     return KWOK_OK;
@@ -2532,6 +2377,16 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     }
     HIPCHK(e, hipStreamSynchronize(st));
     return KWOK_OK;
+}
+
+void* kwok_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void kwok_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {

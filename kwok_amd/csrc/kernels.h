@@ -80,7 +80,7 @@ struct DevState {
     uint8_t* del_fin;
     uint32_t node_ip;
     TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
-    const uint16_t* pod_fill;  // per owned bucket: upper bound of used pod slots (host-maintained)
+    uint16_t* pod_fill;        // per owned bucket: upper bound of used pod slots (only grows; the ingest pass)
     const uint32_t* hb_pre;    // [n_chain + 1] managed nodes before each chain block (host-maintained)
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
@@ -91,6 +91,8 @@ struct DevState {
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)
     uint32_t hb_nt;            // heartbeat stores non-temporal (streams larger than the Infinity Cache)
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
+    uint32_t custom_pod;       // Config.PodStatusTemplate is custom: the caller's CONFORMS digest is ignored
+    uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
     // heartbeat geometry (default: HB_STRIDE / 16, HB_PREFIX, CONDS_LEN; a custom template's otherwise)
@@ -123,5 +125,47 @@ int tick_occupancy();  // resident k_tick blocks per CU
 // the patch bytes of the tick's jobs (after its k_tick launch(es), on the same stream)
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st);
 int emit_occupancy();  // resident k_emit blocks per CU
+
+// ---- GPU pod ingest (ingest.hip): kwok_ingest_pods / kwok_cni_assign --------
+struct IngestBatch {
+    const void* ev;            // [n] kwok_pod_event, copied to the device
+    uint32_t n;
+    uint32_t n_specs;
+    const uint8_t* arena;      // the batch's string arena (device copy)
+    uint64_t arena_len;
+    PodRec* rec;               // [n] prepared records
+    uint32_t* keys;            // [n] sort key: owned local bucket, or nb (nothing to apply)
+    uint32_t* keys_sorted;     // [n]
+    uint32_t* idx_sorted;      // [n] batch indices in (bucket, batch order)
+    int32_t* out_handle;       // [n]
+    int32_t* out_status;       // [n]
+    uint32_t* out_released;    // [n]
+    uint32_t* creates;         // [nb] creates per bucket (growth check)
+    uint32_t* dels;            // [nb] 1: the batch deletes a pod of the bucket (zeroed per batch)
+    uint32_t* byname;          // [n] batch indices of owned by-name creates (host resolution)
+    uint32_t* beg;             // [nb] first sorted position of each bucket (resume position after a stop)
+    uint32_t* end;             // [nb]
+    uint32_t* stopped;         // [nb] buckets that stopped at a REC_HARD record
+    uint32_t* freed;           // [NL] node slots freed by the apply pass
+    IngSummary* sum;
+};
+size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort temporary storage
+// prep (+ growth counts) for every record
+void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st);
+// live pods + creates of every bucket with creates -> sum->need
+void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st);
+// host resolutions of by-name creates: (batch index, node index in its bucket | status << 16)
+void launch_ingest_fix(const DevState& S, const IngestBatch& I, const uint32_t* fix, uint32_t n_fix, hipStream_t st);
+// stable sort by bucket, bucket ranges
+int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_t tmp_bytes, uint32_t key_bits,
+                       hipStream_t st);
+// the WatchPods / ListPods event switch, per bucket in event order (one wave per bucket)
+void launch_ingest_apply(const DevState& S, const IngestBatch& I, hipStream_t st);
+// live pods referencing each node slot of `slots` (a node entry may be freed when 0)
+void launch_node_refs(const DevState& S, const uint32_t* slots, uint32_t n, uint32_t* refs, hipStream_t st);
+// kwok_cni_assign: statuses of every record; wr[i]: record i is the handle's last
+// valid assignment (it writes the podIP)
+void launch_cni_assign(const DevState& S, const int32_t* handles, const uint32_t* ips, const uint8_t* wr, uint32_t n,
+                       int32_t* status, uint32_t* rejected, hipStream_t st);
 
 }  // namespace kwok

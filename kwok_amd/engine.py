@@ -77,6 +77,8 @@ def declare(lib, pre):
             "finalizer_patch": (C.c_char_p, [P(SZ)]),
             "device_outputs": (C.c_int, [VP, P(abi.DeviceView)]),
             "bucket_of": (U32, [C.c_char_p, SZ, U32]),
+            "host_alloc": (VP, [SZ]),
+            "host_free": (None, [VP]),
             "rank_of_bucket": (I32, [U32, U32, I32]),
             "profile_enable": (C.c_int, [VP, C.c_int]),
             "profile_read": (C.c_int, [VP, VP, VP]),
@@ -229,14 +231,21 @@ class EngineBase:
         self._check(rc, "ingest_nodes")
         return hs, st
 
-    def ingest_pods_raw(self, events: np.ndarray, arena: bytes):
+    def ingest_pods_raw(self, events: np.ndarray, arena, out=None):
+        """arena: bytes or a uint8 array; out: optional (handles, status,
+        released) arrays of len(events) (e.g. page-locked, host_array)"""
         n = len(events)
-        hs = np.empty(n, np.int32)
-        st = np.empty(n, np.int32)
-        rel = np.empty(n, np.uint32)
+        if out is None:
+            hs, st, rel = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint32)
+        else:
+            hs, st, rel = (o[:n] for o in out)
         ev = np.ascontiguousarray(events, dtype=abi.POD_EVENT_DTYPE)
-        rc = self._fn("ingest_pods")(self._h, ev.ctypes.data, n, arena or b"\0", len(arena),
-                                     hs.ctypes.data, st.ctypes.data, rel.ctypes.data)
+        if isinstance(arena, np.ndarray):
+            ar, alen = C.cast(arena.ctypes.data, C.c_char_p), arena.nbytes
+        else:
+            ar, alen = arena or b"\0", len(arena)
+        rc = self._fn("ingest_pods")(self._h, ev.ctypes.data, n, ar, alen, hs.ctypes.data, st.ctypes.data,
+                                     rel.ctypes.data)
         self._check(rc, "ingest_pods")
         return hs, st, rel
 
@@ -401,6 +410,21 @@ class Engine(EngineBase):
         v = abi.DeviceView()
         self._check(self._lib.kwok_device_outputs(self._h, C.byref(v)), "device_outputs")
         return v
+
+
+def host_array(shape, dtype):
+    """A numpy array over page-locked host memory (kwok_host_alloc), freed
+    with the array: batch buffers that move to and from the GPU by DMA."""
+    import weakref
+    lib = load_engine_lib()
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    p = lib.kwok_host_alloc(max(n, 1))
+    if not p:
+        raise MemoryError("kwok_host_alloc(%d)" % n)
+    buf = (C.c_uint8 * max(n, 1)).from_address(p)
+    weakref.finalize(buf, lib.kwok_host_free, p)
+    return np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
 
 
 def comm_id() -> bytes:

@@ -174,8 +174,13 @@ class Churn:
     oracle), or one rank's bucket range of a sharded one."""
 
     def __init__(self, pod_handles, node_of_pod, spec_id, n_handles, n_churn, seed=0, node_ip=NODE_IP,
-                 creation=S0 - 60, first=0):
+                 creation=S0 - 60, first=0, alloc=None):
         self.first = first
+        # alloc(shape, dtype): the batch is written into (and reused from) these
+        # buffers - e.g. page-locked host memory (engine.host_array), which the
+        # ingest copies to the GPU by DMA
+        self.alloc = alloc
+        self.bufs = None
         self.live = np.asarray(pod_handles, np.int32).copy()  # FIFO: oldest first
         self.node_of = np.zeros(n_handles, np.int32)
         self.node_of[self.live - first] = node_of_pod
@@ -194,8 +199,18 @@ class Churn:
         used, phase, _, pip = dump()
         assert used[loc].all(), "churn: a live pod is missing from the engine"
         ip_buf, ip_off, ip_len = ip_strings(pip[loc], base=len(self.node_ip))
-        arena = self.node_ip + ip_buf.tobytes()
-        ev = np.zeros(2 * D, abi.POD_EVENT_DTYPE)
+        if self.alloc is None:
+            arena = self.node_ip + ip_buf.tobytes()
+            ev = np.zeros(2 * D, abi.POD_EVENT_DTYPE)
+        else:
+            if self.bufs is None or len(self.bufs[0]) < 2 * D:
+                self.bufs = (self.alloc((2 * self.n,), abi.POD_EVENT_DTYPE),
+                             self.alloc((len(self.node_ip) + 16 * self.n,), np.uint8))
+            ev = self.bufs[0][:2 * D]
+            ev[...] = np.zeros(1, abi.POD_EVENT_DTYPE)[0]
+            arena = self.bufs[1][:len(self.node_ip) + ip_buf.size]
+            arena[:len(self.node_ip)] = np.frombuffer(self.node_ip, np.uint8)
+            arena[len(self.node_ip):] = ip_buf
         d = ev[:D]
         d["op"] = abi.OP_UPSERT
         d["handle"] = dead

@@ -42,6 +42,7 @@ def test_oracle_library_exports():
         if f in ("kwok_engine_create", "kwok_engine_destroy"):
             name = name.replace("engine_", "")
         if f in ("kwok_abi_version", "kwok_comm_id", "kwok_finalizer_patch", "kwok_device_outputs",
+                 "kwok_host_alloc", "kwok_host_free",  # engine only: page-locked batch buffers
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
                  "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
