@@ -87,6 +87,7 @@ def parse():
     ap.add_argument("--roofline-ticks", type=int, default=20)
     ap.add_argument("--churn-ticks", type=int, default=5, help="C4 churn ticks after the steady legs (N=1; 0: skip)")
     ap.add_argument("--flap-ticks", type=int, default=5, help="C5 flap ticks on a partially managed fleet (N=1; 0: skip)")
+    ap.add_argument("--once-ticks", type=int, default=1, help="the KWOK_CFG_HEARTBEAT_ONCE leg (N=1; 0: skip)")
     ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
                                                          "metric size: 2M create/delete per tick)")
     return ap.parse_args()
@@ -211,6 +212,49 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
                 "kwok_host_alloc), the GPU event switch (prep, stable sort by bucket, per-bucket apply), D2H of the "
                 "per-record handles / statuses / releases; event generation between steps untimed (the GPU idles "
                 "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
+
+
+def heartbeat_once_leg(nodes, steps, warmup):
+    """The same fleet and steady ticks with KWOK_CFG_HEARTBEAT_ONCE: the tick
+    materialises ONE heartbeat body (every node's patch is that body,
+    node_controller.go:393-401) and the handle list, for callers that send one
+    body to every node (the cgo drop-in).  The tick then moves the SoA state
+    only: its roofline is the state bytes over the launch time."""
+    e, fl, _ = workload.build_engine_fleet(keng.Engine, nodes, heartbeat_once=True)
+    now = workload.S0 + 30
+    e.tick(now, read=False)  # initial tick
+    for _ in range(warmup):
+        now += 30
+        e.tick(now, read=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e.tick_submit(now + 30)
+    now += 30
+    trans = 0
+    for k in range(steps):
+        if k + 1 < steps:
+            e.tick_submit(now + 30)
+            now += 30
+        trans += transitions(e.tick_collect(read=False).counters)
+    dt = time.perf_counter() - t0
+    e.profile_enable(True)
+    for _ in range(20):
+        now += 30
+        r = e.tick(now, read=False)
+    ph, nt = e.profile_read()
+    e.profile_enable(False)
+    e.close()
+    lc = r.local_counters
+    state_bytes = NODE_STATE_BYTES * lc[8] + POD_BYTES * lc[10]
+    kern = ph["kernel"] / max(nt, 1)
+    return {"workload": "metric configuration, KWOK_CFG_HEARTBEAT_ONCE (one heartbeat body + the handle list per "
+                        "tick); steady ticks queued", "steps": steps,
+            "value": trans / dt, "unit": "transitions/s", "ms_per_step": dt / steps * 1e3,
+            "kernel_ms": kern, "classify_ms": ph["classify"] / max(nt, 1),
+            "roofline": {"bound": "hbm (latency-bound chain)", "kernel": "k_tick", "bytes_per_launch": state_bytes,
+                         "achieved": state_bytes / (kern * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": state_bytes / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "SoA state read + written per tick (node 9 + 9 B, pod 10 B) over the k_tick launch"}}
 
 
 def flap_leg(nodes, ticks):
@@ -416,9 +460,11 @@ def main():
 
     e.close()
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
+    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup) if world == 1 and a.once_ticks else None
 
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
+        classify_ms = phases["classify"] / max(nt, 1)
         lc = last.local_counters
         n_nodes, n_pods = lc[8], lc[10]  # nodes_managed, pods_total (this rank)
         alg_bytes = NODE_BYTES * n_nodes + POD_BYTES * n_pods
@@ -426,13 +472,17 @@ def main():
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-        if os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK:
+        import hashlib
+        ksha = hashlib.sha256(open(os.path.join(ROOT, "kwok_amd", "csrc", "kernels.hip"), "rb").read()).hexdigest()
+        if (os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK and
+                json.load(open(pmc)).get("kernels_sha256") == ksha):  # a stored figure of THIS kernel build
             ks = json.load(open(pmc))["kernels"]
             # the default-geometry kernel: "k_tick" (older builds) or "void k_tick<false>"
             kt = [k for k in ks if k == "k_tick" or k.startswith("void k_tick<false>")]
             if kt:
                 traffic = ks[kt[0]]["hbm_bytes"]
-                traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch, same config)" % PMC_FILE
+                traffic_src = ("stored: profiles/%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch of this "
+                               "kernel build (kernels.hip sha256 %s), same config" % (PMC_FILE, ksha[:12]))
         ilc = r0.local_counters
         init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
         emit_ms = ph0["emit_kernel"]
@@ -481,10 +531,11 @@ def main():
                          "bytes_per_launch": alg_bytes, "avg_launch_ms": kern_ms, "traffic_source": traffic_src,
                          "timing": "HIP events around each k_tick launch (hipExtLaunchKernelGGL), %d ticks" % nt},
             "state_only": {"bytes_per_tick": state_bytes,
-                           "achieved": state_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0,
-                           "unit": "GB/s", "classify_ms": phases["classify"] / max(nt, 1),
-                           "note": "SoA state read + written per tick without the materialised heartbeat "
-                                   "bodies, over the same k_tick launch time"},
+                           "achieved": state_bytes / (classify_ms * 1e-3) / 1e9 if classify_ms > 0 else 0.0,
+                           "unit": "GB/s", "classify_ms": classify_ms,
+                           "note": "SoA state read + written per tick without the materialised heartbeat bodies, "
+                                   "over the classification phase (first chain block start to the last arrival, "
+                                   "kernel clock stamps), which runs under the heartbeat stream"},
         }
         if REHEARSAL:
             out["rehearsal"] = "all ranks on GPU 0, host allgather instead of RCCL: not a reported measurement"
@@ -492,6 +543,8 @@ def main():
             out["churn"] = churn
         if flap is not None:
             out["flap"] = flap
+        if hb_once is not None:
+            out["heartbeat_once"] = hb_once
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
         sys.stdout.flush()

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KWOK_ABI_VERSION 3u
+#define KWOK_ABI_VERSION 4u
 #define KWOK_COMM_ID_BYTES 128u
 
 /* ---- status codes (int return values; per-record codes in out_status) ---- */
@@ -171,7 +171,7 @@ typedef struct kwok_config {
                                       the most pods one bucket can hold (multiple of 8, <= 65528;
                                       0 = pod_slots_per_bucket, i.e. no growth).  Handles stay valid
                                       when a bucket's capacity grows (KWOK_EFULL only past it). */
-    uint32_t reserved0;
+    uint32_t flags;                /* KWOK_CFG_* */
     const char* pod_status_template; /* KWOK_TPL_POD: Config.PodStatusTemplate (controller.go:76),
                                         compiled per registered pod spec into the kernels' byte
                                         program; KWOK_EDOMAIN when its output does not fit that
@@ -184,6 +184,14 @@ typedef struct kwok_config {
                                         every node, <= 1280 bytes (see kwok_heartbeat_template_patch) */
 } kwok_config;
 enum { KWOK_TPL_POD = 1, KWOK_TPL_NODE_INIT = 2, KWOK_TPL_HEARTBEAT = 4 };
+/* kwok_config.flags */
+enum {
+    /* every heartbeat patch of a tick is the same body (node_controller.go:393-401):
+       materialise ONE (at heartbeat_off; kwok_tick_result.heartbeat_stride = 0) with
+       the full handle list, for callers that send one body to every node (the
+       cgo drop-in does) - the tick then moves the SoA state, not n copies */
+    KWOK_CFG_HEARTBEAT_ONCE = 1
+};
 
 /* fleet counters (kwok_tick_result.counters, summed over ranks) */
 enum {
@@ -206,7 +214,8 @@ enum {
 typedef struct kwok_tick_result {
     uint32_t n_heartbeat;       /* number of heartbeat patches (one per managed node) */
     uint32_t heartbeat_len;     /* bytes of every heartbeat patch (identical bodies) */
-    uint64_t heartbeat_stride;  /* arena distance between consecutive heartbeat patches */
+    uint64_t heartbeat_stride;  /* arena distance between consecutive heartbeat patches (0 with
+                                   KWOK_CFG_HEARTBEAT_ONCE: one body for every handle) */
     uint32_t n_node_init;
     uint32_t n_pod_patch;
     uint32_t n_delete;

@@ -50,6 +50,32 @@ type gpuEngine struct {
 	h       *C.kwok_engine
 	hb      []int32 // heartbeat handle list of heartbeat epoch hbEpoch
 	hbEpoch uint32
+	// page-locked batch buffers (kwok_host_alloc), reused: kwok_ingest_pods copies
+	// records and strings to the GPU by DMA from these
+	evBuf, arBuf hostBuf
+}
+
+type hostBuf struct {
+	p unsafe.Pointer
+	n int
+}
+
+func (b *hostBuf) get(n int) unsafe.Pointer {
+	if n > b.n || b.p == nil {
+		if b.p != nil {
+			C.kwok_host_free(b.p)
+		}
+		b.n = n + n/4 + 64
+		b.p = C.kwok_host_alloc(C.size_t(b.n))
+	}
+	return b.p
+}
+
+func (b *hostBuf) free() {
+	if b.p != nil {
+		C.kwok_host_free(b.p)
+		b.p, b.n = nil, 0
+	}
 }
 
 func (g *gpuEngine) lastError() string { return C.GoString(C.kwok_last_error(g.h)) }
@@ -126,6 +152,8 @@ func (g *gpuEngine) close() {
 		C.kwok_engine_destroy(g.h)
 		g.h = nil
 	}
+	g.evBuf.free()
+	g.arBuf.free()
 }
 
 func arenaPtr(arena []byte) *C.char {
@@ -168,12 +196,32 @@ func (g *gpuEngine) ingestNodes(ev []C.kwok_node_event, arena []byte) (handles, 
 	return
 }
 
-func (g *gpuEngine) ingestPods(ev []C.kwok_pod_event, arena []byte) (handles, status []int32, released []uint32, err error) {
-	handles, status, released = make([]int32, len(ev)), make([]int32, len(ev)), make([]uint32, len(ev))
-	if len(ev) == 0 {
+// ingestPods copies the records into the page-locked record buffer and packs
+// the strings they reference (spec.nodeName, status.hostIP / podIP) into the
+// page-locked arena: the batch's object JSON stays on the host.
+func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, status []int32, released []uint32, err error) {
+	handles, status, released = make([]int32, len(evs)), make([]int32, len(evs)), make([]uint32, len(evs))
+	if len(evs) == 0 {
 		return
 	}
-	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(len(ev)), arenaPtr(arena), C.size_t(len(arena)),
+	ev := unsafe.Slice((*C.kwok_pod_event)(g.evBuf.get(len(evs)*int(unsafe.Sizeof(evs[0])))), len(evs))
+	need := 0
+	for i := range evs {
+		need += int(evs[i].node_name.len + evs[i].host_ip.len + evs[i].pod_ip.len)
+	}
+	ar := unsafe.Slice((*byte)(g.arBuf.get(need+1)), need+1)
+	off := 0
+	pack := func(s C.kwok_str) C.kwok_str {
+		n := copy(ar[off:], arena[s.off:s.off+s.len])
+		r := C.kwok_str{off: C.uint32_t(off), len: C.uint32_t(n)}
+		off += n
+		return r
+	}
+	for i := range evs {
+		ev[i] = evs[i]
+		ev[i].node_name, ev[i].host_ip, ev[i].pod_ip = pack(evs[i].node_name), pack(evs[i].host_ip), pack(evs[i].pod_ip)
+	}
+	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(len(ev)), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
 		(*C.int32_t)(&handles[0]), (*C.int32_t)(&status[0]), (*C.uint32_t)(&released[0]))
 	if rc < 0 {
 		err = fmt.Errorf("kwok_ingest_pods: %d: %s", int(rc), g.lastError())

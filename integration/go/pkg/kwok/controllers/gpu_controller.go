@@ -71,8 +71,9 @@ type GPUController struct {
 	pods  objBatch
 
 	// tick loop only
-	nodeName map[int32]string // node handle -> name
-	podByUID map[types.UID]int32
+	nodeName   map[int32]string // node handle -> name
+	nodeHandle map[string]int32 // name -> node handle (nodes the engine holds; pods name them by handle)
+	podByUID   map[types.UID]int32
 	podUID   map[int32]types.UID // pod handle -> UID (the reverse of podByUID)
 	podRef   map[int32]types.NamespacedName
 }
@@ -93,7 +94,8 @@ func newGPUController(conf Config, interval time.Duration) (*GPUController, erro
 	}
 	return &GPUController{
 		conf: conf, eng: eng, codec: codec, interval: interval, finalizer: finalizerPatch(),
-		nodeName: map[int32]string{}, podByUID: map[types.UID]int32{}, podUID: map[int32]types.UID{},
+		nodeName: map[int32]string{}, nodeHandle: map[string]int32{}, podByUID: map[types.UID]int32{},
+		podUID: map[int32]types.UID{},
 		podRef: map[int32]types.NamespacedName{},
 	}, nil
 }
@@ -346,8 +348,10 @@ func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
 		}
 		if keep[i].op == C.KWOK_OP_DELETE {
 			delete(c.nodeName, hs[i])
+			delete(c.nodeHandle, names[i])
 		} else {
 			c.nodeName[hs[i]] = names[i]
+			c.nodeHandle[names[i]] = hs[i]
 		}
 	}
 	return nil
@@ -405,7 +409,12 @@ func (c *GPUController) flushPods(ctx context.Context, tasks *parallelTasks, b o
 					d.ev.handle = C.int32_t(h)
 				}
 				d.ev.spec_id = C.int32_t(id)
+				// the node by handle when the engine holds it (no name lookup on the host);
+				// otherwise by spec.nodeName (a deleted node pods still reference, or none yet)
 				d.ev.node_handle = -1
+				if nh, ok := c.nodeHandle[str(b.arena, d.ev.node_name)]; ok {
+					d.ev.node_handle = C.int32_t(nh)
+				}
 			}
 			evs = append(evs, d.ev)
 			keep = append(keep, r)

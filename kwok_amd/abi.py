@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 COMM_ID_BYTES = 128
 
 OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE, EBUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8, -9
@@ -86,7 +86,7 @@ class Config(C.Structure):
                 ("pod_slots_per_bucket", C.c_uint32), ("max_pod_specs", C.c_uint32),
                 ("rank", C.c_int32), ("world_size", C.c_int32), ("device", C.c_int32),
                 ("comm_id", C.c_void_p), ("allgather", ALLGATHER_FN), ("allgather_user", C.c_void_p),
-                ("pod_handle_stride", C.c_uint32), ("reserved0", C.c_uint32),
+                ("pod_handle_stride", C.c_uint32), ("flags", C.c_uint32),
                 ("pod_status_template", C.c_char_p), ("node_init_template", C.c_char_p),
                 ("node_heartbeat_template", C.c_char_p)]
 
@@ -107,6 +107,7 @@ class Outputs(C.Structure):
                 ("arena_shift", C.c_uint64), ("arena_copied", C.c_uint64)]
 
 READ_HEARTBEAT_ONCE = 1
+CFG_HEARTBEAT_ONCE = 1
 
 
 class DeviceView(C.Structure):

@@ -1149,7 +1149,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     if (!out) return KWOK_EINVAL;
     *out = nullptr;
     if (!cfg || cfg->abi_version != KWOK_ABI_VERSION) return KWOK_EINVAL;
-    if ((cfg->custom_templates & ~(KWOK_TPL_POD | KWOK_TPL_NODE_INIT | KWOK_TPL_HEARTBEAT)) ||
+    if ((cfg->custom_templates & ~(KWOK_TPL_POD | KWOK_TPL_NODE_INIT | KWOK_TPL_HEARTBEAT)) || (cfg->flags & ~1u) ||
         ((cfg->custom_templates & KWOK_TPL_POD) && !cfg->pod_status_template) ||
         ((cfg->custom_templates & KWOK_TPL_NODE_INIT) && !cfg->node_init_template) ||
         ((cfg->custom_templates & KWOK_TPL_HEARTBEAT) && !cfg->node_heartbeat_template))
@@ -1298,6 +1298,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.multi = e->multi ? 1 : 0;
     S.cni = cfg->enable_cni ? 1u : 0u;
     S.custom_pod = (cfg->custom_templates & KWOK_TPL_POD) ? 1u : 0u;
+    S.hb_once = (cfg->flags & KWOK_CFG_HEARTBEAT_ONCE) ? 1u : 0u;
     S.buckets = e->B;
     {
         // a chain block's bucket range must fit its LDS node flags and 64 pod chunks
@@ -1502,22 +1503,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     // a deleted node's entry lives while pods reference it (the pods' node refs,
     // pod_controller.go routes by spec.nodeName): the references of the nodes this
     // batch deletes, counted on the device (no pod changes during a node batch)
-    std::unordered_map<uint32_t, uint32_t> refs;
-    {
-        std::vector<uint32_t> del;
-        for (size_t i = 0; i < n; i++) {
-            const kwok_node_event& x = ev[i];
-            uint32_t slot = 0;
-            if (x.op == KWOK_OP_DELETE && x.name.len && x.name.len <= 253 && in_arena(x.name) &&
-                node_slot(e, arena + x.name.off, x.name.len, false, &slot) == KWOK_OK)
-                del.push_back(slot);
-        }
-        if (!del.empty()) {
-            std::vector<uint32_t> cnt;
-            if (int rc = node_refs(e, del, cnt)) return rc;
-            for (size_t k = 0; k < del.size(); k++) refs[del[k]] = cnt[k];
-        }
-    }
+    std::unordered_map<uint32_t, uint32_t> refs;  // (filled below, before any record is ingested)
     auto refs_of = [&](uint32_t slot) {  // a node created in this batch has none
         auto it = refs.find(slot);
         return it == refs.end() ? 0u : it->second;
@@ -1642,27 +1628,50 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         const uint32_t b = fnv1a32(arena + x.name.off, x.name.len) & (e->B - 1);
         return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
     };
-    const auto tn0 = std::chrono::steady_clock::now();
     std::vector<int> rej((size_t)e->n_part, 0);
     static const size_t par_min = getenv("KWOK_NODE_PAR_MIN") ? strtoull(getenv("KWOK_NODE_PAR_MIN"), nullptr, 10)
                                                              : NODE_PAR_MIN;
-    if (n < par_min || e->n_part == 1) {
+    const bool threaded = n >= par_min && e->n_part > 1;
+    const int P = e->n_part;
+    std::vector<uint8_t> part(threaded ? n : 0);
+    auto tq1 = clk::now();
+    {
+        // pass 1 (read-only, by record chunks): each record's partition, and the
+        // entries of the nodes this batch deletes (their references are counted
+        // on the device before any record is applied: no pod changes during a
+        // node batch)
+        std::vector<std::vector<uint32_t>> dels((size_t)P);
+        auto pass1 = [&](int c) {
+            const size_t lo = threaded ? n * (size_t)c / (size_t)P : 0, hi = threaded ? n * (size_t)(c + 1) / (size_t)P : n;
+            for (size_t i = lo; i < hi; i++) {
+                const int64_t bl = bucket_of_record(ev[i]);
+                if (threaded) part[i] = (uint8_t)(bl < 0 ? 0 : (uint64_t)bl * (uint64_t)P / e->nb);
+                uint32_t slot = 0;
+                if (bl >= 0 && ev[i].op == KWOK_OP_DELETE &&
+                    node_slot(e, arena + ev[i].name.off, ev[i].name.len, false, &slot) == KWOK_OK)
+                    dels[(size_t)c].push_back(slot);
+            }
+        };
+        if (threaded) run_parts(e, true, pass1);
+        else pass1(0);
+        tq1 = clk::now();
+        std::vector<uint32_t> del;
+        for (auto& d : dels) del.insert(del.end(), d.begin(), d.end());
+        if (!del.empty()) {
+            std::vector<uint32_t> cnt;
+            if (int rc = node_refs(e, del, cnt)) return rc;
+            for (size_t k = 0; k < del.size(); k++) refs[del[k]] = cnt[k];
+        }
+    }
+    const auto tn0 = clk::now();  // (refs: tq0 .. tn0)
+    if (!threaded) {
         for (size_t i = 0; i < n; i++) {
             const int64_t bl = bucket_of_record(ev[i]);
-            const int part = bl < 0 ? 0 : (int)((uint64_t)bl * e->n_part / e->nb);
-            rej[(size_t)part] += ingest_one(i, part);
+            const int p = bl < 0 ? 0 : (int)((uint64_t)bl * e->n_part / e->nb);
+            rej[(size_t)p] += ingest_one(i, p);
         }
     } else {
         // partitions own bucket ranges (as for pods); each takes its records in batch order
-        std::vector<uint8_t> part(n);
-        const int P = e->n_part;
-        run_parts(e, true, [&](int c) {
-            const size_t lo = n * (size_t)c / (size_t)P, hi = n * (size_t)(c + 1) / (size_t)P;
-            for (size_t i = lo; i < hi; i++) {
-                const int64_t bl = bucket_of_record(ev[i]);
-                part[i] = (uint8_t)(bl < 0 ? 0 : (uint64_t)bl * (uint64_t)P / e->nb);
-            }
-        });
         run_parts(e, true, [&](int p) {
             for (size_t i = 0; i < n; i++)
                 if (part[i] == (uint8_t)p) rej[(size_t)p] += ingest_one(i, p);
@@ -1685,8 +1694,8 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     if ((rc = size_arena(e))) return rc;
     rc = flush_ops(e);
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu node records: refs %.2f ms, records %.2f ms, flush %.2f ms\n", n,
-                ms_between(tq0, tn0), std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
+        fprintf(stderr, "[kwok ingest] %zu node records (%s): lookups %.2f ms, refs %.2f ms, records %.2f ms, "
+                        "flush %.2f ms\n", n, threaded ? "threaded" : "1 thread", ms_between(tq0, tq1), ms_between(tq1, tn0), std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tn1).count());
     return rc ? rc : rejected;
 }
@@ -1713,6 +1722,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     HIPCHK(e, hipMemsetAsync(G.dels, 0, (size_t)e->nb * 4, st));
     HIPCHK(e, hipMemcpyAsync(G.d_ev, ev, n * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
     if (arena_len) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    double t_h2d = 0;
+    if (e->iprof) {  // diagnostics: the copies on their own
+        HIPCHK(e, hipStreamSynchronize(st));
+        t_h2d = ms_between(t0, clk::now());
+    }
     launch_ingest_prep(e->S, I, st);
     launch_ingest_need(e->S, I, st);
     HIPCHK(e, hipGetLastError());
@@ -1806,8 +1820,9 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     if (out_released) HIPCHK(e, hipMemcpyAsync(out_released, G.out_released, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu pod records (GPU): copy + prep %.2f ms, resolve + sort %.2f ms, apply %.2f ms "
-                        "(%d rounds), results %.2f ms\n", n, ms_between(t0, t1), ms_between(t1, t2), ms_between(t2, t3),
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU): copy + prep %.2f ms (H2D %.2f ms, %.1f GB/s), "
+                        "resolve + sort %.2f ms, apply %.2f ms (%d rounds), results %.2f ms\n", n, ms_between(t0, t1),
+                t_h2d, (n * sizeof(kwok_pod_event) + arena_len) / (t_h2d * 1e6), ms_between(t1, t2), ms_between(t2, t3),
                 rounds, ms_between(t3, clk::now()));
     return (int)G.sum_h->rejected;
 }
@@ -1930,7 +1945,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // (plain stores); a larger one (1M nodes: 1.07 GB) is written non-temporally:
     // 239 -> 216 us per 1M x 10M tick (no L2 pollution under the chain's reads,
     // no dirty L2 left for the kernel-end write-back)
-    const uint64_t hb_bytes = nhb * (uint64_t)e->hb_stride;
+    const uint64_t hb_bytes = (S.hb_once ? std::min<uint32_t>(nhb, 1u) : nhb) * (uint64_t)e->hb_stride;
     S.hb_nt = e->nt_env >= 0 ? (uint32_t)e->nt_env : (hb_bytes >= (256ull << 20) ? 1u : 0u);
     // the streamers' share: with the non-temporal stream the chain blocks finish
     // sooner (1M x 10M: classification 172 -> 122 us) and take more of the tail
@@ -2022,7 +2037,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
 
 // single rank: the kernel publishes the tick's field totals (TickHdr::tot); the
 // counts, output layout and counters follow from them
-void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride) {
+void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride, bool hb_once) {
     const uint64_t* t = H.tot;
     H.n_hb = (uint32_t)t[AG_HB];
     H.n_init = (uint32_t)t[AG_INIT];
@@ -2036,7 +2051,7 @@ void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride) {
     H.init_bytes = t[AG_INIT_BYTES];
     H.pp_bytes = t[AG_PP_BYTES];
     H.hb_base = 0;
-    H.init_base = (uint64_t)H.n_hb * hb_stride;
+    H.init_base = (uint64_t)(hb_once ? std::min<uint32_t>(H.n_hb, 1u) : H.n_hb) * hb_stride;
     H.pod_base = H.init_base + H.init_bytes;
     H.arena_bytes = H.pod_base + H.pp_bytes;
     H.overflow = H.arena_bytes > arena_cap;
@@ -2140,7 +2155,7 @@ int retire(kwok_engine* e) {
         if (rc) return failed(rc);
     }
     const auto t2 = clk::now();
-    if (!e->multi) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride);
+    if (!e->multi) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride, e->S.hb_once != 0);
     const TickHdr& H = *T.hdr_h;
     if (!H.err && (H.n_pp || H.n_init) && !T.emit_queued) {
         // jobs nobody expected (no events since the previous tick): their bytes now
@@ -2217,7 +2232,7 @@ int retire(kwok_engine* e) {
     memset(&r, 0, sizeof(r));
     r.n_heartbeat = H.n_hb;
     r.heartbeat_len = e->hb_len;
-    r.heartbeat_stride = e->hb_stride;
+    r.heartbeat_stride = e->S.hb_once ? 0 : e->hb_stride;
     r.n_node_init = H.n_init;
     r.n_pod_patch = H.n_pp;
     r.n_delete = H.n_del;
@@ -2379,14 +2394,50 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
     return KWOK_OK;
 }
 
+// Page-locked batch buffers: 2 MiB-aligned anonymous memory on transparent huge
+// pages where the kernel grants them, registered with the runtime (the GPU's
+// copies walk 512x fewer page translations than over 4 KiB pages);
+// KWOK_HOST_ALLOC=hip: hipHostMalloc instead.
+namespace {
+std::mutex g_host_mu;
+std::unordered_map<void*, size_t> g_host_reg;  // registered (mmap) buffers -> mapped length
+}  // namespace
 void* kwok_host_alloc(size_t bytes) {
+    bytes = bytes ? bytes : 1;
+    const char* how = getenv("KWOK_HOST_ALLOC");
+    if (!(how && strcmp(how, "hip") == 0)) {
+        const size_t huge = (size_t)2 << 20, len = (bytes + huge - 1) & ~(huge - 1);
+        void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p != MAP_FAILED) {
+            (void)madvise(p, len, MADV_HUGEPAGE);
+            memset(p, 0, len);  // first touch: the pages exist (huge where granted) before pinning
+            if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+                std::lock_guard<std::mutex> l(g_host_mu);
+                g_host_reg[p] = len;
+                return p;
+            }
+            munmap(p, len);
+        }
+    }
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
     return p;
 }
 
 void kwok_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    size_t len = 0;
+    {
+        std::lock_guard<std::mutex> l(g_host_mu);
+        auto it = g_host_reg.find(p);
+        if (it != g_host_reg.end()) len = it->second, g_host_reg.erase(it);
+    }
+    if (len) {
+        (void)hipHostUnregister(p);
+        munmap(p, len);
+    } else {
+        (void)hipHostFree(p);
+    }
 }
 
 int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {

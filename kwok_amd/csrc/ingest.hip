@@ -598,7 +598,17 @@ __global__ void k_node_refs(DevState S, const uint32_t* slots, uint32_t n, uint3
     const uint32_t fill = S.pod_fill[b];
     const size_t sb = (size_t)b * S.cp;
     uint32_t c = 0;
-    for (uint32_t s = lane(); s < fill; s += 64) c += (S.pod_state[sb + s] & PS_USED) && S.pod_node[sb + s] == nd;
+    // 8 slots per lane per step (16-byte loads of state and node index): few round trips
+    for (uint32_t s = lane() * 8; s < fill; s += 512) {
+        const uint4 st = *reinterpret_cast<const uint4*>(S.pod_state + sb + s);
+        const uint4 ndw = *reinterpret_cast<const uint4*>(S.pod_node + sb + s);
+        const uint32_t a[4] = {st.x, st.y, st.z, st.w}, q[4] = {ndw.x, ndw.y, ndw.z, ndw.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            c += (a[k] & PS_USED) && (q[k] & 0xFFFFu) == nd;
+            c += ((a[k] >> 16) & PS_USED) && (q[k] >> 16) == nd;
+        }
+    }
     for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
     if (lane() == 0) refs[i] = c;
 }

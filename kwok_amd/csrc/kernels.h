@@ -90,6 +90,7 @@ struct DevState {
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)
     uint32_t hb_nt;            // heartbeat stores non-temporal (streams larger than the Infinity Cache)
+    uint32_t hb_once;          // KWOK_CFG_HEARTBEAT_ONCE: one heartbeat body per tick, not one per node
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
     uint32_t custom_pod;       // Config.PodStatusTemplate is custom: the caller's CONFORMS digest is ignored
     uint32_t buckets;          // B (all ranks)

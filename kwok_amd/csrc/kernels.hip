@@ -1303,6 +1303,10 @@ __device__ __forceinline__ void build_hb_template(const DevState& S, uint8_t* tm
 // launch completes.  Single rank: when a pool phase follows, its leader
 // publishes the Get plan / cursor (skip_alloc) and its stamps (skip_pool).
 // ---------------------------------------------------------------------------
+// heartbeat bodies the tick materialises: one per managed node, or one in all
+// (KWOK_CFG_HEARTBEAT_ONCE: every node's patch is that body)
+__device__ __forceinline__ uint32_t hb_bodies(const DevState& S, uint32_t n_hb) { return S.hb_once ? min(n_hb, 1u) : n_hb; }
+
 // word i of the tick header (TickHdr as 61 x u64), computed by thread i
 __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint32_t n_hb, uint32_t hb_stride, uint32_t nu,
                                                 uint64_t pool_index, uint64_t arena_cap, bool single, const uint64_t* clk) {
@@ -1312,7 +1316,7 @@ __device__ __forceinline__ uint64_t header_word(int i, const uint64_t* tot, uint
                       offsetof(TickHdr, alloc_total) == 352 && offsetof(TickHdr, clk) == 416 &&
                       offsetof(TickHdr, err) == 480,
                   "TickHdr layout");
-    const uint64_t patch_base = (uint64_t)n_hb * hb_stride;
+    const uint64_t patch_base = (uint64_t)n_hb * hb_stride;  // n_hb: the heartbeat bodies materialised
     const uint64_t arena_bytes = patch_base + tot[AG_INIT_BYTES] + tot[AG_PP_BYTES];
     auto pair = [](uint64_t lo, uint64_t hi) { return (uint64_t)(uint32_t)lo | (uint64_t)(uint32_t)hi << 32; };
     if (i >= W_LC && i < W_C + 16) {
@@ -1367,7 +1371,7 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
     const bool skip_alloc = single && tot[AG_ALLOC] != 0, skip_pool = single && (tot[AG_ALLOC] | tot[AG_REL]) != 0;
     const int i = threadIdx.x;
     if (i < NW) {
-        const uint64_t w = header_word(i, tot, n_hb, 16u * S.hb_units, nu, pool_index, S.arena_cap, single, clk);
+        const uint64_t w = header_word(i, tot, hb_bodies(S, n_hb), 16u * S.hb_units, nu, pool_index, S.arena_cap, single, clk);
         const bool pool_clk = i == C0 + CLK_BACK || i == C0 + CLK_POOL;
         // the pool leader may already have written its fields (it runs concurrently)
         if (!(skip_pool && (pool_clk || (i >= A0 && i < A1)))) reinterpret_cast<uint64_t*>(S.hdr)[i] = w;
@@ -1386,7 +1390,8 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
             X->n_rel = nr;
             constexpr int LC = offsetof(TickHdr, local_counters) / 8;
             for (int k = 0; k < 16; k++)
-                X->counters[k] = header_word(LC + k, tot, n_hb, 16u * S.hb_units, nu, pool_index, S.arena_cap, single, clk);
+                X->counters[k] = header_word(LC + k, tot, hb_bodies(S, n_hb), 16u * S.hb_units, nu, pool_index,
+                                             S.arena_cap, single, clk);
         }
     }
     if (!single && nu + nr <= (uint32_t)XINLINE) {  // exchange lists inline when they fit
@@ -1526,7 +1531,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
         __syncthreads();
     }
     if (t == 0) {
-        const uint64_t patch_base = (uint64_t)n_hb * (16u * S.hb_units);
+        const uint64_t patch_base = (uint64_t)hb_bodies(S, n_hb) * (16u * S.hb_units);
         l.L->init_base = patch_base;
         l.L->pod_base = patch_base + l.sums->tot[AG_INIT_BYTES];
         l.L->alloc_base = alloc_base;
@@ -1618,7 +1623,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             while (__builtin_amdgcn_s_memrealtime() - t0 < S.stream_delay) __builtin_amdgcn_s_sleep(4);
         }
-        if (!(phases & TICK_NOSTREAM)) hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, true, b - S.n_chain, gridDim.x - S.n_chain);
+        if (!(phases & TICK_NOSTREAM))
+            hb_fill_share<GEN_HB>(S, hb_tmpl4, hb_bodies(S, n_hb), true, b - S.n_chain, gridDim.x - S.n_chain);
         if ((phases & TICK_PROF) && t == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             atomicMax(&S.bar->stream_end_max, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1788,7 +1794,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             TSTAMP(12);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
-                hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+                hb_fill_share<GEN_HB>(S, hb_tmpl4, hb_bodies(S, n_hb), false, b, S.n_chain);
             }
             TSTAMP(13);
             if (t < AG_DIRTY && (acc_old >> ACC_SHIFT) == S.n_chain - 1u) {
@@ -1834,7 +1840,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
             if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
-                hb_fill_share<GEN_HB>(S, hb_tmpl4, n_hb, false, b, S.n_chain);
+                hb_fill_share<GEN_HB>(S, hb_tmpl4, hb_bodies(S, n_hb), false, b, S.n_chain);
             }
             return;  // the BACK launch follows the exchange
         }

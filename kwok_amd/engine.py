@@ -130,7 +130,7 @@ class TickOutput:
 def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200, buckets=4096,
                 node_slots_per_bucket=64, pod_slots_per_bucket=512, max_pod_specs=1024, rank=0, world_size=1,
                 device=0, comm_id=None, allgather=None, enable_cni=False, pod_handle_stride=0,
-                pod_status_template=None, node_init_template=None, node_heartbeat_template=None):
+                pod_status_template=None, node_init_template=None, node_heartbeat_template=None, heartbeat_once=False):
     cfg = abi.Config()
     cfg.abi_version = abi.ABI_VERSION
     cfg.cidr = cidr.encode()
@@ -143,6 +143,7 @@ def make_config(cidr="10.0.0.1/24", node_ip="196.168.0.1", start_time=1704067200
     cfg.rank, cfg.world_size, cfg.device = rank, world_size, device
     cfg.enable_cni = 1 if enable_cni else 0
     cfg.pod_handle_stride = pod_handle_stride
+    cfg.flags = abi.CFG_HEARTBEAT_ONCE if heartbeat_once else 0
     keep = []
     if pod_status_template is not None:
         b = C.create_string_buffer(pod_status_template.encode())

@@ -546,6 +546,39 @@ def scenario_churn(seed=0x6B776F6B, n_nodes=24, ticks=8):
     return cfg, out
 
 
+def scenario_e2e_kwok_test(tpl):
+    """test/kwok/kwok.test.sh restated as a trace, with the deployment's flags
+    (kustomize/kwok/kwok-deployment.yaml:22-29: annotation selector
+    kwok.x-k8s.io/node=fake, disregard kwok.x-k8s.io/status=custom, CIDR
+    10.0.0.1/24) and its objects (test/kwok/fake-node.yaml, fake-deployment.yaml:
+    5 replicas of fake-container / fake on fake-node):
+      t0  test_node_ready / test_pod_running (:39-73): fake-node is initialised and
+          heartbeats; the 5 pods go Running with 10.0.0.1..5;
+      t1  test_modify_node_status (:76-89): the node gets the disregard annotation,
+          then a status patch nodeInfo.kubeletVersion = fake-new: heartbeats go on,
+          no init patch overwrites the status;
+      t2  test_modify_pod_status (:92-104): the first pod gets the disregard
+          annotation, then a status patch podIP = 192.168.0.1: it is not patched
+          again and keeps that podIP;
+      t3  a steady tick."""
+    node_ip = "10.244.0.7"  # --node-ip=$(POD_IP): the kwok pod's address
+    spec = {"containers": [["fake-container", "fake"]], "init": [], "gates": []}
+    pods = [pe("fake-pod-7d4b9c5f8d-%s" % s, "fake-node", spec=spec) for s in ("2xkqp", "8hz4w", "c6rnm", "lt9vb", "x5w7j")]
+    t0 = dict(nodes=[ne("fake-node")], pods=pods)
+    # the node's status after its init patch (node.status.tpl), then the user's edit
+    init = json.loads(render_node_init(tpl, ne("fake-node"), rfc3339(S0 + 30), rfc3339(S0), node_ip))["status"]
+    st = dict(addresses=init["addresses"], allocatable=init["allocatable"], capacity=init["capacity"],
+              phase=init["phase"], nodeInfo=dict(init["nodeInfo"]))
+    edited = dict(st, nodeInfo=dict(st["nodeInfo"], kubeletVersion="fake-new"))
+    t1 = dict(nodes=[ne("fake-node", lockable=False, **st), ne("fake-node", lockable=False, **edited)], pods=[])
+    first = pods[0]["key"]
+    running = dict(phase="Running", conforms=True, hostIP=node_ip, podIP="10.0.0.1", spec=spec)
+    t2 = dict(nodes=[], pods=[dict(pe(first, "fake-node", disregard=True, **running), modify=True),
+                              dict(pe(first, "fake-node", disregard=True, **dict(running, podIP="192.168.0.1")),
+                                   modify=True)])
+    return base_cfg(node_ip=node_ip, cidr="10.0.0.1/24"), [t0, t1, t2, dict(nodes=[], pods=[])]
+
+
 def run_scenario(name, cfg, ticks, tpl):
     sim = Sim(cfg, tpl)
     handles = {}
@@ -681,7 +714,8 @@ def main():
                      ("doc_known_answer", scenario_doc_known_answer),
                      ("cidr_overflow", scenario_cidr_overflow),
                      ("specs", scenario_specs),
-                     ("churn", scenario_churn)]:
+                     ("churn", scenario_churn),
+                     ("e2e_kwok_test", lambda: scenario_e2e_kwok_test(tpl))]:
         cfg, ticks = fn()
         fx = run_scenario(name, cfg, ticks, tpl)
         json.dump(fx, open(os.path.join(HERE, "trace_%s.json" % name), "w"), indent=None, separators=(",", ":"))

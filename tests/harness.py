@@ -15,7 +15,8 @@ from kwok_amd import abi
 from kwok_amd.engine import make_config
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-TRACES = ["reference_node_test", "reference_pod_test", "doc_known_answer", "cidr_overflow", "specs", "churn"]
+TRACES = ["reference_node_test", "reference_pod_test", "doc_known_answer", "cidr_overflow", "specs", "churn",
+          "e2e_kwok_test"]
 
 
 def load_trace(name):

@@ -63,7 +63,7 @@ STRUCTS = {
     "kwok_config": (abi.Config, ["abi_version", "cidr", "node_ip", "start_time_unix", "enable_cni",
                                  "custom_templates", "buckets", "node_slots_per_bucket", "pod_slots_per_bucket",
                                  "max_pod_specs", "rank", "world_size", "device", "comm_id", "allgather",
-                                 "allgather_user", "pod_handle_stride", "reserved0", "pod_status_template",
+                                 "allgather_user", "pod_handle_stride", "flags", "pod_status_template",
                                  "node_init_template", "node_heartbeat_template"]),
     "kwok_tick_result": (abi.TickResult, ["n_heartbeat", "heartbeat_len", "heartbeat_stride", "n_node_init",
                                           "n_pod_patch", "n_delete", "heartbeat_epoch", "arena_bytes", "counters",

@@ -1,12 +1,16 @@
 """GPU: custom pod status templates (Config.PodStatusTemplate, controller.go:76;
 SURVEY §8(f) rank 3).  The engine compiles the template per registered pod
 spec into the kernels' A | hostIP | B | podIP | C program; every pod patch
-k_emit writes must equal the host assembly of that program
-(kwok_pod_template_patch, checked against tests/golden/gotmpl.py in
-tests/test_template_cpu.py) and, for a sample, gotmpl.py itself.  Who is
-patched, IP allocation, deletes and counters do not depend on the template:
-they must equal the oracle's (default template) on the same events."""
+k_emit writes must equal tests/golden/gotmpl.py's rendering of the template
+(an independent Go text/template + yaml.v2 -> encoding/json interpreter) over
+the pod, and the host assembly of the program (kwok_pod_template_patch).
+Custom node-initialization and heartbeat bodies are likewise compared with
+gotmpl.py's rendering of the templates (node_controller.go:101 appends the
+heartbeat template to the node template).  Who is patched, IP allocation,
+deletes and counters do not depend on the template: they must equal the
+oracle's (default template) on the same events."""
 import ipaddress
+import json
 
 import numpy as np
 import pytest
@@ -15,7 +19,20 @@ from gpu_common import compare_state, new_pods
 from kwok_amd import abi, engine
 from kwok_amd.engine import Engine, make_config
 from oracle.oracle import Oracle
-from test_template_cpu import expected_patch, tpl
+import gotmpl_path  # noqa: F401
+import gotmpl
+from test_template_cpu import NODE_IP, START, expected_patch, node_doc, rfc3339, tpl
+
+
+def gotmpl_node(text, hb_text, n, now):
+    """configureNode's patch body, rendered by gotmpl.py (node_controller.go:101, :356-391)"""
+    funcs = {"NodeIP": lambda: NODE_IP, "Now": lambda: rfc3339(now), "StartTime": lambda: rfc3339(START)}
+    return ('{"status":%s}' % gotmpl.render_to_json(text + "\n" + hb_text, node_doc(n), funcs)).encode()
+
+
+def gotmpl_heartbeat(text, now):
+    funcs = {"NodeIP": lambda: NODE_IP, "Now": lambda: rfc3339(now), "StartTime": lambda: rfc3339(START)}
+    return ('{"status":%s}' % gotmpl.render_to_json(text, {"metadata": {}, "spec": {}, "status": {}}, funcs)).encode()
 
 pytestmark = pytest.mark.gpu
 
@@ -48,7 +65,7 @@ def test_custom_pod_template_engine(name):
     meta = {}  # handle -> (spec index, creation, original hostIP, status non-empty)
     now = 1704067230
     for t in range(3):
-        pods, par = new_pods(rng, nh, 4000, spec, host_ips=("10.9.8.7", "172.16.0.1"), host_ip_frac=0.3,
+        pods, par = new_pods(rng, nh, 900, spec, host_ips=("10.9.8.7", "172.16.0.1"), host_ip_frac=0.3,
                              years=40)
         pods["flags"] &= np.uint8(0xFF & ~abi.POD_DISREGARD)
         h1, s1, _ = e.ingest_pods_raw(pods, par)
@@ -63,7 +80,7 @@ def test_custom_pod_template_engine(name):
                             bool(pods[i]["flags"] & abi.POD_STATUS_NONEMPTY))
         if t:  # deletions: IP release and reuse in the same tick
             live = np.array(sorted(meta), np.int32)
-            dead = rng.choice(live, 500, replace=False)
+            dead = rng.choice(live, 200, replace=False)
             d = np.zeros(len(dead), abi.POD_EVENT_DTYPE)
             d["op"] = abi.OP_DELETE
             d["handle"] = dead
@@ -83,8 +100,7 @@ def test_custom_pod_template_engine(name):
             want = engine.pod_template_patch(text, cs, ics, gates, 1704067200, "196.168.0.1", ct, hip,
                                              int(pips[h]), ne)
             assert got == want, "tick %d pod %d" % (t, h)
-            if k % 97 == 0:
-                assert got == expected_patch(text, cs, ics, gates, ct, hip, int(pips[h]), ne)
+            assert got == expected_patch(text, cs, ics, gates, ct, hip, int(pips[h]), ne), "gotmpl: tick %d pod %d" % (t, h)
         for h, _ in E.pod_patches:  # applied: the status is no longer empty
             si, ct, hip, _ = meta[h]
             meta[h] = (si, ct, hip, True)
@@ -113,7 +129,7 @@ def test_custom_node_init_template_engine():
         h1, s1 = e.ingest_nodes_raw(ev, ar)
         h2, s2 = o.ingest_nodes_raw(ev, ar)
         assert s1[0] == 0 and h1[0] == h2[0]
-        recs[int(h1[0])] = (ev, ar)
+        recs[int(h1[0])] = (ev, ar, i % len(NODES))
     now = 1704067230
     for t in range(2):
         E, O = e.tick(now), o.tick(now)
@@ -123,9 +139,16 @@ def test_custom_node_init_template_engine():
             assert sorted(h for h, _ in E.node_inits) == sorted(recs)  # every node is initialised once
         else:
             assert E.node_inits == []  # the engine applied its patches: the nodes conform now
+        # the default heartbeat's conditions as a template of our own (the oracle's body
+        # with its Now / StartTime values as the funcs): node_controller.go:101 appends
+        # the heartbeat template to the node template
+        conds = json.dumps(json.loads(O.heartbeat_body(0))["status"]["conditions"], separators=(",", ":"))
+        hb_tpl = "conditions: " + conds.replace(rfc3339(now), "{{ Now }}").replace(rfc3339(START), "{{ StartTime }}")
+        want = {k: gotmpl_node(text, hb_tpl, n, now) for k, n in enumerate(NODES)}
         for h, got in E.node_inits:
-            ev, ar = recs[h]
+            ev, ar, k = recs[h]
             assert got == engine.node_template_patch(text, ev[0], ar, 1704067200, "196.168.0.1", now), h
+            assert got == want[k], "gotmpl: node %d" % h
         now += 30
     e.close()
     o.close()
@@ -148,12 +171,14 @@ def test_custom_heartbeat_template_engine(hb):
         h1, s1 = e.ingest_nodes_raw(ev, ar)
         h2, _ = o.ingest_nodes_raw(ev, ar)
         assert s1[0] == 0 and h1[0] == h2[0]
-        recs[int(h1[0])] = (ev, ar)
+        recs[int(h1[0])] = (ev, ar, i % len(NODES))
     now = 1704067230
     for t in range(3):
         E, O = e.tick(now), o.tick(now)
         assert list(E.heartbeat_nodes) == list(O.heartbeat_nodes)
         body = engine.heartbeat_template_patch(htext, 1704067200, "196.168.0.1", now)
+        assert body == gotmpl_heartbeat(htext, now)
+        want = {k: gotmpl_node(ntext, htext, n, now) for k, n in enumerate(NODES)}
         n = len(E.heartbeat_nodes)
         assert E.heartbeat_len == len(body) and E.heartbeat_stride == (len(body) + 15) // 16 * 16
         a = np.frombuffer(E.arena, np.uint8)[E.heartbeat_off:E.heartbeat_off + n * E.heartbeat_stride]
@@ -161,9 +186,10 @@ def test_custom_heartbeat_template_engine(hb):
         assert (a == np.frombuffer(body, np.uint8)[None, :]).all(), "tick %d heartbeat bodies" % t
         assert len(E.node_inits) == (len(recs) if t == 0 else 0)
         for h, got in E.node_inits:
-            ev, ar = recs[h]
+            ev, ar, k = recs[h]
             assert got == engine.node_template_patch(ntext, ev[0], ar, 1704067200, "196.168.0.1", now,
                                                      heartbeat_tpl=htext), h
+            assert got == want[k], "gotmpl: node %d" % h
         out = e.read_outputs(heartbeat_once=True)  # the compact hand-off carries one body
         assert out.heartbeat_body(0) == body
         now += 30

@@ -40,6 +40,20 @@ def test_engine_golden_trace_queued(name):
     e.close()
 
 
+@pytest.mark.parametrize("name", harness.TRACES)
+@pytest.mark.parametrize("queued", [False, True], ids=["blocking", "queued"])
+def test_engine_golden_trace_heartbeat_once(name, queued):
+    """KWOK_CFG_HEARTBEAT_ONCE: the tick materialises ONE heartbeat body for
+    every handle (heartbeat_stride 0); handles, body, node-init / pod patches,
+    deletes, counters and state are the goldens' (node_controller.go:393-401:
+    the body is the same for every node)"""
+    fx = harness.load_trace(name)
+    e = Engine(harness.config_for(fx, heartbeat_once=True))
+    (harness.replay_queued if queued else harness.replay)(fx, e)
+    assert e.last.heartbeat_stride == 0
+    e.close()
+
+
 @pytest.mark.parametrize("name", ["specs", "churn"])
 def test_engine_compact_readout(name):
     """KWOK_READ_HEARTBEAT_ONCE on the engine: one heartbeat body plus the patch

@@ -21,6 +21,6 @@ python3 $R/tools/trace_summary.py "$T" --last 45 --out $R/gpurun_out/ktrace_$TAG
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || exit 7
 done
-python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_${TAG}_FETCH_SIZE $R/gpurun_out/pmc_${TAG}_WRITE_SIZE $R/gpurun_out/pmc_${TAG}.json \
+python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_${TAG}_FETCH_SIZE $R/gpurun_out/pmc_${TAG}_WRITE_SIZE $R/gpurun_out/pmc_${TAG}.json --kernels $R/kwok_amd/csrc/kernels.hip \
   --source "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace (separate passes), bench.py --steps 20 --warmup 3, 1M nodes x 10M pods, 1x MI355X"
 exit 0
