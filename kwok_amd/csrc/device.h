@@ -47,6 +47,10 @@ constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS nod
 constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
 constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
 constexpr int SPEC_GROUPS = 3;            // pod groups per thread loaded before the fill marks land
+// split ticks (k_pod_jobs): a chain block's live groups in runs of 64, one wave each
+constexpr int WC_GROUPS = 64;
+constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block
+constexpr int WC_DIRTY_WORDS = MAX_WC / 32;
 constexpr int TRACE_SLOTS = 16;           // KWOK_TICK_TRACE=1: per-block phase stamps
 
 // ---- fixed template geometry (default templates) -----------------------------
@@ -127,6 +131,16 @@ constexpr int ACC_SHIFT = 54;  // arrivals in the top 10 bits (<= 1023 chain blo
 constexpr unsigned long long ACC_MASK = (1ull << ACC_SHIFT) - 1;
 constexpr int MAX_CHAIN = 512;  // k_tick chain blocks (reduce_records' LDS; engine_create clamps to it)
 static_assert(MAX_CHAIN < (1 << (64 - ACC_SHIFT)), "the accumulators count arrivals of every chain block");
+
+// split ticks: what k_pod_jobs needs of a chain block that has pod jobs (written
+// by that block in k_tick's BACK phases, after the pool phase): its first output
+// ordinals / byte offset, the tick's layout and pool plan, and the tick's tag
+struct JobBase {
+    uint64_t del, pp, pp_bytes, alloc;     // the block's exclusive prefix (AG_DEL, AG_PP, AG_PP_BYTES, AG_ALLOC)
+    uint64_t pod_base, alloc_base;         // Layout
+    uint64_t take, fin, fout0;             // PoolPlan
+    uint32_t tag, pad;
+};
 
 // exchange message, one per rank (allgather)
 constexpr int XINLINE = 2048;

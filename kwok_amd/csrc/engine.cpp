@@ -252,11 +252,13 @@ struct kwok_engine {
         DevState* S_pin = nullptr;  // pinned staging for its upload
         DevState S_up{};            // the copy last uploaded
         hipEvent_t done = nullptr;  // recorded after the tick's launches
-        hipEvent_t pev[6] = {};     // profiling: FRONT(+BACK) launch start/stop, BACK launch start/stop, k_emit
+        hipEvent_t pev[8] = {};     // profiling: FRONT(+BACK) launch start/stop, BACK launch start/stop, k_emit,
+                                    // k_pod_jobs
         uint4* pp_job = nullptr;    // k_tick -> k_emit job records
         uint64_t* init_job = nullptr;
         uint32_t* emit_n = nullptr;
         bool emit_queued = false;   // k_emit was enqueued behind the tick's launches
+        bool split = false;         // TICK_SPLIT: k_pod_jobs builds the pod jobs after the tick's launches
         bool alloc = false;
         // the tick in the slot
         int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
@@ -286,6 +288,7 @@ struct kwok_engine {
     bool sync_spin = true;      // spin on a tick's completion event (KWOK_SYNC=spin, the default)
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
+    bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
@@ -1119,7 +1122,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->d_hb_pre, e->S.hdr, e->S.xmsg,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg,
                     e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
     for (void* p : ptrs)
@@ -1279,6 +1282,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
+        const char* sj = getenv("KWOK_SPLIT");
+        e->split_jobs = !(sj && sj[0] == '0');
     }
     S.n_node_slots = e->NL;
     S.n_pod_slots = e->PL;
@@ -1326,6 +1331,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
         (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
         (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
+        (rc = dalloc(e, &S.wc_pre, (size_t)S.n_chain * MAX_WC)) ||
+        (rc = dalloc(e, &S.wc_dirty, (size_t)S.n_chain * WC_DIRTY_WORDS)) || (rc = dalloc(e, &S.jbase, (size_t)S.n_chain)) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_MAX_STRIDE)) ||
@@ -1954,7 +1961,12 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
                                        : (hb_bytes < (32ull << 20) ? 1024u : (S.hb_nt ? 860u : 921u));
     int rc = bind_slot(e, k);
     if (rc) return rc;
-    const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0);
+    // ticks that likely emit pod jobs (events since the last tick) build them in
+    // k_pod_jobs, one wave per dirty 64-group run, instead of the chain blocks'
+    // serial chunk walk (KWOK_SPLIT=0: the chain blocks, for A/B)
+    T.split = T.emit_queued && e->split_jobs;
+    const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
+                     (T.split ? TICK_SPLIT : 0);
     if (!requeue) {
         memset(T.hdr_h, 0, sizeof(TickHdr));  // the slot's previous tick was collected
         if (++e->tick_tag == 0) e->tick_tag = 1;
@@ -1977,6 +1989,10 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         if (rc) return rc;
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+        HIPCHK(e, hipGetLastError());
+    }
+    if (T.split) {
+        launch_pod_jobs(S, T.tag, st, ev ? ev[6] : nullptr, ev ? ev[7] : nullptr);
         HIPCHK(e, hipGetLastError());
     }
     // the patch bytes, when events since the last tick make jobs likely (otherwise
@@ -2026,9 +2042,13 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     }
     HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
     launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
-    launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed, TICK_BACK | TICK_XLISTS, T.tag,
-                T.target, st);
+    launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed,
+                TICK_BACK | TICK_XLISTS | (T.split ? TICK_SPLIT : 0), T.tag, T.target, st);
     HIPCHK(e, hipGetLastError());
+    if (T.split) {
+        launch_pod_jobs(S, T.tag, st);
+        HIPCHK(e, hipGetLastError());
+    }
     if ((rc = enqueue_emit(e, k))) return rc;  // this launch built the jobs
     HIPCHK(e, hipStreamSynchronize(st));
     if (next >= 0) return enqueue_tick(e, next, true);
@@ -2197,7 +2217,9 @@ int retire(kwok_engine* e) {
         if (e->multi) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
         float k2 = 0;
         if (T.emit_queued) (void)hipEventElapsedTime(&k2, T.pev[4], T.pev[5]);
-        const double kern = (double)k0 + k1 + k2;
+        float k3 = 0;
+        if (T.split) (void)hipEventElapsedTime(&k3, T.pev[6], T.pev[7]);
+        const double kern = (double)k0 + k1 + k2 + k3;
         // the streamers' latest exit, kept on the device (they never touch the header)
         unsigned long long send = 0;
         (void)release_for_host(e);
@@ -2214,7 +2236,7 @@ int retire(kwok_engine* e) {
         e->prof_ms[KWOK_T_EXCHANGE] += e->multi ? span(CLK_HDR, CLK_BACK) : 0.0;
         e->prof_ms[KWOK_T_POOL] += pool;
         // what follows the header in the chain (pool, job lists) beyond the stream, and k_emit
-        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2;
+        e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2 + k3;
         e->prof_ms[KWOK_T_KERNEL] += kern;
         e->prof_ms[KWOK_T_EMIT_KERNEL] += k2;
         e->prof_ticks++;

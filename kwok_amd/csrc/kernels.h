@@ -85,6 +85,9 @@ struct DevState {
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
+    uint4* wc_pre;             // split ticks: [n_chain][MAX_WC] in-block exclusive prefix of (del, pp, pp bytes, alloc)
+    uint32_t* wc_dirty;        //   per 64-group wave chunk, and [n_chain][WC_DIRTY_WORDS] its dirty bits (FRONT)
+    JobBase* jbase;            //   [n_chain] (BACK) -> k_pod_jobs
     uint64_t* trace;           // [grid][TRACE_SLOTS] per-block phase stamps (KWOK_TICK_TRACE=1), else null
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
@@ -117,11 +120,15 @@ void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStr
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
 // with work to emit, so they must be co-resident (tick_occupancy).
 constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16,  // NOSTREAM: diagnostics only
-              TICK_XLISTS = 32;  // BACK: the exchange lists were applied by k_pool_apply
+              TICK_XLISTS = 32,  // BACK: the exchange lists were applied by k_pool_apply
+              TICK_SPLIT = 64;   // the pod jobs are built by k_pod_jobs after the tick's launch(es)
 // tag: this tick's nonzero id (single-rank dirty records); arrive_target: the
 // arrival count at which every chain block of this FRONT launch has arrived
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// split ticks: the pod jobs (deletes, patch job records, state transitions) of
+// every dirty 64-group run of every chain block, one wave each
+void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
 // the patch bytes of the tick's jobs (after its k_tick launch(es), on the same stream)
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st);

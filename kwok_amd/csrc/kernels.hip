@@ -100,6 +100,17 @@ __device__ __forceinline__ void block_excl_scan(uint32_t (&v)[NF], uint32_t (&to
     __syncthreads();
 }
 
+// the same over one wave (no barrier): v <- exclusive prefix, tot <- wave totals
+template <int NF>
+__device__ __forceinline__ void wave_excl_scan(uint32_t (&v)[NF], uint32_t (&tot)[NF]) {
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        const uint32_t incl = wave_incl_scan(v[f]);
+        tot[f] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        v[f] = incl - v[f];
+    }
+}
+
 template <int NF>
 __device__ __forceinline__ void block_sum(uint32_t (&v)[NF]) {
     uint32_t tot[NF];
@@ -830,9 +841,11 @@ __device__ __forceinline__ uint32_t used_bits(const DevState& S, const PodGrp& g
 }
 
 // counts of one group into f, and its rare pre-count work (wave-uniform entry):
-// the byte counts of patches (spec lengths) and the releases of deleted pods
-__device__ __forceinline__ void count_group(const DevState& S, const PodGrp& g, const GroupMasks& m,
-                                            uint32_t (&f)[AG_STRIDE]) {
+// the byte counts of patches (spec lengths) and the releases of deleted pods.
+// Returns the group's patch bytes.
+__device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp& g, const GroupMasks& m,
+                                                uint32_t (&f)[AG_STRIDE]) {
+    uint32_t bytes = 0;
     f[AG_DEL] += __popc(m.del);
     f[AG_EVAL] += __popc(m.eval);
     f[AG_ALLOC] += __popc(m.alloc);
@@ -857,10 +870,54 @@ __device__ __forceinline__ void count_group(const DevState& S, const PodGrp& g, 
             } else {
                 wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
             }
-            if ((m.need >> k) & 1) f[AG_PP_BYTES] += S.specs[sp[k]].max_len;
+            if ((m.need >> k) & 1) bytes += S.specs[sp[k]].max_len;
         }
+        f[AG_PP_BYTES] += bytes;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before this block arrives
     }
+    return bytes;
+}
+
+// split ticks: a dirty group's counts into its 64-group run (LDS, [MAX_WC][4]
+// then the dirty bits); gi = the group's index among the block's live groups
+__device__ __forceinline__ void wc_add(uint32_t* wcnt, uint32_t gi, const GroupMasks& m, uint32_t bytes) {
+    if (!m.dirty) return;
+    const uint32_t w = gi / WC_GROUPS;
+    if (m.del) atomicAdd(&wcnt[4 * w], (uint32_t)__popc(m.del));
+    if (m.need) {
+        atomicAdd(&wcnt[4 * w + 1], (uint32_t)__popc(m.need));
+        atomicAdd(&wcnt[4 * w + 2], bytes);
+    }
+    if (m.alloc) atomicAdd(&wcnt[4 * w + 3], (uint32_t)__popc(m.alloc));
+    atomicOr(&wcnt[4 * MAX_WC + (w >> 5)], 1u << (w & 31));
+}
+// ... and, once the block's counts are complete, the runs' exclusive prefixes and
+// dirty bits to global memory for k_pod_jobs (wave 0; ng = the block's live groups)
+__device__ __forceinline__ void wc_publish(const DevState& S, uint32_t b, uint32_t ng, const uint32_t* wcnt) {
+    if (threadIdx.x >= 64) return;
+    const int l = lane_id();
+    constexpr int PER = MAX_WC / 64;
+    const uint32_t nwc = (ng + WC_GROUPS - 1) / WC_GROUPS;
+    uint32_t v[PER][4], s[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < PER; e++)
+#pragma unroll
+        for (int f = 0; f < 4; f++) {
+            v[e][f] = wcnt[4 * (PER * l + e) + f];
+            s[f] += v[e][f];
+        }
+    uint32_t run[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) run[f] = wave_incl_scan(s[f]) - s[f];
+    uint4* dst = S.wc_pre + (size_t)b * MAX_WC;
+#pragma unroll
+    for (int e = 0; e < PER; e++) {
+        const uint32_t w = PER * l + e;
+        if (w < nwc) dst[w] = make_uint4(run[0], run[1], run[2], run[3]);
+#pragma unroll
+        for (int f = 0; f < 4; f++) run[f] += v[e][f];
+    }
+    if (l < WC_DIRTY_WORDS) S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + l] = wcnt[4 * MAX_WC + l];
 }
 
 // configurePod (pod_controller.go:378-382): Use() of the group's evaluated in-CIDR
@@ -1010,14 +1067,16 @@ constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs 
 // chunks.  A chunk costs ~9 us of mostly fixed latency (group loads ~2, scan ~1,
 // emission with its reused-address loads ~3.6, the closing barrier ~2.3: trace
 // of the 1M x 10M churn tick, which visits all 19 chunks of every block).
-template <int NC>
+// WAVE: the same for one wave's 64-group run on its own (k_pod_jobs): wave
+// scans, no block barrier; gidx = the thread's group index in each chunk.
+template <int NC, bool WAVE = false>
 __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
-                                                uint32_t nbk, uint32_t ng, const uint32_t (&cs)[NC], Bases& run,
+                                                uint32_t nbk, uint32_t ng, const uint32_t (&gidx)[NC], Bases& run,
                                                 const Layout& L, uint32_t* stage) {
     PodGrp g[NC];
     uint16_t sp[NC][POD_PER_THREAD];
 #pragma unroll
-    for (int i = 0; i < NC; i++) load_group(S, gpre, bk0, nbk, ng, cs[i] * BLOCK + threadIdx.x, g[i]);
+    for (int i = 0; i < NC; i++) load_group(S, gpre, bk0, nbk, ng, gidx[i], g[i]);
 #pragma unroll
     for (int i = 0; i < NC; i++) load_spec_ids(S, g[i], sp[i]);
     PodCls cl[NC][POD_PER_THREAD];
@@ -1078,7 +1137,8 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
 #pragma unroll
     for (int i = 0; i < NC; i++) my_alloc[i] = v[4 * i + 3];
     uint32_t tot[4 * NC];
-    block_excl_scan<4 * NC>(v, tot);
+    if constexpr (WAVE) wave_excl_scan<4 * NC>(v, tot);
+    else block_excl_scan<4 * NC>(v, tot);
     // chunk i's bases: the running prefix plus the totals of the chunks before it
     Bases rb[NC];
 #pragma unroll
@@ -1181,7 +1241,7 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             *reinterpret_cast<uint4*>(S.pod_state + gi.slot) = o;
         }
     }
-    __syncthreads();
+    if constexpr (!WAVE) __syncthreads();
 #pragma unroll
     for (int i = 0; i < NC; i++) {
         run.v[AG_DEL] += tot[4 * i];
@@ -1446,7 +1506,7 @@ struct TickLds {
 __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLds l, uint32_t b, uint32_t bk0, uint32_t nbk,
                                        uint64_t pod_mask, uint32_t node_mask, uint32_t my_init, bool have_sums,
                                        int phases, uint32_t n_hb, uint64_t now_unix, uint64_t start_unix, uint64_t xA,
-                                       uint64_t xrel, uint64_t xbase) {
+                                       uint64_t xrel, uint64_t xbase, uint32_t tag) {
     const DevState& S = *G;
     const int t = threadIdx.x;
     TickHdr* H = S.hdr;
@@ -1547,17 +1607,38 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
         emit_node_chunk(S, nbase, k * NODE_CHUNK, nn, run, L);
     }
     TSTAMP(14);
+    if (phases & TICK_SPLIT) {
+        // split tick: k_pod_jobs emits the pod chunks, one wave per dirty 64-group
+        // run of this block (FRONT published the runs' prefixes); it starts here
+        if (pod_mask && t == 0) {
+            JobBase jb;
+            jb.del = run.v[AG_DEL];
+            jb.pp = run.v[AG_PP];
+            jb.pp_bytes = run.v[AG_PP_BYTES];
+            jb.alloc = run.v[AG_ALLOC];
+            jb.pod_base = L.pod_base;
+            jb.alloc_base = L.alloc_base;
+            jb.take = L.plan.take;
+            jb.fin = L.plan.fin;
+            jb.fout0 = L.plan.fout0;
+            jb.tag = tag;
+            jb.pad = 0;
+            S.jbase[b] = jb;
+        }
+        TSTAMP(6);
+        return;
+    }
     const uint32_t ng = l.gpre[nbk];
     for (uint64_t m = pod_mask; m;) {  // dirty chunks two at a time, in canonical order
         const uint32_t c0 = (uint32_t)__builtin_ctzll(m);
         m &= m - 1;
         if (m) {
-            const uint32_t cs[2] = {c0, (uint32_t)__builtin_ctzll(m)};
+            const uint32_t gx[2] = {c0 * BLOCK + t, (uint32_t)__builtin_ctzll(m) * BLOCK + t};
             m &= m - 1;
-            emit_pod_chunks<2>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, cs, run, L, l.recs);
+            emit_pod_chunks<2>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, gx, run, L, l.recs);
         } else {
-            const uint32_t cs[1] = {c0};
-            emit_pod_chunks<1>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, cs, run, L, l.recs);
+            const uint32_t gx[1] = {c0 * BLOCK + t};
+            emit_pod_chunks<1>(S, l.gpre, reinterpret_cast<const uint8_t*>(l.nflags32), bk0, nbk, ng, gx, run, L, l.recs);
         }
     }
     TSTAMP(6);
@@ -1649,6 +1730,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (t < 3) sh_mask[t] = 0;
         const bool single = !S.multi;
+        const bool split = (phases & TICK_SPLIT) != 0;
+        uint32_t* wcnt = recs;  // split: the 64-group runs' counts (recs is free until reduce_records)
+        if (split)
+            for (uint32_t i = t; i < 4 * MAX_WC + WC_DIRTY_WORDS; i += BLOCK) wcnt[i] = 0;
         const uint32_t hb_base = S.hb_pre[b];
         // round trip 1, all loads independent: the fill marks, the node states and,
         // speculatively, SPEC_GROUPS pod groups per thread at a static thread ->
@@ -1698,7 +1783,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             }
             if (i < nn) {
                 nflags32[i / 4] = tick;
-                if (!single) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
+                if (!single || split) *reinterpret_cast<uint32_t*>(S.node_tick + nbase + i) = tick;
             }
             if (dirty) nmask |= 1u << (i0 / NODE_CHUNK);
         }
@@ -1723,9 +1808,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint32_t a = l + q * tpb;
             clip_group(G[q], jv && a * POD_PER_THREAD < fill);
             const GroupMasks m = masks_of(S, nflags, G[q]);
-            count_group(S, G[q], m, f);
+            const uint32_t gbytes = count_group(S, G[q], m, f);
             // emission chunks are runs of 256 live groups in slot order (gpre)
             if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+            if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
             usec[q] = m.usec;
             if (!single) {  // multi rank: Use lists before the record (the exchange message carries them)
                 const UsedWords u = used_words(S, G[q], m.usec);
@@ -1739,8 +1825,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint32_t a = l + a0;
             load_group_at(S, jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, H);
             const GroupMasks m = masks_of(S, nflags, H);
-            count_group(S, H, m, f);
+            const uint32_t gbytes = count_group(S, H, m, f);
             if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+            if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
             const UsedWords u = used_words(S, H, m.usec);
             apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
         }
@@ -1818,6 +1905,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 TSTAMP(6);
                 return;
             }
+            if (split && pod_mask) wc_publish(S, b, gpre[nbk], wcnt);  // (wait_arrivals synchronises)
             wait_arrivals(S, arrive_target);
             reduce_records(S, b, tag, recs, &sums);
             have_sums = true;
@@ -1828,6 +1916,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 S.dmask[2 * b + 1] = node_mask;
             }
             f[AG_DIRTY] = dirty ? 1u : 0u;
+            if (split && pod_mask) wc_publish(S, b, gpre[nbk], wcnt);  // for the BACK launch's k_pod_jobs
             const uint64_t old = publish_and_arrive(S, b, f);
             TSTAMP(3);
             if ((old + 1) % S.n_chain == 0) {
@@ -1914,9 +2003,56 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
     }
     tick_back(S.self, TickLds{recs, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
-              pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase);
+              pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase, tag);
 #undef TSTAMP
 #undef TWAIT
+}
+
+// ---------------------------------------------------------------------------
+// k_pod_jobs: the pod emission of a split tick (TICK_SPLIT), launched after its
+// k_tick launch(es).  In a chain block the pod chunks are a serial walk (one
+// wave per SIMD, ~9 us of mostly fixed latency per 2048-pod chunk); here every
+// dirty 64-group run of every chain block is one independent wave: its first
+// ordinals / byte offset are the block's JobBase plus the run's in-block prefix
+// (both from k_tick), its node flags the FRONT's node_tick bytes, and the run's
+// deletes, job records and state transitions are exactly what the chain block
+// would have written (emit_pod_chunks<1, true>, canonical order).
+// pod_controller.go:155-183 (DeletePods), 404-439 (configurePod / patch jobs).
+// ---------------------------------------------------------------------------
+constexpr int JOB_WAVES = 4;
+__global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
+    __shared__ uint32_t stage[JOB_WAVES * POD_STAGE_WORDS];
+    __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    const uint32_t b = blockIdx.x / wg_per_block;
+    const uint32_t w = (uint32_t)wave_id();
+    const uint32_t c = (blockIdx.x - b * wg_per_block) * JOB_WAVES + w;  // the wave's run
+    if (b >= S.n_chain || c >= (uint32_t)MAX_WC) return;
+    const JobBase* JB = S.jbase + b;
+    if (JB->tag != tag) return;  // the block has no pod jobs this tick
+    if (!((S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c >> 5)] >> (c & 31)) & 1u)) return;
+    uint32_t bk0, nbk;
+    block_range(S, b, bk0, nbk);
+    const int l = lane_id();
+    uint32_t* gpre = gpre_w[w];
+    const uint32_t inc = wave_incl_scan(l < (int)nbk ? (uint32_t)S.pod_fill[bk0 + l] >> 3 : 0u);
+    gpre[l + 1] = inc;
+    if (l == 0) gpre[0] = 0;
+    const uint32_t ng = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
+    const uint4 wp = S.wc_pre[(size_t)b * MAX_WC + c];
+    Bases run;
+    run.v[AG_INIT] = run.v[AG_INIT_BYTES] = 0;
+    run.v[AG_DEL] = JB->del + wp.x;
+    run.v[AG_PP] = JB->pp + wp.y;
+    run.v[AG_PP_BYTES] = JB->pp_bytes + wp.z;
+    run.v[AG_ALLOC] = JB->alloc + wp.w;
+    Layout L;
+    L.init_base = 0;
+    L.pod_base = JB->pod_base;
+    L.alloc_base = JB->alloc_base;
+    L.plan = PoolPlan{0, 0, JB->take, JB->fin, 0, JB->fout0};
+    const uint32_t gx[1] = {c * WC_GROUPS + (uint32_t)l};
+    emit_pod_chunks<1, true>(S, gpre, S.node_tick + (size_t)bk0 * S.cn, bk0, nbk, ng, gx, run, L, stage);
 }
 
 // ingest-time Put (a Deleted watch event), applied immediately
@@ -2007,6 +2143,17 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
+
+void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
+    // the largest chain block's runs: its buckets x their capacity in 8-slot groups
+    const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
+    const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
+    const uint32_t wpb = cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, JOB_WAVES);
+    const uint32_t grid = S.n_chain * (wpb ? wpb : 1u);
+    if (t0)
+        hipExtLaunchKernelGGL(k_pod_jobs, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb ? wpb : 1u);
+    else hipLaunchKernelGGL(k_pod_jobs, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb ? wpb : 1u);
+}
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
