@@ -25,6 +25,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -289,6 +290,9 @@ struct kwok_engine {
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
+    uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
+    size_t dump_cap = 0;
+    bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
@@ -340,6 +344,27 @@ struct kwok_engine {
     } while (0)
 
 namespace {
+
+// kwok_host_alloc buffers (base -> length, device address, mmap'd + registered)
+struct HostReg {
+    size_t len;
+    uint8_t* dev;
+    bool mmapped;
+};
+std::mutex g_host_mu;
+std::map<uintptr_t, HostReg> g_host_reg;
+// the device address of [p, p + n) when it lies inside one kwok_host_alloc
+// buffer (kernels read it in place over the link), else null
+const void* host_mapped(const void* p, size_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> l(g_host_mu);
+    auto it = g_host_reg.upper_bound(a);
+    if (it == g_host_reg.begin()) return nullptr;
+    --it;
+    const HostReg& r = it->second;
+    if (!r.dev || a + n > it->first + r.len) return nullptr;
+    return r.dev + (a - it->first);
+}
 
 template <class T>
 int dalloc(kwok_engine* e, T** p, size_t n) {
@@ -1102,8 +1127,8 @@ const char* kwok_last_error(const kwok_engine* e) { return e ? e->err.c_str() : 
 void kwok_engine_destroy(kwok_engine* e) {
     if (!e) return;
     if (e->trace_ticks) {
-        static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "pod-jobs", "pool-done",
-                                                 "exit", "header-done", "node-flags", "w:pod-loads", "block-sum",
+        static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "reduced", "pool-done",
+                                                 "exit", "header-done", "node-flags", "pool-folded", "block-sum",
                                                  "drained", "hb-handles", "share-done", "nodes-emitted", "back-start"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
                         "start (min / median / max block)\n",
@@ -1140,6 +1165,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
+    if (e->dump_h) (void)hipHostFree(e->dump_h);
     if (e->comm) ncclCommDestroy(e->comm);
     if (e->d_pod_fill) (void)hipFree(e->d_pod_fill);
     if (e->fence) (void)hipEventDestroy(e->fence);
@@ -1263,6 +1289,11 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         // both when several engines share one GPU (their grids must fit together).
         int cus = 0, occ = tick_occupancy(), want = 1, wants = 1;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->dev);
+        // heartbeat-once ticks stream one body: the CU's second k_tick slot goes to a
+        // second chain block (twice the classification loads in flight), and a few
+        // streamer blocks write the body after the chain blocks
+        const bool once = (cfg->flags & KWOK_CFG_HEARTBEAT_ONCE) != 0;
+        if (once) want = 2;
         if (const char* v = getenv("KWOK_TICK_BLOCKS_PER_CU")) want = std::max(1, atoi(v));
         if (const char* v = getenv("KWOK_TICK_STREAMERS_PER_CU")) wants = std::max(1, atoi(v));
         if (cus <= 0 || occ <= 0) return bail(e->fail(KWOK_EDEVICE, "k_tick occupancy query failed"));
@@ -1270,7 +1301,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         // KWOK_TICK_CHAIN_BLOCKS: fewer chain blocks, so that the grids of many engines
         // sharing one GPU (the 8-rank C3 test) are co-resident together
         if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
-        e->n_stream = (uint32_t)(cus * wants);
+        e->n_stream = once ? 8u : (uint32_t)(cus * wants);
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
         const char* pr = getenv("KWOK_TICK_PRIO");
@@ -1284,6 +1315,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->no_stream = ns && ns[0] == '1';
         const char* sj = getenv("KWOK_SPLIT");
         e->split_jobs = !(sj && sj[0] == '0');
+        const char* zc = getenv("KWOK_INGEST_ZC");
+        e->ingest_zc = !(zc && zc[0] == '0');
     }
     S.n_node_slots = e->NL;
     S.n_pod_slots = e->PL;
@@ -1723,12 +1756,23 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     if (rc) return rc;
     auto& G = e->ing;
     hipStream_t st = e->st;
-    IngestBatch I = ingest_batch(e, (uint32_t)n, arena_len);
-    // the records and their strings -> HBM; prep; the growth need
+    // a batch in kwok_host_alloc memory is read in place by k_ing_prep (the only
+    // kernel that reads the records and their strings): one pass over the link,
+    // no copy engine (KWOK_INGEST_ZC=0: copy it to HBM first)
+    const void* zev = e->ingest_zc ? host_mapped(ev, n * sizeof(kwok_pod_event)) : nullptr;
+    const void* zar = e->ingest_zc && arena_len ? host_mapped(arena, arena_len) : nullptr;
+    auto batch = [&]() {
+        IngestBatch b = ingest_batch(e, (uint32_t)n, arena_len);
+        if (zev) b.ev = zev;
+        if (zar) b.arena = (const uint8_t*)zar;
+        return b;
+    };
+    IngestBatch I = batch();
+    // the records and their strings -> HBM (unless read in place); prep; the growth need
     HIPCHK(e, hipMemsetAsync(G.sum, 0, sizeof(IngSummary), st));
     HIPCHK(e, hipMemsetAsync(G.dels, 0, (size_t)e->nb * 4, st));
-    HIPCHK(e, hipMemcpyAsync(G.d_ev, ev, n * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
-    if (arena_len) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    if (!zev) HIPCHK(e, hipMemcpyAsync(G.d_ev, ev, n * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
+    if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
     double t_h2d = 0;
     if (e->iprof) {  // diagnostics: the copies on their own
         HIPCHK(e, hipStreamSynchronize(st));
@@ -1749,7 +1793,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(((uint64_t)sum.need + 7) & ~7ull, 2ull * e->Cp));
             if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
             if ((rc = grow_pods(e, want))) return rc;
-            I = ingest_batch(e, (uint32_t)n, arena_len);
+            I = batch();
         }
         efull_possible = sum.need > e->Cp;  // at the stride (or the chain blocks' limit): EFULL per record
     }
@@ -1827,8 +1871,9 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     if (out_released) HIPCHK(e, hipMemcpyAsync(out_released, G.out_released, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu pod records (GPU): copy + prep %.2f ms (H2D %.2f ms, %.1f GB/s), "
-                        "resolve + sort %.2f ms, apply %.2f ms (%d rounds), results %.2f ms\n", n, ms_between(t0, t1),
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s): copy + prep %.2f ms (H2D %.2f ms, %.1f GB/s), "
+                        "resolve + sort %.2f ms, apply %.2f ms (%d rounds), results %.2f ms\n", n,
+                zev ? ", read in place" : "", ms_between(t0, t1),
                 t_h2d, (n * sizeof(kwok_pod_event) + arena_len) / (t_h2d * 1e6), ms_between(t1, t2), ms_between(t2, t3),
                 rounds, ms_between(t3, clk::now()));
     return (int)G.sum_h->rejected;
@@ -2417,13 +2462,11 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* o) {
 }
 
 // Page-locked batch buffers: 2 MiB-aligned anonymous memory on transparent huge
-// pages where the kernel grants them, registered with the runtime (the GPU's
-// copies walk 512x fewer page translations than over 4 KiB pages);
-// KWOK_HOST_ALLOC=hip: hipHostMalloc instead.
-namespace {
-std::mutex g_host_mu;
-std::unordered_map<void*, size_t> g_host_reg;  // registered (mmap) buffers -> mapped length
-}  // namespace
+// pages where the kernel grants them, registered (and mapped) with the runtime
+// (the GPU walks 512x fewer page translations than over 4 KiB pages);
+// KWOK_HOST_ALLOC=hip: hipHostMalloc instead.  Both are in the registry, with
+// their device addresses: kwok_ingest_pods reads a batch in such a buffer in
+// place (host_mapped).
 void* kwok_host_alloc(size_t bytes) {
     bytes = bytes ? bytes : 1;
     const char* how = getenv("KWOK_HOST_ALLOC");
@@ -2433,9 +2476,11 @@ void* kwok_host_alloc(size_t bytes) {
         if (p != MAP_FAILED) {
             (void)madvise(p, len, MADV_HUGEPAGE);
             memset(p, 0, len);  // first touch: the pages exist (huge where granted) before pinning
-            if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+            if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
+                void* dev = nullptr;
+                if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) dev = nullptr;
                 std::lock_guard<std::mutex> l(g_host_mu);
-                g_host_reg[p] = len;
+                g_host_reg[(uintptr_t)p] = HostReg{len, (uint8_t*)dev, true};
                 return p;
             }
             munmap(p, len);
@@ -2443,20 +2488,25 @@ void* kwok_host_alloc(size_t bytes) {
     }
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) dev = nullptr;
+    std::lock_guard<std::mutex> l(g_host_mu);
+    g_host_reg[(uintptr_t)p] = HostReg{bytes, (uint8_t*)dev, false};
     return p;
 }
 
 void kwok_host_free(void* p) {
     if (!p) return;
-    size_t len = 0;
+    HostReg r{0, nullptr, false};
+    bool found = false;
     {
         std::lock_guard<std::mutex> l(g_host_mu);
-        auto it = g_host_reg.find(p);
-        if (it != g_host_reg.end()) len = it->second, g_host_reg.erase(it);
+        auto it = g_host_reg.find((uintptr_t)p);
+        if (it != g_host_reg.end()) r = it->second, found = true, g_host_reg.erase(it);
     }
-    if (len) {
+    if (found && r.mmapped) {
         (void)hipHostUnregister(p);
-        munmap(p, len);
+        munmap(p, r.len);
     } else {
         (void)hipHostFree(p);
     }
@@ -2536,12 +2586,25 @@ int kwok_dump_pods(kwok_engine* e, int32_t first, uint32_t count, uint8_t* used,
     if (!e) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
     drain(e);
-    std::vector<uint16_t> sth(e->PL);
-    std::vector<uint32_t> hh(e->PL), ph(e->PL);
+    // through the engine's page-locked dump buffer: a device-to-host copy into
+    // pageable memory made later copies of the ingest path stall (measured: every
+    // other 2M-record churn batch paid 6-20 ms before its first device operation)
+    const size_t PL = e->PL, need = PL * 10;
+    if (need > e->dump_cap) {
+        if (e->dump_h) (void)hipHostFree(e->dump_h);
+        e->dump_h = nullptr;
+        e->dump_cap = 0;
+        if (hipHostMalloc((void**)&e->dump_h, need, hipHostMallocDefault) != hipSuccess)
+            return e->fail(KWOK_ENOMEM, "dump buffer %zu", need);
+        e->dump_cap = need;
+    }
+    uint32_t* hh = reinterpret_cast<uint32_t*>(e->dump_h);
+    uint32_t* ph = hh + PL;
+    const uint16_t* sth = reinterpret_cast<const uint16_t*>(ph + PL);
     if (int rc = release_for_host(e)) return rc;
-    HIPCHK(e, hipMemcpyAsync(sth.data(), e->S.pod_state, (size_t)e->PL * 2, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(hh.data(), e->S.host_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipMemcpyAsync(ph.data(), e->S.pod_ip, (size_t)e->PL * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync((void*)sth, e->S.pod_state, PL * 2, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(hh, e->S.host_ip, PL * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(ph, e->S.pod_ip, PL * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     for (uint32_t i = 0; i < count; i++) {
         uint32_t l = 0;

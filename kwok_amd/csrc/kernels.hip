@@ -873,7 +873,10 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
             if ((m.need >> k) & 1) bytes += S.specs[sp[k]].max_len;
         }
         f[AG_PP_BYTES] += bytes;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before this block arrives
+        // multi rank: the release list entries are performed before this block
+        // arrives (publish_and_arrive drains only wave 0); a single-rank block
+        // drains every wave before its arrival, so its loads stay in flight here
+        if (S.multi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     return bytes;
 }
@@ -935,7 +938,7 @@ __device__ __forceinline__ void apply_uses(const DevState& S, const PodGrp& g, u
                 wave_append(u, ip, S.use_list, &S.list_counts[0]);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before this block arrives
+        if (S.multi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as in count_group)
     }
 }
 
@@ -1534,6 +1537,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
         const uint32_t nwb = (uint32_t)((S.pool.words + POOL_WPB - 1) / POOL_WPB);
         for (uint32_t wb = pidx; wb < nwb; wb += np) pool_prep_wblock(S, wb, rel_total != 0, A != 0);
         pool_barrier(S, np);
+        TSTAMP(9);
         if (A) {
             uint64_t cursor = ~0ull;
             for (uint32_t wb = pidx; wb < nwb; wb += np) {
@@ -1799,7 +1803,6 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         }
         __syncthreads();
         TSTAMP(1);
-        TWAIT(9);
         // ---- pods: the speculative groups, then any further rows (rare) ------------
         uint64_t pmask = 0;
         uint32_t usec[SPEC_GROUPS];  // single rank: Use candidates, checked after the accumulator adds
@@ -1820,16 +1823,26 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             __builtin_amdgcn_sched_barrier(0);
         }
         const uint32_t maxg = sh_mask[3];
-        for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += tpb) {
+        if (SPEC_GROUPS * tpb < maxg) {
+            // one row per iteration, the next row's group loads in flight under this
+            // row's Use check (one round trip per row, not two)
+            auto row_slot = [&](uint32_t a) {
+                return jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u;
+            };
             PodGrp H;
-            const uint32_t a = l + a0;
-            load_group_at(S, jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, H);
-            const GroupMasks m = masks_of(S, nflags, H);
-            const uint32_t gbytes = count_group(S, H, m, f);
-            if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
-            if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
-            const UsedWords u = used_words(S, H, m.usec);
-            apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
+            load_group_at(S, row_slot(l + SPEC_GROUPS * tpb), j, H);
+            for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += tpb) {
+                const uint32_t a = l + a0;
+                PodGrp N;
+                load_group_at(S, a0 + tpb < maxg ? row_slot(a + tpb) : ~0u, j, N);
+                const GroupMasks m = masks_of(S, nflags, H);
+                const uint32_t gbytes = count_group(S, H, m, f);
+                if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+                if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                const UsedWords u = used_words(S, H, m.usec);
+                apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
+                H = N;
+            }
         }
         TSTAMP(2);
         if (nmask) atomicOr(&sh_mask[2], nmask);
@@ -1908,6 +1921,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             if (split && pod_mask) wc_publish(S, b, gpre[nbk], wcnt);  // (wait_arrivals synchronises)
             wait_arrivals(S, arrive_target);
             reduce_records(S, b, tag, recs, &sums);
+            TSTAMP(4);
             have_sums = true;
         } else {
             // ---- multi rank: records; the last arriver writes the exchange message -----
@@ -2020,39 +2034,51 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
 // pod_controller.go:155-183 (DeletePods), 404-439 (configurePod / patch jobs).
 // ---------------------------------------------------------------------------
 constexpr int JOB_WAVES = 4;
+constexpr int JOB_NC = 2;  // consecutive runs per wave, their loads and scans interleaved
 __global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
     __shared__ uint32_t stage[JOB_WAVES * POD_STAGE_WORDS];
     __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
     const uint32_t b = blockIdx.x / wg_per_block;
     const uint32_t w = (uint32_t)wave_id();
-    const uint32_t c = (blockIdx.x - b * wg_per_block) * JOB_WAVES + w;  // the wave's run
-    if (b >= S.n_chain || c >= (uint32_t)MAX_WC) return;
+    const uint32_t c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * JOB_NC;  // the wave's first run
+    if (b >= S.n_chain || c0 >= (uint32_t)MAX_WC) return;
+    // every input of the wave's setup in one round trip: the block's JobBase, the
+    // runs' dirty bits and prefix, the fill marks of the block's buckets
     const JobBase* JB = S.jbase + b;
-    if (JB->tag != tag) return;  // the block has no pod jobs this tick
-    if (!((S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c >> 5)] >> (c & 31)) & 1u)) return;
+    const uint32_t jtag = JB->tag;
+    const uint32_t dirty = (S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c0 >> 5)] >> (c0 & 31)) & 3u;
+    const uint4 wp = S.wc_pre[(size_t)b * MAX_WC + c0];
     uint32_t bk0, nbk;
     block_range(S, b, bk0, nbk);
     const int l = lane_id();
-    uint32_t* gpre = gpre_w[w];
-    const uint32_t inc = wave_incl_scan(l < (int)nbk ? (uint32_t)S.pod_fill[bk0 + l] >> 3 : 0u);
-    gpre[l + 1] = inc;
-    if (l == 0) gpre[0] = 0;
-    const uint32_t ng = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
-    const uint4 wp = S.wc_pre[(size_t)b * MAX_WC + c];
+    const uint32_t fill = l < (int)nbk ? (uint32_t)S.pod_fill[bk0 + l] : 0u;
     Bases run;
     run.v[AG_INIT] = run.v[AG_INIT_BYTES] = 0;
-    run.v[AG_DEL] = JB->del + wp.x;
-    run.v[AG_PP] = JB->pp + wp.y;
-    run.v[AG_PP_BYTES] = JB->pp_bytes + wp.z;
-    run.v[AG_ALLOC] = JB->alloc + wp.w;
+    run.v[AG_DEL] = JB->del;
+    run.v[AG_PP] = JB->pp;
+    run.v[AG_PP_BYTES] = JB->pp_bytes;
+    run.v[AG_ALLOC] = JB->alloc;
     Layout L;
     L.init_base = 0;
     L.pod_base = JB->pod_base;
     L.alloc_base = JB->alloc_base;
     L.plan = PoolPlan{0, 0, JB->take, JB->fin, 0, JB->fout0};
-    const uint32_t gx[1] = {c * WC_GROUPS + (uint32_t)l};
-    emit_pod_chunks<1, true>(S, gpre, S.node_tick + (size_t)bk0 * S.cn, bk0, nbk, ng, gx, run, L, stage);
+    if (jtag != tag || !dirty) return;  // the block has no pod jobs this tick / the runs are clean
+    run.v[AG_DEL] += wp.x;
+    run.v[AG_PP] += wp.y;
+    run.v[AG_PP_BYTES] += wp.z;
+    run.v[AG_ALLOC] += wp.w;
+    uint32_t* gpre = gpre_w[w];
+    const uint32_t inc = wave_incl_scan(fill >> 3);
+    gpre[l + 1] = inc;
+    if (l == 0) gpre[0] = 0;
+    const uint32_t ng = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
+    // both runs (a clean one has nothing to count or emit, so the second run's
+    // bases follow from the first's totals either way)
+    const uint32_t gx[JOB_NC] = {c0 * WC_GROUPS + (uint32_t)l, (c0 + 1) * WC_GROUPS + (uint32_t)l};
+    emit_pod_chunks<JOB_NC, true>(S, gpre, S.node_tick + (size_t)bk0 * S.cn, bk0, nbk, ng, gx, run, L, stage);
 }
 
 // ingest-time Put (a Deleted watch event), applied immediately
@@ -2148,7 +2174,7 @@ void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t
     // the largest chain block's runs: its buckets x their capacity in 8-slot groups
     const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
     const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
-    const uint32_t wpb = cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, JOB_WAVES);
+    const uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, JOB_NC), JOB_WAVES);
     const uint32_t grid = S.n_chain * (wpb ? wpb : 1u);
     if (t0)
         hipExtLaunchKernelGGL(k_pod_jobs, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb ? wpb : 1u);
