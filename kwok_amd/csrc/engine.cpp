@@ -2002,14 +2002,16 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // the streamers' share: with the non-temporal stream the chain blocks finish
     // sooner (1M x 10M: classification 172 -> 122 us) and take more of the tail
     // (tools/share_sweep2.sh: 921 -> 860 /1024, 217 -> 208 us per tick)
-    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
-                                       : (hb_bytes < (32ull << 20) ? 1024u : (S.hb_nt ? 860u : 921u));
-    int rc = bind_slot(e, k);
-    if (rc) return rc;
     // ticks that likely emit pod jobs (events since the last tick) build them in
-    // k_pod_jobs, one wave per dirty 64-group run, instead of the chain blocks'
+    // k_pod_jobs, one wave per two dirty 64-group runs, instead of the chain blocks'
     // serial chunk walk (KWOK_SPLIT=0: the chain blocks, for A/B)
     T.split = T.emit_queued && e->split_jobs;
+    // ... and leave the whole stream to the streamers: a dirty chain block's share
+    // of it would hold up the pool phase, which waits for every dirty block
+    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
+                                       : (hb_bytes < (32ull << 20) || T.split ? 1024u : (S.hb_nt ? 860u : 921u));
+    int rc = bind_slot(e, k);
+    if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
                      (T.split ? TICK_SPLIT : 0);
     if (!requeue) {

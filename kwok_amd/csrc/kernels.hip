@@ -298,13 +298,21 @@ __device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
 constexpr int POOL_WPT = 4;                  // bitmap words per thread
 constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per word-block
 
+// a thread's words of one word-block (pass k: word wb * POOL_WPB + k * BLOCK +
+// thread), as the prep pass left them: the select pass of the same block takes
+// them from registers instead of reading them again
+struct PoolWords {
+    uint64_t used[POOL_WPT], usable[POOL_WPT];
+};
 // fold this tick's Puts, count usable / free bits of word-block wb
-__device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count) {
+__device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count, PoolWords& pw) {
     const uint64_t cb = cursor_bit(S);
     uint32_t f[2] = {0, 0};
+#pragma unroll
     for (int k = 0; k < POOL_WPT; k++) {
-        uint64_t w = (uint64_t)wb * POOL_WPB + threadIdx.x * POOL_WPT + k;
-        if (w >= S.pool.words) break;
+        const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
+        pw.used[k] = ~0ull, pw.usable[k] = 0ull;
+        if (w >= S.pool.words) continue;
         uint64_t used = S.used_bm[w], usable = S.usable_bm[w];
         if (fold) {
             uint64_t r = S.rel_bm[w];
@@ -318,6 +326,7 @@ __device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb,
         }
         f[0] += __popcll(usable);
         f[1] += __popcll(free_mask(S, w, used, usable, cb));
+        pw.used[k] = used, pw.usable[k] = usable;
     }
     block_sum<2>(f);
     if (threadIdx.x == 0 && count) {
@@ -430,16 +439,18 @@ __device__ __forceinline__ void wave_write_addrs(const DevState& S, uint64_t g0,
 // as two masks, and the wave writes their addresses coalesced (one alloc_addr
 // entry per lane per store, instead of a serial bit walk per lane with one
 // scattered store per address: the 1M x 10M initial tick's 10M fresh Gets).
+// pw: the block's words of wb from its prep pass (null: read them)
 __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
-                                   uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out) {
+                                   uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out, const PoolWords* pw) {
     const uint64_t take = p.take, fin = p.fin;
     const uint64_t cb = cursor_bit(S);
     const bool advance = fin > 0 && p.fout == 0;
+#pragma unroll
     for (int k = 0; k < POOL_WPT; k++) {
         const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
         const bool valid = w < S.pool.words;
-        const uint64_t used = valid ? S.used_bm[w] : ~0ull;
-        const uint64_t wu = valid ? S.usable_bm[w] : 0ull;
+        const uint64_t used = pw ? pw->used[k] : (valid ? S.used_bm[w] : ~0ull);
+        const uint64_t wu = pw ? pw->usable[k] : (valid ? S.usable_bm[w] : 0ull);
         const uint64_t wf = valid ? free_mask(S, w, used, wu, cb) : 0ull;
         const uint32_t cu = (uint32_t)__popcll(wu), cf = (uint32_t)__popcll(wf);
         uint32_t v[2] = {cu, cf}, tot[2];
@@ -726,6 +737,12 @@ __device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g
 #pragma unroll
     for (int k = 0; k < POD_PER_THREAD; k++) sp[k] = (uint16_t)(w[k >> 1] >> (16 * (k & 1)));
 }
+// the spec words of a group with a pod that needs a patch (its byte count)
+__device__ __forceinline__ uint4 load_spec_words(const DevState& S, const PodGrp& g, uint32_t need) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (need && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
+    return v;
+}
 __device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uint8_t* nflags, const PodGrp& g, int k) {
     return (g.st(k) & PS_USED) ? nflags[g.j * S.cn + g.nl(k)] : (uint8_t)0;
 }
@@ -843,8 +860,10 @@ __device__ __forceinline__ uint32_t used_bits(const DevState& S, const PodGrp& g
 // counts of one group into f, and its rare pre-count work (wave-uniform entry):
 // the byte counts of patches (spec lengths) and the releases of deleted pods.
 // Returns the group's patch bytes.
+// spw: the group's spec words (load_spec_words, issued with the row's other
+// loads); smax: the specs' reservations in LDS (null: read the descriptors)
 __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp& g, const GroupMasks& m,
-                                                uint32_t (&f)[AG_STRIDE]) {
+                                                uint32_t (&f)[AG_STRIDE], const uint4& spw, const uint16_t* smax) {
     uint32_t bytes = 0;
     f[AG_DEL] += __popc(m.del);
     f[AG_EVAL] += __popc(m.eval);
@@ -855,8 +874,7 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
     f[AG_PENDING] += __popc(m.pend);
     f[AG_RUNNING] += __popc(m.run);
     if (__builtin_expect(__ballot((m.rel | m.need) != 0) != 0, 0)) {
-        uint16_t sp[POD_PER_THREAD];
-        load_spec_ids(S, g, sp);
+        const uint32_t w[4] = {spw.x, spw.y, spw.z, spw.w};
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
             const uint32_t ip = g.ip[k];
@@ -870,7 +888,10 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
             } else {
                 wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
             }
-            if ((m.need >> k) & 1) bytes += S.specs[sp[k]].max_len;
+            if ((m.need >> k) & 1) {
+                const uint32_t sp = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                bytes += smax ? (uint32_t)smax[sp] : (uint32_t)S.specs[sp].max_len;
+            }
         }
         f[AG_PP_BYTES] += bytes;
         // multi rank: the release list entries are performed before this block
@@ -1535,7 +1556,12 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     if (A || rel_total) {
         if (single && pidx == 0 && t == 0) H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
         const uint32_t nwb = (uint32_t)((S.pool.words + POOL_WPB - 1) / POOL_WPB);
-        for (uint32_t wb = pidx; wb < nwb; wb += np) pool_prep_wblock(S, wb, rel_total != 0, A != 0);
+        PoolWords pw;  // the block's first word-block, kept for its select pass
+        for (uint32_t wb = pidx; wb < nwb; wb += np) {
+            PoolWords x;
+            pool_prep_wblock(S, wb, rel_total != 0, A != 0, x);
+            if (wb == pidx) pw = x;
+        }
         pool_barrier(S, np);
         TSTAMP(9);
         if (A) {
@@ -1543,7 +1569,8 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
             for (uint32_t wb = pidx; wb < nwb; wb += np) {
                 uint64_t bu, bf;
                 plan = pool_plan(S, A, nwb, wb, &bu, &bf);
-                pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor);
+                pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor,
+                                   wb == pidx ? &pw : nullptr);
             }
             if (pidx >= nwb) {
                 uint64_t bu, bf;
@@ -1679,6 +1706,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ uint4 hb_tmpl4[HB_MAX_UNITS];
     __shared__ uint32_t nflags32[NODE_LDS / 4];
     __shared__ uint32_t gpre[MAX_BPB + 1];
+    __shared__ uint16_t spec_max[SPEC_LDS];  // the specs' reservations (n_specs <= SPEC_LDS)
     __shared__ uint32_t sh_mask[4];  // pod chunk mask lo / hi, node chunk mask, most groups in a bucket
     __shared__ Sums sums;
     __shared__ Layout sh_L;
@@ -1759,6 +1787,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                                      : 0u;
         const uint64_t pool_index = single ? 0 : *S.pool_index;  // multi rank: the header's default cursor
         if (jv && l == 0) gpre[j + 1] = fill / POD_PER_THREAD;
+        const uint16_t* smax = S.n_specs <= (uint32_t)SPEC_LDS ? spec_max : nullptr;
+        for (uint32_t i = t; i < S.n_specs && i < (uint32_t)SPEC_LDS; i += BLOCK) spec_max[i] = S.specs[i].max_len;
         uint32_t f[AG_STRIDE];
 #pragma unroll
         for (int i = 0; i < AG_STRIDE; i++) f[i] = 0;
@@ -1806,12 +1836,18 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         // ---- pods: the speculative groups, then any further rows (rare) ------------
         uint64_t pmask = 0;
         uint32_t usec[SPEC_GROUPS];  // single rank: Use candidates, checked after the accumulator adds
+        uint4 spw[SPEC_GROUPS];  // the groups' spec words, one round trip for all of them
 #pragma unroll
         for (int q = 0; q < SPEC_GROUPS; q++) {
             const uint32_t a = l + q * tpb;
             clip_group(G[q], jv && a * POD_PER_THREAD < fill);
+            spw[q] = load_spec_words(S, G[q], masks_of(S, nflags, G[q]).need);
+        }
+#pragma unroll
+        for (int q = 0; q < SPEC_GROUPS; q++) {
+            const uint32_t a = l + q * tpb;
             const GroupMasks m = masks_of(S, nflags, G[q]);
-            const uint32_t gbytes = count_group(S, G[q], m, f);
+            const uint32_t gbytes = count_group(S, G[q], m, f, spw[q], smax);
             // emission chunks are runs of 256 live groups in slot order (gpre)
             if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
             if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
@@ -1833,13 +1869,15 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             load_group_at(S, row_slot(l + SPEC_GROUPS * tpb), j, H);
             for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += tpb) {
                 const uint32_t a = l + a0;
+                const GroupMasks m = masks_of(S, nflags, H);
+                // one round trip: the next row's group, this row's spec and `used` words
                 PodGrp N;
                 load_group_at(S, a0 + tpb < maxg ? row_slot(a + tpb) : ~0u, j, N);
-                const GroupMasks m = masks_of(S, nflags, H);
-                const uint32_t gbytes = count_group(S, H, m, f);
+                const uint4 sw = load_spec_words(S, H, m.need);
+                const UsedWords u = used_words(S, H, m.usec);
+                const uint32_t gbytes = count_group(S, H, m, f, sw, smax);
                 if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
                 if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
-                const UsedWords u = used_words(S, H, m.usec);
                 apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
                 H = N;
             }
