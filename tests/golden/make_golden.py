@@ -579,12 +579,39 @@ def scenario_e2e_kwok_test(tpl):
     return base_cfg(node_ip=node_ip, cidr="10.0.0.1/24"), [t0, t1, t2, dict(nodes=[], pods=[])]
 
 
+def scenario_same_interval_echo(tpl):
+    """The reference's in-interval IP for a pod created with an empty status
+    (pod_controller.go:279-319, 404-439): configurePod renders pod.status.tpl
+    with no `.status`, so the first patch carries no hostIP / podIP; the patch's
+    own Modified event re-enters lockPodChan within the same interval, and the
+    second configurePod renders `{{ with .status }}` with NodeIP and
+    ipPool.Get().  The engine does not re-ingest the echo of its own patch
+    (contract point); a caller that wants the reference's timing
+    ingests the echo and ticks again at the same clock (t1 here, `same_now`).
+      t0  e0, e1 (empty status) and r0 (Pending, non-empty) on node n0: e0/e1
+          patched without IPs, r0 gets 10.0.0.1;
+      t1  same clock: the echoes of e0 / e1 (Running, conforming status, no IPs):
+          patched with NodeIP and 10.0.0.2 / 10.0.0.3 - the bytes and IPs the
+          reference's second in-interval configurePod produces;
+      t2  a steady tick."""
+    spec = {"containers": [["c", "img"]], "init": [], "gates": []}
+    t0 = dict(nodes=[ne("n0")], pods=[pe("e0", "n0", phase="", status_nonempty=False, spec=spec),
+                                      pe("e1", "n0", phase="", status_nonempty=False, spec=spec),
+                                      pe("r0", "n0", spec=spec)])
+    echo = dict(phase="Running", status_nonempty=True, conforms=True, hostIP="", podIP="", spec=spec)
+    t1 = dict(nodes=[], pods=[dict(pe("e0", "n0", **echo), modify=True), dict(pe("e1", "n0", **echo), modify=True)],
+              same_now=True)
+    return base_cfg(node_ip="10.0.0.254", cidr="10.0.0.1/24"), [t0, t1, dict(nodes=[], pods=[])]
+
+
 def run_scenario(name, cfg, ticks, tpl):
     sim = Sim(cfg, tpl)
     handles = {}
     fx = {"name": name, "config": cfg, "ticks": []}
+    now = cfg["start_time"]
     for i, tk in enumerate(ticks):
-        now = cfg["start_time"] + 30 * (i + 1)
+        if not tk.get("same_now"):
+            now += 30
         rec = {"now": now, "node_events": [], "pod_events": []}
         for ev in tk["nodes"]:
             h = sim.ingest_node(ev)
@@ -715,7 +742,8 @@ def main():
                      ("cidr_overflow", scenario_cidr_overflow),
                      ("specs", scenario_specs),
                      ("churn", scenario_churn),
-                     ("e2e_kwok_test", lambda: scenario_e2e_kwok_test(tpl))]:
+                     ("e2e_kwok_test", lambda: scenario_e2e_kwok_test(tpl)),
+                     ("same_interval_echo", lambda: scenario_same_interval_echo(tpl))]:
         cfg, ticks = fn()
         fx = run_scenario(name, cfg, ticks, tpl)
         json.dump(fx, open(os.path.join(HERE, "trace_%s.json" % name), "w"), indent=None, separators=(",", ":"))

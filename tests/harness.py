@@ -16,7 +16,7 @@ from kwok_amd.engine import make_config
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 TRACES = ["reference_node_test", "reference_pod_test", "doc_known_answer", "cidr_overflow", "specs", "churn",
-          "e2e_kwok_test"]
+          "e2e_kwok_test", "same_interval_echo"]
 
 
 def load_trace(name):
