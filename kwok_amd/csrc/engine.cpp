@@ -260,6 +260,7 @@ struct kwok_engine {
         uint32_t* emit_n = nullptr;
         bool emit_queued = false;   // k_emit was enqueued behind the tick's launches
         bool split = false;         // TICK_SPLIT: k_pod_jobs builds the pod jobs after the tick's launches
+        bool quiet = false;         // only pods with an event are Use-checked (kwok_engine::quiet)
         bool alloc = false;
         // the tick in the slot
         int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
@@ -290,6 +291,15 @@ struct kwok_engine {
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
+    // Quiet ticks.  A tick's Use(podIP) of an evaluated pod (pod_controller.go:
+    // 378-382) is a no-op when the address is already in `used`.  Only a Put clears
+    // a bit, and Puts come from ingest (Deleted events), kwok_pool_put, and the
+    // deletions a tick makes of the pods marked at the ingest before it.  So after
+    // two submits with nothing in between, the previous tick Use-checked every
+    // evaluated pod and released nothing: this tick need only Use-check pods with
+    // an event (single rank; KWOK_QUIET=0 checks every pod).
+    uint32_t quiet = 0;         // submits since the last ingest / pool_put / cni_assign
+    bool quiet_ok = true;
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
@@ -1313,6 +1323,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
+        const char* qt = getenv("KWOK_QUIET");
+        e->quiet_ok = !(qt && qt[0] == '0');
         const char* sj = getenv("KWOK_SPLIT");
         e->split_jobs = !(sj && sj[0] == '0');
         const char* zc = getenv("KWOK_INGEST_ZC");
@@ -1538,6 +1550,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
+    e->quiet = 0;
     auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
     const auto tq0 = clk::now();
     // a deleted node's entry lives while pods reference it (the pods' node refs,
@@ -1747,6 +1760,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     drain(e);  // the device state reflects every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
+    e->quiet = 0;
     if (!n) return 0;
     const auto t0 = clk::now();
     // node ops an earlier call deferred (retire's frees) land before the pass reads node states
@@ -1915,6 +1929,7 @@ int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips,
     drain(e);
     if (e->poisoned) return poisoned(e);
     if (!n) return 0;
+    e->quiet = 0;
     // a handle assigned twice keeps its last valid IP (configurePod runs once per tick)
     std::vector<uint8_t> wr(n, 0);
     {
@@ -1949,6 +1964,7 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
     e->stage[0].puts.insert(e->stage[0].puts.end(), ips, ips + n);
+    e->quiet = 0;
     return flush_ops(e);
 }
 
@@ -2010,6 +2026,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // of it would hold up the pool phase, which waits for every dirty block
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
                                        : (hb_bytes < (32ull << 20) || T.split ? 1024u : (S.hb_nt ? 860u : 921u));
+    S.use_events_only = T.quiet ? 1u : 0u;
     int rc = bind_slot(e, k);
     if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
@@ -2378,6 +2395,8 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     T.epoch = e->hb_epoch;
     T.emit_queued = e->emit_hint;
     e->emit_hint = false;
+    T.quiet = e->quiet_ok && !e->multi && e->quiet >= 2;
+    if (e->quiet < 0xFFFFFFFFu) e->quiet++;
     rc = enqueue_tick(e, k, false);
     if (rc) return rc;
     T.state = SLOT_QUEUED;

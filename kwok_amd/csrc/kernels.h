@@ -96,6 +96,7 @@ struct DevState {
     uint32_t hb_once;          // KWOK_CFG_HEARTBEAT_ONCE: one heartbeat body per tick, not one per node
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
     uint32_t custom_pod;       // Config.PodStatusTemplate is custom: the caller's CONFORMS digest is ignored
+    uint32_t use_events_only;  // this tick Use-checks only pods with an event (a quiet tick: kwok_tick_submit)
     uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp

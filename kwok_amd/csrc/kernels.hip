@@ -801,7 +801,9 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
         put(m.alloc, alloc);
         put(m.need, need);
         put(m.rel, del & managed & inc);
-        put(m.usec, eval & inc);
+        // quiet ticks (use_events_only): every live pod's address is already in `used`
+        // unless an event changed the pod since (engine.cpp, kwok_tick_submit)
+        put(m.usec, eval & inc & (S.use_events_only ? event : M));
         put(m.total, live);
         put(m.pend, live & ~need & pending);
         put(m.run, live & (need | running));
