@@ -50,9 +50,11 @@ type gpuEngine struct {
 	h       *C.kwok_engine
 	hb      []int32 // heartbeat handle list of heartbeat epoch hbEpoch
 	hbEpoch uint32
-	// page-locked batch buffers (kwok_host_alloc), reused: kwok_ingest_pods copies
-	// records and strings to the GPU by DMA from these
-	evBuf, arBuf hostBuf
+	// page-locked batch buffers (kwok_host_alloc), reused: kwok_ingest_pods reads
+	// the records and strings in place from these (no copy), and writes the
+	// per-record results to resBuf (a copy into pageable Go memory would stall the
+	// engine's next transfers, DESIGN.md §11)
+	evBuf, arBuf, resBuf hostBuf
 }
 
 type hostBuf struct {
@@ -154,6 +156,7 @@ func (g *gpuEngine) close() {
 	}
 	g.evBuf.free()
 	g.arBuf.free()
+	g.resBuf.free()
 }
 
 func arenaPtr(arena []byte) *C.char {
@@ -221,10 +224,18 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 		ev[i] = evs[i]
 		ev[i].node_name, ev[i].host_ip, ev[i].pod_ip = pack(evs[i].node_name), pack(evs[i].host_ip), pack(evs[i].pod_ip)
 	}
-	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(len(ev)), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
-		(*C.int32_t)(&handles[0]), (*C.int32_t)(&status[0]), (*C.uint32_t)(&released[0]))
+	n := len(ev)
+	res := unsafe.Slice((*int32)(g.resBuf.get(3*4*n)), 3*n)
+	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(n), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
+		(*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]), (*C.uint32_t)(unsafe.Pointer(&res[2*n])))
 	if rc < 0 {
 		err = fmt.Errorf("kwok_ingest_pods: %d: %s", int(rc), g.lastError())
+		return
+	}
+	copy(handles, res[:n])
+	copy(status, res[n:2*n])
+	for i := range released {
+		released[i] = uint32(res[2*n+i])
 	}
 	return
 }

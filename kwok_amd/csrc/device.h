@@ -46,7 +46,7 @@ constexpr int MAX_BPB = 64;               // buckets per chain block
 constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS node flags)
 constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
 constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
-constexpr int SPEC_GROUPS = 3;            // pod groups per thread loaded before the fill marks land
+constexpr int SPEC_GROUPS = 2;            // pod groups per thread loaded before the fill marks land
 // split ticks (k_pod_jobs): a chain block's live groups in runs of 64, one wave each
 constexpr int WC_GROUPS = 64;
 constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block

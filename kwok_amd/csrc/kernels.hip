@@ -740,6 +740,9 @@ __device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g
 // the spec words of a group with a pod that needs a patch (its byte count)
 __device__ __forceinline__ uint4 load_spec_words(const DevState& S, const PodGrp& g, uint32_t need) {
     uint4 v = make_uint4(0, 0, 0, 0);
+#ifdef DIAG_NO_SPECW  // timing builds only
+    return v;
+#endif
     if (need && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
     return v;
 }
@@ -803,7 +806,11 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
         put(m.rel, del & managed & inc);
         // quiet ticks (use_events_only): every live pod's address is already in `used`
         // unless an event changed the pod since (engine.cpp, kwok_tick_submit)
+#ifdef DIAG_NO_USE  // timing builds only
+        put(m.usec, 0u);
+#else
         put(m.usec, eval & inc & (S.use_events_only ? event : M));
+#endif
         put(m.total, live);
         put(m.pend, live & ~need & pending);
         put(m.run, live & (need | running));
@@ -877,6 +884,27 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
     f[AG_RUNNING] += __popc(m.run);
     if (__builtin_expect(__ballot((m.rel | m.need) != 0) != 0, 0)) {
         const uint32_t w[4] = {spw.x, spw.y, spw.z, spw.w};
+        // single rank: a group's released addresses usually share one bitmap word
+        // (consecutive allocations): one atomic for all of them, else one per pod
+        uint64_t rm = 0;
+        uint32_t rw = 0;
+        bool one = !S.multi && m.rel != 0;
+        if (one) {
+            uint32_t ip0 = g.ip[0];
+#pragma unroll
+            for (int k = 1; k < POD_PER_THREAD; k++) ip0 = (uint32_t)__builtin_ctz(m.rel) == (uint32_t)k ? g.ip[k] : ip0;
+            rw = (ip0 - S.pool.net) >> 6;
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) {
+                const uint32_t bit = g.ip[k] - S.pool.net;
+                const bool r = (m.rel >> k) & 1;
+                one &= !r || (bit >> 6) == rw;
+                rm |= r ? 1ull << (bit & 63) : 0ull;
+            }
+#ifndef DIAG_NO_REL  // timing builds only (tools/build_variant.sh): the releases skipped
+            if (one) atomicOr((unsigned long long*)&S.rel_bm[rw], rm);
+#endif
+        }
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
             const uint32_t ip = g.ip[k];
@@ -886,7 +914,9 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
             // (pod_controller.go:329-336).  Single rank: the Put waits in rel_bm, folded in
             // the pool phase after every Use of this tick (Use -> Put)
             if (!S.multi) {
-                if (r) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+#ifndef DIAG_NO_REL
+                if (r && !one) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
+#endif
             } else {
                 wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
             }
@@ -907,6 +937,9 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
 // split ticks: a dirty group's counts into its 64-group run (LDS, [MAX_WC][4]
 // then the dirty bits); gi = the group's index among the block's live groups
 __device__ __forceinline__ void wc_add(uint32_t* wcnt, uint32_t gi, const GroupMasks& m, uint32_t bytes) {
+#ifdef DIAG_NO_WC  // timing builds only
+    return;
+#endif
     if (!m.dirty) return;
     const uint32_t w = gi / WC_GROUPS;
     if (m.del) atomicAdd(&wcnt[4 * w], (uint32_t)__popc(m.del));
