@@ -300,6 +300,7 @@ struct kwok_engine {
     // an event (single rank; KWOK_QUIET=0 checks every pod).
     uint32_t quiet = 0;         // submits since the last ingest / pool_put / cni_assign
     bool quiet_ok = true;
+    std::vector<uint32_t> slot_refs;  // kwok_ingest_nodes: pods referencing the batch's deleted nodes (else 0)
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
@@ -1556,11 +1557,18 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     // a deleted node's entry lives while pods reference it (the pods' node refs,
     // pod_controller.go routes by spec.nodeName): the references of the nodes this
     // batch deletes, counted on the device (no pod changes during a node batch)
-    std::unordered_map<uint32_t, uint32_t> refs;  // (filled below, before any record is ingested)
-    auto refs_of = [&](uint32_t slot) {  // a node created in this batch has none
-        auto it = refs.find(slot);
-        return it == refs.end() ? 0u : it->second;
-    };
+    // (filled below, before any record is ingested; a per-slot array the engine
+    // keeps zeroed: the batch's entries are cleared on every way out)
+    if (e->slot_refs.size() < (size_t)e->NL) e->slot_refs.assign((size_t)e->NL, 0u);
+    std::vector<uint32_t> del;
+    struct ClearRefs {
+        std::vector<uint32_t>& a;
+        const std::vector<uint32_t>& d;
+        ~ClearRefs() {
+            for (uint32_t s : d) a[s] = 0;
+        }
+    } clear_refs{e->slot_refs, del};
+    auto refs_of = [&](uint32_t slot) { return e->slot_refs[slot]; };  // a node created in this batch has none
     // per partition: managed-set changes (applied after the batch)
     std::vector<int64_t> d_managed((size_t)e->n_part, 0);
     std::vector<uint8_t> set_changed((size_t)e->n_part, 0);
@@ -1708,12 +1716,11 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         if (threaded) run_parts(e, true, pass1);
         else pass1(0);
         tq1 = clk::now();
-        std::vector<uint32_t> del;
         for (auto& d : dels) del.insert(del.end(), d.begin(), d.end());
         if (!del.empty()) {
             std::vector<uint32_t> cnt;
             if (int rc = node_refs(e, del, cnt)) return rc;
-            for (size_t k = 0; k < del.size(); k++) refs[del[k]] = cnt[k];
+            for (size_t k = 0; k < del.size(); k++) e->slot_refs[del[k]] = cnt[k];
         }
     }
     const auto tn0 = clk::now();  // (refs: tq0 .. tn0)

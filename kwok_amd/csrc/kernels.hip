@@ -1234,6 +1234,12 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
         bool dirty = false;
         uint16_t nst[POD_PER_THREAD];
         uint32_t ai = 0;
+        // the group's hostIP / podIP words after the patches (the loaded values
+        // where unchanged): written as two 16-byte stores each, not one per pod
+        uint32_t nh[POD_PER_THREAD], np[POD_PER_THREAD];
+        bool wh = false, wp = false;
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) nh[k] = hipk[i][k], np[k] = gi.ip[k];
         // the group's 8 slots share a bucket (bk0 + j): handles without a division
         const uint32_t gb = bk0 + gi.j;
         const int32_t h0 = (int32_t)((S.b_lo + gb) * S.pod_stride + (gi.slot - gb * S.cp));
@@ -1264,8 +1270,8 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
                     uint32_t hip = 0;
                     if (stat) {
                         hip = (s & PS_HAS_HOST_IP) ? hipk[i][k] : S.node_ip;
-                        if (!(s & PS_HAS_HOST_IP)) S.host_ip[slot] = hip;
-                        if (pip != gi.ip[k]) S.pod_ip[slot] = pip;
+                        if (!(s & PS_HAS_HOST_IP)) nh[k] = hip, wh = true;
+                        if (pip != gi.ip[k]) np[k] = pip, wp = true;
                     }
                     const uint64_t ord = r.v[AG_PP] + jl;
                     const uint32_t len = sd_len[i][k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
@@ -1290,6 +1296,14 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             uint4* dst = S.pp_job + r.v[AG_PP] + wpre;
             uint64_t* dst_off = S.pp_off + r.v[AG_PP] + wpre;
             for (uint32_t q = lane_id(); q < wend - wpre; q += 64) dst[q] = stg[q], dst_off[q] = stg_off[q];
+        }
+        if (wh) {
+            *reinterpret_cast<uint4*>(S.host_ip + gi.slot) = make_uint4(nh[0], nh[1], nh[2], nh[3]);
+            *reinterpret_cast<uint4*>(S.host_ip + gi.slot + 4) = make_uint4(nh[4], nh[5], nh[6], nh[7]);
+        }
+        if (wp) {
+            *reinterpret_cast<uint4*>(S.pod_ip + gi.slot) = make_uint4(np[0], np[1], np[2], np[3]);
+            *reinterpret_cast<uint4*>(S.pod_ip + gi.slot + 4) = make_uint4(np[4], np[5], np[6], np[7]);
         }
         if (gi.slot != ~0u && dirty) {
             uint4 o;
