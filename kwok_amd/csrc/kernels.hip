@@ -746,8 +746,10 @@ __device__ __forceinline__ uint4 load_spec_words(const DevState& S, const PodGrp
     if (need && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
     return v;
 }
-__device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uint8_t* nflags, const PodGrp& g, int k) {
-    return (g.st(k) & PS_USED) ? nflags[g.j * S.cn + g.nl(k)] : (uint8_t)0;
+// nflags holds the flags of the block's buckets from bucket j0 on
+__device__ __forceinline__ uint8_t group_node_flags(const DevState& S, const uint8_t* nflags, const PodGrp& g, int k,
+                                                    uint32_t j0 = 0) {
+    return (g.st(k) & PS_USED) ? nflags[(g.j - j0) * S.cn + g.nl(k)] : (uint8_t)0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1131,7 +1133,7 @@ constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs 
 template <int NC, bool WAVE = false>
 __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
                                                 uint32_t nbk, uint32_t ng, const uint32_t (&gidx)[NC], Bases& run,
-                                                const Layout& L, uint32_t* stage) {
+                                                const Layout& L, uint32_t* stage, uint32_t nj0 = 0) {
     PodGrp g[NC];
     uint16_t sp[NC][POD_PER_THREAD];
 #pragma unroll
@@ -1151,7 +1153,7 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
         bool any_need = false, one_spec = true;
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
-            cl[i][k] = classify_pod(g[i].st(k), group_node_flags(S, nflags, g[i], k), g[i].ip[k], S.cni != 0);
+            cl[i][k] = classify_pod(g[i].st(k), group_node_flags(S, nflags, g[i], k, nj0), g[i].ip[k], S.cni != 0);
             any_need |= cl[i][k].need;
             one_spec &= sp[i][k] == sp[i][0];
         }
@@ -1245,7 +1247,6 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
         const int32_t h0 = (int32_t)((S.b_lo + gb) * S.pod_stride + (gi.slot - gb * S.cp));
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) {
-            const uint32_t slot = gi.slot + k;
             const int32_t handle = h0 + k;
             uint16_t s = gi.st(k);
             if (cl[i][k].del) {
@@ -2122,9 +2123,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
 // ---------------------------------------------------------------------------
 constexpr int JOB_WAVES = 4;
 constexpr int JOB_NC = 2;  // consecutive runs per wave, their loads and scans interleaved
+constexpr int JOB_NF_BYTES = 768;  // node flags staged per wave (two buckets of ~350 node slots)
 __global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
     __shared__ uint32_t stage[JOB_WAVES * POD_STAGE_WORDS];
     __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    __shared__ uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
     static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
     const uint32_t b = blockIdx.x / wg_per_block;
     const uint32_t w = (uint32_t)wave_id();
@@ -2162,10 +2165,26 @@ __global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_
     if (l == 0) gpre[0] = 0;
     const uint32_t ng = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
+    // the node tick flags of the buckets the two runs span, into LDS with coalesced
+    // loads (the groups then read them there, not with eight byte loads each)
+    const uint8_t* nflags = S.node_tick + (size_t)bk0 * S.cn;
+    uint32_t nj0 = 0;
+    if (c0 * WC_GROUPS < ng) {
+        const uint32_t ja = find_bucket(gpre, nbk, c0 * WC_GROUPS);
+        const uint32_t jb = find_bucket(gpre, nbk, min((c0 + JOB_NC) * WC_GROUPS, ng) - 1u);
+        const uint32_t nwords = (jb - ja + 1u) * S.cn / 4u;  // (cn % 4 == 0)
+        if (nwords * 4u <= (uint32_t)JOB_NF_BYTES) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(nflags + (size_t)ja * S.cn);
+            for (uint32_t v = (uint32_t)l; v < nwords; v += 64) nf_w[w][v] = src[v];
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            nflags = reinterpret_cast<const uint8_t*>(nf_w[w]);
+            nj0 = ja;
+        }
+    }
     // both runs (a clean one has nothing to count or emit, so the second run's
     // bases follow from the first's totals either way)
     const uint32_t gx[JOB_NC] = {c0 * WC_GROUPS + (uint32_t)l, (c0 + 1) * WC_GROUPS + (uint32_t)l};
-    emit_pod_chunks<JOB_NC, true>(S, gpre, S.node_tick + (size_t)bk0 * S.cn, bk0, nbk, ng, gx, run, L, stage);
+    emit_pod_chunks<JOB_NC, true>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0);
 }
 
 // ingest-time Put (a Deleted watch event), applied immediately
