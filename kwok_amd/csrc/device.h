@@ -208,7 +208,10 @@ struct IngSummary {
     uint32_t n_freed;       // node slots the apply pass freed (deleted / placeholder nodes no pod references)
     uint32_t n_stopped;     // buckets whose apply pass stopped at an unresolved REC_HARD record
     uint32_t need;          // max over buckets with creates: live pods + creates (growth check)
-    uint32_t pad[3];
+    uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
+                            // pool: a create with a podIP, an update to another podIP, a Deleted event
+                            // releasing an address its pod does not hold (quiet ticks, engine.cpp)
+    uint32_t pad[2];
 };
 
 // spec descriptor: A | B | C segments of the pod patch (see templates.cpp)

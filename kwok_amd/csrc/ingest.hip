@@ -350,7 +350,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     lds_sync();
     const uint32_t keep_ex = PS_EVENT | PS_DELETE_PENDING;
     uint32_t rejected = 0;
-    bool stopped = false;
+    bool stopped = false, foreign = false;
     uint32_t p0 = pbeg;
     for (; p0 < pend && !stopped; p0 += 64) {
         mem_sync();  // the previous chunk's stores, before this chunk's (coherent) loads
@@ -369,10 +369,11 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         const uint32_t chk = (hfl >> 8) & 0xFFu;
         // prefetch: an existing pod's state and node; the node's state
         const bool ex = v && (chk & REC_EXISTING) && pos < B.cp;
-        uint32_t st0 = 0, nd0 = pos;
+        uint32_t st0 = 0, nd0 = pos, ip0 = 0;
         if (ex) {
             st0 = ld16_coh(S.pod_state + B.sbase + pos);
             nd0 = ld16_coh(S.pod_node + B.sbase + pos);
+            ip0 = ld_coh(S.pod_ip + B.sbase + pos);
         }
         uint32_t ns0 = 0;
         if (v && nd0 < B.cn) ns0 = ld8_coh(S.node_state + B.nbase + nd0);
@@ -437,6 +438,8 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                     else slot = flist[r], cur = 0;
                 }
                 if (act && stt == KWOK_OK) {
+                    // an in-CIDR podIP this pod did not hold (a create with one, an update to another)
+                    foreign |= ra.w && d_in_cidr(S.pool, ra.w) && (!exl || ra.w != ip0);
                     const uint32_t nst = (cur & (exl ? keep_ex : 0u)) | pod_bits(S, fl, hop >> 24, ra.z, ra.w, ns0);
                     const size_t g = B.sbase + slot;
                     S.pod_state[g] = (uint16_t)nst;
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         // ---- serial path: the records one at a time, in event order ----
         // in-chunk hazards: lane j keeps what record j wrote (slot, its state / node;
         // a freed node index)
-        uint32_t wslot = ~0u, wst = 0, wnd = 0, wfreed = ~0u;
+        uint32_t wslot = ~0u, wst = 0, wnd = 0, wip = 0, wfreed = ~0u;
         const uint32_t cnt = pend - p0 < 64u ? pend - p0 : 64u;
         for (uint32_t k = 0; k < cnt; k++) {
             const uint32_t kchk = rdl(chk, k);
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
             int stt = KWOK_OK;
             int32_t handle = -1;
             uint32_t released = 0;
-            uint32_t cur = rdl(st0, k), nd = rdl(nd0, k);
+            uint32_t cur = rdl(st0, k), nd = rdl(nd0, k), curip = rdl(ip0, k);
             if (existing) {
                 if (kpos >= B.cp || !((B.bm[kpos >> 6] >> (kpos & 63)) & 1)) {
                     stt = KWOK_ENOTFOUND;
@@ -494,6 +497,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                         const uint32_t j = 63u - (uint32_t)__builtin_clzll(m);
                         cur = rdl(wst, j);
                         nd = rdl(wnd, j);
+                        curip = rdl(wip, j);
                     }
                 }
             }
@@ -520,6 +524,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                 const uint32_t ip = rdl(ra.w, k);
                 if (!S.cni && (ns & NS_MANAGED) && (kchk & REC_DEL_IP) && d_in_cidr(S.pool, ip)) {
                     released = ip;
+                    foreign |= ip != curip;  // a release of an address its pod does not hold
                     if (l == 0) {
                         const uint64_t bit = ip - S.pool.net;
                         atomicAnd((unsigned long long*)&S.used_bm[bit >> 6], ~(1ull << (bit & 63)));
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                 }
                 lds_sync();
                 if ((kpos >> 6) < B.hint) B.hint = kpos >> 6;
-                if (l == k) wslot = kpos, wst = 0, wnd = nd;
+                if (l == k) wslot = kpos, wst = 0, wnd = nd, wip = 0;
                 // the node entry of a deleted (or placeholder) node lives while pods reference it
                 if ((ns & NS_SLOT) && !(ns & NS_EXISTS) && !node_referenced(S, B, nd)) free_node(nd);
                 handle = (int32_t)((S.b_lo + b) * S.pod_stride + kpos);
@@ -558,6 +563,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                 }
                 if (stt == KWOK_OK) {
                     const uint32_t hip = rdl(ra.z, k), pip = rdl(ra.w, k);
+                    foreign |= pip && d_in_cidr(S.pool, pip) && (!existing || pip != curip);
                     const uint32_t bits = pod_bits(S, flags, rdl(hop, k) >> 24, hip, pip, ns);
                     const uint32_t nst = (cur & (existing ? keep_ex : 0u)) | bits;
                     if (l == 0) {
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                         S.host_ip[g] = hip;
                         S.pod_ip[g] = pip;
                     }
-                    if (l == k) wslot = slot, wst = nst, wnd = nd;
+                    if (l == k) wslot = slot, wst = nst, wnd = nd, wip = pip;
                     handle = (int32_t)((S.b_lo + b) * S.pod_stride + slot);
                 }
             } else if (stt == KWOK_OK) {
@@ -587,6 +593,9 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         if (B.fill != fill0) S.pod_fill[b] = (uint16_t)B.fill;
         if (!stopped) I.beg[b] = pend;  // done: a relaunch after a stop skips the bucket
         if (rejected) atomicAdd(&I.sum->rejected, rejected);
+    }
+    if (__ballot(foreign) && l == 0) {
+        atomicOr(&I.sum->foreign, 1u);
     }
 }
 
