@@ -207,6 +207,14 @@ struct kwok_engine {
         uint32_t* refs_out = nullptr;
         IngSummary* sum = nullptr;
         IngSummary* sum_h = nullptr;  // pinned
+        // a batch runs in chunks (KWOK_INGEST_CHUNK records): chunk k+1's prep reads its
+        // records over the link on `pst` while chunk k is applied and its results copied
+        // back on the engine stream; odd chunks take the second accumulator set
+        uint32_t *creates1 = nullptr, *dels1 = nullptr;
+        IngSummary* sum1 = nullptr;
+        hipStream_t pst = nullptr, dst = nullptr;  // prep (H2D + k_ing_prep) / results (D2H)
+        hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+        size_t chunk = 1048576;
     } ing;
 
     // ---- specs / blobs ----
@@ -937,9 +945,9 @@ IngestBatch ingest_batch(kwok_engine* e, uint32_t n, size_t arena_len) {
     return I;
 }
 // the batch summary -> pinned host memory (waits for the stream)
-int read_summary(kwok_engine* e) {
+int read_summary(kwok_engine* e, const IngSummary* sum = nullptr) {
     if (int rc = release_for_host(e)) return rc;
-    HIPCHK(e, hipMemcpyAsync(e->ing.sum_h, e->ing.sum, sizeof(IngSummary), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(e->ing.sum_h, sum ? sum : e->ing.sum, sizeof(IngSummary), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     return KWOK_OK;
 }
@@ -1175,10 +1183,15 @@ void kwok_engine_destroy(kwok_engine* e) {
         auto& g = e->ing;
         void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
                       g.out_released, g.byname, g.fix, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.stopped,
-                      g.freed, g.refs_q, g.refs_out, g.sum};
+                      g.freed, g.refs_q, g.refs_out, g.sum, g.creates1, g.dels1, g.sum1};
         for (void* p : ip)
             if (p) (void)hipFree(p);
         if (g.sum_h) (void)hipHostFree(g.sum_h);
+        hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1]};
+        for (hipEvent_t x : evs)
+            if (x) (void)hipEventDestroy(x);
+        if (g.pst) (void)hipStreamDestroy(g.pst);
+        if (g.dst) (void)hipStreamDestroy(g.dst);
     }
     if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
@@ -1321,6 +1334,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
         e->n_stream = once ? 8u : (uint32_t)(cus * wants);
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
+        if (const char* v = getenv("KWOK_EMIT_BLOCKS_PER_CU")) e->emit_grid = (uint32_t)(cus * std::max(1, std::min(atoi(v), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
         const char* pr = getenv("KWOK_TICK_PRIO");
         e->chain_prio = pr && pr[0] == '1';
@@ -1453,9 +1467,17 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         auto& g = e->ing;
         if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.dels, e->nb)) || (rc = dalloc(e, &g.beg, e->nb)) ||
             (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.stopped, e->nb)) || (rc = dalloc(e, &g.freed, e->NL)) ||
-            (rc = dalloc(e, &g.refs_q, e->NL)) || (rc = dalloc(e, &g.refs_out, e->NL)) || (rc = dalloc(e, &g.sum, 1)))
+            (rc = dalloc(e, &g.refs_q, e->NL)) || (rc = dalloc(e, &g.refs_out, e->NL)) || (rc = dalloc(e, &g.sum, 1)) ||
+            (rc = dalloc(e, &g.creates1, e->nb)) || (rc = dalloc(e, &g.dels1, e->nb)) || (rc = dalloc(e, &g.sum1, 1)))
             return bail(rc);
         if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
+        hipError_t r = hipStreamCreateWithFlags(&g.pst, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipStreamCreateWithFlags(&g.dst, hipStreamNonBlocking);
+        hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1]};
+        for (hipEvent_t* x : evs)
+            if (r == hipSuccess) r = hipEventCreateWithFlags(x, hipEventDisableTiming);
+        if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "ingest stream/events: %s", hipGetErrorString(r)));
+        if (const char* v = getenv("KWOK_INGEST_CHUNK")) g.chunk = std::max<size_t>(1, strtoull(v, nullptr, 10));
     }
     e->node_stamp.assign(e->NL, 0);
     e->node_opi.assign(e->NL, 0);
@@ -1786,53 +1808,20 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     return rc ? rc : rejected;
 }
 
-int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
-                     int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
-    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
-    if (e->poisoned) return poisoned(e);
-    drain(e);  // the device state reflects every submitted tick
-    if (e->poisoned) return poisoned(e);
-    e->emit_hint = true;
-    e->quiet = 0;
-    if (!n) return 0;
-    const auto t0 = clk::now();
-    // node ops an earlier call deferred (retire's frees) land before the pass reads node states
-    if (node_ops_pending(e))
-        if (int rc = flush_ops(e)) return rc;
-    int rc = ingest_reserve(e, n, arena_len);
-    if (rc) return rc;
+// One chunk of a pod batch after its prep (I: the chunk's records, ev: their host
+// copies, indices chunk-local): the growth check, by-name resolution, the stable
+// sort by bucket and the apply pass, on the engine stream.  Returns the chunk's
+// rejected count (>= 0) or an error.
+int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev, const char* arena) {
     auto& G = e->ing;
     hipStream_t st = e->st;
-    // a batch in kwok_host_alloc memory is read in place by k_ing_prep (the only
-    // kernel that reads the records and their strings): one pass over the link,
-    // no copy engine (KWOK_INGEST_ZC=0: copy it to HBM first)
-    const void* zev = e->ingest_zc ? host_mapped(ev, n * sizeof(kwok_pod_event)) : nullptr;
-    const void* zar = e->ingest_zc && arena_len ? host_mapped(arena, arena_len) : nullptr;
-    auto batch = [&]() {
-        IngestBatch b = ingest_batch(e, (uint32_t)n, arena_len);
-        if (zev) b.ev = zev;
-        if (zar) b.arena = (const uint8_t*)zar;
-        return b;
-    };
-    IngestBatch I = batch();
-    // the records and their strings -> HBM (unless read in place); prep; the growth need
-    HIPCHK(e, hipMemsetAsync(G.sum, 0, sizeof(IngSummary), st));
-    HIPCHK(e, hipMemsetAsync(G.dels, 0, (size_t)e->nb * 4, st));
-    if (!zev) HIPCHK(e, hipMemcpyAsync(G.d_ev, ev, n * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
-    if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
-    double t_h2d = 0;
-    if (e->iprof) {  // diagnostics: the copies on their own
-        HIPCHK(e, hipStreamSynchronize(st));
-        t_h2d = ms_between(t0, clk::now());
-    }
-    launch_ingest_prep(e->S, I, st);
+    int rc = 0;
     launch_ingest_need(e->S, I, st);
     HIPCHK(e, hipGetLastError());
-    if ((rc = read_summary(e))) return rc;
-    const auto t1 = clk::now();
+    if ((rc = read_summary(e, I.sum))) return rc;
     IngSummary sum = *G.sum_h;
     // growth: every bucket to a larger capacity (up to the handle stride) when the
-    // batch's creates could fill one
+    // chunk's creates could fill one
     bool efull_possible = false;
     if (sum.need > e->Cp) {
         const uint32_t cap = max_pod_capacity(e);
@@ -1840,7 +1829,6 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(((uint64_t)sum.need + 7) & ~7ull, 2ull * e->Cp));
             if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
             if ((rc = grow_pods(e, want))) return rc;
-            I = batch();
         }
         efull_possible = sum.need > e->Cp;  // at the stride (or the chain blocks' limit): EFULL per record
     }
@@ -1848,12 +1836,12 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     std::vector<uint32_t> fix;
     if (sum.n_byname) {
         std::vector<uint32_t> idx(sum.n_byname), dels(e->nb);
-        HIPCHK(e, hipMemcpyAsync(idx.data(), G.byname, idx.size() * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipMemcpyAsync(dels.data(), G.dels, dels.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipMemcpyAsync(idx.data(), I.byname, idx.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipMemcpyAsync(dels.data(), I.dels, dels.size() * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipStreamSynchronize(st));
         std::sort(idx.begin(), idx.end());
-        const std::vector<uint32_t> zb0 = e->zb_count;  // zombie entries at the batch's start
-        // A node entry can only be freed during the batch in a bucket that deletes pods
+        const std::vector<uint32_t> zb0 = e->zb_count;  // zombie entries at the chunk's start
+        // A node entry can only be freed during the chunk in a bucket that deletes pods
         // at ingest, holds zombie entries, or may run out of pod slots: there a name
         // that is missing or a zombie is resolved when the apply pass reaches it
         // (REC_HARD).  Elsewhere every lookup (and placeholder) is the one event
@@ -1881,13 +1869,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
     if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
         return e->fail(KWOK_EDEVICE, "ingest sort");
-    const auto t2 = clk::now();
-    int rounds = 0;
     for (;;) {
         launch_ingest_apply(e->S, I, st);
         HIPCHK(e, hipGetLastError());
-        if ((rc = read_summary(e))) return rc;
-        rounds++;
+        if ((rc = read_summary(e, I.sum))) return rc;
         if ((rc = free_device_freed(e))) return rc;  // node entries the pass freed
         if (G.sum_h->foreign) e->foreign_ips = true;
         if (!G.sum_h->n_stopped) break;
@@ -1898,7 +1883,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         HIPCHK(e, hipStreamSynchronize(st));
         for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&pos[k], G.beg + bk[k], 4, hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipStreamSynchronize(st));
-        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&ix[k], G.idx_sorted + pos[k], 4, hipMemcpyDeviceToHost, st));
+        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&ix[k], I.idx_sorted + pos[k], 4, hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipStreamSynchronize(st));
         fix.clear();
         for (uint32_t i : ix) {
@@ -1909,22 +1894,116 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         }
         if ((rc = apply_fixes(e, I, fix))) return rc;
         if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;
-        HIPCHK(e, hipMemsetAsync(&G.sum->n_stopped, 0, 4, st));
-        HIPCHK(e, hipMemsetAsync(&G.sum->n_freed, 0, 4, st));
+        HIPCHK(e, hipMemsetAsync(&I.sum->n_stopped, 0, 4, st));
+        HIPCHK(e, hipMemsetAsync(&I.sum->n_freed, 0, 4, st));
     }
-    const auto t3 = clk::now();
-    // per-record results -> the caller's arrays
-    if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles, G.out_handle, n * 4, hipMemcpyDeviceToHost, st));
-    if (out_status) HIPCHK(e, hipMemcpyAsync(out_status, G.out_status, n * 4, hipMemcpyDeviceToHost, st));
-    if (out_released) HIPCHK(e, hipMemcpyAsync(out_released, G.out_released, n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(e, hipStreamSynchronize(st));
-    if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s): copy + prep %.2f ms (H2D %.2f ms, %.1f GB/s), "
-                        "resolve + sort %.2f ms, apply %.2f ms (%d rounds), results %.2f ms\n", n,
-                zev ? ", read in place" : "", ms_between(t0, t1),
-                t_h2d, (n * sizeof(kwok_pod_event) + arena_len) / (t_h2d * 1e6), ms_between(t1, t2), ms_between(t2, t3),
-                rounds, ms_between(t3, clk::now()));
     return (int)G.sum_h->rejected;
+}
+
+int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
+                     int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
+    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    drain(e);  // the device state reflects every submitted tick
+    if (e->poisoned) return poisoned(e);
+    e->emit_hint = true;
+    e->quiet = 0;
+    if (!n) return 0;
+    const auto t0 = clk::now();
+    // node ops an earlier call deferred (retire's frees) land before the pass reads node states
+    if (node_ops_pending(e))
+        if (int rc = flush_ops(e)) return rc;
+    int rc = ingest_reserve(e, n, arena_len);
+    if (rc) return rc;
+    auto& G = e->ing;
+    hipStream_t st = e->st, ps = G.pst;
+    // Chunks of the batch in event order: applying them one after the other is
+    // applying the batch (every record is applied in event order; a chunk is what
+    // a separate call with those records would do).  The copy engine moves chunk
+    // k+1's records to HBM (and k_ing_prep prepares them) on the prep stream while
+    // the engine stream applies chunk k, and chunk k's results go back on the
+    // results stream: the link carries the batch once in each direction, with the
+    // apply passes under it.  The last chunk is shorter (its apply and results are
+    // the part nothing hides).  The prep of chunk k + 2 waits until chunk k has
+    // released its accumulator set.
+    const uint32_t K = n > G.chunk ? (uint32_t)((n + G.chunk - 1) / G.chunk) : 1u;
+    const double W = K > 1 ? K - 0.4 : 1.0;
+    auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W); };
+    // a one-chunk batch in kwok_host_alloc memory is read in place by k_ing_prep
+    // (the only kernel that reads the records and their strings): one pass over
+    // the link, no copy engine (KWOK_INGEST_ZC=0: copy it to HBM first).  Chunked
+    // batches are copied: kernels reading host memory in place hold their CUs for
+    // the link's latency, and the apply passes beside them stall (1M deletes + 1M
+    // creates in 4 chunks: 4.9 ms read in place against 2.8 ms copied).
+    const bool zc_ok = e->ingest_zc && K == 1;
+    const void* zev = zc_ok ? host_mapped(ev, n * sizeof(kwok_pod_event)) : nullptr;
+    const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
+    auto chunk_batch = [&](uint32_t k) {
+        const size_t lo = lo_of(k);
+        IngestBatch b = ingest_batch(e, (uint32_t)(lo_of(k + 1) - lo), arena_len);
+        b.ev = static_cast<const kwok_pod_event*>(zev ? zev : (const void*)G.d_ev) + lo;
+        if (zar) b.arena = (const uint8_t*)zar;
+        b.rec += lo, b.keys += lo, b.keys_sorted += lo, b.idx_sorted += lo;
+        b.out_handle += lo, b.out_status += lo, b.out_released += lo, b.byname += lo;
+        if (k & 1) b.creates = G.creates1, b.dels = G.dels1, b.sum = G.sum1;
+        return b;
+    };
+    auto prep = [&](uint32_t k) -> int {
+        const IngestBatch b = chunk_batch(k);
+        if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
+        HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
+        HIPCHK(e, hipMemsetAsync(b.dels, 0, (size_t)e->nb * 4, ps));
+        HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, ps));
+        if (!zev)
+            HIPCHK(e, hipMemcpyAsync(static_cast<kwok_pod_event*>(G.d_ev) + lo_of(k), ev + lo_of(k), (size_t)b.n * sizeof(kwok_pod_event),
+                                     hipMemcpyHostToDevice, ps));
+        launch_ingest_prep(e->S, b, ps);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(G.prepped[k & 1], ps));
+        return KWOK_OK;
+    };
+    // the prep stream starts after the work already queued on the engine stream
+    auto run = [&]() -> int {
+        HIPCHK(e, hipEventRecord(G.go, st));
+        HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
+        if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
+        for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
+            if (int r = prep(k)) return r;
+        int rejected = 0;
+        for (uint32_t k = 0; k < K; k++) {
+            const size_t lo = lo_of(k);
+            const IngestBatch I = chunk_batch(k);
+            HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
+            const auto tc = clk::now();
+            const int r = ingest_chunk(e, I, ev + lo, arena);
+            if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
+                                  ms_between(t0, tc), ms_between(t0, clk::now()));
+            if (r < 0) return r;
+            rejected += r;
+            // the chunk's per-record results -> the caller's arrays, on the results
+            // stream (ingest_chunk's last summary read released them for the host)
+            HIPCHK(e, hipEventRecord(G.used[k & 1], st));
+            hipStream_t rs = K > 1 ? G.dst : st;
+            if (K > 1) HIPCHK(e, hipStreamWaitEvent(rs, G.used[k & 1], 0));
+            if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+            if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+            if (out_released)
+                HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+            if (k + 2 < K)
+                if (int r2 = prep(k + 2)) return r2;
+        }
+        HIPCHK(e, hipStreamSynchronize(st));
+        if (K > 1) HIPCHK(e, hipStreamSynchronize(G.dst));
+        return rejected;
+    };
+    rc = run();
+    // nothing of this batch stays queued on the prep / results streams (a failed chunk included)
+    if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
+    if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
+    if (e->iprof)
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s): %.2f ms\n", n, zev ? ", read in place" : "", K,
+                K == 1 ? "" : "s", ms_between(t0, clk::now()));
+    return rc;
 }
 
 int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {

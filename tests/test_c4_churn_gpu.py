@@ -21,7 +21,7 @@ from oracle.oracle import Oracle
 pytestmark = pytest.mark.gpu
 
 
-def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True):
+def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None):
     if threads is not None:
         os.environ["KWOK_INGEST_THREADS"] = str(threads)
     try:
@@ -35,7 +35,8 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
     e.tick(now, read=False)
     o.tick(now, read=False)
     compare_tick(e, o, "churn initial tick")
-    ch = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11)
+    ch = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11,
+                        alloc=alloc)
     dump = lambda: o.dump_pods(0, n_handles)  # noqa: E731
     for t in range(ticks):
         now += 30

@@ -1,0 +1,40 @@
+"""GPU parity of chunked pod ingest.  kwok_ingest_pods runs a batch of more than
+KWOK_INGEST_CHUNK records (default 1048576) in chunks: the copy engine moves chunk
+k+1's records to HBM and k_ing_prep prepares them on a second stream while chunk
+k is applied, and chunk k's results go back on a third (engine.cpp ingest_chunk).  Applying the chunks one after the other
+must equal applying the batch at once, since every record is applied in event
+order (pod_controller.go:301-343).  Tiny chunks put chunk boundaries everywhere:
+between by-name creates and the deletes that free their node entries (REC_HARD),
+inside growth batches, and across the churn generator's deletes and creates,
+for page-locked and pageable batches."""
+import pytest
+
+import harness
+from kwok_amd.engine import Engine, host_array
+from test_c4_churn_gpu import run_churn
+import test_growth_gpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("chunk", ["1", "3"])
+@pytest.mark.parametrize("name", harness.TRACES)
+def test_golden_trace_chunked(name, chunk, monkeypatch):
+    monkeypatch.setenv("KWOK_INGEST_CHUNK", chunk)
+    fx = harness.load_trace(name)
+    e = Engine(harness.config_for(fx))
+    harness.replay(fx, e)
+    e.close()
+
+
+def test_growth_chunked(monkeypatch):
+    monkeypatch.setenv("KWOK_INGEST_CHUNK", "97")
+    test_growth_gpu.test_1000_pods_on_one_node_grow(None, monkeypatch)
+
+
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
+def test_churn_chunked(pinned, monkeypatch):
+    """20k nodes x 200k pods, 40k deletes + 40k creates per tick in chunks of
+    ~7001: batches in page-locked memory (DMA) and in pageable memory (staged)"""
+    monkeypatch.setenv("KWOK_INGEST_CHUNK", "7001")
+    run_churn(20_000, 40_000, 3, alloc=host_array if pinned else None)
