@@ -2335,7 +2335,16 @@ constexpr int EMIT_BLOCK = 256;
 #define EMIT_TAB_UNR 5  // table path: units per lane per step (G * UNR = 40: a default pod patch)
 #endif
 static_assert(EMIT_BLOCK == BLOCK, "build_hb_template strides by BLOCK");
-constexpr int EC_PROG = 4096, EC_NXT = 1152, EC_BLOB = 2048;
+#ifndef EMIT_EC_PROG
+#define EMIT_EC_PROG 4096  // spec programs cached in LDS (bytes)
+#endif
+#ifndef EMIT_EC_NXT
+#define EMIT_EC_NXT 1152   // their timestamp lookups (entries)
+#endif
+#ifndef EMIT_EC_BLOB
+#define EMIT_EC_BLOB 2048  // node blobs (bytes)
+#endif
+constexpr int EC_PROG = EMIT_EC_PROG, EC_NXT = EMIT_EC_NXT, EC_BLOB = EMIT_EC_BLOB;
 constexpr uint32_t SEG_STRIDE = 56;  // per job: "hostIP":"H", (28 bytes) | "podIP":"P", (28 bytes)
 constexpr uint32_t TS_STRIDE = 36;   // per job: its 20-byte timestamp, then 16 zero bytes
 constexpr uint32_t TS_FIRST = 16;    // 16 zero bytes before job 0's timestamp
