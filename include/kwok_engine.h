@@ -279,7 +279,10 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
                       size_t arena_len, int32_t* out_handles, int32_t* out_status);
 /* out_released (optional) receives, per DELETE record, the IPv4 address released
  * into the pool (0 if none); sharded callers replicate these to the other ranks
- * with kwok_pool_put before the next tick. */
+ * with kwok_pool_put before the next tick.  A pod batch of more than
+ * KWOK_INGEST_CHUNK records (environment, default 1048576) is applied in chunks
+ * of consecutive records; a negative return after a chunk was applied poisons
+ * the engine (the batch is partly in the state: every later call fails). */
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena,
                      size_t arena_len, int32_t* out_handles, int32_t* out_status,
                      uint32_t* out_released);

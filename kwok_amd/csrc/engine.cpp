@@ -338,6 +338,7 @@ struct kwok_engine {
     bool poisoned = false;
     bool iprof = false;
     WorkPool workers;  // host threads of the ingest partitions  // KWOK_INGEST_PROF=1: host ingest / retire phase times on stderr
+    uint32_t debug_fail_chunk = 0;  // KWOK_DEBUG_INGEST_FAIL_CHUNK=N: chunk N of a pod batch fails before its apply (tests)
     uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
     int fail(int code, const char* fmt, ...) {
@@ -1342,6 +1343,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_STREAM_SHARE")) e->share_env = std::min(1024, std::max(0, atoi(v)));
         if (const char* v = getenv("KWOK_HB_NT")) e->nt_env = atoi(v) != 0;
         if (const char* v = getenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")) e->debug_fault_tick = strtoull(v, nullptr, 10);
+        if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_CHUNK")) e->debug_fail_chunk = (uint32_t)strtoul(v, nullptr, 10);
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
@@ -1962,6 +1964,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         HIPCHK(e, hipEventRecord(G.prepped[k & 1], ps));
         return KWOK_OK;
     };
+    bool applied = false;  // a chunk of the batch is in the state
     // the prep stream starts after the work already queued on the engine stream
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
@@ -1975,10 +1978,12 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const IngestBatch I = chunk_batch(k);
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
             const auto tc = clk::now();
+            if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
             const int r = ingest_chunk(e, I, ev + lo, arena);
             if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
                                   ms_between(t0, tc), ms_between(t0, clk::now()));
             if (r < 0) return r;
+            applied = true;
             rejected += r;
             // the chunk's per-record results -> the caller's arrays, on the results
             // stream (ingest_chunk's last summary read released them for the host)
@@ -1997,6 +2002,8 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         return rejected;
     };
     rc = run();
+    // a batch that fails after a chunk was applied is partly in the state: every later call fails
+    if (rc < 0 && applied) e->poisoned = true;
     // nothing of this batch stays queued on the prep / results streams (a failed chunk included)
     if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
     if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");

@@ -38,3 +38,33 @@ def test_churn_chunked(pinned, monkeypatch):
     ~7001: batches in page-locked memory (DMA) and in pageable memory (staged)"""
     monkeypatch.setenv("KWOK_INGEST_CHUNK", "7001")
     run_churn(20_000, 40_000, 3, alloc=host_array if pinned else None)
+
+
+def test_failed_chunk_after_an_applied_one_poisons(monkeypatch):
+    """A pod batch that fails after one of its chunks was applied is partly in
+    the state: the engine is poisoned (every later call fails; destroy /
+    recreate is the recovery).  A failure in the first chunk leaves the state
+    as a one-chunk batch failing there would (kwok_engine.h)."""
+    from kwok_amd import abi
+    from kwok_amd.engine import KwokError
+    fx = harness.load_trace("churn")
+    t = fx["ticks"]
+    for fail_chunk, poisoned in ((2, True), (1, False)):
+        monkeypatch.setenv("KWOK_INGEST_CHUNK", "3")
+        monkeypatch.setenv("KWOK_DEBUG_INGEST_FAIL_CHUNK", str(fail_chunk))
+        e = Engine(harness.config_for(fx))
+        monkeypatch.delenv("KWOK_DEBUG_INGEST_FAIL_CHUNK")
+        specs = harness.SpecCache(e)
+        e.ingest_nodes_raw(*harness.node_batch(t[0]["node_events"]))
+        recs, ar = harness.pod_batch(t[0]["pod_events"], specs)
+        assert len(recs) > 6
+        with pytest.raises(KwokError) as ex:
+            e.ingest_pods_raw(recs, ar)
+        assert ex.value.code == abi.EDEVICE
+        if poisoned:
+            with pytest.raises(KwokError) as ex:
+                e.tick(t[0]["now"])
+            assert ex.value.code == abi.EDEVICE and "recreate" in str(ex.value)
+        else:
+            e.tick(t[0]["now"])  # nothing of the batch applied; the engine goes on
+        e.close()
