@@ -72,7 +72,7 @@ NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only
 #   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
 INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
-PMC_FILE = "r3x_pmc.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
+PMC_FILE = "r3ai_pmc.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
 
 
 def parse():
