@@ -775,6 +775,27 @@ void free_node(kwok_engine* e, uint32_t slot, bool dev_cleared) {
 }
 
 // find (or create a placeholder for) the node entry of `name`
+// Software prefetch of a name lookup (node_slot), in two stages a few records
+// apart: stage 0 the name-table line, stage 1 (the table line now cached) the
+// node entry it points to.  A batch's lookups are two dependent cache misses
+// each over tables of ~1M nodes; issued ahead, they overlap.
+void name_prefetch(const kwok_engine* e, const char* name, size_t len, int stage) {
+    const uint32_t h = fnv1a32(name, len), b = h & (e->B - 1);
+    if (!e->owns(b)) return;
+    const uint32_t bl = b - e->b_lo, mask = e->name_mask;
+    const uint32_t* tab = e->name_tab.data() + (size_t)bl * (mask + 1);
+    const uint32_t i = name_home(h, mask);
+    if (stage == 0) {
+        __builtin_prefetch(tab + i);
+        return;
+    }
+    if (const uint32_t t = tab[i]) {
+        const char* hn = reinterpret_cast<const char*>(&e->nodes[(size_t)bl * e->Cn + t - 1]);
+        __builtin_prefetch(hn);
+        __builtin_prefetch(hn + sizeof(kwok_engine::HNode) - 1);
+    }
+}
+
 int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_t* out) {
     const uint32_t h = fnv1a32(name, len), b = h & (e->B - 1);
     if (!e->owns(b)) return KWOK_ENOTMINE;
@@ -1734,6 +1755,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         const uint32_t b = fnv1a32(arena + x.name.off, x.name.len) & (e->B - 1);
         return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
     };
+    static const size_t PF_DIST = getenv("KWOK_NODE_PF") ? strtoull(getenv("KWOK_NODE_PF"), nullptr, 10) : 16;
     static const size_t par_min = getenv("KWOK_NODE_PAR_MIN") ? strtoull(getenv("KWOK_NODE_PAR_MIN"), nullptr, 10)
                                                              : NODE_PAR_MIN;
     const bool threaded = n >= par_min && e->n_part > 1;
@@ -1747,7 +1769,14 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         // node batch)
         auto pass1 = [&](int c) {
             const size_t lo = threaded ? n * (size_t)c / (size_t)P : 0, hi = threaded ? n * (size_t)(c + 1) / (size_t)P : n;
+            auto pf = [&](size_t j, int stage) {
+                const kwok_node_event& y = ev[j];
+                if (y.op == KWOK_OP_DELETE && y.name.len && y.name.len <= 253 && in_arena(y.name))
+                    name_prefetch(e, arena + y.name.off, y.name.len, stage);
+            };
             for (size_t i = lo; i < hi; i++) {
+                if (i + PF_DIST < hi) pf(i + PF_DIST, 0);
+                if (i + PF_DIST / 2 < hi) pf(i + PF_DIST / 2, 1);
                 const int64_t bl = bucket_of_record(ev[i]);
                 if (threaded) part[i] = (uint8_t)(bl < 0 ? 0 : (uint64_t)bl * (uint64_t)P / e->nb);
                 uint32_t slot = 0;
@@ -1778,8 +1807,25 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         threaded_results = true;
         run_parts(e, true, [&](int p) {
             PartAcc& a = acc[(size_t)p];
+            // the partition's next records' lookups prefetched (two stages, as pass 1)
+            size_t q0 = 0, q1 = 0;  // the scan positions of stage 0 / stage 1
+            int ahead0 = 0, ahead1 = 0;  // this partition's records each stage is ahead by
+            auto advance = [&](size_t& q, int& ahead, int want, int stage) {
+                for (; ahead < want && q < n; q++)
+                    if (part[q] == (uint8_t)p) {
+                        const kwok_node_event& y = ev[q];
+                        if (y.name.len && y.name.len <= 253 && in_arena(y.name))
+                            name_prefetch(e, arena + y.name.off, y.name.len, stage);
+                        ahead++;
+                    }
+            };
             for (size_t i = 0; i < n; i++)
-                if (part[i] == (uint8_t)p) a.rej += ingest_one(i, p);
+                if (part[i] == (uint8_t)p) {
+                    advance(q0, ahead0, PF_DIST, 0);
+                    advance(q1, ahead1, PF_DIST / 2, 1);
+                    a.rej += ingest_one(i, p);
+                    ahead0--, ahead1--;
+                }
         });
         for (const PartAcc& a : acc)
             for (const auto& r : a.results) {
