@@ -774,7 +774,6 @@ void free_node(kwok_engine* e, uint32_t slot, bool dev_cleared) {
     if (!dev_cleared) node_op(e, slot, 0, 0, true, 0);
 }
 
-// find (or create a placeholder for) the node entry of `name`
 // Software prefetch of a name lookup (node_slot), in two stages a few records
 // apart: stage 0 the name-table line, stage 1 (the table line now cached) the
 // node entry it points to.  A batch's lookups are two dependent cache misses
@@ -790,12 +789,19 @@ void name_prefetch(const kwok_engine* e, const char* name, size_t len, int stage
         return;
     }
     if (const uint32_t t = tab[i]) {
-        const char* hn = reinterpret_cast<const char*>(&e->nodes[(size_t)bl * e->Cn + t - 1]);
+        const size_t slot = (size_t)bl * e->Cn + t - 1;
+        const char* hn = reinterpret_cast<const char*>(&e->nodes[slot]);
         __builtin_prefetch(hn);
         __builtin_prefetch(hn + sizeof(kwok_engine::HNode) - 1);
+        // what applying the record touches next: its staged-op index (node_op) and,
+        // for a delete, the references the batch counted (ingest_one)
+        __builtin_prefetch(&e->node_stamp[slot]);
+        __builtin_prefetch(&e->node_opi[slot]);
+        if (slot < e->slot_refs.size()) __builtin_prefetch(&e->slot_refs[slot]);
     }
 }
 
+// find (or create a placeholder for) the node entry of `name`
 int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_t* out) {
     const uint32_t h = fnv1a32(name, len), b = h & (e->B - 1);
     if (!e->owns(b)) return KWOK_ENOTMINE;
