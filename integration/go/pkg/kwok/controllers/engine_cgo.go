@@ -51,9 +51,10 @@ type gpuEngine struct {
 	hb      []int32 // heartbeat handle list of heartbeat epoch hbEpoch
 	hbEpoch uint32
 	// page-locked batch buffers (kwok_host_alloc), reused: kwok_ingest_pods reads
-	// the records and strings in place from these (no copy), and writes the
-	// per-record results to resBuf (a copy into pageable Go memory would stall the
-	// engine's next transfers, DESIGN.md §11)
+	// the records and strings in place from these (batches over KWOK_INGEST_CHUNK
+	// records: copied by DMA, chunk by chunk), and writes the per-record results to
+	// resBuf (a copy into pageable Go memory would stall the engine's next
+	// transfers, DESIGN.md §11)
 	evBuf, arBuf, resBuf hostBuf
 }
 
