@@ -209,7 +209,8 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         "exchange_ms": xch / ticks if (world > 1 or os.environ.get("KWOK_FORCE_MULTI")) else None,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods: H2D of the records and their strings (page-locked batch buffers, "
-                "kwok_host_alloc), the GPU event switch (prep, stable sort by bucket, per-bucket apply), D2H of the "
+                "kwok_host_alloc; batches over KWOK_INGEST_CHUNK records in chunks, each copied while the previous "
+                "one is applied), the GPU event switch (prep, stable sort by bucket, per-bucket apply), D2H of the "
                 "per-record handles / statuses / releases; event generation between steps untimed (the GPU idles "
                 "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
 
