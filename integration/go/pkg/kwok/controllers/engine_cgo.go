@@ -63,15 +63,20 @@ type hostBuf struct {
 	n int
 }
 
-func (b *hostBuf) get(n int) unsafe.Pointer {
+func (b *hostBuf) get(n int) (unsafe.Pointer, error) {
 	if n > b.n || b.p == nil {
 		if b.p != nil {
 			C.kwok_host_free(b.p)
+			b.p, b.n = nil, 0
 		}
-		b.n = n + n/4 + 64
-		b.p = C.kwok_host_alloc(C.size_t(b.n))
+		want := n + n/4 + 64
+		p := C.kwok_host_alloc(C.size_t(want))
+		if p == nil {
+			return nil, fmt.Errorf("kwok_host_alloc(%d): out of page-locked memory", want)
+		}
+		b.p, b.n = p, want
 	}
-	return b.p
+	return b.p, nil
 }
 
 func (b *hostBuf) free() {
@@ -117,6 +122,9 @@ func newGPUEngine(conf Config, startUnix int64, rank, world int, commID []byte) 
 		pod_status_template:     podTpl,
 		node_init_template:      nodeTpl,
 		node_heartbeat_template: hbTpl,
+		// every heartbeat patch of a tick is the same body (node_controller.go:393-401): the
+		// tick materialises ONE, tick() reads it once and sends it to every managed node
+		flags:                   C.KWOK_CFG_HEARTBEAT_ONCE,
 		buckets:                 4096,
 		node_slots_per_bucket:   64,
 		pod_slots_per_bucket:    640,   // initial capacity; a bucket grows when a batch would fill it ...
@@ -208,12 +216,20 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 	if len(evs) == 0 {
 		return
 	}
-	ev := unsafe.Slice((*C.kwok_pod_event)(g.evBuf.get(len(evs)*int(unsafe.Sizeof(evs[0])))), len(evs))
+	evp, err := g.evBuf.get(len(evs) * int(unsafe.Sizeof(evs[0])))
+	if err != nil {
+		return
+	}
+	ev := unsafe.Slice((*C.kwok_pod_event)(evp), len(evs))
 	need := 0
 	for i := range evs {
 		need += int(evs[i].node_name.len + evs[i].host_ip.len + evs[i].pod_ip.len)
 	}
-	ar := unsafe.Slice((*byte)(g.arBuf.get(need+1)), need+1)
+	arp, err := g.arBuf.get(need + 1)
+	if err != nil {
+		return
+	}
+	ar := unsafe.Slice((*byte)(arp), need+1)
 	off := 0
 	pack := func(s C.kwok_str) C.kwok_str {
 		n := copy(ar[off:], arena[s.off:s.off+s.len])
@@ -226,7 +242,11 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 		ev[i].node_name, ev[i].host_ip, ev[i].pod_ip = pack(evs[i].node_name), pack(evs[i].host_ip), pack(evs[i].pod_ip)
 	}
 	n := len(ev)
-	res := unsafe.Slice((*int32)(g.resBuf.get(3*4*n)), 3*n)
+	resp, err := g.resBuf.get(3 * 4 * n)
+	if err != nil {
+		return
+	}
+	res := unsafe.Slice((*int32)(resp), 3*n)
 	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(n), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
 		(*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]), (*C.uint32_t)(unsafe.Pointer(&res[2*n])))
 	if rc < 0 {
@@ -260,7 +280,9 @@ func finalizerPatch() []byte {
 
 // tick runs one heartbeat interval and hands every body to apply.  The lists
 // come first (kwok_read_outputs without an arena); then ONE heartbeat body (all
-// bodies of a tick are identical, node_controller.go:393-401) and the node-init
+// bodies of a tick are identical, node_controller.go:393-401; the engine is
+// created with KWOK_CFG_HEARTBEAT_ONCE, so the tick wrote only that one, at
+// heartbeat_off, and moved the SoA state, not 1M copies) and the node-init
 // / pod patches in bounded pieces (kwok_read_arena, 64-bit offsets), each copied
 // once, straight into Go memory (the engine keeps no pointer past the call).  A
 // steady tick at 1M nodes moves ~1 KB over PCIe, not 1 GB.  The heartbeat handle

@@ -1,9 +1,12 @@
 //go:build kwok_mi355x
 
 // gpu_controller.go - the client-go side of the drop-in: watch events are
-// batched as object JSON, decoded by the engine's host codec and ingested
-// before each tick; every body the tick returns is applied through the
-// clientset with the reference's 16-wide task pools (utils.go:119-161).
+// batched, encoded as object JSON, decoded by the engine's host codec and
+// ingested before each tick; every body the tick returns is applied through the
+// clientset with the reference's 16-wide task pools (utils.go:119-161).  The
+// watch echoes of the engine's own patches are dropped by resourceVersion
+// (echoes).  kwok_amd/controller.py is the same controller in Python, which
+// the tests run against a fake clientset (tests/test_controller*.py).
 // NewController builds this in place of NodeController + PodController when
 // the package is built with -tags kwok_mi355x (controller_mi355x.go).
 //
@@ -36,7 +39,17 @@ import (
 	"sigs.k8s.io/kwok/pkg/log"
 )
 
-// objBatch: watch objects since the last tick, as concatenated JSON
+// watchObj: one watch event since the last tick.  The object is encoded to
+// JSON only at the next tick, after the echoes of the engine's own patches are
+// dropped (echoes).
+type watchObj struct {
+	obj     interface{}
+	uid     types.UID
+	rv      string // metadata.resourceVersion
+	deleted bool
+}
+
+// objBatch: the watch objects of one tick as concatenated JSON (the codec's input)
 type objBatch struct {
 	arena []byte
 	offs  []uint64
@@ -45,17 +58,92 @@ type objBatch struct {
 	uids  []types.UID
 }
 
-func (b *objBatch) add(obj interface{}, uid types.UID, deleted bool) error {
-	raw, err := json.Marshal(obj)
+func (b *objBatch) add(w watchObj) error {
+	raw, err := json.Marshal(w.obj)
 	if err != nil {
 		return err
 	}
 	b.offs = append(b.offs, uint64(len(b.arena)))
 	b.lens = append(b.lens, uint32(len(raw)))
 	b.arena = append(b.arena, raw...)
-	b.del = append(b.del, deleted)
-	b.uids = append(b.uids, uid)
+	b.del = append(b.del, w.deleted)
+	b.uids = append(b.uids, w.uid)
 	return nil
+}
+
+// echoes: the resourceVersions the engine's own patches returned, per object.
+// Their Modified watch events (the echoes) are states the engine already
+// assumed when it emitted the patches (DESIGN.md §1: patches are assumed
+// applied; a heartbeat's echo re-lock, node_controller.go:152 -> :256-263, is
+// part of every tick), so echoes are dropped instead of re-ingested.  An object
+// can take several patches in one tick (a node's heartbeat and its init patch,
+// a pod's finalizer patch), each with its own echo: every returned version is
+// kept until its echo is seen (the last echoKeep per object, so echoes lost to a
+// watch restart do not pile up).  Any other event of the object is ingested.
+type echoes struct {
+	mu sync.Mutex
+	rv map[types.UID][]string
+}
+
+const echoKeep = 8
+
+func (x *echoes) note(uid types.UID, rv string) {
+	if uid == "" || rv == "" {
+		return
+	}
+	x.mu.Lock()
+	v := append(x.rv[uid], rv)
+	if len(v) > echoKeep {
+		v = v[1:]
+	}
+	x.rv[uid] = v
+	x.mu.Unlock()
+}
+
+// is: the event is the echo of one of the engine's patches of the object (each
+// echo is consumed: a second event with that resourceVersion is not expected)
+func (x *echoes) is(uid types.UID, rv string) bool {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	v := x.rv[uid]
+	for i, r := range v {
+		if r == rv {
+			v = append(v[:i], v[i+1:]...)
+			if len(v) == 0 {
+				delete(x.rv, uid)
+			} else {
+				x.rv[uid] = v
+			}
+			return true
+		}
+	}
+	return false
+}
+
+func (x *echoes) forget(uid types.UID) {
+	x.mu.Lock()
+	delete(x.rv, uid)
+	x.mu.Unlock()
+}
+
+// encode drops the echoes among ws (those whose patch returned after the watch
+// event arrived: onEvent could not match them yet) and encodes the rest
+func (x *echoes) encode(ws []watchObj) (objBatch, int, error) {
+	var b objBatch
+	dropped := 0
+	seen := map[types.UID]struct{}{} // (the rule of onEvent: only before any kept event of the object)
+	for _, w := range ws {
+		_, after := seen[w.uid]
+		if !w.deleted && x.is(w.uid, w.rv) && !after {
+			dropped++
+			continue
+		}
+		seen[w.uid] = struct{}{}
+		if err := b.add(w); err != nil {
+			return b, dropped, err
+		}
+	}
+	return b, dropped, nil
 }
 
 // GPUController: one engine (one GPU) behind the reference's Controller API.
@@ -67,8 +155,10 @@ type GPUController struct {
 	finalizer []byte
 
 	mu    sync.Mutex // guards the batches (watch goroutines append, the tick loop swaps)
-	nodes objBatch
-	pods  objBatch
+	nodes  []watchObj
+	pods   []watchObj
+	queued map[types.UID]struct{} // objects with an event in the batches
+	echo   echoes
 
 	// tick loop only
 	nodeName   map[int32]string // node handle -> name
@@ -97,6 +187,8 @@ func newGPUController(conf Config, interval time.Duration) (*GPUController, erro
 		nodeName: map[int32]string{}, nodeHandle: map[string]int32{}, podByUID: map[types.UID]int32{},
 		podUID: map[int32]types.UID{},
 		podRef: map[int32]types.NamespacedName{},
+		echo:   echoes{rv: map[types.UID][]string{}},
+		queued: map[types.UID]struct{}{},
 	}, nil
 }
 
@@ -165,21 +257,36 @@ func (c *GPUController) onEvent(ctx context.Context, nodes bool, ev watch.Event)
 	if ev.Type != watch.Added && ev.Type != watch.Modified && ev.Type != watch.Deleted {
 		return
 	}
-	var err error
-	c.mu.Lock()
+	var w watchObj
 	switch obj := ev.Object.(type) {
 	case *corev1.Node:
-		if nodes {
-			err = c.nodes.add(obj, obj.UID, ev.Type == watch.Deleted)
-		}
-	case *corev1.Pod:
 		if !nodes {
-			err = c.pods.add(obj, obj.UID, ev.Type == watch.Deleted)
+			return
 		}
+		w = watchObj{obj, obj.UID, obj.ResourceVersion, ev.Type == watch.Deleted}
+	case *corev1.Pod:
+		if nodes {
+			return
+		}
+		w = watchObj{obj, obj.UID, obj.ResourceVersion, ev.Type == watch.Deleted}
+	default:
+		return
 	}
-	c.mu.Unlock()
-	if err != nil {
-		log.FromContext(ctx).Error("Failed to encode watch object", err)
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	// the echo of one of the engine's own patches (its apply already returned):
+	// not queued, not encoded - unless another event of the object waits in this
+	// tick's batch: that one is a change the engine has not seen, older than the
+	// patch, and the echo is the object's newest state, carrying both
+	_, waiting := c.queued[w.uid]
+	if ev.Type == watch.Modified && c.echo.is(w.uid, w.rv) && !waiting {
+		return
+	}
+	c.queued[w.uid] = struct{}{}
+	if nodes {
+		c.nodes = append(c.nodes, w)
+	} else {
+		c.pods = append(c.pods, w)
 	}
 }
 
@@ -220,9 +327,19 @@ func (c *GPUController) Size() int               { return c.eng.nodeSize() }
 // body to the task pool
 func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int64) (int, error) {
 	c.mu.Lock()
-	nb, pb := c.nodes, c.pods
-	c.nodes, c.pods = objBatch{}, objBatch{}
+	nw, pw := c.nodes, c.pods
+	c.nodes, c.pods, c.queued = nil, nil, map[types.UID]struct{}{}
 	c.mu.Unlock()
+	// every apply of the previous tick has returned (loop waits for the task pool):
+	// the echoes that overtook their patch's response are dropped here
+	nb, _, err := c.echo.encode(nw)
+	if err != nil {
+		return 0, err
+	}
+	pb, _, err := c.echo.encode(pw)
+	if err != nil {
+		return 0, err
+	}
 	if err := c.flushNodes(ctx, nb); err != nil {
 		return 0, err
 	}
@@ -238,24 +355,31 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 	nodesAPI := c.conf.ClientSet.CoreV1().Nodes()
 	var gone []int32
 	n := 0
-	err := c.eng.tick(now, func(kind int, h int32, body []byte) {
+	err = c.eng.tick(now, func(kind int, h int32, body []byte) {
 		n++
 		switch kind {
 		case kindHeartbeat, kindNodeInit: // configureHeartbeatNode / configureNode bodies
 			name := c.nodeName[h]
 			tasks.Add(func() {
-				if _, err := nodesAPI.PatchStatus(ctx, name, body); err != nil {
+				n, err := nodesAPI.PatchStatus(ctx, name, body)
+				if err != nil {
 					logger.Error("Failed to patch node status", err, "node", name)
+					return
 				}
+				c.echo.note(n.UID, n.ResourceVersion)
 			})
 		case kindPodPatch: // LockPod (pod_controller.go:205-231)
 			ref := c.podRef[h]
 			tasks.Add(func() {
-				_, err := c.conf.ClientSet.CoreV1().Pods(ref.Namespace).Patch(ctx, ref.Name,
+				p, err := c.conf.ClientSet.CoreV1().Pods(ref.Namespace).Patch(ctx, ref.Name,
 					types.StrategicMergePatchType, body, metav1.PatchOptions{}, "status")
-				if err != nil && !apierrors.IsNotFound(err) {
-					logger.Error("Failed to lock pod", err, "pod", ref.String())
+				if err != nil {
+					if !apierrors.IsNotFound(err) {
+						logger.Error("Failed to lock pod", err, "pod", ref.String())
+					}
+					return
 				}
+				c.echo.note(p.UID, p.ResourceVersion)
 			})
 		case kindDelete, kindDeleteFin: // DeletePod (pod_controller.go:155-183); the engine freed the handle
 			ref, fin := c.podRef[h], kind == kindDeleteFin
@@ -263,12 +387,16 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 			tasks.Add(func() {
 				pods := c.conf.ClientSet.CoreV1().Pods(ref.Namespace)
 				if fin { // only pods with finalizers (len(pod.Finalizers) != 0, :161)
-					if _, err := pods.Patch(ctx, ref.Name, types.MergePatchType, c.finalizer, metav1.PatchOptions{}); err != nil {
+					p, err := pods.Patch(ctx, ref.Name, types.MergePatchType, c.finalizer, metav1.PatchOptions{})
+					if err != nil {
 						if !apierrors.IsNotFound(err) {
 							logger.Error("Failed to patch pod finalizers", err, "pod", ref.String())
 						}
 						return
 					}
+					// its echo (deletionTimestamp, no finalizers) would re-enter DeletePod
+					// for a pod the engine already deleted
+					c.echo.note(p.UID, p.ResourceVersion)
 				}
 				if err := pods.Delete(ctx, ref.Name, deleteOpt); err != nil && !apierrors.IsNotFound(err) {
 					logger.Error("Failed to delete pod", err, "pod", ref.String())
@@ -277,6 +405,7 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 		}
 	})
 	for _, h := range gone { // the later Deleted watch event finds no handle (CNI: it still runs cni.Remove)
+		c.echo.forget(c.podUID[h])
 		delete(c.podByUID, c.podUID[h])
 		delete(c.podUID, h)
 		delete(c.podRef, h)

@@ -51,8 +51,8 @@ constexpr int SPEC_GROUPS = 2;            // pod groups per thread loaded before
 constexpr int WC_GROUPS = 64;
 constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block
 constexpr int WC_DIRTY_WORDS = MAX_WC / 32;
-constexpr int TRACE_SLOTS = 16;
-constexpr int SPEC_LDS = 256;           // k_tick caches the reservations of up to this many specs           // KWOK_TICK_TRACE=1: per-block phase stamps
+constexpr int TRACE_SLOTS = 16;         // KWOK_TICK_TRACE=1: per-block phase stamps
+constexpr int SPEC_LDS = 256;           // k_tick caches the reservations of up to this many specs
 
 // ---- fixed template geometry (default templates) -----------------------------
 constexpr int HB_LEN = 1059;     // {"status":{"conditions":[5 conditions]}} with 20-byte T/S

@@ -339,6 +339,12 @@ struct kwok_engine {
     bool iprof = false;
     WorkPool workers;  // host threads of the ingest partitions  // KWOK_INGEST_PROF=1: host ingest / retire phase times on stderr
     uint32_t debug_fail_chunk = 0;  // KWOK_DEBUG_INGEST_FAIL_CHUNK=N: chunk N of a pod batch fails before its apply (tests)
+    uint32_t debug_fail_apply = 0;  // KWOK_DEBUG_INGEST_FAIL_APPLY=N: chunk N fails after its first apply pass (tests)
+    // the pod batch in progress changed the state (placeholder nodes, capacity, the
+    // apply pass): a failure from then on leaves the batch partly applied (poison)
+    bool ing_mutated = false;
+    bool zombie_check = false;  // a retired tick deleted pods: free_zombies when the queue drains
+    uint32_t ing_chunk = 0;     // the chunk ingest_chunk works on (debug injection)
     uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
     int fail(int code, const char* fmt, ...) {
@@ -1371,6 +1377,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_HB_NT")) e->nt_env = atoi(v) != 0;
         if (const char* v = getenv("KWOK_DEBUG_LAYOUT_FAULT_TICK")) e->debug_fault_tick = strtoull(v, nullptr, 10);
         if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_CHUNK")) e->debug_fail_chunk = (uint32_t)strtoul(v, nullptr, 10);
+        if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_APPLY")) e->debug_fail_apply = (uint32_t)strtoul(v, nullptr, 10);
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
@@ -1880,6 +1887,7 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
     if (sum.need > e->Cp) {
         const uint32_t cap = max_pod_capacity(e);
         if (cap > e->Cp) {
+            e->ing_mutated = true;  // (a failed growth leaves the layout half changed)
             const uint32_t want = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(((uint64_t)sum.need + 7) & ~7ull, 2ull * e->Cp));
             if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
             if ((rc = grow_pods(e, want))) return rc;
@@ -1889,6 +1897,7 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
     // by-name creates (spec.nodeName): resolved on the host, in event order
     std::vector<uint32_t> fix;
     if (sum.n_byname) {
+        e->ing_mutated = true;  // placeholder node entries from here on
         std::vector<uint32_t> idx(sum.n_byname), dels(e->nb);
         HIPCHK(e, hipMemcpyAsync(idx.data(), I.byname, idx.size() * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipMemcpyAsync(dels.data(), I.dels, dels.size() * 4, hipMemcpyDeviceToHost, st));
@@ -1924,9 +1933,12 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
     if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
         return e->fail(KWOK_EDEVICE, "ingest sort");
     for (;;) {
+        e->ing_mutated = true;  // pod slots, node references and the pool change from here on
         launch_ingest_apply(e->S, I, st);
         HIPCHK(e, hipGetLastError());
         if ((rc = read_summary(e, I.sum))) return rc;
+        if (e->debug_fail_apply == e->ing_chunk + 1)
+            return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", e->ing_chunk);
         if ((rc = free_device_freed(e))) return rc;  // node entries the pass freed
         if (G.sum_h->foreign) e->foreign_ips = true;
         if (!G.sum_h->n_stopped) break;
@@ -2016,7 +2028,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         HIPCHK(e, hipEventRecord(G.prepped[k & 1], ps));
         return KWOK_OK;
     };
-    bool applied = false;  // a chunk of the batch is in the state
+    e->ing_mutated = false;  // set by ingest_chunk once the batch changes any state
     // the prep stream starts after the work already queued on the engine stream
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
@@ -2031,11 +2043,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
             const auto tc = clk::now();
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
+            e->ing_chunk = k;
             const int r = ingest_chunk(e, I, ev + lo, arena);
             if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
                                   ms_between(t0, tc), ms_between(t0, clk::now()));
             if (r < 0) return r;
-            applied = true;
             rejected += r;
             // the chunk's per-record results -> the caller's arrays, on the results
             // stream (ingest_chunk's last summary read released them for the host)
@@ -2054,8 +2066,10 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         return rejected;
     };
     rc = run();
-    // a batch that fails after a chunk was applied is partly in the state: every later call fails
-    if (rc < 0 && applied) e->poisoned = true;
+    // a batch that fails once it changed the state (a chunk applied, or the failing
+    // chunk's own apply pass, placeholders or growth) is partly in the state: every
+    // later call fails
+    if (rc < 0 && e->ing_mutated) e->poisoned = true;
     // nothing of this batch stays queued on the prep / results streams (a failed chunk included)
     if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
     if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
@@ -2479,8 +2493,15 @@ int retire(kwok_engine* e) {
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));
-    if (H.n_del)  // deleted nodes whose last pod this tick deleted
+    // deleted nodes whose last pod this tick deleted: freed once no tick is queued
+    // behind this one (node_refs synchronises the engine stream, which would wait
+    // for that tick too); every ingest drains the queue first, so the slots are
+    // free again before any record could take them
+    if (H.n_del) e->zombie_check = true;
+    if (e->zombie_check && next < 0) {
+        e->zombie_check = false;
         if (int rc = free_zombies(e)) return failed(rc);
+    }
     // the slot-freeing ops of deleted nodes without pods: no tick reads such a
     // node, so with a tick already queued they wait for the next flush
     if (node_ops_pending(e) && next < 0) {

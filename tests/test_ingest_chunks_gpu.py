@@ -68,3 +68,29 @@ def test_failed_chunk_after_an_applied_one_poisons(monkeypatch):
         else:
             e.tick(t[0]["now"])  # nothing of the batch applied; the engine goes on
         e.close()
+
+
+@pytest.mark.parametrize("chunk", ["3", "1000000"], ids=["chunked", "one-chunk"])
+def test_failure_after_an_apply_pass_poisons(chunk, monkeypatch):
+    """A batch that fails after its (first) chunk's apply pass ran is partly in
+    the state - pod slots, node references and the pool changed - even when no
+    chunk completed: the engine is poisoned, for one-chunk batches too, so that
+    a caller's retry cannot apply the creates twice."""
+    from kwok_amd import abi
+    from kwok_amd.engine import KwokError
+    fx = harness.load_trace("churn")
+    t = fx["ticks"]
+    monkeypatch.setenv("KWOK_INGEST_CHUNK", chunk)
+    monkeypatch.setenv("KWOK_DEBUG_INGEST_FAIL_APPLY", "1")
+    e = Engine(harness.config_for(fx))
+    monkeypatch.delenv("KWOK_DEBUG_INGEST_FAIL_APPLY")
+    specs = harness.SpecCache(e)
+    e.ingest_nodes_raw(*harness.node_batch(t[0]["node_events"]))
+    recs, ar = harness.pod_batch(t[0]["pod_events"], specs)
+    with pytest.raises(KwokError) as ex:
+        e.ingest_pods_raw(recs, ar)
+    assert ex.value.code == abi.EDEVICE and "apply pass" in str(ex.value)
+    with pytest.raises(KwokError) as ex:
+        e.ingest_pods_raw(recs, ar)  # the retry is refused
+    assert ex.value.code == abi.EDEVICE and "recreate" in str(ex.value)
+    e.close()
