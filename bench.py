@@ -135,7 +135,8 @@ def cpu_baseline(nodes, threads, ticks):
                       % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
 
 
-def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None):
+def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
+              packed=True, ch=None):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -146,7 +147,10 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     world > 1: every rank churns n_churn of its own pods per tick (weak
     scaling); the releases of all ranks cross the exchange (their lists are
     longer than the inline message: the second allgather), and each step is
-    timed between barriers, max over ranks."""
+    timed between barriers, max over ranks.  packed: the batch in the compact
+    wire form (kwok_pod_rec, 20 B per record, kwok_ingest_pods_packed; statuses
+    as bytes, no release list at N=1); otherwise kwok_pod_event records with
+    dotted-quad strings (48 B + strings)."""
     barrier = barrier or torch.cuda.synchronize
     max_over_ranks = max_over_ranks or (lambda x: x)
     lo = rank * workload.BUCKETS // world
@@ -154,10 +158,16 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     n_handles = (hi - lo) * fl.cp
     # the batch and the per-record results live in page-locked host memory
     # (kwok_host_alloc): the ingest's copies to and from the GPU run by DMA
-    ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=7,
-                        first=lo * fl.cp, alloc=keng.host_array)
-    outs = (keng.host_array((2 * n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int32),
-            keng.host_array((2 * n_churn,), np.uint32))
+    if ch is None:  # (a later leg continues the previous leg's generator: its live pods)
+        ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn,
+                            seed=7, first=lo * fl.cp, alloc=keng.host_array)
+    ch.packed, ch.bufs = packed, None
+    if packed:  # multi rank: the ingest-time releases too (kwok_pool_put material)
+        outs = (keng.host_array((2 * n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int8),
+                keng.host_array((2 * n_churn,), np.uint32) if world > 1 else None)
+    else:
+        outs = (keng.host_array((2 * n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int32),
+                keng.host_array((2 * n_churn,), np.uint32))
     dump = lambda: e.dump_pods(lo * fl.cp, n_handles)  # noqa: E731
     ing = tck = 0.0
     trans = recs = 0
@@ -171,7 +181,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         if prof:
             e.profile_enable(True)
         t0 = time.perf_counter()
-        hs, st, _ = e.ingest_pods_raw(ev, ar, out=outs)
+        hs, st, _ = e.ingest_pods_packed(ev, out=outs) if packed else e.ingest_pods_raw(ev, ar, out=outs)
         t1 = time.perf_counter()
         r = e.tick(now, read=False)
         t2 = time.perf_counter()
@@ -192,10 +202,12 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
             trans += transitions(r.counters)
             recs += len(ev)
             last = dict(zip(abi.COUNTERS, list(r.counters)))
-    return now, {
+    return now, ch, {
         "workload": "C4 pod churn storm (BASELINE configs[3]) on the metric fleet: %d deletion-marked pods (50%% with "
                     "finalizers) + %d creates per tick%s" % (n_churn, n_churn, " per rank" if world > 1 else ""),
         "ticks": ticks, "records_per_tick": recs // max(ticks, 1) * world,
+        "wire": "kwok_pod_rec, 20 B per record (kwok_ingest_pods_packed)" if packed else
+                "kwok_pod_event, 48 B per record + dotted-quad strings (kwok_ingest_pods)",
         "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
         "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
         "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
@@ -462,10 +474,13 @@ def main():
     phases, nt = e.profile_read()
     e.profile_enable(False)
 
-    churn = None
+    churn = churn_ev = None
     if a.churn_ticks > 0:
-        now, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, rank, world, barrier,
-                               max_over_ranks)
+        now, ch, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, rank, world,
+                                   barrier, max_over_ranks)
+        if world == 1:  # the same storm through the full record form, beside it
+            now, ch, churn_ev = churn_leg(e, fl, pods, now, max(2, a.churn_ticks // 2), a.churn or a.nodes_per_rank,
+                                          rank, world, barrier, max_over_ranks, packed=False, ch=ch)
 
     e.close()
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
@@ -550,6 +565,8 @@ def main():
             out["rehearsal"] = "all ranks on GPU 0, host allgather instead of RCCL: not a reported measurement"
         if churn is not None:
             out["churn"] = churn
+        if churn_ev is not None:
+            out["churn_events"] = churn_ev
         if flap is not None:
             out["flap"] = flap
         if hb_once is not None:

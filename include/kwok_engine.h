@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KWOK_ABI_VERSION 4u
+#define KWOK_ABI_VERSION 5u
 #define KWOK_COMM_ID_BYTES 128u
 
 /* ---- status codes (int return values; per-record codes in out_status) ---- */
@@ -130,6 +130,24 @@ typedef struct kwok_pod_event {
     kwok_str host_ip;    /* status.hostIP (dotted IPv4 or empty) */
     kwok_str pod_ip;     /* status.podIP  (dotted IPv4 or empty) */
 } kwok_pod_event;
+
+/* The compact wire form of a pod event (20 bytes, kwok_ingest_pods_packed):
+ * the same event as kwok_pod_event with its strings already parsed - IPs as
+ * IPv4 integers, the node as its handle - so a churn batch moves ~20 B per
+ * record over the link instead of ~54 (a 48-byte record plus dotted quads).
+ * A create names its node by handle only (a pod naming a node the engine does
+ * not hold by handle goes through kwok_ingest_pods, by spec.nodeName). */
+typedef struct kwok_pod_rec {
+    uint8_t op;          /* KWOK_OP_UPSERT / KWOK_OP_DELETE, | KWOK_REC_NEW for a create */
+    uint8_t flags;       /* KWOK_POD_* in bits 0-4, status.phase (KWOK_PHASE_*) in bits 5-7 */
+    uint16_t spec_id;    /* UPSERT: from kwok_register_pod_spec */
+    int32_t target;      /* the pod's handle; with KWOK_REC_NEW: the handle of its node */
+    uint32_t creation;   /* metadata.creationTimestamp, unix seconds (UTC) */
+    uint32_t host_ip;    /* status.hostIP as an IPv4 integer (0: empty) */
+    uint32_t pod_ip;     /* status.podIP  as an IPv4 integer (0: empty) */
+} kwok_pod_rec;
+#define KWOK_REC_NEW 0x80u
+#define KWOK_REC_PHASE_SHIFT 5
 
 typedef struct kwok_container {
     kwok_str name;
@@ -286,6 +304,20 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena,
                      size_t arena_len, int32_t* out_handles, int32_t* out_status,
                      uint32_t* out_released);
+/* kwok_ingest_pods over the compact wire form: the same event switch, the same
+ * per-record results (out_status as int8_t codes; out_released optional).  A
+ * batch in kwok_host_alloc memory of up to KWOK_INGEST_CHUNK records is read in
+ * place by the GPU. */
+int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, int32_t* out_handles,
+                            int8_t* out_status, uint32_t* out_released);
+/* Host only: kwok_pod_event records (strings in `arena`) -> the compact form,
+ * with the checks that need the strings (canonical dotted quads, creation time
+ * range, spec id and phase bounds).  status[i] = KWOK_OK, KWOK_EDOMAIN (an IP,
+ * a time outside the domain) or KWOK_EINVAL (a create naming its node by
+ * spec.nodeName: not expressible, use kwok_ingest_pods); out[i] is valid only
+ * for KWOK_OK.  Returns the number of records not packed. */
+int kwok_pack_pod_events(const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len, kwok_pod_rec* out,
+                         int32_t* status);
 /* Page-locked host memory for ingest batches.  kwok_ingest_pods copies its
  * records, string arena and per-record results between host and GPU (the pod
  * event switch runs on the device); buffers from kwok_host_alloc move by DMA at

@@ -55,7 +55,7 @@ type gpuEngine struct {
 	// records: copied by DMA, chunk by chunk), and writes the per-record results to
 	// resBuf (a copy into pageable Go memory would stall the engine's next
 	// transfers, DESIGN.md §11)
-	evBuf, arBuf, resBuf hostBuf
+	evBuf, arBuf, resBuf, recBuf hostBuf
 }
 
 type hostBuf struct {
@@ -166,6 +166,7 @@ func (g *gpuEngine) close() {
 	g.evBuf.free()
 	g.arBuf.free()
 	g.resBuf.free()
+	g.recBuf.free()
 }
 
 func arenaPtr(arena []byte) *C.char {
@@ -208,17 +209,76 @@ func (g *gpuEngine) ingestNodes(ev []C.kwok_node_event, arena []byte) (handles, 
 	return
 }
 
-// ingestPods copies the records into the page-locked record buffer and packs
-// the strings they reference (spec.nodeName, status.hostIP / podIP) into the
-// page-locked arena: the batch's object JSON stays on the host.
+// ingestPods: one batch of pod records in event order.  Every record the
+// compact wire form can carry (kwok_pack_pod_events: IPs as integers, a new pod's
+// node by handle) goes as a 20-byte kwok_pod_rec through
+// kwok_ingest_pods_packed; the rest (a pod naming a node the engine holds no
+// handle for) as kwok_pod_event with its strings through kwok_ingest_pods.
+// Consecutive records of one form are one call: applying the calls in order is
+// applying the batch.  Both read page-locked buffers (kwok_host_alloc).
 func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, status []int32, released []uint32, err error) {
-	handles, status, released = make([]int32, len(evs)), make([]int32, len(evs)), make([]uint32, len(evs))
-	if len(evs) == 0 {
+	n := len(evs)
+	handles, status, released = make([]int32, n), make([]int32, n), make([]uint32, n)
+	if n == 0 {
 		return
 	}
-	evp, err := g.evBuf.get(len(evs) * int(unsafe.Sizeof(evs[0])))
+	recp, err := g.recBuf.get(n * int(unsafe.Sizeof(C.kwok_pod_rec{})))
 	if err != nil {
 		return
+	}
+	recs := unsafe.Slice((*C.kwok_pod_rec)(recp), n)
+	pst := make([]int32, n)
+	C.kwok_pack_pod_events(&evs[0], C.size_t(n), arenaPtr(arena), C.size_t(len(arena)), &recs[0], (*C.int32_t)(&pst[0]))
+	for i := 0; i < n; {
+		packed := pst[i] == C.KWOK_OK
+		j := i + 1
+		for j < n && (pst[j] == C.KWOK_OK) == packed {
+			j++
+		}
+		if packed {
+			err = g.ingestPacked(recs[i:j], handles[i:j], status[i:j], released[i:j])
+		} else {
+			err = g.ingestFull(evs[i:j], arena, handles[i:j], status[i:j], released[i:j])
+		}
+		if err != nil {
+			return
+		}
+		i = j
+	}
+	return
+}
+
+// ingestPacked: kwok_ingest_pods_packed of records in page-locked memory
+// (statuses come back as bytes)
+func (g *gpuEngine) ingestPacked(recs []C.kwok_pod_rec, handles, status []int32, released []uint32) error {
+	n := len(recs)
+	resp, err := g.resBuf.get(9 * n)
+	if err != nil {
+		return err
+	}
+	h := unsafe.Slice((*int32)(resp), n)
+	rel := unsafe.Slice((*uint32)(unsafe.Add(resp, 4*n)), n)
+	st := unsafe.Slice((*int8)(unsafe.Add(resp, 8*n)), n)
+	rc := C.kwok_ingest_pods_packed(g.h, &recs[0], C.size_t(n), (*C.int32_t)(&h[0]), (*C.int8_t)(&st[0]),
+		(*C.uint32_t)(&rel[0]))
+	if rc < 0 {
+		return fmt.Errorf("kwok_ingest_pods_packed: %d: %s", int(rc), g.lastError())
+	}
+	copy(handles, h)
+	copy(released, rel)
+	for i := range st {
+		status[i] = int32(st[i])
+	}
+	return nil
+}
+
+// ingestFull copies the records into the page-locked record buffer and packs
+// the strings they reference (spec.nodeName, status.hostIP / podIP) into the
+// page-locked arena: the batch's object JSON stays on the host.
+func (g *gpuEngine) ingestFull(evs []C.kwok_pod_event, arena []byte, handles, status []int32, released []uint32) error {
+	evp, err := g.evBuf.get(len(evs) * int(unsafe.Sizeof(evs[0])))
+	if err != nil {
+		return err
 	}
 	ev := unsafe.Slice((*C.kwok_pod_event)(evp), len(evs))
 	need := 0
@@ -227,7 +287,7 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 	}
 	arp, err := g.arBuf.get(need + 1)
 	if err != nil {
-		return
+		return err
 	}
 	ar := unsafe.Slice((*byte)(arp), need+1)
 	off := 0
@@ -244,21 +304,20 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 	n := len(ev)
 	resp, err := g.resBuf.get(3 * 4 * n)
 	if err != nil {
-		return
+		return err
 	}
 	res := unsafe.Slice((*int32)(resp), 3*n)
 	rc := C.kwok_ingest_pods(g.h, &ev[0], C.size_t(n), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
 		(*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]), (*C.uint32_t)(unsafe.Pointer(&res[2*n])))
 	if rc < 0 {
-		err = fmt.Errorf("kwok_ingest_pods: %d: %s", int(rc), g.lastError())
-		return
+		return fmt.Errorf("kwok_ingest_pods: %d: %s", int(rc), g.lastError())
 	}
 	copy(handles, res[:n])
 	copy(status, res[n:2*n])
 	for i := range released {
 		released[i] = uint32(res[2*n+i])
 	}
-	return
+	return nil
 }
 
 // poolPut replicates IPs another rank released at ingest time (multi-GPU).

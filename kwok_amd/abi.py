@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 COMM_ID_BYTES = 128
 
 OK, EINVAL, ENOMEM, EDOMAIN, EFULL, EDEVICE, ECOMM, ENOTFOUND, ENOTMINE, EBUSY = 0, -1, -2, -3, -4, -5, -6, -7, -8, -9
@@ -47,6 +47,16 @@ class PodEvent(C.Structure):
     _fields_ = [("op", C.c_uint8), ("phase", C.c_uint8), ("flags", C.c_uint8), ("reserved0", C.c_uint8),
                 ("handle", C.c_int32), ("spec_id", C.c_int32), ("node_handle", C.c_int32),
                 ("creation_unix", C.c_int64), ("node_name", KwokStr), ("host_ip", KwokStr), ("pod_ip", KwokStr)]
+
+
+class PodRec(C.Structure):
+    """kwok_pod_rec: the compact wire form of a pod event (kwok_ingest_pods_packed)"""
+    _fields_ = [("op", C.c_uint8), ("flags", C.c_uint8), ("spec_id", C.c_uint16), ("target", C.c_int32),
+                ("creation", C.c_uint32), ("host_ip", C.c_uint32), ("pod_ip", C.c_uint32)]
+
+
+REC_NEW = 0x80
+REC_PHASE_SHIFT = 5
 
 
 class Container(C.Structure):
@@ -132,6 +142,7 @@ def _np_dtype(st):
 
 NODE_EVENT_DTYPE = _np_dtype(NodeEvent)
 POD_EVENT_DTYPE = _np_dtype(PodEvent)
+POD_REC_DTYPE = _np_dtype(PodRec)
 
 
 def ip4(s: str) -> int:
@@ -178,3 +189,22 @@ class Arena:
     def cbuf(self):
         b = bytes(self.buf) or b"\0"
         return C.create_string_buffer(b, len(b)), len(self.buf)
+
+
+def pack_pod_events(ev: np.ndarray, ips_host: np.ndarray | None = None, ips_pod: np.ndarray | None = None):
+    """kwok_pod_event rows (POD_EVENT_DTYPE) whose IPs are given as integers
+    (ips_*: per row, 0 = empty) -> POD_REC_DTYPE rows, vectorised: what
+    kwok_pack_pod_events computes from the strings"""
+    n = len(ev)
+    out = np.zeros(n, POD_REC_DTYPE)
+    create = (ev["op"] == OP_UPSERT) & (ev["handle"] < 0)
+    out["op"] = ev["op"] | np.where(create, REC_NEW, 0).astype(np.uint8)
+    out["flags"] = (ev["flags"] & 31) | (ev["phase"].astype(np.uint8) << REC_PHASE_SHIFT)
+    out["spec_id"] = np.where(ev["op"] == OP_UPSERT, ev["spec_id"], 0)
+    out["target"] = np.where(create, ev["node_handle"], ev["handle"])
+    out["creation"] = np.where(ev["op"] == OP_UPSERT, ev["creation_unix"], 0)
+    if ips_host is not None:
+        out["host_ip"] = np.where(ev["op"] == OP_UPSERT, ips_host, 0)
+    if ips_pod is not None:
+        out["pod_ip"] = ips_pod
+    return out

@@ -65,6 +65,33 @@ HEARTBEAT, NODE_INIT, POD_PATCH, DELETE, DELETE_FIN = range(5)  # engine_cgo.go 
 NOT_SENT = 1  # ingest_pod_runs: a record not sent to the engine (a Deleted event of an unknown pod)
 
 
+def ingest_pods_wire(eng, recs, arena):
+    """engine_cgo.go ingestPods: every record the compact wire form can carry
+    (kwok_pack_pod_events: IPs as integers, a new pod's node by handle) as a
+    20-byte kwok_pod_rec through kwok_ingest_pods_packed, the rest (a pod naming
+    a node the engine holds no handle for) as kwok_pod_event through
+    kwok_ingest_pods; consecutive records of one form in one call, in event
+    order (applying the calls in order is applying the batch).  Returns
+    (handles, statuses, released, calls)."""
+    from .engine import pack_pod_events
+    packed, pst = pack_pod_events(recs, arena)
+    n = len(recs)
+    hs, st, rel = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint32)
+    i = calls = 0
+    while i < n:
+        form = pst[i] == abi.OK
+        j = i + 1
+        while j < n and (pst[j] == abi.OK) == form:
+            j += 1
+        if form:
+            hs[i:j], st[i:j], rel[i:j] = eng.ingest_pods_packed(packed[i:j])
+        else:
+            hs[i:j], st[i:j], rel[i:j] = eng.ingest_pods_raw(recs[i:j], arena)
+        calls += 1
+        i = j
+    return hs, st, rel, calls
+
+
 def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
     """gpu_controller.go flushPods' ingest, on decoded records: the batch in
     event order, cut into runs in which no new pod appears twice - a pod's first
@@ -95,7 +122,7 @@ def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
             return
         recs["op"][idx] = np.where(dl, abi.OP_DELETE, abi.OP_UPSERT)
         recs["handle"][idx] = hv
-        h1, s1, _rel = eng.ingest_pods_raw(recs[idx], arena)
+        h1, s1, _rel, _calls = ingest_pods_wire(eng, recs[idx], arena)
         runs += 1
         hs[idx], st[idx] = h1, s1
         for k in np.nonzero(s1 == abi.OK)[0].tolist():

@@ -27,7 +27,13 @@ enum : uint16_t {
     PS_CONFORMS = 32,
     PS_EVENT = 64,         // needLockPod at event time -> lockPodChan (:318-319)
     PS_HAS_HOST_IP = 128,
+    // bits 8..10: phase.  Bits 11-12 mirror pod_ip (written with it): the tick's
+    // classification reads these instead of the 4-byte address, which it needs only
+    // for a Use or a release (loaded then)
+    PS_IP_SET = 1u << 11,   // pod_ip != 0
+    PS_IP_POOL = 1u << 12,  // pod_ip != 0 and inside the CIDR (ipPool Put / Use apply)
 };
+constexpr uint16_t PS_IP_BITS = PS_IP_SET | PS_IP_POOL;
 constexpr int PS_PHASE_SHIFT = 8;
 constexpr uint16_t PS_PHASE_MASK = 7u << PS_PHASE_SHIFT;
 constexpr uint32_t PHASE_PENDING = 1, PHASE_RUNNING = 2;
@@ -47,6 +53,17 @@ constexpr int NODE_LDS = 16384;           // node slots per chain block (LDS nod
 constexpr int MAX_NODE_CHUNKS = NODE_LDS / NODE_CHUNK;  // 16
 constexpr int MAX_POD_CHUNKS = 64;        // pod chunks per chain block (u64 dirty mask)
 constexpr int SPEC_GROUPS = 2;            // pod groups per thread loaded before the fill marks land
+#ifndef KWOK_ROW_BATCH
+#define KWOK_ROW_BATCH 2
+#endif
+constexpr int ROW_BATCH = KWOK_ROW_BATCH; // further pod rows per thread loaded together (one round trip)
+#ifndef KWOK_ROW_PREFETCH
+#define KWOK_ROW_PREFETCH 1                // ... and the next batch's loads in flight while one is counted
+#endif
+#ifndef KWOK_NODE_PRE
+#define KWOK_NODE_PRE 4
+#endif
+constexpr int NODE_PRE = KWOK_NODE_PRE;   // node chunks of a chain block loaded in its first round trip
 // split ticks (k_pod_jobs): a chain block's live groups in runs of 64, one wave each
 constexpr int WC_GROUPS = 64;
 constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block
@@ -100,7 +117,9 @@ struct TickHdr {
     // accumulator add completed each field; the host derives the header from them
     uint64_t tot[16];
     // multi rank: a BACK launch found exchange lists too long to be inline
-    uint32_t xovf, pad3;
+    uint32_t xovf;
+    // multi rank: some rank's message carried its foreign-IP flag (BACK, every rank alike)
+    uint32_t xforeign;
 };
 
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
@@ -148,6 +167,8 @@ constexpr int XINLINE = 2048;
 struct XMsg {
     uint64_t alloc, n_use, n_rel;
     uint64_t seq;  // the FRONT launch's tick tag: equal on every rank that ticks in step
+    uint64_t foreign;  // the rank's sticky foreign-IP flag (engine.cpp quiet ticks: Use checks skipped
+                       // only while no rank ever had one)
     uint64_t counters[16];
     uint32_t ips[XINLINE];  // uses then releases (when they fit)
 };
@@ -159,6 +180,16 @@ struct PoolGeom {
     uint64_t size;       // 2^(32-prefix) addresses
     uint64_t words;      // size/64 (bitmap words), >= 1
 };
+
+// the PS_IP_* bits of a podIP
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint16_t ip_state_bits(const PoolGeom& g, uint32_t ip) {
+    if (!ip) return 0;
+    const bool pool = ip >= g.net && (uint64_t)(ip - g.net) < g.size;
+    return (uint16_t)(PS_IP_SET | (pool ? PS_IP_POOL : 0));
+}
 
 // ingest ops
 struct NodeOp {

@@ -196,6 +196,7 @@ struct kwok_engine {
         PodRec* rec = nullptr;
         uint32_t *keys = nullptr, *keys_sorted = nullptr, *idx_sorted = nullptr;
         int32_t *out_handle = nullptr, *out_status = nullptr;
+        int8_t* out_status8 = nullptr;  // kwok_ingest_pods_packed: the statuses as bytes
         uint32_t* out_released = nullptr;
         uint32_t* byname = nullptr;
         uint32_t* fix = nullptr;  // [2 * cap] (batch index, code) pairs
@@ -314,6 +315,7 @@ struct kwok_engine {
     // and the Use checks of pods without an event are skipped in every tick.
     uint32_t quiet = 0;         // submits since the last ingest / pool_put / cni_assign
     bool foreign_ips = false;   // sticky: a podIP not assigned by this engine entered the pool
+    bool global_foreign = false;  // multi rank, sticky: some rank's exchange message carried its foreign_ips
     bool quiet_ok = true;
     std::vector<uint32_t> slot_refs;  // kwok_ingest_nodes: pods referencing the batch's deleted nodes (else 0)
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
@@ -925,10 +927,11 @@ int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
     if (n > G.cap) {
         const size_t cap = std::max<size_t>(n + n / 4, 4096);
         void* ptrs[] = {G.d_ev, G.rec, G.keys, G.keys_sorted, G.idx_sorted, G.out_handle, G.out_status,
-                        G.out_released, G.byname, G.fix, G.sort_tmp};
+                        G.out_released, G.byname, G.fix, G.sort_tmp, G.out_status8};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         G.d_ev = G.sort_tmp = nullptr;
+        G.out_status8 = nullptr;
         G.rec = nullptr;
         G.keys = G.keys_sorted = G.idx_sorted = G.out_released = G.byname = G.fix = nullptr;
         G.out_handle = G.out_status = nullptr;
@@ -937,7 +940,8 @@ int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
         if ((rc = dalloc(e, (uint8_t**)&G.d_ev, cap * sizeof(kwok_pod_event))) || (rc = dalloc(e, &G.rec, cap)) ||
             (rc = dalloc(e, &G.keys, cap)) || (rc = dalloc(e, &G.keys_sorted, cap)) || (rc = dalloc(e, &G.idx_sorted, cap)) ||
             (rc = dalloc(e, &G.out_handle, cap)) || (rc = dalloc(e, &G.out_status, cap)) ||
-            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.byname, cap)) || (rc = dalloc(e, &G.fix, 2 * cap)))
+            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.byname, cap)) || (rc = dalloc(e, &G.fix, 2 * cap)) ||
+            (rc = dalloc(e, &G.out_status8, cap)))
             return rc;
         G.sort_bytes = ingest_sort_bytes((uint32_t)cap, 32);
         if ((rc = dalloc(e, (uint8_t**)&G.sort_tmp, G.sort_bytes))) return rc;
@@ -1217,7 +1221,7 @@ void kwok_engine_destroy(kwok_engine* e) {
         auto& g = e->ing;
         void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
                       g.out_released, g.byname, g.fix, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.stopped,
-                      g.freed, g.refs_q, g.refs_out, g.sum, g.creates1, g.dels1, g.sum1};
+                      g.freed, g.refs_q, g.refs_out, g.sum, g.creates1, g.dels1, g.sum1, g.out_status8};
         for (void* p : ip)
             if (p) (void)hipFree(p);
         if (g.sum_h) (void)hipHostFree(g.sum_h);
@@ -1966,9 +1970,14 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
     return (int)G.sum_h->rejected;
 }
 
-int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
-                     int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
-    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
+// kwok_ingest_pods / kwok_ingest_pods_packed: recs are kwok_pod_event (with their
+// string arena) or, packed, kwok_pod_rec (no arena); statuses to out_status
+// (int32) or out_status8 (int8)
+int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, const char* arena, size_t arena_len,
+                     int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released) {
+    const size_t RB = packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);  // record bytes
+    const kwok_pod_event* ev = packed ? nullptr : static_cast<const kwok_pod_event*>(recs);
+    auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
     drain(e);  // the device state reflects every submitted tick
     if (e->poisoned) return poisoned(e);
@@ -2002,12 +2011,13 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
     // the link's latency, and the apply passes beside them stall (1M deletes + 1M
     // creates in 4 chunks: 4.9 ms read in place against 2.8 ms copied).
     const bool zc_ok = e->ingest_zc && K == 1;
-    const void* zev = zc_ok ? host_mapped(ev, n * sizeof(kwok_pod_event)) : nullptr;
+    const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
     auto chunk_batch = [&](uint32_t k) {
         const size_t lo = lo_of(k);
         IngestBatch b = ingest_batch(e, (uint32_t)(lo_of(k + 1) - lo), arena_len);
-        b.ev = static_cast<const kwok_pod_event*>(zev ? zev : (const void*)G.d_ev) + lo;
+        b.packed = packed ? 1u : 0u;
+        b.ev = rec_at(zev ? zev : (const void*)G.d_ev, lo);
         if (zar) b.arena = (const uint8_t*)zar;
         b.rec += lo, b.keys += lo, b.keys_sorted += lo, b.idx_sorted += lo;
         b.out_handle += lo, b.out_status += lo, b.out_released += lo, b.byname += lo;
@@ -2021,7 +2031,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         HIPCHK(e, hipMemsetAsync(b.dels, 0, (size_t)e->nb * 4, ps));
         HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, ps));
         if (!zev)
-            HIPCHK(e, hipMemcpyAsync(static_cast<kwok_pod_event*>(G.d_ev) + lo_of(k), ev + lo_of(k), (size_t)b.n * sizeof(kwok_pod_event),
+            HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
         launch_ingest_prep(e->S, b, ps);
         HIPCHK(e, hipGetLastError());
@@ -2044,7 +2054,7 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             const auto tc = clk::now();
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
             e->ing_chunk = k;
-            const int r = ingest_chunk(e, I, ev + lo, arena);
+            const int r = ingest_chunk(e, I, ev ? ev + lo : nullptr, arena);
             if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
                                   ms_between(t0, tc), ms_between(t0, clk::now()));
             if (r < 0) return r;
@@ -2056,6 +2066,11 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
             if (K > 1) HIPCHK(e, hipStreamWaitEvent(rs, G.used[k & 1], 0));
             if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
             if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+            if (out_status8) {  // one byte per record over the link
+                launch_ingest_status8(I, G.out_status8 + lo, rs);
+                HIPCHK(e, hipGetLastError());
+                HIPCHK(e, hipMemcpyAsync(out_status8 + lo, G.out_status8 + lo, I.n, hipMemcpyDeviceToHost, rs));
+            }
             if (out_released)
                 HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
             if (k + 2 < K)
@@ -2077,6 +2092,53 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
         fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s): %.2f ms\n", n, zev ? ", read in place" : "", K,
                 K == 1 ? "" : "s", ms_between(t0, clk::now()));
     return rc;
+}
+
+int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
+                     int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
+    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
+    return ingest_pods_impl(e, ev, false, n, arena, arena_len, out_handles, out_status, nullptr, out_released);
+}
+
+int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, int32_t* out_handles, int8_t* out_status,
+                            uint32_t* out_released) {
+    if (!e || (n && !recs) || n > 0x7FFFFFF0ull) return KWOK_EINVAL;
+    return ingest_pods_impl(e, recs, true, n, nullptr, 0, out_handles, nullptr, out_status, out_released);
+}
+
+int kwok_pack_pod_events(const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len, kwok_pod_rec* out,
+                         int32_t* status) {
+    if ((n && (!ev || !out)) || (arena_len && !arena)) return KWOK_EINVAL;
+    int bad = 0;
+    auto ip_of = [&](kwok_str s, uint32_t* ip) {  // "" -> 0; otherwise a canonical, non-zero dotted quad
+        *ip = 0;
+        if (!s.len) return true;
+        if ((uint64_t)s.off + s.len > arena_len) return false;
+        return parse_ipv4(arena + s.off, s.len, ip) && *ip != 0;
+    };
+    for (size_t i = 0; i < n; i++) {
+        const kwok_pod_event& x = ev[i];
+        kwok_pod_rec r{};
+        int st = KWOK_OK;
+        const bool create = x.op == KWOK_OP_UPSERT && x.handle < 0;
+        r.op = (uint8_t)(x.op | (create ? KWOK_REC_NEW : 0u));
+        r.flags = (uint8_t)((x.flags & 31u) | ((x.phase & 7u) << KWOK_REC_PHASE_SHIFT));
+        r.spec_id = x.op == KWOK_OP_UPSERT ? (uint16_t)x.spec_id : (uint16_t)0;
+        r.target = create ? x.node_handle : x.handle;
+        if (x.op != KWOK_OP_UPSERT && x.op != KWOK_OP_DELETE) st = KWOK_EINVAL;
+        else if (create && x.node_handle < 0) st = KWOK_EINVAL;  // by spec.nodeName: the full form only
+        else if (x.phase > KWOK_PHASE_OTHER) st = KWOK_EINVAL;
+        else if (x.op == KWOK_OP_UPSERT && (x.spec_id < 0 || x.spec_id > 0xFFFF)) st = KWOK_EINVAL;
+        else if (x.op == KWOK_OP_UPSERT && (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll)) st = KWOK_EDOMAIN;
+        else if (x.op == KWOK_OP_UPSERT && (!ip_of(x.host_ip, &r.host_ip) || !ip_of(x.pod_ip, &r.pod_ip)))
+            st = KWOK_EDOMAIN;
+        else if (x.op == KWOK_OP_DELETE && !ip_of(x.pod_ip, &r.pod_ip)) r.pod_ip = 0;  // not released (as unparsed)
+        r.creation = x.op == KWOK_OP_UPSERT && st == KWOK_OK ? (uint32_t)x.creation_unix : 0u;
+        if (status) status[i] = st;
+        if (st == KWOK_OK) out[i] = r;
+        bad += st != KWOK_OK;
+    }
+    return bad;
 }
 
 int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {
@@ -2214,6 +2276,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
                                        : (hb_bytes < (32ull << 20) || T.split ? 1024u : (S.hb_nt ? 860u : 921u));
     S.use_events_only = T.quiet ? 1u : 0u;
+    S.foreign = e->foreign_ips ? 1u : 0u;
     int rc = bind_slot(e, k);
     if (rc) return rc;
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
@@ -2425,6 +2488,7 @@ int retire(kwok_engine* e) {
         int rc = finish_long_lists(e, k, next);
         if (rc) return failed(rc);
     }
+    if (e->multi && T.hdr_h->xforeign) e->global_foreign = true;  // (the BACK launch that ran to the end)
     const auto t2 = clk::now();
     if (!e->multi) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride, e->S.hb_once != 0);
     const TickHdr& H = *T.hdr_h;
@@ -2589,7 +2653,12 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     T.epoch = e->hb_epoch;
     T.emit_queued = e->emit_hint;
     e->emit_hint = false;
-    T.quiet = e->quiet_ok && !e->multi && (e->quiet >= 2 || !e->foreign_ips);
+    // multi rank: every rank's pods hold the addresses the global pool gave them
+    // unless some rank ever took a foreign one - its flag travels in the exchange
+    // message; a rank that became foreign since the last exchange cannot make a
+    // Use of this tick a change (its Puts come after the Uses, its ingest-time
+    // releases reach the others through kwok_pool_put, which marks them foreign)
+    T.quiet = e->quiet_ok && (e->multi ? !e->foreign_ips && !e->global_foreign : (e->quiet >= 2 || !e->foreign_ips));
     if (e->quiet < 0xFFFFFFFFu) e->quiet++;
     rc = enqueue_tick(e, k, false);
     if (rc) return rc;

@@ -108,9 +108,71 @@ __device__ __forceinline__ bool d_in_cidr(const PoolGeom& g, uint32_t ip) {
 // every status that does not depend on state.  keys[i] = the owned local bucket
 // whose records the apply pass takes in order, or nb (decided here).
 // ---------------------------------------------------------------------------
+// The compact record (kwok_pod_rec): its strings were parsed by the caller, so
+// only the checks on values remain; a create names its node by handle.
+__device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i) {
+    const uint8_t* p = static_cast<const uint8_t*>(I.ev) + (size_t)i * sizeof(kwok_pod_rec);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);  // 20 bytes: five dwords
+    const uint32_t w0 = w[0], ctime = w[2], hip = w[3], pip = w[4];
+    const int32_t target = (int32_t)w[1];
+    const uint32_t op = w0 & 0x7Fu, create = w0 & KWOK_REC_NEW, fl = (w0 >> 8) & 0xFFu, spec = w0 >> 16;
+    PodRec r;
+    r.bucket = REC_NONE;
+    r.pos = 0;
+    r.hip = r.pip = 0;
+    r.ctime = 0;
+    r.spec = 0;
+    r.op = (uint8_t)op;
+    r.phase = (uint8_t)(fl >> KWOK_REC_PHASE_SHIFT);
+    r.flags = (uint8_t)(fl & 31u);
+    r.chk = 0;
+    r.fst = KWOK_OK;
+    r.pst = KWOK_OK;
+    r.pad[0] = r.pad[1] = r.pad[2] = r.pad[3] = 0;
+    int st = 1;  // 1: the apply pass decides
+    if (op == KWOK_OP_DELETE) {
+        if (pip) r.pip = pip, r.chk |= REC_DEL_IP;
+    } else if (op == KWOK_OP_UPSERT) {
+        r.hip = hip, r.pip = pip;
+        if (spec >= I.n_specs) r.fst = KWOK_EINVAL;
+        else if (r.phase > KWOK_PHASE_UNKNOWN) r.fst = KWOK_EINVAL;
+        else r.ctime = ctime, r.spec = (uint16_t)spec;
+    }
+    if (!create && target >= 0) {
+        r.chk |= REC_EXISTING;
+        const uint32_t h = (uint32_t)target, b = h / S.pod_stride;
+        if (b >= S.buckets) r.pst = KWOK_ENOTFOUND;
+        else if (b < S.b_lo || b >= S.b_lo + S.nb) r.pst = KWOK_ENOTMINE;
+        else r.bucket = b - S.b_lo, r.pos = h - b * S.pod_stride;
+        if (r.pst != KWOK_OK) st = r.pst;
+    } else if (!create || op != KWOK_OP_UPSERT || target < 0) {
+        st = KWOK_EINVAL;  // a DELETE / update needs its handle, a create its node's handle
+    } else if (r.fst != KWOK_OK) {
+        st = r.fst;
+    } else {
+        const int64_t l = (int64_t)target - (int64_t)S.b_lo * S.cn;
+        if (l >= 0 && l < (int64_t)S.n_node_slots) r.bucket = (uint32_t)(l / S.cn), r.pos = (uint32_t)(l % S.cn);
+        else st = KWOK_ENOTMINE;
+    }
+    if (st == 1 && op == KWOK_OP_UPSERT && create) atomicAdd(&I.creates[r.bucket], 1u);
+    if (st == 1 && op == KWOK_OP_DELETE && !I.dels[r.bucket]) I.dels[r.bucket] = 1u;
+    I.rec[i] = r;
+    I.keys[i] = st == 1 ? r.bucket : S.nb;
+    if (st != 1) {
+        I.out_handle[i] = -1;
+        I.out_status[i] = st;
+        I.out_released[i] = 0;
+        if (st != KWOK_OK) atomicAdd(&I.sum->rejected, 1u);
+    }
+}
+
 __global__ void k_ing_prep(DevState S, IngestBatch I) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= I.n) return;
+    if (I.packed) {
+        prep_packed(S, I, i);
+        return;
+    }
     const kwok_pod_event x = static_cast<const kwok_pod_event*>(I.ev)[i];
     PodRec r;
     r.bucket = REC_NONE;
@@ -304,6 +366,7 @@ __device__ __forceinline__ uint32_t pod_bits(const DevState& S, uint32_t flags, 
     // conforms once the engine has patched it (an extra, idempotent patch at most)
     if ((flags & KWOK_POD_CONFORMS) && !S.custom_pod) bits |= PS_CONFORMS;
     if (hip) bits |= PS_HAS_HOST_IP;
+    bits |= ip_state_bits(S.pool, pip);
     if (flags & KWOK_POD_DELETING) {
         if (ns & NS_MANAGED) bits |= PS_DELETE_PENDING;  // pod_controller.go:306-308 -> deletePodChan
     } else if ((ns & NS_MANAGED) && !(flags & KWOK_POD_DISREGARD)) {
@@ -645,7 +708,7 @@ __global__ void k_cni_assign(DevState S, const int32_t* handles, const uint32_t*
     }
     if (st == KWOK_OK && wr[i]) {  // the last valid assignment of the handle
         S.pod_ip[slot] = ips[i];
-        S.pod_state[slot] = (uint16_t)(S.pod_state[slot] | PS_STATUS_NONEMPTY);
+        S.pod_state[slot] = (uint16_t)((S.pod_state[slot] & ~PS_IP_BITS) | PS_STATUS_NONEMPTY | ip_state_bits(S.pool, ips[i]));
     }
     if (st != KWOK_OK) atomicAdd(rejected, 1u);
     status[i] = st;
@@ -663,6 +726,13 @@ size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits) {
     return bytes;
 }
 
+__global__ void k_ing_status8(IngestBatch I, int8_t* dst) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < I.n) dst[i] = (int8_t)I.out_status[i];
+}
+void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st) {
+    if (I.n) hipLaunchKernelGGL(k_ing_status8, dim3(cdiv(I.n, 256)), dim3(256), 0, st, I, dst);
+}
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st) {
     if (I.n) hipLaunchKernelGGL(k_ing_prep, dim3(cdiv(I.n, 256)), dim3(256), 0, st, S, I);
 }

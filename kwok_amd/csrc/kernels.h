@@ -97,6 +97,7 @@ struct DevState {
     uint32_t cni;              // Config.EnableCNI: pod IPs come from the caller's CNI (kwok_cni_assign), not the ipPool
     uint32_t custom_pod;       // Config.PodStatusTemplate is custom: the caller's CONFORMS digest is ignored
     uint32_t use_events_only;  // this tick Use-checks only pods with an event (a quiet tick: kwok_tick_submit)
+    uint32_t foreign;          // multi rank: this rank's sticky foreign-IP flag, sent in the exchange message
     uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
@@ -137,9 +138,11 @@ int emit_occupancy();  // resident k_emit blocks per CU
 
 // ---- GPU pod ingest (ingest.hip): kwok_ingest_pods / kwok_cni_assign --------
 struct IngestBatch {
-    const void* ev;            // [n] kwok_pod_event, copied to the device
+    const void* ev;            // [n] kwok_pod_event (packed: kwok_pod_rec), on the device or read in place
     uint32_t n;
     uint32_t n_specs;
+    uint32_t packed;           // 1: kwok_pod_rec records (no arena)
+    uint32_t pad0;
     const uint8_t* arena;      // the batch's string arena (device copy)
     uint64_t arena_len;
     PodRec* rec;               // [n] prepared records
@@ -161,6 +164,8 @@ struct IngestBatch {
 size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort temporary storage
 // prep (+ growth counts) for every record
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st);
+// the batch's per-record statuses as bytes (kwok_ingest_pods_packed's out_status)
+void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st);
 // live pods + creates of every bucket with creates -> sum->need
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st);
 // host resolutions of by-name creates: (batch index, node index in its bucket | status << 16)

@@ -770,19 +770,19 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
     // bit 16 of every plane); integer arithmetic keeps it all in VGPRs
     static_assert(PS_USED == 1 && PS_DISREGARD == 2 && PS_DELETE_PENDING == 4 && PS_STATUS_NONEMPTY == 16 &&
                       PS_CONFORMS == 32 && PS_EVENT == 64 && PS_HAS_HOST_IP == 128 && PS_PHASE_SHIFT == 8 &&
-                      NT_RELOCK == 1 && NT_MANAGED == 2 && PHASE_PENDING == 1 && PHASE_RUNNING == 2,
+                      NT_RELOCK == 1 && NT_MANAGED == 2 && PHASE_PENDING == 1 && PHASE_RUNNING == 2 &&
+                      PS_IP_SET == (1u << 11) && PS_IP_POOL == (1u << 12),
                   "state bit layout");
     constexpr uint32_t M = 0x00010001u;
-    // the CIDR spans at most 2^28 addresses (prefix >= 4): one u32 compare tests it
-    const uint32_t net = S.pool.net, size = (uint32_t)S.pool.size;
     GroupMasks m{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const uint32_t s = g.stw[w];
         const uint32_t nf = (uint32_t)ntf[2 * w] | (uint32_t)ntf[2 * w + 1] << 16;
-        const uint32_t ia = g.ip[2 * w], ib = g.ip[2 * w + 1];
-        const uint32_t ipz = (ia == 0 ? 1u : 0u) | (ib == 0 ? M ^ 1u : 0u);
-        const uint32_t inc_pool = ((ia - net < size ? 1u : 0u) | (ib - net < size ? M ^ 1u : 0u)) & ~ipz;
+        // podIP == 0 / in the CIDR: the state's PS_IP_SET / PS_IP_POOL (pod_ip itself is
+        // loaded only for a Use or a release)
+        const uint32_t ipz = ~(s >> 11) & M;
+        const uint32_t inc_pool = (s >> 12) & M;
         const uint32_t used = s & M, disr = (s >> 1) & M, del = used & (s >> 2);
         const uint32_t nonempty = (s >> 4) & M, conf = (s >> 5) & M, event = (s >> 6) & M, hhost = (s >> 7) & M;
         const uint32_t ph = (s >> 8) & (7u * M);
@@ -1000,21 +1000,38 @@ __device__ __forceinline__ void apply_uses(const DevState& S, const PodGrp& g, u
     }
 }
 
-// one 8-slot group at a known slot (~0u: none), pods at or past `fill` read as empty
-__device__ __forceinline__ void load_group_at(const DevState& S, uint32_t slot, uint32_t j, PodGrp& g) {
+// one 8-slot group at a known slot (~0u: none), pods at or past `fill` read as
+// empty.  with_ip = false: state and node words only (the classification's
+// predicates read the podIP bits of the state; load_group_ips adds the
+// addresses when a Use or a release needs them)
+__device__ __forceinline__ void load_group_at(const DevState& S, uint32_t slot, uint32_t j, PodGrp& g,
+                                              bool with_ip = true) {
     uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
     g.slot = slot;
     g.j = j;
     if (slot != ~0u) {
         st4 = *reinterpret_cast<const uint4*>(S.pod_state + slot);
         nd4 = *reinterpret_cast<const uint4*>(S.pod_node + slot);
-        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + slot);
-        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + slot + 4);
+        if (with_ip) {
+            ipa = *reinterpret_cast<const uint4*>(S.pod_ip + slot);
+            ipb = *reinterpret_cast<const uint4*>(S.pod_ip + slot + 4);
+        }
     }
     g.stw[0] = st4.x, g.stw[1] = st4.y, g.stw[2] = st4.z, g.stw[3] = st4.w;
     g.ndw[0] = nd4.x, g.ndw[1] = nd4.y, g.ndw[2] = nd4.z, g.ndw[3] = nd4.w;
     g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
     g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
+}
+// the podIPs of a group loaded without them, for the lanes that need them (a Use
+// check or a release: GroupMasks usec / rel); wave-uniform entry
+__device__ __forceinline__ void load_group_ips(const DevState& S, PodGrp& g, bool need) {
+    if (__builtin_expect(__ballot(need) == 0, 1)) return;
+    if (need && g.slot != ~0u) {
+        const uint4 ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
+        const uint4 ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
+        g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
+        g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
+    }
 }
 // a speculatively loaded group past its bucket's fill mark holds no pods
 __device__ __forceinline__ void clip_group(PodGrp& g, bool live) {
@@ -1285,6 +1302,7 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
                     // the apiserver applied the patch
                     s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS |
                                    PS_STATUS_NONEMPTY | (stat ? PS_HAS_HOST_IP : 0));
+                    if (stat) s = (uint16_t)((s & ~PS_IP_BITS) | ip_state_bits(S.pool, pip));
                 }
                 s &= (uint16_t)~PS_EVENT;
             }
@@ -1520,6 +1538,7 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
             XMsg* X = S.xmsg;
             X->alloc = tot[AG_ALLOC];
             X->seq = tag;
+            X->foreign = S.foreign;
             X->n_use = nu;
             X->n_rel = nr;
             constexpr int LC = offsetof(TickHdr, local_counters) / 8;
@@ -1825,16 +1844,22 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         const uint32_t j = t / tpb, l = t - j * tpb;
         const bool jv = j < nbk;
         const uint32_t gcap = S.cp / POD_PER_THREAD;
+        // the node states of the block's first NODE_PRE chunks first: loads complete in
+        // issue order, so the node classification below waits for these and the fill
+        // marks only, not for the pod groups behind them
+        uint32_t packed_pre[NODE_PRE];
+#pragma unroll
+        for (int c = 0; c < NODE_PRE; c++) {
+            const uint32_t i = (uint32_t)c * NODE_CHUNK + t * NODE_PER_THREAD;
+            packed_pre[c] = i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u;
+        }
         const uint32_t fill = jv ? S.pod_fill[bk0 + j] : 0u;
         PodGrp G[SPEC_GROUPS];
 #pragma unroll
         for (int q = 0; q < SPEC_GROUPS; q++) {
             const uint32_t a = l + q * tpb;
-            load_group_at(S, jv && a < gcap ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, G[q]);
+            load_group_at(S, jv && a < gcap ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, G[q], false);
         }
-        const uint32_t packed0 = (uint32_t)t * NODE_PER_THREAD < nn
-                                     ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + t * NODE_PER_THREAD)
-                                     : 0u;
         const uint64_t pool_index = single ? 0 : *S.pool_index;  // multi rank: the header's default cursor
         if (jv && l == 0) gpre[j + 1] = fill / POD_PER_THREAD;
         const uint16_t* smax = S.n_specs <= (uint32_t)SPEC_LDS ? spec_max : nullptr;
@@ -1846,8 +1871,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         uint32_t nmask = 0;
         for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
             const uint32_t i = i0 + t * NODE_PER_THREAD;
-            const uint32_t packed =
-                i0 == 0 ? packed0 : (i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int c = 0; c < NODE_PRE; c++) packed = i0 == (uint32_t)c * NODE_CHUNK ? packed_pre[c] : packed;
+            if (i0 >= (uint32_t)NODE_PRE * NODE_CHUNK && i < nn)
+                packed = *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i);
             uint32_t tick = 0;
             bool dirty = false;
 #pragma unroll
@@ -1885,45 +1913,110 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         TSTAMP(1);
         // ---- pods: the speculative groups, then any further rows (rare) ------------
         uint64_t pmask = 0;
-        uint32_t usec[SPEC_GROUPS];  // single rank: Use candidates, checked after the accumulator adds
-        uint4 spw[SPEC_GROUPS];  // the groups' spec words, one round trip for all of them
+        {
+            // the groups' spec words and the `used` words of their Use candidates
+            // (configurePod, pod_controller.go:378-382): one round trip for all of them
+            uint4 spw[SPEC_GROUPS];
+            UsedWords uw[SPEC_GROUPS];
 #pragma unroll
-        for (int q = 0; q < SPEC_GROUPS; q++) {
-            const uint32_t a = l + q * tpb;
-            clip_group(G[q], jv && a * POD_PER_THREAD < fill);
-            spw[q] = load_spec_words(S, G[q], masks_of(S, nflags, G[q]).need);
-        }
-#pragma unroll
-        for (int q = 0; q < SPEC_GROUPS; q++) {
-            const uint32_t a = l + q * tpb;
-            const GroupMasks m = masks_of(S, nflags, G[q]);
-            const uint32_t gbytes = count_group(S, G[q], m, f, spw[q], smax);
-            // emission chunks are runs of 256 live groups in slot order (gpre)
-            if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
-            if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
-            usec[q] = m.usec;
-            if (!single) {  // multi rank: Use lists before the record (the exchange message carries them)
-                const UsedWords u = used_words(S, G[q], m.usec);
-                apply_uses(S, G[q], m.usec & ~used_bits(S, G[q], m.usec, u));
+            for (int q = 0; q < SPEC_GROUPS; q++) {
+                const uint32_t a = l + q * tpb;
+                clip_group(G[q], jv && a * POD_PER_THREAD < fill);
+                const GroupMasks m = masks_of(S, nflags, G[q]);
+                spw[q] = load_spec_words(S, G[q], m.need);
+                load_group_ips(S, G[q], (m.usec | m.rel) != 0);
+                uw[q] = used_words(S, G[q], m.usec);
             }
-            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < SPEC_GROUPS; q++) {
+                const uint32_t a = l + q * tpb;
+                const GroupMasks m = masks_of(S, nflags, G[q]);
+                const uint32_t gbytes = count_group(S, G[q], m, f, spw[q], smax);
+                // emission chunks are runs of 256 live groups in slot order (gpre)
+                if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+                if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                // single rank: into `used` now; multi rank: the Use list (the exchange message)
+                apply_uses(S, G[q], m.usec & ~used_bits(S, G[q], m.usec, uw[q]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         const uint32_t maxg = sh_mask[3];
-        if (SPEC_GROUPS * tpb < maxg) {
+        auto row_slot = [&](uint32_t a) {
+            return jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u;
+        };
+        if (SPEC_GROUPS * tpb < maxg && S.hb_once) {
+            // heartbeat-once ticks (nothing to hide the chain under): ROW_BATCH rows
+            // per iteration, all their group loads in one round trip.  A wave whose
+            // rows hold nothing but counts (no patch, Use, release or event: every
+            // row of a quiet steady tick) only counts them; otherwise each row in
+            // turn is loaded again (from the caches) with its podIPs, spec and
+            // `used` words and takes the rare paths
+#if KWOK_ROW_PREFETCH
+            // (double-buffered: the next batch's loads are issued before this batch is counted)
+            PodGrp N[ROW_BATCH];
+#pragma unroll
+            for (int r = 0; r < ROW_BATCH; r++)
+                load_group_at(S, row_slot(l + SPEC_GROUPS * tpb + r * tpb), j, N[r], false);
+#endif
+            for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += ROW_BATCH * tpb) {
+                PodGrp H[ROW_BATCH];
+#if KWOK_ROW_PREFETCH
+#pragma unroll
+                for (int r = 0; r < ROW_BATCH; r++) H[r] = N[r];
+                const uint32_t an = a0 + ROW_BATCH * tpb;
+#pragma unroll
+                for (int r = 0; r < ROW_BATCH; r++)
+                    load_group_at(S, an < maxg ? row_slot(l + an + r * tpb) : ~0u, j, N[r], false);
+#else
+#pragma unroll
+                for (int r = 0; r < ROW_BATCH; r++) load_group_at(S, row_slot(l + a0 + r * tpb), j, H[r], false);
+#endif
+                // counts of a clean batch (no delete, patch, Get, Put, Use or event:
+                // count_group reduces to these four fields)
+                bool rare = false;
+                uint32_t n_eval = 0, n_total = 0, n_pend = 0, n_run = 0;
+#pragma unroll
+                for (int r = 0; r < ROW_BATCH; r++) {
+                    const GroupMasks m = masks_of(S, nflags, H[r]);
+                    rare |= (m.need | m.usec | m.rel | m.dirty | m.del | m.alloc) != 0;
+                    n_eval += __popc(m.eval);
+                    n_total += __popc(m.total);
+                    n_pend += __popc(m.pend);
+                    n_run += __popc(m.run);
+                }
+                if (__builtin_expect(__ballot(rare) == 0, 1)) {
+                    f[AG_EVAL] += n_eval;
+                    f[AG_TOTAL] += n_total;
+                    f[AG_PENDING] += n_pend;
+                    f[AG_RUNNING] += n_run;
+                } else {
+                    for (int r = 0; r < ROW_BATCH; r++) {
+                        const uint32_t a = l + a0 + r * tpb;
+                        PodGrp g;
+                        load_group_at(S, row_slot(a), j, g);
+                        const GroupMasks m = masks_of(S, nflags, g);
+                        const uint4 sw = load_spec_words(S, g, m.need);
+                        const UsedWords u = used_words(S, g, m.usec);
+                        const uint32_t gbytes = count_group(S, g, m, f, sw, smax);
+                        if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+                        if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                        apply_uses(S, g, m.usec & ~used_bits(S, g, m.usec, u));
+                    }
+                }
+            }
+        } else if (SPEC_GROUPS * tpb < maxg) {
             // one row per iteration, the next row's group loads in flight under this
-            // row's Use check (one round trip per row, not two)
-            auto row_slot = [&](uint32_t a) {
-                return jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u;
-            };
+            // row's spec / Use loads (one round trip per row, not two); the podIPs
+            // only for a row with a Use or a release
             PodGrp H;
-            load_group_at(S, row_slot(l + SPEC_GROUPS * tpb), j, H);
+            load_group_at(S, row_slot(l + SPEC_GROUPS * tpb), j, H, false);
             for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += tpb) {
                 const uint32_t a = l + a0;
                 const GroupMasks m = masks_of(S, nflags, H);
-                // one round trip: the next row's group, this row's spec and `used` words
                 PodGrp N;
-                load_group_at(S, a0 + tpb < maxg ? row_slot(a + tpb) : ~0u, j, N);
+                load_group_at(S, a0 + tpb < maxg ? row_slot(a + tpb) : ~0u, j, N, false);
                 const uint4 sw = load_spec_words(S, H, m.need);
+                load_group_ips(S, H, (m.usec | m.rel) != 0);
                 const UsedWords u = used_words(S, H, m.usec);
                 const uint32_t gbytes = count_group(S, H, m, f, sw, smax);
                 if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
@@ -1956,15 +2049,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                     w = t == i ? ((uint64_t)f[2 * i] | (uint64_t)f[2 * i + 1] << 32) : w;
                 st_sc1(reinterpret_cast<uint64_t*>(S.blockagg + (size_t)b * AG_STRIDE) + t, w);
             }
-            // the Use checks of the speculative groups
-            UsedWords u[SPEC_GROUPS];
-#pragma unroll
-            for (int q = 0; q < SPEC_GROUPS; q++) u[q] = used_words(S, G[q], usec[q]);
             uint32_t acc_v = 0;  // lane t < AG_DIRTY: this block's value of field t
 #pragma unroll
             for (int i = 0; i < AG_DIRTY; i++) acc_v = t == i ? f[i] : acc_v;
-#pragma unroll
-            for (int q = 0; q < SPEC_GROUPS; q++) apply_uses(S, G[q], usec[q] & ~used_bits(S, G[q], usec[q], u[q]));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             TSTAMP(11);
@@ -2086,6 +2173,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 H->alloc_total = xA;
                 H->alloc_base = xbase;
                 H->rel_total = xrel;
+                uint32_t fx = 0;
+                for (int r = 0; r < S.world; r++) fx |= X[r].foreign ? 1u : 0u;
+                H->xforeign = fx;
+                st_host(&S.hdr_host->xforeign, fx);
             }
         }
         // this block's masks from the FRONT launch
@@ -2234,7 +2325,9 @@ __global__ void k_apply_pod_ops(DevState S, const PodOp* ops, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     PodOp o = ops[i];
-    S.pod_state[o.slot] = (uint16_t)((S.pod_state[o.slot] & o.keep_mask) | o.bits);
+    uint16_t st = (uint16_t)((S.pod_state[o.slot] & o.keep_mask) | o.bits);
+    if (o.set_fields) st = (uint16_t)((st & ~PS_IP_BITS) | ip_state_bits(S.pool, o.pod_ip));
+    S.pod_state[o.slot] = st;
     if (o.set_fields == 1) {  // add / modify carry the whole decoded object
         S.pod_node[o.slot] = o.node;
         S.pod_spec[o.slot] = o.spec;

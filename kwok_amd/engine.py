@@ -60,6 +60,7 @@ def declare(lib, pre):
         "register_pod_spec": (C.c_int, [VP, P(abi.PodSpec), C.c_char_p, SZ, P(I32)]),
         "ingest_nodes": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP]),
         "ingest_pods": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP, VP]),
+        "ingest_pods_packed": (C.c_int, [VP, VP, SZ, VP, VP, VP]),
         "pool_put": (C.c_int, [VP, VP, SZ]),
         "cni_pending": (C.c_int, [VP, VP, SZ, P(SZ)]),
         "cni_assign": (C.c_int, [VP, VP, VP, SZ, VP]),
@@ -78,6 +79,7 @@ def declare(lib, pre):
             "device_outputs": (C.c_int, [VP, P(abi.DeviceView)]),
             "bucket_of": (U32, [C.c_char_p, SZ, U32]),
             "host_alloc": (VP, [SZ]),
+            "pack_pod_events": (C.c_int, [VP, SZ, C.c_char_p, SZ, VP, VP]),
             "host_free": (None, [VP]),
             "rank_of_bucket": (I32, [U32, U32, I32]),
             "profile_enable": (C.c_int, [VP, C.c_int]),
@@ -248,6 +250,22 @@ class EngineBase:
         rc = self._fn("ingest_pods")(self._h, ev.ctypes.data, n, ar, alen, hs.ctypes.data, st.ctypes.data,
                                      rel.ctypes.data)
         self._check(rc, "ingest_pods")
+        return hs, st, rel
+
+    def ingest_pods_packed(self, recs: np.ndarray, out=None, released=True):
+        """kwok_ingest_pods_packed over POD_REC_DTYPE rows; out: optional
+        (handles, status int8, released) arrays (e.g. page-locked, host_array)"""
+        n = len(recs)
+        if out is None:
+            hs, st = np.empty(n, np.int32), np.empty(n, np.int8)
+            rel = np.empty(n, np.uint32) if released else None
+        else:
+            hs, st, rel = (o[:n] if o is not None else None for o in out)
+        r = recs if recs.flags.c_contiguous and recs.dtype == abi.POD_REC_DTYPE else \
+            np.ascontiguousarray(recs, dtype=abi.POD_REC_DTYPE)
+        rc = self._fn("ingest_pods_packed")(self._h, r.ctypes.data, n, hs.ctypes.data, st.ctypes.data,
+                                            rel.ctypes.data if rel is not None else None)
+        self._check(rc, "ingest_pods_packed")
         return hs, st, rel
 
     def pool_put(self, ips):
@@ -514,3 +532,17 @@ def heartbeat_template_patch(tpl=None, start=1704067200, node_ip="196.168.0.1", 
     if rc != 0:
         raise KwokError(rc, (lib.kwok_template_last_error() or b"").decode())
     return out.raw[:m.value]
+
+
+def pack_pod_events(events: np.ndarray, arena) -> tuple[np.ndarray, np.ndarray]:
+    """kwok_pack_pod_events: kwok_pod_event rows + their string arena -> the
+    compact records and a status per row (host only)"""
+    lib = load_engine_lib()
+    ev = np.ascontiguousarray(events, dtype=abi.POD_EVENT_DTYPE)
+    out = np.zeros(len(ev), abi.POD_REC_DTYPE)
+    st = np.empty(len(ev), np.int32)
+    a = bytes(arena) if arena is not None else b""
+    rc = lib.kwok_pack_pod_events(ev.ctypes.data, len(ev), a or b"\0", len(a), out.ctypes.data, st.ctypes.data)
+    if rc < 0:
+        raise KwokError(rc, "pack_pod_events")
+    return out, st

@@ -174,8 +174,11 @@ class Churn:
     oracle), or one rank's bucket range of a sharded one."""
 
     def __init__(self, pod_handles, node_of_pod, spec_id, n_handles, n_churn, seed=0, node_ip=NODE_IP,
-                 creation=S0 - 60, first=0, alloc=None):
+                 creation=S0 - 60, first=0, alloc=None, packed=False):
         self.first = first
+        # packed: the batch as kwok_pod_rec (kwok_ingest_pods_packed: 20 B per record,
+        # IPs as integers, nodes by handle) instead of kwok_pod_event + dotted quads
+        self.packed = packed
         # alloc(shape, dtype): the batch is written into (and reused from) these
         # buffers - e.g. page-locked host memory (engine.host_array), which the
         # ingest copies to the GPU by DMA
@@ -192,12 +195,15 @@ class Churn:
         self.node_ip = node_ip.encode()
 
     def batch(self, dump, now):
-        """(events, arena): n_churn deletion-marked pods, then n_churn new pods"""
+        """(events, arena): n_churn deletion-marked pods, then n_churn new pods
+        (packed: (records, None))"""
         D = min(self.n, self.live.shape[0])
         dead = self.live[:D]
         loc = dead - self.first
         used, phase, _, pip = dump()
         assert used[loc].all(), "churn: a live pod is missing from the engine"
+        if self.packed:
+            return self._batch_packed(D, dead, loc, phase, pip, now), None
         ip_buf, ip_off, ip_len = ip_strings(pip[loc], base=len(self.node_ip))
         if self.alloc is None:
             arena = self.node_ip + ip_buf.tobytes()
@@ -236,6 +242,36 @@ class Churn:
         c["creation_unix"] = now - 5
         self._pending = (D, c["node_handle"].copy(), now - 5)
         return ev, arena
+
+    def _batch_packed(self, D, dead, loc, phase, pip, now):
+        if self.alloc is None:
+            ev = np.zeros(2 * D, abi.POD_REC_DTYPE)
+        else:
+            if self.bufs is None or len(self.bufs[0]) < 2 * D:
+                self.bufs = (self.alloc((2 * self.n,), abi.POD_REC_DTYPE),)
+            ev = self.bufs[0][:2 * D]
+        d = ev[:D]
+        running = phase[loc] == abi.PHASE_RUNNING
+        fin = np.where(self.rng.random(D) < 0.5, abi.POD_HAS_FINALIZERS, 0)
+        d["op"] = abi.OP_UPSERT
+        d["target"] = dead
+        d["spec_id"] = self.spec
+        d["creation"] = self.ctime[loc]
+        d["flags"] = ((abi.POD_DELETING | fin | np.where(running, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
+                       | np.where(pip[loc] != 0, abi.POD_STATUS_NONEMPTY, 0))
+                      | (phase[loc].astype(np.int64) << abi.REC_PHASE_SHIFT))
+        d["host_ip"] = np.where(running, abi.ip4(self.node_ip.decode()), 0)
+        d["pod_ip"] = pip[loc]
+        c = ev[D:]
+        c["op"] = abi.OP_UPSERT | abi.REC_NEW
+        c["target"] = self.rng.permutation(self.node_of[loc])
+        c["spec_id"] = self.spec
+        c["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
+        c["creation"] = now - 5
+        c["host_ip"] = 0
+        c["pod_ip"] = 0
+        self._pending = (D, c["target"].copy(), now - 5)
+        return ev
 
     def applied(self, handles, status):
         """account the ingest result of the last batch"""

@@ -739,6 +739,63 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
 static inline int keep_eval(const kwok_oracle* o, size_t h);
 /* EnableCNI: the pods the next tick evaluates without a podIP (configurePod's
  * cni.Setup set, pod_controller.go:383-389), canonical order */
+/* kwok_ingest_pods_packed: the compact records as the kwok_pod_event they stand
+ * for (dotted quads of the IPs, the node by handle), through the event switch
+ * above; a create without a node handle is not expressible (KWOK_EINVAL) */
+int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, size_t n, int32_t* out_handles,
+                                   int8_t* out_status, uint32_t* out_released) {
+    kwok_pod_event* ev = (kwok_pod_event*)calloc(n + 1, sizeof(kwok_pod_event));
+    char* ar = (char*)calloc(32 * n + 1, 1);
+    int32_t* st = (int32_t*)calloc(n + 1, sizeof(int32_t));
+    int32_t* hs = (int32_t*)calloc(n + 1, sizeof(int32_t));
+    size_t* pre = (size_t*)calloc(n + 1, sizeof(size_t)); /* records sent before record i */
+    size_t m = 0, off = 0;
+    int bad = 0;
+    for (size_t i = 0; i < n; i++) {
+        const kwok_pod_rec* r = &recs[i];
+        const int create = (r->op & KWOK_REC_NEW) != 0;
+        pre[i] = m;
+        if (create && r->target < 0) {
+            st[i] = KWOK_EINVAL; /* not sent */
+            continue;
+        }
+        st[i] = 1; /* sent: the status comes from the event switch */
+        kwok_pod_event* e = &ev[m++];
+        e->op = r->op & ~KWOK_REC_NEW;
+        e->flags = r->flags & 31;
+        e->phase = r->flags >> KWOK_REC_PHASE_SHIFT;
+        e->spec_id = r->spec_id;
+        e->handle = create ? -1 : r->target;
+        e->node_handle = create ? r->target : -1;
+        e->creation_unix = r->creation;
+        uint32_t ips[2] = {r->host_ip, r->pod_ip};
+        kwok_str* dst[2] = {&e->host_ip, &e->pod_ip};
+        for (int k = 0; k < 2; k++) {
+            if (!ips[k]) continue;
+            const int len = sprintf(ar + off, "%u.%u.%u.%u", ips[k] >> 24, (ips[k] >> 16) & 255, (ips[k] >> 8) & 255,
+                                    ips[k] & 255);
+            dst[k]->off = (uint32_t)off;
+            dst[k]->len = (uint32_t)len;
+            off += (size_t)len;
+        }
+    }
+    int32_t* st2 = (int32_t*)calloc(m + 1, sizeof(int32_t));
+    uint32_t* rel = (uint32_t*)calloc(m + 1, sizeof(uint32_t));
+    const int rc = kwok_oracle_ingest_pods(o, ev, m, ar, off, hs, st2, rel);
+    if (rc >= 0) {
+        for (size_t i = 0; i < n; i++) {
+            const int sent = st[i] == 1;
+            const int code = sent ? st2[pre[i]] : st[i];
+            if (out_status) out_status[i] = (int8_t)code;
+            if (out_handles) out_handles[i] = sent ? hs[pre[i]] : -1;
+            if (out_released) out_released[i] = sent ? rel[pre[i]] : 0;
+            bad += code != KWOK_OK;
+        }
+    }
+    free(ev), free(ar), free(st), free(hs), free(pre), free(st2), free(rel);
+    return rc < 0 ? rc : bad;
+}
+
 int kwok_oracle_cni_pending(kwok_oracle* o, int32_t* out, size_t cap, size_t* n_out) {
     if (!o->cni || !n_out) return KWOK_EINVAL;
     size_t n = 0;

@@ -7,7 +7,8 @@ so the exchange runs over the host allgather hook: the same FRONT / exchange
 over gloo, a small fleet).  Each rank owns B/W of the buckets.  Compared:
   * the initial tick (every node init, every Pending->Running patch with its
     IP in the global canonical order): fleet counters, every rank's pod state
-    (phase, hostIP, podIP) and its heartbeat / init / patch / delete lists;
+    (phase, hostIP, podIP), its heartbeat / init / patch / delete lists and
+    every pod patch's and node-init patch's bytes (64-bit digests);
   * a C4-style churn tick (10% of the pods marked for deletion, half with
     finalizers, and as many created, so every rank's release list is longer
     than the inline exchange message: the second allgather + pool apply):
@@ -67,6 +68,9 @@ def _worker(rank, world, port, d, nodes, backend):
     out = {"first": lo * fl.cp, "pods": ph}
     a = _tick(e, workload.S0 + 30, out, "0")
     out["l0"] = {k: a[k] for k in LISTS}
+    out["dig0"] = patch_digests(a["arena"], a["pod_patch_off"], a["pod_patch_len"])
+    out["dig0n"] = patch_digests(a["arena"], a["node_init_off"], a["node_init_len"])
+    del a
     out["dump0"] = e.dump_pods(lo * fl.cp, (hi - lo) * fl.cp)
     ev = np.load(os.path.join(d, "ev%d.npy" % rank))
     with open(os.path.join(d, "arena.bin"), "rb") as f:
@@ -92,6 +96,9 @@ def run_c3(world, nodes, churn, backend):
     ref = {}
     A = _tick(o, workload.S0 + 30, ref, "0")
     ref["l0"] = {k: A[k] for k in LISTS}
+    ref["dig0"] = patch_digests(A["arena"], A["pod_patch_off"], A["pod_patch_len"])
+    ref["dig0n"] = patch_digests(A["arena"], A["node_init_off"], A["node_init_len"])
+    del A
     ref["dump0"] = o.dump_pods(0, n_slots)
     assert ref["c0"][2] == 10 * nodes  # every pod patched in the initial tick
     ch = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_slots, churn, seed=3)
@@ -137,6 +144,11 @@ def run_c3(world, nodes, churn, backend):
                 assert np.array_equal(p["l" + tick][k], R[k][sel]), "rank %d tick %s %s" % (r, tick, k)
         pp = ref["l1"]["pod_patch_pods"]
         assert np.array_equal(p["dig1"], ref["dig1"][(pp >= lo_h) & (pp < hi_h)]), "rank %d churn patch bytes" % r
+        # the initial tick's bytes too: every Pending->Running patch (its IP in the
+        # global order) and every node-init patch of the rank
+        pp0, ni0 = ref["l0"]["pod_patch_pods"], ref["l0"]["node_init_nodes"]
+        assert np.array_equal(p["dig0"], ref["dig0"][(pp0 >= lo_h) & (pp0 < hi_h)]), "rank %d initial patch bytes" % r
+        assert np.array_equal(p["dig0n"], ref["dig0n"][(ni0 >= lo_n) & (ni0 < hi_n)]), "rank %d node-init bytes" % r
         mine = np.nonzero(own == r)[0]  # the rank's ingest results are the oracle's for its records
         for k in range(3):
             assert np.array_equal(p["ingest"][k], ref["ingest"][k][mine]), "rank %d ingest output %d" % (r, k)

@@ -54,10 +54,13 @@ def make(cls, rank, world, allgather=None, device=0, big=False, comm_id=None):
     return cls(cfg)
 
 
-def scenario(seed=11, ticks=5, big=False):
+def scenario(seed=11, ticks=5, big=False, foreign_from=0):
     """A deterministic list of per-tick event batches (dict form).  big: 12000
     pods, then 6000 deletions in one tick (every rank's release list is longer
-    than the inline exchange message holds)."""
+    than the inline exchange message holds).  foreign_from: pods are created
+    with podIPs of their own (3%, possibly another pod's address) only from
+    that tick on: the ticks before it run quiet (Use checks skipped) on every
+    rank, and the first foreign address ends that on every rank."""
     rng = np.random.default_rng(seed)
     names = ["node-%07d" % i for i in range(400)]
     out = []
@@ -84,6 +87,7 @@ def scenario(seed=11, ticks=5, big=False):
             key = "pod-%06d" % pid
             pid += 1
             ip = "10.0.%d.%d" % (rng.integers(0, 4), rng.integers(1, 255)) if rng.random() < 0.03 else ""
+            ip = ip if t >= foreign_from else ""
             pods.append(dict(op="new", key=key, node=str(rng.choice(names)), ip=ip,
                              phase=int(rng.choice([abi.PHASE_PENDING, abi.PHASE_PENDING, abi.PHASE_NONE])),
                              fin=bool(rng.random() < 0.3)))

@@ -215,20 +215,50 @@ def config_for(fx, **kw):
                        pod_slots_per_bucket=c["pod_slots_per_bucket"], **kw)
 
 
-def replay(fx, backend, check=True, on_tick=None, codec=None):
+def ingest_pods_mixed(backend, recs, arena, node_handle):
+    """The batch in event order, every record the compact form can carry as
+    kwok_pod_rec (kwok_ingest_pods_packed: its node by handle, node_handle maps
+    names to the handles the node ingest returned) and the rest (a pod naming a
+    node the engine holds no handle for) through kwok_ingest_pods, consecutive
+    records of one form in one call: applying the calls in order is applying
+    the batch.  Returns (handles, status, released) and the number of calls."""
+    from kwok_amd.controller import ingest_pods_wire
+    recs = recs.copy()
+    for i in range(len(recs)):
+        r = recs[i]
+        if r["op"] == abi.OP_UPSERT and r["handle"] < 0 and r["node_handle"] < 0:
+            name = bytes(arena[r["node_name"]["off"]:r["node_name"]["off"] + r["node_name"]["len"]]).decode()
+            r["node_handle"] = node_handle.get(name, -1)
+    hs, st, rel, calls = ingest_pods_wire(backend, recs, arena)
+    return (hs, st, rel), calls
+
+
+def replay(fx, backend, check=True, on_tick=None, codec=None, packed=False):
     """Replay a fixture through backend; assert equality tick by tick.  With a
-    codec, events travel as Kubernetes JSON objects decoded by the host codec."""
+    codec, events travel as Kubernetes JSON objects decoded by the host codec;
+    packed: pods travel in the compact form where it can carry them
+    (ingest_pods_mixed)."""
     specs = SpecCache(backend)
+    node_handle = {}
     for ti, t in enumerate(fx["ticks"]):
         if t["node_events"]:
             recs, arena = json_node_batch(t["node_events"], codec) if codec else node_batch(t["node_events"])
             hs, st = backend.ingest_nodes_raw(recs, arena)
+            for e, h, s_ in zip(t["node_events"], hs, st):
+                if s_ == 0:
+                    if e["op"] == "delete":
+                        node_handle.pop(e["name"], None)
+                    else:
+                        node_handle[e["name"]] = int(h)
             if check:
                 assert list(st) == [0] * len(st), (ti, list(st))
                 assert list(hs) == [e["expect_handle"] for e in t["node_events"]], ti
         if t["pod_events"]:
             recs, arena = json_pod_batch(t["pod_events"], specs, codec) if codec else pod_batch(t["pod_events"], specs)
-            hs, st, _rel = backend.ingest_pods_raw(recs, arena)
+            if packed:
+                (hs, st, _rel), _calls = ingest_pods_mixed(backend, recs, arena, node_handle)
+            else:
+                hs, st, _rel = backend.ingest_pods_raw(recs, arena)
             if check:
                 assert list(st) == [0] * len(st), (ti, list(st))
                 assert list(hs) == [e["expect_handle"] for e in t["pod_events"]], ti

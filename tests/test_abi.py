@@ -43,6 +43,7 @@ def test_oracle_library_exports():
             name = name.replace("engine_", "")
         if f in ("kwok_abi_version", "kwok_comm_id", "kwok_finalizer_patch", "kwok_device_outputs",
                  "kwok_host_alloc", "kwok_host_free",  # engine only: page-locked batch buffers
+                 "kwok_pack_pod_events",  # host helper of the compact wire form (engine library)
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
                  "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
@@ -58,6 +59,7 @@ STRUCTS = {
                                         "capacity", "node_info"]),
     "kwok_pod_event": (abi.PodEvent, ["op", "phase", "flags", "handle", "spec_id", "node_handle", "creation_unix",
                                       "node_name", "host_ip", "pod_ip"]),
+    "kwok_pod_rec": (abi.PodRec, ["op", "flags", "spec_id", "target", "creation", "host_ip", "pod_ip"]),
     "kwok_pod_spec": (abi.PodSpec, ["containers", "n_containers", "init_containers", "n_init_containers",
                                     "readiness_gates", "n_readiness_gates"]),
     "kwok_config": (abi.Config, ["abi_version", "cidr", "node_ip", "start_time_unix", "enable_cni",
@@ -102,6 +104,7 @@ def test_struct_layout_matches_header():
             assert int(got["%s.%s" % (cname, f)]) == getattr(st, f).offset, (cname, f)
     assert abi.NODE_EVENT_DTYPE.itemsize == C.sizeof(abi.NodeEvent)
     assert abi.POD_EVENT_DTYPE.itemsize == C.sizeof(abi.PodEvent)
+    assert abi.POD_REC_DTYPE.itemsize == C.sizeof(abi.PodRec) == 20
 
 
 def test_bucket_helpers():

@@ -21,7 +21,10 @@ from oracle.oracle import Oracle
 pytestmark = pytest.mark.gpu
 
 
-def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None):
+def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None,
+              packed=False):
+    """packed: the engine ingests the compact wire form (kwok_ingest_pods_packed),
+    the oracle the same events as kwok_pod_event with dotted quads"""
     if threads is not None:
         os.environ["KWOK_INGEST_THREADS"] = str(threads)
     try:
@@ -37,11 +40,18 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
     compare_tick(e, o, "churn initial tick")
     ch = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11,
                         alloc=alloc)
+    chp = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11,
+                         alloc=alloc, packed=True) if packed else None
     dump = lambda: o.dump_pods(0, n_handles)  # noqa: E731
     for t in range(ticks):
         now += 30
         ev, ar = ch.batch(dump, now)
-        h1, s1, r1 = e.ingest_pods_raw(ev, ar)
+        if packed:
+            recs, _ = chp.batch(dump, now)
+            h1, s1, r1 = e.ingest_pods_packed(recs)
+            chp.applied(h1.copy(), s1)
+        else:
+            h1, s1, r1 = e.ingest_pods_raw(ev, ar)
         h2, s2, r2 = o.ingest_pods_raw(ev, ar)
         assert (h1 == h2).all() and (s1 == s2).all() and (r1 == r2).all(), "churn tick %d ingest" % t
         ch.applied(h1, s1)
@@ -66,3 +76,17 @@ def test_churn_threaded_ingest_parity(threads):
 def test_c4_churn_metric_size():
     """1M nodes x 10M pods, 1M deletes (50% finalizers) + 1M creates per tick"""
     run_churn(1_000_000, 1_000_000, 2, full_state=False)
+
+
+@pytest.mark.timeout(900)
+def test_c4_churn_metric_size_packed():
+    """the same churn storm with the engine fed the compact wire form (20 B per
+    record, kwok_ingest_pods_packed, page-locked and read in place), the
+    oracle the full kwok_pod_event records: equal per record and per tick"""
+    from kwok_amd.engine import host_array
+    run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=True, alloc=host_array)
+
+
+def test_churn_packed_parity():
+    """20k nodes x 200k pods, 40k + 40k per tick, compact records in pageable memory"""
+    run_churn(20_000, 40_000, 3, packed=True)

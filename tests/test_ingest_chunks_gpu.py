@@ -32,12 +32,26 @@ def test_growth_chunked(monkeypatch):
     test_growth_gpu.test_1000_pods_on_one_node_grow(None, monkeypatch)
 
 
+@pytest.mark.parametrize("packed", [False, True], ids=["events", "packed"])
 @pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
-def test_churn_chunked(pinned, monkeypatch):
+def test_churn_chunked(pinned, packed, monkeypatch):
     """20k nodes x 200k pods, 40k deletes + 40k creates per tick in chunks of
-    ~7001: batches in page-locked memory (DMA) and in pageable memory (staged)"""
+    ~7001: batches in page-locked memory (DMA) and in pageable memory (staged),
+    as kwok_pod_event and in the compact form"""
     monkeypatch.setenv("KWOK_INGEST_CHUNK", "7001")
-    run_churn(20_000, 40_000, 3, alloc=host_array if pinned else None)
+    run_churn(20_000, 40_000, 3, alloc=host_array if pinned else None, packed=packed)
+
+
+@pytest.mark.parametrize("chunk", ["1", "3"])
+@pytest.mark.parametrize("name", harness.TRACES)
+def test_golden_trace_packed_chunked(name, chunk, monkeypatch):
+    """the golden traces with the pods in the compact form where it carries
+    them (harness.ingest_pods_mixed), in tiny chunks"""
+    monkeypatch.setenv("KWOK_INGEST_CHUNK", chunk)
+    fx = harness.load_trace(name)
+    e = Engine(harness.config_for(fx))
+    harness.replay(fx, e, packed=True)
+    e.close()
 
 
 def test_failed_chunk_after_an_applied_one_poisons(monkeypatch):

@@ -20,6 +20,17 @@ def test_engine_golden_trace(name):
 
 
 @pytest.mark.parametrize("name", harness.TRACES)
+def test_engine_golden_trace_packed(name):
+    """Pods in the compact wire form (kwok_ingest_pods_packed) wherever it can
+    carry them, read in place from page-locked memory when the batch is one
+    chunk: same goldens"""
+    fx = harness.load_trace(name)
+    e = Engine(harness.config_for(fx))
+    harness.replay(fx, e, packed=True)
+    e.close()
+
+
+@pytest.mark.parametrize("name", harness.TRACES)
 def test_engine_golden_trace_via_json(name):
     """Events as Kubernetes JSON objects through the host codec
     (kwok_decode_node / kwok_decode_pod) into the HIP engine: same goldens."""

@@ -59,7 +59,8 @@ def test_failed_exchange_poisons_engine(monkeypatch, pair):
     calls = {"long": 0}
 
     def gather(user, send, nbytes, recv):
-        if nbytes != 8 * 4 + 16 * 8 + 2048 * 4:  # not the fixed-size message: the long-list exchange
+        # (XMsg: alloc, n_use, n_rel, seq, foreign, counters[16], ips[XINLINE])
+        if nbytes != 8 * 5 + 16 * 8 + 2048 * 4:  # not the fixed-size message: the long-list exchange
             calls["long"] += 1
             return 1
         C.memmove(recv, send, nbytes)
