@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--once-ticks", type=int, default=1, help="the KWOK_CFG_HEARTBEAT_ONCE leg (N=1; 0: skip)")
     ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
                                                          "metric size: 2M create/delete per tick)")
+    ap.add_argument("--emulate-ranks", type=int, default=8, help="N=1: a one-rank RCCL engine folding this many "
+                                                                 "ranks' exchange messages (0: skip)")
     return ap.parse_args()
 
 
@@ -276,6 +278,60 @@ def heartbeat_once_leg(nodes, steps, warmup):
                          "achieved": state_bytes / (kern * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": state_bytes / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "note": "SoA state read + written per tick (node 9 + 9 B, pod 10 B) over the k_tick launch"}}
+
+
+def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
+    """The per-rank cost of the multi-rank exchange at N = `ranks`, on one GPU:
+    a one-rank engine on the FRONT / RCCL allgather / BACK path
+    (KWOK_FORCE_MULTI) whose BACK launch folds `ranks` exchange messages - its
+    own and `ranks` - 1 copies with their addresses moved inside the CIDR
+    (KWOK_EMULATE_RANKS) - so every tick commits `ranks` ranks' Gets and applies
+    their Uses and Puts to the replicated pool, as each rank of an N-GPU run
+    does.  The fleet is one rank's (1M x 10M) under the CIDR an
+    N-rank fleet takes.  Steady ticks (queued) and C4 churn ticks (1M + 1M per
+    rank per tick: `ranks` x 1M releases and Gets per tick at every rank).
+    Diagnostics: the pool's addresses stop matching a real fleet after the
+    first emulated tick, so nothing here is checked against the oracle."""
+    env = {"KWOK_FORCE_MULTI": "1", "KWOK_EMULATE_RANKS": str(ranks)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        e, fl, pods = workload.build_engine_fleet(keng.Engine, nodes, comm_id=keng.comm_id(),
+                                                  cidr=cidr_for(nodes * workload.PODS_PER_NODE * ranks))
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    now = workload.S0 + 30
+    e.tick(now, read=False)
+    for _ in range(3):
+        now += 30
+        e.tick(now, read=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        now += 30
+        e.tick(now, read=False)
+    dt = (time.perf_counter() - t0) / steps
+    e.profile_enable(True)
+    for _ in range(10):
+        now += 30
+        e.tick(now, read=False)
+    ph, nt = e.profile_read()
+    e.profile_enable(False)
+    churn = None
+    if churn_ticks:
+        now, _, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
+    e.close()
+    return {"ranks": ranks, "workload": "one rank's 1M x 10M fleet; BACK folds %d ranks' exchange messages and lists "
+                                        "(KWOK_FORCE_MULTI + KWOK_EMULATE_RANKS, one-rank RCCL allgather)" % ranks,
+            "steady_ms_per_tick": dt * 1e3, "steady_phase_ms": {k: v / max(nt, 1) for k, v in ph.items()},
+            "churn": None if churn is None else {k: churn[k] for k in ("ms_per_step", "ingest_ms", "tick_ms",
+                                                                       "kernel_ms", "exchange_ms", "median_ms")},
+            "note": "blocking kwok_tick steps; the allgather is a one-rank copy (the xGMI transfer of N ranks' "
+                    "8 KiB messages / MB lists is not in it)"}
 
 
 def flap_leg(nodes, ticks):
@@ -485,6 +541,8 @@ def main():
     e.close()
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
     hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup) if world == 1 and a.once_ticks else None
+    emul = emulated_ranks_leg(a.nodes_per_rank, a.emulate_ranks, 20, min(a.churn_ticks, 3)) \
+        if world == 1 and a.emulate_ranks > 1 and not REHEARSAL else None
 
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
@@ -571,6 +629,8 @@ def main():
             out["flap"] = flap
         if hb_once is not None:
             out["heartbeat_once"] = hb_once
+        if emul is not None:
+            out["emulated_ranks"] = emul
         if world == 1 and a.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.nodes_per_rank, a.cpu_threads, a.cpu_ticks)
         sys.stdout.flush()

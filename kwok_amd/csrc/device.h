@@ -64,6 +64,9 @@ constexpr int ROW_BATCH = KWOK_ROW_BATCH; // further pod rows per thread loaded 
 #define KWOK_NODE_PRE 4
 #endif
 constexpr int NODE_PRE = KWOK_NODE_PRE;   // node chunks of a chain block loaded in its first round trip
+#ifndef KWOK_RT1_NODES_FIRST
+#define KWOK_RT1_NODES_FIRST 1              // ... issued before the speculative pod groups
+#endif
 // split ticks (k_pod_jobs): a chain block's live groups in runs of 64, one wave each
 constexpr int WC_GROUPS = 64;
 constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block

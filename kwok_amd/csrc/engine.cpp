@@ -124,6 +124,7 @@ struct kwok_engine {
     kwok_config cfg{};
     std::string err;
     int W = 1, rank = 0, dev = 0;
+    int XW = 1;  // exchange messages per tick: W, or KWOK_EMULATE_RANKS on a one-rank multi engine (diagnostics)
     bool multi = false;  // the FRONT / exchange / BACK tick (W > 1, or KWOK_FORCE_MULTI with one rank)
     uint32_t B = 0, Cn = 0, Cp = 0, b_lo = 0, b_hi = 0, nb = 0, NL = 0, PL = 0;
     uint32_t Hs = 0;  // pod handle stride: handle = bucket * Hs + slot in the bucket; Cp grows up to it
@@ -293,6 +294,17 @@ struct kwok_engine {
     uint32_t* d_xsend = nullptr;
     uint32_t* d_xrecv = nullptr;
     size_t xlist_cap = 0;
+    // TICK_XSPEC: after a tick whose lists were too long to be inline, the next
+    // ticks send their lists in a second allgather right behind the messages (no
+    // host round trip) with capacities from that tick's longest lists; every rank
+    // takes the same decisions (from the same gathered messages, in lockstep)
+    uint32_t xspec_u = 0, xspec_r = 0;  // capacities per rank (0: off)
+    uint32_t xspec_ttl = 0;             // ticks left
+    uint32_t xspec_alloc = 0;           // entries allocated per rank in d_ssend / d_srecv
+    uint32_t* d_ssend = nullptr;
+    uint32_t* d_srecv = nullptr;
+    int xspec_env = -1;                 // KWOK_XSPEC: 0 off, N: ticks kept on after a long-list tick (default 256)
+    uint64_t xspec_miss = 0;  // diagnostics: speculative ticks whose lists did not fit
     uint32_t n_stream = 0;      // k_tick heartbeat streamer blocks (the chain blocks: S.n_chain)
     uint32_t emit_grid = 0;     // k_emit blocks
     bool emit_hint = true;      // events were ingested since the last submit: the tick likely emits patches
@@ -1211,9 +1223,9 @@ void kwok_engine_destroy(kwok_engine* e) {
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg,
                     e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
-                    e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv};
+                    e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv, e->d_ssend, e->d_srecv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& T : e->slots) free_slot(T);
@@ -1406,7 +1418,11 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pod_stride = e->Hs;
     S.pool = e->pool;
     S.node_ip = e->node_ip;
-    S.world = W;
+    e->XW = W;
+    if (const char* v = getenv("KWOK_XSPEC")) e->xspec_env = atoi(v);
+    if (const char* v = getenv("KWOK_EMULATE_RANKS"))
+        if (e->multi && W == 1) e->XW = std::max(1, std::min(atoi(v), 64));
+    S.world = e->XW;  // the messages BACK folds
     S.multi = e->multi ? 1 : 0;
     S.cni = cfg->enable_cni ? 1u : 0u;
     S.custom_pod = (cfg->custom_templates & KWOK_TPL_POD) ? 1u : 0u;
@@ -1437,14 +1453,14 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.list_counts, 2)) || (rc = dalloc(e, &e->d_pod_fill, e->nb)) || (rc = dalloc(e, &S.pool_index, 1)) ||
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
         (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
-        (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
+        (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &S.list_blk, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
         (rc = dalloc(e, &S.wc_pre, (size_t)S.n_chain * MAX_WC)) ||
         (rc = dalloc(e, &S.wc_dirty, (size_t)S.n_chain * WC_DIRTY_WORDS)) || (rc = dalloc(e, &S.jbase, (size_t)S.n_chain)) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
-        (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(W, 1))) ||
+        (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(e->XW, 1))) ||
         (rc = alloc_slot(e, 0)))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
@@ -1473,9 +1489,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     S.pod_fill = e->d_pod_fill;
     S.rank = e->rank;
     if (e->multi) {
-        if ((rc = dalloc(e, &e->d_xall, (size_t)W))) return bail(rc);
+        if ((rc = dalloc(e, &e->d_xall, (size_t)e->XW))) return bail(rc);
         S.xall = e->d_xall;
-        if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * W, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc((void**)&e->h_xall, sizeof(XMsg) * e->XW, hipHostMallocDefault) != hipSuccess)
             return bail(KWOK_ENOMEM);
         if (cfg->comm_id) {
             ncclUniqueId id;
@@ -2299,10 +2315,27 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         // gathered messages and applies the inline lists itself (no host round trip).
         // Lists too long to be inline: BACK flags it and the host finishes the tick
         // with a second allgather (finish_long_lists).
+        // After a long-list tick (TICK_XSPEC): the lists follow in a second allgather
+        // of fixed capacity and k_pool_apply_spec applies them if every rank's fit.
+        if (!requeue && e->xspec_ttl && --e->xspec_ttl == 0) e->xspec_u = e->xspec_r = 0;
+        const bool spec = e->xspec_u + e->xspec_r != 0;
+        if (spec) {
+            S.xcap_u = e->xspec_u, S.xcap_r = e->xspec_r;
+            launch_gather_lists(S, e->d_ssend, st, S.xcap_u, S.xcap_u, S.xcap_r);
+            HIPCHK(e, hipGetLastError());
+        }
         rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
         if (rc) return rc;
-        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof, T.tag, T.target, st,
-                    ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
+        launch_emulate_msgs(S, e->d_xall, (uint32_t)e->XW, st);  // (diagnostics only: XW > W)
+        if (spec) {
+            const uint32_t per = S.xcap_u + S.xcap_r;
+            if ((rc = exchange(e, e->d_ssend, (size_t)per * 4, e->d_srecv))) return rc;
+            launch_emulate_lists(S, e->d_srecv, per, (uint32_t)e->XW, per, st);  // (diagnostics)
+            launch_pool_apply_spec(S, e->d_srecv, st);
+            HIPCHK(e, hipGetLastError());
+        }
+        launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_BACK | prof | (spec ? TICK_XSPEC : 0), T.tag,
+                    T.target, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
         HIPCHK(e, hipGetLastError());
     }
     if (T.split) {
@@ -2327,35 +2360,62 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     // the skipped tick's allgather re-gathered the same messages (its FRONT did not run)
     if (int rc = release_for_host(e)) return rc;
     HIPCHK(e, hipStreamSynchronize(st));
-    HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->W, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipMemcpyAsync(e->h_xall, e->d_xall, sizeof(XMsg) * e->XW, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
-    uint64_t maxl = 0;
-    for (int r = 0; r < e->W; r++) maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
+    uint64_t maxl = 0, mu = 0, mr = 0;
+    for (int r = 0; r < e->XW; r++) {
+        maxl = std::max<uint64_t>(maxl, e->h_xall[r].n_use + e->h_xall[r].n_rel);
+        mu = std::max<uint64_t>(mu, e->h_xall[r].n_use);
+        mr = std::max<uint64_t>(mr, e->h_xall[r].n_rel);
+    }
+    if (e->xspec_env != 0) {
+        // the next ticks' speculative list exchange: room for 1.25x this tick's
+        // longest lists (the same on every rank: the gathered messages)
+        if (e->xspec_u + e->xspec_r) e->xspec_miss++;
+        auto cap = [](uint64_t m) { return (uint32_t)std::min<uint64_t>(((m + m / 4) | 1023) + 1, 1u << 30); };
+        const bool miss = e->xspec_u + e->xspec_r != 0;  // a speculative tick whose lists did not fit: grow
+        const uint32_t cu = miss ? std::max(e->xspec_u, cap(mu)) : cap(mu), cr = miss ? std::max(e->xspec_r, cap(mr)) : cap(mr);
+        if (cu + cr > e->xspec_alloc) {
+            if (e->d_ssend) (void)hipFree(e->d_ssend);
+            if (e->d_srecv) (void)hipFree(e->d_srecv);
+            e->d_ssend = e->d_srecv = nullptr;
+            e->xspec_alloc = 0;
+            if (hipMalloc((void**)&e->d_ssend, (size_t)(cu + cr) * 4) != hipSuccess ||
+                hipMalloc((void**)&e->d_srecv, (size_t)(cu + cr) * 4 * e->XW) != hipSuccess)
+                return e->fail(KWOK_ENOMEM, "speculative exchange lists");
+            e->xspec_alloc = cu + cr;
+        }
+        e->xspec_u = cu, e->xspec_r = cr;
+        e->xspec_ttl = e->xspec_env > 0 ? (uint32_t)e->xspec_env : 256u;
+    }
     if (maxl > e->xlist_cap) {
         if (e->d_xsend) (void)hipFree(e->d_xsend);
         if (e->d_xrecv) (void)hipFree(e->d_xrecv);
         e->xlist_cap = maxl;
         if (hipMalloc((void**)&e->d_xsend, maxl * 4) != hipSuccess ||
-            hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->W) != hipSuccess)
+            hipMalloc((void**)&e->d_xrecv, maxl * 4 * e->XW) != hipSuccess)
             return e->fail(KWOK_ENOMEM, "exchange lists");
     }
     int rc = bind_slot(e, k);
     if (rc) return rc;
     HIPCHK(e, hipMemsetAsync(&S.bar->skip, 0, sizeof(uint32_t), st));
     const XMsg& me = e->h_xall[e->rank];
-    if (me.n_use) HIPCHK(e, hipMemcpyAsync(e->d_xsend, S.use_list, me.n_use * 4, hipMemcpyDeviceToDevice, st));
-    if (me.n_rel) HIPCHK(e, hipMemcpyAsync(e->d_xsend + me.n_use, S.rel_list, me.n_rel * 4, hipMemcpyDeviceToDevice, st));
+    if (me.n_use + me.n_rel) {  // the chain blocks' list segments, gathered in block order
+        launch_gather_lists(S, e->d_xsend, st);
+        HIPCHK(e, hipGetLastError());
+    }
     rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
     if (rc) return rc;
-    std::vector<ListDesc> ld(e->W);
-    for (int r = 0; r < e->W; r++) {
+    launch_emulate_lists(S, e->d_xrecv, maxl, (uint32_t)e->XW, (uint32_t)(me.n_use + me.n_rel), st);  // (diagnostics)
+    std::vector<ListDesc> ld(e->XW);
+    for (int r = 0; r < e->XW; r++) {
         ld[r].use = e->d_xrecv + (size_t)r * maxl;
         ld[r].rel = e->d_xrecv + (size_t)r * maxl + e->h_xall[r].n_use;
         ld[r].n_use = (uint32_t)e->h_xall[r].n_use;
         ld[r].n_rel = (uint32_t)e->h_xall[r].n_rel;
     }
-    HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->W, hipMemcpyHostToDevice, st));
-    launch_pool_apply(S, e->d_ld, e->W, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
+    HIPCHK(e, hipMemcpyAsync(e->d_ld, ld.data(), sizeof(ListDesc) * e->XW, hipMemcpyHostToDevice, st));
+    launch_pool_apply(S, e->d_ld, e->XW, (uint32_t)maxl, st);  // every rank's Uses, then Puts pending
     launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed,
                 TICK_BACK | TICK_XLISTS | (T.split ? TICK_SPLIT : 0), T.tag, T.target, st);
     HIPCHK(e, hipGetLastError());

@@ -85,6 +85,8 @@ struct DevState {
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
+    uint32_t* list_blk;        // multi rank: [n_chain][2] the block's Use / release list lengths; its entries sit in
+                               // use_list / rel_list from its first pod slot (bk0 * cp) on
     uint4* wc_pre;             // split ticks: [n_chain][MAX_WC] in-block exclusive prefix of (del, pp, pp bytes, alloc)
     uint32_t* wc_dirty;        //   per 64-group wave chunk, and [n_chain][WC_DIRTY_WORDS] its dirty bits (FRONT)
     JobBase* jbase;            //   [n_chain] (BACK) -> k_pod_jobs
@@ -98,6 +100,7 @@ struct DevState {
     uint32_t custom_pod;       // Config.PodStatusTemplate is custom: the caller's CONFORMS digest is ignored
     uint32_t use_events_only;  // this tick Use-checks only pods with an event (a quiet tick: kwok_tick_submit)
     uint32_t foreign;          // multi rank: this rank's sticky foreign-IP flag, sent in the exchange message
+    uint32_t xcap_u, xcap_r;   // multi rank, TICK_XSPEC: the list allgather's Use / release capacity per rank
     uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
@@ -114,6 +117,16 @@ void launch_apply_ops(const DevState& S, const NodeOp* nops, uint32_t nn, const 
                       hipStream_t st);
 void launch_pool_puts_now(const DevState& S, const uint32_t* ips, uint32_t n, hipStream_t st);
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st);
+// multi rank, long lists: the chain blocks' Use / release segments -> dst (uses, then releases, canonical order);
+// rel_at: where the releases start (~0u: right after the uses); cap_u / cap_r: entries kept (the rest dropped)
+void launch_gather_lists(const DevState& S, uint32_t* dst, hipStream_t st, uint32_t rel_at = ~0u,
+                         uint32_t cap_u = ~0u, uint32_t cap_r = ~0u);
+// TICK_XSPEC: every rank's gathered lists (rank r at recv + r * (cap_u + cap_r), releases from cap_u) into
+// `used` / rel_bm when every rank's lists fit the capacities (the messages say); otherwise nothing
+void launch_pool_apply_spec(const DevState& S, const uint32_t* recv, hipStream_t st);
+// KWOK_EMULATE_RANKS diagnostics: xw - 1 synthetic ranks' messages / long lists from this rank's
+void launch_emulate_msgs(const DevState& S, XMsg* X, uint32_t xw, hipStream_t st);
+void launch_emulate_lists(const DevState& S, uint32_t* recv, uint64_t maxl, uint32_t xw, uint32_t n, hipStream_t st);
 // EnableCNI: handles of the pods the next tick evaluates that hold no podIP
 // (configurePod's cni.Setup set), appended in any order at out[*count]
 void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStream_t st);
@@ -123,7 +136,9 @@ void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStr
 // with work to emit, so they must be co-resident (tick_occupancy).
 constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16,  // NOSTREAM: diagnostics only
               TICK_XLISTS = 32,  // BACK: the exchange lists were applied by k_pool_apply
-              TICK_SPLIT = 64;   // the pod jobs are built by k_pod_jobs after the tick's launch(es)
+              TICK_SPLIT = 64,   // the pod jobs are built by k_pod_jobs after the tick's launch(es)
+              TICK_XSPEC = 128;  // BACK: the lists went out in a second allgather of capacity xcap_u + xcap_r
+                                 // and k_pool_apply_spec applied them if every rank's fit
 // tag: this tick's nonzero id (single-rank dirty records); arrive_target: the
 // arrival count at which every chain block of this FRONT launch has arrived
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,

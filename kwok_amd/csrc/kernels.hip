@@ -505,15 +505,25 @@ constexpr uint64_t SPIN_LIMIT = 200000000ull;  // 2 s at 100 MHz
 
 // append x to a device list with one atomic per wave; entries are stored
 // write-through: the FRONT launch's last arriver reads them (multi-rank)
-__device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* list, uint32_t* counter) {
+// multi rank: the chain block's exchange lists.  Each block appends to its own
+// segment of use_list / rel_list (from its first pod slot: a block never holds
+// more entries than pod slots) through LDS counters, so an append costs no
+// global round trip; the lengths go out with the block's record
+// (publish_and_arrive) and the segments are gathered in block order.
+__device__ __forceinline__ uint32_t* list_lds() {
+    __shared__ uint32_t c[3];  // Use count, release count, the segment base (the block's first pod slot)
+    return c;
+}
+__device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* list, int which) {
     uint64_t m = __ballot(pred);
     if (!m) return;
     uint32_t base = 0;
     const int l = lane_id();
     int leader = __ffsll((unsigned long long)m) - 1;
-    if (l == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    uint32_t* c = list_lds();
+    if (l == leader) base = atomicAdd(&c[which], (uint32_t)__popcll(m));
     base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-    if (pred) st32_sc1(&list[base + __popcll(m & ((1ull << l) - 1))], x);
+    if (pred) st32_sc1(&list[c[2] + base + __popcll(m & ((1ull << l) - 1))], x);
 }
 
 // publish this block's record and arrive; returns the arrival counter before
@@ -522,6 +532,7 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t x, uint32_t* lis
 // block's other stores (output lists) are issued after the arrival.
 __device__ __forceinline__ uint64_t publish_and_arrive(const DevState& S, uint32_t b, const uint32_t (&rec)[AG_STRIDE]) {
     __shared__ unsigned long long sh_old;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's list entries (wave_append)
     __syncthreads();
     if (threadIdx.x < 64) {
         const int l = lane_id();
@@ -532,6 +543,7 @@ __device__ __forceinline__ uint64_t publish_and_arrive(const DevState& S, uint32
                 if (l == i) v = (uint64_t)rec[2 * i] | (uint64_t)rec[2 * i + 1] << 32;
             st_sc1(reinterpret_cast<uint64_t*>(S.blockagg + (size_t)b * AG_STRIDE) + l, v);
         }
+        if (l < 2) st32_sc1(&S.list_blk[2 * b + l], list_lds()[l]);  // the block's list lengths
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (l == 0)
             sh_old = __hip_atomic_fetch_add(&S.bar->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -567,6 +579,12 @@ __device__ __forceinline__ void wait_arrivals(const DevState& S, uint64_t target
 }
 
 // sense-reversal barrier among the n blocks of the pool phase
+// TICK_XSPEC: every rank's lists fit the speculative exchange's capacities
+__device__ __forceinline__ bool spec_fits(const DevState& S) {
+    bool ok = true;
+    for (int r = 0; r < S.world; r++) ok &= S.xall[r].n_use <= S.xcap_u && S.xall[r].n_rel <= S.xcap_r;
+    return ok;
+}
 __device__ __forceinline__ void pool_barrier(const DevState& S, uint32_t n) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -920,7 +938,7 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
                 if (r && !one) atomicOr((unsigned long long*)&S.rel_bm[bit >> 6], 1ull << (bit & 63));
 #endif
             } else {
-                wave_append(r, ip, S.rel_list, &S.list_counts[1]);  // ballots over every lane
+                wave_append(r, ip, S.rel_list, 1);  // ballots over every lane
             }
             if ((m.need >> k) & 1) {
                 const uint32_t sp = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
@@ -928,10 +946,8 @@ __device__ __forceinline__ uint32_t count_group(const DevState& S, const PodGrp&
             }
         }
         f[AG_PP_BYTES] += bytes;
-        // multi rank: the release list entries are performed before this block
-        // arrives (publish_and_arrive drains only wave 0); a single-rank block
-        // drains every wave before its arrival, so its loads stay in flight here
-        if (S.multi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (multi rank: the release list entries are drained before the block's
+        // arrival, publish_and_arrive)
     }
     return bytes;
 }
@@ -993,10 +1009,9 @@ __device__ __forceinline__ void apply_uses(const DevState& S, const PodGrp& g, u
             if (!S.multi) {
                 if (u) atomicOr((unsigned long long*)&S.used_bm[bit >> 6], 1ull << (bit & 63));
             } else {
-                wave_append(u, ip, S.use_list, &S.list_counts[0]);
+                wave_append(u, ip, S.use_list, 0);
             }
         }
-        if (S.multi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as in count_group)
     }
 }
 
@@ -1512,7 +1527,18 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
                                                    uint64_t c_p1, bool prof, uint32_t tag) {
     const uint64_t* tot = r.tot;
     const bool single = !S.multi;
-    const uint32_t nu = single ? 0u : ld32_sc1(&S.list_counts[0]), nr = single ? 0u : ld32_sc1(&S.list_counts[1]);
+    // multi rank: the blocks' list lengths (every block arrived: their records and lengths are out)
+    __shared__ uint32_t lsum[2];
+    if (threadIdx.x < 2) lsum[threadIdx.x] = 0;
+    __syncthreads();
+    if (!single) {
+        uint32_t u = 0, r = 0;
+        for (uint32_t b = threadIdx.x; b < S.n_chain; b += BLOCK) u += ld32_sc1(&S.list_blk[2 * b]), r += ld32_sc1(&S.list_blk[2 * b + 1]);
+        if (u) atomicAdd(&lsum[0], u);
+        if (r) atomicAdd(&lsum[1], r);
+    }
+    __syncthreads();
+    const uint32_t nu = lsum[0], nr = lsum[1];
     uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     clk[CLK_P1_MAX] = c_p1;
     if (prof) clk[CLK_ENTRY_MIN] = ~ld_sc1(&S.bar->neg_entry_max);
@@ -1547,9 +1573,18 @@ __device__ __forceinline__ void write_front_header(const DevState& S, const Sums
                                              S.arena_cap, single, clk);
         }
     }
-    if (!single && nu + nr <= (uint32_t)XINLINE) {  // exchange lists inline when they fit
-        for (uint32_t j = threadIdx.x; j < nu; j += BLOCK) S.xmsg->ips[j] = ld32_sc1(&S.use_list[j]);
-        for (uint32_t j = threadIdx.x; j < nr; j += BLOCK) S.xmsg->ips[nu + j] = ld32_sc1(&S.rel_list[j]);
+    if (!single && nu + nr <= (uint32_t)XINLINE && nu + nr) {  // exchange lists inline when they fit
+        uint32_t pu = 0, pr = nu;  // the blocks' segments in block order
+        for (uint32_t b = 0; b < S.n_chain; b++) {
+            const uint32_t cu = ld32_sc1(&S.list_blk[2 * b]), cr = ld32_sc1(&S.list_blk[2 * b + 1]);
+            if (!(cu | cr)) continue;
+            uint32_t bk0, nbk;
+            block_range(S, b, bk0, nbk);
+            const uint32_t seg = bk0 * S.cp;
+            for (uint32_t j = threadIdx.x; j < cu; j += BLOCK) S.xmsg->ips[pu + j] = ld32_sc1(&S.use_list[seg + j]);
+            for (uint32_t j = threadIdx.x; j < cr; j += BLOCK) S.xmsg->ips[pr + j] = ld32_sc1(&S.rel_list[seg + j]);
+            pu += cu, pr += cr;
+        }
     }
 }
 
@@ -1831,6 +1866,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (t < 3) sh_mask[t] = 0;
         const bool single = !S.multi;
+        if (t < 3) list_lds()[t] = t == 2 ? bk0 * S.cp : 0u;  // (multi rank: the block's list segment)
         const bool split = (phases & TICK_SPLIT) != 0;
         uint32_t* wcnt = recs;  // split: the 64-group runs' counts (recs is free until reduce_records)
         if (split)
@@ -1848,11 +1884,16 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         // issue order, so the node classification below waits for these and the fill
         // marks only, not for the pod groups behind them
         uint32_t packed_pre[NODE_PRE];
+        auto load_nodes = [&]() {
 #pragma unroll
-        for (int c = 0; c < NODE_PRE; c++) {
-            const uint32_t i = (uint32_t)c * NODE_CHUNK + t * NODE_PER_THREAD;
-            packed_pre[c] = i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u;
-        }
+            for (int c = 0; c < NODE_PRE; c++) {
+                const uint32_t i = (uint32_t)c * NODE_CHUNK + t * NODE_PER_THREAD;
+                packed_pre[c] = i < nn ? *reinterpret_cast<const uint32_t*>(S.node_state + nbase + i) : 0u;
+            }
+        };
+#if KWOK_RT1_NODES_FIRST
+        load_nodes();
+#endif
         const uint32_t fill = jv ? S.pod_fill[bk0 + j] : 0u;
         PodGrp G[SPEC_GROUPS];
 #pragma unroll
@@ -1860,6 +1901,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             const uint32_t a = l + q * tpb;
             load_group_at(S, jv && a < gcap ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u, j, G[q], false);
         }
+#if !KWOK_RT1_NODES_FIRST
+        load_nodes();
+#endif
         const uint64_t pool_index = single ? 0 : *S.pool_index;  // multi rank: the header's default cursor
         if (jv && l == 0) gpre[j + 1] = fill / POD_PER_THREAD;
         const uint16_t* smax = S.n_specs <= (uint32_t)SPEC_LDS ? spec_max : nullptr;
@@ -2139,7 +2183,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         }
         if (!step && b == 0 && t == 0) st_host(&S.hdr_host->err, TICK_ERR_SEQ);  // ranks out of step: results void
         xbase = base;
-        if (!(phases & TICK_XLISTS)) {
+        // TICK_XSPEC: the second allgather ran speculatively (the previous tick had long
+        // lists) and k_pool_apply_spec applied every rank's lists if they fit
+        const bool spec = (phases & TICK_XSPEC) && spec_fits(S);
+        if (!(phases & TICK_XLISTS) && !spec) {
             if (maxl > (uint32_t)XINLINE) {
                 // lists that did not fit inline: the host runs the second allgather,
                 // applies them and launches BACK again (TICK_XLISTS)
@@ -2314,6 +2361,34 @@ __global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
     }
 }
 
+// KWOK_EMULATE_RANKS (diagnostics, one rank): messages 1..xw-1 are copies of
+// this rank's message 0, their inline addresses moved by r * size / xw inside the
+// CIDR, so BACK folds and applies xw ranks' worth of Gets, Uses and Puts
+__device__ __forceinline__ uint32_t emul_shift(const PoolGeom& g, uint32_t ip, uint32_t r, uint32_t xw) {
+    if (!in_cidr(g, ip)) return ip;
+    return g.net + (uint32_t)(((uint64_t)(ip - g.net) + (g.size / xw) * r) % g.size);
+}
+__global__ void k_emulate_msgs(DevState S, XMsg* X, uint32_t xw) {
+    const uint32_t r = blockIdx.x + 1;
+    if (r >= xw) return;
+    const XMsg& m = X[0];
+    XMsg& o = X[r];
+    const uint32_t nl = (uint32_t)min<uint64_t>(m.n_use + m.n_rel, (uint64_t)XINLINE);
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) o.ips[i] = emul_shift(S.pool, m.ips[i], r, xw);
+    if (threadIdx.x == 0) {
+        o.alloc = m.alloc, o.n_use = m.n_use, o.n_rel = m.n_rel, o.seq = m.seq, o.foreign = m.foreign;
+        for (int k = 0; k < 16; k++) o.counters[k] = m.counters[k];
+    }
+}
+// ... and their long lists: slot 0 of each rank-major list block copied, moved
+__global__ void k_emulate_lists(DevState S, uint32_t* recv, uint64_t maxl, uint32_t xw, uint32_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)n * (xw - 1);
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(i / n) + 1, k = (uint32_t)(i % n);
+        recv[r * maxl + k] = emul_shift(S.pool, recv[k], r, xw);
+    }
+}
+
 __global__ void k_apply_node_ops(DevState S, const NodeOp* ops, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -2362,6 +2437,61 @@ void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStr
     hipLaunchKernelGGL(k_cni_pending, dim3(g ? g : 1), dim3(256), 0, st, S, out, count);
 }
 
+void launch_emulate_msgs(const DevState& S, XMsg* X, uint32_t xw, hipStream_t st) {
+    if (xw > 1) hipLaunchKernelGGL(k_emulate_msgs, dim3(xw - 1), dim3(256), 0, st, S, X, xw);
+}
+void launch_emulate_lists(const DevState& S, uint32_t* recv, uint64_t maxl, uint32_t xw, uint32_t n, hipStream_t st) {
+    if (xw > 1 && n) hipLaunchKernelGGL(k_emulate_lists, dim3(1024), dim3(256), 0, st, S, recv, maxl, xw, n);
+}
+// one block per chain block: its Use and release segments to their place in dst
+// (every block's Uses, then every block's releases, in block order)
+__global__ void k_gather_lists(DevState S, uint32_t* dst, uint32_t rel_at, uint32_t cap_u, uint32_t cap_r) {
+    const uint32_t b = blockIdx.x;
+    __shared__ uint32_t pre[4];  // Uses / releases of the blocks before b, all Uses
+    if (threadIdx.x < 4) pre[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t pu = 0, pr = 0, tu = 0;
+    for (uint32_t q = threadIdx.x; q < S.n_chain; q += blockDim.x) {
+        const uint32_t cu = S.list_blk[2 * q], cr = S.list_blk[2 * q + 1];
+        tu += cu;
+        if (q < b) pu += cu, pr += cr;
+    }
+    if (pu) atomicAdd(&pre[0], pu);
+    if (pr) atomicAdd(&pre[1], pr);
+    if (tu) atomicAdd(&pre[2], tu);
+    __syncthreads();
+    const uint32_t cu = S.list_blk[2 * b], cr = S.list_blk[2 * b + 1];
+    uint32_t bk0, nbk;
+    block_range(S, b, bk0, nbk);
+    const uint32_t seg = bk0 * S.cp;
+    const uint32_t r0 = rel_at == ~0u ? pre[2] : rel_at;
+    for (uint32_t j = threadIdx.x; j < cu && pre[0] + j < cap_u; j += blockDim.x) dst[pre[0] + j] = S.use_list[seg + j];
+    for (uint32_t j = threadIdx.x; j < cr && pre[1] + j < cap_r; j += blockDim.x) dst[r0 + pre[1] + j] = S.rel_list[seg + j];
+}
+void launch_gather_lists(const DevState& S, uint32_t* dst, hipStream_t st, uint32_t rel_at, uint32_t cap_u,
+                         uint32_t cap_r) {
+    hipLaunchKernelGGL(k_gather_lists, dim3(S.n_chain), dim3(256), 0, st, S, dst, rel_at, cap_u, cap_r);
+}
+__global__ void k_pool_apply_spec(DevState S, const uint32_t* recv) {
+    // a tick skipped behind one the host finishes (GridBar::skip): its FRONT did not run
+    if (__hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    if (!spec_fits(S)) return;  // BACK takes the long-list way (the host's second exchange)
+    const uint64_t per = (uint64_t)S.xcap_u + S.xcap_r;
+    for (int r = 0; r < S.world; r++) {
+        const uint32_t nu = (uint32_t)S.xall[r].n_use, nr = (uint32_t)S.xall[r].n_rel;
+        const uint32_t* base = recv + r * per;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu + nr; i += gridDim.x * blockDim.x) {
+            const bool use = i < nu;
+            const uint32_t ip = use ? base[i] : base[S.xcap_u + (i - nu)];
+            if (!in_cidr(S.pool, ip)) continue;
+            const uint64_t b = ip - S.pool.net;
+            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
+        }
+    }
+}
+void launch_pool_apply_spec(const DevState& S, const uint32_t* recv, hipStream_t st) {
+    hipLaunchKernelGGL(k_pool_apply_spec, dim3(1024), dim3(256), 0, st, S, recv);
+}
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st) {
     uint32_t g = max_n ? cdiv(max_n, 256) : 1;
     if (g > 1024) g = 1024;
