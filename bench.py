@@ -348,12 +348,14 @@ def flap_leg(nodes, ticks):
     ing = tck = 0.0
     trans = 0
     last = None
+    outs = (keng.host_array((2 * f.k,), np.int32), keng.host_array((2 * f.k,), np.int32))
     for k in range(ticks + 1):
         now += 30
-        ev, ar = f.batch()
+        # the batch as a watch client holds it: its own arena of the names, page-locked
+        ev, ar = f.batch(compact=True, alloc=keng.host_array)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        e.ingest_nodes_raw(ev, ar)
+        e.ingest_nodes_raw(ev, ar, out=outs)
         t1 = time.perf_counter()
         r = e.tick(now, read=False)
         t2 = time.perf_counter()

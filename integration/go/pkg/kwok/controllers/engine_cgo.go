@@ -194,18 +194,62 @@ func (g *gpuEngine) registerPodSpec(doc *C.kwok_pod_doc, arena []byte) (int32, e
 	return int32(id), nil
 }
 
-// ingestNodes / ingestPods: one batch of watch records in event order; per
-// record the handle and status (KWOK_OK, KWOK_EDOMAIN, ...).
-func (g *gpuEngine) ingestNodes(ev []C.kwok_node_event, arena []byte) (handles, status []int32, err error) {
-	handles, status = make([]int32, len(ev)), make([]int32, len(ev))
-	if len(ev) == 0 {
+// ingestNodes: one batch of node watch records in event order; per record the
+// handle and status (KWOK_OK, KWOK_EDOMAIN, ...).  The records go into the
+// page-locked record buffer and the strings they reference (the name, the status
+// JSON and nodeInfo fields) into the page-locked arena, which kwok_ingest_nodes'
+// prep kernel reads in place: the batch's object JSON stays on the host.
+func (g *gpuEngine) ingestNodes(evs []C.kwok_node_event, arena []byte) (handles, status []int32, err error) {
+	n := len(evs)
+	handles, status = make([]int32, n), make([]int32, n)
+	if n == 0 {
 		return
 	}
-	rc := C.kwok_ingest_nodes(g.h, &ev[0], C.size_t(len(ev)), arenaPtr(arena), C.size_t(len(arena)),
-		(*C.int32_t)(&handles[0]), (*C.int32_t)(&status[0]))
+	evp, err := g.evBuf.get(n * int(unsafe.Sizeof(evs[0])))
+	if err != nil {
+		return
+	}
+	ev := unsafe.Slice((*C.kwok_node_event)(evp), n)
+	strs := func(x *C.kwok_node_event) []*C.kwok_str {
+		out := []*C.kwok_str{&x.name, &x.addresses, &x.allocatable, &x.capacity}
+		for k := range x.node_info {
+			out = append(out, &x.node_info[k])
+		}
+		return out
+	}
+	need := 0
+	for i := range evs {
+		for _, s := range strs(&evs[i]) {
+			need += int(s.len)
+		}
+	}
+	arp, err := g.arBuf.get(need + 1)
+	if err != nil {
+		return
+	}
+	ar := unsafe.Slice((*byte)(arp), need+1)
+	off := 0
+	for i := range evs {
+		ev[i] = evs[i]
+		for _, s := range strs(&ev[i]) {
+			k := copy(ar[off:], arena[s.off:s.off+s.len])
+			s.off, s.len = C.uint32_t(off), C.uint32_t(k)
+			off += k
+		}
+	}
+	resp, err := g.resBuf.get(2 * 4 * n)
+	if err != nil {
+		return
+	}
+	res := unsafe.Slice((*int32)(resp), 2*n)
+	rc := C.kwok_ingest_nodes(g.h, &ev[0], C.size_t(n), (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(off),
+		(*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]))
 	if rc < 0 {
 		err = fmt.Errorf("kwok_ingest_nodes: %d: %s", int(rc), g.lastError())
+		return
 	}
+	copy(handles, res[:n])
+	copy(status, res[n:])
 	return
 }
 

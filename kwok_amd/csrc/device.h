@@ -215,7 +215,7 @@ struct PodOp {
 // pass reads these in bucket order (a stable sort of the batch by bucket).
 struct PodRec {             // 32 bytes
     uint32_t bucket;        // owned local bucket whose slots the record may change (REC_NONE: none)
-    uint32_t pos;           // existing: the handle's index in its bucket; create: the node's index
+    uint32_t pos;           // existing: the handle's index in its bucket; create by handle: the node's index
     uint32_t hip, pip;      // UPSERT: status.hostIP / status.podIP (0: empty); DELETE: the parsed podIP
     uint32_t ctime;
     uint16_t spec;          // UPSERT with fst == KWOK_OK: the spec id
@@ -229,23 +229,45 @@ constexpr uint32_t REC_NONE = 0xFFFFFFFFu;
 enum : uint8_t {
     REC_EXISTING = 1,  // handle >= 0
     REC_DEL_IP = 2,    // DELETE: the event's podIP parsed
-    REC_BY_NAME = 4,   // create naming its node by spec.nodeName: the host resolves it (pos)
-    REC_HARD = 8,      // by name, and the node entry could be freed before the record in event order:
-                       // the apply pass stops at it until the host resolves it
-    REC_RESOLVED = 16, // pos holds the node the host resolved
-    REC_FINAL = 32,    // the host gave the record its status (the apply pass skips it)
+    REC_BY_NAME = 4,   // create naming its node by spec.nodeName: the apply pass resolves the name in
+                       // the bucket's node directory when it reaches the record (a placeholder entry
+                       // if none, pod_controller.go routing of spec.nodeName)
 };
 // per-batch counters of the GPU ingest (device memory, read back by the host)
 struct IngSummary {
-    uint32_t n_byname;      // owned by-name creates listed for host resolution
+    uint32_t n_byname;      // owned by-name creates (diagnostics)
     uint32_t rejected;      // records with a status other than KWOK_OK
-    uint32_t n_freed;       // node slots the apply pass freed (deleted / placeholder nodes no pod references)
-    uint32_t n_stopped;     // buckets whose apply pass stopped at an unresolved REC_HARD record
+    uint32_t n_freed;       // node entries the apply pass freed (diagnostics)
+    uint32_t n_placeholders;  // placeholder node entries by-name creates made (diagnostics)
     uint32_t need;          // max over buckets with creates: live pods + creates (growth check)
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)
     uint32_t pad[2];
+};
+
+// ---- node directory (device-authoritative, ingest.hip) -------------------------
+// A node slot's name lives on the device: node_key[slot] = fnv1a32(name) | len << 32
+// (0: no entry), node_name[slot * NAME_STRIDE ...] its bytes.  A name's bucket is
+// fnv1a32(name) & (B - 1) (the reference's nodes are routed by name, node_controller.go:
+// 256-270); lookups compare the keys of the bucket's Cn slots, then the bytes.
+constexpr uint32_t NAME_STRIDE = 256;  // names are 1..253 bytes
+constexpr uint32_t NODE_NAME_MAX = 253;
+// A node watch record after the checks that depend on the record alone (k_nd_prep),
+// at its batch index; its name bytes at names[i * NAME_STRIDE].
+struct NodeRec {            // 16 bytes
+    uint32_t hash;          // fnv1a32(name)
+    uint8_t len, op, fl, pad;  // fl: NR_*
+    uint64_t blob;          // UPSERT: the node's init blob word (node_blob)
+};
+enum : uint8_t { NR_MANAGED = 1, NR_LOCKABLE = 2, NR_CONFORMS = 4, NR_HOST = 8 };
+// per-batch counters of a node batch (device memory, read back by the host)
+struct NodeSummary {
+    uint32_t n_host;        // UPSERT records whose status strings need the host (blob, conforms)
+    uint32_t rejected;
+    int32_t d_managed;      // managed-set size change
+    uint32_t changed;       // the managed set changed (heartbeat handle list epoch)
+    uint32_t freed, created, pad[2];
 };
 
 // spec descriptor: A | B | C segments of the pod patch (see templates.cpp)

@@ -137,51 +137,22 @@ struct kwok_engine {
     hipStream_t rst = nullptr;  // kwok_read_outputs: copies of a collected tick, beside the next tick's kernels
     DevState S{};
 
-    // ---- host mirrors (slot policy) ----
-    struct HNode {
-        std::string name;
-        uint8_t used = 0, exists = 0, managed = 0, lockable = 0;
-        uint8_t zombie = 0;  // used && !exists: a deleted node (or a placeholder) pods may still reference;
-                             // the entry is freed once none does (the device knows the references)
-        uint32_t hash = 0;   // fnv1a32(name): bucket (low bits) and name-table home
-    };
-    std::vector<HNode> nodes;                        // [NL]
-    // name -> node slot: per owned bucket, an open-addressing table (linear probing,
-    // backward-shift deletion) of local index + 1 (0: empty), at least twice the
-    // bucket's node capacity; names compare against the slot's mirror.  Replaces a
-    // node-based hash map per bucket (~4 dependent cache misses per lookup).
-    std::vector<uint32_t> name_tab;                  // [nb][name_mask + 1]
-    uint32_t name_mask = 0;
-    std::vector<uint64_t> node_bits;                 // occupancy bitset per bucket
+    // ---- nodes: the directory (names -> slots), occupancy, managed / zombie counts
+    // live on the device (ingest.hip); the host keeps the managed-set size ----
     uint64_t n_managed = 0;
-    std::vector<uint32_t> mb_count;                  // [nb] managed nodes per owned bucket
-    bool hb_pre_dirty = true;                        // the per-chain-block heartbeat bases need an upload
+    bool hb_pre_dirty = true;                        // the per-chain-block heartbeat bases need k_hb_pre
     uint32_t hb_epoch = 0;                           // kwok_tick_result.heartbeat_epoch: bumped when the managed set changes
-    uint32_t* hb_pre_h = nullptr;                    // pinned [n_chain + 1]
     uint32_t* d_hb_pre = nullptr;
-    std::vector<uint32_t> zb_count;                  // [nb] zombie node entries per owned bucket
     // pods: no host mirror.  The device's pod_state (USED = slot occupancy),
     // pod_node and node_state (NS_SLOT) are the state the GPU ingest pass
     // (ingest.hip) applies batches to; pod_fill is its per-bucket fill mark.
     uint16_t* d_pod_fill = nullptr;
 
-    // ---- node batch staging, one Stage per ingest partition ----
-    // Partition p owns the bucket range [p*nb/n_part, (p+1)*nb/n_part): every op on
-    // a node slot of those buckets is staged (and coalesced) in stage[p], so
-    // partitions run on their own host threads with no shared writes.  Slot policy,
-    // op coalescing and event order are per bucket, so results do not depend on
-    // n_part.  One cache-line pair per partition: every staged op moves a vector's
-    // end pointer, and partitions run on different threads.
-    struct alignas(128) Stage {
-        std::vector<NodeOp> nops;
-        std::vector<uint32_t> puts;         // kwok_pool_put (other ranks' ingest-time releases)
-        int rejected = 0;
-    };
-    std::vector<Stage> stage;
+    // ---- host work of node batches: the status strings of UPSERT records with a
+    // non-empty status (string checks, blob interning, custom node templates), on up
+    // to n_part host threads ----
     int n_part = 1;
-    std::vector<uint32_t> node_stamp, node_opi;  // opi: index in the slot's stage
-    uint32_t gen = 1;  // ops of the unflushed batch carry stamp == gen (flush_ops advances it)
-    Stage& stage_of(uint32_t bucket_local) { return stage[(size_t)((uint64_t)bucket_local * n_part / nb)]; }
+    std::vector<uint32_t> puts;  // kwok_pool_put (other ranks' ingest-time releases), staged for flush_ops
     void* pinned = nullptr;
     size_t pinned_cap = 0;
     void* d_ops = nullptr;
@@ -199,15 +170,20 @@ struct kwok_engine {
         int32_t *out_handle = nullptr, *out_status = nullptr;
         int8_t* out_status8 = nullptr;  // kwok_ingest_pods_packed: the statuses as bytes
         uint32_t* out_released = nullptr;
-        uint32_t* byname = nullptr;
-        uint32_t* fix = nullptr;  // [2 * cap] (batch index, code) pairs
         void* sort_tmp = nullptr;
-        // per bucket / per node slot (allocated once)
-        uint32_t *creates = nullptr, *dels = nullptr, *beg = nullptr, *end = nullptr, *stopped = nullptr;
-        uint32_t* freed = nullptr;
-        uint32_t* refs_q = nullptr;   // [NL] node slots to count references of / their counts
-        uint32_t* refs_out = nullptr;
+        // per bucket (allocated once)
+        uint32_t *creates = nullptr, *dels = nullptr, *beg = nullptr, *end = nullptr;
         IngSummary* sum = nullptr;
+        // node batches (kwok_ingest_nodes): records, names, prepared records, host list
+        size_t ncap = 0;
+        kwok_node_event* d_nev = nullptr;
+        uint8_t* d_nnames = nullptr;  // [ncap * NAME_STRIDE]
+        NodeRec* nrec = nullptr;
+        uint32_t* host_idx = nullptr;
+        NodeFix* d_nfix = nullptr;
+        NodeSummary* nsum = nullptr;
+        NodeSummary* nsum_h = nullptr;  // pinned
+        int32_t* res_h = nullptr;       // pinned [2 * ncap]: handles, statuses
         IngSummary* sum_h = nullptr;  // pinned
         // a batch runs in chunks (KWOK_INGEST_CHUNK records): chunk k+1's prep reads its
         // records over the link on `pst` while chunk k is applied and its results copied
@@ -329,7 +305,6 @@ struct kwok_engine {
     bool foreign_ips = false;   // sticky: a podIP not assigned by this engine entered the pool
     bool global_foreign = false;  // multi rank, sticky: some rank's exchange message carried its foreign_ips
     bool quiet_ok = true;
-    std::vector<uint32_t> slot_refs;  // kwok_ingest_nodes: pods referencing the batch's deleted nodes (else 0)
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
@@ -357,7 +332,6 @@ struct kwok_engine {
     // the pod batch in progress changed the state (placeholder nodes, capacity, the
     // apply pass): a failure from then on leaves the batch partly applied (poison)
     bool ing_mutated = false;
-    bool zombie_check = false;  // a retired tick deleted pods: free_zombies when the queue drains
     uint32_t ing_chunk = 0;     // the chunk ingest_chunk works on (debug injection)
     uint64_t debug_fault_tick = 0;  // KWOK_DEBUG_LAYOUT_FAULT_TICK=N: tick N gets a wrong heartbeat layout (tests)
 
@@ -454,23 +428,6 @@ int ensure_pinned(kwok_engine* e, size_t bytes) {
     return KWOK_OK;
 }
 
-// first free slot in a bucket's occupancy bitset (lowest index: canonical policy)
-int32_t first_free(std::vector<uint64_t>& bits, uint32_t bucket_local, uint32_t cap) {
-    uint32_t wpb = (cap + 63) / 64;
-    uint64_t* w = bits.data() + (size_t)bucket_local * wpb;
-    for (uint32_t i = 0; i < wpb; i++) {
-        uint64_t free = ~w[i];
-        if (i == wpb - 1 && (cap & 63)) free &= (1ull << (cap & 63)) - 1;
-        if (free) return (int32_t)(i * 64 + __builtin_ctzll(free));
-    }
-    return -1;
-}
-void set_bit(std::vector<uint64_t>& bits, uint32_t cap, uint32_t bucket_local, uint32_t idx, bool v) {
-    uint32_t wpb = (cap + 63) / 64;
-    uint64_t& w = bits[(size_t)bucket_local * wpb + idx / 64];
-    if (v) w |= 1ull << (idx & 63);
-    else w &= ~(1ull << (idx & 63));
-}
 
 // Run f(p) for every ingest partition p: on n_part host threads when the batch
 // is large enough to pay for them, else in order on the caller's thread.
@@ -485,63 +442,18 @@ void run_parts(kwok_engine* e, bool parallel, F&& f) {
 }
 constexpr size_t NODE_PAR_MIN = 2048;  // node records (the per-record work is heavier)
 
-// ---- per-batch op coalescing: ops for the same slot compose in order ----
-void node_op(kwok_engine* e, uint32_t slot, uint8_t and_mask, uint8_t or_bits, bool set_blob, uint64_t blob) {
-    auto& g = e->stage_of(slot / e->Cn);
-    if (e->node_stamp[slot] == e->gen) {
-        NodeOp& o = g.nops[e->node_opi[slot]];
-        o.or_bits = (uint8_t)((o.or_bits & and_mask) | or_bits);
-        o.and_mask = (uint8_t)(o.and_mask & and_mask);
-        if (set_blob) o.set_blob = 1, o.blob = blob;
-        return;
-    }
-    e->node_stamp[slot] = e->gen;
-    e->node_opi[slot] = (uint32_t)g.nops.size();
-    NodeOp o{};
-    o.slot = slot;
-    o.and_mask = and_mask;
-    o.or_bits = or_bits;
-    o.set_blob = set_blob;
-    o.blob = blob;
-    g.nops.push_back(o);
-}
-bool node_ops_pending(const kwok_engine* e) {
-    for (const auto& g : e->stage)
-        if (!g.nops.empty()) return true;
-    return false;
-}
-
-// Every partition's staged node ops (and Puts) -> one host-to-device copy -> the
-// apply kernels.  Each slot has at most one op per batch (coalesced), so the
-// kernels apply them in any order.
+// kwok_pool_put's staged releases -> one host-to-device copy -> the pool
 int flush_ops(kwok_engine* e) {
-    size_t nn = 0, nu = 0;
-    for (const auto& g : e->stage) nn += g.nops.size(), nu += g.puts.size();
-    const size_t nb = nn * sizeof(NodeOp), ub = nu * 4;
-    const size_t uo = (nb + 255) & ~(size_t)255;
-    if (int rc = ensure_pinned(e, uo + ub + 256)) return rc;
-    char* h = (char*)e->pinned;
-    for (size_t p = 0, a = 0, c = 0; p < (size_t)e->n_part; p++) {
-        auto& g = e->stage[p];
-        if (!g.nops.empty()) memcpy(h + a * sizeof(NodeOp), g.nops.data(), g.nops.size() * sizeof(NodeOp));
-        if (!g.puts.empty()) memcpy(h + uo + c * 4, g.puts.data(), g.puts.size() * 4);
-        a += g.nops.size(), c += g.puts.size();
-    }
-    char* d = (char*)e->d_ops;
-    if (nn || nu) HIPCHK(e, hipMemcpyAsync(d, h, uo + ub, hipMemcpyHostToDevice, e->st));
-    launch_apply_ops(e->S, (const NodeOp*)d, (uint32_t)nn, nullptr, 0, e->st);
-    if (nu)  // kwok_pool_put: ingest-time releases of other ranks (pod_controller.go:329-336)
-        launch_pool_puts_now(e->S, (const uint32_t*)(d + uo), (uint32_t)nu, e->st);
+    const size_t nu = e->puts.size();
+    if (!nu) return KWOK_OK;
+    if (int rc = ensure_pinned(e, nu * 4 + 256)) return rc;
+    memcpy(e->pinned, e->puts.data(), nu * 4);
+    HIPCHK(e, hipMemcpyAsync(e->d_ops, e->pinned, nu * 4, hipMemcpyHostToDevice, e->st));
+    // ingest-time releases of other ranks (pod_controller.go:329-336)
+    launch_pool_puts_now(e->S, (const uint32_t*)e->d_ops, (uint32_t)nu, e->st);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->st));
-    for (auto& g : e->stage) {
-        g.nops.clear();
-        g.puts.clear();
-    }
-    if (++e->gen == 0) {  // stamps wrapped: forget them all
-        std::fill(e->node_stamp.begin(), e->node_stamp.end(), 0u);
-        e->gen = 1;
-    }
+    e->puts.clear();
     return KWOK_OK;
 }
 
@@ -696,20 +608,6 @@ int release_for_host(kwok_engine* e) {
     return KWOK_OK;
 }
 
-// live pods referencing each node slot of `slots` (drained: nothing else runs)
-int node_refs(kwok_engine* e, const std::vector<uint32_t>& slots, std::vector<uint32_t>& out) {
-    out.assign(slots.size(), 0);
-    if (slots.empty()) return KWOK_OK;
-    if (slots.size() > e->NL) return e->fail(KWOK_EINVAL, "node_refs: %zu slots", slots.size());
-    HIPCHK(e, hipMemcpyAsync(e->ing.refs_q, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, e->st));
-    launch_node_refs(e->S, e->ing.refs_q, (uint32_t)slots.size(), e->ing.refs_out, e->st);
-    HIPCHK(e, hipGetLastError());
-    if (int rc = release_for_host(e)) return rc;
-    HIPCHK(e, hipMemcpyAsync(out.data(), e->ing.refs_out, slots.size() * 4, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
-    return KWOK_OK;
-}
-
 // The blobs interned since the last upload -> the device copy (SRC_PAD_FRONT
 // zero bytes, the blobs, SRC_PAD_BACK zero bytes: k_emit reads around them).
 // Once per node batch, after every ingest thread is done appending to blob_h,
@@ -744,111 +642,6 @@ bool node_conforms(const kwok_node_event& ev, const std::string info[10]) {
            !info[KWOK_NI_ARCHITECTURE].empty() && !info[KWOK_NI_KUBE_PROXY_VERSION].empty() &&
            !info[KWOK_NI_KUBELET_VERSION].empty() && !info[KWOK_NI_OPERATING_SYSTEM].empty() &&
            info[KWOK_NI_SYSTEM_UUID] == info[KWOK_NI_OS_IMAGE];
-}
-
-// a name's home position in its bucket's name table (a mix of the fnv hash,
-// whose low bits chose the bucket)
-inline uint32_t name_home(uint32_t h, uint32_t mask) {
-    h ^= h >> 16;
-    h *= 0x7feb352du;
-    h ^= h >> 15;
-    h *= 0x846ca68bu;
-    h ^= h >> 16;
-    return h & mask;
-}
-// remove local index idx (hash h) from bucket bl's name table: backward-shift
-// deletion keeps every other entry reachable from its home without tombstones
-void name_erase(kwok_engine* e, uint32_t bl, uint32_t idx, uint32_t h) {
-    const uint32_t mask = e->name_mask;
-    uint32_t* tab = e->name_tab.data() + (size_t)bl * (mask + 1);
-    uint32_t i = name_home(h, mask);
-    while (tab[i] != idx + 1) i = (i + 1) & mask;  // present: the caller's node is in the table
-    for (uint32_t j = i;;) {
-        j = (j + 1) & mask;
-        if (!tab[j]) break;
-        const uint32_t k = name_home(e->nodes[(size_t)bl * e->Cn + tab[j] - 1].hash, mask);
-        // the entry at j stays if its home lies cyclically in (i, j]
-        if (i <= j ? (i < k && k <= j) : (i < k || k <= j)) continue;
-        tab[i] = tab[j];
-        i = j;
-    }
-    tab[i] = 0;
-}
-
-// a node entry's zombie mark (used && !exists: pods may still reference it)
-void set_zombie(kwok_engine* e, uint32_t slot, bool z) {
-    auto& n = e->nodes[slot];
-    if (n.zombie == (uint8_t)z) return;
-    n.zombie = z;
-    e->zb_count[slot / e->Cn] += z ? 1u : (uint32_t)-1;
-}
-// drop node entry `slot` from the host side (name table, occupancy); the device
-// entry is cleared by the staged op (dev_cleared: the device already did it)
-void free_node(kwok_engine* e, uint32_t slot, bool dev_cleared) {
-    auto& n = e->nodes[slot];
-    if (!n.used) return;
-    name_erase(e, slot / e->Cn, slot % e->Cn, n.hash);
-    set_bit(e->node_bits, e->Cn, slot / e->Cn, slot % e->Cn, false);
-    set_zombie(e, slot, false);
-    n = kwok_engine::HNode();
-    if (!dev_cleared) node_op(e, slot, 0, 0, true, 0);
-}
-
-// Software prefetch of a name lookup (node_slot), in two stages a few records
-// apart: stage 0 the name-table line, stage 1 (the table line now cached) the
-// node entry it points to.  A batch's lookups are two dependent cache misses
-// each over tables of ~1M nodes; issued ahead, they overlap.
-void name_prefetch(const kwok_engine* e, const char* name, size_t len, int stage) {
-    const uint32_t h = fnv1a32(name, len), b = h & (e->B - 1);
-    if (!e->owns(b)) return;
-    const uint32_t bl = b - e->b_lo, mask = e->name_mask;
-    const uint32_t* tab = e->name_tab.data() + (size_t)bl * (mask + 1);
-    const uint32_t i = name_home(h, mask);
-    if (stage == 0) {
-        __builtin_prefetch(tab + i);
-        return;
-    }
-    if (const uint32_t t = tab[i]) {
-        const size_t slot = (size_t)bl * e->Cn + t - 1;
-        const char* hn = reinterpret_cast<const char*>(&e->nodes[slot]);
-        __builtin_prefetch(hn);
-        __builtin_prefetch(hn + sizeof(kwok_engine::HNode) - 1);
-        // what applying the record touches next: its staged-op index (node_op) and,
-        // for a delete, the references the batch counted (ingest_one)
-        __builtin_prefetch(&e->node_stamp[slot]);
-        __builtin_prefetch(&e->node_opi[slot]);
-        if (slot < e->slot_refs.size()) __builtin_prefetch(&e->slot_refs[slot]);
-    }
-}
-
-// find (or create a placeholder for) the node entry of `name`
-int node_slot(kwok_engine* e, const char* name, size_t len, bool create, uint32_t* out) {
-    const uint32_t h = fnv1a32(name, len), b = h & (e->B - 1);
-    if (!e->owns(b)) return KWOK_ENOTMINE;
-    const uint32_t bl = b - e->b_lo, mask = e->name_mask;
-    uint32_t* tab = e->name_tab.data() + (size_t)bl * (mask + 1);
-    uint32_t i = name_home(h, mask);
-    for (; tab[i]; i = (i + 1) & mask) {
-        const uint32_t slot = bl * e->Cn + tab[i] - 1;
-        const auto& hn = e->nodes[slot];
-        if (hn.hash == h && hn.name.size() == len && memcmp(hn.name.data(), name, len) == 0) {
-            *out = slot;
-            return KWOK_OK;
-        }
-    }
-    if (!create) return KWOK_ENOTFOUND;
-    int32_t idx = first_free(e->node_bits, bl, e->Cn);
-    if (idx < 0) return KWOK_EFULL;
-    uint32_t slot = bl * e->Cn + (uint32_t)idx;
-    set_bit(e->node_bits, e->Cn, bl, (uint32_t)idx, true);
-    auto& n = e->nodes[slot];
-    n = kwok_engine::HNode();
-    n.used = 1;
-    n.name.assign(name, len);
-    n.hash = h;
-    tab[i] = (uint32_t)idx + 1;  // i: the empty position the probe ended at
-    *out = slot;
-    return KWOK_OK;
 }
 
 int parse_opt_ip(const char* arena, kwok_str s, uint32_t* ip) {
@@ -939,21 +732,20 @@ int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
     if (n > G.cap) {
         const size_t cap = std::max<size_t>(n + n / 4, 4096);
         void* ptrs[] = {G.d_ev, G.rec, G.keys, G.keys_sorted, G.idx_sorted, G.out_handle, G.out_status,
-                        G.out_released, G.byname, G.fix, G.sort_tmp, G.out_status8};
+                        G.out_released, G.sort_tmp, G.out_status8};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         G.d_ev = G.sort_tmp = nullptr;
         G.out_status8 = nullptr;
         G.rec = nullptr;
-        G.keys = G.keys_sorted = G.idx_sorted = G.out_released = G.byname = G.fix = nullptr;
+        G.keys = G.keys_sorted = G.idx_sorted = G.out_released = nullptr;
         G.out_handle = G.out_status = nullptr;
         G.cap = G.sort_bytes = 0;
         int rc = 0;
         if ((rc = dalloc(e, (uint8_t**)&G.d_ev, cap * sizeof(kwok_pod_event))) || (rc = dalloc(e, &G.rec, cap)) ||
             (rc = dalloc(e, &G.keys, cap)) || (rc = dalloc(e, &G.keys_sorted, cap)) || (rc = dalloc(e, &G.idx_sorted, cap)) ||
             (rc = dalloc(e, &G.out_handle, cap)) || (rc = dalloc(e, &G.out_status, cap)) ||
-            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.byname, cap)) || (rc = dalloc(e, &G.fix, 2 * cap)) ||
-            (rc = dalloc(e, &G.out_status8, cap)))
+            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.out_status8, cap)))
             return rc;
         G.sort_bytes = ingest_sort_bytes((uint32_t)cap, 32);
         if ((rc = dalloc(e, (uint8_t**)&G.sort_tmp, G.sort_bytes))) return rc;
@@ -986,11 +778,8 @@ IngestBatch ingest_batch(kwok_engine* e, uint32_t n, size_t arena_len) {
     I.out_released = G.out_released;
     I.creates = G.creates;
     I.dels = G.dels;
-    I.byname = G.byname;
     I.beg = G.beg;
     I.end = G.end;
-    I.stopped = G.stopped;
-    I.freed = G.freed;
     I.sum = G.sum;
     return I;
 }
@@ -1001,38 +790,6 @@ int read_summary(kwok_engine* e, const IngSummary* sum = nullptr) {
     HIPCHK(e, hipStreamSynchronize(e->st));
     return KWOK_OK;
 }
-// host resolutions -> the prepared records (REC_RESOLVED / REC_HARD / a final status)
-int apply_fixes(kwok_engine* e, const IngestBatch& I, const std::vector<uint32_t>& fix) {
-    if (fix.empty()) return KWOK_OK;
-    HIPCHK(e, hipMemcpyAsync(e->ing.fix, fix.data(), fix.size() * 4, hipMemcpyHostToDevice, e->st));
-    launch_ingest_fix(e->S, I, e->ing.fix, (uint32_t)(fix.size() / 2), e->st);
-    HIPCHK(e, hipGetLastError());
-    HIPCHK(e, hipStreamSynchronize(e->st));  // `fix` is pageable and reused
-    return KWOK_OK;
-}
-// a pod names a node without an entry: a placeholder entry (node_slot), which the
-// pod references until it goes; the fix code of the record
-uint32_t resolve_placeholder(kwok_engine* e, const char* name, size_t len) {
-    uint32_t slot = 0;
-    const int st = node_slot(e, name, len, true, &slot);
-    if (st != KWOK_OK) return 0x80000000u | (uint8_t)(int8_t)st;
-    if (!e->nodes[slot].exists) {
-        node_op(e, slot, 0xFF, NS_SLOT, false, 0);
-        set_zombie(e, slot, true);
-    }
-    return slot % e->Cn;
-}
-// node entries the apply pass freed (the device cleared them) -> the host side
-int free_device_freed(kwok_engine* e) {
-    const uint32_t nf = e->ing.sum_h->n_freed;
-    if (!nf) return KWOK_OK;
-    std::vector<uint32_t> fr(nf);
-    HIPCHK(e, hipMemcpyAsync(fr.data(), e->ing.freed, (size_t)nf * 4, hipMemcpyDeviceToHost, e->st));
-    HIPCHK(e, hipStreamSynchronize(e->st));
-    for (uint32_t s : fr) free_node(e, s, true);
-    return KWOK_OK;
-}
-
 // The largest pod capacity a chain block's pod chunks cover (engine_create's limit)
 uint32_t max_pod_capacity(const kwok_engine* e) {
     const uint64_t bpb = (e->nb + e->S.n_chain - 1) / e->S.n_chain;
@@ -1223,7 +980,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
                     e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv, e->d_ssend, e->d_srecv};
     for (void* p : ptrs)
@@ -1232,18 +989,19 @@ void kwok_engine_destroy(kwok_engine* e) {
     {
         auto& g = e->ing;
         void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
-                      g.out_released, g.byname, g.fix, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.stopped,
-                      g.freed, g.refs_q, g.refs_out, g.sum, g.creates1, g.dels1, g.sum1, g.out_status8};
+                      g.out_released, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.sum, g.creates1, g.dels1, g.sum1,
+                      g.out_status8, g.d_nev, g.d_nnames, g.nrec, g.host_idx, g.d_nfix, g.nsum};
         for (void* p : ip)
             if (p) (void)hipFree(p);
         if (g.sum_h) (void)hipHostFree(g.sum_h);
+        if (g.nsum_h) (void)hipHostFree(g.nsum_h);
+        if (g.res_h) (void)hipHostFree(g.res_h);
         hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1]};
         for (hipEvent_t x : evs)
             if (x) (void)hipEventDestroy(x);
         if (g.pst) (void)hipStreamDestroy(g.pst);
         if (g.dst) (void)hipStreamDestroy(g.dst);
     }
-    if (e->hb_pre_h) (void)hipHostFree(e->hb_pre_h);
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->dump_h) (void)hipHostFree(e->dump_h);
@@ -1461,6 +1219,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
         (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(e->XW, 1))) ||
+        (rc = dalloc(e, &S.node_key, NLa)) || (rc = dalloc(e, &S.node_name, NLa * NAME_STRIDE)) ||
+        (rc = dalloc(e, &S.mb_count, e->nb)) || (rc = dalloc(e, &S.zb_count, e->nb)) ||
         (rc = alloc_slot(e, 0)))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
@@ -1483,8 +1243,6 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         const char* sy = getenv("KWOK_SYNC");
         e->sync_spin = !(sy && strcmp(sy, "block") == 0);
     }
-    if (hipHostMalloc((void**)&e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipHostMallocDefault) != hipSuccess)
-        return bail(KWOK_ENOMEM);
     S.hb_pre = e->d_hb_pre;
     S.pod_fill = e->d_pod_fill;
     S.rank = e->rank;
@@ -1500,33 +1258,22 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
             if (r != ncclSuccess) return bail(e->fail(KWOK_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(r)));
         }
     }
-    // host mirrors
-    e->nodes.resize(e->NL);
-    e->node_bits.assign((size_t)e->nb * ((e->Cn + 63) / 64), 0);
-    e->mb_count.assign(e->nb, 0);
     {
-        uint32_t t = 16;
-        while (t < 2 * e->Cn) t <<= 1;  // load factor <= 1/2
-        e->name_mask = t - 1;
-        e->name_tab.assign((size_t)e->nb * t, 0);
-    }
-    {
-        // host ingest partitions of node batches (threads): KWOK_INGEST_THREADS, else up to 16
+        // host threads of node batches' string work: KWOK_INGEST_THREADS, else up to 16
         unsigned hw = std::thread::hardware_concurrency();
         int np = (int)std::min(16u, hw ? hw : 1u);
         if (const char* v = getenv("KWOK_INGEST_THREADS")) np = atoi(v);
-        e->n_part = std::max(1, std::min(np, (int)std::min<uint32_t>(e->nb, 64)));
-        e->stage.resize((size_t)e->n_part);
+        e->n_part = std::max(1, std::min(np, 64));
     }
-    e->zb_count.assign(e->nb, 0);
     {  // GPU pod ingest: per-bucket / per-node-slot scratch and the batch summary
         auto& g = e->ing;
         if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.dels, e->nb)) || (rc = dalloc(e, &g.beg, e->nb)) ||
-            (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.stopped, e->nb)) || (rc = dalloc(e, &g.freed, e->NL)) ||
-            (rc = dalloc(e, &g.refs_q, e->NL)) || (rc = dalloc(e, &g.refs_out, e->NL)) || (rc = dalloc(e, &g.sum, 1)) ||
+            (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.sum, 1)) || (rc = dalloc(e, &g.nsum, 1)) ||
             (rc = dalloc(e, &g.creates1, e->nb)) || (rc = dalloc(e, &g.dels1, e->nb)) || (rc = dalloc(e, &g.sum1, 1)))
             return bail(rc);
-        if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess) return bail(KWOK_ENOMEM);
+        if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&g.nsum_h, sizeof(NodeSummary), hipHostMallocDefault) != hipSuccess)
+            return bail(KWOK_ENOMEM);
         hipError_t r = hipStreamCreateWithFlags(&g.pst, hipStreamNonBlocking);
         if (r == hipSuccess) r = hipStreamCreateWithFlags(&g.dst, hipStreamNonBlocking);
         hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1]};
@@ -1535,8 +1282,6 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "ingest stream/events: %s", hipGetErrorString(r)));
         if (const char* v = getenv("KWOK_INGEST_CHUNK")) g.chunk = std::max<size_t>(1, strtoull(v, nullptr, 10));
     }
-    e->node_stamp.assign(e->NL, 0);
-    e->node_opi.assign(e->NL, 0);
     e->max_init_len = 0;
     if ((rc = size_arena(e)) || (rc = grow_arena(e, e->slots[0]))) return bail(rc);
     {
@@ -1629,281 +1374,205 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     return KWOK_OK;
 }
 
+// node batch buffers for n records (the pod batch's sort buffers are shared)
+int node_reserve(kwok_engine* e, size_t n, size_t arena_len) {
+    auto& G = e->ing;
+    if (int rc = ingest_reserve(e, n, arena_len)) return rc;
+    if (n <= G.ncap) return KWOK_OK;
+    void* ptrs[] = {G.d_nev, G.d_nnames, G.nrec, G.host_idx, G.d_nfix};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (G.res_h) (void)hipHostFree(G.res_h);
+    G.d_nev = nullptr, G.d_nnames = nullptr, G.nrec = nullptr, G.host_idx = nullptr, G.d_nfix = nullptr, G.res_h = nullptr;
+    G.ncap = 0;
+    const size_t cap = std::max<size_t>(n + n / 4, 4096);
+    int rc = 0;
+    if ((rc = dalloc(e, &G.d_nev, cap)) || (rc = dalloc(e, &G.d_nnames, cap * NAME_STRIDE)) || (rc = dalloc(e, &G.nrec, cap)) ||
+        (rc = dalloc(e, &G.host_idx, cap)) || (rc = dalloc(e, &G.d_nfix, cap)))
+        return rc;
+    if (hipHostMalloc((void**)&G.res_h, cap * 8, hipHostMallocDefault) != hipSuccess) return e->fail(KWOK_ENOMEM, "node results");
+    G.ncap = cap;
+    return KWOK_OK;
+}
+
+// The status of a node the device could not settle alone (a non-empty status, or
+// a custom node template): the string checks and the init blob (node.init.tpl /
+// Config.NodeInitializationTemplate), CONFORMS (A.5).  Host string work, on the
+// partition threads; blob interning under blob_mu.
+NodeFix complete_node(kwok_engine* e, const kwok_node_event& x, uint32_t idx, const char* arena, std::mutex& blob_mu) {
+    NodeFix f{};
+    f.idx = idx;
+    int st = KWOK_OK;
+    std::string info[KWOK_NI_COUNT];
+    for (int k = 0; k < KWOK_NI_COUNT && st == KWOK_OK; k++)
+        if (x.node_info[k].len) {
+            info[k].assign(arena + x.node_info[k].off, x.node_info[k].len);
+            if (!safe_string(info[k].data(), info[k].size())) st = KWOK_EDOMAIN;
+        }
+    std::string js[3];
+    const kwok_str* jr[3] = {&x.addresses, &x.allocatable, &x.capacity};
+    for (int k = 0; k < 3 && st == KWOK_OK; k++)
+        if (jr[k]->len) {
+            js[k].assign(arena + jr[k]->off, jr[k]->len);
+            if (!valid_json_blob(js[k].data(), js[k].size(), k == 0 ? '[' : '{')) st = KWOK_EDOMAIN;
+        }
+    if (st == KWOK_OK) {
+        std::lock_guard<std::mutex> lock(blob_mu);
+        if (e->custom_node) {
+            // one compile per distinct status (the fields the template may read)
+            std::string key = std::to_string(x.phase);
+            for (int k = 0; k < 3; k++) key += '\x01' + js[k];
+            for (int k = 0; k < KWOK_NI_COUNT; k++) key += '\x01' + info[k];
+            auto it = e->node_tpl_blobs.find(key);
+            if (it != e->node_tpl_blobs.end()) {
+                f.blob = it->second;
+            } else {
+                NodeBlob nb;
+                std::string why;
+                if (!compile_node_template(e->node_tpl, js[0], js[1], js[2], info, x.phase, e->node_ip_s, e->start_s,
+                                           e->hb_tpl, nb, why)) {
+                    st = KWOK_EDOMAIN;
+                } else {
+                    f.blob = intern_blob(e, nb, &st);
+                    if (st == KWOK_OK) e->node_tpl_blobs.emplace(std::move(key), f.blob);
+                }
+            }
+        } else {
+            f.blob = intern_blob(e, build_node_blob(js[0], js[1], js[2], info, e->node_ip_s), &st);
+        }
+    }
+    f.status = st;
+    f.conforms = st == KWOK_OK && !e->custom_node && node_conforms(x, info) ? 1u : 0u;
+    return f;
+}
+
+// kwok_ingest_nodes: the WatchNodes / ListNodes event switch (node_controller.go:
+// 256-270) on the GPU over the device node directory (ingest.hip): prep, the host's
+// completions of non-empty statuses, a stable sort by bucket, one wave per bucket
+// in event order.  Two host round trips per batch (the prep summary, the results).
 int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
                       int32_t* out_handles, int32_t* out_status) {
-    if (!e || (n && !ev)) return KWOK_EINVAL;
+    if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
-    drain(e);  // the host mirrors reflect every submitted tick
+    drain(e);  // the device state reflects every submitted tick
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     e->quiet = 0;
-    auto in_arena = [&](kwok_str s) { return (size_t)s.off + s.len <= arena_len; };
-    const auto tq0 = clk::now();
-    // a deleted node's entry lives while pods reference it (the pods' node refs,
-    // pod_controller.go routes by spec.nodeName): the references of the nodes this
-    // batch deletes, counted on the device (no pod changes during a node batch)
-    // (filled below, before any record is ingested; a per-slot array the engine
-    // keeps zeroed: the batch's entries are cleared on every way out)
-    if (e->slot_refs.size() < (size_t)e->NL) e->slot_refs.assign((size_t)e->NL, 0u);
-    std::vector<uint32_t> del;
-    struct ClearRefs {
-        std::vector<uint32_t>& a;
-        const std::vector<uint32_t>& d;
-        ~ClearRefs() {
-            for (uint32_t s : d) a[s] = 0;
-        }
-    } clear_refs{e->slot_refs, del};
-    auto refs_of = [&](uint32_t slot) { return e->slot_refs[slot]; };  // a node created in this batch has none
-    // per partition: managed-set changes (applied after the batch)
-    // (each partition's accumulators and results on cache lines of their own: the
-    // partitions interleave in batch order, and shared lines cost more than the
-    // records' own work - C5 records phase 1.0 ms on 16 threads, 1.5 ms on 4)
-    struct alignas(64) PartAcc {
-        int64_t d_managed = 0;
-        int rej = 0;
-        uint8_t set_changed = 0;
-        std::vector<uint32_t> dels;                           // pass 1: slots of deleted nodes
-        std::vector<std::pair<uint32_t, uint64_t>> results;  // (record, handle | status << 32)
-    };
-    std::vector<PartAcc> acc((size_t)e->n_part);
-    bool threaded_results = false;  // set below when the records are applied by partition threads
-    std::mutex blob_mu;  // blob interning (host string + device upload) and the template cache
-    // WatchNodes / ListNodes event switch (node_controller.go:256-270) for one record
-    auto ingest_one = [&](size_t i, int part) {
-        const kwok_node_event& x = ev[i];
-        int st = KWOK_OK;
-        int32_t handle = -1;
-        if (!x.name.len || x.name.len > 253 || !in_arena(x.name)) st = KWOK_EDOMAIN;
-        const char* name = arena + x.name.off;
-        uint32_t slot = 0;
-        if (st == KWOK_OK && x.op == KWOK_OP_DELETE) {
-            // node_controller.go:265-269: Deleted -> nodesSets.Delete
-            st = node_slot(e, name, x.name.len, false, &slot);
-            if (st == KWOK_OK) {
-                auto& hn = e->nodes[slot];
-                if (hn.managed) acc[(size_t)part].d_managed--, e->mb_count[slot / e->Cn]--, acc[(size_t)part].set_changed = 1;
-                hn.exists = hn.managed = 0;
-                node_op(e, slot, (uint8_t)~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE), 0,
-                        false, 0);
-                handle = (int32_t)(e->b_lo * e->Cn + slot);
-                if (refs_of(slot) == 0) free_node(e, slot, false);
-                else set_zombie(e, slot, true);  // freed when its last pod goes (ingest / tick)
-            }
-        } else if (st == KWOK_OK && x.op == KWOK_OP_UPSERT) {
-            std::string info[KWOK_NI_COUNT];
-            for (int k = 0; k < KWOK_NI_COUNT && st == KWOK_OK; k++) {
-                if (!in_arena(x.node_info[k])) st = KWOK_EDOMAIN;
-                else if (x.node_info[k].len) {
-                    info[k].assign(arena + x.node_info[k].off, x.node_info[k].len);
-                    if (!safe_string(info[k].data(), info[k].size())) st = KWOK_EDOMAIN;
-                }
-            }
-            std::string js[3];
-            const kwok_str* jr[3] = {&x.addresses, &x.allocatable, &x.capacity};
-            for (int k = 0; k < 3 && st == KWOK_OK; k++) {
-                if (!in_arena(*jr[k])) st = KWOK_EDOMAIN;
-                else if (jr[k]->len) {
-                    js[k].assign(arena + jr[k]->off, jr[k]->len);
-                    if (!valid_json_blob(js[k].data(), js[k].size(), k == 0 ? '[' : '{')) st = KWOK_EDOMAIN;
-                }
-            }
-            if (st == KWOK_OK) st = node_slot(e, name, x.name.len, true, &slot);
-            if (st == KWOK_OK) {
-                // a Node created with an empty status (kwok's own fleets) renders the
-                // one default blob: built once
-                bool empty = js[0].empty() && js[1].empty() && js[2].empty();
-                for (int k = 0; k < KWOK_NI_COUNT; k++) empty = empty && info[k].empty();
-                int brc = KWOK_OK;
-                uint64_t blob = 0;
-                // the empty-status blob, once built, is read without the lock (it is
-                // written only under it, before any thread can see has_empty_blob)
-                const bool fast = !e->custom_node && empty && e->has_empty_blob.load(std::memory_order_acquire);
-                std::unique_lock<std::mutex> lock(blob_mu, std::defer_lock);
-                if (!fast) lock.lock();
-                if (fast) {
-                    blob = e->empty_blob;
-                } else if (e->custom_node) {
-                    // one compile per distinct status (the fields the template may read)
-                    std::string key = std::to_string(x.phase);
-                    for (int k = 0; k < 3; k++) key += '\x01' + js[k];
-                    for (int k = 0; k < KWOK_NI_COUNT; k++) key += '\x01' + info[k];
-                    auto it = e->node_tpl_blobs.find(key);
-                    if (it != e->node_tpl_blobs.end()) {
-                        blob = it->second;
-                    } else {
-                        NodeBlob nb;
-                        std::string why;
-                        if (!compile_node_template(e->node_tpl, js[0], js[1], js[2], info, x.phase, e->node_ip_s,
-                                                   e->start_s, e->hb_tpl, nb, why)) {
-                            brc = KWOK_EDOMAIN;
-                        } else {
-                            blob = intern_blob(e, nb, &brc);
-                            if (!brc) e->node_tpl_blobs.emplace(std::move(key), blob);
-                        }
-                    }
-                } else if (empty && e->has_empty_blob.load(std::memory_order_acquire)) {
-                    blob = e->empty_blob;
-                } else {
-                    NodeBlob nb = build_node_blob(js[0], js[1], js[2], info, e->node_ip_s);
-                    blob = intern_blob(e, nb, &brc);
-                    if (empty && !brc) {
-                        e->empty_blob = blob;
-                        e->has_empty_blob.store(true, std::memory_order_release);
-                    }
-                }
-                if (brc) st = brc;
-                else {
-                    auto& hn = e->nodes[slot];
-                    hn.exists = 1;
-                    set_zombie(e, slot, false);
-                    if (x.managed && !hn.managed) {  // never cleared but by Delete
-                        hn.managed = 1;
-                        acc[(size_t)part].d_managed++;
-                        e->mb_count[slot / e->Cn]++;
-                        acc[(size_t)part].set_changed = 1;
-                    }
-                    hn.lockable = x.lockable ? 1 : 0;
-                    bool ev_lock = x.managed && x.lockable;
-                    uint8_t bits = (uint8_t)(NS_SLOT | NS_EXISTS | (hn.managed ? NS_MANAGED : 0) | (hn.lockable ? NS_LOCKABLE : 0) |
-                                             (!e->custom_node && node_conforms(x, info) ? NS_CONFORMS : 0) |
-                                             (ev_lock ? NS_EVENT_LOCK : 0));
-                    node_op(e, slot, ev_lock ? 0 : NS_EVENT_LOCK, bits, true, blob);
-                    handle = (int32_t)(e->b_lo * e->Cn + slot);
-                }
-            }
-        } else if (st == KWOK_OK) {
-            st = KWOK_EINVAL;
-        }
-        if (threaded_results) {
-            acc[(size_t)part].results.emplace_back((uint32_t)i, (uint64_t)(uint32_t)handle | (uint64_t)(uint32_t)st << 32);
-        } else {
-            if (out_handles) out_handles[i] = handle;
-            if (out_status) out_status[i] = st;
-        }
-        return st != KWOK_OK;
-    };
-    // the bucket (owned, local) a record changes, or -1 (rejected / another rank's)
-    auto bucket_of_record = [&](const kwok_node_event& x) -> int64_t {
-        if (!x.name.len || x.name.len > 253 || !in_arena(x.name)) return -1;
-        const uint32_t b = fnv1a32(arena + x.name.off, x.name.len) & (e->B - 1);
-        return e->owns(b) ? (int64_t)(b - e->b_lo) : -1;
-    };
-    static const size_t PF_DIST = getenv("KWOK_NODE_PF") ? strtoull(getenv("KWOK_NODE_PF"), nullptr, 10) : 16;
-    static const size_t par_min = getenv("KWOK_NODE_PAR_MIN") ? strtoull(getenv("KWOK_NODE_PAR_MIN"), nullptr, 10)
-                                                             : NODE_PAR_MIN;
-    const bool threaded = n >= par_min && e->n_part > 1;
-    const int P = e->n_part;
-    std::vector<uint8_t> part(threaded ? n : 0);
-    auto tq1 = clk::now();
-    {
-        // pass 1 (read-only, by record chunks): each record's partition, and the
-        // entries of the nodes this batch deletes (their references are counted
-        // on the device before any record is applied: no pod changes during a
-        // node batch)
-        auto pass1 = [&](int c) {
-            const size_t lo = threaded ? n * (size_t)c / (size_t)P : 0, hi = threaded ? n * (size_t)(c + 1) / (size_t)P : n;
-            auto pf = [&](size_t j, int stage) {
-                const kwok_node_event& y = ev[j];
-                if (y.op == KWOK_OP_DELETE && y.name.len && y.name.len <= 253 && in_arena(y.name))
-                    name_prefetch(e, arena + y.name.off, y.name.len, stage);
-            };
-            for (size_t i = lo; i < hi; i++) {
-                if (i + PF_DIST < hi) pf(i + PF_DIST, 0);
-                if (i + PF_DIST / 2 < hi) pf(i + PF_DIST / 2, 1);
-                const int64_t bl = bucket_of_record(ev[i]);
-                if (threaded) part[i] = (uint8_t)(bl < 0 ? 0 : (uint64_t)bl * (uint64_t)P / e->nb);
-                uint32_t slot = 0;
-                if (bl >= 0 && ev[i].op == KWOK_OP_DELETE &&
-                    node_slot(e, arena + ev[i].name.off, ev[i].name.len, false, &slot) == KWOK_OK)
-                    acc[(size_t)c].dels.push_back(slot);
-            }
-        };
-        if (threaded) run_parts(e, true, pass1);
-        else pass1(0);
-        tq1 = clk::now();
-        for (auto& a : acc) del.insert(del.end(), a.dels.begin(), a.dels.end());
-        if (!del.empty()) {
-            std::vector<uint32_t> cnt;
-            if (int rc = node_refs(e, del, cnt)) return rc;
-            for (size_t k = 0; k < del.size(); k++) e->slot_refs[del[k]] = cnt[k];
-        }
+    if (!n) return 0;
+    const auto t0 = clk::now();
+    int rc = node_reserve(e, n, arena_len);
+    if (rc) return rc;
+    auto& G = e->ing;
+    hipStream_t st = e->st;
+    // the empty-status blob (kwok's own fleets create Nodes with an empty status)
+    if (!e->custom_node && !e->has_empty_blob.load()) {
+        std::string empty[KWOK_NI_COUNT];
+        int brc = KWOK_OK;
+        const uint64_t b = intern_blob(e, build_node_blob("", "", "", empty, e->node_ip_s), &brc);
+        if (brc) return e->fail(brc, "empty node status blob");
+        e->empty_blob = b;
+        e->has_empty_blob.store(true);
     }
-    const auto tn0 = clk::now();  // (refs: tq0 .. tn0)
-    if (!threaded) {
-        for (size_t i = 0; i < n; i++) {
-            const int64_t bl = bucket_of_record(ev[i]);
-            const int p = bl < 0 ? 0 : (int)((uint64_t)bl * e->n_part / e->nb);
-            acc[(size_t)p].rej += ingest_one(i, p);
-        }
-    } else {
-        // partitions own bucket ranges (as for pods); each takes its records in batch order
-        threaded_results = true;
-        run_parts(e, true, [&](int p) {
-            PartAcc& a = acc[(size_t)p];
-            // the partition's next records' lookups prefetched (two stages, as pass 1)
-            size_t q0 = 0, q1 = 0;  // the scan positions of stage 0 / stage 1
-            int ahead0 = 0, ahead1 = 0;  // this partition's records each stage is ahead by
-            auto advance = [&](size_t& q, int& ahead, int want, int stage) {
-                for (; ahead < want && q < n; q++)
-                    if (part[q] == (uint8_t)p) {
-                        const kwok_node_event& y = ev[q];
-                        if (y.name.len && y.name.len <= 253 && in_arena(y.name))
-                            name_prefetch(e, arena + y.name.off, y.name.len, stage);
-                        ahead++;
-                    }
-            };
-            for (size_t i = 0; i < n; i++)
-                if (part[i] == (uint8_t)p) {
-                    advance(q0, ahead0, PF_DIST, 0);
-                    advance(q1, ahead1, PF_DIST / 2, 1);
-                    a.rej += ingest_one(i, p);
-                    ahead0--, ahead1--;
-                }
+    // the batch in kwok_host_alloc memory is read in place by k_nd_prep; any other is copied
+    const void* zev = e->ingest_zc ? host_mapped(ev, n * sizeof(kwok_node_event)) : nullptr;
+    const void* zar = e->ingest_zc && arena_len ? host_mapped(arena, arena_len) : nullptr;
+    if (!zev) HIPCHK(e, hipMemcpyAsync(G.d_nev, ev, n * sizeof(kwok_node_event), hipMemcpyHostToDevice, st));
+    if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    NodeBatch N{};
+    N.ev = static_cast<const kwok_node_event*>(zev ? zev : (const void*)G.d_nev);
+    N.n = (uint32_t)n;
+    N.host_all = e->custom_node ? 1u : 0u;
+    N.arena = zar ? static_cast<const uint8_t*>(zar) : G.d_arena;
+    N.arena_len = arena_len;
+    N.empty_blob = e->empty_blob;
+    N.rec = G.nrec;
+    N.names = G.d_nnames;
+    N.keys = G.keys;
+    N.keys_sorted = G.keys_sorted;
+    N.idx_sorted = G.idx_sorted;
+    N.beg = G.beg;
+    N.end = G.end;
+    N.out_handle = G.out_handle;
+    N.out_status = G.out_status;
+    N.host_idx = G.host_idx;
+    N.sum = G.nsum;
+    HIPCHK(e, hipMemsetAsync(G.nsum, 0, sizeof(NodeSummary), st));
+    launch_node_prep(e->S, N, st);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = release_for_host(e))) return rc;
+    HIPCHK(e, hipMemcpyAsync(G.nsum_h, G.nsum, sizeof(NodeSummary), hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    const auto t1 = clk::now();
+    const uint32_t n_host = G.nsum_h->n_host;
+    if (n_host) {
+        // the records whose status strings need the host, in batch order (blob offsets do not
+        // depend on it, but a deterministic interning order keeps the blob store reproducible)
+        std::vector<uint32_t> idx(n_host);
+        HIPCHK(e, hipMemcpyAsync(idx.data(), G.host_idx, (size_t)n_host * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        std::sort(idx.begin(), idx.end());
+        std::vector<NodeFix> fix(n_host);
+        std::mutex blob_mu;
+        const bool par = n_host >= NODE_PAR_MIN && e->n_part > 1;
+        run_parts(e, par, [&](int p) {
+            const size_t lo = par ? (size_t)n_host * p / e->n_part : (p ? n_host : 0);
+            const size_t hi = par ? (size_t)n_host * (p + 1) / e->n_part : (p ? n_host : n_host);
+            for (size_t k = lo; k < hi; k++) fix[k] = complete_node(e, ev[idx[k]], idx[k], arena, blob_mu);
         });
-        for (const PartAcc& a : acc)
-            for (const auto& r : a.results) {
-                if (out_handles) out_handles[r.first] = (int32_t)(uint32_t)r.second;
-                if (out_status) out_status[r.first] = (int32_t)(uint32_t)(r.second >> 32);
-            }
+        if ((rc = upload_blobs(e))) return rc;
+        HIPCHK(e, hipMemcpyAsync(G.d_nfix, fix.data(), fix.size() * sizeof(NodeFix), hipMemcpyHostToDevice, st));
+        launch_node_fix(e->S, N, G.d_nfix, n_host, st);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipStreamSynchronize(st));  // `fix` is pageable
     }
-    int rejected = 0;
-    bool changed = false;
-    for (const PartAcc& a : acc) {
-        rejected += a.rej;
-        e->n_managed = (uint64_t)((int64_t)e->n_managed + a.d_managed);
-        changed |= a.set_changed != 0;
-    }
-    if (changed) {
+    if ((rc = upload_blobs(e))) return rc;  // (the empty-status blob, first batch)
+    const auto t2 = clk::now();
+    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
+    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
+    if (launch_node_sort(e->S, N, G.sort_tmp, G.sort_bytes, sort_bits(e), st)) return e->fail(KWOK_EDEVICE, "node sort");
+    launch_node_apply(e->S, N, st);
+    // from here the batch is in the device state: a failure poisons the engine
+    auto failed = [&](int r) {
+        e->poisoned = true;
+        return r;
+    };
+    if (hipGetLastError() != hipSuccess) return failed(e->fail(KWOK_EDEVICE, "k_nd_apply launch"));
+    if (release_for_host(e) != KWOK_OK ||
+        (out_handles && hipMemcpyAsync(G.res_h, G.out_handle, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        (out_status && hipMemcpyAsync(G.res_h + n, G.out_status, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipMemcpyAsync(G.nsum_h, G.nsum, sizeof(NodeSummary), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return failed(e->fail(KWOK_EDEVICE, "node batch results"));
+    if (out_handles) memcpy(out_handles, G.res_h, n * 4);
+    if (out_status) memcpy(out_status, G.res_h + n, n * 4);
+    const NodeSummary sum = *G.nsum_h;
+    e->n_managed = (uint64_t)((int64_t)e->n_managed + sum.d_managed);
+    if (sum.changed) {
         e->hb_pre_dirty = true;
         e->hb_epoch++;  // the managed set changed in this batch
     }
-    const auto tn1 = std::chrono::steady_clock::now();
-    int rc = upload_blobs(e);
-    if (rc) return rc;
-    if ((rc = size_arena(e))) return rc;
-    rc = flush_ops(e);
+    if ((rc = size_arena(e))) return failed(rc);
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu node records (%s): lookups %.2f ms, refs %.2f ms, records %.2f ms, "
-                        "flush %.2f ms\n", n, threaded ? "threaded" : "1 thread", ms_between(tq0, tq1), ms_between(tq1, tn0), std::chrono::duration<double, std::milli>(tn1 - tn0).count(),
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tn1).count());
-    return rc ? rc : rejected;
+        fprintf(stderr, "[kwok ingest] %zu node records (GPU%s): prep %.3f ms, host %u records %.3f ms, apply + results "
+                        "%.3f ms (%u created, %u freed)\n", n, zev ? ", read in place" : "", ms_between(t0, t1), n_host,
+                ms_between(t1, t2), ms_between(t2, clk::now()), sum.created, sum.freed);
+    return (int)sum.rejected;
 }
 
-// One chunk of a pod batch after its prep (I: the chunk's records, ev: their host
-// copies, indices chunk-local): the growth check, by-name resolution, the stable
-// sort by bucket and the apply pass, on the engine stream.  Returns the chunk's
-// rejected count (>= 0) or an error.
-int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev, const char* arena) {
+// One chunk of a pod batch after its prep (I: the chunk's records, indices
+// chunk-local): the growth check, the stable sort by bucket and the apply pass
+// (by-name creates resolve their node in it), on the engine stream.  Returns the
+// chunk's rejected count (>= 0) or an error.
+int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
     auto& G = e->ing;
     hipStream_t st = e->st;
     int rc = 0;
     launch_ingest_need(e->S, I, st);
     HIPCHK(e, hipGetLastError());
     if ((rc = read_summary(e, I.sum))) return rc;
-    IngSummary sum = *G.sum_h;
+    const IngSummary sum = *G.sum_h;
     // growth: every bucket to a larger capacity (up to the handle stride) when the
     // chunk's creates could fill one
-    bool efull_possible = false;
     if (sum.need > e->Cp) {
         const uint32_t cap = max_pod_capacity(e);
         if (cap > e->Cp) {
@@ -1912,77 +1581,19 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
             if (e->iprof) fprintf(stderr, "[kwok grow] pod capacity per bucket %u -> %u\n", e->Cp, want);
             if ((rc = grow_pods(e, want))) return rc;
         }
-        efull_possible = sum.need > e->Cp;  // at the stride (or the chain blocks' limit): EFULL per record
     }
-    // by-name creates (spec.nodeName): resolved on the host, in event order
-    std::vector<uint32_t> fix;
-    if (sum.n_byname) {
-        e->ing_mutated = true;  // placeholder node entries from here on
-        std::vector<uint32_t> idx(sum.n_byname), dels(e->nb);
-        HIPCHK(e, hipMemcpyAsync(idx.data(), I.byname, idx.size() * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipMemcpyAsync(dels.data(), I.dels, dels.size() * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipStreamSynchronize(st));
-        std::sort(idx.begin(), idx.end());
-        const std::vector<uint32_t> zb0 = e->zb_count;  // zombie entries at the chunk's start
-        // A node entry can only be freed during the chunk in a bucket that deletes pods
-        // at ingest, holds zombie entries, or may run out of pod slots: there a name
-        // that is missing or a zombie is resolved when the apply pass reaches it
-        // (REC_HARD).  Elsewhere every lookup (and placeholder) is the one event
-        // order would give.
-        for (uint32_t i : idx) {
-            const kwok_str nm = ev[i].node_name;
-            const uint32_t bl = (fnv1a32(arena + nm.off, nm.len) & (e->B - 1)) - e->b_lo;
-            const bool dirty = efull_possible || dels[bl] || zb0[bl];
-            uint32_t slot = 0;
-            int s0 = node_slot(e, arena + nm.off, nm.len, false, &slot);
-            if (s0 == KWOK_OK && !(dirty && e->nodes[slot].zombie)) {
-                fix.push_back(i), fix.push_back(slot % e->Cn);
-            } else if (dirty) {
-                fix.push_back(i), fix.push_back(0x40000000u);  // REC_HARD
-            } else {
-                fix.push_back(i);
-                fix.push_back(resolve_placeholder(e, arena + nm.off, nm.len));
-            }
-        }
-    }
-    if ((rc = apply_fixes(e, I, fix))) return rc;
-    if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;  // placeholders' NS_SLOT
     // stable sort by bucket; the apply pass, one wave per bucket, in event order
     HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
     HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
     if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
         return e->fail(KWOK_EDEVICE, "ingest sort");
-    for (;;) {
-        e->ing_mutated = true;  // pod slots, node references and the pool change from here on
-        launch_ingest_apply(e->S, I, st);
-        HIPCHK(e, hipGetLastError());
-        if ((rc = read_summary(e, I.sum))) return rc;
-        if (e->debug_fail_apply == e->ing_chunk + 1)
-            return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", e->ing_chunk);
-        if ((rc = free_device_freed(e))) return rc;  // node entries the pass freed
-        if (G.sum_h->foreign) e->foreign_ips = true;
-        if (!G.sum_h->n_stopped) break;
-        // buckets stopped at a REC_HARD record: resolve it now (after the frees so far)
-        const uint32_t ns = G.sum_h->n_stopped;
-        std::vector<uint32_t> bk(ns), pos(ns), ix(ns);
-        HIPCHK(e, hipMemcpyAsync(bk.data(), G.stopped, ns * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipStreamSynchronize(st));
-        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&pos[k], G.beg + bk[k], 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipStreamSynchronize(st));
-        for (uint32_t k = 0; k < ns; k++) HIPCHK(e, hipMemcpyAsync(&ix[k], I.idx_sorted + pos[k], 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(e, hipStreamSynchronize(st));
-        fix.clear();
-        for (uint32_t i : ix) {
-            const kwok_str nm = ev[i].node_name;
-            uint32_t slot = 0;
-            if (node_slot(e, arena + nm.off, nm.len, false, &slot) == KWOK_OK) fix.push_back(i), fix.push_back(slot % e->Cn);
-            else fix.push_back(i), fix.push_back(resolve_placeholder(e, arena + nm.off, nm.len));
-        }
-        if ((rc = apply_fixes(e, I, fix))) return rc;
-        if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;
-        HIPCHK(e, hipMemsetAsync(&I.sum->n_stopped, 0, 4, st));
-        HIPCHK(e, hipMemsetAsync(&I.sum->n_freed, 0, 4, st));
-    }
+    e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
+    launch_ingest_apply(e->S, I, st);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = read_summary(e, I.sum))) return rc;
+    if (e->debug_fail_apply == e->ing_chunk + 1)
+        return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", e->ing_chunk);
+    if (G.sum_h->foreign) e->foreign_ips = true;
     return (int)G.sum_h->rejected;
 }
 
@@ -1992,7 +1603,6 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I, const kwok_pod_event* ev,
 int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released) {
     const size_t RB = packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);  // record bytes
-    const kwok_pod_event* ev = packed ? nullptr : static_cast<const kwok_pod_event*>(recs);
     auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
     drain(e);  // the device state reflects every submitted tick
@@ -2001,9 +1611,6 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     e->quiet = 0;
     if (!n) return 0;
     const auto t0 = clk::now();
-    // node ops an earlier call deferred (retire's frees) land before the pass reads node states
-    if (node_ops_pending(e))
-        if (int rc = flush_ops(e)) return rc;
     int rc = ingest_reserve(e, n, arena_len);
     if (rc) return rc;
     auto& G = e->ing;
@@ -2036,7 +1643,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         b.ev = rec_at(zev ? zev : (const void*)G.d_ev, lo);
         if (zar) b.arena = (const uint8_t*)zar;
         b.rec += lo, b.keys += lo, b.keys_sorted += lo, b.idx_sorted += lo;
-        b.out_handle += lo, b.out_status += lo, b.out_released += lo, b.byname += lo;
+        b.out_handle += lo, b.out_status += lo, b.out_released += lo;
         if (k & 1) b.creates = G.creates1, b.dels = G.dels1, b.sum = G.sum1;
         return b;
     };
@@ -2070,7 +1677,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             const auto tc = clk::now();
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
             e->ing_chunk = k;
-            const int r = ingest_chunk(e, I, ev ? ev + lo : nullptr, arena);
+            const int r = ingest_chunk(e, I);
             if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
                                   ms_between(t0, tc), ms_between(t0, clk::now()));
             if (r < 0) return r;
@@ -2163,8 +1770,6 @@ int kwok_cni_pending(kwok_engine* e, int32_t* out, size_t cap, size_t* n_out) {
     if (!e->S.cni) return e->fail(KWOK_EINVAL, "kwok_cni_pending: the engine was created without enable_cni");
     drain(e);
     if (e->poisoned) return poisoned(e);
-    if (node_ops_pending(e))
-        if (int rc = flush_ops(e)) return rc;
     // scratch: the exchange list buffer (multi-rank ticks only, none in flight) and its counter
     HIPCHK(e, hipMemsetAsync(e->S.list_counts, 0, 4, e->st));
     launch_cni_pending(e->S, (int32_t*)e->S.use_list, e->S.list_counts, e->st);
@@ -2227,7 +1832,7 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     if (e->poisoned) return poisoned(e);
     drain(e);  // the host mirrors reflect every submitted tick
     if (e->poisoned) return poisoned(e);
-    e->stage[0].puts.insert(e->stage[0].puts.end(), ips, ips + n);
+    e->puts.insert(e->puts.end(), ips, ips + n);
     e->quiet = 0;
     e->foreign_ips = true;  // releases of another rank's pods (multi rank)
     return flush_ops(e);
@@ -2261,15 +1866,10 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     if (e->debug_fault_tick && e->front_launches + 1 == e->debug_fault_tick && !requeue) nhb++;  // tests: TICK_ERR_LAYOUT
     if (e->hb_pre_dirty) {
         // heartbeat handles are written in node order at per-chain-block bases:
-        // managed nodes of the buckets before each block's range (host-maintained)
-        HIPCHK(e, hipStreamSynchronize(st));  // hb_pre_h is pinned staging read by a queued copy
-        uint32_t acc = 0, bk = 0;
-        for (uint32_t b = 0; b <= S.n_chain; b++) {
-            const uint32_t lo = (uint32_t)((uint64_t)e->nb * b / S.n_chain);
-            for (; bk < lo; bk++) acc += e->mb_count[bk];
-            e->hb_pre_h[b] = acc;
-        }
-        HIPCHK(e, hipMemcpyAsync(e->d_hb_pre, e->hb_pre_h, sizeof(uint32_t) * (S.n_chain + 1), hipMemcpyHostToDevice, st));
+        // managed nodes of the buckets before each block's range (k_hb_pre, from
+        // the node batches' per-bucket counts)
+        launch_hb_pre(S, e->d_hb_pre, st);
+        HIPCHK(e, hipGetLastError());
         e->hb_pre_dirty = false;
     }
     // a long heartbeat stream is shared with the chain blocks once they are done
@@ -2326,11 +1926,11 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         }
         rc = exchange(e, S.xmsg, sizeof(XMsg), e->d_xall);
         if (rc) return rc;
-        launch_emulate_msgs(S, e->d_xall, (uint32_t)e->XW, st);  // (diagnostics only: XW > W)
+        if (e->XW > e->W) launch_emulate_msgs(S, e->d_xall, (uint32_t)e->XW, st);  // (diagnostics: one rank, XW > 1)
         if (spec) {
             const uint32_t per = S.xcap_u + S.xcap_r;
             if ((rc = exchange(e, e->d_ssend, (size_t)per * 4, e->d_srecv))) return rc;
-            launch_emulate_lists(S, e->d_srecv, per, (uint32_t)e->XW, per, st);  // (diagnostics)
+            if (e->XW > e->W) launch_emulate_lists(S, e->d_srecv, per, (uint32_t)e->XW, per, st);  // (diagnostics)
             launch_pool_apply_spec(S, e->d_srecv, st);
             HIPCHK(e, hipGetLastError());
         }
@@ -2406,7 +2006,8 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     }
     rc = exchange(e, e->d_xsend, maxl * 4, e->d_xrecv);
     if (rc) return rc;
-    launch_emulate_lists(S, e->d_xrecv, maxl, (uint32_t)e->XW, (uint32_t)(me.n_use + me.n_rel), st);  // (diagnostics)
+    if (e->XW > e->W)  // (diagnostics)
+        launch_emulate_lists(S, e->d_xrecv, maxl, (uint32_t)e->XW, (uint32_t)(me.n_use + me.n_rel), st);
     std::vector<ListDesc> ld(e->XW);
     for (int r = 0; r < e->XW; r++) {
         ld[r].use = e->d_xrecv + (size_t)r * maxl;
@@ -2499,7 +2100,6 @@ void trace_tick(kwok_engine* e) {
 }
 
 
-int free_zombies(kwok_engine* e);  // (below)
 
 // Finish the oldest queued tick on the host: wait for it, complete a multi-rank
 // tick with long lists, derive the header, check errors, mirror DeletePods into
@@ -2617,20 +2217,12 @@ int retire(kwok_engine* e) {
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));
-    // deleted nodes whose last pod this tick deleted: freed once no tick is queued
-    // behind this one (node_refs synchronises the engine stream, which would wait
-    // for that tick too); every ingest drains the queue first, so the slots are
-    // free again before any record could take them
-    if (H.n_del) e->zombie_check = true;
-    if (e->zombie_check && next < 0) {
-        e->zombie_check = false;
-        if (int rc = free_zombies(e)) return failed(rc);
-    }
-    // the slot-freeing ops of deleted nodes without pods: no tick reads such a
-    // node, so with a tick already queued they wait for the next flush
-    if (node_ops_pending(e) && next < 0) {
-        int rc = flush_ops(e);
-        if (rc) return failed(rc);
+    // deleted nodes (and placeholders) whose last pod this tick deleted: their
+    // entries go (k_free_zombies, queued on the engine stream: a tick already
+    // queued behind this one reads no such node; every ingest follows it)
+    if (H.n_del) {
+        launch_free_zombies(e->S, e->st);
+        if (hipGetLastError() != hipSuccess) return failed(e->fail(KWOK_EDEVICE, "k_free_zombies"));
     }
     kwok_tick_result& r = T.res;
     memset(&r, 0, sizeof(r));
@@ -2656,22 +2248,6 @@ int retire(kwok_engine* e) {
     return KWOK_OK;
 }
 
-// After a tick that deleted pods (DeletePods): the entries of deleted nodes
-// (zombies) no pod references any more are freed, as the last pod's removal
-// frees them at ingest (the device counts the references).
-int free_zombies(kwok_engine* e) {
-    std::vector<uint32_t> z;
-    for (uint32_t bl = 0; bl < e->nb; bl++)
-        if (e->zb_count[bl])
-            for (uint32_t i = 0; i < e->Cn; i++)
-                if (e->nodes[(size_t)bl * e->Cn + i].zombie) z.push_back(bl * e->Cn + i);
-    if (z.empty()) return KWOK_OK;
-    std::vector<uint32_t> refs;
-    if (int rc = node_refs(e, z, refs)) return rc;
-    for (size_t k = 0; k < z.size(); k++)
-        if (!refs[k]) free_node(e, z[k], false);
-    return KWOK_OK;
-}
 
 // every queued tick finished on the host (before anything that reads or changes
 // the host mirrors or device state outside the tick stream)
@@ -2707,7 +2283,6 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     kwok_engine::TickSlot& T = e->slots[k];
     int rc = grow_arena(e, T);
     if (rc) return rc;
-    if (node_ops_pending(e) && (rc = flush_ops(e))) return rc;  // deferred by retire
     if (k == e->cur) e->cur = -1;  // its outputs are overwritten
     T.now = (uint64_t)now_unix;
     T.epoch = e->hb_epoch;
@@ -2918,9 +2493,24 @@ int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], ui
 }
 
 int kwok_node_has(kwok_engine* e, const char* name, size_t len) {
-    if (!e || !name) return 0;
-    uint32_t slot = 0;
-    return node_slot(e, name, len, false, &slot) == KWOK_OK && e->nodes[slot].managed;
+    // nodesSets.Has (node_controller.go:140-143): the device directory's entry is managed
+    if (!e || !name || !len || len > NODE_NAME_MAX || e->poisoned) return 0;
+    if (ensure_pinned(e, NAME_STRIDE + 64)) return 0;
+    uint8_t* h = static_cast<uint8_t*>(e->pinned);
+    uint8_t* d = static_cast<uint8_t*>(e->d_ops);
+    memcpy(h, name, len);
+    const uint32_t n32 = (uint32_t)len;
+    memcpy(h + NAME_STRIDE, &n32, 4);
+    uint32_t res = 0;
+    if (hipMemcpyAsync(d, h, NAME_STRIDE + 4, hipMemcpyHostToDevice, e->st) != hipSuccess) return 0;
+    launch_node_lookup(e->S, d, reinterpret_cast<const uint32_t*>(d + NAME_STRIDE), 1,
+                       reinterpret_cast<uint32_t*>(d + NAME_STRIDE + 16), e->st);
+    if (hipGetLastError() != hipSuccess || release_for_host(e) ||
+        hipMemcpyAsync(h + NAME_STRIDE + 16, d + NAME_STRIDE + 16, 4, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+        hipStreamSynchronize(e->st) != hipSuccess)
+        return 0;
+    memcpy(&res, h + NAME_STRIDE + 16, 4);
+    return (res & NS_MANAGED) != 0;
 }
 
 uint64_t kwok_node_size(kwok_engine* e) { return e ? e->n_managed : 0; }

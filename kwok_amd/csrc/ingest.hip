@@ -9,18 +9,26 @@
 //
 //   k_ing_prep    one thread per record: every check that depends on the
 //                 record alone (arena bounds, IPv4 strings, spec id, phase,
-//                 creation time, handle -> owned bucket), the statuses that
-//                 need no state, per-bucket create counts (growth check), the
-//                 owned by-name creates (spec.nodeName: the host resolves the
-//                 name to its node slot).
+//                 creation time, handle -> owned bucket, spec.nodeName -> its
+//                 bucket), the statuses that need no state, per-bucket create
+//                 counts (growth check).
 //   k_ing_need    live pods + creates of every bucket with creates.
 //   radix sort    a stable sort of the batch by bucket (rocprim), bucket ranges.
 //   k_ing_apply   one wave per bucket, its records in event order: the slot
 //                 policy (lowest free slot, canonical), coalescing by applying
-//                 each record to the state in order, node references (a
-//                 deleted node's entry lives while pods reference it,
-//                 node_controller.go:265-269), ingest-time IP release
-//                 (ipPool.Put, pod_controller.go:329-336), statuses and handles.
+//                 each record to the state in order, a by-name create's node
+//                 resolved in the bucket's node directory (a placeholder entry
+//                 if it has none), node references (a deleted node's entry
+//                 lives while pods reference it, node_controller.go:265-269),
+//                 ingest-time IP release (ipPool.Put, pod_controller.go:329-336),
+//                 statuses and handles.
+//
+// Node batches (kwok_ingest_nodes, node_controller.go:256-270) take the same
+// shape over the device-side node directory (node_key / node_name): k_nd_prep
+// (record checks, names copied and hashed; statuses that need the host's string
+// work are completed by k_nd_fix), the same stable sort, and k_nd_apply, one wave
+// per bucket in event order (lookup, lowest free entry, managed-set counts,
+// references of a deleted node).
 //
 // Records are 48-byte kwok_pod_event; the per-record work is a handful of
 // loads and stores, so the batch is bound by its H2D copy and by the serial
@@ -226,12 +234,12 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
             } else {
                 const uint32_t b = d_fnv1a32(I.arena + x.node_name.off, x.node_name.len) & (S.buckets - 1);
                 if (b < S.b_lo || b >= S.b_lo + S.nb) st = KWOK_ENOTMINE;
-                else r.bucket = b - S.b_lo, I.byname[atomicAdd(&I.sum->n_byname, 1u)] = i;
+                else r.bucket = b - S.b_lo, atomicAdd(&I.sum->n_byname, 1u);
             }
         }
         // growth check: creates per bucket (an upper bound: the batch's deletes are not netted out)
         if (st == 1 && x.op == KWOK_OP_UPSERT && x.handle < 0) atomicAdd(&I.creates[r.bucket], 1u);
-        // buckets where a pod leaves at ingest (a node entry may be freed mid-batch: by-name resolution)
+        // buckets where a pod leaves at ingest
         if (st == 1 && x.op == KWOK_OP_DELETE && !I.dels[r.bucket]) I.dels[r.bucket] = 1u;
     }
     I.rec[i] = r;
@@ -264,28 +272,6 @@ __global__ void k_ing_need(DevState S, IngestBatch I) {
     }
 }
 
-// host resolutions of by-name creates: code = node index in the bucket, or
-// 0x8000'0000 | (uint8)status (final), or 0x4000'0000 (REC_HARD: resolved later)
-__global__ void k_ing_fix(DevState S, IngestBatch I, const uint32_t* fix, uint32_t n_fix) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_fix) return;
-    const uint32_t i = fix[2 * k], code = fix[2 * k + 1];
-    if (code & 0x80000000u) {
-        const int st = (int)(int8_t)(code & 0xFFu);
-        I.out_handle[i] = -1;
-        I.out_status[i] = st;
-        I.out_released[i] = 0;
-        I.keys[i] = S.nb;
-        I.rec[i].chk = (uint8_t)(I.rec[i].chk | REC_FINAL);  // (a stopped bucket's record: skipped on relaunch)
-        if (st != KWOK_OK) atomicAdd(&I.sum->rejected, 1u);
-    } else if (code & 0x40000000u) {
-        I.rec[i].chk = (uint8_t)((I.rec[i].chk | REC_HARD) & ~REC_RESOLVED);
-    } else {
-        I.rec[i].pos = code;
-        I.rec[i].chk = (uint8_t)((I.rec[i].chk | REC_RESOLVED) & ~REC_HARD);
-    }
-}
-
 // bucket ranges of the sorted batch: beg / end (zeroed before: empty buckets are [0, 0))
 __global__ void k_ing_ranges(DevState S, IngestBatch I) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -300,6 +286,84 @@ __global__ void k_ing_ranges(DevState S, IngestBatch I) {
 // k_ing_apply: one wave per bucket, its records in event order.
 // ---------------------------------------------------------------------------
 constexpr int APPLY_WAVES = 4;
+
+// ---- node directory (device.h): one wave owns a bucket's entries at a time ----
+__device__ __forceinline__ uint64_t name_key(uint32_t h, uint32_t len) { return (uint64_t)h | ((uint64_t)len << 32); }
+// lane l's 4 name bytes (zero past len) from any alignment
+__device__ __forceinline__ uint32_t name_word(const uint8_t* nm, uint32_t len, uint32_t o) {
+    uint32_t w = 0;
+    for (uint32_t j = 0; j < 4; j++)
+        if (o + j < len) w |= (uint32_t)nm[o + j] << (8 * j);
+    return w;
+}
+// do node entry g's name bytes equal nm's (len bytes)?  (coherent loads: this wave may have written them)
+__device__ bool name_eq(const DevState& S, size_t g, const uint8_t* nm, uint32_t len) {
+    const uint32_t o = lane() * 4;
+    bool bad = false;
+    if (o < len) bad = ld_coh(reinterpret_cast<const uint32_t*>(S.node_name + g * NAME_STRIDE + o)) != name_word(nm, len, o);
+    return !__ballot(bad);
+}
+// the index of bucket b's entry named nm, or -1
+__device__ int32_t dir_find(const DevState& S, uint32_t b, uint64_t key, const uint8_t* nm, uint32_t len) {
+    const size_t nbase = (size_t)b * S.cn;
+    for (uint32_t j0 = 0; j0 < S.cn; j0 += 64) {
+        const uint32_t j = j0 + lane();
+        uint64_t m = __ballot(j < S.cn && ld_coh(S.node_key + nbase + j) == key);
+        while (m) {
+            const uint32_t c = j0 + (uint32_t)__builtin_ctzll(m);
+            if (name_eq(S, nbase + c, nm, len)) return (int32_t)c;
+            m &= m - 1;
+        }
+    }
+    return -1;
+}
+// the lowest free entry of bucket b (no NS_SLOT; the host's first_free of round 3), or -1
+__device__ int32_t dir_free(const DevState& S, uint32_t b) {
+    const size_t nbase = (size_t)b * S.cn;
+    for (uint32_t j0 = 0; j0 < S.cn; j0 += 64) {
+        const uint32_t j = j0 + lane();
+        const uint64_t m = __ballot(j < S.cn && !(ld8_coh(S.node_state + nbase + j) & NS_SLOT));
+        if (m) return (int32_t)(j0 + (uint32_t)__builtin_ctzll(m));
+    }
+    return -1;
+}
+// entry g takes the name (its state is the caller's)
+__device__ void dir_write(const DevState& S, size_t g, uint64_t key, const uint8_t* nm, uint32_t len) {
+    const uint32_t o = lane() * 4;
+    if (o < len) *reinterpret_cast<uint32_t*>(S.node_name + g * NAME_STRIDE + o) = name_word(nm, len, o);
+    if (lane() == 0) S.node_key[g] = key;
+}
+// entry g goes (no name, no state, no blob)
+__device__ __forceinline__ void dir_clear(const DevState& S, size_t g) {
+    if (lane() == 0) {
+        S.node_key[g] = 0;
+        S.node_state[g] = 0;
+        S.node_blob[g] = 0;
+    }
+}
+// does a live pod of bucket b (pods below its fill mark) reference node index nd?
+// (node batches: no pod changes during one, plain loads)
+__device__ bool pods_reference(const DevState& S, uint32_t b, uint32_t nd) {
+    const uint32_t fill = S.pod_fill[b];
+    const size_t sb = (size_t)b * S.cp;
+    bool hit = false;
+    for (uint32_t s0 = 0; s0 < fill && !hit; s0 += 512) {
+        const uint32_t s = s0 + lane() * 8;
+        bool h = false;
+        if (s < fill) {
+            const uint4 st = *reinterpret_cast<const uint4*>(S.pod_state + sb + s);
+            const uint4 ndw = *reinterpret_cast<const uint4*>(S.pod_node + sb + s);
+            const uint32_t a[4] = {st.x, st.y, st.z, st.w}, q[4] = {ndw.x, ndw.y, ndw.z, ndw.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                h |= (a[k] & PS_USED) && (q[k] & 0xFFFFu) == nd;
+                h |= ((a[k] >> 16) & PS_USED) && (q[k] >> 16) == nd;
+            }
+        }
+        hit = __ballot(h) != 0;
+    }
+    return hit;
+}
 constexpr uint32_t MAX_BM_WORDS = 65536 / 64;  // Cp <= 65528 (pod_handle_stride)
 
 struct Bucket {
@@ -412,10 +476,11 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     }
     lds_sync();
     const uint32_t keep_ex = PS_EVENT | PS_DELETE_PENDING;
-    uint32_t rejected = 0;
-    bool stopped = false, foreign = false;
+    uint32_t rejected = 0, n_freed = 0, n_ph = 0;
+    int32_t dzb = 0;  // zombie entries made (placeholders) and freed
+    bool foreign = false;
     uint32_t p0 = pbeg;
-    for (; p0 < pend && !stopped; p0 += 64) {
+    for (; p0 < pend; p0 += 64) {
         mem_sync();  // the previous chunk's stores, before this chunk's (coherent) loads
         const uint32_t p = p0 + l;
         const bool v = p < pend;
@@ -441,13 +506,13 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         uint32_t ns0 = 0;
         if (v && nd0 < B.cn) ns0 = ld8_coh(S.node_state + B.nbase + nd0);
         // ---- parallel path: a chunk in which no record can see another's effect
-        // except through the creates' slot order (no DELETE, no record waiting for
-        // the host, no slot named twice, no existing record on a free slot beside
-        // creates, enough free slots for every create: no node entry can go) ----
+        // except through the creates' slot order (no DELETE, no by-name create, no
+        // slot named twice, no existing record on a free slot beside creates, enough
+        // free slots for every create: no node entry can go) ----
         {
             const uint32_t op = (hop >> 16) & 0xFFu, fl = hfl & 0xFFu;
             const int fst = (int)(int8_t)((hfl >> 16) & 0xFFu);
-            const bool act = v && !(chk & REC_FINAL);
+            const bool act = v;
             const bool exl = act && (chk & REC_EXISTING);
             const bool used = exl && pos < B.cp && ((B.bm[pos >> 6] >> (pos & 63)) & 1);
             const bool crt = act && !exl;  // (prep decided creates with a bad field, or foreign / unknown)
@@ -455,7 +520,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
             const uint32_t key = exl ? pos : (0x80000000u | l);
             bool dup = false;
             for (uint32_t j = 0; j < 63; j++) dup |= (l > j) && key == rdl(key, j);
-            bool par = !__ballot((act && ((chk & REC_HARD) && !(chk & REC_RESOLVED))) || (act && op == KWOK_OP_DELETE) || dup) &&
+            bool par = !__ballot((act && !exl && (chk & REC_BY_NAME)) || (act && op == KWOK_OP_DELETE) || dup) &&
                        !(__ballot(exl && !used) && __ballot(crt));
             uint32_t* flist = flist_all[w];
             const uint64_t tm = __ballot(take);
@@ -531,17 +596,6 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         for (uint32_t k = 0; k < cnt; k++) {
             const uint32_t kchk = rdl(chk, k);
             const uint32_t kop = (rdl(hop, k) >> 16) & 0xFFu;
-            if (kchk & REC_FINAL) continue;  // its status came from the host's resolution
-            if ((kchk & REC_HARD) && !(kchk & REC_RESOLVED)) {
-                // by name, and the node entry may have been freed by the records before:
-                // the host resolves it and launches the bucket again from here
-                if (l == 0) {
-                    I.beg[b] = p0 + k;
-                    I.stopped[atomicAdd(&I.sum->n_stopped, 1u)] = b;
-                }
-                stopped = true;
-                break;
-            }
             const uint32_t kidx = rdl(idx, k), kpos = rdl(pos, k);
             const uint32_t kfl = rdl(hfl, k);
             const uint32_t flags = kfl & 0xFFu;
@@ -565,20 +619,50 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                 }
             }
             uint32_t ns = rdl(ns0, k);
-            if (nd != rdl(nd0, k) && nd < B.cn) {  // the slot's node changed in this chunk: its state now
+            // a create naming its node by spec.nodeName: the bucket's entry of that name
+            // now (after the records before it), or a placeholder entry the pod references
+            // (the oracle's node_entry); EFULL when the bucket has no free entry
+            const bool byname = !existing && (kchk & REC_BY_NAME) && kop == KWOK_OP_UPSERT && fst == KWOK_OK;
+            int bst = KWOK_OK;
+            uint32_t bnd = kpos;
+            if (byname) {
+                const kwok_str nr = static_cast<const kwok_pod_event*>(I.ev)[kidx].node_name;
+                const uint8_t* nm = I.arena + nr.off;
+                const uint64_t key = name_key(d_fnv1a32(nm, nr.len), nr.len);
                 mem_sync();
-                ns = ld8_coh(S.node_state + B.nbase + nd);
-            }
-            if (nd < B.cn) {
-                const uint64_t m = __ballot(wfreed == nd);
-                if (m) ns = 0;  // freed by an earlier record of this chunk
+                int32_t r = dir_find(S, b, key, nm, nr.len);
+                if (r < 0) {
+                    r = dir_free(S, b);
+                    if (r < 0) {
+                        bst = KWOK_EFULL;
+                    } else {
+                        dir_write(S, B.nbase + r, key, nm, nr.len);
+                        if (l == 0) {
+                            S.node_state[B.nbase + r] = NS_SLOT;
+                            S.node_blob[B.nbase + r] = 0;
+                        }
+                        dzb++, n_ph++;
+                        if (wfreed == (uint32_t)r) wfreed = ~0u;  // the index holds an entry again
+                    }
+                }
+                if (r >= 0) {
+                    bnd = (uint32_t)r;
+                    mem_sync();
+                    ns = ld8_coh(S.node_state + B.nbase + bnd);
+                }
+            } else {
+                if (nd != rdl(nd0, k) && nd < B.cn) {  // the slot's node changed in this chunk: its state now
+                    mem_sync();
+                    ns = ld8_coh(S.node_state + B.nbase + nd);
+                }
+                if (nd < B.cn) {
+                    const uint64_t m = __ballot(wfreed == nd);
+                    if (m) ns = 0;  // freed by an earlier record of this chunk
+                }
             }
             auto free_node = [&](uint32_t n) {  // the node entry goes (free_node_if_unused)
-                if (l == 0) {
-                    S.node_state[B.nbase + n] = 0;
-                    S.node_blob[B.nbase + n] = 0;
-                    I.freed[atomicAdd(&I.sum->n_freed, 1u)] = (uint32_t)(B.nbase + n);
-                }
+                dir_clear(S, B.nbase + n);
+                dzb--, n_freed++;  // (a zombie: NS_SLOT without NS_EXISTS)
                 if (l == k) wfreed = n;
             };
             if (stt == KWOK_OK && kop == KWOK_OP_DELETE) {
@@ -605,10 +689,10 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                 if ((ns & NS_SLOT) && !(ns & NS_EXISTS) && !node_referenced(S, B, nd)) free_node(nd);
                 handle = (int32_t)((S.b_lo + b) * S.pod_stride + kpos);
             } else if (stt == KWOK_OK && kop == KWOK_OP_UPSERT) {
-                stt = fst;
+                stt = fst != KWOK_OK ? fst : bst;
                 uint32_t slot = kpos;
                 if (stt == KWOK_OK && !existing) {
-                    nd = kpos;  // the node's index (by handle, or resolved by the host)
+                    nd = bnd;  // the node's index (by handle, or resolved by name above)
                     if (!(ns & NS_SLOT)) stt = KWOK_ENOTFOUND;
                     if (stt == KWOK_OK) {
                         const int32_t s = first_free(B);
@@ -654,35 +738,14 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     }
     if (l == 0) {
         if (B.fill != fill0) S.pod_fill[b] = (uint16_t)B.fill;
-        if (!stopped) I.beg[b] = pend;  // done: a relaunch after a stop skips the bucket
+        if (dzb) S.zb_count[b] += (uint32_t)dzb;
         if (rejected) atomicAdd(&I.sum->rejected, rejected);
+        if (n_freed) atomicAdd(&I.sum->n_freed, n_freed);
+        if (n_ph) atomicAdd(&I.sum->n_placeholders, n_ph);
     }
     if (__ballot(foreign) && l == 0) {
         atomicOr(&I.sum->foreign, 1u);
     }
-}
-
-// live pods referencing node slot slots[i] (one wave each)
-__global__ void k_node_refs(DevState S, const uint32_t* slots, uint32_t n, uint32_t* refs) {
-    const uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    if (i >= n) return;
-    const uint32_t slot = slots[i], b = slot / S.cn, nd = slot % S.cn;
-    const uint32_t fill = S.pod_fill[b];
-    const size_t sb = (size_t)b * S.cp;
-    uint32_t c = 0;
-    // 8 slots per lane per step (16-byte loads of state and node index): few round trips
-    for (uint32_t s = lane() * 8; s < fill; s += 512) {
-        const uint4 st = *reinterpret_cast<const uint4*>(S.pod_state + sb + s);
-        const uint4 ndw = *reinterpret_cast<const uint4*>(S.pod_node + sb + s);
-        const uint32_t a[4] = {st.x, st.y, st.z, st.w}, q[4] = {ndw.x, ndw.y, ndw.z, ndw.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            c += (a[k] & PS_USED) && (q[k] & 0xFFFFu) == nd;
-            c += ((a[k] >> 16) & PS_USED) && (q[k] >> 16) == nd;
-        }
-    }
-    for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
-    if (lane() == 0) refs[i] = c;
 }
 
 // kwok_cni_assign (handles deduplicated by the host, last assignment kept):
@@ -714,6 +777,256 @@ __global__ void k_cni_assign(DevState S, const int32_t* handles, const uint32_t*
     status[i] = st;
 }
 
+
+// ===========================================================================
+// Node batches: the WatchNodes / ListNodes event switch (node_controller.go:
+// 256-270) over the device node directory.
+// ===========================================================================
+// k_nd_prep: one thread per record.  Name bounds (1..253 bytes inside the
+// arena), op, the status strings inside the arena; the name copied to
+// names[i * NAME_STRIDE] and hashed (its bucket; another rank's: ENOTMINE).  An
+// UPSERT with an empty status renders the empty-status blob (kwok's own fleets);
+// any other status (or a custom node template) is completed by the host
+// (string checks, blob, CONFORMS: k_nd_fix) before the sort.
+__global__ void k_nd_prep(DevState S, NodeBatch N) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N.n) return;
+    const kwok_node_event x = N.ev[i];
+    NodeRec r;
+    r.hash = 0;
+    r.len = 0;
+    r.op = x.op;
+    r.fl = (uint8_t)((x.managed ? NR_MANAGED : 0) | (x.lockable ? NR_LOCKABLE : 0));
+    r.pad = 0;
+    r.blob = 0;
+    auto in_arena = [&](kwok_str q) { return (uint64_t)q.off + q.len <= N.arena_len; };
+    int st = 1;  // 1: the apply pass decides
+    bool host = false, mine = false;
+    uint32_t bucket = S.nb;
+    if (!x.name.len || x.name.len > NODE_NAME_MAX || !in_arena(x.name)) {
+        st = KWOK_EDOMAIN;
+    } else if (x.op != KWOK_OP_DELETE && x.op != KWOK_OP_UPSERT) {
+        st = KWOK_EINVAL;
+    } else {
+        bool inside = true, empty = true;
+        if (x.op == KWOK_OP_UPSERT) {
+            const kwok_str* q = &x.addresses;  // addresses, allocatable, capacity, node_info[]
+            for (int k = 0; k < 3 + KWOK_NI_COUNT; k++) inside &= in_arena(q[k]), empty &= q[k].len == 0;
+        }
+        if (!inside) {
+            st = KWOK_EDOMAIN;
+        } else {
+            const uint8_t* nm = N.arena + x.name.off;
+            uint8_t* dst = N.names + (size_t)i * NAME_STRIDE;
+            uint32_t h = 0x811C9DC5u;
+            for (uint32_t j = 0; j < x.name.len; j++) {
+                const uint8_t c = nm[j];
+                dst[j] = c;
+                h = (h ^ c) * 0x01000193u;
+            }
+            r.hash = h;
+            r.len = (uint8_t)x.name.len;
+            const uint32_t b = h & (S.buckets - 1);
+            mine = b >= S.b_lo && b < S.b_lo + S.nb;
+            if (mine) bucket = b - S.b_lo;
+            host = x.op == KWOK_OP_UPSERT && (!empty || N.host_all);
+            if (host) {
+                r.pad = mine ? 0 : 1;  // the host's string checks come first; then ENOTMINE (k_nd_fix)
+                N.host_idx[atomicAdd(&N.sum->n_host, 1u)] = i;
+            } else if (!mine) {
+                st = KWOK_ENOTMINE;
+            } else if (x.op == KWOK_OP_UPSERT) {
+                r.blob = N.empty_blob;  // an empty status: no CONFORMS (addresses etc. are absent, A.5)
+            }
+        }
+    }
+    if (host) r.fl |= NR_HOST;
+    N.rec[i] = r;
+    N.keys[i] = st == 1 && mine ? bucket : S.nb;
+    if (st != 1) {
+        N.out_handle[i] = -1;
+        N.out_status[i] = st;
+        if (st != KWOK_OK) atomicAdd(&N.sum->rejected, 1u);
+    }
+}
+
+// the host's completions: a status (the record changes nothing) or blob + CONFORMS
+__global__ void k_nd_fix(DevState S, NodeBatch N, const NodeFix* fix, uint32_t n_fix) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_fix) return;
+    const NodeFix f = fix[k];
+    const uint32_t i = f.idx;
+    const bool foreign = N.rec[i].pad != 0;
+    if (f.status != KWOK_OK || foreign) {
+        N.out_handle[i] = -1;
+        N.out_status[i] = f.status != KWOK_OK ? f.status : KWOK_ENOTMINE;
+        N.keys[i] = S.nb;
+        atomicAdd(&N.sum->rejected, 1u);
+    } else {
+        N.rec[i].blob = f.blob;
+        if (f.conforms) N.rec[i].fl = (uint8_t)(N.rec[i].fl | NR_CONFORMS);
+    }
+}
+
+__global__ void k_nd_ranges(DevState S, NodeBatch N) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N.n) return;
+    const uint32_t k = N.keys_sorted[p];
+    if (k >= S.nb) return;
+    if (p == 0 || N.keys_sorted[p - 1] != k) N.beg[k] = p;
+    if (p + 1 == N.n || N.keys_sorted[p + 1] != k) N.end[k] = p + 1;
+}
+
+// k_nd_apply: one wave per bucket, its records in event order (the round-3 host
+// pass, engine.cpp, restated per bucket: slots, names and states are per bucket)
+__global__ __launch_bounds__(64 * APPLY_WAVES) void k_nd_apply(DevState S, NodeBatch N) {
+    const uint32_t l = lane();
+    const uint32_t b = blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6);
+    if (b >= S.nb) return;
+    const uint32_t pbeg = N.beg[b], pend = N.end[b];
+    if (pbeg >= pend) return;
+    const size_t nbase = (size_t)b * S.cn;
+    int32_t dman = 0, dzb = 0;
+    uint32_t rejected = 0, freed = 0, created = 0;
+    bool changed = false;
+    for (uint32_t p = pbeg; p < pend; p++) {
+        const uint32_t idx = N.idx_sorted[p];
+        const NodeRec r = N.rec[idx];
+        const uint8_t* nm = N.names + (size_t)idx * NAME_STRIDE;
+        const uint64_t key = name_key(r.hash, r.len);
+        mem_sync();  // this wave's stores of the records before, ahead of its coherent loads
+        int32_t nd = dir_find(S, b, key, nm, r.len);
+        int st = KWOK_OK;
+        int32_t handle = -1;
+        if (r.op == KWOK_OP_DELETE) {
+            // node_controller.go:265-269: Deleted -> nodesSets.Delete; the entry lives
+            // while pods reference it (a zombie), else it goes
+            if (nd < 0) {
+                st = KWOK_ENOTFOUND;
+            } else {
+                const size_t g = nbase + (uint32_t)nd;
+                const uint32_t ns = ld8_coh(S.node_state + g);
+                if (ns & NS_MANAGED) dman--, changed = true;
+                const bool zombie = (ns & NS_SLOT) && !(ns & NS_EXISTS);
+                if (!pods_reference(S, b, (uint32_t)nd)) {
+                    dir_clear(S, g);
+                    dzb -= zombie ? 1 : 0;
+                    freed++;
+                } else {
+                    if (l == 0)
+                        S.node_state[g] = (uint8_t)(ns & ~(NS_EXISTS | NS_MANAGED | NS_EVENT_LOCK | NS_CONFORMS | NS_LOCKABLE));
+                    dzb += zombie ? 0 : 1;
+                }
+                handle = (int32_t)((S.b_lo + b) * S.cn + (uint32_t)nd);
+            }
+        } else {
+            // Added / Modified: the entry (a new one at the lowest free index), then
+            // needHeartbeat -> nodesSets.Put (never undone but by Delete), needLockNode
+            // -> the lock queue (:256-264)
+            uint32_t ns = 0;
+            if (nd < 0) {
+                nd = dir_free(S, b);
+                if (nd < 0) st = KWOK_EFULL;
+                else dir_write(S, nbase + (uint32_t)nd, key, nm, r.len), created++;
+            } else {
+                ns = ld8_coh(S.node_state + nbase + (uint32_t)nd);
+            }
+            if (st == KWOK_OK) {
+                const size_t g = nbase + (uint32_t)nd;
+                if ((ns & NS_SLOT) && !(ns & NS_EXISTS)) dzb--;  // a zombie exists again
+                const bool put = (r.fl & NR_MANAGED) && !(ns & NS_MANAGED);
+                if (put) dman++, changed = true;
+                const bool managed = (ns & NS_MANAGED) || (r.fl & NR_MANAGED);
+                const bool lock = (r.fl & NR_MANAGED) && (r.fl & NR_LOCKABLE);
+                const uint32_t bits = NS_SLOT | NS_EXISTS | (managed ? NS_MANAGED : 0) | ((r.fl & NR_LOCKABLE) ? NS_LOCKABLE : 0) |
+                                      ((r.fl & NR_CONFORMS) ? NS_CONFORMS : 0) | (lock ? NS_EVENT_LOCK : 0);
+                if (l == 0) {
+                    S.node_state[g] = (uint8_t)((ns & (lock ? 0u : (uint32_t)NS_EVENT_LOCK)) | bits);
+                    S.node_blob[g] = r.blob;
+                }
+                handle = (int32_t)((S.b_lo + b) * S.cn + (uint32_t)nd);
+            }
+        }
+        if (st != KWOK_OK) rejected++;
+        if (l == 0) {
+            N.out_handle[idx] = handle;
+            N.out_status[idx] = st;
+        }
+    }
+    if (l == 0) {
+        if (dman) S.mb_count[b] += (uint32_t)dman;
+        if (dzb) S.zb_count[b] += (uint32_t)dzb;
+        if (dman) atomicAdd(&N.sum->d_managed, dman);
+        if (changed) atomicOr(&N.sum->changed, 1u);
+        if (rejected) atomicAdd(&N.sum->rejected, rejected);
+        if (freed) atomicAdd(&N.sum->freed, freed);
+        if (created) atomicAdd(&N.sum->created, created);
+    }
+}
+
+// after a tick that deleted pods: zombie entries (deleted nodes, placeholders) no
+// live pod references any more go, as the last pod's removal at ingest frees them
+// (one wave per bucket holding zombies)
+__global__ __launch_bounds__(256) void k_free_zombies(DevState S) {
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= S.nb || S.zb_count[b] == 0) return;
+    const size_t nbase = (size_t)b * S.cn;
+    uint32_t gone = 0;
+    for (uint32_t j0 = 0; j0 < S.cn; j0 += 64) {
+        const uint32_t j = j0 + lane();
+        uint32_t ns = j < S.cn ? S.node_state[nbase + j] : 0u;
+        uint64_t m = __ballot((ns & NS_SLOT) && !(ns & NS_EXISTS));
+        while (m) {
+            const uint32_t c = j0 + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            if (!pods_reference(S, b, c)) dir_clear(S, nbase + c), gone++;
+        }
+    }
+    if (gone && lane() == 0) S.zb_count[b] -= gone;
+}
+
+// heartbeat handle bases: hb_pre[c] = managed nodes of the buckets before chain
+// block c's range [nb*c/Gc, ...); hb_pre[Gc] = all (one block)
+__global__ __launch_bounds__(1024) void k_hb_pre(DevState S, uint32_t* pre) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, T = blockDim.x, nc = S.n_chain;
+    auto lo = [&](uint32_t c) { return (uint32_t)((uint64_t)S.nb * c / nc); };
+    const uint32_t c0 = (uint32_t)((uint64_t)nc * t / T), c1 = (uint32_t)((uint64_t)nc * (t + 1) / T);
+    uint32_t sum = 0;
+    for (uint32_t bk = lo(c0); bk < lo(c1); bk++) sum += S.mb_count[bk];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < T; o <<= 1) {  // inclusive scan
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t acc = part[t] - sum;
+    for (uint32_t c = c0; c < c1; c++) {
+        pre[c] = acc;
+        for (uint32_t bk = lo(c); bk < lo(c + 1); bk++) acc += S.mb_count[bk];
+    }
+    if (t == T - 1) pre[nc] = acc;
+}
+
+// kwok_node_has: one wave per name
+__global__ void k_node_lookup(DevState S, const uint8_t* names, const uint32_t* lens, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const uint8_t* nm = names + (size_t)i * NAME_STRIDE;
+    const uint32_t len = lens[i];
+    uint32_t res = 0;
+    if (len && len <= NODE_NAME_MAX) {
+        const uint32_t h = d_fnv1a32(nm, len), b = h & (S.buckets - 1);
+        if (b >= S.b_lo && b < S.b_lo + S.nb) {
+            const int32_t nd = dir_find(S, b - S.b_lo, name_key(h, len), nm, len);
+            if (nd >= 0) res = S.node_state[(size_t)(b - S.b_lo) * S.cn + (uint32_t)nd];
+        }
+    }
+    if (lane() == 0) out[i] = res;
+}
+
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 }  // namespace
@@ -739,9 +1052,6 @@ void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st)
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st) {
     hipLaunchKernelGGL(k_ing_need, dim3(cdiv(S.nb, 4)), dim3(256), 0, st, S, I);
 }
-void launch_ingest_fix(const DevState& S, const IngestBatch& I, const uint32_t* fix, uint32_t n_fix, hipStream_t st) {
-    if (n_fix) hipLaunchKernelGGL(k_ing_fix, dim3(cdiv(n_fix, 256)), dim3(256), 0, st, S, I, fix, n_fix);
-}
 int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_t tmp_bytes, uint32_t key_bits,
                        hipStream_t st) {
     if (!I.n) return 0;
@@ -755,8 +1065,34 @@ int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_
 void launch_ingest_apply(const DevState& S, const IngestBatch& I, hipStream_t st) {
     hipLaunchKernelGGL(k_ing_apply, dim3(cdiv(S.nb, APPLY_WAVES)), dim3(64 * APPLY_WAVES), 0, st, S, I);
 }
-void launch_node_refs(const DevState& S, const uint32_t* slots, uint32_t n, uint32_t* refs, hipStream_t st) {
-    if (n) hipLaunchKernelGGL(k_node_refs, dim3(cdiv(n, 4)), dim3(256), 0, st, S, slots, n, refs);
+void launch_node_prep(const DevState& S, const NodeBatch& N, hipStream_t st) {
+    if (N.n) hipLaunchKernelGGL(k_nd_prep, dim3(cdiv(N.n, 256)), dim3(256), 0, st, S, N);
+}
+void launch_node_fix(const DevState& S, const NodeBatch& N, const NodeFix* fix, uint32_t n_fix, hipStream_t st) {
+    if (n_fix) hipLaunchKernelGGL(k_nd_fix, dim3(cdiv(n_fix, 256)), dim3(256), 0, st, S, N, fix, n_fix);
+}
+int launch_node_sort(const DevState& S, const NodeBatch& N, void* tmp, size_t tmp_bytes, uint32_t key_bits,
+                     hipStream_t st) {
+    if (!N.n) return 0;
+    rocprim::counting_iterator<uint32_t> it(0u);
+    if (rocprim::radix_sort_pairs(tmp, tmp_bytes, N.keys, N.keys_sorted, it, N.idx_sorted, N.n, 0u, key_bits, st) !=
+        hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_nd_ranges, dim3(cdiv(N.n, 256)), dim3(256), 0, st, S, N);
+    return 0;
+}
+void launch_node_apply(const DevState& S, const NodeBatch& N, hipStream_t st) {
+    hipLaunchKernelGGL(k_nd_apply, dim3(cdiv(S.nb, APPLY_WAVES)), dim3(64 * APPLY_WAVES), 0, st, S, N);
+}
+void launch_free_zombies(const DevState& S, hipStream_t st) {
+    hipLaunchKernelGGL(k_free_zombies, dim3(cdiv(S.nb, 4)), dim3(256), 0, st, S);
+}
+void launch_hb_pre(const DevState& S, uint32_t* hb_pre, hipStream_t st) {
+    hipLaunchKernelGGL(k_hb_pre, dim3(1), dim3(1024), 0, st, S, hb_pre);
+}
+void launch_node_lookup(const DevState& S, const uint8_t* names, const uint32_t* lens, uint32_t n, uint32_t* out,
+                        hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_node_lookup, dim3(cdiv(n, 4)), dim3(256), 0, st, S, names, lens, n, out);
 }
 void launch_cni_assign(const DevState& S, const int32_t* handles, const uint32_t* ips, const uint8_t* wr, uint32_t n,
                        int32_t* status, uint32_t* rejected, hipStream_t st) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "../../include/kwok_engine.h"
 #include "device.h"
 
 namespace kwok {
@@ -21,6 +22,11 @@ struct DevState {
     uint64_t* node_blob;
     uint8_t* node_tick;
     uint32_t n_node_slots;
+    // node directory (ingest.hip): names of the node entries, managed / zombie entries per bucket
+    uint64_t* node_key;        // [NL] fnv1a32(name) | len << 32, 0: free
+    uint8_t* node_name;        // [NL * NAME_STRIDE]
+    uint32_t* mb_count;        // [nb] managed nodes per owned bucket (heartbeat handle bases: k_hb_pre)
+    uint32_t* zb_count;        // [nb] zombie entries per owned bucket (NS_SLOT without NS_EXISTS)
     // pods (local slots)
     uint16_t* pod_state;
     uint16_t* pod_node;
@@ -81,7 +87,7 @@ struct DevState {
     uint32_t node_ip;
     TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
     uint16_t* pod_fill;        // per owned bucket: upper bound of used pod slots (only grows; the ingest pass)
-    const uint32_t* hb_pre;    // [n_chain + 1] managed nodes before each chain block (host-maintained)
+    const uint32_t* hb_pre;    // [n_chain + 1] managed nodes before each chain block (k_hb_pre)
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
@@ -169,11 +175,8 @@ struct IngestBatch {
     uint32_t* out_released;    // [n]
     uint32_t* creates;         // [nb] creates per bucket (growth check)
     uint32_t* dels;            // [nb] 1: the batch deletes a pod of the bucket (zeroed per batch)
-    uint32_t* byname;          // [n] batch indices of owned by-name creates (host resolution)
-    uint32_t* beg;             // [nb] first sorted position of each bucket (resume position after a stop)
+    uint32_t* beg;             // [nb] first sorted position of each bucket
     uint32_t* end;             // [nb]
-    uint32_t* stopped;         // [nb] buckets that stopped at a REC_HARD record
-    uint32_t* freed;           // [NL] node slots freed by the apply pass
     IngSummary* sum;
 };
 size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort temporary storage
@@ -183,15 +186,54 @@ void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st)
 void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st);
 // live pods + creates of every bucket with creates -> sum->need
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st);
-// host resolutions of by-name creates: (batch index, node index in its bucket | status << 16)
-void launch_ingest_fix(const DevState& S, const IngestBatch& I, const uint32_t* fix, uint32_t n_fix, hipStream_t st);
 // stable sort by bucket, bucket ranges
 int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_t tmp_bytes, uint32_t key_bits,
                        hipStream_t st);
 // the WatchPods / ListPods event switch, per bucket in event order (one wave per bucket)
 void launch_ingest_apply(const DevState& S, const IngestBatch& I, hipStream_t st);
-// live pods referencing each node slot of `slots` (a node entry may be freed when 0)
-void launch_node_refs(const DevState& S, const uint32_t* slots, uint32_t n, uint32_t* refs, hipStream_t st);
+
+// ---- node batches on the GPU (kwok_ingest_nodes, node_controller.go:256-270) ----
+struct NodeBatch {
+    const kwok_node_event* ev;  // [n] on the device or read in place
+    uint32_t n;
+    uint32_t host_all;          // custom node template: every UPSERT's blob comes from the host
+    const uint8_t* arena;
+    uint64_t arena_len;
+    uint64_t empty_blob;        // the blob word of an empty status (default template)
+    NodeRec* rec;               // [n]
+    uint8_t* names;             // [n * NAME_STRIDE] the records' names
+    uint32_t* keys;             // [n] owned local bucket, or nb (decided by prep / the host)
+    uint32_t* keys_sorted;
+    uint32_t* idx_sorted;
+    uint32_t* beg;              // [nb]
+    uint32_t* end;              // [nb]
+    int32_t* out_handle;        // [n]
+    int32_t* out_status;        // [n]
+    uint32_t* host_idx;         // [n] UPSERT records the host completes (status strings)
+    NodeSummary* sum;
+};
+// one host-completed record: its status, or its blob and flags
+struct NodeFix {
+    uint32_t idx;
+    int32_t status;  // KWOK_OK: apply with blob / conforms
+    uint64_t blob;
+    uint32_t conforms, pad;
+};
+// record-local checks, names copied, hashes, statuses that need no state
+void launch_node_prep(const DevState& S, const NodeBatch& N, hipStream_t st);
+void launch_node_fix(const DevState& S, const NodeBatch& N, const NodeFix* fix, uint32_t n_fix, hipStream_t st);
+// stable sort by bucket + bucket ranges (tmp: rocprim temporary storage, ingest_sort_bytes)
+int launch_node_sort(const DevState& S, const NodeBatch& N, void* tmp, size_t tmp_bytes, uint32_t key_bits,
+                     hipStream_t st);
+// the WatchNodes / ListNodes event switch, one wave per bucket in event order
+void launch_node_apply(const DevState& S, const NodeBatch& N, hipStream_t st);
+// zombie node entries (deleted / placeholder) no pod references any more are freed
+void launch_free_zombies(const DevState& S, hipStream_t st);
+// the managed nodes before each chain block (heartbeat handle bases) from mb_count
+void launch_hb_pre(const DevState& S, uint32_t* hb_pre, hipStream_t st);
+// kwok_node_has: names[i * NAME_STRIDE] (lens[i] bytes) -> out[i] = the entry's node_state (0: none)
+void launch_node_lookup(const DevState& S, const uint8_t* names, const uint32_t* lens, uint32_t n, uint32_t* out,
+                        hipStream_t st);
 // kwok_cni_assign: statuses of every record; wr[i]: record i is the handle's last
 // valid assignment (it writes the podIP)
 void launch_cni_assign(const DevState& S, const int32_t* handles, const uint32_t* ips, const uint8_t* wr, uint32_t n,

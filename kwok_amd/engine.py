@@ -224,13 +224,20 @@ class EngineBase:
         return out.value
 
     # -- ingest ---------------------------------------------------------------
-    def ingest_nodes_raw(self, events: np.ndarray, arena: bytes):
+    def ingest_nodes_raw(self, events: np.ndarray, arena, out=None):
+        """arena: bytes or a uint8 array; out: optional (handles, status)
+        arrays of len(events) (e.g. page-locked, host_array)"""
         n = len(events)
-        hs = np.empty(n, np.int32)
-        st = np.empty(n, np.int32)
+        if out is None:
+            hs, st = np.empty(n, np.int32), np.empty(n, np.int32)
+        else:
+            hs, st = (o[:n] for o in out)
         ev = np.ascontiguousarray(events, dtype=abi.NODE_EVENT_DTYPE)
-        rc = self._fn("ingest_nodes")(self._h, ev.ctypes.data, n, arena or b"\0", len(arena),
-                                      hs.ctypes.data, st.ctypes.data)
+        if isinstance(arena, np.ndarray):
+            ar, alen = C.cast(arena.ctypes.data, C.c_char_p), arena.nbytes
+        else:
+            ar, alen = arena or b"\0", len(arena)
+        rc = self._fn("ingest_nodes")(self._h, ev.ctypes.data, n, ar, alen, hs.ctypes.data, st.ctypes.data)
         self._check(rc, "ingest_nodes")
         return hs, st
 

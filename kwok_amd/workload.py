@@ -298,10 +298,22 @@ class Flap:
         self.k = max(1, int(len(self.idx) * frac))
         self.rng = np.random.default_rng(seed)
 
-    def batch(self):
-        """(events, arena): k Deleted records, then k Added records"""
+    def batch(self, compact=False, alloc=None):
+        """(events, arena): k Deleted records, then k Added records.  compact:
+        the batch's own arena of the k names (as a watch client decodes a
+        batch into one buffer), in alloc(shape, dtype) memory if given"""
         pick = self.rng.choice(self.idx, self.k, replace=False)
         src = self.fleet.node_events[pick]
         ev = np.concatenate([src, src])
         ev["op"][:self.k] = abi.OP_DELETE
-        return ev, self.fleet.arena
+        if not compact:
+            return ev, self.fleet.arena
+        names = self.fleet.names[pick]
+        w = names.shape[1]
+        ev["name"]["off"] = np.tile(np.arange(self.k, dtype=np.uint32) * w, 2)
+        mk = alloc or (lambda shape, dt: np.empty(shape, dt))
+        ar = mk((names.size,), np.uint8)
+        ar[:] = names.reshape(-1)
+        evp = mk((len(ev),), abi.NODE_EVENT_DTYPE)
+        evp[:] = ev
+        return evp, ar

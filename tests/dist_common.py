@@ -200,7 +200,10 @@ def run_all(runner, sc, pair=False):
     """Summaries of every tick of scenario sc (pair: each step is two ticks,
     queued back to back on backends that can)."""
     out = []
-    for n, p in sc:
+    trace = os.environ.get("KWOK_TEST_TRACE")
+    for t, (n, p) in enumerate(sc):
+        if trace:
+            print("[run_all] rank %d tick %d: %d node, %d pod records" % (runner.rank, t, len(n), len(p)), flush=True)
         r = runner.run_tick(n, p, pair=pair)
         out += [summarize(x) for x in (r if pair else [r])]
     return out

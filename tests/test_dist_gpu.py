@@ -22,6 +22,9 @@ def _worker(rank, world, port, outdir, big=False, pair=False, foreign_from=0):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     # two engines share one GPU: each persistent tick grid must fit beside the other
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KWOK_TICK_BLOCKS_PER_CU="1")
+    if os.environ.get("KWOK_TEST_TRACE"):  # a stuck rank shows where
+        import faulthandler
+        faulthandler.dump_traceback_later(60, exit=True)
     import torch.distributed as dist
     import dist_common as dc2
     from kwok_amd.engine import Engine
