@@ -1499,9 +1499,30 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     HIPCHK(e, hipMemsetAsync(G.nsum, 0, sizeof(NodeSummary), st));
     launch_node_prep(e->S, N, st);
     HIPCHK(e, hipGetLastError());
-    if ((rc = release_for_host(e))) return rc;
-    HIPCHK(e, hipMemcpyAsync(G.nsum_h, G.nsum, sizeof(NodeSummary), hipMemcpyDeviceToHost, st));
-    HIPCHK(e, hipStreamSynchronize(st));
+    // sort + apply + results queued right behind the prep: the apply pass returns at
+    // once on the device when the prep listed records for the host (then the host
+    // completes them and runs the sort and the pass again); one round trip otherwise
+    auto sort_apply_results = [&]() -> int {
+        HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
+        HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
+        if (launch_node_sort(e->S, N, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
+            return e->fail(KWOK_EDEVICE, "node sort");
+        launch_node_apply(e->S, N, st);
+        HIPCHK(e, hipGetLastError());
+        if (int r = release_for_host(e)) return r;
+        if (out_handles) HIPCHK(e, hipMemcpyAsync(G.res_h, G.out_handle, n * 4, hipMemcpyDeviceToHost, st));
+        if (out_status) HIPCHK(e, hipMemcpyAsync(G.res_h + n, G.out_status, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipMemcpyAsync(G.nsum_h, G.nsum, sizeof(NodeSummary), hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        return KWOK_OK;
+    };
+    // from the apply pass on the batch is in the device state: a failure poisons the engine
+    auto failed = [&](int r) {
+        e->poisoned = true;
+        return r;
+    };
+    if ((rc = upload_blobs(e))) return rc;  // (the empty-status blob, first batch)
+    if ((rc = sort_apply_results())) return failed(rc);
     const auto t1 = clk::now();
     const uint32_t n_host = G.nsum_h->n_host;
     if (n_host) {
@@ -1516,33 +1537,17 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         const bool par = n_host >= NODE_PAR_MIN && e->n_part > 1;
         run_parts(e, par, [&](int p) {
             const size_t lo = par ? (size_t)n_host * p / e->n_part : (p ? n_host : 0);
-            const size_t hi = par ? (size_t)n_host * (p + 1) / e->n_part : (p ? n_host : n_host);
+            const size_t hi = par ? (size_t)n_host * (p + 1) / e->n_part : n_host;
             for (size_t k = lo; k < hi; k++) fix[k] = complete_node(e, ev[idx[k]], idx[k], arena, blob_mu);
         });
         if ((rc = upload_blobs(e))) return rc;
         HIPCHK(e, hipMemcpyAsync(G.d_nfix, fix.data(), fix.size() * sizeof(NodeFix), hipMemcpyHostToDevice, st));
         launch_node_fix(e->S, N, G.d_nfix, n_host, st);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipStreamSynchronize(st));  // `fix` is pageable
+        N.force = 1;
+        if ((rc = sort_apply_results())) return failed(rc);
     }
-    if ((rc = upload_blobs(e))) return rc;  // (the empty-status blob, first batch)
     const auto t2 = clk::now();
-    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
-    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
-    if (launch_node_sort(e->S, N, G.sort_tmp, G.sort_bytes, sort_bits(e), st)) return e->fail(KWOK_EDEVICE, "node sort");
-    launch_node_apply(e->S, N, st);
-    // from here the batch is in the device state: a failure poisons the engine
-    auto failed = [&](int r) {
-        e->poisoned = true;
-        return r;
-    };
-    if (hipGetLastError() != hipSuccess) return failed(e->fail(KWOK_EDEVICE, "k_nd_apply launch"));
-    if (release_for_host(e) != KWOK_OK ||
-        (out_handles && hipMemcpyAsync(G.res_h, G.out_handle, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        (out_status && hipMemcpyAsync(G.res_h + n, G.out_status, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipMemcpyAsync(G.nsum_h, G.nsum, sizeof(NodeSummary), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return failed(e->fail(KWOK_EDEVICE, "node batch results"));
     if (out_handles) memcpy(out_handles, G.res_h, n * 4);
     if (out_status) memcpy(out_status, G.res_h + n, n * 4);
     const NodeSummary sum = *G.nsum_h;
@@ -1553,9 +1558,9 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     }
     if ((rc = size_arena(e))) return failed(rc);
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu node records (GPU%s): prep %.3f ms, host %u records %.3f ms, apply + results "
-                        "%.3f ms (%u created, %u freed)\n", n, zev ? ", read in place" : "", ms_between(t0, t1), n_host,
-                ms_between(t1, t2), ms_between(t2, clk::now()), sum.created, sum.freed);
+        fprintf(stderr, "[kwok ingest] %zu node records (GPU%s): prep + sort + apply + results %.3f ms, host %u "
+                        "records + again %.3f ms (%u created, %u freed)\n", n, zev ? ", read in place" : "",
+                ms_between(t0, t1), n_host, ms_between(t1, t2), sum.created, sum.freed);
     return (int)sum.rejected;
 }
 

@@ -885,6 +885,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_nd_apply(DevState S, NodeB
     if (b >= S.nb) return;
     const uint32_t pbeg = N.beg[b], pend = N.end[b];
     if (pbeg >= pend) return;
+    if (!N.force && N.sum->n_host) return;  // the host completes records first, then launches this again
     const size_t nbase = (size_t)b * S.cn;
     int32_t dman = 0, dzb = 0;
     uint32_t rejected = 0, freed = 0, created = 0;

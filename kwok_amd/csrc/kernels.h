@@ -197,6 +197,9 @@ struct NodeBatch {
     const kwok_node_event* ev;  // [n] on the device or read in place
     uint32_t n;
     uint32_t host_all;          // custom node template: every UPSERT's blob comes from the host
+    uint32_t force;             // k_nd_apply runs although records await the host (0: it returns then,
+                                // having been queued behind the prep speculatively)
+    uint32_t pad0;
     const uint8_t* arena;
     uint64_t arena_len;
     uint64_t empty_blob;        // the blob word of an empty status (default template)
