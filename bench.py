@@ -215,6 +215,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
                       "ingest": float(np.median([a for a, _ in steps])) * 1e3,
                       "tick": float(np.median([b for _, b in steps])) * 1e3},
+        "steps_ms": [[round(a * 1e3, 3), round(b * 1e3, 3)] for a, b in steps],  # (ingest, tick) per step
         "ingest_records_per_s": recs * world / ing if ing else None,
         "tick_transitions_per_s": trans / tck if tck else None,
         "kernel_ms": kern / ticks, "k_emit_ms": emit / ticks,
