@@ -308,6 +308,7 @@ struct kwok_engine {
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
+    bool results_kernel = false;  // KWOK_INGEST_RESULTS_KERNEL=1: pod batch results written into mapped host arrays by a kernel
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
@@ -1153,6 +1154,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_CHUNK")) e->debug_fail_chunk = (uint32_t)strtoul(v, nullptr, 10);
         if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_APPLY")) e->debug_fail_apply = (uint32_t)strtoul(v, nullptr, 10);
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
+        if (const char* v = getenv("KWOK_INGEST_RESULTS_KERNEL")) e->results_kernel = v[0] == '1';
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
         const char* qt = getenv("KWOK_QUIET");
@@ -1678,8 +1680,11 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         for (uint32_t k = 0; k < K; k++) {
             const size_t lo = lo_of(k);
             const IngestBatch I = chunk_batch(k);
+            const auto tw = clk::now();
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
             const auto tc = clk::now();
+            if (e->iprof && ms_between(tw, tc) > 0.5)
+                fprintf(stderr, "[kwok ingest]   chunk %u: wait for its prep enqueued in %.3f ms\n", k, ms_between(tw, tc));
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
             e->ing_chunk = k;
             const int r = ingest_chunk(e, I);
@@ -1692,15 +1697,30 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             HIPCHK(e, hipEventRecord(G.used[k & 1], st));
             hipStream_t rs = K > 1 ? G.dst : st;
             if (K > 1) HIPCHK(e, hipStreamWaitEvent(rs, G.used[k & 1], 0));
-            if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
-            if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
-            if (out_status8) {  // one byte per record over the link
-                launch_ingest_status8(I, G.out_status8 + lo, rs);
+            // KWOK_INGEST_RESULTS_KERNEL=1: results into kwok_host_alloc arrays written by a
+            // kernel through their mapped addresses instead of the copy engine (slower:
+            // 1.9 vs 1.45 ms per C4 batch; kept for A/B of the host-side stalls, §11)
+            int32_t* mh = out_handles ? (int32_t*)host_mapped(out_handles + lo, (size_t)I.n * 4) : nullptr;
+            int32_t* ms = out_status ? (int32_t*)host_mapped(out_status + lo, (size_t)I.n * 4) : nullptr;
+            int8_t* m8 = out_status8 ? (int8_t*)host_mapped(out_status8 + lo, I.n) : nullptr;
+            uint32_t* mr = out_released ? (uint32_t*)host_mapped(out_released + lo, (size_t)I.n * 4) : nullptr;
+            const bool mapped = e->results_kernel && (!out_handles || mh) && (!out_status || ms) &&
+                                (!out_status8 || m8) && (!out_released || mr);
+            if (mapped) {
+                launch_ingest_results(I, mh, ms, m8, mr, rs);
                 HIPCHK(e, hipGetLastError());
-                HIPCHK(e, hipMemcpyAsync(out_status8 + lo, G.out_status8 + lo, I.n, hipMemcpyDeviceToHost, rs));
+                HIPCHK(e, hipEventRecord(e->fence, rs));  // (system-scope release: the host reads them)
+            } else {
+                if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+                if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+                if (out_status8) {  // one byte per record over the link
+                    launch_ingest_status8(I, G.out_status8 + lo, rs);
+                    HIPCHK(e, hipGetLastError());
+                    HIPCHK(e, hipMemcpyAsync(out_status8 + lo, G.out_status8 + lo, I.n, hipMemcpyDeviceToHost, rs));
+                }
+                if (out_released)
+                    HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
             }
-            if (out_released)
-                HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
             if (k + 2 < K)
                 if (int r2 = prep(k + 2)) return r2;
         }
@@ -2398,7 +2418,8 @@ void* kwok_host_alloc(size_t bytes) {
         const size_t huge = (size_t)2 << 20, len = (bytes + huge - 1) & ~(huge - 1);
         void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p != MAP_FAILED) {
-            (void)madvise(p, len, MADV_HUGEPAGE);
+            const char* thp = getenv("KWOK_HOST_THP");
+            if (!(thp && thp[0] == '0')) (void)madvise(p, len, MADV_HUGEPAGE);
             memset(p, 0, len);  // first touch: the pages exist (huge where granted) before pinning
             if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
                 void* dev = nullptr;

@@ -1047,6 +1047,24 @@ __global__ void k_ing_status8(IngestBatch I, int8_t* dst) {
 void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st) {
     if (I.n) hipLaunchKernelGGL(k_ing_status8, dim3(cdiv(I.n, 256)), dim3(256), 0, st, I, dst);
 }
+// the batch's results straight into the caller's kwok_host_alloc arrays (their
+// device addresses; null: not wanted), four records per thread, no copy engine
+__global__ void k_ing_results(IngestBatch I, int32_t* handles, int32_t* status, int8_t* status8, uint32_t* released) {
+    const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = i0 + q;
+        if (i >= I.n) break;
+        if (handles) handles[i] = I.out_handle[i];
+        if (status) status[i] = I.out_status[i];
+        if (status8) status8[i] = (int8_t)I.out_status[i];
+        if (released) released[i] = I.out_released[i];
+    }
+}
+void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* status, int8_t* status8, uint32_t* released,
+                           hipStream_t st) {
+    if (I.n) hipLaunchKernelGGL(k_ing_results, dim3(cdiv(I.n, 1024)), dim3(256), 0, st, I, handles, status, status8, released);
+}
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st) {
     if (I.n) hipLaunchKernelGGL(k_ing_prep, dim3(cdiv(I.n, 256)), dim3(256), 0, st, S, I);
 }

@@ -184,6 +184,9 @@ size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort 
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st);
 // the batch's per-record statuses as bytes (kwok_ingest_pods_packed's out_status)
 void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st);
+// the per-record results written into mapped host arrays (device addresses of kwok_host_alloc memory; null: skip)
+void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* status, int8_t* status8, uint32_t* released,
+                           hipStream_t st);
 // live pods + creates of every bucket with creates -> sum->need
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st);
 // stable sort by bucket, bucket ranges
