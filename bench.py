@@ -72,6 +72,7 @@ NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only
 #   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
 INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
+CHURN_WARMUP = 8  # untimed churn batches before the timed steps (see churn_leg)
 PMC_FILE = "r3am_pmc.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
 
 
@@ -145,7 +146,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     kwok_ingest_pods of that batch (2 x n_churn records, host threads + H2D +
     apply kernel) + one kwok_tick (1M deletes + releases, 1M Pending->Running
     patches reusing the released IPs).  Event generation (which reads the pod
-    IPs back) sits between the timed steps.  The first step is warmup.
+    IPs back) sits between the timed steps.  CHURN_WARMUP untimed batches first.
     world > 1: every rank churns n_churn of its own pods per tick (weak
     scaling); the releases of all ranks cross the exchange (their lists are
     longer than the inline message: the second allgather), and each step is
@@ -176,10 +177,14 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     kern = emit = xch = 0.0
     last = None
     steps = []
-    for k in range(ticks + 2):
+    # warmup batches: the first ~6 churn batches of a process hold one ~6 ms host stall inside
+    # the HIP runtime, at any call, whatever the host allocation (tools/stall_probe.py,
+    # profiles/r4r_stall_ab.txt); once past it, the steps run within a few percent
+    warm = CHURN_WARMUP
+    for k in range(ticks + warm + 1):
         ev, ar = ch.batch(dump, now)
         barrier()
-        prof = k == ticks + 1  # one more step, profiled (HIP events), for the kernel times only
+        prof = k == ticks + warm  # one more step, profiled (HIP events), for the kernel times only
         if prof:
             e.profile_enable(True)
         t0 = time.perf_counter()
@@ -196,7 +201,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
             ph, nt = e.profile_read()
             e.profile_enable(False)
             kern, emit, xch = ph["kernel"] * ticks, ph["emit_kernel"] * ticks, ph["exchange"] * ticks
-        elif k:
+        elif k >= warm:
             a, b = max_over_ranks(t1 - t0), max_over_ranks(t2 - t0)
             ing += a
             tck += b - a
