@@ -72,7 +72,7 @@ NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only
 #   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
 INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
-CHURN_WARMUP = 8  # untimed churn batches before the timed steps (see churn_leg)
+CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
 PMC_FILE = "r3am_pmc.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
 
 
@@ -177,9 +177,8 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     kern = emit = xch = 0.0
     last = None
     steps = []
-    # warmup batches: the first ~6 churn batches of a process hold one ~6 ms host stall inside
-    # the HIP runtime, at any call, whatever the host allocation (tools/stall_probe.py,
-    # profiles/r4r_stall_ab.txt); once past it, the steps run within a few percent
+    # (the runtime's ~6 ms copy-engine queue creations, which used to land in one or two of a
+    # process's first churn batches, now happen at engine create: profiles/r4v_sdma_ab.txt)
     warm = CHURN_WARMUP
     for k in range(ticks + warm + 1):
         ev, ar = ch.batch(dump, now)

@@ -172,7 +172,11 @@ struct kwok_engine {
         uint32_t* out_released = nullptr;
         void* sort_tmp = nullptr;
         // per bucket (allocated once)
-        uint32_t *creates = nullptr, *dels = nullptr, *beg = nullptr, *end = nullptr;
+        uint32_t *creates = nullptr, *beg = nullptr, *end = nullptr;
+        uint32_t* abort = nullptr;          // [1] a chunk of the batch needs growth (speculative apply passes)
+        IngSummary* sums = nullptr;         // [nsums] one per chunk of a batch
+        IngSummary* sums_h = nullptr;       // pinned
+        size_t nsums = 0;
         IngSummary* sum = nullptr;
         // node batches (kwok_ingest_nodes): records, names, prepared records, host list
         size_t ncap = 0;
@@ -188,9 +192,10 @@ struct kwok_engine {
         // a batch runs in chunks (KWOK_INGEST_CHUNK records): chunk k+1's prep reads its
         // records over the link on `pst` while chunk k is applied and its results copied
         // back on the engine stream; odd chunks take the second accumulator set
-        uint32_t *creates1 = nullptr, *dels1 = nullptr;
+        uint32_t* creates1 = nullptr;
         IngSummary* sum1 = nullptr;
         hipStream_t pst = nullptr, dst = nullptr;  // prep (H2D + k_ing_prep) / results (D2H)
+        hipEvent_t tev[8] = {};  // KWOK_INGEST_PROF: device-side phase stamps of a two-chunk batch
         hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
         size_t chunk = 1048576;
     } ing;
@@ -308,6 +313,7 @@ struct kwok_engine {
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
+    bool results_stream = true;   // KWOK_INGEST_RS=0: a chunked batch's results copied on the engine stream
     bool results_kernel = false;  // KWOK_INGEST_RESULTS_KERNEL=1: pod batch results written into mapped host arrays by a kernel
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
@@ -778,7 +784,6 @@ IngestBatch ingest_batch(kwok_engine* e, uint32_t n, size_t arena_len) {
     I.out_status = G.out_status;
     I.out_released = G.out_released;
     I.creates = G.creates;
-    I.dels = G.dels;
     I.beg = G.beg;
     I.end = G.end;
     I.sum = G.sum;
@@ -990,12 +995,13 @@ void kwok_engine_destroy(kwok_engine* e) {
     {
         auto& g = e->ing;
         void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
-                      g.out_released, g.sort_tmp, g.creates, g.dels, g.beg, g.end, g.sum, g.creates1, g.dels1, g.sum1,
+                      g.out_released, g.sort_tmp, g.creates, g.abort, g.sums, g.beg, g.end, g.sum, g.creates1, g.sum1,
                       g.out_status8, g.d_nev, g.d_nnames, g.nrec, g.host_idx, g.d_nfix, g.nsum};
         for (void* p : ip)
             if (p) (void)hipFree(p);
         if (g.sum_h) (void)hipHostFree(g.sum_h);
         if (g.nsum_h) (void)hipHostFree(g.nsum_h);
+        if (g.sums_h) (void)hipHostFree(g.sums_h);
         if (g.res_h) (void)hipHostFree(g.res_h);
         hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1]};
         for (hipEvent_t x : evs)
@@ -1155,6 +1161,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_DEBUG_INGEST_FAIL_APPLY")) e->debug_fail_apply = (uint32_t)strtoul(v, nullptr, 10);
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         if (const char* v = getenv("KWOK_INGEST_RESULTS_KERNEL")) e->results_kernel = v[0] == '1';
+        if (const char* v = getenv("KWOK_INGEST_RS")) e->results_stream = v[0] != '0';
+        if (e->iprof)
+            for (hipEvent_t& x : e->ing.tev) (void)hipEventCreate(&x);
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
         e->no_stream = ns && ns[0] == '1';
         const char* qt = getenv("KWOK_QUIET");
@@ -1269,9 +1278,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     {  // GPU pod ingest: per-bucket / per-node-slot scratch and the batch summary
         auto& g = e->ing;
-        if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.dels, e->nb)) || (rc = dalloc(e, &g.beg, e->nb)) ||
+        if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.abort, 1)) || (rc = dalloc(e, &g.beg, e->nb)) ||
             (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.sum, 1)) || (rc = dalloc(e, &g.nsum, 1)) ||
-            (rc = dalloc(e, &g.creates1, e->nb)) || (rc = dalloc(e, &g.dels1, e->nb)) || (rc = dalloc(e, &g.sum1, 1)))
+            (rc = dalloc(e, &g.creates1, e->nb)) || (rc = dalloc(e, &g.sum1, 1)))
             return bail(rc);
         if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void**)&g.nsum_h, sizeof(NodeSummary), hipHostMallocDefault) != hipSuccess)
@@ -1283,6 +1292,30 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
             if (r == hipSuccess) r = hipEventCreateWithFlags(x, hipEventDisableTiming);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "ingest stream/events: %s", hipGetErrorString(r)));
         if (const char* v = getenv("KWOK_INGEST_CHUNK")) g.chunk = std::max<size_t>(1, strtoull(v, nullptr, 10));
+        // The runtime creates a copy engine's queue the first time it hands that engine a
+        // copy, holding the submitting host thread ~6 ms (C4: one or two batches of a
+        // process's first ~10 paid it inside the timed ingest, whatever the host memory;
+        // tools/gpu_r4v.sh, profiles/r4v_sdma_ab.txt).  Copies in both directions on every
+        // stream the engine uses, several in flight at once, spread over the engines here
+        // at create time instead (KWOK_COPY_WARM=0: off).
+        const char* cw = getenv("KWOK_COPY_WARM");
+        if (!(cw && cw[0] == '0')) {
+            const size_t wb = (size_t)8 << 20;
+            void *hbuf = nullptr, *dbuf = nullptr;
+            if (hipHostMalloc(&hbuf, wb * 4, hipHostMallocDefault) == hipSuccess && hipMalloc(&dbuf, wb * 4) == hipSuccess) {
+                hipStream_t ss[4] = {e->st, g.pst, g.dst, e->rst};
+                for (int round = 0; round < 4; round++)
+                    for (int q = 0; q < 4; q++) {
+                        char* h = (char*)hbuf + (size_t)q * wb;
+                        char* d = (char*)dbuf + (size_t)q * wb;
+                        (void)hipMemcpyAsync(round & 1 ? h : d, round & 1 ? d : h, wb,
+                                             round & 1 ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, ss[q]);
+                    }
+                for (hipStream_t x : ss) (void)hipStreamSynchronize(x);
+            }
+            if (dbuf) (void)hipFree(dbuf);
+            if (hbuf) (void)hipHostFree(hbuf);
+        }
     }
     e->max_init_len = 0;
     if ((rc = size_arena(e)) || (rc = grow_arena(e, e->slots[0]))) return bail(rc);
@@ -1566,10 +1599,28 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     return (int)sum.rejected;
 }
 
+// The stable sort by bucket and the apply pass of one chunk, queued on the engine
+// stream (spec: without the host's growth check; the pass then returns on the
+// device if the chunk needs growth)
+int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
+    auto& G = e->ing;
+    hipStream_t st = e->st;
+    I.spec = spec ? 1u : 0u;
+    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
+    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
+    if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
+        return e->fail(KWOK_EDEVICE, "ingest sort");
+    e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
+    launch_ingest_apply(e->S, I, st);
+    HIPCHK(e, hipGetLastError());
+    return KWOK_OK;
+}
+
 // One chunk of a pod batch after its prep (I: the chunk's records, indices
-// chunk-local): the growth check, the stable sort by bucket and the apply pass
-// (by-name creates resolve their node in it), on the engine stream.  Returns the
-// chunk's rejected count (>= 0) or an error.
+// chunk-local), with the host in the loop: the growth check, the stable sort by
+// bucket and the apply pass (by-name creates resolve their node in it).  Returns
+// the chunk's rejected count (>= 0) or an error.  (The batch path queues the
+// chunks without it and comes here only for a chunk that needs growth.)
 int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
     auto& G = e->ing;
     hipStream_t st = e->st;
@@ -1589,17 +1640,8 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
             if ((rc = grow_pods(e, want))) return rc;
         }
     }
-    // stable sort by bucket; the apply pass, one wave per bucket, in event order
-    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
-    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
-    if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
-        return e->fail(KWOK_EDEVICE, "ingest sort");
-    e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
-    launch_ingest_apply(e->S, I, st);
-    HIPCHK(e, hipGetLastError());
+    if ((rc = enqueue_apply(e, I, false))) return rc;
     if ((rc = read_summary(e, I.sum))) return rc;
-    if (e->debug_fail_apply == e->ing_chunk + 1)
-        return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", e->ing_chunk);
     if (G.sum_h->foreign) e->foreign_ips = true;
     return (int)G.sum_h->rejected;
 }
@@ -1640,6 +1682,16 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     // batches are copied: kernels reading host memory in place hold their CUs for
     // the link's latency, and the apply passes beside them stall (1M deletes + 1M
     // creates in 4 chunks: 4.9 ms read in place against 2.8 ms copied).
+    if (K > G.nsums) {  // one summary per chunk: the batch reads them back once, at its end
+        if (G.sums) (void)hipFree(G.sums);
+        if (G.sums_h) (void)hipHostFree(G.sums_h);
+        G.sums = nullptr, G.sums_h = nullptr, G.nsums = 0;
+        const size_t m = std::max<size_t>(K, 16);
+        if ((rc = dalloc(e, &G.sums, m))) return rc;
+        if (hipHostMalloc((void**)&G.sums_h, m * sizeof(IngSummary), hipHostMallocDefault) != hipSuccess)
+            return e->fail(KWOK_ENOMEM, "ingest summaries");
+        G.nsums = m;
+    }
     const bool zc_ok = e->ingest_zc && K == 1;
     const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
@@ -1651,81 +1703,137 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         if (zar) b.arena = (const uint8_t*)zar;
         b.rec += lo, b.keys += lo, b.keys_sorted += lo, b.idx_sorted += lo;
         b.out_handle += lo, b.out_status += lo, b.out_released += lo;
-        if (k & 1) b.creates = G.creates1, b.dels = G.dels1, b.sum = G.sum1;
+        if (k & 1) b.creates = G.creates1;
+        b.sum = G.sums + k;
+        b.abort = G.abort;
         return b;
     };
+    // prep of chunk k on stream s (the batch: the prep stream; a redo: the engine stream)
+    auto prep_on = [&](uint32_t k, hipStream_t s) -> int {
+        const IngestBatch b = chunk_batch(k);
+        HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), s));
+        HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, s));
+        if (!zev)
+            HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
+                                     hipMemcpyHostToDevice, s));
+        launch_ingest_prep(e->S, b, s);
+        HIPCHK(e, hipGetLastError());
+        return KWOK_OK;
+    };
+    const bool tstamp = e->iprof && G.tev[0] && K == 2;
     auto prep = [&](uint32_t k) -> int {
         const IngestBatch b = chunk_batch(k);
         if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
+        if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k], ps));  // 0 / 2: chunk k's copy starts
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
-        HIPCHK(e, hipMemsetAsync(b.dels, 0, (size_t)e->nb * 4, ps));
         HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, ps));
         if (!zev)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
         launch_ingest_prep(e->S, b, ps);
         HIPCHK(e, hipGetLastError());
+        if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k + 1], ps));  // 1 / 3: its prep done
         HIPCHK(e, hipEventRecord(G.prepped[k & 1], ps));
         return KWOK_OK;
     };
     e->ing_mutated = false;  // set by ingest_chunk once the batch changes any state
     // the prep stream starts after the work already queued on the engine stream
+    // results of chunk k (after its apply pass, on the results stream) -> the caller's arrays
+    auto results = [&](uint32_t k, hipStream_t rs) -> int {
+        const size_t lo = lo_of(k);
+        const IngestBatch I = chunk_batch(k);
+        // KWOK_INGEST_RESULTS_KERNEL=1: results into kwok_host_alloc arrays written by a
+        // kernel through their mapped addresses instead of the copy engine (slower:
+        // 1.9 vs 1.45 ms per C4 batch; kept for A/B of the host-side stalls, §11)
+        int32_t* mh = out_handles ? (int32_t*)host_mapped(out_handles + lo, (size_t)I.n * 4) : nullptr;
+        int32_t* ms = out_status ? (int32_t*)host_mapped(out_status + lo, (size_t)I.n * 4) : nullptr;
+        int8_t* m8 = out_status8 ? (int8_t*)host_mapped(out_status8 + lo, I.n) : nullptr;
+        uint32_t* mr = out_released ? (uint32_t*)host_mapped(out_released + lo, (size_t)I.n * 4) : nullptr;
+        const bool mapped = e->results_kernel && (!out_handles || mh) && (!out_status || ms) && (!out_status8 || m8) &&
+                            (!out_released || mr);
+        if (mapped) {
+            launch_ingest_results(I, mh, ms, m8, mr, rs);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipEventRecord(e->fence, rs));  // (system-scope release: the host reads them)
+            return KWOK_OK;
+        }
+        if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+        if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+        if (out_status8) {  // one byte per record over the link
+            launch_ingest_status8(I, G.out_status8 + lo, rs);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipMemcpyAsync(out_status8 + lo, G.out_status8 + lo, I.n, hipMemcpyDeviceToHost, rs));
+        }
+        if (out_released)
+            HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
+        return KWOK_OK;
+    };
+    // The whole batch is queued without a host round trip per chunk: each chunk's
+    // growth check (k_ing_need), sort and apply pass go behind its prep, and the
+    // apply pass itself returns when the chunk needs more pod slots than a bucket
+    // has (or an earlier chunk did).  One read-back of the chunks' summaries at the
+    // end: the rare chunk that needs growth and the chunks after it are then applied
+    // again with the host in the loop (ingest_chunk), in order.
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
         HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
         if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
+        HIPCHK(e, hipMemsetAsync(G.abort, 0, 4, st));
         for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
             if (int r = prep(k)) return r;
-        int rejected = 0;
+        hipStream_t rs = K > 1 && e->results_stream ? G.dst : st;
         for (uint32_t k = 0; k < K; k++) {
-            const size_t lo = lo_of(k);
             const IngestBatch I = chunk_batch(k);
-            const auto tw = clk::now();
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
-            const auto tc = clk::now();
-            if (e->iprof && ms_between(tw, tc) > 0.5)
-                fprintf(stderr, "[kwok ingest]   chunk %u: wait for its prep enqueued in %.3f ms\n", k, ms_between(tw, tc));
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
-            e->ing_chunk = k;
-            const int r = ingest_chunk(e, I);
-            if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u: %u records at +%.3f ms, applied +%.3f ms\n", k, I.n,
-                                  ms_between(t0, tc), ms_between(t0, clk::now()));
-            if (r < 0) return r;
-            rejected += r;
-            // the chunk's per-record results -> the caller's arrays, on the results
-            // stream (ingest_chunk's last summary read released them for the host)
+            launch_ingest_need(e->S, I, st);
+            HIPCHK(e, hipGetLastError());
+            if (int r = enqueue_apply(e, I, true)) return r;
+            if (tstamp) HIPCHK(e, hipEventRecord(G.tev[4 + k], st));  // 4 / 5: chunk k applied
+            // chunk k's results on the results stream; its accumulator set free for chunk k + 2
             HIPCHK(e, hipEventRecord(G.used[k & 1], st));
-            hipStream_t rs = K > 1 ? G.dst : st;
-            if (K > 1) HIPCHK(e, hipStreamWaitEvent(rs, G.used[k & 1], 0));
-            // KWOK_INGEST_RESULTS_KERNEL=1: results into kwok_host_alloc arrays written by a
-            // kernel through their mapped addresses instead of the copy engine (slower:
-            // 1.9 vs 1.45 ms per C4 batch; kept for A/B of the host-side stalls, §11)
-            int32_t* mh = out_handles ? (int32_t*)host_mapped(out_handles + lo, (size_t)I.n * 4) : nullptr;
-            int32_t* ms = out_status ? (int32_t*)host_mapped(out_status + lo, (size_t)I.n * 4) : nullptr;
-            int8_t* m8 = out_status8 ? (int8_t*)host_mapped(out_status8 + lo, I.n) : nullptr;
-            uint32_t* mr = out_released ? (uint32_t*)host_mapped(out_released + lo, (size_t)I.n * 4) : nullptr;
-            const bool mapped = e->results_kernel && (!out_handles || mh) && (!out_status || ms) &&
-                                (!out_status8 || m8) && (!out_released || mr);
-            if (mapped) {
-                launch_ingest_results(I, mh, ms, m8, mr, rs);
-                HIPCHK(e, hipGetLastError());
-                HIPCHK(e, hipEventRecord(e->fence, rs));  // (system-scope release: the host reads them)
-            } else {
-                if (out_handles) HIPCHK(e, hipMemcpyAsync(out_handles + lo, I.out_handle, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
-                if (out_status) HIPCHK(e, hipMemcpyAsync(out_status + lo, I.out_status, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
-                if (out_status8) {  // one byte per record over the link
-                    launch_ingest_status8(I, G.out_status8 + lo, rs);
-                    HIPCHK(e, hipGetLastError());
-                    HIPCHK(e, hipMemcpyAsync(out_status8 + lo, G.out_status8 + lo, I.n, hipMemcpyDeviceToHost, rs));
-                }
-                if (out_released)
-                    HIPCHK(e, hipMemcpyAsync(out_released + lo, I.out_released, (size_t)I.n * 4, hipMemcpyDeviceToHost, rs));
-            }
+            if (rs != st) HIPCHK(e, hipStreamWaitEvent(rs, G.used[k & 1], 0));
+            if (int r = results(k, rs)) return r;
             if (k + 2 < K)
                 if (int r2 = prep(k + 2)) return r2;
         }
+        if (int r = release_for_host(e)) return r;
+        HIPCHK(e, hipMemcpyAsync(G.sums_h, G.sums, (size_t)K * sizeof(IngSummary), hipMemcpyDeviceToHost, st));
+        if (tstamp) HIPCHK(e, hipEventRecord(G.tev[6], rs));  // 6: results copied
+        const auto tq = clk::now();
         HIPCHK(e, hipStreamSynchronize(st));
         if (K > 1) HIPCHK(e, hipStreamSynchronize(G.dst));
+        if (tstamp) {
+            float ms[6] = {};
+            for (int q = 1; q < 7; q++) (void)hipEventElapsedTime(&ms[q - 1], G.tev[0], G.tev[q]);
+            fprintf(stderr, "[kwok ingest]   queued in %.3f ms; device from chunk 0's copy: prep0 %.3f, copy1 start %.3f, "
+                            "prep1 %.3f, apply0 %.3f, apply1 %.3f, results %.3f ms\n", ms_between(t0, tq), ms[0], ms[1],
+                    ms[2], ms[3], ms[4], ms[5]);
+        }
+        if (e->iprof) fprintf(stderr, "[kwok ingest]   %u chunk%s queued and applied +%.3f ms\n", K, K == 1 ? "" : "s",
+                              ms_between(t0, clk::now()));
+        int rejected = 0;
+        uint32_t k = 0;
+        for (; k < K; k++) {
+            const IngSummary& q = G.sums_h[k];
+            if (q.need > e->Cp) break;  // its pass (and every later chunk's) returned: growth first
+            rejected += (int)q.rejected;
+            if (q.foreign) e->foreign_ips = true;
+            if (e->debug_fail_apply == k + 1)
+                return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
+        }
+        for (; k < K; k++) {  // chunks from the first that needs growth: the host in the loop
+            if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u again with the growth check\n", k);
+            if (int r = prep_on(k, st)) return r;
+            e->ing_chunk = k;
+            const int r = ingest_chunk(e, chunk_batch(k));
+            if (r < 0) return r;
+            if (e->debug_fail_apply == k + 1)
+                return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
+            rejected += r;
+            if (int r2 = results(k, st)) return r2;
+            HIPCHK(e, hipStreamSynchronize(st));
+        }
         return rejected;
     };
     rc = run();
@@ -1733,7 +1841,8 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     // chunk's own apply pass, placeholders or growth) is partly in the state: every
     // later call fails
     if (rc < 0 && e->ing_mutated) e->poisoned = true;
-    // nothing of this batch stays queued on the prep / results streams (a failed chunk included)
+    // nothing of this batch stays queued on the engine / prep / results streams (a failed chunk included)
+    if (hipStreamSynchronize(st) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest engine stream");
     if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
     if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
     if (e->iprof)

@@ -163,7 +163,6 @@ __device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i)
         else st = KWOK_ENOTMINE;
     }
     if (st == 1 && op == KWOK_OP_UPSERT && create) atomicAdd(&I.creates[r.bucket], 1u);
-    if (st == 1 && op == KWOK_OP_DELETE && !I.dels[r.bucket]) I.dels[r.bucket] = 1u;
     I.rec[i] = r;
     I.keys[i] = st == 1 ? r.bucket : S.nb;
     if (st != 1) {
@@ -239,8 +238,6 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
         }
         // growth check: creates per bucket (an upper bound: the batch's deletes are not netted out)
         if (st == 1 && x.op == KWOK_OP_UPSERT && x.handle < 0) atomicAdd(&I.creates[r.bucket], 1u);
-        // buckets where a pod leaves at ingest
-        if (st == 1 && x.op == KWOK_OP_DELETE && !I.dels[r.bucket]) I.dels[r.bucket] = 1u;
     }
     I.rec[i] = r;
     I.keys[i] = st == 1 ? r.bucket : S.nb;
@@ -444,6 +441,13 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     __shared__ uint32_t flist_all[APPLY_WAVES][64];  // a chunk's creates' slots (parallel path)
     const uint32_t w = threadIdx.x >> 6, l = lane();
     const uint32_t b = blockIdx.x * APPLY_WAVES + w;
+    if (I.spec) {
+        // queued ahead of the host's growth check: a chunk that could fill a bucket (or
+        // follows one that could) changes nothing; the host grows and applies it again
+        const bool over = I.sum->need > S.cp;
+        if (over && blockIdx.x == 0 && threadIdx.x == 0) *I.abort = 1u;
+        if (over || __hip_atomic_load(I.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    }
     if (b >= S.nb) return;
     const uint32_t pbeg = I.beg[b], pend = I.end[b];
     if (pbeg >= pend) return;

@@ -163,7 +163,9 @@ struct IngestBatch {
     uint32_t n;
     uint32_t n_specs;
     uint32_t packed;           // 1: kwok_pod_rec records (no arena)
-    uint32_t pad0;
+    uint32_t spec;             // the apply pass was queued without the host's growth check: it returns at once
+                               // when the chunk needs more pod slots than a bucket has (sum->need > cp) or an
+                               // earlier chunk of the batch did (*abort), setting *abort (the host redoes them)
     const uint8_t* arena;      // the batch's string arena (device copy)
     uint64_t arena_len;
     PodRec* rec;               // [n] prepared records
@@ -174,10 +176,10 @@ struct IngestBatch {
     int32_t* out_status;       // [n]
     uint32_t* out_released;    // [n]
     uint32_t* creates;         // [nb] creates per bucket (growth check)
-    uint32_t* dels;            // [nb] 1: the batch deletes a pod of the bucket (zeroed per batch)
     uint32_t* beg;             // [nb] first sorted position of each bucket
     uint32_t* end;             // [nb]
     IngSummary* sum;
+    uint32_t* abort;           // [1] per batch (spec)
 };
 size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort temporary storage
 // prep (+ growth counts) for every record
