@@ -292,7 +292,12 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
 /* Ingest a batch of watch events in order.  out_handles[i] receives the node/pod
  * handle (canonical slot id), out_status[i] a per-record code (KWOK_OK,
  * KWOK_EDOMAIN, KWOK_EFULL, KWOK_ENOTFOUND, KWOK_ENOTMINE).  Returns the number of
- * rejected records (>= 0) or a negative error for the whole batch. */
+ * rejected records (>= 0) or a negative error for the whole batch.  Both event
+ * switches run on the GPU, in event order per bucket, over device-resident state
+ * (the node directory of names and the pod slots); records and arena in
+ * kwok_host_alloc memory are read in place, other buffers are copied first.
+ * Nodes: only a non-empty status (its JSON blobs and nodeInfo strings) or a
+ * custom node template takes host string work. */
 int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena,
                       size_t arena_len, int32_t* out_handles, int32_t* out_status);
 /* out_released (optional) receives, per DELETE record, the IPv4 address released
@@ -384,6 +389,8 @@ int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst);
  * (removeFinalizers, pod_controller.go:45). */
 const char* kwok_finalizer_patch(size_t* len);
 
+/* nodesSets.Has: the node of that name is in the managed set (a device lookup in
+ * the node directory; waits for the engine stream). */
 int kwok_node_has(kwok_engine* e, const char* name, size_t len);
 uint64_t kwok_node_size(kwok_engine* e);
 
