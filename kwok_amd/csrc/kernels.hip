@@ -847,32 +847,29 @@ __device__ __forceinline__ GroupMasks group_masks(const DevState& S, const PodGr
 __device__ __forceinline__ bool group_counts_fast(const DevState& S, const PodGrp& g, const uint8_t (&ntf)[POD_PER_THREAD],
                                                   uint32_t& n_eval, uint32_t& n_total, uint32_t& n_pend,
                                                   uint32_t& n_run) {
+    // the planes are used at bit 0 (even pod) and bit 16 (odd pod) only: the shifted
+    // copies of the word are combined unmasked and masked once at the end
     constexpr uint32_t M = 0x00010001u;
     uint32_t rare = 0, pe = 0, pt = 0, pp = 0, pr = 0;
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const uint32_t s = g.stw[w];
         const uint32_t nf = (uint32_t)ntf[2 * w] | (uint32_t)ntf[2 * w + 1] << 16;
-        const uint32_t ipz = ~(s >> 11) & M;
-        const uint32_t inc_pool = (s >> 12) & M;
-        const uint32_t used = s & M, disr = (s >> 1) & M, del = used & (s >> 2);
-        const uint32_t nonempty = (s >> 4) & M, conf = (s >> 5) & M, event = (s >> 6) & M, hhost = (s >> 7) & M;
-        const uint32_t ph = (s >> 8) & (7u * M);
-        const uint32_t xr = ph ^ (PHASE_RUNNING * M), xp = ph ^ (PHASE_PENDING * M);
-        const uint32_t running = ~(xr | (xr >> 1) | (xr >> 2)) & M, pending = ~(xp | (xp >> 1) | (xp >> 2)) & M;
-        const uint32_t relock = nf & M;
-        const uint32_t live = used & ~del & M;
-        const uint32_t eval = live & (event | (relock & ~disr));
-        const uint32_t stale = (running & conf & hhost) ^ M;
-        const uint32_t need = S.cni ? eval & stale & ~ipz : eval & (stale | ipz);
-        const uint32_t alloc = S.cni ? 0u : eval & nonempty & ipz;
-        const uint32_t usec = S.cni ? 0u : eval & inc_pool & (S.use_events_only ? event : M);
-        // rare: del, need, alloc, usec, eval & event (dirty); a release needs del
-        rare |= del | need | alloc | usec | (eval & event);
-        // two pods per plane: bit 0 and bit 16 -> 1 + 1 after the fold
-        pe += eval, pt += live, pp += live & ~need & pending, pr += live & (need | running);
+        const uint32_t s1 = s >> 1, s2 = s >> 2, s4 = s >> 4, s5 = s >> 5, s6 = s >> 6, s7 = s >> 7;
+        const uint32_t s8 = s >> 8, s9 = s >> 9, s10 = s >> 10, s11 = s >> 11, s12 = s >> 12;
+        const uint32_t del = s & s2;                     // USED & DELETE_PENDING
+        const uint32_t live = s & ~s2;                   // USED, not DELETE_PENDING
+        const uint32_t eval = live & (s6 | (nf & ~s1));  // EVENT, or RELOCK & !DISREGARD
+        const uint32_t running = s9 & ~(s8 | s10), pending = s8 & ~(s9 | s10);
+        const uint32_t ok = running & s5 & s7;           // Running, CONFORMS, HAS_HOST_IP
+        // computePatchData: a no-op unless the podIP is empty (IP_SET = s11); EnableCNI: not before it has one
+        const uint32_t need = S.cni ? eval & ~ok & s11 : eval & ~(ok & s11);
+        const uint32_t alloc = S.cni ? 0u : eval & s4 & ~s11;                             // STATUS_NONEMPTY, no podIP
+        const uint32_t usec = S.cni ? 0u : eval & s12 & (S.use_events_only ? s6 : ~0u);  // IP_POOL
+        rare |= del | need | alloc | usec | (eval & s6);
+        pe += eval & M, pt += live & M, pp += live & pending & ~need & M, pr += live & (need | running) & M;
     }
-    n_eval += (pe & 0xFFFFu) + (pe >> 16);  // each plane sum stays below 2^16: at most 4 per half
+    n_eval += (pe & 0xFFFFu) + (pe >> 16);  // at most 4 per half
     n_total += (pt & 0xFFFFu) + (pt >> 16);
     n_pend += (pp & 0xFFFFu) + (pp >> 16);
     n_run += (pr & 0xFFFFu) + (pr >> 16);
@@ -1640,22 +1637,23 @@ __device__ __forceinline__ void publish_header(const DevState& S) {
 // KeepNodeHeartbeat handles (node_controller.go:175-204): the block's managed
 // nodes in node order from the host-maintained base, after the block arrived
 // (nothing waits on them)
+// the block's managed nodes' handles, in node order, from position hb_run: each
+// thread takes a contiguous run of the block's nodes (node order = thread order),
+// so one block scan of the per-thread counts places them all
 __device__ __forceinline__ void write_hb_handles(const DevState& S, const uint32_t* nflags32, uint32_t nbase, uint32_t nn,
                                                  uint32_t hb_run) {
-    for (uint32_t i0 = 0; i0 < nn; i0 += NODE_CHUNK) {
-        const uint32_t i = i0 + threadIdx.x * NODE_PER_THREAD;
-        const uint32_t hbm = i < nn ? (nflags32[i / 4] >> 1) & 0x01010101u : 0u;  // NT_MANAGED of 4 nodes
-        uint32_t hb[1] = {(uint32_t)__popc(hbm)}, tot[1];
-        block_excl_scan<1>(hb, tot);
-        uint32_t pos = hb_run + hb[0];
-#pragma unroll
-        for (int k = 0; k < NODE_PER_THREAD; k++)
-            if ((hbm >> (8 * k)) & 1) {
-                if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i + k);
-                pos++;
-            }
-        hb_run += tot[0];
-    }
+    const uint8_t* nf = reinterpret_cast<const uint8_t*>(nflags32);
+    const uint32_t q = (nn + BLOCK - 1) / BLOCK;
+    const uint32_t a = min(nn, threadIdx.x * q), e = min(nn, a + q);
+    uint32_t c[1] = {0}, tot[1];
+    for (uint32_t i = a; i < e; i++) c[0] += (nf[i] >> 1) & 1u;  // NT_MANAGED
+    block_excl_scan<1>(c, tot);
+    uint32_t pos = hb_run + c[0];
+    for (uint32_t i = a; i < e; i++)
+        if ((nf[i] >> 1) & 1u) {
+            if (pos < S.n_node_slots) S.hb_nodes[pos] = S.node_handle_base + (int32_t)(nbase + i);
+            pos++;
+        }
 }
 
 // pointers into k_tick's LDS for the out-of-line BACK phases
@@ -2049,62 +2047,71 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         auto row_slot = [&](uint32_t a) {
             return jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u;
         };
-        if (SPEC_GROUPS * tpb < maxg && S.hb_once) {
-            // heartbeat-once ticks (nothing to hide the chain under): ROW_BATCH rows
-            // per iteration, all their group loads in one round trip.  A wave whose
-            // rows hold nothing but counts (no patch, Use, release or event: every
-            // row of a quiet steady tick) only counts them; otherwise each row in
-            // turn is loaded again (from the caches) with its podIPs, spec and
-            // `used` words and takes the rare paths
-#if KWOK_ROW_PREFETCH
-            // (double-buffered: the next batch's loads are issued before this batch is counted)
-            PodGrp N[ROW_BATCH];
+        const uint32_t once_iters = SPEC_GROUPS * tpb < maxg ? (maxg - SPEC_GROUPS * tpb + ROW_BATCH * tpb - 1) / (ROW_BATCH * tpb) : 0u;
+        if (once_iters && S.hb_once && once_iters <= 64) {
+            // heartbeat-once ticks (nothing to hide the chain under): ROW_BATCH rows per
+            // iteration, their state and node words only, loaded one iteration ahead; a
+            // batch with nothing but counts (every row of a quiet steady tick) is counted
+            // from the state planes.  A batch with a delete, patch, Get, Put, Use or event
+            // is noted and taken by the full path after the loop (the loop body stays
+            // small: its registers hold the loads in flight, not the rare path's)
+            auto lean = [&](uint32_t a, uint4& st, uint4& nd) {
+                const uint32_t slot = row_slot(a);
+                st = nd = make_uint4(0, 0, 0, 0);
+                if (slot != ~0u) {
+                    st = *reinterpret_cast<const uint4*>(S.pod_state + slot);
+                    nd = *reinterpret_cast<const uint4*>(S.pod_node + slot);
+                }
+            };
+            uint64_t rare_iters = 0;  // wave-uniform
+            uint4 Ns[ROW_BATCH], Nn[ROW_BATCH];
 #pragma unroll
-            for (int r = 0; r < ROW_BATCH; r++)
-                load_group_at(S, row_slot(l + SPEC_GROUPS * tpb + r * tpb), j, N[r], false);
-#endif
-            for (uint32_t a0 = SPEC_GROUPS * tpb; a0 < maxg; a0 += ROW_BATCH * tpb) {
-                PodGrp H[ROW_BATCH];
-#if KWOK_ROW_PREFETCH
+            for (int r = 0; r < ROW_BATCH; r++) lean(l + SPEC_GROUPS * tpb + r * tpb, Ns[r], Nn[r]);
+            uint32_t n_eval = 0, n_total = 0, n_pend = 0, n_run = 0;
+            for (uint32_t it = 0; it < once_iters; it++) {
+                uint4 Hs[ROW_BATCH], Hn[ROW_BATCH];
 #pragma unroll
-                for (int r = 0; r < ROW_BATCH; r++) H[r] = N[r];
-                const uint32_t an = a0 + ROW_BATCH * tpb;
-#pragma unroll
-                for (int r = 0; r < ROW_BATCH; r++)
-                    load_group_at(S, an < maxg ? row_slot(l + an + r * tpb) : ~0u, j, N[r], false);
-#else
-#pragma unroll
-                for (int r = 0; r < ROW_BATCH; r++) load_group_at(S, row_slot(l + a0 + r * tpb), j, H[r], false);
-#endif
-                // counts of a clean batch (no delete, patch, Get, Put, Use or event:
-                // count_group reduces to these four fields)
-                bool rare = false;
-                uint32_t n_eval = 0, n_total = 0, n_pend = 0, n_run = 0;
+                for (int r = 0; r < ROW_BATCH; r++) Hs[r] = Ns[r], Hn[r] = Nn[r];
+                const uint32_t an = SPEC_GROUPS * tpb + (it + 1) * ROW_BATCH * tpb;
 #pragma unroll
                 for (int r = 0; r < ROW_BATCH; r++) {
+                    if (an < maxg) lean(l + an + r * tpb, Ns[r], Nn[r]);
+                    else Ns[r] = Nn[r] = make_uint4(0, 0, 0, 0);
+                }
+                bool rare = false;
+                uint32_t ce = 0, ct = 0, cpn = 0, cr = 0;
+#pragma unroll
+                for (int r = 0; r < ROW_BATCH; r++) {
+                    PodGrp g;
+                    g.slot = 0, g.j = j;
+                    g.stw[0] = Hs[r].x, g.stw[1] = Hs[r].y, g.stw[2] = Hs[r].z, g.stw[3] = Hs[r].w;
+                    g.ndw[0] = Hn[r].x, g.ndw[1] = Hn[r].y, g.ndw[2] = Hn[r].z, g.ndw[3] = Hn[r].w;
                     uint8_t nf[POD_PER_THREAD];
 #pragma unroll
-                    for (int k = 0; k < POD_PER_THREAD; k++) nf[k] = group_node_flags(S, nflags, H[r], k);
-                    rare |= group_counts_fast(S, H[r], nf, n_eval, n_total, n_pend, n_run);
+                    for (int k = 0; k < POD_PER_THREAD; k++) nf[k] = group_node_flags(S, nflags, g, k);
+                    rare |= group_counts_fast(S, g, nf, ce, ct, cpn, cr);
                 }
-                if (__builtin_expect(__ballot(rare) == 0, 1)) {
-                    f[AG_EVAL] += n_eval;
-                    f[AG_TOTAL] += n_total;
-                    f[AG_PENDING] += n_pend;
-                    f[AG_RUNNING] += n_run;
-                } else {
-                    for (int r = 0; r < ROW_BATCH; r++) {
-                        const uint32_t a = l + a0 + r * tpb;
-                        PodGrp g;
-                        load_group_at(S, row_slot(a), j, g);
-                        const GroupMasks m = masks_of(S, nflags, g);
-                        const uint4 sw = load_spec_words(S, g, m.need);
-                        const UsedWords u = used_words(S, g, m.usec);
-                        const uint32_t gbytes = count_group(S, g, m, f, sw, smax);
-                        if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
-                        if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
-                        apply_uses(S, g, m.usec & ~used_bits(S, g, m.usec, u));
-                    }
+                if (__builtin_expect(__ballot(rare) == 0, 1)) n_eval += ce, n_total += ct, n_pend += cpn, n_run += cr;
+                else rare_iters |= 1ull << it;
+            }
+            f[AG_EVAL] += n_eval;
+            f[AG_TOTAL] += n_total;
+            f[AG_PENDING] += n_pend;
+            f[AG_RUNNING] += n_run;
+            while (rare_iters) {
+                const uint32_t it = (uint32_t)__builtin_ctzll(rare_iters);
+                rare_iters &= rare_iters - 1;
+                for (int r = 0; r < ROW_BATCH; r++) {
+                    const uint32_t a = l + SPEC_GROUPS * tpb + it * ROW_BATCH * tpb + r * tpb;
+                    PodGrp g;
+                    load_group_at(S, a < maxg ? row_slot(a) : ~0u, j, g);
+                    const GroupMasks m = masks_of(S, nflags, g);
+                    const uint4 sw = load_spec_words(S, g, m.need);
+                    const UsedWords u = used_words(S, g, m.usec);
+                    const uint32_t gbytes = count_group(S, g, m, f, sw, smax);
+                    if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
+                    if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                    apply_uses(S, g, m.usec & ~used_bits(S, g, m.usec, u));
                 }
             }
         } else if (SPEC_GROUPS * tpb < maxg) {
