@@ -56,10 +56,7 @@ constexpr int SPEC_GROUPS = 2;            // pod groups per thread loaded before
 #ifndef KWOK_ROW_BATCH
 #define KWOK_ROW_BATCH 2
 #endif
-constexpr int ROW_BATCH = KWOK_ROW_BATCH; // further pod rows per thread loaded together (one round trip)
-#ifndef KWOK_ROW_PREFETCH
-#define KWOK_ROW_PREFETCH 1                // ... and the next batch's loads in flight while one is counted
-#endif
+constexpr int ROW_BATCH = KWOK_ROW_BATCH; // heartbeat-once ticks: pod rows per thread loaded together, one batch ahead
 #ifndef KWOK_NODE_PRE
 #define KWOK_NODE_PRE 4
 #endif
