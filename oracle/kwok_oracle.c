@@ -650,7 +650,8 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
             if (h < 0) {
                 st = KWOK_EINVAL; /* a Deleted event names an object the caller ingested */
             } else if ((uint32_t)h >= o->B * o->cp || !o->pods[h].used) {
-                st = KWOK_ENOTFOUND;
+                st = KWOK_ENOTFOUND; /* a rejected record carries no handle (as an update's) */
+                h = -1;
             } else {
                 opod_t* p = &o->pods[h];
                 int32_t nh = p->node;
