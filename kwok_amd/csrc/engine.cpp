@@ -1538,8 +1538,6 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     // once on the device when the prep listed records for the host (then the host
     // completes them and runs the sort and the pass again); one round trip otherwise
     auto sort_apply_results = [&]() -> int {
-        HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
-        HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
         if (launch_node_sort(e->S, N, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
             return e->fail(KWOK_EDEVICE, "node sort");
         launch_node_apply(e->S, N, st);
@@ -1606,8 +1604,6 @@ int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
     auto& G = e->ing;
     hipStream_t st = e->st;
     I.spec = spec ? 1u : 0u;
-    HIPCHK(e, hipMemsetAsync(G.beg, 0, (size_t)e->nb * 4, st));
-    HIPCHK(e, hipMemsetAsync(G.end, 0, (size_t)e->nb * 4, st));
     if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
         return e->fail(KWOK_EDEVICE, "ingest sort");
     e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on

@@ -300,16 +300,26 @@ __device__ bool name_eq(const DevState& S, size_t g, const uint8_t* nm, uint32_t
     if (o < len) bad = ld_coh(reinterpret_cast<const uint32_t*>(S.node_name + g * NAME_STRIDE + o)) != name_word(nm, len, o);
     return !__ballot(bad);
 }
-// the index of bucket b's entry named nm, or -1
+// the index of bucket b's entry named nm, or -1.  The bucket's keys are loaded
+// DIR_UNROLL x 64 at a time (one round trip for buckets of up to 512 entries)
+constexpr uint32_t DIR_UNROLL = 8;
 __device__ int32_t dir_find(const DevState& S, uint32_t b, uint64_t key, const uint8_t* nm, uint32_t len) {
     const size_t nbase = (size_t)b * S.cn;
-    for (uint32_t j0 = 0; j0 < S.cn; j0 += 64) {
-        const uint32_t j = j0 + lane();
-        uint64_t m = __ballot(j < S.cn && ld_coh(S.node_key + nbase + j) == key);
-        while (m) {
-            const uint32_t c = j0 + (uint32_t)__builtin_ctzll(m);
-            if (name_eq(S, nbase + c, nm, len)) return (int32_t)c;
-            m &= m - 1;
+    for (uint32_t j0 = 0; j0 < S.cn; j0 += 64 * DIR_UNROLL) {
+        uint64_t k[DIR_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < DIR_UNROLL; u++) {
+            const uint32_t j = j0 + u * 64 + lane();
+            k[u] = j < S.cn ? ld_coh(S.node_key + nbase + j) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < DIR_UNROLL; u++) {
+            uint64_t m = __ballot(k[u] == key);
+            while (m) {
+                const uint32_t c = j0 + u * 64 + (uint32_t)__builtin_ctzll(m);
+                if (name_eq(S, nbase + c, nm, len)) return (int32_t)c;
+                m &= m - 1;
+            }
         }
     }
     return -1;
@@ -341,25 +351,33 @@ __device__ __forceinline__ void dir_clear(const DevState& S, size_t g) {
 // does a live pod of bucket b (pods below its fill mark) reference node index nd?
 // (node batches: no pod changes during one, plain loads)
 __device__ bool pods_reference(const DevState& S, uint32_t b, uint32_t nd) {
+    constexpr uint32_t U = 4;  // 512-slot steps whose loads are in flight together
     const uint32_t fill = S.pod_fill[b];
     const size_t sb = (size_t)b * S.cp;
-    bool hit = false;
-    for (uint32_t s0 = 0; s0 < fill && !hit; s0 += 512) {
-        const uint32_t s = s0 + lane() * 8;
+    for (uint32_t s0 = 0; s0 < fill; s0 += 512 * U) {
+        uint4 st[U], ndw[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t s = s0 + u * 512 + lane() * 8;
+            st[u] = ndw[u] = make_uint4(0, 0, 0, 0);
+            if (s < fill) {
+                st[u] = *reinterpret_cast<const uint4*>(S.pod_state + sb + s);
+                ndw[u] = *reinterpret_cast<const uint4*>(S.pod_node + sb + s);
+            }
+        }
         bool h = false;
-        if (s < fill) {
-            const uint4 st = *reinterpret_cast<const uint4*>(S.pod_state + sb + s);
-            const uint4 ndw = *reinterpret_cast<const uint4*>(S.pod_node + sb + s);
-            const uint32_t a[4] = {st.x, st.y, st.z, st.w}, q[4] = {ndw.x, ndw.y, ndw.z, ndw.w};
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t a[4] = {st[u].x, st[u].y, st[u].z, st[u].w}, q[4] = {ndw[u].x, ndw[u].y, ndw[u].z, ndw[u].w};
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 h |= (a[k] & PS_USED) && (q[k] & 0xFFFFu) == nd;
                 h |= ((a[k] >> 16) & PS_USED) && (q[k] >> 16) == nd;
             }
         }
-        hit = __ballot(h) != 0;
+        if (__ballot(h)) return true;
     }
-    return hit;
+    return false;
 }
 constexpr uint32_t MAX_BM_WORDS = 65536 / 64;  // Cp <= 65528 (pod_handle_stride)
 
@@ -450,7 +468,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     }
     if (b >= S.nb) return;
     const uint32_t pbeg = I.beg[b], pend = I.end[b];
-    if (pbeg >= pend) return;
+    if (pbeg >= pend || pend > I.n || I.keys_sorted[pbeg] != b) return;  // (stale ranges: k_nd_apply)
     Bucket B;
     B.b = b;
     B.cp = S.cp;
@@ -820,13 +838,36 @@ __global__ void k_nd_prep(DevState S, NodeBatch N) {
         if (!inside) {
             st = KWOK_EDOMAIN;
         } else {
+            // the name by aligned dwords (a batch read in place crosses the link: one
+            // round trip for a name of up to 61 bytes instead of one per byte), copied
+            // and hashed; longer names byte by byte
             const uint8_t* nm = N.arena + x.name.off;
             uint8_t* dst = N.names + (size_t)i * NAME_STRIDE;
             uint32_t h = 0x811C9DC5u;
-            for (uint32_t j = 0; j < x.name.len; j++) {
-                const uint8_t c = nm[j];
-                dst[j] = c;
-                h = (h ^ c) * 0x01000193u;
+            const uintptr_t p0 = reinterpret_cast<uintptr_t>(nm);
+            const uint32_t lead = (uint32_t)(p0 & 3u), nw = (lead + x.name.len + 3u) / 4u;
+            constexpr uint32_t NW = 16;
+            if (nw <= NW) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(p0 & ~(uintptr_t)3);
+                uint32_t wv[NW + 1];
+#pragma unroll
+                for (uint32_t q = 0; q < NW; q++) wv[q] = q < nw ? src[q] : 0u;
+                wv[NW] = 0u;
+#pragma unroll
+                for (uint32_t q = 0; q < NW; q++) {
+                    if (4 * q >= x.name.len) break;
+                    const uint32_t w = lead ? __builtin_amdgcn_alignbit(wv[q + 1], wv[q], 8 * lead) : wv[q];
+                    *reinterpret_cast<uint32_t*>(dst + 4 * q) = w;
+#pragma unroll
+                    for (uint32_t c = 0; c < 4; c++)
+                        if (4 * q + c < x.name.len) h = (h ^ ((w >> (8 * c)) & 0xFFu)) * 0x01000193u;
+                }
+            } else {
+                for (uint32_t j = 0; j < x.name.len; j++) {
+                    const uint8_t c = nm[j];
+                    dst[j] = c;
+                    h = (h ^ c) * 0x01000193u;
+                }
             }
             r.hash = h;
             r.len = (uint8_t)x.name.len;
@@ -887,8 +928,11 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_nd_apply(DevState S, NodeB
     const uint32_t l = lane();
     const uint32_t b = blockIdx.x * APPLY_WAVES + (threadIdx.x >> 6);
     if (b >= S.nb) return;
+    // the bucket's records: k_nd_ranges wrote beg / end of the buckets present; a
+    // bucket absent from this batch may hold an older batch's range, which no
+    // sorted key of this batch matches (no memset of the ranges per batch)
     const uint32_t pbeg = N.beg[b], pend = N.end[b];
-    if (pbeg >= pend) return;
+    if (pbeg >= pend || pend > N.n || N.keys_sorted[pbeg] != b) return;
     if (!N.force && N.sum->n_host) return;  // the host completes records first, then launches this again
     const size_t nbase = (size_t)b * S.cn;
     int32_t dman = 0, dzb = 0;
