@@ -18,6 +18,10 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 > $R/gpurun_out/bench_${TAG}_prof.json 2>&1 || exit 4
 T=$(find $R/gpurun_out/prof_$TAG -name 'run_kernel_trace.csv' | head -n 1)
 python3 $R/tools/trace_summary.py "$T" --last 45 --out $R/gpurun_out/ktrace_$TAG.txt || exit 6
+# the heartbeat-once leg alone after a short steady leg: its ticks are the last k_tick dispatches
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_once_$TAG -o run -- python3 $R/bench.py --steps 60 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --emulate-ranks 0 > $R/gpurun_out/bench_${TAG}_once_prof.json 2>&1 || exit 8
+T=$(find $R/gpurun_out/prof_once_$TAG -name 'run_kernel_trace.csv' | head -n 1)
+python3 $R/tools/trace_summary.py "$T" --last 50 --out $R/gpurun_out/ktrace_once_$TAG.txt || exit 9
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || exit 7
 done
