@@ -20,7 +20,8 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     by = {}
     for r in rows:
-        n = r["Kernel_Name"].split("(")[0].replace("kwok::", "")
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("kwok::", "")
+        n = n.replace("rocprim::ROCPRIM_400200_NS::detail::", "rocprim::")[:48]
         by.setdefault(n, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     lines = ["source: %s" % a.trace,
              "durations in us; 'steady' = the last %d dispatches of each kernel (timed bench steps)" % a.last,
