@@ -418,9 +418,10 @@ int kwok_device_outputs(kwok_engine* e, kwok_device_view* view);
  * header publication, EXCHANGE = between the two launches of a multi-rank tick
  * (allgather + pool apply), POOL = ipPool phase (ticks with Gets / Puts),
  * EMIT = the rest of the launch beyond the longer of chain and stream, plus the patch-byte
- * kernel; EMIT_KERNEL = that kernel alone (ticks with patches). */
+ * kernel; EMIT_KERNEL = the emission kernels alone (ticks with patches: k_emit, plus
+ * k_pod_jobs on split ticks, which writes the pod patch bytes when fused). */
 enum { KWOK_T_CLASSIFY = 0, KWOK_T_STREAM, KWOK_T_HEADER, KWOK_T_EXCHANGE, KWOK_T_POOL, KWOK_T_EMIT,
-       KWOK_T_KERNEL, KWOK_T_EMIT_KERNEL /* the patch-byte kernel alone (k_emit) */, KWOK_T_COUNT };
+       KWOK_T_KERNEL, KWOK_T_EMIT_KERNEL /* the emission kernels (k_pod_jobs + k_emit) */, KWOK_T_COUNT };
 int kwok_profile_enable(kwok_engine* e, int on);
 int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* ticks);
 /* Host-side wall time of kwok_tick (always measured): enqueue,

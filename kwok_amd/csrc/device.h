@@ -125,6 +125,7 @@ struct TickHdr {
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
 constexpr uint32_t TICK_ERR_LAYOUT = 2;   // device heartbeat count != the host's managed-node count
 constexpr uint32_t TICK_ERR_SEQ = 4;      // multi rank: the gathered messages are of different ticks
+constexpr uint32_t TICK_ERR_EMIT = 8;     // a fused pod emission met a spec without unit tables (host flag stale)
 enum : int {
     CLK_ENTRY = 0,   // block 0 starts the tick (FRONT launch)
     CLK_P1_MAX,      // the last chain block arrives (classification complete)
@@ -240,7 +241,8 @@ struct IngSummary {
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)
-    uint32_t pad[2];
+    uint32_t creates;       // creates of the chunk (before the apply's checks: an upper bound; fused emission)
+    uint32_t pad;
 };
 
 // ---- node directory (device-authoritative, ingest.hip) -------------------------

@@ -251,6 +251,7 @@ struct kwok_engine {
         uint32_t* emit_n = nullptr;
         bool emit_queued = false;   // k_emit was enqueued behind the tick's launches
         bool split = false;         // TICK_SPLIT: k_pod_jobs builds the pod jobs after the tick's launches
+        bool fuse = false;          // ... and writes their patch bytes itself (DevState::fuse_pods)
         bool quiet = false;         // only pods with an event are Use-checked (kwok_engine::quiet)
         bool alloc = false;
         // the tick in the slot
@@ -293,6 +294,9 @@ struct kwok_engine {
     bool chain_prio = false;    // KWOK_TICK_PRIO=1: s_setprio 3 on the chain blocks
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
+    int fuse_emit = -1;         // KWOK_FUSE_EMIT: 1 always / 0 never fuse the pod bytes into k_pod_jobs; -1 dense ticks
+    uint64_t creates_since_tick = 0;  // pod creates ingested since the last tick was enqueued (fused emission)
+    uint32_t n_untabled = 0;    // registered specs without unit tables (no fused emission while any)
     // Quiet ticks.  A tick's Use(podIP) of an evaluated pod (pod_controller.go:
     // 378-382) is a no-op when the address is already in `used`.  Only a Put clears
     // a bit, and Puts come from ingest (Deleted events), kwok_pool_put, and the
@@ -1170,6 +1174,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->quiet_ok = !(qt && qt[0] == '0');
         const char* sj = getenv("KWOK_SPLIT");
         e->split_jobs = !(sj && sj[0] == '0');
+        const char* fe = getenv("KWOK_FUSE_EMIT");
+        e->fuse_emit = fe && fe[0] ? (fe[0] == '0' ? 0 : 1) : -1;
         const char* zc = getenv("KWOK_INGEST_ZC");
         e->ingest_zc = !(zc && zc[0] == '0');
     }
@@ -1394,6 +1400,7 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
         e->S.unit_tab = reinterpret_cast<const uint4*>(e->d_unit_tab.p);
         e->S.unit_desc = e->d_unit_desc.p;
     }
+    if (d.tab_off == NO_TAB) e->n_untabled++;
     const std::string kinds = p.ka + p.kb + p.kc;
     for (size_t i = 0; i < kinds.size(); i++)  // slot starts (kinds 0..19 in a row)
         if (kinds[i] == 0) d.n_ts++;
@@ -1636,6 +1643,7 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
             if ((rc = grow_pods(e, want))) return rc;
         }
     }
+    e->creates_since_tick += sum.creates;
     if ((rc = enqueue_apply(e, I, false))) return rc;
     if ((rc = read_summary(e, I.sum))) return rc;
     if (G.sum_h->foreign) e->foreign_ips = true;
@@ -1814,6 +1822,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             const IngSummary& q = G.sums_h[k];
             if (q.need > e->Cp) break;  // its pass (and every later chunk's) returned: growth first
             rejected += (int)q.rejected;
+            e->creates_since_tick += q.creates;
             if (q.foreign) e->foreign_ips = true;
             if (e->debug_fail_apply == k + 1)
                 return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
@@ -2017,6 +2026,17 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // k_pod_jobs, one wave per two dirty 64-group runs, instead of the chain blocks'
     // serial chunk walk (KWOK_SPLIT=0: the chain blocks, for A/B)
     T.split = T.emit_queued && e->split_jobs;
+    // ... writing the pod patch bytes there too when every spec has unit tables
+    // (no 16-byte job record per patch written by k_pod_jobs and read back by k_emit)
+    // and the tick is dense: creates since the last tick >= 1/4 of the pod slots,
+    // so most dirty runs hold hundreds of jobs (1M x 10M initial tick: emission
+    // 1.79 -> 1.72 ms).  A sparse tick's runs hold a few jobs each; their serial
+    // emission per wave loses to k_emit's packed 64-job chunks (C4 churn tick
+    // 0.51 -> 0.57 ms fused; tools/gpu_r6b.sh)
+    const bool dense = e->creates_since_tick * 4 >= (uint64_t)S.nb * e->Cp;
+    if (!requeue) e->creates_since_tick = 0;
+    T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
+    S.fuse_pods = T.fuse ? 1u : 0u;
     // ... and leave the whole stream to the streamers: a dirty chain block's share
     // of it would hold up the pool phase, which waits for every dirty block
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
@@ -2128,6 +2148,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     }
     int rc = bind_slot(e, k);
     if (rc) return rc;
+    S.fuse_pods = T.fuse ? 1u : 0u;
     HIPCHK(e, hipMemsetAsync(&S.bar->skip, 0, sizeof(uint32_t), st));
     const XMsg& me = e->h_xall[e->rank];
     if (me.n_use + me.n_rel) {  // the chain blocks' list segments, gathered in block order
@@ -2303,6 +2324,8 @@ int retire(kwok_engine* e) {
                                e->S.n_chain)
                  : (err & TICK_ERR_SEQ)
                      ? e->fail(KWOK_ECOMM, "ranks out of step: the gathered exchange messages are of different ticks")
+                 : (err & TICK_ERR_EMIT)
+                     ? e->fail(KWOK_EDEVICE, "k_pod_jobs: a pod spec without unit tables in a fused emission")
                      : e->fail(KWOK_EDEVICE, "k_tick: device heartbeat count differs from the host's (%llu)",
                                (unsigned long long)e->n_managed);
         e->poisoned = true;
@@ -2343,7 +2366,7 @@ int retire(kwok_engine* e) {
         // what follows the header in the chain (pool, job lists) beyond the stream, and k_emit
         e->prof_ms[KWOK_T_EMIT] += std::max(0.0, k0 + k1 - std::max(classify + header + pool, stream)) + k2 + k3;
         e->prof_ms[KWOK_T_KERNEL] += kern;
-        e->prof_ms[KWOK_T_EMIT_KERNEL] += k2;
+        e->prof_ms[KWOK_T_EMIT_KERNEL] += k2 + k3;  // k_emit and k_pod_jobs (split ticks)
         e->prof_ticks++;
     }
     if (H.overflow) return failed(e->fail(KWOK_ENOMEM, "output arena overflow (%llu bytes)", (unsigned long long)H.arena_bytes));

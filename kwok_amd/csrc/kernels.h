@@ -107,6 +107,7 @@ struct DevState {
     uint32_t use_events_only;  // this tick Use-checks only pods with an event (a quiet tick: kwok_tick_submit)
     uint32_t foreign;          // multi rank: this rank's sticky foreign-IP flag, sent in the exchange message
     uint32_t xcap_u, xcap_r;   // multi rank, TICK_XSPEC: the list allgather's Use / release capacity per rank
+    uint32_t fuse_pods;        // split ticks: k_pod_jobs writes the pod patch bytes itself (every spec has unit tables)
     uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp

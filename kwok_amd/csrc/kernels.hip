@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include <type_traits>
+
 #include "device.h"
 #include "kernels.h"
 
@@ -1186,6 +1188,14 @@ __device__ __forceinline__ void emit_node_chunk(const DevState& S, uint32_t nbas
 
 // pod chunk c: the block's live groups [c*256, c*256 + 256)
 constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs x (record + offset)
+constexpr uint32_t POD_STAGE_WORDS_F = 512 * 16 / 4;      // fused (k_pod_jobs<true>): the records only
+// fused emission (k_pod_jobs<true>): the patch bytes of a wave's staged jobs,
+// written by the wave itself (defined with k_emit's table path below)
+struct TabWave {  // k_emit's EmitWave, table path only: job records, value rows
+    uint4 rec[64];
+    uint8_t seg[(VROW_BIAS + 64 * VROW_STRIDE + 4 + 15) & ~15];
+};
+__device__ __forceinline__ void fused_pod_emit(const DevState& S, TabWave* W, const uint4* stg, uint32_t n, uint64_t ord0, uint64_t off0);
 // A thread's jobs take consecutive ordinals (thread-major canonical order), so a
 // wave's jobs are one contiguous ordinal range: their 16-byte k_emit records and
 // 8-byte arena offsets are staged in LDS (`stage`, 12 KiB per wave: up to 512
@@ -1199,7 +1209,10 @@ constexpr uint32_t POD_STAGE_WORDS = 512 * (16 + 8) / 4;  // per wave: 512 jobs 
 // of the 1M x 10M churn tick, which visits all 19 chunks of every block).
 // WAVE: the same for one wave's 64-group run on its own (k_pod_jobs): wave
 // scans, no block barrier; gidx = the thread's group index in each chunk.
-template <int NC, bool WAVE = false>
+// FUSE (k_pod_jobs<true>): the staged records carry the patch length (record.w
+// = spec | len << 16) and the wave emits their bytes itself (fused_pod_emit, over
+// its own stage); no k_emit job records, offsets written by the emission.
+template <int NC, bool WAVE = false, bool FUSE = false>
 __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
                                                 uint32_t nbk, uint32_t ng, const uint32_t (&gidx)[NC], Bases& run,
                                                 const Layout& L, uint32_t* stage, uint32_t nj0 = 0) {
@@ -1292,7 +1305,7 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             const uint64_t o = rb[i].v[AG_ALLOC] + v[4 * i + 3] + (uint32_t)k;
             areuse[i][k] = ((uint32_t)k < my_alloc[i] && L.alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
         }
-    uint4* stg = reinterpret_cast<uint4*>(stage + (threadIdx.x >> 6) * POD_STAGE_WORDS);
+    uint4* stg = reinterpret_cast<uint4*>(stage + (threadIdx.x >> 6) * (FUSE ? POD_STAGE_WORDS_F : POD_STAGE_WORDS));
     uint64_t* stg_off = reinterpret_cast<uint64_t*>(stg + 512);
 #pragma unroll
     for (int i = 0; i < NC; i++) {
@@ -1346,9 +1359,10 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
                     const uint64_t ord = r.v[AG_PP] + jl;
                     const uint32_t len = sd_len[i][k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
                     S.pp_pods[ord] = handle;
-                    stg_off[jl - wpre] = chunk_bytes + vbytes;
+                    if constexpr (!FUSE) stg_off[jl - wpre] = chunk_bytes + vbytes;
                     S.pp_len[ord] = len;
-                    stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, ctm[i][k], sp[i][k]);  // the bytes: k_emit
+                    // the bytes: k_emit (FUSE: this wave, below; len <= max_len < 2^16)
+                    stg[jl - wpre] = make_uint4(stat ? pip : 0u, hip, ctm[i][k], FUSE ? (uint32_t)sp[i][k] | len << 16 : sp[i][k]);
                     jl++;
                     vbytes += sd_max[i][k];
                     // the apiserver applied the patch
@@ -1361,7 +1375,12 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             dirty |= s != gi.st(k);
             nst[k] = s;
         }
-        {  // the wave's staged records -> pp_job[base + wpre, base + wend); the wave's
+        uint32_t fuse_n = 0;  // FUSE: the wave's job count (emitted below, after the state stores)
+        uint64_t fuse_off0 = 0;
+        if constexpr (FUSE) {
+            fuse_n = (uint32_t)__shfl((int)jl, 63) - wpre;
+            fuse_off0 = chunk_bytes + (uint32_t)__shfl((int)v[4 * i + 2], 0);  // the wave's first job's offset
+        } else {  // the wave's staged records -> pp_job[base + wpre, base + wend); the wave's
            // LDS operations run in order, so the next chunk's staging follows these reads
             const uint32_t wend = (uint32_t)__shfl((int)jl, 63);
             uint4* dst = S.pp_job + r.v[AG_PP] + wpre;
@@ -1383,6 +1402,11 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             o.z = nst[4] | (uint32_t)nst[5] << 16;
             o.w = nst[6] | (uint32_t)nst[7] << 16;
             *reinterpret_cast<uint4*>(S.pod_state + gi.slot) = o;
+        }
+        if constexpr (FUSE) {  // the staged jobs' bytes: the wave's stage becomes the emission's rows
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            fused_pod_emit(S, reinterpret_cast<TabWave*>(stg), stg, fuse_n, r.v[AG_PP] + wpre, fuse_off0);
         }
     }
     if constexpr (!WAVE) __syncthreads();
@@ -2186,7 +2210,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 const uint64_t total = (acc_old & ACC_MASK) + acc_v;
                 st_sc1(&S.bar->acc[t][0], 0ull);  // the next tick starts from zero
                 st_host(&S.hdr_host->tot[t], total);
-                if (t == AG_PP) S.emit_n[0] = (uint32_t)total;  // for k_emit, which runs after this launch
+                // for k_emit, which runs after this launch (a fused split tick: k_pod_jobs writes the bytes)
+                if (t == AG_PP) S.emit_n[0] = ((phases & TICK_SPLIT) && S.fuse_pods) ? 0u : (uint32_t)total;
                 if (t == AG_INIT) S.emit_n[1] = (uint32_t)total;
                 if (t == AG_HB) {
                     if (total != n_hb)  // the heartbeat stream was laid out for the host's count
@@ -2277,7 +2302,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             }
             if (xA || xrel) pool_barrier(S, S.n_chain);  // the pool phase reads every rank's bits
         }
-        if (b == 0 && t < 2) S.emit_n[t] = t ? H->n_init : H->n_pp;  // this launch builds k_emit's jobs
+        if (b == 0 && t < 2)  // this launch builds k_emit's jobs (a fused split tick: k_pod_jobs writes the pod bytes)
+            S.emit_n[t] = t ? H->n_init : (((phases & TICK_SPLIT) && S.fuse_pods) ? 0u : H->n_pp);
         if (b == 0 && t < 16) {  // fleet counters
             uint64_t c = 0;
             for (int r = 0; r < S.world; r++) c += X[r].counters[t];
@@ -2328,20 +2354,24 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
 constexpr int JOB_WAVES = 4;
 constexpr int JOB_NC = 2;  // consecutive runs per wave, their loads and scans interleaved
 constexpr int JOB_NF_BYTES = 768;  // node flags staged per wave (two buckets of ~350 node slots)
-__global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
-    __shared__ uint32_t stage[JOB_WAVES * POD_STAGE_WORDS];
+// FUSE: the runs' pod patch bytes too (fused_pod_emit over each run's staged jobs,
+// when every spec has unit tables): no job records written and read back by k_emit
+template <bool FUSE>
+__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
+    constexpr int NC = FUSE ? 1 : JOB_NC;  // fused: one run per wave (its emission holds the registers)
+    __shared__ uint32_t stage[JOB_WAVES * (FUSE ? POD_STAGE_WORDS_F : POD_STAGE_WORDS)];
     __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
     __shared__ uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
     static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
     const uint32_t b = blockIdx.x / wg_per_block;
     const uint32_t w = (uint32_t)wave_id();
-    const uint32_t c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * JOB_NC;  // the wave's first run
+    const uint32_t c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * NC;  // the wave's first run
     if (b >= S.n_chain || c0 >= (uint32_t)MAX_WC) return;
     // every input of the wave's setup in one round trip: the block's JobBase, the
     // runs' dirty bits and prefix, the fill marks of the block's buckets
     const JobBase* JB = S.jbase + b;
     const uint32_t jtag = JB->tag;
-    const uint32_t dirty = (S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c0 >> 5)] >> (c0 & 31)) & 3u;
+    const uint32_t dirty = (S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c0 >> 5)] >> (c0 & 31)) & (NC == 2 ? 3u : 1u);
     const uint4 wp = S.wc_pre[(size_t)b * MAX_WC + c0];
     uint32_t bk0, nbk;
     block_range(S, b, bk0, nbk);
@@ -2375,7 +2405,7 @@ __global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_
     uint32_t nj0 = 0;
     if (c0 * WC_GROUPS < ng) {
         const uint32_t ja = find_bucket(gpre, nbk, c0 * WC_GROUPS);
-        const uint32_t jb = find_bucket(gpre, nbk, min((c0 + JOB_NC) * WC_GROUPS, ng) - 1u);
+        const uint32_t jb = find_bucket(gpre, nbk, min((c0 + NC) * WC_GROUPS, ng) - 1u);
         const uint32_t nwords = (jb - ja + 1u) * S.cn / 4u;  // (cn % 4 == 0)
         if (nwords * 4u <= (uint32_t)JOB_NF_BYTES) {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(nflags + (size_t)ja * S.cn);
@@ -2387,8 +2417,10 @@ __global__ __launch_bounds__(64 * JOB_WAVES) void k_pod_jobs(DevState S, uint32_
     }
     // both runs (a clean one has nothing to count or emit, so the second run's
     // bases follow from the first's totals either way)
-    const uint32_t gx[JOB_NC] = {c0 * WC_GROUPS + (uint32_t)l, (c0 + 1) * WC_GROUPS + (uint32_t)l};
-    emit_pod_chunks<JOB_NC, true>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0);
+    uint32_t gx[NC];
+#pragma unroll
+    for (int i = 0; i < NC; i++) gx[i] = (c0 + i) * WC_GROUPS + (uint32_t)l;
+    emit_pod_chunks<NC, true, FUSE>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0);
 }
 
 // ingest-time Put (a Deleted watch event), applied immediately
@@ -2569,11 +2601,12 @@ void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t
     // the largest chain block's runs: its buckets x their capacity in 8-slot groups
     const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
     const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
-    const uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, JOB_NC), JOB_WAVES);
+    const uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
     const uint32_t grid = S.n_chain * (wpb ? wpb : 1u);
+    auto kern = S.fuse_pods ? k_pod_jobs<true> : k_pod_jobs<false>;
     if (t0)
-        hipExtLaunchKernelGGL(k_pod_jobs, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb ? wpb : 1u);
-    else hipLaunchKernelGGL(k_pod_jobs, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb ? wpb : 1u);
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb ? wpb : 1u);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb ? wpb : 1u);
 }
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
@@ -2938,7 +2971,8 @@ __device__ __forceinline__ TabJob emit_job_tab(const DevState& S, const JobRaw& 
     return J;
 }
 // the job's value row (25 dwords: TS, zeros, H, zeros, P, zeros) and record
-__device__ __forceinline__ void emit_row_tab(EmitWave* W, const TabJob& J) {
+template <class WV>
+__device__ __forceinline__ void emit_row_tab(WV* W, const TabJob& J) {
     const uint32_t l = lane_id();
     uint32_t* r = reinterpret_cast<uint32_t*>(W->seg + VROW_BIAS + l * VROW_STRIDE);
     const uint32_t v[25] = {(uint32_t)J.ts.w0, (uint32_t)(J.ts.w0 >> 32), (uint32_t)J.ts.w1, (uint32_t)(J.ts.w1 >> 32),
@@ -2962,8 +2996,8 @@ struct TabStep {
     uint32_t d[UNR];
     uint32_t o16, nu, k, u0;
 };
-template <int G, int UNR>
-__device__ __forceinline__ TabStep<UNR> tab_load(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t item,
+template <int G, int UNR, class WV>
+__device__ __forceinline__ TabStep<UNR> tab_load(const DevState& S, const WV* W, uint32_t cnt, uint32_t item,
                                                  uint32_t nsteps) {
     const uint32_t l = lane_id(), li = l % G;
     const uint32_t pass = item / nsteps, step = item - pass * nsteps;  // wave-uniform
@@ -2984,8 +3018,8 @@ __device__ __forceinline__ TabStep<UNR> tab_load(const DevState& S, const EmitWa
     }
     return T;
 }
-template <int G, int UNR>
-__device__ __forceinline__ void tab_store(const DevState& S, const EmitWave* W, const TabStep<UNR>& T) {
+template <int G, int UNR, class WV>
+__device__ __forceinline__ void tab_store(const DevState& S, const WV* W, const TabStep<UNR>& T) {
     const uint8_t* row = W->seg + T.k * VROW_STRIDE;  // biased: row k starts VROW_BIAS bytes in
     uint32_t dor = 0;
 #pragma unroll
@@ -3009,8 +3043,8 @@ __device__ __forceinline__ void tab_store(const DevState& S, const EmitWave* W, 
     }
 }
 // maxnu: the chunk's largest unit count (wave-uniform)
-template <int G, int UNR>
-__device__ __forceinline__ void emit_phase2_tab(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t maxnu) {
+template <int G, int UNR, class WV>
+__device__ __forceinline__ void emit_phase2_tab(const DevState& S, const WV* W, uint32_t cnt, uint32_t maxnu) {
     const uint32_t nsteps = (maxnu + G * UNR - 1) / (G * UNR);
     const uint32_t items = ((cnt + 64 / G - 1) / (64 / G)) * nsteps;
     if (items == 0) return;
@@ -3033,8 +3067,8 @@ struct FlatStep {
     uint4 t[UNR];
     uint32_t d[UNR], k[UNR], ok[UNR];
 };
-template <int UNR>
-__device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const EmitWave* W, uint32_t& k, uint32_t& u,
+template <int UNR, class WV>
+__device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const WV* W, uint32_t& k, uint32_t& u,
                                                    uint32_t dk, uint32_t du, uint32_t mu, uint32_t cnt) {
     FlatStep<UNR> F;
 #pragma unroll
@@ -3056,8 +3090,8 @@ __device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const Emit
     }
     return F;
 }
-template <int UNR>
-__device__ __forceinline__ void flat_store(const DevState& S, const EmitWave* W, const FlatStep<UNR>& F, uint64_t o16,
+template <int UNR, class WV>
+__device__ __forceinline__ void flat_store(const DevState& S, const WV* W, const FlatStep<UNR>& F, uint64_t o16,
                                            uint32_t g) {
     uint32_t dor = 0;
 #pragma unroll
@@ -3078,8 +3112,8 @@ __device__ __forceinline__ void flat_store(const DevState& S, const EmitWave* W,
             emit_st(S.arena, (o16 + g + 64u * i) << 4,
                     make_uint4(F.t[i].x | v[i].x, F.t[i].y | v[i].y, F.t[i].z | v[i].z, F.t[i].w | v[i].w));
 }
-template <int UNR>
-__device__ __forceinline__ void emit_phase2_flat(const DevState& S, const EmitWave* W, uint32_t cnt, uint32_t mu) {
+template <int UNR, class WV>
+__device__ __forceinline__ void emit_phase2_flat(const DevState& S, const WV* W, uint32_t cnt, uint32_t mu) {
     const uint32_t l = lane_id();
     const uint64_t o16 = W->rec[0].x;
     const uint32_t total = cnt * mu;
@@ -3092,6 +3126,62 @@ __device__ __forceinline__ void emit_phase2_flat(const DevState& S, const EmitWa
         flat_store<UNR>(S, W, cur, o16, g0 + l);
         cur = nxt;
     }
+}
+
+// ---- fused pod emission (k_pod_jobs<true>) ---------------------------------
+// A wave's jobs (staged records, record.w = spec | len << 16, consecutive
+// ordinals from ord0, reservations back to back from off0) in chunks of 64:
+// their arena offsets (a wave scan of the specs' max_len), pp_off, and the
+// bytes by the table path as k_emit writes them.  The host fuses only while
+// every spec has unit tables; a job without them fails the tick (TICK_ERR_EMIT).
+static_assert(sizeof(TabWave::seg) >= VROW_AREA, "value rows fit TabWave");
+static_assert(sizeof(TabWave) <= POD_STAGE_WORDS_F * 4, "TabWave aliases a wave's fused stage");
+__device__ __forceinline__ void fused_pod_emit(const DevState& S, TabWave* W, const uint4* stg, uint32_t n, uint64_t ord0, uint64_t off0) {
+    const uint32_t l = lane_id();
+    // the wave's <= 512 records into registers (lane l: jobs l, l + 64, ...): the
+    // stage they leave is W (TabWave aliases it)
+    uint4 rr[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) rr[q] = 64u * q + l < n ? stg[64u * q + l] : make_uint4(0u, 0u, 0u, 0u);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    SpecCache sc{0xFFFFFFFFu, NO_TAB, 0u};
+    uint64_t base = off0;
+    bool bad = false;
+    for (uint32_t c = 0; c < n; c += 64u) {
+        const uint32_t cnt = min(64u, n - c);
+        const bool live = l < cnt;
+        JobRaw R;
+        R.j = rr[0];
+#pragma unroll
+        for (int k = 0; k < 7; k++) rr[k] = rr[k + 1];  // (a select on the chunk index would put rr in scratch)
+        R.len = R.j.w >> 16;
+        R.j.w &= 0xFFFFu;
+        if (live && R.j.w != sc.id) {
+            const SpecDesc& sd = S.specs[R.j.w];
+            sc.id = R.j.w, sc.tab_off = sd.tab_off, sc.max_len = sd.max_len;
+        }
+        const uint32_t mb = live ? sc.max_len : 0u;
+        const uint32_t incl = wave_incl_scan(mb);
+        R.off = base + (incl - mb);
+        base += rdlane(incl, 63);
+        if (live) S.pp_off[ord0 + c + l] = R.off;
+        const TabJob J = emit_job_tab(S, R, live, sc);
+        if (__ballot(!J.ok) != 0) {
+            bad = true;
+            continue;
+        }
+        emit_row_tab(W, J);
+        uint32_t mx = J.nu;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        const uint32_t mu = __builtin_amdgcn_readfirstlane(J.mu);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rows before phase 2 reads them
+        if (__ballot(live && J.mu != mu) == 0) emit_phase2_flat<EMIT_FLAT_UNR>(S, W, cnt, mu);
+        else emit_phase2_tab<EMIT_TAB_G, EMIT_TAB_UNR>(S, W, cnt, __builtin_amdgcn_readfirstlane(mx));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // phase 2's reads before the next rows
+    }
+    if (bad && l == 0) st_host(&S.hdr_host->err, TICK_ERR_EMIT);
 }
 
 // ---- node inits of one blob (the common case: nodes created alike) --------

@@ -4,7 +4,8 @@ k_emit writes a pod patch from its spec's per-shape unit tables (static bytes
 plus value-row overlays) or, for specs without tables, assembles each 16-byte
 unit from at most two source regions (kernels.hip "k_emit"); the spec programs
 and node blobs come from the block's LDS cache when they fit and from global
-memory otherwise.  Every test runs with the tables, without them, and mixed.  These
+memory otherwise.  Every test runs with the tables (fused into k_pod_jobs and
+not), without them, and mixed.  These
 tests drive both paths for pod patches (pod_controller.go:404-439 over
 pod.status.tpl) and node-init patches (node_controller.go:356-391 over
 node.status.tpl), in the same tick and separately, with patches far past
@@ -19,12 +20,19 @@ from kwok_amd import abi
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["table", "general", "mixed"])
+@pytest.fixture(autouse=True, params=["table", "table-fused", "table-unfused", "general", "mixed"])
 def emit_path(request, monkeypatch):
-    """pod patches from the per-shape unit tables, from the general region
-    emitter (KWOK_EMIT_TAB_UNITS=0), or both (a cap that tables only the first
-    specs registered, so chunks mix the two and fall back as a whole)"""
-    if request.param == "general":
+    """pod patches from the per-shape unit tables (on split ticks written by
+    k_pod_jobs itself, the fused emission, when the tick is dense; "table-fused"
+    on every split tick, KWOK_FUSE_EMIT=1; "table-unfused": always by k_emit
+    from job records, KWOK_FUSE_EMIT=0), from the general region emitter
+    (KWOK_EMIT_TAB_UNITS=0), or both (a cap that tables only the first specs
+    registered, so chunks mix the two and fall back as a whole; no fusion)"""
+    if request.param == "table-fused":
+        monkeypatch.setenv("KWOK_FUSE_EMIT", "1")
+    elif request.param == "table-unfused":
+        monkeypatch.setenv("KWOK_FUSE_EMIT", "0")
+    elif request.param == "general":
         monkeypatch.setenv("KWOK_EMIT_TAB_UNITS", "0")
     elif request.param == "mixed":
         monkeypatch.setenv("KWOK_EMIT_TAB_UNITS", "20000")
