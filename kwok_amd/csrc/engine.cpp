@@ -2033,9 +2033,11 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     // 1.79 -> 1.72 ms).  A sparse tick's runs hold a few jobs each; their serial
     // emission per wave loses to k_emit's packed 64-job chunks (C4 churn tick
     // 0.51 -> 0.57 ms fused; tools/gpu_r6b.sh)
-    const bool dense = e->creates_since_tick * 4 >= (uint64_t)S.nb * e->Cp;
-    if (!requeue) e->creates_since_tick = 0;
-    T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
+    if (!requeue) {  // (a requeued tick keeps its decision)
+        const bool dense = e->creates_since_tick * 4 >= (uint64_t)S.nb * e->Cp;
+        e->creates_since_tick = 0;
+        T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
+    }
     S.fuse_pods = T.fuse ? 1u : 0u;
     // ... and leave the whole stream to the streamers: a dirty chain block's share
     // of it would hold up the pool phase, which waits for every dirty block
