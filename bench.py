@@ -73,7 +73,7 @@ NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only
 INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
-PMC_FILE = "r5z_pmc.json"  # rocprofv3 FETCH_SIZE / WRITE_SIZE of this configuration
+PMC_FILE = "r6c_pmc.json"
 
 
 def parse():

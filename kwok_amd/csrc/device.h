@@ -241,8 +241,7 @@ struct IngSummary {
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)
-    uint32_t creates;       // creates of the chunk (before the apply's checks: an upper bound; fused emission)
-    uint32_t pad;
+    uint32_t pad[2];
 };
 
 // ---- node directory (device-authoritative, ingest.hip) -------------------------

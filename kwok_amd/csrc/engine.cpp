@@ -295,7 +295,7 @@ struct kwok_engine {
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
     int fuse_emit = -1;         // KWOK_FUSE_EMIT: 1 always / 0 never fuse the pod bytes into k_pod_jobs; -1 dense ticks
-    uint64_t creates_since_tick = 0;  // pod creates ingested since the last tick was enqueued (fused emission)
+    uint64_t pod_records_since_tick = 0;  // pod records ingested since the last tick was enqueued (fused emission)
     uint32_t n_untabled = 0;    // registered specs without unit tables (no fused emission while any)
     // Quiet ticks.  A tick's Use(podIP) of an evaluated pod (pod_controller.go:
     // 378-382) is a no-op when the address is already in `used`.  Only a Put clears
@@ -1643,7 +1643,6 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
             if ((rc = grow_pods(e, want))) return rc;
         }
     }
-    e->creates_since_tick += sum.creates;
     if ((rc = enqueue_apply(e, I, false))) return rc;
     if ((rc = read_summary(e, I.sum))) return rc;
     if (G.sum_h->foreign) e->foreign_ips = true;
@@ -1663,6 +1662,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     e->emit_hint = true;
     e->quiet = 0;
     if (!n) return 0;
+    e->pod_records_since_tick += n;
     const auto t0 = clk::now();
     int rc = ingest_reserve(e, n, arena_len);
     if (rc) return rc;
@@ -1822,7 +1822,6 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             const IngSummary& q = G.sums_h[k];
             if (q.need > e->Cp) break;  // its pass (and every later chunk's) returned: growth first
             rejected += (int)q.rejected;
-            e->creates_since_tick += q.creates;
             if (q.foreign) e->foreign_ips = true;
             if (e->debug_fail_apply == k + 1)
                 return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
@@ -2028,14 +2027,15 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     T.split = T.emit_queued && e->split_jobs;
     // ... writing the pod patch bytes there too when every spec has unit tables
     // (no 16-byte job record per patch written by k_pod_jobs and read back by k_emit)
-    // and the tick is dense: creates since the last tick >= 1/4 of the pod slots,
+    // and the tick is dense: pod records ingested since the last tick (creates,
+    // updates, deletes: a bound on the patches their pods can need) >= 1/4 of the pod slots,
     // so most dirty runs hold hundreds of jobs (1M x 10M initial tick: emission
     // 1.79 -> 1.72 ms).  A sparse tick's runs hold a few jobs each; their serial
     // emission per wave loses to k_emit's packed 64-job chunks (C4 churn tick
     // 0.51 -> 0.57 ms fused; tools/gpu_r6b.sh)
     if (!requeue) {  // (a requeued tick keeps its decision)
-        const bool dense = e->creates_since_tick * 4 >= (uint64_t)S.nb * e->Cp;
-        e->creates_since_tick = 0;
+        const bool dense = e->pod_records_since_tick * 4 >= (uint64_t)S.nb * e->Cp;
+        e->pod_records_since_tick = 0;
         T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
     }
     S.fuse_pods = T.fuse ? 1u : 0u;

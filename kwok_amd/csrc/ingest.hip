@@ -265,7 +265,6 @@ __global__ void k_ing_need(DevState S, IngestBatch I) {
     for (int o = 32; o; o >>= 1) live += (uint32_t)__shfl_xor((int)live, o);
     if (lane() == 0) {
         atomicMax(&I.sum->need, live + c);
-        atomicAdd(&I.sum->creates, c);
         I.creates[b] = 0;  // zero for the next batch
     }
 }
