@@ -428,6 +428,14 @@ int kwok_profile_read(kwok_engine* e, double ms_sum[KWOK_T_COUNT], uint64_t* tic
  * waiting for the device, host bookkeeping after the wait, whole call. */
 enum { KWOK_H_ENQUEUE = 0, KWOK_H_WAIT, KWOK_H_POST, KWOK_H_TOTAL, KWOK_H_COUNT };
 int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], uint64_t* ticks);
+/* Which tick kernel ran (diagnostics, tests): heartbeat-once ticks expected to
+ * have nothing to emit run a counting kernel (k_once); one that had work after
+ * all runs again with the full tick kernel.  Counts since create. */
+enum { KWOK_STAT_TICKS_FULL = 0 /* ticks run by the full tick kernel (redone ticks included) */,
+       KWOK_STAT_TICKS_ONCE /* heartbeat-once ticks completed by the counting kernel */,
+       KWOK_STAT_ONCE_REDO /* counting-kernel ticks that had work and ran again with the full kernel */,
+       KWOK_STAT_COUNT };
+int kwok_engine_stats(const kwok_engine* e, uint64_t out[KWOK_STAT_COUNT]);
 
 /* Host only (no device): renderer.renderToJSON (renderer.go:49-89) - the
  * covered subset of Go text/template, then sigs.k8s.io/yaml.YAMLToJSON - of

@@ -142,6 +142,9 @@ func (x *echoes) encode(ws []watchObj) (objBatch, int, error) {
 		if err := b.add(w); err != nil {
 			return b, dropped, err
 		}
+		if w.deleted { // the object's last event: echoes still noted for it will not come
+			x.forget(w.uid)
+		}
 	}
 	return b, dropped, nil
 }
@@ -384,6 +387,9 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 		case kindDelete, kindDeleteFin: // DeletePod (pod_controller.go:155-183); the engine freed the handle
 			ref, fin := c.podRef[h], kind == kindDeleteFin
 			gone = append(gone, h)
+			// the pod's noted echoes go here, before the task: the echo its finalizer
+			// patch notes (whenever the task runs) is then dropped, not re-ingested
+			c.echo.forget(c.podUID[h])
 			tasks.Add(func() {
 				pods := c.conf.ClientSet.CoreV1().Pods(ref.Namespace)
 				if fin { // only pods with finalizers (len(pod.Finalizers) != 0, :161)
@@ -405,7 +411,6 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 		}
 	})
 	for _, h := range gone { // the later Deleted watch event finds no handle (CNI: it still runs cni.Remove)
-		c.echo.forget(c.podUID[h])
 		delete(c.podByUID, c.podUID[h])
 		delete(c.podUID, h)
 		delete(c.podRef, h)

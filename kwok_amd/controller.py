@@ -323,6 +323,8 @@ class Controller:
                 continue
             seen.add(w.uid)
             keep.append(w)
+            if w.deleted:  # the object's last event: echoes still noted for it will not come
+                self.echo.forget(w.uid)
         return keep, [json.dumps(w.obj, separators=(",", ":")).encode() for w in keep]
 
     def _flush_nodes(self, batch):
@@ -457,12 +459,15 @@ class Controller:
         n += self._apply_patches(POD_PATCH, L["pp"], L["pp_off"], L["pp_len"])
         gone = []
         for h, f in zip(L["dl"], L["dlf"]):  # Patch(removeFinalizers) if finalizers, then Delete(grace 0)
+            # the engine freed the handle: the pod's noted echoes go BEFORE the apply, so
+            # that the echo of its finalizer patch (noted by the apply) is dropped
+            # (gpu_controller.go forgets in the tick callback, ahead of the task)
+            self.echo.forget(self.pod_uid.get(int(h)))
             self._apply(DELETE_FIN if f else DELETE, int(h), None)
             gone.append(int(h))
             n += 1
         for h in gone:  # the later Deleted watch event finds no handle
             uid = self.pod_uid.pop(h, None)
-            self.echo.forget(uid)
             self.pod_by_uid.pop(uid, None)
             self.pod_ref.pop(h, None)
         self.stats.bodies += n

@@ -120,6 +120,9 @@ struct TickHdr {
     uint32_t xovf;
     // multi rank: some rank's message carried its foreign-IP flag (BACK, every rank alike)
     uint32_t xforeign;
+    // k_once found work to emit (a delete, patch, Get, Put, Use, event or node init): the
+    // host runs the tick again with k_tick (kernels queued behind it skipped)
+    uint32_t redo, pad3;
 };
 
 constexpr uint32_t TICK_ERR_BARRIER = 1;  // a cross-block wait timed out
@@ -137,6 +140,13 @@ enum : int {
     CLK_RSVD,
 };
 
+// k_once (heartbeat-once ticks with nothing to emit): one wave per bucket,
+// ONCE_WAVES buckets per block; its counts in ONCE_ACC_WORDS packed words
+constexpr int ONCE_WAVES = 8;
+constexpr int ONCE_ACC_WORDS = 5;       // (hb, lock) (managed, ready) (eval, total) (pending, running) (rare, -)
+constexpr int ONCE_FIELD_BITS = 27;     // each packed partial sum < 2^27 (node / pod slots of the rank)
+constexpr int ONCE_NODE_LDS = 1024;     // node slots per bucket it handles (S.cn)
+
 // cross-block state of the tick kernel (device memory, zeroed at create and
 // after a failed tick), every word on its own 128-byte line
 struct GridBar {
@@ -145,8 +155,12 @@ struct GridBar {
     uint32_t pcnt, pad1[31];    // pool-phase barrier: arrivals of the current instance
     uint32_t pgen, pad2[31];    //                     generation
     unsigned long long neg_entry_max, p1_max, stream_end_max, pad3[13];  // profiled ticks
-    uint32_t skip, pad4[31];    // multi rank: a BACK stopped for long lists; launches queued behind it skip
+    uint32_t skip, pad4[31];    // a tick the host must finish (multi rank: a BACK stopped for long lists; k_once:
+                                // work to emit): launches queued behind it skip
     unsigned long long acc[16][16];  // single rank: field accumulators (arrivals << ACC_SHIFT | sum), one line each
+    // k_once: packed accumulators (arrivals << ACC_SHIFT | hi << 27 | lo), per XCD shard [0, 8) and the
+    // fleet [8], word w of a shard on a line of its own
+    unsigned long long once_acc[9][ONCE_ACC_WORDS][16];
 };
 constexpr int ACC_SHIFT = 54;  // arrivals in the top 10 bits (<= 1023 chain blocks), sums below
 constexpr unsigned long long ACC_MASK = (1ull << ACC_SHIFT) - 1;

@@ -143,6 +143,7 @@ struct kwok_engine {
     bool hb_pre_dirty = true;                        // the per-chain-block heartbeat bases need k_hb_pre
     uint32_t hb_epoch = 0;                           // kwok_tick_result.heartbeat_epoch: bumped when the managed set changes
     uint32_t* d_hb_pre = nullptr;
+    uint32_t* d_hb_bpre = nullptr;                   // [nb + 1] per-bucket bases (k_once)
     // pods: no host mirror.  The device's pod_state (USED = slot occupancy),
     // pod_node and node_state (NS_SLOT) are the state the GPU ingest pass
     // (ingest.hip) applies batches to; pod_fill is its per-bucket fill mark.
@@ -253,6 +254,8 @@ struct kwok_engine {
         bool split = false;         // TICK_SPLIT: k_pod_jobs builds the pod jobs after the tick's launches
         bool fuse = false;          // ... and writes their patch bytes itself (DevState::fuse_pods)
         bool quiet = false;         // only pods with an event are Use-checked (kwok_engine::quiet)
+        bool once = false;          // launched as k_once (a heartbeat-once tick expected to have nothing to emit)
+        bool no_once = false;       // k_once found work: the tick runs again with k_tick
         bool alloc = false;
         // the tick in the slot
         int state = 0;  // SLOT_FREE, SLOT_QUEUED (enqueued), SLOT_DONE (finished on the host, not collected)
@@ -314,6 +317,8 @@ struct kwok_engine {
     bool foreign_ips = false;   // sticky: a podIP not assigned by this engine entered the pool
     bool global_foreign = false;  // multi rank, sticky: some rank's exchange message carried its foreign_ips
     bool quiet_ok = true;
+    bool once_ok = true;        // KWOK_ONCE=0: heartbeat-once ticks always run k_tick (A/B)
+    uint64_t stats[KWOK_STAT_COUNT] = {};  // kwok_engine_stats
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
@@ -990,7 +995,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->d_hb_bpre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
                     e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv, e->d_ssend, e->d_srecv};
     for (void* p : ptrs)
@@ -1176,6 +1181,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->split_jobs = !(sj && sj[0] == '0');
         const char* fe = getenv("KWOK_FUSE_EMIT");
         e->fuse_emit = fe && fe[0] ? (fe[0] == '0' ? 0 : 1) : -1;
+        const char* on = getenv("KWOK_ONCE");
+        e->once_ok = !(on && on[0] == '0');
         const char* zc = getenv("KWOK_INGEST_ZC");
         e->ingest_zc = !(zc && zc[0] == '0');
     }
@@ -1229,6 +1236,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.pool_blk, 2 * (size_t)nblk)) || (rc = dalloc(e, &S.bar, 1)) ||
         (rc = dalloc(e, &S.blockagg, (size_t)S.n_chain * AG_STRIDE)) ||
         (rc = dalloc(e, &S.dmask, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &S.list_blk, (size_t)S.n_chain * 2)) || (rc = dalloc(e, &e->d_hb_pre, (size_t)S.n_chain + 1)) ||
+        (rc = dalloc(e, &e->d_hb_bpre, (size_t)e->nb + 1)) ||
         (rc = dalloc(e, &S.wc_pre, (size_t)S.n_chain * MAX_WC)) ||
         (rc = dalloc(e, &S.wc_dirty, (size_t)S.n_chain * WC_DIRTY_WORDS)) || (rc = dalloc(e, &S.jbase, (size_t)S.n_chain)) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
@@ -1261,6 +1269,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->sync_spin = !(sy && strcmp(sy, "block") == 0);
     }
     S.hb_pre = e->d_hb_pre;
+    S.hb_bpre = e->d_hb_bpre;
     S.pod_fill = e->d_pod_fill;
     S.rank = e->rank;
     if (e->multi) {
@@ -1888,7 +1897,7 @@ int kwok_pack_pod_events(const kwok_pod_event* ev, size_t n, const char* arena, 
         r.target = create ? x.node_handle : x.handle;
         if (x.op != KWOK_OP_UPSERT && x.op != KWOK_OP_DELETE) st = KWOK_EINVAL;
         else if (create && x.node_handle < 0) st = KWOK_EINVAL;  // by spec.nodeName: the full form only
-        else if (x.phase > KWOK_PHASE_OTHER) st = KWOK_EINVAL;
+        else if (x.phase > KWOK_PHASE_UNKNOWN) st = KWOK_EINVAL;  // (a pod phase: the device prep's bound)
         else if (x.op == KWOK_OP_UPSERT && (x.spec_id < 0 || x.spec_id > 0xFFFF)) st = KWOK_EINVAL;
         else if (x.op == KWOK_OP_UPSERT && (x.creation_unix < 0 || x.creation_unix > 0xFFFFFFFFll)) st = KWOK_EDOMAIN;
         else if (x.op == KWOK_OP_UPSERT && (!ip_of(x.host_ip, &r.host_ip) || !ip_of(x.pod_ip, &r.pod_ip)))
@@ -2006,7 +2015,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         // heartbeat handles are written in node order at per-chain-block bases:
         // managed nodes of the buckets before each block's range (k_hb_pre, from
         // the node batches' per-bucket counts)
-        launch_hb_pre(S, e->d_hb_pre, st);
+        launch_hb_pre(S, e->d_hb_pre, e->d_hb_bpre, st);
         HIPCHK(e, hipGetLastError());
         e->hb_pre_dirty = false;
     }
@@ -2050,13 +2059,23 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
                      (T.split ? TICK_SPLIT : 0);
     if (!requeue) {
+        T.no_once = false;
         memset(T.hdr_h, 0, sizeof(TickHdr));  // the slot's previous tick was collected
         if (++e->tick_tag == 0) e->tick_tag = 1;
         T.tag = e->tick_tag;
         T.target = ++e->front_launches * S.n_chain;
     }
     const uint64_t now = T.now;
-    if (!e->multi) {
+    // a heartbeat-once tick expected to have nothing to emit (no events since the
+    // previous tick, quiet Use checks) runs k_once: one wave per bucket, every load
+    // of the bucket in flight at once.  One that has work after all is run again
+    // with k_tick by retire (TickHdr::redo; a launch queued behind it skips)
+    T.once = !e->multi && S.hb_once && e->once_ok && !T.emit_queued && !T.split && T.quiet && !T.no_once &&
+             S.cn <= (uint32_t)ONCE_NODE_LDS && e->PL < (1u << ONCE_FIELD_BITS) && e->NL < (1u << ONCE_FIELD_BITS);
+    if (T.once) {
+        launch_tick_once(S, now, (uint64_t)e->start, nhb, prof & TICK_PROF, st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+        HIPCHK(e, hipGetLastError());
+    } else if (!e->multi) {
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
@@ -2254,6 +2273,21 @@ void trace_tick(kwok_engine* e) {
 
 
 
+// k_once met work to emit in slot k's tick (a delete, patch, Get, Put, Use, pod
+// event or node init): run the tick again with k_tick (same tag and arrival
+// target: k_once made no arrivals).  The launch queued behind it skipped on the
+// device (GridBar::skip); retire enqueues it again afterwards.
+int redo_tick(kwok_engine* e, int k) {
+    kwok_engine::TickSlot& T = e->slots[k];
+    e->stats[KWOK_STAT_ONCE_REDO]++;
+    memset(T.hdr_h, 0, sizeof(TickHdr));
+    HIPCHK(e, hipMemsetAsync(&e->S.bar->skip, 0, sizeof(uint32_t), e->st));
+    T.no_once = true;
+    if (int rc = enqueue_tick(e, k, true)) return rc;
+    HIPCHK(e, hipEventSynchronize(T.done));
+    return KWOK_OK;
+}
+
 // Finish the oldest queued tick on the host: wait for it, complete a multi-rank
 // tick with long lists, derive the header, check errors, mirror DeletePods into
 // the host slot state.  The result stays in the slot until kwok_tick_collect.
@@ -2302,6 +2336,11 @@ int retire(kwok_engine* e) {
         if (rc) return failed(rc);
     }
     if (e->multi && T.hdr_h->xforeign) e->global_foreign = true;  // (the BACK launch that ran to the end)
+    bool requeue_next = false;
+    if (T.once && T.hdr_h->redo) {
+        if (int rc = redo_tick(e, k)) return failed(rc);
+        requeue_next = next >= 0 && e->slots[next].state == SLOT_QUEUED;
+    }
     const auto t2 = clk::now();
     if (!e->multi) derive_header(*T.hdr_h, T.arena_cap, e->hb_stride, e->S.hb_once != 0);
     const TickHdr& H = *T.hdr_h;
@@ -2400,6 +2439,16 @@ int retire(kwok_engine* e) {
     e->host_ms[KWOK_H_POST] += ms_between(t2, t3);
     e->host_ms[KWOK_H_TOTAL] += ms_between(t1, t3);
     e->host_ticks++;
+    e->stats[T.once ? KWOK_STAT_TICKS_ONCE : KWOK_STAT_TICKS_FULL]++;
+    if (requeue_next) {  // the tick queued behind a redone one skipped on the device
+        if (int rc = enqueue_tick(e, next, true)) {
+            kwok_engine::TickSlot& U = e->slots[next];
+            U.state = SLOT_DONE;
+            U.rc = rc;
+            U.err = e->err;
+            e->poisoned = true;
+        }
+    }
     return KWOK_OK;
 }
 
@@ -2457,6 +2506,12 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     if (e->iprof) fprintf(stderr, "[kwok submit] enqueue %.3f ms\n", ms_between(t0, clk::now()));
     e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
     e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
+    return KWOK_OK;
+}
+
+extern "C" int kwok_engine_stats(const kwok_engine* e, uint64_t out[KWOK_STAT_COUNT]) {
+    if (!e || !out) return KWOK_EINVAL;
+    for (int i = 0; i < KWOK_STAT_COUNT; i++) out[i] = e->stats[i];
     return KWOK_OK;
 }
 

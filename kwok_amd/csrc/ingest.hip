@@ -1035,8 +1035,9 @@ __global__ __launch_bounds__(256) void k_free_zombies(DevState S) {
 }
 
 // heartbeat handle bases: hb_pre[c] = managed nodes of the buckets before chain
-// block c's range [nb*c/Gc, ...); hb_pre[Gc] = all (one block)
-__global__ __launch_bounds__(1024) void k_hb_pre(DevState S, uint32_t* pre) {
+// block c's range [nb*c/Gc, ...); hb_pre[Gc] = all; bpre[bk] = managed nodes of
+// the buckets before bucket bk, bpre[nb] = all (one block)
+__global__ __launch_bounds__(1024) void k_hb_pre(DevState S, uint32_t* pre, uint32_t* bpre) {
     __shared__ uint32_t part[1024];
     const uint32_t t = threadIdx.x, T = blockDim.x, nc = S.n_chain;
     auto lo = [&](uint32_t c) { return (uint32_t)((uint64_t)S.nb * c / nc); };
@@ -1054,9 +1055,12 @@ __global__ __launch_bounds__(1024) void k_hb_pre(DevState S, uint32_t* pre) {
     uint32_t acc = part[t] - sum;
     for (uint32_t c = c0; c < c1; c++) {
         pre[c] = acc;
-        for (uint32_t bk = lo(c); bk < lo(c + 1); bk++) acc += S.mb_count[bk];
+        for (uint32_t bk = lo(c); bk < lo(c + 1); bk++) {
+            bpre[bk] = acc;
+            acc += S.mb_count[bk];
+        }
     }
-    if (t == T - 1) pre[nc] = acc;
+    if (t == T - 1) pre[nc] = bpre[S.nb] = acc;
 }
 
 // kwok_node_has: one wave per name
@@ -1154,8 +1158,8 @@ void launch_node_apply(const DevState& S, const NodeBatch& N, hipStream_t st) {
 void launch_free_zombies(const DevState& S, hipStream_t st) {
     hipLaunchKernelGGL(k_free_zombies, dim3(cdiv(S.nb, 4)), dim3(256), 0, st, S);
 }
-void launch_hb_pre(const DevState& S, uint32_t* hb_pre, hipStream_t st) {
-    hipLaunchKernelGGL(k_hb_pre, dim3(1), dim3(1024), 0, st, S, hb_pre);
+void launch_hb_pre(const DevState& S, uint32_t* hb_pre, uint32_t* hb_bpre, hipStream_t st) {
+    hipLaunchKernelGGL(k_hb_pre, dim3(1), dim3(1024), 0, st, S, hb_pre, hb_bpre);
 }
 void launch_node_lookup(const DevState& S, const uint8_t* names, const uint32_t* lens, uint32_t n, uint32_t* out,
                         hipStream_t st) {

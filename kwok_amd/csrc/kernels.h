@@ -88,6 +88,7 @@ struct DevState {
     TickHdr* hdr_host;         // pinned host copy of the tick header (written by k_emit_pods)
     uint16_t* pod_fill;        // per owned bucket: upper bound of used pod slots (only grows; the ingest pass)
     const uint32_t* hb_pre;    // [n_chain + 1] managed nodes before each chain block (k_hb_pre)
+    const uint32_t* hb_bpre;   // [nb + 1] managed nodes before each owned bucket (k_hb_pre; k_once)
     GridBar* bar;              // cross-block state
     uint32_t* blockagg;        // [n_chain][AG_STRIDE] per-chain-block records of the classify phase
     uint64_t* dmask;           // [n_chain][2] dirty pod-chunk / node-chunk masks (FRONT -> BACK)
@@ -150,6 +151,12 @@ constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_
 // arrival count at which every chain block of this FRONT launch has arrived
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// a heartbeat-once tick expected to have nothing to emit (single rank): one
+// wave per bucket counts it; a tick that has work after all sets TickHdr::redo
+// and GridBar::skip (the host runs it again with launch_tick)
+void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, hipStream_t st,
+                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+uint32_t once_blocks(const DevState& S);
 // split ticks: the pod jobs (deletes, patch job records, state transitions) of
 // every dirty 64-group run of every chain block, one wave each
 void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
@@ -238,8 +245,8 @@ int launch_node_sort(const DevState& S, const NodeBatch& N, void* tmp, size_t tm
 void launch_node_apply(const DevState& S, const NodeBatch& N, hipStream_t st);
 // zombie node entries (deleted / placeholder) no pod references any more are freed
 void launch_free_zombies(const DevState& S, hipStream_t st);
-// the managed nodes before each chain block (heartbeat handle bases) from mb_count
-void launch_hb_pre(const DevState& S, uint32_t* hb_pre, hipStream_t st);
+// the managed nodes before each chain block and each bucket (heartbeat handle bases) from mb_count
+void launch_hb_pre(const DevState& S, uint32_t* hb_pre, uint32_t* hb_bpre, hipStream_t st);
 // kwok_node_has: names[i * NAME_STRIDE] (lens[i] bytes) -> out[i] = the entry's node_state (0: none)
 void launch_node_lookup(const DevState& S, const uint8_t* names, const uint32_t* lens, uint32_t n, uint32_t* out,
                         hipStream_t st);

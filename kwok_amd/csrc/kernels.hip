@@ -1878,9 +1878,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ Layout sh_L;
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
-    if (S.multi && !(phases & TICK_XLISTS) &&
-        __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        return;  // queued behind a tick the host has not finished (long lists): re-launched later
+    if (!(phases & TICK_XLISTS) && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        return;  // queued behind a tick the host has not finished (long lists; k_once redo): re-launched later
 #define TSTAMP(k)                                                                                         \
     do {                                                                                                  \
         if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -2338,6 +2337,286 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
               pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase, tag);
 #undef TSTAMP
 #undef TWAIT
+}
+
+// ---------------------------------------------------------------------------
+// k_once: a heartbeat-once tick expected to have nothing to emit
+// (KWOK_CFG_HEARTBEAT_ONCE, single rank, no events ingested since the previous
+// tick, quiet Use checks) - the steady tick of the cgo drop-in.  Its work is
+// k_tick's FRONT classification, counted: KeepNodeHeartbeat's handle list
+// (node_controller.go:159-172), needLockNode / configureNode's predicate per node
+// (:210-223, 356-391), needLockPod / configurePod / computePatchData's per pod
+// (pod_controller.go:252-269, 371-439), and ONE heartbeat body (:393-401).
+//
+// One wave per bucket with every load of the bucket in flight at once: the node
+// bytes, then the pod state rows (no chain of round trips).  The pods' node
+// indices are read only when the bucket's node entries disagree on the re-lock
+// flag: with every node of a bucket re-locked (or none), a pod's node cannot
+// change its counts.  A wave that meets work to emit (a delete, patch, Get, Put,
+// Use, pod event, node init or queued node lock) marks the tick: its last
+// arriver then sets TickHdr::redo and GridBar::skip instead of completing it,
+// and the host runs the tick again with k_tick (launches queued behind it skip
+// and are enqueued again).  Counts go to per-XCD shards of packed accumulators
+// (blocks are dealt to the 8 XCDs round robin); a shard's last arriver adds its
+// totals to the fleet words, whose last arriver publishes them.  A completed
+// tick adds n_chain to GridBar::arrive, as k_tick's chain blocks would have.
+// ---------------------------------------------------------------------------
+constexpr int ONCE_ROWS = 8;          // 64-group rows (512 pod slots) of a bucket a wave holds in registers
+constexpr int ONCE_SPEC_ROWS = 4;     // rows loaded before the bucket's fill mark lands
+constexpr int ONCE_NODE_WORDS = ONCE_NODE_LDS / 256;  // node-state words per lane
+constexpr uint32_t ONCE_M27 = (1u << ONCE_FIELD_BITS) - 1u;
+
+// the fleet total of packed word k (the last arriver of word k)
+__device__ __forceinline__ void once_publish(const DevState& S, uint32_t k, uint64_t total, uint32_t n_hb, int phases,
+                                             uint64_t c_arrive) {
+    TickHdr* P = S.hdr_host;
+    const uint64_t lo = total & ONCE_M27, hi = total >> ONCE_FIELD_BITS;
+    switch (k) {
+        case 0:
+            st_host(&P->tot[AG_HB], lo);
+            st_host(&P->tot[AG_LOCK], hi);
+            if (lo != n_hb) st_host(&P->err, TICK_ERR_LAYOUT);  // the host's managed-node count
+            st32_sc1(&S.emit_n[0], 0u);
+            st32_sc1(&S.emit_n[1], 0u);
+            st_host(&P->clk[CLK_P1_MAX], c_arrive);
+            if (phases & TICK_PROF) {
+                st_host(&P->clk[CLK_ENTRY_MIN], ~ld_sc1(&S.bar->neg_entry_max));
+                st_sc1(&S.bar->neg_entry_max, 0ull);
+            }
+            break;
+        case 1:
+            st_host(&P->tot[AG_MANAGED], lo);
+            st_host(&P->tot[AG_READY], hi);
+            break;
+        case 2:
+            st_host(&P->tot[AG_EVAL], lo);
+            st_host(&P->tot[AG_TOTAL], hi);
+            break;
+        case 3:
+            st_host(&P->tot[AG_PENDING], lo);
+            st_host(&P->tot[AG_RUNNING], hi);
+            break;
+        default:
+            if (lo) {  // work to emit: the host finishes the tick with k_tick
+                st32_sc1(&S.bar->skip, 1u);
+                st_host(&P->redo, 1u);
+            } else {   // the arrivals k_tick's chain blocks would have made (GridBar::arrive is cumulative)
+                __hip_atomic_fetch_add(&S.bar->arrive, (unsigned long long)S.n_chain, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+    }
+}
+
+// one 8-slot group of a k_once bucket: group_counts_fast's planes for a quiet
+// tick (Use checks of pods with an event only: such a pod is evaluated, which
+// is work to emit anyway), counted as if nothing were rare - a rare group voids
+// the tick (it runs again with k_tick).  rl: the pods' RELOCK flags as two-pod
+// planes (bit 0 / bit 16 of each word).  Returns whether anything is rare.
+template <bool CNI>
+__device__ __forceinline__ uint32_t once_group(const uint32_t (&stw)[4], const uint32_t (&rl)[4], uint32_t& n_eval,
+                                               uint32_t& n_total, uint32_t& n_pend, uint32_t& n_run) {
+    constexpr uint32_t M = 0x00010001u;
+    uint32_t rare = 0, pe = 0, pt = 0, pp = 0, pr = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t s = stw[w];
+        const uint32_t s1 = s >> 1, s2 = s >> 2, s5 = s >> 5, s6 = s >> 6, s7 = s >> 7;
+        const uint32_t s8 = s >> 8, s9 = s >> 9, s10 = s >> 10, s11 = s >> 11;
+        const uint32_t live = s & ~s2;                       // USED, not DELETE_PENDING
+        const uint32_t eval = live & (s6 | (rl[w] & ~s1));  // EVENT, or RELOCK & !DISREGARD
+        const uint32_t running = s9 & ~(s8 | s10), pending = s8 & ~(s9 | s10);
+        const uint32_t ok = running & s5 & s7;               // Running, CONFORMS, HAS_HOST_IP
+        // computePatchData's patch (a Get with it when the podIP is empty); EnableCNI: only once it has one
+        const uint32_t need = CNI ? eval & ~ok & s11 : eval & ~(ok & s11);
+        rare |= (s & s2) | need | (eval & s6);               // a delete, a patch, an event
+        pe += eval & M, pt += live & M, pp += live & pending & M, pr += live & running & M;
+    }
+    n_eval += (pe & 0xFFFFu) + (pe >> 16);
+    n_total += (pt & 0xFFFFu) + (pt >> 16);
+    n_pend += (pp & 0xFFFFu) + (pp >> 16);
+    n_run += (pr & 0xFFFFu) + (pr >> 16);
+    return rare & M;
+}
+
+template <bool CNI>
+__global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_t now_unix, uint64_t start_unix,
+                                                            uint32_t n_hb, int phases) {
+    __shared__ uint32_t nfl32[ONCE_WAVES][ONCE_NODE_LDS / 4];  // the bucket's node tick flags, per wave
+    __shared__ uint64_t part[ONCE_WAVES][ONCE_ACC_WORDS];
+    __shared__ uint8_t tmpl[16 * HB_MAX_UNITS];
+    const uint32_t t = threadIdx.x, l = t & 63u, w = (uint32_t)wave_id(), b = blockIdx.x;
+    if (ld32_sc1(&S.bar->skip)) return;  // queued behind a tick the host must finish (re-enqueued then)
+    const bool stamp = S.trace && t == 0 && b < S.n_chain;
+#define OSTAMP(k) \
+    if (stamp) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime()
+    OSTAMP(0);
+    if ((phases & TICK_PROF) && t == 0)
+        atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const uint32_t bk = b * ONCE_WAVES + w;
+    uint32_t hb = 0, lock = 0, mng = 0, rdy = 0, ev = 0, tot = 0, pnd = 0, run = 0, rare = 0;
+    if (bk < S.nb) {  // (wave-uniform)
+        const uint32_t cn = S.cn, cp = S.cp;
+        const uint32_t fill = min((uint32_t)S.pod_fill[bk], cp);
+        // ---- every load of the bucket: node bytes first (classified first), pod state rows
+        const uint8_t* nst = S.node_state + (size_t)bk * cn;
+        uint32_t nw[ONCE_NODE_WORDS];
+#pragma unroll
+        for (int c = 0; c < ONCE_NODE_WORDS; c++) {
+            const uint32_t i = 4u * (l + 64u * c);
+            nw[c] = 0;
+            if (256u * c < cn && i < cn) nw[c] = *reinterpret_cast<const uint32_t*>(nst + i);
+        }
+        const uint16_t* pst = S.pod_state + (size_t)bk * cp;
+        uint4 st[ONCE_ROWS];
+#pragma unroll
+        for (int r = 0; r < ONCE_ROWS; r++) {
+            const uint32_t g8 = 8u * (l + 64u * r);
+            st[r] = make_uint4(0, 0, 0, 0);
+            if (g8 < (r < ONCE_SPEC_ROWS ? cp : fill)) st[r] = *reinterpret_cast<const uint4*>(pst + g8);
+        }
+        // ---- nodes: LockNode / configureNode (A.5), heartbeat handles, re-lock flags
+        uint32_t or0 = 0, and0 = 1, has = 0, base = S.hb_bpre[bk];
+#pragma unroll
+        for (int c = 0; c < ONCE_NODE_WORDS; c++) {
+            if (256u * c < cn) {  // (uniform)
+                const uint32_t word = nw[c], i0 = 4u * (l + 64u * c);
+                uint32_t tickw = 0, m = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint8_t s = (uint8_t)(word >> (8 * k));
+                    const NodeCls nc = classify_node(s);
+                    hb += nc.hb;
+                    lock += nc.lock;
+                    mng += nc.managed;
+                    rdy += nc.ready;
+                    rare |= (nc.init || (s & NS_EVENT_LOCK)) ? 1u : 0u;
+                    const uint32_t f = node_tick_flags(s);
+                    tickw |= f << (8 * k);
+                    if (s) or0 |= f & 1u, and0 &= f & 1u, has = 1;
+                    m += (uint32_t)nc.managed << k;
+                }
+                if (i0 < cn) nfl32[w][l + 64u * c] = tickw;
+                // KeepNodeHeartbeat's handles, node order: the wave's managed nodes of this word
+                const uint32_t cnt = (uint32_t)__popc(m), inc = wave_incl_scan(cnt);
+                uint32_t pos = base + inc - cnt;
+                for (uint32_t mm = m; mm; mm &= mm - 1) {
+                    if (pos < S.n_node_slots)
+                        S.hb_nodes[pos] = S.node_handle_base + (int32_t)((size_t)bk * cn + i0 + (uint32_t)__builtin_ctz(mm));
+                    pos++;
+                }
+                base += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            }
+        }
+        // a pod's node matters only if the bucket's node entries disagree on RELOCK
+        const bool any_set = __ballot(has && or0) != 0, any_clr = __ballot(has && !and0) != 0;
+        const bool uni = !(any_set && any_clr);
+        const uint8_t u = any_set ? (uint8_t)NT_RELOCK : (uint8_t)0;
+        OSTAMP(8);
+        const uint16_t* pnd_ = S.pod_node + (size_t)bk * cp;
+        // ---- pods: needLockPod / computePatchData, counted (once_group)
+        auto count_row = [&](uint32_t g8, const uint4& s4, const uint32_t (&rl)[4]) {
+            const bool in = g8 < fill;
+            const uint32_t stw[4] = {in ? s4.x : 0u, in ? s4.y : 0u, in ? s4.z : 0u, in ? s4.w : 0u};
+            rare |= once_group<CNI>(stw, rl, ev, tot, pnd, run);
+        };
+        auto lds_flags = [&](const uint4& n4, uint32_t (&rl)[4]) {
+            const uint8_t* nfw = reinterpret_cast<const uint8_t*>(nfl32[w]);
+            const uint32_t q[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t a = nfw[min(q[k] & 0xFFFFu, (uint32_t)ONCE_NODE_LDS - 1u)];
+                const uint32_t c = nfw[min(q[k] >> 16, (uint32_t)ONCE_NODE_LDS - 1u)];
+                rl[k] = a | c << 16;  // (NT_RELOCK is bit 0)
+            }
+        };
+        if (uni) {
+            const uint32_t p = u ? 0x00010001u : 0u;
+            const uint32_t rl[4] = {p, p, p, p};
+#pragma unroll
+            for (int r = 0; r < ONCE_ROWS; r++) count_row(8u * (l + 64u * r), st[r], rl);
+            for (uint32_t r = ONCE_ROWS; 512u * r < fill; r++) {  // buckets of more than 4096 pod slots
+                const uint32_t g8 = 8u * (l + 64u * r);
+                const uint4 s4 = g8 < fill ? *reinterpret_cast<const uint4*>(pst + g8) : make_uint4(0, 0, 0, 0);
+                count_row(g8, s4, rl);
+            }
+        } else {
+            uint4 nd[ONCE_ROWS];
+#pragma unroll
+            for (int r = 0; r < ONCE_ROWS; r++) {
+                const uint32_t g8 = 8u * (l + 64u * r);
+                nd[r] = g8 < fill ? *reinterpret_cast<const uint4*>(pnd_ + g8) : make_uint4(0, 0, 0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();  // (the wave's node flags are in LDS)
+#pragma unroll
+            for (int r = 0; r < ONCE_ROWS; r++) {
+                uint32_t rl[4];
+                lds_flags(nd[r], rl);
+                count_row(8u * (l + 64u * r), st[r], rl);
+            }
+            for (uint32_t r = ONCE_ROWS; 512u * r < fill; r++) {
+                const uint32_t g8 = 8u * (l + 64u * r);
+                uint4 s4 = make_uint4(0, 0, 0, 0), n4 = s4;
+                if (g8 < fill) {
+                    s4 = *reinterpret_cast<const uint4*>(pst + g8);
+                    n4 = *reinterpret_cast<const uint4*>(pnd_ + g8);
+                }
+                uint32_t rl[4];
+                lds_flags(n4, rl);
+                count_row(g8, s4, rl);
+            }
+        }
+        OSTAMP(2);
+    }
+    // ---- counts: wave -> block -> XCD shard -> fleet
+    auto wsum = [](uint32_t x) { return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(x), 63); };
+    {
+        const uint64_t v0 = wsum(hb) | wsum(lock) << ONCE_FIELD_BITS, v1 = wsum(mng) | wsum(rdy) << ONCE_FIELD_BITS;
+        const uint64_t v2 = wsum(ev) | wsum(tot) << ONCE_FIELD_BITS, v3 = wsum(pnd) | wsum(run) << ONCE_FIELD_BITS;
+        const uint64_t v4 = __ballot(rare != 0) ? 1u : 0u;
+        if (l == 0) part[w][0] = v0, part[w][1] = v1, part[w][2] = v2, part[w][3] = v3, part[w][4] = v4;
+    }
+    __syncthreads();
+    if (t < (uint32_t)ONCE_ACC_WORDS) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int i = 0; i < ONCE_WAVES; i++) v += part[i][t];
+        const uint32_t G = gridDim.x, x = b & 7u, nsh = min(G, 8u), nx = (G - x + 7u) / 8u;
+        const unsigned long long old = atomicAdd(&S.bar->once_acc[x][t][0], (1ull << ACC_SHIFT) | v);
+        if ((old >> ACC_SHIFT) == nx - 1u) {  // the shard is complete
+            const uint64_t sx = (old & ACC_MASK) + v;
+            st_sc1(&S.bar->once_acc[x][t][0], 0ull);  // the next tick starts from zero
+            const unsigned long long o2 = atomicAdd(&S.bar->once_acc[8][t][0], (1ull << ACC_SHIFT) | sx);
+            if ((o2 >> ACC_SHIFT) == nsh - 1u) {
+                st_sc1(&S.bar->once_acc[8][t][0], 0ull);
+                once_publish(S, t, (o2 & ACC_MASK) + sx, n_hb, phases, __builtin_amdgcn_s_memrealtime());
+            }
+        }
+    }
+    OSTAMP(3);
+    // ---- the one heartbeat body (hb_bodies), arena offset 0
+    if (b == 0 && n_hb) {
+        const Ts nw = format_ts(now_unix), sw = format_ts(start_unix);
+        const uint32_t nb16 = 16u * S.hb_units;
+        for (uint32_t i = t; i < nb16; i += 64u * ONCE_WAVES) {
+            const uint8_t k = S.hb_kind[i];
+            tmpl[i] = (uint8_t)(k == 0xFF ? S.hb_static[i] : k < TS_LEN ? ts_byte(nw, k) : ts_byte(sw, k - TS_LEN));
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < S.hb_units; i += 64u * ONCE_WAVES)
+            reinterpret_cast<uint4*>(S.arena)[i] = reinterpret_cast<const uint4*>(tmpl)[i];
+    }
+    OSTAMP(6);
+#undef OSTAMP
+}
+
+uint32_t once_blocks(const DevState& S) { return (S.nb + ONCE_WAVES - 1) / ONCE_WAVES; }
+
+void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, hipStream_t st,
+                      hipEvent_t t0, hipEvent_t t1) {
+    const uint32_t grid = once_blocks(S);
+    auto kern = S.cni ? k_once<true> : k_once<false>;
+    if (t0) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, t0, t1, 0, S, now, start, n_hb, phases);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, S, now, start, n_hb, phases);
 }
 
 // ---------------------------------------------------------------------------

@@ -432,6 +432,14 @@ class Engine(EngineBase):
         self._check(self._lib.kwok_profile_host(self._h, 1 if reset else 0, ms, C.byref(n)), "profile_host")
         return dict(zip(self.HOST, list(ms))), n.value
 
+    STATS = ("ticks_full", "ticks_once", "once_redo")  # KWOK_STAT_* order
+
+    def stats(self):
+        """kwok_engine_stats: ticks run by k_tick / completed by k_once / k_once ticks redone"""
+        out = (C.c_uint64 * len(self.STATS))()
+        self._check(self._lib.kwok_engine_stats(self._h, out), "engine_stats")
+        return dict(zip(self.STATS, list(out)))
+
     def device_outputs(self):
         v = abi.DeviceView()
         self._check(self._lib.kwok_device_outputs(self._h, C.byref(v)), "device_outputs")

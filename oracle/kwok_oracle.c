@@ -737,9 +737,6 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
     return rejected;
 }
 
-static inline int keep_eval(const kwok_oracle* o, size_t h);
-/* EnableCNI: the pods the next tick evaluates without a podIP (configurePod's
- * cni.Setup set, pod_controller.go:383-389), canonical order */
 /* kwok_ingest_pods_packed: the compact records as the kwok_pod_event they stand
  * for (dotted quads of the IPs, the node by handle), through the event switch
  * above; a create without a node handle is not expressible (KWOK_EINVAL) */
@@ -752,6 +749,10 @@ int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, siz
     size_t* pre = (size_t*)calloc(n + 1, sizeof(size_t)); /* records sent before record i */
     size_t m = 0, off = 0;
     int bad = 0;
+    if (!ev || !ar || !st || !hs || !pre) {
+        free(ev), free(ar), free(st), free(hs), free(pre);
+        return KWOK_ENOMEM;
+    }
     for (size_t i = 0; i < n; i++) {
         const kwok_pod_rec* r = &recs[i];
         const int create = (r->op & KWOK_REC_NEW) != 0;
@@ -782,7 +783,7 @@ int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, siz
     }
     int32_t* st2 = (int32_t*)calloc(m + 1, sizeof(int32_t));
     uint32_t* rel = (uint32_t*)calloc(m + 1, sizeof(uint32_t));
-    const int rc = kwok_oracle_ingest_pods(o, ev, m, ar, off, hs, st2, rel);
+    const int rc = st2 && rel ? kwok_oracle_ingest_pods(o, ev, m, ar, off, hs, st2, rel) : KWOK_ENOMEM;
     if (rc >= 0) {
         for (size_t i = 0; i < n; i++) {
             const int sent = st[i] == 1;
@@ -797,6 +798,9 @@ int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, siz
     return rc < 0 ? rc : bad;
 }
 
+static inline int keep_eval(const kwok_oracle* o, size_t h);
+/* EnableCNI: the pods the next tick evaluates without a podIP (configurePod's
+ * cni.Setup set, pod_controller.go:383-389), canonical order */
 int kwok_oracle_cni_pending(kwok_oracle* o, int32_t* out, size_t cap, size_t* n_out) {
     if (!o->cni || !n_out) return KWOK_EINVAL;
     size_t n = 0;

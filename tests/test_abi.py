@@ -46,6 +46,7 @@ def test_oracle_library_exports():
                  "kwok_pack_pod_events",  # host helper of the compact wire form (engine library)
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
                  "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
+                 "kwok_engine_stats",  # engine only: which tick kernel ran
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
                  "kwok_decode_node", "kwok_decode_pod", "kwok_decode_nodes", "kwok_decode_pods",  # host codec: feeds both, lives in the engine library
                  "kwok_template_render", "kwok_template_last_error", "kwok_pod_template_patch",
@@ -133,7 +134,7 @@ def test_profile_enums_match_python_mirrors():
     must list exactly the KWOK_T_* / KWOK_H_* entries of the header, in order."""
     from kwok_amd.engine import Engine
     hdr = open(os.path.join(ROOT, "include", "kwok_engine.h")).read()
-    for prefix, names in (("KWOK_T_", Engine.PHASES), ("KWOK_H_", Engine.HOST)):
+    for prefix, names in (("KWOK_T_", Engine.PHASES), ("KWOK_H_", Engine.HOST), ("KWOK_STAT_", Engine.STATS)):
         body = re.search(r"enum\s*\{\s*(%s\w+[^}]*)\}" % prefix, hdr).group(1)
         ents = [re.sub(r"\s*=.*", "", x).strip() for x in re.sub(r"/\*.*?\*/", "", body).split(",")]
         ents = [x for x in ents if x]

@@ -104,7 +104,7 @@ def test_reference_pod_controller():
     c.close()
 
 
-def scenario(cs, c, ticks=5, nodes=20, pods_per_node=4, seed=3):
+def scenario(cs, c, ticks=5, nodes=20, pods_per_node=4, seed=3, fin_frac=0.3):
     """nodes and pods created, modified, deleted between ticks; returns the
     clientset's write calls per tick"""
     import random
@@ -116,7 +116,7 @@ def scenario(cs, c, ticks=5, nodes=20, pods_per_node=4, seed=3):
     for t in range(ticks):
         for _ in range(nodes * pods_per_node // ticks):
             status = {"phase": "Pending"} if rng.random() < 0.8 else {}
-            fin = ["kwok.x-k8s.io/x"] if rng.random() < 0.3 else []
+            fin = ["kwok.x-k8s.io/x"] if rng.random() < fin_frac else []
             p = pod("pod-%05d" % k, "node-%03d" % rng.randrange(nodes), status=status)
             if fin:
                 p["metadata"]["finalizers"] = fin
@@ -153,12 +153,16 @@ def test_echoes_dropped_and_change_nothing(deliver):
     engine.  Every write call (PatchStatus / Patch / Delete with its body) is
     the same in both runs, tick by tick.  deliver=sync: echoes overtake their
     patch's response (dropped at the next tick's flush); queued: they arrive
-    after it (dropped on arrival)."""
+    after it (dropped on arrival).  No finalizers here: the echo of a pod's
+    finalizer patch is the one echo whose ingest is NOT harmless - the engine
+    already deleted the pod and released its podIP, so re-ingesting the echo
+    (a pod holding that address) and its Deleted event would release the address
+    a second time while another pod holds it (test_finalizer_patch_echo_is_dropped)."""
     runs = {}
     for sup in (True, False):
         cs = FakeClientset(deliver=deliver)
         c = controller(cs, suppress=sup, manage_nodes_with_annotation_selector=MANAGE, cidr="10.0.0.1/24")
-        runs[sup] = (scenario(cs, c), c.stats, {k: v["status"] for k, v in cs.store["pods"].items()})
+        runs[sup] = (scenario(cs, c, fin_frac=0.0), c.stats, {k: v["status"] for k, v in cs.store["pods"].items()})
         c.close()
     (a, sa, pa), (b, sb, pb) = runs[True], runs[False]
     assert [len(x) for x in a] == [len(x) for x in b]
@@ -174,6 +178,42 @@ def test_echoes_dropped_and_change_nothing(deliver):
     assert sb.pod_records > sa.pod_records
     # pods on managed nodes ended Running with IPs
     assert sum(1 for st in pa.values() if st.get("phase") == "Running" and st.get("podIP")) > 0
+
+
+@pytest.mark.parametrize("deliver", ["sync", "queued"])
+def test_finalizer_patch_echo_is_dropped(deliver):
+    """DeletePod of a pod with finalizers (pod_controller.go:155-183): the
+    finalizer patch's echo (deletionTimestamp, no finalizers) is dropped - the
+    engine already deleted the pod - so no second Delete is ever issued, and the
+    Deleted event forgets the pod's echoes.  (The controller forgets a deleted
+    pod's echoes before its apply notes the finalizer patch's: the Go drop-in does
+    so in the tick callback, ahead of the concurrent task.)"""
+    cs = FakeClientset(node("n0"), deliver=deliver)
+    c = controller(cs, manage_nodes_with_annotation_selector=MANAGE, cidr="10.0.0.1/24")
+    cs.create(pod("a", "n0", status={"phase": "Pending"}, finalizers=["x.io/f"]))
+    cs.create(pod("b", "n0", status={"phase": "Pending"}))
+    c.step(S0 + 30)
+    cs.pump()
+    uids = [cs.get("pods", ("default", name))["metadata"]["uid"] for name in ("a", "b")]
+    for name in ("a", "b"):  # kubectl delete: deletionTimestamp set, finalizers kept
+        q = cs.get("pods", ("default", name))
+        q["metadata"]["deletionTimestamp"] = "2024-01-01T00:01:00Z"
+        cs.update(q)
+    cs.pump()
+    n0 = len(cs.calls)
+    d0 = c.stats.echoes_on_arrival + c.stats.echoes_at_flush
+    c.step(S0 + 60)
+    cs.pump()
+    calls = [(v, k) for v, kind, k, _ in cs.calls[n0:] if kind == "pods"]
+    assert calls == [("patch_merge", ("default", "a")), ("delete", ("default", "a")), ("delete", ("default", "b"))]
+    for t in range(2):
+        n1 = len(cs.calls)
+        c.step(S0 + 90 + 30 * t)
+        cs.pump()
+        assert not [x for x in cs.calls[n1:] if x[1] == "pods"], "tick %d: pod calls after the deletes" % t
+    assert c.stats.echoes_on_arrival + c.stats.echoes_at_flush >= d0 + 1  # the finalizer patch's echo
+    assert cs.list("pods") == [] and not any(u in c.echo.rv for u in uids)  # forgotten at their Deleted events
+    c.close()
 
 
 def test_runs_for_added_modified_deleted_in_one_batch():

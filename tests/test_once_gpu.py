@@ -1,0 +1,190 @@
+"""GPU: heartbeat-once ticks through k_once ("k_once").
+
+An engine created with KWOK_CFG_HEARTBEAT_ONCE (the cgo drop-in's flags,
+engine_cgo.go) runs a tick that follows no ingest and Use-checks only pods
+with an event through k_once, the counting kernel: KeepNodeHeartbeat's handle
+list and one body (node_controller.go:159-172, 393-401), the lock predicate
+per node (:210-223, 356-391) and the pod predicates (pod_controller.go:252-269,
+371-439), counted.  A tick that turns out to have work (a pod patched without
+an IP last tick that now takes its Get, a pod on a node whose lock was queued)
+is run again with k_tick, and a tick queued behind it skips and is enqueued
+again.  Every tick is compared with the oracle (a full-body engine of the same
+trace): handles, the one body, node-init / pod patches, deletes, counters and
+the pod state; kwok_engine_stats says which kernel ran."""
+import numpy as np
+import pytest
+
+from gpu_common import Driver, compare_state, external_deletes, mark_deleting, new_pods
+from kwok_amd import abi, workload
+from kwok_amd.engine import Engine, make_config
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def compare_once(eo, oo, where):
+    assert list(eo.heartbeat_nodes) == list(oo.heartbeat_nodes), where + " heartbeat handles"
+    if len(oo.heartbeat_nodes):
+        assert eo.heartbeat_body(0) == oo.heartbeat_body(0), where + " heartbeat body"
+    assert eo.node_inits == oo.node_inits, where + " node inits"
+    assert eo.pod_patches == oo.pod_patches, where + " pod patches"
+    assert eo.deletes == oo.deletes, where + " deletes"
+    assert eo.counters == oo.counters, where + " counters"
+
+
+class OnceDriver(Driver):
+    """gpu_common.Driver with a heartbeat-once engine beside a full-body oracle"""
+
+    def __init__(self, cfg_kw, seed, specs=None):
+        super().__init__(cfg_kw, seed, specs)
+        self.e.close()
+        self.e = Engine(make_config(heartbeat_once=True, **cfg_kw))
+        assert self.spec == [self.e.register_pod_spec(*sp) for sp in (specs or self.DEFAULT_SPECS)]
+
+    def tick(self, where):
+        self.e.tick(self.now, read=False)
+        eo, oo = self.e.read_outputs(heartbeat_once=True), self.o.tick(self.now)
+        self.now += 30
+        compare_once(eo, oo, where)
+        compare_state(self.e, self.o, self.n_slots, where)
+        return eo
+
+    def tick_pair(self, where):
+        self.e.tick_submit(self.now)
+        self.e.tick_submit(self.now + 30)
+        for k in range(2):
+            self.e.tick_collect(read=False)
+            eo, oo = self.e.read_outputs(heartbeat_once=True), self.o.tick(self.now)
+            self.now += 30
+            compare_once(eo, oo, "%s (queued %d)" % (where, k))
+        compare_state(self.e, self.o, self.n_slots, where)
+
+
+KW = dict(cidr="10.0.0.1/16", node_ip="196.168.0.1", buckets=64, node_slots_per_bucket=16, pod_slots_per_bucket=128)
+
+
+def _fleet(seed, managed_all):
+    d = OnceDriver(KW, seed)
+    rng = d.rng
+    n = 300
+    managed = np.ones(n, np.uint8) if managed_all else (rng.random(n) < 0.6).astype(np.uint8)
+    nodes, st = d.nodes(["node-%04d" % i for i in range(n)], managed, (rng.random(n) < 0.95).astype(np.uint8))
+    assert (st == 0).all()
+    ev, ar = new_pods(rng, nodes, 2000, d.spec)
+    ev["phase"] = abi.PHASE_PENDING
+    ev["flags"] |= abi.POD_STATUS_NONEMPTY
+    d.pods(ev, ar)
+    return d, nodes, rng
+
+
+@pytest.mark.parametrize("managed_all", [True, False], ids=["uniform-buckets", "mixed-buckets"])
+def test_steady_ticks_run_k_once(managed_all):
+    """After the initial tick every quiet tick is k_once; a bucket whose nodes
+    all share the re-lock flag counts without the pods' node indices, a mixed one
+    with them (managed_all=False: 60% managed, 5% not lockable)"""
+    d, nodes, rng = _fleet(11, managed_all)
+    d.tick("initial")
+    s0 = d.e.stats()
+    for t in range(4):
+        d.tick("steady %d" % t)
+    d.tick_pair("steady queued")
+    s1 = d.e.stats()
+    assert s1["ticks_once"] - s0["ticks_once"] >= 5, s1
+    assert s1["once_redo"] == s0["once_redo"], s1
+    d.e.close()
+    d.o.close()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_work_without_events_is_redone(seed):
+    """Pods created with an empty status are patched without IPs; the next tick
+    (no events in between) gives them their Gets: k_once finds the work and the
+    tick runs again with k_tick.  Queued: the tick behind a redone one skipped and
+    ran after it.  Then churn (deletes with finalizers, external deletes, creates)
+    and quiet ticks again."""
+    d, nodes, rng = _fleet(seed, False)
+    d.tick("initial")
+    d.tick("steady")
+    ev, ar = new_pods(rng, nodes, 200, d.spec)
+    ev["phase"] = abi.PHASE_NONE
+    ev["flags"] &= ~np.uint8(abi.POD_STATUS_NONEMPTY)
+    d.pods(ev, ar)
+    d.tick("empty-status creates")  # (events: k_tick) patches without IPs
+    s0 = d.e.stats()
+    d.tick("their Gets")            # no events: k_once, work found, redone
+    s1 = d.e.stats()
+    assert s1["once_redo"] == s0["once_redo"] + 1, s1
+    ev, ar = new_pods(rng, nodes, 100, d.spec)
+    ev["phase"] = abi.PHASE_NONE
+    ev["flags"] &= ~np.uint8(abi.POD_STATUS_NONEMPTY)
+    d.pods(ev, ar)
+    d.tick("more empty-status creates")
+    d.tick_pair("Gets, then quiet (queued)")
+    s2 = d.e.stats()
+    assert s2["once_redo"] == s1["once_redo"] + 1, s2
+    assert s2["ticks_once"] >= s1["ticks_once"] + 1, s2
+    idx, _, _, _ = d.live()
+    pick = rng.choice(idx, 80, replace=False)
+    d.pods(*mark_deleting(rng, d, pick[:50]))
+    d.pods(*external_deletes(d, pick[50:]))
+    d.tick("deletes")
+    ev, ar = new_pods(rng, nodes, 60, d.spec)
+    d.pods(ev, ar)
+    d.tick("creates")
+    for t in range(3):
+        d.tick("quiet %d" % t)
+    d.tick_pair("quiet queued")
+    d.e.close()
+    d.o.close()
+
+
+def test_node_delete_and_recreate():
+    """Nodes deleted (their pods stay, on zombie entries, unmanaged) and created
+    again (init patches, re-locked pods): the ticks after the node events run
+    k_tick, the quiet ticks between and after them k_once (zombie entries in a
+    bucket make it mixed), every tick equal to the oracle"""
+    d, nodes, rng = _fleet(7, True)
+    d.tick("initial")
+    names = ["node-%04d" % i for i in range(0, 300, 7)]
+    d.nodes(names, 0, 1, op=abi.OP_DELETE)
+    d.tick("deleted nodes")
+    d.tick("quiet after deletes")
+    d.nodes(names, 1, 1)
+    d.tick("re-created nodes")
+    for t in range(2):
+        d.tick("quiet %d" % t)
+    assert d.e.stats()["ticks_once"] >= 3
+    d.e.close()
+    d.o.close()
+
+
+@pytest.mark.parametrize("managed_frac", [1.0, 0.5])
+def test_fleet_steady_ticks(managed_frac):
+    """200k nodes x 2M pods (the metric's shape at a fifth): the initial tick,
+    then queued quiet ticks through k_once; counters and heartbeat handle lists
+    equal the oracle's every tick"""
+    nodes = 200_000
+    e, fl, _ = workload.build_engine_fleet(Engine, nodes, managed_frac=managed_frac, lockable_frac=0.999, seed=5,
+                                           heartbeat_once=True)
+    o, _, _ = workload.build_engine_fleet(Oracle, nodes, managed_frac=managed_frac, lockable_frac=0.999, seed=5)
+    now = workload.S0 + 30
+    e.tick(now, read=False)
+    o.tick(now, read=False)
+    for k in range(3):
+        now += 30
+        e.tick_submit(now)
+        e.tick_submit(now + 30)
+        for q in range(2):
+            r = e.tick_collect(read=False)
+            E = e.read_arrays(heartbeat_once=True)
+            o.tick(now + 30 * q, read=False)
+            O = o.read_arrays()
+            assert E["counters"] == O["counters"], (k, q)
+            assert (E["heartbeat_nodes"] == O["heartbeat_nodes"]).all(), (k, q)
+            body = O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]
+            assert (E["arena"][E["heartbeat_off"]:E["heartbeat_off"] + r.heartbeat_len] == body).all(), (k, q)
+            assert r.n_pod_patch == r.n_node_init == r.n_delete == 0
+        now += 30
+    assert e.stats()["ticks_once"] == 6 and e.stats()["once_redo"] == 0, e.stats()
+    e.close()
+    o.close()

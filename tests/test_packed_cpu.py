@@ -44,7 +44,7 @@ def test_pack_matches_vectorised_packing():
 
 def test_pack_rejections():
     ar = abi.Arena()
-    ev = np.zeros(6, abi.POD_EVENT_DTYPE)
+    ev = np.zeros(7, abi.POD_EVENT_DTYPE)
     ev["op"] = abi.OP_UPSERT
     ev["handle"] = -1
     ev["node_handle"] = 3
@@ -55,8 +55,9 @@ def test_pack_rejections():
     ev[3]["creation_unix"] = -5                  # before 1970
     ev[4]["op"] = 7                              # no such op
     ev[5]["pod_ip"] = ar.ref("10.0.0.7")         # fine
+    ev[6]["phase"] = abi.PHASE_OTHER             # a node phase, not a pod's (kwok_ingest_pods rejects it too)
     out, st = pack_pod_events(ev, bytes(ar.buf))
-    assert list(st) == [abi.EINVAL, abi.EDOMAIN, abi.EDOMAIN, abi.EDOMAIN, abi.EINVAL, abi.OK]
+    assert list(st) == [abi.EINVAL, abi.EDOMAIN, abi.EDOMAIN, abi.EDOMAIN, abi.EINVAL, abi.OK, abi.EINVAL]
     assert out[5]["pod_ip"] == abi.ip4("10.0.0.7") and out[5]["op"] == abi.OP_UPSERT | abi.REC_NEW
     assert out[5]["target"] == 3
 
