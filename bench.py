@@ -74,6 +74,7 @@ INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
 PMC_FILE = "r6c_pmc.json"
+ONCE_PMC_FILE = "r7_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
 
 
 def parse():
@@ -88,7 +89,8 @@ def parse():
     ap.add_argument("--roofline-ticks", type=int, default=20)
     ap.add_argument("--churn-ticks", type=int, default=5, help="C4 churn ticks after the steady legs (N=1; 0: skip)")
     ap.add_argument("--flap-ticks", type=int, default=5, help="C5 flap ticks on a partially managed fleet (N=1; 0: skip)")
-    ap.add_argument("--once-ticks", type=int, default=1, help="the KWOK_CFG_HEARTBEAT_ONCE leg (N=1; 0: skip)")
+    ap.add_argument("--once-ticks", type=int, default=1, help="the KWOK_CFG_HEARTBEAT_ONCE legs (N=1; 0: skip)")
+    ap.add_argument("--c2", type=int, default=1, help="BASELINE configs[1] at 100k x 1M (N=1; 0: skip)")
     ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
                                                          "metric size: 2M create/delete per tick)")
     ap.add_argument("--emulate-ranks", type=int, default=8, help="N=1: a one-rank RCCL engine folding this many "
@@ -105,10 +107,11 @@ def transitions(c):
     return c[0] + c[1] + c[2] + c[3] + c[5]
 
 
-def cpu_baseline(nodes, threads, ticks):
-    """The C restatement (oracle/kwok_oracle.c, test infrastructure) on the same
-    fleet: built and initial-ticked with all threads, then `ticks` steady ticks
-    on `threads` threads (its OpenMP sweeps) and on one thread."""
+def oracle_steady(nodes, threads, ticks):
+    """The C restatement (oracle/kwok_oracle.c, test infrastructure) on a fleet
+    of `nodes` nodes x 10 pods: built and initial-ticked with all threads, then
+    steady ticks on `threads` threads (its OpenMP sweeps) and on one thread.
+    Returns ({threads: (transitions/s, ms per tick)}, cores, setup + initial s)."""
     from oracle.oracle import Oracle  # test infrastructure: baseline only
     t0 = time.perf_counter()
     o, _, _ = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=threads), nodes,
@@ -121,25 +124,41 @@ def cpu_baseline(nodes, threads, ticks):
     for th in (cores, 1):
         o.set_threads(th)
         trans = 0
+        n = ticks if th > 1 else max(2, ticks // 2)
         t1 = time.perf_counter()
-        for _ in range(ticks if th > 1 else max(2, ticks // 2)):
+        for _ in range(n):
             r = o.tick(now, read=False)
             now += 30
             trans += transitions(r.counters)
         dt = time.perf_counter() - t1
-        legs[th] = (trans / dt, dt / (ticks if th > 1 else max(2, ticks // 2)) * 1e3)
+        legs[th] = (trans / dt, dt / n * 1e3)
     o.close()
+    return legs, cores, t_init
+
+
+def cpu_baseline(nodes, threads, ticks):
+    """The oracle timed on the GPU box's host cores: at the metric fleet (the
+    baseline of `value`) and at BASELINE configs[0] (C1, 1k x 10k) and
+    configs[1] (C2, 100k x 1M), each on all cores and on one"""
+    legs, cores, t_init = oracle_steady(nodes, threads, ticks)
+    cfgs = {}
+    for label, n, k in (("C1", 1_000, 200), ("C2", 100_000, 2 * ticks)):
+        lg, c, ti = oracle_steady(n, threads, k)
+        cfgs[label] = {"nodes": n, "pods": n * workload.PODS_PER_NODE, "cores": c,
+                       "value": lg[c][0], "ms_per_step": lg[c][1],
+                       "single_core": {"value": lg[1][0], "ms_per_step": lg[1][1]}, "setup_initial_s": ti}
     return {"value": legs[cores][0], "unit": "transitions/s", "cores": cores, "kind": "port",
             "ms_per_step": legs[cores][1],
             "single_core": {"value": legs[1][0], "cores": 1, "ms_per_step": legs[1][1]},
+            "configs": cfgs,
             "sample": "oracle/kwok_oracle.c (the C restatement, OpenMP sweeps), the same %d nodes x %d pods "
                       "fleet, steady ticks after the initial tick (setup + initial tick %.1fs on %d threads); "
-                      "the reference Go controllers cannot run here (no Go toolchain)"
-                      % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
+                      "configs: C1 / C2 at their own sizes; the reference Go controllers cannot run here (no Go "
+                      "toolchain)" % (nodes, nodes * workload.PODS_PER_NODE, t_init, cores)}
 
 
 def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
-              packed=True, ch=None):
+              packed=True, ch=None, multi=False):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -225,7 +244,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         "kernel_ms": kern / ticks, "emission_ms": emit / ticks,
         # multi-rank tick: the FRONT header to the (last) BACK launch's start -
         # allgather, and for long lists the host round trip, second allgather, k_pool_apply
-        "exchange_ms": xch / ticks if (world > 1 or os.environ.get("KWOK_FORCE_MULTI")) else None,
+        "exchange_ms": xch / ticks if (world > 1 or multi) else None,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods: H2D of the records and their strings (page-locked batch buffers, "
                 "kwok_host_alloc; batches over KWOK_INGEST_CHUNK records in chunks, each copied while the previous "
@@ -234,19 +253,11 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
                 "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
 
 
-def heartbeat_once_leg(nodes, steps, warmup):
-    """The same fleet and steady ticks with KWOK_CFG_HEARTBEAT_ONCE: the tick
-    materialises ONE heartbeat body (every node's patch is that body,
-    node_controller.go:393-401) and the handle list, for callers that send one
-    body to every node (the cgo drop-in).  The tick then moves the SoA state
-    only: its roofline is the state bytes over the launch time."""
-    e, fl, _ = workload.build_engine_fleet(keng.Engine, nodes, heartbeat_once=True)
-    now = workload.S0 + 30
-    e.tick(now, read=False)  # initial tick
-    # warmup on the timed steps' path (queued two deep), so that the second tick
-    # slot is allocated before timing (as the main leg; blocking warmup ticks left
-    # that allocation to the first timed submit: 68 us per step measured against
-    # 44.5 us between the queued kernels in the kernel trace, profiles/r3am_once_trace.txt)
+def steady_queued(e, now, steps, warmup):
+    """`steps` steady ticks queued two deep (kwok_tick_submit of tick k+1 before
+    kwok_tick_collect of tick k) after `warmup` on the same path (the first
+    queued submit allocates the second tick slot); returns (seconds, transitions,
+    the clock after them)"""
     now += 30
     e.tick_submit(now)
     for w in range(max(warmup, 2)):
@@ -264,31 +275,109 @@ def heartbeat_once_leg(nodes, steps, warmup):
             e.tick_submit(now + 30)
             now += 30
         trans += transitions(e.tick_collect(read=False).counters)
-    dt = time.perf_counter() - t0
+    return time.perf_counter() - t0, trans, now
+
+
+def stored_pmc(name, kernel):
+    """HBM bytes per launch of `kernel` from a stored rocprofv3 FETCH_SIZE /
+    WRITE_SIZE summary, if it was measured on THIS kernels.hip (else None)"""
+    import hashlib
+    pmc = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(pmc):
+        return None, None
+    d = json.load(open(pmc))
+    ksha = hashlib.sha256(open(os.path.join(ROOT, "kwok_amd", "csrc", "kernels.hip"), "rb").read()).hexdigest()
+    if d.get("kernels_sha256") != ksha:
+        return None, None
+    ks = [k for k in d["kernels"] if k == kernel or k.startswith("void %s<" % kernel) or k.startswith(kernel + "<")]
+    if not ks:
+        return None, None
+    return d["kernels"][ks[0]]["hbm_bytes"], ("stored: profiles/%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady "
+                                              "launch of %s on this kernel build (kernels.hip sha256 %s)"
+                                              % (name, ks[0], ksha[:12]))
+
+
+def heartbeat_once_leg(nodes, steps, warmup, churn_ticks):
+    """The drop-in's engine: KWOK_CFG_HEARTBEAT_ONCE (engine_cgo.go), on the
+    metric's fleet.  The tick materialises ONE heartbeat body (every node's
+    patch is that body, node_controller.go:393-401) and the handle list, for
+    callers that send one body to every node.  Legs: the initial tick (1M node
+    inits + 10M Pending->Running patches), steady ticks queued (k_once: a
+    heartbeat-once tick with nothing to emit, one wave per bucket), and C4
+    churn ticks on the same engine."""
+    e, fl, pods = workload.build_engine_fleet(keng.Engine, nodes, heartbeat_once=True)
+    now = workload.S0 + 30
+    e.profile_enable(True)
+    t1 = time.perf_counter()
+    r0 = e.tick(now, read=False)  # initial tick
+    init_wall = time.perf_counter() - t1
+    ph0, _ = e.profile_read()
+    e.profile_enable(False)
+    dt, trans, now = steady_queued(e, now, steps, warmup)
     e.profile_enable(True)
     for _ in range(20):
         now += 30
         r = e.tick(now, read=False)
     ph, nt = e.profile_read()
     e.profile_enable(False)
+    stats = e.stats()
+    churn = None
+    if churn_ticks:
+        now, _, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
     e.close()
     lc = r.local_counters
     state_bytes = NODE_STATE_BYTES * lc[8] + POD_BYTES * lc[10]
     kern = ph["kernel"] / max(nt, 1)
     step_ms = dt / steps * 1e3
+    traffic, traffic_src = stored_pmc(ONCE_PMC_FILE, "k_once")
+    ilc = r0.local_counters
+    init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
     # the roofline over the queued step (kernel + the gap to the next launch), a lower
-    # bound on the kernel's rate: a ~30 us kernel's HIP event pair reads a few us long
-    # (it exceeded the step in round 3); the rocprofv3 kernel durations of this leg are
-    # committed under profiles/ (<round>_once_ktrace.txt, tools/gpu_full.sh)
-    return {"workload": "metric configuration, KWOK_CFG_HEARTBEAT_ONCE (one heartbeat body + the handle list per "
-                        "tick); steady ticks queued", "steps": steps,
+    # bound on the kernel's rate: a ~15 us kernel's HIP event pair reads a few us long;
+    # the rocprofv3 kernel durations of this leg are committed under profiles/
+    # (<round>_once_ktrace.txt, tools/gpu_full.sh)
+    return {"workload": "metric configuration, KWOK_CFG_HEARTBEAT_ONCE (the cgo drop-in's engine: one heartbeat body "
+                        "+ the handle list per tick); steady ticks queued", "steps": steps,
             "value": trans / dt, "unit": "transitions/s", "ms_per_step": step_ms,
             "kernel_ms_events": kern, "classify_ms": ph["classify"] / max(nt, 1),
-            "roofline": {"bound": "hbm (latency-bound chain)", "kernel": "k_tick", "bytes_per_launch": state_bytes,
+            "tick_kernels": stats,
+            "roofline": {"bound": "hbm (one round trip per bucket, launch-bound at this size)", "kernel": "k_once",
+                         "bytes_per_launch": state_bytes,
                          "achieved": state_bytes / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": state_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_per_step_gbs": traffic / (step_ms * 1e-3) / 1e9 if traffic else None,
                          "timing": "queued step time (launch-to-launch), not the event pair",
-                         "note": "SoA state read + written per tick (node 9 + 9 B, pod 10 B)"}}
+                         "note": "bytes: SURVEY 8(d)'s state model without the materialised bodies (node 9 + 9 B, pod "
+                                 "10 B); k_once reads less - a pod's 2-byte state word, its node index only in "
+                                 "buckets whose nodes disagree on the re-lock flag - see traffic"},
+            "initial_tick": {"wall_ms": init_wall * 1e3, "kernel_ms": ph0["kernel"], "emission_ms": ph0["emit_kernel"],
+                             "transitions": transitions(r0.counters),
+                             "emit_roofline": {"kernel": "k_pod_jobs + k_emit", "bytes": init_bytes,
+                                               "achieved": init_bytes / (ph0["emit_kernel"] * 1e-3) / 1e9
+                                               if ph0["emit_kernel"] else None,
+                                               "frac": init_bytes / (ph0["emit_kernel"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                               if ph0["emit_kernel"] else None}},
+            "churn": None if churn is None else {k: churn[k] for k in (
+                "workload", "ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "emission_ms", "value",
+                "unit", "tick_transitions_per_s")}}
+
+
+def c2_leg(steps, warmup):
+    """BASELINE configs[1] at its own size (100k nodes x 1M pods, one MI355X):
+    steady ticks queued, full heartbeat bodies and heartbeat-once"""
+    out = {}
+    for once in (False, True):
+        e, fl, _ = workload.build_engine_fleet(keng.Engine, 100_000, heartbeat_once=once)
+        now = workload.S0 + 30
+        e.tick(now, read=False)
+        dt, trans, now = steady_queued(e, now, steps, warmup)
+        out["heartbeat_once" if once else "full_bodies"] = {"value": trans / dt, "ms_per_step": dt / steps * 1e3,
+                                                            "tick_kernels": e.stats()}
+        e.close()
+    out["workload"] = "BASELINE configs[1]: 100k nodes x 1M pods steady heartbeat + status ticks, 1x MI355X, queued"
+    out["unit"] = "transitions/s"
+    return out
 
 
 def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
@@ -334,7 +423,7 @@ def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
     e.profile_enable(False)
     churn = None
     if churn_ticks:
-        now, _, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
+        now, _, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes, multi=True)  # (a one-rank multi engine)
     e.close()
     return {"ranks": ranks, "workload": "one rank's 1M x 10M fleet; BACK folds %d ranks' exchange messages and lists "
                                         "(KWOK_FORCE_MULTI + KWOK_EMULATE_RANKS, one-rank RCCL allgather)" % ranks,
@@ -345,14 +434,15 @@ def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
                     "8 KiB messages / MB lists is not in it)"}
 
 
-def flap_leg(nodes, ticks):
+def flap_leg(nodes, ticks, heartbeat_once=False):
     """BASELINE configs[4] (C5): a fleet of `nodes` nodes x 10 pods with
     ManageAllNodes=false (annotation selector on 50% of the nodes, disregard
     annotation on 0.1%); per tick 1% of the managed nodes are deleted and
     created again (workload.Flap).  A step = kwok_ingest_nodes of that batch +
     one kwok_tick (heartbeats of the managed half, the flapped nodes' init
     patches, re-evaluation of the managed nodes' pods).  First step warmup."""
-    e, fl, _ = workload.build_engine_fleet(keng.Engine, nodes, managed_frac=0.5, lockable_frac=0.999, seed=5)
+    e, fl, _ = workload.build_engine_fleet(keng.Engine, nodes, managed_frac=0.5, lockable_frac=0.999, seed=5,
+                                           heartbeat_once=heartbeat_once)
     now = workload.S0 + 30
     e.tick(now, read=False)
     f = workload.Flap(fl, 0.01, seed=6)
@@ -377,8 +467,8 @@ def flap_leg(nodes, ticks):
             last = dict(zip(abi.COUNTERS, list(r.counters)))
     e.close()
     return {"workload": "C5 node flap under partial management (BASELINE configs[4]): %d nodes x %d pods, "
-                        "annotation selector on 50%%, 1%% of the managed nodes deleted + re-added per tick"
-                        % (nodes, nodes * workload.PODS_PER_NODE),
+                        "annotation selector on 50%%, 1%% of the managed nodes deleted + re-added per tick%s"
+                        % (nodes, nodes * workload.PODS_PER_NODE, ", KWOK_CFG_HEARTBEAT_ONCE" if heartbeat_once else ""),
             "ticks": ticks, "flapped_nodes_per_tick": f.k,
             "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
             "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
@@ -546,14 +636,18 @@ def main():
     churn = churn_ev = None
     if a.churn_ticks > 0:
         now, ch, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, rank, world,
-                                   barrier, max_over_ranks)
+                                   barrier, max_over_ranks, multi=comm is not None or gather is not None)
         if world == 1:  # the same storm through the full record form, beside it
             now, ch, churn_ev = churn_leg(e, fl, pods, now, max(2, a.churn_ticks // 2), a.churn or a.nodes_per_rank,
                                           rank, world, barrier, max_over_ranks, packed=False, ch=ch)
 
     e.close()
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
-    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup) if world == 1 and a.once_ticks else None
+    flap_once = flap_leg(a.nodes_per_rank, a.flap_ticks, True) if world == 1 and a.flap_ticks > 0 and a.once_ticks \
+        else None
+    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup, a.churn_ticks) \
+        if world == 1 and a.once_ticks else None
+    c2 = c2_leg(a.steps, a.warmup) if world == 1 and a.c2 and a.nodes_per_rank == NODES_PER_RANK else None
     emul = emulated_ranks_leg(a.nodes_per_rank, a.emulate_ranks, 20, min(a.churn_ticks, 3)) \
         if world == 1 and a.emulate_ranks > 1 and not REHEARSAL else None
 
@@ -565,19 +659,7 @@ def main():
         alg_bytes = NODE_BYTES * n_nodes + POD_BYTES * n_pods
         state_bytes = NODE_STATE_BYTES * n_nodes + POD_BYTES * n_pods
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-        traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", PMC_FILE)
-        import hashlib
-        ksha = hashlib.sha256(open(os.path.join(ROOT, "kwok_amd", "csrc", "kernels.hip"), "rb").read()).hexdigest()
-        if (os.path.exists(pmc) and a.nodes_per_rank == NODES_PER_RANK and
-                json.load(open(pmc)).get("kernels_sha256") == ksha):  # a stored figure of THIS kernel build
-            ks = json.load(open(pmc))["kernels"]
-            # the default-geometry kernel: "k_tick" (older builds) or "void k_tick<false>"
-            kt = [k for k in ks if k == "k_tick" or k.startswith("void k_tick<false>")]
-            if kt:
-                traffic = ks[kt[0]]["hbm_bytes"]
-                traffic_src = ("stored: profiles/%s, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per steady launch of this "
-                               "kernel build (kernels.hip sha256 %s), same config" % (PMC_FILE, ksha[:12]))
+        traffic, traffic_src = stored_pmc(PMC_FILE, "k_tick") if a.nodes_per_rank == NODES_PER_RANK else (None, None)
         ilc = r0.local_counters
         init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
         emit_ms = ph0["emit_kernel"]
@@ -642,7 +724,11 @@ def main():
         if flap is not None:
             out["flap"] = flap
         if hb_once is not None:
+            if flap_once is not None:
+                hb_once["flap"] = flap_once
             out["heartbeat_once"] = hb_once
+        if c2 is not None:
+            out["c2"] = c2
         if emul is not None:
             out["emulated_ranks"] = emul
         if world == 1 and a.cpu_baseline:

@@ -15,16 +15,21 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/gpurun
 timeout -k 10 400 python bench.py > $R/gpurun_out/bench_$TAG.json 2> $R/gpurun_out/bench_$TAG.err || { tail -20 $R/gpurun_out/bench_$TAG.err; exit 3; }
 cut -c1-900 $R/gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 > $R/gpurun_out/bench_${TAG}_prof.json 2>&1 || exit 4
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 50 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 --c2 0 > $R/gpurun_out/bench_${TAG}_prof.json 2>&1 || exit 4
 T=$(find $R/gpurun_out/prof_$TAG -name 'run_kernel_trace.csv' | head -n 1)
 python3 $R/tools/trace_summary.py "$T" --last 45 --out $R/gpurun_out/ktrace_$TAG.txt || exit 6
-# the heartbeat-once leg alone after a short steady leg: its ticks are the last k_tick dispatches
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_once_$TAG -o run -- python3 $R/bench.py --steps 60 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --emulate-ranks 0 > $R/gpurun_out/bench_${TAG}_once_prof.json 2>&1 || exit 8
+# the heartbeat-once steady tick alone (k_once; tools/once_probe.py: queued, then blocking ticks)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_once_$TAG -o run -- python3 $R/tools/once_probe.py 100 prof > $R/gpurun_out/bench_${TAG}_once_prof.json 2>&1 || exit 8
 T=$(find $R/gpurun_out/prof_once_$TAG -name 'run_kernel_trace.csv' | head -n 1)
-python3 $R/tools/trace_summary.py "$T" --last 50 --out $R/gpurun_out/ktrace_once_$TAG.txt || exit 9
+python3 $R/tools/trace_summary.py "$T" --last 100 --out $R/gpurun_out/ktrace_once_$TAG.txt || exit 9
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || exit 7
+  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$C -o run -- python3 $R/bench.py --steps 20 --warmup 3 --cpu-baseline 0 --roofline-ticks 0 --churn-ticks 0 --flap-ticks 0 --once-ticks 0 --emulate-ranks 0 --c2 0 > $R/gpurun_out/pmc_${TAG}_$C.log 2>&1 || exit 7
 done
 python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_${TAG}_FETCH_SIZE $R/gpurun_out/pmc_${TAG}_WRITE_SIZE $R/gpurun_out/pmc_${TAG}.json --kernels $R/kwok_amd/csrc/kernels.hip \
   --source "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace (separate passes), bench.py --steps 20 --warmup 3, 1M nodes x 10M pods, 1x MI355X"
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 200 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $R/gpurun_out/pmc_once_${TAG}_$C -o run -- python3 $R/tools/once_probe.py 30 pmc > $R/gpurun_out/pmc_once_${TAG}_$C.log 2>&1 || exit 10
+done
+python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_once_${TAG}_FETCH_SIZE $R/gpurun_out/pmc_once_${TAG}_WRITE_SIZE $R/gpurun_out/pmc_once_${TAG}.json --kernels $R/kwok_amd/csrc/kernels.hip \
+  --source "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace (separate passes), tools/once_probe.py 30 (KWOK_CFG_HEARTBEAT_ONCE steady ticks: k_once), 1M nodes x 10M pods, 1x MI355X"
 exit 0
