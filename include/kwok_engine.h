@@ -121,7 +121,7 @@ typedef struct kwok_pod_event {
     uint8_t op;        /* KWOK_OP_* */
     uint8_t phase;     /* status.phase */
     uint8_t flags;     /* KWOK_POD_* */
-    uint8_t reserved0;
+    uint8_t reserved0; /* 0; nonzero: the record's status (an int8 KWOK_E*), not applied (a failed GPU decode) */
     int32_t handle;    /* UPSERT of a new pod: -1; otherwise the handle returned at add */
     int32_t spec_id;   /* from kwok_register_pod_spec */
     int32_t node_handle; /* -1: resolve node_name */
@@ -527,6 +527,34 @@ int kwok_decode_nodes(const kwok_codec* c, char* arena, size_t arena_len, const 
                       const uint32_t* doc_len, size_t n, int threads, kwok_node_event* ev, int32_t* status);
 int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
                      const uint32_t* doc_len, size_t n, int threads, kwok_pod_doc* out, int32_t* status);
+
+/* ---- the pod codec on the GPU ("later as a GPU JSON
+ * scanner"): the same per-document decision as kwok_decode_pod, made on the
+ * engine's device by a one-pass scanner (one thread per document).  Documents
+ * the scanner leaves undecided (a status ahead of metadata / spec, a JSON
+ * escape in a compared string) are decoded by the host codec, and counted in
+ * *n_host; nothing is guessed.  Node documents stay with kwok_decode_nodes.
+ *
+ * kwok_decode_pods_gpu: the decode alone (tests, diagnostics): per document its
+ *   kwok_pod_event (op UPSERT, handle / spec_id / node_handle -1, as
+ *   kwok_decode_pod), name_ns[2i] / name_ns[2i+1] = metadata.name / namespace,
+ *   spec_key[i] = kwok_spec_key of its containers / init containers / readiness
+ *   gates (optional), status[i].  Returns the number of rejected documents.
+ * kwok_ingest_pods_json: WatchPods / ListPods from the documents themselves
+ *   (pod_controller.go:252-269, 301-343): decode on the device, then the GPU
+ *   event switch of kwok_ingest_pods over the decoded records, which never leave
+ *   the device.  op[i] / handle[i]: the caller's event (KWOK_OP_UPSERT with the
+ *   handle of a known pod or -1, KWOK_OP_DELETE with its handle); a new pod's
+ *   node by its spec.nodeName; pod specs are registered as they first appear
+ *   (kwok_register_pod_spec).  A document that fails to decode gets its decode
+ *   status in out_status and changes nothing.  Outputs as kwok_ingest_pods. */
+uint64_t kwok_spec_key(const kwok_pod_spec* spec, const char* arena, size_t arena_len);
+int kwok_decode_pods_gpu(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                         const uint64_t* doc_off, const uint32_t* doc_len, size_t n, kwok_pod_event* ev,
+                         kwok_str* name_ns, uint64_t* spec_key, int32_t* status, size_t* n_host);
+int kwok_ingest_pods_json(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                          const uint64_t* doc_off, const uint32_t* doc_len, const uint8_t* op, const int32_t* handle,
+                          size_t n, int32_t* out_handles, int32_t* out_status, uint32_t* out_released, size_t* n_host);
 
 #ifdef __cplusplus
 }

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "../../include/kwok_engine.h"
+#include "codec.h"
 #include "templates.h"
 
 namespace {
@@ -594,6 +595,50 @@ int kwok_selector_matches(const char* selector, const char* json_map, size_t len
     *out = s.set && s.matches(m) ? 1 : 0;
     return KWOK_OK;
 }
+
+}  // extern "C"
+
+// the codec's selectors for the device scanner (json.hip): KWOK_EDOMAIN when they
+// exceed its fixed tables (JSEL_REQ requirements, JSEL_VAL values, JSEL_BYTES bytes)
+int kwok::codec_export(const kwok_codec* c, kwok::JsonCfg* out) {
+    if (!c || !out) return KWOK_EINVAL;
+    memset(out, 0, sizeof *out);
+    out->manage_all = c->manage_all ? 1u : 0u;
+    uint32_t nb = 0, nv = 0;
+    auto put = [&](const std::string& t, uint16_t* off, uint16_t* len) {
+        if (nb + t.size() > (size_t)JSEL_BYTES) return false;
+        memcpy(out->bytes + nb, t.data(), t.size());
+        *off = (uint16_t)nb;
+        *len = (uint16_t)t.size();
+        nb += (uint32_t)t.size();
+        return true;
+    };
+    const Selector* src[4] = {&c->manage_ann, &c->manage_label, &c->disregard_ann, &c->disregard_label};
+    JsonSel* dst[4] = {&out->man_ann, &out->man_lab, &out->dis_ann, &out->dis_lab};
+    for (int q = 0; q < 4; q++) {
+        const Selector& S = *src[q];
+        JsonSel& D = *dst[q];
+        D.set = S.set ? 1u : 0u;
+        if (S.reqs.size() > (size_t)JSEL_REQ) return fail(KWOK_EDOMAIN, "selector: too many requirements for the device codec");
+        D.nreq = (uint32_t)S.reqs.size();
+        for (size_t r = 0; r < S.reqs.size(); r++) {
+            const Req& R = S.reqs[r];
+            D.op[r] = R.op == Req::IN ? JREQ_IN : R.op == Req::NOTIN ? JREQ_NOTIN : R.op == Req::EXISTS ? JREQ_EXISTS
+                                                                                                         : JREQ_NOTEXISTS;
+            if (!put(R.key, &D.key_off[r], &D.key_len[r])) return fail(KWOK_EDOMAIN, "selector: too long for the device codec");
+            if (nv + R.vals.size() > (size_t)JSEL_VAL) return fail(KWOK_EDOMAIN, "selector: too many values for the device codec");
+            D.val_first[r] = (uint8_t)nv;
+            D.val_n[r] = (uint8_t)R.vals.size();
+            for (auto& v : R.vals) {
+                if (!put(v, &D.val_off[nv], &D.val_len[nv])) return fail(KWOK_EDOMAIN, "selector: too long for the device codec");
+                nv++;
+            }
+        }
+    }
+    return KWOK_OK;
+}
+
+extern "C" {
 
 int kwok_decode_node(const kwok_codec* c, char* arena, size_t arena_len, size_t doc_off, size_t doc_len,
                      kwok_node_event* ev) {

@@ -258,6 +258,34 @@ struct IngSummary {
     uint32_t pad[2];
 };
 
+// ---- the watch-event codec on the GPU (json.hip) -------------------------------
+// A compiled labels.Parse selector (codec.cpp parse_selector), flattened for the
+// device: requirement r is op[r] on key bytes[key_off[r], +key_len[r]) with values
+// val_*[val_first[r], +val_n[r]).  set = 0: the nil selector.
+constexpr int JSEL_REQ = 8, JSEL_VAL = 32, JSEL_BYTES = 2048;
+enum : uint8_t { JREQ_IN = 0, JREQ_NOTIN, JREQ_EXISTS, JREQ_NOTEXISTS };
+struct JsonSel {
+    uint32_t set, nreq;
+    uint8_t op[JSEL_REQ], val_first[JSEL_REQ], val_n[JSEL_REQ], pad[JSEL_REQ];
+    uint16_t key_off[JSEL_REQ], key_len[JSEL_REQ];
+    uint16_t val_off[JSEL_VAL], val_len[JSEL_VAL];
+};
+// the codec's configuration (kwok_codec_config as compiled by kwok_codec_create)
+struct JsonCfg {
+    uint32_t manage_all, pad;
+    JsonSel man_ann, man_lab, dis_ann, dis_lab;
+    uint8_t bytes[JSEL_BYTES];  // every selector's keys and values
+};
+// per decoded pod document, beside its kwok_pod_event
+struct JsonPodSide {
+    uint32_t name_off, name_len, ns_off, ns_len;  // metadata.name / namespace (kwok_pod_doc)
+    uint64_t spec_key;    // json_spec_key of its containers / init containers / readiness gates
+    uint8_t n_cont, n_init, n_gates, pad;
+    int32_t status;       // KWOK_OK / KWOK_EDOMAIN / KWOK_EINVAL, or JSON_HOST / JSON_SPEC
+};
+constexpr int32_t JSON_HOST = 1;  // outside what the device scanner decides: the host codec decodes it
+constexpr int32_t JSON_SPEC = 2;  // decoded; its pod spec is not registered yet (the host registers it)
+
 // ---- node directory (device-authoritative, ingest.hip) -------------------------
 // A node slot's name lives on the device: node_key[slot] = fnv1a32(name) | len << 32
 // (0: no entry), node_name[slot * NAME_STRIDE ...] its bytes.  A name's bucket is

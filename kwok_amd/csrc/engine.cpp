@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/kwok_engine.h"
+#include "codec.h"
 #include "device.h"
 #include "gotemplate.h"
 #include "kernels.h"
@@ -41,6 +42,24 @@
 using namespace kwok;
 
 namespace {
+
+// FNV-1a 64 of a pod spec's strings (json.hip spec_key is the same function):
+// each container's name 0x1F image 0x1E, 0x1D, the init containers alike, 0x1D,
+// each readiness gate 0x1E
+uint64_t json_spec_key(const std::vector<Container>& cs, const std::vector<Container>& ics,
+                       const std::vector<std::string>& gates) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    auto byte = [&](uint8_t b) { h = (h ^ b) * 0x100000001B3ull; };
+    auto str = [&](const std::string& x) {
+        for (unsigned char c : x) byte(c);
+    };
+    for (auto& c : cs) str(c.name), byte(0x1F), str(c.image), byte(0x1E);
+    byte(0x1D);
+    for (auto& c : ics) str(c.name), byte(0x1F), str(c.image), byte(0x1E);
+    byte(0x1D);
+    for (auto& g : gates) str(g), byte(0x1E);
+    return h;
+}
 
 thread_local std::string g_create_err;  // kwok_last_error(NULL) after a failed create
 using clk = std::chrono::steady_clock;
@@ -200,6 +219,29 @@ struct kwok_engine {
         hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
         size_t chunk = 1048576;
     } ing;
+
+    // ---- the pod codec on the GPU (json.hip): per-document buffers, the codec's
+    // selectors, the spec table (kwok_spec_key -> spec id) ----
+    struct Json {
+        size_t cap = 0;
+        uint64_t* off = nullptr;
+        uint32_t* len = nullptr;
+        uint8_t* op = nullptr;
+        int32_t* handle = nullptr;
+        JsonPodSide* side = nullptr;
+        uint32_t* host_list = nullptr;
+        kwok_pod_event* fix_ev = nullptr;  // the listed documents' records (gathered, completed, scattered)
+        JsonPodSide* fix_side = nullptr;
+        uint32_t* n_host = nullptr;        // device [1]
+        uint32_t* n_host_h = nullptr;      // pinned [1]
+        JsonCfg* cfg = nullptr;
+        JsonCfg* cfg_h = nullptr;          // pinned staging
+        uint64_t* tab_key = nullptr;
+        int32_t* tab_id = nullptr;
+        uint32_t tab_mask = 0;
+        bool tab_dirty = true;
+    } json;
+    std::unordered_map<uint64_t, int32_t> spec_keys;  // kwok_spec_key -> spec id (-2: two specs share the key)
 
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
@@ -1018,6 +1060,15 @@ void kwok_engine_destroy(kwok_engine* e) {
         if (g.pst) (void)hipStreamDestroy(g.pst);
         if (g.dst) (void)hipStreamDestroy(g.dst);
     }
+    {
+        auto& J = e->json;
+        void* jp[] = {J.off, J.len, J.op, J.handle, J.side, J.host_list, J.fix_ev, J.fix_side, J.n_host, J.cfg,
+                      J.tab_key, J.tab_id};
+        for (void* p : jp)
+            if (p) (void)hipFree(p);
+        if (J.cfg_h) (void)hipHostFree(J.cfg_h);
+        if (J.n_host_h) (void)hipHostFree(J.n_host_h);
+    }
     if (e->h_xall) (void)hipHostFree(e->h_xall);
     if (e->pinned) (void)hipHostFree(e->pinned);
     if (e->dump_h) (void)hipHostFree(e->dump_h);
@@ -1378,9 +1429,16 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     std::vector<uint16_t> tdesc;
     const bool tabled = build_unit_tables(p, tab, tdesc);  // else: the general emitter path only
     std::string key = p.a + '\x01' + p.ka + '\x01' + p.b + '\x01' + p.kb + '\x01' + p.c + '\x01' + p.kc;
+    const uint64_t skey = json_spec_key(cs, ics, gates);  // the GPU codec finds the spec by this key
+    auto note = [&](int32_t id) {
+        auto k = e->spec_keys.emplace(skey, id);
+        if (!k.second && k.first->second != id) k.first->second = -2;  // (a 64-bit collision: the host decides)
+        if (k.second || k.first->second == -2) e->json.tab_dirty = true;
+    };
     auto it = e->spec_ids.find(key);
     if (it != e->spec_ids.end()) {
         *out_id = it->second;
+        note(it->second);
         return KWOK_OK;
     }
     uint32_t cap = e->cfg.max_pod_specs ? std::min<uint32_t>(e->cfg.max_pod_specs, 65535) : 1024;
@@ -1422,6 +1480,7 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     if ((rc = size_arena(e))) return rc;
     *out_id = (int32_t)(e->specs_h.size() - 1);
     e->spec_ids.emplace(key, *out_id);
+    note(*out_id);
     return KWOK_OK;
 }
 
@@ -1661,8 +1720,11 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
 // kwok_ingest_pods / kwok_ingest_pods_packed: recs are kwok_pod_event (with their
 // string arena) or, packed, kwok_pod_rec (no arena); statuses to out_status
 // (int32) or out_status8 (int8)
+// resident: the records (kwok_pod_event) and their arena are on the device already,
+// in the ingest buffers (kwok_ingest_pods_json decoded them there)
 int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, const char* arena, size_t arena_len,
-                     int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released) {
+                     int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released,
+                     bool resident = false) {
     const size_t RB = packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);  // record bytes
     auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
@@ -1705,7 +1767,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             return e->fail(KWOK_ENOMEM, "ingest summaries");
         G.nsums = m;
     }
-    const bool zc_ok = e->ingest_zc && K == 1;
+    const bool zc_ok = e->ingest_zc && K == 1 && !resident;
     const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
     auto chunk_batch = [&](uint32_t k) {
@@ -1726,7 +1788,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         const IngestBatch b = chunk_batch(k);
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), s));
         HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, s));
-        if (!zev)
+        if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, s));
         launch_ingest_prep(e->S, b, s);
@@ -1740,7 +1802,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k], ps));  // 0 / 2: chunk k's copy starts
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
         HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, ps));
-        if (!zev)
+        if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
         launch_ingest_prep(e->S, b, ps);
@@ -1790,7 +1852,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
         HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
-        if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
+        if (arena_len && !zar && !resident) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
         HIPCHK(e, hipMemsetAsync(G.abort, 0, 4, st));
         for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
             if (int r = prep(k)) return r;
@@ -1874,6 +1936,256 @@ int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, 
                             uint32_t* out_released) {
     if (!e || (n && !recs) || n > 0x7FFFFFF0ull) return KWOK_EINVAL;
     return ingest_pods_impl(e, recs, true, n, nullptr, 0, out_handles, nullptr, out_status, out_released);
+}
+
+// ---- the pod codec on the GPU (json.hip) ------------------------------------
+namespace {
+int json_reserve(kwok_engine* e, size_t n) {
+    auto& J = e->json;
+    if (!J.cfg) {
+        int rc = 0;
+        if ((rc = dalloc(e, &J.cfg, 1)) || (rc = dalloc(e, &J.n_host, 1))) return rc;
+        if (hipHostMalloc((void**)&J.cfg_h, sizeof(JsonCfg), hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&J.n_host_h, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            return e->fail(KWOK_ENOMEM, "GPU codec staging");
+    }
+    if (n > J.cap) {
+        void* ptrs[] = {J.off, J.len, J.op, J.handle, J.side, J.host_list, J.fix_ev, J.fix_side};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        J.off = nullptr, J.len = nullptr, J.op = nullptr, J.handle = nullptr, J.side = nullptr;
+        J.host_list = nullptr, J.fix_ev = nullptr, J.fix_side = nullptr;
+        J.cap = 0;
+        const size_t cap = std::max<size_t>(n + n / 4, 4096);
+        int rc = 0;
+        if ((rc = dalloc(e, &J.off, cap)) || (rc = dalloc(e, &J.len, cap)) || (rc = dalloc(e, &J.op, cap)) ||
+            (rc = dalloc(e, &J.handle, cap)) || (rc = dalloc(e, &J.side, cap)) || (rc = dalloc(e, &J.host_list, cap)) ||
+            (rc = dalloc(e, &J.fix_ev, cap)) || (rc = dalloc(e, &J.fix_side, cap)))
+            return rc;
+        J.cap = cap;
+    }
+    if (J.tab_dirty) {  // the spec table: open addressing at <= 50% load, rebuilt from spec_keys
+        uint32_t slots = 1024;
+        while (slots < 2 * e->spec_keys.size() + 2) slots <<= 1;
+        if (slots - 1 != J.tab_mask || !J.tab_key) {
+            if (J.tab_key) (void)hipFree(J.tab_key);
+            if (J.tab_id) (void)hipFree(J.tab_id);
+            J.tab_key = nullptr, J.tab_id = nullptr;
+            int rc = 0;
+            if ((rc = dalloc(e, &J.tab_key, slots)) || (rc = dalloc(e, &J.tab_id, slots))) return rc;
+            J.tab_mask = slots - 1;
+        }
+        std::vector<uint64_t> key(slots, 0);
+        std::vector<int32_t> id(slots, -1);
+        for (auto& kv : e->spec_keys) {
+            uint64_t k = kv.first ? kv.first : 1;  // (0 marks an empty slot: key 0 is never found)
+            if (!kv.first) continue;
+            uint32_t h = (uint32_t)k & J.tab_mask;
+            while (key[h]) h = (h + 1) & J.tab_mask;
+            key[h] = k;
+            id[h] = kv.second;
+        }
+        HIPCHK(e, hipMemcpyAsync(J.tab_key, key.data(), slots * 8, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipMemcpyAsync(J.tab_id, id.data(), slots * 4, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+        J.tab_dirty = false;
+    }
+    return KWOK_OK;
+}
+
+// decode documents [0, n) on the device: the arena and the spans go to the ingest
+// buffers, k_json_pods writes the records there (ingest form when op != null);
+// returns the number of documents listed for the host (JSON_HOST / JSON_SPEC)
+int json_decode(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len, const uint64_t* doc_off,
+                const uint32_t* doc_len, size_t n, const uint8_t* op, const int32_t* handle, uint32_t* n_host) {
+    auto& G = e->ing;
+    auto& J = e->json;
+    hipStream_t st = e->st;
+    int rc = ingest_reserve(e, n, arena_len + 16);  // (the scanner reads whole 16-byte windows)
+    if (rc) return rc;
+    if ((rc = json_reserve(e, n))) return rc;
+    if ((rc = codec_export(c, J.cfg_h))) return e->fail(rc, "%s", kwok_codec_last_error());
+    HIPCHK(e, hipMemcpyAsync(J.cfg, J.cfg_h, sizeof(JsonCfg), hipMemcpyHostToDevice, st));
+    if (arena_len) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(J.off, doc_off, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(J.len, doc_len, n * 4, hipMemcpyHostToDevice, st));
+    if (op) {
+        HIPCHK(e, hipMemcpyAsync(J.op, op, n, hipMemcpyHostToDevice, st));
+        HIPCHK(e, hipMemcpyAsync(J.handle, handle, n * 4, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(e, hipMemsetAsync(J.n_host, 0, 4, st));
+    JsonPodArgs A{};
+    A.arena = G.d_arena;
+    A.arena_len = arena_len;
+    A.doc_off = J.off;
+    A.doc_len = J.len;
+    A.n = (uint32_t)n;
+    A.tab_mask = J.tab_mask;
+    A.cfg = J.cfg;
+    A.op = op ? J.op : nullptr;
+    A.handle = op ? J.handle : nullptr;
+    A.tab_key = J.tab_key;
+    A.tab_id = J.tab_id;
+    A.ev = static_cast<kwok_pod_event*>(G.d_ev);
+    A.side = J.side;
+    A.host_list = J.host_list;
+    A.n_host = J.n_host;
+    launch_json_pods(A, st);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemcpyAsync(J.n_host_h, J.n_host, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    *n_host = *J.n_host_h;
+    return KWOK_OK;
+}
+
+// the documents the scanner listed: decoded by the host codec (JSON_HOST), or their
+// spec registered (JSON_SPEC: one host decode per new spec key); their records
+// completed and written back.  ingest: the records take the caller's op / handle
+// and a spec id (kwok_ingest_pods_json); else they stay as the codec writes them
+// (names / spec keys back in names_ns / spec_key of the caller, indexed by document).
+int json_complete(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len, const uint64_t* doc_off,
+                  const uint32_t* doc_len, uint32_t nh, const uint8_t* op, const int32_t* handle,
+                  std::vector<JsonPodSide>* sides_out, std::vector<uint32_t>* list_out) {
+    auto& G = e->ing;
+    auto& J = e->json;
+    hipStream_t st = e->st;
+    if (!nh) return KWOK_OK;
+    std::vector<uint32_t> list(nh);
+    std::vector<kwok_pod_event> ev(nh);
+    std::vector<JsonPodSide> side(nh);
+    launch_json_gather(static_cast<const kwok_pod_event*>(G.d_ev), J.side, J.host_list, nh, J.fix_ev, J.fix_side, st);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipMemcpyAsync(list.data(), J.host_list, (size_t)nh * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipMemcpyAsync(ev.data(), J.fix_ev, (size_t)nh * sizeof(kwok_pod_event), hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipMemcpyAsync(side.data(), J.fix_side, (size_t)nh * sizeof(JsonPodSide), hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    std::unordered_map<uint64_t, int32_t> fresh;  // spec keys registered here (JSON_SPEC)
+    char* ar = const_cast<char*>(arena);  // (kwok_decode_pod writes only node blobs)
+    kwok_pod_doc d;
+    for (uint32_t q = 0; q < nh; q++) {
+        const uint32_t i = list[q];
+        JsonPodSide& s = side[q];
+        const bool ups = !op || op[i] == KWOK_OP_UPSERT;
+        if (s.status == JSON_SPEC) {
+            auto f = fresh.find(s.spec_key);
+            if (f != fresh.end()) {
+                ev[q].spec_id = f->second;
+                ev[q].reserved0 = 0;
+                s.status = KWOK_OK;
+                continue;
+            }
+        }
+        // the host codec decides this document (a new spec: one decode registers it)
+        int rc = kwok_decode_pod(c, ar, arena_len, doc_off[i], doc_len[i], &d);
+        kwok_pod_event x = rc == KWOK_OK ? d.ev : kwok_pod_event{};
+        int32_t id = -1;
+        if (rc == KWOK_OK) {
+            kwok_pod_spec sp{d.containers, d.n_containers, d.init_containers, d.n_init_containers,
+                             d.readiness_gates, d.n_readiness_gates};
+            s.name_off = d.name.off, s.name_len = d.name.len, s.ns_off = d.namespace_.off, s.ns_len = d.namespace_.len;
+            s.n_cont = (uint8_t)d.n_containers, s.n_init = (uint8_t)d.n_init_containers;
+            s.n_gates = (uint8_t)d.n_readiness_gates;
+            s.spec_key = kwok_spec_key(&sp, arena, arena_len);
+            if (op && ups) {
+                const int r2 = kwok_register_pod_spec(e, &sp, arena, arena_len, &id);
+                if (r2 == KWOK_OK) fresh[s.spec_key] = id;
+                else if (r2 == KWOK_EDOMAIN || r2 == KWOK_EFULL) rc = r2;  // the spec is outside the domain
+                else return r2;
+            }
+        }
+        if (op) {
+            x.op = op[i];
+            x.handle = handle[i];
+            x.spec_id = ups ? id : -1;
+            x.node_handle = -1;
+            x.reserved0 = rc == KWOK_OK ? 0 : (uint8_t)(int8_t)rc;
+        } else if (rc != KWOK_OK) {
+            x = kwok_pod_event{};
+        }
+        ev[q] = x;
+        s.status = rc;
+    }
+    HIPCHK(e, hipMemcpyAsync(J.fix_ev, ev.data(), (size_t)nh * sizeof(kwok_pod_event), hipMemcpyHostToDevice, st));
+    launch_json_scatter(static_cast<kwok_pod_event*>(G.d_ev), J.fix_ev, J.host_list, nh, st);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(st));
+    if (sides_out) *sides_out = std::move(side);
+    if (list_out) *list_out = std::move(list);
+    return KWOK_OK;
+}
+}  // namespace
+
+uint64_t kwok_spec_key(const kwok_pod_spec* spec, const char* arena, size_t arena_len) {
+    if (!spec) return 0;
+    auto str = [&](kwok_str s) {
+        return (size_t)s.off + s.len <= arena_len ? std::string(arena + s.off, s.len) : std::string();
+    };
+    std::vector<Container> cs(spec->n_containers), ics(spec->n_init_containers);
+    std::vector<std::string> gates(spec->n_readiness_gates);
+    for (uint32_t i = 0; i < spec->n_containers; i++) cs[i] = {str(spec->containers[i].name), str(spec->containers[i].image)};
+    for (uint32_t i = 0; i < spec->n_init_containers; i++)
+        ics[i] = {str(spec->init_containers[i].name), str(spec->init_containers[i].image)};
+    for (uint32_t i = 0; i < spec->n_readiness_gates; i++) gates[i] = str(spec->readiness_gates[i]);
+    return json_spec_key(cs, ics, gates);
+}
+
+int kwok_decode_pods_gpu(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                         const uint64_t* doc_off, const uint32_t* doc_len, size_t n, kwok_pod_event* ev,
+                         kwok_str* name_ns, uint64_t* spec_key, int32_t* status, size_t* n_host) {
+    if (!e || !c || (n && (!doc_off || !doc_len || !ev || !status)) || (arena_len && !arena) || n > 0x7FFFFFF0ull)
+        return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    if (n_host) *n_host = 0;
+    if (!n) return 0;
+    uint32_t nh = 0;
+    int rc = json_decode(e, c, arena, arena_len, doc_off, doc_len, n, nullptr, nullptr, &nh);
+    if (rc) return rc;
+    std::vector<JsonPodSide> hs;
+    std::vector<uint32_t> hl;
+    if ((rc = json_complete(e, c, arena, arena_len, doc_off, doc_len, nh, nullptr, nullptr, &hs, &hl))) return rc;
+    std::vector<JsonPodSide> side(n);
+    HIPCHK(e, hipMemcpyAsync(ev, e->ing.d_ev, n * sizeof(kwok_pod_event), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(side.data(), e->json.side, n * sizeof(JsonPodSide), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    for (size_t q = 0; q < hl.size(); q++) side[hl[q]] = hs[q];  // the host-decided documents
+    int bad = 0;
+    for (size_t i = 0; i < n; i++) {
+        status[i] = side[i].status;
+        bad += side[i].status != KWOK_OK;
+        if (name_ns) {
+            name_ns[2 * i] = kwok_str{side[i].name_off, side[i].name_len};
+            name_ns[2 * i + 1] = kwok_str{side[i].ns_off, side[i].ns_len};
+        }
+        if (spec_key) spec_key[i] = side[i].spec_key;
+    }
+    if (n_host) *n_host = nh;
+    return bad;
+}
+
+int kwok_ingest_pods_json(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                          const uint64_t* doc_off, const uint32_t* doc_len, const uint8_t* op, const int32_t* handle,
+                          size_t n, int32_t* out_handles, int32_t* out_status, uint32_t* out_released, size_t* n_host) {
+    if (!e || !c || (n && (!doc_off || !doc_len || !op || !handle)) || (arena_len && !arena) || n > 0x7FFFFFF0ull)
+        return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    if (n_host) *n_host = 0;
+    if (!n) return 0;
+    const auto t0 = clk::now();
+    uint32_t nh = 0;
+    int rc = json_decode(e, c, arena, arena_len, doc_off, doc_len, n, op, handle, &nh);
+    if (rc) return rc;
+    if ((rc = json_complete(e, c, arena, arena_len, doc_off, doc_len, nh, op, handle, nullptr, nullptr))) return rc;
+    if (n_host) *n_host = nh;
+    if (e->iprof)
+        fprintf(stderr, "[kwok json] %zu pod documents decoded on the GPU (%u by the host): %.2f ms\n", n, nh,
+                ms_between(t0, clk::now()));
+    // the event switch over the decoded records, which stayed on the device
+    return ingest_pods_impl(e, e->ing.d_ev, false, n, nullptr, arena_len, out_handles, out_status, nullptr, out_released,
+                            true);
 }
 
 int kwok_pack_pod_events(const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len, kwok_pod_rec* out,

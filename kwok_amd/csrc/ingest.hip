@@ -196,7 +196,9 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
     r.pad[0] = r.pad[1] = r.pad[2] = r.pad[3] = 0;
     int st = 1;  // 1: the apply pass decides
     auto in_arena = [&](kwok_str s) { return (uint64_t)s.off + s.len <= I.arena_len; };
-    if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
+    if (x.reserved0) {
+        st = (int8_t)x.reserved0;  // a record the GPU codec could not decode (kwok_ingest_pods_json)
+    } else if (!in_arena(x.node_name) || !in_arena(x.host_ip) || !in_arena(x.pod_ip)) {
         st = KWOK_EDOMAIN;
     } else {
         if (x.op == KWOK_OP_DELETE) {

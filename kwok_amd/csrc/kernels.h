@@ -205,6 +205,29 @@ int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_
 // the WatchPods / ListPods event switch, per bucket in event order (one wave per bucket)
 void launch_ingest_apply(const DevState& S, const IngestBatch& I, hipStream_t st);
 
+// ---- the watch-event codec on the GPU (json.hip): one thread per pod document ----
+struct JsonPodArgs {
+    const uint8_t* arena;        // the documents (16-aligned, 16 bytes of padding past arena_len)
+    uint64_t arena_len;
+    const uint64_t* doc_off;
+    const uint32_t* doc_len;
+    uint32_t n;
+    uint32_t tab_mask;           // the spec table (kwok_register_pod_spec): open addressing, mask + 1 slots
+    const JsonCfg* cfg;
+    const uint8_t* op;           // ingest form (null: decode only): the caller's op and handle per document,
+    const int32_t* handle;       //   the spec id from the table, a failed decode's status in reserved0
+    const uint64_t* tab_key;     // json_spec_key (0: empty slot)
+    const int32_t* tab_id;
+    kwok_pod_event* ev;          // [n] out
+    JsonPodSide* side;           // [n] out
+    uint32_t* host_list;         // [n] out: documents the host completes (JSON_HOST / JSON_SPEC)
+    uint32_t* n_host;            // [1] (zeroed by the caller)
+};
+void launch_json_pods(const JsonPodArgs& A, hipStream_t st);
+void launch_json_gather(const kwok_pod_event* ev, const JsonPodSide* side, const uint32_t* list, uint32_t n,
+                        kwok_pod_event* out_ev, JsonPodSide* out_side, hipStream_t st);
+void launch_json_scatter(kwok_pod_event* ev, const kwok_pod_event* in, const uint32_t* list, uint32_t n, hipStream_t st);
+
 // ---- node batches on the GPU (kwok_ingest_nodes, node_controller.go:256-270) ----
 struct NodeBatch {
     const kwok_node_event* ev;  // [n] on the device or read in place

@@ -2450,7 +2450,9 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
 #define OSTAMP(k) \
     if (stamp) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime()
     OSTAMP(0);
-    if ((phases & TICK_PROF) && t == 0)
+    // profiled ticks: the earliest start, from the first block of each XCD (512 adds to one
+    // word would serialise ~6 us into the kernel)
+    if ((phases & TICK_PROF) && t == 0 && b < 8u)
         atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
     const uint32_t bk = b * ONCE_WAVES + w;
     uint32_t hb = 0, lock = 0, mng = 0, rdy = 0, ev = 0, tot = 0, pnd = 0, run = 0, rare = 0;

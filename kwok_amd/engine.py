@@ -102,6 +102,10 @@ def declare(lib, pre):
             "decode_pod": (C.c_int, [VP, VP, SZ, SZ, SZ, P(abi.PodDoc)]),
             "decode_nodes": (C.c_int, [VP, VP, SZ, VP, VP, SZ, C.c_int, VP, VP]),
             "decode_pods": (C.c_int, [VP, VP, SZ, VP, VP, SZ, C.c_int, VP, VP]),
+            "engine_stats": (C.c_int, [VP, VP]),
+            "spec_key": (U64, [P(abi.PodSpec), C.c_char_p, SZ]),
+            "decode_pods_gpu": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, SZ, VP, VP, VP, VP, P(SZ)]),
+            "ingest_pods_json": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, VP, VP, SZ, VP, VP, VP, P(SZ)]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name, None)
@@ -432,6 +436,64 @@ class Engine(EngineBase):
         self._check(self._lib.kwok_profile_host(self._h, 1 if reset else 0, ms, C.byref(n)), "profile_host")
         return dict(zip(self.HOST, list(ms))), n.value
 
+    # ---- the pod codec on the GPU (kwok_decode_pods_gpu / kwok_ingest_pods_json) ----
+    @staticmethod
+    def _docs(docs):
+        """concatenated documents (bytes or JSON-able values) -> (arena, offsets, lengths)"""
+        import json as _json
+        raws = [d if isinstance(d, (bytes, bytearray)) else _json.dumps(d).encode() for d in docs]
+        lens = np.fromiter((len(r) for r in raws), np.uint32, len(raws))
+        offs = np.zeros(len(raws), np.uint64)
+        if len(raws):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return b"".join(raws), offs, lens
+
+    def decode_pods_gpu(self, codec, docs=None, arena=None, offs=None, lens=None):
+        """kwok_decode_pods_gpu: per document its kwok_pod_event (POD_EVENT_DTYPE),
+        (name, namespace) spans, spec key and status, and the number the host decided.
+        Documents as a list, or as (arena, offs, lens)."""
+        if docs is not None:
+            arena, offs, lens = self._docs(docs)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n = len(offs)
+        ev = np.zeros(n, abi.POD_EVENT_DTYPE)
+        names = np.zeros((n, 2, 2), np.uint32)
+        keys = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.int32)
+        nh = C.c_size_t()
+        ar, alen = self._arena_arg(arena)
+        rc = self._lib.kwok_decode_pods_gpu(self._h, codec._h, ar, alen, offs.ctypes.data, lens.ctypes.data, n,
+                                            ev.ctypes.data, names.ctypes.data, keys.ctypes.data, st.ctypes.data,
+                                            C.byref(nh))
+        self._check(rc, "decode_pods_gpu")
+        return ev, names, keys, st, nh.value
+
+    def ingest_pods_json(self, codec, arena, offs, lens, ops, handles, out=None):
+        """kwok_ingest_pods_json: (handles, statuses, released, documents the host decided)"""
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        ops = np.ascontiguousarray(ops, np.uint8)
+        handles = np.ascontiguousarray(handles, np.int32)
+        n = len(offs)
+        if out is None:
+            hs, st, rel = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint32)
+        else:
+            hs, st, rel = (o[:n] for o in out)
+        nh = C.c_size_t()
+        ar, alen = self._arena_arg(arena)
+        rc = self._lib.kwok_ingest_pods_json(self._h, codec._h, ar, alen, offs.ctypes.data, lens.ctypes.data,
+                                             ops.ctypes.data, handles.ctypes.data, n, hs.ctypes.data, st.ctypes.data,
+                                             rel.ctypes.data, C.byref(nh))
+        self._check(rc, "ingest_pods_json")
+        return hs, st, rel, nh.value
+
+    @staticmethod
+    def _arena_arg(arena):
+        if isinstance(arena, np.ndarray):
+            return C.cast(arena.ctypes.data, C.c_char_p), arena.nbytes
+        return (arena or b"\0"), len(arena or b"")
+
     STATS = ("ticks_full", "ticks_once", "once_redo")  # KWOK_STAT_* order
 
     def stats(self):
@@ -468,6 +530,19 @@ def comm_id() -> bytes:
     if rc != 0:
         raise KwokError(rc, "comm_id")
     return b.raw
+
+
+def spec_key(containers, init_containers=(), gates=()) -> int:
+    """kwok_spec_key: the key the GPU codec finds a registered pod spec by"""
+    lib = load_engine_lib()
+    ar = abi.Arena()
+    cs = (abi.Container * max(1, len(containers)))(*[abi.Container(ar.ref(n), ar.ref(i)) for n, i in containers])
+    ics = (abi.Container * max(1, len(init_containers)))(*[abi.Container(ar.ref(n), ar.ref(i))
+                                                            for n, i in init_containers])
+    gs = (abi.KwokStr * max(1, len(gates)))(*[ar.ref(g) for g in gates])
+    sp = abi.PodSpec(cs, len(containers), ics, len(init_containers), gs, len(gates))
+    buf = bytes(ar.buf) or b"\0"
+    return int(lib.kwok_spec_key(C.byref(sp), buf, len(ar.buf)))
 
 
 def finalizer_patch() -> bytes:

@@ -317,3 +317,182 @@ class Flap:
         evp = mk((len(ev),), abi.NODE_EVENT_DTYPE)
         evp[:] = ev
         return evp, ar
+
+
+# ---- the C4 storm as the documents a watch carries (kwok_ingest_pods_json) ----
+def rfc3339_rows(t: np.ndarray) -> np.ndarray:
+    """RFC3339 UTC strings of unix seconds as a (n, 20) uint8 array"""
+    import time as _time
+    t = np.asarray(t, np.int64)
+    u, inv = np.unique(t, return_inverse=True)
+    rows = np.frombuffer(b"".join(_time.strftime("%Y-%m-%dT%H:%M:%SZ", _time.gmtime(int(x))).encode() for x in u),
+                         np.uint8).reshape(len(u), 20)
+    return rows[inv.reshape(-1)]
+
+
+def _digits(v: np.ndarray, width: int) -> np.ndarray:
+    v = np.asarray(v, np.int64)
+    out = np.empty((v.shape[0], width), np.uint8)
+    for k in range(width):
+        out[:, width - 1 - k] = ord("0") + (v // 10 ** k) % 10
+    return out
+
+
+class DocTemplate:
+    """A JSON document with fixed-width slots, filled for many documents at
+    once (numpy): `text` with slot markers {name} of the slot's width in
+    placeholder bytes '@'.  Variable-length strings go in a slot followed by
+    spaces (whitespace between tokens), e.g. an IP `"10.0.0.5"` in a 17-byte
+    slot."""
+
+    def __init__(self, text: str, widths: dict):
+        import re
+        parts = re.split(r"\{(\w+)\}", text)
+        buf, self.slots = bytearray(), {}
+        for i, p in enumerate(parts):
+            if i % 2:
+                self.slots.setdefault(p, []).append((len(buf), widths[p]))
+                buf += b"@" * widths[p]
+            else:
+                buf += p.encode()
+        self.tpl = np.frombuffer(bytes(buf), np.uint8)
+
+    def fill(self, n: int, values: dict, out=None, static=True) -> np.ndarray:
+        """n documents into out ((n, len) uint8, allocated if None); static=False:
+        only the slots are written (out already holds the template)"""
+        if out is None:
+            out = np.empty((n, self.tpl.size), np.uint8)
+        if static:
+            out[...] = self.tpl[None, :]
+        for name, where in self.slots.items():
+            v = values[name]
+            for off, w in where:
+                out[:, off:off + w] = v if v.ndim == 2 else v[None, :]
+        return out
+
+
+def quoted_ips(ips: np.ndarray, width: int = 17) -> np.ndarray:
+    """`"a.b.c.d"` + spaces, (n, width) uint8 (net.IP.String() of each address)"""
+    buf, off, ln = ip_strings(ips)
+    n = len(ips)
+    out = np.full((n, width), ord(" "), np.uint8)
+    out[:, 0] = ord('"')
+    for k in range(15):
+        m = k < ln
+        out[m, 1 + k] = buf[off[m] + k]
+    out[np.arange(n), 1 + ln] = ord('"')
+    return out
+
+
+_META = ('{"metadata":{"name":"{name}","namespace":"default","uid":"{uid}","resourceVersion":"{rv}",'
+         '"creationTimestamp":"{ct}",')
+_SPEC = ('"spec":{"containers":[{"name":"fake-pod","image":"fake","resources":{},'
+         '"terminationMessagePath":"/dev/termination-log","terminationMessagePolicy":"File",'
+         '"imagePullPolicy":"Always"}],"restartPolicy":"Always","terminationGracePeriodSeconds":30,'
+         '"dnsPolicy":"ClusterFirst","serviceAccountName":"default","serviceAccount":"default","nodeName":"{node}",'
+         '"securityContext":{},"schedulerName":"default-scheduler","tolerations":[{"key":"node.kubernetes.io/not-ready",'
+         '"operator":"Exists","effect":"NoExecute","tolerationSeconds":300},{"key":"node.kubernetes.io/unreachable",'
+         '"operator":"Exists","effect":"NoExecute","tolerationSeconds":300}],"priority":0,"enableServiceLinks":true,'
+         '"preemptionPolicy":"PreemptLowerPriority"},')
+_COND = '{"type":"%s","status":"True","lastProbeTime":null,"lastTransitionTime":"{ct}"}'
+# a Running pod kwok patched (pod.status.tpl's fields as the apiserver stores them), now marked for deletion
+DELETING_DOC = DocTemplate(
+    _META + '"deletionTimestamp":"{dt}","deletionGracePeriodSeconds":0,"labels":{"app":"fake"},"finalizers":{fin}},'
+    + _SPEC + '"status":{"phase":"Running","conditions":[' + ",".join(_COND % t for t in (
+        "Initialized", "Ready", "ContainersReady")).replace("{ct}", "{ct2}") +
+    '],"hostIP":{hip},"podIP":{pip},"podIPs":[{"ip":{pip}}],"startTime":"{ct3}","containerStatuses":[{"name":'
+    '"fake-pod","state":{"running":{"startedAt":"{ct4}"}},"lastState":{},"ready":true,"restartCount":0,'
+    '"image":"fake","imageID":""}],"qosClass":"BestEffort"}}',
+    dict(name=12, uid=36, rv=8, ct=20, ct2=20, ct3=20, ct4=20, dt=20, fin=22, node=12, hip=17, pip=17))
+# a new Pending pod, scheduled (spec.nodeName) and defaulted by the apiserver
+PENDING_DOC = DocTemplate(_META + '"labels":{"app":"fake"}},' + _SPEC +
+                          '"status":{"phase":"Pending","qosClass":"BestEffort"}}',
+                          dict(name=12, uid=36, rv=8, ct=20, node=12))
+
+
+class ChurnJson(Churn):
+    """Churn's storm as Kubernetes documents (kwok_ingest_pods_json): the
+    deletion-marked pods as the Running objects kwok patched (full status,
+    deletionTimestamp, half with a finalizer), the creates as scheduled Pending
+    pods, ~1.6 KB / ~1.1 KB each.  node_name_of[handle]: the (12,) name bytes
+    of each node handle (the fleet's names)."""
+
+    def __init__(self, *a, node_name_of=None, **kw):
+        super().__init__(*a, **kw)
+        self.node_name_of = node_name_of
+        self.serial = 0
+
+    def names(self, n):
+        s = np.arange(self.serial, self.serial + n, dtype=np.int64)
+        self.serial += n
+        name = np.empty((n, 12), np.uint8)
+        name[:, :4] = np.frombuffer(b"pod-", np.uint8)
+        name[:, 4:] = _digits(s, 8)
+        uid = np.broadcast_to(np.frombuffer(b"0b7f2c2e-0000-4000-8000-", np.uint8), (n, 24))
+        return name, np.concatenate([uid, _digits(s, 12)], axis=1), _digits(s % 10 ** 8, 8)
+
+    def batch_json(self, dump, now):
+        D = min(self.n, self.live.shape[0])
+        dead = self.live[:D]
+        loc = dead - self.first
+        used, phase, _, pip = dump()
+        assert used[loc].all() and (phase[loc] == abi.PHASE_RUNNING).all(), "churn: live Running pods"
+        nm, uid, rv = self.names(D)
+        ct = rfc3339_rows(self.ctime[loc])
+        fin = self.rng.random(D) < 0.5
+        finb = np.full((D, 22), ord(" "), np.uint8)
+        finb[:, :2] = np.frombuffer(b"[]", np.uint8)
+        finb[fin] = np.frombuffer(b'["kwok.x-k8s.io/fake"]', np.uint8)
+        ips = quoted_ips(pip[loc])
+        # the documents live in one buffer (self.alloc'ed: page-locked), the templates written once;
+        # every batch rewrites the slots only
+        Ld, Lc = DELETING_DOC.tpl.size, PENDING_DOC.tpl.size
+        static = getattr(self, "jbuf", None) is None or self.jbuf.size < D * (Ld + Lc) or self.jD != D
+        if static:
+            mk = self.alloc or (lambda shape, dt: np.empty(shape, dt))
+            self.jbuf = mk((D * (Ld + Lc),), np.uint8)
+            self.jD = D
+        d = self.jbuf[:D * Ld].reshape(D, Ld)
+        c = self.jbuf[D * Ld:D * (Ld + Lc)].reshape(D, Lc)
+        DELETING_DOC.fill(D, dict(name=nm, uid=uid, rv=rv, ct=ct, ct2=ct, ct3=ct, ct4=ct,
+                                  dt=rfc3339_rows(np.full(1, now))[0], fin=finb,
+                                  node=self.node_name_of[self.node_of[loc]],
+                                  hip=quoted_ips(np.array([abi.ip4(self.node_ip.decode())], np.uint32))[0],
+                                  pip=ips), out=d, static=static)
+        nodes = self.rng.permutation(self.node_of[loc])
+        nm2, uid2, rv2 = self.names(D)
+        PENDING_DOC.fill(D, dict(name=nm2, uid=uid2, rv=rv2, ct=rfc3339_rows(np.full(1, now - 5))[0],
+                                 node=self.node_name_of[nodes]), out=c, static=static)
+        arena = self.jbuf[:D * (Ld + Lc)]
+        lens = np.concatenate([np.full(D, Ld, np.uint32), np.full(D, Lc, np.uint32)])
+        offs = np.zeros(2 * D, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        ops = np.full(2 * D, abi.OP_UPSERT, np.uint8)
+        handles = np.concatenate([dead, np.full(D, -1, np.int32)]).astype(np.int32)
+        self._pending = (D, nodes.copy(), now - 5)
+        return arena, offs, lens, ops, handles
+
+
+def node_names_by_handle(fl) -> np.ndarray:
+    """(max handle + 1, 12) name bytes of the fleet's node handles"""
+    out = np.zeros((int(fl.node_handles.max()) + 1, 12), np.uint8)
+    out[fl.node_handles] = fl.names
+    return out
+
+
+def host_decode_arrays(codec, arena, offs, lens, threads=8):
+    """kwok_decode_pods (the host codec) over documents already in one arena:
+    {"ev": POD_EVENT_DTYPE, "names": (n, 2, 2) u32, "status": i32}"""
+    import ctypes as C
+    n = len(offs)
+    rec = np.zeros(n * C.sizeof(abi.PodDoc), np.uint8)
+    st = np.zeros(n, np.int32)
+    a = np.ascontiguousarray(arena, np.uint8)
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint32)
+    codec._lib.kwok_decode_pods(codec._h, a.ctypes.data, a.nbytes, o.ctypes.data, ln.ctypes.data, n, threads,
+                                rec.ctypes.data, st.ctypes.data)
+    r = rec.reshape(n, C.sizeof(abi.PodDoc))
+    ev = np.ascontiguousarray(r[:, :48]).view(abi.POD_EVENT_DTYPE).reshape(n)
+    names = np.ascontiguousarray(r[:, 48:64]).view(np.uint32).reshape(n, 2, 2)
+    return {"ev": ev, "names": names, "status": st}

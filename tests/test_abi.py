@@ -47,6 +47,7 @@ def test_oracle_library_exports():
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
                  "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
                  "kwok_engine_stats",  # engine only: which tick kernel ran
+                 "kwok_spec_key", "kwok_decode_pods_gpu", "kwok_ingest_pods_json",  # the GPU codec (engine library)
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
                  "kwok_decode_node", "kwok_decode_pod", "kwok_decode_nodes", "kwok_decode_pods",  # host codec: feeds both, lives in the engine library
                  "kwok_template_render", "kwok_template_last_error", "kwok_pod_template_patch",
