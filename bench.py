@@ -91,6 +91,7 @@ def parse():
     ap.add_argument("--flap-ticks", type=int, default=5, help="C5 flap ticks on a partially managed fleet (N=1; 0: skip)")
     ap.add_argument("--once-ticks", type=int, default=1, help="the KWOK_CFG_HEARTBEAT_ONCE legs (N=1; 0: skip)")
     ap.add_argument("--c2", type=int, default=1, help="BASELINE configs[1] at 100k x 1M (N=1; 0: skip)")
+    ap.add_argument("--json-ticks", type=int, default=2, help="C4 from JSON documents, GPU codec (N=1; 0: skip)")
     ap.add_argument("--churn", type=int, default=0, help="pods churned per tick (0: nodes_per_rank, i.e. 1M at the "
                                                          "metric size: 2M create/delete per tick)")
     ap.add_argument("--emulate-ranks", type=int, default=8, help="N=1: a one-rank RCCL engine folding this many "
@@ -297,7 +298,7 @@ def stored_pmc(name, kernel):
                                               % (name, ks[0], ksha[:12]))
 
 
-def heartbeat_once_leg(nodes, steps, warmup, churn_ticks):
+def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     """The drop-in's engine: KWOK_CFG_HEARTBEAT_ONCE (engine_cgo.go), on the
     metric's fleet.  The tick materialises ONE heartbeat body (every node's
     patch is that body, node_controller.go:393-401) and the handle list, for
@@ -321,9 +322,11 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks):
     ph, nt = e.profile_read()
     e.profile_enable(False)
     stats = e.stats()
-    churn = None
+    churn = cjson = None
     if churn_ticks:
-        now, _, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
+        now, ch, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
+        if json_ticks:
+            now, _, cjson = churn_json_leg(e, fl, ch, now, json_ticks, nodes)
     e.close()
     lc = r.local_counters
     state_bytes = NODE_STATE_BYTES * lc[8] + POD_BYTES * lc[10]
@@ -360,7 +363,63 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks):
                                                if ph0["emit_kernel"] else None}},
             "churn": None if churn is None else {k: churn[k] for k in (
                 "workload", "ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "emission_ms", "value",
-                "unit", "tick_transitions_per_s")}}
+                "unit", "tick_transitions_per_s")},
+            "churn_json": cjson}
+
+
+def churn_json_leg(e, fl, ch, now, ticks, n_churn):
+    """C4 from the documents themselves: per tick the 2 x n_churn pod documents
+    a watch carries (workload.ChurnJson: the deletion-marked Running pods as
+    kwok patched them, ~1.6 KB, and the scheduled Pending creates, ~1.1 KB),
+    decoded on the GPU and routed there (kwok_ingest_pods_json), then the tick.
+    Beside it: the host codec (kwok_decode_pods, all host threads) on one such
+    batch - the drop-in's other path from the same documents."""
+    from kwok_amd.codec import Codec
+    codec = Codec(manage_all_nodes=True)
+    ch = workload.ChurnJson.from_churn(ch, workload.node_names_by_handle(fl), alloc=keng.host_array)  # (its live pods)
+    dump = lambda: e.dump_pods(0, workload.BUCKETS * fl.cp)  # noqa: E731
+    outs = (keng.host_array((2 * n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int32),
+            keng.host_array((2 * n_churn,), np.uint32))
+    steps, host = [], None
+    trans = n_host = docs = nbytes = 0
+    for k in range(ticks + 1):
+        arena, offs, lens, ops, handles = ch.batch_json(dump, now)
+        if k == 0:  # the host codec on this batch (untimed leg warmup)
+            t0 = time.perf_counter()
+            h = workload.host_decode_arrays(codec, arena, offs, lens, threads=os.cpu_count() and min(16, os.cpu_count()))
+            host = (time.perf_counter() - t0, int((h["status"] == 0).sum()))
+            del h
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hs, st, _rel, nh = e.ingest_pods_json(codec, arena, offs, lens, ops, handles, out=outs)
+        t1 = time.perf_counter()
+        r = e.tick(now, read=False)
+        t2 = time.perf_counter()
+        ch.applied(hs.copy(), st)
+        now += 30
+        if k:
+            steps.append((t1 - t0, t2 - t1))
+            trans += transitions(r.counters)
+            n_host += nh
+            docs += len(offs)
+            nbytes += int(lens.sum())
+    ing = sum(a for a, _ in steps)
+    tck = sum(b for _, b in steps)
+    codec.close()
+    return now, ch, {
+        "workload": "C4 from JSON: %d deletion-marked + %d created pod documents per tick on the metric fleet "
+                    "(heartbeat-once engine)" % (n_churn, n_churn),
+        "ticks": ticks, "documents_per_tick": docs // max(ticks, 1), "json_bytes_per_tick": nbytes // max(ticks, 1),
+        "value": trans / (ing + tck), "unit": "transitions/s (decode + ingest + tick)",
+        "ms_per_step": (ing + tck) / ticks * 1e3, "decode_ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
+        "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
+                      "decode_ingest": float(np.median([a for a, _ in steps])) * 1e3},
+        "documents_per_s": docs / ing if ing else None, "documents_decided_by_host": n_host,
+        "host_codec": {"ms": host[0] * 1e3, "documents_per_s": len(offs) / host[0], "threads": min(16, os.cpu_count()),
+                       "what": "kwok_decode_pods (codec.cpp) on one batch of the same documents, records only "
+                               "(no ingest): the drop-in's host path"},
+        "note": "decode_ingest = kwok_ingest_pods_json: the documents (page-locked) copied to HBM, k_json_pods (one "
+                "thread per document), then kwok_ingest_pods' GPU event switch over the decoded records"}
 
 
 def c2_leg(steps, warmup):
@@ -645,7 +704,7 @@ def main():
     flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
     flap_once = flap_leg(a.nodes_per_rank, a.flap_ticks, True) if world == 1 and a.flap_ticks > 0 and a.once_ticks \
         else None
-    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup, a.churn_ticks) \
+    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup, a.churn_ticks, a.json_ticks) \
         if world == 1 and a.once_ticks else None
     c2 = c2_leg(a.steps, a.warmup) if world == 1 and a.c2 and a.nodes_per_rank == NODES_PER_RANK else None
     emul = emulated_ranks_leg(a.nodes_per_rank, a.emulate_ranks, 20, min(a.churn_ticks, 3)) \

@@ -20,6 +20,7 @@ package controllers
 import "C"
 
 import (
+	"bytes"
 	"context"
 	"encoding/binary"
 	"encoding/json"
@@ -327,7 +328,14 @@ func (c *GPUController) Size() int               { return c.eng.nodeSize() }
 
 // step: ingest the batches (nodes first, so new pods find their node), give
 // the tick's pending pods their CNI IPs (EnableCNI), run the tick, hand every
-// body to the task pool
+// body to the task pool; then the same interval again for the pods patched
+// without a podIP (created with an empty status: pod.status.tpl renders no IPs
+// then, `{{ with .status }}`).  In the reference that patch's own Modified event
+// re-enters lockPodChan (pod_controller.go:279-319) and the pod gets hostIP /
+// podIP at once; here the object the patch returned is ingested as that event
+// (its watch echo is dropped like every echo) and the engine ticks again at the
+// same clock, applying that tick's pod patches, node inits and deletes but not
+// its heartbeats (the interval's heartbeats were sent).
 func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int64) (int, error) {
 	c.mu.Lock()
 	nw, pw := c.nodes, c.pods
@@ -354,11 +362,55 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 			return 0, err
 		}
 	}
+	var re reentry
+	n, err := c.tickApply(ctx, tasks, now, true, &re)
+	for round := 0; round < 4 && err == nil; round++ { // (a re-entered pod's second patch carries its IPs)
+		tasks.Wait()
+		if len(re.objs) == 0 {
+			break
+		}
+		var b objBatch
+		for _, p := range re.objs {
+			if err = b.add(watchObj{p, p.UID, p.ResourceVersion, false}); err != nil {
+				return n, err
+			}
+		}
+		re.objs = nil
+		if err = c.flushPods(ctx, tasks, b); err != nil {
+			return n, err
+		}
+		if c.conf.EnableCNI {
+			if err = c.setupCNI(ctx, tasks); err != nil {
+				return n, err
+			}
+		}
+		var m int
+		m, err = c.tickApply(ctx, tasks, now, false, &re)
+		n += m
+	}
+	return n, err
+}
+
+// reentry: the objects returned by pod patches that carried no podIP
+type reentry struct {
+	mu   sync.Mutex
+	objs []*corev1.Pod
+}
+
+var podIPKey = []byte(`"podIP"`)
+
+// tickApply: one tick at now, every body handed to the task pool (heartbeats
+// only when asked); pod patches without a podIP leave their returned object in re
+func (c *GPUController) tickApply(ctx context.Context, tasks *parallelTasks, now int64, heartbeats bool,
+	re *reentry) (int, error) {
 	logger := log.FromContext(ctx)
 	nodesAPI := c.conf.ClientSet.CoreV1().Nodes()
 	var gone []int32
 	n := 0
-	err = c.eng.tick(now, func(kind int, h int32, body []byte) {
+	err := c.eng.tick(now, func(kind int, h int32, body []byte) {
+		if kind == kindHeartbeat && !heartbeats {
+			return
+		}
 		n++
 		switch kind {
 		case kindHeartbeat, kindNodeInit: // configureHeartbeatNode / configureNode bodies
@@ -383,6 +435,11 @@ func (c *GPUController) step(ctx context.Context, tasks *parallelTasks, now int6
 					return
 				}
 				c.echo.note(p.UID, p.ResourceVersion)
+				if !bytes.Contains(body, podIPKey) { // an empty status: its echo re-enters
+					re.mu.Lock()
+					re.objs = append(re.objs, p)
+					re.mu.Unlock()
+				}
 			})
 		case kindDelete, kindDeleteFin: // DeletePod (pod_controller.go:155-183); the engine freed the handle
 			ref, fin := c.podRef[h], kind == kindDeleteFin

@@ -40,7 +40,15 @@ Per tick (step):
      ONE heartbeat body (the engine is created with KWOK_CFG_HEARTBEAT_ONCE) sent
      to every managed node, node-init and pod patches read in pieces of at most
      READ_CHUNK bytes (kwok_read_arena), deletes; every body applied through the
-     clientset, every returned resourceVersion noted as an echo.
+     clientset, every returned resourceVersion noted as an echo;
+  6. the same interval again for pods patched without a podIP (created with an
+     empty status: pod.status.tpl renders no IPs then, `{{ with .status }}`):
+     in the reference that patch's own Modified event re-enters lockPodChan
+     (pod_controller.go:279-319) and the pod gets hostIP / podIP at once.  Here
+     the object the patch returned is ingested as that event (its watch echo is
+     then dropped like every echo) and the engine ticks again at the same clock;
+     that tick's pod patches, node inits and deletes are applied, its heartbeats
+     are not (the interval's heartbeats were sent).
 
 The backend is the HIP engine; tests may pass another implementation of the
 same ABI (the CPU oracle) as the checker.
@@ -215,6 +223,7 @@ class Stats:
     """what the controller did (tests read it; the Go shim logs it)"""
     echoes_on_arrival: int = 0
     echoes_at_flush: int = 0
+    reentered: int = 0    # pods patched without a podIP, ingested again in the same interval
     node_records: int = 0
     pod_records: int = 0
     pod_runs: int = 0
@@ -269,6 +278,7 @@ class Controller:
         self.hb_epoch = None
         self.spec_ids = {}
         self.finalizer = None
+        self.reenter = []     # objects of pod patches without a podIP (step 6)
 
     def close(self):
         self.eng.close()
@@ -312,7 +322,19 @@ class Controller:
         self._flush_pods(pb)
         if self.conf.enable_cni:
             self._setup_cni()
-        return self._tick(now)
+        n = self._tick(now)
+        # step 6: pods patched without a podIP re-enter at once (pod_controller.go:279-319)
+        for _ in range(4):  # (a re-entered pod's second patch carries its IPs: one round suffices)
+            if not self.reenter:
+                break
+            objs, self.reenter = self.reenter, []
+            self.stats.reentered += len(objs)
+            ws = [WatchObj(o, _meta(o).get("uid", ""), _meta(o).get("resourceVersion", ""), False) for o in objs]
+            self._flush_pods((ws, [json.dumps(w.obj, separators=(",", ":")).encode() for w in ws]))
+            if self.conf.enable_cni:
+                self._setup_cni()
+            n += self._tick(now, heartbeats=False)
+        return n
 
     def _encode(self, ws):
         keep, seen = [], set()
@@ -432,7 +454,7 @@ class Controller:
             self.eng.cni_assign(keep, ips)
 
     # ---- tick + apply (engine_cgo.go tick / applyPatches, gpu_controller.go step) -----
-    def _tick(self, now):
+    def _tick(self, now, heartbeats=True):
         e = self.eng
         res = e.tick_raw(now)
         new_epoch = self.hb is None or res.heartbeat_epoch != self.hb_epoch
@@ -450,7 +472,7 @@ class Controller:
         e._check(e._fn("read_outputs")(e._h, C.byref(out)), "read_outputs")
         self.hb_epoch = res.heartbeat_epoch
         n = 0
-        if res.n_heartbeat:
+        if res.n_heartbeat and heartbeats:
             body = e.read_arena(out.heartbeat_off, res.heartbeat_len).tobytes()
             for h in self.hb:
                 self._apply(HEARTBEAT, int(h), body)
@@ -502,6 +524,8 @@ class Controller:
             except NotFound:
                 return
             self.echo.note(_meta(obj).get("uid"), _meta(obj).get("resourceVersion"))
+            if b'"podIP"' not in body:  # an empty status: its echo re-enters (step 6)
+                self.reenter.append(obj)
         else:  # DeletePod (pod_controller.go:155-183)
             ns, name = self.pod_ref[h]
             if kind == DELETE_FIN:

@@ -939,7 +939,7 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
     side.status = status;
     A.ev[i] = ev;
     A.side[i] = side;
-    if (status == JSON_HOST || status == JSON_SPEC) A.host_list[atomicAdd(A.n_host, 1u)] = i;
+    if (status == JSON_HOST || status == JSON_SPEC) A.host_list[atomicAdd(A.n_host, 1u)] = A.base + i;
 }
 
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st) {

@@ -220,7 +220,8 @@ struct JsonPodArgs {
     const int32_t* tab_id;
     kwok_pod_event* ev;          // [n] out
     JsonPodSide* side;           // [n] out
-    uint32_t* host_list;         // [n] out: documents the host completes (JSON_HOST / JSON_SPEC)
+    uint32_t* host_list;         // [n] out: documents the host completes (JSON_HOST / JSON_SPEC), as base + index
+    uint32_t base;               // the batch index of document 0 of this launch (a piece of the batch)
     uint32_t* n_host;            // [1] (zeroed by the caller)
 };
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st);

@@ -422,6 +422,14 @@ class ChurnJson(Churn):
         self.node_name_of = node_name_of
         self.serial = 0
 
+    @classmethod
+    def from_churn(cls, ch, node_name_of, alloc=None):
+        """the storm continued from another Churn's live pods, as documents"""
+        x = cls.__new__(cls)
+        x.__dict__.update(ch.__dict__)
+        x.node_name_of, x.serial, x.alloc, x.packed, x.bufs, x.jbuf = node_name_of, 0, alloc, False, None, None
+        return x
+
     def names(self, n):
         s = np.arange(self.serial, self.serial + n, dtype=np.int64)
         self.serial += n

@@ -216,6 +216,54 @@ def test_finalizer_patch_echo_is_dropped(deliver):
     c.close()
 
 
+def empty_status_scenario(cs, c):
+    """pods created with an empty status next to Pending ones; returns the pod
+    write calls of each of three steps"""
+    cs.create(node("n0"))
+    cs.create(node("n1", managed=False))
+    c.step(S0 + 30)
+    cs.pump()
+    cs.create(pod("e0", "n0"))
+    cs.create(pod("r0", "n0", status={"phase": "Pending"}))
+    cs.create(pod("e1", "n0", containers=(("a", "img-a"), ("b", "img-b"))))
+    cs.create(pod("u0", "n1"))  # unmanaged node: never patched
+    cs.pump()
+    per = []
+    for t in range(3):
+        n0 = len(cs.calls)
+        c.step(S0 + 60 + 30 * t)
+        cs.pump()
+        per.append([x for x in cs.calls[n0:] if x[1] == "pods"])
+    return per
+
+
+@pytest.mark.parametrize("deliver", ["sync", "queued"])
+def test_empty_status_pod_gets_its_ip_in_the_same_interval(deliver):
+    """pod_controller.go:279-319 with pod.status.tpl's `{{ with .status }}`: a
+    pod created with an empty status is patched without hostIP / podIP; that
+    patch's Modified event re-enters lockPodChan and the second configurePod,
+    in the same interval, renders NodeIP and a pool address.  The drop-in
+    ingests the patch's returned object and ticks again at the same clock: both
+    patches land in one step, the IPs follow the pool order of the reference
+    (r0 in the first pass, e0 / e1 in the second), the echoes of both patches
+    are dropped and the next steps write nothing."""
+    cs = FakeClientset(deliver=deliver)
+    c = controller(cs, manage_nodes_with_annotation_selector=MANAGE, node_ip="10.0.0.254", cidr="10.0.0.1/24")
+    per = empty_status_scenario(cs, c)
+    names = [k[1] for _, _, k, _ in per[0]]
+    assert names == ["e0", "r0", "e1", "e0", "e1"], names
+    first, second = per[0][0][3], per[0][3][3]
+    assert b'"podIP"' not in first and b'"hostIP"' not in first
+    assert b'"hostIP":"10.0.0.254"' in second and b'"podIP":"10.0.0.2"' in second
+    assert per[1] == [] and per[2] == []
+    st = {p["metadata"]["name"]: p["status"] for p in cs.list("pods")}
+    assert (st["e0"]["podIP"], st["r0"]["podIP"], st["e1"]["podIP"]) == ("10.0.0.2", "10.0.0.1", "10.0.0.3")
+    assert all(st[k]["phase"] == "Running" and st[k]["hostIP"] == "10.0.0.254" for k in ("e0", "r0", "e1"))
+    assert st["u0"] == {}
+    assert c.stats.reentered == 2
+    c.close()
+
+
 def test_runs_for_added_modified_deleted_in_one_batch():
     """flushPods' cut: a new pod's second event needs its handle, so the batch
     is ingested in runs; Added + Deleted leaves no pod and releases nothing it

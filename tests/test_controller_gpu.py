@@ -49,6 +49,22 @@ def test_drop_in_engine_equals_oracle(deliver):
     o.close()
 
 
+@pytest.mark.parametrize("deliver", ["sync", "queued"])
+def test_empty_status_same_interval_engine_vs_oracle(deliver):
+    """the drop-in's step 6 (controller.py: an IP-less pod patch re-enters and
+    the engine ticks again at the same clock) on the engine and on the oracle:
+    every pod write equal, body for body, and both IPs in the first step"""
+    (ce, e), (co, o) = _pair(deliver, manage_nodes_with_annotation_selector=T.MANAGE, node_ip="10.0.0.254",
+                             cidr="10.0.0.1/24")
+    a = T.empty_status_scenario(ce, e)
+    b = T.empty_status_scenario(co, o)
+    assert a == b and len(a[0]) == 5 and a[1] == a[2] == []
+    assert e.stats.reentered == o.stats.reentered == 2
+    assert ce.store == co.store
+    e.close()
+    o.close()
+
+
 @pytest.mark.parametrize("name", ["test_reference_node_controller", "test_reference_pod_controller"])
 def test_reference_tests_through_the_engine(name, monkeypatch):
     """node_controller_test.go / pod_controller_test.go, restated through the
