@@ -195,6 +195,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     ing = tck = 0.0
     trans = recs = 0
     kern = emit = xch = 0.0
+    phases = {}
     last = None
     steps = []
     # (the runtime's ~6 ms copy-engine queue creations, which used to land in one or two of a
@@ -220,6 +221,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
             ph, nt = e.profile_read()
             e.profile_enable(False)
             kern, emit, xch = ph["kernel"] * ticks, ph["emit_kernel"] * ticks, ph["exchange"] * ticks
+            phases = {k: v / max(nt, 1) for k, v in ph.items()}
         elif k >= warm:
             a, b = max_over_ranks(t1 - t0), max_over_ranks(t2 - t0)
             ing += a
@@ -246,6 +248,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         # multi-rank tick: the FRONT header to the (last) BACK launch's start -
         # allgather, and for long lists the host round trip, second allgather, k_pool_apply
         "exchange_ms": xch / ticks if (world > 1 or multi) else None,
+        "phase_ms": phases,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods: H2D of the records and their strings (page-locked batch buffers, "
                 "kwok_host_alloc; batches over KWOK_INGEST_CHUNK records in chunks, each copied while the previous "
@@ -488,7 +491,8 @@ def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
                                         "(KWOK_FORCE_MULTI + KWOK_EMULATE_RANKS, one-rank RCCL allgather)" % ranks,
             "steady_ms_per_tick": dt * 1e3, "steady_phase_ms": {k: v / max(nt, 1) for k, v in ph.items()},
             "churn": None if churn is None else {k: churn[k] for k in ("ms_per_step", "ingest_ms", "tick_ms",
-                                                                       "kernel_ms", "exchange_ms", "median_ms")},
+                                                                       "kernel_ms", "exchange_ms", "median_ms",
+                                                                       "phase_ms")},
             "note": "blocking kwok_tick steps; the allgather is a one-rank copy (the xGMI transfer of N ranks' "
                     "8 KiB messages / MB lists is not in it)"}
 

@@ -2704,6 +2704,54 @@ __global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevSt
     emit_pod_chunks<NC, true, FUSE>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0);
 }
 
+// One rank's Use or release list ORed into a bitmap, OR_RUN consecutive entries
+// per thread: entries that fall in one bitmap word one after the other (a
+// rank's lists follow canonical order, and addresses were handed out lowest
+// first in that order, so neighbours usually share a word) take ONE atomic
+// together.  A list in no order costs what one atomic per entry costs.
+// (chunk c covers entries [c * OR_RUN, +OR_RUN) of a; out-of-CIDR entries skipped)
+constexpr uint32_t OR_RUN = 16;
+__device__ __forceinline__ void or_run(const PoolGeom& g, uint64_t* bm, const uint32_t* a, uint32_t n, uint32_t c) {
+    const uint32_t s0 = c * OR_RUN, e = min(s0 + OR_RUN, n);
+    uint32_t ip[OR_RUN];
+#pragma unroll
+    for (uint32_t k = 0; k < OR_RUN; k++) ip[k] = s0 + k < e ? a[s0 + k] : 0u;  // (loads in flight together)
+    uint64_t m = 0, w = ~0ull;
+#pragma unroll
+    for (uint32_t k = 0; k < OR_RUN; k++) {
+        if (s0 + k >= e || !in_cidr(g, ip[k])) continue;
+        const uint64_t bit = ip[k] - g.net;
+        if ((bit >> 6) != w) {
+            if (m) atomicOr((unsigned long long*)&bm[w], m);
+            w = bit >> 6, m = 0;
+        }
+        m |= 1ull << (bit & 63);
+    }
+    if (m) atomicOr((unsigned long long*)&bm[w], m);
+}
+// every rank's Uses into used_bm and releases into rel_bm: chunks of OR_RUN
+// entries over all ranks' lists (rank-major; each rank's Use chunks, then its
+// release chunks), the grid striding over the chunks
+template <class ListOf>
+__device__ __forceinline__ void or_lists(const DevState& S, int nranks, ListOf list) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t c0 = 0;  // the chunks of the ranks before r
+    for (int r = 0; r < nranks; r++) {
+        const uint32_t* u, * rl;
+        uint32_t nu, nr;
+        list(r, u, nu, rl, nr);
+        const uint32_t cu = (nu + OR_RUN - 1) / OR_RUN, cr = (nr + OR_RUN - 1) / OR_RUN;
+        // this thread's first chunk at or after c0
+        const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+        const uint32_t first = c0 + (t + stride - c0 % stride) % stride;
+        for (uint32_t c = first; c < c0 + cu + cr; c += stride) {
+            if (c - c0 < cu) or_run(S.pool, S.used_bm, u, nu, c - c0);
+            else or_run(S.pool, S.rel_bm, rl, nr, c - c0 - cu);
+        }
+        c0 += cu + cr;
+    }
+}
+
 // ingest-time Put (a Deleted watch event), applied immediately
 __global__ void k_pool_puts_now(DevState S, const uint32_t* ips, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -2728,16 +2776,10 @@ __global__ void k_cni_pending(DevState S, int32_t* out, uint32_t* count) {
 }
 // multi-rank: every rank's Uses into used_bm, every rank's Puts into rel_bm
 __global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
-    for (int r = 0; r < nranks; r++) {
+    or_lists(S, nranks, [&](int r, const uint32_t*& u, uint32_t& nu, const uint32_t*& rl, uint32_t& nr) {
         const ListDesc d = ld[r];
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_use + d.n_rel; i += gridDim.x * blockDim.x) {
-            bool use = i < d.n_use;
-            uint32_t ip = use ? d.use[i] : d.rel[i - d.n_use];
-            if (!in_cidr(S.pool, ip)) continue;
-            uint64_t b = ip - S.pool.net;
-            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
-        }
-    }
+        u = d.use, nu = d.n_use, rl = d.rel, nr = d.n_rel;
+    });
 }
 
 // KWOK_EMULATE_RANKS (diagnostics, one rank): messages 1..xw-1 are copies of
@@ -2856,23 +2898,16 @@ __global__ void k_pool_apply_spec(DevState S, const uint32_t* recv) {
     if (__hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     if (!spec_fits(S)) return;  // BACK takes the long-list way (the host's second exchange)
     const uint64_t per = (uint64_t)S.xcap_u + S.xcap_r;
-    for (int r = 0; r < S.world; r++) {
-        const uint32_t nu = (uint32_t)S.xall[r].n_use, nr = (uint32_t)S.xall[r].n_rel;
-        const uint32_t* base = recv + r * per;
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu + nr; i += gridDim.x * blockDim.x) {
-            const bool use = i < nu;
-            const uint32_t ip = use ? base[i] : base[S.xcap_u + (i - nu)];
-            if (!in_cidr(S.pool, ip)) continue;
-            const uint64_t b = ip - S.pool.net;
-            atomicOr((unsigned long long*)&(use ? S.used_bm : S.rel_bm)[b >> 6], 1ull << (b & 63));
-        }
-    }
+    or_lists(S, S.world, [&](int r, const uint32_t*& u, uint32_t& nu, const uint32_t*& rl, uint32_t& nr) {
+        u = recv + r * per, nu = (uint32_t)S.xall[r].n_use;
+        rl = u + S.xcap_u, nr = (uint32_t)S.xall[r].n_rel;
+    });
 }
 void launch_pool_apply_spec(const DevState& S, const uint32_t* recv, hipStream_t st) {
     hipLaunchKernelGGL(k_pool_apply_spec, dim3(1024), dim3(256), 0, st, S, recv);
 }
 void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32_t max_n, hipStream_t st) {
-    uint32_t g = max_n ? cdiv(max_n, 256) : 1;
+    uint32_t g = max_n ? cdiv((uint64_t)cdiv(max_n, OR_RUN) * (uint32_t)nranks, 256) : 1;
     if (g > 1024) g = 1024;
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }

@@ -1,6 +1,6 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_json_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread > $R/gpurun_out/json_t.log 2>&1 || { tail -20 $R/gpurun_out/json_t.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_json_gpu.py tests/test_controller_gpu.py -k 'not 1m_10m' -x -q -m gpu --timeout 300 --timeout-method thread > $R/gpurun_out/json_t.log 2>&1 || { tail -20 $R/gpurun_out/json_t.log; exit 1; }
 tail -2 $R/gpurun_out/json_t.log
 KWOK_INGEST_PROF=1 timeout -k 10 400 python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --churn-ticks 2 --flap-ticks 0 --emulate-ranks 0 --c2 0 --json-ticks 3 > $R/gpurun_out/bench_json.json 2> $R/gpurun_out/bench_json.err || { tail -30 $R/gpurun_out/bench_json.err; exit 2; }
 python3 -c "
