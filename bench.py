@@ -72,6 +72,8 @@ NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only
 #   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
 INIT_BYTES = 1471
 POD_PATCH_BYTES = 577
+#   C4 tick, per deleted pod: 10 B re-check + 4 B handle + 1 B finalizer flag + 4 B release
+DELETE_BYTES = 19
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
 PMC_FILE = "r6c_pmc.json"
 ONCE_PMC_FILE = "r7_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
@@ -159,7 +161,7 @@ def cpu_baseline(nodes, threads, ticks):
 
 
 def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
-              packed=True, ch=None, multi=False):
+              packed=16, ch=None, multi=False):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -170,10 +172,11 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     world > 1: every rank churns n_churn of its own pods per tick (weak
     scaling); the releases of all ranks cross the exchange (their lists are
     longer than the inline message: the second allgather), and each step is
-    timed between barriers, max over ranks.  packed: the batch in the compact
-    wire form (kwok_pod_rec, 20 B per record, kwok_ingest_pods_packed; statuses
-    as bytes, no release list at N=1); otherwise kwok_pod_event records with
-    dotted-quad strings (48 B + strings)."""
+    timed between barriers, max over ranks.  packed=16: the batch as
+    kwok_pod_rec16 (16 B per record, kwok_ingest_pods_packed16: statuses as
+    bytes, the creates' handles only, no release list at N=1); packed=20:
+    kwok_pod_rec (20 B, kwok_ingest_pods_packed, every handle back); otherwise
+    kwok_pod_event records with dotted-quad strings (48 B + strings)."""
     barrier = barrier or torch.cuda.synchronize
     max_over_ranks = max_over_ranks or (lambda x: x)
     lo = rank * workload.BUCKETS // world
@@ -184,8 +187,11 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     if ch is None:  # (a later leg continues the previous leg's generator: its live pods)
         ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn,
                             seed=7, first=lo * fl.cp, alloc=keng.host_array)
-    ch.packed, ch.bufs = packed, None
-    if packed:  # multi rank: the ingest-time releases too (kwok_pool_put material)
+    ch.packed, ch.bufs = (packed if packed == 16 else bool(packed)), None
+    if packed == 16:  # the creates' handles; multi rank: the releases too (kwok_pool_put material)
+        outs = (keng.host_array((n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int8),
+                keng.host_array((2 * n_churn,), np.uint32) if world > 1 else None)
+    elif packed:
         outs = (keng.host_array((2 * n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int8),
                 keng.host_array((2 * n_churn,), np.uint32) if world > 1 else None)
     else:
@@ -208,14 +214,17 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         if prof:
             e.profile_enable(True)
         t0 = time.perf_counter()
-        hs, st, _ = e.ingest_pods_packed(ev, out=outs) if packed else e.ingest_pods_raw(ev, ar, out=outs)
+        if packed == 16:
+            hs, st, _ = e.ingest_pods_packed16(ev, new_cap=len(ev) // 2, out=outs)
+        else:
+            hs, st, _ = e.ingest_pods_packed(ev, out=outs) if packed else e.ingest_pods_raw(ev, ar, out=outs)
         t1 = time.perf_counter()
         r = e.tick(now, read=False)
         t2 = time.perf_counter()
         if world > 1:
             barrier()
             t2 = time.perf_counter()
-        ch.applied(hs.copy(), st)
+        ch.applied(hs.copy(), st, new_only=packed == 16)
         now += 30
         if prof:
             ph, nt = e.profile_read()
@@ -234,8 +243,12 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         "workload": "C4 pod churn storm (BASELINE configs[3]) on the metric fleet: %d deletion-marked pods (50%% with "
                     "finalizers) + %d creates per tick%s" % (n_churn, n_churn, " per rank" if world > 1 else ""),
         "ticks": ticks, "records_per_tick": recs // max(ticks, 1) * world,
-        "wire": "kwok_pod_rec, 20 B per record (kwok_ingest_pods_packed)" if packed else
+        "wire": "kwok_pod_rec16, 16 B per record in, 1 B status per record + 4 B handle per create back "
+                "(kwok_ingest_pods_packed16)" if packed == 16 else
+                "kwok_pod_rec, 20 B per record (kwok_ingest_pods_packed)" if packed else
                 "kwok_pod_event, 48 B per record + dotted-quad strings (kwok_ingest_pods)",
+        "link_bytes_per_step": (2 * n_churn * 16 + 2 * n_churn + 4 * n_churn if packed == 16 else
+                                2 * n_churn * 20 + 2 * n_churn * 5 if packed else None),
         "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
         "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
         "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
@@ -249,12 +262,25 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         # allgather, and for long lists the host round trip, second allgather, k_pool_apply
         "exchange_ms": xch / ticks if (world > 1 or multi) else None,
         "phase_ms": phases,
+        "roofline": c4_roofline(last, kern / ticks) if last else None,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods: H2D of the records and their strings (page-locked batch buffers, "
                 "kwok_host_alloc; batches over KWOK_INGEST_CHUNK records in chunks, each copied while the previous "
                 "one is applied), the GPU event switch (prep, stable sort by bucket, per-bucket apply), D2H of the "
                 "per-record handles / statuses / releases; event generation between steps untimed (the GPU idles "
                 "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
+
+
+def c4_roofline(c, kern_ms):
+    """the churn tick's kernels (k_tick + the emission) against HBM: the steady
+    tick's bytes (heartbeats, node and pod re-checks) + per Pending->Running
+    patch POD_PATCH_BYTES + per deletion DELETE_BYTES, over the profiled tick's
+    kernel time (HIP events around its launches)"""
+    b = NODE_BYTES * c["heartbeat"] + POD_BYTES * c["pods_total"] + POD_PATCH_BYTES * c["pod_patch"] + \
+        DELETE_BYTES * c["delete"]
+    ach = b / (kern_ms * 1e-3) / 1e9 if kern_ms else None
+    return {"bound": "hbm", "kernel": "k_tick + k_pod_jobs + k_emit", "bytes_per_tick": b, "kernel_ms": kern_ms,
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None}
 
 
 def steady_queued(e, now, steps, warmup):

@@ -20,7 +20,9 @@ package controllers
 import "C"
 
 import (
+	"encoding/binary"
 	"fmt"
+	"net"
 	"unsafe"
 
 	"sigs.k8s.io/kwok/pkg/kwok/controllers/templates"
@@ -55,7 +57,8 @@ type gpuEngine struct {
 	// records: copied by DMA, chunk by chunk), and writes the per-record results to
 	// resBuf (a copy into pageable Go memory would stall the engine's next
 	// transfers, DESIGN.md §11)
-	evBuf, arBuf, resBuf, recBuf hostBuf
+	evBuf, arBuf, resBuf, recBuf, rec16Buf hostBuf
+	nodeIP                               uint32 // Config.NodeIP (kwok_pod_rec16's KWOK_REC_HOST_NODE_IP)
 }
 
 type hostBuf struct {
@@ -146,7 +149,11 @@ func newGPUEngine(conf Config, startUnix int64, rank, world int, commID []byte) 
 	if rc := C.kwok_engine_create(&cfg, &h); rc != C.KWOK_OK {
 		return nil, fmt.Errorf("kwok_engine_create: %d: %s", int(rc), C.GoString(C.kwok_last_error(nil)))
 	}
-	return &gpuEngine{h: h}, nil
+	g := &gpuEngine{h: h}
+	if ip := net.ParseIP(conf.NodeIP).To4(); ip != nil {
+		g.nodeIP = binary.BigEndian.Uint32(ip)
+	}
+	return g, nil
 }
 
 // kwokCommID: the RCCL communicator id rank 0 creates and sends to the other ranks.
@@ -167,6 +174,7 @@ func (g *gpuEngine) close() {
 	g.arBuf.free()
 	g.resBuf.free()
 	g.recBuf.free()
+	g.rec16Buf.free()
 }
 
 func arenaPtr(arena []byte) *C.char {
@@ -254,12 +262,14 @@ func (g *gpuEngine) ingestNodes(evs []C.kwok_node_event, arena []byte) (handles,
 }
 
 // ingestPods: one batch of pod records in event order.  Every record the
-// compact wire form can carry (kwok_pack_pod_events: IPs as integers, a new pod's
-// node by handle) goes as a 20-byte kwok_pod_rec through
+// compact wire forms can carry (kwok_pack_pod_events: IPs as integers, a new
+// pod's node by handle) goes as a 16-byte kwok_pod_rec16 through
+// kwok_ingest_pods_packed16 when its hostIP is empty or NodeIP (every pod kwok
+// runs: pod.status.tpl renders NodeIP), else as a 20-byte kwok_pod_rec through
 // kwok_ingest_pods_packed; the rest (a pod naming a node the engine holds no
 // handle for) as kwok_pod_event with its strings through kwok_ingest_pods.
 // Consecutive records of one form are one call: applying the calls in order is
-// applying the batch.  Both read page-locked buffers (kwok_host_alloc).
+// applying the batch.  All read page-locked buffers (kwok_host_alloc).
 func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, status []int32, released []uint32, err error) {
 	n := len(evs)
 	handles, status, released = make([]int32, n), make([]int32, n), make([]uint32, n)
@@ -273,13 +283,24 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 	recs := unsafe.Slice((*C.kwok_pod_rec)(recp), n)
 	pst := make([]int32, n)
 	C.kwok_pack_pod_events(&evs[0], C.size_t(n), arenaPtr(arena), C.size_t(len(arena)), &recs[0], (*C.int32_t)(&pst[0]))
+	form := func(k int) int {
+		if pst[k] != C.KWOK_OK {
+			return 0
+		}
+		if h := uint32(recs[k].host_ip); h == 0 || h == g.nodeIP {
+			return 16
+		}
+		return 20
+	}
 	for i := 0; i < n; {
-		packed := pst[i] == C.KWOK_OK
+		f := form(i)
 		j := i + 1
-		for j < n && (pst[j] == C.KWOK_OK) == packed {
+		for j < n && form(j) == f {
 			j++
 		}
-		if packed {
+		if f == 16 {
+			err = g.ingestPacked16(recs[i:j], handles[i:j], status[i:j], released[i:j])
+		} else if f == 20 {
 			err = g.ingestPacked(recs[i:j], handles[i:j], status[i:j], released[i:j])
 		} else {
 			err = g.ingestFull(evs[i:j], arena, handles[i:j], status[i:j], released[i:j])
@@ -313,6 +334,54 @@ func (g *gpuEngine) ingestPacked(recs []C.kwok_pod_rec, handles, status []int32,
 	for i := range st {
 		status[i] = int32(st[i])
 	}
+	return nil
+}
+
+// ingestPacked16: kwok_ingest_pods_packed16 of the records as kwok_pod_rec16 in
+// page-locked memory; the creates' handles come back in create order, every
+// other record's handle is its target
+func (g *gpuEngine) ingestPacked16(recs []C.kwok_pod_rec, handles, status []int32, released []uint32) error {
+	n := len(recs)
+	rp, err := g.rec16Buf.get(n * int(unsafe.Sizeof(C.kwok_pod_rec16{})))
+	if err != nil {
+		return err
+	}
+	r16 := unsafe.Slice((*C.kwok_pod_rec16)(rp), n)
+	nNew := 0
+	for i := range recs {
+		op := recs[i].op
+		if recs[i].host_ip != 0 {
+			op |= C.KWOK_REC_HOST_NODE_IP
+		}
+		if recs[i].op&C.KWOK_REC_NEW != 0 {
+			nNew++
+		}
+		r16[i] = C.kwok_pod_rec16{op: op, flags: recs[i].flags, spec_id: recs[i].spec_id, target: recs[i].target,
+			creation: recs[i].creation, pod_ip: recs[i].pod_ip}
+	}
+	resp, err := g.resBuf.get(9 * n)
+	if err != nil {
+		return err
+	}
+	h := unsafe.Slice((*int32)(resp), n) // (the first nNew entries: the creates' handles)
+	rel := unsafe.Slice((*uint32)(unsafe.Add(resp, 4*n)), n)
+	st := unsafe.Slice((*int8)(unsafe.Add(resp, 8*n)), n)
+	rc := C.kwok_ingest_pods_packed16(g.h, &r16[0], C.size_t(n), (*C.int32_t)(&h[0]), C.size_t(nNew),
+		(*C.int8_t)(&st[0]), (*C.uint32_t)(&rel[0]))
+	if rc < 0 {
+		return fmt.Errorf("kwok_ingest_pods_packed16: %d: %s", int(rc), g.lastError())
+	}
+	k := 0
+	for i := range recs {
+		if recs[i].op&C.KWOK_REC_NEW != 0 {
+			handles[i] = h[k]
+			k++
+		} else {
+			handles[i] = int32(recs[i].target)
+		}
+		status[i] = int32(st[i])
+	}
+	copy(released, rel)
 	return nil
 }
 

@@ -234,7 +234,8 @@ struct PodRec {             // 32 bytes
     uint8_t op, phase, flags, chk;  // chk: REC_*
     int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
     int8_t pst;             // existing: the handle lookup's status
-    uint8_t pad[4];
+    uint8_t is_new;         // kwok_pod_rec16: a KWOK_REC_NEW record (its handle goes to out_new_handles)
+    uint8_t pad[3];
 };
 static_assert(sizeof(PodRec) == 32, "prepared pod records are 32 bytes");
 constexpr uint32_t REC_NONE = 0xFFFFFFFFu;
@@ -255,7 +256,8 @@ struct IngSummary {
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)
-    uint32_t pad[2];
+    uint32_t n_new;         // kwok_pod_rec16: the batch's KWOK_REC_NEW records up to this chunk
+    uint32_t pad;
 };
 
 // ---- the watch-event codec on the GPU (json.hip) -------------------------------

@@ -191,8 +191,12 @@ struct kwok_engine {
         int8_t* out_status8 = nullptr;  // kwok_ingest_pods_packed: the statuses as bytes
         uint32_t* out_released = nullptr;
         void* sort_tmp = nullptr;
+        // kwok_ingest_pods_packed16: NEW records per 256-record tile, the tiles' prefixes,
+        // the creates' handles in create order
+        uint32_t *tile_new = nullptr, *tile_pre = nullptr;
+        int32_t* new_handle = nullptr;
         // per bucket (allocated once)
-        uint32_t *creates = nullptr, *beg = nullptr, *end = nullptr;
+        uint32_t *beg = nullptr, *end = nullptr;
         uint32_t* abort = nullptr;          // [1] a chunk of the batch needs growth (speculative apply passes)
         IngSummary* sums = nullptr;         // [nsums] one per chunk of a batch
         IngSummary* sums_h = nullptr;       // pinned
@@ -211,12 +215,12 @@ struct kwok_engine {
         IngSummary* sum_h = nullptr;  // pinned
         // a batch runs in chunks (KWOK_INGEST_CHUNK records): chunk k+1's prep reads its
         // records over the link on `pst` while chunk k is applied and its results copied
-        // back on the engine stream; odd chunks take the second accumulator set
-        uint32_t* creates1 = nullptr;
+        // back on the engine stream
         IngSummary* sum1 = nullptr;
         hipStream_t pst = nullptr, dst = nullptr;  // prep (H2D + k_ing_prep) / results (D2H)
         hipEvent_t tev[8] = {};  // KWOK_INGEST_PROF: device-side phase stamps of a two-chunk batch
         hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+        hipEvent_t rdone = nullptr;  // the results stream's work of a batch (kwok_pod_rec16: before the summaries)
         size_t chunk = 1048576;
     } ing;
 
@@ -790,10 +794,12 @@ int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
     if (n > G.cap) {
         const size_t cap = std::max<size_t>(n + n / 4, 4096);
         void* ptrs[] = {G.d_ev, G.rec, G.keys, G.keys_sorted, G.idx_sorted, G.out_handle, G.out_status,
-                        G.out_released, G.sort_tmp, G.out_status8};
+                        G.out_released, G.sort_tmp, G.out_status8, G.tile_new, G.tile_pre, G.new_handle};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         G.d_ev = G.sort_tmp = nullptr;
+        G.tile_new = G.tile_pre = nullptr;
+        G.new_handle = nullptr;
         G.out_status8 = nullptr;
         G.rec = nullptr;
         G.keys = G.keys_sorted = G.idx_sorted = G.out_released = nullptr;
@@ -803,7 +809,9 @@ int ingest_reserve(kwok_engine* e, size_t n, size_t arena_len) {
         if ((rc = dalloc(e, (uint8_t**)&G.d_ev, cap * sizeof(kwok_pod_event))) || (rc = dalloc(e, &G.rec, cap)) ||
             (rc = dalloc(e, &G.keys, cap)) || (rc = dalloc(e, &G.keys_sorted, cap)) || (rc = dalloc(e, &G.idx_sorted, cap)) ||
             (rc = dalloc(e, &G.out_handle, cap)) || (rc = dalloc(e, &G.out_status, cap)) ||
-            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.out_status8, cap)))
+            (rc = dalloc(e, &G.out_released, cap)) || (rc = dalloc(e, &G.out_status8, cap)) ||
+            (rc = dalloc(e, &G.tile_new, cap / 256 + 2)) || (rc = dalloc(e, &G.tile_pre, cap / 256 + 2)) ||
+            (rc = dalloc(e, &G.new_handle, cap)))
             return rc;
         G.sort_bytes = ingest_sort_bytes((uint32_t)cap, 32);
         if ((rc = dalloc(e, (uint8_t**)&G.sort_tmp, G.sort_bytes))) return rc;
@@ -834,7 +842,6 @@ IngestBatch ingest_batch(kwok_engine* e, uint32_t n, size_t arena_len) {
     I.out_handle = G.out_handle;
     I.out_status = G.out_status;
     I.out_released = G.out_released;
-    I.creates = G.creates;
     I.beg = G.beg;
     I.end = G.end;
     I.sum = G.sum;
@@ -1046,7 +1053,8 @@ void kwok_engine_destroy(kwok_engine* e) {
     {
         auto& g = e->ing;
         void* ip[] = {g.d_ev, g.d_arena, g.rec, g.keys, g.keys_sorted, g.idx_sorted, g.out_handle, g.out_status,
-                      g.out_released, g.sort_tmp, g.creates, g.abort, g.sums, g.beg, g.end, g.sum, g.creates1, g.sum1,
+                      g.out_released, g.sort_tmp, g.abort, g.sums, g.beg, g.end, g.sum, g.sum1, g.tile_new, g.tile_pre,
+                      g.new_handle,
                       g.out_status8, g.d_nev, g.d_nnames, g.nrec, g.host_idx, g.d_nfix, g.nsum};
         for (void* p : ip)
             if (p) (void)hipFree(p);
@@ -1054,7 +1062,7 @@ void kwok_engine_destroy(kwok_engine* e) {
         if (g.nsum_h) (void)hipHostFree(g.nsum_h);
         if (g.sums_h) (void)hipHostFree(g.sums_h);
         if (g.res_h) (void)hipHostFree(g.res_h);
-        hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1]};
+        hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1], g.rdone};
         for (hipEvent_t x : evs)
             if (x) (void)hipEventDestroy(x);
         if (g.pst) (void)hipStreamDestroy(g.pst);
@@ -1344,16 +1352,15 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     {  // GPU pod ingest: per-bucket / per-node-slot scratch and the batch summary
         auto& g = e->ing;
-        if ((rc = dalloc(e, &g.creates, e->nb)) || (rc = dalloc(e, &g.abort, 1)) || (rc = dalloc(e, &g.beg, e->nb)) ||
-            (rc = dalloc(e, &g.end, e->nb)) || (rc = dalloc(e, &g.sum, 1)) || (rc = dalloc(e, &g.nsum, 1)) ||
-            (rc = dalloc(e, &g.creates1, e->nb)) || (rc = dalloc(e, &g.sum1, 1)))
+        if ((rc = dalloc(e, &g.abort, 1)) || (rc = dalloc(e, &g.beg, e->nb)) || (rc = dalloc(e, &g.end, e->nb)) ||
+            (rc = dalloc(e, &g.sum, 1)) || (rc = dalloc(e, &g.nsum, 1)) || (rc = dalloc(e, &g.sum1, 1)))
             return bail(rc);
         if (hipHostMalloc((void**)&g.sum_h, sizeof(IngSummary), hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void**)&g.nsum_h, sizeof(NodeSummary), hipHostMallocDefault) != hipSuccess)
             return bail(KWOK_ENOMEM);
         hipError_t r = hipStreamCreateWithFlags(&g.pst, hipStreamNonBlocking);
         if (r == hipSuccess) r = hipStreamCreateWithFlags(&g.dst, hipStreamNonBlocking);
-        hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1]};
+        hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1], &g.rdone};
         for (hipEvent_t* x : evs)
             if (r == hipSuccess) r = hipEventCreateWithFlags(x, hipEventDisableTiming);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "ingest stream/events: %s", hipGetErrorString(r)));
@@ -1672,17 +1679,23 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     return (int)sum.rejected;
 }
 
-// The stable sort by bucket and the apply pass of one chunk, queued on the engine
-// stream (spec: without the host's growth check; the pass then returns on the
-// device if the chunk needs growth)
-int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
+// The stable sort by bucket of one chunk and its growth check (k_ing_need counts
+// the creates in each bucket's sorted range), queued on the engine stream
+int enqueue_sort_need(kwok_engine* e, const IngestBatch& I) {
     auto& G = e->ing;
     hipStream_t st = e->st;
-    I.spec = spec ? 1u : 0u;
     if (launch_ingest_sort(e->S, I, G.sort_tmp, G.sort_bytes, sort_bits(e), st))
         return e->fail(KWOK_EDEVICE, "ingest sort");
+    launch_ingest_need(e->S, I, st);
+    HIPCHK(e, hipGetLastError());
+    return KWOK_OK;
+}
+// ... and its apply pass (spec: queued without the host's growth check; the pass
+// then returns on the device if the chunk needs growth)
+int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
+    I.spec = spec ? 1u : 0u;
     e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
-    launch_ingest_apply(e->S, I, st);
+    launch_ingest_apply(e->S, I, e->st);
     HIPCHK(e, hipGetLastError());
     return KWOK_OK;
 }
@@ -1694,10 +1707,8 @@ int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
 // chunks without it and comes here only for a chunk that needs growth.)
 int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
     auto& G = e->ing;
-    hipStream_t st = e->st;
     int rc = 0;
-    launch_ingest_need(e->S, I, st);
-    HIPCHK(e, hipGetLastError());
+    if ((rc = enqueue_sort_need(e, I))) return rc;
     if ((rc = read_summary(e, I.sum))) return rc;
     const IngSummary sum = *G.sum_h;
     // growth: every bucket to a larger capacity (up to the handle stride) when the
@@ -1722,10 +1733,12 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
 // (int32) or out_status8 (int8)
 // resident: the records (kwok_pod_event) and their arena are on the device already,
 // in the ingest buffers (kwok_ingest_pods_json decoded them there)
-int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, const char* arena, size_t arena_len,
+// packed: 0 kwok_pod_event, 1 kwok_pod_rec, 2 kwok_pod_rec16 (the creates' handles to
+// out_new[k < new_cap], in create order; out_handles unused)
+int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released,
-                     bool resident = false) {
-    const size_t RB = packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);  // record bytes
+                     bool resident = false, int32_t* out_new = nullptr, size_t new_cap = 0) {
+    const size_t RB = packed == 2 ? sizeof(kwok_pod_rec16) : packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);
     auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
     drain(e);  // the device state reflects every submitted tick
@@ -1750,7 +1763,8 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     // released its accumulator set.
     const uint32_t K = n > G.chunk ? (uint32_t)((n + G.chunk - 1) / G.chunk) : 1u;
     const double W = K > 1 ? K - 0.4 : 1.0;
-    auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W); };
+    // (chunks start at multiples of 256 records: kwok_pod_rec16's create counts are per 256-record tile)
+    auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W) & ~(size_t)255; };
     // a one-chunk batch in kwok_host_alloc memory is read in place by k_ing_prep
     // (the only kernel that reads the records and their strings): one pass over
     // the link, no copy engine (KWOK_INGEST_ZC=0: copy it to HBM first).  Chunked
@@ -1767,18 +1781,19 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             return e->fail(KWOK_ENOMEM, "ingest summaries");
         G.nsums = m;
     }
-    const bool zc_ok = e->ingest_zc && K == 1 && !resident;
+    // (kwok_pod_rec16 records are read as one 16-byte load each: in place only when aligned)
+    const bool zc_ok = e->ingest_zc && K == 1 && !resident && (packed != 2 || ((uintptr_t)recs & 15) == 0);
     const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
     auto chunk_batch = [&](uint32_t k) {
         const size_t lo = lo_of(k);
         IngestBatch b = ingest_batch(e, (uint32_t)(lo_of(k + 1) - lo), arena_len);
-        b.packed = packed ? 1u : 0u;
+        b.packed = (uint32_t)packed;
+        if (packed == 2) b.tile_new = G.tile_new, b.tile_pre = G.tile_pre, b.tile0 = (uint32_t)(lo / 256);
         b.ev = rec_at(zev ? zev : (const void*)G.d_ev, lo);
         if (zar) b.arena = (const uint8_t*)zar;
         b.rec += lo, b.keys += lo, b.keys_sorted += lo, b.idx_sorted += lo;
         b.out_handle += lo, b.out_status += lo, b.out_released += lo;
-        if (k & 1) b.creates = G.creates1;
         b.sum = G.sums + k;
         b.abort = G.abort;
         return b;
@@ -1787,7 +1802,6 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
     auto prep_on = [&](uint32_t k, hipStream_t s) -> int {
         const IngestBatch b = chunk_batch(k);
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), s));
-        HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, s));
         if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, s));
@@ -1801,7 +1815,6 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k], ps));  // 0 / 2: chunk k's copy starts
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
-        HIPCHK(e, hipMemsetAsync(b.creates, 0, (size_t)e->nb * 4, ps));
         if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
@@ -1824,6 +1837,10 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
         int32_t* ms = out_status ? (int32_t*)host_mapped(out_status + lo, (size_t)I.n * 4) : nullptr;
         int8_t* m8 = out_status8 ? (int8_t*)host_mapped(out_status8 + lo, I.n) : nullptr;
         uint32_t* mr = out_released ? (uint32_t*)host_mapped(out_released + lo, (size_t)I.n * 4) : nullptr;
+        if (packed == 2) {  // the chunk's creates' handles at their ordinals (copied back at the batch's end)
+            launch_ingest_new_handles(I, G.new_handle, (uint32_t)std::min<size_t>(new_cap, G.cap), rs);
+            HIPCHK(e, hipGetLastError());
+        }
         const bool mapped = e->results_kernel && (!out_handles || mh) && (!out_status || ms) && (!out_status8 || m8) &&
                             (!out_released || mr);
         if (mapped) {
@@ -1861,8 +1878,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
             const IngestBatch I = chunk_batch(k);
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
             if (e->debug_fail_chunk == k + 1) return e->fail(KWOK_EDEVICE, "injected failure of ingest chunk %u", k);
-            launch_ingest_need(e->S, I, st);
-            HIPCHK(e, hipGetLastError());
+            if (int r = enqueue_sort_need(e, I)) return r;
             if (int r = enqueue_apply(e, I, true)) return r;
             if (tstamp) HIPCHK(e, hipEventRecord(G.tev[4 + k], st));  // 4 / 5: chunk k applied
             // chunk k's results on the results stream; its accumulator set free for chunk k + 2
@@ -1873,6 +1889,13 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
                 if (int r2 = prep(k + 2)) return r2;
         }
         if (int r = release_for_host(e)) return r;
+        if (packed == 2) {  // the creates' handles (every chunk's), and the summaries after them (n_new)
+            HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, rs));
+            if (rs != st) {
+                HIPCHK(e, hipEventRecord(G.rdone, rs));
+                HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
+            }
+        }
         HIPCHK(e, hipMemcpyAsync(G.sums_h, G.sums, (size_t)K * sizeof(IngSummary), hipMemcpyDeviceToHost, st));
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[6], rs));  // 6: results copied
         const auto tq = clk::now();
@@ -1907,8 +1930,15 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
                 return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
             rejected += r;
             if (int r2 = results(k, st)) return r2;
+            if (packed == 2 && k + 1 == K) {
+                HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(e, hipMemcpyAsync(G.sums_h + k, G.sums + k, sizeof(IngSummary), hipMemcpyDeviceToHost, st));
+            }
             HIPCHK(e, hipStreamSynchronize(st));
         }
+        if (packed == 2 && G.sums_h[K - 1].n_new > new_cap)
+            return e->fail(KWOK_EINVAL, "kwok_ingest_pods_packed16: %u creates, out_new_handles holds %zu",
+                           G.sums_h[K - 1].n_new, new_cap);
         return rejected;
     };
     rc = run();
@@ -1929,13 +1959,20 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, bool packed, size_t n, co
 int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, uint32_t* out_released) {
     if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
-    return ingest_pods_impl(e, ev, false, n, arena, arena_len, out_handles, out_status, nullptr, out_released);
+    return ingest_pods_impl(e, ev, 0, n, arena, arena_len, out_handles, out_status, nullptr, out_released);
 }
 
 int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, int32_t* out_handles, int8_t* out_status,
                             uint32_t* out_released) {
     if (!e || (n && !recs) || n > 0x7FFFFFF0ull) return KWOK_EINVAL;
-    return ingest_pods_impl(e, recs, true, n, nullptr, 0, out_handles, nullptr, out_status, out_released);
+    return ingest_pods_impl(e, recs, 1, n, nullptr, 0, out_handles, nullptr, out_status, out_released);
+}
+
+int kwok_ingest_pods_packed16(kwok_engine* e, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+                              size_t new_cap, int8_t* out_status, uint32_t* out_released) {
+    if (!e || (n && !recs) || n > 0x7FFFFFF0ull || (new_cap && !out_new_handles)) return KWOK_EINVAL;
+    return ingest_pods_impl(e, recs, 2, n, nullptr, 0, nullptr, nullptr, out_status, out_released, false,
+                            out_new_handles, new_cap);
 }
 
 // ---- the pod codec on the GPU (json.hip) ------------------------------------
@@ -2217,7 +2254,7 @@ int kwok_ingest_pods_json(kwok_engine* e, const kwok_codec* c, const char* arena
         fprintf(stderr, "[kwok json] %zu pod documents decoded on the GPU (%u by the host): %.2f ms\n", n, nh,
                 ms_between(t0, clk::now()));
     // the event switch over the decoded records, which stayed on the device
-    return ingest_pods_impl(e, e->ing.d_ev, false, n, nullptr, arena_len, out_handles, out_status, nullptr, out_released,
+    return ingest_pods_impl(e, e->ing.d_ev, 0, n, nullptr, arena_len, out_handles, out_status, nullptr, out_released,
                             true);
 }
 

@@ -10,10 +10,10 @@
 //   k_ing_prep    one thread per record: every check that depends on the
 //                 record alone (arena bounds, IPv4 strings, spec id, phase,
 //                 creation time, handle -> owned bucket, spec.nodeName -> its
-//                 bucket), the statuses that need no state, per-bucket create
-//                 counts (growth check).
-//   k_ing_need    live pods + creates of every bucket with creates.
-//   radix sort    a stable sort of the batch by bucket (rocprim), bucket ranges.
+//                 bucket), the statuses that need no state.
+//   bucket sort   a stable counting sort of the batch by bucket, every bucket's
+//                 range (k_bs_*; rocprim's radix sort past 8191 local buckets).
+//   k_ing_need    live pods + creates of every bucket with creates (growth check).
 //   k_ing_apply   one wave per bucket, its records in event order: the slot
 //                 policy (lowest free slot, canonical), coalescing by applying
 //                 each record to the state in order, a by-name create's node
@@ -116,13 +116,22 @@ __device__ __forceinline__ bool d_in_cidr(const PoolGeom& g, uint32_t ip) {
 // every status that does not depend on state.  keys[i] = the owned local bucket
 // whose records the apply pass takes in order, or nb (decided here).
 // ---------------------------------------------------------------------------
-// The compact record (kwok_pod_rec): its strings were parsed by the caller, so
-// only the checks on values remain; a create names its node by handle.
-__device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i) {
-    const uint8_t* p = static_cast<const uint8_t*>(I.ev) + (size_t)i * sizeof(kwok_pod_rec);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);  // 20 bytes: five dwords
-    const uint32_t w0 = w[0], ctime = w[2], hip = w[3], pip = w[4];
-    const int32_t target = (int32_t)w[1];
+// The compact records (kwok_pod_rec, kwok_pod_rec16): their strings were parsed
+// by the caller, so only the checks on values remain; a create names its node by
+// handle.  kwok_pod_rec16 carries no hostIP word: KWOK_REC_HOST_NODE_IP stands
+// for the engine's node_ip.  Returns whether the record is a KWOK_REC_NEW one.
+__device__ bool prep_packed(const DevState& S, const IngestBatch& I, uint32_t i) {
+    uint32_t w0, ctime, hip, pip;
+    int32_t target;
+    if (I.packed == 2) {
+        const uint4 v = reinterpret_cast<const uint4*>(I.ev)[i];  // 16 bytes: one load
+        w0 = v.x, target = (int32_t)v.y, ctime = v.z, pip = v.w;
+        hip = (w0 & KWOK_REC_HOST_NODE_IP) ? S.node_ip : 0u;
+        w0 &= ~KWOK_REC_HOST_NODE_IP;
+    } else {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(I.ev) + (size_t)i * sizeof(kwok_pod_rec));
+        w0 = w[0], target = (int32_t)w[1], ctime = w[2], hip = w[3], pip = w[4];  // 20 bytes: five dwords
+    }
     const uint32_t op = w0 & 0x7Fu, create = w0 & KWOK_REC_NEW, fl = (w0 >> 8) & 0xFFu, spec = w0 >> 16;
     PodRec r;
     r.bucket = REC_NONE;
@@ -136,7 +145,8 @@ __device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i)
     r.chk = 0;
     r.fst = KWOK_OK;
     r.pst = KWOK_OK;
-    r.pad[0] = r.pad[1] = r.pad[2] = r.pad[3] = 0;
+    r.is_new = create ? 1 : 0;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
     int st = 1;  // 1: the apply pass decides
     if (op == KWOK_OP_DELETE) {
         if (pip) r.pip = pip, r.chk |= REC_DEL_IP;
@@ -162,7 +172,6 @@ __device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i)
         if (l >= 0 && l < (int64_t)S.n_node_slots) r.bucket = (uint32_t)(l / S.cn), r.pos = (uint32_t)(l % S.cn);
         else st = KWOK_ENOTMINE;
     }
-    if (st == 1 && op == KWOK_OP_UPSERT && create) atomicAdd(&I.creates[r.bucket], 1u);
     I.rec[i] = r;
     I.keys[i] = st == 1 ? r.bucket : S.nb;
     if (st != 1) {
@@ -171,15 +180,20 @@ __device__ void prep_packed(const DevState& S, const IngestBatch& I, uint32_t i)
         I.out_released[i] = 0;
         if (st != KWOK_OK) atomicAdd(&I.sum->rejected, 1u);
     }
+    return create != 0;
 }
 
 __global__ void k_ing_prep(DevState S, IngestBatch I) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= I.n) return;
     if (I.packed) {
-        prep_packed(S, I, i);
+        const bool nw = i < I.n && prep_packed(S, I, i);
+        if (I.tile_new) {  // kwok_pod_rec16: the block's creates (blocks are the batch's 256-record tiles)
+            const int c = __syncthreads_count(nw);
+            if (threadIdx.x == 0) I.tile_new[I.tile0 + blockIdx.x] = (uint32_t)c;
+        }
         return;
     }
+    if (i >= I.n) return;
     const kwok_pod_event x = static_cast<const kwok_pod_event*>(I.ev)[i];
     PodRec r;
     r.bucket = REC_NONE;
@@ -193,7 +207,8 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
     r.chk = 0;
     r.fst = KWOK_OK;
     r.pst = KWOK_OK;
-    r.pad[0] = r.pad[1] = r.pad[2] = r.pad[3] = 0;
+    r.is_new = 0;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
     int st = 1;  // 1: the apply pass decides
     auto in_arena = [&](kwok_str s) { return (uint64_t)s.off + s.len <= I.arena_len; };
     if (x.reserved0) {
@@ -238,8 +253,6 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
                 else r.bucket = b - S.b_lo, atomicAdd(&I.sum->n_byname, 1u);
             }
         }
-        // growth check: creates per bucket (an upper bound: the batch's deletes are not netted out)
-        if (st == 1 && x.op == KWOK_OP_UPSERT && x.handle < 0) atomicAdd(&I.creates[r.bucket], 1u);
     }
     I.rec[i] = r;
     I.keys[i] = st == 1 ? r.bucket : S.nb;
@@ -252,23 +265,42 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
 }
 
 // ---------------------------------------------------------------------------
-// k_ing_need: one wave per bucket with creates: live pods (USED below the fill
-// mark) + creates -> the batch's growth need (max over buckets)
-// ---------------------------------------------------------------------------
+// k_ing_need: one wave per bucket, after the sort: the creates among the
+// bucket's records (an UPSERT without a handle) + its live pods (USED below the
+// fill mark) -> the batch's growth need (max over buckets with creates; an upper
+// bound: the batch's deletes are not netted out).  (Counting the creates here
+// instead of with a global atomic per create in k_ing_prep: 0.5M creates over
+// 4096 counters held the prep ~40 us.)
 __global__ void k_ing_need(DevState S, IngestBatch I) {
     const uint32_t b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (b >= S.nb) return;
-    const uint32_t c = I.creates[b];
-    if (!c) return;
-    const uint32_t fill = S.pod_fill[b];
-    const uint16_t* ps = S.pod_state + (size_t)b * S.cp;
-    uint32_t live = 0;
-    for (uint32_t s = lane(); s < fill; s += 64) live += ps[s] & PS_USED;
-    for (int o = 32; o; o >>= 1) live += (uint32_t)__shfl_xor((int)live, o);
-    if (lane() == 0) {
-        atomicMax(&I.sum->need, live + c);
-        I.creates[b] = 0;  // zero for the next batch
+    const uint32_t pbeg = I.beg[b], pend = I.end[b];
+    if (!(pbeg < pend && pend <= I.n && I.keys_sorted[pbeg] == b)) return;  // (a stale range: not this batch's)
+    uint32_t c = 0;
+    for (uint32_t p = pbeg + lane(); p < pend; p += 64) {
+        const PodRec& r = I.rec[I.idx_sorted[p]];
+        c += r.op == KWOK_OP_UPSERT && !(r.chk & REC_EXISTING);
     }
+    for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if (!c) return;
+    // live pods: the bucket's state words below the fill mark, 8 per lane-load
+    const uint32_t fill = S.pod_fill[b];
+    const uint16_t* ps = S.pod_state + (size_t)b * S.cp;  // (cp and fill are multiples of 8: 16-byte aligned rows)
+    uint32_t live = 0;
+    for (uint32_t s0 = lane() * 8; s0 < fill; s0 += 64 * 8 * 4) {
+        uint4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            v[q] = s0 + q * 512 < fill ? *reinterpret_cast<const uint4*>(ps + s0 + q * 512) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) live += (w[j] & PS_USED) + ((w[j] >> 16) & PS_USED);
+        }
+    }
+    for (int o = 32; o; o >>= 1) live += (uint32_t)__shfl_xor((int)live, o);
+    if (lane() == 0) atomicMax(&I.sum->need, live + c);
 }
 
 // bucket ranges of the sorted batch: beg / end (zeroed before: empty buckets are [0, 0))
@@ -1086,12 +1118,217 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// The stable sort by bucket: a counting sort over the batch's keys (local
+// buckets 0..nb, nb = nothing to apply), in tiles of BS_TILE records.
+//   k_bs_hist     per tile: its key counts (LDS histogram) -> hist[tile][key]
+//   k_bs_cols     per key: the exclusive prefix over the tiles, in place; the total
+//   k_bs_base     one block: the exclusive scan of the totals (each key's first
+//                 sorted position) and every bucket's range [beg, end)
+//   k_bs_scatter  one wave per tile, its records in order, 64 at a time: the
+//                 lanes of a key (13 ballots) take consecutive positions after the
+//                 key's running count in LDS -> idx_sorted, keys_sorted
+// Four small launches instead of rocPRIM's radix sort, which on these batches
+// (12-bit keys, 0.7-1.3M records) ran the onesweep path at ~75 us or its block
+// merge sort path at ~120 us (17 launches).  Every bucket's range is written, so
+// no range of an earlier batch survives (k_ing_ranges / k_nd_ranges are not run).
+// ---------------------------------------------------------------------------
+constexpr uint32_t BS_TILE = 4096;
+constexpr uint32_t BS_MAX_KEYS = 8192;  // LDS: 32 KB of counts (+ 16 KB of a tile's keys) per block
+struct BucketSort {
+    const uint32_t* keys;
+    uint32_t n, nk;         // records, keys (nb + 1)
+    uint32_t* hist;         // [tiles][nk]
+    uint32_t* tot;          // [nk] totals, then each key's base
+    uint32_t* keys_sorted;
+    uint32_t* idx_sorted;
+    uint32_t* beg;          // [nk - 1] bucket ranges
+    uint32_t* end;
+};
+__global__ void k_bs_hist(BucketSort B) {
+    extern __shared__ uint32_t h[];
+    const uint32_t t = blockIdx.x;
+    for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) atomicAdd(&h[B.keys[i]], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) B.hist[(size_t)t * B.nk + k] = h[k];
+}
+// 64 keys per block, their tiles in 16 groups (one wave each): every thread sums
+// its group's counts (loads in flight together), the groups' sums are scanned in
+// LDS, and the thread writes its group's exclusive prefixes
+constexpr uint32_t BS_GROUPS = 16;
+__global__ void k_bs_cols(BucketSort B, uint32_t tiles) {
+    __shared__ uint32_t gs[BS_GROUPS][64];
+    const uint32_t k = blockIdx.x * 64 + lane(), g = threadIdx.x >> 6;
+    const uint32_t tpg = (tiles + BS_GROUPS - 1) / BS_GROUPS;
+    const uint32_t t0 = min(g * tpg, tiles), t1 = min(t0 + tpg, tiles);
+    const bool ok = k < B.nk;
+    constexpr uint32_t R = 16;  // a group's counts held in registers (tiles <= 256: 1M records)
+    uint32_t v[R], sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < R; q++) v[q] = ok && t0 + q < t1 ? B.hist[(size_t)(t0 + q) * B.nk + k] : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < R; q++) sum += v[q];
+    if (ok)
+        for (uint32_t t = t0 + R; t < t1; t++) sum += B.hist[(size_t)t * B.nk + k];
+    gs[g][lane()] = sum;
+    __syncthreads();
+    uint32_t run = 0, all = 0;
+    for (uint32_t q = 0; q < BS_GROUPS; q++) {
+        const uint32_t x = gs[q][lane()];
+        run += q < g ? x : 0u;
+        all += x;
+    }
+    if (!ok) return;
+#pragma unroll
+    for (uint32_t q = 0; q < R; q++)
+        if (t0 + q < t1) {
+            B.hist[(size_t)(t0 + q) * B.nk + k] = run;
+            run += v[q];
+        }
+    for (uint32_t t = t0 + R; t < t1; t++) {
+        const uint32_t x = B.hist[(size_t)t * B.nk + k];
+        B.hist[(size_t)t * B.nk + k] = run;
+        run += x;
+    }
+    if (g == 0) B.tot[k] = all;
+}
+__global__ void k_bs_base(BucketSort B) {
+    __shared__ uint32_t wsum[16];
+    constexpr uint32_t PER = BS_MAX_KEYS / 1024;  // keys per thread (blockDim 1024)
+    const uint32_t k0 = threadIdx.x * PER;
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) v[q] = k0 + q < B.nk ? B.tot[k0 + q] : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) s += v[q];
+    // block exclusive scan of the per-thread sums (1024 threads = 16 waves)
+    uint32_t x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane() >= (uint32_t)o) x += y;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane() == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = x - s;
+    for (uint32_t q = 0; q < w; q++) pre += wsum[q];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t k = k0 + q;
+        if (k < B.nk) {
+            B.tot[k] = pre;
+            if (k + 1 < B.nk) {
+                B.beg[k] = pre;
+                B.end[k] = pre + v[q];
+            }
+        }
+        pre += v[q];
+    }
+}
+__global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
+    extern __shared__ uint32_t cnt[];  // [nk] running positions, then the tile's keys [BS_TILE]
+    uint32_t* tk = cnt + B.nk;
+    const uint32_t t = blockIdx.x;
+    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
+    // every wave stages (the loads of a thread in flight together)
+    for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) cnt[k] = B.tot[k] + B.hist[(size_t)t * B.nk + k];
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) tk[i - i0] = B.keys[i];
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    // wave 0: the tile's records in order, 64 at a time
+    const uint64_t lt = (1ull << lane()) - 1ull;
+    for (uint32_t r = i0; r < i1; r += 64) {
+        const uint32_t i = r + lane();
+        const bool valid = i < i1;
+        const uint32_t key = valid ? tk[i - i0] : 0u;
+        uint64_t m = __ballot(valid);
+        for (uint32_t b = 0; b < key_bits; b++) {
+            const uint64_t ones = __ballot((key >> b) & 1u);
+            m &= ((key >> b) & 1u) ? ones : ~ones;
+        }
+        if (valid) {
+            const uint32_t c = cnt[key];
+            const uint32_t pos = c + (uint32_t)__popcll(m & lt);
+            B.idx_sorted[pos] = i;
+            B.keys_sorted[pos] = key;
+            if ((m >> lane()) == 1ull) cnt[key] = c + (uint32_t)__popcll(m);  // the key's last lane
+        }
+        lds_sync();
+    }
+}
+size_t bucket_sort_bytes(uint32_t n, uint32_t nk) { return ((size_t)((n + BS_TILE - 1) / BS_TILE) * nk + nk + 64) * 4; }
+bool bucket_sort(const uint32_t* keys, uint32_t n, uint32_t nk, uint32_t* keys_sorted, uint32_t* idx_sorted, uint32_t* beg,
+                 uint32_t* end, void* tmp, size_t tmp_bytes, hipStream_t st) {
+    if (nk > BS_MAX_KEYS || bucket_sort_bytes(n, nk) > tmp_bytes) return false;
+    const uint32_t tiles = (n + BS_TILE - 1) / BS_TILE;
+    uint32_t bits = 1;
+    while ((1u << bits) < nk) bits++;
+    BucketSort B{keys, n, nk, static_cast<uint32_t*>(tmp), static_cast<uint32_t*>(tmp) + (size_t)tiles * nk, keys_sorted,
+                 idx_sorted, beg, end};
+    hipLaunchKernelGGL(k_bs_hist, dim3(tiles), dim3(256), nk * 4, st, B);
+    hipLaunchKernelGGL(k_bs_cols, dim3((nk + 63) / 64), dim3(64 * BS_GROUPS), 0, st, B, tiles);
+    hipLaunchKernelGGL(k_bs_base, dim3(1), dim3(1024), 0, st, B);
+    hipLaunchKernelGGL(k_bs_scatter, dim3(tiles), dim3(256), (nk + BS_TILE) * 4, st, B, bits);
+    return true;
+}
+
 size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits) {
     size_t bytes = 0;
     rocprim::counting_iterator<uint32_t> it(0u);
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, it,
                                     (uint32_t*)nullptr, n, 0u, key_bits);
-    return bytes;
+    return std::max(bytes, bucket_sort_bytes(n, BS_MAX_KEYS));
+}
+
+// kwok_pod_rec16's create handles.  k_ing_tile_scan (one block): the exclusive
+// prefixes of the NEW counts of the batch's tiles [0, ntiles) and their total;
+// k_ing_new_handles (a block per tile of the chunk): each create's ordinal = its
+// tile's prefix + the creates before it in the tile.
+__global__ void k_ing_tile_scan(IngestBatch I, uint32_t ntiles) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t per = (ntiles + blockDim.x - 1) / blockDim.x;
+    const uint32_t t0 = min(threadIdx.x * per, ntiles), t1 = min(t0 + per, ntiles);
+    uint32_t s = 0;
+    for (uint32_t t = t0; t < t1; t++) s += I.tile_new[t];
+    uint32_t x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane() >= (uint32_t)o) x += y;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane() == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t pre = x - s, all = 0;
+    for (uint32_t q = 0; q < blockDim.x / 64; q++) {
+        pre += q < w ? wsum[q] : 0u;
+        all += wsum[q];
+    }
+    for (uint32_t t = t0; t < t1; t++) {
+        I.tile_pre[t] = pre;
+        pre += I.tile_new[t];
+    }
+    if (threadIdx.x == 0) I.sum->n_new = all;
+}
+__global__ void k_ing_new_handles(IngestBatch I, int32_t* dst, uint32_t cap) {
+    __shared__ uint32_t wc[4];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool nw = i < I.n && I.rec[i].is_new;
+    const uint64_t m = __ballot(nw);
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane() == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (!nw) return;
+    uint32_t ord = I.tile_pre[I.tile0 + blockIdx.x] + (uint32_t)__popcll(m & ((1ull << lane()) - 1ull));
+    for (uint32_t q = 0; q < w; q++) ord += wc[q];
+    if (ord < cap) dst[ord] = I.out_handle[i];
+}
+void launch_ingest_new_handles(const IngestBatch& I, int32_t* new_handles, uint32_t cap, hipStream_t st) {
+    const uint32_t tiles = cdiv(I.n, 256);
+    hipLaunchKernelGGL(k_ing_tile_scan, dim3(1), dim3(1024), 0, st, I, I.tile0 + tiles);
+    if (I.n) hipLaunchKernelGGL(k_ing_new_handles, dim3(tiles), dim3(256), 0, st, I, new_handles, cap);
 }
 
 __global__ void k_ing_status8(IngestBatch I, int8_t* dst) {
@@ -1120,6 +1357,7 @@ void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* stat
     if (I.n) hipLaunchKernelGGL(k_ing_results, dim3(cdiv(I.n, 1024)), dim3(256), 0, st, I, handles, status, status8, released);
 }
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st) {
+    // (256-record blocks: kwok_pod_rec16's create counts are per 256-record tile)
     if (I.n) hipLaunchKernelGGL(k_ing_prep, dim3(cdiv(I.n, 256)), dim3(256), 0, st, S, I);
 }
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st) {
@@ -1128,6 +1366,7 @@ void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st)
 int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_t tmp_bytes, uint32_t key_bits,
                        hipStream_t st) {
     if (!I.n) return 0;
+    if (bucket_sort(I.keys, I.n, S.nb + 1, I.keys_sorted, I.idx_sorted, I.beg, I.end, tmp, tmp_bytes, st)) return 0;
     rocprim::counting_iterator<uint32_t> it(0u);
     if (rocprim::radix_sort_pairs(tmp, tmp_bytes, I.keys, I.keys_sorted, it, I.idx_sorted, I.n, 0u, key_bits, st) !=
         hipSuccess)
@@ -1147,6 +1386,7 @@ void launch_node_fix(const DevState& S, const NodeBatch& N, const NodeFix* fix, 
 int launch_node_sort(const DevState& S, const NodeBatch& N, void* tmp, size_t tmp_bytes, uint32_t key_bits,
                      hipStream_t st) {
     if (!N.n) return 0;
+    if (bucket_sort(N.keys, N.n, S.nb + 1, N.keys_sorted, N.idx_sorted, N.beg, N.end, tmp, tmp_bytes, st)) return 0;
     rocprim::counting_iterator<uint32_t> it(0u);
     if (rocprim::radix_sort_pairs(tmp, tmp_bytes, N.keys, N.keys_sorted, it, N.idx_sorted, N.n, 0u, key_bits, st) !=
         hipSuccess)

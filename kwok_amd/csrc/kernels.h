@@ -170,7 +170,7 @@ struct IngestBatch {
     const void* ev;            // [n] kwok_pod_event (packed: kwok_pod_rec), on the device or read in place
     uint32_t n;
     uint32_t n_specs;
-    uint32_t packed;           // 1: kwok_pod_rec records (no arena)
+    uint32_t packed;           // 1: kwok_pod_rec records (no arena); 2: kwok_pod_rec16
     uint32_t spec;             // the apply pass was queued without the host's growth check: it returns at once
                                // when the chunk needs more pod slots than a bucket has (sum->need > cp) or an
                                // earlier chunk of the batch did (*abort), setting *abort (the host redoes them)
@@ -183,13 +183,19 @@ struct IngestBatch {
     int32_t* out_handle;       // [n]
     int32_t* out_status;       // [n]
     uint32_t* out_released;    // [n]
-    uint32_t* creates;         // [nb] creates per bucket (growth check)
     uint32_t* beg;             // [nb] first sorted position of each bucket
     uint32_t* end;             // [nb]
     IngSummary* sum;
     uint32_t* abort;           // [1] per batch (spec)
+    // kwok_pod_rec16: handles of the creates only.  The chunk starts at a multiple of
+    // 256 records; k_ing_prep counts the KWOK_REC_NEW records of each 256-record tile
+    // of the batch (tile_new[tile0 + block]), k_ing_new_handles writes their handles
+    // at their ordinals among the batch's creates (tile_pre: the tiles' prefixes)
+    uint32_t* tile_new;
+    uint32_t* tile_pre;
+    uint32_t tile0;
 };
-size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // rocprim radix sort temporary storage
+size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits);  // the bucket sort's (or rocprim's) temporary storage
 // prep (+ growth counts) for every record
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st);
 // the batch's per-record statuses as bytes (kwok_ingest_pods_packed's out_status)
@@ -197,7 +203,10 @@ void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st);
 // the per-record results written into mapped host arrays (device addresses of kwok_host_alloc memory; null: skip)
 void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* status, int8_t* status8, uint32_t* released,
                            hipStream_t st);
-// live pods + creates of every bucket with creates -> sum->need
+// kwok_pod_rec16: the chunk's creates' handles at their ordinals in new_handles (< cap),
+// after scanning the NEW counts of the batch's tiles up to the chunk's last (sum->n_new)
+void launch_ingest_new_handles(const IngestBatch& I, int32_t* new_handles, uint32_t cap, hipStream_t st);
+// after the sort: live pods + creates of every bucket with creates -> sum->need
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st);
 // stable sort by bucket, bucket ranges
 int launch_ingest_sort(const DevState& S, const IngestBatch& I, void* tmp, size_t tmp_bytes, uint32_t key_bits,

@@ -340,30 +340,61 @@ __device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb,
 struct PoolPlan {
     uint64_t U, Fin, take, fin, fout, fout0;
 };
-// every block derives the same plan from the per-word-block counts
-__device__ __forceinline__ PoolPlan pool_plan(const DevState& S, uint64_t A, uint32_t nwb, uint32_t upto, uint64_t* bu, uint64_t* bf) {
-    __shared__ uint64_t sh[4];
-    if (threadIdx.x < 64) {
-        uint64_t u = 0, fr = 0, pu = 0, pf = 0;
-        for (uint32_t i = threadIdx.x; i < nwb; i += 64) {
-            uint64_t a = S.pool_blk[2 * i], c = S.pool_blk[2 * i + 1];
-            u += a;
-            fr += c;
-            if (i < upto) pu += a, pf += c;
-        }
-        u = wave_sum64(u);
-        fr = wave_sum64(fr);
-        pu = wave_sum64(pu);
-        pf = wave_sum64(pf);
-        if (threadIdx.x == 0) sh[0] = u, sh[1] = fr, sh[2] = pu, sh[3] = pf;
+// The word-block counts' prefixes, read once per block: thread t sums its chunk
+// [t * per, +per) of the counts, the chunk sums are scanned over the block into
+// LDS and the totals returned; a word-block's prefix is then its chunk's plus
+// the counts before it inside the chunk (pool_prefix).  (Reading every count
+// per selected word-block cost the /4 pool of an 8-rank fleet - 4096 word-blocks,
+// 8 per chain block - a serial 64-step loop per word-block.)
+struct PoolPre {
+    uint64_t U, Fin;
+    uint32_t per;
+};
+__device__ __forceinline__ PoolPre pool_scan(const DevState& S, uint32_t nwb, uint64_t (&cp)[2][BLOCK]) {
+    __shared__ uint64_t ws[BLOCK / 64][2];
+    const uint32_t per = (nwb + BLOCK - 1) / BLOCK;
+    const uint32_t i0 = min(threadIdx.x * per, nwb), i1 = min(i0 + per, nwb);
+    uint64_t v[2] = {0, 0};
+#pragma unroll 8
+    for (uint32_t i = i0; i < i1; i++) v[0] += S.pool_blk[2 * i], v[1] += S.pool_blk[2 * i + 1];
+    const int l = lane_id(), w = wave_id();
+    uint64_t incl[2];
+#pragma unroll
+    for (int f = 0; f < 2; f++) {
+        incl[f] = wave_incl_scan64(v[f]);
+        if (l == 63) ws[w][f] = incl[f];
     }
     __syncthreads();
-    PoolPlan p;
-    p.U = sh[0];
-    p.Fin = sh[1];
-    *bu = sh[2];
-    *bf = sh[3];
+    uint64_t tot[2];
+#pragma unroll
+    for (int f = 0; f < 2; f++) {
+        uint64_t pre = 0, t = 0;
+#pragma unroll
+        for (int k = 0; k < BLOCK / 64; k++) {
+            const uint64_t s = ws[k][f];
+            pre += k < w ? s : 0ull;
+            t += s;
+        }
+        cp[f][threadIdx.x] = pre + incl[f] - v[f];
+        tot[f] = t;
+    }
     __syncthreads();
+    return PoolPre{tot[0], tot[1], per};
+}
+// usable / free bits of the word-blocks before wb (uniform)
+__device__ __forceinline__ void pool_prefix(const DevState& S, const PoolPre& q, const uint64_t (&cp)[2][BLOCK], uint32_t wb,
+                                            uint64_t* bu, uint64_t* bf) {
+    const uint32_t o = wb / q.per;
+    uint64_t u = 0, f = 0;
+    for (uint32_t i = o * q.per + lane_id(); i < wb; i += 64) u += S.pool_blk[2 * i], f += S.pool_blk[2 * i + 1];
+    *bu = cp[0][o] + wave_sum64(u);
+    *bf = cp[1][o] + wave_sum64(f);
+}
+// every block derives the same plan from the totals
+__device__ __forceinline__ PoolPlan pool_plan(const DevState& S, uint64_t A, const PoolPre& q) {
+    PoolPlan p;
+    p.U = q.U;
+    p.Fin = q.Fin;
     p.take = A < p.U ? A : p.U;
     const uint64_t F = A - p.take;
     p.fin = F < p.Fin ? F : p.Fin;
@@ -1732,15 +1763,17 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
         TSTAMP(9);
         if (A) {
             uint64_t cursor = ~0ull;
+            __shared__ uint64_t cp[2][BLOCK];
+            const PoolPre q = pool_scan(S, nwb, cp);
+            plan = pool_plan(S, A, q);
             for (uint32_t wb = pidx; wb < nwb; wb += np) {
                 uint64_t bu, bf;
-                plan = pool_plan(S, A, nwb, wb, &bu, &bf);
+                pool_prefix(S, q, cp, wb, &bu, &bf);
+                // every Get is taken before this word-block (and so before the block's later
+                // ones): nothing to select from here on (a pool much larger than the fleet)
+                if (bu >= plan.take && bf >= plan.fin) break;
                 pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor,
                                    wb == pidx ? &pw : nullptr);
-            }
-            if (pidx >= nwb) {
-                uint64_t bu, bf;
-                plan = pool_plan(S, A, nwb, 0, &bu, &bf);
             }
             // ipPool.index after the last fresh address (committed after the barrier)
             if (cursor != ~0ull) H->cursor_index = cursor;

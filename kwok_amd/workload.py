@@ -177,7 +177,8 @@ class Churn:
                  creation=S0 - 60, first=0, alloc=None, packed=False):
         self.first = first
         # packed: the batch as kwok_pod_rec (kwok_ingest_pods_packed: 20 B per record,
-        # IPs as integers, nodes by handle) instead of kwok_pod_event + dotted quads
+        # IPs as integers, nodes by handle) instead of kwok_pod_event + dotted quads;
+        # packed=16: as kwok_pod_rec16 (kwok_ingest_pods_packed16: 16 B, hostIP by flag)
         self.packed = packed
         # alloc(shape, dtype): the batch is written into (and reused from) these
         # buffers - e.g. page-locked host memory (engine.host_array), which the
@@ -244,23 +245,26 @@ class Churn:
         return ev, arena
 
     def _batch_packed(self, D, dead, loc, phase, pip, now):
+        r16 = self.packed == 16
+        dt = abi.POD_REC16_DTYPE if r16 else abi.POD_REC_DTYPE
         if self.alloc is None:
-            ev = np.zeros(2 * D, abi.POD_REC_DTYPE)
+            ev = np.zeros(2 * D, dt)
         else:
-            if self.bufs is None or len(self.bufs[0]) < 2 * D:
-                self.bufs = (self.alloc((2 * self.n,), abi.POD_REC_DTYPE),)
+            if self.bufs is None or len(self.bufs[0]) < 2 * D or self.bufs[0].dtype != dt:
+                self.bufs = (self.alloc((2 * self.n,), dt),)
             ev = self.bufs[0][:2 * D]
         d = ev[:D]
         running = phase[loc] == abi.PHASE_RUNNING
         fin = np.where(self.rng.random(D) < 0.5, abi.POD_HAS_FINALIZERS, 0)
-        d["op"] = abi.OP_UPSERT
+        d["op"] = abi.OP_UPSERT | np.where(running, abi.REC_HOST_NODE_IP, 0) if r16 else abi.OP_UPSERT
         d["target"] = dead
         d["spec_id"] = self.spec
         d["creation"] = self.ctime[loc]
         d["flags"] = ((abi.POD_DELETING | fin | np.where(running, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
                        | np.where(pip[loc] != 0, abi.POD_STATUS_NONEMPTY, 0))
                       | (phase[loc].astype(np.int64) << abi.REC_PHASE_SHIFT))
-        d["host_ip"] = np.where(running, abi.ip4(self.node_ip.decode()), 0)
+        if not r16:
+            d["host_ip"] = np.where(running, abi.ip4(self.node_ip.decode()), 0)
         d["pod_ip"] = pip[loc]
         c = ev[D:]
         c["op"] = abi.OP_UPSERT | abi.REC_NEW
@@ -268,16 +272,18 @@ class Churn:
         c["spec_id"] = self.spec
         c["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
         c["creation"] = now - 5
-        c["host_ip"] = 0
+        if not r16:
+            c["host_ip"] = 0
         c["pod_ip"] = 0
         self._pending = (D, c["target"].copy(), now - 5)
         return ev
 
-    def applied(self, handles, status):
-        """account the ingest result of the last batch"""
+    def applied(self, handles, status, new_only=False):
+        """account the ingest result of the last batch (new_only: handles are the
+        creates' only, kwok_ingest_pods_packed16)"""
         D, nodes, ct = self._pending
         assert (status == 0).all(), "churn batch rejected: %s" % np.unique(status[status != 0])
-        new = handles[D:]
+        new = handles[:D] if new_only else handles[D:]
         self.node_of[new - self.first] = nodes
         self.ctime[new - self.first] = ct
         self.live = np.concatenate([self.live[D:], new])

@@ -798,6 +798,40 @@ int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, siz
     return rc < 0 ? rc : bad;
 }
 
+/* kwok_ingest_pods_packed16: each record as the kwok_pod_rec it stands for
+ * (KWOK_REC_HOST_NODE_IP: hostIP = the configured NodeIP), through the packed
+ * path; the handles of the KWOK_REC_NEW records only, in create order */
+int kwok_oracle_ingest_pods_packed16(kwok_oracle* o, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+                                     size_t new_cap, int8_t* out_status, uint32_t* out_released) {
+    kwok_pod_rec* r = (kwok_pod_rec*)calloc(n + 1, sizeof(kwok_pod_rec));
+    int32_t* hs = (int32_t*)calloc(n + 1, sizeof(int32_t));
+    if (!r || !hs) {
+        free(r), free(hs);
+        return KWOK_ENOMEM;
+    }
+    for (size_t i = 0; i < n; i++) {
+        r[i].op = recs[i].op & (uint8_t)~KWOK_REC_HOST_NODE_IP;
+        r[i].flags = recs[i].flags;
+        r[i].spec_id = recs[i].spec_id;
+        r[i].target = recs[i].target;
+        r[i].creation = recs[i].creation;
+        r[i].host_ip = (recs[i].op & KWOK_REC_HOST_NODE_IP) ? o->node_ip : 0;
+        r[i].pod_ip = recs[i].pod_ip;
+    }
+    int rc = kwok_oracle_ingest_pods_packed(o, r, n, hs, out_status, out_released);
+    if (rc >= 0) {
+        size_t k = 0;
+        for (size_t i = 0; i < n; i++)
+            if (recs[i].op & KWOK_REC_NEW) {
+                if (k < new_cap) out_new_handles[k] = hs[i];
+                k++;
+            }
+        if (k > new_cap) rc = KWOK_EINVAL;
+    }
+    free(r), free(hs);
+    return rc;
+}
+
 static inline int keep_eval(const kwok_oracle* o, size_t h);
 /* EnableCNI: the pods the next tick evaluates without a podIP (configurePod's
  * cni.Setup set, pod_controller.go:383-389), canonical order */

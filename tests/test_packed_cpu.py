@@ -79,3 +79,39 @@ def test_packed_create_without_node_handle_is_rejected_per_record():
     hs, st, rel = o.ingest_pods_packed(recs)
     assert list(st) == [abi.EINVAL, abi.EINVAL] and list(hs) == [-1, -1]
     o.close()
+
+
+def test_packed16_on_the_oracle():
+    """kwok_pod_rec16 (16 B: the hostIP as a flag for the node IP) on the oracle
+    against kwok_pod_rec on a twin: the same statuses and releases, the creates'
+    handles in create order (-1 for a rejected one), a create count above
+    new_cap fails with KWOK_EINVAL after the batch is applied"""
+    fx = harness.load_trace("doc_known_answer")
+    cfg = harness.config_for(fx)
+    o1, o2 = Oracle(cfg), Oracle(harness.config_for(fx))
+    node_ip = o1.node_ip
+    for o in (o1, o2):
+        o.register_pod_spec([("c", "img")])
+    recs, arena = harness.node_batch([{"op": "add", "name": "n0", "managed": True, "lockable": True},
+                                      {"op": "add", "name": "n1", "managed": True, "lockable": True}])
+    nh1, _ = o1.ingest_nodes_raw(recs, arena)
+    o2.ingest_nodes_raw(recs, arena)
+    r = np.zeros(6, abi.POD_REC_DTYPE)
+    r["op"] = abi.OP_UPSERT | abi.REC_NEW
+    r["target"] = [nh1[0], nh1[1], -1, nh1[0], nh1[1], nh1[0]]
+    r["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
+    r["creation"] = fx["config"]["start_time"]
+    r["host_ip"][3] = node_ip
+    h2, s2, rel2 = o2.ingest_pods_packed(r)
+    r16 = abi.pack16(r, node_ip)
+    assert r16["op"][3] & abi.REC_HOST_NODE_IP and not r16["op"][0] & abi.REC_HOST_NODE_IP
+    nh, s1, rel1 = o1.ingest_pods_packed16(r16)
+    assert (s1 == s2).all() and (rel1 == rel2).all() and (nh == h2).all() and nh[2] == -1
+    m = np.zeros(2, abi.POD_REC16_DTYPE)
+    m["op"] = [abi.OP_UPSERT, abi.OP_UPSERT | abi.REC_NEW]
+    m["target"] = [nh[0], nh1[0]]
+    m["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
+    with pytest.raises(RuntimeError):
+        o1.ingest_pods_packed16(m, new_cap=0)
+    o1.close()
+    o2.close()
