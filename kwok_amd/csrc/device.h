@@ -68,7 +68,7 @@ constexpr int NODE_PRE = KWOK_NODE_PRE;   // node chunks of a chain block loaded
 constexpr int WC_GROUPS = 64;
 constexpr int MAX_WC = MAX_POD_CHUNKS * BLOCK / WC_GROUPS;  // 256 wave chunks per chain block
 constexpr int WC_DIRTY_WORDS = MAX_WC / 32;
-constexpr int TRACE_SLOTS = 16;         // KWOK_TICK_TRACE=1: per-block phase stamps
+constexpr int TRACE_SLOTS = 24;         // KWOK_TICK_TRACE=1: per-block phase stamps
 constexpr int SPEC_LDS = 256;           // k_tick caches the reservations of up to this many specs
 
 // ---- fixed template geometry (default templates) -----------------------------

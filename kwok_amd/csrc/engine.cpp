@@ -1026,7 +1026,10 @@ void kwok_engine_destroy(kwok_engine* e) {
     if (e->trace_ticks) {
         static const char* names[TRACE_SLOTS] = {"entry", "nodes-done", "pods-done", "arrived", "reduced", "pool-done",
                                                  "exit", "header-done", "node-flags", "pool-folded", "block-sum",
-                                                 "drained", "hb-handles", "share-done", "nodes-emitted", "back-start"};
+                                                 "drained", "hb-handles", "share-done", "nodes-emitted", "back-start",
+                                                 // tick_back's pool phase (multi rank: the BACK launch)
+                                                 "B-entry", "B-records", "B-prepped", "B-scanned", "B-selected",
+                                                 "-", "-", "-"};
         fprintf(stderr, "[kwok trace] %u chain + %u streamer blocks, %llu ticks, us after the first chain block "
                         "start (min / median / max block)\n",
                 e->S.n_chain, e->n_stream, (unsigned long long)e->trace_ticks);
@@ -1216,6 +1219,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         // sharing one GPU (the 8-rank C3 test) are co-resident together
         if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
         e->n_stream = once ? 8u : (uint32_t)(cus * wants);
+        // multi rank: the BACK launch fills the CUs' spare k_tick slots with pool-only
+        // blocks (the pool phase's word-blocks over more blocks; all co-resident)
+        S.n_pool_extra = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, (int64_t)cus * occ - S.n_chain), e->n_stream);
+        if (const char* v = getenv("KWOK_POOL_EXTRA")) S.n_pool_extra = std::min<uint32_t>(S.n_pool_extra, (uint32_t)atoi(v));
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_EMIT_BLOCKS_PER_CU")) e->emit_grid = (uint32_t)(cus * std::max(1, std::min(atoi(v), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
@@ -1936,16 +1943,18 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
             }
             HIPCHK(e, hipStreamSynchronize(st));
         }
-        if (packed == 2 && G.sums_h[K - 1].n_new > new_cap)
-            return e->fail(KWOK_EINVAL, "kwok_ingest_pods_packed16: %u creates, out_new_handles holds %zu",
-                           G.sums_h[K - 1].n_new, new_cap);
         return rejected;
     };
     rc = run();
-    // a batch that fails once it changed the state (a chunk applied, or the failing
-    // chunk's own apply pass, placeholders or growth) is partly in the state: every
-    // later call fails
-    if (rc < 0 && e->ing_mutated) e->poisoned = true;
+    // kwok_pod_rec16 with more creates than out_new_handles holds: the batch is applied
+    // (not a failure of the engine), the call reports the lost handles.  A batch that
+    // fails once it changed the state (a chunk applied, or the failing chunk's own
+    // apply pass, placeholders or growth) is partly in the state: every later call fails
+    if (rc >= 0 && packed == 2 && G.sums_h[K - 1].n_new > new_cap)
+        rc = e->fail(KWOK_EINVAL, "kwok_ingest_pods_packed16: %u creates, out_new_handles holds %zu",
+                     G.sums_h[K - 1].n_new, new_cap);
+    else if (rc < 0 && e->ing_mutated)
+        e->poisoned = true;
     // nothing of this batch stays queued on the engine / prep / results streams (a failed chunk included)
     if (hipStreamSynchronize(st) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest engine stream");
     if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
@@ -2612,7 +2621,7 @@ void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride, bool hb_o
     H.rel_total = t[AG_REL];
 }
 
-bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr && !e->multi; }
+bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr; }
 
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
 void trace_tick(kwok_engine* e) {

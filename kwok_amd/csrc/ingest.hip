@@ -35,6 +35,8 @@
 // chain of one bucket's records (~500 per bucket at 2M records over 4096
 // buckets), not by HBM bandwidth.
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -271,15 +273,30 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
 // bound: the batch's deletes are not netted out).  (Counting the creates here
 // instead of with a global atomic per create in k_ing_prep: 0.5M creates over
 // 4096 counters held the prep ~40 us.)
+static_assert(offsetof(PodRec, spec) == 20 && offsetof(PodRec, op) == 22 && offsetof(PodRec, chk) == 25,
+              "k_ing_need reads op and chk as the words at bytes 20 and 24 of a PodRec");
 __global__ void k_ing_need(DevState S, IngestBatch I) {
     const uint32_t b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (b >= S.nb) return;
     const uint32_t pbeg = I.beg[b], pend = I.end[b];
     if (!(pbeg < pend && pend <= I.n && I.keys_sorted[pbeg] == b)) return;  // (a stale range: not this batch's)
     uint32_t c = 0;
-    for (uint32_t p = pbeg + lane(); p < pend; p += 64) {
-        const PodRec& r = I.rec[I.idx_sorted[p]];
-        c += r.op == KWOK_OP_UPSERT && !(r.chk & REC_EXISTING);
+    for (uint32_t p0 = pbeg; p0 < pend; p0 += 64 * 8) {  // (eight records per lane in flight)
+        uint32_t ix[8], w0[8], w1[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t p = p0 + 64 * q + lane();
+            ix[q] = p < pend ? I.idx_sorted[p] : ~0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {  // PodRec bytes 20..27: spec, op, phase | flags, chk, fst, pst
+            const uint32_t* rw = reinterpret_cast<const uint32_t*>(I.rec + (ix[q] != ~0u ? ix[q] : 0u)) + 5;
+            w0[q] = ix[q] != ~0u ? rw[0] : 0u;
+            w1[q] = ix[q] != ~0u ? rw[1] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            c += ix[q] != ~0u && ((w0[q] >> 16) & 0xFFu) == KWOK_OP_UPSERT && !((w1[q] >> 8) & REC_EXISTING);
     }
     for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
     if (!c) return;
@@ -1123,12 +1140,14 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 // buckets 0..nb, nb = nothing to apply), in tiles of BS_TILE records.
 //   k_bs_hist     per tile: its key counts (LDS histogram) -> hist[tile][key]
 //   k_bs_cols     per key: the exclusive prefix over the tiles, in place; the total
-//   k_bs_base     one block: the exclusive scan of the totals (each key's first
-//                 sorted position) and every bucket's range [beg, end)
-//   k_bs_scatter  one wave per tile, its records in order, 64 at a time: the
-//                 lanes of a key (13 ballots) take consecutive positions after the
-//                 key's running count in LDS -> idx_sorted, keys_sorted
-// Four small launches instead of rocPRIM's radix sort, which on these batches
+//   k_bs_scatter  per tile: the exclusive scan of the totals (each key's first
+//                 sorted position; block 0 writes every bucket's range [beg, end)),
+//                 then one wave takes the tile's records in order, 64 at a time:
+//                 the lanes of a key (13 ballots) take consecutive positions after
+//                 the key's running count in LDS -> idx_sorted, keys_sorted
+// Every global input of a block is loaded in unrolled batches (a strided loop
+// with one load per trip waits out one round trip per trip).
+// Three small launches instead of rocPRIM's radix sort, which on these batches
 // (12-bit keys, 0.7-1.3M records) ran the onesweep path at ~75 us or its block
 // merge sort path at ~120 us (17 launches).  Every bucket's range is written, so
 // no range of an earlier batch survives (k_ing_ranges / k_nd_ranges are not run).
@@ -1149,9 +1168,18 @@ __global__ void k_bs_hist(BucketSort B) {
     extern __shared__ uint32_t h[];
     const uint32_t t = blockIdx.x;
     for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) h[k] = 0;
-    __syncthreads();
     const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) atomicAdd(&h[B.keys[i]], 1u);
+    constexpr uint32_t R = BS_TILE / 256;  // keys per thread (blockDim 256)
+    uint32_t key[R];
+#pragma unroll
+    for (uint32_t q = 0; q < R; q++) {
+        const uint32_t i = i0 + q * 256 + threadIdx.x;
+        key[q] = i < i1 ? B.keys[i] : ~0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < R; q++)
+        if (key[q] != ~0u) atomicAdd(&h[key[q]], 1u);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) B.hist[(size_t)t * B.nk + k] = h[k];
 }
@@ -1195,47 +1223,53 @@ __global__ void k_bs_cols(BucketSort B, uint32_t tiles) {
     }
     if (g == 0) B.tot[k] = all;
 }
-__global__ void k_bs_base(BucketSort B) {
-    __shared__ uint32_t wsum[16];
-    constexpr uint32_t PER = BS_MAX_KEYS / 1024;  // keys per thread (blockDim 1024)
+__global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
+    extern __shared__ uint32_t cnt[];  // [nk] running positions, then the tile's keys [BS_TILE]
+    __shared__ uint32_t wsum[4];
+    uint32_t* tk = cnt + B.nk;
+    const uint32_t t = blockIdx.x;
+    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
+    // the key totals: thread th holds keys [th * PER, +PER) (all loads in flight), their
+    // exclusive scan over the block gives each key's first sorted position
+    constexpr uint32_t PER = BS_MAX_KEYS / 256;
     const uint32_t k0 = threadIdx.x * PER;
-    uint32_t v[PER], s = 0;
+    uint32_t tot[PER], hst[PER], sum = 0;
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) v[q] = k0 + q < B.nk ? B.tot[k0 + q] : 0u;
+    for (uint32_t q = 0; q < PER; q++) {
+        const bool ok = k0 + q < B.nk;
+        tot[q] = ok ? B.tot[k0 + q] : 0u;
+        hst[q] = ok ? B.hist[(size_t)t * B.nk + k0 + q] : 0u;
+    }
+    constexpr uint32_t RK = BS_TILE / 256;
+    uint32_t key[RK];
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) s += v[q];
-    // block exclusive scan of the per-thread sums (1024 threads = 16 waves)
-    uint32_t x = s;
+    for (uint32_t q = 0; q < RK; q++) {
+        const uint32_t i = i0 + q * 256 + threadIdx.x;
+        key[q] = i < i1 ? B.keys[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) sum += tot[q];
+    uint32_t x = sum;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)x, o);
         if (lane() >= (uint32_t)o) x += y;
     }
     const uint32_t w = threadIdx.x >> 6;
     if (lane() == 63) wsum[w] = x;
+#pragma unroll
+    for (uint32_t q = 0; q < RK; q++) tk[q * 256 + threadIdx.x] = key[q];
     __syncthreads();
-    uint32_t pre = x - s;
+    uint32_t pre = x - sum;
     for (uint32_t q = 0; q < w; q++) pre += wsum[q];
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
         const uint32_t k = k0 + q;
         if (k < B.nk) {
-            B.tot[k] = pre;
-            if (k + 1 < B.nk) {
-                B.beg[k] = pre;
-                B.end[k] = pre + v[q];
-            }
+            cnt[k] = pre + hst[q];
+            if (t == 0 && k + 1 < B.nk) B.beg[k] = pre, B.end[k] = pre + tot[q];
         }
-        pre += v[q];
+        pre += tot[q];
     }
-}
-__global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
-    extern __shared__ uint32_t cnt[];  // [nk] running positions, then the tile's keys [BS_TILE]
-    uint32_t* tk = cnt + B.nk;
-    const uint32_t t = blockIdx.x;
-    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
-    // every wave stages (the loads of a thread in flight together)
-    for (uint32_t k = threadIdx.x; k < B.nk; k += blockDim.x) cnt[k] = B.tot[k] + B.hist[(size_t)t * B.nk + k];
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) tk[i - i0] = B.keys[i];
     __syncthreads();
     if (threadIdx.x >= 64) return;
     // wave 0: the tile's records in order, 64 at a time
@@ -1270,7 +1304,6 @@ bool bucket_sort(const uint32_t* keys, uint32_t n, uint32_t nk, uint32_t* keys_s
                  idx_sorted, beg, end};
     hipLaunchKernelGGL(k_bs_hist, dim3(tiles), dim3(256), nk * 4, st, B);
     hipLaunchKernelGGL(k_bs_cols, dim3((nk + 63) / 64), dim3(64 * BS_GROUPS), 0, st, B, tiles);
-    hipLaunchKernelGGL(k_bs_base, dim3(1), dim3(1024), 0, st, B);
     hipLaunchKernelGGL(k_bs_scatter, dim3(tiles), dim3(256), (nk + BS_TILE) * 4, st, B, bits);
     return true;
 }

@@ -38,6 +38,8 @@ struct DevState {
     uint32_t cn, cp;
     uint32_t nb;               // owned buckets
     uint32_t n_chain;          // k_tick chain blocks (own bucket ranges); streamer blocks follow them
+    uint32_t n_pool_extra;     // multi rank: BACK launch blocks past the chain blocks that only take part
+                               // in the pool phase (the CUs' spare k_tick slots; 0 on heartbeat-once engines)
     int32_t node_handle_base, pod_handle_base;
     // pool replica
     uint64_t* used_bm;

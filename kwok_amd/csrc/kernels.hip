@@ -1736,7 +1736,9 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     do {                                                                                                  \
         if (S.trace && t == 0) S.trace[(size_t)b * TRACE_SLOTS + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+    TSTAMP(16);
     if (!have_sums) reduce_records(S, b, 0, l.recs, l.sums);
+    TSTAMP(17);
 
     // ---- pool phase (ticks with Gets or Puts) -------------------------------------
     const bool single = !S.multi;
@@ -1746,7 +1748,8 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     const uint64_t n_alloc_local = l.sums->tot[AG_ALLOC];
     // participants: single rank - the dirty blocks (every Get / Put belongs to one);
     // multi rank - every block (each rank commits every rank's Gets to its replica)
-    const uint32_t np = single ? (uint32_t)l.sums->tot[AG_DIRTY] : S.n_chain;
+    // (+ the BACK launch's pool-only blocks, S.n_pool_extra: the whole grid)
+    const uint32_t np = single ? (uint32_t)l.sums->tot[AG_DIRTY] : gridDim.x;
     const uint32_t pidx = single ? (uint32_t)l.sums->pre[AG_DIRTY] : b;
     const bool dirty = (pod_mask | node_mask) != 0;
     PoolPlan plan{};
@@ -1759,6 +1762,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
             pool_prep_wblock(S, wb, rel_total != 0, A != 0, x);
             if (wb == pidx) pw = x;
         }
+        TSTAMP(18);
         pool_barrier(S, np);
         TSTAMP(9);
         if (A) {
@@ -1766,6 +1770,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
             __shared__ uint64_t cp[2][BLOCK];
             const PoolPre q = pool_scan(S, nwb, cp);
             plan = pool_plan(S, A, q);
+            TSTAMP(19);
             for (uint32_t wb = pidx; wb < nwb; wb += np) {
                 uint64_t bu, bf;
                 pool_prefix(S, q, cp, wb, &bu, &bf);
@@ -1775,6 +1780,7 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
                 pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor,
                                    wb == pidx ? &pw : nullptr);
             }
+            TSTAMP(20);
             // ipPool.index after the last fresh address (committed after the barrier)
             if (cursor != ~0ull) H->cursor_index = cursor;
             if (pidx == 0 && t == 0) {
@@ -1928,7 +1934,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     TSTAMP(0);
 
     // ---- heartbeat streamers ------------------------------------------------------
-    if (b >= S.n_chain) {
+    // (a multi-rank BACK launch's blocks past the chain blocks are pool-only blocks)
+    if (b >= S.n_chain && (phases & TICK_FRONT)) {
         build_hb_template(S, hb_tmpl, now_unix, start_unix);
         if (S.stream_delay) {  // diagnostics: hold the stream back while the chain's first round trips run
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2325,14 +2332,14 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             // the pool phase after all of them: Use -> Put), from the inline lists
             for (int r = 0; r < S.world; r++) {
                 const uint32_t nu = (uint32_t)X[r].n_use, nl = nu + (uint32_t)X[r].n_rel;
-                for (uint32_t i = b * BLOCK + t; i < nl; i += S.n_chain * BLOCK) {
+                for (uint32_t i = b * BLOCK + t; i < nl; i += gridDim.x * BLOCK) {
                     const uint32_t ip = X[r].ips[i];
                     if (!in_cidr(S.pool, ip)) continue;
                     const uint64_t bit = ip - S.pool.net;
                     atomicOr((unsigned long long*)&(i < nu ? S.used_bm : S.rel_bm)[bit >> 6], 1ull << (bit & 63));
                 }
             }
-            if (xA || xrel) pool_barrier(S, S.n_chain);  // the pool phase reads every rank's bits
+            if (xA || xrel) pool_barrier(S, gridDim.x);  // the pool phase reads every rank's bits
         }
         if (b == 0 && t < 2)  // this launch builds k_emit's jobs (a fused split tick: k_pod_jobs writes the pod bytes)
             S.emit_n[t] = t ? H->n_init : (((phases & TICK_SPLIT) && S.fuse_pods) ? 0u : H->n_pp);
@@ -2350,11 +2357,12 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 st_host(&S.hdr_host->xforeign, fx);
             }
         }
-        // this block's masks from the FRONT launch
+        // this block's masks from the FRONT launch (a pool-only block has none)
         if (t == 0) {
-            sh_mask[0] = (uint32_t)S.dmask[2 * b];
-            sh_mask[1] = (uint32_t)(S.dmask[2 * b] >> 32);
-            sh_mask[2] = (uint32_t)S.dmask[2 * b + 1];
+            const bool chain = b < S.n_chain;
+            sh_mask[0] = chain ? (uint32_t)S.dmask[2 * b] : 0u;
+            sh_mask[1] = chain ? (uint32_t)(S.dmask[2 * b] >> 32) : 0u;
+            sh_mask[2] = chain ? (uint32_t)S.dmask[2 * b + 1] : 0u;
             if (b == 0) {
                 H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
                 S.list_counts[0] = 0;  // exchange lists for the next tick
@@ -2364,7 +2372,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         __syncthreads();
         pod_mask = (uint64_t)sh_mask[0] | (uint64_t)sh_mask[1] << 32;
         node_mask = sh_mask[2];
-        my_init = S.blockagg[(size_t)b * AG_STRIDE + AG_INIT];  // the FRONT launch's record
+        my_init = b < S.n_chain ? S.blockagg[(size_t)b * AG_STRIDE + AG_INIT] : 0u;  // the FRONT launch's record
     }
     tick_back(S.self, TickLds{recs, nflags32, gpre, &sums, &sh_L}, b, bk0, nbk,
               pod_mask, node_mask, my_init, have_sums, phases, n_hb, now_unix, start_unix, xA, xrel, xbase, tag);
@@ -2960,7 +2968,7 @@ void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
-    const uint32_t grid = S.n_chain + ((phases & TICK_FRONT) ? n_stream : 0u);
+    const uint32_t grid = S.n_chain + ((phases & TICK_FRONT) ? n_stream : (S.multi ? S.n_pool_extra : 0u));
     auto kern = S.hb_units == (uint32_t)HB_CHUNKS ? k_tick<false> : k_tick<true>;
     if (t0)
         hipExtLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, st, t0, t1, 0, S, now, start, n_hb, phases, tag,

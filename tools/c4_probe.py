@@ -1,0 +1,33 @@
+"""The bench's C4 churn leg alone (1M x 10M fleet, 1M + 1M records per tick,
+kwok_pod_rec16 by default) for kernel traces: tools/gpu_c4.sh runs it under
+rocprofv3 and prints the timeline of the last step.
+
+usage: c4_probe.py [--ticks 3] [--wire 16|20|0]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from kwok_amd import engine as keng, workload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ticks", type=int, default=3)
+    ap.add_argument("--wire", type=int, default=16)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    a = ap.parse_args()
+    e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes)
+    now = workload.S0 + 30
+    e.tick(now, read=False)
+    now += 30
+    _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire)
+    e.close()
+    print(json.dumps({k: c[k] for k in ("ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "roofline",
+                                        "phase_ms")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
