@@ -1220,9 +1220,13 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
         e->n_stream = once ? 8u : (uint32_t)(cus * wants);
         // multi rank: the BACK launch fills the CUs' spare k_tick slots with pool-only
-        // blocks (the pool phase's word-blocks over more blocks; all co-resident)
-        S.n_pool_extra = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, (int64_t)cus * occ - S.n_chain), e->n_stream);
-        if (const char* v = getenv("KWOK_POOL_EXTRA")) S.n_pool_extra = std::min<uint32_t>(S.n_pool_extra, (uint32_t)atoi(v));
+        // blocks (the pool phase's word-blocks over more blocks; all co-resident).  Not
+        // when several engines share the GPU (KWOK_TICK_BLOCKS_PER_CU / _CHAIN_BLOCKS:
+        // their grids must fit together, and a BACK launch waits for all its blocks)
+        const bool shared = getenv("KWOK_TICK_BLOCKS_PER_CU") || getenv("KWOK_TICK_CHAIN_BLOCKS");
+        S.n_pool_extra = shared ? 0u : (uint32_t)std::min<int64_t>(std::max<int64_t>(0, (int64_t)cus * occ - S.n_chain), e->n_stream);
+        if (const char* v = getenv("KWOK_POOL_EXTRA"))
+            S.n_pool_extra = (uint32_t)std::min<int64_t>(std::max(0, atoi(v)), std::min<int64_t>((int64_t)cus * occ - S.n_chain, e->n_stream));
         e->emit_grid = (uint32_t)(cus * std::max(1, std::min(emit_occupancy(), 8)));
         if (const char* v = getenv("KWOK_EMIT_BLOCKS_PER_CU")) e->emit_grid = (uint32_t)(cus * std::max(1, std::min(atoi(v), 8)));
         if (const char* v = getenv("KWOK_TICK_STREAMERS")) e->n_stream = (uint32_t)std::max(1, atoi(v));
