@@ -252,7 +252,8 @@ struct IngSummary {
     uint32_t rejected;      // records with a status other than KWOK_OK
     uint32_t n_freed;       // node entries the apply pass freed (diagnostics)
     uint32_t n_placeholders;  // placeholder node entries by-name creates made (diagnostics)
-    uint32_t need;          // max over buckets with creates: live pods + creates (growth check)
+    uint32_t need;          // growth check: max over the buckets that would overflow (live pods +
+                            // creates > cp), else 0
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)

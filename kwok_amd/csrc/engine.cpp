@@ -370,6 +370,7 @@ struct kwok_engine {
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
     bool results_stream = true;   // KWOK_INGEST_RS=0: a chunked batch's results copied on the engine stream
     bool results_kernel = false;  // KWOK_INGEST_RESULTS_KERNEL=1: pod batch results written into mapped host arrays by a kernel
+    bool new_mapped = true;       // KWOK_INGEST_NEW_MAPPED=0: kwok_pod_rec16 create handles copied back, not written in place
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
@@ -1241,6 +1242,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->iprof = getenv("KWOK_INGEST_PROF") != nullptr;
         if (const char* v = getenv("KWOK_INGEST_RESULTS_KERNEL")) e->results_kernel = v[0] == '1';
         if (const char* v = getenv("KWOK_INGEST_RS")) e->results_stream = v[0] != '0';
+        if (const char* v = getenv("KWOK_INGEST_NEW_MAPPED")) e->new_mapped = v[0] != '0';
         if (e->iprof)
             for (hipEvent_t& x : e->ing.tev) (void)hipEventCreate(&x);
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
@@ -1794,6 +1796,11 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     }
     // (kwok_pod_rec16 records are read as one 16-byte load each: in place only when aligned)
     const bool zc_ok = e->ingest_zc && K == 1 && !resident && (packed != 2 || ((uintptr_t)recs & 15) == 0);
+    // kwok_pod_rec16's create handles: written by the kernel straight into a
+    // kwok_host_alloc out_new_handles (each chunk's as it completes; no copy at the
+    // batch's end), else into HBM and copied back after the last chunk
+    int32_t* new_map = packed == 2 && new_cap && e->new_mapped ? (int32_t*)host_mapped(out_new, new_cap * 4) : nullptr;
+    int32_t* new_dst = new_map ? new_map : G.new_handle;
     const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
     auto chunk_batch = [&](uint32_t k) {
@@ -1849,7 +1856,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         int8_t* m8 = out_status8 ? (int8_t*)host_mapped(out_status8 + lo, I.n) : nullptr;
         uint32_t* mr = out_released ? (uint32_t*)host_mapped(out_released + lo, (size_t)I.n * 4) : nullptr;
         if (packed == 2) {  // the chunk's creates' handles at their ordinals (copied back at the batch's end)
-            launch_ingest_new_handles(I, G.new_handle, (uint32_t)std::min<size_t>(new_cap, G.cap), rs);
+            launch_ingest_new_handles(I, new_dst, (uint32_t)std::min<size_t>(new_cap, new_map ? new_cap : G.cap), rs);
             HIPCHK(e, hipGetLastError());
         }
         const bool mapped = e->results_kernel && (!out_handles || mh) && (!out_status || ms) && (!out_status8 || m8) &&
@@ -1901,7 +1908,8 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         }
         if (int r = release_for_host(e)) return r;
         if (packed == 2) {  // the creates' handles (every chunk's), and the summaries after them (n_new)
-            HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, rs));
+            if (new_map) HIPCHK(e, hipEventRecord(e->fence, rs));  // (system-scope release: the host reads them)
+            else HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, rs));
             if (rs != st) {
                 HIPCHK(e, hipEventRecord(G.rdone, rs));
                 HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
@@ -1942,7 +1950,8 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
             rejected += r;
             if (int r2 = results(k, st)) return r2;
             if (packed == 2 && k + 1 == K) {
-                HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, st));
+                if (new_map) HIPCHK(e, hipEventRecord(e->fence, st));
+                else HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(e, hipMemcpyAsync(G.sums_h + k, G.sums + k, sizeof(IngSummary), hipMemcpyDeviceToHost, st));
             }
             HIPCHK(e, hipStreamSynchronize(st));

@@ -278,8 +278,11 @@ static_assert(offsetof(PodRec, spec) == 20 && offsetof(PodRec, op) == 22 && offs
 __global__ void k_ing_need(DevState S, IngestBatch I) {
     const uint32_t b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (b >= S.nb) return;
-    const uint32_t pbeg = I.beg[b], pend = I.end[b];
+    const uint32_t pbeg = I.beg[b], pend = I.end[b], fill0 = S.pod_fill[b];
     if (!(pbeg < pend && pend <= I.n && I.keys_sorted[pbeg] == b)) return;  // (a stale range: not this batch's)
+    // the fill mark bounds the live pods and the bucket's records its creates: when
+    // that bound fits, the bucket cannot overflow
+    if (fill0 + (pend - pbeg) <= S.cp) return;
     uint32_t c = 0;
     for (uint32_t p0 = pbeg; p0 < pend; p0 += 64 * 8) {  // (eight records per lane in flight)
         uint32_t ix[8], w0[8], w1[8];
@@ -301,7 +304,7 @@ __global__ void k_ing_need(DevState S, IngestBatch I) {
     for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
     if (!c) return;
     // live pods: the bucket's state words below the fill mark, 8 per lane-load
-    const uint32_t fill = S.pod_fill[b];
+    const uint32_t fill = fill0;
     const uint16_t* ps = S.pod_state + (size_t)b * S.cp;  // (cp and fill are multiples of 8: 16-byte aligned rows)
     uint32_t live = 0;
     for (uint32_t s0 = lane() * 8; s0 < fill; s0 += 64 * 8 * 4) {
@@ -317,7 +320,9 @@ __global__ void k_ing_need(DevState S, IngestBatch I) {
         }
     }
     for (int o = 32; o; o >>= 1) live += (uint32_t)__shfl_xor((int)live, o);
-    if (lane() == 0) atomicMax(&I.sum->need, live + c);
+    // only a bucket that would overflow raises the need (one device-scope atomic on one
+    // word from each of 4096 waves cost ~50 us)
+    if (lane() == 0 && live + c > S.cp) atomicMax(&I.sum->need, live + c);
 }
 
 // bucket ranges of the sorted batch: beg / end (zeroed before: empty buckets are [0, 0))
@@ -1143,8 +1148,11 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 //   k_bs_scatter  per tile: the exclusive scan of the totals (each key's first
 //                 sorted position; block 0 writes every bucket's range [beg, end)),
 //                 then one wave takes the tile's records in order, 64 at a time:
-//                 the lanes of a key (13 ballots) take consecutive positions after
-//                 the key's running count in LDS -> idx_sorted, keys_sorted
+//                 the lanes of a key (LDS tags, a ballot per shared key) take consecutive positions after
+//                 the key's running count in LDS -> idx_sorted (keys_sorted only at
+//                 each bucket's first position: what the range checks read; the
+//                 records land ~1 per bucket per tile, so every store is a line of
+//                 its own and the fewer the better)
 // Every global input of a block is loaded in unrolled batches (a strided loop
 // with one load per trip waits out one round trip per trip).
 // Three small launches instead of rocPRIM's radix sort, which on these batches
@@ -1223,10 +1231,11 @@ __global__ void k_bs_cols(BucketSort B, uint32_t tiles) {
     }
     if (g == 0) B.tot[k] = all;
 }
-__global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
-    extern __shared__ uint32_t cnt[];  // [nk] running positions, then the tile's keys [BS_TILE]
+__global__ void k_bs_scatter(BucketSort B) {
+    extern __shared__ uint32_t cnt[];  // [nk] running positions, the tile's keys [BS_TILE], tags [nk] (bytes)
     __shared__ uint32_t wsum[4];
     uint32_t* tk = cnt + B.nk;
+    uint8_t* tag = reinterpret_cast<uint8_t*>(tk + BS_TILE);
     const uint32_t t = blockIdx.x;
     const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
     // the key totals: thread th holds keys [th * PER, +PER) (all loads in flight), their
@@ -1266,7 +1275,10 @@ __global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
         const uint32_t k = k0 + q;
         if (k < B.nk) {
             cnt[k] = pre + hst[q];
-            if (t == 0 && k + 1 < B.nk) B.beg[k] = pre, B.end[k] = pre + tot[q];
+            if (t == 0 && k + 1 < B.nk) {
+                B.beg[k] = pre, B.end[k] = pre + tot[q];
+                if (tot[q]) B.keys_sorted[pre] = k;  // (the consumers check a range's first key only)
+            }
         }
         pre += tot[q];
     }
@@ -1278,17 +1290,30 @@ __global__ void k_bs_scatter(BucketSort B, uint32_t key_bits) {
         const uint32_t i = r + lane();
         const bool valid = i < i1;
         const uint32_t key = valid ? tk[i - i0] : 0u;
-        uint64_t m = __ballot(valid);
-        for (uint32_t b = 0; b < key_bits; b++) {
-            const uint64_t ones = __ballot((key >> b) & 1u);
-            m &= ((key >> b) & 1u) ? ones : ~ones;
+        // lanes that share a key (rare: ~0.5 pairs per 64 records over 4096 buckets)
+        // rank among themselves in lane order; every other lane is alone.  Each lane
+        // writes its lane id to its key's tag: a lane that reads another's id shares
+        // its key, and one ballot per shared key finds the key's lanes
+        if (valid) tag[key] = (uint8_t)lane();
+        lds_sync();
+        uint64_t todo = __ballot(valid && tag[key] != (uint8_t)lane());
+        uint32_t rank = 0, grp = 1;
+        bool last = true;
+        while (todo) {
+            const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(todo));
+            const uint64_t m = __ballot(valid && key == kl);
+            if (valid && key == kl) {
+                rank = (uint32_t)__popcll(m & lt);
+                grp = (uint32_t)__popcll(m);
+                last = (m >> lane()) == 1ull;
+            }
+            todo &= ~m;
         }
         if (valid) {
             const uint32_t c = cnt[key];
-            const uint32_t pos = c + (uint32_t)__popcll(m & lt);
+            const uint32_t pos = c + rank;
             B.idx_sorted[pos] = i;
-            B.keys_sorted[pos] = key;
-            if ((m >> lane()) == 1ull) cnt[key] = c + (uint32_t)__popcll(m);  // the key's last lane
+            if (last) cnt[key] = c + grp;  // the key's last lane
         }
         lds_sync();
     }
@@ -1298,13 +1323,11 @@ bool bucket_sort(const uint32_t* keys, uint32_t n, uint32_t nk, uint32_t* keys_s
                  uint32_t* end, void* tmp, size_t tmp_bytes, hipStream_t st) {
     if (nk > BS_MAX_KEYS || bucket_sort_bytes(n, nk) > tmp_bytes) return false;
     const uint32_t tiles = (n + BS_TILE - 1) / BS_TILE;
-    uint32_t bits = 1;
-    while ((1u << bits) < nk) bits++;
     BucketSort B{keys, n, nk, static_cast<uint32_t*>(tmp), static_cast<uint32_t*>(tmp) + (size_t)tiles * nk, keys_sorted,
                  idx_sorted, beg, end};
     hipLaunchKernelGGL(k_bs_hist, dim3(tiles), dim3(256), nk * 4, st, B);
     hipLaunchKernelGGL(k_bs_cols, dim3((nk + 63) / 64), dim3(64 * BS_GROUPS), 0, st, B, tiles);
-    hipLaunchKernelGGL(k_bs_scatter, dim3(tiles), dim3(256), (nk + BS_TILE) * 4, st, B, bits);
+    hipLaunchKernelGGL(k_bs_scatter, dim3(tiles), dim3(256), (nk + BS_TILE) * 4 + ((nk + 3) & ~3u), st, B);
     return true;
 }
 
