@@ -370,6 +370,7 @@ struct kwok_engine {
     bool ingest_zc = true;      // KWOK_INGEST_ZC=0: pod batches in kwok_host_alloc memory copied to HBM first
     bool results_stream = true;   // KWOK_INGEST_RS=0: a chunked batch's results copied on the engine stream
     bool results_kernel = false;  // KWOK_INGEST_RESULTS_KERNEL=1: pod batch results written into mapped host arrays by a kernel
+    double last_chunk_cut = 0.4;  // KWOK_INGEST_LAST_CUT: a chunked batch's last chunk is (1 - this) of the others
     bool new_mapped = true;       // KWOK_INGEST_NEW_MAPPED=0: kwok_pod_rec16 create handles copied back, not written in place
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
@@ -1243,6 +1244,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         if (const char* v = getenv("KWOK_INGEST_RESULTS_KERNEL")) e->results_kernel = v[0] == '1';
         if (const char* v = getenv("KWOK_INGEST_RS")) e->results_stream = v[0] != '0';
         if (const char* v = getenv("KWOK_INGEST_NEW_MAPPED")) e->new_mapped = v[0] != '0';
+        if (const char* v = getenv("KWOK_INGEST_LAST_CUT")) e->last_chunk_cut = std::min(0.9, std::max(0.0, atof(v)));
         if (e->iprof)
             for (hipEvent_t& x : e->ing.tev) (void)hipEventCreate(&x);
         const char* ns = getenv("KWOK_TICK_NO_STREAM");
@@ -1292,7 +1294,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
                                 "(%d buckets, %d node slots, %d pod groups): shard over more GPUs",
                                 bpb, e->Cn, e->Cp, MAX_BPB, NODE_LDS, MAX_POD_CHUNKS * BLOCK));
     }
-    const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * 4 - 1) / (BLOCK * 4));
+    const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * POOL_WPT - 1) / (BLOCK * POOL_WPT));
     // node / pod arrays: whole 16-byte vectors at the end (Cn % 4 == 0, Cp % 8 == 0)
     const size_t NLa = (size_t)e->NL + 16, PLa = (size_t)e->PL + 16;
     e->NLa = NLa;
@@ -1775,7 +1777,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     // the part nothing hides).  The prep of chunk k + 2 waits until chunk k has
     // released its accumulator set.
     const uint32_t K = n > G.chunk ? (uint32_t)((n + G.chunk - 1) / G.chunk) : 1u;
-    const double W = K > 1 ? K - 0.4 : 1.0;
+    const double W = K > 1 ? K - e->last_chunk_cut : 1.0;
     // (chunks start at multiples of 256 records: kwok_pod_rec16's create counts are per 256-record tile)
     auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W) & ~(size_t)255; };
     // a one-chunk batch in kwok_host_alloc memory is read in place by k_ing_prep

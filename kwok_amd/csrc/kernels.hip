@@ -297,7 +297,6 @@ __device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
     return a >= S.pool.net ? a - S.pool.net : 0;
 }
 
-constexpr int POOL_WPT = 4;                  // bitmap words per thread
 constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per word-block
 
 // a thread's words of one word-block (pass k: word wb * POOL_WPB + k * BLOCK +
@@ -429,9 +428,11 @@ __device__ __forceinline__ uint64_t lowest_bits(uint64_t m, uint32_t n, uint32_t
 // the lowest n of the set bits of m (word w0 + l); the wave's selections are the
 // ordinals [g0, g0 + total) in lane order.  Every word taken whole (a fresh
 // fleet's run of free words): the addresses are the words' bits in order, one
-// entry per lane per store.  Otherwise lane by lane (a uniform walk over the
-// lanes that took bits): the wave writes lane j's selections together, lane l
-// its (l)-th set bit.  Only this rank's ordinals [lo_g, hi_g) are recorded.
+// entry per lane per store.  At most 8 per word (a churned pool's scattered
+// usable addresses): each lane its own, one per step.  Otherwise lane by lane (a
+// uniform walk over the lanes that took bits): the wave writes lane j's
+// selections together, lane l its (l)-th set bit.  Only this rank's ordinals
+// [lo_g, hi_g) are recorded.
 __device__ __forceinline__ void wave_write_addrs(const DevState& S, uint64_t g0, uint32_t n, uint64_t m, uint64_t w0,
                                                  uint64_t lo_g, uint64_t hi_g) {
     const uint32_t l = lane_id();
@@ -447,6 +448,22 @@ __device__ __forceinline__ void wave_write_addrs(const DevState& S, uint64_t g0,
         return;
     }
     const uint32_t ex = incl - n;
+    // sparse words (a churned fleet's reused addresses: a few per word): each lane
+    // writes its own selections, one per step, neighbouring lanes' ordinals adjacent
+    uint32_t mx = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (mx <= 8u) {
+        uint64_t mm = m;
+        for (uint32_t i = 0; i < mx; i++) {
+            if (i < n) {
+                const uint64_t g = g0 + ex + i;
+                if (g >= lo_g && g < hi_g) S.alloc_addr[g - lo_g] = S.pool.net + (uint32_t)((w0 + l) * 64 + __builtin_ctzll(mm));
+                mm &= mm - 1;
+            }
+        }
+        return;
+    }
     for (uint64_t act = __ballot(n != 0); act; act &= act - 1) {
         const int j = (int)__builtin_ctzll(act);
         const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)n, j);
