@@ -144,9 +144,9 @@ void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStr
 // the tick kernel: n_chain chain blocks (+ n_stream heartbeat streamers in
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
 // with work to emit, so they must be co-resident (tick_occupancy).
-// pool phase: bitmap words per thread of a word-block (BLOCK * POOL_WPT words; 8:
-// the 8-rank /4 pool's prep passes half as many, with twice the loads in flight)
-constexpr int POOL_WPT = 8;
+// pool phase: bitmap words per thread of a word-block (BLOCK * POOL_WPT words; a
+// multi-rank engine takes twice as many, kernels.hip POOL_WPT_MULTI)
+constexpr int POOL_WPT = 4;
 constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16,  // NOSTREAM: diagnostics only
               TICK_XLISTS = 32,  // BACK: the exchange lists were applied by k_pool_apply
               TICK_SPLIT = 64,   // the pod jobs are built by k_pod_jobs after the tick's launch(es)

@@ -297,21 +297,26 @@ __device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
     return a >= S.pool.net ? a - S.pool.net : 0;
 }
 
-constexpr int POOL_WPB = BLOCK * POOL_WPT;   // bitmap words per word-block
+// bitmap words per word-block: BLOCK * W, W = POOL_WPT_MULTI on a multi-rank
+// engine (the N-rank pool is N times larger: half the passes, twice the loads in
+// flight), POOL_WPT otherwise (a single rank's pool phase runs among its dirty
+// blocks: more, smaller word-blocks keep them all busy)
+constexpr int POOL_WPT_MULTI = 2 * POOL_WPT;
 
 // a thread's words of one word-block (pass k: word wb * POOL_WPB + k * BLOCK +
 // thread), as the prep pass left them: the select pass of the same block takes
 // them from registers instead of reading them again
+template <int W>
 struct PoolWords {
-    uint64_t used[POOL_WPT], usable[POOL_WPT];
+    uint64_t used[W], usable[W];
 };
-// fold this tick's Puts, count usable / free bits of word-block wb
-__device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count, PoolWords& pw) {
+template <int W>
+__device__ __forceinline__ void pool_prep_wblock(const DevState& S, uint32_t wb, bool fold, bool count, PoolWords<W>& pw) {
     const uint64_t cb = cursor_bit(S);
     uint32_t f[2] = {0, 0};
 #pragma unroll
-    for (int k = 0; k < POOL_WPT; k++) {
-        const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
+    for (int k = 0; k < W; k++) {
+        const uint64_t w = (uint64_t)wb * (BLOCK * W) + (uint64_t)k * BLOCK + threadIdx.x;
         pw.used[k] = ~0ull, pw.usable[k] = 0ull;
         if (w >= S.pool.words) continue;
         uint64_t used = S.used_bm[w], usable = S.usable_bm[w];
@@ -490,17 +495,28 @@ __device__ __forceinline__ void wave_write_addrs(const DevState& S, uint64_t g0,
 // entry per lane per store, instead of a serial bit walk per lane with one
 // scattered store per address: the 1M x 10M initial tick's 10M fresh Gets).
 // pw: the block's words of wb from its prep pass (null: read them)
+template <int W>
 __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t wb, const PoolPlan& p, uint64_t base_u, uint64_t base_f,
-                                   uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out, const PoolWords* pw) {
+                                   uint64_t lo_g, uint64_t hi_g, uint64_t* cursor_out, const PoolWords<W>* pw) {
     const uint64_t take = p.take, fin = p.fin;
     const uint64_t cb = cursor_bit(S);
     const bool advance = fin > 0 && p.fout == 0;
+    // every word of the word-block loaded up front (the passes below synchronise the
+    // block: a load inside them would be a round trip per pass)
+    uint64_t xu[W], xs[W];
 #pragma unroll
-    for (int k = 0; k < POOL_WPT; k++) {
-        const uint64_t w = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + threadIdx.x;
+    for (int k = 0; k < W; k++) {
+        const uint64_t w = (uint64_t)wb * (BLOCK * W) + (uint64_t)k * BLOCK + threadIdx.x;
         const bool valid = w < S.pool.words;
-        const uint64_t used = pw ? pw->used[k] : (valid ? S.used_bm[w] : ~0ull);
-        const uint64_t wu = pw ? pw->usable[k] : (valid ? S.usable_bm[w] : 0ull);
+        xu[k] = pw ? pw->used[k] : (valid ? S.used_bm[w] : ~0ull);
+        xs[k] = pw ? pw->usable[k] : (valid ? S.usable_bm[w] : 0ull);
+    }
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+        const uint64_t w = (uint64_t)wb * (BLOCK * W) + (uint64_t)k * BLOCK + threadIdx.x;
+        const bool valid = w < S.pool.words;
+        const uint64_t used = xu[k];
+        const uint64_t wu = xs[k];
         const uint64_t wf = valid ? free_mask(S, w, used, wu, cb) : 0ull;
         const uint32_t cu = (uint32_t)__popcll(wu), cf = (uint32_t)__popcll(wf);
         uint32_t v[2] = {cu, cf}, tot[2];
@@ -513,7 +529,7 @@ __device__ __forceinline__ void pool_select_wblock(const DevState& S, uint32_t w
         if (selu | self) S.used_bm[w] = used | selu | self;  // ... used[ip]; ipPool.new: used[ip]  (one thread owns word w)
         if (advance && nf && rf + nf == fin)
             *cursor_out = (uint64_t)S.pool.net + w * 64 + nth_set_bit(wf, nf - 1) + 1 - S.pool.base;
-        const uint64_t w0 = (uint64_t)wb * POOL_WPB + (uint64_t)k * BLOCK + (threadIdx.x & ~63u);
+        const uint64_t w0 = (uint64_t)wb * (BLOCK * W) + (uint64_t)k * BLOCK + (threadIdx.x & ~63u);
         const uint64_t gu0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ru) |
                              ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ru >> 32)) << 32);
         const uint64_t gf0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)rf) |
@@ -1737,6 +1753,38 @@ struct TickLds {
     Layout* L;
 };
 
+// The pool phase's passes among np blocks (this one: pidx): fold the tick's Puts
+// and count every word-block, the barrier, the plan from the counts, then the
+// Gets' selection (A > 0).  W: bitmap words per thread of a word-block.
+template <int W>
+__device__ __forceinline__ void pool_passes(const DevState& S, uint32_t pidx, uint32_t np, uint64_t A, uint64_t rel_total,
+                                            uint64_t alloc_base, uint64_t n_alloc_local, uint64_t (&cp)[2][BLOCK],
+                                            PoolPlan& plan, uint64_t& cursor, uint64_t* stamps) {
+    const uint32_t nwb = (uint32_t)((S.pool.words + BLOCK * W - 1) / (BLOCK * W));
+    PoolWords<W> pw;  // the block's first word-block, kept for its select pass
+    for (uint32_t wb = pidx; wb < nwb; wb += np) {
+        PoolWords<W> x;
+        pool_prep_wblock<W>(S, wb, rel_total != 0, A != 0, x);
+        if (wb == pidx) pw = x;
+    }
+    if (stamps) stamps[18] = __builtin_amdgcn_s_memrealtime();
+    pool_barrier(S, np);
+    if (stamps) stamps[9] = __builtin_amdgcn_s_memrealtime();
+    if (!A) return;
+    const PoolPre q = pool_scan(S, nwb, cp);
+    plan = pool_plan(S, A, q);
+    if (stamps) stamps[19] = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t wb = pidx; wb < nwb; wb += np) {
+        uint64_t bu, bf;
+        pool_prefix(S, q, cp, wb, &bu, &bf);
+        // every Get is taken before this word-block (and so before the block's later
+        // ones): nothing to select from here on (a pool much larger than the fleet)
+        if (bu >= plan.take && bf >= plan.fin) break;
+        pool_select_wblock<W>(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor,
+                              wb == pidx ? &pw : nullptr);
+    }
+}
+
 // BACK phases of a chain block that has something to emit (and, multi rank,
 // every block when the pool phase runs): prefix over the records, ipPool phase,
 // emission.  Out of line so the steady-state path keeps its registers; the
@@ -1770,33 +1818,16 @@ __device__ __forceinline__ void tick_back(const DevState* __restrict__ G, TickLd
     const uint32_t pidx = single ? (uint32_t)l.sums->pre[AG_DIRTY] : b;
     const bool dirty = (pod_mask | node_mask) != 0;
     PoolPlan plan{};
+    uint64_t cursor = ~0ull;
     if (A || rel_total) {
         if (single && pidx == 0 && t == 0) H->clk[CLK_BACK] = __builtin_amdgcn_s_memrealtime();
-        const uint32_t nwb = (uint32_t)((S.pool.words + POOL_WPB - 1) / POOL_WPB);
-        PoolWords pw;  // the block's first word-block, kept for its select pass
-        for (uint32_t wb = pidx; wb < nwb; wb += np) {
-            PoolWords x;
-            pool_prep_wblock(S, wb, rel_total != 0, A != 0, x);
-            if (wb == pidx) pw = x;
-        }
-        TSTAMP(18);
-        pool_barrier(S, np);
-        TSTAMP(9);
+        uint64_t* stamps = S.trace && t == 0 ? S.trace + (size_t)b * TRACE_SLOTS : nullptr;
+        __shared__ uint64_t cp[2][BLOCK];
+        if (single)
+            pool_passes<POOL_WPT>(S, pidx, np, A, rel_total, alloc_base, n_alloc_local, cp, plan, cursor, stamps);
+        else
+            pool_passes<POOL_WPT_MULTI>(S, pidx, np, A, rel_total, alloc_base, n_alloc_local, cp, plan, cursor, stamps);
         if (A) {
-            uint64_t cursor = ~0ull;
-            __shared__ uint64_t cp[2][BLOCK];
-            const PoolPre q = pool_scan(S, nwb, cp);
-            plan = pool_plan(S, A, q);
-            TSTAMP(19);
-            for (uint32_t wb = pidx; wb < nwb; wb += np) {
-                uint64_t bu, bf;
-                pool_prefix(S, q, cp, wb, &bu, &bf);
-                // every Get is taken before this word-block (and so before the block's later
-                // ones): nothing to select from here on (a pool much larger than the fleet)
-                if (bu >= plan.take && bf >= plan.fin) break;
-                pool_select_wblock(S, wb, plan, bu, bf, alloc_base, alloc_base + n_alloc_local, &cursor,
-                                   wb == pidx ? &pw : nullptr);
-            }
             TSTAMP(20);
             // ipPool.index after the last fresh address (committed after the barrier)
             if (cursor != ~0ull) H->cursor_index = cursor;

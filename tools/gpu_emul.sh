@@ -7,8 +7,7 @@ TAG=${1:-x}
 timeout -k 10 900 python -u -m pytest tests/test_parity_gpu.py tests/test_rccl_gpu.py tests/test_dist_gpu.py tests/test_c3_8rank_gpu.py tests/test_c4_churn_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread > $R/gpurun_out/emul_t_$TAG.log 2>&1 || { tail -30 $R/gpurun_out/emul_t_$TAG.log; exit 1; }
 tail -2 $R/gpurun_out/emul_t_$TAG.log
 timeout -k 10 300 python -u $R/tools/emul_probe.py > $R/gpurun_out/emul_$TAG.json 2> $R/gpurun_out/emul_$TAG.err || { tail -20 $R/gpurun_out/emul_$TAG.err; exit 1; }
-python3 -c "
-import json; d=json.loads([l for l in open("$R/gpurun_out/emul_$TAG.json") if l.startswith("{")][-1]); print('steady', d['steady_ms_per_tick'], 'churn', json.dumps(d['churn']))"
+python3 $R/tools/last_json.py $R/gpurun_out/emul_$TAG.json steady_ms_per_tick churn
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_emul_$TAG -o run -- python3 $R/tools/emul_probe.py --churn-ticks 2 > $R/gpurun_out/prof_emul_$TAG.log 2>&1 || exit 3
 T=$(find $R/gpurun_out/prof_emul_$TAG -name 'run_kernel_trace.csv' | head -n 1)
