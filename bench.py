@@ -161,7 +161,7 @@ def cpu_baseline(nodes, threads, ticks):
 
 
 def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
-              packed=16, ch=None, multi=False):
+              packed=12, ch=None, multi=False):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -172,8 +172,8 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     world > 1: every rank churns n_churn of its own pods per tick (weak
     scaling); the releases of all ranks cross the exchange (their lists are
     longer than the inline message: the second allgather), and each step is
-    timed between barriers, max over ranks.  packed=16: the batch as
-    kwok_pod_rec16 (16 B per record, kwok_ingest_pods_packed16: statuses as
+    timed between barriers, max over ranks.  packed=12: the batch as
+    kwok_pod_rec12 (12 B per record, kwok_ingest_pods_packed12: statuses as
     bytes, the creates' handles only, no release list at N=1); packed=20:
     kwok_pod_rec (20 B, kwok_ingest_pods_packed, every handle back); otherwise
     kwok_pod_event records with dotted-quad strings (48 B + strings)."""
@@ -187,8 +187,8 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     if ch is None:  # (a later leg continues the previous leg's generator: its live pods)
         ch = workload.Churn(pod_handles, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn,
                             seed=7, first=lo * fl.cp, alloc=keng.host_array)
-    ch.packed, ch.bufs = (packed if packed == 16 else bool(packed)), None
-    if packed == 16:  # the creates' handles; multi rank: the releases too (kwok_pool_put material)
+    ch.packed, ch.bufs = (packed if packed == 12 else bool(packed)), None
+    if packed == 12:  # the creates' handles; multi rank: the releases too (kwok_pool_put material)
         outs = (keng.host_array((n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int8),
                 keng.host_array((2 * n_churn,), np.uint32) if world > 1 else None)
     elif packed:
@@ -214,8 +214,8 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         if prof:
             e.profile_enable(True)
         t0 = time.perf_counter()
-        if packed == 16:
-            hs, st, _ = e.ingest_pods_packed16(ev, new_cap=len(ev) // 2, out=outs)
+        if packed == 12:
+            hs, st, _ = e.ingest_pods_packed12(ev, new_cap=len(ev) // 2, out=outs)
         else:
             hs, st, _ = e.ingest_pods_packed(ev, out=outs) if packed else e.ingest_pods_raw(ev, ar, out=outs)
         t1 = time.perf_counter()
@@ -224,7 +224,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         if world > 1:
             barrier()
             t2 = time.perf_counter()
-        ch.applied(hs.copy(), st, new_only=packed == 16)
+        ch.applied(hs.copy(), st, new_only=packed == 12)
         now += 30
         if prof:
             ph, nt = e.profile_read()
@@ -243,11 +243,11 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         "workload": "C4 pod churn storm (BASELINE configs[3]) on the metric fleet: %d deletion-marked pods (50%% with "
                     "finalizers) + %d creates per tick%s" % (n_churn, n_churn, " per rank" if world > 1 else ""),
         "ticks": ticks, "records_per_tick": recs // max(ticks, 1) * world,
-        "wire": "kwok_pod_rec16, 16 B per record in, 1 B status per record + 4 B handle per create back "
-                "(kwok_ingest_pods_packed16)" if packed == 16 else
+        "wire": "kwok_pod_rec12, 12 B per record in, 1 B status per record + 4 B handle per create back "
+                "(kwok_ingest_pods_packed12)" if packed == 12 else
                 "kwok_pod_rec, 20 B per record (kwok_ingest_pods_packed)" if packed else
                 "kwok_pod_event, 48 B per record + dotted-quad strings (kwok_ingest_pods)",
-        "link_bytes_per_step": (2 * n_churn * 16 + 2 * n_churn + 4 * n_churn if packed == 16 else
+        "link_bytes_per_step": (2 * n_churn * 12 + 2 * n_churn + 4 * n_churn if packed == 12 else
                                 2 * n_churn * 20 + 2 * n_churn * 5 if packed else None),
         "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
         "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,

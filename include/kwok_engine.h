@@ -149,20 +149,24 @@ typedef struct kwok_pod_rec {
 #define KWOK_REC_NEW 0x80u
 #define KWOK_REC_PHASE_SHIFT 5
 
-/* The 16-byte wire form (kwok_ingest_pods_packed16): kwok_pod_rec without its
- * hostIP word.  configurePod renders status.hostIP as the pod's own or NodeIP
- * (pod.status.tpl `hostIP: {{ with .hostIP }} {{ . }} {{ else }} {{ NodeIP }}`),
- * so a pod kwok has run holds NodeIP and a new one none: KWOK_REC_HOST_NODE_IP
- * in op says hostIP = the engine's node_ip, its absence an empty hostIP.  A pod
- * holding any other hostIP goes through kwok_ingest_pods_packed. */
-typedef struct kwok_pod_rec16 {
+/* The 12-byte wire form (kwok_ingest_pods_packed12): kwok_pod_rec with one value
+ * word instead of three.
+ *   hostIP: configurePod renders status.hostIP as the pod's own or NodeIP
+ *     (pod.status.tpl `hostIP: {{ with .hostIP }} {{ . }} {{ else }} {{ NodeIP }}`),
+ *     so a pod kwok has run holds NodeIP and a new one none: KWOK_REC_HOST_NODE_IP
+ *     in op says hostIP = the engine's node_ip, its absence an empty hostIP.
+ *   creationTimestamp: immutable (metadata), so only a create carries it; an
+ *     update or delete of a pod the engine holds keeps the one it was created with.
+ * value = a create's creationTimestamp (unix seconds; the new pod holds no podIP),
+ * any other record's status.podIP (0: empty).  A pod with another hostIP, or
+ * created with a podIP, goes through kwok_ingest_pods_packed. */
+typedef struct kwok_pod_rec12 {
     uint8_t op;          /* KWOK_OP_UPSERT / KWOK_OP_DELETE, | KWOK_REC_NEW, | KWOK_REC_HOST_NODE_IP */
     uint8_t flags;       /* as kwok_pod_rec */
     uint16_t spec_id;    /* as kwok_pod_rec */
     int32_t target;      /* as kwok_pod_rec */
-    uint32_t creation;   /* as kwok_pod_rec */
-    uint32_t pod_ip;     /* as kwok_pod_rec */
-} kwok_pod_rec16;
+    uint32_t value;      /* KWOK_REC_NEW: metadata.creationTimestamp; otherwise status.podIP */
+} kwok_pod_rec12;
 #define KWOK_REC_HOST_NODE_IP 0x40u
 
 typedef struct kwok_container {
@@ -331,17 +335,17 @@ int kwok_ingest_pods(kwok_engine* e, const kwok_pod_event* ev, size_t n, const c
  * place by the GPU. */
 int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, int32_t* out_handles,
                             int8_t* out_status, uint32_t* out_released);
-/* kwok_ingest_pods_packed over kwok_pod_rec16 records, returning the handles of
+/* kwok_ingest_pods_packed over kwok_pod_rec12 records, returning the handles of
  * the creates only (every other record's handle is its target, which the caller
  * holds): out_new_handles[k] = the handle of the batch's k-th KWOK_REC_NEW record
  * (-1 when rejected; out_status says why), for k < new_cap.  new_cap must be at
  * least the number of KWOK_REC_NEW records: handles past it are not returned and
  * the call returns KWOK_EINVAL once the batch is applied (the engine stays
  * usable); entries past that number are undefined.  out_status (int8, per
- * record) and out_released as kwok_ingest_pods_packed.  Over the link: 16 bytes
- * per record in, 1 byte per record and 4 per create back (C4: 32 + 6 MB per 2M
+ * record) and out_released as kwok_ingest_pods_packed.  Over the link: 12 bytes
+ * per record in, 1 byte per record and 4 per create back (C4: 24 + 6 MB per 2M
  * records, against 40 + 10 MB for kwok_pod_rec). */
-int kwok_ingest_pods_packed16(kwok_engine* e, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+int kwok_ingest_pods_packed12(kwok_engine* e, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
                               size_t new_cap, int8_t* out_status, uint32_t* out_released);
 /* Host only: kwok_pod_event records (strings in `arena`) -> the compact form,
  * with the checks that need the strings (canonical dotted quads, creation time

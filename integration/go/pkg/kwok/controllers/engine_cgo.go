@@ -57,8 +57,8 @@ type gpuEngine struct {
 	// records: copied by DMA, chunk by chunk), and writes the per-record results to
 	// resBuf (a copy into pageable Go memory would stall the engine's next
 	// transfers, DESIGN.md §11)
-	evBuf, arBuf, resBuf, recBuf, rec16Buf hostBuf
-	nodeIP                               uint32 // Config.NodeIP (kwok_pod_rec16's KWOK_REC_HOST_NODE_IP)
+	evBuf, arBuf, resBuf, recBuf, rec12Buf hostBuf
+	nodeIP                               uint32 // Config.NodeIP (kwok_pod_rec12's KWOK_REC_HOST_NODE_IP)
 }
 
 type hostBuf struct {
@@ -174,7 +174,7 @@ func (g *gpuEngine) close() {
 	g.arBuf.free()
 	g.resBuf.free()
 	g.recBuf.free()
-	g.rec16Buf.free()
+	g.rec12Buf.free()
 }
 
 func arenaPtr(arena []byte) *C.char {
@@ -263,10 +263,10 @@ func (g *gpuEngine) ingestNodes(evs []C.kwok_node_event, arena []byte) (handles,
 
 // ingestPods: one batch of pod records in event order.  Every record the
 // compact wire forms can carry (kwok_pack_pod_events: IPs as integers, a new
-// pod's node by handle) goes as a 16-byte kwok_pod_rec16 through
-// kwok_ingest_pods_packed16 when its hostIP is empty or NodeIP (every pod kwok
-// runs: pod.status.tpl renders NodeIP), else as a 20-byte kwok_pod_rec through
-// kwok_ingest_pods_packed; the rest (a pod naming a node the engine holds no
+// pod's node by handle) goes as a 12-byte kwok_pod_rec12 through
+// kwok_ingest_pods_packed12 when its hostIP is empty or NodeIP (every pod kwok
+// runs: pod.status.tpl renders NodeIP) and it is no create holding a podIP, else
+// as a 20-byte kwok_pod_rec through kwok_ingest_pods_packed; the rest (a pod naming a node the engine holds no
 // handle for) as kwok_pod_event with its strings through kwok_ingest_pods.
 // Consecutive records of one form are one call: applying the calls in order is
 // applying the batch.  All read page-locked buffers (kwok_host_alloc).
@@ -287,8 +287,9 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 		if pst[k] != C.KWOK_OK {
 			return 0
 		}
-		if h := uint32(recs[k].host_ip); h == 0 || h == g.nodeIP {
-			return 16
+		newWithIP := recs[k].op&C.KWOK_REC_NEW != 0 && recs[k].pod_ip != 0
+		if h := uint32(recs[k].host_ip); (h == 0 || h == g.nodeIP) && !newWithIP {
+			return 12
 		}
 		return 20
 	}
@@ -298,8 +299,8 @@ func (g *gpuEngine) ingestPods(evs []C.kwok_pod_event, arena []byte) (handles, s
 		for j < n && form(j) == f {
 			j++
 		}
-		if f == 16 {
-			err = g.ingestPacked16(recs[i:j], handles[i:j], status[i:j], released[i:j])
+		if f == 12 {
+			err = g.ingestPacked12(recs[i:j], handles[i:j], status[i:j], released[i:j])
 		} else if f == 20 {
 			err = g.ingestPacked(recs[i:j], handles[i:j], status[i:j], released[i:j])
 		} else {
@@ -337,27 +338,30 @@ func (g *gpuEngine) ingestPacked(recs []C.kwok_pod_rec, handles, status []int32,
 	return nil
 }
 
-// ingestPacked16: kwok_ingest_pods_packed16 of the records as kwok_pod_rec16 in
-// page-locked memory; the creates' handles come back in create order, every
-// other record's handle is its target
-func (g *gpuEngine) ingestPacked16(recs []C.kwok_pod_rec, handles, status []int32, released []uint32) error {
+// ingestPacked12: kwok_ingest_pods_packed12 of the records as kwok_pod_rec12 in
+// page-locked memory (value: a create's creationTimestamp, any other record's
+// podIP); the creates' handles come back in create order, every other record's
+// handle is its target
+func (g *gpuEngine) ingestPacked12(recs []C.kwok_pod_rec, handles, status []int32, released []uint32) error {
 	n := len(recs)
-	rp, err := g.rec16Buf.get(n * int(unsafe.Sizeof(C.kwok_pod_rec16{})))
+	rp, err := g.rec12Buf.get(n * int(unsafe.Sizeof(C.kwok_pod_rec12{})))
 	if err != nil {
 		return err
 	}
-	r16 := unsafe.Slice((*C.kwok_pod_rec16)(rp), n)
+	r12 := unsafe.Slice((*C.kwok_pod_rec12)(rp), n)
 	nNew := 0
 	for i := range recs {
 		op := recs[i].op
 		if recs[i].host_ip != 0 {
 			op |= C.KWOK_REC_HOST_NODE_IP
 		}
+		value := recs[i].pod_ip
 		if recs[i].op&C.KWOK_REC_NEW != 0 {
 			nNew++
+			value = recs[i].creation
 		}
-		r16[i] = C.kwok_pod_rec16{op: op, flags: recs[i].flags, spec_id: recs[i].spec_id, target: recs[i].target,
-			creation: recs[i].creation, pod_ip: recs[i].pod_ip}
+		r12[i] = C.kwok_pod_rec12{op: op, flags: recs[i].flags, spec_id: recs[i].spec_id, target: recs[i].target,
+			value: value}
 	}
 	resp, err := g.resBuf.get(9 * n)
 	if err != nil {
@@ -366,10 +370,10 @@ func (g *gpuEngine) ingestPacked16(recs []C.kwok_pod_rec, handles, status []int3
 	h := unsafe.Slice((*int32)(resp), n) // (the first nNew entries: the creates' handles)
 	rel := unsafe.Slice((*uint32)(unsafe.Add(resp, 4*n)), n)
 	st := unsafe.Slice((*int8)(unsafe.Add(resp, 8*n)), n)
-	rc := C.kwok_ingest_pods_packed16(g.h, &r16[0], C.size_t(n), (*C.int32_t)(&h[0]), C.size_t(nNew),
+	rc := C.kwok_ingest_pods_packed12(g.h, &r12[0], C.size_t(n), (*C.int32_t)(&h[0]), C.size_t(nNew),
 		(*C.int8_t)(&st[0]), (*C.uint32_t)(&rel[0]))
 	if rc < 0 {
-		return fmt.Errorf("kwok_ingest_pods_packed16: %d: %s", int(rc), g.lastError())
+		return fmt.Errorf("kwok_ingest_pods_packed12: %d: %s", int(rc), g.lastError())
 	}
 	k := 0
 	for i := range recs {

@@ -55,11 +55,12 @@ class PodRec(C.Structure):
                 ("creation", C.c_uint32), ("host_ip", C.c_uint32), ("pod_ip", C.c_uint32)]
 
 
-class PodRec16(C.Structure):
-    """kwok_pod_rec16: kwok_pod_rec without its hostIP word (kwok_ingest_pods_packed16):
-    REC_HOST_NODE_IP in op stands for hostIP = the engine's node_ip"""
+class PodRec12(C.Structure):
+    """kwok_pod_rec12 (kwok_ingest_pods_packed12): REC_HOST_NODE_IP in op stands for
+    hostIP = the engine's node_ip; value = a create's creationTimestamp, any other
+    record's podIP"""
     _fields_ = [("op", C.c_uint8), ("flags", C.c_uint8), ("spec_id", C.c_uint16), ("target", C.c_int32),
-                ("creation", C.c_uint32), ("pod_ip", C.c_uint32)]
+                ("value", C.c_uint32)]
 
 
 REC_NEW = 0x80
@@ -151,7 +152,7 @@ def _np_dtype(st):
 NODE_EVENT_DTYPE = _np_dtype(NodeEvent)
 POD_EVENT_DTYPE = _np_dtype(PodEvent)
 POD_REC_DTYPE = _np_dtype(PodRec)
-POD_REC16_DTYPE = _np_dtype(PodRec16)
+POD_REC12_DTYPE = _np_dtype(PodRec12)
 
 
 def ip4(s: str) -> int:
@@ -219,14 +220,19 @@ def pack_pod_events(ev: np.ndarray, ips_host: np.ndarray | None = None, ips_pod:
     return out
 
 
-def pack16(recs: np.ndarray, node_ip: int, out: np.ndarray | None = None) -> np.ndarray:
-    """POD_REC_DTYPE rows -> POD_REC16_DTYPE rows (every hostIP empty or node_ip;
-    ValueError otherwise: such a record goes through kwok_ingest_pods_packed)"""
+def pack12(recs: np.ndarray, node_ip: int, out: np.ndarray | None = None) -> np.ndarray:
+    """POD_REC_DTYPE rows -> POD_REC12_DTYPE rows (every hostIP empty or node_ip,
+    no create holding a podIP; ValueError otherwise: such a record goes through
+    kwok_ingest_pods_packed)"""
     hip = recs["host_ip"]
+    new = (recs["op"] & REC_NEW) != 0
     if ((hip != 0) & (hip != node_ip)).any():
-        raise ValueError("a hostIP other than the node IP: not expressible as kwok_pod_rec16")
-    o = np.empty(len(recs), POD_REC16_DTYPE) if out is None else out[:len(recs)]
+        raise ValueError("a hostIP other than the node IP: not expressible as kwok_pod_rec12")
+    if (new & (recs["pod_ip"] != 0)).any():
+        raise ValueError("a create holding a podIP: not expressible as kwok_pod_rec12")
+    o = np.empty(len(recs), POD_REC12_DTYPE) if out is None else out[:len(recs)]
     o["op"] = recs["op"] | np.where(hip != 0, REC_HOST_NODE_IP, 0).astype(np.uint8)
-    for f in ("flags", "spec_id", "target", "creation", "pod_ip"):
+    for f in ("flags", "spec_id", "target"):
         o[f] = recs[f]
+    o["value"] = np.where(new, recs["creation"], recs["pod_ip"])
     return o

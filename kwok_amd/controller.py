@@ -76,20 +76,22 @@ NOT_SENT = 1  # ingest_pod_runs: a record not sent to the engine (a Deleted even
 def ingest_pods_wire(eng, recs, arena):
     """engine_cgo.go ingestPods: every record the compact wire forms can carry
     (kwok_pack_pod_events: IPs as integers, a new pod's node by handle) as a
-    16-byte kwok_pod_rec16 through kwok_ingest_pods_packed16 when its hostIP is
-    empty or the engine's NodeIP (every pod kwok runs), else as a 20-byte
-    kwok_pod_rec through kwok_ingest_pods_packed, and the rest (a pod naming a
-    node the engine holds no handle for) as kwok_pod_event through
-    kwok_ingest_pods; consecutive records of one form in one call, in event
-    order (applying the calls in order is applying the batch).  Returns
-    (handles, statuses, released, calls)."""
+    12-byte kwok_pod_rec12 through kwok_ingest_pods_packed12 when its hostIP is
+    empty or the engine's NodeIP (every pod kwok runs) and it is no create
+    holding a podIP, else as a 20-byte kwok_pod_rec through
+    kwok_ingest_pods_packed, and the rest (a pod naming a node the engine holds
+    no handle for) as kwok_pod_event through kwok_ingest_pods; consecutive
+    records of one form in one call, in event order (applying the calls in order
+    is applying the batch).  Returns (handles, statuses, released, calls)."""
     from .engine import pack_pod_events
     packed, pst = pack_pod_events(recs, arena)
     n = len(recs)
     node_ip = eng.node_ip
     ok = pst == abi.OK
     hip = packed["host_ip"]
-    form = np.where(ok, np.where((hip == 0) | (hip == node_ip), 16, 20), 0)
+    new = (packed["op"] & abi.REC_NEW) != 0
+    small = ((hip == 0) | (hip == node_ip)) & ~(new & (packed["pod_ip"] != 0))
+    form = np.where(ok, np.where(small, 12, 20), 0)
     hs, st, rel = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.uint32)
     i = calls = 0
     while i < n:
@@ -97,12 +99,12 @@ def ingest_pods_wire(eng, recs, arena):
         j = i + 1
         while j < n and form[j] == f:
             j += 1
-        if f == 16:
-            r16 = abi.pack16(packed[i:j], node_ip)
-            nh, st[i:j], rel[i:j] = eng.ingest_pods_packed16(r16)
-            new = (r16["op"] & abi.REC_NEW) != 0
-            hs[i:j] = r16["target"]  # every other record's handle is its target
-            hs[i:j][new] = nh
+        if f == 12:
+            r12 = abi.pack12(packed[i:j], node_ip)
+            nh, st[i:j], rel[i:j] = eng.ingest_pods_packed12(r12)
+            nw = (r12["op"] & abi.REC_NEW) != 0
+            hs[i:j] = r12["target"]  # every other record's handle is its target
+            hs[i:j][nw] = nh
         elif f == 20:
             hs[i:j], st[i:j], rel[i:j] = eng.ingest_pods_packed(packed[i:j])
         else:

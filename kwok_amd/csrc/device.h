@@ -234,7 +234,7 @@ struct PodRec {             // 32 bytes
     uint8_t op, phase, flags, chk;  // chk: REC_*
     int8_t fst;             // UPSERT: the first failing field check (KWOK_OK: none)
     int8_t pst;             // existing: the handle lookup's status
-    uint8_t is_new;         // kwok_pod_rec16: a KWOK_REC_NEW record (its handle goes to out_new_handles)
+    uint8_t is_new;         // kwok_pod_rec12: a KWOK_REC_NEW record (its handle goes to out_new_handles)
     uint8_t pad[3];
 };
 static_assert(sizeof(PodRec) == 32, "prepared pod records are 32 bytes");
@@ -245,6 +245,7 @@ enum : uint8_t {
     REC_BY_NAME = 4,   // create naming its node by spec.nodeName: the apply pass resolves the name in
                        // the bucket's node directory when it reaches the record (a placeholder entry
                        // if none, pod_controller.go routing of spec.nodeName)
+    REC_KEEP_CTIME = 8,  // kwok_pod_rec12 update of a held pod: its creationTimestamp stays (immutable)
 };
 // per-batch counters of the GPU ingest (device memory, read back by the host)
 struct IngSummary {
@@ -257,7 +258,7 @@ struct IngSummary {
     uint32_t foreign;       // an in-CIDR podIP the engine did not assign to that pod entered (or left) the
                             // pool: a create with a podIP, an update to another podIP, a Deleted event
                             // releasing an address its pod does not hold (quiet ticks, engine.cpp)
-    uint32_t n_new;         // kwok_pod_rec16: the batch's KWOK_REC_NEW records up to this chunk
+    uint32_t n_new;         // kwok_pod_rec12: the batch's KWOK_REC_NEW records up to this chunk
     uint32_t pad;
 };
 

@@ -191,7 +191,7 @@ struct kwok_engine {
         int8_t* out_status8 = nullptr;  // kwok_ingest_pods_packed: the statuses as bytes
         uint32_t* out_released = nullptr;
         void* sort_tmp = nullptr;
-        // kwok_ingest_pods_packed16: NEW records per 256-record tile, the tiles' prefixes,
+        // kwok_ingest_pods_packed12: NEW records per 256-record tile, the tiles' prefixes,
         // the creates' handles in create order
         uint32_t *tile_new = nullptr, *tile_pre = nullptr;
         int32_t* new_handle = nullptr;
@@ -220,7 +220,7 @@ struct kwok_engine {
         hipStream_t pst = nullptr, dst = nullptr;  // prep (H2D + k_ing_prep) / results (D2H)
         hipEvent_t tev[8] = {};  // KWOK_INGEST_PROF: device-side phase stamps of a two-chunk batch
         hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
-        hipEvent_t rdone = nullptr;  // the results stream's work of a batch (kwok_pod_rec16: before the summaries)
+        hipEvent_t rdone = nullptr;  // the results stream's work of a batch (kwok_pod_rec12: before the summaries)
         size_t chunk = 1048576;
     } ing;
 
@@ -371,7 +371,7 @@ struct kwok_engine {
     bool results_stream = true;   // KWOK_INGEST_RS=0: a chunked batch's results copied on the engine stream
     bool results_kernel = false;  // KWOK_INGEST_RESULTS_KERNEL=1: pod batch results written into mapped host arrays by a kernel
     double last_chunk_cut = 0.4;  // KWOK_INGEST_LAST_CUT: a chunked batch's last chunk is (1 - this) of the others
-    bool new_mapped = true;       // KWOK_INGEST_NEW_MAPPED=0: kwok_pod_rec16 create handles copied back, not written in place
+    bool new_mapped = true;       // KWOK_INGEST_NEW_MAPPED=0: kwok_pod_rec12 create handles copied back, not written in place
     int nt_env = -1;            // KWOK_HB_NT (0 / 1: heartbeat stores plain / non-temporal), else automatic
     int share_env = -1;         // KWOK_TICK_STREAM_SHARE (/1024 of the stream to the streamer blocks), else automatic
     uint32_t tick_tag = 0;      // nonzero id of the last FRONT launch
@@ -1748,12 +1748,13 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
 // (int32) or out_status8 (int8)
 // resident: the records (kwok_pod_event) and their arena are on the device already,
 // in the ingest buffers (kwok_ingest_pods_json decoded them there)
-// packed: 0 kwok_pod_event, 1 kwok_pod_rec, 2 kwok_pod_rec16 (the creates' handles to
+// packed: 0 kwok_pod_event, 1 kwok_pod_rec, 2 kwok_pod_rec12 (the creates' handles to
 // out_new[k < new_cap], in create order; out_handles unused)
 int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released,
                      bool resident = false, int32_t* out_new = nullptr, size_t new_cap = 0) {
-    const size_t RB = packed == 2 ? sizeof(kwok_pod_rec16) : packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);
+    const size_t RB = packed == 2 ? sizeof(kwok_pod_rec12) : packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);
+    static_assert(sizeof(kwok_pod_rec12) == 12, "kwok_pod_rec12 is 12 bytes");
     auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
     drain(e);  // the device state reflects every submitted tick
@@ -1778,7 +1779,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     // released its accumulator set.
     const uint32_t K = n > G.chunk ? (uint32_t)((n + G.chunk - 1) / G.chunk) : 1u;
     const double W = K > 1 ? K - e->last_chunk_cut : 1.0;
-    // (chunks start at multiples of 256 records: kwok_pod_rec16's create counts are per 256-record tile)
+    // (chunks start at multiples of 256 records: kwok_pod_rec12's create counts are per 256-record tile)
     auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W) & ~(size_t)255; };
     // a one-chunk batch in kwok_host_alloc memory is read in place by k_ing_prep
     // (the only kernel that reads the records and their strings): one pass over
@@ -1796,9 +1797,9 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
             return e->fail(KWOK_ENOMEM, "ingest summaries");
         G.nsums = m;
     }
-    // (kwok_pod_rec16 records are read as one 16-byte load each: in place only when aligned)
-    const bool zc_ok = e->ingest_zc && K == 1 && !resident && (packed != 2 || ((uintptr_t)recs & 15) == 0);
-    // kwok_pod_rec16's create handles: written by the kernel straight into a
+    // (kwok_pod_rec12 records are read as three dwords: in place only when 4-byte aligned)
+    const bool zc_ok = e->ingest_zc && K == 1 && !resident && (packed != 2 || ((uintptr_t)recs & 3) == 0);
+    // kwok_pod_rec12's create handles: written by the kernel straight into a
     // kwok_host_alloc out_new_handles (each chunk's as it completes; no copy at the
     // batch's end), else into HBM and copied back after the last chunk
     int32_t* new_map = packed == 2 && new_cap && e->new_mapped ? (int32_t*)host_mapped(out_new, new_cap * 4) : nullptr;
@@ -1961,12 +1962,12 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         return rejected;
     };
     rc = run();
-    // kwok_pod_rec16 with more creates than out_new_handles holds: the batch is applied
+    // kwok_pod_rec12 with more creates than out_new_handles holds: the batch is applied
     // (not a failure of the engine), the call reports the lost handles.  A batch that
     // fails once it changed the state (a chunk applied, or the failing chunk's own
     // apply pass, placeholders or growth) is partly in the state: every later call fails
     if (rc >= 0 && packed == 2 && G.sums_h[K - 1].n_new > new_cap)
-        rc = e->fail(KWOK_EINVAL, "kwok_ingest_pods_packed16: %u creates, out_new_handles holds %zu",
+        rc = e->fail(KWOK_EINVAL, "kwok_ingest_pods_packed12: %u creates, out_new_handles holds %zu",
                      G.sums_h[K - 1].n_new, new_cap);
     else if (rc < 0 && e->ing_mutated)
         e->poisoned = true;
@@ -1992,7 +1993,7 @@ int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, 
     return ingest_pods_impl(e, recs, 1, n, nullptr, 0, out_handles, nullptr, out_status, out_released);
 }
 
-int kwok_ingest_pods_packed16(kwok_engine* e, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+int kwok_ingest_pods_packed12(kwok_engine* e, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
                               size_t new_cap, int8_t* out_status, uint32_t* out_released) {
     if (!e || (n && !recs) || n > 0x7FFFFFF0ull || (new_cap && !out_new_handles)) return KWOK_EINVAL;
     return ingest_pods_impl(e, recs, 2, n, nullptr, 0, nullptr, nullptr, out_status, out_released, false,

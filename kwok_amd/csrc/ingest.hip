@@ -118,18 +118,26 @@ __device__ __forceinline__ bool d_in_cidr(const PoolGeom& g, uint32_t ip) {
 // every status that does not depend on state.  keys[i] = the owned local bucket
 // whose records the apply pass takes in order, or nb (decided here).
 // ---------------------------------------------------------------------------
-// The compact records (kwok_pod_rec, kwok_pod_rec16): their strings were parsed
+// The compact records (kwok_pod_rec, kwok_pod_rec12): their strings were parsed
 // by the caller, so only the checks on values remain; a create names its node by
-// handle.  kwok_pod_rec16 carries no hostIP word: KWOK_REC_HOST_NODE_IP stands
-// for the engine's node_ip.  Returns whether the record is a KWOK_REC_NEW one.
+// handle.  kwok_pod_rec12 carries one value word: KWOK_REC_HOST_NODE_IP stands
+// for the engine's node_ip, a create's value is its creationTimestamp (no
+// podIP), any other record's its podIP (an update keeps the pod's creation
+// time: REC_KEEP_CTIME).  Returns whether the record is a KWOK_REC_NEW one.
 __device__ bool prep_packed(const DevState& S, const IngestBatch& I, uint32_t i) {
     uint32_t w0, ctime, hip, pip;
     int32_t target;
+    bool keep = false;
     if (I.packed == 2) {
-        const uint4 v = reinterpret_cast<const uint4*>(I.ev)[i];  // 16 bytes: one load
-        w0 = v.x, target = (int32_t)v.y, ctime = v.z, pip = v.w;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(I.ev) + (size_t)i * sizeof(kwok_pod_rec12));
+        w0 = w[0], target = (int32_t)w[1];  // 12 bytes: three dwords
+        const uint32_t val = w[2];
         hip = (w0 & KWOK_REC_HOST_NODE_IP) ? S.node_ip : 0u;
         w0 &= ~KWOK_REC_HOST_NODE_IP;
+        const bool nw = (w0 & KWOK_REC_NEW) != 0;
+        ctime = nw ? val : 0u;
+        pip = nw ? 0u : val;
+        keep = !nw;
     } else {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(I.ev) + (size_t)i * sizeof(kwok_pod_rec));
         w0 = w[0], target = (int32_t)w[1], ctime = w[2], hip = w[3], pip = w[4];  // 20 bytes: five dwords
@@ -157,6 +165,7 @@ __device__ bool prep_packed(const DevState& S, const IngestBatch& I, uint32_t i)
         if (spec >= I.n_specs) r.fst = KWOK_EINVAL;
         else if (r.phase > KWOK_PHASE_UNKNOWN) r.fst = KWOK_EINVAL;
         else r.ctime = ctime, r.spec = (uint16_t)spec;
+        if (keep) r.chk |= REC_KEEP_CTIME;
     }
     if (!create && target >= 0) {
         r.chk |= REC_EXISTING;
@@ -189,7 +198,7 @@ __global__ void k_ing_prep(DevState S, IngestBatch I) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (I.packed) {
         const bool nw = i < I.n && prep_packed(S, I, i);
-        if (I.tile_new) {  // kwok_pod_rec16: the block's creates (blocks are the batch's 256-record tiles)
+        if (I.tile_new) {  // kwok_pod_rec12: the block's creates (blocks are the batch's 256-record tiles)
             const int c = __syncthreads_count(nw);
             if (threadIdx.x == 0) I.tile_new[I.tile0 + blockIdx.x] = (uint32_t)c;
         }
@@ -651,7 +660,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                     S.pod_state[g] = (uint16_t)nst;
                     S.pod_node[g] = (uint16_t)nd;
                     S.pod_spec[g] = (uint16_t)(hop & 0xFFFFu);
-                    S.pod_ctime[g] = rb.x;
+                    if (!(exl && (chk & REC_KEEP_CTIME))) S.pod_ctime[g] = rb.x;
                     S.host_ip[g] = ra.z;
                     S.pod_ip[g] = ra.w;
                     handle = (int32_t)((S.b_lo + b) * S.pod_stride + slot);
@@ -796,7 +805,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
                         S.pod_state[g] = (uint16_t)nst;
                         S.pod_node[g] = (uint16_t)nd;
                         S.pod_spec[g] = (uint16_t)(rdl(hop, k) & 0xFFFFu);
-                        S.pod_ctime[g] = rdl(rb.x, k);
+                        if (!(existing && (kchk & REC_KEEP_CTIME))) S.pod_ctime[g] = rdl(rb.x, k);
                         S.host_ip[g] = hip;
                         S.pod_ip[g] = pip;
                     }
@@ -1339,7 +1348,7 @@ size_t ingest_sort_bytes(uint32_t n, uint32_t key_bits) {
     return std::max(bytes, bucket_sort_bytes(n, BS_MAX_KEYS));
 }
 
-// kwok_pod_rec16's create handles.  k_ing_tile_scan (one block): the exclusive
+// kwok_pod_rec12's create handles.  k_ing_tile_scan (one block): the exclusive
 // prefixes of the NEW counts of the batch's tiles [0, ntiles) and their total;
 // k_ing_new_handles (a block per tile of the chunk): each create's ordinal = its
 // tile's prefix + the creates before it in the tile.
@@ -1413,7 +1422,7 @@ void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* stat
     if (I.n) hipLaunchKernelGGL(k_ing_results, dim3(cdiv(I.n, 1024)), dim3(256), 0, st, I, handles, status, status8, released);
 }
 void launch_ingest_prep(const DevState& S, const IngestBatch& I, hipStream_t st) {
-    // (256-record blocks: kwok_pod_rec16's create counts are per 256-record tile)
+    // (256-record blocks: kwok_pod_rec12's create counts are per 256-record tile)
     if (I.n) hipLaunchKernelGGL(k_ing_prep, dim3(cdiv(I.n, 256)), dim3(256), 0, st, S, I);
 }
 void launch_ingest_need(const DevState& S, const IngestBatch& I, hipStream_t st) {

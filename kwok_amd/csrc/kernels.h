@@ -175,7 +175,7 @@ struct IngestBatch {
     const void* ev;            // [n] kwok_pod_event (packed: kwok_pod_rec), on the device or read in place
     uint32_t n;
     uint32_t n_specs;
-    uint32_t packed;           // 1: kwok_pod_rec records (no arena); 2: kwok_pod_rec16
+    uint32_t packed;           // 1: kwok_pod_rec records (no arena); 2: kwok_pod_rec12
     uint32_t spec;             // the apply pass was queued without the host's growth check: it returns at once
                                // when the chunk needs more pod slots than a bucket has (sum->need > cp) or an
                                // earlier chunk of the batch did (*abort), setting *abort (the host redoes them)
@@ -192,7 +192,7 @@ struct IngestBatch {
     uint32_t* end;             // [nb]
     IngSummary* sum;
     uint32_t* abort;           // [1] per batch (spec)
-    // kwok_pod_rec16: handles of the creates only.  The chunk starts at a multiple of
+    // kwok_pod_rec12: handles of the creates only.  The chunk starts at a multiple of
     // 256 records; k_ing_prep counts the KWOK_REC_NEW records of each 256-record tile
     // of the batch (tile_new[tile0 + block]), k_ing_new_handles writes their handles
     // at their ordinals among the batch's creates (tile_pre: the tiles' prefixes)
@@ -208,7 +208,7 @@ void launch_ingest_status8(const IngestBatch& I, int8_t* dst, hipStream_t st);
 // the per-record results written into mapped host arrays (device addresses of kwok_host_alloc memory; null: skip)
 void launch_ingest_results(const IngestBatch& I, int32_t* handles, int32_t* status, int8_t* status8, uint32_t* released,
                            hipStream_t st);
-// kwok_pod_rec16: the chunk's creates' handles at their ordinals in new_handles (< cap),
+// kwok_pod_rec12: the chunk's creates' handles at their ordinals in new_handles (< cap),
 // after scanning the NEW counts of the batch's tiles up to the chunk's last (sum->n_new)
 void launch_ingest_new_handles(const IngestBatch& I, int32_t* new_handles, uint32_t cap, hipStream_t st);
 // after the sort: live pods + creates of every bucket with creates -> sum->need

@@ -61,7 +61,7 @@ def declare(lib, pre):
         "ingest_nodes": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP]),
         "ingest_pods": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP, VP]),
         "ingest_pods_packed": (C.c_int, [VP, VP, SZ, VP, VP, VP]),
-        "ingest_pods_packed16": (C.c_int, [VP, VP, SZ, VP, SZ, VP, VP]),
+        "ingest_pods_packed12": (C.c_int, [VP, VP, SZ, VP, SZ, VP, VP]),
         "pool_put": (C.c_int, [VP, VP, SZ]),
         "cni_pending": (C.c_int, [VP, VP, SZ, P(SZ)]),
         "cni_assign": (C.c_int, [VP, VP, VP, SZ, VP]),
@@ -196,7 +196,7 @@ class EngineBase:
             raise KwokError(rc, "create: %s" % (msg or b"").decode())
         self._h = h
         self.last = None
-        self.node_ip = abi.ip4(cfg.node_ip.decode())  # Config.NodeIP (kwok_pod_rec16's hostIP flag)
+        self.node_ip = abi.ip4(cfg.node_ip.decode())  # Config.NodeIP (kwok_pod_rec12's hostIP flag)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -281,14 +281,14 @@ class EngineBase:
         self._check(rc, "ingest_pods_packed")
         return hs, st, rel
 
-    def ingest_pods_packed16(self, recs: np.ndarray, new_cap=None, out=None, released=True):
-        """kwok_ingest_pods_packed16 over POD_REC16_DTYPE rows -> (handles of the
+    def ingest_pods_packed12(self, recs: np.ndarray, new_cap=None, out=None, released=True):
+        """kwok_ingest_pods_packed12 over POD_REC12_DTYPE rows -> (handles of the
         creates in create order, status int8 per record, released).  new_cap: the
         room for create handles (default: the number of REC_NEW rows); out:
         optional (new handles, status, released) arrays (e.g. page-locked)"""
         n = len(recs)
-        r = recs if recs.flags.c_contiguous and recs.dtype == abi.POD_REC16_DTYPE else \
-            np.ascontiguousarray(recs, dtype=abi.POD_REC16_DTYPE)
+        r = recs if recs.flags.c_contiguous and recs.dtype == abi.POD_REC12_DTYPE else \
+            np.ascontiguousarray(recs, dtype=abi.POD_REC12_DTYPE)
         if new_cap is None:
             new_cap = int(np.count_nonzero(r["op"] & abi.REC_NEW))
         if out is None:
@@ -297,9 +297,9 @@ class EngineBase:
         else:
             nh, st, rel = out[0], out[1][:n], (out[2][:n] if out[2] is not None else None)
             assert len(nh) >= new_cap
-        rc = self._fn("ingest_pods_packed16")(self._h, r.ctypes.data, n, nh.ctypes.data, new_cap, st.ctypes.data,
+        rc = self._fn("ingest_pods_packed12")(self._h, r.ctypes.data, n, nh.ctypes.data, new_cap, st.ctypes.data,
                                               rel.ctypes.data if rel is not None else None)
-        self._check(rc, "ingest_pods_packed16")
+        self._check(rc, "ingest_pods_packed12")
         return nh[:new_cap], st, rel
 
     def pool_put(self, ips):

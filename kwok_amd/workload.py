@@ -178,7 +178,7 @@ class Churn:
         self.first = first
         # packed: the batch as kwok_pod_rec (kwok_ingest_pods_packed: 20 B per record,
         # IPs as integers, nodes by handle) instead of kwok_pod_event + dotted quads;
-        # packed=16: as kwok_pod_rec16 (kwok_ingest_pods_packed16: 16 B, hostIP by flag)
+        # packed=12: as kwok_pod_rec12 (kwok_ingest_pods_packed12: 12 B, hostIP by flag)
         self.packed = packed
         # alloc(shape, dtype): the batch is written into (and reused from) these
         # buffers - e.g. page-locked host memory (engine.host_array), which the
@@ -245,8 +245,8 @@ class Churn:
         return ev, arena
 
     def _batch_packed(self, D, dead, loc, phase, pip, now):
-        r16 = self.packed == 16
-        dt = abi.POD_REC16_DTYPE if r16 else abi.POD_REC_DTYPE
+        r12 = self.packed == 12
+        dt = abi.POD_REC12_DTYPE if r12 else abi.POD_REC_DTYPE
         if self.alloc is None:
             ev = np.zeros(2 * D, dt)
         else:
@@ -256,31 +256,35 @@ class Churn:
         d = ev[:D]
         running = phase[loc] == abi.PHASE_RUNNING
         fin = np.where(self.rng.random(D) < 0.5, abi.POD_HAS_FINALIZERS, 0)
-        d["op"] = abi.OP_UPSERT | np.where(running, abi.REC_HOST_NODE_IP, 0) if r16 else abi.OP_UPSERT
         d["target"] = dead
         d["spec_id"] = self.spec
-        d["creation"] = self.ctime[loc]
         d["flags"] = ((abi.POD_DELETING | fin | np.where(running, abi.POD_CONFORMS | abi.POD_STATUS_NONEMPTY, 0)
                        | np.where(pip[loc] != 0, abi.POD_STATUS_NONEMPTY, 0))
                       | (phase[loc].astype(np.int64) << abi.REC_PHASE_SHIFT))
-        if not r16:
-            d["host_ip"] = np.where(running, abi.ip4(self.node_ip.decode()), 0)
-        d["pod_ip"] = pip[loc]
         c = ev[D:]
-        c["op"] = abi.OP_UPSERT | abi.REC_NEW
         c["target"] = self.rng.permutation(self.node_of[loc])
         c["spec_id"] = self.spec
         c["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
-        c["creation"] = now - 5
-        if not r16:
+        if r12:  # (the marked pods keep their creationTimestamp; a create's is its value)
+            d["op"] = abi.OP_UPSERT | np.where(running, abi.REC_HOST_NODE_IP, 0)
+            d["value"] = pip[loc]
+            c["op"] = abi.OP_UPSERT | abi.REC_NEW
+            c["value"] = now - 5
+        else:
+            d["op"] = abi.OP_UPSERT
+            d["creation"] = self.ctime[loc]
+            d["host_ip"] = np.where(running, abi.ip4(self.node_ip.decode()), 0)
+            d["pod_ip"] = pip[loc]
+            c["op"] = abi.OP_UPSERT | abi.REC_NEW
+            c["creation"] = now - 5
             c["host_ip"] = 0
-        c["pod_ip"] = 0
+            c["pod_ip"] = 0
         self._pending = (D, c["target"].copy(), now - 5)
         return ev
 
     def applied(self, handles, status, new_only=False):
         """account the ingest result of the last batch (new_only: handles are the
-        creates' only, kwok_ingest_pods_packed16)"""
+        creates' only, kwok_ingest_pods_packed12)"""
         D, nodes, ct = self._pending
         assert (status == 0).all(), "churn batch rejected: %s" % np.unique(status[status != 0])
         new = handles[:D] if new_only else handles[D:]

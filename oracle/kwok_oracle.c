@@ -798,37 +798,60 @@ int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, siz
     return rc < 0 ? rc : bad;
 }
 
-/* kwok_ingest_pods_packed16: each record as the kwok_pod_rec it stands for
- * (KWOK_REC_HOST_NODE_IP: hostIP = the configured NodeIP), through the packed
- * path; the handles of the KWOK_REC_NEW records only, in create order */
-int kwok_oracle_ingest_pods_packed16(kwok_oracle* o, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+/* kwok_ingest_pods_packed12: each record as the kwok_pod_rec it stands for
+ * (KWOK_REC_HOST_NODE_IP: hostIP = the configured NodeIP; value: a create's
+ * creationTimestamp, any other record's podIP, an update keeping the held pod's
+ * creation time), through the packed path; the handles of the KWOK_REC_NEW
+ * records only, in create order.  The creation time an update keeps is the
+ * pod's when the update applies: the batch runs in pieces, cut before an update
+ * of a handle the state does not hold yet (one created earlier in the batch). */
+int kwok_oracle_ingest_pods_packed12(kwok_oracle* o, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
                                      size_t new_cap, int8_t* out_status, uint32_t* out_released) {
     kwok_pod_rec* r = (kwok_pod_rec*)calloc(n + 1, sizeof(kwok_pod_rec));
     int32_t* hs = (int32_t*)calloc(n + 1, sizeof(int32_t));
-    if (!r || !hs) {
-        free(r), free(hs);
+    int8_t* st = (int8_t*)calloc(n + 1, 1);
+    uint32_t* rel = (uint32_t*)calloc(n + 1, sizeof(uint32_t));
+    if (!r || !hs || !st || !rel) {
+        free(r), free(hs), free(st), free(rel);
         return KWOK_ENOMEM;
     }
-    for (size_t i = 0; i < n; i++) {
+    const size_t npods = (size_t)o->B * o->cp;
+    int rc = 0, bad = 0;
+    size_t run = 0;  /* the first record not yet applied */
+    for (size_t i = 0; i <= n && rc >= 0; i++) {
+        const int held_later = i < n && !(recs[i].op & KWOK_REC_NEW) &&
+                               (recs[i].op & (uint8_t)~KWOK_REC_HOST_NODE_IP) == KWOK_OP_UPSERT &&
+                               recs[i].target >= 0 && (size_t)recs[i].target < npods && !o->pods[recs[i].target].used;
+        if ((i == n || held_later) && i > run) {  /* apply [run, i) */
+            rc = kwok_oracle_ingest_pods_packed(o, r + run, i - run, hs + run, st + run, rel + run);
+            if (rc >= 0) bad += rc;
+            run = i;
+        }
+        if (i == n || rc < 0) break;
+        const int nw = (recs[i].op & KWOK_REC_NEW) != 0;
+        const int32_t h = recs[i].target;
         r[i].op = recs[i].op & (uint8_t)~KWOK_REC_HOST_NODE_IP;
         r[i].flags = recs[i].flags;
         r[i].spec_id = recs[i].spec_id;
-        r[i].target = recs[i].target;
-        r[i].creation = recs[i].creation;
+        r[i].target = h;
         r[i].host_ip = (recs[i].op & KWOK_REC_HOST_NODE_IP) ? o->node_ip : 0;
-        r[i].pod_ip = recs[i].pod_ip;
+        r[i].pod_ip = nw ? 0u : recs[i].value;
+        r[i].creation = nw ? recs[i].value
+                           : (h >= 0 && (size_t)h < npods && o->pods[h].used ? (uint32_t)o->pods[h].creation : 0u);
     }
-    int rc = kwok_oracle_ingest_pods_packed(o, r, n, hs, out_status, out_released);
     if (rc >= 0) {
         size_t k = 0;
-        for (size_t i = 0; i < n; i++)
+        for (size_t i = 0; i < n; i++) {
+            if (out_status) out_status[i] = st[i];
+            if (out_released) out_released[i] = rel[i];
             if (recs[i].op & KWOK_REC_NEW) {
                 if (k < new_cap) out_new_handles[k] = hs[i];
                 k++;
             }
-        if (k > new_cap) rc = KWOK_EINVAL;
+        }
+        rc = k > new_cap ? KWOK_EINVAL : bad;
     }
-    free(r), free(hs);
+    free(r), free(hs), free(st), free(rel);
     return rc;
 }
 

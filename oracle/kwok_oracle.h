@@ -19,7 +19,7 @@ int kwok_oracle_ingest_pods(kwok_oracle* o, const kwok_pod_event* ev, size_t n, 
                             int32_t* out_handles, int32_t* out_status, uint32_t* out_released);
 int kwok_oracle_ingest_pods_packed(kwok_oracle* o, const kwok_pod_rec* recs, size_t n, int32_t* out_handles,
                                    int8_t* out_status, uint32_t* out_released);
-int kwok_oracle_ingest_pods_packed16(kwok_oracle* o, const kwok_pod_rec16* recs, size_t n, int32_t* out_new_handles,
+int kwok_oracle_ingest_pods_packed12(kwok_oracle* o, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
                                      size_t new_cap, int8_t* out_status, uint32_t* out_released);
 int kwok_oracle_pool_put(kwok_oracle* o, const uint32_t* ips, size_t n);
 int kwok_oracle_cni_pending(kwok_oracle* o, int32_t* out, size_t cap, size_t* n_out);

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None,
               packed=False):
     """packed: the engine ingests the compact wire form (kwok_ingest_pods_packed;
-    packed=16: kwok_pod_rec16 through kwok_ingest_pods_packed16, which returns the
+    packed=12: kwok_pod_rec12 through kwok_ingest_pods_packed12, which returns the
     creates' handles only), the oracle the same events as kwok_pod_event with
     dotted quads"""
     if threads is not None:
@@ -48,10 +48,10 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
     for t in range(ticks):
         now += 30
         ev, ar = ch.batch(dump, now)
-        if packed == 16:
+        if packed == 12:
             recs, _ = chp.batch(dump, now)
-            assert recs.dtype.itemsize == 16
-            nh, s1, r1 = e.ingest_pods_packed16(recs)
+            assert recs.dtype.itemsize == 12
+            nh, s1, r1 = e.ingest_pods_packed12(recs)
             assert len(nh) == n_churn
             chp.applied(nh.copy(), s1, new_only=True)
             # every other record's handle is its target
@@ -103,30 +103,31 @@ def test_churn_packed_parity():
 
 
 @pytest.mark.timeout(900)
-def test_c4_churn_metric_size_packed16():
-    """the metric-size storm through kwok_pod_rec16 (16 B per record, hostIP as
-    a flag, the creates' handles only back, page-locked and read in place):
-    equal to the oracle per record and per tick"""
+def test_c4_churn_metric_size_packed12():
+    """the metric-size storm through kwok_pod_rec12 (12 B per record: hostIP as
+    a flag, the marked pods' creation times kept by the engine; the creates'
+    handles only back; page-locked and read in place): equal to the oracle per
+    record and per tick"""
     from kwok_amd.engine import host_array
-    run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=16, alloc=host_array)
+    run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array)
 
 
 @pytest.mark.parametrize("chunk", [None, "70000"])
-def test_churn_packed16_parity(chunk, monkeypatch):
-    """20k nodes x 200k pods, 40k + 40k per tick as kwok_pod_rec16 in pageable
+def test_churn_packed12_parity(chunk, monkeypatch):
+    """20k nodes x 200k pods, 40k + 40k per tick as kwok_pod_rec12 in pageable
     memory; chunk: KWOK_INGEST_CHUNK small enough that every batch runs in two
     chunks (the creates' ordinals cross the chunk boundary)"""
     if chunk:
         monkeypatch.setenv("KWOK_INGEST_CHUNK", chunk)
-    run_churn(20_000, 40_000, 3, packed=16)
+    run_churn(20_000, 40_000, 3, packed=12)
 
 
-def test_packed16_edges():
-    """kwok_ingest_pods_packed16 on a small engine against kwok_ingest_pods_packed
+def test_packed12_edges():
+    """kwok_ingest_pods_packed12 on a small engine against kwok_ingest_pods_packed
     on a twin: rejected creates (a node handle the engine does not hold, a bad
-    spec) get -1 at their create ordinal; a hostIP flag stands for the node IP; a
-    create count above new_cap fails after the batch is applied (the engine
-    stays usable); an empty batch"""
+    spec) get -1 at their create ordinal; a hostIP flag stands for the node IP; an
+    update keeps the pod's creation time; a create count above new_cap fails
+    after the batch is applied (the engine stays usable); an empty batch"""
     from kwok_amd import abi
     e1, fl, ph = workload.build_engine_fleet(Engine, 2_000)
     e2, _, _ = workload.build_engine_fleet(Engine, 2_000)
@@ -143,13 +144,14 @@ def test_packed16_edges():
     r["target"][5] = 1 << 30      # a node handle nobody holds
     r["spec_id"][9] = 4000        # no such spec
     r["host_ip"][11] = node_ip    # a create that already holds the node IP
-    r[20]["op"] = abi.OP_UPSERT   # a modify of an existing pod
+    r[20]["op"] = abi.OP_UPSERT   # a modify of an existing pod (its creation time: the fleet's)
     r[20]["target"] = ph[0]
     r[20]["host_ip"] = node_ip
+    r[20]["creation"] = workload.S0 - 60
     r[20]["flags"] = abi.POD_STATUS_NONEMPTY | abi.POD_CONFORMS | (abi.PHASE_RUNNING << abi.REC_PHASE_SHIFT)
-    r16 = abi.pack16(r, node_ip)
+    r12 = abi.pack12(r, node_ip)
     h2, s2, rel2 = e2.ingest_pods_packed(r)
-    nh, s1, rel1 = e1.ingest_pods_packed16(r16)
+    nh, s1, rel1 = e1.ingest_pods_packed12(r12)
     new = (r["op"] & abi.REC_NEW) != 0
     assert (s1 == s2).all() and (rel1 == rel2).all()
     assert (nh == h2[new]).all() and nh[5] == -1 and nh[9] == -1 and (s1[[5, 9]] != 0).all()
@@ -157,13 +159,13 @@ def test_packed16_edges():
     t1, t2 = e1.tick(now), e2.tick(now)
     assert list(t1.counters) == list(t2.counters)
     with pytest.raises(ValueError):  # another hostIP: not expressible
-        abi.pack16(np.array([(abi.OP_UPSERT, 0, 0, ph[1], now, node_ip + 1, 0)], abi.POD_REC_DTYPE), node_ip)
+        abi.pack12(np.array([(abi.OP_UPSERT, 0, 0, ph[1], now, node_ip + 1, 0)], abi.POD_REC_DTYPE), node_ip)
     # new_cap below the creates: the batch applies, the call fails, the engine carries on
-    r2 = r16[:8].copy()
+    r2 = r12[:8].copy()
     r2["target"][5] = fl.node_handles[0]
     with pytest.raises(RuntimeError):
-        e1.ingest_pods_packed16(r2, new_cap=4)
-    e1.ingest_pods_packed16(r16[:0])
+        e1.ingest_pods_packed12(r2, new_cap=4)
+    e1.ingest_pods_packed12(r12[:0])
     now += 30
     e1.tick(now)
     e1.close()

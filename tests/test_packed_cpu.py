@@ -81,11 +81,14 @@ def test_packed_create_without_node_handle_is_rejected_per_record():
     o.close()
 
 
-def test_packed16_on_the_oracle():
-    """kwok_pod_rec16 (16 B: the hostIP as a flag for the node IP) on the oracle
-    against kwok_pod_rec on a twin: the same statuses and releases, the creates'
-    handles in create order (-1 for a rejected one), a create count above
-    new_cap fails with KWOK_EINVAL after the batch is applied"""
+def test_packed12_on_the_oracle():
+    """kwok_pod_rec12 (12 B: the hostIP as a flag for the node IP, one value word:
+    a create's creationTimestamp, any other record's podIP) on the oracle against
+    kwok_pod_rec on a twin: the same statuses and releases, the creates' handles
+    in create order (-1 for a rejected one); an update keeps the pod's creation
+    time (the 20-byte twin carries the same); creates holding a podIP and other
+    hostIPs are not expressible; a create count above new_cap fails with
+    KWOK_EINVAL after the batch is applied"""
     fx = harness.load_trace("doc_known_answer")
     cfg = harness.config_for(fx)
     o1, o2 = Oracle(cfg), Oracle(harness.config_for(fx))
@@ -96,22 +99,43 @@ def test_packed16_on_the_oracle():
                                       {"op": "add", "name": "n1", "managed": True, "lockable": True}])
     nh1, _ = o1.ingest_nodes_raw(recs, arena)
     o2.ingest_nodes_raw(recs, arena)
+    t0 = fx["config"]["start_time"]
     r = np.zeros(6, abi.POD_REC_DTYPE)
     r["op"] = abi.OP_UPSERT | abi.REC_NEW
     r["target"] = [nh1[0], nh1[1], -1, nh1[0], nh1[1], nh1[0]]
     r["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
-    r["creation"] = fx["config"]["start_time"]
+    r["creation"] = t0 - np.arange(6)
     r["host_ip"][3] = node_ip
     h2, s2, rel2 = o2.ingest_pods_packed(r)
-    r16 = abi.pack16(r, node_ip)
-    assert r16["op"][3] & abi.REC_HOST_NODE_IP and not r16["op"][0] & abi.REC_HOST_NODE_IP
-    nh, s1, rel1 = o1.ingest_pods_packed16(r16)
+    r12 = abi.pack12(r, node_ip)
+    assert r12["op"][3] & abi.REC_HOST_NODE_IP and not r12["op"][0] & abi.REC_HOST_NODE_IP
+    assert list(r12["value"]) == list(r["creation"])
+    nh, s1, rel1 = o1.ingest_pods_packed12(r12)
     assert (s1 == s2).all() and (rel1 == rel2).all() and (nh == h2).all() and nh[2] == -1
-    m = np.zeros(2, abi.POD_REC16_DTYPE)
+    # updates (Running, with IPs) of two of them: the creation times stay
+    u = np.zeros(2, abi.POD_REC_DTYPE)
+    u["op"] = abi.OP_UPSERT
+    u["target"] = [nh[0], nh[3]]
+    u["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_RUNNING << abi.REC_PHASE_SHIFT)
+    u["creation"] = [t0, t0 - 3]
+    u["host_ip"] = node_ip
+    u["pod_ip"] = [abi.ip4("10.0.0.9"), abi.ip4("10.0.0.10")]
+    u12 = abi.pack12(u, node_ip)
+    assert list(u12["value"]) == list(u["pod_ip"])
+    o2.ingest_pods_packed(u)
+    _, s1, _ = o1.ingest_pods_packed12(u12)
+    assert (s1 == 0).all()
+    a, b = o1.tick(t0 + 30), o2.tick(t0 + 30)
+    assert list(a.counters) == list(b.counters)
+    for k in range(4):
+        assert (o1.dump_pods(0, 1 << 12)[k] == o2.dump_pods(0, 1 << 12)[k]).all()
+    with pytest.raises(ValueError):  # a create holding a podIP
+        abi.pack12(np.array([(abi.OP_UPSERT | abi.REC_NEW, 0, 0, nh1[0], t0, 0, 5)], abi.POD_REC_DTYPE), node_ip)
+    m = np.zeros(2, abi.POD_REC12_DTYPE)
     m["op"] = [abi.OP_UPSERT, abi.OP_UPSERT | abi.REC_NEW]
     m["target"] = [nh[0], nh1[0]]
     m["flags"] = abi.POD_STATUS_NONEMPTY | (abi.PHASE_PENDING << abi.REC_PHASE_SHIFT)
     with pytest.raises(RuntimeError):
-        o1.ingest_pods_packed16(m, new_cap=0)
+        o1.ingest_pods_packed12(m, new_cap=0)
     o1.close()
     o2.close()

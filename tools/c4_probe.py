@@ -1,8 +1,8 @@
 """The bench's C4 churn leg alone (1M x 10M fleet, 1M + 1M records per tick,
-kwok_pod_rec16 by default) for kernel traces: tools/gpu_c4.sh runs it under
+kwok_pod_rec12 by default) for kernel traces: tools/gpu_c4.sh runs it under
 rocprofv3 and prints the timeline of the last step.
 
-usage: c4_probe.py [--ticks 3] [--wire 16|20|0]"""
+usage: c4_probe.py [--ticks 3] [--wire 12|20|0]"""
 import argparse
 import json
 import os
@@ -16,7 +16,7 @@ from kwok_amd import engine as keng, workload  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ticks", type=int, default=3)
-    ap.add_argument("--wire", type=int, default=16)
+    ap.add_argument("--wire", type=int, default=12)
     ap.add_argument("--nodes", type=int, default=1_000_000)
     a = ap.parse_args()
     e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes)
