@@ -8,5 +8,5 @@ mkdir -p lib/var
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -munsafe-fp-atomics -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $2 \
   -c ${3:-csrc/kernels.hip} -o lib/var/kernels_$1.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/var/libkwok_engine_$1.so lib/engine.o lib/templates.o \
-  lib/codec.o lib/gotemplate.o lib/ingest.o lib/var/kernels_$1.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  lib/codec.o lib/gotemplate.o lib/ingest.o lib/json.o lib/var/kernels_$1.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 strip lib/var/libkwok_engine_$1.so; echo lib/var/libkwok_engine_$1.so
