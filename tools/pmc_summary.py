@@ -22,7 +22,7 @@ def load(d, counter):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] != counter:
                 continue
-            name = row["Kernel_Name"].split("(")[0]
+            name = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             name = name.replace("kwok::", "")
             per.setdefault(name, []).append((int(row["Dispatch_Id"]), float(row["Counter_Value"]) * 1024.0))
     return per
