@@ -1046,7 +1046,7 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->trace_sum[TRACE_SLOTS + k][2] / e->trace_ticks);
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
-    void* ptrs[] = {e->S.trace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
+    void* ptrs[] = {e->S.trace, e->S.jtrace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->d_hb_bpre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
@@ -1314,6 +1314,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.wc_pre, (size_t)S.n_chain * MAX_WC)) ||
         (rc = dalloc(e, &S.wc_dirty, (size_t)S.n_chain * WC_DIRTY_WORDS)) || (rc = dalloc(e, &S.jbase, (size_t)S.n_chain)) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
+        (getenv("KWOK_JOBS_TRACE") && (rc = dalloc(e, &S.jtrace, (size_t)S.n_chain * (MAX_WC + 4) * 4))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, (uint8_t**)&S.hb_kind, HB_MAX_STRIDE)) ||
         (rc = dalloc(e, &S.hdr, 1)) || (rc = dalloc(e, &S.xmsg, 1)) || (rc = dalloc(e, &S.use_list, PLa)) ||
@@ -2639,6 +2640,20 @@ void derive_header(TickHdr& H, uint64_t arena_cap, uint32_t hb_stride, bool hb_o
 
 bool trace_enabled(const kwok_engine* e) { return e->S.trace != nullptr; }
 
+// KWOK_JOBS_TRACE=file: the k_pod_jobs wave stamps of the last tick with pod jobs
+// (tools/jobs_trace.py reads them), zeroed for the next
+void jobs_trace_dump(kwok_engine* e) {
+    const size_t n = (size_t)e->S.n_chain * (MAX_WC + 4) * 4;
+    std::vector<uint64_t> h(n);
+    if (hipMemcpy(h.data(), e->S.jtrace, n * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(e->S.jtrace, 0, n * 8) != hipSuccess)
+        return;
+    if (FILE* f = fopen(getenv("KWOK_JOBS_TRACE"), "wb")) {
+        fwrite(h.data(), 8, n, f);
+        fclose(f);
+    }
+}
+
 // per stamp k: earliest / median / latest block, microseconds after the earliest block start
 void trace_tick(kwok_engine* e) {
     const size_t G = e->S.n_chain, N = G + e->n_stream;
@@ -2760,6 +2775,7 @@ int retire(kwok_engine* e) {
             return failed(e->fail(KWOK_EDEVICE, "k_emit"));
     }
     if (trace_enabled(e)) trace_tick(e);
+    if (e->S.jtrace && H.n_pp) jobs_trace_dump(e);
     if (H.err) {
         const uint32_t err = H.err;
         // a tick queued behind a failed one ran on its state: fail it as well

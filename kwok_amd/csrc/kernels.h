@@ -100,6 +100,7 @@ struct DevState {
     uint32_t* wc_dirty;        //   per 64-group wave chunk, and [n_chain][WC_DIRTY_WORDS] its dirty bits (FRONT)
     JobBase* jbase;            //   [n_chain] (BACK) -> k_pod_jobs
     uint64_t* trace;           // [grid][TRACE_SLOTS] per-block phase stamps (KWOK_TICK_TRACE=1), else null
+    uint64_t* jtrace;          // [n_chain * MAX_WC][4] k_pod_jobs per-wave stamps (KWOK_JOBS_TRACE=file), else null
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
     uint32_t stream_share;     // /1024 of the heartbeat stream written by the streamer blocks (the rest: chain blocks)

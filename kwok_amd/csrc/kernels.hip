@@ -1279,7 +1279,7 @@ __device__ __forceinline__ void fused_pod_emit(const DevState& S, TabWave* W, co
 template <int NC, bool WAVE = false, bool FUSE = false>
 __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_t* gpre, const uint8_t* nflags, uint32_t bk0,
                                                 uint32_t nbk, uint32_t ng, const uint32_t (&gidx)[NC], Bases& run,
-                                                const Layout& L, uint32_t* stage, uint32_t nj0 = 0) {
+                                                const Layout& L, uint32_t* stage, uint32_t nj0 = 0, uint32_t jt = 0) {
     PodGrp g[NC];
     uint16_t sp[NC][POD_PER_THREAD];
 #pragma unroll
@@ -1470,6 +1470,12 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
         if constexpr (FUSE) {  // the staged jobs' bytes: the wave's stage becomes the emission's rows
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (S.jtrace && lane_id() == 0) {
+                const size_t q = (size_t)jt * 4;
+                S.jtrace[q + 1] = __builtin_amdgcn_s_memrealtime();
+                S.jtrace[q + 3] = (uint64_t)fuse_n << 32 | __builtin_amdgcn_s_getreg((4) | (15 << 11)) |
+                                  (uint64_t)(__builtin_amdgcn_s_getreg((20) | (15 << 11)) & 15u) << 28;
+            }
             fused_pod_emit(S, reinterpret_cast<TabWave*>(stg), stg, fuse_n, r.v[AG_PP] + wpre, fuse_off0);
         }
     }
@@ -2722,20 +2728,18 @@ void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t 
 // pod_controller.go:155-183 (DeletePods), 404-439 (configurePod / patch jobs).
 // ---------------------------------------------------------------------------
 constexpr int JOB_WAVES = 4;
+// KWOK_JOBS_TRACE diagnostics: per item (entry, emission start, exit, hw ids | jobs << 32)
+__device__ __forceinline__ void jstamp(const DevState& S, uint32_t item, int k, uint64_t v) {
+    if (S.jtrace && lane_id() == 0) S.jtrace[(size_t)item * 4 + k] = v;
+}
 constexpr int JOB_NC = 2;  // consecutive runs per wave, their loads and scans interleaved
 constexpr int JOB_NF_BYTES = 768;  // node flags staged per wave (two buckets of ~350 node slots)
-// FUSE: the runs' pod patch bytes too (fused_pod_emit over each run's staged jobs,
-// when every spec has unit tables): no job records written and read back by k_emit
+// One wave's runs c0 .. c0 + NC - 1 of chain block b (item: the trace slot)
 template <bool FUSE>
-__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
+__device__ __forceinline__ void pod_jobs_item(const DevState& S, uint32_t tag, uint32_t b, uint32_t c0, uint32_t item,
+                                              uint32_t* stage, uint32_t* gpre, uint32_t* nf) {
     constexpr int NC = FUSE ? 1 : JOB_NC;  // fused: one run per wave (its emission holds the registers)
-    __shared__ uint32_t stage[JOB_WAVES * (FUSE ? POD_STAGE_WORDS_F : POD_STAGE_WORDS)];
-    __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
-    __shared__ uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
-    static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
-    const uint32_t b = blockIdx.x / wg_per_block;
-    const uint32_t w = (uint32_t)wave_id();
-    const uint32_t c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * NC;  // the wave's first run
+    jstamp(S, item, 0, __builtin_amdgcn_s_memrealtime());
     if (b >= S.n_chain || c0 >= (uint32_t)MAX_WC) return;
     // every input of the wave's setup in one round trip: the block's JobBase, the
     // runs' dirty bits and prefix, the fill marks of the block's buckets
@@ -2763,7 +2767,6 @@ __global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevSt
     run.v[AG_PP] += wp.y;
     run.v[AG_PP_BYTES] += wp.z;
     run.v[AG_ALLOC] += wp.w;
-    uint32_t* gpre = gpre_w[w];
     const uint32_t inc = wave_incl_scan(fill >> 3);
     gpre[l + 1] = inc;
     if (l == 0) gpre[0] = 0;
@@ -2779,9 +2782,9 @@ __global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevSt
         const uint32_t nwords = (jb - ja + 1u) * S.cn / 4u;  // (cn % 4 == 0)
         if (nwords * 4u <= (uint32_t)JOB_NF_BYTES) {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(nflags + (size_t)ja * S.cn);
-            for (uint32_t v = (uint32_t)l; v < nwords; v += 64) nf_w[w][v] = src[v];
+            for (uint32_t v = (uint32_t)l; v < nwords; v += 64) nf[v] = src[v];
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            nflags = reinterpret_cast<const uint8_t*>(nf_w[w]);
+            nflags = reinterpret_cast<const uint8_t*>(nf);
             nj0 = ja;
         }
     }
@@ -2790,7 +2793,33 @@ __global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevSt
     uint32_t gx[NC];
 #pragma unroll
     for (int i = 0; i < NC; i++) gx[i] = (c0 + i) * WC_GROUPS + (uint32_t)l;
-    emit_pod_chunks<NC, true, FUSE>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0);
+    emit_pod_chunks<NC, true, FUSE>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0, item);
+    jstamp(S, item, 2, __builtin_amdgcn_s_memrealtime());
+}
+// FUSE: the runs' pod patch bytes too (fused_pod_emit over each run's staged jobs,
+// when every spec has unit tables): no job records written and read back by k_emit.
+// Its waves take the runs run-major (run c0 of every chain block, then c0 + 1, ...):
+// the empty runs past the blocks' pods are the grid's last waves, and the dispatch
+// order mixes the blocks' regions of the arena.
+template <bool FUSE>
+__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
+    constexpr int NC = FUSE ? 1 : JOB_NC;
+    __shared__ uint32_t stage[JOB_WAVES * (FUSE ? POD_STAGE_WORDS_F : POD_STAGE_WORDS)];
+    __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    __shared__ uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
+    static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
+    const uint32_t w = (uint32_t)wave_id(), it = blockIdx.x * JOB_WAVES + w;
+    uint32_t b, c0;
+#ifndef JOBS_BLOCK_MAJOR  // (A/B builds)
+    if constexpr (FUSE) {
+        c0 = it / S.n_chain, b = it - c0 * S.n_chain;
+    } else
+#endif
+    {
+        b = blockIdx.x / wg_per_block;
+        c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * NC;  // the wave's first run
+    }
+    pod_jobs_item<FUSE>(S, tag, b, c0, it, stage, gpre_w[w], nf_w[w]);
 }
 
 // One rank's Use or release list ORed into a bitmap, OR_RUN consecutive entries
@@ -3006,12 +3035,13 @@ void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t
     // the largest chain block's runs: its buckets x their capacity in 8-slot groups
     const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
     const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
-    const uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
-    const uint32_t grid = S.n_chain * (wpb ? wpb : 1u);
+    uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
+    wpb = wpb ? wpb : 1u;
+    const uint32_t grid = S.n_chain * wpb;
     auto kern = S.fuse_pods ? k_pod_jobs<true> : k_pod_jobs<false>;
     if (t0)
-        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb ? wpb : 1u);
-    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb ? wpb : 1u);
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb);
 }
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
@@ -3111,10 +3141,10 @@ static_assert(sizeof(EmitLds) <= 40960, "four k_emit blocks per CU");
 // copy engine): 1M x 10M initial k_emit 1.70 -> 1.62 ms against plain stores
 __device__ __forceinline__ void emit_st(uint8_t* arena, uint64_t off, uint4 v) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifdef EMIT_PLAIN  // A/B builds
-    *reinterpret_cast<u32x4*>(arena + off) = u32x4{v.x, v.y, v.z, v.w};
-#else
+#ifdef EMIT_NT  // A/B builds (plain stores: initial-tick emission -2-4%, round 5)
     __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(arena + off));
+#else
+    *reinterpret_cast<u32x4*>(arena + off) = u32x4{v.x, v.y, v.z, v.w};
 #endif
 }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k); }
@@ -3481,7 +3511,12 @@ __device__ __forceinline__ FlatStep<UNR> flat_load(const DevState& S, const WV* 
         const bool live = k < cnt;
         const uint4 R = W->rec[live ? k : 0u];  // arena offset / 16, table unit base, unit count
         F.k[i] = k;
+#ifdef EMIT_PATCH_ONLY  // A/B builds: only the patch's units
         F.ok[i] = live && u < R.z;
+#else  // the whole reservation (zeros past the patch): the run is one unbroken stream of
+       // whole 128-byte lines, none written in part (initial-tick emission -2-4%, round 5)
+        F.ok[i] = live;
+#endif
         const uint32_t uu = F.ok[i] ? u : 0u;
 #ifdef EMIT_DIAG_NO_TAB  // timing builds only: no table loads
         F.t[i] = make_uint4(uu, R.y, 0u, 0u);

@@ -1,0 +1,70 @@
+// Microbenchmark: how much a small read stream mixed into a write stream costs.
+// The initial tick's emission writes 7.2 GB of patch bytes while its classification
+// reads a few percent of that (pod state, node flags, tables).  Each wave writes a
+// contiguous piece of a 7.2 GB buffer (1 KiB per store instruction, plain stores)
+// and, every `every` stores, reads one 16-byte word per lane from its own piece of a
+// second buffer (the read share = 1 / every).  usage: fill_mix [mb_written]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ void k_mix(u32x4* dst, uint64_t n16, const u32x4* src, uint64_t s16, int every, u32x4* sink) {
+    const int l = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6), q = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nrow = n16 / 64, r0 = nrow * q / W, r1 = nrow * (q + 1) / W;
+    const uint64_t srow = s16 / 64, sr0 = srow * q / W, sr1 = srow * (q + 1) / W;
+    u32x4 acc = u32x4{0u, 0u, 0u, 0u}, v = u32x4{(uint32_t)l, 1u, 2u, 3u};
+    uint64_t sr = sr0;
+    int k = 0;
+    for (uint64_t r = r0; r < r1; r++) {
+        dst[r * 64 + l] = v;
+        if (every && ++k == every) {
+            k = 0;
+            if (sr < sr1) {
+                const u32x4 x = src[sr * 64 + l];
+                acc += x;
+                v.y ^= x.x;  // the stores depend on the reads (as the emission's do)
+                sr++;
+            }
+        }
+    }
+    if (acc.x == 0xFFFFFFFFu) sink[l] = acc;
+}
+int main(int argc, char** argv) {
+    const uint64_t mb = argc > 1 ? strtoull(argv[1], 0, 10) : 7240;
+    const uint64_t n16 = mb * 1000000ull / 16;
+    u32x4 *dst, *src, *sink;
+    const uint64_t s16 = n16 / 8;  // up to 1/8 of the written bytes read
+    if (hipMalloc(&dst, n16 * 16) != hipSuccess || hipMalloc(&src, s16 * 16) != hipSuccess ||
+        hipMalloc(&sink, 64 * 16) != hipSuccess)
+        return 1;
+    (void)hipMemset(src, 1, s16 * 16);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    printf("%llu MB written, %d CUs\n", (unsigned long long)mb, cus);
+    for (int every : {0, 64, 32, 16, 8})
+        for (int wpc : {4, 12}) {
+            const int threads = 256, grid = cus * wpc / 4;
+            auto launch = [&] { hipLaunchKernelGGL(k_mix, dim3(grid), dim3(threads), 0, 0, dst, n16, src, s16, every, sink); };
+            for (int w = 0; w < 2; w++) launch();
+            (void)hipDeviceSynchronize();
+            float best = 1e9, sum = 0;
+            for (int r = 0; r < 8; r++) {
+                (void)hipEventRecord(e0);
+                launch();
+                (void)hipEventRecord(e1);
+                (void)hipEventSynchronize(e1);
+                float ms;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                best = std::min(best, ms);
+                sum += ms;
+            }
+            printf("read 1/%-3d waves/CU %2d: best %7.1f us mean %7.1f us -> write %.2f TB/s (best)\n", every ? every : 0,
+                   wpc, best * 1e3, sum / 8 * 1e3, n16 * 16 / (best * 1e-3) / 1e12);
+        }
+    return 0;
+}
