@@ -299,6 +299,7 @@ struct kwok_engine {
         bool emit_queued = false;   // k_emit was enqueued behind the tick's launches
         bool split = false;         // TICK_SPLIT: k_pod_jobs builds the pod jobs after the tick's launches
         bool fuse = false;          // ... and writes their patch bytes itself (DevState::fuse_pods)
+        bool inits_folded = false;  // ... and the node inits' too (no k_emit launch: KWOK_FOLD_INITS)
         bool quiet = false;         // only pods with an event are Use-checked (kwok_engine::quiet)
         bool once = false;          // launched as k_once (a heartbeat-once tick expected to have nothing to emit)
         bool no_once = false;       // k_once found work: the tick runs again with k_tick
@@ -344,6 +345,7 @@ struct kwok_engine {
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
     int fuse_emit = -1;         // KWOK_FUSE_EMIT: 1 always / 0 never fuse the pod bytes into k_pod_jobs; -1 dense ticks
+    bool fold_inits = true;     // KWOK_FOLD_INITS=0: a fused tick's node inits by k_emit (A/B)
     uint64_t pod_records_since_tick = 0;  // pod records ingested since the last tick was enqueued (fused emission)
     uint32_t n_untabled = 0;    // registered specs without unit tables (no fused emission while any)
     // Quiet ticks.  A tick's Use(podIP) of an evaluated pod (pod_controller.go:
@@ -1255,6 +1257,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->split_jobs = !(sj && sj[0] == '0');
         const char* fe = getenv("KWOK_FUSE_EMIT");
         e->fuse_emit = fe && fe[0] ? (fe[0] == '0' ? 0 : 1) : -1;
+        const char* fi = getenv("KWOK_FOLD_INITS");
+        e->fold_inits = !(fi && fi[0] == '0');
         const char* on = getenv("KWOK_ONCE");
         e->once_ok = !(on && on[0] == '0');
         const char* zc = getenv("KWOK_INGEST_ZC");
@@ -2456,6 +2460,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
     }
     S.fuse_pods = T.fuse ? 1u : 0u;
+    T.inits_folded = false;  // (set where k_pod_jobs is launched)
     // ... and leave the whole stream to the streamers: a dirty chain block's share
     // of it would hold up the pool phase, which waits for every dirty block
     S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
@@ -2517,13 +2522,16 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
                     T.target, st, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr);
         HIPCHK(e, hipGetLastError());
     }
+    // a fused launch writes the node inits too (its last blocks): no k_emit
+    T.inits_folded = T.fuse && e->fold_inits;
     if (T.split) {
-        launch_pod_jobs(S, T.tag, st, ev ? ev[6] : nullptr, ev ? ev[7] : nullptr);
+        launch_pod_jobs(S, T.tag, st, T.inits_folded ? e->emit_grid : 0u, now, (uint64_t)e->start, ev ? ev[6] : nullptr,
+                        ev ? ev[7] : nullptr);
         HIPCHK(e, hipGetLastError());
     }
     // the patch bytes, when events since the last tick make jobs likely (otherwise
     // retire launches k_emit if the tick turns out to have jobs)
-    if (T.emit_queued && (rc = enqueue_emit(e, k))) return rc;
+    if (T.emit_queued && !T.inits_folded && (rc = enqueue_emit(e, k))) return rc;
     HIPCHK(e, hipEventRecord(T.done, st));
     return KWOK_OK;
 }
@@ -2600,11 +2608,13 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     launch_tick(S, e->n_stream, T.now, (uint64_t)e->start, (uint32_t)e->n_managed,
                 TICK_BACK | TICK_XLISTS | (T.split ? TICK_SPLIT : 0), T.tag, T.target, st);
     HIPCHK(e, hipGetLastError());
+    T.inits_folded = T.fuse && e->fold_inits;
     if (T.split) {
-        launch_pod_jobs(S, T.tag, st);
+        launch_pod_jobs(S, T.tag, st, T.inits_folded ? e->emit_grid : 0u, T.now, (uint64_t)e->start);
         HIPCHK(e, hipGetLastError());
     }
-    if ((rc = enqueue_emit(e, k))) return rc;  // this launch built the jobs
+    if (T.inits_folded) T.emit_queued = true;  // (the fused launch wrote every patch)
+    else if ((rc = enqueue_emit(e, k))) return rc;  // this launch built the jobs
     HIPCHK(e, hipStreamSynchronize(st));
     if (next >= 0) return enqueue_tick(e, next, true);
     return KWOK_OK;
@@ -2808,7 +2818,7 @@ int retire(kwok_engine* e) {
         (void)hipEventElapsedTime(&k0, T.pev[0], T.pev[1]);
         if (e->multi) (void)hipEventElapsedTime(&k1, T.pev[2], T.pev[3]);
         float k2 = 0;
-        if (T.emit_queued) (void)hipEventElapsedTime(&k2, T.pev[4], T.pev[5]);
+        if (T.emit_queued && !T.inits_folded) (void)hipEventElapsedTime(&k2, T.pev[4], T.pev[5]);
         float k3 = 0;
         if (T.split) (void)hipEventElapsedTime(&k3, T.pev[6], T.pev[7]);
         const double kern = (double)k0 + k1 + k2 + k3;

@@ -165,7 +165,9 @@ void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t 
 uint32_t once_blocks(const DevState& S);
 // split ticks: the pod jobs (deletes, patch job records, state transitions) of
 // every dirty 64-group run of every chain block, one wave each
-void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// k_pod_jobs; a fused launch (DevState::fuse_pods) also writes the node inits with init_blocks blocks
+void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, uint32_t init_blocks, uint64_t now, uint64_t start,
+                     hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
 // the patch bytes of the tick's jobs (after its k_tick launch(es), on the same stream)
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st);

@@ -2796,32 +2796,6 @@ __device__ __forceinline__ void pod_jobs_item(const DevState& S, uint32_t tag, u
     emit_pod_chunks<NC, true, FUSE>(S, gpre, nflags, bk0, nbk, ng, gx, run, L, stage, nj0, item);
     jstamp(S, item, 2, __builtin_amdgcn_s_memrealtime());
 }
-// FUSE: the runs' pod patch bytes too (fused_pod_emit over each run's staged jobs,
-// when every spec has unit tables): no job records written and read back by k_emit.
-// Its waves take the runs run-major (run c0 of every chain block, then c0 + 1, ...):
-// the empty runs past the blocks' pods are the grid's last waves, and the dispatch
-// order mixes the blocks' regions of the arena.
-template <bool FUSE>
-__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block) {
-    constexpr int NC = FUSE ? 1 : JOB_NC;
-    __shared__ uint32_t stage[JOB_WAVES * (FUSE ? POD_STAGE_WORDS_F : POD_STAGE_WORDS)];
-    __shared__ uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
-    __shared__ uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
-    static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
-    const uint32_t w = (uint32_t)wave_id(), it = blockIdx.x * JOB_WAVES + w;
-    uint32_t b, c0;
-#ifndef JOBS_BLOCK_MAJOR  // (A/B builds)
-    if constexpr (FUSE) {
-        c0 = it / S.n_chain, b = it - c0 * S.n_chain;
-    } else
-#endif
-    {
-        b = blockIdx.x / wg_per_block;
-        c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * NC;  // the wave's first run
-    }
-    pod_jobs_item<FUSE>(S, tag, b, c0, it, stage, gpre_w[w], nf_w[w]);
-}
-
 // One rank's Use or release list ORed into a bitmap, OR_RUN consecutive entries
 // per thread: entries that fall in one bitmap word one after the other (a
 // rank's lists follow canonical order, and addresses were handed out lowest
@@ -3030,19 +3004,6 @@ void launch_pool_apply(const DevState& S, const ListDesc* ld, int nranks, uint32
     hipLaunchKernelGGL(k_pool_apply, dim3(g), dim3(256), 0, st, S, ld, nranks);
 }
 
-
-void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
-    // the largest chain block's runs: its buckets x their capacity in 8-slot groups
-    const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
-    const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
-    uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
-    wpb = wpb ? wpb : 1u;
-    const uint32_t grid = S.n_chain * wpb;
-    auto kern = S.fuse_pods ? k_pod_jobs<true> : k_pod_jobs<false>;
-    if (t0)
-        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb);
-    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb);
-}
 
 void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t start, uint32_t n_hb, int phases,
                  uint32_t tag, uint64_t arrive_target, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
@@ -3733,6 +3694,78 @@ __global__ __launch_bounds__(EMIT_BLOCK, 4) void k_emit(DevState S, uint64_t now
 
 void launch_emit(const DevState& S, uint32_t grid, uint64_t now, uint64_t start, hipStream_t st) {
     hipLaunchKernelGGL(k_emit, dim3(grid), dim3(EMIT_BLOCK), 0, st, S, now, start);
+}
+
+// FUSE: the runs' pod patch bytes too (fused_pod_emit over each run's staged jobs,
+// when every spec has unit tables): no job records written and read back by k_emit.
+// Its waves take the runs run-major (run c0 of every chain block, then c0 + 1, ...):
+// the empty runs past the blocks' pods are the grid's last waves, and the dispatch
+// order mixes the blocks' regions of the arena.  The fused grid's last blocks (from
+// pod_blocks on) write the tick's node inits as k_emit would (one launch for the
+// whole emission: they start as the pod waves drain and fill the CUs those leave).
+struct JobsLdsF {
+    uint32_t stage[JOB_WAVES * POD_STAGE_WORDS_F];
+    uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];  // the node flags of the runs' buckets
+};
+struct JobsLds {
+    uint32_t stage[JOB_WAVES * POD_STAGE_WORDS];
+    uint32_t gpre_w[JOB_WAVES][MAX_BPB + 1];
+    uint32_t nf_w[JOB_WAVES][JOB_NF_BYTES / 4];
+};
+union FusedLds {
+    JobsLdsF j;
+    EmitLds e;
+};
+static_assert(64 * JOB_WAVES == EMIT_BLOCK, "node-init blocks of k_pod_jobs<true> are k_emit blocks");
+template <bool FUSE>
+__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block,
+                                                                          uint32_t pod_blocks, uint64_t now_unix,
+                                                                          uint64_t start_unix) {
+    constexpr int NC = FUSE ? 1 : JOB_NC;
+    __shared__ typename std::conditional<FUSE, FusedLds, JobsLds>::type sh;
+    auto& J = reinterpret_cast<typename std::conditional<FUSE, JobsLdsF, JobsLds>::type&>(sh);
+    static_assert(JOB_NC == 2 && MAX_WC % 32 == 0, "a wave's runs share one dirty word");
+    const uint32_t w = (uint32_t)wave_id(), it = blockIdx.x * JOB_WAVES + w;
+    if constexpr (FUSE) {
+        if (blockIdx.x >= pod_blocks) {  // node inits (block-uniform)
+            if (S.multi && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+            const uint32_t n_init = S.emit_n[1];
+            if (n_init == 0) return;
+            EmitLds* L = reinterpret_cast<EmitLds*>(&sh);
+            stage_emit(S, L, false, true, now_unix, start_unix);
+            const uint32_t w0 = (blockIdx.x - pod_blocks) * JOB_WAVES + w, nw = (gridDim.x - pod_blocks) * JOB_WAVES;
+            if (L->blob_ok) emit_jobs<false, true>(S, L, w0, nw, n_init);
+            else emit_jobs<false, false>(S, L, w0, nw, n_init);
+            return;
+        }
+    }
+    uint32_t b, c0;
+#ifndef JOBS_BLOCK_MAJOR  // (A/B builds)
+    if constexpr (FUSE) {
+        c0 = it / S.n_chain, b = it - c0 * S.n_chain;
+    } else
+#endif
+    {
+        b = blockIdx.x / wg_per_block;
+        c0 = ((blockIdx.x - b * wg_per_block) * JOB_WAVES + w) * NC;  // the wave's first run
+    }
+    pod_jobs_item<FUSE>(S, tag, b, c0, it, J.stage, J.gpre_w[w], J.nf_w[w]);
+}
+
+// init_blocks: the fused launch's node-init blocks (0: k_emit writes the node inits)
+void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, uint32_t init_blocks, uint64_t now, uint64_t start,
+                     hipEvent_t t0, hipEvent_t t1) {
+    // the largest chain block's runs: its buckets x their capacity in 8-slot groups
+    const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
+    const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
+    uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
+    wpb = wpb ? wpb : 1u;
+    const uint32_t pod_blocks = S.n_chain * wpb, grid = pod_blocks + (S.fuse_pods ? init_blocks : 0u);
+    auto kern = S.fuse_pods ? k_pod_jobs<true> : k_pod_jobs<false>;
+    if (t0)
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, t0, t1, 0, S, tag, wpb, pod_blocks, now, start);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * JOB_WAVES), 0, st, S, tag, wpb, pod_blocks, now, start);
 }
 
 int emit_occupancy() {

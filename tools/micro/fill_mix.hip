@@ -3,12 +3,14 @@
 // reads a few percent of that (pod state, node flags, tables).  Each wave writes a
 // contiguous piece of a 7.2 GB buffer (1 KiB per store instruction, plain stores)
 // and, every `every` stores, reads one 16-byte word per lane from its own piece of a
-// second buffer (the read share = 1 / every).  usage: fill_mix [mb_written]
+// second buffer (the read share = 1 / every).  The reads cycle over `rmb` MB (small:
+// Infinity-Cache resident), the stores plain or non-temporal.  usage: fill_mix [mb_written]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
 __global__ void k_mix(u32x4* dst, uint64_t n16, const u32x4* src, uint64_t s16, int every, u32x4* sink) {
     const int l = threadIdx.x & 63;
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6), q = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -18,15 +20,14 @@ __global__ void k_mix(u32x4* dst, uint64_t n16, const u32x4* src, uint64_t s16, 
     uint64_t sr = sr0;
     int k = 0;
     for (uint64_t r = r0; r < r1; r++) {
-        dst[r * 64 + l] = v;
+        if (NT) __builtin_nontemporal_store(v, dst + r * 64 + l);
+        else dst[r * 64 + l] = v;
         if (every && ++k == every) {
             k = 0;
-            if (sr < sr1) {
-                const u32x4 x = src[sr * 64 + l];
-                acc += x;
-                v.y ^= x.x;  // the stores depend on the reads (as the emission's do)
-                sr++;
-            }
+            const u32x4 x = src[sr * 64 + l];
+            acc += x;
+            v.y ^= x.x;  // the stores depend on the reads (as the emission's do)
+            if (++sr >= sr1) sr = sr0;
         }
     }
     if (acc.x == 0xFFFFFFFFu) sink[l] = acc;
@@ -46,25 +47,32 @@ int main(int argc, char** argv) {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     printf("%llu MB written, %d CUs\n", (unsigned long long)mb, cus);
-    for (int every : {0, 64, 32, 16, 8})
-        for (int wpc : {4, 12}) {
-            const int threads = 256, grid = cus * wpc / 4;
-            auto launch = [&] { hipLaunchKernelGGL(k_mix, dim3(grid), dim3(threads), 0, 0, dst, n16, src, s16, every, sink); };
-            for (int w = 0; w < 2; w++) launch();
-            (void)hipDeviceSynchronize();
-            float best = 1e9, sum = 0;
-            for (int r = 0; r < 8; r++) {
-                (void)hipEventRecord(e0);
-                launch();
-                (void)hipEventRecord(e1);
-                (void)hipEventSynchronize(e1);
-                float ms;
-                (void)hipEventElapsedTime(&ms, e0, e1);
-                best = std::min(best, ms);
-                sum += ms;
+    for (int nt = 0; nt < 2; nt++)
+        for (uint64_t rmb : {(uint64_t)0, (uint64_t)64, (uint64_t)800})
+            for (int every : {0, 32}) {
+                if ((every == 0) != (rmb == 0)) continue;
+                const uint64_t r16 = rmb ? rmb * 1000000ull / 16 : s16;
+                const int threads = 256, grid = cus * 3;
+                auto launch = [&] {
+                    if (nt) hipLaunchKernelGGL(k_mix<1>, dim3(grid), dim3(threads), 0, 0, dst, n16, src, r16, every, sink);
+                    else hipLaunchKernelGGL(k_mix<0>, dim3(grid), dim3(threads), 0, 0, dst, n16, src, r16, every, sink);
+                };
+                for (int w = 0; w < 2; w++) launch();
+                (void)hipDeviceSynchronize();
+                float best = 1e9, sum = 0;
+                for (int r = 0; r < 8; r++) {
+                    (void)hipEventRecord(e0);
+                    launch();
+                    (void)hipEventRecord(e1);
+                    (void)hipEventSynchronize(e1);
+                    float ms;
+                    (void)hipEventElapsedTime(&ms, e0, e1);
+                    best = std::min(best, ms);
+                    sum += ms;
+                }
+                printf("%s stores, read 1/%-2d over %4llu MB: best %7.1f us mean %7.1f us -> write %.2f TB/s (best)\n",
+                       nt ? "nt   " : "plain", every, (unsigned long long)rmb, best * 1e3, sum / 8 * 1e3,
+                       n16 * 16 / (best * 1e-3) / 1e12);
             }
-            printf("read 1/%-3d waves/CU %2d: best %7.1f us mean %7.1f us -> write %.2f TB/s (best)\n", every ? every : 0,
-                   wpc, best * 1e3, sum / 8 * 1e3, n16 * 16 / (best * 1e-3) / 1e12);
-        }
     return 0;
 }
