@@ -68,6 +68,7 @@ NODES_PER_RANK = 1_000_000
 NODE_BYTES = 1068 + 9
 POD_BYTES = 10
 NODE_STATE_BYTES = 9 + 9   # the same without the materialised patch (state-only line)
+NODE_SLOT_BYTES = 1          # k_once: a node's state byte
 #   initial tick, per node init 1471 B (9 B check + 4 B index + 1458 B patch), per
 #   Pending->Running pod 577 B (10 + 4 + 8 B reads, 1 + 4 + 4 B writes, ~542 B patch)
 INIT_BYTES = 1471
@@ -359,6 +360,10 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     e.close()
     lc = r.local_counters
     state_bytes = NODE_STATE_BYTES * lc[8] + POD_BYTES * lc[10]
+    # what a k_once launch that reads the per-bucket summaries must move: a managed
+    # node's state byte, one 16-byte summary per bucket, the heartbeat handle list
+    # (4 B per managed node) and the one body
+    once_bytes = NODE_SLOT_BYTES * lc[8] + 16 * workload.BUCKETS + 4 * r.counters[0] + 1072
     kern = ph["kernel"] / max(nt, 1)
     step_ms = dt / steps * 1e3
     traffic, traffic_src = stored_pmc(ONCE_PMC_FILE, "k_once")
@@ -373,16 +378,20 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
             "value": trans / dt, "unit": "transitions/s", "ms_per_step": step_ms,
             "kernel_ms_events": kern, "classify_ms": ph["classify"] / max(nt, 1),
             "tick_kernels": stats,
-            "roofline": {"bound": "hbm (one round trip per bucket, launch-bound at this size)", "kernel": "k_once",
-                         "bytes_per_launch": state_bytes,
-                         "achieved": state_bytes / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": state_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "roofline": {"bound": "latency (two dependent round trips per bucket wave + the count atomics; "
+                                  "launch-bound at this size)", "kernel": "k_once",
+                         "bytes_per_launch": once_bytes,
+                         "achieved": once_bytes / (step_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": once_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_per_step_gbs": traffic / (step_ms * 1e-3) / 1e9 if traffic else None,
                          "timing": "queued step time (launch-to-launch), not the event pair",
-                         "note": "bytes: SURVEY 8(d)'s state model without the materialised bodies (node 9 + 9 B, pod "
-                                 "10 B); k_once reads less - a pod's 2-byte state word, its node index only in "
-                                 "buckets whose nodes disagree on the re-lock flag - see traffic"},
+                         "note": "bytes: what a launch reading the per-bucket summaries moves (node state bytes, "
+                                 "16 B per bucket, 4 B per heartbeat handle, one body; DESIGN.md §16). The state "
+                                 "model of SURVEY 8(d) (node 9 + 9 B, pod 10 B per tick) is state_model_bytes: the "
+                                 "summaries make reading it unnecessary while no pod state changes",
+                         "state_model_bytes": state_bytes,
+                         "state_model_equiv_gbs": state_bytes / (step_ms * 1e-3) / 1e9},
             "initial_tick": {"wall_ms": init_wall * 1e3, "kernel_ms": ph0["kernel"], "emission_ms": ph0["emit_kernel"],
                              "transitions": transitions(r0.counters),
                              "emit_roofline": {"kernel": "k_pod_jobs + k_emit", "bytes": init_bytes,

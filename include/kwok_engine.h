@@ -466,6 +466,7 @@ int kwok_profile_host(kwok_engine* e, int reset, double ms_sum[KWOK_H_COUNT], ui
 enum { KWOK_STAT_TICKS_FULL = 0 /* ticks run by the full tick kernel (redone ticks included) */,
        KWOK_STAT_TICKS_ONCE /* heartbeat-once ticks completed by the counting kernel */,
        KWOK_STAT_ONCE_REDO /* counting-kernel ticks that had work and ran again with the full kernel */,
+       KWOK_STAT_ONCE_SUMMARY /* counting-kernel launches that read the per-bucket summaries, not the pod rows */,
        KWOK_STAT_COUNT };
 int kwok_engine_stats(const kwok_engine* e, uint64_t out[KWOK_STAT_COUNT]);
 

@@ -146,6 +146,7 @@ constexpr int ONCE_WAVES = 8;
 constexpr int ONCE_ACC_WORDS = 5;       // (hb, lock) (managed, ready) (eval, total) (pending, running) (rare, -)
 constexpr int ONCE_FIELD_BITS = 27;     // each packed partial sum < 2^27 (node / pod slots of the rank)
 constexpr int ONCE_NODE_LDS = 1024;     // node slots per bucket it handles (S.cn)
+constexpr uint32_t ONCE_SUM_OFF = 0, ONCE_SUM_BUILD = 1, ONCE_SUM_USE = 2;  // k_once's per-bucket summaries
 
 // cross-block state of the tick kernel (device memory, zeroed at create and
 // after a failed tick), every word on its own 128-byte line

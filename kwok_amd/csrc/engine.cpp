@@ -366,6 +366,12 @@ struct kwok_engine {
     bool global_foreign = false;  // multi rank, sticky: some rank's exchange message carried its foreign_ips
     bool quiet_ok = true;
     bool once_ok = true;        // KWOK_ONCE=0: heartbeat-once ticks always run k_tick (A/B)
+    // k_once's per-bucket summaries (DevState::once_sum): valid while nothing has changed a
+    // pod state since the BUILD tick of generation sum_gen was enqueued (every ingest, CNI
+    // assignment, pool Put, zombie sweep and k_tick launch clears sum_valid)
+    bool once_sum_ok = true;    // KWOK_ONCE_SUM=0: every k_once tick reads the pod rows (A/B)
+    bool sum_valid = false;
+    uint32_t sum_gen = 0;
     uint64_t stats[KWOK_STAT_COUNT] = {};  // kwok_engine_stats
     uint8_t* dump_h = nullptr;  // kwok_dump_pods' page-locked staging
     size_t dump_cap = 0;
@@ -1048,7 +1054,7 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->trace_sum[TRACE_SLOTS + k][2] / e->trace_ticks);
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
-    void* ptrs[] = {e->S.trace, e->S.jtrace, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
+    void* ptrs[] = {e->S.trace, e->S.jtrace, e->S.once_sum, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
                     (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->d_hb_bpre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
@@ -1261,6 +1267,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->fold_inits = !(fi && fi[0] == '0');
         const char* on = getenv("KWOK_ONCE");
         e->once_ok = !(on && on[0] == '0');
+        const char* os = getenv("KWOK_ONCE_SUM");
+        e->once_sum_ok = !(os && os[0] == '0');
         const char* zc = getenv("KWOK_INGEST_ZC");
         e->ingest_zc = !(zc && zc[0] == '0');
     }
@@ -1325,6 +1333,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &S.rel_list, PLa)) || (rc = dalloc(e, &e->d_ld, (size_t)std::max(e->XW, 1))) ||
         (rc = dalloc(e, &S.node_key, NLa)) || (rc = dalloc(e, &S.node_name, NLa * NAME_STRIDE)) ||
         (rc = dalloc(e, &S.mb_count, e->nb)) || (rc = dalloc(e, &S.zb_count, e->nb)) ||
+        (rc = dalloc(e, &S.once_sum, e->nb)) ||
         (rc = alloc_slot(e, 0)))
         return bail(rc);
     // heartbeat template: static bytes + kinds (0..19 Now, 20..39 StartTime)
@@ -1595,6 +1604,7 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     e->quiet = 0;
+    e->sum_valid = false;
     if (!n) return 0;
     const auto t0 = clk::now();
     int rc = node_reserve(e, n, arena_len);
@@ -1766,6 +1776,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     if (e->poisoned) return poisoned(e);
     e->emit_hint = true;
     e->quiet = 0;
+    e->sum_valid = false;
     if (!n) return 0;
     e->pod_records_since_tick += n;
     const auto t0 = clk::now();
@@ -2358,6 +2369,7 @@ int kwok_cni_assign(kwok_engine* e, const int32_t* handles, const uint32_t* ips,
     if (e->poisoned) return poisoned(e);
     if (!n) return 0;
     e->quiet = 0;
+    e->sum_valid = false;
     // a handle assigned twice keeps its last valid IP (configurePod runs once per tick)
     std::vector<uint8_t> wr(n, 0);
     {
@@ -2393,6 +2405,7 @@ int kwok_pool_put(kwok_engine* e, const uint32_t* ips, size_t n) {
     if (e->poisoned) return poisoned(e);
     e->puts.insert(e->puts.end(), ips, ips + n);
     e->quiet = 0;
+    e->sum_valid = false;
     e->foreign_ips = true;  // releases of another rank's pods (multi rank)
     return flush_ops(e);
 }
@@ -2486,13 +2499,28 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     T.once = !e->multi && S.hb_once && e->once_ok && !T.emit_queued && !T.split && T.quiet && !T.no_once &&
              S.cn <= (uint32_t)ONCE_NODE_LDS && e->PL < (1u << ONCE_FIELD_BITS) && e->NL < (1u << ONCE_FIELD_BITS);
     if (T.once) {
-        launch_tick_once(S, now, (uint64_t)e->start, nhb, prof & TICK_PROF, st, ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
+        // per-bucket summaries: BUILD them on the first once tick after a change, USE them after
+        uint32_t mode = ONCE_SUM_OFF;
+        if (e->once_sum_ok && e->Cp <= 0xFFFFu) {
+            if (!e->sum_valid) {
+                if (++e->sum_gen == 0) e->sum_gen = 1;
+                e->sum_valid = true;
+                mode = ONCE_SUM_BUILD;
+            } else {
+                mode = ONCE_SUM_USE;
+                e->stats[KWOK_STAT_ONCE_SUMMARY]++;
+            }
+        }
+        launch_tick_once(S, now, (uint64_t)e->start, nhb, prof & TICK_PROF, mode, e->sum_gen, st, ev ? ev[0] : nullptr,
+                         ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
     } else if (!e->multi) {
+        e->sum_valid = false;  // (a k_tick may change pod states)
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
     } else {
+        e->sum_valid = false;
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         // one allgather of the fixed-size exchange message, then BACK: it folds the
@@ -2712,6 +2740,7 @@ void trace_tick(kwok_engine* e) {
 int redo_tick(kwok_engine* e, int k) {
     kwok_engine::TickSlot& T = e->slots[k];
     e->stats[KWOK_STAT_ONCE_REDO]++;
+    e->sum_valid = false;
     memset(T.hdr_h, 0, sizeof(TickHdr));
     HIPCHK(e, hipMemsetAsync(&e->S.bar->skip, 0, sizeof(uint32_t), e->st));
     T.no_once = true;
@@ -2848,6 +2877,7 @@ int retire(kwok_engine* e) {
     // entries go (k_free_zombies, queued on the engine stream: a tick already
     // queued behind this one reads no such node; every ingest follows it)
     if (H.n_del) {
+        e->sum_valid = false;
         launch_free_zombies(e->S, e->st);
         if (hipGetLastError() != hipSuccess) return failed(e->fail(KWOK_EDEVICE, "k_free_zombies"));
     }

@@ -100,6 +100,7 @@ struct DevState {
     uint32_t* wc_dirty;        //   per 64-group wave chunk, and [n_chain][WC_DIRTY_WORDS] its dirty bits (FRONT)
     JobBase* jbase;            //   [n_chain] (BACK) -> k_pod_jobs
     uint64_t* trace;           // [grid][TRACE_SLOTS] per-block phase stamps (KWOK_TICK_TRACE=1), else null
+    uint4* once_sum;           // [nb] k_once per-bucket summaries (ONCE_SUM_BUILD / _USE)
     uint64_t* jtrace;          // [n_chain * MAX_WC][4] k_pod_jobs per-wave stamps (KWOK_JOBS_TRACE=file), else null
     const DevState* self;      // this struct's copy in device memory (out-of-line kernel phases)
     uint32_t stream_delay;     // streamers start this many 10 ns ticks late (KWOK_TICK_STREAM_DELAY_NS, diagnostics)
@@ -160,8 +161,10 @@ void launch_tick(const DevState& S, uint32_t n_stream, uint64_t now, uint64_t st
 // a heartbeat-once tick expected to have nothing to emit (single rank): one
 // wave per bucket counts it; a tick that has work after all sets TickHdr::redo
 // and GridBar::skip (the host runs it again with launch_tick)
-void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, hipStream_t st,
-                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// sum_mode: ONCE_SUM_OFF / _BUILD (also write the per-bucket summaries of generation gen) /
+// _USE (read those summaries instead of the pod rows where they apply)
+void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, uint32_t sum_mode,
+                      uint32_t gen, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 uint32_t once_blocks(const DevState& S);
 // split ticks: the pod jobs (deletes, patch job records, state transitions) of
 // every dirty 64-group run of every chain block, one wave each

@@ -2533,9 +2533,45 @@ __device__ __forceinline__ uint32_t once_group(const uint32_t (&stw)[4], const u
     return rare & M;
 }
 
+// once_group for a summary (ONCE_SUM_BUILD): the group under both uniform RELOCK
+// flags (every pod's node re-locked, none), for a bucket whose node entries agree
 template <bool CNI>
+__device__ __forceinline__ void once_group_both(const uint32_t (&stw)[4], uint32_t& ev0, uint32_t& ev1, uint32_t& rare0,
+                                                uint32_t& rare1) {
+    constexpr uint32_t M = 0x00010001u;
+    uint32_t r0 = 0, r1 = 0, e0 = 0, e1 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t s = stw[w];
+        const uint32_t s1 = s >> 1, s2 = s >> 2, s5 = s >> 5, s6 = s >> 6, s7 = s >> 7;
+        const uint32_t s8 = s >> 8, s9 = s >> 9, s10 = s >> 10, s11 = s >> 11;
+        const uint32_t live = s & ~s2;
+        const uint32_t a = live & s6, b = live & (s6 | ~s1);  // eval without / with RELOCK
+        const uint32_t running = s9 & ~(s8 | s10);
+        const uint32_t ok = running & s5 & s7;
+        const uint32_t na = CNI ? a & ~ok & s11 : a & ~(ok & s11), nb = CNI ? b & ~ok & s11 : b & ~(ok & s11);
+        const uint32_t base = (s & s2) | (a & s6);  // (eval & EVENT is the same under both flags)
+        r0 |= base | na, r1 |= base | nb;
+        e0 += a & M, e1 += b & M;
+    }
+    ev0 += (e0 & 0xFFFFu) + (e0 >> 16);
+    ev1 += (e1 & 0xFFFFu) + (e1 >> 16);
+    rare0 |= r0 & M, rare1 |= r1 & M;
+}
+
+// Per-bucket summaries (ONCE_SUM_*): a steady fleet's pod states do not change
+// between heartbeat-once ticks that emit nothing, and a pod's counts depend on
+// its node only through the RELOCK flag - uniform over a bucket whose node
+// entries agree.  A BUILD tick reads every pod state row as usual and also writes
+// each bucket's counts under both uniform flags (uint4: eval | eval-with-RELOCK,
+// total | pending, running | rare bits, generation).  A USE tick, enqueued only
+// while no ingest, CNI assignment, pool Put or k_tick has run since the BUILD
+// (the host's DevState::once_sum validity), reads the node words and the 16-byte
+// summary instead of the pod rows; a bucket whose nodes disagree on RELOCK, or
+// whose summary is of another generation, is read in full.
+template <bool CNI, uint32_t SUM>  // SUM: ONCE_SUM_OFF / _BUILD / _USE (each its own registers)
 __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_t now_unix, uint64_t start_unix,
-                                                            uint32_t n_hb, int phases) {
+                                                            uint32_t n_hb, int phases, uint32_t gen) {
     __shared__ uint32_t nfl32[ONCE_WAVES][ONCE_NODE_LDS / 4];  // the bucket's node tick flags, per wave
     __shared__ uint64_t part[ONCE_WAVES][ONCE_ACC_WORDS];
     __shared__ uint8_t tmpl[16 * HB_MAX_UNITS];
@@ -2551,6 +2587,7 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
         atomicMax(&S.bar->neg_entry_max, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
     const uint32_t bk = b * ONCE_WAVES + w;
     uint32_t hb = 0, lock = 0, mng = 0, rdy = 0, ev = 0, tot = 0, pnd = 0, run = 0, rare = 0;
+    uint32_t be0 = 0, be1 = 0, br0 = 0, br1 = 0;  // SUM == ONCE_SUM_BUILD: eval / rare under both uniform flags
     if (bk < S.nb) {  // (wave-uniform)
         const uint32_t cn = S.cn, cp = S.cp;
         const uint32_t fill = min((uint32_t)S.pod_fill[bk], cp);
@@ -2564,12 +2601,14 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
             if (256u * c < cn && i < cn) nw[c] = *reinterpret_cast<const uint32_t*>(nst + i);
         }
         const uint16_t* pst = S.pod_state + (size_t)bk * cp;
-        uint4 st[ONCE_ROWS];
+        constexpr bool use = SUM == ONCE_SUM_USE;
+        uint4 sm = make_uint4(0, 0, 0, 0), st[ONCE_ROWS];
+        if (use) sm = S.once_sum[bk];  // (one address: one request)
 #pragma unroll
         for (int r = 0; r < ONCE_ROWS; r++) {
             const uint32_t g8 = 8u * (l + 64u * r);
             st[r] = make_uint4(0, 0, 0, 0);
-            if (g8 < (r < ONCE_SPEC_ROWS ? cp : fill)) st[r] = *reinterpret_cast<const uint4*>(pst + g8);
+            if (!use && g8 < (r < ONCE_SPEC_ROWS ? cp : fill)) st[r] = *reinterpret_cast<const uint4*>(pst + g8);
         }
         // ---- nodes: LockNode / configureNode (A.5), heartbeat handles, re-lock flags
         uint32_t or0 = 0, and0 = 1, has = 0, base = S.hb_bpre[bk];
@@ -2615,6 +2654,7 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
             const bool in = g8 < fill;
             const uint32_t stw[4] = {in ? s4.x : 0u, in ? s4.y : 0u, in ? s4.z : 0u, in ? s4.w : 0u};
             rare |= once_group<CNI>(stw, rl, ev, tot, pnd, run);
+            if constexpr (SUM == ONCE_SUM_BUILD) once_group_both<CNI>(stw, be0, be1, br0, br1);
         };
         auto lds_flags = [&](const uint4& n4, uint32_t (&rl)[4]) {
             const uint8_t* nfw = reinterpret_cast<const uint8_t*>(nfl32[w]);
@@ -2626,7 +2666,20 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
                 rl[k] = a | c << 16;  // (NT_RELOCK is bit 0)
             }
         };
-        if (uni) {
+        if (use && uni && sm.w == gen) {  // the bucket's summary (lane 0's counts; rare from any lane)
+            if (l == 0) {
+                ev += u ? sm.x >> 16 : sm.x & 0xFFFFu;
+                tot += sm.y & 0xFFFFu, pnd += sm.y >> 16, run += sm.z & 0xFFFFu;
+            }
+            rare |= (sm.z >> (u ? 17 : 16)) & 1u;
+        } else if (uni) {
+            if (use) {  // (another generation: the rows now)
+#pragma unroll
+                for (int r = 0; r < ONCE_ROWS; r++) {
+                    const uint32_t g8 = 8u * (l + 64u * r);
+                    if (g8 < fill) st[r] = *reinterpret_cast<const uint4*>(pst + g8);
+                }
+            }
             const uint32_t p = u ? 0x00010001u : 0u;
             const uint32_t rl[4] = {p, p, p, p};
 #pragma unroll
@@ -2642,6 +2695,7 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
             for (int r = 0; r < ONCE_ROWS; r++) {
                 const uint32_t g8 = 8u * (l + 64u * r);
                 nd[r] = g8 < fill ? *reinterpret_cast<const uint4*>(pnd_ + g8) : make_uint4(0, 0, 0, 0);
+                if (use && g8 < fill) st[r] = *reinterpret_cast<const uint4*>(pst + g8);
             }
             __builtin_amdgcn_wave_barrier();  // (the wave's node flags are in LDS)
 #pragma unroll
@@ -2671,6 +2725,13 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
         const uint64_t v2 = wsum(ev) | wsum(tot) << ONCE_FIELD_BITS, v3 = wsum(pnd) | wsum(run) << ONCE_FIELD_BITS;
         const uint64_t v4 = __ballot(rare != 0) ? 1u : 0u;
         if (l == 0) part[w][0] = v0, part[w][1] = v1, part[w][2] = v2, part[w][3] = v3, part[w][4] = v4;
+        if constexpr (SUM == ONCE_SUM_BUILD) {  // the bucket's summary (one wave = one bucket)
+            const uint32_t E0 = (uint32_t)wsum(be0), E1 = (uint32_t)wsum(be1);
+            const uint32_t k0 = __ballot(br0 != 0) ? 1u : 0u, k1 = __ballot(br1 != 0) ? 1u : 0u;
+            if (l == 0 && bk < S.nb)
+                S.once_sum[bk] = make_uint4(E0 | E1 << 16, (uint32_t)(v2 >> ONCE_FIELD_BITS) | (uint32_t)(v3 & ONCE_M27) << 16,
+                                            (uint32_t)(v3 >> ONCE_FIELD_BITS) | k0 << 16 | k1 << 17, gen);
+        }
     }
     __syncthreads();
     if (t < (uint32_t)ONCE_ACC_WORDS) {
@@ -2708,12 +2769,16 @@ __global__ __launch_bounds__(64 * ONCE_WAVES, 2) void k_once(DevState S, uint64_
 
 uint32_t once_blocks(const DevState& S) { return (S.nb + ONCE_WAVES - 1) / ONCE_WAVES; }
 
-void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, hipStream_t st,
-                      hipEvent_t t0, hipEvent_t t1) {
+void launch_tick_once(const DevState& S, uint64_t now, uint64_t start, uint32_t n_hb, int phases, uint32_t sum_mode,
+                      uint32_t gen, hipStream_t st, hipEvent_t t0, hipEvent_t t1) {
     const uint32_t grid = once_blocks(S);
-    auto kern = S.cni ? k_once<true> : k_once<false>;
-    if (t0) hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, t0, t1, 0, S, now, start, n_hb, phases);
-    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, S, now, start, n_hb, phases);
+    decltype(&k_once<false, ONCE_SUM_OFF>) kern;
+    if (sum_mode == ONCE_SUM_BUILD) kern = S.cni ? k_once<true, ONCE_SUM_BUILD> : k_once<false, ONCE_SUM_BUILD>;
+    else if (sum_mode == ONCE_SUM_USE) kern = S.cni ? k_once<true, ONCE_SUM_USE> : k_once<false, ONCE_SUM_USE>;
+    else kern = S.cni ? k_once<true, ONCE_SUM_OFF> : k_once<false, ONCE_SUM_OFF>;
+    if (t0)
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, t0, t1, 0, S, now, start, n_hb, phases, gen);
+    else hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * ONCE_WAVES), 0, st, S, now, start, n_hb, phases, gen);
 }
 
 // ---------------------------------------------------------------------------

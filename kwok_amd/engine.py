@@ -517,10 +517,11 @@ class Engine(EngineBase):
             return C.cast(arena.ctypes.data, C.c_char_p), arena.nbytes
         return (arena or b"\0"), len(arena or b"")
 
-    STATS = ("ticks_full", "ticks_once", "once_redo")  # KWOK_STAT_* order
+    STATS = ("ticks_full", "ticks_once", "once_redo", "once_summary")  # KWOK_STAT_* order
 
     def stats(self):
-        """kwok_engine_stats: ticks run by k_tick / completed by k_once / k_once ticks redone"""
+        """kwok_engine_stats: ticks run by k_tick / completed by k_once / k_once ticks redone / k_once
+        launches that read the per-bucket summaries"""
         out = (C.c_uint64 * len(self.STATS))()
         self._check(self._lib.kwok_engine_stats(self._h, out), "engine_stats")
         return dict(zip(self.STATS, list(out)))

@@ -91,6 +91,58 @@ def test_steady_ticks_run_k_once(managed_all):
     s1 = d.e.stats()
     assert s1["ticks_once"] - s0["ticks_once"] >= 5, s1
     assert s1["once_redo"] == s0["once_redo"], s1
+    # the first quiet tick builds the per-bucket summaries, the later ones read them
+    assert s1["once_summary"] - s0["once_summary"] >= 4, s1
+    d.e.close()
+    d.o.close()
+
+
+def test_summaries_follow_cni_assignments():
+    """k_once's per-bucket summaries (built by the first quiet tick, read by the
+    next ones) go stale when kwok_cni_assign gives pods their IPs between quiet
+    ticks (no ingest): the tick after the assignment builds them again and finds
+    the pods' patches (a redo), equal to the oracle; after a kwok_pool_put
+    (non-CNI engine) they are built again before they are read"""
+    import ipaddress
+    d = OnceDriver(dict(KW, enable_cni=True), 31)
+    rng = d.rng
+    nodes, st = d.nodes(["node-%04d" % i for i in range(300)], np.ones(300, np.uint8), np.ones(300, np.uint8))
+    assert (st == 0).all()
+    ev, ar = new_pods(rng, nodes, 2000, d.spec)
+    d.pods(ev, ar)
+    d.tick("initial")
+    for t in range(3):
+        d.tick("quiet %d" % t)
+    s0 = d.e.stats()
+    assert s0["once_summary"] >= 2, s0
+    pe, po = d.e.cni_pending(), d.o.cni_pending()
+    assert (pe == po).all() and len(pe) >= 2, len(pe)
+    base = int(ipaddress.IPv4Address("172.20.0.2"))
+    take = pe[: len(pe) // 2]
+    ips = np.arange(base, base + len(take), dtype=np.uint32)
+    assert (d.e.cni_assign(take, ips) == d.o.cni_assign(take, ips)).all()
+    d.tick("after the assignment")
+    s1 = d.e.stats()
+    assert s1["once_redo"] == s0["once_redo"] + 1, s1
+    assert s1["once_summary"] == s0["once_summary"], s1  # (rebuilt, not read)
+    for t in range(2):
+        d.tick("quiet after %d" % t)
+    d.tick_pair("quiet queued")
+    d.e.close()
+    d.o.close()
+
+    d, nodes, rng = _fleet(33, True)
+    d.tick("initial")
+    for t in range(2):
+        d.tick("quiet %d" % t)
+    s0 = d.e.stats()
+    put = np.array([int(ipaddress.IPv4Address("10.0.250.5"))], np.uint32)
+    d.e.pool_put(put)
+    d.o.pool_put(put)
+    for t in range(4):  # (a Put makes the next two ticks Use-check every pod: k_tick)
+        d.tick("after a pool Put %d" % t)
+    s1 = d.e.stats()
+    assert s1["once_summary"] == s0["once_summary"] + 1, (s0, s1)  # built by the third, read by the fourth
     d.e.close()
     d.o.close()
 

@@ -6,12 +6,14 @@ set -o pipefail
 TAG=${1:-x}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_once_gpu.py tests/test_parity_gpu.py tests/test_controller_gpu.py -x -v -m gpu --timeout 200 --timeout-method thread > $R/gpurun_out/once_tests_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_once_gpu.py tests/test_cni_gpu.py tests/test_parity_gpu.py tests/test_controller_gpu.py -x -v -m gpu --timeout 200 --timeout-method thread > $R/gpurun_out/once_tests_$TAG.log 2>&1
 rc=$?
 tail -4 $R/gpurun_out/once_tests_$TAG.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $R/gpurun_out/once_tests_$TAG.log | head -30; exit $rc; }
+# (AB=KWOK_ONCE_SUM: per-bucket summaries on / off instead of k_once on / off)
+AB=${AB:-KWOK_ONCE}
 for ab in 1 0 1 0; do
-  KWOK_ONCE=$ab timeout -k 10 200 python tools/once_probe.py 200 "once=$ab" 2>&1 | tail -1 || exit 3
+  env $AB=$ab timeout -k 10 200 python tools/once_probe.py 200 "$AB=$ab" 2>&1 | tail -1 || exit 3
 done
 KWOK_TICK_TRACE=1 KWOK_TICK_TRACE_SKIP=8 timeout -k 10 200 python tools/once_probe.py 40 trace > $R/gpurun_out/once_trace_$TAG.txt 2>&1 || exit 4
 grep -E "kwok trace|queued" $R/gpurun_out/once_trace_$TAG.txt | head -30
