@@ -76,8 +76,8 @@ POD_PATCH_BYTES = 577
 #   C4 tick, per deleted pod: 10 B re-check + 4 B handle + 1 B finalizer flag + 4 B release
 DELETE_BYTES = 19
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
-PMC_FILE = "r8x_pmc.json"
-ONCE_PMC_FILE = "r8x_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
+PMC_FILE = "r9d_pmc.json"
+ONCE_PMC_FILE = "r9d_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
 
 
 def parse():
@@ -366,7 +366,8 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     once_bytes = NODE_SLOT_BYTES * lc[8] + 16 * workload.BUCKETS + 4 * r.counters[0] + 1072
     kern = ph["kernel"] / max(nt, 1)
     step_ms = dt / steps * 1e3
-    traffic, traffic_src = stored_pmc(ONCE_PMC_FILE, "k_once")
+    # (the steady ticks' instance: k_once reading the per-bucket summaries, ONCE_SUM_USE = 2)
+    traffic, traffic_src = stored_pmc(ONCE_PMC_FILE, "void k_once<false, 2u>")
     ilc = r0.local_counters
     init_bytes = INIT_BYTES * ilc[1] + POD_PATCH_BYTES * ilc[2]
     # the roofline over the queued step (kernel + the gap to the next launch), a lower
