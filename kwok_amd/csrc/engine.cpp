@@ -1421,6 +1421,10 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
     }
     e->max_init_len = 0;
     if ((rc = size_arena(e)) || (rc = grow_arena(e, e->slots[0]))) return bail(rc);
+    // a warm-up launch of k_tick (phases 0: every block returns at once): the runtime
+    // sets up the queue's scratch for the kernel here, not inside the first tick
+    // (measured ~0.3-0.6 ms on the initial tick when k_tick's frame is not empty)
+    launch_tick(S, e->n_stream, 0, 0, 0, 0, 0, 0, e->st);
     {
         hipError_t r = hipStreamSynchronize(e->st);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "create sync: %s", hipGetErrorString(r)));

@@ -1971,6 +1971,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
     __shared__ Layout sh_L;
     uint8_t* hb_tmpl = reinterpret_cast<uint8_t*>(hb_tmpl4);
     const uint8_t* nflags = reinterpret_cast<const uint8_t*>(nflags32);
+    if (phases == 0) return;  // the engine's warm-up launch (its scratch is set up before the first tick)
     if (!(phases & TICK_XLISTS) && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return;  // queued behind a tick the host has not finished (long lists; k_once redo): re-launched later
 #define TSTAMP(k)                                                                                         \
