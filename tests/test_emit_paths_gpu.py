@@ -20,16 +20,22 @@ from kwok_amd import abi
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["table", "table-fused", "table-unfused", "general", "mixed"])
+@pytest.fixture(autouse=True, params=["table", "table-fused", "table-fused-k_emit-inits", "table-unfused", "general",
+                                      "mixed"])
 def emit_path(request, monkeypatch):
     """pod patches from the per-shape unit tables (on split ticks written by
-    k_pod_jobs itself, the fused emission, when the tick is dense; "table-fused"
-    on every split tick, KWOK_FUSE_EMIT=1; "table-unfused": always by k_emit
-    from job records, KWOK_FUSE_EMIT=0), from the general region emitter
+    k_pod_jobs itself, the fused emission, when the tick is dense, its last
+    blocks writing the node inits; "table-fused" on every split tick,
+    KWOK_FUSE_EMIT=1; "table-fused-k_emit-inits" the same with the node inits
+    left to k_emit, KWOK_FOLD_INITS=0; "table-unfused": always by k_emit from
+    job records, KWOK_FUSE_EMIT=0), from the general region emitter
     (KWOK_EMIT_TAB_UNITS=0), or both (a cap that tables only the first specs
     registered, so chunks mix the two and fall back as a whole; no fusion)"""
     if request.param == "table-fused":
         monkeypatch.setenv("KWOK_FUSE_EMIT", "1")
+    elif request.param == "table-fused-k_emit-inits":
+        monkeypatch.setenv("KWOK_FUSE_EMIT", "1")
+        monkeypatch.setenv("KWOK_FOLD_INITS", "0")
     elif request.param == "table-unfused":
         monkeypatch.setenv("KWOK_FUSE_EMIT", "0")
     elif request.param == "general":
