@@ -2945,7 +2945,9 @@ __global__ void k_pool_apply(DevState S, const ListDesc* ld, int nranks) {
 // CIDR, so BACK folds and applies xw ranks' worth of Gets, Uses and Puts
 __device__ __forceinline__ uint32_t emul_shift(const PoolGeom& g, uint32_t ip, uint32_t r, uint32_t xw) {
     if (!in_cidr(g, ip)) return ip;
-    return g.net + (uint32_t)(((uint64_t)(ip - g.net) + (g.size / xw) * r) % g.size);
+    uint64_t v = (uint64_t)(ip - g.net) + (g.size / xw) * r;  // < 2 * size (r < xw)
+    if (v >= g.size) v -= g.size;
+    return g.net + (uint32_t)v;
 }
 __global__ void k_emulate_msgs(DevState S, XMsg* X, uint32_t xw) {
     const uint32_t r = blockIdx.x + 1;
@@ -2960,12 +2962,12 @@ __global__ void k_emulate_msgs(DevState S, XMsg* X, uint32_t xw) {
     }
 }
 // ... and their long lists: slot 0 of each rank-major list block copied, moved
+// (grid.y = the synthetic rank, r - 1)
 __global__ void k_emulate_lists(DevState S, uint32_t* recv, uint64_t maxl, uint32_t xw, uint32_t n) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)n * (xw - 1);
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(i / n) + 1, k = (uint32_t)(i % n);
-        recv[r * maxl + k] = emul_shift(S.pool, recv[k], r, xw);
-    }
+    const uint32_t r = blockIdx.y + 1;
+    uint32_t* dst = recv + r * maxl;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+        dst[k] = emul_shift(S.pool, recv[k], r, xw);
 }
 
 __global__ void k_apply_node_ops(DevState S, const NodeOp* ops, uint32_t n) {
@@ -3020,7 +3022,8 @@ void launch_emulate_msgs(const DevState& S, XMsg* X, uint32_t xw, hipStream_t st
     if (xw > 1) hipLaunchKernelGGL(k_emulate_msgs, dim3(xw - 1), dim3(256), 0, st, S, X, xw);
 }
 void launch_emulate_lists(const DevState& S, uint32_t* recv, uint64_t maxl, uint32_t xw, uint32_t n, hipStream_t st) {
-    if (xw > 1 && n) hipLaunchKernelGGL(k_emulate_lists, dim3(1024), dim3(256), 0, st, S, recv, maxl, xw, n);
+    if (xw > 1 && n) hipLaunchKernelGGL(k_emulate_lists, dim3(std::min<uint32_t>(cdiv(n, 256), 512), xw - 1), dim3(256), 0, st, S,
+                                        recv, maxl, xw, n);
 }
 // one block per chain block: its Use and release segments to their place in dst
 // (every block's Uses, then every block's releases, in block order)
