@@ -786,8 +786,9 @@ struct PodGrp {
     __device__ __forceinline__ uint32_t st(int k) const { return (stw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; }
     __device__ __forceinline__ uint32_t nl(int k) const { return (ndw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; }
 };
+// (with_ip = false: the podIPs stay 0, for load_group_ips_set after the state lands)
 __device__ __forceinline__ void load_group(const DevState& S, const uint32_t* gpre, uint32_t bk0, uint32_t nbk,
-                                           uint32_t ng, uint32_t gi, PodGrp& g) {
+                                           uint32_t ng, uint32_t gi, PodGrp& g, bool with_ip = true) {
     uint4 st4 = make_uint4(0, 0, 0, 0), nd4 = st4, ipa = st4, ipb = st4;
     g.slot = ~0u;
     g.j = 0;
@@ -797,24 +798,42 @@ __device__ __forceinline__ void load_group(const DevState& S, const uint32_t* gp
         g.slot = (bk0 + j) * S.cp + (gi - gpre[j]) * (uint32_t)POD_PER_THREAD;
         st4 = *reinterpret_cast<const uint4*>(S.pod_state + g.slot);
         nd4 = *reinterpret_cast<const uint4*>(S.pod_node + g.slot);
-        ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
-        ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
+        if (with_ip) {
+            ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
+            ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
+        }
     }
     g.stw[0] = st4.x, g.stw[1] = st4.y, g.stw[2] = st4.z, g.stw[3] = st4.w;
     g.ndw[0] = nd4.x, g.ndw[1] = nd4.y, g.ndw[2] = nd4.z, g.ndw[3] = nd4.w;
     g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
     g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
 }
-// could this pod need a patch (computePatchData), given it is evaluated?
-__device__ __forceinline__ bool maybe_need(uint16_t st, uint32_t ip) {
+// could this pod need a patch (computePatchData), given it is evaluated?  (podIP == 0:
+// the state's PS_IP_SET, so the podIPs need not have landed)
+__device__ __forceinline__ bool maybe_need(uint16_t st) {
     const uint32_t phase = (st & PS_PHASE_MASK) >> PS_PHASE_SHIFT;
-    return (st & PS_USED) && (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || ip == 0);
+    return (st & PS_USED) &&
+           (phase != PHASE_RUNNING || !(st & PS_CONFORMS) || !(st & PS_HAS_HOST_IP) || !(st & PS_IP_SET));
+}
+// the podIPs of a group loaded without them, when one of its pods holds one
+// (PS_IP_SET; a pod without it has pod_ip 0): the dense initial tick's new pods
+// hold none, so their 4 bytes each are not read
+__device__ __forceinline__ void load_group_ips_set(const DevState& S, PodGrp& g) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) any |= (g.st(k) & PS_IP_SET) != 0;
+    if (any && g.slot != ~0u) {
+        const uint4 ipa = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot);
+        const uint4 ipb = *reinterpret_cast<const uint4*>(S.pod_ip + g.slot + 4);
+        g.ip[0] = ipa.x, g.ip[1] = ipa.y, g.ip[2] = ipa.z, g.ip[3] = ipa.w;
+        g.ip[4] = ipb.x, g.ip[5] = ipb.y, g.ip[6] = ipb.z, g.ip[7] = ipb.w;
+    }
 }
 // spec ids of a group, loaded only when one of its pods may need a patch
 __device__ __forceinline__ void load_spec_ids(const DevState& S, const PodGrp& g, uint16_t (&sp)[POD_PER_THREAD]) {
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(g.st(k), g.ip[k]);
+    for (int k = 0; k < POD_PER_THREAD; k++) any |= maybe_need(g.st(k));
     uint4 v = make_uint4(0, 0, 0, 0);
     if (any && g.slot != ~0u) v = *reinterpret_cast<const uint4*>(S.pod_spec + g.slot);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -1283,7 +1302,11 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
     PodGrp g[NC];
     uint16_t sp[NC][POD_PER_THREAD];
 #pragma unroll
-    for (int i = 0; i < NC; i++) load_group(S, gpre, bk0, nbk, ng, gidx[i], g[i]);
+    for (int i = 0; i < NC; i++) load_group(S, gpre, bk0, nbk, ng, gidx[i], g[i], !FUSE);
+    if constexpr (FUSE) {  // (issued with the spec ids: the same round trip)
+#pragma unroll
+        for (int i = 0; i < NC; i++) load_group_ips_set(S, g[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NC; i++) load_spec_ids(S, g[i], sp[i]);
     PodCls cl[NC][POD_PER_THREAD];
@@ -1319,8 +1342,16 @@ __device__ __forceinline__ void emit_pod_chunks(const DevState& S, const uint32_
             }
             const uint4 ta = *reinterpret_cast<const uint4*>(S.pod_ctime + g[i].slot);
             const uint4 tb = *reinterpret_cast<const uint4*>(S.pod_ctime + g[i].slot + 4);
-            const uint4 ha = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot);
-            const uint4 hb = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot + 4);
+            // held host IPs only when a pod holds one (a pod without PS_HAS_HOST_IP gets the
+            // node's; its host_ip word is not read, and is written as 0 with the group's)
+            bool any_hip = false;
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) any_hip |= (g[i].st(k) & PS_HAS_HOST_IP) != 0;
+            uint4 ha = make_uint4(0, 0, 0, 0), hb = ha;
+            if (any_hip) {
+                ha = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot);
+                hb = *reinterpret_cast<const uint4*>(S.host_ip + g[i].slot + 4);
+            }
             ctm[i][0] = ta.x, ctm[i][1] = ta.y, ctm[i][2] = ta.z, ctm[i][3] = ta.w;
             ctm[i][4] = tb.x, ctm[i][5] = tb.y, ctm[i][6] = tb.z, ctm[i][7] = tb.w;
             hipk[i][0] = ha.x, hipk[i][1] = ha.y, hipk[i][2] = ha.z, hipk[i][3] = ha.w;
@@ -3787,8 +3818,12 @@ union FusedLds {
     EmitLds e;
 };
 static_assert(64 * JOB_WAVES == EMIT_BLOCK, "node-init blocks of k_pod_jobs<true> are k_emit blocks");
+#ifndef JOBS_MIN_WAVES_UNFUSED
+#define JOBS_MIN_WAVES_UNFUSED 1
+#endif
+#define JOBS_MIN_WAVES (FUSE ? 3 : JOBS_MIN_WAVES_UNFUSED)  // waves per SIMD
 template <bool FUSE>
-__global__ __launch_bounds__(64 * JOB_WAVES, FUSE ? 3 : 1) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block,
+__global__ __launch_bounds__(64 * JOB_WAVES, JOBS_MIN_WAVES) void k_pod_jobs(DevState S, uint32_t tag, uint32_t wg_per_block,
                                                                           uint32_t pod_blocks, uint64_t now_unix,
                                                                           uint64_t start_unix) {
     constexpr int NC = FUSE ? 1 : JOB_NC;
