@@ -1851,14 +1851,20 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         return KWOK_OK;
     };
     const bool tstamp = e->iprof && G.tev[0] && K == 2;
+    clk::time_point t_copy0 = t0, t_synced = t0;
+    // (the copy is issued first: each chunk has its own range of the record buffer, and
+    // no earlier work still reads it - the previous call returned synchronised - so the
+    // link starts as soon as possible; the waits guard the prep kernel)
     auto prep = [&](uint32_t k) -> int {
         const IngestBatch b = chunk_batch(k);
-        if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
+        if (k == 0) t_copy0 = clk::now();
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k], ps));  // 0 / 2: chunk k's copy starts
-        HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
         if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
+        if (k == 0) HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));  // the engine stream's earlier work
+        if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
+        HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
         launch_ingest_prep(e->S, b, ps);
         HIPCHK(e, hipGetLastError());
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k + 1], ps));  // 1 / 3: its prep done
@@ -1909,11 +1915,13 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     // again with the host in the loop (ingest_chunk), in order.
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
-        HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
-        if (arena_len && !zar && !resident) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
-        HIPCHK(e, hipMemsetAsync(G.abort, 0, 4, st));
+        if (arena_len && !zar && !resident) {  // (the arena ahead of the records: prep reads both)
+            HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
+            HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
+        }
         for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
             if (int r = prep(k)) return r;
+        HIPCHK(e, hipMemsetAsync(G.abort, 0, 4, st));
         hipStream_t rs = K > 1 && e->results_stream ? G.dst : st;
         for (uint32_t k = 0; k < K; k++) {
             const IngestBatch I = chunk_batch(k);
@@ -1943,6 +1951,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         const auto tq = clk::now();
         HIPCHK(e, hipStreamSynchronize(st));
         if (K > 1) HIPCHK(e, hipStreamSynchronize(G.dst));
+        t_synced = clk::now();
         if (tstamp) {
             float ms[6] = {};
             for (int q = 1; q < 7; q++) (void)hipEventElapsedTime(&ms[q - 1], G.tev[0], G.tev[q]);
@@ -1991,13 +2000,18 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
                      G.sums_h[K - 1].n_new, new_cap);
     else if (rc < 0 && e->ing_mutated)
         e->poisoned = true;
-    // nothing of this batch stays queued on the engine / prep / results streams (a failed chunk included)
-    if (hipStreamSynchronize(st) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest engine stream");
-    if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
-    if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
+    // nothing of this batch stays queued on the engine / prep / results streams (a failed
+    // chunk included; a batch that ran to its end synchronised them in run(): the engine
+    // stream's applies waited for every prep, the results stream was synchronised)
+    if (rc < 0) {
+        if (hipStreamSynchronize(st) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest engine stream");
+        if (hipStreamSynchronize(ps) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest prep stream");
+        if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
+    }
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s): %.2f ms\n", n, zev ? ", read in place" : "", K,
-                K == 1 ? "" : "s", ms_between(t0, clk::now()));
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s): %.3f ms (first copy queued at %.3f, synced at %.3f)\n",
+                n, zev ? ", read in place" : "", K, K == 1 ? "" : "s", ms_between(t0, clk::now()), ms_between(t0, t_copy0),
+                ms_between(t0, t_synced));
     return rc;
 }
 
@@ -2437,6 +2451,10 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     DevState& S = e->S;
     kwok_engine::TickSlot& T = e->slots[k];
     hipStream_t st = e->st;
+    // KWOK_INGEST_PROF: the host time to each launch of the tick (us after entry)
+    const auto q0 = clk::now();
+    double qs[4] = {-1, -1, -1, -1};  // hb_pre queued, slot bound, k_tick / k_once queued, k_pod_jobs queued
+    auto qstamp = [&](int i) { if (e->iprof) qs[i] = ms_between(q0, clk::now()) * 1e3; };
     hipEvent_t* ev = e->prof ? T.pev : nullptr;
     uint32_t nhb = (uint32_t)e->n_managed;  // = the device's count of managed local node slots
     if (e->debug_fault_tick && e->front_launches + 1 == e->debug_fault_tick && !requeue) nhb++;  // tests: TICK_ERR_LAYOUT
@@ -2447,6 +2465,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         launch_hb_pre(S, e->d_hb_pre, e->d_hb_bpre, st);
         HIPCHK(e, hipGetLastError());
         e->hb_pre_dirty = false;
+        qstamp(0);
     }
     // a long heartbeat stream is shared with the chain blocks once they are done
     // (measured at C2: 921/1024 to the streamers; short streams: streamers only)
@@ -2486,6 +2505,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     S.foreign = e->foreign_ips ? 1u : 0u;
     int rc = bind_slot(e, k);
     if (rc) return rc;
+    qstamp(1);
     const int prof = (ev ? TICK_PROF : 0) | (e->chain_prio ? TICK_PRIO : 0) | (e->no_stream ? TICK_NOSTREAM : 0) |
                      (T.split ? TICK_SPLIT : 0);
     if (!requeue) {
@@ -2518,11 +2538,13 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         launch_tick_once(S, now, (uint64_t)e->start, nhb, prof & TICK_PROF, mode, e->sum_gen, st, ev ? ev[0] : nullptr,
                          ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
+        qstamp(2);
     } else if (!e->multi) {
         e->sum_valid = false;  // (a k_tick may change pod states)
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | TICK_BACK | prof, T.tag, T.target, st,
                     ev ? ev[0] : nullptr, ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
+        qstamp(2);
     } else {
         e->sum_valid = false;
         launch_tick(S, e->n_stream, now, (uint64_t)e->start, nhb, TICK_FRONT | prof, T.tag, T.target, st,
@@ -2560,11 +2582,15 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         launch_pod_jobs(S, T.tag, st, T.inits_folded ? e->emit_grid : 0u, now, (uint64_t)e->start, ev ? ev[6] : nullptr,
                         ev ? ev[7] : nullptr);
         HIPCHK(e, hipGetLastError());
+        qstamp(3);
     }
     // the patch bytes, when events since the last tick make jobs likely (otherwise
     // retire launches k_emit if the tick turns out to have jobs)
     if (T.emit_queued && !T.inits_folded && (rc = enqueue_emit(e, k))) return rc;
     HIPCHK(e, hipEventRecord(T.done, st));
+    if (e->iprof)
+        fprintf(stderr, "[kwok enqueue] us: hb_pre %.1f, bound %.1f, tick %.1f, pod_jobs %.1f, all %.1f\n", qs[0], qs[1], qs[2],
+                qs[3], ms_between(q0, clk::now()) * 1e3);
     return KWOK_OK;
 }
 // multi rank, after the BACK launch of slot k's tick found lists too long to be
@@ -2942,6 +2968,7 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     // its collectives in the same order whatever its submit / collect pattern
     if (e->multi) drain(e);
     if (e->poisoned) return poisoned(e);  // the drained tick failed (its error stays collectable)
+    const auto t_drained = clk::now();
     int k = -1;
     for (int pass = 0; pass < 2 && k < 0; pass++)  // prefer keeping the last collected tick's outputs
         for (int i = 0; i < 2 && k < 0; i++)
@@ -2970,7 +2997,8 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     if (rc) return rc;
     T.state = SLOT_QUEUED;
     e->queue[e->nq++] = k;
-    if (e->iprof) fprintf(stderr, "[kwok submit] enqueue %.3f ms\n", ms_between(t0, clk::now()));
+    if (e->iprof)
+        fprintf(stderr, "[kwok submit] enqueue %.3f ms (drain %.3f)\n", ms_between(t0, clk::now()), ms_between(t0, t_drained));
     e->host_ms[KWOK_H_ENQUEUE] += ms_between(t0, clk::now());
     e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
     return KWOK_OK;
