@@ -2,7 +2,7 @@
 kwok_pod_rec12 by default) for kernel traces: tools/gpu_c4.sh runs it under
 rocprofv3 and prints the timeline of the last step.
 
-usage: c4_probe.py [--ticks 3] [--wire 12|20|0]"""
+usage: c4_probe.py [--ticks 3] [--wire 12|20|0] [--once]  (--once: a KWOK_CFG_HEARTBEAT_ONCE engine)"""
 import argparse
 import json
 import os
@@ -18,8 +18,9 @@ def main():
     ap.add_argument("--ticks", type=int, default=3)
     ap.add_argument("--wire", type=int, default=12)
     ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--once", action="store_true")
     a = ap.parse_args()
-    e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes)
+    e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes, heartbeat_once=a.once)
     now = workload.S0 + 30
     e.tick(now, read=False)
     now += 30
