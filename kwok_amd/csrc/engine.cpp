@@ -1852,17 +1852,19 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     };
     const bool tstamp = e->iprof && G.tev[0] && K == 2;
     clk::time_point t_copy0 = t0, t_synced = t0;
-    // (the copy is issued first: each chunk has its own range of the record buffer, and
-    // no earlier work still reads it - the previous call returned synchronised - so the
-    // link starts as soon as possible; the waits guard the prep kernel)
+    // (the copy goes ahead of the summary reset: the link starts as early as possible.
+    // Chunk 0 waits for the engine stream's earlier work first - the buffers' zeroing
+    // when ingest_reserve just allocated them, above all)
     auto prep = [&](uint32_t k) -> int {
         const IngestBatch b = chunk_batch(k);
-        if (k == 0) t_copy0 = clk::now();
+        if (k == 0) {
+            t_copy0 = clk::now();
+            HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
+        }
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[2 * k], ps));  // 0 / 2: chunk k's copy starts
         if (!zev && !resident)
             HIPCHK(e, hipMemcpyAsync(const_cast<uint8_t*>(rec_at(G.d_ev, lo_of(k))), rec_at(recs, lo_of(k)), (size_t)b.n * RB,
                                      hipMemcpyHostToDevice, ps));
-        if (k == 0) HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));  // the engine stream's earlier work
         if (k >= 2) HIPCHK(e, hipStreamWaitEvent(ps, G.used[k & 1], 0));
         HIPCHK(e, hipMemsetAsync(b.sum, 0, sizeof(IngSummary), ps));
         launch_ingest_prep(e->S, b, ps);
@@ -1916,7 +1918,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
         if (arena_len && !zar && !resident) {  // (the arena ahead of the records: prep reads both)
-            HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
+            HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));  // (its buffer's zeroing, if just allocated)
             HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, ps));
         }
         for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
