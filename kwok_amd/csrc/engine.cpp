@@ -220,6 +220,7 @@ struct kwok_engine {
         hipStream_t pst = nullptr, dst = nullptr;  // prep (H2D + k_ing_prep) / results (D2H)
         hipEvent_t tev[8] = {};  // KWOK_INGEST_PROF: device-side phase stamps of a two-chunk batch
         hipEvent_t go = nullptr, prepped[2] = {nullptr, nullptr}, used[2] = {nullptr, nullptr};
+        hipEvent_t idone = nullptr;  // a pod batch's last operation (the host spins on it: KWOK_SYNC)
         hipEvent_t rdone = nullptr;  // the results stream's work of a batch (kwok_pod_rec12: before the summaries)
         size_t chunk = 1048576;
     } ing;
@@ -1075,7 +1076,7 @@ void kwok_engine_destroy(kwok_engine* e) {
         if (g.nsum_h) (void)hipHostFree(g.nsum_h);
         if (g.sums_h) (void)hipHostFree(g.sums_h);
         if (g.res_h) (void)hipHostFree(g.res_h);
-        hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1], g.rdone};
+        hipEvent_t evs[] = {g.go, g.prepped[0], g.prepped[1], g.used[0], g.used[1], g.rdone, g.idone};
         for (hipEvent_t x : evs)
             if (x) (void)hipEventDestroy(x);
         if (g.pst) (void)hipStreamDestroy(g.pst);
@@ -1389,7 +1390,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
             return bail(KWOK_ENOMEM);
         hipError_t r = hipStreamCreateWithFlags(&g.pst, hipStreamNonBlocking);
         if (r == hipSuccess) r = hipStreamCreateWithFlags(&g.dst, hipStreamNonBlocking);
-        hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1], &g.rdone};
+        hipEvent_t* evs[] = {&g.go, &g.prepped[0], &g.prepped[1], &g.used[0], &g.used[1], &g.rdone, &g.idone};
         for (hipEvent_t* x : evs)
             if (r == hipSuccess) r = hipEventCreateWithFlags(x, hipEventDisableTiming);
         if (r != hipSuccess) return bail(e->fail(KWOK_EDEVICE, "ingest stream/events: %s", hipGetErrorString(r)));
@@ -1948,11 +1949,22 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
                 HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
             }
         }
+        if (packed != 2 && rs != st) {  // (the results stream joins the engine stream: one wait below)
+            HIPCHK(e, hipEventRecord(G.rdone, rs));
+            HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
+        }
         HIPCHK(e, hipMemcpyAsync(G.sums_h, G.sums, (size_t)K * sizeof(IngSummary), hipMemcpyDeviceToHost, st));
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[6], rs));  // 6: results copied
         const auto tq = clk::now();
-        HIPCHK(e, hipStreamSynchronize(st));
-        if (K > 1) HIPCHK(e, hipStreamSynchronize(G.dst));
+        if (e->sync_spin) {  // spin on the batch's last operation (as a tick's completion: no wake-up latency)
+            HIPCHK(e, hipEventRecord(G.idone, st));
+            hipError_t q;
+            while ((q = hipEventQuery(G.idone)) == hipErrorNotReady) {
+            }
+            if (q != hipSuccess) return e->fail(KWOK_EDEVICE, "ingest: %s", hipGetErrorString(q));
+        } else {
+            HIPCHK(e, hipStreamSynchronize(st));
+        }
         t_synced = clk::now();
         if (tstamp) {
             float ms[6] = {};
