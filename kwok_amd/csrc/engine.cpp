@@ -2023,9 +2023,10 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         if (hipStreamSynchronize(G.dst) != hipSuccess && rc >= 0) rc = e->fail(KWOK_EDEVICE, "ingest results stream");
     }
     if (e->iprof)
-        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s): %.3f ms (first copy queued at %.3f, synced at %.3f)\n",
-                n, zev ? ", read in place" : "", K, K == 1 ? "" : "s", ms_between(t0, clk::now()), ms_between(t0, t_copy0),
-                ms_between(t0, t_synced));
+        fprintf(stderr, "[kwok ingest] %zu pod records (GPU%s, %u chunk%s%s): %.3f ms (first copy queued at %.3f, synced at %.3f)\n",
+                n, zev ? ", read in place" : "", K, K == 1 ? "" : "s",
+                packed == 2 ? (new_map ? ", create handles mapped" : ", create handles copied") : "", ms_between(t0, clk::now()),
+                ms_between(t0, t_copy0), ms_between(t0, t_synced));
     return rc;
 }
 

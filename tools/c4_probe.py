@@ -2,7 +2,8 @@
 kwok_pod_rec12 by default) for kernel traces: tools/gpu_c4.sh runs it under
 rocprofv3 and prints the timeline of the last step.
 
-usage: c4_probe.py [--ticks 3] [--wire 12|20|0] [--once]  (--once: a KWOK_CFG_HEARTBEAT_ONCE engine)"""
+usage: c4_probe.py [--ticks 3] [--wire 12|20|0] [--once] [--steady N]  (--once: a KWOK_CFG_HEARTBEAT_ONCE engine;
+--steady: N queued steady ticks before the churn, as bench.py's legs)"""
 import argparse
 import json
 import os
@@ -19,10 +20,13 @@ def main():
     ap.add_argument("--wire", type=int, default=12)
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--once", action="store_true")
+    ap.add_argument("--steady", type=int, default=0)
     a = ap.parse_args()
     e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes, heartbeat_once=a.once)
     now = workload.S0 + 30
     e.tick(now, read=False)
+    if a.steady:
+        _, _, now = bench.steady_queued(e, now, a.steady, 3)
     now += 30
     _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire)
     e.close()
