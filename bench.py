@@ -99,7 +99,44 @@ def parse():
                                                          "metric size: 2M create/delete per tick)")
     ap.add_argument("--emulate-ranks", type=int, default=8, help="N=1: a one-rank RCCL engine folding this many "
                                                                  "ranks' exchange messages (0: skip)")
+    ap.add_argument("--leg", default="", help=argparse.SUPPRESS)  # (internal: one secondary leg, in a child process)
+    ap.add_argument("--legs-inline", type=int, default=0,
+                    help="run the secondary legs in this process instead of one child process each")
     return ap.parse_args()
+
+
+SECONDARY_LEGS = ("flap", "flap_once", "hb_once", "c2", "emul")
+
+
+def run_leg(name, a):
+    """One secondary leg (N=1) of this process's arguments"""
+    if name == "flap":
+        return flap_leg(a.nodes_per_rank, a.flap_ticks)
+    if name == "flap_once":
+        return flap_leg(a.nodes_per_rank, a.flap_ticks, True)
+    if name == "hb_once":
+        return heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup, a.churn_ticks, a.json_ticks)
+    if name == "c2":
+        return c2_leg(a.steps, a.warmup)
+    if name == "emul":
+        return emulated_ranks_leg(a.nodes_per_rank, a.emulate_ranks, 20, min(a.churn_ticks, 3))
+    raise ValueError(name)
+
+
+def leg(name, a):
+    """A secondary leg in a child process of its own (the default): each leg's engine
+    starts on a fresh device context, as a deployment's one engine per process does.
+    Engines created one after another in one process measured slower ingest, ~0.1-0.2 ms
+    per C4 batch by the third (tools/c4_seq_probe.py).  The child writes the leg's JSON
+    on its stdout; its stderr is this process's."""
+    if a.legs_inline:
+        return run_leg(name, a)
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + ["--leg", name]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError("bench leg %s failed (exit %d)" % (name, r.returncode))
+    return json.loads(r.stdout.decode().strip().splitlines()[-1])
 
 
 def cidr_for(total_pods):
@@ -616,6 +653,10 @@ def main():
     os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if a.leg:  # a child process of leg(): one secondary leg, its JSON on stdout
+        torch.cuda.set_device(0)
+        os.write(json_out, (json.dumps(run_leg(a.leg, a)) + "\n").encode())
+        return
     local = 0 if REHEARSAL else int(os.environ.get("LOCAL_RANK", "0"))
     if REHEARSAL:
         os.environ.setdefault("KWOK_TICK_BLOCKS_PER_CU", "1")
@@ -741,14 +782,11 @@ def main():
                                           rank, world, barrier, max_over_ranks, packed=False, ch=ch)
 
     e.close()
-    flap = flap_leg(a.nodes_per_rank, a.flap_ticks) if world == 1 and a.flap_ticks > 0 else None
-    flap_once = flap_leg(a.nodes_per_rank, a.flap_ticks, True) if world == 1 and a.flap_ticks > 0 and a.once_ticks \
-        else None
-    hb_once = heartbeat_once_leg(a.nodes_per_rank, a.steps, a.warmup, a.churn_ticks, a.json_ticks) \
-        if world == 1 and a.once_ticks else None
-    c2 = c2_leg(a.steps, a.warmup) if world == 1 and a.c2 and a.nodes_per_rank == NODES_PER_RANK else None
-    emul = emulated_ranks_leg(a.nodes_per_rank, a.emulate_ranks, 20, min(a.churn_ticks, 3)) \
-        if world == 1 and a.emulate_ranks > 1 and not REHEARSAL else None
+    flap = leg("flap", a) if world == 1 and a.flap_ticks > 0 else None
+    flap_once = leg("flap_once", a) if world == 1 and a.flap_ticks > 0 and a.once_ticks else None
+    hb_once = leg("hb_once", a) if world == 1 and a.once_ticks else None
+    c2 = leg("c2", a) if world == 1 and a.c2 and a.nodes_per_rank == NODES_PER_RANK else None
+    emul = leg("emul", a) if world == 1 and a.emulate_ranks > 1 and not REHEARSAL else None
 
     if rank == 0:
         kern_ms = phases["kernel"] / max(nt, 1)
