@@ -78,6 +78,7 @@ DELETE_BYTES = 19
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
 PMC_FILE = "r9k_pmc.json"
 ONCE_PMC_FILE = "r9k_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
+C4_PMC_FILE = "r10_c4once_pmc.json"  # the heartbeat-once engine's C4 tick kernels (tools/gpu_c4once.sh)
 
 
 def parse():
@@ -199,7 +200,7 @@ def cpu_baseline(nodes, threads, ticks):
 
 
 def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
-              packed=12, ch=None, multi=False):
+              packed=12, ch=None, multi=False, once=False):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -300,7 +301,7 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
         # allgather, and for long lists the host round trip, second allgather, k_pool_apply
         "exchange_ms": xch / ticks if (world > 1 or multi) else None,
         "phase_ms": phases,
-        "roofline": c4_roofline(last, kern / ticks) if last else None,
+        "roofline": c4_roofline(last, kern / ticks, once) if last else None,
         "counters_last_tick": last,
         "note": "ingest = kwok_ingest_pods: H2D of the records and their strings (page-locked batch buffers, "
                 "kwok_host_alloc; batches over KWOK_INGEST_CHUNK records in chunks, each copied while the previous "
@@ -309,16 +310,33 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
                 "~0.2 s there, so the first device work of a step can pay a clock ramp: medians beside means)"}
 
 
-def c4_roofline(c, kern_ms):
-    """the churn tick's kernels (k_tick + the emission) against HBM: the steady
-    tick's bytes (heartbeats, node and pod re-checks) + per Pending->Running
-    patch POD_PATCH_BYTES + per deletion DELETE_BYTES, over the profiled tick's
-    kernel time (HIP events around its launches)"""
-    b = NODE_BYTES * c["heartbeat"] + POD_BYTES * c["pods_total"] + POD_PATCH_BYTES * c["pod_patch"] + \
-        DELETE_BYTES * c["delete"]
+def c4_roofline(c, kern_ms, once=False):
+    """the churn tick's kernels (k_tick + the job build + k_emit) against HBM: the
+    steady tick's bytes (heartbeats - once: the node's state model only, one body
+    - node and pod re-checks) + per Pending->Running patch POD_PATCH_BYTES + per
+    deletion DELETE_BYTES, over the profiled tick's kernel time (HIP events
+    around its launches).  once: traffic from the stored PMC passes of this
+    kernel build (tools/gpu_c4once.sh), summed over the tick's kernels"""
+    nb = NODE_STATE_BYTES if once else NODE_BYTES
+    b = nb * c["heartbeat"] + POD_BYTES * c["pods_total"] + POD_PATCH_BYTES * c["pod_patch"] + DELETE_BYTES * c["delete"]
     ach = b / (kern_ms * 1e-3) / 1e9 if kern_ms else None
-    return {"bound": "hbm", "kernel": "k_tick + k_pod_jobs + k_emit", "bytes_per_tick": b, "kernel_ms": kern_ms,
-            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None}
+    out = {"bound": "hbm", "kernel": "k_tick + k_sparse_jobs + k_emit", "bytes_per_tick": b, "kernel_ms": kern_ms,
+           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
+           "byte_model": "per node %d B, per live pod %d B, per patch %d B, per delete %d B" % (
+               nb, POD_BYTES, POD_PATCH_BYTES, DELETE_BYTES)}
+    if once:
+        tr, src = 0, []
+        for k in ("k_tick", "k_sparse_jobs", "k_emit"):
+            t, sname = stored_pmc(C4_PMC_FILE, k)
+            if t is None:
+                tr = None
+                break
+            tr += t
+            src.append(sname)
+        out["traffic"] = tr
+        out["traffic_source"] = "; ".join(src) if tr else None
+        out["traffic_ratio"] = tr / b if tr else None
+    return out
 
 
 def steady_queued(e, now, steps, warmup):
@@ -381,6 +399,10 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     init_wall = time.perf_counter() - t1
     ph0, _ = e.profile_read()
     e.profile_enable(False)
+    # the drop-in's read-back of that tick (ShimReader: lists + every patch byte, page-locked)
+    t1 = time.perf_counter()
+    init_read = ShimReader(e).read(r0)
+    init_read_s = time.perf_counter() - t1
     dt, trans, now = steady_queued(e, now, steps, warmup)
     e.profile_enable(True)
     for _ in range(20):
@@ -390,8 +412,12 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     e.profile_enable(False)
     stats = e.stats()
     churn = cjson = None
+    handoff = {}
     if churn_ticks:
-        now, ch, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes)
+        now, ch, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes, once=True)
+        for ov in (False, True):
+            now, ch, handoff["overlapped" if ov else "sequential"] = churn_handoff_leg(e, fl, ch, now, max(3, churn_ticks),
+                                                                                     nodes, ov)
         if json_ticks:
             now, _, cjson = churn_json_leg(e, fl, ch, now, json_ticks, nodes)
     e.close()
@@ -432,14 +458,20 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
                          "state_model_equiv_gbs": state_bytes / (step_ms * 1e-3) / 1e9},
             "initial_tick": {"wall_ms": init_wall * 1e3, "kernel_ms": ph0["kernel"], "emission_ms": ph0["emit_kernel"],
                              "transitions": transitions(r0.counters),
+                             "with_handoff": {"ms": (init_wall + init_read_s) * 1e3, "read_ms": init_read_s * 1e3,
+                                              "bytes_to_host": init_read[0], "pieces": init_read[1],
+                                              "link_gbs": init_read[0] / init_read_s / 1e9,
+                                              "what": "the tick, then the drop-in's read-back (ShimReader: lists, one "
+                                                      "heartbeat body, every node-init and pod patch byte in 64 MiB "
+                                                      "pieces into page-locked memory)"},
                              "emit_roofline": {"kernel": "k_pod_jobs + k_emit", "bytes": init_bytes,
                                                "achieved": init_bytes / (ph0["emit_kernel"] * 1e-3) / 1e9
                                                if ph0["emit_kernel"] else None,
                                                "frac": init_bytes / (ph0["emit_kernel"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                                                if ph0["emit_kernel"] else None}},
-            "churn": None if churn is None else {k: churn[k] for k in (
+            "churn": None if churn is None else dict({k: churn[k] for k in (
                 "workload", "ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "emission_ms", "value",
-                "unit", "tick_transitions_per_s")},
+                "unit", "tick_transitions_per_s", "roofline", "phase_ms")}, with_handoff=handoff),
             "churn_json": cjson}
 
 
@@ -609,6 +641,127 @@ def flap_leg(nodes, ticks, heartbeat_once=False):
             "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
             "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
             "counters_last_tick": last}
+
+
+class ShimReader:
+    """What the Go drop-in reads back after a tick (engine_cgo.go tick /
+    applyPatches): the lists (kwok_read_outputs without an
+    arena: heartbeat handles only when their epoch changed, node-init / pod-patch
+    handles with offsets and lengths, the delete list), ONE heartbeat body, then
+    every node-init and pod patch byte in pieces of at most READ_CHUNK bytes
+    (kwok_read_arena), all into page-locked host memory (kwok_host_alloc).  The
+    apply callback gets views of the staging buffer (no copy here; the Go shim
+    hands them to its PATCH pool).  asynchronous=True: the pieces are queued with
+    kwok_read_arena_async into one staging buffer of the tick's patch bytes and
+    waited for later (read_wait), so the next batch's ingest and tick run under
+    the device-to-host copy."""
+
+    READ_CHUNK = 64 << 20  # engine_cgo.go readChunk
+
+    def __init__(self, e, asynchronous=False):
+        self.e = e
+        self.asynchronous = asynchronous
+        self.epoch = None
+        self.bufs = {}
+
+    def buf(self, name, n, dt):
+        b = self.bufs.get(name)
+        if b is None or b.size < n:
+            b = self.bufs[name] = keng.host_array((max(int(n * 1.25), 1),), dt)
+        return b
+
+    def read(self, res):
+        """returns (bytes over the link, arena pieces)"""
+        e = self.e
+        hb = self.buf("hb", res.n_heartbeat, np.int32) if res.heartbeat_epoch != self.epoch else None
+        self.epoch = res.heartbeat_epoch
+        ini, ini_off, ini_len = (self.buf("ini", res.n_node_init, np.int32), self.buf("ini_off", res.n_node_init, np.uint64),
+                                 self.buf("ini_len", res.n_node_init, np.uint32))
+        pp, pp_off, pp_len = (self.buf("pp", res.n_pod_patch, np.int32), self.buf("pp_off", res.n_pod_patch, np.uint64),
+                              self.buf("pp_len", res.n_pod_patch, np.uint32))
+        dl, dlf = self.buf("dl", res.n_delete, np.int32), self.buf("dlf", res.n_delete, np.uint8)
+        out = abi.Outputs(hb.ctypes.data if hb is not None else None, 0, ini.ctypes.data, ini_off.ctypes.data,
+                          ini_len.ctypes.data, pp.ctypes.data, pp_off.ctypes.data, pp_len.ctypes.data,
+                          dl.ctypes.data, dlf.ctypes.data, None, 0, 0)
+        e._check(e._lib.kwok_read_outputs(e._h, C.byref(out)), "read_outputs (lists)")
+        nbytes = (res.n_heartbeat * 4 if hb is not None else 0) + res.n_node_init * 16 + res.n_pod_patch * 16 + \
+            res.n_delete * 5
+        pieces = 0
+        if res.n_heartbeat:
+            body = self.buf("body", res.heartbeat_len, np.uint8)
+            e.read_arena(out.heartbeat_off, res.heartbeat_len, body)
+            nbytes += res.heartbeat_len
+        total = sum(int(ln[:n].sum()) for n, ln in ((res.n_node_init, ini_len), (res.n_pod_patch, pp_len)))
+        stage = self.buf("stage", total if self.asynchronous else self.READ_CHUNK, np.uint8)
+        at = 0
+        for n, offs, lens in ((res.n_node_init, ini_off, ini_len), (res.n_pod_patch, pp_off, pp_len)):
+            if not n:
+                continue
+            offs, ends = offs[:n], offs[:n].astype(np.int64) + lens[:n]
+            i = 0
+            while i < n:  # the shim's greedy pieces: consecutive patches within READ_CHUNK bytes
+                lo = int(offs[i])
+                j = max(i + 1, int(np.searchsorted(ends, lo + self.READ_CHUNK, side="right")))
+                ln = int(ends[j - 1]) - lo
+                if self.asynchronous:
+                    e.read_arena_async(lo, ln, stage[at:at + ln])
+                    at += ln
+                else:
+                    e.read_arena(lo, ln, stage)
+                nbytes += ln
+                pieces += 1
+                i = j
+        return nbytes, pieces
+
+    def wait(self):
+        self.e.read_wait()
+
+
+def churn_handoff_leg(e, fl, ch, now, ticks, n_churn, overlap):
+    """C4 as the drop-in runs it (heartbeat-once engine): ingest + tick + the
+    shim's read-back of every list and patch byte (ShimReader).  overlap=False:
+    one after the other.  overlap=True: tick k's pieces are queued
+    (kwok_read_arena_async) at the start of step k+1 and waited for at its end, so
+    the device-to-host copy runs beside batch k+1's ingest (host-to-device) and
+    tick; the step is then bounded by the larger of the two.  Batch generation
+    (which reads the pod states back) sits between the timed steps."""
+    outs = (keng.host_array((n_churn,), np.int32), keng.host_array((2 * n_churn,), np.int8), None)
+    rd = ShimReader(e, asynchronous=overlap)
+    dump = lambda: e.dump_pods(0, workload.BUCKETS * fl.cp)  # noqa: E731
+    ch.packed, ch.bufs = 12, None
+    steps, nbytes, pieces, trans = [], 0, 0, 0
+    pending = None
+    for k in range(ticks + 2):
+        ev, _ = ch.batch(dump, now)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if pending is not None:  # tick k-1's read, queued beside this step's work
+            nb, pc = rd.read(pending)
+        hs, st, _ = e.ingest_pods_packed12(ev, new_cap=len(ev) // 2, out=outs)
+        r = e.tick(now, read=False)
+        if overlap:
+            if pending is not None:
+                rd.wait()
+            pending = r
+        else:
+            nb, pc = rd.read(r)
+        dt = time.perf_counter() - t0
+        ch.applied(hs.copy(), st, new_only=True)
+        now += 30
+        if k >= 1:  # (step 0: warmup; overlapped, it also has no earlier tick to read)
+            steps.append(dt)
+            nbytes += nb
+            pieces += pc
+            trans += transitions(r.counters)
+    if overlap:  # (the last tick's read: done outside the timed steps)
+        rd.read(pending)
+        rd.wait()
+    ms = float(np.mean(steps)) * 1e3
+    return now, ch, {"overlap": overlap, "ticks": len(steps), "ms_per_step": ms,
+                     "median_ms": float(np.median(steps)) * 1e3,
+                     "bytes_to_host_per_step": nbytes / len(steps), "pieces_per_step": pieces / len(steps),
+                     "link_gbs_equivalent": nbytes / len(steps) / (ms * 1e-3) / 1e9,
+                     "value": trans / sum(steps), "unit": "transitions/s (ingest + tick + read-back)"}
 
 
 class Handoff:

@@ -416,6 +416,14 @@ int kwok_read_outputs(kwok_engine* e, kwok_outputs* out);
  * copy with a C int).  The patches lie in increasing offset order (node inits,
  * then pod patches, each in canonical order).  KWOK_EINVAL outside the arena. */
 int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst);
+/* kwok_read_arena queued on the engine's read stream without waiting (dst:
+ * kwok_host_alloc memory, which the copy engine fills while the caller goes on -
+ * the next batch's ingest and tick overlap the link's device-to-host direction);
+ * kwok_read_wait waits for every read queued so far.  A later submit that takes
+ * the read slot waits for its reads on the device.  (Stands in for the same
+ * read sequence as kwok_read_arena: engine_cgo.go applyPatches, INTEGRATION.md.) */
+int kwok_read_arena_async(kwok_engine* e, uint64_t off, uint64_t len, void* dst);
+int kwok_read_wait(kwok_engine* e);
 
 /* The constant merge patch sent before Delete when a pod has finalizers
  * (removeFinalizers, pod_controller.go:45). */
@@ -565,8 +573,11 @@ int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const u
  * scanner"): the same per-document decision as kwok_decode_pod, made on the
  * engine's device by a one-pass scanner (one thread per document).  Documents
  * the scanner leaves undecided (a status ahead of metadata / spec, a JSON
- * escape in a compared string) are decoded by the host codec, and counted in
- * *n_host; nothing is guessed.  Node documents stay with kwok_decode_nodes.
+ * escape in a compared string, a spec whose key matches a registered spec's
+ * while its strings differ) are decoded by the host codec, and counted in
+ * *n_host; nothing is guessed.  Selectors larger than the device's tables (8
+ * requirements, 32 values, 2 KiB of keys and values per codec) send every
+ * document to the host codec.  Node documents stay with kwok_decode_nodes.
  *
  * kwok_decode_pods_gpu: the decode alone (tests, diagnostics): per document its
  *   kwok_pod_event (op UPSERT, handle / spec_id / node_handle -1, as

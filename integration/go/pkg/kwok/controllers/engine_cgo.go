@@ -437,6 +437,46 @@ func (g *gpuEngine) ingestFull(evs []C.kwok_pod_event, arena []byte, handles, st
 	return nil
 }
 
+// ingestPodsJSON: kwok_ingest_pods_json - the pod documents themselves (one run of
+// a batch, see flushPods) decoded on the GPU (the host codec only for the
+// documents the device scanner leaves undecided, specs registered as they
+// first appear) and routed by the GPU event switch, the records never leaving
+// HBM.  The documents are staged in page-locked memory (the engine copies them
+// in pieces, each decoded as it lands).  ops[i] / handles[i]: Deleted ->
+// KWOK_OP_DELETE with the pod's handle; else KWOK_OP_UPSERT with its handle, -1
+// for a new pod (its node by spec.nodeName).
+func (g *gpuEngine) ingestPodsJSON(codec *gpuCodec, arena []byte, offs []uint64, lens []uint32, ops []uint8,
+	handles []int32) (outHandles, status []int32, nHost int, err error) {
+	n := len(offs)
+	outHandles, status = make([]int32, n), make([]int32, n)
+	if n == 0 {
+		return
+	}
+	arp, err := g.arBuf.get(len(arena) + 1)
+	if err != nil {
+		return
+	}
+	ar := unsafe.Slice((*byte)(arp), len(arena)+1)
+	copy(ar, arena)
+	resp, err := g.resBuf.get(3 * 4 * n)
+	if err != nil {
+		return
+	}
+	res := unsafe.Slice((*int32)(resp), 3*n)
+	var nh C.size_t
+	rc := C.kwok_ingest_pods_json(g.h, codec.c, (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(len(arena)),
+		(*C.uint64_t)(&offs[0]), (*C.uint32_t)(&lens[0]), (*C.uint8_t)(&ops[0]), (*C.int32_t)(&handles[0]),
+		C.size_t(n), (*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]), (*C.uint32_t)(unsafe.Pointer(&res[2*n])), &nh)
+	if rc < 0 {
+		err = fmt.Errorf("kwok_ingest_pods_json: %d: %s", int(rc), g.lastError())
+		return
+	}
+	copy(outHandles, res[:n])
+	copy(status, res[n:2*n])
+	nHost = int(nh)
+	return
+}
+
 // poolPut replicates IPs another rank released at ingest time (multi-GPU).
 func (g *gpuEngine) poolPut(ips []uint32) error {
 	if len(ips) == 0 {

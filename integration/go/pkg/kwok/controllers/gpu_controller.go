@@ -26,6 +26,7 @@ import (
 	"encoding/json"
 	"fmt"
 	"net"
+	"os"
 	"runtime"
 	"sync"
 	"time"
@@ -57,6 +58,8 @@ type objBatch struct {
 	lens  []uint32
 	del   []bool
 	uids  []types.UID
+	refs  []types.NamespacedName // pods: namespace / name (the apply's target)
+	nodes []string               // pods: spec.nodeName (EnableCNI's cni.Remove check)
 }
 
 func (b *objBatch) add(w watchObj) error {
@@ -69,6 +72,13 @@ func (b *objBatch) add(w watchObj) error {
 	b.arena = append(b.arena, raw...)
 	b.del = append(b.del, w.deleted)
 	b.uids = append(b.uids, w.uid)
+	var ref types.NamespacedName // (one entry per object, so the indices stay aligned)
+	var node string
+	if p, ok := w.obj.(*corev1.Pod); ok {
+		ref, node = types.NamespacedName{Namespace: p.Namespace, Name: p.Name}, p.Spec.NodeName
+	}
+	b.refs = append(b.refs, ref)
+	b.nodes = append(b.nodes, node)
 	return nil
 }
 
@@ -170,6 +180,9 @@ type GPUController struct {
 	podByUID   map[types.UID]int32
 	podUID   map[int32]types.UID // pod handle -> UID (the reverse of podByUID)
 	podRef   map[int32]types.NamespacedName
+
+	gpuCodec    bool // pod documents decoded on the GPU (kwok_ingest_pods_json); KWOK_GPU_CODEC=0: the host codec
+	podDocsHost int  // pod documents the GPU codec left to the host codec (logged)
 }
 
 func newGPUController(conf Config, interval time.Duration) (*GPUController, error) {
@@ -191,8 +204,9 @@ func newGPUController(conf Config, interval time.Duration) (*GPUController, erro
 		nodeName: map[int32]string{}, nodeHandle: map[string]int32{}, podByUID: map[types.UID]int32{},
 		podUID: map[int32]types.UID{},
 		podRef: map[int32]types.NamespacedName{},
-		echo:   echoes{rv: map[types.UID][]string{}},
-		queued: map[types.UID]struct{}{},
+		echo:     echoes{rv: map[types.UID][]string{}},
+		queued:   map[types.UID]struct{}{},
+		gpuCodec: os.Getenv("KWOK_GPU_CODEC") != "0",
 	}, nil
 }
 
@@ -554,10 +568,99 @@ func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
 // ingested after run k, once run k's handles are known.  (Added then Modified,
 // or Added then Deleted, within one interval: one slot, then its update or its
 // Deleted event with the pod's podIP release, pod_controller.go:329-336.)
+// flushPods: the batch's pod documents decoded on the GPU (kwok_ingest_pods_json)
+// in runs in which no new pod appears twice - a pod's first event may create it
+// and its later events need that handle (Added + Modified, Added + Deleted in one
+// interval) - the same runs as flushPodsHost, which decodes on the host
+// (kwok_decode_pods) and is kept for engines built without the device codec
+// (kwok_amd/controller.py ingest_doc_runs is this function in Python)
 func (c *GPUController) flushPods(ctx context.Context, tasks *parallelTasks, b objBatch) error {
 	if len(b.offs) == 0 {
 		return nil
 	}
+	if !c.gpuCodec {
+		return c.flushPodsHost(ctx, tasks, b)
+	}
+	logger := log.FromContext(ctx)
+	var run []int
+	created := map[types.UID]bool{} // new pods of the current run
+	flush := func() error {
+		offs, lens := make([]uint64, 0, len(run)), make([]uint32, 0, len(run))
+		ops, hs := make([]uint8, 0, len(run)), make([]int32, 0, len(run))
+		keep := run[:0]
+		for _, i := range run {
+			h, known := c.podByUID[b.uids[i]]
+			if b.del[i] {
+				// EnableCNI: cni.Remove for a pod on a managed node (pod_controller.go:337-342),
+				// also when the engine deleted it already (its handle is gone)
+				if c.conf.EnableCNI && c.eng.nodeHas(b.nodes[i]) {
+					uid, ref := b.uids[i], b.refs[i]
+					tasks.Add(func() {
+						if err := cni.Remove(context.Background(), string(uid), ref.Name, ref.Namespace); err != nil {
+							logger.Error("cni remove", err)
+						}
+					})
+				}
+				if !known { // never ingested, or already deleted by the engine
+					continue
+				}
+				ops = append(ops, C.KWOK_OP_DELETE) // releases status.podIP (pod_controller.go:329-336)
+				hs = append(hs, h)
+			} else {
+				ops = append(ops, C.KWOK_OP_UPSERT)
+				if !known {
+					h = -1
+				}
+				hs = append(hs, h)
+			}
+			offs, lens = append(offs, b.offs[i]), append(lens, b.lens[i])
+			keep = append(keep, i)
+		}
+		run = run[:0]
+		for k := range created {
+			delete(created, k)
+		}
+		out, ss, nHost, err := c.eng.ingestPodsJSON(c.codec, b.arena, offs, lens, ops, hs)
+		if err != nil {
+			return err
+		}
+		c.podDocsHost += nHost
+		for k, i := range keep {
+			if ss[k] != C.KWOK_OK {
+				logger.Warn("Pod outside the supported domain", fmt.Errorf("kwok status %d", ss[k]))
+				continue
+			}
+			uid := b.uids[i]
+			if ops[k] == C.KWOK_OP_DELETE {
+				delete(c.podByUID, uid)
+				delete(c.podUID, out[k])
+				delete(c.podRef, out[k])
+			} else {
+				c.podByUID[uid] = out[k]
+				c.podUID[out[k]] = uid
+				c.podRef[out[k]] = b.refs[i]
+			}
+		}
+		return nil
+	}
+	for i := range b.offs {
+		uid := b.uids[i]
+		if created[uid] { // its handle comes from the run before
+			if err := flush(); err != nil {
+				return err
+			}
+		}
+		if _, known := c.podByUID[uid]; !known && !b.del[i] {
+			created[uid] = true
+		}
+		run = append(run, i)
+	}
+	return flush()
+}
+
+// flushPodsHost: flushPods with the host codec (kwok_decode_pods) and the packed
+// wire forms (ingestPods)
+func (c *GPUController) flushPodsHost(ctx context.Context, tasks *parallelTasks, b objBatch) error {
 	logger := log.FromContext(ctx)
 	docs, st := c.codec.decodePods(b.arena, b.offs, b.lens, runtime.NumCPU())
 	type rec struct {

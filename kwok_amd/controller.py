@@ -114,7 +114,7 @@ def ingest_pods_wire(eng, recs, arena):
     return hs, st, rel, calls
 
 
-def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
+def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena, sender=None):
     """gpu_controller.go flushPods' ingest, on decoded records: the batch in
     event order, cut into runs in which no new pod appears twice - a pod's first
     event in the batch may create it (handle -1) and its later events need that
@@ -125,7 +125,9 @@ def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
     POD_EVENT_DTYPE with spec_id / node_handle set for upserts (op and handle are
     set here); uids: hashable per record; pod_by_uid: the caller's uid -> handle
     map, updated.  Returns (handles, statuses, runs): per record, NOT_SENT for
-    those not sent."""
+    those not sent.  sender(idx, ops, handles) -> (handles, statuses): another
+    ingest of the records idx (the documents on the GPU codec, ingest_doc_runs);
+    recs is then only its length."""
     n = len(recs)
     uids = list(uids)
     deleted = np.asarray(deleted, bool)
@@ -142,9 +144,13 @@ def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
         idx, hv, dl = idx[send], hv[send], dl[send]
         if not len(idx):
             return
-        recs["op"][idx] = np.where(dl, abi.OP_DELETE, abi.OP_UPSERT)
-        recs["handle"][idx] = hv
-        h1, s1, _rel, _calls = ingest_pods_wire(eng, recs[idx], arena)
+        ops = np.where(dl, abi.OP_DELETE, abi.OP_UPSERT)
+        if sender is not None:
+            h1, s1 = sender(idx, ops, hv)
+        else:
+            recs["op"][idx] = ops
+            recs["handle"][idx] = hv
+            h1, s1, _rel, _calls = ingest_pods_wire(eng, recs[idx], arena)
         runs += 1
         hs[idx], st[idx] = h1, s1
         for k in np.nonzero(s1 == abi.OK)[0].tolist():
@@ -165,6 +171,25 @@ def ingest_pod_runs(eng, pod_by_uid, recs, uids, deleted, arena):
             created.add(u)
     flush(lo, n)
     return hs, st, runs
+
+
+def ingest_doc_runs(eng, codec, pod_by_uid, docs, uids, deleted):
+    """gpu_controller.go flushPodsJSON: the batch's pod documents decoded on the
+    GPU (kwok_ingest_pods_json: k_json_pods, the host codec only for the
+    documents the device leaves undecided, specs registered as they appear, the
+    records never leaving HBM), in the same runs as ingest_pod_runs.  Returns
+    (handles, statuses, runs, documents the host decided)."""
+    arena, offs, lens = Engine._docs(docs)
+    n_host = [0]
+
+    def send(idx, ops, hv):
+        hs, st, _rel, nh = eng.ingest_pods_json(codec, arena, offs[idx], lens[idx], ops.astype(np.uint8),
+                                                hv.astype(np.int32))
+        n_host[0] += nh
+        return hs, st
+
+    hs, st, runs = ingest_pod_runs(eng, pod_by_uid, np.empty(len(docs)), uids, deleted, None, sender=send)
+    return hs, st, runs, n_host[0]
 
 
 class NotFound(Exception):
@@ -240,6 +265,7 @@ class Stats:
     reentered: int = 0    # pods patched without a podIP, ingested again in the same interval
     node_records: int = 0
     pod_records: int = 0
+    pod_docs_host: int = 0  # pod documents the GPU codec left to the host codec
     pod_runs: int = 0
     bodies: int = 0
     rejected: list = field(default_factory=list)
@@ -257,7 +283,8 @@ class Controller:
     GEOMETRY = dict(buckets=4096, node_slots_per_bucket=64, pod_slots_per_bucket=640, pod_handle_stride=65528,
                     max_pod_specs=4096)
 
-    def __init__(self, conf: Config, backend=None, codec_threads=1, suppress_echoes=True, geometry=None):
+    def __init__(self, conf: Config, backend=None, codec_threads=1, suppress_echoes=True, geometry=None,
+                 gpu_codec=True):
         self.conf = conf
         self.suppress = suppress_echoes  # False: every echo re-ingested (tests: the A/B that echoes change nothing)
         custom = {}
@@ -278,6 +305,8 @@ class Controller:
                            disregard_status_with_annotation_selector=conf.disregard_status_with_annotation_selector,
                            disregard_status_with_label_selector=conf.disregard_status_with_label_selector)
         self.threads = codec_threads
+        # pod documents decoded on the GPU (kwok_ingest_pods_json) when the backend has it
+        self.gpu_codec = gpu_codec and hasattr(self.eng, "ingest_pods_json")
         self.nodes: list[WatchObj] = []
         self.pods: list[WatchObj] = []
         self.queued = set()  # uids with an event in the current batch
@@ -402,10 +431,14 @@ class Controller:
         return sid
 
     def _flush_pods(self, batch):
-        """gpu_controller.go flushPods: decode, then ingest in runs (ingest_pod_runs)"""
+        """gpu_controller.go flushPods: decode, then ingest in runs (ingest_pod_runs).
+        On the HIP engine the documents are decoded on the GPU (ingest_doc_runs);
+        a backend without kwok_ingest_pods_json (the CPU oracle) takes the host codec."""
         ws, docs = batch
         if not ws:
             return
+        if self.gpu_codec:
+            return self._flush_pods_gpu(ws, docs)
         b = self.codec.decode_pods(docs, strict=False, threads=self.threads)
         idx, recs = [], []
         for i, w in enumerate(ws):
@@ -448,6 +481,33 @@ class Controller:
             else:
                 self.pod_uid[h] = uids[k]
                 self.pod_ref[h] = refs[k]
+
+    def _flush_pods_gpu(self, ws, docs):
+        """gpu_controller.go flushPodsJSON: the documents straight to
+        kwok_ingest_pods_json in runs; names and nodes from the watch objects"""
+        uids = [w.uid for w in ws]
+        deleted = [w.deleted for w in ws]
+        hs, st, runs, n_host = ingest_doc_runs(self.eng, self.codec, self.pod_by_uid, docs, uids, deleted)
+        self.stats.pod_records += int((st != NOT_SENT).sum())
+        self.stats.pod_runs += runs
+        self.stats.pod_docs_host += n_host
+        for k, w in enumerate(ws):
+            md = _meta(w.obj)
+            if st[k] not in (abi.OK, NOT_SENT):
+                self.stats.rejected.append(("pod", md.get("name"), int(st[k])))
+                continue
+            if w.deleted:
+                # EnableCNI: cni.Remove for a pod on a managed node (pod_controller.go:337-342),
+                # also when the engine deleted it already (its handle is gone)
+                if self.conf.enable_cni and self.conf.cni and self.has((w.obj.get("spec") or {}).get("nodeName", "")):
+                    self.conf.cni.remove(w.uid, md.get("name", ""), md.get("namespace", ""))
+                if st[k] == abi.OK:
+                    self.pod_uid.pop(int(hs[k]), None)
+                    self.pod_ref.pop(int(hs[k]), None)
+            else:
+                h = int(hs[k])
+                self.pod_uid[h] = w.uid
+                self.pod_ref[h] = (md.get("namespace", ""), md.get("name", ""))
 
     def _setup_cni(self):
         hs = self.eng.cni_pending()

@@ -277,7 +277,8 @@ struct JsonSel {
 };
 // the codec's configuration (kwok_codec_config as compiled by kwok_codec_create)
 struct JsonCfg {
-    uint32_t manage_all, pad;
+    uint32_t manage_all;
+    uint32_t all_host;  // the selectors exceed these tables: every document goes to the host codec
     JsonSel man_ann, man_lab, dis_ann, dis_lab;
     uint8_t bytes[JSEL_BYTES];  // every selector's keys and values
 };
@@ -285,11 +286,13 @@ struct JsonCfg {
 struct JsonPodSide {
     uint32_t name_off, name_len, ns_off, ns_len;  // metadata.name / namespace (kwok_pod_doc)
     uint64_t spec_key;    // json_spec_key of its containers / init containers / readiness gates
+    uint64_t spec_key2;   // a second, independent hash of the same bytes (json_complete's batch-local specs)
     uint8_t n_cont, n_init, n_gates, pad;
-    int32_t status;       // KWOK_OK / KWOK_EDOMAIN / KWOK_EINVAL, or JSON_HOST / JSON_SPEC
+    int32_t status;       // KWOK_OK / KWOK_EDOMAIN / KWOK_EINVAL, or JSON_HOST / JSON_SPEC / JSON_SPEC_X
 };
 constexpr int32_t JSON_HOST = 1;  // outside what the device scanner decides: the host codec decodes it
 constexpr int32_t JSON_SPEC = 2;  // decoded; its pod spec is not registered yet (the host registers it)
+constexpr int32_t JSON_SPEC_X = 3;  // decoded; its spec key is a registered spec's, its strings are not (the host decodes it)
 
 // ---- node directory (device-authoritative, ingest.hip) -------------------------
 // A node slot's name lives on the device: node_key[slot] = fnv1a32(name) | len << 32

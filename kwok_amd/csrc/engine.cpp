@@ -46,19 +46,33 @@ namespace {
 // FNV-1a 64 of a pod spec's strings (json.hip spec_key is the same function):
 // each container's name 0x1F image 0x1E, 0x1D, the init containers alike, 0x1D,
 // each readiness gate 0x1E
+// The canonical byte string the key hashes; the GPU codec compares a document's
+// spec with it after a table hit (the key alone is not collision-resistant)
+std::string json_spec_canon(const std::vector<Container>& cs, const std::vector<Container>& ics,
+                            const std::vector<std::string>& gates) {
+    std::string o;
+    for (auto& c : cs) o += c.name, o += '\x1F', o += c.image, o += '\x1E';
+    o += '\x1D';
+    for (auto& c : ics) o += c.name, o += '\x1F', o += c.image, o += '\x1E';
+    o += '\x1D';
+    for (auto& g : gates) o += g, o += '\x1E';
+    return o;
+}
+// KWOK_DEBUG_SPEC_KEY_BITS=b (tests): keys cut to their low b bits, so that
+// distinct specs collide and the device's byte check decides
+uint64_t spec_key_mask() {  // (read per call: registrations and decode launches are rare)
+    const char* v = getenv("KWOK_DEBUG_SPEC_KEY_BITS");
+    const unsigned b = v ? (unsigned)atoi(v) : 64u;
+    return b >= 64 || b == 0 ? ~0ull : (1ull << b) - 1ull;
+}
+uint64_t json_spec_key(const std::string& canon) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (unsigned char c : canon) h = (h ^ c) * 0x100000001B3ull;
+    return h & spec_key_mask();
+}
 uint64_t json_spec_key(const std::vector<Container>& cs, const std::vector<Container>& ics,
                        const std::vector<std::string>& gates) {
-    uint64_t h = 0xCBF29CE484222325ull;
-    auto byte = [&](uint8_t b) { h = (h ^ b) * 0x100000001B3ull; };
-    auto str = [&](const std::string& x) {
-        for (unsigned char c : x) byte(c);
-    };
-    for (auto& c : cs) str(c.name), byte(0x1F), str(c.image), byte(0x1E);
-    byte(0x1D);
-    for (auto& c : ics) str(c.name), byte(0x1F), str(c.image), byte(0x1E);
-    byte(0x1D);
-    for (auto& g : gates) str(g), byte(0x1E);
-    return h;
+    return json_spec_key(json_spec_canon(cs, ics, gates));
 }
 
 thread_local std::string g_create_err;  // kwok_last_error(NULL) after a failed create
@@ -243,10 +257,14 @@ struct kwok_engine {
         JsonCfg* cfg_h = nullptr;          // pinned staging
         uint64_t* tab_key = nullptr;
         int32_t* tab_id = nullptr;
+        uint2* tab_canon = nullptr;        // per slot: offset / length of its spec's canonical string in canon
+        uint8_t* canon = nullptr;          // the registered specs' canonical strings (json_spec_canon)
+        size_t canon_cap = 0;
         uint32_t tab_mask = 0;
         bool tab_dirty = true;
     } json;
     std::unordered_map<uint64_t, int32_t> spec_keys;  // kwok_spec_key -> spec id (-2: two specs share the key)
+    std::unordered_map<uint64_t, std::string> spec_canon;  // kwok_spec_key -> the canonical string of its spec
 
     // ---- specs / blobs ----
     std::unordered_map<std::string, int32_t> spec_ids;
@@ -303,6 +321,9 @@ struct kwok_engine {
         bool inits_folded = false;  // ... and the node inits' too (no k_emit launch: KWOK_FOLD_INITS)
         bool quiet = false;         // only pods with an event are Use-checked (kwok_engine::quiet)
         bool once = false;          // launched as k_once (a heartbeat-once tick expected to have nothing to emit)
+        bool once_use = false;      // ... reading the per-bucket summaries (counted when it retires as a once tick)
+        hipEvent_t rd = nullptr;    // kwok_read_arena_async: the last read queued from this slot's arena
+        bool rd_pending = false;    //   (a submit or an arena growth that takes the slot waits for it)
         bool no_once = false;       // k_once found work: the tick runs again with k_tick
         bool alloc = false;
         // the tick in the slot
@@ -346,6 +367,7 @@ struct kwok_engine {
     bool no_stream = false;     // KWOK_TICK_NO_STREAM=1: diagnostics - heartbeat bodies not written
     bool split_jobs = true;     // KWOK_SPLIT=0: pod jobs of event ticks in the chain blocks (A/B)
     int fuse_emit = -1;         // KWOK_FUSE_EMIT: 1 always / 0 never fuse the pod bytes into k_pod_jobs; -1 dense ticks
+    bool sparse_jobs = true;    // unfused split ticks: k_sparse_jobs over FRONT's group records (KWOK_SPARSE_JOBS=0: off)
     bool fold_inits = true;     // KWOK_FOLD_INITS=0: a fused tick's node inits by k_emit (A/B)
     uint64_t pod_records_since_tick = 0;  // pod records ingested since the last tick was enqueued (fused emission)
     uint32_t n_untabled = 0;    // registered specs without unit tables (no fused emission while any)
@@ -581,6 +603,10 @@ int size_arena(kwok_engine* e) {
 }
 int grow_arena(kwok_engine* e, kwok_engine::TickSlot& T) {  // T holds no queued tick
     if (e->arena_need <= T.arena_cap) return KWOK_OK;
+    if (T.rd_pending) {  // (an asynchronous read of the old arena still in flight)
+        if (hipEventSynchronize(T.rd) != hipSuccess) return e->fail(KWOK_EDEVICE, "kwok_read_arena_async");
+        T.rd_pending = false;
+    }
     const uint64_t need = std::max<uint64_t>(e->arena_need, T.arena_cap + T.arena_cap / 2);
     if (T.arena) (void)hipFree(T.arena);
     T.arena = nullptr;
@@ -621,6 +647,7 @@ void free_slot(kwok_engine::TickSlot& T) {
     if (T.hdr_h) (void)hipHostFree(T.hdr_h);
     if (T.S_pin) (void)hipHostFree(T.S_pin);
     if (T.done) (void)hipEventDestroy(T.done);
+    if (T.rd) (void)hipEventDestroy(T.rd);
     for (auto& ev : T.pev)
         if (ev) (void)hipEventDestroy(ev);
 }
@@ -1055,10 +1082,11 @@ void kwok_engine_destroy(kwok_engine* e) {
                     e->trace_sum[TRACE_SLOTS + k][2] / e->trace_ticks);
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
+    if (e->rst) (void)hipStreamSynchronize(e->rst);  // (asynchronous arena reads)
     void* ptrs[] = {e->S.trace, e->S.jtrace, e->S.once_sum, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
-                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->d_hb_pre, e->d_hb_bpre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
+                    (void*)e->S.hb_kind, e->S.bar, e->S.blockagg, e->S.dmask, e->S.list_blk, e->S.wc_pre, e->S.wc_dirty, e->S.jbase, e->S.gjob, e->d_hb_pre, e->d_hb_bpre, e->S.hdr, e->S.xmsg, e->S.node_key, e->S.node_name, e->S.mb_count, e->S.zb_count,
                     e->S.use_list, e->S.rel_list, e->d_specs.p, e->d_spec_bytes.p, e->d_spec_nxt.p, e->d_unit_tab.p, e->d_unit_desc.p, e->d_blob.p, e->d_ops,
                     e->d_ld, e->d_xall, e->d_xsend, e->d_xrecv, e->d_ssend, e->d_srecv};
     for (void* p : ptrs)
@@ -1085,7 +1113,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     {
         auto& J = e->json;
         void* jp[] = {J.off, J.len, J.op, J.handle, J.side, J.host_list, J.fix_ev, J.fix_side, J.n_host, J.cfg,
-                      J.tab_key, J.tab_id};
+                      J.tab_key, J.tab_id, J.tab_canon, J.canon};
         for (void* p : jp)
             if (p) (void)hipFree(p);
         if (J.cfg_h) (void)hipHostFree(J.cfg_h);
@@ -1262,6 +1290,8 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->quiet_ok = !(qt && qt[0] == '0');
         const char* sj = getenv("KWOK_SPLIT");
         e->split_jobs = !(sj && sj[0] == '0');
+        const char* sj2 = getenv("KWOK_SPARSE_JOBS");  // 0: k_pod_jobs<false> re-classifies the runs (A/B)
+        e->sparse_jobs = !(sj2 && sj2[0] == '0');
         const char* fe = getenv("KWOK_FUSE_EMIT");
         e->fuse_emit = fe && fe[0] ? (fe[0] == '0' ? 0 : 1) : -1;
         const char* fi = getenv("KWOK_FOLD_INITS");
@@ -1326,6 +1356,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         (rc = dalloc(e, &e->d_hb_bpre, (size_t)e->nb + 1)) ||
         (rc = dalloc(e, &S.wc_pre, (size_t)S.n_chain * MAX_WC)) ||
         (rc = dalloc(e, &S.wc_dirty, (size_t)S.n_chain * WC_DIRTY_WORDS)) || (rc = dalloc(e, &S.jbase, (size_t)S.n_chain)) ||
+        (e->sparse_jobs && (rc = dalloc(e, &S.gjob, (size_t)S.n_chain * MAX_WC * WC_GROUPS))) ||
         (getenv("KWOK_TICK_TRACE") && (rc = dalloc(e, &S.trace, (size_t)(S.n_chain + e->n_stream) * TRACE_SLOTS))) ||
         (getenv("KWOK_JOBS_TRACE") && (rc = dalloc(e, &S.jtrace, (size_t)S.n_chain * (MAX_WC + 4) * 4))) ||
         (rc = dalloc(e, &S.alloc_addr, PLa)) || (rc = dalloc(e, (uint8_t**)&S.hb_static, HB_MAX_STRIDE)) ||
@@ -1470,9 +1501,11 @@ int kwok_register_pod_spec(kwok_engine* e, const kwok_pod_spec* spec, const char
     std::vector<uint16_t> tdesc;
     const bool tabled = build_unit_tables(p, tab, tdesc);  // else: the general emitter path only
     std::string key = p.a + '\x01' + p.ka + '\x01' + p.b + '\x01' + p.kb + '\x01' + p.c + '\x01' + p.kc;
-    const uint64_t skey = json_spec_key(cs, ics, gates);  // the GPU codec finds the spec by this key
+    std::string canon = json_spec_canon(cs, ics, gates);
+    const uint64_t skey = json_spec_key(canon);  // the GPU codec finds the spec by this key (and checks canon)
     auto note = [&](int32_t id) {
         auto k = e->spec_keys.emplace(skey, id);
+        if (k.second) e->spec_canon[skey] = std::move(canon);
         if (!k.second && k.first->second != id) k.first->second = -2;  // (a 64-bit collision: the host decides)
         if (k.second || k.first->second == -2) e->json.tab_dirty = true;
     };
@@ -1729,7 +1762,7 @@ int enqueue_sort_need(kwok_engine* e, const IngestBatch& I) {
 // then returns on the device if the chunk needs growth)
 int enqueue_apply(kwok_engine* e, IngestBatch I, bool spec) {
     I.spec = spec ? 1u : 0u;
-    e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
+    if (I.n) e->ing_mutated = true;  // pod slots, node entries and references and the pool change from here on
     launch_ingest_apply(e->S, I, e->st);
     HIPCHK(e, hipGetLastError());
     return KWOK_OK;
@@ -1798,10 +1831,15 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     // apply passes under it.  The last chunk is shorter (its apply and results are
     // the part nothing hides).  The prep of chunk k + 2 waits until chunk k has
     // released its accumulator set.
-    const uint32_t K = n > G.chunk ? (uint32_t)((n + G.chunk - 1) / G.chunk) : 1u;
+    // kwok_pod_rec12's chunks start at multiples of 256 records (its create counts are
+    // per 256-record tile, tile_new[lo / 256 + block]); its chunks hold at least 512
+    // records, so that every chunk start rounds to a new tile and no chunk is empty.
+    // The other wire forms split anywhere.
+    const size_t chunk = packed == 2 ? std::max<size_t>(G.chunk, 512) : G.chunk;
+    const uint32_t K = n > chunk ? (uint32_t)((n + chunk - 1) / chunk) : 1u;
     const double W = K > 1 ? K - e->last_chunk_cut : 1.0;
-    // (chunks start at multiples of 256 records: kwok_pod_rec12's create counts are per 256-record tile)
-    auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W) & ~(size_t)255; };
+    const size_t lo_mask = packed == 2 ? ~(size_t)255 : ~(size_t)0;
+    auto lo_of = [&](uint32_t k) { return k >= K ? n : (size_t)((double)n * k / W) & lo_mask; };
     // a one-chunk batch in kwok_host_alloc memory is read in place by k_ing_prep
     // (the only kernel that reads the records and their strings): one pass over
     // the link, no copy engine (KWOK_INGEST_ZC=0: copy it to HBM first).  Chunked
@@ -2081,13 +2119,18 @@ int json_reserve(kwok_engine* e, size_t n) {
         if (slots - 1 != J.tab_mask || !J.tab_key) {
             if (J.tab_key) (void)hipFree(J.tab_key);
             if (J.tab_id) (void)hipFree(J.tab_id);
-            J.tab_key = nullptr, J.tab_id = nullptr;
+            if (J.tab_canon) (void)hipFree(J.tab_canon);
+            J.tab_key = nullptr, J.tab_id = nullptr, J.tab_canon = nullptr;
             int rc = 0;
-            if ((rc = dalloc(e, &J.tab_key, slots)) || (rc = dalloc(e, &J.tab_id, slots))) return rc;
+            if ((rc = dalloc(e, &J.tab_key, slots)) || (rc = dalloc(e, &J.tab_id, slots)) ||
+                (rc = dalloc(e, &J.tab_canon, slots)))
+                return rc;
             J.tab_mask = slots - 1;
         }
         std::vector<uint64_t> key(slots, 0);
         std::vector<int32_t> id(slots, -1);
+        std::vector<uint2> cref(slots, uint2{0, 0});
+        std::string canon;
         for (auto& kv : e->spec_keys) {
             uint64_t k = kv.first ? kv.first : 1;  // (0 marks an empty slot: key 0 is never found)
             if (!kv.first) continue;
@@ -2095,9 +2138,21 @@ int json_reserve(kwok_engine* e, size_t n) {
             while (key[h]) h = (h + 1) & J.tab_mask;
             key[h] = k;
             id[h] = kv.second;
+            const std::string& c = e->spec_canon[kv.first];
+            cref[h] = uint2{(uint32_t)canon.size(), (uint32_t)c.size()};
+            canon += c;
+        }
+        if (canon.size() + 16 > J.canon_cap) {
+            if (J.canon) (void)hipFree(J.canon);
+            J.canon = nullptr, J.canon_cap = 0;
+            const size_t cap = std::max<size_t>(2 * canon.size() + 16, 4096);
+            if (int rc = dalloc(e, &J.canon, cap)) return rc;
+            J.canon_cap = cap;
         }
         HIPCHK(e, hipMemcpyAsync(J.tab_key, key.data(), slots * 8, hipMemcpyHostToDevice, e->st));
         HIPCHK(e, hipMemcpyAsync(J.tab_id, id.data(), slots * 4, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, hipMemcpyAsync(J.tab_canon, cref.data(), slots * sizeof(uint2), hipMemcpyHostToDevice, e->st));
+        if (!canon.empty()) HIPCHK(e, hipMemcpyAsync(J.canon, canon.data(), canon.size(), hipMemcpyHostToDevice, e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));
         J.tab_dirty = false;
     }
@@ -2115,7 +2170,13 @@ int json_decode(kwok_engine* e, const kwok_codec* c, const char* arena, size_t a
     int rc = ingest_reserve(e, n, arena_len + 16);  // (the scanner reads whole 16-byte windows)
     if (rc) return rc;
     if ((rc = json_reserve(e, n))) return rc;
-    if ((rc = codec_export(c, J.cfg_h))) return e->fail(rc, "%s", kwok_codec_last_error());
+    // selectors beyond the device's tables (JSEL_*): every document is decoded by the
+    // host codec (JSON_HOST), as any other document the scanner does not decide
+    if ((rc = codec_export(c, J.cfg_h))) {
+        if (rc != KWOK_EDOMAIN) return e->fail(rc, "%s", kwok_codec_last_error());
+        memset(J.cfg_h, 0, sizeof(JsonCfg));
+        J.cfg_h->all_host = 1;
+    }
     HIPCHK(e, hipMemcpyAsync(J.cfg, J.cfg_h, sizeof(JsonCfg), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(J.off, doc_off, n * 8, hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(J.len, doc_len, n * 4, hipMemcpyHostToDevice, st));
@@ -2160,6 +2221,9 @@ int json_decode(kwok_engine* e, const kwok_codec* c, const char* arena, size_t a
         A.handle = op ? J.handle + d0 : nullptr;
         A.tab_key = J.tab_key;
         A.tab_id = J.tab_id;
+        A.tab_canon = J.tab_canon;
+        A.key_mask = spec_key_mask();
+        A.canon = J.canon;
         A.ev = static_cast<kwok_pod_event*>(G.d_ev) + d0;
         A.side = J.side + d0;
         A.host_list = J.host_list;
@@ -2203,15 +2267,23 @@ int json_complete(kwok_engine* e, const kwok_codec* c, const char* arena, size_t
     HIPCHK(e, hipMemcpyAsync(ev.data(), J.fix_ev, (size_t)nh * sizeof(kwok_pod_event), hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipMemcpyAsync(side.data(), J.fix_side, (size_t)nh * sizeof(JsonPodSide), hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
-    std::unordered_map<uint64_t, int32_t> fresh;  // spec keys registered here (JSON_SPEC)
+    // specs registered here (JSON_SPEC), by both of the device's keys of their
+    // canonical string (kwok_spec_key and a second, independent 64-bit hash): a later
+    // document of the batch with both keys takes that spec without a host decode
+    struct K2Hash {
+        size_t operator()(const std::pair<uint64_t, uint64_t>& k) const { return (size_t)(k.first ^ (k.second * 31)); }
+    };
+    std::unordered_map<std::pair<uint64_t, uint64_t>, int32_t, K2Hash> fresh;
     char* ar = const_cast<char*>(arena);  // (kwok_decode_pod writes only node blobs)
     kwok_pod_doc d;
     for (uint32_t q = 0; q < nh; q++) {
         const uint32_t i = list[q];
         JsonPodSide& s = side[q];
         const bool ups = !op || op[i] == KWOK_OP_UPSERT;
-        if (s.status == JSON_SPEC) {
-            auto f = fresh.find(s.spec_key);
+        const std::pair<uint64_t, uint64_t> dkey{s.spec_key, s.spec_key2};  // (the device's, before the host decode)
+        const bool miss = s.status == JSON_SPEC;  // (JSON_SPEC_X, a key that collides with a registered spec: decoded)
+        if (miss) {
+            auto f = fresh.find(dkey);
             if (f != fresh.end()) {
                 ev[q].spec_id = f->second;
                 ev[q].reserved0 = 0;
@@ -2232,7 +2304,7 @@ int json_complete(kwok_engine* e, const kwok_codec* c, const char* arena, size_t
             s.spec_key = kwok_spec_key(&sp, arena, arena_len);
             if (op && ups) {
                 const int r2 = kwok_register_pod_spec(e, &sp, arena, arena_len, &id);
-                if (r2 == KWOK_OK) fresh[s.spec_key] = id;
+                if (r2 == KWOK_OK && miss) fresh[dkey] = id;
                 else if (r2 == KWOK_EDOMAIN || r2 == KWOK_EFULL) rc = r2;  // the spec is outside the domain
                 else return r2;
             }
@@ -2511,6 +2583,7 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
         T.fuse = T.split && e->n_untabled == 0 && (e->fuse_emit > 0 || (e->fuse_emit < 0 && dense));
     }
     S.fuse_pods = T.fuse ? 1u : 0u;
+    S.sparse_jobs = T.split && !T.fuse && e->sparse_jobs ? 1u : 0u;
     T.inits_folded = false;  // (set where k_pod_jobs is launched)
     // ... and leave the whole stream to the streamers: a dirty chain block's share
     // of it would hold up the pool phase, which waits for every dirty block
@@ -2547,9 +2620,9 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
                 mode = ONCE_SUM_BUILD;
             } else {
                 mode = ONCE_SUM_USE;
-                e->stats[KWOK_STAT_ONCE_SUMMARY]++;
             }
         }
+        T.once_use = mode == ONCE_SUM_USE;
         launch_tick_once(S, now, (uint64_t)e->start, nhb, prof & TICK_PROF, mode, e->sum_gen, st, ev ? ev[0] : nullptr,
                          ev ? ev[1] : nullptr);
         HIPCHK(e, hipGetLastError());
@@ -2659,6 +2732,7 @@ int finish_long_lists(kwok_engine* e, int k, int next) {
     int rc = bind_slot(e, k);
     if (rc) return rc;
     S.fuse_pods = T.fuse ? 1u : 0u;
+    S.sparse_jobs = T.split && !T.fuse && e->sparse_jobs ? 1u : 0u;
     HIPCHK(e, hipMemsetAsync(&S.bar->skip, 0, sizeof(uint32_t), st));
     const XMsg& me = e->h_xall[e->rank];
     if (me.n_use + me.n_rel) {  // the chain blocks' list segments, gathered in block order
@@ -2948,6 +3022,7 @@ int retire(kwok_engine* e) {
     e->host_ms[KWOK_H_TOTAL] += ms_between(t1, t3);
     e->host_ticks++;
     e->stats[T.once ? KWOK_STAT_TICKS_ONCE : KWOK_STAT_TICKS_FULL]++;
+    if (T.once && T.once_use) e->stats[KWOK_STAT_ONCE_SUMMARY]++;  // (a launch that skipped or was redone read none)
     if (requeue_next) {  // the tick queued behind a redone one skipped on the device
         if (int rc = enqueue_tick(e, next, true)) {
             kwok_engine::TickSlot& U = e->slots[next];
@@ -2996,6 +3071,10 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     kwok_engine::TickSlot& T = e->slots[k];
     int rc = grow_arena(e, T);
     if (rc) return rc;
+    if (T.rd_pending) {  // the tick's kernels write the arena after the reads queued from it
+        HIPCHK(e, hipStreamWaitEvent(e->st, T.rd, 0));
+        T.rd_pending = false;
+    }
     if (k == e->cur) e->cur = -1;  // its outputs are overwritten
     T.now = (uint64_t)now_unix;
     T.epoch = e->hb_epoch;
@@ -3167,6 +3246,39 @@ int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {
     HIPCHK(e, hipEventRecord(e->fence, st));
     HIPCHK(e, hipMemcpyAsync(dst, S.arena + off, len, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
+    return KWOK_OK;
+}
+
+// kwok_read_arena queued without waiting: dst should be kwok_host_alloc memory (the
+// copy engine writes it while the caller goes on: the next batch's ingest, the
+// next tick); kwok_read_wait waits for every read queued so far.  The slot stays
+// the caller's until the next submit that takes it, which waits for the reads on
+// the device (or, when the arena must grow, on the host)
+int kwok_read_arena_async(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {
+    if (!e || (len && !dst)) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    if (e->cur < 0) return e->fail(KWOK_EINVAL, "no collected tick (or its slot was reused by a submit)");
+    kwok_engine::TickSlot& S = e->slots[e->cur];
+    const uint64_t total = S.hdr_h->arena_bytes;
+    if (off > total || len > total - off)
+        return e->fail(KWOK_EINVAL, "arena range [%llu, +%llu) outside the tick's %llu bytes", (unsigned long long)off,
+                       (unsigned long long)len, (unsigned long long)total);
+    if (!len) return KWOK_OK;
+    hipStream_t st = e->rst;
+    if (!S.rd && hipEventCreateWithFlags(&S.rd, hipEventDisableTiming) != hipSuccess)
+        return e->fail(KWOK_EDEVICE, "event create");
+    HIPCHK(e, hipStreamWaitEvent(st, S.done, 0));
+    HIPCHK(e, hipEventRecord(e->fence, st));
+    HIPCHK(e, hipMemcpyAsync(dst, S.arena + off, len, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipEventRecord(S.rd, st));
+    S.rd_pending = true;
+    return KWOK_OK;
+}
+
+int kwok_read_wait(kwok_engine* e) {
+    if (!e) return KWOK_EINVAL;
+    HIPCHK(e, hipStreamSynchronize(e->rst));
+    for (auto& T : e->slots) T.rd_pending = false;
     return KWOK_OK;
 }
 

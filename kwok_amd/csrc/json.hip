@@ -846,18 +846,37 @@ struct PodScan {
 // FNV-1a 64 of the pod spec the engine interns (kwok_register_pod_spec): each
 // container's name 0x1F image 0x1E, 0x1D, the init containers alike, 0x1D, each
 // readiness gate 0x1E (engine.cpp json_spec_key is the same function)
-__device__ __forceinline__ uint64_t fnv_byte(uint64_t h, uint32_t b) { return (h ^ b) * 0x100000001B3ull; }
-__device__ uint64_t spec_key(JRd& r, const PodScan& p) {
-    uint64_t h = 0xCBF29CE484222325ull;
+// The walk over those bytes (engine.cpp json_spec_canon writes the same string)
+template <class F>
+__device__ __forceinline__ void spec_walk(JRd& r, const PodScan& p, F&& byte) {
     auto str = [&](Span s) {
-        for (uint32_t q = 0; q < s.len; q++) h = fnv_byte(h, r.at(s.off + q));
+        for (uint32_t q = 0; q < s.len; q++) byte(r.at(s.off + q));
     };
-    for (uint32_t q = 0; q < p.n_cont; q++) str(p.cname[q]), h = fnv_byte(h, 0x1F), str(p.cimage[q]), h = fnv_byte(h, 0x1E);
-    h = fnv_byte(h, 0x1D);
-    for (uint32_t q = 0; q < p.n_init; q++) str(p.iname[q]), h = fnv_byte(h, 0x1F), str(p.iimage[q]), h = fnv_byte(h, 0x1E);
-    h = fnv_byte(h, 0x1D);
-    for (uint32_t q = 0; q < p.n_gates; q++) str(p.gate[q]), h = fnv_byte(h, 0x1E);
-    return h;
+    for (uint32_t q = 0; q < p.n_cont; q++) str(p.cname[q]), byte(0x1F), str(p.cimage[q]), byte(0x1E);
+    byte(0x1D);
+    for (uint32_t q = 0; q < p.n_init; q++) str(p.iname[q]), byte(0x1F), str(p.iimage[q]), byte(0x1E);
+    byte(0x1D);
+    for (uint32_t q = 0; q < p.n_gates; q++) str(p.gate[q]), byte(0x1E);
+}
+// the key (FNV-1a 64) and a second, independent hash of the same bytes
+__device__ void spec_keys(JRd& r, const PodScan& p, uint64_t& k1, uint64_t& k2) {
+    uint64_t h = 0xCBF29CE484222325ull, g = 0x243F6A8885A308D3ull;
+    spec_walk(r, p, [&](uint32_t b) {
+        h = (h ^ b) * 0x100000001B3ull;
+        g = (g + b + 1) * 0x9E3779B97F4A7C15ull;
+        g ^= g >> 29;
+    });
+    k1 = h, k2 = g;
+}
+// the document's spec is exactly the registered one (a key hit is not proof)
+__device__ bool spec_equal(JRd& r, const PodScan& p, const uint8_t* canon, uint2 ref) {
+    uint32_t k = 0;
+    bool eq = true;
+    spec_walk(r, p, [&](uint32_t b) {
+        eq = eq && k < ref.y && canon[ref.x + k] == (uint8_t)b;
+        k++;
+    });
+    return eq && k == ref.y;
 }
 
 }  // namespace
@@ -887,8 +906,9 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
         JRd rd{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
         p.r = &rd;
         p.cfg = A.cfg;
-        const bool ok = jparse(rd, p);
-        if (!ok || !p.root_obj) status = KWOK_EDOMAIN;
+        const bool ok = !A.cfg->all_host && jparse(rd, p);
+        if (A.cfg->all_host) status = JSON_HOST;  // (selectors the device tables do not hold)
+        else if (!ok || !p.root_obj) status = KWOK_EDOMAIN;
         else if (p.err) status = p.err;
         else if (!p.meta_obj || !p.spec_obj || !p.ct_ok) status = p.host ? JSON_HOST : KWOK_EDOMAIN;
         else if (p.host) status = JSON_HOST;
@@ -914,7 +934,8 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
             side.name_off = p.name.off, side.name_len = p.name.len;
             side.ns_off = p.ns.off, side.ns_len = p.ns.len;
             side.n_cont = (uint8_t)p.n_cont, side.n_init = (uint8_t)p.n_init, side.n_gates = (uint8_t)p.n_gates;
-            side.spec_key = spec_key(rd, p);
+            spec_keys(rd, p, side.spec_key, side.spec_key2);
+            side.spec_key &= A.key_mask;
         }
     }
     // the ingest form: the caller's op / handle, the registered spec (device table)
@@ -923,23 +944,30 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
         ev.handle = A.handle[i];
         if (status == KWOK_OK && ev.op == KWOK_OP_UPSERT) {
             int32_t id = -1;
+            uint32_t hs = 0;
             for (uint32_t q = 0, h = (uint32_t)side.spec_key & A.tab_mask; q <= A.tab_mask; q++, h = (h + 1) & A.tab_mask) {
                 const uint64_t kk = A.tab_key[h];
                 if (kk == side.spec_key) {
                     id = A.tab_id[h];
+                    hs = h;
                     break;
                 }
                 if (!kk) break;
             }
-            if (id < 0) status = JSON_SPEC;
+            // a key hit whose strings differ from the registered spec's (FNV-1a is not
+            // collision-resistant and specs come from users): the host decides it
+            JRd rc{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
+            if (id >= 0 && !spec_equal(rc, p, A.canon, A.tab_canon[hs])) status = JSON_SPEC_X;
+            else if (id < 0) status = JSON_SPEC;
             else ev.spec_id = id;
         }
-        if (status != KWOK_OK) ev.reserved0 = (uint8_t)(int8_t)(status == JSON_HOST || status == JSON_SPEC ? KWOK_EINVAL : status);
+        const bool listed = status == JSON_HOST || status == JSON_SPEC || status == JSON_SPEC_X;
+        if (status != KWOK_OK) ev.reserved0 = (uint8_t)(int8_t)(listed ? KWOK_EINVAL : status);
     }
     side.status = status;
     A.ev[i] = ev;
     A.side[i] = side;
-    if (status == JSON_HOST || status == JSON_SPEC) A.host_list[atomicAdd(A.n_host, 1u)] = A.base + i;
+    if (status == JSON_HOST || status == JSON_SPEC || status == JSON_SPEC_X) A.host_list[atomicAdd(A.n_host, 1u)] = A.base + i;
 }
 
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st) {

@@ -113,6 +113,9 @@ struct DevState {
     uint32_t foreign;          // multi rank: this rank's sticky foreign-IP flag, sent in the exchange message
     uint32_t xcap_u, xcap_r;   // multi rank, TICK_XSPEC: the list allgather's Use / release capacity per rank
     uint32_t fuse_pods;        // split ticks: k_pod_jobs writes the pod patch bytes itself (every spec has unit tables)
+    uint32_t sparse_jobs;      // unfused split ticks: FRONT publishes its dirty groups (gjob), k_sparse_jobs builds the jobs
+    uint4* gjob;               //   [n_chain][MAX_WC * WC_GROUPS]: slot, masks (del | need << 8 | alloc << 16 | j << 24 |
+                               //   any held hostIP << 30 | any held podIP << 31), patch bytes, tick tag
     uint32_t buckets;          // B (all ranks)
     uint32_t b_lo;             // first owned bucket
     uint32_t pod_stride;       // pod handle = (b_lo + slot / cp) * pod_stride + slot % cp
@@ -169,6 +172,7 @@ uint32_t once_blocks(const DevState& S);
 // split ticks: the pod jobs (deletes, patch job records, state transitions) of
 // every dirty 64-group run of every chain block, one wave each
 // k_pod_jobs; a fused launch (DevState::fuse_pods) also writes the node inits with init_blocks blocks
+// (DevState::sparse_jobs: k_sparse_jobs from the groups FRONT published instead of k_pod_jobs<false>)
 void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, uint32_t init_blocks, uint64_t now, uint64_t start,
                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 int tick_occupancy();  // resident k_tick blocks per CU
@@ -238,6 +242,9 @@ struct JsonPodArgs {
     const int32_t* handle;       //   the spec id from the table, a failed decode's status in reserved0
     const uint64_t* tab_key;     // json_spec_key (0: empty slot)
     const int32_t* tab_id;
+    const uint2* tab_canon;      // per slot: its spec's canonical string (offset, length) in canon, checked
+    const uint8_t* canon;        //   byte for byte against the document's spec after a key hit
+    uint64_t key_mask;           // ~0 (KWOK_DEBUG_SPEC_KEY_BITS: fewer bits, for collision tests)
     kwok_pod_event* ev;          // [n] out
     JsonPodSide* side;           // [n] out
     uint32_t* host_list;         // [n] out: documents the host completes (JSON_HOST / JSON_SPEC), as base + index

@@ -1090,6 +1090,23 @@ __device__ __forceinline__ void wc_add(uint32_t* wcnt, uint32_t gi, const GroupM
     if (m.alloc) atomicAdd(&wcnt[4 * w + 3], (uint32_t)__popc(m.alloc));
     atomicOr(&wcnt[4 * MAX_WC + (w >> 5)], 1u << (w & 31));
 }
+// ... and (DevState::sparse_jobs) the dirty group itself for k_sparse_jobs: its slot,
+// masks and patch bytes at its index among the block's live groups, tagged with the
+// tick (a group clean this tick keeps an older tag: k_sparse_jobs reads it as clean)
+__device__ __forceinline__ void gjob_put(const DevState& S, uint32_t b, uint32_t gi, const PodGrp& g, const GroupMasks& m,
+                                         uint32_t bytes, uint32_t tag) {
+    if (!m.dirty) return;
+    // a pod of the group holds a hostIP / a podIP: k_sparse_jobs reads those words (a
+    // patch rewrites the group's words whole, its other pods' addresses included)
+    uint32_t hipf = 0, ipf = 0;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        hipf |= g.st(k) >> 7;   // PS_HAS_HOST_IP
+        ipf |= g.st(k) >> 11;   // PS_IP_SET
+    }
+    const uint32_t mk = m.del | m.need << 8 | m.alloc << 16 | g.j << 24 | (hipf & 1u) << 30 | (ipf & 1u) << 31;
+    S.gjob[(size_t)b * (MAX_WC * WC_GROUPS) + gi] = make_uint4(g.slot, mk, m.need ? bytes : 0u, tag);
+}
 // ... and, once the block's counts are complete, the runs' exclusive prefixes and
 // dirty bits to global memory for k_pod_jobs (wave 0; ng = the block's live groups)
 __device__ __forceinline__ void wc_publish(const DevState& S, uint32_t b, uint32_t ng, const uint32_t* wcnt) {
@@ -2146,7 +2163,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         uint64_t pmask = 0;
         // heartbeat-once ticks: a wave whose speculative groups are all clean only counts them
         bool spec_clean = false;
-        if (S.hb_once) {
+        if (S.hb_once && !split) {
             bool rare = false;
             uint32_t ne = 0, nt = 0, npd = 0, nr = 0;
 #pragma unroll
@@ -2187,6 +2204,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 // emission chunks are runs of 256 live groups in slot order (gpre)
                 if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
                 if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                if (split && S.sparse_jobs) gjob_put(S, b, gpre[j] + a, G[q], m, gbytes, tag);
                 // single rank: into `used` now; multi rank: the Use list (the exchange message)
                 apply_uses(S, G[q], m.usec & ~used_bits(S, G[q], m.usec, uw[q]));
                 __builtin_amdgcn_sched_barrier(0);
@@ -2197,7 +2215,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             return jv && a * POD_PER_THREAD < fill ? (bk0 + j) * S.cp + a * POD_PER_THREAD : ~0u;
         };
         const uint32_t once_iters = SPEC_GROUPS * tpb < maxg ? (maxg - SPEC_GROUPS * tpb + ROW_BATCH * tpb - 1) / (ROW_BATCH * tpb) : 0u;
-        if (once_iters && S.hb_once && once_iters <= 64) {
+        // (not on split ticks: rows with work to emit are most rows there, and a rare
+        // row costs the lean loop's load plus two round trips of its own)
+        if (once_iters && S.hb_once && !split && once_iters <= 64) {
             // heartbeat-once ticks (nothing to hide the chain under): ROW_BATCH rows per
             // iteration, their state and node words only, loaded one iteration ahead; a
             // batch with nothing but counts (every row of a quiet steady tick) is counted
@@ -2260,6 +2280,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                     const uint32_t gbytes = count_group(S, g, m, f, sw, smax);
                     if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
                     if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                    if (split && S.sparse_jobs) gjob_put(S, b, gpre[j] + a, g, m, gbytes, tag);
                     apply_uses(S, g, m.usec & ~used_bits(S, g, m.usec, u));
                 }
             }
@@ -2280,6 +2301,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 const uint32_t gbytes = count_group(S, H, m, f, sw, smax);
                 if (m.dirty) pmask |= 1ull << ((gpre[j] + a) / BLOCK);
                 if (split) wc_add(wcnt, gpre[j] + a, m, gbytes);
+                if (split && S.sparse_jobs) gjob_put(S, b, gpre[j] + a, H, m, gbytes, tag);
                 apply_uses(S, H, m.usec & ~used_bits(S, H, m.usec, u));
                 H = N;
             }
@@ -3857,12 +3879,179 @@ __global__ __launch_bounds__(64 * JOB_WAVES, JOBS_MIN_WAVES) void k_pod_jobs(Dev
     pod_jobs_item<FUSE>(S, tag, b, c0, it, J.stage, J.gpre_w[w], J.nf_w[w]);
 }
 
+// ---------------------------------------------------------------------------
+// k_sparse_jobs: the pod jobs of an unfused split tick (a churn tick: a fifth of
+// the pods deleted or created, the initial tick's dense shape takes the fused
+// k_pod_jobs<true>) from the dirty groups FRONT published (gjob_put): one wave per
+// 64-group run of a chain block, lane l the run's group l.  FRONT already
+// classified every group against the same state and node flags (its masks are
+// what k_pod_jobs<false> derived again), so the run costs two dependent round
+// trips: {bases, the run's prefix, its 64 group records}, then {the dirty groups'
+// state / spec / creation-time / IP words, the reused addresses of its Gets} (the
+// ordinals come from a wave scan of the records' counts), and the stores.  No fill
+// marks, node flags or group prefix are read.  The outputs are k_pod_jobs<false>'s,
+// byte for byte: DeletePods' list (pod_controller.go:155-183), the patch jobs for
+// k_emit in canonical order (configurePod / computePatchData :377-439, the pool's
+// Gets, utils.go:83-108), the state transitions.
+// ---------------------------------------------------------------------------
+constexpr int SJ_WAVES = 4;
+__global__ __launch_bounds__(64 * SJ_WAVES, 4) void k_sparse_jobs(DevState S, uint32_t tag, uint32_t blocks_per_chain) {
+    const uint32_t b = blockIdx.x / blocks_per_chain;
+    const uint32_t c = (blockIdx.x - b * blocks_per_chain) * SJ_WAVES + (uint32_t)wave_id();  // the wave's run
+    if (b >= S.n_chain || c >= (uint32_t)MAX_WC) return;
+    const int l = lane_id();
+    // round trip 1 (all independent): the block's bases, the run's dirty bit and prefix, its groups
+    const JobBase* JB = S.jbase + b;
+    const uint32_t jtag = JB->tag;
+    const uint32_t dbit = (S.wc_dirty[(size_t)b * WC_DIRTY_WORDS + (c >> 5)] >> (c & 31)) & 1u;
+    const uint4 wp = S.wc_pre[(size_t)b * MAX_WC + c];
+    const uint4 gj = S.gjob[((size_t)b * MAX_WC + c) * WC_GROUPS + l];
+    const uint64_t b_del = JB->del, b_pp = JB->pp, b_bytes = JB->pp_bytes, b_alloc = JB->alloc;
+    const uint64_t pod_base = JB->pod_base, alloc_base = JB->alloc_base, take = JB->take, fin = JB->fin, fout0 = JB->fout0;
+    if (jtag != tag || !dbit) return;  // the block has no pod jobs this tick / the run is clean
+    const bool valid = gj.w == tag;     // (a group clean this tick holds an older record)
+    const uint32_t mk = valid ? gj.y : 0u;
+    const uint32_t dm = mk & 0xFFu, nm = (mk >> 8) & 0xFFu, am = (mk >> 16) & 0xFFu, j = (mk >> 24) & 63u;
+    const uint32_t slot = gj.x;
+    uint32_t v[4] = {(uint32_t)__popc(dm), (uint32_t)__popc(nm), valid ? gj.z : 0u, (uint32_t)__popc(am)}, tot[4];
+    const uint32_t n_alloc = v[3];
+    wave_excl_scan<4>(v, tot);
+    const uint64_t o_del = b_del + wp.x + v[0], o_pp = b_pp + wp.y + v[1], o_alloc = b_alloc + wp.w + v[3];
+    uint64_t off = pod_base + b_bytes + wp.z + v[2];
+    // round trip 2: the group's words; the reused addresses of its Gets (ordinals known)
+    uint4 st4 = make_uint4(0, 0, 0, 0), sp4 = st4, ta = st4, tb = st4, ha = st4, hb = st4, pa = st4, pb = st4;
+    if (valid) {
+        st4 = *reinterpret_cast<const uint4*>(S.pod_state + slot);
+        if (nm) {
+            sp4 = *reinterpret_cast<const uint4*>(S.pod_spec + slot);
+            ta = *reinterpret_cast<const uint4*>(S.pod_ctime + slot);
+            tb = *reinterpret_cast<const uint4*>(S.pod_ctime + slot + 4);
+            if (mk >> 30 & 1u) {
+                ha = *reinterpret_cast<const uint4*>(S.host_ip + slot);
+                hb = *reinterpret_cast<const uint4*>(S.host_ip + slot + 4);
+            }
+            if (mk >> 31) {
+                pa = *reinterpret_cast<const uint4*>(S.pod_ip + slot);
+                pb = *reinterpret_cast<const uint4*>(S.pod_ip + slot + 4);
+            }
+        }
+    }
+    uint32_t areuse[POD_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const uint64_t o = o_alloc + (uint32_t)k;
+        areuse[k] = ((uint32_t)k < n_alloc && alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
+    }
+    if (!valid) return;
+    const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w}, spw[4] = {sp4.x, sp4.y, sp4.z, sp4.w};
+    const uint32_t ctm[POD_PER_THREAD] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+    const uint32_t hipk[POD_PER_THREAD] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+    const uint32_t ip0[POD_PER_THREAD] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+    auto st_of = [&](int k) { return (uint16_t)(stw[k >> 1] >> (16 * (k & 1))); };
+    auto sp_of = [&](int k) { return (uint16_t)(spw[k >> 1] >> (16 * (k & 1))); };
+    // the spec lengths (one descriptor when the group's patched pods share a spec, the usual case)
+    uint32_t sd_len[POD_PER_THREAD], sd_max[POD_PER_THREAD];
+    {
+        bool one = true;
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) one &= !((nm >> k) & 1u) || sp_of(k) == sp_of(__builtin_ctz(nm | 256u) & 7);
+        if (nm && one) {
+            const SpecDesc& sd = S.specs[sp_of(__builtin_ctz(nm) & 7)];
+            const uint32_t ln = (uint32_t)sd.len_a + sd.len_b + sd.len_c, mx = sd.max_len;
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) sd_len[k] = ln, sd_max[k] = mx;
+        } else {
+#pragma unroll
+            for (int k = 0; k < POD_PER_THREAD; k++) {
+                sd_len[k] = sd_max[k] = 0;
+                if ((nm >> k) & 1u) {
+                    const SpecDesc& sd = S.specs[sp_of(k)];
+                    sd_len[k] = (uint32_t)sd.len_a + sd.len_b + sd.len_c;
+                    sd_max[k] = sd.max_len;
+                }
+            }
+        }
+    }
+    uint32_t bk0, nbk;
+    block_range(S, b, bk0, nbk);
+    const uint32_t gb = bk0 + j;
+    const int32_t h0 = (int32_t)((S.b_lo + gb) * S.pod_stride + (slot - gb * S.cp));
+    uint64_t od = o_del, op = o_pp;
+    uint32_t ai = 0;
+    uint32_t nst[POD_PER_THREAD], nh[POD_PER_THREAD], np[POD_PER_THREAD];
+    bool dirty = false, wh = false, wpi = false;
+#pragma unroll
+    for (int k = 0; k < POD_PER_THREAD; k++) {
+        const int32_t handle = h0 + k;
+        const uint16_t s0 = st_of(k);
+        uint16_t s = s0;
+        nh[k] = hipk[k], np[k] = ip0[k];
+        if ((dm >> k) & 1u) {
+            S.del_pods[od] = handle;
+            S.del_fin[od] = (s & PS_HAS_FIN) ? 1 : 0;
+            od++;
+            s = 0;  // DeletePod -> Delete(grace 0): the object is gone
+        } else if (s & PS_USED) {
+            if ((nm >> k) & 1u) {
+                uint32_t pip = ip0[k];
+                if ((am >> k) & 1u) {  // the lane's a-th Get (ordinal o_alloc + a)
+                    const uint32_t a = ai++;
+                    const uint64_t gidx = alloc_base + o_alloc + a;
+                    uint32_t ra = areuse[0];
+#pragma unroll
+                    for (int q = 1; q < POD_PER_THREAD; q++) ra = a == (uint32_t)q ? areuse[q] : ra;
+                    pip = gidx < take + fin ? ra : (uint32_t)(fout0 + (gidx - take - fin));
+                }
+                const bool stat = s & PS_STATUS_NONEMPTY;
+                uint32_t hip = 0;
+                if (stat) {
+                    hip = (s & PS_HAS_HOST_IP) ? hipk[k] : S.node_ip;
+                    if (!(s & PS_HAS_HOST_IP)) nh[k] = hip, wh = true;
+                    if (pip != ip0[k]) np[k] = pip, wpi = true;
+                }
+                const uint32_t len = sd_len[k] + (stat ? 23u + ip_len(hip) + ip_len(pip) : 0u);
+                S.pp_pods[op] = handle;
+                S.pp_len[op] = len;
+                S.pp_off[op] = off;
+                S.pp_job[op] = make_uint4(stat ? pip : 0u, hip, ctm[k], sp_of(k));
+                op++;
+                off += sd_max[k];
+                // the apiserver applied the patch
+                s = (uint16_t)((s & ~PS_PHASE_MASK) | (PHASE_RUNNING << PS_PHASE_SHIFT) | PS_CONFORMS | PS_STATUS_NONEMPTY |
+                               (stat ? PS_HAS_HOST_IP : 0));
+                if (stat) s = (uint16_t)((s & ~PS_IP_BITS) | ip_state_bits(S.pool, pip));
+            }
+            s &= (uint16_t)~PS_EVENT;  // (a live pod with an event is evaluated)
+        }
+        dirty |= s != s0;
+        nst[k] = s;
+    }
+    if (wh) {
+        *reinterpret_cast<uint4*>(S.host_ip + slot) = make_uint4(nh[0], nh[1], nh[2], nh[3]);
+        *reinterpret_cast<uint4*>(S.host_ip + slot + 4) = make_uint4(nh[4], nh[5], nh[6], nh[7]);
+    }
+    if (wpi) {
+        *reinterpret_cast<uint4*>(S.pod_ip + slot) = make_uint4(np[0], np[1], np[2], np[3]);
+        *reinterpret_cast<uint4*>(S.pod_ip + slot + 4) = make_uint4(np[4], np[5], np[6], np[7]);
+    }
+    if (dirty)
+        *reinterpret_cast<uint4*>(S.pod_state + slot) =
+            make_uint4(nst[0] | nst[1] << 16, nst[2] | nst[3] << 16, nst[4] | nst[5] << 16, nst[6] | nst[7] << 16);
+}
+
 // init_blocks: the fused launch's node-init blocks (0: k_emit writes the node inits)
 void launch_pod_jobs(const DevState& S, uint32_t tag, hipStream_t st, uint32_t init_blocks, uint64_t now, uint64_t start,
                      hipEvent_t t0, hipEvent_t t1) {
     // the largest chain block's runs: its buckets x their capacity in 8-slot groups
     const uint32_t bpb = (S.nb + S.n_chain - 1) / S.n_chain;
     const uint32_t runs = cdiv((uint64_t)bpb * (S.cp / POD_PER_THREAD), WC_GROUPS);
+    if (S.sparse_jobs && !S.fuse_pods) {
+        const uint32_t bpc = cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, SJ_WAVES);
+        if (t0)
+            hipExtLaunchKernelGGL(k_sparse_jobs, dim3(S.n_chain * bpc), dim3(64 * SJ_WAVES), 0, st, t0, t1, 0, S, tag, bpc);
+        else hipLaunchKernelGGL(k_sparse_jobs, dim3(S.n_chain * bpc), dim3(64 * SJ_WAVES), 0, st, S, tag, bpc);
+        return;
+    }
     uint32_t wpb = cdiv(cdiv(runs < (uint32_t)MAX_WC ? runs : (uint32_t)MAX_WC, S.fuse_pods ? 1 : JOB_NC), JOB_WAVES);
     wpb = wpb ? wpb : 1u;
     const uint32_t pod_blocks = S.n_chain * wpb, grid = pod_blocks + (S.fuse_pods ? init_blocks : 0u);

@@ -107,6 +107,8 @@ def declare(lib, pre):
             "spec_key": (U64, [P(abi.PodSpec), C.c_char_p, SZ]),
             "decode_pods_gpu": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, SZ, VP, VP, VP, VP, P(SZ)]),
             "ingest_pods_json": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, VP, VP, SZ, VP, VP, VP, P(SZ)]),
+            "read_arena_async": (C.c_int, [VP, U64, U64, VP]),
+            "read_wait": (C.c_int, [VP]),
         })
     for name, (res, args) in sig.items():
         f = getattr(lib, pre + name, None)
@@ -516,6 +518,14 @@ class Engine(EngineBase):
         if isinstance(arena, np.ndarray):
             return C.cast(arena.ctypes.data, C.c_char_p), arena.nbytes
         return (arena or b"\0"), len(arena or b"")
+
+    def read_arena_async(self, off, n, out):
+        """kwok_read_arena_async: bytes [off, off + n) of the collected tick's arena
+        queued into `out` (page-locked: host_array); read_wait() waits for them"""
+        self._check(self._lib.kwok_read_arena_async(self._h, off, n, out.ctypes.data), "read_arena_async")
+
+    def read_wait(self):
+        self._check(self._lib.kwok_read_wait(self._h), "read_wait")
 
     STATS = ("ticks_full", "ticks_once", "once_redo", "once_summary")  # KWOK_STAT_* order
 

@@ -277,3 +277,14 @@ def test_c4_documents_equal_the_host_codec():
     assert 0.45 < (ev["flags"][:n] & abi.POD_HAS_FINALIZERS).astype(bool).mean() < 0.55
     assert (ev["phase"][n:] == abi.PHASE_PENDING).all() and not (ev["flags"][n:] & abi.POD_CONFORMS).any()
     e.close()
+
+
+@pytest.mark.parametrize("name", ["specs", "reference_pod_test", "churn"])
+def test_spec_key_collisions_are_decided_exactly(name, monkeypatch):
+    """kwok_spec_key is FNV-1a 64, not collision-resistant, and pod specs come
+    from users.  With the keys cut to 1 bit (KWOK_DEBUG_SPEC_KEY_BITS) every
+    spec collides with another: a document whose key hits a registered spec of
+    other strings is handed to the host (JSON_SPEC_X) after the device compares
+    the strings, so every trace still replays to the golden outputs"""
+    monkeypatch.setenv("KWOK_DEBUG_SPEC_KEY_BITS", "1")
+    test_golden_trace_through_gpu_ingest(name)

@@ -28,7 +28,7 @@ def main():
     if a.steady:
         _, _, now = bench.steady_queued(e, now, a.steady, 3)
     now += 30
-    _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire)
+    _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire, once=a.once)
     e.close()
     print(json.dumps({k: c[k] for k in ("ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "roofline",
                                         "phase_ms")}), flush=True)
