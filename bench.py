@@ -490,6 +490,8 @@ def churn_json_leg(e, fl, ch, now, ticks, n_churn):
             keng.host_array((2 * n_churn,), np.uint32))
     steps, host = [], None
     trans = n_host = docs = nbytes = 0
+    rd = ShimReader(e)
+    reads = []
     for k in range(ticks + 1):
         arena, offs, lens, ops, handles = ch.batch_json(dump, now)
         if k == 0:  # the host codec on this batch (untimed leg warmup)
@@ -503,9 +505,13 @@ def churn_json_leg(e, fl, ch, now, ticks, n_churn):
         t1 = time.perf_counter()
         r = e.tick(now, read=False)
         t2 = time.perf_counter()
+        t3 = time.perf_counter()
+        rd.read(r)  # the drop-in's read-back: every list and patch byte (ShimReader)
+        t4 = time.perf_counter()
         ch.applied(hs.copy(), st)
         now += 30
         if k:
+            reads.append(t4 - t3)
             steps.append((t1 - t0, t2 - t1))
             trans += transitions(r.counters)
             n_host += nh
@@ -523,6 +529,7 @@ def churn_json_leg(e, fl, ch, now, ticks, n_churn):
         "median_ms": {"step": float(np.median([a + b for a, b in steps])) * 1e3,
                       "decode_ingest": float(np.median([a for a, _ in steps])) * 1e3},
         "documents_per_s": docs / ing if ing else None, "documents_decided_by_host": n_host,
+        "with_handoff_ms": (ing + tck + sum(reads)) / ticks * 1e3, "read_back_ms": sum(reads) / ticks * 1e3,
         "host_codec": {"ms": host[0] * 1e3, "documents_per_s": len(offs) / host[0], "threads": min(16, os.cpu_count()),
                        "what": "kwok_decode_pods (codec.cpp) on one batch of the same documents, records only "
                                "(no ingest): the drop-in's host path"},
@@ -633,6 +640,7 @@ def flap_leg(nodes, ticks, heartbeat_once=False):
             tck += t2 - t1
             trans += transitions(r.counters)
             last = dict(zip(abi.COUNTERS, list(r.counters)))
+    js = flap_json(e, f, now, ticks) if heartbeat_once else None
     e.close()
     return {"workload": "C5 node flap under partial management (BASELINE configs[4]): %d nodes x %d pods, "
                         "annotation selector on 50%%, 1%% of the managed nodes deleted + re-added per tick%s"
@@ -640,7 +648,40 @@ def flap_leg(nodes, ticks, heartbeat_once=False):
             "ticks": ticks, "flapped_nodes_per_tick": f.k,
             "value": trans / (ing + tck), "unit": "transitions/s (ingest + tick)",
             "ms_per_step": (ing + tck) / ticks * 1e3, "ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
-            "counters_last_tick": last}
+            "counters_last_tick": last, "from_json": js}
+
+
+def flap_json(e, f, now, ticks):
+    """C5 from the node documents a watch carries (kwok_ingest_nodes_json: decoded on
+    the GPU, Deleted events' statuses not read, Added nodes with a zero status), then
+    the tick; the same flap generator continued on the same engine"""
+    from kwok_amd.codec import Codec
+    codec = Codec(manage_all_nodes=False, manage_nodes_with_annotation_selector="kwok.x-k8s.io/node=fake",
+                  disregard_status_with_annotation_selector="kwok.x-k8s.io/status=custom")
+    ing = tck = 0.0
+    n_host = docs = nbytes = 0
+    for k in range(ticks + 1):
+        now += 30
+        arena, offs, lens, ops, _ = f.batch_json()
+        arena = np.frombuffer(arena, np.uint8).copy()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hs, st, nh = e.ingest_nodes_json(codec, arena, offs, lens, ops)
+        t1 = time.perf_counter()
+        e.tick(now, read=False)
+        t2 = time.perf_counter()
+        if k:
+            ing += t1 - t0
+            tck += t2 - t1
+            n_host += nh
+            docs += len(offs)
+            nbytes += int(lens.sum())
+    codec.close()
+    return {"ms_per_step": (ing + tck) / ticks * 1e3, "decode_ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
+            "documents_per_tick": docs // ticks, "json_bytes_per_tick": nbytes // ticks,
+            "documents_decided_by_host": n_host,
+            "note": "kwok_ingest_nodes_json: the documents (pageable) copied to HBM, k_json_nodes (one thread per "
+                    "document), kwok_ingest_nodes' GPU event switch over the records"}
 
 
 class ShimReader:
@@ -731,7 +772,8 @@ def churn_handoff_leg(e, fl, ch, now, ticks, n_churn, overlap):
     ch.packed, ch.bufs = 12, None
     steps, nbytes, pieces, trans = [], 0, 0, 0
     pending = None
-    for k in range(ticks + 2):
+    warm = 2 if overlap else 1  # (overlapped: step 1 reads tick 0 into freshly pinned staging)
+    for k in range(ticks + warm):
         ev, _ = ch.batch(dump, now)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -748,7 +790,7 @@ def churn_handoff_leg(e, fl, ch, now, ticks, n_churn, overlap):
         dt = time.perf_counter() - t0
         ch.applied(hs.copy(), st, new_only=True)
         now += 30
-        if k >= 1:  # (step 0: warmup; overlapped, it also has no earlier tick to read)
+        if k >= warm:  # (step 0: warmup; overlapped, it also has no earlier tick to read)
             steps.append(dt)
             nbytes += nb
             pieces += pc

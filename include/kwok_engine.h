@@ -577,7 +577,7 @@ int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const u
  * while its strings differ) are decoded by the host codec, and counted in
  * *n_host; nothing is guessed.  Selectors larger than the device's tables (8
  * requirements, 32 values, 2 KiB of keys and values per codec) send every
- * document to the host codec.  Node documents stay with kwok_decode_nodes.
+ * document to the host codec.  Node documents: kwok_ingest_nodes_json below.
  *
  * kwok_decode_pods_gpu: the decode alone (tests, diagnostics): per document its
  *   kwok_pod_event (op UPSERT, handle / spec_id / node_handle -1, as
@@ -599,6 +599,30 @@ int kwok_decode_pods_gpu(kwok_engine* e, const kwok_codec* c, const char* arena,
 int kwok_ingest_pods_json(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
                           const uint64_t* doc_off, const uint32_t* doc_len, const uint8_t* op, const int32_t* handle,
                           size_t n, int32_t* out_handles, int32_t* out_status, uint32_t* out_released, size_t* n_host);
+/* kwok_ingest_nodes_json: WatchNodes / ListNodes from the node documents
+ * themselves (node_controller.go:206-279): decoded on the device - name,
+ * needHeartbeat (the codec's node selector, controller.go:81-98),
+ * needLockNode's disregard selectors, status.phase and the ten nodeInfo
+ * strings - then the GPU event switch of kwok_ingest_nodes over the decoded
+ * records, which never leave the device.  A document with a non-empty
+ * addresses / allocatable / capacity blob (re-serialised canonically by the
+ * host codec, `YAML . 1` in node.status.tpl) or an escaped routed string is
+ * decoded by the host codec and counted in *n_host.  op[i]: the watch event
+ * (KWOK_OP_UPSERT / KWOK_OP_DELETE; a Deleted event's status is not read:
+ * WatchNodes uses its name only, node_controller.go:265-269, so the last state
+ * of a node kwok patched needs no host codec).  A document that fails to decode gets its
+ * decode status (handle -1) and changes nothing.  Outputs and return as
+ * kwok_ingest_nodes.  The arena must be below 4 GiB (kwok_str offsets). */
+int kwok_ingest_nodes_json(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                           const uint64_t* doc_off, const uint32_t* doc_len, const uint8_t* op, size_t n,
+                           int32_t* out_handles, int32_t* out_status, size_t* n_host);
+/* kwok_decode_nodes_gpu: the decode alone (tests, diagnostics): per document
+ * the kwok_node_event kwok_decode_node writes (op UPSERT) and its status; the
+ * documents the device leaves undecided are decoded by the host codec in place
+ * (which re-serialises their blobs over their own spans, as kwok_decode_nodes
+ * does: the arena is written).  Returns the number of rejected documents. */
+int kwok_decode_nodes_gpu(kwok_engine* e, const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                          const uint32_t* doc_len, size_t n, kwok_node_event* ev, int32_t* status, size_t* n_host);
 
 #ifdef __cplusplus
 }

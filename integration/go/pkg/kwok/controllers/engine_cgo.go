@@ -477,6 +477,42 @@ func (g *gpuEngine) ingestPodsJSON(codec *gpuCodec, arena []byte, offs []uint64,
 	return
 }
 
+// ingestNodesJSON: kwok_ingest_nodes_json - one batch of node documents decoded on
+// the GPU and routed by the GPU event switch (the documents staged in page-locked
+// memory).  ops[i]: Deleted -> KWOK_OP_DELETE (its status is not read), else
+// KWOK_OP_UPSERT.
+func (g *gpuEngine) ingestNodesJSON(codec *gpuCodec, arena []byte, offs []uint64, lens []uint32,
+	ops []uint8) (handles, status []int32, nHost int, err error) {
+	n := len(offs)
+	handles, status = make([]int32, n), make([]int32, n)
+	if n == 0 {
+		return
+	}
+	arp, err := g.arBuf.get(len(arena) + 1)
+	if err != nil {
+		return
+	}
+	ar := unsafe.Slice((*byte)(arp), len(arena)+1)
+	copy(ar, arena)
+	resp, err := g.resBuf.get(2 * 4 * n)
+	if err != nil {
+		return
+	}
+	res := unsafe.Slice((*int32)(resp), 2*n)
+	var nh C.size_t
+	rc := C.kwok_ingest_nodes_json(g.h, codec.c, (*C.char)(unsafe.Pointer(&ar[0])), C.size_t(len(arena)),
+		(*C.uint64_t)(&offs[0]), (*C.uint32_t)(&lens[0]), (*C.uint8_t)(&ops[0]), C.size_t(n),
+		(*C.int32_t)(&res[0]), (*C.int32_t)(&res[n]), &nh)
+	if rc < 0 {
+		err = fmt.Errorf("kwok_ingest_nodes_json: %d: %s", int(rc), g.lastError())
+		return
+	}
+	copy(handles, res[:n])
+	copy(status, res[n:2*n])
+	nHost = int(nh)
+	return
+}
+
 // poolPut replicates IPs another rank released at ingest time (multi-GPU).
 func (g *gpuEngine) poolPut(ips []uint32) error {
 	if len(ips) == 0 {

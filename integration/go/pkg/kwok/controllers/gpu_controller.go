@@ -58,7 +58,7 @@ type objBatch struct {
 	lens  []uint32
 	del   []bool
 	uids  []types.UID
-	refs  []types.NamespacedName // pods: namespace / name (the apply's target)
+	refs  []types.NamespacedName // namespace / name (a pod's: the apply's target; a node's name)
 	nodes []string               // pods: spec.nodeName (EnableCNI's cni.Remove check)
 }
 
@@ -74,8 +74,11 @@ func (b *objBatch) add(w watchObj) error {
 	b.uids = append(b.uids, w.uid)
 	var ref types.NamespacedName // (one entry per object, so the indices stay aligned)
 	var node string
-	if p, ok := w.obj.(*corev1.Pod); ok {
-		ref, node = types.NamespacedName{Namespace: p.Namespace, Name: p.Name}, p.Spec.NodeName
+	switch o := w.obj.(type) {
+	case *corev1.Pod:
+		ref, node = types.NamespacedName{Namespace: o.Namespace, Name: o.Name}, o.Spec.NodeName
+	case *corev1.Node:
+		ref = types.NamespacedName{Name: o.Name}
 	}
 	b.refs = append(b.refs, ref)
 	b.nodes = append(b.nodes, node)
@@ -183,6 +186,7 @@ type GPUController struct {
 
 	gpuCodec    bool // pod documents decoded on the GPU (kwok_ingest_pods_json); KWOK_GPU_CODEC=0: the host codec
 	podDocsHost int  // pod documents the GPU codec left to the host codec (logged)
+	nodeDocsHost int // node documents the GPU codec left to the host codec (logged)
 }
 
 func newGPUController(conf Config, interval time.Duration) (*GPUController, error) {
@@ -523,10 +527,52 @@ func (c *GPUController) setupCNI(ctx context.Context, tasks *parallelTasks) erro
 	return c.eng.cniAssign(keep, kept)
 }
 
+// flushNodes: the batch's node documents decoded on the GPU (kwok_ingest_nodes_json:
+// a Deleted event's status is not read; a non-empty addresses / allocatable /
+// capacity blob goes to the host codec inside the call) and routed by the GPU
+// event switch; flushNodesHost decodes on the host (KWOK_GPU_CODEC=0).
+// kwok_amd/controller.py _flush_nodes_gpu is this function in Python.
 func (c *GPUController) flushNodes(ctx context.Context, b objBatch) error {
 	if len(b.offs) == 0 {
 		return nil
 	}
+	if !c.gpuCodec {
+		return c.flushNodesHost(ctx, b)
+	}
+	logger := log.FromContext(ctx)
+	ops := make([]uint8, len(b.offs))
+	for i := range ops {
+		ops[i] = C.KWOK_OP_UPSERT
+		if b.del[i] {
+			ops[i] = C.KWOK_OP_DELETE
+		}
+	}
+	hs, ss, nHost, err := c.eng.ingestNodesJSON(c.codec, b.arena, b.offs, b.lens, ops)
+	if err != nil {
+		return err
+	}
+	c.nodeDocsHost += nHost
+	for i := range ops {
+		if ss[i] != C.KWOK_OK {
+			if ss[i] == C.KWOK_EDOMAIN || ss[i] == C.KWOK_EINVAL { // outside the engine's domain (DESIGN.md §2)
+				logger.Warn("Node outside the supported domain", fmt.Errorf("kwok status %d", ss[i]))
+			}
+			continue
+		}
+		name := b.refs[i].Name
+		if b.del[i] {
+			delete(c.nodeName, hs[i])
+			delete(c.nodeHandle, name)
+		} else {
+			c.nodeName[hs[i]] = name
+			c.nodeHandle[name] = hs[i]
+		}
+	}
+	return nil
+}
+
+// flushNodesHost: flushNodes with the host codec (kwok_decode_nodes)
+func (c *GPUController) flushNodesHost(ctx context.Context, b objBatch) error {
 	logger := log.FromContext(ctx)
 	ev, st := c.codec.decodeNodes(b.arena, b.offs, b.lens, runtime.NumCPU())
 	keep := make([]C.kwok_node_event, 0, len(ev))

@@ -266,6 +266,7 @@ class Stats:
     node_records: int = 0
     pod_records: int = 0
     pod_docs_host: int = 0  # pod documents the GPU codec left to the host codec
+    node_docs_host: int = 0  # node documents the GPU codec left to the host codec
     pod_runs: int = 0
     bodies: int = 0
     rejected: list = field(default_factory=list)
@@ -305,7 +306,8 @@ class Controller:
                            disregard_status_with_annotation_selector=conf.disregard_status_with_annotation_selector,
                            disregard_status_with_label_selector=conf.disregard_status_with_label_selector)
         self.threads = codec_threads
-        # pod documents decoded on the GPU (kwok_ingest_pods_json) when the backend has it
+        # node and pod documents decoded on the GPU (kwok_ingest_nodes_json / kwok_ingest_pods_json)
+        # when the backend has them (the CPU oracle backend takes the host codec)
         self.gpu_codec = gpu_codec and hasattr(self.eng, "ingest_pods_json")
         self.nodes: list[WatchObj] = []
         self.pods: list[WatchObj] = []
@@ -393,9 +395,13 @@ class Controller:
         return keep, [json.dumps(w.obj, separators=(",", ":")).encode() for w in keep]
 
     def _flush_nodes(self, batch):
+        """gpu_controller.go flushNodes: on the HIP engine the documents are decoded on
+        the GPU (kwok_ingest_nodes_json); a backend without it takes the host codec"""
         ws, docs = batch
         if not ws:
             return
+        if self.gpu_codec:
+            return self._flush_nodes_gpu(ws, docs)
         b = self.codec.decode_nodes(docs, strict=False, threads=self.threads)
         keep, names = [], []
         for i, w in enumerate(ws):
@@ -420,6 +426,28 @@ class Controller:
             else:
                 self.node_name[int(hs[k])] = names[k]
                 self.node_handle[names[k]] = int(hs[k])
+
+    def _flush_nodes_gpu(self, ws, docs):
+        """gpu_controller.go flushNodes on the device codec: the documents straight to
+        kwok_ingest_nodes_json (a Deleted event's status is not read); names from the
+        watch objects"""
+        arena, offs, lens = Engine._docs(docs)
+        ops = np.array([abi.OP_DELETE if w.deleted else abi.OP_UPSERT for w in ws], np.uint8)
+        hs, st, nh = self.eng.ingest_nodes_json(self.codec, arena, offs, lens, ops)
+        self.stats.node_docs_host += nh
+        self.stats.node_records += int(np.isin(st, (abi.EDOMAIN, abi.EINVAL), invert=True).sum())
+        for k, w in enumerate(ws):
+            name = _meta(w.obj).get("name", "")
+            if st[k] != abi.OK:
+                if st[k] in (abi.EDOMAIN, abi.EINVAL):  # outside the engine's domain: not simulated (DESIGN.md §2)
+                    self.stats.rejected.append(("node", name, int(st[k])))
+                continue
+            if w.deleted:
+                self.node_name.pop(int(hs[k]), None)
+                self.node_handle.pop(name, None)
+            else:
+                self.node_name[int(hs[k])] = name
+                self.node_handle[name] = int(hs[k])
 
     def _spec_id(self, b, d):
         spec = (tuple((b.text(c.name), b.text(c.image)) for c in d.containers[:d.n_containers]),

@@ -257,6 +257,9 @@ struct kwok_engine {
         JsonCfg* cfg_h = nullptr;          // pinned staging
         uint64_t* tab_key = nullptr;
         int32_t* tab_id = nullptr;
+        int32_t* nstat = nullptr;          // node documents: the device decode's status per document
+        kwok_node_event* nev_fix = nullptr;  // node records gathered for / scattered from the host
+        size_t ncap = 0;
         uint2* tab_canon = nullptr;        // per slot: offset / length of its spec's canonical string in canon
         uint8_t* canon = nullptr;          // the registered specs' canonical strings (json_spec_canon)
         size_t canon_cap = 0;
@@ -1113,7 +1116,7 @@ void kwok_engine_destroy(kwok_engine* e) {
     {
         auto& J = e->json;
         void* jp[] = {J.off, J.len, J.op, J.handle, J.side, J.host_list, J.fix_ev, J.fix_side, J.n_host, J.cfg,
-                      J.tab_key, J.tab_id, J.tab_canon, J.canon};
+                      J.tab_key, J.tab_id, J.tab_canon, J.canon, J.nstat, J.nev_fix};
         for (void* p : jp)
             if (p) (void)hipFree(p);
         if (J.cfg_h) (void)hipHostFree(J.cfg_h);
@@ -1257,7 +1260,9 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         // KWOK_TICK_CHAIN_BLOCKS: fewer chain blocks, so that the grids of many engines
         // sharing one GPU (the 8-rank C3 test) are co-resident together
         if (const char* v = getenv("KWOK_TICK_CHAIN_BLOCKS")) S.n_chain = std::min<uint32_t>(S.n_chain, (uint32_t)std::max(1, atoi(v)));
-        e->n_stream = once ? 8u : (uint32_t)(cus * wants);
+        // (heartbeat-once: no streamer blocks - the one body is a chain block's slice,
+        // written after its arrival, not by blocks that wait for the chain's CUs)
+        e->n_stream = once ? 0u : (uint32_t)(cus * wants);
         // multi rank: the BACK launch fills the CUs' spare k_tick slots with pool-only
         // blocks (the pool phase's word-blocks over more blocks; all co-resident).  Not
         // when several engines share the GPU (KWOK_TICK_BLOCKS_PER_CU / _CHAIN_BLOCKS:
@@ -1634,6 +1639,16 @@ NodeFix complete_node(kwok_engine* e, const kwok_node_event& x, uint32_t idx, co
 // 256-270) on the GPU over the device node directory (ingest.hip): prep, the host's
 // completions of non-empty statuses, a stable sort by bucket, one wave per bucket
 // in event order.  Two host round trips per batch (the prep summary, the results).
+// kwok_ingest_nodes_json: the records were decoded on the device (G.d_nev, the
+// documents in G.d_arena); the records the host completes come from here
+struct NodeJsonCtx {
+    const char* arena;                            // the caller's documents (device-decoded records' spans)
+    const std::unordered_map<uint32_t, uint32_t>* hdoc;  // document -> its host decode (hrec / hbuf)
+    const std::vector<kwok_node_event>* hrec;     // host-decoded records, spans into their hbuf
+    const std::vector<std::string>* hbuf;
+};
+int ingest_nodes_impl(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
+                      int32_t* out_handles, int32_t* out_status, const NodeJsonCtx* nj);
 int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
                       int32_t* out_handles, int32_t* out_status) {
     if (!e || (n && !ev) || n > 0x7FFFFFF0ull || (arena_len && !arena)) return KWOK_EINVAL;
@@ -1644,9 +1659,14 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
     e->quiet = 0;
     e->sum_valid = false;
     if (!n) return 0;
-    const auto t0 = clk::now();
     int rc = node_reserve(e, n, arena_len);
     if (rc) return rc;
+    return ingest_nodes_impl(e, ev, n, arena, arena_len, out_handles, out_status, nullptr);
+}
+int ingest_nodes_impl(kwok_engine* e, const kwok_node_event* ev, size_t n, const char* arena, size_t arena_len,
+                      int32_t* out_handles, int32_t* out_status, const NodeJsonCtx* nj) {
+    const auto t0 = clk::now();
+    int rc = 0;
     auto& G = e->ing;
     hipStream_t st = e->st;
     // the empty-status blob (kwok's own fleets create Nodes with an empty status)
@@ -1659,10 +1679,11 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         e->has_empty_blob.store(true);
     }
     // the batch in kwok_host_alloc memory is read in place by k_nd_prep; any other is copied
-    const void* zev = e->ingest_zc ? host_mapped(ev, n * sizeof(kwok_node_event)) : nullptr;
-    const void* zar = e->ingest_zc && arena_len ? host_mapped(arena, arena_len) : nullptr;
-    if (!zev) HIPCHK(e, hipMemcpyAsync(G.d_nev, ev, n * sizeof(kwok_node_event), hipMemcpyHostToDevice, st));
-    if (arena_len && !zar) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
+    // (kwok_ingest_nodes_json: both on the device already)
+    const void* zev = !nj && e->ingest_zc ? host_mapped(ev, n * sizeof(kwok_node_event)) : nullptr;
+    const void* zar = !nj && e->ingest_zc && arena_len ? host_mapped(arena, arena_len) : nullptr;
+    if (!zev && !nj) HIPCHK(e, hipMemcpyAsync(G.d_nev, ev, n * sizeof(kwok_node_event), hipMemcpyHostToDevice, st));
+    if (arena_len && !zar && !nj) HIPCHK(e, hipMemcpyAsync(G.d_arena, arena, arena_len, hipMemcpyHostToDevice, st));
     NodeBatch N{};
     N.ev = static_cast<const kwok_node_event*>(zev ? zev : (const void*)G.d_nev);
     N.n = (uint32_t)n;
@@ -1718,10 +1739,32 @@ int kwok_ingest_nodes(kwok_engine* e, const kwok_node_event* ev, size_t n, const
         std::vector<NodeFix> fix(n_host);
         std::mutex blob_mu;
         const bool par = n_host >= NODE_PAR_MIN && e->n_part > 1;
+        // kwok_ingest_nodes_json: the listed records the device decoded come back from
+        // the device (their spans index the caller's documents); the host-decoded ones
+        // are at hand with their canonical blobs
+        std::vector<kwok_node_event> dev_rec;
+        if (nj) {
+            dev_rec.resize(n_host);
+            HIPCHK(e, hipMemcpyAsync(G.host_idx, idx.data(), (size_t)n_host * 4, hipMemcpyHostToDevice, st));
+            launch_node_gather(G.d_nev, G.host_idx, n_host, e->json.nev_fix, st);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipMemcpyAsync(dev_rec.data(), e->json.nev_fix, (size_t)n_host * sizeof(kwok_node_event),
+                                     hipMemcpyDeviceToHost, st));
+            HIPCHK(e, hipStreamSynchronize(st));
+        }
         run_parts(e, par, [&](int p) {
             const size_t lo = par ? (size_t)n_host * p / e->n_part : (p ? n_host : 0);
             const size_t hi = par ? (size_t)n_host * (p + 1) / e->n_part : n_host;
-            for (size_t k = lo; k < hi; k++) fix[k] = complete_node(e, ev[idx[k]], idx[k], arena, blob_mu);
+            for (size_t k = lo; k < hi; k++) {
+                if (!nj) {
+                    fix[k] = complete_node(e, ev[idx[k]], idx[k], arena, blob_mu);
+                    continue;
+                }
+                auto h = nj->hdoc->find(idx[k]);
+                fix[k] = h == nj->hdoc->end()
+                             ? complete_node(e, dev_rec[k], idx[k], nj->arena, blob_mu)
+                             : complete_node(e, (*nj->hrec)[h->second], idx[k], (*nj->hbuf)[h->second].data(), blob_mu);
+            }
         });
         if ((rc = upload_blobs(e))) return rc;
         HIPCHK(e, hipMemcpyAsync(G.d_nfix, fix.data(), fix.size() * sizeof(NodeFix), hipMemcpyHostToDevice, st));
@@ -2345,6 +2388,215 @@ uint64_t kwok_spec_key(const kwok_pod_spec* spec, const char* arena, size_t aren
     return json_spec_key(cs, ics, gates);
 }
 
+// ---- node documents on the GPU (json.hip k_json_nodes) -----------------------
+// kwok_ingest_nodes_json: WatchNodes / ListNodes from the documents themselves
+// (node_controller.go:206-279): decoded on the device, the host codec only for
+// the documents the scanner lists (a non-empty addresses / allocatable /
+// capacity blob, whose canonical form is the host's, or an escaped routed
+// string), then kwok_ingest_nodes' GPU event switch over the records, which
+// stay on the device.
+namespace {
+// documents [0, n) decoded on the device: records in ing.d_nev (op: the caller's, or
+// KWOK_OP_UPSERT when op is null; 0xFF for a document not decided there), the
+// decode statuses into dstat, the number listed for the host (json.host_list) in *nh
+int json_nodes_decode(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len, const uint64_t* doc_off,
+                      const uint32_t* doc_len, const uint8_t* op, size_t n, std::vector<int32_t>& dstat, uint32_t* nh) {
+    int rc = node_reserve(e, n, arena_len + 16);  // (the scanner reads whole 16-byte windows)
+    if (rc) return rc;
+    if ((rc = json_reserve(e, n))) return rc;
+    auto& G = e->ing;
+    auto& J = e->json;
+    if (n > J.ncap) {
+        if (J.nstat) (void)hipFree(J.nstat);
+        if (J.nev_fix) (void)hipFree(J.nev_fix);
+        J.nstat = nullptr, J.nev_fix = nullptr, J.ncap = 0;
+        const size_t cap = std::max<size_t>(n + n / 4, 4096);
+        if ((rc = dalloc(e, &J.nstat, cap)) || (rc = dalloc(e, &J.nev_fix, cap))) return rc;
+        J.ncap = cap;
+    }
+    hipStream_t st = e->st, ps = G.pst;
+    if ((rc = codec_export(c, J.cfg_h))) {  // (selectors beyond the device tables: every document to the host)
+        if (rc != KWOK_EDOMAIN) return e->fail(rc, "%s", kwok_codec_last_error());
+        memset(J.cfg_h, 0, sizeof(JsonCfg));
+        J.cfg_h->all_host = 1;
+    }
+    HIPCHK(e, hipMemcpyAsync(J.cfg, J.cfg_h, sizeof(JsonCfg), hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(J.off, doc_off, n * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(J.len, doc_len, n * 4, hipMemcpyHostToDevice, st));
+    if (op) HIPCHK(e, hipMemcpyAsync(J.op, op, n, hipMemcpyHostToDevice, st));
+    else HIPCHK(e, hipMemsetAsync(J.op, KWOK_OP_UPSERT, n, st));
+    HIPCHK(e, hipMemsetAsync(J.n_host, 0, 4, st));
+    // the arena in pieces on the prep stream, each piece's documents decoded as it lands
+    bool sorted = true;
+    for (size_t i = 1; i < n && sorted; i++) sorted = doc_off[i] >= doc_off[i - 1] + doc_len[i - 1];
+    const uint32_t K = sorted && arena_len > (64u << 20) ? (uint32_t)std::min<size_t>(8, n / 4096 + 1) : 1u;
+    HIPCHK(e, hipEventRecord(G.go, st));
+    HIPCHK(e, hipStreamWaitEvent(ps, G.go, 0));
+    uint64_t copied = 0;
+    for (uint32_t k = 0; k < K; k++) {
+        const size_t d0 = n * k / K, d1 = n * (k + 1) / K;
+        const uint64_t hi = k + 1 == K ? arena_len : std::min<uint64_t>(arena_len, doc_off[d1 - 1] + doc_len[d1 - 1]);
+        if (hi > copied) {
+            HIPCHK(e, hipMemcpyAsync(G.d_arena + copied, arena + copied, hi - copied, hipMemcpyHostToDevice, ps));
+            copied = hi;
+        }
+        HIPCHK(e, hipEventRecord(G.prepped[k & 1], ps));
+        HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
+        JsonNodeArgs A{};
+        A.arena = G.d_arena;
+        A.arena_len = arena_len;
+        A.doc_off = J.off + d0;
+        A.doc_len = J.len + d0;
+        A.op = J.op + d0;
+        A.n = (uint32_t)(d1 - d0);
+        A.cfg = J.cfg;
+        A.ev = G.d_nev + d0;
+        A.status = J.nstat + d0;
+        A.host_list = J.host_list;
+        A.n_host = J.n_host;
+        A.base = (uint32_t)d0;
+        launch_json_nodes(A, st);
+        HIPCHK(e, hipGetLastError());
+    }
+    dstat.resize(n);
+    HIPCHK(e, hipMemcpyAsync(dstat.data(), J.nstat, n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipMemcpyAsync(J.n_host_h, J.n_host, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    *nh = *J.n_host_h;
+    return KWOK_OK;
+}
+// the documents json_nodes_decode listed, sorted
+int json_nodes_listed(kwok_engine* e, uint32_t nh, std::vector<uint32_t>& list) {
+    list.resize(nh);
+    if (!nh) return KWOK_OK;
+    HIPCHK(e, hipMemcpyAsync(list.data(), e->json.host_list, (size_t)nh * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    std::sort(list.begin(), list.end());
+    return KWOK_OK;
+}
+}  // namespace
+
+// ---- node documents on the GPU (json.hip k_json_nodes) -----------------------
+// kwok_ingest_nodes_json: WatchNodes / ListNodes from the documents themselves
+// (node_controller.go:206-279): decoded on the device, the host codec only for
+// the documents the scanner lists (a non-empty addresses / allocatable /
+// capacity blob, whose canonical form is the host's, or an escaped routed
+// string), then kwok_ingest_nodes' GPU event switch over the records, which
+// stay on the device.
+int kwok_ingest_nodes_json(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
+                           const uint64_t* doc_off, const uint32_t* doc_len, const uint8_t* op, size_t n,
+                           int32_t* out_handles, int32_t* out_status, size_t* n_host) {
+    if (!e || !c || (n && (!doc_off || !doc_len || !op)) || (arena_len && !arena) || n > 0x7FFFFFF0ull ||
+        arena_len > 0xFFFFFFF0ull)
+        return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    e->emit_hint = true;
+    e->quiet = 0;
+    e->sum_valid = false;
+    if (n_host) *n_host = 0;
+    if (!n) return 0;
+    const auto t0 = clk::now();
+    std::vector<int32_t> dstat;
+    uint32_t nh = 0;
+    int rc = json_nodes_decode(e, c, arena, arena_len, doc_off, doc_len, op, n, dstat, &nh);
+    if (rc) return rc;
+    auto& G = e->ing;
+    auto& J = e->json;
+    hipStream_t st = e->st;
+    // the listed documents: the host codec on a private copy of each (it writes the
+    // canonical blobs over their spans); their records to the device, spans moved to
+    // the batch's arena (the device only bounds-checks the blob spans: the host
+    // completion below interns the canonical bytes from the private copy)
+    std::unordered_map<uint32_t, uint32_t> hdoc;
+    std::vector<kwok_node_event> hrec(nh), hdev(nh);
+    std::vector<std::string> hbuf(nh);
+    if (nh) {
+        std::vector<uint32_t> list;
+        if ((rc = json_nodes_listed(e, nh, list))) return rc;
+        const bool par = nh >= NODE_PAR_MIN && e->n_part > 1;
+        run_parts(e, par, [&](int p) {
+            const size_t lo = par ? (size_t)nh * p / e->n_part : (p ? nh : 0);
+            const size_t hi = par ? (size_t)nh * (p + 1) / e->n_part : nh;
+            for (size_t q = lo; q < hi; q++) {
+                const uint32_t i = list[q];
+                hbuf[q].assign(arena + doc_off[i], doc_len[i]);
+                kwok_node_event x{};
+                const int r = kwok_decode_node(c, hbuf[q].data(), hbuf[q].size(), 0, hbuf[q].size(), &x);
+                hrec[q] = x;
+                kwok_node_event d = x;
+                auto mv = [&](kwok_str& s) {
+                    if (s.len) s.off += (uint32_t)doc_off[i];
+                };
+                mv(d.name), mv(d.addresses), mv(d.allocatable), mv(d.capacity);
+                for (int k = 0; k < KWOK_NI_COUNT; k++) mv(d.node_info[k]);
+                d.op = r == KWOK_OK ? op[i] : (uint8_t)0xFF;
+                if (r != KWOK_OK) d.name = kwok_str{0, 0};
+                hdev[q] = d;
+                dstat[i] = r;
+            }
+        });
+        for (uint32_t q = 0; q < nh; q++) hdoc.emplace(list[q], q);
+        HIPCHK(e, hipMemcpyAsync(J.host_list, list.data(), (size_t)nh * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(e, hipMemcpyAsync(J.nev_fix, hdev.data(), (size_t)nh * sizeof(kwok_node_event), hipMemcpyHostToDevice, st));
+        launch_node_scatter(G.d_nev, J.nev_fix, J.host_list, nh, st);
+        HIPCHK(e, hipGetLastError());
+    }
+    if (n_host) *n_host = nh;
+    if (e->iprof)
+        fprintf(stderr, "[kwok json] %zu node documents decoded on the GPU (%u by the host): %.2f ms\n", n, nh,
+                ms_between(t0, clk::now()));
+    NodeJsonCtx ctx{arena, &hdoc, &hrec, &hbuf};
+    std::vector<int32_t> stat(out_status ? 0 : n);
+    int32_t* so = out_status ? out_status : stat.data();
+    rc = ingest_nodes_impl(e, nullptr, n, arena, arena_len, out_handles, so, &ctx);
+    if (rc < 0) return rc;
+    for (size_t i = 0; i < n; i++)  // a document that failed to decode: its decode status
+        if (dstat[i] != KWOK_OK) {
+            so[i] = dstat[i];
+            if (out_handles) out_handles[i] = -1;
+        }
+    return rc;
+}
+
+// kwok_decode_nodes_gpu: the decode alone (tests): the records kwok_decode_nodes
+// would write, the listed documents decoded by the host codec in place (it
+// re-serialises their blobs over their spans, as kwok_decode_nodes does)
+int kwok_decode_nodes_gpu(kwok_engine* e, const kwok_codec* c, char* arena, size_t arena_len, const uint64_t* doc_off,
+                          const uint32_t* doc_len, size_t n, kwok_node_event* ev, int32_t* status, size_t* n_host) {
+    if (!e || !c || (n && (!doc_off || !doc_len || !ev || !status)) || (arena_len && !arena) || n > 0x7FFFFFF0ull ||
+        arena_len > 0xFFFFFFF0ull)
+        return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    drain(e);
+    if (e->poisoned) return poisoned(e);
+    if (n_host) *n_host = 0;
+    if (!n) return 0;
+    std::vector<int32_t> dstat;
+    uint32_t nh = 0;
+    int rc = json_nodes_decode(e, c, arena, arena_len, doc_off, doc_len, nullptr, n, dstat, &nh);
+    if (rc) return rc;
+    HIPCHK(e, hipMemcpyAsync(ev, e->ing.d_nev, n * sizeof(kwok_node_event), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    std::vector<uint32_t> list;
+    if ((rc = json_nodes_listed(e, nh, list))) return rc;
+    for (uint32_t i : list) {
+        kwok_node_event x{};
+        dstat[i] = kwok_decode_node(c, arena, arena_len, doc_off[i], doc_len[i], &x);
+        ev[i] = x;
+    }
+    int bad = 0;
+    for (size_t i = 0; i < n; i++) {
+        status[i] = dstat[i];
+        if (dstat[i] != KWOK_OK) ev[i] = kwok_node_event{};
+        else ev[i].op = KWOK_OP_UPSERT;
+        bad += dstat[i] != KWOK_OK;
+    }
+    if (n_host) *n_host = nh;
+    return bad;
+}
+
 int kwok_decode_pods_gpu(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len,
                          const uint64_t* doc_off, const uint32_t* doc_len, size_t n, kwok_pod_event* ev,
                          kwok_str* name_ns, uint64_t* spec_key, int32_t* status, size_t* n_host) {
@@ -2587,8 +2839,9 @@ int enqueue_tick(kwok_engine* e, int k, bool requeue) {
     T.inits_folded = false;  // (set where k_pod_jobs is launched)
     // ... and leave the whole stream to the streamers: a dirty chain block's share
     // of it would hold up the pool phase, which waits for every dirty block
-    S.stream_share = e->share_env >= 0 ? (uint32_t)e->share_env
-                                       : (hb_bytes < (32ull << 20) || T.split ? 1024u : (S.hb_nt ? 860u : 921u));
+    S.stream_share = e->n_stream == 0 ? 0u
+                     : e->share_env >= 0 ? (uint32_t)e->share_env
+                                         : (hb_bytes < (32ull << 20) || T.split ? 1024u : (S.hb_nt ? 860u : 921u));
     S.use_events_only = T.quiet ? 1u : 0u;
     S.foreign = e->foreign_ips ? 1u : 0u;
     int rc = bind_slot(e, k);

@@ -907,11 +907,13 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
         p.r = &rd;
         p.cfg = A.cfg;
         const bool ok = !A.cfg->all_host && jparse(rd, p);
+        // (a document the scan routed past an escaped key may hold errors the host's
+        // first-key lookup does not see: the host decides it, errors included)
         if (A.cfg->all_host) status = JSON_HOST;  // (selectors the device tables do not hold)
         else if (!ok || !p.root_obj) status = KWOK_EDOMAIN;
-        else if (p.err) status = p.err;
-        else if (!p.meta_obj || !p.spec_obj || !p.ct_ok) status = p.host ? JSON_HOST : KWOK_EDOMAIN;
         else if (p.host) status = JSON_HOST;
+        else if (p.err) status = p.err;
+        else if (!p.meta_obj || !p.spec_obj || !p.ct_ok) status = KWOK_EDOMAIN;
         else status = KWOK_OK;
         if (status == KWOK_OK) {
             const JsonCfg& C = *A.cfg;
@@ -973,6 +975,301 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st) {
     if (!A.n) return;
     hipLaunchKernelGGL(k_json_pods, dim3((A.n + 255) / 256), dim3(256), 0, st, A);
+}
+
+// ---------------------------------------------------------------------------
+// the node document (kwok_decode_node, codec.cpp): WatchNodes / ListNodes'
+// routing facts (node_controller.go:206-223, 256-270) - needHeartbeat = the
+// node selector (controller.go:81-98: all nodes, an annotation selector or a
+// label selector), needLockNode = not disregarded (empty label maps never
+// match) - and the A.5 inputs configureNode reads (node_controller.go:356-391):
+// status.phase, the ten nodeInfo strings and the addresses / allocatable /
+// capacity blobs.  Those blobs are re-serialised canonically by the host codec
+// (`YAML . 1` echoes, node.status.tpl): a document holding a non-empty one is
+// listed for the host (JSON_HOST), as is any string the scan would have to
+// compare as decoded text (an escaped routed key, label key or compared value).
+// kwok's own fleets create Nodes with an empty status: none of them is listed.
+// ---------------------------------------------------------------------------
+enum : uint8_t {
+    N_NONE = 0, N_ROOT, N_META, N_STATUS, N_NAME, N_ANN, N_LAB, N_ANNV, N_LABV, N_PHASE, N_ADDR, N_ALLOC, N_CAP,
+    N_INFO, N_INFOV,
+};
+struct NodeScan {
+    JRd* r;
+    const JsonCfg* cfg;
+    uint64_t cx = 0;
+    uint8_t next = N_NONE;
+    uint8_t info_k = 0;   // the nodeInfo key the next value belongs to
+    int err = 0;          // KWOK_EDOMAIN
+    bool host = false;    // JSON_HOST
+    bool root_obj = false, meta_obj = false;
+    bool skip_status = false;  // a Deleted event: its status is not read (node_controller.go:265-269: the name only)
+    uint32_t seen_root = 0, seen_meta = 0, seen_status = 0, seen_info = 0;
+    Span name{0, 0};
+    uint32_t n_ann = 0, n_lab = 0;
+    uint32_t km_man = 0, km_dis = 0;  // the current entry's key: requirements of the manage / disregard selector
+    SelState man{0, 0}, dis_a{0, 0}, dis_l{0, 0};
+    uint8_t phase = KWOK_PHASE_NONE;
+    Span info[KWOK_NI_COUNT];
+
+    __device__ uint8_t ctx(int d) const { return d < XD ? (uint8_t)(cx >> (8 * d)) : N_NONE; }
+    __device__ void set_ctx(int d, uint8_t c) {
+        if (d < XD) cx = (cx & ~(0xFFull << (8 * d))) | ((uint64_t)c << (8 * d));
+    }
+    __device__ uint8_t first(uint32_t& seen, int bit, uint8_t c) {
+        if (seen & (1u << bit)) return N_NONE;
+        seen |= 1u << bit;
+        return c;
+    }
+    __device__ bool k_is(const JTok& t, const char* s, uint32_t n) {
+        if (t.len != n) return false;
+        for (uint32_t q = 0; q < n; q++)
+            if (r->at(t.off + q) != (uint8_t)s[q]) return false;
+        return true;
+    }
+    // the selector that decides `managed` over this label map (null: none does)
+    __device__ const JsonSel* man_sel(bool ann) const {
+        if (cfg->manage_all) return nullptr;
+        if (cfg->man_ann.set) return ann ? &cfg->man_ann : nullptr;
+        return ann ? nullptr : &cfg->man_lab;
+    }
+    __device__ uint32_t key_reqs(const JsonSel* S, const JTok& t) {
+        uint32_t m = 0;
+        if (!S || !S->set) return 0;
+        for (uint32_t q = 0; q < S->nreq; q++)
+            if (bytes_eq(*r, t.off, t.len, cfg->bytes + S->key_off[q], S->key_len[q])) m |= 1u << q;
+        return m;
+    }
+    __device__ void sel_value(const JsonSel* S, SelState& st, uint32_t km, const JTok& t) {
+        for (uint32_t q = 0; q < S->nreq; q++) {  // the last entry of a key wins (a Go map)
+            if (!((km >> q) & 1)) continue;
+            bool in = false;
+            for (uint32_t v = 0; v < S->val_n[q]; v++) {
+                const uint32_t vi = S->val_first[q] + v;
+                in |= bytes_eq(*r, t.off, t.len, cfg->bytes + S->val_off[vi], S->val_len[vi]);
+            }
+            st.has |= 1u << q;
+            st.in = in ? st.in | (1u << q) : st.in & ~(1u << q);
+        }
+    }
+#define KIS(lit) k_is(t, lit, sizeof(lit) - 1)
+    __device__ void key(int d, const JTok& t) {
+        const uint8_t c = ctx(d);
+        next = N_NONE;
+        if (c == N_NONE) return;
+        if (c == N_ANN || c == N_LAB) {  // a label / annotation entry
+            const bool ann = c == N_ANN;
+            (ann ? n_ann : n_lab)++;
+            next = ann ? N_ANNV : N_LABV;
+            const JsonSel* M = man_sel(ann);
+            const JsonSel* D = ann ? &cfg->dis_ann : &cfg->dis_lab;
+            const bool any = (M && M->set && M->nreq) || (D->set && D->nreq);
+            km_man = km_dis = 0;
+            if (!any) return;
+            if (t.esc) {
+                host = true;
+                return;
+            }
+            km_man = key_reqs(M, t);
+            km_dis = key_reqs(D, t);
+            return;
+        }
+        if (t.esc) {  // a routed key whose decoded text the scan does not compare
+            if (c == N_ROOT || c == N_META || c == N_STATUS || c == N_INFO) host = true;
+            return;
+        }
+        switch (c) {
+            case N_ROOT:
+                if (KIS("metadata")) next = first(seen_root, 0, N_META);
+                else if (KIS("status") && !skip_status) next = first(seen_root, 1, N_STATUS);
+                break;
+            case N_META:
+                if (KIS("name")) next = first(seen_meta, 0, N_NAME);
+                else if (KIS("annotations")) next = first(seen_meta, 1, N_ANN);
+                else if (KIS("labels")) next = first(seen_meta, 2, N_LAB);
+                break;
+            case N_STATUS:
+                if (KIS("phase")) next = first(seen_status, 0, N_PHASE);
+                else if (KIS("addresses")) next = first(seen_status, 1, N_ADDR);
+                else if (KIS("allocatable")) next = first(seen_status, 2, N_ALLOC);
+                else if (KIS("capacity")) next = first(seen_status, 3, N_CAP);
+                else if (KIS("nodeInfo")) next = first(seen_status, 4, N_INFO);
+                break;
+            case N_ALLOC:
+            case N_CAP:
+                host = true;  // a non-empty blob: its canonical form is the host codec's
+                break;
+            case N_INFO: {  // codec.cpp nik[], KWOK_NI_* order
+#define NI(i, lit) else if (KIS(lit)) { next = first(seen_info, i, N_INFOV); info_k = i; }
+                if (false) {}
+                NI(0, "architecture") NI(1, "bootID") NI(2, "containerRuntimeVersion") NI(3, "kernelVersion")
+                NI(4, "kubeProxyVersion") NI(5, "kubeletVersion") NI(6, "machineID") NI(7, "operatingSystem")
+                NI(8, "osImage") NI(9, "systemUUID")
+#undef NI
+                break;
+            }
+            default:
+                break;
+        }
+    }
+#undef KIS
+    __device__ uint8_t value_ctx(int d, bool pa) const { return d == 0 ? N_ROOT : pa ? N_NONE : next; }
+    __device__ void ref(const JTok& t, Span& out) {  // codec.cpp ref
+        if (t.kind == J_NULL) return;
+        if (t.kind != J_STR || t.esc) {
+            err = KWOK_EDOMAIN;
+            return;
+        }
+        if (t.len) out = Span{(uint32_t)t.off, t.len};
+    }
+    __device__ void scalar(int d, const JTok& t, bool pa) {
+        const uint8_t c = value_ctx(d, pa);
+        if (d == 0) return;
+        if (pa && ctx(d - 1) == N_ADDR) host = true;  // a non-empty addresses list (canonical: the host codec's)
+        switch (c) {
+            case N_META: err = KWOK_EDOMAIN; break;  // metadata must be an object (null included)
+            case N_NAME: ref(t, name); break;
+            case N_ANN:
+            case N_LAB:
+                if (t.kind != J_NULL) err = KWOK_EDOMAIN;  // a label map: an object or null
+                break;
+            case N_ANNV:
+            case N_LABV: {
+                if (t.kind != J_STR) {
+                    err = KWOK_EDOMAIN;  // label / annotation values are strings
+                    break;
+                }
+                if (!km_man && !km_dis) break;
+                if (t.esc) {
+                    host = true;
+                    break;
+                }
+                const bool ann = c == N_ANNV;
+                if (km_man) sel_value(man_sel(ann), man, km_man, t);
+                if (km_dis) sel_value(ann ? &cfg->dis_ann : &cfg->dis_lab, ann ? dis_a : dis_l, km_dis, t);
+                break;
+            }
+            case N_PHASE:
+                if (t.kind == J_STR) {
+                    if (t.esc) host = true;
+                    else phase = !t.len ? KWOK_PHASE_NONE : lit_eq(*r, t.off, t.len, "Running") ? KWOK_PHASE_RUNNING
+                                                                                                 : KWOK_PHASE_OTHER;
+                }
+                break;
+            case N_ADDR:
+            case N_ALLOC:
+            case N_CAP:
+                if (t.kind != J_NULL) err = KWOK_EDOMAIN;  // the wrong type
+                break;
+            case N_INFOV: ref(t, info[info_k]); break;
+            default: break;
+        }
+    }
+    __device__ void begin(int d, bool a, bool pa) {
+        const uint8_t c = value_ctx(d, pa);
+        uint8_t mine = N_NONE;
+        if (d == 0) {
+            root_obj = !a;
+            set_ctx(0, a ? N_NONE : N_ROOT);
+            return;
+        }
+        if (pa && ctx(d - 1) == N_ADDR) host = true;
+        switch (c) {
+            case N_META: if (a) err = KWOK_EDOMAIN; else mine = N_META, meta_obj = true; break;
+            case N_STATUS: if (!a) mine = N_STATUS; break;  // (a status that is no object is ignored)
+            case N_NAME: case N_ANNV: case N_LABV: case N_INFOV: err = KWOK_EDOMAIN; break;  // strings
+            case N_ANN: case N_LAB: if (a) err = KWOK_EDOMAIN; else mine = c; break;
+            case N_ADDR: if (!a) err = KWOK_EDOMAIN; else mine = c; break;
+            case N_ALLOC: case N_CAP: if (a) err = KWOK_EDOMAIN; else mine = c; break;
+            case N_INFO: if (!a) mine = N_INFO; break;  // (ignored unless an object)
+            default: break;
+        }
+        set_ctx(d, mine);
+    }
+    __device__ void end(int, bool, bool) {}  // (a blob was listed at its first member; an empty one is absent)
+    __device__ bool matches(const JsonSel& S, const SelState& st) const {
+        for (uint32_t q = 0; q < S.nreq; q++) {
+            const bool has = (st.has >> q) & 1, in = (st.in >> q) & 1;
+            switch (S.op[q]) {
+                case JREQ_IN: if (!in) return false; break;
+                case JREQ_NOTIN: if (in) return false; break;
+                case JREQ_EXISTS: if (!has) return false; break;
+                default: if (has) return false; break;
+            }
+        }
+        return true;
+    }
+};
+
+// one thread per node document; op[i]: the caller's watch event (the record's op)
+__global__ __launch_bounds__(256) void k_json_nodes(JsonNodeArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint64_t off = A.doc_off[i];
+    const uint32_t len = A.doc_len[i];
+    kwok_node_event ev;
+    ev.op = A.op[i];
+    ev.managed = ev.lockable = 0;
+    ev.phase = KWOK_PHASE_NONE;
+    ev.name = ev.addresses = ev.allocatable = ev.capacity = kwok_str{0, 0};
+    for (int k = 0; k < KWOK_NI_COUNT; k++) ev.node_info[k] = kwok_str{0, 0};
+    int32_t status;
+    NodeScan p;
+    for (int k = 0; k < KWOK_NI_COUNT; k++) p.info[k] = Span{0, 0};
+    if (off > A.arena_len || len > A.arena_len - off) {
+        status = KWOK_EINVAL;  // (codec.cpp parse_doc: a span outside the arena)
+    } else if (A.cfg->all_host) {
+        status = JSON_HOST;
+    } else {
+        JRd rd{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
+        p.r = &rd;
+        p.cfg = A.cfg;
+        p.skip_status = ev.op == KWOK_OP_DELETE;
+        const bool ok = jparse(rd, p);
+        // (a document the scan routed past an escaped key may hold errors the host's
+        // first-key lookup does not see: the host decides it, errors included)
+        if (!ok || !p.root_obj) status = KWOK_EDOMAIN;
+        else if (p.host) status = JSON_HOST;
+        else if (p.err) status = p.err;
+        else if (!p.meta_obj || !p.name.len) status = KWOK_EDOMAIN;
+        else status = KWOK_OK;
+        if (status == KWOK_OK) {
+            const JsonCfg& C = *A.cfg;
+            ev.managed = C.manage_all ? 1 : C.man_ann.set ? (p.matches(C.man_ann, p.man) ? 1 : 0)
+                                                           : (C.man_lab.set && p.matches(C.man_lab, p.man) ? 1 : 0);
+            const bool disregard = (C.dis_ann.set && p.n_ann && p.matches(C.dis_ann, p.dis_a)) ||
+                                   (C.dis_lab.set && p.n_lab && p.matches(C.dis_lab, p.dis_l));
+            ev.lockable = disregard ? 0 : 1;
+            ev.phase = p.phase;
+            ev.name = kwok_str{p.name.off, p.name.len};
+            for (int k = 0; k < KWOK_NI_COUNT; k++) ev.node_info[k] = kwok_str{p.info[k].off, p.info[k].len};
+        }
+    }
+    if (status != KWOK_OK) ev.op = 0xFF;  // (not applied: the host completes it, or its status is the decode's)
+    A.ev[i] = ev;
+    A.status[i] = status;
+    if (status == JSON_HOST) A.host_list[atomicAdd(A.n_host, 1u)] = A.base + i;
+}
+
+void launch_json_nodes(const JsonNodeArgs& A, hipStream_t st) {
+    if (!A.n) return;
+    hipLaunchKernelGGL(k_json_nodes, dim3((A.n + 255) / 256), dim3(256), 0, st, A);
+}
+
+// node records of a batch gathered for the host (list[k] -> out[k]) / written back (in[k] -> list[k])
+__global__ void k_node_gather(const kwok_node_event* ev, const uint32_t* list, uint32_t n, kwok_node_event* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) out[k] = ev[list[k]];
+}
+__global__ void k_node_scatter(kwok_node_event* ev, const kwok_node_event* in, const uint32_t* list, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) ev[list[k]] = in[k];
+}
+void launch_node_gather(const kwok_node_event* ev, const uint32_t* list, uint32_t n, kwok_node_event* out, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_node_gather, dim3((n + 255) / 256), dim3(256), 0, st, ev, list, n, out);
+}
+void launch_node_scatter(kwok_node_event* ev, const kwok_node_event* in, const uint32_t* list, uint32_t n, hipStream_t st) {
+    if (n) hipLaunchKernelGGL(k_node_scatter, dim3((n + 255) / 256), dim3(256), 0, st, ev, in, list, n);
 }
 
 }  // namespace kwok

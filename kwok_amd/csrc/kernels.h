@@ -252,6 +252,24 @@ struct JsonPodArgs {
     uint32_t* n_host;            // [1] (zeroed by the caller)
 };
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st);
+// one thread per node document (kwok_ingest_nodes_json)
+struct JsonNodeArgs {
+    const uint8_t* arena;        // the documents (16 bytes of padding past arena_len)
+    uint64_t arena_len;
+    const uint64_t* doc_off;
+    const uint32_t* doc_len;
+    const uint8_t* op;           // the caller's watch event per document (the record's op)
+    uint32_t n;
+    const JsonCfg* cfg;
+    kwok_node_event* ev;         // [n] out (op 0xFF: not applied - listed for the host, or a failed decode)
+    int32_t* status;             // [n] out: KWOK_OK / KWOK_EDOMAIN / KWOK_EINVAL / JSON_HOST
+    uint32_t* host_list;         // [n] out: documents the host codec decodes (JSON_HOST), as base + index
+    uint32_t* n_host;            // [1] (zeroed by the caller)
+    uint32_t base;               // the batch index of document 0 of this launch (a piece of the batch)
+};
+void launch_json_nodes(const JsonNodeArgs& A, hipStream_t st);
+void launch_node_gather(const kwok_node_event* ev, const uint32_t* list, uint32_t n, kwok_node_event* out, hipStream_t st);
+void launch_node_scatter(kwok_node_event* ev, const kwok_node_event* in, const uint32_t* list, uint32_t n, hipStream_t st);
 void launch_json_gather(const kwok_pod_event* ev, const JsonPodSide* side, const uint32_t* list, uint32_t n,
                         kwok_pod_event* out_ev, JsonPodSide* out_side, hipStream_t st);
 void launch_json_scatter(kwok_pod_event* ev, const kwok_pod_event* in, const uint32_t* list, uint32_t n, hipStream_t st);

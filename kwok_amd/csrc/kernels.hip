@@ -1619,6 +1619,13 @@ __device__ __forceinline__ void hb_fill_groups(const DevState& S, const uint4* t
 // static shares of the heartbeat stream: the streamer blocks split the first
 // stream_share/1024 of it, and every chain block writes an equal slice of the
 // rest once its own work is done (so the stream's tail overlaps nothing idle)
+// a chain block's slice of the stream is not empty (block-uniform; heartbeat-once
+// engines have no streamers: one chain block writes the one body)
+__device__ __forceinline__ bool hb_share_any(const DevState& S, uint64_t n_hb, uint32_t idx, uint32_t cnt) {
+    const uint64_t groups = (n_hb + HB_GROUP_SLOTS - 1) / HB_GROUP_SLOTS;
+    const uint64_t cut = groups * S.stream_share / 1024, n = groups - cut;
+    return n * idx / cnt < n * (idx + 1) / cnt;
+}
 template <bool GEN>
 __device__ __forceinline__ void hb_fill_share(const DevState& S, const uint4* tmpl, uint64_t n_hb, bool streamer,
                                               uint32_t idx, uint32_t cnt) {
@@ -2348,8 +2355,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
             TSTAMP(3);
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
             TSTAMP(12);
-            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {  // this block's slice of the stream
-                build_hb_template(S, hb_tmpl, now_unix, start_unix);
+            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM) && hb_share_any(S, hb_bodies(S, n_hb), b, S.n_chain)) {
+                build_hb_template(S, hb_tmpl, now_unix, start_unix);  // (this block's slice of the stream)
                 hb_fill_share<GEN_HB>(S, hb_tmpl4, hb_bodies(S, n_hb), false, b, S.n_chain);
             }
             TSTAMP(13);
@@ -2398,7 +2405,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
                 TSTAMP(7);
             }
             write_hb_handles(S, nflags32, nbase, nn, hb_base);
-            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM)) {
+            if (S.stream_share < 1024 && !(phases & TICK_NOSTREAM) && hb_share_any(S, hb_bodies(S, n_hb), b, S.n_chain)) {
                 build_hb_template(S, hb_tmpl, now_unix, start_unix);
                 hb_fill_share<GEN_HB>(S, hb_tmpl4, hb_bodies(S, n_hb), false, b, S.n_chain);
             }

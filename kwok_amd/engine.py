@@ -108,6 +108,8 @@ def declare(lib, pre):
             "decode_pods_gpu": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, SZ, VP, VP, VP, VP, P(SZ)]),
             "ingest_pods_json": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, VP, VP, SZ, VP, VP, VP, P(SZ)]),
             "read_arena_async": (C.c_int, [VP, U64, U64, VP]),
+            "ingest_nodes_json": (C.c_int, [VP, VP, C.c_char_p, SZ, VP, VP, VP, SZ, VP, VP, P(SZ)]),
+            "decode_nodes_gpu": (C.c_int, [VP, VP, VP, SZ, VP, VP, SZ, VP, VP, P(SZ)]),
             "read_wait": (C.c_int, [VP]),
         })
     for name, (res, args) in sig.items():
@@ -493,6 +495,41 @@ class Engine(EngineBase):
                                             C.byref(nh))
         self._check(rc, "decode_pods_gpu")
         return ev, names, keys, st, nh.value
+
+    def ingest_nodes_json(self, codec, arena, offs, lens, ops, out=None):
+        """kwok_ingest_nodes_json: (handles, statuses, documents the host decided)"""
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        ops = np.ascontiguousarray(ops, np.uint8)
+        n = len(offs)
+        if out is None:
+            hs, st = np.empty(n, np.int32), np.empty(n, np.int32)
+        else:
+            hs, st = (o[:n] for o in out)
+        nh = C.c_size_t()
+        ar, alen = self._arena_arg(arena)
+        rc = self._lib.kwok_ingest_nodes_json(self._h, codec._h, ar, alen, offs.ctypes.data, lens.ctypes.data,
+                                              ops.ctypes.data, n, hs.ctypes.data, st.ctypes.data, C.byref(nh))
+        self._check(rc, "ingest_nodes_json")
+        return hs, st, nh.value
+
+    def decode_nodes_gpu(self, codec, docs=None, arena=None, offs=None, lens=None):
+        """kwok_decode_nodes_gpu: per document its kwok_node_event (NODE_EVENT_DTYPE) and
+        status, the number the host decided, and the arena (the host codec rewrites the
+        listed documents' blobs in place).  Documents as a list, or as (arena, offs, lens)."""
+        if docs is not None:
+            arena, offs, lens = self._docs(docs)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n = len(offs)
+        buf = np.frombuffer(bytearray(bytes(arena) + b"\0"), np.uint8)
+        ev = np.zeros(n, abi.NODE_EVENT_DTYPE)
+        st = np.zeros(n, np.int32)
+        nh = C.c_size_t()
+        rc = self._lib.kwok_decode_nodes_gpu(self._h, codec._h, buf.ctypes.data, len(arena), offs.ctypes.data,
+                                             lens.ctypes.data, n, ev.ctypes.data, st.ctypes.data, C.byref(nh))
+        self._check(rc, "decode_nodes_gpu")
+        return ev, st, nh.value, bytes(buf[:len(arena)])
 
     def ingest_pods_json(self, codec, arena, offs, lens, ops, handles, out=None):
         """kwok_ingest_pods_json: (handles, statuses, released, documents the host decided)"""

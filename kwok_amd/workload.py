@@ -329,6 +329,54 @@ class Flap:
         return evp, ar
 
 
+    # the node documents a watch carries for a flap (batch_json): the Deleted event holds the
+    # node as kwok patched it (node.status.tpl's init patch: addresses, allocatable, capacity,
+    # nodeInfo, phase, conditions), the Added event a Node created again with a zero status
+    # (json.Marshal of corev1.Node: daemonEndpoints and the ten nodeInfo strings always present)
+    _NI_ZERO = (b'"nodeInfo":{"machineID":"","systemUUID":"","bootID":"","kernelVersion":"","osImage":"",'
+                b'"containerRuntimeVersion":"","kubeletVersion":"","kubeProxyVersion":"","operatingSystem":"",'
+                b'"architecture":""}')
+    _DEL_STATUS = (b'"status":{"capacity":{"cpu":"1k","memory":"1Ti","pods":"1M"},'
+                   b'"allocatable":{"cpu":"1k","memory":"1Ti","pods":"1M"},"conditions":[{"type":"Ready",'
+                   b'"status":"True","lastHeartbeatTime":"2024-01-01T00:00:00Z","lastTransitionTime":'
+                   b'"2024-01-01T00:00:00Z","reason":"KubeletReady","message":"kubelet is posting ready status"}],'
+                   b'"addresses":[{"type":"InternalIP","address":"196.168.0.1"}],"daemonEndpoints":'
+                   b'{"kubeletEndpoint":{"Port":0}},"nodeInfo":{"machineID":"","systemUUID":"","bootID":"",'
+                   b'"kernelVersion":"","osImage":"","containerRuntimeVersion":"","kubeletVersion":"fake",'
+                   b'"kubeProxyVersion":"fake","operatingSystem":"linux","architecture":"amd64"},"phase":"Running"}')
+
+    def _doc(self, name, lockable, deleted, serial):
+        ann = b'"kwok.x-k8s.io/node":"fake"' + (b'' if lockable else b',"kwok.x-k8s.io/status":"custom"')
+        md = (b'"metadata":{"name":"' + name + b'","uid":"7d3c0e9a-0000-4000-8000-%012d",' % serial +
+              b'"resourceVersion":"%d","creationTimestamp":"2024-01-01T00:00:00Z","annotations":{' % (1000 + serial) +
+              ann + b'}}')
+        st = self._DEL_STATUS if deleted else b'"status":{"daemonEndpoints":{"kubeletEndpoint":{"Port":0}},' + \
+            self._NI_ZERO + b'}'
+        return b'{"kind":"Node","apiVersion":"v1",' + md + b',"spec":{},' + st + b'}'
+
+    def batch_json(self):
+        """the same batch as batch() (k Deleted, then k Added), as the watch's node
+        documents: (arena, offs, lens, ops, events) - events: batch()'s records"""
+        pick = self.rng.choice(self.idx, self.k, replace=False)
+        src = self.fleet.node_events[pick]
+        names = self.fleet.names[pick]
+        docs = []
+        serial = getattr(self, "serial", 0)
+        for deleted in (True, False):
+            for q in range(self.k):
+                docs.append(self._doc(names[q].tobytes(), bool(src["lockable"][q]), deleted, serial))
+                serial += 1
+        self.serial = serial
+        lens = np.fromiter((len(d) for d in docs), np.uint32, len(docs))
+        offs = np.zeros(len(docs), np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        ops = np.full(len(docs), abi.OP_UPSERT, np.uint8)
+        ops[:self.k] = abi.OP_DELETE
+        ev = np.concatenate([src, src])
+        ev["op"][:self.k] = abi.OP_DELETE
+        return b"".join(docs), offs, lens, ops, ev
+
+
 # ---- the C4 storm as the documents a watch carries (kwok_ingest_pods_json) ----
 def rfc3339_rows(t: np.ndarray) -> np.ndarray:
     """RFC3339 UTC strings of unix seconds as a (n, 20) uint8 array"""

@@ -49,6 +49,7 @@ def test_oracle_library_exports():
                  "kwok_read_arena_async", "kwok_read_wait",  # engine only: reads overlapping the next tick
                  "kwok_engine_stats",  # engine only: which tick kernel ran
                  "kwok_spec_key", "kwok_decode_pods_gpu", "kwok_ingest_pods_json",  # the GPU codec (engine library)
+                 "kwok_ingest_nodes_json", "kwok_decode_nodes_gpu",
                  "kwok_codec_create", "kwok_codec_destroy", "kwok_codec_last_error", "kwok_selector_matches",
                  "kwok_decode_node", "kwok_decode_pod", "kwok_decode_nodes", "kwok_decode_pods",  # host codec: feeds both, lives in the engine library
                  "kwok_template_render", "kwok_template_last_error", "kwok_pod_template_patch",
