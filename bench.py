@@ -663,7 +663,9 @@ def flap_json(e, f, now, ticks):
     for k in range(ticks + 1):
         now += 30
         arena, offs, lens, ops, _ = f.batch_json()
-        arena = np.frombuffer(arena, np.uint8).copy()
+        ap = keng.host_array((len(arena),), np.uint8)  # (page-locked, as the Go shim stages the documents)
+        ap[:] = np.frombuffer(arena, np.uint8)
+        arena = ap
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         hs, st, nh = e.ingest_nodes_json(codec, arena, offs, lens, ops)
@@ -680,7 +682,7 @@ def flap_json(e, f, now, ticks):
     return {"ms_per_step": (ing + tck) / ticks * 1e3, "decode_ingest_ms": ing / ticks * 1e3, "tick_ms": tck / ticks * 1e3,
             "documents_per_tick": docs // ticks, "json_bytes_per_tick": nbytes // ticks,
             "documents_decided_by_host": n_host,
-            "note": "kwok_ingest_nodes_json: the documents (pageable) copied to HBM, k_json_nodes (one thread per "
+            "note": "kwok_ingest_nodes_json: the documents (page-locked) copied to HBM, k_json_nodes (one thread per "
                     "document), kwok_ingest_nodes' GPU event switch over the records"}
 
 

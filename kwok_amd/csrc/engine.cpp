@@ -168,6 +168,11 @@ struct kwok_engine {
     hipStream_t st = nullptr;   // tick pipeline
     hipEvent_t fence = nullptr; // recorded (system-scope release) before device -> host copies of kernel output
     hipStream_t rst = nullptr;  // kwok_read_outputs: copies of a collected tick, beside the next tick's kernels
+    // large arena reads split over more copy streams (KWOK_READ_STREAMS, default 1: two or
+    // four streams measured no faster than one, ~44 GB/s device-to-host either way)
+    int read_streams = 1;
+    hipStream_t rsx[3] = {};
+    hipEvent_t rd_go = nullptr, rd_part[3] = {};
     DevState S{};
 
     // ---- nodes: the directory (names -> slots), occupancy, managed / zombie counts
@@ -1086,6 +1091,11 @@ void kwok_engine_destroy(kwok_engine* e) {
     }
     if (e->st) (void)hipStreamSynchronize(e->st);
     if (e->rst) (void)hipStreamSynchronize(e->rst);  // (asynchronous arena reads)
+    for (int i = 0; i < 3; i++) {
+        if (e->rsx[i]) (void)hipStreamSynchronize(e->rsx[i]), (void)hipStreamDestroy(e->rsx[i]);
+        if (e->rd_part[i]) (void)hipEventDestroy(e->rd_part[i]);
+    }
+    if (e->rd_go) (void)hipEventDestroy(e->rd_go);
     void* ptrs[] = {e->S.trace, e->S.jtrace, e->S.once_sum, e->S.node_state, e->S.node_blob, e->S.node_tick, e->S.pod_state, e->S.pod_node, e->S.pod_spec,
                     e->S.pod_ctime, e->S.pod_ip, e->S.host_ip, e->S.used_bm, e->S.usable_bm, e->S.pool_index,
                     e->S.pool_blk, e->S.alloc_addr, e->S.rel_bm, e->S.list_counts, (void*)e->S.hb_static,
@@ -1295,6 +1305,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
         e->quiet_ok = !(qt && qt[0] == '0');
         const char* sj = getenv("KWOK_SPLIT");
         e->split_jobs = !(sj && sj[0] == '0');
+        if (const char* v = getenv("KWOK_READ_STREAMS")) e->read_streams = std::max(1, std::min(4, atoi(v)));
         const char* sj2 = getenv("KWOK_SPARSE_JOBS");  // 0: k_pod_jobs<false> re-classifies the runs (A/B)
         e->sparse_jobs = !(sj2 && sj2[0] == '0');
         const char* fe = getenv("KWOK_FUSE_EMIT");
@@ -1342,7 +1353,7 @@ int kwok_engine_create(const kwok_config* cfg, kwok_engine** out) {
                                 "(%d buckets, %d node slots, %d pod groups): shard over more GPUs",
                                 bpb, e->Cn, e->Cp, MAX_BPB, NODE_LDS, MAX_POD_CHUNKS * BLOCK));
     }
-    const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * POOL_WPT - 1) / (BLOCK * POOL_WPT));
+    const uint32_t nblk = (uint32_t)((e->pool.words + BLOCK * POOL_WPT_MIN - 1) / (BLOCK * POOL_WPT_MIN));
     // node / pod arrays: whole 16-byte vectors at the end (Cn % 4 == 0, Cp % 8 == 0)
     const size_t NLa = (size_t)e->NL + 16, PLa = (size_t)e->PL + 16;
     e->NLa = NLa;
@@ -3092,6 +3103,32 @@ void trace_tick(kwok_engine* e) {
     for (int k = 0; k < TRACE_SLOTS; k++) summarise(0, G, k, e->trace_sum[k]);
     summarise(G, N, 0, e->trace_sum[TRACE_SLOTS]);
     summarise(G, N, 6, e->trace_sum[TRACE_SLOTS + 1]);
+    if (getenv("KWOK_TICK_TRACE_SLOW")) {  // per XCC: median / max pods-done and arrival; the slowest blocks
+        std::vector<double> pd[16], ar[16];
+        std::vector<std::pair<double, size_t>> slow;
+        for (size_t b = 0; b < G; b++) {
+            const uint64_t* T = &e->trace_h[b * TS];
+            if (T[2] < t0 || T[3] < t0) continue;
+            const uint32_t x = (uint32_t)(T[21] >> 28) & 15u;
+            pd[x].push_back((double)(T[2] - t0) * 0.01);
+            ar[x].push_back((double)(T[3] - t0) * 0.01);
+            slow.emplace_back((double)(T[3] - t0) * 0.01, b);
+        }
+        for (int x = 0; x < 16; x++) {
+            if (pd[x].empty()) continue;
+            std::sort(pd[x].begin(), pd[x].end());
+            std::sort(ar[x].begin(), ar[x].end());
+            fprintf(stderr, "[kwok trace xcc %d] blocks %zu pods-done %.1f / %.1f arrived %.1f / %.1f\n", x, pd[x].size(),
+                    pd[x][pd[x].size() / 2], pd[x].back(), ar[x][ar[x].size() / 2], ar[x].back());
+        }
+        std::sort(slow.rbegin(), slow.rend());
+        for (size_t q = 0; q < std::min<size_t>(8, slow.size()); q++) {
+            const uint64_t* T = &e->trace_h[slow[q].second * TS];
+            fprintf(stderr, "[kwok trace slow] block %zu hw %08llx nodes %.1f pods %.1f sum %.1f drained %.1f arrived %.1f\n",
+                    slow[q].second, (unsigned long long)T[21], (double)(T[1] - t0) * 0.01, (double)(T[2] - t0) * 0.01,
+                    (double)(T[10] - t0) * 0.01, (double)(T[11] - t0) * 0.01, (double)(T[3] - t0) * 0.01);
+        }
+    }
     if (getenv("KWOK_TICK_TRACE_RAW")) {  // the last block's 16 stamps (ad-hoc kernel probes), us after t0
         fprintf(stderr, "[kwok trace raw]");
         for (size_t k = 0; k < TS; k++) {
@@ -3484,6 +3521,33 @@ void kwok_host_free(void* p) {
     }
 }
 
+// dst <- src (len bytes) on the read stream (after its fence), a large read in
+// parts over the extra read streams, joined back on the read stream
+int read_copy(kwok_engine* e, void* dst, const uint8_t* src, uint64_t len) {
+    const int ns = len >= (16ull << 20) ? std::max(1, std::min(e->read_streams, 4)) : 1;
+    if (ns > 1) {
+        if (!e->rd_go) HIPCHK(e, hipEventCreateWithFlags(&e->rd_go, hipEventDisableTiming));
+        for (int i = 0; i < ns - 1; i++) {
+            if (!e->rsx[i]) HIPCHK(e, hipStreamCreateWithFlags(&e->rsx[i], hipStreamNonBlocking));
+            if (!e->rd_part[i]) HIPCHK(e, hipEventCreateWithFlags(&e->rd_part[i], hipEventDisableTiming));
+        }
+        HIPCHK(e, hipEventRecord(e->rd_go, e->rst));
+    }
+    const uint64_t step = ((len + ns - 1) / ns + 4095) & ~4095ull;
+    for (int i = ns - 1; i >= 0; i--) {
+        const uint64_t lo = std::min<uint64_t>(len, step * i), hi = std::min<uint64_t>(len, step * (i + 1));
+        if (hi <= lo) continue;
+        hipStream_t s = i ? e->rsx[i - 1] : e->rst;
+        if (i) HIPCHK(e, hipStreamWaitEvent(s, e->rd_go, 0));
+        HIPCHK(e, hipMemcpyAsync(static_cast<uint8_t*>(dst) + lo, src + lo, hi - lo, hipMemcpyDeviceToHost, s));
+        if (i) {
+            HIPCHK(e, hipEventRecord(e->rd_part[i - 1], s));
+            HIPCHK(e, hipStreamWaitEvent(e->rst, e->rd_part[i - 1], 0));
+        }
+    }
+    return KWOK_OK;
+}
+
 int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {
     if (!e || (len && !dst)) return KWOK_EINVAL;
     if (e->poisoned) return poisoned(e);
@@ -3497,7 +3561,7 @@ int kwok_read_arena(kwok_engine* e, uint64_t off, uint64_t len, void* dst) {
     hipStream_t st = e->rst;  // beside a tick queued behind the collected one (as kwok_read_outputs)
     HIPCHK(e, hipStreamWaitEvent(st, S.done, 0));
     HIPCHK(e, hipEventRecord(e->fence, st));
-    HIPCHK(e, hipMemcpyAsync(dst, S.arena + off, len, hipMemcpyDeviceToHost, st));
+    if (int rc = read_copy(e, dst, S.arena + off, len)) return rc;
     HIPCHK(e, hipStreamSynchronize(st));
     return KWOK_OK;
 }
@@ -3522,7 +3586,7 @@ int kwok_read_arena_async(kwok_engine* e, uint64_t off, uint64_t len, void* dst)
         return e->fail(KWOK_EDEVICE, "event create");
     HIPCHK(e, hipStreamWaitEvent(st, S.done, 0));
     HIPCHK(e, hipEventRecord(e->fence, st));
-    HIPCHK(e, hipMemcpyAsync(dst, S.arena + off, len, hipMemcpyDeviceToHost, st));
+    if (int rc = read_copy(e, dst, S.arena + off, len)) return rc;
     HIPCHK(e, hipEventRecord(S.rd, st));
     S.rd_pending = true;
     return KWOK_OK;

@@ -150,8 +150,13 @@ void launch_cni_pending(const DevState& S, int32_t* out, uint32_t* count, hipStr
 // launches with TICK_FRONT).  Chain blocks wait on each other only in ticks
 // with work to emit, so they must be co-resident (tick_occupancy).
 // pool phase: bitmap words per thread of a word-block (BLOCK * POOL_WPT words; a
-// multi-rank engine takes twice as many, kernels.hip POOL_WPT_MULTI)
-constexpr int POOL_WPT = 4;
+// multi-rank engine takes 8, kernels.hip POOL_WPT_MULTI).  The per-word-block
+// counts (pool_blk) are allocated for POOL_WPT_MIN, the smallest a build uses.
+#ifndef KWOK_POOL_WPT
+#define KWOK_POOL_WPT 2
+#endif
+constexpr int POOL_WPT = KWOK_POOL_WPT;
+constexpr int POOL_WPT_MIN = 1;
 constexpr int TICK_FRONT = 1, TICK_BACK = 2, TICK_PROF = 4, TICK_PRIO = 8, TICK_NOSTREAM = 16,  // NOSTREAM: diagnostics only
               TICK_XLISTS = 32,  // BACK: the exchange lists were applied by k_pool_apply
               TICK_SPLIT = 64,   // the pod jobs are built by k_pod_jobs after the tick's launch(es)

@@ -301,7 +301,8 @@ __device__ __forceinline__ uint64_t cursor_bit(const DevState& S) {
 // engine (the N-rank pool is N times larger: half the passes, twice the loads in
 // flight), POOL_WPT otherwise (a single rank's pool phase runs among its dirty
 // blocks: more, smaller word-blocks keep them all busy)
-constexpr int POOL_WPT_MULTI = 2 * POOL_WPT;
+constexpr int POOL_WPT_MULTI = 8;
+static_assert(POOL_WPT >= POOL_WPT_MIN, "pool_blk is allocated for POOL_WPT_MIN");
 
 // a thread's words of one word-block (pass k: word wb * POOL_WPB + k * BLOCK +
 // thread), as the prep pass left them: the select pass of the same block takes
@@ -2042,6 +2043,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_tick(DevState S, uint64_t now_unix
         }                                                            \
     } while (0)
     TSTAMP(0);
+    if (S.trace && t == 0)  // (diagnostics: where the block runs - HW_ID, XCC_ID << 28)
+        S.trace[(size_t)b * TRACE_SLOTS + 21] = (uint64_t)__builtin_amdgcn_s_getreg((4) | (15 << 11)) |
+                                                (uint64_t)(__builtin_amdgcn_s_getreg((20) | (15 << 11)) & 15u) << 28;
 
     // ---- heartbeat streamers ------------------------------------------------------
     // (a multi-rank BACK launch's blocks past the chain blocks are pool-only blocks)
@@ -3903,10 +3907,25 @@ __global__ __launch_bounds__(64 * JOB_WAVES, JOBS_MIN_WAVES) void k_pod_jobs(Dev
 // ---------------------------------------------------------------------------
 constexpr int SJ_WAVES = 4;
 __global__ __launch_bounds__(64 * SJ_WAVES, 4) void k_sparse_jobs(DevState S, uint32_t tag, uint32_t blocks_per_chain) {
+    // the specs' patch lengths / reservations (len << 16 | max_len), loaded with the
+    // first round trip into the wave's LDS: a patch's spec is then no dependent load
+    __shared__ uint32_t spec_lm_w[SJ_WAVES][SPEC_LDS];
+    const bool spec_lds = S.n_specs <= (uint32_t)SPEC_LDS;
     const uint32_t b = blockIdx.x / blocks_per_chain;
     const uint32_t c = (blockIdx.x - b * blocks_per_chain) * SJ_WAVES + (uint32_t)wave_id();  // the wave's run
     if (b >= S.n_chain || c >= (uint32_t)MAX_WC) return;
     const int l = lane_id();
+    uint32_t* spec_lm = spec_lm_w[wave_id()];
+    uint32_t spw_l[SPEC_LDS / 64];
+#pragma unroll
+    for (int q = 0; q < SPEC_LDS / 64; q++) {
+        const uint32_t i = (uint32_t)(l + 64 * q);
+        spw_l[q] = 0;
+        if (spec_lds && i < S.n_specs) {
+            const SpecDesc& sd = S.specs[i];
+            spw_l[q] = ((uint32_t)sd.len_a + sd.len_b + sd.len_c) << 16 | sd.max_len;
+        }
+    }
     // round trip 1 (all independent): the block's bases, the run's dirty bit and prefix, its groups
     const JobBase* JB = S.jbase + b;
     const uint32_t jtag = JB->tag;
@@ -3949,6 +3968,9 @@ __global__ __launch_bounds__(64 * SJ_WAVES, 4) void k_sparse_jobs(DevState S, ui
         const uint64_t o = o_alloc + (uint32_t)k;
         areuse[k] = ((uint32_t)k < n_alloc && alloc_base + o < take + fin) ? S.alloc_addr[o] : 0u;
     }
+#pragma unroll
+    for (int q = 0; q < SPEC_LDS / 64; q++) spec_lm[l + 64 * q] = spw_l[q];
+    __builtin_amdgcn_wave_barrier();  // (one wave's LDS operations complete in order)
     if (!valid) return;
     const uint32_t stw[4] = {st4.x, st4.y, st4.z, st4.w}, spw[4] = {sp4.x, sp4.y, sp4.z, sp4.w};
     const uint32_t ctm[POD_PER_THREAD] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
@@ -3956,9 +3978,15 @@ __global__ __launch_bounds__(64 * SJ_WAVES, 4) void k_sparse_jobs(DevState S, ui
     const uint32_t ip0[POD_PER_THREAD] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
     auto st_of = [&](int k) { return (uint16_t)(stw[k >> 1] >> (16 * (k & 1))); };
     auto sp_of = [&](int k) { return (uint16_t)(spw[k >> 1] >> (16 * (k & 1))); };
-    // the spec lengths (one descriptor when the group's patched pods share a spec, the usual case)
+    // the spec lengths (LDS; else one descriptor when the group's patched pods share a spec)
     uint32_t sd_len[POD_PER_THREAD], sd_max[POD_PER_THREAD];
-    {
+    if (spec_lds) {
+#pragma unroll
+        for (int k = 0; k < POD_PER_THREAD; k++) {
+            const uint32_t lm = (nm >> k) & 1u ? spec_lm[sp_of(k)] : 0u;
+            sd_len[k] = lm >> 16, sd_max[k] = lm & 0xFFFFu;
+        }
+    } else {
         bool one = true;
 #pragma unroll
         for (int k = 0; k < POD_PER_THREAD; k++) one &= !((nm >> k) & 1u) || sp_of(k) == sp_of(__builtin_ctz(nm | 256u) & 7);
