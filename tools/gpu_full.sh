@@ -35,4 +35,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_once_${TAG}_FETCH_SIZE $R/gpurun_out/pmc_once_${TAG}_WRITE_SIZE $R/gpurun_out/pmc_once_${TAG}.json --kernels $R/kwok_amd/csrc/kernels.hip \
   --source "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace (separate passes), tools/once_probe.py 30 (KWOK_CFG_HEARTBEAT_ONCE steady ticks: k_once), 1M nodes x 10M pods, 1x MI355X"
+# the C4 churn tick on the heartbeat-once engine: kernel trace + timeline, FETCH_SIZE / WRITE_SIZE
+bash $R/tools/gpu_c4once.sh $TAG > $R/gpurun_out/c4once_${TAG}_summary.txt 2>&1 || { tail -20 $R/gpurun_out/c4once_${TAG}_summary.txt; exit 11; }
+tail -8 $R/gpurun_out/c4once_${TAG}_summary.txt
 exit 0
