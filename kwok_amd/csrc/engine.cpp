@@ -2412,6 +2412,7 @@ namespace {
 // decode statuses into dstat, the number listed for the host (json.host_list) in *nh
 int json_nodes_decode(kwok_engine* e, const kwok_codec* c, const char* arena, size_t arena_len, const uint64_t* doc_off,
                       const uint32_t* doc_len, const uint8_t* op, size_t n, std::vector<int32_t>& dstat, uint32_t* nh) {
+    const auto t0 = clk::now();
     int rc = node_reserve(e, n, arena_len + 16);  // (the scanner reads whole 16-byte windows)
     if (rc) return rc;
     if ((rc = json_reserve(e, n))) return rc;
@@ -2469,11 +2470,15 @@ int json_nodes_decode(kwok_engine* e, const kwok_codec* c, const char* arena, si
         launch_json_nodes(A, st);
         HIPCHK(e, hipGetLastError());
     }
+    const auto tq = clk::now();
     dstat.resize(n);
     HIPCHK(e, hipMemcpyAsync(dstat.data(), J.nstat, n * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipMemcpyAsync(J.n_host_h, J.n_host, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(e, hipStreamSynchronize(st));
     *nh = *J.n_host_h;
+    if (e->iprof)
+        fprintf(stderr, "[kwok json]   %zu node documents: queued %.3f ms, decoded + statuses back %.3f ms\n", n,
+                ms_between(t0, tq), ms_between(tq, clk::now()));
     return KWOK_OK;
 }
 // the documents json_nodes_decode listed, sorted

@@ -35,7 +35,10 @@ namespace kwok {
 namespace {
 
 // ---------------------------------------------------------------------------
-// a document's bytes, read 16 at a time (the arena is 16-aligned and padded)
+// a document's bytes, read 16 at a time (the arena is 16-aligned and padded).
+// A 64-byte window (a quarter of the refills) measured slower: a C5 batch of 10k
+// node documents 0.68 -> 1.01 ms in k_json_nodes - the scan is bound by its
+// per-byte instructions and the lanes' divergent paths, not by the refills
 // ---------------------------------------------------------------------------
 struct JRd {
     const uint8_t* a;
@@ -881,6 +884,12 @@ __device__ bool spec_equal(JRd& r, const PodScan& p, const uint8_t* canon, uint2
 
 }  // namespace
 
+// A batch of fewer documents than the chip has CUs x 4 waves goes one wave per block:
+// each scanning wave reads 64 documents' 16-byte windows (64 lines per load), so
+// waves spread over all CUs share no CU's SIMDs (a 10k-document node batch: 0.82 ms
+// in 40 blocks of 4 waves, 0.68 ms in 157 blocks of one)
+__host__ __device__ inline uint32_t json_block(uint32_t n) { return n < 256u * 64u * 4u ? 64u : 256u; }
+
 // one thread per document
 __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -974,7 +983,8 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
 
 void launch_json_pods(const JsonPodArgs& A, hipStream_t st) {
     if (!A.n) return;
-    hipLaunchKernelGGL(k_json_pods, dim3((A.n + 255) / 256), dim3(256), 0, st, A);
+    const uint32_t bs = json_block(A.n);
+    hipLaunchKernelGGL(k_json_pods, dim3((A.n + bs - 1) / bs), dim3(bs), 0, st, A);
 }
 
 // ---------------------------------------------------------------------------
@@ -1253,7 +1263,8 @@ __global__ __launch_bounds__(256) void k_json_nodes(JsonNodeArgs A) {
 
 void launch_json_nodes(const JsonNodeArgs& A, hipStream_t st) {
     if (!A.n) return;
-    hipLaunchKernelGGL(k_json_nodes, dim3((A.n + 255) / 256), dim3(256), 0, st, A);
+    const uint32_t bs = json_block(A.n);
+    hipLaunchKernelGGL(k_json_nodes, dim3((A.n + bs - 1) / bs), dim3(bs), 0, st, A);
 }
 
 // node records of a batch gathered for the host (list[k] -> out[k]) / written back (in[k] -> list[k])

@@ -263,12 +263,16 @@ def shim_read_check(e, O, res, chunk=64 << 20):
     return pieces, total
 
 
-def compare_tick(e, o, where):
-    E, O = e.read_arrays(), o.read_arrays()
+def compare_tick(e, o, where, once=False):
+    """once: a heartbeat-once engine, whose arena holds the one heartbeat body"""
+    E, O = e.read_arrays(heartbeat_once=once) if once else e.read_arrays(), o.read_arrays()
     assert E["counters"] == O["counters"], where
     assert (E["heartbeat_nodes"] == O["heartbeat_nodes"]).all(), where + " heartbeat handles"
     n = len(E["heartbeat_nodes"])
-    if n:
+    if n and once:
+        body = O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]
+        assert (E["arena"][E["heartbeat_off"]:E["heartbeat_off"] + E["heartbeat_len"]] == body).all(), where
+    elif n:
         body = O["arena"][O["heartbeat_off"]:O["heartbeat_off"] + O["heartbeat_len"]]
         hb = E["arena"][E["heartbeat_off"]:E["heartbeat_off"] + n * E["heartbeat_stride"]]
         hb = hb.reshape(n, E["heartbeat_stride"])[:, :E["heartbeat_len"]]

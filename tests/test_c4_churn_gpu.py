@@ -22,15 +22,19 @@ pytestmark = pytest.mark.gpu
 
 
 def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None,
-              packed=False):
+              packed=False, once=False, shim=False):
     """packed: the engine ingests the compact wire form (kwok_ingest_pods_packed;
     packed=12: kwok_pod_rec12 through kwok_ingest_pods_packed12, which returns the
     creates' handles only), the oracle the same events as kwok_pod_event with
-    dotted quads"""
+    dotted quads.  once: heartbeat-once engines (the drop-in's).  shim: every churn
+    tick is also read back as the Go drop-in reads it (gpu_common.shim_read_check:
+    lists, one heartbeat body, every patch byte in 64 MiB pieces) and compared with
+    the oracle byte for byte"""
+    from gpu_common import shim_read_check
     if threads is not None:
         os.environ["KWOK_INGEST_THREADS"] = str(threads)
     try:
-        e, fl, ph = workload.build_engine_fleet(Engine, nodes, buckets=buckets)
+        e, fl, ph = workload.build_engine_fleet(Engine, nodes, buckets=buckets, heartbeat_once=once)
     finally:
         os.environ.pop("KWOK_INGEST_THREADS", None)
     o, _, ph2 = workload.build_engine_fleet(lambda cfg: Oracle(cfg, threads=0), nodes, buckets=buckets)
@@ -39,7 +43,7 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
     now = workload.S0 + 30
     e.tick(now, read=False)
     o.tick(now, read=False)
-    compare_tick(e, o, "churn initial tick")
+    compare_tick(e, o, "churn initial tick", once)
     ch = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11,
                         alloc=alloc)
     chp = workload.Churn(ph, np.repeat(fl.node_handles, workload.PODS_PER_NODE), 0, n_handles, n_churn, seed=11,
@@ -65,9 +69,12 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
         h2, s2, r2 = o.ingest_pods_raw(ev, ar)
         assert (h1 == h2).all() and (s1 == s2).all() and (r1 == r2).all(), "churn tick %d ingest" % t
         ch.applied(h1, s1)
-        e.tick(now, read=False)
+        res = e.tick(now, read=False)
         o.tick(now, read=False)
-        c = compare_tick(e, o, "churn tick %d" % t)
+        if shim:
+            pieces, nbytes = shim_read_check(e, o.read_arrays(), res)
+            assert nbytes > 0.5e9 or nodes < 1_000_000, nbytes
+        c = compare_tick(e, o, "churn tick %d" % t, once)
         assert (c["delete"], c["release"], c["pod_patch"], c["alloc"]) == (n_churn,) * 4, c
         if full_state or t == ticks - 1:
             compare_state(e, o, n_handles, "churn tick %d" % t)
@@ -110,6 +117,15 @@ def test_c4_churn_metric_size_packed12():
     record and per tick"""
     from kwok_amd.engine import host_array
     run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array)
+
+
+@pytest.mark.timeout(900)
+def test_c4_churn_metric_size_drop_in_read_back():
+    """the drop-in's C4: heartbeat-once engines, kwok_pod_rec12, and every churn
+    tick read back as engine_cgo.go reads it (0.58 GB of patches per tick in 64 MiB
+    pieces), byte for byte against the oracle at 1M nodes x 10M pods"""
+    from kwok_amd.engine import host_array
+    run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array, once=True, shim=True)
 
 
 @pytest.mark.parametrize("chunk", [None, "70000"])
