@@ -15,9 +15,6 @@
 // documents it accepts: the same kwok_pod_event (flags, phase, creation time,
 // string spans into the arena), name, namespace and pod spec.  What it does not
 // decide is listed for the host codec, never guessed (JSON_HOST):
-//   * a status that precedes the document's metadata or spec (its no-op test
-//     needs the creation time, the containers and readiness gates; Go's
-//     json.Marshal writes metadata, spec, status in that order);
 //   * a JSON escape in a string that is compared or mapped (a key the scan
 //     routes on, a label / annotation key, a selector-matched value, the status
 //     phase, condition fields, container status fields): the host compares
@@ -26,6 +23,11 @@
 // Documents outside the accepted JSON are KWOK_EDOMAIN, as malformed documents
 // are for the host parser (same grammar: its lenient numbers, depth <= 64,
 // surrogate pairs).
+// A status that precedes the metadata or spec (its no-op test needs the creation
+// time, the containers and readiness gates) is skipped by the first pass and
+// scanned by a second one over its own bytes once the document has been read
+// (Go's json.Marshal writes metadata, spec, status in that order; other writers
+// need not).
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -141,9 +143,10 @@ __device__ __forceinline__ bool jstring(JRd& r, JTok& t) {
 
 // Handler interface: key(d, tok) - a key of the object at depth d; begin(d, arr,
 // parent_arr) / end(d, arr, nz) - a container at depth d; scalar(d, tok,
-// parent_arr).  Returns false on malformed JSON.
+// parent_arr).  Returns false on malformed JSON.  d0 > 0: one value at depth d0
+// starting at r.pos (a member the handler deferred), parsed up to its end.
 template <class H>
-__device__ bool jparse(JRd& r, H& h) {
+__device__ bool jparse(JRd& r, H& h, int d0 = 0) {
     uint64_t arr = 0, nzm = 0;  // depth 0..63: the container is an array / holds a non-zero value
     bool arr64 = false, nz64 = false;
     auto is_arr = [&](int d) { return d < 64 ? ((arr >> d) & 1) != 0 : arr64; };
@@ -158,7 +161,7 @@ __device__ bool jparse(JRd& r, H& h) {
             r.pos++;
         }
     };
-    int d = -1;     // the innermost open container
+    int d = d0 - 1;  // the innermost open container
     int state = 0;  // 0: a value; 1: after a value; 2: a key
     for (;;) {
         ws();
@@ -221,7 +224,7 @@ __device__ bool jparse(JRd& r, H& h) {
             continue;
         }
         if (state == 1) {
-            if (d < 0) return c == -1;  // only whitespace after the document's value
+            if (d < d0) return d0 ? true : c == -1;  // only whitespace after the document's value
             const bool a = is_arr(d);
             if (c == ',') {
                 r.pos++;
@@ -311,6 +314,8 @@ struct PodScan {
     // first occurrences (codec.cpp JV::get returns the first key)
     uint32_t seen_root = 0, seen_meta = 0, seen_spec = 0, seen_status = 0;
     bool meta_done = false, spec_done = false, meta_obj = false, spec_obj = false;
+    bool st_defer = false, pass2 = false;  // a status read before metadata / spec: scanned again at the end
+    uint64_t st_pos = 0;                   // its '{'
     // metadata
     Span name{0, 0}, ns{0, 0};
     bool ct_ok = false;
@@ -666,8 +671,13 @@ struct PodScan {
                     err = KWOK_EDOMAIN;
                     break;
                 }
-                // its no-op test needs the creation time, containers and gates
-                if (!meta_done || !spec_done || !ct_ok) host = true;
+                // its no-op test needs the creation time, containers and gates: before
+                // them, skipped (X_NONE) and scanned by the second pass
+                if (!pass2 && (!meta_done || !spec_done || !ct_ok)) {
+                    st_defer = true;
+                    st_pos = r->pos - 1;
+                    break;
+                }
                 has_status = true;
                 mine = X_STATUS;
                 break;
@@ -915,7 +925,17 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
         JRd rd{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
         p.r = &rd;
         p.cfg = A.cfg;
-        const bool ok = !A.cfg->all_host && jparse(rd, p);
+        bool ok = !A.cfg->all_host && jparse(rd, p);
+        if (ok && p.st_defer && !p.host && !p.err) {
+            if (!p.meta_done || !p.spec_done || !p.ct_ok) {
+                p.host = true;  // (the host decides a status it cannot test)
+            } else {
+                p.pass2 = true;
+                p.next = X_STATUS;
+                rd.pos = p.st_pos;
+                ok = jparse(rd, p, 1);
+            }
+        }
         // (a document the scan routed past an escaped key may hold errors the host's
         // first-key lookup does not see: the host decides it, errors included)
         if (A.cfg->all_host) status = JSON_HOST;  // (selectors the device tables do not hold)

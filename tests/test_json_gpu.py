@@ -89,16 +89,16 @@ def eng():
 
 @pytest.mark.parametrize("sel", range(len(SELECTORS)))
 def test_golden_documents_equal_the_host_codec(eng, sel):
-    """canonical documents (metadata, spec, status in Go's order) are decided on
-    the device; scrambled key order puts some statuses ahead of spec (listed for
-    the host); the apiserver echo of expected patches conforms on both sides"""
+    """canonical documents (metadata, spec, status in Go's order), the apiserver
+    echo of expected patches (conforming on both sides) and documents with
+    scrambled key order (statuses ahead of spec or metadata: the second pass) are
+    all decided on the device"""
     rng = random.Random(5)
     canon, scr, echo = golden_docs(rng)
     codec = Codec(manage_all_nodes=True, **SELECTORS[sel])
     compare(eng, codec, canon, want_host=0, where="canonical")
     compare(eng, codec, echo, want_host=0, where="echo")
-    n_host, _ = compare(eng, codec, scr, where="scrambled")
-    assert 0 < n_host < len(scr)
+    compare(eng, codec, scr, want_host=0, where="scrambled")
 
 
 def test_no_op_cases_and_rejections(eng):
@@ -191,6 +191,13 @@ def test_no_op_cases_and_rejections(eng):
     n_host, hs = compare(eng, codec, docs + raw, where="cases")
     assert (hs[:len(docs)] == abi.OK).sum() > len(muts)
     assert n_host >= 2
+    # the same documents with the status first, and between metadata and spec: the
+    # device's second pass decides the same no-op test (no more listed for the host)
+    for order in (("status", "metadata", "spec"), ("metadata", "status", "spec")):
+        moved = [json.dumps({k: d[k] for k in order + tuple(k for k in d if k not in order) if k in d}).encode()
+                 if isinstance(d, dict) else d for d in docs]
+        n2, hs2 = compare(eng, codec, moved + raw, where="status first %r" % (order,))
+        assert (hs2 == hs).all() and n2 == n_host, order
 
 
 def test_mutated_and_nested_documents(eng):
