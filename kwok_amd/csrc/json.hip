@@ -58,21 +58,26 @@ struct JRd {
         return (x >> (8 * (o & 3))) & 0xFFu;
     }
     __device__ __forceinline__ int peek() { return pos < end ? (int)at(pos) : -1; }
-    // the bytes from p to the end of p's 4-byte word, shifted down; n of them
-    __device__ __forceinline__ uint32_t word(uint64_t p, uint32_t& n) {
-        (void)at(p);
-        const uint32_t o = (uint32_t)(p - wb);
-        const uint32_t x = o < 8 ? (o < 4 ? w.x : w.y) : (o < 12 ? w.z : w.w);
-        n = 4u - (o & 3u);
-        return x >> (8 * (o & 3));
-    }
+    // bytes from p up to the first one that ends a string's plain run (a quote, a
+    // backslash or a control character), within p's 16-byte window: that byte's
+    // offset from p, or the bytes to the window's end when the window holds none
+    __device__ __forceinline__ uint32_t plain_run(uint64_t p);
 };
 
-// 0x80 in each byte of x that ends a string's plain run: a quote, a backslash or a
-// control character (SWAR: a byte is zero iff its high bit stays clear below)
-__device__ __forceinline__ uint32_t str_special(uint32_t x) {
+// bit k set for each byte k of x that ends a string's plain run: a quote, a
+// backslash or a control character (SWAR: a byte is zero iff its high bit stays
+// clear below; the four high bits gathered by one multiply)
+__device__ __forceinline__ uint32_t str_special4(uint32_t x) {
     auto zero = [](uint32_t y) { return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu); };
-    return zero(x ^ 0x22222222u) | zero(x ^ 0x5C5C5C5Cu) | zero(x & 0xE0E0E0E0u);
+    const uint32_t m = zero(x ^ 0x22222222u) | zero(x ^ 0x5C5C5C5Cu) | zero(x & 0xE0E0E0E0u);
+    return (((m >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+__device__ __forceinline__ uint32_t JRd::plain_run(uint64_t p) {
+    (void)at(p);
+    const uint32_t o = (uint32_t)(p - wb);
+    const uint32_t m = (str_special4(w.x) | str_special4(w.y) << 4 | str_special4(w.z) << 8 | str_special4(w.w) << 12) &
+                       (0xFFFFu << o);
+    return (m ? (uint32_t)__builtin_ctz(m) : 16u) - o;
 }
 
 __device__ __forceinline__ bool bytes_eq(JRd& r, uint64_t off, uint32_t len, const uint8_t* s, uint32_t n) {
@@ -128,16 +133,14 @@ __device__ __forceinline__ bool jstring(JRd& r, JTok& t) {
     t.esc = false;
     for (;;) {
         if (r.pos >= r.end) return false;
-        {  // the rest of the 4-byte word in one step when it holds no special byte
-            uint32_t n;
-            const uint32_t x = r.word(r.pos, n);
-            if (r.end - r.pos < n) n = (uint32_t)(r.end - r.pos);
-            const uint32_t sp = str_special(x) & (n >= 4u ? ~0u : (1u << (8 * n)) - 1u);
-            if (!sp) {
-                r.pos += n;
-                continue;
+        {  // the plain bytes of the 16-byte window in one step
+            const uint32_t k = r.plain_run(r.pos);
+            if (k >= r.end - r.pos) {
+                r.pos = r.end;  // (the document ends inside the string)
+                return false;
             }
-            r.pos += (uint32_t)__builtin_ctz(sp) >> 3;  // the first special byte
+            r.pos += k;
+            if (r.pos - r.wb == 16) continue;  // (no special byte in the window)
         }
         const uint32_t c = r.at(r.pos);
         if (c == '"') break;
