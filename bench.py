@@ -200,7 +200,7 @@ def cpu_baseline(nodes, threads, ticks):
 
 
 def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=None, max_over_ranks=None,
-              packed=12, ch=None, multi=False, once=False):
+              packed=12, ch=None, multi=False, once=False, together=False):
     """BASELINE configs[3] (C4) on the same fleet: per tick, n_churn pods marked
     for deletion (Modified events with their status, half with finalizers) and
     n_churn new Pending pods on the same nodes (workload.Churn).  A step =
@@ -215,7 +215,10 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
     kwok_pod_rec12 (12 B per record, kwok_ingest_pods_packed12: statuses as
     bytes, the creates' handles only, no release list at N=1); packed=20:
     kwok_pod_rec (20 B, kwok_ingest_pods_packed, every handle back); otherwise
-    kwok_pod_event records with dotted-quad strings (48 B + strings)."""
+    kwok_pod_event records with dotted-quad strings (48 B + strings).
+    together (packed=12, one rank): kwok_ingest_pods_packed12_tick - the tick
+    queued behind the batch's apply passes, collected after the call (ingest_ms:
+    the call, tick_ms: kwok_tick_collect)."""
     barrier = barrier or torch.cuda.synchronize
     max_over_ranks = max_over_ranks or (lambda x: x)
     lo = rank * workload.BUCKETS // world
@@ -254,11 +257,11 @@ def churn_leg(e, fl, pod_handles, now, ticks, n_churn, rank=0, world=1, barrier=
             e.profile_enable(True)
         t0 = time.perf_counter()
         if packed == 12:
-            hs, st, _ = e.ingest_pods_packed12(ev, new_cap=len(ev) // 2, out=outs)
+            hs, st, _ = e.ingest_pods_packed12(ev, new_cap=len(ev) // 2, out=outs, tick_now=now if together else None)
         else:
             hs, st, _ = e.ingest_pods_packed(ev, out=outs) if packed else e.ingest_pods_raw(ev, ar, out=outs)
         t1 = time.perf_counter()
-        r = e.tick(now, read=False)
+        r = e.tick_collect(read=False) if together else e.tick(now, read=False)
         t2 = time.perf_counter()
         if world > 1:
             barrier()
@@ -415,6 +418,11 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
     handoff = {}
     if churn_ticks:
         now, ch, churn = churn_leg(e, fl, pods, now, churn_ticks, nodes, once=True)
+        now, ch, tog = churn_leg(e, fl, pods, now, churn_ticks, nodes, ch=ch, once=True, together=True)
+        churn["together"] = {k: tog[k] for k in ("ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms",
+                                                  "value", "unit")}
+        churn["together"]["what"] = ("kwok_ingest_pods_packed12_tick: the tick queued behind the batch's apply "
+                                     "passes (its kernels run while the results travel back), then kwok_tick_collect")
         for ov in (False, True):
             now, ch, handoff["overlapped" if ov else "sequential"] = churn_handoff_leg(e, fl, ch, now, max(3, churn_ticks),
                                                                                      nodes, ov)
@@ -471,7 +479,7 @@ def heartbeat_once_leg(nodes, steps, warmup, churn_ticks, json_ticks=0):
                                                if ph0["emit_kernel"] else None}},
             "churn": None if churn is None else dict({k: churn[k] for k in (
                 "workload", "ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "emission_ms", "value",
-                "unit", "tick_transitions_per_s", "roofline", "phase_ms")}, with_handoff=handoff),
+                "unit", "tick_transitions_per_s", "roofline", "phase_ms", "together")}, with_handoff=handoff),
             "churn_json": cjson}
 
 

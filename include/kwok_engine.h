@@ -347,6 +347,20 @@ int kwok_ingest_pods_packed(kwok_engine* e, const kwok_pod_rec* recs, size_t n, 
  * records, against 40 + 10 MB for kwok_pod_rec). */
 int kwok_ingest_pods_packed12(kwok_engine* e, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
                               size_t new_cap, int8_t* out_status, uint32_t* out_released);
+/* kwok_ingest_pods_packed12, then kwok_tick_submit(e, now_unix) queued right behind
+ * the batch's apply passes (single-rank engines): the tick's kernels run while
+ * the per-record results travel back, so a churn step (a batch, then a tick) does
+ * not wait for the results and the call's return before its tick starts.
+ * Returns as kwok_ingest_pods_packed12 once the results are in the caller's
+ * arrays; the tick is then collected with kwok_tick_collect (it may still be
+ * running).  The tick submit's own checks (now, two ticks outstanding, profiled
+ * queues) are made before the batch is touched.  A chunk that needs more pod
+ * slots than a bucket has makes the tick's launches skip on the device; the
+ * call grows the buckets, applies the chunk and queues the tick again.
+ * Equivalent to the two calls, record for record and tick for tick
+ * (tests/test_c4_churn_gpu.py, tests/test_growth_gpu.py). */
+int kwok_ingest_pods_packed12_tick(kwok_engine* e, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
+                                   size_t new_cap, int8_t* out_status, uint32_t* out_released, int64_t now_unix);
 /* Host only: kwok_pod_event records (strings in `arena`) -> the compact form,
  * with the checks that need the strings (canonical dotted quads, creation time
  * range, spec id and phase bounds).  status[i] = KWOK_OK, KWOK_EDOMAIN (an IP,

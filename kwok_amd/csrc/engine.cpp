@@ -586,6 +586,9 @@ int upload_specs(kwok_engine* e) {
 }
 
 int drain(kwok_engine* e);  // finish every queued tick on the host (below)
+int tick_submit_check(kwok_engine* e, int64_t now_unix);  // kwok_tick_submit's checks / the rest (below)
+int tick_submit_impl(kwok_engine* e, int64_t now_unix);
+int enqueue_tick(kwok_engine* e, int k, bool requeue);
 int poisoned(kwok_engine* e) {
     return e->fail(KWOK_EDEVICE, "a failed tick left the engine out of step with the device: destroy it and "
                                  "recreate it (re-ingest by List)");
@@ -1859,17 +1862,21 @@ int ingest_chunk(kwok_engine* e, const IngestBatch& I) {
 // out_new[k < new_cap], in create order; out_handles unused)
 int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, const char* arena, size_t arena_len,
                      int32_t* out_handles, int32_t* out_status, int8_t* out_status8, uint32_t* out_released,
-                     bool resident = false, int32_t* out_new = nullptr, size_t new_cap = 0) {
+                     bool resident = false, int32_t* out_new = nullptr, size_t new_cap = 0, int64_t tick_now = -1) {
     const size_t RB = packed == 2 ? sizeof(kwok_pod_rec12) : packed ? sizeof(kwok_pod_rec) : sizeof(kwok_pod_event);
     static_assert(sizeof(kwok_pod_rec12) == 12, "kwok_pod_rec12 is 12 bytes");
     auto rec_at = [&](const void* base, size_t i) { return static_cast<const uint8_t*>(base) + i * RB; };
     if (e->poisoned) return poisoned(e);
     drain(e);  // the device state reflects every submitted tick
     if (e->poisoned) return poisoned(e);
+    if (tick_now >= 0) {  // (checked before anything is queued)
+        if (e->multi) return e->fail(KWOK_EINVAL, "ingest + tick in one call: single-rank engines only");
+        if (int rc = tick_submit_check(e, tick_now)) return rc;
+    }
     e->emit_hint = true;
     e->quiet = 0;
     e->sum_valid = false;
-    if (!n) return 0;
+    if (!n) return tick_now >= 0 ? tick_submit_impl(e, tick_now) : 0;
     e->pod_records_since_tick += n;
     const auto t0 = clk::now();
     int rc = ingest_reserve(e, n, arena_len);
@@ -2008,6 +2015,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     // has (or an earlier chunk did).  One read-back of the chunks' summaries at the
     // end: the rare chunk that needs growth and the chunks after it are then applied
     // again with the host in the loop (ingest_chunk), in order.
+    int tick_k = -1;  // tick mode: the slot of the tick queued behind the batch
     auto run = [&]() -> int {
         HIPCHK(e, hipEventRecord(G.go, st));
         if (arena_len && !zar && !resident) {  // (the arena ahead of the records: prep reads both)
@@ -2017,7 +2025,8 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
         for (uint32_t k = 0; k < std::min<uint32_t>(K, 2); k++)
             if (int r = prep(k)) return r;
         HIPCHK(e, hipMemsetAsync(G.abort, 0, 4, st));
-        hipStream_t rs = K > 1 && e->results_stream ? G.dst : st;
+        // (tick mode: the results always on their own stream, the tick's launches on the engine's)
+        hipStream_t rs = (K > 1 && e->results_stream) || tick_now >= 0 ? G.dst : st;
         for (uint32_t k = 0; k < K; k++) {
             const IngestBatch I = chunk_batch(k);
             HIPCHK(e, hipStreamWaitEvent(st, G.prepped[k & 1], 0));
@@ -2033,29 +2042,39 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
                 if (int r2 = prep(k + 2)) return r2;
         }
         if (int r = release_for_host(e)) return r;
+        if (tick_now >= 0) {
+            // the tick, right behind the last apply pass (its kernels run while the results
+            // travel); every launch of it skips while G.abort says a chunk needs growth
+            HIPCHK(e, hipMemcpyAsync(&e->S.bar->skip, G.abort, 4, hipMemcpyDeviceToDevice, st));
+            if (int r = tick_submit_impl(e, tick_now)) return r;
+            tick_k = e->queue[e->nq - 1];
+        }
+        // the host waits for the results stream alone when the tick is behind the batch
+        hipStream_t ws = tick_now >= 0 ? rs : st;
         if (packed == 2) {  // the creates' handles (every chunk's), and the summaries after them (n_new)
             if (new_map) HIPCHK(e, hipEventRecord(e->fence, rs));  // (system-scope release: the host reads them)
             else HIPCHK(e, hipMemcpyAsync(out_new, G.new_handle, std::min(new_cap, n) * 4, hipMemcpyDeviceToHost, rs));
-            if (rs != st) {
+            if (rs != st && ws == st) {
                 HIPCHK(e, hipEventRecord(G.rdone, rs));
                 HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
             }
         }
-        if (packed != 2 && rs != st) {  // (the results stream joins the engine stream: one wait below)
+        if (packed != 2 && rs != st && ws == st) {  // (the results stream joins the engine stream: one wait below)
             HIPCHK(e, hipEventRecord(G.rdone, rs));
             HIPCHK(e, hipStreamWaitEvent(st, G.rdone, 0));
         }
-        HIPCHK(e, hipMemcpyAsync(G.sums_h, G.sums, (size_t)K * sizeof(IngSummary), hipMemcpyDeviceToHost, st));
+        // (tick mode: rs waited for the last apply pass, whose summary is then final)
+        HIPCHK(e, hipMemcpyAsync(G.sums_h, G.sums, (size_t)K * sizeof(IngSummary), hipMemcpyDeviceToHost, ws));
         if (tstamp) HIPCHK(e, hipEventRecord(G.tev[6], rs));  // 6: results copied
         const auto tq = clk::now();
         if (e->sync_spin) {  // spin on the batch's last operation (as a tick's completion: no wake-up latency)
-            HIPCHK(e, hipEventRecord(G.idone, st));
+            HIPCHK(e, hipEventRecord(G.idone, ws));
             hipError_t q;
             while ((q = hipEventQuery(G.idone)) == hipErrorNotReady) {
             }
             if (q != hipSuccess) return e->fail(KWOK_EDEVICE, "ingest: %s", hipGetErrorString(q));
         } else {
-            HIPCHK(e, hipStreamSynchronize(st));
+            HIPCHK(e, hipStreamSynchronize(ws));
         }
         t_synced = clk::now();
         if (tstamp) {
@@ -2077,6 +2096,7 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
             if (e->debug_fail_apply == k + 1)
                 return e->fail(KWOK_EDEVICE, "injected failure after the apply pass of ingest chunk %u", k);
         }
+        const bool regrow = k < K;
         for (; k < K; k++) {  // chunks from the first that needs growth: the host in the loop
             if (e->iprof) fprintf(stderr, "[kwok ingest]   chunk %u again with the growth check\n", k);
             if (int r = prep_on(k, st)) return r;
@@ -2094,6 +2114,13 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
             }
             HIPCHK(e, hipStreamSynchronize(st));
         }
+        if (regrow && tick_k >= 0) {  // the tick's launches skipped: queued again behind the chunks
+            kwok_engine::TickSlot& T = e->slots[tick_k];
+            if (int r = grow_arena(e, T)) return r;  // (the growth may have raised the tick's worst case)
+            memset(T.hdr_h, 0, sizeof(TickHdr));
+            HIPCHK(e, hipMemsetAsync(&e->S.bar->skip, 0, sizeof(uint32_t), st));
+            if (int r = enqueue_tick(e, tick_k, true)) return r;
+        }
         return rejected;
     };
     rc = run();
@@ -2106,6 +2133,15 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
                      G.sums_h[K - 1].n_new, new_cap);
     else if (rc < 0 && e->ing_mutated)
         e->poisoned = true;
+    if (rc < 0 && tick_k >= 0 && e->poisoned) {  // the tick behind a batch that failed half applied fails with it
+        kwok_engine::TickSlot& T = e->slots[tick_k];
+        if (T.state == SLOT_QUEUED) {
+            (void)hipStreamSynchronize(st);
+            T.state = SLOT_DONE;
+            T.rc = rc;
+            T.err = e->err;
+        }
+    }
     // nothing of this batch stays queued on the engine / prep / results streams (a failed
     // chunk included; a batch that ran to its end synchronised them in run(): the engine
     // stream's applies waited for every prep, the results stream was synchronised)
@@ -2139,6 +2175,13 @@ int kwok_ingest_pods_packed12(kwok_engine* e, const kwok_pod_rec12* recs, size_t
     if (!e || (n && !recs) || n > 0x7FFFFFF0ull || (new_cap && !out_new_handles)) return KWOK_EINVAL;
     return ingest_pods_impl(e, recs, 2, n, nullptr, 0, nullptr, nullptr, out_status, out_released, false,
                             out_new_handles, new_cap);
+}
+
+int kwok_ingest_pods_packed12_tick(kwok_engine* e, const kwok_pod_rec12* recs, size_t n, int32_t* out_new_handles,
+                                   size_t new_cap, int8_t* out_status, uint32_t* out_released, int64_t now_unix) {
+    if (!e || (n && !recs) || n > 0x7FFFFFF0ull || (new_cap && !out_new_handles) || now_unix < 0) return KWOK_EINVAL;
+    return ingest_pods_impl(e, recs, 2, n, nullptr, 0, nullptr, nullptr, out_status, out_released, false,
+                            out_new_handles, new_cap, now_unix);
 }
 
 // ---- the pod codec on the GPU (json.hip) ------------------------------------
@@ -3340,13 +3383,28 @@ int drain(kwok_engine* e) {
 }
 }  // namespace
 
-extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
-    if (!e) return KWOK_EINVAL;
-    if (e->poisoned) return poisoned(e);
+namespace {
+// what kwok_tick_submit checks before it queues anything
+int tick_submit_check(kwok_engine* e, int64_t now_unix) {
     if (now_unix < 0 || now_unix > 0xFFFFFFFFll) return e->fail(KWOK_EDOMAIN, "now out of range");
     if (e->nq >= 2) return e->fail(KWOK_EBUSY, "two ticks outstanding: collect one first");
     if (e->nq >= 1 && (e->prof || trace_enabled(e)))
         return e->fail(KWOK_EBUSY, "profiled / traced ticks are not queued behind each other");
+    return KWOK_OK;
+}
+}  // namespace
+
+extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
+    if (!e) return KWOK_EINVAL;
+    if (e->poisoned) return poisoned(e);
+    if (int rc = tick_submit_check(e, now_unix)) return rc;
+    return tick_submit_impl(e, now_unix);
+}
+
+namespace {
+// kwok_tick_submit after its checks (kwok_ingest_pods_packed12_tick queues it
+// behind the batch's apply passes)
+int tick_submit_impl(kwok_engine* e, int64_t now_unix) {
     const auto t0 = clk::now();
     // multi rank: the previous tick is finished (its long-list allgather, if any,
     // included) before this one's collectives are enqueued, so every rank issues
@@ -3392,6 +3450,7 @@ extern "C" int kwok_tick_submit(kwok_engine* e, int64_t now_unix) {
     e->host_ms[KWOK_H_TOTAL] += ms_between(t0, clk::now());
     return KWOK_OK;
 }
+}  // namespace
 
 extern "C" int kwok_engine_stats(const kwok_engine* e, uint64_t out[KWOK_STAT_COUNT]) {
     if (!e || !out) return KWOK_EINVAL;

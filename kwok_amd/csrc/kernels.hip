@@ -3801,8 +3801,9 @@ __device__ __forceinline__ void emit_jobs(const DevState& S, EmitLds* L, uint32_
 
 __global__ __launch_bounds__(EMIT_BLOCK, 4) void k_emit(DevState S, uint64_t now_unix, uint64_t start_unix) {
     __shared__ EmitLds L;
-    if (S.multi && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        return;  // the tick's launches were skipped (queued behind one the host has not finished)
+    // the tick's launches were skipped: queued behind one the host has not finished, or
+    // (kwok_ingest_pods_packed12_tick) behind a batch whose chunk needs more pod slots
+    if (__hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     const uint32_t n_pp = S.emit_n[0], n_init = S.emit_n[1];
     if (n_pp == 0 && n_init == 0) return;
     stage_emit(S, &L, n_pp != 0, n_init != 0, now_unix, start_unix);
@@ -3866,7 +3867,7 @@ __global__ __launch_bounds__(64 * JOB_WAVES, JOBS_MIN_WAVES) void k_pod_jobs(Dev
     const uint32_t w = (uint32_t)wave_id(), it = blockIdx.x * JOB_WAVES + w;
     if constexpr (FUSE) {
         if (blockIdx.x >= pod_blocks) {  // node inits (block-uniform)
-            if (S.multi && __hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+            if (__hip_atomic_load(&S.bar->skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
             const uint32_t n_init = S.emit_n[1];
             if (n_init == 0) return;
             EmitLds* L = reinterpret_cast<EmitLds*>(&sh);

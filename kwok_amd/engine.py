@@ -62,6 +62,7 @@ def declare(lib, pre):
         "ingest_pods": (C.c_int, [VP, VP, SZ, C.c_char_p, SZ, VP, VP, VP]),
         "ingest_pods_packed": (C.c_int, [VP, VP, SZ, VP, VP, VP]),
         "ingest_pods_packed12": (C.c_int, [VP, VP, SZ, VP, SZ, VP, VP]),
+        "ingest_pods_packed12_tick": (C.c_int, [VP, VP, SZ, VP, SZ, VP, VP, C.c_int64]),
         "pool_put": (C.c_int, [VP, VP, SZ]),
         "cni_pending": (C.c_int, [VP, VP, SZ, P(SZ)]),
         "cni_assign": (C.c_int, [VP, VP, VP, SZ, VP]),
@@ -285,11 +286,13 @@ class EngineBase:
         self._check(rc, "ingest_pods_packed")
         return hs, st, rel
 
-    def ingest_pods_packed12(self, recs: np.ndarray, new_cap=None, out=None, released=True):
+    def ingest_pods_packed12(self, recs: np.ndarray, new_cap=None, out=None, released=True, tick_now=None):
         """kwok_ingest_pods_packed12 over POD_REC12_DTYPE rows -> (handles of the
         creates in create order, status int8 per record, released).  new_cap: the
         room for create handles (default: the number of REC_NEW rows); out:
-        optional (new handles, status, released) arrays (e.g. page-locked)"""
+        optional (new handles, status, released) arrays (e.g. page-locked).
+        tick_now: kwok_ingest_pods_packed12_tick - the tick at tick_now queued
+        behind the batch's apply passes (collect it with tick_collect)"""
         n = len(recs)
         r = recs if recs.flags.c_contiguous and recs.dtype == abi.POD_REC12_DTYPE else \
             np.ascontiguousarray(recs, dtype=abi.POD_REC12_DTYPE)
@@ -301,8 +304,13 @@ class EngineBase:
         else:
             nh, st, rel = out[0], out[1][:n], (out[2][:n] if out[2] is not None else None)
             assert len(nh) >= new_cap
-        rc = self._fn("ingest_pods_packed12")(self._h, r.ctypes.data, n, nh.ctypes.data, new_cap, st.ctypes.data,
-                                              rel.ctypes.data if rel is not None else None)
+        if tick_now is None:
+            rc = self._fn("ingest_pods_packed12")(self._h, r.ctypes.data, n, nh.ctypes.data, new_cap, st.ctypes.data,
+                                                  rel.ctypes.data if rel is not None else None)
+        else:
+            rc = self._fn("ingest_pods_packed12_tick")(self._h, r.ctypes.data, n, nh.ctypes.data, new_cap,
+                                                       st.ctypes.data, rel.ctypes.data if rel is not None else None,
+                                                       int(tick_now))
         self._check(rc, "ingest_pods_packed12")
         return nh[:new_cap], st, rel
 

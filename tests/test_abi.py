@@ -46,6 +46,7 @@ def test_oracle_library_exports():
                  "kwok_pack_pod_events",  # host helper of the compact wire form (engine library)
                  "kwok_bucket_of", "kwok_rank_of_bucket", "kwok_profile_enable", "kwok_profile_read", "kwok_profile_host",
                  "kwok_tick_submit", "kwok_tick_collect",  # engine only: queued ticks (the oracle is sequential)
+                 "kwok_ingest_pods_packed12_tick",  # engine only: a batch with its tick queued behind it
                  "kwok_read_arena_async", "kwok_read_wait",  # engine only: reads overlapping the next tick
                  "kwok_engine_stats",  # engine only: which tick kernel ran
                  "kwok_spec_key", "kwok_decode_pods_gpu", "kwok_ingest_pods_json",  # the GPU codec (engine library)

@@ -22,14 +22,15 @@ pytestmark = pytest.mark.gpu
 
 
 def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, full_state=True, alloc=None,
-              packed=False, once=False, shim=False):
+              packed=False, once=False, shim=False, together=False):
     """packed: the engine ingests the compact wire form (kwok_ingest_pods_packed;
     packed=12: kwok_pod_rec12 through kwok_ingest_pods_packed12, which returns the
     creates' handles only), the oracle the same events as kwok_pod_event with
     dotted quads.  once: heartbeat-once engines (the drop-in's).  shim: every churn
     tick is also read back as the Go drop-in reads it (gpu_common.shim_read_check:
     lists, one heartbeat body, every patch byte in 64 MiB pieces) and compared with
-    the oracle byte for byte"""
+    the oracle byte for byte.  together: kwok_ingest_pods_packed12_tick (the tick
+    queued behind the batch's apply passes), the oracle's two calls beside it"""
     from gpu_common import shim_read_check
     if threads is not None:
         os.environ["KWOK_INGEST_THREADS"] = str(threads)
@@ -55,7 +56,7 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
         if packed == 12:
             recs, _ = chp.batch(dump, now)
             assert recs.dtype.itemsize == 12
-            nh, s1, r1 = e.ingest_pods_packed12(recs)
+            nh, s1, r1 = e.ingest_pods_packed12(recs, tick_now=now if together else None)
             assert len(nh) == n_churn
             chp.applied(nh.copy(), s1, new_only=True)
             # every other record's handle is its target
@@ -69,7 +70,7 @@ def run_churn(nodes, n_churn, ticks, buckets=workload.BUCKETS, threads=None, ful
         h2, s2, r2 = o.ingest_pods_raw(ev, ar)
         assert (h1 == h2).all() and (s1 == s2).all() and (r1 == r2).all(), "churn tick %d ingest" % t
         ch.applied(h1, s1)
-        res = e.tick(now, read=False)
+        res = e.tick_collect(read=False) if together else e.tick(now, read=False)
         o.tick(now, read=False)
         if shim:
             pieces, nbytes = shim_read_check(e, o.read_arrays(), res)
@@ -117,6 +118,21 @@ def test_c4_churn_metric_size_packed12():
     record and per tick"""
     from kwok_amd.engine import host_array
     run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array)
+
+
+@pytest.mark.timeout(900)
+def test_c4_churn_metric_size_ingest_then_tick():
+    """kwok_ingest_pods_packed12_tick at 1M nodes x 10M pods (the tick's kernels
+    queued behind the batch, running while the results travel), heartbeat-once
+    engines, every churn tick read back as the drop-in reads it"""
+    from kwok_amd.engine import host_array
+    run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array, once=True, shim=True,
+              together=True)
+
+
+def test_churn_ingest_then_tick_parity():
+    """20k nodes x 200k pods, 40k + 40k per tick, the full state every tick"""
+    run_churn(20_000, 40_000, 3, packed=12, together=True)
 
 
 @pytest.mark.timeout(900)

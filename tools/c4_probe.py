@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--once", action="store_true")
     ap.add_argument("--steady", type=int, default=0)
+    ap.add_argument("--together", action="store_true", help="kwok_ingest_pods_packed12_tick (the tick behind the batch)")
     a = ap.parse_args()
     e, fl, pods = workload.build_engine_fleet(keng.Engine, a.nodes, heartbeat_once=a.once)
     now = workload.S0 + 30
@@ -28,7 +29,8 @@ def main():
     if a.steady:
         _, _, now = bench.steady_queued(e, now, a.steady, 3)
     now += 30
-    _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire, once=a.once)
+    _, _, c = bench.churn_leg(e, fl, pods, now, a.ticks, a.nodes, packed=a.wire, once=a.once,
+                              together=a.together)
     e.close()
     print(json.dumps({k: c[k] for k in ("ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms", "roofline",
                                         "phase_ms")}), flush=True)
