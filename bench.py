@@ -982,6 +982,13 @@ def main():
     if a.churn_ticks > 0:
         now, ch, churn = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, rank, world,
                                    barrier, max_over_ranks, multi=comm is not None or gather is not None)
+        if world == 1 and comm is None and gather is None:  # the batch with its tick behind it (one call)
+            now, ch, tog = churn_leg(e, fl, pods, now, a.churn_ticks, a.churn or a.nodes_per_rank, ch=ch,
+                                     together=True)
+            churn["together"] = {k: tog[k] for k in ("ms_per_step", "ingest_ms", "tick_ms", "median_ms", "kernel_ms",
+                                                      "value", "unit")}
+            churn["together"]["what"] = ("kwok_ingest_pods_packed12_tick: the tick queued behind the batch's apply "
+                                         "passes, then kwok_tick_collect")
         if world == 1:  # the same storm through the full record form, beside it
             now, ch, churn_ev = churn_leg(e, fl, pods, now, max(2, a.churn_ticks // 2), a.churn or a.nodes_per_rank,
                                           rank, world, barrier, max_over_ranks, packed=False, ch=ch)
