@@ -76,9 +76,9 @@ POD_PATCH_BYTES = 577
 #   C4 tick, per deleted pod: 10 B re-check + 4 B handle + 1 B finalizer flag + 4 B release
 DELETE_BYTES = 19
 CHURN_WARMUP = 2  # untimed churn batches before the timed steps (see churn_leg)
-PMC_FILE = "r10_pmc.json"
-ONCE_PMC_FILE = "r10_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
-C4_PMC_FILE = "r10_c4once_pmc.json"  # the heartbeat-once engine's C4 tick kernels (tools/gpu_c4once.sh)
+PMC_FILE = "r12_pmc.json"
+ONCE_PMC_FILE = "r12_once_pmc.json"  # the heartbeat-once leg's k_once (tools/gpu_full.sh)
+C4_PMC_FILE = "r12_c4once_pmc.json"  # the heartbeat-once engine's C4 tick kernels (tools/gpu_c4once.sh)
 
 
 def parse():
