@@ -585,10 +585,12 @@ int kwok_decode_pods(const kwok_codec* c, char* arena, size_t arena_len, const u
 
 /* ---- the pod codec on the GPU ("later as a GPU JSON
  * scanner"): the same per-document decision as kwok_decode_pod, made on the
- * engine's device by a one-pass scanner (one thread per document).  Documents
- * the scanner leaves undecided (a status ahead of metadata / spec, a JSON
- * escape in a compared string, a spec whose key matches a registered spec's
- * while its strings differ) are decoded by the host codec, and counted in
+ * engine's device by a one-pass scanner (one thread per document; a status
+ * ahead of metadata / spec is scanned again once they are read).  Documents
+ * the scanner leaves undecided (a JSON escape in a compared string, a status
+ * with no metadata, spec or creation time to test against, a spec whose key
+ * matches a registered spec's while its strings differ) are decoded by the
+ * host codec, and counted in
  * *n_host; nothing is guessed.  Selectors larger than the device's tables (8
  * requirements, 32 values, 2 KiB of keys and values per codec) send every
  * document to the host codec.  Node documents: kwok_ingest_nodes_json below.
