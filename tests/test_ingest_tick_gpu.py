@@ -134,3 +134,33 @@ def test_ingest_then_tick_checks_first():
     compare_state(d.e, d.o, d.n_slots, "after the refused batch")
     d.e.close()
     d.o.close()
+
+
+def test_ingest_then_tick_edges():
+    """an empty batch (the tick alone), and a batch with more creates than
+    out_new_handles holds: the call reports KWOK_EINVAL once the batch is applied
+    (the engine stays usable) and the tick behind it is the oracle's"""
+    kw = dict(cidr="10.0.0.1/16", node_ip=NODE_IP, buckets=16, node_slots_per_bucket=8, pod_slots_per_bucket=64)
+    d = Driver(kw, 13, specs=[Driver.DEFAULT_SPECS[0]])
+    nh, _ = d.nodes(["node-%07d" % i for i in range(20)], managed=1, lockable=1)
+    ev, ar = new_pods(d.rng, nh, 100, d.spec)
+    step(d, ev, ar, "first batch")
+    # the tick alone
+    d.e.ingest_pods_packed12(np.zeros(0, abi.POD_REC12_DTYPE), tick_now=d.now)
+    eo, oo = d.e.tick_collect(), d.o.tick(d.now)
+    d.now += 30
+    compare(eo, oo, "empty batch")
+    # room for 10 of 40 create handles
+    ev, ar = new_pods(d.rng, nh, 40, d.spec)
+    with pytest.raises(KwokError, match="out_new_handles"):
+        d.e.ingest_pods_packed12(packed12(d, ev), new_cap=10, tick_now=d.now)
+    h2, s2, _ = d.o.ingest_pods_raw(ev, ar)
+    ok = s2 == 0
+    d.spec_of[h2[ok]] = ev["spec_id"][ok]
+    d.ctime_of[h2[ok]] = ev["creation_unix"][ok]
+    eo, oo = d.e.tick_collect(), d.o.tick(d.now)
+    d.now += 30
+    compare(eo, oo, "batch past new_cap")
+    compare_state(d.e, d.o, d.n_slots, "batch past new_cap")
+    d.e.close()
+    d.o.close()
