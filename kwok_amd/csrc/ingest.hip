@@ -12,7 +12,7 @@
 //                 creation time, handle -> owned bucket, spec.nodeName -> its
 //                 bucket), the statuses that need no state.
 //   bucket sort   a stable counting sort of the batch by bucket, every bucket's
-//                 range (k_bs_*; rocprim's radix sort past 8191 local buckets).
+//                 range (k_bs_*; rocprim's radix sort past 8447 local buckets).
 //   k_ing_need    live pods + creates of every bucket with creates (growth check).
 //   k_ing_apply   one wave per bucket, its records in event order: the slot
 //                 policy (lowest free slot, canonical), coalescing by applying
@@ -545,14 +545,35 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
     B.nw = (S.cp + 63) / 64;
     B.hint = 0;
     const uint32_t fill0 = B.fill;
-    // occupancy bitmap of [0, fill): pod_state's USED bits (8 slots per 16-byte load)
+    // the next chunk's records (idx_sorted / rec are this pass's inputs: no hazard),
+    // loaded one chunk ahead so that a chunk waits on its state loads only
+    uint32_t nidx = 0;
+    uint4 na = make_uint4(0, 0, 0, 0), nb = na;
+    auto fetch = [&](uint32_t q0) {
+        const uint32_t p = q0 + l;
+        nidx = 0;
+        na = nb = make_uint4(0, 0, 0, 0);
+        if (p < pend) {
+            nidx = I.idx_sorted[p];
+            const uint4* rp = reinterpret_cast<const uint4*>(I.rec + nidx);
+            na = rp[0];
+            nb = rp[1];
+        }
+    };
+    fetch(pbeg);
+    // occupancy bitmap of [0, fill): pod_state's USED bits (8 slots per 16-byte
+    // load, a lane's 8 loads in flight together)
     for (uint32_t q = l; q < B.nw; q += 64) {
-        uint64_t word = 0;
+        uint4 vs[8];
+#pragma unroll
         for (uint32_t g = 0; g < 8; g++) {
             const uint32_t s = q * 64 + g * 8;
-            if (s >= B.fill) break;
-            const uint4 v = *reinterpret_cast<const uint4*>(S.pod_state + B.sbase + s);
-            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+            vs[g] = s < B.fill ? *reinterpret_cast<const uint4*>(S.pod_state + B.sbase + s) : make_uint4(0, 0, 0, 0);
+        }
+        uint64_t word = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < 8; g++) {
+            const uint32_t u[4] = {vs[g].x, vs[g].y, vs[g].z, vs[g].w};
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 word |= (uint64_t)(u[k] & PS_USED) << (g * 8 + 2 * k);
@@ -571,13 +592,8 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         mem_sync();  // the previous chunk's stores, before this chunk's (coherent) loads
         const uint32_t p = p0 + l;
         const bool v = p < pend;
-        const uint32_t idx = v ? I.idx_sorted[p] : 0u;
-        uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-        if (v) {
-            const uint4* rp = reinterpret_cast<const uint4*>(I.rec + idx);
-            ra = rp[0];
-            rb = rp[1];
-        }
+        const uint32_t idx = nidx;
+        const uint4 ra = na, rb = nb;
         // PodRec: bucket, pos, hip, pip | ctime, spec|op<<16|phase<<24, flags|chk<<8|fst<<16|pst<<24, pad
         const uint32_t pos = ra.y;
         const uint32_t hop = rb.y, hfl = rb.z;
@@ -592,6 +608,7 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
         }
         uint32_t ns0 = 0;
         if (v && nd0 < B.cn) ns0 = ld8_coh(S.node_state + B.nbase + nd0);
+        if (p0 + 64 < pend) fetch(p0 + 64);
         // ---- parallel path: a chunk in which no record can see another's effect
         // except through the creates' slot order (no DELETE, no by-name create, no
         // slot named twice, no existing record on a free slot beside creates, enough
@@ -1156,7 +1173,8 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 //   k_bs_cols     per key: the exclusive prefix over the tiles, in place; the total
 //   k_bs_scatter  per tile: the exclusive scan of the totals (each key's first
 //                 sorted position; block 0 writes every bucket's range [beg, end)),
-//                 then one wave takes the tile's records in order, 64 at a time:
+//                 then the tile's W waves take a sub-tile each (the key's records in the
+//                 earlier sub-tiles counted first), its records in order, 64 at a time:
 //                 the lanes of a key (LDS tags, a ballot per shared key) take consecutive positions after
 //                 the key's running count in LDS -> idx_sorted (keys_sorted only at
 //                 each bucket's first position: what the range checks read; the
@@ -1170,7 +1188,7 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 // no range of an earlier batch survives (k_ing_ranges / k_nd_ranges are not run).
 // ---------------------------------------------------------------------------
 constexpr uint32_t BS_TILE = 4096;
-constexpr uint32_t BS_MAX_KEYS = 8192;  // LDS: 32 KB of counts (+ 16 KB of a tile's keys) per block
+constexpr uint32_t BS_MAX_KEYS = 8448;  // 8192 local buckets + 1 (k_bs_scatter's LDS: 4 waves past BS_KEYS8 keys, ~135 KB)
 struct BucketSort {
     const uint32_t* keys;
     uint32_t n, nk;         // records, keys (nb + 1)
@@ -1240,93 +1258,111 @@ __global__ void k_bs_cols(BucketSort B, uint32_t tiles) {
     }
     if (g == 0) B.tot[k] = all;
 }
-__global__ void k_bs_scatter(BucketSort B) {
-    extern __shared__ uint32_t cnt[];  // [nk] running positions, the tile's keys [BS_TILE], tags [nk] (bytes)
-    __shared__ uint32_t wsum[4];
-    uint32_t* tk = cnt + B.nk;
-    uint8_t* tag = reinterpret_cast<uint8_t*>(tk + BS_TILE);
-    const uint32_t t = blockIdx.x;
-    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n);
-    // the key totals: thread th holds keys [th * PER, +PER) (all loads in flight), their
-    // exclusive scan over the block gives each key's first sorted position
-    constexpr uint32_t PER = BS_MAX_KEYS / 256;
+// W waves per tile, a sub-tile of BS_TILE / W records each: every wave counts its
+// sub-tile's keys (u16 pairs in LDS), the counts become per-wave offsets (the key's
+// records in the tile's earlier sub-tiles), and the waves place their records at
+// the same time, each in order, 64 at a time (W = 8: 8 rounds per tile, not 64)
+template <uint32_t W, uint32_t NKMAX>
+__global__ __launch_bounds__(64 * W) void k_bs_scatter(BucketSort B) {
+    constexpr uint32_t NT = 64 * W, SUB = BS_TILE / W, IT = SUB / 64, PER = NKMAX / NT;
+    __shared__ uint32_t cnt[NKMAX];          // each key's first position in the tile
+    __shared__ uint32_t offp[W][NKMAX / 2];  // per wave, per key (u16 pairs): its offset past cnt
+    __shared__ uint8_t tag[W][NKMAX];        // per wave: the lane that wrote a key last
+    __shared__ uint32_t wsum[W];
+    const uint32_t t = blockIdx.x, w = threadIdx.x >> 6, l = lane(), nk = B.nk, nkp = (nk + 1) / 2;
+    const uint32_t i0 = t * BS_TILE, i1 = min(i0 + BS_TILE, B.n), s0 = i0 + w * SUB;
+    // the key totals and the tile's prefixes (thread th: keys [th * PER, +PER)) and
+    // the wave's keys, all loads in flight together
     const uint32_t k0 = threadIdx.x * PER;
-    uint32_t tot[PER], hst[PER], sum = 0;
+    uint32_t tot[PER], hst[PER], key[IT], sum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
-        const bool ok = k0 + q < B.nk;
+        const bool ok = k0 + q < nk;
         tot[q] = ok ? B.tot[k0 + q] : 0u;
-        hst[q] = ok ? B.hist[(size_t)t * B.nk + k0 + q] : 0u;
+        hst[q] = ok ? B.hist[(size_t)t * nk + k0 + q] : 0u;
     }
-    constexpr uint32_t RK = BS_TILE / 256;
-    uint32_t key[RK];
 #pragma unroll
-    for (uint32_t q = 0; q < RK; q++) {
-        const uint32_t i = i0 + q * 256 + threadIdx.x;
-        key[q] = i < i1 ? B.keys[i] : 0u;
+    for (uint32_t q = 0; q < IT; q++) {
+        const uint32_t i = s0 + q * 64 + l;
+        key[q] = i < i1 ? B.keys[i] : ~0u;
     }
+    uint32_t* ow32 = offp[w];
+    for (uint32_t j = l; j < nkp; j += 64) ow32[j] = 0;
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) sum += tot[q];
     uint32_t x = sum;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane() >= (uint32_t)o) x += y;
+        if (l >= (uint32_t)o) x += y;
     }
-    const uint32_t w = threadIdx.x >> 6;
-    if (lane() == 63) wsum[w] = x;
+    if (l == 63) wsum[w] = x;
+    lds_sync();  // (the wave's zeroes before its counts)
 #pragma unroll
-    for (uint32_t q = 0; q < RK; q++) tk[q * 256 + threadIdx.x] = key[q];
+    for (uint32_t q = 0; q < IT; q++)
+        if (key[q] != ~0u) atomicAdd(&ow32[key[q] >> 1], 1u << (16 * (key[q] & 1)));
     __syncthreads();
     uint32_t pre = x - sum;
     for (uint32_t q = 0; q < w; q++) pre += wsum[q];
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
         const uint32_t k = k0 + q;
-        if (k < B.nk) {
+        if (k < nk) {
             cnt[k] = pre + hst[q];
-            if (t == 0 && k + 1 < B.nk) {
+            if (t == 0 && k + 1 < nk) {
                 B.beg[k] = pre, B.end[k] = pre + tot[q];
                 if (tot[q]) B.keys_sorted[pre] = k;  // (the consumers check a range's first key only)
             }
         }
         pre += tot[q];
     }
+    // the waves' counts -> exclusive offsets over the waves (both halves at once: < 2^16)
+    for (uint32_t j = threadIdx.x; j < nkp; j += NT) {
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < W; q++) {
+            const uint32_t c = offp[q][j];
+            offp[q][j] = run;
+            run += c;
+        }
+    }
     __syncthreads();
-    if (threadIdx.x >= 64) return;
-    // wave 0: the tile's records in order, 64 at a time
-    const uint64_t lt = (1ull << lane()) - 1ull;
-    for (uint32_t r = i0; r < i1; r += 64) {
-        const uint32_t i = r + lane();
+    uint16_t* ow = reinterpret_cast<uint16_t*>(ow32);
+    uint8_t* tg = tag[w];
+    const uint64_t lt = (1ull << l) - 1ull;
+#pragma unroll
+    for (uint32_t q = 0; q < IT; q++) {
+        if (s0 + q * 64 >= i1) break;
+        const uint32_t i = s0 + q * 64 + l;
         const bool valid = i < i1;
-        const uint32_t key = valid ? tk[i - i0] : 0u;
+        const uint32_t k = valid ? key[q] : 0u;
         // lanes that share a key (rare: ~0.5 pairs per 64 records over 4096 buckets)
         // rank among themselves in lane order; every other lane is alone.  Each lane
         // writes its lane id to its key's tag: a lane that reads another's id shares
         // its key, and one ballot per shared key finds the key's lanes
-        if (valid) tag[key] = (uint8_t)lane();
+        if (valid) tg[k] = (uint8_t)l;
         lds_sync();
-        uint64_t todo = __ballot(valid && tag[key] != (uint8_t)lane());
+        uint64_t todo = __ballot(valid && tg[k] != (uint8_t)l);
         uint32_t rank = 0, grp = 1;
         bool last = true;
         while (todo) {
-            const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)__builtin_ctzll(todo));
-            const uint64_t m = __ballot(valid && key == kl);
-            if (valid && key == kl) {
+            const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)__builtin_ctzll(todo));
+            const uint64_t m = __ballot(valid && k == kl);
+            if (valid && k == kl) {
                 rank = (uint32_t)__popcll(m & lt);
                 grp = (uint32_t)__popcll(m);
-                last = (m >> lane()) == 1ull;
+                last = (m >> l) == 1ull;
             }
             todo &= ~m;
         }
         if (valid) {
-            const uint32_t c = cnt[key];
-            const uint32_t pos = c + rank;
-            B.idx_sorted[pos] = i;
-            if (last) cnt[key] = c + grp;  // the key's last lane
+            const uint32_t c = ow[k];
+            B.idx_sorted[cnt[k] + c + rank] = i;
+            if (last) ow[k] = (uint16_t)(c + grp);  // the key's last lane
         }
         lds_sync();
     }
 }
+constexpr uint32_t BS_KEYS8 = 4608;  // the 8-wave scatter's key limit (its LDS: ~129 KB)
 size_t bucket_sort_bytes(uint32_t n, uint32_t nk) { return ((size_t)((n + BS_TILE - 1) / BS_TILE) * nk + nk + 64) * 4; }
 bool bucket_sort(const uint32_t* keys, uint32_t n, uint32_t nk, uint32_t* keys_sorted, uint32_t* idx_sorted, uint32_t* beg,
                  uint32_t* end, void* tmp, size_t tmp_bytes, hipStream_t st) {
@@ -1336,7 +1372,8 @@ bool bucket_sort(const uint32_t* keys, uint32_t n, uint32_t nk, uint32_t* keys_s
                  idx_sorted, beg, end};
     hipLaunchKernelGGL(k_bs_hist, dim3(tiles), dim3(256), nk * 4, st, B);
     hipLaunchKernelGGL(k_bs_cols, dim3((nk + 63) / 64), dim3(64 * BS_GROUPS), 0, st, B, tiles);
-    hipLaunchKernelGGL(k_bs_scatter, dim3(tiles), dim3(256), (nk + BS_TILE) * 4 + ((nk + 3) & ~3u), st, B);
+    if (nk <= BS_KEYS8) hipLaunchKernelGGL((k_bs_scatter<8, BS_KEYS8>), dim3(tiles), dim3(512), 0, st, B);
+    else hipLaunchKernelGGL((k_bs_scatter<4, BS_MAX_KEYS>), dim3(tiles), dim3(256), 0, st, B);
     return true;
 }
 

@@ -144,6 +144,14 @@ def test_c4_churn_metric_size_drop_in_read_back():
     run_churn(1_000_000, 1_000_000, 2, full_state=False, packed=12, alloc=host_array, once=True, shim=True)
 
 
+@pytest.mark.parametrize("buckets", [1024, 8192, 16384])
+def test_churn_bucket_counts(buckets):
+    """the bucket sort's three forms (ingest.hip bucket_sort): 8 scatter waves per
+    tile up to 4607 local buckets, 4 waves up to 8447, rocPRIM's radix sort past
+    that - 20k nodes x 200k pods, 40k + 40k per tick in kwok_pod_rec12"""
+    run_churn(20_000, 40_000, 2, buckets=buckets, packed=12)
+
+
 @pytest.mark.parametrize("chunk", [None, "70000"])
 def test_churn_packed12_parity(chunk, monkeypatch):
     """20k nodes x 200k pods, 40k + 40k per tick as kwok_pod_rec12 in pageable
