@@ -1,7 +1,8 @@
 """The last dispatches of a rocprofv3 kernel trace as a timeline: start offset
 from the first of them, duration, gap to the previous end (microseconds).
 
-usage: timeline.py run_kernel_trace.csv [--last N]"""
+usage: timeline.py run_kernel_trace.csv [--last N] [--copies run_memory_copy_trace.csv]
+(--copies: the copies that start inside the window, merged in as "copy <direction> <bytes>")"""
 import argparse
 import csv
 
@@ -10,9 +11,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=40)
+    ap.add_argument("--copies")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))[-a.last:]
     t0 = int(rows[0]["Start_Timestamp"])
+    if a.copies:
+        for r in csv.DictReader(open(a.copies)):
+            if int(r["Start_Timestamp"]) >= t0:
+                size = r.get("Bytes") or r.get("Size") or r.get("Copy_Bytes") or "?"
+                r["Kernel_Name"] = "copy %s %s" % (r.get("Direction", r.get("Kind", "")), size)
+                rows.append(r)
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     prev = t0
     for r in rows:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
