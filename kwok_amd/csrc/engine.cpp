@@ -1921,8 +1921,13 @@ int ingest_pods_impl(kwok_engine* e, const void* recs, int packed, size_t n, con
     const bool zc_ok = e->ingest_zc && K == 1 && !resident && (packed != 2 || ((uintptr_t)recs & 3) == 0);
     // kwok_pod_rec12's create handles: written by the kernel straight into a
     // kwok_host_alloc out_new_handles (each chunk's as it completes; no copy at the
-    // batch's end), else into HBM and copied back after the last chunk
-    int32_t* new_map = packed == 2 && new_cap && e->new_mapped ? (int32_t*)host_mapped(out_new, new_cap * 4) : nullptr;
+    // batch's end), else into HBM and copied back after the last chunk.  With the
+    // tick behind the batch they always take the copy: the kernel's writes over the
+    // link hold CUs beside the tick's persistent blocks (C4 step 1.08-1.10 -> 1.04-1.05
+    // ms, profiles/r13_new_handles_ab.txt; as two calls the in-place form is as fast)
+    int32_t* new_map = packed == 2 && new_cap && e->new_mapped && tick_now < 0
+                           ? (int32_t*)host_mapped(out_new, new_cap * 4)
+                           : nullptr;
     int32_t* new_dst = new_map ? new_map : G.new_handle;
     const void* zev = zc_ok ? host_mapped(recs, n * RB) : nullptr;
     const void* zar = zc_ok && arena_len ? host_mapped(arena, arena_len) : nullptr;
