@@ -53,9 +53,12 @@ struct JRd {
             wb = b;
             w = *reinterpret_cast<const uint4*>(a + b);
         }
+        // (the byte picked from values, not by a select of the window's field addresses,
+        // which the compiler would form from `o < 4 ? w.x : ...`: an indexed load keeps
+        // the reader - and the scan state beside it - in scratch memory)
         const uint32_t o = (uint32_t)(p - b);
-        const uint32_t x = o < 8 ? (o < 4 ? w.x : w.y) : (o < 12 ? w.z : w.w);
-        return (x >> (8 * (o & 3))) & 0xFFu;
+        const uint64_t q = o < 8 ? ((uint64_t)w.y << 32 | w.x) : ((uint64_t)w.w << 32 | w.z);
+        return (uint32_t)(q >> (8 * (o & 7))) & 0xFFu;
     }
     __device__ __forceinline__ int peek() { return pos < end ? (int)at(pos) : -1; }
     // bytes from p up to the first one that ends a string's plain run (a quote, a
@@ -1118,7 +1121,8 @@ struct NodeScan {
         if (c == N_NONE) return;
         if (c == N_ANN || c == N_LAB) {  // a label / annotation entry
             const bool ann = c == N_ANN;
-            (ann ? n_ann : n_lab)++;
+            if (ann) n_ann++;  // (no reference picked by a condition: the scan's state stays in registers)
+            else n_lab++;
             next = ann ? N_ANNV : N_LABV;
             const JsonSel* M = man_sel(ann);
             const JsonSel* D = ann ? &cfg->dis_ann : &cfg->dis_lab;
@@ -1205,7 +1209,10 @@ struct NodeScan {
                 }
                 const bool ann = c == N_ANNV;
                 if (km_man) sel_value(man_sel(ann), man, km_man, t);
-                if (km_dis) sel_value(ann ? &cfg->dis_ann : &cfg->dis_lab, ann ? dis_a : dis_l, km_dis, t);
+                if (km_dis) {
+                    if (ann) sel_value(&cfg->dis_ann, dis_a, km_dis, t);
+                    else sel_value(&cfg->dis_lab, dis_l, km_dis, t);
+                }
                 break;
             }
             case N_PHASE:
@@ -1220,7 +1227,20 @@ struct NodeScan {
             case N_CAP:
                 if (t.kind != J_NULL) err = KWOK_EDOMAIN;  // the wrong type
                 break;
-            case N_INFOV: ref(t, info[info_k]); break;
+            case N_INFOV:  // (constant indices: an indexed span would keep the scan state in scratch)
+                switch (info_k) {
+                    case 0: ref(t, info[0]); break;
+                    case 1: ref(t, info[1]); break;
+                    case 2: ref(t, info[2]); break;
+                    case 3: ref(t, info[3]); break;
+                    case 4: ref(t, info[4]); break;
+                    case 5: ref(t, info[5]); break;
+                    case 6: ref(t, info[6]); break;
+                    case 7: ref(t, info[7]); break;
+                    case 8: ref(t, info[8]); break;
+                    default: ref(t, info[9]); break;
+                }
+                break;
             default: break;
         }
     }
