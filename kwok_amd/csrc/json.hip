@@ -42,13 +42,16 @@ namespace {
 // node documents 0.68 -> 1.01 ms in k_json_nodes - the scan is bound by its
 // per-byte instructions and the lanes' divergent paths, not by the refills
 // ---------------------------------------------------------------------------
+// positions are 32-bit: the JSON entry points take arenas below 4 GiB (engine.cpp), and
+// half the scan's position arithmetic was 64-bit pairs
+typedef uint32_t jpos;
 struct JRd {
     const uint8_t* a;
-    uint64_t pos, end;
-    uint64_t wb;
+    jpos pos, end;
+    jpos wb;
     uint4 w;
-    __device__ __forceinline__ uint32_t at(uint64_t p) {
-        const uint64_t b = p & ~15ull;
+    __device__ __forceinline__ uint32_t at(jpos p) {
+        const jpos b = p & ~15u;
         if (b != wb) {
             wb = b;
             w = *reinterpret_cast<const uint4*>(a + b);
@@ -64,7 +67,7 @@ struct JRd {
     // bytes from p up to the first one that ends a string's plain run (a quote, a
     // backslash or a control character), within p's 16-byte window: that byte's
     // offset from p, or the bytes to the window's end when the window holds none
-    __device__ __forceinline__ uint32_t plain_run(uint64_t p);
+    __device__ __forceinline__ uint32_t plain_run(jpos p);
 };
 
 // bit k set for each byte k of x that ends a string's plain run: a quote, a
@@ -75,7 +78,7 @@ __device__ __forceinline__ uint32_t str_special4(uint32_t x) {
     const uint32_t m = zero(x ^ 0x22222222u) | zero(x ^ 0x5C5C5C5Cu) | zero(x & 0xE0E0E0E0u);
     return (((m >> 7) & 0x01010101u) * 0x01020408u) >> 24;
 }
-__device__ __forceinline__ uint32_t JRd::plain_run(uint64_t p) {
+__device__ __forceinline__ uint32_t JRd::plain_run(jpos p) {
     (void)at(p);
     const uint32_t o = (uint32_t)(p - wb);
     const uint32_t m = (str_special4(w.x) | str_special4(w.y) << 4 | str_special4(w.z) << 8 | str_special4(w.w) << 12) &
@@ -83,19 +86,19 @@ __device__ __forceinline__ uint32_t JRd::plain_run(uint64_t p) {
     return (m ? (uint32_t)__builtin_ctz(m) : 16u) - o;
 }
 
-__device__ __forceinline__ bool bytes_eq(JRd& r, uint64_t off, uint32_t len, const uint8_t* s, uint32_t n) {
+__device__ __forceinline__ bool bytes_eq(JRd& r, jpos off, uint32_t len, const uint8_t* s, uint32_t n) {
     if (len != n) return false;
     for (uint32_t k = 0; k < n; k++)
         if (r.at(off + k) != s[k]) return false;
     return true;
 }
-__device__ __forceinline__ bool span_eq(JRd& r, uint64_t a, uint64_t b, uint32_t len) {
+__device__ __forceinline__ bool span_eq(JRd& r, jpos a, jpos b, uint32_t len) {
     for (uint32_t k = 0; k < len; k++)
         if (r.at(a + k) != r.at(b + k)) return false;
     return true;
 }
 template <int N>
-__device__ __forceinline__ bool lit_eq(JRd& r, uint64_t off, uint32_t len, const char (&s)[N]) {
+__device__ __forceinline__ bool lit_eq(JRd& r, jpos off, uint32_t len, const char (&s)[N]) {
     if (len != N - 1) return false;
     for (int k = 0; k < N - 1; k++)
         if (r.at(off + k) != (uint8_t)s[k]) return false;
@@ -107,7 +110,7 @@ __device__ __forceinline__ bool lit_eq(JRd& r, uint64_t off, uint32_t len, const
 // ---------------------------------------------------------------------------
 enum : uint8_t { J_STR, J_NUM, J_TRUE, J_FALSE, J_NULL };
 struct JTok {
-    uint64_t off;  // STR: inside the quotes; else the token
+    jpos off;  // STR: inside the quotes; else the token
     uint32_t len;
     uint8_t kind;
     bool esc;      // STR held an escape (the span is not the value)
@@ -239,7 +242,7 @@ __device__ bool jparse(JRd& r, H& h, int d0 = 0) {
                 t.nz = c == 't';
                 r.pos += n;
             } else {  // codec.cpp num(): '-'? then any run of [0-9.eE+-]
-                const uint64_t s = r.pos;
+                const jpos s = r.pos;
                 if (c == '-') r.pos++;
                 for (;;) {
                     const int x = r.peek();
@@ -285,7 +288,7 @@ __device__ bool jparse(JRd& r, H& h, int d0 = 0) {
 }
 
 // RFC3339 "YYYY-MM-DDTHH:MM:SSZ" -> unix seconds (codec.cpp parse_time)
-__device__ bool jtime(JRd& r, uint64_t off, uint32_t len, int64_t* out) {
+__device__ bool jtime(JRd& r, jpos off, uint32_t len, int64_t* out) {
     if (len != 20) return false;
     uint32_t b[20];
     for (int k = 0; k < 20; k++) b[k] = r.at(off + k);
@@ -347,11 +350,11 @@ struct PodScan {
     uint32_t seen_root = 0, seen_meta = 0, seen_spec = 0, seen_status = 0;
     bool meta_done = false, spec_done = false, meta_obj = false, spec_obj = false;
     bool st_defer = false, pass2 = false;  // a status read before metadata / spec: scanned again at the end
-    uint64_t st_pos = 0;                   // its '{'
+    jpos st_pos = 0;                       // its '{'
     // metadata
     Span name{0, 0}, ns{0, 0};
     bool ct_ok = false;
-    uint64_t ct_off = 0;
+    jpos ct_off = 0;
     int64_t creation = 0;
     uint8_t flags = 0, phase = 0;
     uint32_t n_ann = 0, n_lab = 0;
@@ -954,7 +957,7 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
     if (off > A.arena_len || len > A.arena_len - off) {
         status = KWOK_EINVAL;  // (codec.cpp parse_doc: a span outside the arena)
     } else {
-        JRd rd{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
+        JRd rd{A.arena, (jpos)off, (jpos)(off + len), ~0u, make_uint4(0, 0, 0, 0)};
         p.r = &rd;
         p.cfg = A.cfg;
         bool ok = !A.cfg->all_host && jparse(rd, p);
@@ -1019,7 +1022,7 @@ __global__ __launch_bounds__(256) void k_json_pods(JsonPodArgs A) {
             }
             // a key hit whose strings differ from the registered spec's (FNV-1a is not
             // collision-resistant and specs come from users): the host decides it
-            JRd rc{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
+            JRd rc{A.arena, (jpos)off, (jpos)(off + len), ~0u, make_uint4(0, 0, 0, 0)};
             if (id >= 0 && !spec_equal(rc, p, A.canon, A.tab_canon[hs])) status = JSON_SPEC_X;
             else if (id < 0) status = JSON_SPEC;
             else ev.spec_id = id;
@@ -1300,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_json_nodes(JsonNodeArgs A) {
     } else if (A.cfg->all_host) {
         status = JSON_HOST;
     } else {
-        JRd rd{A.arena, off, off + len, ~0ull, make_uint4(0, 0, 0, 0)};
+        JRd rd{A.arena, (jpos)off, (jpos)(off + len), ~0u, make_uint4(0, 0, 0, 0)};
         p.r = &rd;
         p.cfg = A.cfg;
         p.skip_status = ev.op == KWOK_OP_DELETE;
