@@ -597,6 +597,9 @@ def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
         now += 30
         e.tick(now, read=False)
     dt = (time.perf_counter() - t0) / steps
+    # the same steady ticks queued two deep, as the headline's (kwok_tick_submit of tick
+    # k+1 before kwok_tick_collect of tick k: no host round trip between ticks)
+    dq, _, now = steady_queued(e, now, steps, 3)
     e.profile_enable(True)
     for _ in range(10):
         now += 30
@@ -609,12 +612,14 @@ def emulated_ranks_leg(nodes, ranks, steps, churn_ticks):
     e.close()
     return {"ranks": ranks, "workload": "one rank's 1M x 10M fleet; BACK folds %d ranks' exchange messages and lists "
                                         "(KWOK_FORCE_MULTI + KWOK_EMULATE_RANKS, one-rank RCCL allgather)" % ranks,
-            "steady_ms_per_tick": dt * 1e3, "steady_phase_ms": {k: v / max(nt, 1) for k, v in ph.items()},
+            "steady_ms_per_tick": dt * 1e3, "steady_queued_ms_per_tick": dq / steps * 1e3,
+            "steady_phase_ms": {k: v / max(nt, 1) for k, v in ph.items()},
             "churn": None if churn is None else {k: churn[k] for k in ("ms_per_step", "ingest_ms", "tick_ms",
                                                                        "kernel_ms", "exchange_ms", "median_ms",
                                                                        "phase_ms")},
-            "note": "blocking kwok_tick steps; the allgather is a one-rank copy (the xGMI transfer of N ranks' "
-                    "8 KiB messages / MB lists is not in it)"}
+            "note": "steady_ms_per_tick: blocking kwok_tick steps; steady_queued_ms_per_tick: the headline's "
+                    "queued steps; the allgather is a one-rank copy (the xGMI transfer of N ranks' 8 KiB messages / "
+                    "MB lists is not in it)"}
 
 
 def flap_leg(nodes, ticks, heartbeat_once=False):
