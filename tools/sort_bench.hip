@@ -1,8 +1,7 @@
 // Timing harness of the ingest's bucket sort (kwok_amd/csrc/ingest.hip,
-// bucket_sort): 1M keys over 4096 buckets (+5% "nothing to apply"), sorted 20
-// times; run under rocprofv3 --kernel-trace --stats for per-kernel times.
-// Built with -DBS_DIAG_NO_STORE for timing variants only
-// (tools/gpu_sortbench.sh).  Checks the result against a host stable sort.
+// bucket_sort): n keys (argv[1], 1M) over nb buckets (argv[2], 4096; +5% "nothing
+// to apply"), sorted 20 times; run under rocprofv3 --kernel-trace --stats for
+// per-kernel times (tools/gpu_s40.sh).  Checks the result against a host stable sort.
 #include "../kwok_amd/csrc/ingest.hip"
 
 #include <algorithm>
@@ -11,7 +10,8 @@
 #include <vector>
 
 int main(int argc, char** argv) {
-    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000000u, nb = 4096, nk = nb + 1;
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000000u, nb = argc > 2 ? (uint32_t)atoi(argv[2]) : 4096u,
+                   nk = nb + 1;
     std::vector<uint32_t> keys(n);
     std::mt19937 rng(7);
     for (auto& k : keys) k = (rng() % 20 == 0) ? nb : rng() % nb;
