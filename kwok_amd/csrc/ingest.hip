@@ -522,6 +522,7 @@ __device__ __forceinline__ uint32_t pod_bits(const DevState& S, uint32_t flags, 
 __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, IngestBatch I) {
     __shared__ uint64_t bm_all[APPLY_WAVES][MAX_BM_WORDS];
     __shared__ uint32_t flist_all[APPLY_WAVES][64];  // a chunk's creates' slots (parallel path)
+    __shared__ uint8_t dtag_all[APPLY_WAVES][1024];  // a chunk's slots named twice? (lane ids by slot hash)
     const uint32_t w = threadIdx.x >> 6, l = lane();
     const uint32_t b = blockIdx.x * APPLY_WAVES + w;
     if (I.spec) {
@@ -621,10 +622,23 @@ __global__ __launch_bounds__(64 * APPLY_WAVES) void k_ing_apply(DevState S, Inge
             const bool used = exl && pos < B.cp && ((B.bm[pos >> 6] >> (pos & 63)) & 1);
             const bool crt = act && !exl;  // (prep decided creates with a bad field, or foreign / unknown)
             const bool take = crt && (ns0 & NS_SLOT);
-            const uint32_t key = exl ? pos : (0x80000000u | l);
+            // a slot named by two records of the chunk: each lane writes its id at its slot's
+            // hash; a lane that reads another's id shares the hash, and one ballot per
+            // such slot value finds whether two lanes name it (a few rounds, not 63)
             bool dup = false;
-            for (uint32_t j = 0; j < 63; j++) dup |= (l > j) && key == rdl(key, j);
-            bool par = !__ballot((act && !exl && (chk & REC_BY_NAME)) || (act && op == KWOK_OP_DELETE) || dup) &&
+            {
+                uint8_t* tg = dtag_all[w];
+                if (exl) tg[pos & 1023u] = (uint8_t)l;
+                lds_sync();
+                uint64_t todo = __ballot(exl && tg[pos & 1023u] != (uint8_t)l);
+                while (todo && !dup) {
+                    const uint32_t kl = rdl(pos, (uint32_t)__builtin_ctzll(todo));
+                    const uint64_t m = __ballot(exl && pos == kl);
+                    dup = __popcll(m) > 1;
+                    todo &= ~m;
+                }
+            }
+            bool par = !__ballot((act && !exl && (chk & REC_BY_NAME)) || (act && op == KWOK_OP_DELETE)) && !dup &&
                        !(__ballot(exl && !used) && __ballot(crt));
             uint32_t* flist = flist_all[w];
             const uint64_t tm = __ballot(take);
